@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Benchmark: hyperedge TEPS of batched multi-source BFS (+ pattern-match queries/sec).
+
+Workload (BASELINE.json configs[1]): config 2 -- 10M nodes, 40M links, arity
+U{2..8}, Chung-Lu gamma 2.1, 1024-source BFS to depth 4 on one MI355X.  A step = one
+hgx_bfs_batch over the 1024 sources with the CSR resident in HBM (all per-depth visited sets
+materialised on the device).  Secondary: config 3, one step = one hgx_pattern_batch of 10,000
+hg.and(hg.type(T), hg.incident(a), hg.orderedLink(x, ANY, y)) queries over 50M typed links.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the sources
+are independent units; every rank holds a replica of the snapshot and runs its own 1024-source
+batch (weak scaling, no data-path collective).  torch.distributed is used only for the barrier
+and the max-over-ranks of the elapsed time.
+
+The CPU baseline is the C restatement of the reference path (oracle/, test infrastructure) timed
+on the host cores on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/pmc_<workload>.json,
+    written by tools/pmc_summary.py with the gfx950 FETCH_SIZE correction), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def roofline(stats_list, workload):
+    """Dominant kernel of the BFS step: achieved = algorithmic bytes / device time (HIP events)."""
+    from hypergraphdb_amd._lib import KERNELS
+    tot = {k: {"ms": 0.0, "bytes": 0.0, "launches": 0} for k in KERNELS}
+    for st in stats_list:
+        for k, v in st["kernels"].items():
+            tot[k]["ms"] += v["ms"]
+            tot[k]["bytes"] += v["bytes"]
+            tot[k]["launches"] += v["launches"]
+    dom = max(tot, key=lambda k: tot[k]["ms"])
+    t = tot[dom]
+    achieved = t["bytes"] / (t["ms"] / 1e3) / 1e9 if t["ms"] > 0 else 0.0
+    traffic = pmc_traffic(dom, workload)
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": t["bytes"] / max(t["launches"], 1),
+            "avg_launch_ms": t["ms"] / max(t["launches"], 1), "launches": t["launches"]}, tot
+
+
+def cpu_bfs_baseline(g, seeds, depth, budget_s):
+    """C restatement (oracle/) of HGBreadthFirstTraversal + DefaultALGenerator, OpenMP over seeds."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_ctypes import OracleGraph
+    threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    t0 = time.time()
+    orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    log(f"cpu baseline: host snapshot built in {time.time() - t0:.1f}s; {threads} threads")
+    done, trav, elapsed, i = 0, 0, 0.0, 0
+    while elapsed < budget_s and i < len(seeds):
+        batch = seeds[i:i + threads]
+        t1 = time.time()
+        _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads)
+        elapsed += time.time() - t1
+        trav += int(tr.sum())
+        done += len(batch)
+        i += threads
+    del orc
+    return {"value": trav / elapsed, "unit": "TEPS", "cores": threads, "kind": "port",
+            "sample": f"{done} of the {len(seeds)} config-2 sources, depth {depth}, one traversal per thread "
+                      f"(C restatement of HGBreadthFirstTraversal/DefaultALGenerator), {elapsed:.1f}s",
+            "seconds": round(elapsed, 2)}
+
+
+def cpu_query_baseline(g, qs, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_ctypes import OracleGraph
+    threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    n_done, elapsed, i, step = 0, 0.0, 0, max(threads * 8, 64)
+    while elapsed < budget_s and i < len(qs["type"]):
+        sl = slice(i, i + step)
+        t = qs["type"][sl]
+        n = len(t)
+        inc_off = np.arange(n + 1, dtype=np.int64)
+        pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
+        pat = np.stack([qs["x"][sl], np.full(n, -1, np.int32), qs["y"][sl]], 1).reshape(-1)
+        t1 = time.time()
+        orc.and_query_many(t, inc_off, qs["a"][sl], pat_off, pat, np.ones(n, np.int32), nthreads=threads)
+        elapsed += time.time() - t1
+        n_done += n
+        i += step
+    del orc
+    return {"value": n_done / elapsed, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{n_done} of the {len(qs['type'])} config-3 queries (C restatement of AndToQuery + "
+                      f"ZigZagIntersectionResult + OrderedLinkCondition), {elapsed:.1f}s",
+            "seconds": round(elapsed, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config-2/3 sizes (1.0 = full)")
+    ap.add_argument("--sources", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=4)
+    ap.add_argument("--no-queries", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work per metric")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    import hypergraphdb_amd as H
+    from hypergraphdb_amd import synth
+
+    # ---------------- config 2: batched BFS ----------------
+    t0 = time.time()
+    g = synth.config2(scale=args.scale, n_sources=args.sources)
+    if rank > 0:   # weak scaling: every rank its own 1024 sources
+        g["seeds"] = synth.sources(g, args.sources, 7 + 1000 * rank)
+    log(f"rank {rank}: config2 generated in {time.time() - t0:.1f}s: A={g['num_atoms']} M={len(g['link_atom'])} "
+        f"P={len(g['tgt_idx'])}")
+    t0 = time.time()
+    snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"],
+                                device=local)
+    log(f"rank {rank}: snapshot on device {local} in {time.time() - t0:.1f}s (I={snap.num_incidences})")
+    snap.set_timing(True)
+    acct = None
+    for w in range(args.warmup):
+        res = H.bfs_batch(snap, g["seeds"], args.depth)
+        if acct is None:
+            acct = res.stats(accounting=True)     # TEPS numerator / |U_d| (deterministic per batch)
+            log(f"rank {rank}: levels |U_d|={acct['union_frontier']} traversed={acct['traversed_edges']:.3e}")
+        res.close()
+        log(f"rank {rank}: warmup {w} done")
+    if acct is None:
+        res = H.bfs_batch(snap, g["seeds"], args.depth)
+        acct = res.stats(accounting=True)
+        res.close()
+    stats = []
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = H.bfs_batch(snap, g["seeds"], args.depth)
+        stats.append(res.stats(accounting=False))
+        res.close()
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    edges_total = sum_over_ranks(acct["traversed_edges"] * args.steps)
+    teps = edges_total / dt
+    roof, per_kernel = roofline(stats, "config2")
+    ms_dev = sum(s["ms_total"] for s in stats) / len(stats)
+    log(f"rank {rank}: {args.steps} steps in {dt:.3f}s -> {teps:.3e} TEPS; device ms/step {ms_dev:.2f}; "
+        f"dominant {roof['kernel']} {roof['achieved']} GB/s")
+    snap.close()
+    del snap
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_bfs_baseline(g, g["seeds"], args.depth, args.cpu_budget)
+        log(f"cpu baseline {cpu['value']:.3e} TEPS on {cpu['cores']} threads")
+    del g
+
+    # ---------------- config 3: pattern queries ----------------
+    pattern = None
+    if not args.no_queries:
+        t0 = time.time()
+        g3 = synth.config3(scale=args.scale, n_queries=10_000)
+        Q = g3["queries"]
+        log(f"rank {rank}: config3 generated in {time.time() - t0:.1f}s")
+        snap3 = H.HyperGraphSnapshot(g3["num_atoms"], g3["link_atom"], g3["tgt_off"], g3["tgt_idx"],
+                                     g3["link_type"], device=local)
+        snap3.set_timing(True)
+        qs = [(int(Q["type"][i]), [int(Q["a"][i])], (int(Q["x"][i]), -1, int(Q["y"][i])))
+              for i in range(len(Q["type"]))]
+        for _ in range(args.warmup):
+            H.pattern_batch(snap3, qs)
+        ms, nres = [], 0
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            r = H.pattern_batch(snap3, qs)
+            ms.append(r.ms)
+            nres = int(r.offsets[-1])
+        barrier_sync()
+        dtq = max_over_ranks(time.perf_counter() - t0)
+        qps = sum_over_ranks(len(qs) * args.steps) / dtq
+        mm = sum(m["ms_match"] for m in ms) / len(ms)
+        bm = sum(m["bytes_match"] for m in ms) / len(ms)
+        ach = bm / (mm / 1e3) / 1e9 if mm > 0 else 0.0
+        pattern = {"metric": "pattern-match queries/sec", "value": round(qps, 1), "unit": "queries/s",
+                   "ms_per_step": round(dtq / args.steps * 1e3, 3), "queries_per_step": len(qs),
+                   "results_per_step": nres,
+                   "workload": "config3: 50M links over 10M nodes, arity 3-6, 64 types, 10K queries",
+                   "roofline": {"bound": "hbm", "kernel": "hgx_pattern_match", "achieved": round(ach, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                                "traffic": pmc_traffic("hgx_pattern_match", "config3"),
+                                "avg_launch_ms": round(mm, 4), "bytes_per_launch": bm}}
+        log(f"rank {rank}: pattern {qps:.1f} q/s, match kernel {mm:.3f} ms")
+        snap3.close()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            pattern["cpu_baseline"] = cpu_query_baseline(g3, Q, args.cpu_budget)
+            log(f"cpu pattern baseline {pattern['cpu_baseline']['value']:.1f} q/s")
+
+    if rank == 0:
+        line = {
+            "metric": "hyperedge TEPS for batched multi-source BFS; pattern-match queries/sec",
+            "value": teps, "unit": "TEPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32 ids / u64 source bitmasks", "data": "synthetic",
+            "config": {"workload": ("config2: 10M nodes / 40M links, Chung-Lu gamma 2.1, arity 2-8, "
+                                    f"{args.sources}-source BFS depth {args.depth}") if args.scale == 1.0 else
+                       f"config2 at scale {args.scale}, {args.sources} sources, depth {args.depth}",
+                       "sources_per_gpu": args.sources, "depth": args.depth, "scale": args.scale,
+                       "parallelism": f"sources sharded over {world} rank(s), snapshot replicated"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "device_ms_per_step": round(ms_dev, 3),
+            "traversed_edges_per_step": acct["traversed_edges"],
+            "union_frontier": acct["union_frontier"],
+            "survey_model_bytes_per_step": acct["bytes_survey"],
+            "kernels": {k: {"ms_per_step": round(v["ms"] / args.steps, 4), "launches_per_step": v["launches"] / args.steps,
+                            "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] > 0 else None}
+                        for k, v in per_kernel.items()},
+            "pattern": pattern,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

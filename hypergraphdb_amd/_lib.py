@@ -1,0 +1,160 @@
+"""ctypes binding of libhgx.so (the C ABI declared in include/hgx.h).
+
+The engine is native code only: if libhgx.so is missing or cannot be loaded this module
+raises -- there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhgx.so")
+GEN_PATH = os.path.join(_HERE, "libhgx_gen.so")
+
+HGX_OK = 0
+HGX_E_INVALID = -1
+HGX_E_DEVICE = -2
+HGX_E_NOMEM = -3
+HGX_E_UNSUPPORTED = -4
+HGX_E_NOTFOUND = -5
+HGX_ANY_HANDLE = -1
+HGX_NO_TYPE = -1
+HGX_UNBOUNDED = -1
+
+# Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
+EXPORTED = (
+    "hgx_version", "hgx_last_error", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
+    "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_bfs_batch", "hgx_bfs_result_info",
+    "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
+    "hgx_bfs_result_free", "hgx_pattern_batch", "hgx_query_result_offsets", "hgx_query_result_ids",
+    "hgx_query_result_ms", "hgx_query_result_free",
+)
+
+
+class GraphDesc(C.Structure):
+    _fields_ = [("num_atoms", C.c_int64), ("num_links", C.c_int64), ("link_atom", C.c_void_p),
+                ("tgt_off", C.c_void_p), ("tgt_idx", C.c_void_p), ("link_type", C.c_void_p)]
+
+
+class AlgenOpts(C.Structure):
+    _fields_ = [("link_type", C.c_int32), ("return_preceding", C.c_uint8), ("return_succeeding", C.c_uint8),
+                ("reverse_order", C.c_uint8), ("return_source", C.c_uint8)]
+
+
+class AndQuery(C.Structure):
+    _fields_ = [("type", C.c_int32), ("n_incident", C.c_int32), ("incident", C.c_void_p),
+                ("has_ordered", C.c_int32), ("n_pattern", C.c_int32), ("pattern", C.c_void_p)]
+
+
+KERNELS = ("hgx_link_gather", "hgx_atom_pull", "hgx_atom_pull_heavy", "hgx_hub_finalize")
+
+
+class BfsStats(C.Structure):
+    _fields_ = [("n_levels_expanded", C.c_int32), ("n_batches", C.c_int32), ("ms_total", C.c_double),
+                ("ms_kernel", C.c_double * 4), ("launches", C.c_int64 * 4), ("bytes_kernel", C.c_double * 4),
+                ("bytes_survey", C.c_double), ("traversed_edges", C.c_double),
+                ("union_frontier", C.c_int64 * 64)]
+
+    def as_dict(self):
+        d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
+             "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges}
+        d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
+                            "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
+        d["union_frontier"] = [int(x) for x in self.union_frontier[: max(self.n_levels_expanded, 0)]]
+        return d
+
+
+class HGXError(RuntimeError):
+    """A failed hgx_* call (the reference maps these to HGException)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"hgx error {code}: {msg}")
+        self.code = code
+
+
+class HGXUnsupported(HGXError):
+    """The shape is not accelerated (HGX_E_UNSUPPORTED); a Java shim would delegate to the CPU compiler."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (make -C hypergraphdb_amd/csrc).  There is no CPU fallback.")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "hgx_version": ([], C.c_char_p),
+        "hgx_last_error": ([], C.c_char_p),
+        "hgx_graph_create": ([C.POINTER(GraphDesc), i32, C.POINTER(vp)], C.c_int),
+        "hgx_graph_destroy": ([vp], None),
+        "hgx_graph_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "hgx_graph_degree": ([vp, vp, i32, vp], C.c_int),
+        "hgx_graph_incidence": ([vp, i32, vp, i64, C.POINTER(i64)], C.c_int),
+        "hgx_set_timing": ([vp, i32], C.c_int),
+        "hgx_bfs_batch": ([vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
+        "hgx_bfs_result_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "hgx_bfs_result_counts": ([vp, vp], C.c_int),
+        "hgx_bfs_result_visited": ([vp, i32, i32, vp, i64, C.POINTER(i64)], C.c_int),
+        "hgx_bfs_result_depth_of": ([vp, i32, i32, C.POINTER(i32)], C.c_int),
+        "hgx_bfs_result_stats": ([vp, i32, C.POINTER(BfsStats)], C.c_int),
+        "hgx_bfs_result_free": ([vp], None),
+        "hgx_pattern_batch": ([vp, C.POINTER(AndQuery), i32, C.POINTER(vp)], C.c_int),
+        "hgx_query_result_offsets": ([vp, vp], C.c_int),
+        "hgx_query_result_ids": ([vp, vp], C.c_int),
+        "hgx_query_result_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
+        "hgx_query_result_free": ([vp], None),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != HGX_OK:
+        msg = lib().hgx_last_error().decode(errors="replace")
+        if rc == HGX_E_UNSUPPORTED:
+            raise HGXUnsupported(rc, msg)
+        raise HGXError(rc, msg)
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+_gen = None
+
+
+def gen_lib():
+    """Synthetic generators (host C, OpenMP) -- benchmark/test input only."""
+    global _gen
+    if _gen is None:
+        if not os.path.exists(GEN_PATH):
+            raise ImportError(f"{GEN_PATH} is missing (make -C hypergraphdb_amd/csrc)")
+        G = C.CDLL(GEN_PATH)
+        vp, i32, i64, u64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+        G.hgx_gen_hypergraph_offsets.argtypes = [i64, i32, i32, u64, vp]
+        G.hgx_gen_hypergraph_offsets.restype = i64
+        G.hgx_gen_hypergraph_fill.argtypes = [i64, i64, i32, i32, dbl, i32, u64, vp, vp, vp]
+        G.hgx_gen_hypergraph_fill.restype = C.c_int
+        G.hgx_gen_permutation_prefix.argtypes = [i64, i64, u64, vp]
+        G.hgx_gen_permutation_prefix.restype = C.c_int
+        G.hgx_gen_sources.argtypes = [i64, i64, vp, i64, u64, vp]
+        G.hgx_gen_sources.restype = C.c_int
+        G.hgx_gen_queries.argtypes = [i64, i64, vp, vp, vp, i64, dbl, u64, vp, vp, vp, vp, vp]
+        G.hgx_gen_queries.restype = C.c_int
+        G.hgx_gen_ontology.argtypes = [i64, i64, u64, i32, i32, vp, vp]
+        G.hgx_gen_ontology.restype = i64
+        _gen = G
+    return _gen

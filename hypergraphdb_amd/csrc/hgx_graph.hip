@@ -1,0 +1,396 @@
+// hgx_graph.hip -- snapshot upload and on-device incidence-index build.
+//
+// Replaces the reference's per-call incidence materialisation
+// (HyperGraph.getIncidenceSet C/HyperGraph.java:1415-1418 -> ISRefResolver C/ISRefResolver.java:72-105
+//  -> BJEStorageImplementation.getIncidenceResultSet storage/bdb-je/.../BJEStorageImplementation.java:405-439)
+// with one device-resident CSR built once per snapshot: pins are keyed (target << 32 | link row),
+// radix-sorted on the GPU, de-duplicated (putNoDupData, :300-307) and cut into rows.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "hgx_internal.h"
+
+namespace hgx {
+
+static thread_local std::string t_last_error;
+
+void set_last_error(const std::string& msg) { t_last_error = msg; }
+[[noreturn]] void fail(int code, const std::string& msg) { throw Error{code, msg}; }
+
+void graph_release(hgx_graph* g) {
+    if (!g) return;
+    if (g->refs.fetch_sub(1) != 1) return;
+    (void)hipSetDevice(g->device);
+    if (g->stream) (void)hipStreamSynchronize(g->stream);
+    for (auto& b : g->pool) (void)hipFree(b.p);
+    g->pool.clear();
+    (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
+    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
+    if (g->pinned) (void)hipHostFree(g->pinned);
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------------------
+
+// One key per (target, link row); a target repeated inside one link keeps its first
+// position only (putNoDupData).  Repeats become UINT64_MAX and sort to the end.
+__global__ void __launch_bounds__(256) k_pin_keys(int64_t M, const int64_t* __restrict__ tgt_off,
+                                                  const int32_t* __restrict__ tgt_idx,
+                                                  uint64_t* __restrict__ keys,
+                                                  unsigned long long* __restrict__ n_dup) {
+    unsigned long long dups = 0;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        int64_t b = tgt_off[r], e = tgt_off[r + 1];
+        for (int64_t p = b; p < e; ++p) {
+            int32_t t = tgt_idx[p];
+            bool dup = false;
+            for (int64_t q = b; q < p; ++q) dup |= (tgt_idx[q] == t);
+            keys[p] = dup ? ~0ull : (((uint64_t)(uint32_t)t << 32) | (uint32_t)r);
+            dups += dup;
+        }
+    }
+    if (dups) atomicAdd(n_dup, dups);
+}
+
+// inc_row[i] = low word; inc_off[a] = first i with key atom >= a.
+__global__ void __launch_bounds__(256) k_cut_rows(int64_t I, int64_t A, const uint64_t* __restrict__ keys,
+                                                  int32_t* __restrict__ inc_row,
+                                                  int64_t* __restrict__ inc_off) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= I;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a = i < I ? (int64_t)(keys[i] >> 32) : A;
+        int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> 32) : -1;
+        if (i < I) inc_row[i] = (int32_t)(uint32_t)keys[i];
+        for (int64_t x = prev + 1; x <= a; ++x) inc_off[x] = i;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_validate(int64_t A, int64_t M, const int32_t* __restrict__ link_atom,
+                                                  const int64_t* __restrict__ tgt_off,
+                                                  const int32_t* __restrict__ tgt_idx, int64_t P,
+                                                  unsigned int* __restrict__ bad) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        int32_t la = link_atom[r];
+        if (la < 0 || la >= A || (r > 0 && link_atom[r - 1] >= la)) atomicOr(bad, 1u);
+        if (tgt_off[r] > tgt_off[r + 1] || tgt_off[r + 1] > P) atomicOr(bad, 2u);
+    }
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        int32_t t = tgt_idx[p];
+        if (t < 0 || t >= A) atomicOr(bad, 4u);
+    }
+}
+
+__global__ void k_degrees(int32_t n, const int32_t* __restrict__ atoms, const int64_t* __restrict__ inc_off,
+                          int64_t A, int64_t* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        int32_t a = atoms[i];
+        out[i] = (a >= 0 && a < A) ? inc_off[a + 1] - inc_off[a] : -1;
+    }
+}
+
+__global__ void k_rows_to_atoms(int64_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ link_atom,
+                                int32_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = link_atom[rows[i]];
+}
+
+// heavy atoms: deg > kHeavyDegree (order-free compaction; the chunk table is rebuilt on host)
+__global__ void __launch_bounds__(256) k_find_heavy(int64_t A, const int64_t* __restrict__ inc_off, int64_t thr,
+                                                    int32_t* __restrict__ out, unsigned int* __restrict__ n) {
+    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A; a += (int64_t)gridDim.x * blockDim.x)
+        if (inc_off[a + 1] - inc_off[a] > thr) out[atomicAdd(n, 1u)] = (int32_t)a;
+}
+
+// out[i] = inc_off[atoms[i]], out[n + i] = deg(atoms[i])
+__global__ void k_ranges(int32_t n, const int32_t* __restrict__ atoms, const int64_t* __restrict__ inc_off,
+                         int64_t* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        int64_t b = inc_off[atoms[i]];
+        out[i] = b;
+        out[n + i] = inc_off[atoms[i] + 1] - b;
+    }
+}
+
+}  // namespace hgx
+
+using namespace hgx;
+
+// ---------------------------------------------------------------------------------------------
+// Pool
+// ---------------------------------------------------------------------------------------------
+
+void* hgx_graph::alloc(size_t bytes) {
+    if (bytes == 0) bytes = 256;
+    bytes = (bytes + 255) & ~(size_t)255;
+    size_t best = (size_t)-1;
+    for (size_t i = 0; i < pool.size(); ++i)
+        if (pool[i].n >= bytes && pool[i].n <= 2 * bytes && (best == (size_t)-1 || pool[i].n < pool[best].n))
+            best = i;
+    if (best != (size_t)-1) {
+        void* p = pool[best].p;
+        pool.erase(pool.begin() + best);
+        return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(stream);
+        for (auto& b : pool) (void)hipFree(b.p);
+        pool.clear();
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            fail(HGX_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+        }
+    }
+    return p;
+}
+
+void hgx_graph::release(void* p, size_t bytes) {
+    if (!p) return;
+    if (bytes == 0) bytes = 256;
+    bytes = (bytes + 255) & ~(size_t)255;
+    pool.push_back({p, bytes});
+}
+
+void* hgx_graph::pinned_buf(size_t bytes) {
+    if (bytes > pinned_bytes) {
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+        size_t n = std::max<size_t>(bytes, 1 << 16);
+        HGX_HIP(hipHostMalloc(&pinned, n, hipHostMallocDefault));
+        pinned_bytes = n;
+    }
+    return pinned;
+}
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------
+
+extern "C" {
+
+const char* hgx_version(void) { return "hgx 0.1.0 (gfx950)"; }
+
+const char* hgx_last_error(void) { return t_last_error.c_str(); }
+
+int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
+    HGX_API_BEGIN
+    if (!d || !out) fail(HGX_E_INVALID, "hgx_graph_create: null argument");
+    *out = nullptr;
+    if (d->num_atoms < 0 || d->num_links < 0 || d->num_links > d->num_atoms)
+        fail(HGX_E_INVALID, "hgx_graph_create: bad sizes");
+    if (d->num_atoms >= (int64_t)INT32_MAX) fail(HGX_E_INVALID, "hgx_graph_create: more than 2^31-1 atoms");
+    if (d->num_links > 0 && (!d->link_atom || !d->tgt_off || !d->tgt_idx))
+        fail(HGX_E_INVALID, "hgx_graph_create: null link arrays");
+    int ndev = 0;
+    HGX_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) fail(HGX_E_INVALID, "hgx_graph_create: no such device");
+    HGX_HIP(hipSetDevice(device));
+
+    hgx_graph* g = new hgx_graph();
+    struct Guard {
+        hgx_graph* g;
+        ~Guard() { if (g) graph_release(g); }
+    } guard{g};
+    g->device = device;
+    HGX_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    const int64_t A = d->num_atoms, M = d->num_links;
+    const int64_t P = M > 0 ? d->tgt_off[M] : 0;
+    if (M > 0 && d->tgt_off[0] != 0) fail(HGX_E_INVALID, "hgx_graph_create: tgt_off[0] != 0");
+    if (P < 0 || P >= ((int64_t)1 << 40)) fail(HGX_E_INVALID, "hgx_graph_create: bad pin count");
+    g->A = A; g->M = M; g->P = P;
+    hipStream_t s = g->stream;
+
+    HGX_HIP(hipMalloc(&g->link_atom, sizeof(int32_t) * std::max<int64_t>(M, 1)));
+    HGX_HIP(hipMalloc(&g->tgt_off, sizeof(int64_t) * (M + 1)));
+    HGX_HIP(hipMalloc(&g->tgt_idx, sizeof(int32_t) * std::max<int64_t>(P, 1)));
+    HGX_HIP(hipMalloc(&g->link_type, sizeof(int32_t) * std::max<int64_t>(M, 1)));
+    HGX_HIP(hipMalloc(&g->inc_off, sizeof(int64_t) * (A + 1)));
+    if (M > 0) {
+        HGX_HIP(hipMemcpyAsync(g->link_atom, d->link_atom, sizeof(int32_t) * M, hipMemcpyHostToDevice, s));
+        HGX_HIP(hipMemcpyAsync(g->tgt_off, d->tgt_off, sizeof(int64_t) * (M + 1), hipMemcpyHostToDevice, s));
+        if (P > 0)
+            HGX_HIP(hipMemcpyAsync(g->tgt_idx, d->tgt_idx, sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
+        if (d->link_type)
+            HGX_HIP(hipMemcpyAsync(g->link_type, d->link_type, sizeof(int32_t) * M, hipMemcpyHostToDevice, s));
+        else
+            HGX_HIP(hipMemsetAsync(g->link_type, 0, sizeof(int32_t) * M, s));
+    } else {
+        int64_t z = 0;
+        HGX_HIP(hipMemcpyAsync(g->tgt_off, &z, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    }
+    // validation on device (ids in range, strictly ascending link ranks, monotone offsets)
+    unsigned int* bad = (unsigned int*)g->alloc(sizeof(unsigned int) + sizeof(unsigned long long));
+    unsigned long long* ndup = (unsigned long long*)((char*)bad + 8);
+    HGX_HIP(hipMemsetAsync(bad, 0, 16, s));
+    if (M > 0) {
+        k_validate<<<grid_for(std::max(M, P), 256), 256, 0, s>>>(A, M, g->link_atom, g->tgt_off, g->tgt_idx, P, bad);
+        HGX_CHECK_LAUNCH();
+    }
+    unsigned int hbad = 0;
+    HGX_HIP(hipMemcpyAsync(&hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    if (hbad & 1u) fail(HGX_E_INVALID, "hgx_graph_create: link_atom not strictly ascending / out of range");
+    if (hbad & 2u) fail(HGX_E_INVALID, "hgx_graph_create: tgt_off not monotone");
+    if (hbad & 4u) fail(HGX_E_INVALID, "hgx_graph_create: target id out of range");
+
+    // incidence index: key sort on the device
+    int64_t I = 0;
+    if (P > 0) {
+        uint64_t* keys = (uint64_t*)g->alloc(sizeof(uint64_t) * P);
+        uint64_t* sorted = (uint64_t*)g->alloc(sizeof(uint64_t) * P);
+        k_pin_keys<<<grid_for(M, 256), 256, 0, s>>>(M, g->tgt_off, g->tgt_idx, keys, ndup);
+        HGX_CHECK_LAUNCH();
+        int end_bit = 64;
+        {
+            int ab = 1;
+            while (((int64_t)1 << ab) <= A) ab++;
+            end_bit = 32 + ab;            // UINT64_MAX sentinels still sort last
+            if (end_bit > 64) end_bit = 64;
+        }
+        size_t tmp_bytes = 0;
+        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, sorted, (int)0, 0, end_bit, s));
+        // hipcub takes int num_items: sort in one call when it fits, else fail loudly.
+        if (P > (int64_t)INT32_MAX) fail(HGX_E_UNSUPPORTED, "hgx_graph_create: more than 2^31-1 pins per device");
+        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, sorted, (int)P, 0, end_bit, s));
+        void* tmp = g->alloc(tmp_bytes);
+        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, sorted, (int)P, 0, end_bit, s));
+        unsigned long long hdup = 0;
+        HGX_HIP(hipMemcpyAsync(&hdup, ndup, sizeof(hdup), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        I = P - (int64_t)hdup;
+        HGX_HIP(hipMalloc(&g->inc_row, sizeof(int32_t) * std::max<int64_t>(I, 1)));
+        k_cut_rows<<<grid_for(I + 1, 256), 256, 0, s>>>(I, A, sorted, g->inc_row, g->inc_off);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipStreamSynchronize(s));
+        g->release(tmp, tmp_bytes);
+        g->release(keys, sizeof(uint64_t) * P);
+        g->release(sorted, sizeof(uint64_t) * P);
+    } else {
+        HGX_HIP(hipMalloc(&g->inc_row, sizeof(int32_t)));
+        HGX_HIP(hipMemsetAsync(g->inc_off, 0, sizeof(int64_t) * (A + 1), s));
+    }
+    g->I = I;
+
+    // heavy atoms + chunk table (load balance for power-law incidence rows)
+    {
+        int32_t* dheavy = (int32_t*)g->alloc(sizeof(int32_t) * std::max<int64_t>(A, 1));
+        HGX_HIP(hipMemsetAsync(bad, 0, 4, s));
+        k_find_heavy<<<grid_for(A, 256), 256, 0, s>>>(A, g->inc_off, kHeavyDegree, dheavy, bad);
+        HGX_CHECK_LAUNCH();
+        unsigned int nh = 0;
+        HGX_HIP(hipMemcpyAsync(&nh, bad, 4, hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        std::vector<int32_t> heavy(nh);
+        if (nh) HGX_HIP(hipMemcpyAsync(heavy.data(), dheavy, sizeof(int32_t) * nh, hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        std::sort(heavy.begin(), heavy.end());
+        std::vector<int64_t> hb(nh), hd(nh);
+        if (nh) {
+            int32_t* dh = (int32_t*)g->alloc(sizeof(int32_t) * nh);
+            int64_t* dr = (int64_t*)g->alloc(sizeof(int64_t) * 2 * nh);
+            HGX_HIP(hipMemcpyAsync(dh, heavy.data(), sizeof(int32_t) * nh, hipMemcpyHostToDevice, s));
+            k_ranges<<<grid_for(nh, 256), 256, 0, s>>>((int32_t)nh, dh, g->inc_off, dr);
+            HGX_CHECK_LAUNCH();
+            HGX_HIP(hipMemcpyAsync(hb.data(), dr, sizeof(int64_t) * nh, hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipMemcpyAsync(hd.data(), dr + nh, sizeof(int64_t) * nh, hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+            g->release(dh, sizeof(int32_t) * nh);
+            g->release(dr, sizeof(int64_t) * 2 * nh);
+        }
+        std::vector<HeavyChunk> ch;
+        for (unsigned int h = 0; h < nh; ++h)
+            for (int64_t b = hb[h]; b < hb[h] + hd[h]; b += kChunkEntries)
+                ch.push_back({b, std::min(hb[h] + hd[h], b + kChunkEntries), heavy[h], (int32_t)h});
+        g->n_heavy = nh;
+        g->I_heavy = 0;
+        for (unsigned int h = 0; h < nh; ++h) g->I_heavy += hd[h];
+        g->n_chunks = (int64_t)ch.size();
+        HGX_HIP(hipMalloc(&g->heavy_atom, sizeof(int32_t) * std::max<int64_t>(nh, 1)));
+        HGX_HIP(hipMalloc(&g->chunks, sizeof(HeavyChunk) * std::max<int64_t>(g->n_chunks, 1)));
+        if (nh) HGX_HIP(hipMemcpyAsync(g->heavy_atom, heavy.data(), sizeof(int32_t) * nh, hipMemcpyHostToDevice, s));
+        if (!ch.empty())
+            HGX_HIP(hipMemcpyAsync(g->chunks, ch.data(), sizeof(HeavyChunk) * ch.size(), hipMemcpyHostToDevice, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        g->release(dheavy, sizeof(int32_t) * std::max<int64_t>(A, 1));
+    }
+    g->release(bad, 16);
+    guard.g = nullptr;
+    *out = g;
+    HGX_API_END
+}
+
+void hgx_graph_destroy(hgx_graph* g) { graph_release(g); }
+
+int hgx_graph_info(const hgx_graph* g, int64_t* num_atoms, int64_t* num_links, int64_t* num_incidences) {
+    HGX_API_BEGIN
+    if (!g) fail(HGX_E_INVALID, "null graph");
+    if (num_atoms) *num_atoms = g->A;
+    if (num_links) *num_links = g->M;
+    if (num_incidences) *num_incidences = g->I;
+    HGX_API_END
+}
+
+int hgx_set_timing(hgx_graph* g, int32_t enabled) {
+    HGX_API_BEGIN
+    if (!g) fail(HGX_E_INVALID, "null graph");
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->timing = enabled != 0;
+    HGX_API_END
+}
+
+int hgx_graph_degree(hgx_graph* g, const int32_t* atoms, int32_t n, int64_t* out_deg) {
+    HGX_API_BEGIN
+    if (!g || (n > 0 && (!atoms || !out_deg)) || n < 0) fail(HGX_E_INVALID, "hgx_graph_degree: bad argument");
+    if (n == 0) return HGX_OK;
+    std::lock_guard<std::mutex> lk(g->mu);
+    HGX_HIP(hipSetDevice(g->device));
+    int32_t* da = (int32_t*)g->alloc(sizeof(int32_t) * n);
+    int64_t* dd = (int64_t*)g->alloc(sizeof(int64_t) * n);
+    HGX_HIP(hipMemcpyAsync(da, atoms, sizeof(int32_t) * n, hipMemcpyHostToDevice, g->stream));
+    k_degrees<<<grid_for(n, 256, 1 << 20), 256, 0, g->stream>>>(n, da, g->inc_off, g->A, dd);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipMemcpyAsync(out_deg, dd, sizeof(int64_t) * n, hipMemcpyDeviceToHost, g->stream));
+    HGX_HIP(hipStreamSynchronize(g->stream));
+    g->release(da, sizeof(int32_t) * n);
+    g->release(dd, sizeof(int64_t) * n);
+    for (int32_t i = 0; i < n; ++i)
+        if (out_deg[i] < 0) fail(HGX_E_INVALID, "hgx_graph_degree: atom id out of range");
+    HGX_API_END
+}
+
+int hgx_graph_incidence(hgx_graph* g, int32_t atom, int32_t* out, int64_t cap, int64_t* n_out) {
+    HGX_API_BEGIN
+    if (!g || !n_out || (cap > 0 && !out)) fail(HGX_E_INVALID, "hgx_graph_incidence: bad argument");
+    if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "hgx_graph_incidence: atom id out of range");
+    std::lock_guard<std::mutex> lk(g->mu);
+    HGX_HIP(hipSetDevice(g->device));
+    int64_t off[2];
+    HGX_HIP(hipMemcpyAsync(off, g->inc_off + atom, sizeof(off), hipMemcpyDeviceToHost, g->stream));
+    HGX_HIP(hipStreamSynchronize(g->stream));
+    int64_t n = off[1] - off[0];
+    *n_out = n;
+    int64_t k = std::min(n, cap);
+    if (k > 0) {
+        int32_t* tmp = (int32_t*)g->alloc(sizeof(int32_t) * k);
+        k_rows_to_atoms<<<grid_for(k, 256), 256, 0, g->stream>>>(k, g->inc_row + off[0], g->link_atom, tmp);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipMemcpyAsync(out, tmp, sizeof(int32_t) * k, hipMemcpyDeviceToHost, g->stream));
+        HGX_HIP(hipStreamSynchronize(g->stream));
+        g->release(tmp, sizeof(int32_t) * k);
+    }
+    HGX_API_END
+}
+
+}  // extern "C"

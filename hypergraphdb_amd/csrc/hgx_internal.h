@@ -1,0 +1,117 @@
+// hgx_internal.h -- shared definitions of the MI355X engine (libhgx.so).
+//
+// Device layout of a snapshot:
+//   link_atom [M]   int32   atom id of link row r (ascending)
+//   tgt_off   [M+1] int64   target row offsets
+//   tgt_idx   [P]   int32   target atom ids, layout order t0..tk-1
+//   link_type [M]   int32   type key of link row r
+//   inc_off   [A+1] int64   incidence row offsets
+//   inc_row   [I]   int32   incident LINK ROWS, ascending (row order == atom rank order)
+// plus the heavy-atom chunk table used to balance power-law incidence rows.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hgx.h"
+
+namespace hgx {
+
+struct Error {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& msg);
+void set_last_error(const std::string& msg);
+
+#define HGX_HIP(x)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess)                                                                   \
+            ::hgx::fail(HGX_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+#define HGX_CHECK_LAUNCH() HGX_HIP(hipGetLastError())
+
+#define HGX_API_BEGIN try {
+#define HGX_API_END                                                                             \
+    }                                                                                           \
+    catch (const ::hgx::Error& e) {                                                             \
+        ::hgx::set_last_error(e.msg);                                                           \
+        return e.code;                                                                          \
+    }                                                                                           \
+    catch (const std::bad_alloc&) {                                                             \
+        ::hgx::set_last_error("host allocation failed");                                        \
+        return HGX_E_NOMEM;                                                                     \
+    }                                                                                           \
+    catch (const std::exception& e) {                                                           \
+        ::hgx::set_last_error(e.what());                                                        \
+        return HGX_E_DEVICE;                                                                    \
+    }                                                                                           \
+    catch (...) {                                                                               \
+        ::hgx::set_last_error("unknown error");                                                 \
+        return HGX_E_DEVICE;                                                                    \
+    }                                                                                           \
+    return HGX_OK;
+
+// Incidence rows longer than this are split into chunks processed by whole workgroups.
+constexpr int64_t kHeavyDegree = 512;
+constexpr int64_t kChunkEntries = 4096;
+
+struct HeavyChunk {
+    int64_t beg, end;   // incidence entry range
+    int32_t atom;       // atom id
+    int32_t slot;       // heavy-atom slot (accumulator row)
+};
+
+struct PoolBuf {
+    void* p;
+    size_t n;
+};
+
+}  // namespace hgx
+
+struct hgx_graph {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::atomic<int> refs{1};
+    bool timing = false;
+
+    int64_t A = 0, M = 0, P = 0, I = 0;
+    int32_t* link_atom = nullptr;
+    int64_t* tgt_off = nullptr;
+    int32_t* tgt_idx = nullptr;
+    int32_t* link_type = nullptr;
+    int64_t* inc_off = nullptr;
+    int32_t* inc_row = nullptr;
+
+    int64_t n_heavy = 0;            // heavy atoms (deg > kHeavyDegree)
+    int64_t I_heavy = 0;            // incidence entries of heavy atoms
+    int64_t n_chunks = 0;
+    int32_t* heavy_atom = nullptr;  // [n_heavy]
+    hgx::HeavyChunk* chunks = nullptr;
+
+    std::vector<hgx::PoolBuf> pool;  // free device buffers for reuse across batches
+    void* pinned = nullptr;          // small pinned host staging area
+    size_t pinned_bytes = 0;
+
+    void* alloc(size_t bytes);
+    void release(void* p, size_t bytes);
+    void* pinned_buf(size_t bytes);
+};
+
+namespace hgx {
+void graph_release(hgx_graph* g);   // drop a reference; frees at zero
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int grid_for(int64_t work_items, int block, int max_blocks = 8192) {
+    int64_t b = ceil_div(work_items > 0 ? work_items : 1, block);
+    return (int)(b < max_blocks ? b : max_blocks);
+}
+}  // namespace hgx

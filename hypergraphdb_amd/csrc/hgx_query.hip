@@ -1,0 +1,365 @@
+// hgx_query.hip -- batched conjunctive pattern matching over typed hyperedges.
+//
+// Replaces, for And{AtomTypeCondition?, IncidentCondition*, OrderedLinkCondition?}:
+//   ExpressionBasedQuery.expand (C/query/cond2qry/ExpressionBasedQuery.java:730-737; orderedLink
+//   adds incident(x) for each non-ANY target) -> AndToQuery (C/query/cond2qry/AndToQuery.java:102-306):
+//   nested ZigZagIntersectionResult (C/query/impl/ZigZagIntersectionResult.java) over sorted
+//   incidence sets and the type index, then PredicateBasedFilter(OrderedLinkCondition)
+//   (C/query/impl/PredicateBasedFilter.java:67-86, C/query/OrderedLinkCondition.java:92-124).
+//
+// GPU formulation: L is in inc(a) <=> a is a target of L.  So the intersection of the anchor
+// incidence sets is the smallest anchor set filtered by "every other anchor is in targets(L)",
+// which reads one short target row per candidate instead of zig-zag probes.  Candidates are
+// visited in ascending order, so the result is ascending like the reference's.  A candidate
+// failing the type filter (one 4-byte read) never touches its target row.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "hgx_internal.h"
+
+namespace hgx {
+
+typedef unsigned long long u64;
+
+constexpr int kQChunk = 256;        // candidates per wave-chunk (4 per lane)
+constexpr int kMaxAnchors = 32;
+constexpr int kMaxPattern = 64;
+
+struct QPlan {
+    int64_t beg;    // first incidence entry of the smallest anchor set
+    int64_t n;      // its size (0: empty result)
+    int32_t amin;   // index of that anchor inside the query's anchor list
+    int32_t pad;
+};
+
+enum QCtr { qCand = 0, qTyped, qArity, qHits, qNum = 4 };
+
+__device__ __forceinline__ void wave_add_q(u64* ctr, u64 v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
+}
+
+__global__ void __launch_bounds__(256) hgx_q_plan(int32_t n, const int64_t* __restrict__ inc_off,
+                                                  const int32_t* __restrict__ q_nop,
+                                                  const int64_t* __restrict__ a_off, const int32_t* __restrict__ anchors,
+                                                  QPlan* __restrict__ plan, int32_t* __restrict__ nchunks) {
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    QPlan p{0, 0, 0, 0};
+    if (!q_nop[q]) {
+        int64_t best = -1;
+        for (int64_t k = a_off[q]; k < a_off[q + 1]; ++k) {
+            int32_t a = anchors[k];
+            int64_t d = inc_off[a + 1] - inc_off[a];
+            if (best < 0 || d < best) {   // first smallest (AndToQuery sorts ORA by size)
+                best = d;
+                p.beg = inc_off[a];
+                p.amin = (int32_t)(k - a_off[q]);
+            }
+        }
+        p.n = best < 0 ? 0 : best;
+    }
+    plan[q] = p;
+    nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
+}
+
+__global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_q) {
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    for (int32_t c = chunk_off[q]; c < chunk_off[q + 1]; ++c) chunk_q[c] = q;
+}
+
+// One wave per chunk of kQChunk candidates of one query.
+__global__ void __launch_bounds__(256) hgx_pattern_match(
+    int32_t n_chunks, const int32_t* __restrict__ chunk_q, const int32_t* __restrict__ chunk_off,
+    const QPlan* __restrict__ plan, const int32_t* __restrict__ q_type, const int64_t* __restrict__ a_off,
+    const int32_t* __restrict__ anchors, const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern,
+    const int32_t* __restrict__ q_has_ordered, const int32_t* __restrict__ inc_row,
+    const int32_t* __restrict__ link_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+    int32_t* __restrict__ slots, int64_t* __restrict__ counts, u64* __restrict__ ctr) {
+    const int lane = threadIdx.x & 63;
+    const int64_t chunk = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (chunk >= n_chunks) return;   // whole wave exits together
+    const int32_t q = chunk_q[chunk];
+    const QPlan pl = plan[q];
+    const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
+    const int32_t T = q_type[q];
+    const int64_t ab = a_off[q], na = a_off[q + 1] - ab;
+    const int64_t pb = p_off[q], np = p_off[q + 1] - pb;
+    const bool ordered = q_has_ordered[q] != 0;
+    int32_t written = 0;
+    u64 n_cand = 0, n_typed = 0, n_ar = 0;
+    for (int k = 0; k < kQChunk / 64; ++k) {
+        const int64_t ci = c0 + k * 64 + lane;
+        bool hit = false;
+        int32_t L = -1;
+        if (ci < pl.n) {
+            ++n_cand;
+            L = inc_row[pl.beg + ci];
+            if (T < 0 || link_type[L] == T) {
+                ++n_typed;
+                const int64_t b = tgt_off[L], e = tgt_off[L + 1];
+                n_ar += (u64)(e - b);
+                hit = true;
+                // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
+                for (int64_t j = 0; j < na && hit; ++j) {
+                    if (j == pl.amin) continue;
+                    const int32_t a = anchors[ab + j];
+                    bool found = false;
+                    for (int64_t i = b; i < e; ++i) found |= (tgt_idx[i] == a);
+                    hit = found;
+                }
+                // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
+                if (hit && ordered) {
+                    int64_t i = b, j = 0;
+                    while (i < e && j < np) {
+                        const int32_t pj = pattern[pb + j];
+                        if (pj < 0 || pj == tgt_idx[i]) ++j;
+                        ++i;
+                    }
+                    hit = (j == np);
+                }
+            }
+        }
+        const u64 m = __ballot(hit);
+        if (hit) slots[chunk * kQChunk + written + __popcll(m & ((1ull << lane) - 1ull))] = L;
+        written += __popcll(m);
+    }
+    if (lane == 0) counts[chunk] = written;
+    wave_add_q(ctr + qCand, n_cand);
+    wave_add_q(ctr + qTyped, n_typed);
+    wave_add_q(ctr + qArity, n_ar);
+    if (lane == 0) atomicAdd(ctr + qHits, (u64)written);
+}
+
+// Copy each chunk's hits to its output position, mapping link rows to atom ids.
+__global__ void __launch_bounds__(256) hgx_q_scatter(int32_t n_chunks, const int64_t* __restrict__ counts,
+                                                     const int64_t* __restrict__ out_off,
+                                                     const int32_t* __restrict__ slots,
+                                                     const int32_t* __restrict__ link_atom, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t chunk = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (chunk >= n_chunks) return;
+    const int64_t c = counts[chunk];
+    const int64_t o = out_off[chunk];
+    for (int64_t i = lane; i < c; i += 64) out[o + i] = link_atom[slots[chunk * kQChunk + i]];
+}
+
+__global__ void hgx_q_offsets(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ out_off,
+                              int64_t* __restrict__ q_off) {
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q <= n) q_off[q] = out_off[chunk_off[q]];
+}
+
+}  // namespace hgx
+
+using namespace hgx;
+
+struct hgx_query_result {
+    int32_t n = 0;
+    std::vector<int64_t> offsets;
+    std::vector<int32_t> ids;
+    double ms_total = 0, ms_match = 0, bytes_match = 0;
+};
+
+extern "C" {
+
+int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t n, hgx_query_result** out) {
+    HGX_API_BEGIN
+    if (!g || !out || n < 0 || (n > 0 && !qs)) fail(HGX_E_INVALID, "hgx_pattern_batch: bad argument");
+    *out = nullptr;
+    // host-side normalisation (ExpressionBasedQuery.expand + toDNF dedupe)
+    std::vector<int32_t> q_type(n), q_nop(n), q_ord(n);
+    std::vector<int64_t> a_off(n + 1, 0), p_off(n + 1, 0);
+    std::vector<int32_t> anchors, pattern;
+    for (int32_t q = 0; q < n; ++q) {
+        const hgx_and_query& Q = qs[q];
+        if (Q.n_incident < 0 || Q.n_pattern < 0 || (Q.n_incident > 0 && !Q.incident) ||
+            (Q.n_pattern > 0 && !Q.pattern))
+            fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(q));
+        if (Q.type < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type in query " + std::to_string(q));
+        q_type[q] = Q.type;
+        q_ord[q] = Q.has_ordered ? 1 : 0;
+        const int32_t m = Q.has_ordered ? Q.n_pattern : 0;
+        if (m > kMaxPattern) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: ordered pattern too long");
+        size_t a0 = anchors.size();
+        auto add = [&](int32_t h) {
+            if (h < 0 || h >= g->A) fail(HGX_E_INVALID, "hgx_pattern_batch: atom id out of range in query " + std::to_string(q));
+            for (size_t k = a0; k < anchors.size(); ++k)
+                if (anchors[k] == h) return;
+            anchors.push_back(h);
+        };
+        for (int32_t i = 0; i < Q.n_incident; ++i) add(Q.incident[i]);
+        for (int32_t i = 0; i < m; ++i) {
+            if (Q.pattern[i] == HGX_ANY_HANDLE) continue;
+            if (Q.pattern[i] < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern id");
+            add(Q.pattern[i]);
+        }
+        if (anchors.size() == a0)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(q) + " has no incidence anchor");
+        if ((int64_t)(anchors.size() - a0) > kMaxAnchors) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: too many anchors");
+        // an empty OrderedLinkCondition gets QueryMetaData.EMPTY, lands in ORA and compiles to HGQuery.NOP
+        q_nop[q] = (Q.has_ordered && m == 0) ? 1 : 0;
+        for (int32_t i = 0; i < m; ++i) pattern.push_back(Q.pattern[i]);
+        a_off[q + 1] = (int64_t)anchors.size();
+        p_off[q + 1] = (int64_t)pattern.size();
+    }
+    hgx_query_result* r = new hgx_query_result();
+    struct Guard {
+        hgx_query_result* r;
+        ~Guard() { delete r; }
+    } guard{r};
+    r->n = n;
+    r->offsets.assign(n + 1, 0);
+    if (n == 0) {
+        guard.r = nullptr;
+        *out = r;
+        return HGX_OK;
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    HGX_HIP(hipSetDevice(g->device));
+    hipStream_t s = g->stream;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
+    } evg{ev};
+    if (g->timing)
+        for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&ev[i]));
+
+    // upload
+    const size_t nA = std::max<size_t>(anchors.size(), 1), nP = std::max<size_t>(pattern.size(), 1);
+    std::vector<std::pair<void*, size_t>> tmp;
+    auto dalloc = [&](size_t bytes) {
+        void* p = g->alloc(bytes);
+        tmp.push_back({p, bytes});
+        return p;
+    };
+    struct TmpGuard {
+        hgx_graph* g;
+        std::vector<std::pair<void*, size_t>>* t;
+        ~TmpGuard() { for (auto& x : *t) g->release(x.first, x.second); }
+    } tg{g, &tmp};
+    int32_t* d_type = (int32_t*)dalloc(sizeof(int32_t) * n);
+    int32_t* d_nop = (int32_t*)dalloc(sizeof(int32_t) * n);
+    int32_t* d_ord = (int32_t*)dalloc(sizeof(int32_t) * n);
+    int64_t* d_aoff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
+    int64_t* d_poff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
+    int32_t* d_anch = (int32_t*)dalloc(sizeof(int32_t) * nA);
+    int32_t* d_pat = (int32_t*)dalloc(sizeof(int32_t) * nP);
+    QPlan* d_plan = (QPlan*)dalloc(sizeof(QPlan) * n);
+    int32_t* d_nch = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
+    int32_t* d_choff = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
+    u64* d_ctr = (u64*)dalloc(sizeof(u64) * qNum);
+    HGX_HIP(hipMemcpyAsync(d_type, q_type.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemcpyAsync(d_nop, q_nop.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemcpyAsync(d_ord, q_ord.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemcpyAsync(d_aoff, a_off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemcpyAsync(d_poff, p_off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s));
+    if (!anchors.empty())
+        HGX_HIP(hipMemcpyAsync(d_anch, anchors.data(), sizeof(int32_t) * anchors.size(), hipMemcpyHostToDevice, s));
+    if (!pattern.empty())
+        HGX_HIP(hipMemcpyAsync(d_pat, pattern.data(), sizeof(int32_t) * pattern.size(), hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * qNum, s));
+    HGX_HIP(hipMemsetAsync(d_nch + n, 0, sizeof(int32_t), s));
+
+    if (g->timing) HGX_HIP(hipEventRecord(ev[0], s));
+    hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, g->inc_off, d_nop, d_aoff, d_anch, d_plan, d_nch);
+    HGX_CHECK_LAUNCH();
+    size_t scan_bytes = 0;
+    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_nch, d_choff, n + 1, s));
+    void* d_scan = dalloc(scan_bytes);
+    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_nch, d_choff, n + 1, s));
+    int32_t n_chunks = 0;
+    HGX_HIP(hipMemcpyAsync(&n_chunks, d_choff + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    if (n_chunks < 0) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
+    const int32_t nc = std::max(n_chunks, 1);
+    int32_t* d_chq = (int32_t*)dalloc(sizeof(int32_t) * nc);
+    int32_t* d_slots = (int32_t*)dalloc(sizeof(int32_t) * (size_t)nc * kQChunk);
+    int64_t* d_cnt = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
+    int64_t* d_outoff = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
+    int64_t* d_qoff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
+    HGX_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * (nc + 1), s));
+    hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_chq);
+    HGX_CHECK_LAUNCH();
+    if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
+    if (n_chunks > 0) {
+        hgx_pattern_match<<<(unsigned)ceil_div((int64_t)n_chunks * 64, 256), 256, 0, s>>>(
+            n_chunks, d_chq, d_choff, d_plan, d_type, d_aoff, d_anch, d_poff, d_pat, d_ord, g->inc_row, g->link_type,
+            g->tgt_off, g->tgt_idx, d_slots, d_cnt, d_ctr);
+        HGX_CHECK_LAUNCH();
+    }
+    if (g->timing) HGX_HIP(hipEventRecord(ev[2], s));
+    // per-chunk hit counts -> exclusive output offsets
+    {
+        size_t sb = 0;
+        HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, d_cnt, d_outoff, nc + 1, s));
+        void* d_sc2 = dalloc(sb);
+        HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_sc2, sb, d_cnt, d_outoff, nc + 1, s));
+    }
+    int64_t total = 0;
+    HGX_HIP(hipMemcpyAsync(&total, d_outoff + n_chunks, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_outoff, d_qoff);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipMemcpyAsync(r->offsets.data(), d_qoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    r->ids.resize((size_t)std::max<int64_t>(total, 0));
+    if (total > 0) {
+        int32_t* d_out = (int32_t*)dalloc(sizeof(int32_t) * total);
+        hgx_q_scatter<<<(unsigned)ceil_div((int64_t)n_chunks * 64, 256), 256, 0, s>>>(n_chunks, d_cnt, d_outoff,
+                                                                                       d_slots, g->link_atom, d_out);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipMemcpyAsync(r->ids.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, s));
+    }
+    if (g->timing) HGX_HIP(hipEventRecord(ev[3], s));
+    u64 hctr[qNum];
+    HGX_HIP(hipMemcpyAsync(hctr, d_ctr, sizeof(hctr), hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    if (g->timing) {
+        float a = 0, b = 0;
+        HGX_HIP(hipEventElapsedTime(&a, ev[0], ev[3]));
+        HGX_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
+        r->ms_total = a;
+        r->ms_match = b;
+    }
+    // algorithmic bytes of hgx_pattern_match: plan + per candidate inc_row + link_type,
+    // per type-passing candidate its tgt_off pair and target row, 4 B per hit, 4 B per chunk count
+    {
+        double anchors_bytes = 4.0 * anchors.size() + 16.0 * anchors.size() + 4.0 * pattern.size();
+        r->bytes_match = 8.0 * (double)hctr[qCand] + 16.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
+                         4.0 * (double)hctr[qHits] + 4.0 * (double)n_chunks + anchors_bytes;
+    }
+    guard.r = nullptr;
+    *out = r;
+    HGX_API_END
+}
+
+int hgx_query_result_offsets(const hgx_query_result* r, int64_t* offsets) {
+    HGX_API_BEGIN
+    if (!r || !offsets) fail(HGX_E_INVALID, "hgx_query_result_offsets: bad argument");
+    std::memcpy(offsets, r->offsets.data(), sizeof(int64_t) * r->offsets.size());
+    HGX_API_END
+}
+
+int hgx_query_result_ids(const hgx_query_result* r, int32_t* ids) {
+    HGX_API_BEGIN
+    if (!r || (!ids && !r->ids.empty())) fail(HGX_E_INVALID, "hgx_query_result_ids: bad argument");
+    if (!r->ids.empty()) std::memcpy(ids, r->ids.data(), sizeof(int32_t) * r->ids.size());
+    HGX_API_END
+}
+
+int hgx_query_result_ms(const hgx_query_result* r, double* ms_total, double* ms_match, double* bytes_match) {
+    HGX_API_BEGIN
+    if (!r) fail(HGX_E_INVALID, "null result");
+    if (ms_total) *ms_total = r->ms_total;
+    if (ms_match) *ms_match = r->ms_match;
+    if (bytes_match) *bytes_match = r->bytes_match;
+    HGX_API_END
+}
+
+void hgx_query_result_free(hgx_query_result* r) { delete r; }
+
+}  // extern "C"

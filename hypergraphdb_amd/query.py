@@ -1,0 +1,277 @@
+"""GPU-backed And-condition evaluation behind the reference's query API.
+
+Reference (C = core/src/java/org/hypergraphdb):
+  * HGQuery.hg DSL: hg.and / hg.type / hg.incident / hg.orderedLink / hg.anyHandle /
+    hg.bfs / hg.subsumed / hg.subsumes / hg.apply(hg.targetAt)   (C/HGQuery.java:364-1823)
+  * ConditionToQuery (C/query/cond2qry/ConditionToQuery.java:14-18) registered per graph with
+    HGQueryConfiguration.addCompiler (C/query/HGQueryConfiguration.java:48) -- consulted before
+    ToQueryMap by QueryCompile.translator (C/query/QueryCompile.java:80-87).
+  * ExpressionBasedQuery.expand (C/query/cond2qry/ExpressionBasedQuery.java:689-737) flattening
+    nested And and adding incident(x) for every non-ANY orderedLink target.
+  * SubsumedCondition / SubsumesCondition -> BFS over HGSubsumes links
+    (C/query/cond2qry/ToQueryMap.java:282-370).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import HGXUnsupported, check, lib, ptr
+from .algorithms import AtomTypeCondition, DefaultALGenerator, HGException, bfs_batch
+
+ANY = _lib.HGX_ANY_HANDLE
+
+
+class IncidentCondition:
+    def __init__(self, target):
+        self.target = int(target)
+
+    def __eq__(self, o):
+        return isinstance(o, IncidentCondition) and o.target == self.target
+
+    def __hash__(self):
+        return hash(("incident", self.target))
+
+    def __repr__(self):
+        return f"incident({self.target})"
+
+
+class OrderedLinkCondition:
+    def __init__(self, *targets):
+        if len(targets) == 1 and isinstance(targets[0], (list, tuple)):
+            targets = tuple(targets[0])
+        self.targets = tuple(int(t) for t in targets)
+
+    def satisfies(self, snapshot, link) -> bool:
+        """C/query/OrderedLinkCondition.java:92-124 (host form, used by the API, not the batch path)."""
+        if snapshot.row_of(link) < 0:
+            return False
+        tg = snapshot.targets(link)
+        i = j = 0
+        while i < len(tg) and j < len(self.targets):
+            if self.targets[j] == ANY or self.targets[j] == tg[i]:
+                j += 1
+            i += 1
+        return j == len(self.targets)
+
+    def __repr__(self):
+        return f"orderedLink{self.targets}"
+
+
+class And(list):
+    def __repr__(self):
+        return "and(" + ", ".join(map(repr, self)) + ")"
+
+
+class MapCondition:
+    """hg.apply(mapping, cond)"""
+
+    def __init__(self, mapping, cond):
+        self.mapping, self.cond = mapping, cond
+
+
+class TargetAt:
+    """hg.targetAt(graph, i): link -> its i-th target."""
+
+    def __init__(self, snapshot, pos):
+        self.snapshot, self.pos = snapshot, int(pos)
+
+    def __call__(self, link):
+        tg = self.snapshot.targets(link)
+        return int(tg[self.pos]) if self.pos < len(tg) else None
+
+
+class BFSCondition:
+    def __init__(self, start, link_predicate=None, return_preceding=True, return_succeeding=True,
+                 reverse_order=False, max_distance=None):
+        self.start = int(start)
+        self.link_predicate = link_predicate
+        self.flags = (return_preceding, return_succeeding, reverse_order)
+        self.max_distance = max_distance
+
+
+class hg:
+    """The subset of HGQuery.hg on the accelerated path."""
+
+    @staticmethod
+    def type(t):
+        return AtomTypeCondition(t)
+
+    @staticmethod
+    def incident(h):
+        return IncidentCondition(h)
+
+    @staticmethod
+    def orderedLink(*targets):
+        return OrderedLinkCondition(*targets)
+
+    @staticmethod
+    def anyHandle():
+        return ANY
+
+    @staticmethod
+    def and_(*conds):
+        return And(conds)
+
+    @staticmethod
+    def bfs(start, link_predicate=None, return_preceding=True, return_succeeding=True, reverse_order=False):
+        return BFSCondition(start, link_predicate, return_preceding, return_succeeding, reverse_order)
+
+    @staticmethod
+    def subsumed(general, subsumes_type):
+        """descendants: BFS(G) over HGSubsumes links, preceding=False, succeeding=True (ToQueryMap.java:340-370)"""
+        return BFSCondition(general, AtomTypeCondition(subsumes_type), False, True, False)
+
+    @staticmethod
+    def subsumes(specific, subsumes_type):
+        """ancestors: the same with reverseOrder=True (ToQueryMap.java:282-312)"""
+        return BFSCondition(specific, AtomTypeCondition(subsumes_type), False, True, True)
+
+    @staticmethod
+    def apply(mapping, cond):
+        return MapCondition(mapping, cond)
+
+    @staticmethod
+    def targetAt(snapshot, pos):
+        return TargetAt(snapshot, pos)
+
+
+def _flatten(cond, out):
+    if isinstance(cond, And):
+        for c in cond:
+            _flatten(c, out)
+    else:
+        out.append(cond)
+    return out
+
+
+def normalize(cond):
+    """And{type?, incident*, orderedLink?} -> (type, incident list, pattern or None); raises
+    HGXUnsupported for any other shape (a Java shim delegates those to AndToQuery)."""
+    if isinstance(cond, (IncidentCondition, OrderedLinkCondition, AtomTypeCondition)):
+        cond = And([cond])
+    if not isinstance(cond, And):
+        raise HGXUnsupported(_lib.HGX_E_UNSUPPORTED, f"not an And: {cond!r}")
+    subs = _flatten(cond, [])
+    types = [c for c in subs if isinstance(c, AtomTypeCondition)]
+    incs = [c for c in subs if isinstance(c, IncidentCondition)]
+    ords = [c for c in subs if isinstance(c, OrderedLinkCondition)]
+    if len(types) + len(incs) + len(ords) != len(subs) or len(ords) > 1:
+        raise HGXUnsupported(_lib.HGX_E_UNSUPPORTED, f"shape not accelerated: {cond!r}")
+    tset = {t.type for t in types}
+    if len(tset) > 1:
+        return "empty", None, None       # two different exact types: nothing satisfies both
+    t = types[0].type if types else _lib.HGX_NO_TYPE
+    pattern = ords[0].targets if ords else None
+    return t, [c.target for c in incs], pattern
+
+
+class QueryResult:
+    def __init__(self, offsets, ids, ms=None):
+        self.offsets, self.ids, self.ms = offsets, ids, ms
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+    def __getitem__(self, q):
+        return self.ids[self.offsets[q]:self.offsets[q + 1]]
+
+
+def pattern_batch(snapshot, queries) -> QueryResult:
+    """Evaluate many And{type?, incident*, orderedLink?} queries in one GPU launch sequence.
+    ``queries``: conditions or (type, incident, pattern) tuples."""
+    norm = [q if isinstance(q, tuple) else normalize(q) for q in queries]
+    n = len(norm)
+    keep = []
+    arr = (_lib.AndQuery * max(n, 1))()
+    empty = np.zeros(n, bool)
+    for i, (t, inc, pat) in enumerate(norm):
+        if t == "empty":
+            empty[i] = True
+            t, inc, pat = _lib.HGX_NO_TYPE, [], []
+            inc = [0]
+        ia = np.ascontiguousarray(list(inc) or [0], np.int32)
+        pa = np.ascontiguousarray(list(pat) if pat else [0], np.int32)
+        keep += [ia, pa]
+        arr[i] = _lib.AndQuery(int(t), len(inc), ptr(ia), int(pat is not None), len(pat or ()), ptr(pa))
+    h = C.c_void_p()
+    check(lib().hgx_pattern_batch(snapshot.handle, arr, n, C.byref(h)))
+    try:
+        off = np.zeros(n + 1, np.int64)
+        check(lib().hgx_query_result_offsets(h, ptr(off)))
+        ids = np.zeros(max(int(off[-1]), 1), np.int32)
+        check(lib().hgx_query_result_ids(h, ptr(ids)))
+        a, b, c = C.c_double(), C.c_double(), C.c_double()
+        check(lib().hgx_query_result_ms(h, C.byref(a), C.byref(b), C.byref(c)))
+    finally:
+        lib().hgx_query_result_free(h)
+    ids = ids[: int(off[-1])]
+    if empty.any():   # drop the placeholder queries' results
+        parts = [np.empty(0, np.int32) if empty[i] else ids[off[i]:off[i + 1]] for i in range(n)]
+        off = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64)
+        ids = np.concatenate(parts).astype(np.int32) if parts else ids
+    return QueryResult(off, ids, {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+
+
+class QueryMetaData:
+    """C/query/cond2qry/QueryMetaData.java -- ORACCESS for the accelerated And."""
+
+    def __init__(self, ordered=True, random_access=True, predicate_cost=-1):
+        self.ordered, self.randomAccess, self.predicateCost = ordered, random_access, predicate_cost
+
+
+class GpuAndToQuery:
+    """ConditionToQuery for And, registered with HGQueryConfiguration.addCompiler(And, ...)."""
+
+    def getQuery(self, snapshot, cond):
+        norm = normalize(cond)
+
+        class _Q:
+            def execute(_self):
+                return list(pattern_batch(snapshot, [norm])[0].tolist())
+
+        return _Q()
+
+    def getMetaData(self, snapshot, cond):
+        normalize(cond)
+        return QueryMetaData(True, True, -1)
+
+
+class HGQueryConfiguration:
+    """Per-graph compiler registry (C/query/HGQueryConfiguration.java:37-66)."""
+
+    def __init__(self):
+        self._compilers = {}
+
+    def addCompiler(self, cls, compiler):
+        self._compilers[cls] = compiler
+
+    def compiler(self, cls):
+        return self._compilers.get(cls)
+
+
+def find_all(snapshot, cond, config: HGQueryConfiguration | None = None):
+    """hg.findAll(graph, cond) for the accelerated shapes."""
+    if isinstance(cond, BFSCondition):
+        lp = cond.link_predicate
+        gen = DefaultALGenerator(snapshot, lp, None, *cond.flags)
+        res = bfs_batch(snapshot, [cond.start], cond.max_distance, gen)
+        try:
+            return sorted(int(a) for d in range(1, res.n_levels) for a in res.visited(0, d))
+        finally:
+            res.close()
+    if isinstance(cond, MapCondition):
+        return sorted({v for v in (cond.mapping(x) for x in find_all(snapshot, cond.cond, config)) if v is not None})
+    if isinstance(cond, And):
+        subs = _flatten(cond, [])
+        if any(isinstance(c, (MapCondition, BFSCondition)) for c in subs):
+            # And of mapped / traversal sub-queries: set intersection of the parts
+            sets = [set(find_all(snapshot, c, config)) for c in subs if isinstance(c, (MapCondition, BFSCondition))]
+            rest = [c for c in subs if not isinstance(c, (MapCondition, BFSCondition))]
+            if rest:
+                sets.append(set(find_all(snapshot, And(rest), config)))
+            return sorted(set.intersection(*sets))
+    compiler = (config.compiler(And) if config else None) or GpuAndToQuery()
+    return compiler.getQuery(snapshot, cond).execute()

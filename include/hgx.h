@@ -1,0 +1,163 @@
+/*
+ * hgx.h -- C ABI of the MI355X engine for HyperGraphDB's data-parallel query path.
+ *
+ * Plain pointers and sizes only; no C++ or torch types.  Every entry point returns an
+ * int status (HGX_OK = 0) and never throws or aborts across the ABI; the message of the
+ * last failure on the calling thread is hgx_last_error().  All entry points are
+ * thread-safe (one mutex per graph; calls on one graph are serialised).
+ *
+ * Reference interfaces replaced (paths relative to the reference root,
+ * C = core/src/java/org/hypergraphdb):
+ *   hgx_graph_create      <- the HGStore incidence index + link records read by
+ *                            HyperGraph.getIncidenceSet (C/HyperGraph.java:1415-1418) and
+ *                            HGStore.getLink (C/HGStore.java:179-191), snapshotted once.
+ *   hgx_bfs_batch         <- HGBreadthFirstTraversal(start, DefaultALGenerator, maxDistance)
+ *                            (C/algorithms/HGBreadthFirstTraversal.java:122-164) driven to
+ *                            exhaustion, for many start atoms at once; HGTraversal
+ *                            (C/algorithms/HGTraversal.java:36-63).
+ *   hgx_pattern_batch     <- ConditionToQuery.getQuery for And (C/query/cond2qry/AndToQuery.java:102-306)
+ *                            on And{AtomTypeCondition?, IncidentCondition*, OrderedLinkCondition?}
+ *                            after ExpressionBasedQuery.expand (:603-762), executed
+ *                            (ZigZagIntersectionResult + PredicateBasedFilter), for many queries.
+ *
+ * Identity: every atom (node or link) is an int32 id = its rank in persistent-handle
+ * byte order (C/handle/UUID.java:364-376; IntPersistentHandle via C/storage/BAUtils.java:55-80).
+ * Rank order preserves every sorted list of the reference, so GPU result order is the
+ * reference's result order.  The caller keeps the rank -> handle table.
+ */
+#ifndef HGX_H
+#define HGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGX_OK              0
+#define HGX_E_INVALID      -1   /* bad argument (null pointer, id out of range, unsorted ranks) */
+#define HGX_E_DEVICE       -2   /* HIP runtime / kernel failure                               */
+#define HGX_E_NOMEM        -3   /* device or host allocation failed                           */
+#define HGX_E_UNSUPPORTED  -4   /* shape not accelerated: the caller falls back to the CPU path */
+#define HGX_E_NOTFOUND     -5   /* no such seed / depth / query in a result                  */
+
+#define HGX_ANY_HANDLE     (-1) /* hg.anyHandle() inside an ordered pattern                  */
+#define HGX_NO_TYPE        (-1) /* no AtomTypeCondition / no link predicate                  */
+#define HGX_UNBOUNDED      (-1) /* maxDistance == Integer.MAX_VALUE                          */
+
+typedef struct hgx_graph hgx_graph;
+typedef struct hgx_bfs_result hgx_bfs_result;
+typedef struct hgx_query_result hgx_query_result;
+
+/* Snapshot of the store.  Link row r (0..num_links-1) is atom link_atom[r] (strictly
+ * ascending); its layout is [type, value, t0..tk-1] (C/HyperGraph.java:1603-1608) of
+ * which link_type[r] = type key and tgt_idx[tgt_off[r] .. tgt_off[r+1]) = t0..tk-1.
+ * Targets may be links.  The incidence index (atom -> incident links) is derived on the
+ * device: one entry per distinct (target, link), ascending (BJE putNoDupData + sorted
+ * duplicates, storage/bdb-je/.../BJEStorageImplementation.java:109-111,300-307).
+ * All arrays are deep-copied; the caller may free them on return. */
+typedef struct hgx_graph_desc {
+    int64_t        num_atoms;   /* A: nodes + links                                 */
+    int64_t        num_links;   /* M                                                */
+    const int32_t *link_atom;   /* [M]                                              */
+    const int64_t *tgt_off;     /* [M+1]                                            */
+    const int32_t *tgt_idx;     /* [tgt_off[M]]                                     */
+    const int32_t *link_type;   /* [M] type key (>= 0), or NULL = all 0             */
+} hgx_graph_desc;
+
+/* DefaultALGenerator configuration (C/algorithms/DefaultALGenerator.java:437-502).
+ * link_type: HGX_NO_TYPE = linkPredicate null, else AtomTypeCondition(type) on the
+ * incident link (C/query/AtomTypeCondition.java:121-135).  A siblingPredicate or any
+ * other link predicate is not accelerated (the caller keeps the CPU traversal). */
+typedef struct hgx_algen_opts {
+    int32_t link_type;
+    uint8_t return_preceding;    /* default 1 */
+    uint8_t return_succeeding;   /* default 1 */
+    uint8_t reverse_order;       /* default 0 */
+    uint8_t return_source;       /* default 0 */
+} hgx_algen_opts;
+
+/* One And{type?, incident*, orderedLink?} query after ExpressionBasedQuery.expand. */
+typedef struct hgx_and_query {
+    int32_t        type;         /* HGX_NO_TYPE or the AtomTypeCondition type key        */
+    int32_t        n_incident;   /* IncidentCondition targets                           */
+    const int32_t *incident;
+    int32_t        has_ordered;  /* 0: no OrderedLinkCondition                          */
+    int32_t        n_pattern;    /* OrderedLinkCondition targets (HGX_ANY_HANDLE = any) */
+    const int32_t *pattern;
+} hgx_and_query;
+
+/* Device-timed breakdown of one hgx_bfs_batch (kernel times are filled when timing is enabled,
+ * hgx_set_timing(g, 1)).  Per-kernel arrays are indexed by HGX_K_*.  Bytes are the algorithmic
+ * bytes of the implemented kernels; bytes_survey follows SURVEY.md 8(d)'s
+ * push model.  traversed_edges is the hyperedge-TEPS numerator
+ * sum_s sum_{d<D} sum_{v in F_sd} |inc(v)|. */
+#define HGX_K_LINK_GATHER   0   /* hgx_link_gather          */
+#define HGX_K_ATOM_PULL     1   /* hgx_atom_pull            */
+#define HGX_K_PULL_HEAVY    2   /* hgx_atom_pull_heavy      */
+#define HGX_K_HUB_FINALIZE  3   /* hgx_hub_finalize         */
+#define HGX_K_COUNT         4
+typedef struct hgx_bfs_stats {
+    int32_t n_levels_expanded;
+    int32_t n_batches;
+    double  ms_total;                  /* first kernel -> last level counter D2H, device events */
+    double  ms_kernel[HGX_K_COUNT];    /* summed over launches                                 */
+    int64_t launches[HGX_K_COUNT];
+    double  bytes_kernel[HGX_K_COUNT]; /* algorithmic bytes, summed over launches             */
+    double  bytes_survey;
+    double  traversed_edges;
+    int64_t union_frontier[64];        /* |U_d| per expanded level (summed over batches)       */
+} hgx_bfs_stats;
+
+const char *hgx_version(void);
+const char *hgx_last_error(void);
+
+/* device: HIP device ordinal to place the snapshot on. */
+int  hgx_graph_create(const hgx_graph_desc *desc, int32_t device, hgx_graph **out);
+void hgx_graph_destroy(hgx_graph *g);
+int  hgx_graph_info(const hgx_graph *g, int64_t *num_atoms, int64_t *num_links, int64_t *num_incidences);
+/* |inc(atom)| for n atoms (HyperGraph.getIncidenceSet(h).size()). */
+int  hgx_graph_degree(hgx_graph *g, const int32_t *atoms, int32_t n, int64_t *out_deg);
+/* inc(atom) as link ATOM ids, ascending; *n_out = |inc(atom)| even when > cap. */
+int  hgx_graph_incidence(hgx_graph *g, int32_t atom, int32_t *out, int64_t cap, int64_t *n_out);
+int  hgx_set_timing(hgx_graph *g, int32_t enabled);
+
+/* Batched multi-source BFS.  Seed i is HGBreadthFirstTraversal(seeds[i], gen, max_depth)
+ * (max_depth HGX_UNBOUNDED = Integer.MAX_VALUE).  The result holds, per seed and per
+ * distance d, the set V_d of atoms returned by next() at distance d (V_0 = {seed}),
+ * which is the reference's per-depth visited set. */
+int  hgx_bfs_batch(hgx_graph *g, const int32_t *seeds, int32_t n_seeds, int32_t max_depth,
+                   const hgx_algen_opts *opts, hgx_bfs_result **out);
+/* n_levels = 1 + the largest distance reached by any seed. */
+int  hgx_bfs_result_info(const hgx_bfs_result *r, int32_t *n_seeds, int32_t *n_levels);
+/* counts[i * n_levels + d] = |V_d| of seed i. */
+int  hgx_bfs_result_counts(hgx_bfs_result *r, int64_t *counts);
+/* V_d of seed i, ascending atom ids; *n_out = |V_d| even when > cap. */
+int  hgx_bfs_result_visited(hgx_bfs_result *r, int32_t seed_index, int32_t depth,
+                            int32_t *out, int64_t cap, int64_t *n_out);
+/* isVisited after draining (C/algorithms/HGBreadthFirstTraversal.java:137-141):
+ * *depth_out = distance of atom from seed i, or -1 when never reached. */
+int  hgx_bfs_result_depth_of(hgx_bfs_result *r, int32_t seed_index, int32_t atom, int32_t *depth_out);
+/* with_accounting = 0: timing and algorithmic bytes only (cheap); 1: also run the accounting
+ * kernels for traversed_edges, bytes_survey and union_frontier (reads every level once). */
+int  hgx_bfs_result_stats(hgx_bfs_result *r, int32_t with_accounting, hgx_bfs_stats *stats);
+void hgx_bfs_result_free(hgx_bfs_result *r);
+
+/* Batched conjunctive pattern queries.  Result of query q = the link atoms L with
+ * type(L) == type, every incident/pattern anchor in targets(L) and
+ * OrderedLinkCondition(pattern) true on targets(L), ascending.  A query with no
+ * incidence anchor returns HGX_E_UNSUPPORTED for the whole batch (the caller keeps
+ * AndToQuery, which scans the type index). */
+int  hgx_pattern_batch(hgx_graph *g, const hgx_and_query *queries, int32_t n,
+                       hgx_query_result **out);
+/* offsets[n+1]: results of query q are ids[offsets[q] .. offsets[q+1]). */
+int  hgx_query_result_offsets(const hgx_query_result *r, int64_t *offsets);
+int  hgx_query_result_ids(const hgx_query_result *r, int32_t *ids);
+/* device milliseconds of the last pattern batch (timing enabled). */
+int  hgx_query_result_ms(const hgx_query_result *r, double *ms_total, double *ms_match, double *bytes_match);
+void hgx_query_result_free(hgx_query_result *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,92 @@
+"""CPU tests of the boundary: libhgx.so loads and exports every symbol include/hgx.h declares;
+host-side logic (handle ranking, And normalisation, generator determinism).  No GPU compute."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "hgx.h")).read()
+    return sorted(set(re.findall(r"\b(hgx_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from hypergraphdb_amd import _lib
+    L = C.CDLL(_lib.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_lib.EXPORTED) == syms
+
+
+def test_exports_are_c_abi():
+    """extern "C": the exported names are unmangled."""
+    out = os.popen(f"nm -D --defined-only {os.path.join(ROOT, 'hypergraphdb_amd', 'libhgx.so')}").read()
+    for s in header_symbols():
+        assert re.search(rf"\sT {s}$", out, re.M), s
+
+
+def test_version_and_error_without_gpu():
+    from hypergraphdb_amd import _lib
+    L = _lib.lib()
+    assert L.hgx_version().decode().startswith("hgx ")
+    # a null descriptor is rejected with a status, never a crash
+    h = C.c_void_p()
+    assert L.hgx_graph_create(None, 0, C.byref(h)) == _lib.HGX_E_INVALID
+    assert b"null" in L.hgx_last_error()
+
+
+def test_handle_ranking_is_byte_order():
+    """IntPersistentHandle bytes = x ^ 0x80000000 big-endian (BAUtils.java:69-80): rank == int order;
+    UUID handles: unsigned lexicographic (UUID.java:364-376)."""
+    from hypergraphdb_amd.snapshot import handle_bytes, rank_handles
+    ints = [1000, -5, 7, 2**31 - 1, -2**31, 0]
+    r = rank_handles(ints)
+    assert [h for h, _ in sorted(r.items(), key=lambda kv: kv[1])] == sorted(ints)
+    assert handle_bytes(1000) == bytes([0x80, 0x00, 0x03, 0xE8])
+    uu = [bytes([0xFF] + [0] * 15), bytes([0x01] + [0] * 15), bytes([0x7F] + [9] * 15)]
+    r = rank_handles(uu)
+    assert r[uu[1]] == 0 and r[uu[2]] == 1 and r[uu[0]] == 2
+
+
+def test_and_normalisation():
+    from hypergraphdb_amd import HGXUnsupported, hg
+    from hypergraphdb_amd.query import normalize
+    t, inc, pat = normalize(hg.and_(hg.type(3), hg.incident(5), hg.and_(hg.orderedLink(1, hg.anyHandle(), 2))))
+    assert t == 3 and inc == [5] and pat == (1, -1, 2)
+    with pytest.raises(HGXUnsupported):
+        normalize(hg.and_(hg.orderedLink(1), hg.orderedLink(2)))
+    assert normalize(hg.and_(hg.type(1), hg.type(2), hg.incident(0)))[0] == "empty"
+
+
+def test_generator_deterministic_and_valid():
+    from hypergraphdb_amd import synth
+    a = synth.hypergraph(1000, 3000, 2, 8, 2.1, 4, seed=42)
+    b = synth.hypergraph(1000, 3000, 2, 8, 2.1, 4, seed=42)
+    for k in ("tgt_off", "tgt_idx", "link_type"):
+        assert np.array_equal(a[k], b[k])
+    off, tg = a["tgt_off"], a["tgt_idx"]
+    assert tg.min() >= 0 and tg.max() < 1000
+    ar = np.diff(off)
+    assert ar.min() >= 2 and ar.max() <= 8
+    for r in range(0, 3000, 97):   # distinct targets within a link
+        row = tg[off[r]:off[r + 1]]
+        assert len(set(row.tolist())) == len(row)
+    # power law: node 0 is the heaviest
+    deg = np.bincount(tg, minlength=1000)
+    assert deg[0] == deg.max()
+
+
+def test_generator_ontology_shape():
+    from hypergraphdb_amd import synth
+    g = synth.config5(scale=1e-3)
+    tg = g["tgt_idx"].reshape(-1, 2)
+    sub = g["link_type"] == g["subsumes_type"]
+    assert (tg[sub, 0] < tg[sub, 1]).all()          # parents have lower ids (a DAG)
+    assert (tg[:, 0] != tg[:, 1]).all()

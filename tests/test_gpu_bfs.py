@@ -1,0 +1,225 @@
+"""GPU parity: batched BFS through the C ABI against the oracle / golden fixtures (bit-exact
+per-depth visited sets)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import kat_graphs as K
+from oracle_ctypes import OracleGraph, algen
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def snapshot(g):
+    from hypergraphdb_amd import HyperGraphSnapshot
+    return HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g.get("link_type"))
+
+
+def oracle(g):
+    return OracleGraph(g["num_atoms"], np.asarray(g["link_atom"], np.int32), np.asarray(g["tgt_off"], np.int64),
+                       np.asarray(g["tgt_idx"], np.int32),
+                       None if g.get("link_type") is None else np.asarray(g["link_type"], np.int32))
+
+
+def gen(snap, mode, lt=-1):
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator
+    P, S, R, RS = mode
+    return DefaultALGenerator(snap, None if lt < 0 else AtomTypeCondition(lt), None, P, S, R, RS)
+
+
+def levels_from_seq(seed, seq):
+    d = {0: [seed]}
+    for _, a, k in seq:
+        d.setdefault(k, []).append(a)
+    n = max(d) + 1
+    return [sorted(d.get(k, [])) for k in range(n)]
+
+
+def gpu_levels(res, i):
+    lv = [res.visited(i, d).tolist() for d in range(res.n_levels)]
+    while len(lv) > 1 and not lv[-1]:
+        lv.pop()
+    return lv
+
+
+def check_batch(g, seeds, maxd, mode, lt=-1, snap=None, orc=None):
+    from hypergraphdb_amd import bfs_batch
+    snap = snap or snapshot(g)
+    orc = orc or oracle(g)
+    res = bfs_batch(snap, seeds, maxd, gen(snap, mode, lt))
+    counts = res.counts()
+    for i, s in enumerate(seeds):
+        l, a, d, _ = orc.bfs(int(s), -1 if maxd is None else maxd, algen(lt, *mode))
+        exp = levels_from_seq(int(s), zip(l.tolist(), a.tolist(), d.tolist()))
+        got = gpu_levels(res, i)
+        assert got == exp, (i, s, mode, maxd, lt)
+        assert counts[i, :len(exp)].tolist() == [len(x) for x in exp]
+        assert counts[i, len(exp):].sum() == 0
+    res.close()
+
+
+def test_kat_fixture_graphs_every_seed_every_mode():
+    with open(os.path.join(GOLD, "kat.json")) as f:
+        kat = json.load(f)
+    for name, e in kat.items():
+        g = {k: np.asarray(v) if isinstance(v, list) else v for k, v in e.items() if k not in ("bfs", "incidence")}
+        snap = snapshot(g)
+        from hypergraphdb_amd import bfs_batch
+        seeds = list(range(g["num_atoms"]))
+        for a, inc in e["incidence"].items():
+            assert snap.incidence(int(a)).tolist() == inc
+        for mi, mode in enumerate(K.ALGEN_MODES):
+            for maxd in (None, 1, 2):
+                res = bfs_batch(snap, seeds, maxd, gen(snap, mode))
+                for s in seeds:
+                    exp = levels_from_seq(s, e["bfs"][f"{s}/{mi}/{maxd}"])
+                    assert gpu_levels(res, s) == exp, (name, s, mode, maxd)
+                res.close()
+        snap.close()
+
+
+def test_kat_linkage_reaches_x3():
+    from hypergraphdb_amd import find_all, hg
+    g = K.linkage_graph()
+    snap = snapshot(g)
+    assert g["names"]["x3"] in find_all(snap, hg.bfs(g["names"]["x1"]))
+
+
+def test_random_fixture_graphs():
+    d = np.load(os.path.join(GOLD, "random_small.npz"))
+    gi = 0
+    while f"g{gi}_A" in d:
+        g = dict(num_atoms=int(d[f"g{gi}_A"][0]), link_atom=d[f"g{gi}_link_atom"], tgt_off=d[f"g{gi}_tgt_off"],
+                 tgt_idx=d[f"g{gi}_tgt_idx"], link_type=d[f"g{gi}_link_type"])
+        snap = snapshot(g)
+        from hypergraphdb_amd import bfs_batch
+        pos = 0
+        seq_all = d[f"g{gi}_bfs_seq"].tolist()
+        for seed, mi, lt, maxd, n in d[f"g{gi}_bfs_keys"].tolist():
+            res = bfs_batch(snap, [seed], None if maxd < 0 else maxd, gen(snap, K.ALGEN_MODES[mi], lt))
+            assert gpu_levels(res, 0) == levels_from_seq(seed, seq_all[pos:pos + n])
+            pos += n
+            res.close()
+        snap.close()
+        gi += 1
+
+
+def test_config1_golden_all_64_seeds():
+    """64 seeds, depth 3, per-depth sets bit-identical to the fixture."""
+    from hypergraphdb_amd import bfs_batch, synth
+    fx = np.load(os.path.join(GOLD, "config1.npz"))
+    g = synth.config1()
+    snap = snapshot(g)
+    res = bfs_batch(snap, g["seeds"], 3)
+    off, ids = fx["level_off"], fx["level_ids"]
+    k = 0
+    for i in range(64):
+        for depth in range(4):
+            exp = ids[off[k]:off[k + 1]]
+            got = res.visited(i, depth) if depth < res.n_levels else np.empty(0, np.int32)
+            assert np.array_equal(got, exp), (i, depth)
+            k += 1
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_random_graphs_all_modes_multi_batch(case):
+    """Links targeting links, repeated targets, arity 0/1 links, random rank interleaving, typed link
+    predicates, duplicate seeds, batches not a multiple of 64 and > 1024 seeds (several batches)."""
+    rng = np.random.default_rng(500 + case)
+    g = K.random_graph(rng, int(rng.integers(200, 2000)), int(rng.integers(200, 3000)), max_arity=7,
+                       link_targets=case % 2 == 0, n_types=3)
+    snap, orc = snapshot(g), oracle(g)
+    mode = K.ALGEN_MODES[case % len(K.ALGEN_MODES)]
+    n_seeds = [1, 63, 64, 65, 200, 1024, 1100, 2100][case]
+    seeds = rng.integers(0, g["num_atoms"], n_seeds).astype(np.int32)
+    lt = [-1, 0, 1, -1, 2, -1, 0, -1][case]
+    maxd = [None, 2, 3, None, 1, 4, None, 2][case]
+    check_batch(g, seeds, maxd, mode, lt, snap, orc)
+
+
+def test_heavy_atoms_power_law():
+    """Hubs with > 512 incident links take the chunked workgroup path; results stay exact."""
+    from hypergraphdb_amd import synth
+    g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=11)
+    deg = np.bincount(g["tgt_idx"], minlength=g["num_atoms"])
+    assert deg.max() > 4096            # several chunks for the top hub
+    snap, orc = snapshot(g), oracle(g)
+    seeds = np.concatenate([np.arange(5), np.arange(2900, 3000)]).astype(np.int32)
+    for mode in (K.ALGEN_MODES[0], K.ALGEN_MODES[1], K.ALGEN_MODES[4]):
+        check_batch(g, seeds, 3, mode, -1, snap, orc)
+    check_batch(g, seeds, None, K.ALGEN_MODES[0], 1, snap, orc)
+
+
+def test_config2_scaled_counts_and_sets():
+    """Config 2 shape (Chung-Lu gamma 2.1, arity 2..8) at 1% scale, 1024 seeds, depth 4:
+    every seed's per-depth counts equal the oracle's; full sets for 6 sampled seeds."""
+    from hypergraphdb_amd import bfs_batch, synth
+    g = synth.config2(scale=0.01)
+    snap, orc = snapshot(g), oracle(g)
+    res = bfs_batch(snap, g["seeds"], 4)
+    counts = res.counts()
+    oc, trav = orc.bfs_many(g["seeds"], 4, 5)
+    assert np.array_equal(counts[:, :5], oc)
+    st = res.stats()
+    assert st["traversed_edges"] == float(trav.sum())      # the TEPS numerator is exact
+    for i in (0, 1, 100, 511, 512, 1023):
+        lv = orc.bfs_levels(int(g["seeds"][i]), 4)
+        for d_, exp in enumerate(lv):
+            assert np.array_equal(res.visited(i, d_), exp), (i, d_)
+
+
+def test_subsumption_config5_scaled():
+    """hg.subsumed / hg.subsumes: unbounded BFS over HGSubsumes links only (ToQueryMap.java:282-370)."""
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, bfs_batch, synth
+    g = synth.config5(scale=0.002, n_sources=300)
+    snap, orc = snapshot(g), oracle(g)
+    T = g["subsumes_type"]
+    for reverse in (False, True):
+        gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, reverse)
+        res = bfs_batch(snap, g["seeds"], None, gen_)
+        counts = res.counts()
+        oc, _ = orc.bfs_many(g["seeds"], -1, res.n_levels + 1, algen(T, False, True, reverse, False))
+        assert np.array_equal(counts, oc[:, :res.n_levels])
+        assert oc[:, res.n_levels:].sum() == 0
+        for i in (0, 7, 299):
+            lv = orc.bfs_levels(int(g["seeds"][i]), -1, algen(T, False, True, reverse, False))
+            for d_, exp in enumerate(lv):
+                assert np.array_equal(res.visited(i, d_), exp)
+        res.close()
+
+
+def test_traversal_api_and_is_visited():
+    from hypergraphdb_amd import DefaultALGenerator, HGBreadthFirstTraversal
+    g = K.queries_graph()
+    snap = snapshot(g)
+    n = g["names"]
+    tr = HGBreadthFirstTraversal(n["linkH"], DefaultALGenerator(snap))
+    seen = []
+    while tr.hasNext():
+        link, atom = tr.next()
+        assert atom in snap.targets(link).tolist()
+        assert tr.isVisited(atom)
+        seen.append(atom)
+    orc = oracle(g)
+    _, a, _, _ = orc.bfs(n["linkH"], -1)
+    assert sorted(seen) == sorted(a.tolist())
+    with pytest.raises(NotImplementedError):
+        tr.remove()
+
+
+def test_depth_of_and_errors():
+    from hypergraphdb_amd import HGXError, bfs_batch
+    g = K.queries_graph()
+    snap = snapshot(g)
+    res = bfs_batch(snap, [g["names"]["n0"], g["names"]["n10"]], None)
+    assert res.depth_of(0, g["names"]["n0"]) == 0
+    assert res.depth_of(0, g["names"]["n1"]) == 1
+    assert res.depth_of(1, g["names"]["n0"]) == -1      # n10 has no incident link
+    assert res.counts()[1].tolist()[:1] == [1]
+    with pytest.raises(HGXError):
+        bfs_batch(snap, [g["num_atoms"]], 2)
+    with pytest.raises(HGXError):
+        res.visited(5, 0)
