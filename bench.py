@@ -75,19 +75,18 @@ def cpu_bfs_baseline(g, seeds, depth, budget_s):
     t0 = time.time()
     orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     log(f"cpu baseline: host snapshot built in {time.time() - t0:.1f}s; {threads} threads")
-    done, trav, elapsed, i = 0, 0, 0.0, 0
-    while elapsed < budget_s and i < len(seeds):
-        batch = seeds[i:i + threads]
-        t1 = time.time()
-        _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads)
-        elapsed += time.time() - t1
-        trav += int(tr.sum())
-        done += len(batch)
-        i += threads
+    # one traversal per thread, each stopped after budget_s (a bounded sample of the same workload:
+    # the rate is the reference path's edge rate over the first budget_s of every traversal)
+    batch = np.asarray(seeds[:threads], np.int32)
+    tm = {}
+    _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads, time_budget_s=budget_s, timing=tm)
+    elapsed = tm["elapsed_s"]
+    trav = int(tr.sum())
     del orc
     return {"value": trav / elapsed, "unit": "TEPS", "cores": threads, "kind": "port",
-            "sample": f"{done} of the {len(seeds)} config-2 sources, depth {depth}, one traversal per thread "
-                      f"(C restatement of HGBreadthFirstTraversal/DefaultALGenerator), {elapsed:.1f}s",
+            "sample": f"{len(batch)} of the {len(seeds)} config-2 sources, depth {depth}, one traversal per thread "
+                      f"(C restatement of HGBreadthFirstTraversal/DefaultALGenerator), each stopped after "
+                      f"{budget_s:.0f}s; {trav:.3e} hyperedges in {elapsed:.1f}s",
             "seconds": round(elapsed, 2)}
 
 
@@ -129,37 +128,18 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work per metric")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from hypergraphdb_amd import dist as hdist
+    from hypergraphdb_amd._lib import device_synchronize
+
+    # one process per GPU; only the barrier and scalar max/sum cross processes (gloo, CPU)
+    ctx = hdist.init_from_env("gloo")
+    rank, world, local = ctx.rank, ctx.world, ctx.device
 
     def barrier_sync():
-        if dist is not None:
-            import torch
-            dist.barrier()
-            torch.cuda.synchronize()
+        ctx.barrier()
+        device_synchronize(local)   # hipDeviceSynchronize (the torch.cuda.synchronize equivalent)
 
-    def max_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+    max_over_ranks, sum_over_ranks = ctx.max, ctx.sum
 
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
@@ -167,8 +147,7 @@ def main():
     # ---------------- config 2: batched BFS ----------------
     t0 = time.time()
     g = synth.config2(scale=args.scale, n_sources=args.sources)
-    if rank > 0:   # weak scaling: every rank its own 1024 sources
-        g["seeds"] = synth.sources(g, args.sources, 7 + 1000 * rank)
+    g["seeds"] = hdist.rank_sources(g, args.sources, rank)   # weak scaling: every rank its own sources
     log(f"rank {rank}: config2 generated in {time.time() - t0:.1f}s: A={g['num_atoms']} M={len(g['link_atom'])} "
         f"P={len(g['tgt_idx'])}")
     t0 = time.time()
@@ -276,8 +255,7 @@ def main():
             "pattern": pattern,
         }
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -23,11 +23,12 @@ HGX_E_NOTFOUND = -5
 HGX_ANY_HANDLE = -1
 HGX_NO_TYPE = -1
 HGX_UNBOUNDED = -1
+HGX_OPT_BFS_FLAGS = 1
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
-    "hgx_version", "hgx_last_error", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
-    "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_bfs_batch", "hgx_bfs_result_info",
+    "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
+    "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
     "hgx_bfs_result_free", "hgx_pattern_batch", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
@@ -56,14 +57,17 @@ class BfsStats(C.Structure):
     _fields_ = [("n_levels_expanded", C.c_int32), ("n_batches", C.c_int32), ("ms_total", C.c_double),
                 ("ms_kernel", C.c_double * 4), ("launches", C.c_int64 * 4), ("bytes_kernel", C.c_double * 4),
                 ("bytes_survey", C.c_double), ("traversed_edges", C.c_double),
-                ("union_frontier", C.c_int64 * 64)]
+                ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
              "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges}
         d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
                             "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
-        d["union_frontier"] = [int(x) for x in self.union_frontier[: max(self.n_levels_expanded, 0)]]
+        n = max(self.n_levels_expanded, 0)
+        d["union_frontier"] = [int(x) for x in self.union_frontier[:n]]
+        d["level_ms"] = [round(float(x), 4) for x in self.level_ms[:n]]
+        d["level_new"] = [int(x) for x in self.level_new[:n]]
         return d
 
 
@@ -94,12 +98,14 @@ def lib():
     sig = {
         "hgx_version": ([], C.c_char_p),
         "hgx_last_error": ([], C.c_char_p),
+        "hgx_device_synchronize": ([i32], C.c_int),
         "hgx_graph_create": ([C.POINTER(GraphDesc), i32, C.POINTER(vp)], C.c_int),
         "hgx_graph_destroy": ([vp], None),
         "hgx_graph_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
         "hgx_graph_degree": ([vp, vp, i32, vp], C.c_int),
         "hgx_graph_incidence": ([vp, i32, vp, i64, C.POINTER(i64)], C.c_int),
         "hgx_set_timing": ([vp, i32], C.c_int),
+        "hgx_set_option": ([vp, i32, i64], C.c_int),
         "hgx_bfs_batch": ([vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
         "hgx_bfs_result_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "hgx_bfs_result_counts": ([vp, vp], C.c_int),
@@ -127,6 +133,10 @@ def check(rc):
         if rc == HGX_E_UNSUPPORTED:
             raise HGXUnsupported(rc, msg)
         raise HGXError(rc, msg)
+
+
+def device_synchronize(device: int = 0):
+    check(lib().hgx_device_synchronize(int(device)))
 
 
 def ptr(a: np.ndarray):

@@ -15,8 +15,16 @@
 // which is exactly lf/pull above; v itself is removed by ~vis because v is visited for every bit
 // of its own frontier row.  Ordered modes (succeeding-only / reverse, used by hg.subsumed /
 // hg.subsumes, C/query/cond2qry/ToQueryMap.java:282-370) use the position rule of DESIGN.md 3.2
-// inside the pull instead of lf.  Rows are only read behind per-level activity bitmaps, so a
-// sparse level costs the CSR scan, not the full mask traffic.
+// inside the pull instead of lf.
+//
+// Work avoidance (all exact):
+//   * rows are only read behind per-level activity bitmaps (fa: atom frontier, la: link active),
+//     so a sparse level costs the CSR scan, not the mask traffic;
+//   * an atom visited by every traversal ('full') is never pulled again, and a link whose targets
+//     are all full is never gathered;
+//   * a pull stops as soon as acc | vis covers every traversal, a gather as soon as acc does.
+// Bitmaps are 64-bit words owned by one wavefront each (a wave processes 64 consecutive rows), so
+// they are written with plain stores -- no per-row atomics.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -49,6 +57,7 @@ static int mode_of(const hgx_algen_opts& o) {
 template <int W> struct Lay {
     static constexpr int WPL = W >= 2 ? 2 : 1;
     static constexpr int G = W / WPL;
+    static constexpr int PER_WAVE = 64 / G;   // rows handled by one wave per iteration
 };
 
 template <int WPL> struct Vec;
@@ -56,25 +65,37 @@ template <> struct Vec<1> {
     typedef u64 T;
     static __device__ __forceinline__ T zero() { return 0ull; }
     static __device__ __forceinline__ bool nz(T x) { return x != 0ull; }
+    static __device__ __forceinline__ bool eq(T x, T y) { return x == y; }
     static __device__ __forceinline__ T ld(const u64* p) { return *p; }
     static __device__ __forceinline__ void st(u64* p, T x) { *p = x; }
-    static __device__ __forceinline__ int pop(T x) { return __popcll(x); }
 };
 template <> struct Vec<2> {
     typedef u64x2 T;
     static __device__ __forceinline__ T zero() { return u64x2{0ull, 0ull}; }
     static __device__ __forceinline__ bool nz(T x) { return (x.x | x.y) != 0ull; }
+    static __device__ __forceinline__ bool eq(T x, T y) { return x.x == y.x && x.y == y.y; }
     static __device__ __forceinline__ T ld(const u64* p) { return *reinterpret_cast<const u64x2*>(p); }
     static __device__ __forceinline__ void st(u64* p, T x) { *reinterpret_cast<u64x2*>(p) = x; }
-    static __device__ __forceinline__ int pop(T x) { return __popcll(x.x) + __popcll(x.y); }
 };
 
-__device__ __forceinline__ bool bit(const uint32_t* __restrict__ bm, int64_t i) {
-    return (bm[i >> 5] >> (i & 31)) & 1u;
-}
-__device__ __forceinline__ void set_bit(uint32_t* bm, int64_t i) { atomicOr(&bm[i >> 5], 1u << (i & 31)); }
+// Valid-source mask of a row (S need not be a multiple of 64 or a power of two).
+struct FullMask {
+    u64 w[16];
+};
 
-// true if predicate holds on any lane of this lane's G-lane group (groups are G-aligned in the wave).
+template <int W>
+__device__ __forceinline__ typename Vec<Lay<W>::WPL>::T full_part(const FullMask& fm, int sub) {
+    if constexpr (Lay<W>::WPL == 1) {
+        return fm.w[sub];
+    } else {
+        return u64x2{fm.w[sub * 2], fm.w[sub * 2 + 1]};
+    }
+}
+
+__device__ __forceinline__ bool bit(const u64* __restrict__ bm, int64_t i) { return (bm[i >> 6] >> (i & 63)) & 1ull; }
+__device__ __forceinline__ void set_bit(u64* bm, int64_t i) { atomicOr(&bm[i >> 6], 1ull << (i & 63)); }
+
+// true if predicate holds on any / every lane of this lane's G-lane group (groups are G-aligned).
 template <int G> __device__ __forceinline__ bool group_any(bool p) {
     if constexpr (G == 1) {
         return p;
@@ -84,84 +105,155 @@ template <int G> __device__ __forceinline__ bool group_any(bool p) {
         return ((b >> base) & ((1ull << G) - 1ull)) != 0ull;
     }
 }
+template <int G> __device__ __forceinline__ bool group_all(bool p) { return !group_any<G>(!p); }
 
-// per-level counters (device), used for the early stop and for the byte accounting
+// Compress a wave ballot whose bit of group g sits at lane g*G into bits [pos0, pos0 + 64/G).
+template <int G> __device__ __forceinline__ u64 compress_groups(u64 b, int pos0) {
+    if constexpr (G == 1) {
+        return b;   // pos0 == 0 (one iteration covers the 64-row tile)
+    } else {
+        u64 out = 0;
+#pragma unroll
+        for (int g = 0; g < 64 / G; ++g) out |= ((b >> (g * G)) & 1ull) << (pos0 + g);
+        return out;
+    }
+}
+
+// per-level counters (device): early stop + byte accounting
 enum Ctr {
-    cActiveLinks = 0,   // links whose lf row is nonzero                      (link gather)
-    cActivePins,        // (link, target) pairs whose target row was gathered (link gather)
-    cIncLight,          // incidence entries with an active link, light atoms (atom pull)
-    cAccLight,          // light atoms with a nonzero pull result (vis read)
+    cActiveLinks = 0,   // lf rows written                                   (link gather)
+    cActivePins,        // target rows gathered                              (link gather)
+    cIncLight,          // lf rows pulled, light atoms                       (atom pull)
+    cVisLight,          // vis rows read, light atoms
     cNewLight,          // light atoms with a new bit (lvl + vis written)
-    cIncHeavy,          // incidence entries with an active link, heavy chunks
-    cAccHub,            // heavy atoms with a nonzero pull result
+    cIncHeavy,          // lf rows pulled, heavy chunks
+    cAccHub,            // heavy atoms finalised with a nonzero pull
     cNewHub,            // heavy atoms with a new bit
     cNewAtoms,          // all new atoms of the level (early stop)
-    cNum = 10
+    cDirRows,           // ordered modes: target rows re-read in the pull
+    cNewDeg,            // sum of |inc(v)| over the new atoms (next level's push volume)
+    cNum = 12
 };
 
 __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
-    // one atomic per wave: sum over lanes via DPP-free shuffles
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
 // ---------------------------------------------------------------------------------------------
-// Link gather: lf[L] = OR_{v in targets(L), fa_d(v)} lvl_d[v]; la(L) set iff any target active.
-// One G-lane group per link row, grid-stride.  WRITE_LF = false in the ordered modes.
+// Link gather: lf[L] = OR_{v in targets(L), fa_d(v)} lvl_d[v]; la(L) set iff the row was written.
+// A wave owns 64 consecutive link rows (one la word); a G-lane group handles one row at a time.
+// WRITE_LF = false in the ordered modes (only la is needed there).
 // ---------------------------------------------------------------------------------------------
 template <int W, bool WRITE_LF>
 __global__ void __launch_bounds__(256) hgx_link_gather(int64_t M, const int64_t* __restrict__ tgt_off,
                                                        const int32_t* __restrict__ tgt_idx,
                                                        const int32_t* __restrict__ link_type, int32_t want_type,
-                                                       const uint32_t* __restrict__ fa,
+                                                       const u64* __restrict__ fa, const u64* __restrict__ full,
                                                        const u64* __restrict__ lvl, u64* __restrict__ lf,
-                                                       uint32_t* __restrict__ la, u64* __restrict__ ctr) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+                                                       u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm,
+                                                       int flags, const u64* __restrict__ lcand,
+                                                       u64* __restrict__ cand) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
+    const bool early = flags & 1, skip_full = flags & 4;
     typedef Vec<WPL> V;
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
     u64 n_links = 0, n_pins = 0;
-    for (int64_t L = grp; L < M; L += ngrp) {
-        if (want_type >= 0 && link_type[L] != want_type) continue;
-        const int64_t b = tgt_off[L], e = tgt_off[L + 1];
-        typename V::T acc = V::zero();
-        int nact = 0;
-        int64_t p = b;
-        for (; p + 4 <= e; p += 4) {
-            int32_t v0 = tgt_idx[p], v1 = tgt_idx[p + 1], v2 = tgt_idx[p + 2], v3 = tgt_idx[p + 3];
-            bool a0 = bit(fa, v0), a1 = bit(fa, v1), a2 = bit(fa, v2), a3 = bit(fa, v3);
-            if (a0) acc |= V::ld(lvl + (int64_t)v0 * W + sub * WPL);
-            if (a1) acc |= V::ld(lvl + (int64_t)v1 * W + sub * WPL);
-            if (a2) acc |= V::ld(lvl + (int64_t)v2 * W + sub * WPL);
-            if (a3) acc |= V::ld(lvl + (int64_t)v3 * W + sub * WPL);
-            nact += (int)a0 + (int)a1 + (int)a2 + (int)a3;
+    for (int64_t tile = wave; tile * 64 < M; tile += nwave) {
+        u64 word = 0;
+        // sparse levels: only links incident to a frontier atom (lcand) can be active
+        const u64 lc = lcand ? lcand[tile] : ~0ull;
+        if (lc == 0) {
+            if (lane == 0) la[tile] = 0;
+            continue;
         }
-        for (; p < e; ++p) {
-            int32_t v = tgt_idx[p];
-            if (bit(fa, v)) {
-                acc |= V::ld(lvl + (int64_t)v * W + sub * WPL);
-                ++nact;
+        for (int j = 0; j < G; ++j) {
+            const int64_t L = tile * 64 + j * PW + g;
+            bool act = false;
+            if (L < M && ((lc >> (j * PW + g)) & 1ull) && (want_type < 0 || link_type[L] == want_type)) {
+                const int64_t b = tgt_off[L], e = tgt_off[L + 1];
+                typename V::T acc = V::zero();
+                int nact = 0;
+                bool all_full = true;
+                if constexpr (G >= 4) {
+                    // lane `sub` loads target p+sub and checks its own bitmap bits; the group then
+                    // gathers the active rows (16 B per lane) via ballot + shuffle
+                    const int base = lane & ~(G - 1);
+                    bool any_not_full = !skip_full;
+                    for (int64_t p = b; p < e; p += G) {
+                        const int64_t q = p + sub;
+                        const int32_t myv = q < e ? tgt_idx[q] : -1;
+                        const bool mya = myv >= 0 && bit(fa, myv);
+                        const bool mynf = myv >= 0 && skip_full && !bit(full, myv);
+                        const unsigned ga = (unsigned)((__ballot(mya) >> base) & ((1ull << G) - 1ull));
+                        any_not_full |= ((__ballot(mynf) >> base) & ((1ull << G) - 1ull)) != 0ull;
+                        typename V::T r[G];
+#pragma unroll
+                        for (int k = 0; k < G; ++k) {
+                            const int32_t vk = __shfl(myv, base + k);
+                            r[k] = ((ga >> k) & 1u) ? V::ld(lvl + (int64_t)vk * W + sub * WPL) : V::zero();
+                        }
+#pragma unroll
+                        for (int k = 0; k < G; ++k) acc |= r[k];
+                        nact += __popc(ga);
+                        if (early && p + G < e && group_all<G>(V::eq(acc, FULL))) {
+                            any_not_full = true;
+                            break;
+                        }
+                    }
+                    all_full = !any_not_full;
+                } else {
+                    for (int64_t p = b; p < e; p += 4) {
+                        int32_t v[4];
+                        bool a[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) v[k] = p + k < e ? tgt_idx[p + k] : -1;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            a[k] = v[k] >= 0 && bit(fa, v[k]);
+                            if (skip_full) all_full &= v[k] < 0 || bit(full, v[k]);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            if (a[k]) acc |= V::ld(lvl + (int64_t)v[k] * W + sub * WPL);
+                        nact += (int)a[0] + (int)a[1] + (int)a[2] + (int)a[3];
+                        if (early && p + 4 < e && group_all<G>(V::eq(acc, FULL))) {   // every traversal present
+                            all_full = false;
+                            break;
+                        }
+                    }
+                }
+                act = nact > 0 && !(skip_full && all_full);   // all targets full: nobody pulls this row
+                if (act && cand) {   // sparse levels: the targets of an active link are the pull candidates
+                    for (int64_t p = b + sub; p < e; p += G) {
+                        const int32_t v = tgt_idx[p];
+                        atomicOr(&cand[v >> 6], 1ull << (v & 63));
+                    }
+                }
+                if (act) {
+                    if (WRITE_LF) V::st(lf + L * W + sub * WPL, acc);
+                    if (sub == 0) {
+                        ++n_links;
+                        n_pins += nact;
+                    }
+                }
             }
+            word |= compress_groups<G>(__ballot(act), j * PW);
         }
-        if (nact) {
-            if (WRITE_LF) V::st(lf + L * W + sub * WPL, acc);
-            if (sub == 0) {
-                set_bit(la, L);
-                ++n_links;
-                n_pins += nact;
-            }
-        }
+        if (lane == 0) la[tile] = word;
     }
     wave_add(ctr + cActiveLinks, n_links);
     wave_add(ctr + cActivePins, n_pins);
 }
 
-// Ordered modes: the frontier rows of the co-targets of t in link row Lr that may yield t.
+// Ordered modes: the frontier rows of the co-targets of t in one link row that may yield t.
 template <int W, int MODE>
 __device__ __forceinline__ typename Vec<Lay<W>::WPL>::T pull_ordered(int32_t t, int64_t b, int64_t e,
                                                                       const int32_t* __restrict__ tgt_idx,
-                                                                      const uint32_t* __restrict__ fa,
+                                                                      const u64* __restrict__ fa,
                                                                       const u64* __restrict__ lvl, int sub) {
     constexpr int WPL = Lay<W>::WPL;
     typedef Vec<WPL> V;
@@ -193,128 +285,196 @@ __device__ __forceinline__ typename Vec<Lay<W>::WPL>::T pull_ordered(int32_t t, 
     return acc;
 }
 
-// Accumulate the pull of incidence entries [b, e) of atom t.
+// Pull incidence entries [b, e) of atom t into acc, stopping once acc | old covers FULL.
+// `old` is loaded lazily from vis (only when the first active link is met and t has a vis row).
 template <int W, int MODE>
-__device__ __forceinline__ typename Vec<Lay<W>::WPL>::T pull_range(
-    int32_t t, int64_t b, int64_t e, const int32_t* __restrict__ inc_row, const uint32_t* __restrict__ la,
-    const u64* __restrict__ lf, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
-    const uint32_t* __restrict__ fa, const u64* __restrict__ lvl, int sub, u64& n_inc) {
-    constexpr int WPL = Lay<W>::WPL;
+__device__ __forceinline__ void pull_range(int32_t t, int64_t b, int64_t e, const int32_t* __restrict__ inc_row,
+                                           const u64* __restrict__ la, const u64* __restrict__ lf,
+                                           const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+                                           const u64* __restrict__ fa, const u64* __restrict__ lvl,
+                                           const u64* __restrict__ vis_row, bool have_vis,
+                                           typename Vec<Lay<W>::WPL>::T FULL, int sub,
+                                           typename Vec<Lay<W>::WPL>::T& acc, typename Vec<Lay<W>::WPL>::T& old,
+                                           bool& have_old, u64& n_inc, u64& n_vis, bool early) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
-    typename V::T acc = V::zero();
-    int64_t i = b;
-    if constexpr (MODE == kSym) {
-        for (; i + 8 <= e; i += 8) {
+    if constexpr (G >= 4 && MODE == kSym) {
+        // lane `sub` loads entry i+sub and tests its la bit; the group then pulls the active lf rows
+        const int base = (threadIdx.x & 63) & ~(G - 1);
+        for (int64_t i = b; i < e; i += G) {
+            const int64_t q = i + sub;
+            const int32_t myL = q < e ? inc_row[q] : -1;
+            const bool mya = myL >= 0 && bit(la, myL);
+            const unsigned ga = (unsigned)((__ballot(mya) >> base) & ((1ull << G) - 1ull));
+            typename V::T r[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int32_t Lk = __shfl(myL, base + k);
+                r[k] = ((ga >> k) & 1u) ? V::ld(lf + (int64_t)Lk * W + sub * WPL) : V::zero();
+            }
+#pragma unroll
+            for (int k = 0; k < G; ++k) acc |= r[k];
+            n_inc += __popc(ga);
+            if (!early) continue;
+            if (!have_old && group_any<G>(V::nz(acc))) {
+                if (have_vis) {
+                    old = V::ld(vis_row + sub * WPL);
+                    ++n_vis;
+                }
+                have_old = true;
+            }
+            if (have_old && i + G < e && group_all<G>(V::eq(acc | old, FULL))) break;
+        }
+    } else {
+        for (int64_t i = b; i < e; i += 8) {
             int32_t L[8];
             bool act[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) L[k] = inc_row[i + k];
+            for (int k = 0; k < 8; ++k) L[k] = i + k < e ? inc_row[i + k] : -1;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) act[k] = bit(la, L[k]);
+            for (int k = 0; k < 8; ++k) act[k] = L[k] >= 0 && bit(la, L[k]);
+            if constexpr (MODE == kSym) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (act[k]) {
-                    acc |= V::ld(lf + (int64_t)L[k] * W + sub * WPL);
-                    ++n_inc;
+                for (int k = 0; k < 8; ++k)
+                    if (act[k]) {
+                        acc |= V::ld(lf + (int64_t)L[k] * W + sub * WPL);
+                        ++n_inc;
+                    }
+            } else {
+                for (int k = 0; k < 8; ++k)
+                    if (act[k]) {
+                        acc |= pull_ordered<W, MODE>(t, tgt_off[L[k]], tgt_off[L[k] + 1], tgt_idx, fa, lvl, sub);
+                        ++n_inc;
+                    }
+            }
+            if (!early) continue;
+            if (!have_old && group_any<G>(V::nz(acc))) {
+                if (have_vis) {
+                    old = V::ld(vis_row + sub * WPL);
+                    ++n_vis;
                 }
-        }
-        for (; i < e; ++i) {
-            int32_t L = inc_row[i];
-            if (bit(la, L)) {
-                acc |= V::ld(lf + (int64_t)L * W + sub * WPL);
-                ++n_inc;
+                have_old = true;
             }
-        }
-    } else {
-        for (; i < e; ++i) {
-            int32_t L = inc_row[i];
-            if (bit(la, L)) {
-                acc |= pull_ordered<W, MODE>(t, tgt_off[L], tgt_off[L + 1], tgt_idx, fa, lvl, sub);
-                ++n_inc;
-            }
+            if (have_old && i + 8 < e && group_all<G>(V::eq(acc | old, FULL))) break;
         }
     }
-    return acc;
-}
-
-// new = acc & ~vis[t]; write lvl_next/vis/fa_next/ever (owner of t only).
-template <int W>
-__device__ __forceinline__ void finalize(int64_t t, typename Vec<Lay<W>::WPL>::T acc, int sub,
-                                         u64* __restrict__ vis, uint32_t* __restrict__ ever,
-                                         u64* __restrict__ lvl_next, uint32_t* __restrict__ fa_next,
-                                         u64& n_acc, u64& n_new) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    typedef Vec<WPL> V;
-    if (!group_any<G>(V::nz(acc))) return;
-    const bool ev = bit(ever, t);
-    typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
-    typename V::T nw = acc & ~old;
-    if (sub == 0) ++n_acc;
-    if (!group_any<G>(V::nz(nw))) return;
-    V::st(lvl_next + t * W + sub * WPL, nw);
-    V::st(vis + t * W + sub * WPL, old | nw);
-    if (sub == 0) {
-        set_bit(fa_next, t);
-        if (!ev) set_bit(ever, t);
-        ++n_new;
+    if (!have_old && group_any<G>(V::nz(acc))) {   // no early exit: vis read once at the end
+        if (have_vis) {
+            old = V::ld(vis_row + sub * WPL);
+            ++n_vis;
+        }
+        have_old = true;
     }
 }
 
-// Atom pull for light atoms (deg <= kHeavyDegree): one G-lane group per atom.
+// Atom pull for light atoms (deg <= kHeavyDegree).  A wave owns 64 consecutive atoms (one word of
+// fa_next / ever / full); a G-lane group handles one atom at a time.  Heavy atoms are skipped here
+// (hgx_atom_pull_heavy + hgx_hub_finalize run afterwards and OR their bits in).
 template <int W, int MODE>
 __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* __restrict__ inc_off,
                                                      const int32_t* __restrict__ inc_row,
-                                                     const uint32_t* __restrict__ la, const u64* __restrict__ lf,
+                                                     const u64* __restrict__ la, const u64* __restrict__ lf,
                                                      const int64_t* __restrict__ tgt_off,
                                                      const int32_t* __restrict__ tgt_idx,
-                                                     const uint32_t* __restrict__ fa, const u64* __restrict__ lvl,
-                                                     u64* __restrict__ vis, uint32_t* __restrict__ ever,
-                                                     u64* __restrict__ lvl_next, uint32_t* __restrict__ fa_next,
-                                                     u64* __restrict__ ctr) {
-    constexpr int G = Lay<W>::G;
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    u64 n_inc = 0, n_acc = 0, n_new = 0;
-    for (int64_t t = grp; t < A; t += ngrp) {
-        const int64_t b = inc_off[t], e = inc_off[t + 1];
-        if (e == b || e - b > kHeavyDegree) continue;
-        auto acc = pull_range<W, MODE>((int32_t)t, b, e, inc_row, la, lf, tgt_off, tgt_idx, fa, lvl, sub, n_inc);
-        finalize<W>(t, acc, sub, vis, ever, lvl_next, fa_next, n_acc, n_new);
+                                                     const u64* __restrict__ fa, const u64* __restrict__ lvl,
+                                                     u64* __restrict__ vis, u64* __restrict__ ever,
+                                                     u64* __restrict__ full, u64* __restrict__ lvl_next,
+                                                     u64* __restrict__ fa_next, u64* __restrict__ ctr, FullMask fm,
+                                                     int flags, const u64* __restrict__ cand) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
+    const bool early = flags & 2, skip_full = flags & 4;
+    typedef Vec<WPL> V;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0;
+    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+        // sparse levels: only targets of active links (cand) can gain a bit
+        const u64 cw = cand ? cand[tile] : ~0ull;
+        if (cw == 0) {
+            if (lane == 0) fa_next[tile] = 0;
+            continue;
+        }
+        const u64 ever_w = ever[tile], full_w = full[tile];
+        u64 new_w = 0, fullnew_w = 0;
+        for (int j = 0; j < G; ++j) {
+            const int pos = j * PW + g;
+            const int64_t t = tile * 64 + pos;
+            bool isnew = false, becomes_full = false;
+            if (t < A && ((cw >> pos) & 1ull) && !(skip_full && ((full_w >> pos) & 1ull))) {
+                const int64_t b = inc_off[t], e = inc_off[t + 1];
+                if (e > b && e - b <= kHeavyDegree) {
+                    const bool ev = (ever_w >> pos) & 1ull;
+                    typename V::T acc = V::zero(), old = V::zero();
+                    bool have_old = false;
+                    pull_range<W, MODE>((int32_t)t, b, e, inc_row, la, lf, tgt_off, tgt_idx, fa, lvl, vis + t * W,
+                                        ev, FULL, sub, acc, old, have_old, n_inc, n_vis, early);
+                    const typename V::T nw = acc & ~old;
+                    if (group_any<G>(V::nz(nw))) {
+                        V::st(lvl_next + t * W + sub * WPL, nw);
+                        V::st(vis + t * W + sub * WPL, old | nw);
+                        isnew = true;
+                        becomes_full = group_all<G>(V::eq(old | nw, FULL));
+                        if (sub == 0) n_newdeg += (u64)(e - b);
+                    }
+                }
+            }
+            new_w |= compress_groups<G>(__ballot(isnew), j * PW);
+            fullnew_w |= compress_groups<G>(__ballot(becomes_full), j * PW);
+        }
+        if (lane == 0) {
+            fa_next[tile] = new_w;
+            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
+            if (fullnew_w) full[tile] = full_w | fullnew_w;
+            n_new += __popcll(new_w);
+        }
     }
-    if (sub != 0) n_inc = 0;
+    if (sub != 0) {
+        n_inc = 0;
+        n_vis = 0;
+    }
     wave_add(ctr + cIncLight, n_inc);
-    wave_add(ctr + cAccLight, n_acc);
+    wave_add(ctr + cVisLight, n_vis);
     wave_add(ctr + cNewLight, n_new);
     wave_add(ctr + cNewAtoms, n_new);
+    wave_add(ctr + cNewDeg, n_newdeg);
 }
 
 // Heavy atoms: one workgroup per chunk of <= kChunkEntries incidence entries; groups OR their
-// share, the block reduces through LDS and ORs the chunk result into hubacc[slot].
+// share (stopping early once every traversal is covered), the block reduces through LDS and ORs
+// the chunk result into hubacc[slot].  Hubs already visited by every traversal exit at once.
 template <int W, int MODE>
 __global__ void __launch_bounds__(256) hgx_atom_pull_heavy(const HeavyChunk* __restrict__ chunks,
                                                            const int32_t* __restrict__ inc_row,
-                                                           const uint32_t* __restrict__ la,
-                                                           const u64* __restrict__ lf,
+                                                           const u64* __restrict__ la, const u64* __restrict__ lf,
                                                            const int64_t* __restrict__ tgt_off,
                                                            const int32_t* __restrict__ tgt_idx,
-                                                           const uint32_t* __restrict__ fa,
-                                                           const u64* __restrict__ lvl, u64* __restrict__ hubacc,
-                                                           u64* __restrict__ ctr) {
+                                                           const u64* __restrict__ fa, const u64* __restrict__ lvl,
+                                                           const u64* __restrict__ vis, const u64* __restrict__ ever,
+                                                           const u64* __restrict__ full, u64* __restrict__ hubacc,
+                                                           u64* __restrict__ ctr, FullMask fm, int flags,
+                                                           const u64* __restrict__ cand) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     constexpr int NG = 256 / G;
     typedef Vec<WPL> V;
     __shared__ u64 red[NG * W];
     const HeavyChunk c = chunks[blockIdx.x];
+    if ((flags & 4) && bit(full, c.atom)) return;   // block-uniform
+    if (cand && !bit(cand, c.atom)) return;
     const int sub = threadIdx.x & (G - 1);
     const int gi = threadIdx.x / G;
     const int64_t n = c.end - c.beg;
     const int64_t per = (n + NG - 1) / NG;
     const int64_t b = c.beg + gi * per;
     const int64_t e = b + per < c.end ? b + per : c.end;
-    u64 n_inc = 0;
-    typename V::T acc = V::zero();
-    if (b < e) acc = pull_range<W, MODE>(c.atom, b, e, inc_row, la, lf, tgt_off, tgt_idx, fa, lvl, sub, n_inc);
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_inc = 0, n_vis = 0;
+    typename V::T acc = V::zero(), old = V::zero();
+    bool have_old = false;
+    if (b < e)
+        pull_range<W, MODE>(c.atom, b, e, inc_row, la, lf, tgt_off, tgt_idx, fa, lvl, vis + (int64_t)c.atom * W,
+                            bit(ever, c.atom), FULL, sub, acc, old, have_old, n_inc, n_vis, (flags & 2) != 0);
     V::st(red + gi * W + sub * WPL, acc);
     __syncthreads();
     for (int j = threadIdx.x; j < W; j += 256) {
@@ -328,41 +488,223 @@ __global__ void __launch_bounds__(256) hgx_atom_pull_heavy(const HeavyChunk* __r
 
 template <int W>
 __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t* __restrict__ heavy_atom,
+                                                        const int64_t* __restrict__ inc_off,
                                                         u64* __restrict__ hubacc, u64* __restrict__ vis,
-                                                        uint32_t* __restrict__ ever, u64* __restrict__ lvl_next,
-                                                        uint32_t* __restrict__ fa_next, u64* __restrict__ ctr) {
+                                                        u64* __restrict__ ever, u64* __restrict__ full,
+                                                        u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                        u64* __restrict__ ctr, FullMask fm) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
     const int sub = threadIdx.x & (G - 1);
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    u64 n_acc = 0, n_new = 0;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_acc = 0, n_new = 0, n_newdeg = 0;
     for (int64_t h = grp; h < H; h += ngrp) {
+        const int64_t t = heavy_atom[h];
         typename V::T acc = V::ld(hubacc + h * W + sub * WPL);
+        if (!group_any<G>(V::nz(acc))) continue;
         V::st(hubacc + h * W + sub * WPL, V::zero());
-        finalize<W>(heavy_atom[h], acc, sub, vis, ever, lvl_next, fa_next, n_acc, n_new);
+        const bool ev = bit(ever, t);
+        typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        typename V::T nw = acc & ~old;
+        if (sub == 0) ++n_acc;
+        if (!group_any<G>(V::nz(nw))) continue;
+        V::st(lvl_next + t * W + sub * WPL, nw);
+        V::st(vis + t * W + sub * WPL, old | nw);
+        const bool becomes_full = group_all<G>(V::eq(old | nw, FULL));
+        if (sub == 0) {
+            set_bit(fa_next, t);
+            if (!ev) set_bit(ever, t);
+            if (becomes_full) set_bit(full, t);
+            ++n_new;
+            n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+        }
     }
     wave_add(ctr + cAccHub, n_acc);
     wave_add(ctr + cNewHub, n_new);
     wave_add(ctr + cNewAtoms, n_new);
+    wave_add(ctr + cNewDeg, n_newdeg);
+}
+
+// Sparse levels: mark every (typed) link incident to a frontier atom.  One wave per frontier word:
+// for each frontier atom of the word, the 64 lanes stride over its incidence row.  Heavy atoms are
+// left to hgx_frontier_links_heavy (one workgroup per chunk).
+__global__ void __launch_bounds__(256) hgx_frontier_links(int64_t A, const u64* __restrict__ fa,
+                                                          const int64_t* __restrict__ inc_off,
+                                                          const int32_t* __restrict__ inc_row,
+                                                          const int32_t* __restrict__ link_type, int32_t want_type,
+                                                          u64* __restrict__ lcand) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t w = wave; w * 64 < A; w += nwave) {
+        u64 x = fa[w];
+        while (x) {
+            const int b = __ffsll((long long)x) - 1;
+            x &= x - 1;
+            const int64_t v = w * 64 + b;
+            const int64_t lo = inc_off[v], hi = inc_off[v + 1];
+            if (hi - lo > kHeavyDegree) continue;
+            for (int64_t i = lo + lane; i < hi; i += 64) {
+                const int32_t L = inc_row[i];
+                if (want_type < 0 || link_type[L] == want_type) atomicOr(&lcand[L >> 6], 1ull << (L & 63));
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_frontier_links_heavy(const HeavyChunk* __restrict__ chunks,
+                                                                const u64* __restrict__ fa,
+                                                                const int32_t* __restrict__ inc_row,
+                                                                const int32_t* __restrict__ link_type,
+                                                                int32_t want_type, u64* __restrict__ lcand) {
+    const HeavyChunk c = chunks[blockIdx.x];
+    if (!bit(fa, c.atom)) return;
+    for (int64_t i = c.beg + threadIdx.x; i < c.end; i += 256) {
+        const int32_t L = inc_row[i];
+        if (want_type < 0 || link_type[L] == want_type) atomicOr(&lcand[L >> 6], 1ull << (L & 63));
+    }
+}
+
+// ---- sparse levels, default mode: push instead of pull ------------------------------------------
+// (1) zero the next-level rows of the candidate atoms, (2) OR every active link's lf row into the
+// rows of its targets with 64-bit atomics, (3) finalise the candidates (new = acc & ~vis).
+
+__global__ void __launch_bounds__(256) hgx_push_zero(int64_t A, int W, const u64* __restrict__ cand,
+                                                     const u64* __restrict__ full, u64* __restrict__ lvl_next) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int per = (64 / W) < 8 ? (64 / W) : 8;   // atoms zeroed per wave instruction
+    for (int64_t w = wave; w * 64 < A; w += nwave) {
+        u64 x = cand[w] & ~full[w];
+        while (x) {
+            int64_t t[8];
+            int n = 0;
+            while (x && n < per) {
+                t[n++] = w * 64 + __ffsll((long long)x) - 1;
+                x &= x - 1;
+            }
+            const int k = lane / W;
+            if (k < n) {
+                int64_t tk = t[0];
+                for (int q = 1; q < 8; ++q)
+                    if (q == k) tk = t[q];
+                lvl_next[tk * W + (lane % W)] = 0ull;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_push_rows(int64_t M, int W, const u64* __restrict__ la,
+                                                     const int64_t* __restrict__ tgt_off,
+                                                     const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lf,
+                                                     const u64* __restrict__ full, u64* __restrict__ lvl_next) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t w = wave; w * 64 < M; w += nwave) {
+        u64 x = la[w];
+        while (x) {
+            const int64_t L = w * 64 + __ffsll((long long)x) - 1;
+            x &= x - 1;
+            const int64_t b = tgt_off[L], n = (tgt_off[L + 1] - b) * W;
+            for (int64_t j = lane; j < n; j += 64) {
+                const int32_t t = tgt_idx[b + j / W];
+                const int wd = (int)(j % W);
+                const u64 r = lf[L * W + wd];
+                if (r && !bit(full, t)) atomicOr(&lvl_next[(int64_t)t * W + wd], r);
+            }
+        }
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_t* __restrict__ inc_off,
+                                                         const u64* __restrict__ cand, u64* __restrict__ vis,
+                                                         u64* __restrict__ ever, u64* __restrict__ full,
+                                                         u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                         u64* __restrict__ ctr, FullMask fm) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
+    typedef Vec<WPL> V;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_vis = 0, n_new = 0, n_newdeg = 0;
+    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+        const u64 full_w = full[tile];
+        const u64 cw = cand[tile] & ~full_w;
+        if (cw == 0) {
+            if (lane == 0) fa_next[tile] = 0;
+            continue;
+        }
+        const u64 ever_w = ever[tile];
+        u64 new_w = 0, fullnew_w = 0;
+        for (int j = 0; j < G; ++j) {
+            const int pos = j * PW + g;
+            const int64_t t = tile * 64 + pos;
+            bool isnew = false, becomes_full = false;
+            if (t < A && ((cw >> pos) & 1ull)) {
+                const typename V::T acc = V::ld(lvl_next + t * W + sub * WPL);
+                if (group_any<G>(V::nz(acc))) {
+                    const bool ev = (ever_w >> pos) & 1ull;
+                    const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+                    n_vis += ev;
+                    const typename V::T nw = acc & ~old;
+                    if (group_any<G>(V::nz(nw))) {
+                        V::st(lvl_next + t * W + sub * WPL, nw);
+                        V::st(vis + t * W + sub * WPL, old | nw);
+                        isnew = true;
+                        becomes_full = group_all<G>(V::eq(old | nw, FULL));
+                        if (sub == 0) n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+                    }
+                }
+            }
+            new_w |= compress_groups<G>(__ballot(isnew), j * PW);
+            fullnew_w |= compress_groups<G>(__ballot(becomes_full), j * PW);
+        }
+        if (lane == 0) {
+            fa_next[tile] = new_w;
+            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
+            if (fullnew_w) full[tile] = full_w | fullnew_w;
+            n_new += __popcll(new_w);
+        }
+    }
+    if (sub != 0) n_vis = 0;
+    wave_add(ctr + cVisLight, n_vis);
+    wave_add(ctr + cNewLight, n_new);
+    wave_add(ctr + cNewAtoms, n_new);
+    wave_add(ctr + cNewDeg, n_newdeg);
+}
+
+// sum of |inc(v)| over the seed atoms (level-0 push volume)
+__global__ void hgx_seed_degree(int32_t n, const int32_t* __restrict__ atoms, const int64_t* __restrict__ inc_off,
+                                u64* __restrict__ out) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    u64 d = k < n ? (u64)(inc_off[atoms[k] + 1] - inc_off[atoms[k]]) : 0ull;
+    wave_add(out, d);
 }
 
 // Level 0: seed rows.  rows[i*W ..] is the mask row of unique seed atom atoms[i].
 template <int W>
 __global__ void hgx_seed(int32_t n, const int32_t* __restrict__ atoms, const u64* __restrict__ rows,
-                         u64* __restrict__ lvl0, u64* __restrict__ vis, uint32_t* __restrict__ fa0,
-                         uint32_t* __restrict__ ever) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * W) return;
-    int k = i / W, w = i % W;
+                         u64* __restrict__ lvl0, u64* __restrict__ vis, u64* __restrict__ fa0,
+                         u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
     int64_t a = atoms[k];
-    u64 r = rows[(int64_t)k * W + w];
-    lvl0[a * W + w] = r;
-    vis[a * W + w] = r;
-    if (w == 0) {
-        set_bit(fa0, a);
-        set_bit(ever, a);
+    bool is_full = true;
+    for (int w = 0; w < W; ++w) {
+        u64 r = rows[(int64_t)k * W + w];
+        lvl0[a * W + w] = r;
+        vis[a * W + w] = r;
+        is_full &= (r == fm.w[w]);
     }
+    set_bit(fa0, a);
+    set_bit(ever, a);
+    if (is_full) set_bit(full, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -372,7 +714,7 @@ __global__ void hgx_seed(int32_t n, const int32_t* __restrict__ atoms, const u64
 // Bit-sliced per-source counts of one level: counts[w*64 + b] += |{v : bit b of lvl[v][w]}|.
 // Also traversed += sum_v popcount(lvl[v]) * deg(v) (the hyperedge TEPS numerator).
 template <int W>
-__global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const uint32_t* __restrict__ fa,
+__global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const u64* __restrict__ fa,
                                                        const u64* __restrict__ lvl,
                                                        const int64_t* __restrict__ inc_off,
                                                        u64* __restrict__ counts, u64* __restrict__ traversed) {
@@ -415,7 +757,7 @@ __global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const uint32_t
 // counts per block; pass 2 writes at the block's exclusive offset.  Each block owns the
 // contiguous atom range [blk*span, (blk+1)*span).
 __global__ void __launch_bounds__(256) hgx_extract(int64_t A, int64_t span, int W, int s,
-                                                   const uint32_t* __restrict__ fa, const u64* __restrict__ lvl,
+                                                   const u64* __restrict__ fa, const u64* __restrict__ lvl,
                                                    const int64_t* __restrict__ blk_off, int64_t* __restrict__ blk_cnt,
                                                    int32_t* __restrict__ out, int64_t cap, bool write) {
     __shared__ int64_t wave_tot[4];
@@ -444,30 +786,35 @@ __global__ void __launch_bounds__(256) hgx_extract(int64_t A, int64_t span, int 
     if (!write && threadIdx.x == 0) blk_cnt[blockIdx.x] = run;
 }
 
-// |U_d|, sum deg(v), P_d = sum_{v in U_d} sum_{L in inc v} arity(L)  
-__global__ void __launch_bounds__(256) hgx_level_survey(int64_t A, const uint32_t* __restrict__ fa,
-                                                        const int64_t* __restrict__ inc_off,
-                                                        const int32_t* __restrict__ inc_row,
-                                                        const int64_t* __restrict__ tgt_off, u64* __restrict__ out) {
+// SURVEY.md 8(d) push-model quantities of one level, link-parallel:
+//   out[0] = |U_d|, out[1] = sum_{v in U_d} deg(v) = sum_L |distinct targets of L in U_d|,
+//   out[2] = P_d = sum_{v in U_d} sum_{L in inc v} arity(L) = sum_L arity(L) * |distinct U_d targets|
+__global__ void __launch_bounds__(256) hgx_level_survey(int64_t A, int64_t M, const u64* __restrict__ fa,
+                                                        const int64_t* __restrict__ tgt_off,
+                                                        const int32_t* __restrict__ tgt_idx, u64* __restrict__ out) {
     u64 nu = 0, sd = 0, pd = 0;
-    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < A; v += (int64_t)gridDim.x * blockDim.x) {
-        if (!bit(fa, v)) continue;
-        ++nu;
-        const int64_t b = inc_off[v], e = inc_off[v + 1];
-        sd += (u64)(e - b);
-        for (int64_t i = b; i < e; ++i) {
-            int32_t L = inc_row[i];
-            pd += (u64)(tgt_off[L + 1] - tgt_off[L]);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w * 64 < A; w += stride) nu += __popcll(fa[w]);
+    for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < M; L += stride) {
+        const int64_t b = tgt_off[L], e = tgt_off[L + 1];
+        u64 k = 0;
+        for (int64_t p = b; p < e; ++p) {
+            const int32_t v = tgt_idx[p];
+            if (!bit(fa, v)) continue;
+            bool dup = false;
+            for (int64_t q = b; q < p; ++q) dup |= tgt_idx[q] == v;
+            k += !dup;
         }
+        sd += k;
+        pd += k * (u64)(e - b);
     }
     wave_add(out + 0, nu);
     wave_add(out + 1, sd);
     wave_add(out + 2, pd);
 }
 
-__global__ void hgx_depth_probe(int32_t nlev, const uint32_t* const* __restrict__ fa,
-                                const u64* const* __restrict__ lvl, int W, int s, int64_t atom,
-                                int32_t* __restrict__ out) {
+__global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa, const u64* const* __restrict__ lvl,
+                                int W, int s, int64_t atom, int32_t* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int32_t d = -1;
     for (int k = 0; k < nlev && d < 0; ++k)
@@ -487,8 +834,7 @@ struct BfsBatch {
     int32_t seed0 = 0, S = 0, W = 0;
     int32_t n_expanded = 0;       // levels whose frontier was expanded (advance() iterated)
     std::vector<u64*> lvl;        // per level, A*W words (rows valid where fa bit set)
-    std::vector<uint32_t*> fa;    // per level, A bits
-    std::vector<int64_t> counts;  // [S * n_levels] after hgx_bfs_result_counts
+    std::vector<u64*> fa;         // per level, A bits
 };
 
 struct hgx_bfs_result {
@@ -500,7 +846,7 @@ struct hgx_bfs_result {
     bool typed = false;
     std::vector<int64_t> counts;   // [n_seeds * n_levels]
     size_t row_bytes(const BfsBatch& b) const { return sizeof(u64) * (size_t)g->A * b.W; }
-    size_t bm_bytes() const { return sizeof(uint32_t) * (size_t)(g->A / 32 + 2); }
+    size_t bm_bytes() const { return sizeof(u64) * (size_t)(g->A / 64 + 2); }
 };
 
 namespace {
@@ -509,52 +855,63 @@ struct Events {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
-// Launch helper that brackets a kernel with events when timing is on.
+// Brackets kernels with events when timing is on; kind = HGX_K_*, level = BFS level.
 struct Timer {
     hgx_graph* g;
-    std::vector<std::pair<int, Events>> rec;   // (kind, events)
-    Events begin_all{}, end_all{};
+    struct Rec {
+        int kind, level;
+        Events e;
+    };
+    std::vector<Rec> rec;
+    Events all{};
     bool on;
     explicit Timer(hgx_graph* gg) : g(gg), on(gg->timing) {
         if (on) {
-            HGX_HIP(hipEventCreate(&begin_all.a));
-            HGX_HIP(hipEventCreate(&end_all.a));
+            HGX_HIP(hipEventCreate(&all.a));
+            HGX_HIP(hipEventCreate(&all.b));
         }
     }
     ~Timer() {
         for (auto& r : rec) {
-            (void)hipEventDestroy(r.second.a);
-            (void)hipEventDestroy(r.second.b);
+            (void)hipEventDestroy(r.e.a);
+            (void)hipEventDestroy(r.e.b);
         }
-        if (begin_all.a) (void)hipEventDestroy(begin_all.a);
-        if (end_all.a) (void)hipEventDestroy(end_all.a);
+        if (all.a) (void)hipEventDestroy(all.a);
+        if (all.b) (void)hipEventDestroy(all.b);
     }
-    Events start(int kind) {
+    Events start(int kind, int level) {
         Events e{};
         if (!on) return e;
         HGX_HIP(hipEventCreate(&e.a));
         HGX_HIP(hipEventCreate(&e.b));
         HGX_HIP(hipEventRecord(e.a, g->stream));
-        rec.push_back({kind, e});
+        rec.push_back({kind, level, e});
         return e;
     }
     void stop(const Events& e) {
         if (on) HGX_HIP(hipEventRecord(e.b, g->stream));
     }
-    double total(int kind) {
-        double t = 0;
-        for (auto& r : rec)
-            if (r.first == kind) {
-                float ms = 0;
-                HGX_HIP(hipEventElapsedTime(&ms, r.second.a, r.second.b));
-                t += ms;
-            }
-        return t;
+    void collect(hgx_bfs_stats& st) {
+        for (auto& r : rec) {
+            float ms = 0;
+            HGX_HIP(hipEventElapsedTime(&ms, r.e.a, r.e.b));
+            st.ms_kernel[r.kind] += ms;
+            if (r.level < 64) st.level_ms[r.level] += ms;
+        }
     }
 };
 
 enum { kKindGather = HGX_K_LINK_GATHER, kKindPull = HGX_K_ATOM_PULL, kKindHeavy = HGX_K_PULL_HEAVY,
        kKindHub = HGX_K_HUB_FINALIZE };
+
+FullMask full_mask(int S, int W) {
+    FullMask fm;
+    for (int w = 0; w < 16; ++w) {
+        int n = S - w * 64;
+        fm.w[w] = (w >= W || n <= 0) ? 0ull : (n >= 64 ? ~0ull : ((1ull << n) - 1ull));
+    }
+    return fm;
+}
 
 template <int W, int MODE>
 void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_depth, int32_t want_type,
@@ -564,13 +921,15 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const int64_t A = g->A, M = g->M;
     const size_t row_bytes = sizeof(u64) * (size_t)A * W;
     const size_t bm_bytes = res->bm_bytes();
-    const size_t la_bytes = sizeof(uint32_t) * (size_t)(M / 32 + 2);
+    const size_t la_bytes = sizeof(u64) * (size_t)(M / 64 + 2);
+    const FullMask fm = full_mask(bt.S, W);
 
     u64* vis = (u64*)g->alloc(row_bytes);
     u64* lf = (MODE == kSym) ? (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W) : nullptr;
     u64* hubacc = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W);
-    uint32_t* ever = (uint32_t*)g->alloc(bm_bytes);
-    uint32_t* la = (uint32_t*)g->alloc(la_bytes);
+    u64* ever = (u64*)g->alloc(bm_bytes);
+    u64* full = (u64*)g->alloc(bm_bytes);
+    u64* la = (u64*)g->alloc(la_bytes);
     const int max_levels_cap = 4096;
     u64* ctr = (u64*)g->alloc(sizeof(u64) * cNum * max_levels_cap);
     int32_t* d_atoms = (int32_t*)g->alloc(sizeof(int32_t) * seed_atoms.size());
@@ -578,61 +937,113 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* h_new = (u64*)g->pinned_buf(sizeof(u64) * cNum);
 
     HGX_HIP(hipMemsetAsync(ever, 0, bm_bytes, s));
+    HGX_HIP(hipMemsetAsync(full, 0, bm_bytes, s));
     HGX_HIP(hipMemsetAsync(hubacc, 0, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W, s));
     HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * cNum * max_levels_cap, s));
     HGX_HIP(hipMemcpyAsync(d_atoms, seed_atoms.data(), sizeof(int32_t) * seed_atoms.size(), hipMemcpyHostToDevice, s));
     HGX_HIP(hipMemcpyAsync(d_rows, seed_rows.data(), sizeof(u64) * seed_rows.size(), hipMemcpyHostToDevice, s));
 
     bt.lvl.push_back((u64*)g->alloc(row_bytes));
-    bt.fa.push_back((uint32_t*)g->alloc(bm_bytes));
+    bt.fa.push_back((u64*)g->alloc(bm_bytes));
     HGX_HIP(hipMemsetAsync(bt.fa[0], 0, bm_bytes, s));
     {
         int n = (int)seed_atoms.size();
-        hgx_seed<W><<<grid_for((int64_t)n * W, 256, 1 << 20), 256, 0, s>>>(n, d_atoms, d_rows, bt.lvl[0], vis,
-                                                                           bt.fa[0], ever);
+        hgx_seed<W><<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_atoms, d_rows, bt.lvl[0], vis, bt.fa[0], ever,
+                                                              full, fm);
         HGX_CHECK_LAUNCH();
     }
 
     const int block = 256;
-    const int gather_grid = grid_for(M * Lay<W>::G, block, 256 * 16);
-    const int pull_grid = grid_for(A * Lay<W>::G, block, 256 * 16);
+    const int gather_grid = grid_for(ceil_div(M, 64) * 64, block, 256 * 16);
+    const int pull_grid = grid_for(ceil_div(A, 64) * 64, block, 256 * 16);
     const int hub_grid = grid_for(std::max<int64_t>(g->n_heavy, 1) * Lay<W>::G, block, 256 * 16);
     const int32_t maxd = max_depth < 0 ? INT32_MAX : max_depth;
 
+    // Direction choice per level (Beamer-style): when the frontier's incidence volume
+    // sum_{v in F} |inc(v)| is small, the level runs sparse -- candidate links are pushed from the
+    // frontier atoms and only candidate tiles are gathered / pulled.  Otherwise every tile is scanned.
+    const bool sparse_ok = (g->bfs_flags & 8) != 0;
+    u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
+    u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
+    u64 push_volume = 0;
+    if (sparse_ok) {
+        u64* dv = ctr + (size_t)(max_levels_cap - 1) * cNum;   // scratch slot
+        hgx_seed_degree<<<grid_for((int64_t)seed_atoms.size(), 256, 1 << 20), 256, 0, s>>>(
+            (int32_t)seed_atoms.size(), d_atoms, g->inc_off, dv);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipMemcpyAsync(&push_volume, dv, sizeof(u64), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+    }
+    const u64 sparse_limit = (u64)std::max<int64_t>(M / 16, 1024);
+
     for (int32_t d = 0; d < maxd && d < max_levels_cap - 1; ++d) {
         u64* lvl = bt.lvl[d];
-        uint32_t* fa = bt.fa[d];
+        u64* fa = bt.fa[d];
         u64* lvl_next = (u64*)g->alloc(row_bytes);
-        uint32_t* fa_next = (uint32_t*)g->alloc(bm_bytes);
+        u64* fa_next = (u64*)g->alloc(bm_bytes);   // every word written by hgx_atom_pull
         u64* c = ctr + (size_t)d * cNum;
-        HGX_HIP(hipMemsetAsync(la, 0, la_bytes, s));
-        HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
+        const bool sparse = sparse_ok && push_volume < sparse_limit;
+        if (sparse) {
+            Events e0 = tm.start(kKindGather, d);
+            HGX_HIP(hipMemsetAsync(lcand, 0, la_bytes, s));
+            HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
+            hgx_frontier_links<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(
+                A, fa, g->inc_off, g->inc_row, g->link_type, want_type, lcand);
+            HGX_CHECK_LAUNCH();
+            if (g->n_chunks > 0) {
+                hgx_frontier_links_heavy<<<(unsigned)g->n_chunks, 256, 0, s>>>(g->chunks, fa, g->inc_row,
+                                                                             g->link_type, want_type, lcand);
+                HGX_CHECK_LAUNCH();
+            }
+            tm.stop(e0);
+        }
+        u64* lc = sparse ? lcand : nullptr;
+        u64* cd = sparse ? cand : nullptr;
 
-        Events e1 = tm.start(kKindGather);
+        Events e1 = tm.start(kKindGather, d);
         hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
-                                                                      want_type, fa, lvl, lf, la, c);
+                                                                      want_type, fa, full, lvl, lf, la, c, fm,
+                                                                      g->bfs_flags, lc, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
-        Events e2 = tm.start(kKindPull);
+        if (sparse && MODE == kSym) {
+            // push direction: candidates are few, hubs must not be re-scanned
+            Events e2 = tm.start(kKindPull, d);
+            hgx_push_zero<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, W, cand, full, lvl_next);
+            HGX_CHECK_LAUNCH();
+            hgx_push_rows<<<grid_for(ceil_div(M, 64) * 64, 256, 4096), 256, 0, s>>>(M, W, la, g->tgt_off, g->tgt_idx,
+                                                                                 lf, full, lvl_next);
+            HGX_CHECK_LAUNCH();
+            hgx_push_finalize<W><<<pull_grid, block, 0, s>>>(A, g->inc_off, cand, vis, ever, full, lvl_next, fa_next,
+                                                             c, fm);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e2);
+        } else {
+        Events e2 = tm.start(kKindPull, d);
         hgx_atom_pull<W, MODE><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, g->tgt_off,
-                                                           g->tgt_idx, fa, lvl, vis, ever, lvl_next, fa_next, c);
+                                                           g->tgt_idx, fa, lvl, vis, ever, full, lvl_next, fa_next, c,
+                                                           fm, g->bfs_flags, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
         if (g->n_chunks > 0) {
-            Events e3 = tm.start(kKindHeavy);
+            Events e3 = tm.start(kKindHeavy, d);
             hgx_atom_pull_heavy<W, MODE><<<(unsigned)g->n_chunks, block, 0, s>>>(
-                g->chunks, g->inc_row, la, lf, g->tgt_off, g->tgt_idx, fa, lvl, hubacc, c);
+                g->chunks, g->inc_row, la, lf, g->tgt_off, g->tgt_idx, fa, lvl, vis, ever, full, hubacc, c, fm,
+                g->bfs_flags, cd);
             HGX_CHECK_LAUNCH();
             tm.stop(e3);
-            Events e4 = tm.start(kKindHub);
-            hgx_hub_finalize<W><<<hub_grid, block, 0, s>>>(g->n_heavy, g->heavy_atom, hubacc, vis, ever, lvl_next,
-                                                           fa_next, c);
+            Events e4 = tm.start(kKindHub, d);
+            hgx_hub_finalize<W><<<hub_grid, block, 0, s>>>(g->n_heavy, g->heavy_atom, g->inc_off, hubacc, vis, ever,
+                                                           full, lvl_next, fa_next, c, fm);
             HGX_CHECK_LAUNCH();
             tm.stop(e4);
+        }
         }
         HGX_HIP(hipMemcpyAsync(h_new, c, sizeof(u64) * cNum, hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
+        level_ctr.back()[cDirRows] = sparse ? 1 : 0;   // (host-side) mode of this level
+        push_volume = h_new[cNewDeg];
         if (h_new[cNewAtoms] == 0) {
             g->release(lvl_next, row_bytes);
             g->release(fa_next, bm_bytes);
@@ -645,7 +1056,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     if (lf) g->release(lf, sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W);
     g->release(hubacc, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W);
     g->release(ever, bm_bytes);
+    g->release(full, bm_bytes);
     g->release(la, la_bytes);
+    if (lcand) g->release(lcand, la_bytes);
+    if (cand) g->release(cand, bm_bytes);
     g->release(ctr, sizeof(u64) * cNum * max_levels_cap);
     g->release(d_atoms, sizeof(int32_t) * seed_atoms.size());
     g->release(d_rows, sizeof(u64) * seed_rows.size());
@@ -672,16 +1086,15 @@ int words_for(int S) {
 }
 
 template <int W>
-void count_level(hgx_graph* g, const uint32_t* fa, const u64* lvl, u64* counts, u64* trav) {
+void count_level(hgx_graph* g, const u64* fa, const u64* lvl, u64* counts, u64* trav) {
     const int per_block = 256 / W;
     int64_t blocks = ceil_div(g->A, per_block);
-    // keep atoms per thread < 2^22 (bit-sliced planes)
-    int grid = (int)std::min<int64_t>(blocks, 8192);
+    int grid = (int)std::min<int64_t>(blocks, 8192);   // keeps atoms per thread < 2^22
     hgx_level_count<W><<<std::max(grid, 1), 256, 0, g->stream>>>(g->A, fa, lvl, g->inc_off, counts, trav);
     HGX_CHECK_LAUNCH();
 }
 
-void count_level_dispatch(int W, hgx_graph* g, const uint32_t* fa, const u64* lvl, u64* counts, u64* trav) {
+void count_level_dispatch(int W, hgx_graph* g, const u64* fa, const u64* lvl, u64* counts, u64* trav) {
     switch (W) {
         case 1: count_level<1>(g, fa, lvl, counts, trav); break;
         case 2: count_level<2>(g, fa, lvl, counts, trav); break;
@@ -691,7 +1104,7 @@ void count_level_dispatch(int W, hgx_graph* g, const uint32_t* fa, const u64* lv
     }
 }
 
-// Fill res->counts and the TEPS numerator (first call only).
+// Fill res->counts, the TEPS numerator and the survey-model bytes (first call only).
 void ensure_counts(hgx_bfs_result* r) {
     if (r->counts_ready) return;
     hgx_graph* g = r->g;
@@ -708,13 +1121,11 @@ void ensure_counts(hgx_bfs_result* r) {
             HGX_HIP(hipMemcpyAsync(hc.data(), dc, sizeof(u64) * 1025, hipMemcpyDeviceToHost, g->stream));
             HGX_HIP(hipStreamSynchronize(g->stream));
             for (int s = 0; s < bt.S; ++s) r->counts[(size_t)(bt.seed0 + s) * r->n_levels + d] = (int64_t)hc[s];
-            // expanded levels are those below the last level that was expanded
             if (d < bt.n_expanded) {
                 trav_total += (double)hc[1024];
-                // SURVEY.md 8(d) push-model bytes from the union frontier of this level
                 HGX_HIP(hipMemsetAsync(dc, 0, sizeof(u64) * 4, g->stream));
-                hgx_level_survey<<<grid_for(g->A, 256, 8192), 256, 0, g->stream>>>(g->A, bt.fa[d], g->inc_off,
-                                                                                    g->inc_row, g->tgt_off, dc);
+                hgx_level_survey<<<grid_for(std::max(g->A, g->M), 256, 8192), 256, 0, g->stream>>>(
+                    g->A, g->M, bt.fa[d], g->tgt_off, g->tgt_idx, dc);
                 HGX_CHECK_LAUNCH();
                 u64 sv[3];
                 HGX_HIP(hipMemcpyAsync(sv, dc, sizeof(sv), hipMemcpyDeviceToHost, g->stream));
@@ -761,7 +1172,7 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
     r->typed = o.link_type >= 0;
 
     Timer tm(g);
-    if (tm.on) HGX_HIP(hipEventRecord(tm.begin_all.a, g->stream));
+    if (tm.on) HGX_HIP(hipEventRecord(tm.all.a, g->stream));
     std::vector<std::vector<u64>> level_ctr;
     int max_expanded = 0;
     for (int32_t s0 = 0; s0 < n_seeds; s0 += 1024) {
@@ -790,26 +1201,30 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
             case 8: run_mode<8>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
             default: run_mode<16>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
         }
-        // accounting for this batch (levels expanded = level_ctr entries added)
+        // algorithmic bytes of every launch of this batch
         const int64_t A = g->A, M = g->M, P = g->P, I = g->I;
-        (void)I;
         const double rowb = 8.0 * bt.W;
         const bool typed = o.link_type >= 0;
-        int nexp = (int)(level_ctr.size() - before);
+        const int nexp = (int)(level_ctr.size() - before);
         bt.n_expanded = nexp;
         max_expanded = std::max(max_expanded, nexp);
         const double I_light = (double)(I - g->I_heavy), I_heavy = (double)g->I_heavy;
         for (int d = 0; d < nexp; ++d) {
             const auto& c = level_ctr[before + d];
-            // hgx_link_gather: tgt_off + tgt_idx (+ link_type) + frontier bitmap + gathered rows + lf/la writes
+            // hgx_link_gather: tgt_off + tgt_idx (+ link_type) + frontier/full bitmaps + gathered rows
+            //                  + lf writes + la words
+            const bool sparse_level = c[cDirRows] != 0;
+            const double scan_links = sparse_level ? (double)c[cActiveLinks] : (double)M;
+            const double scan_pins = sparse_level ? (double)c[cActivePins] : (double)P;
             r->stats.bytes_kernel[HGX_K_LINK_GATHER] +=
-                8.0 * (M + 1) + 4.0 * P + (typed ? 4.0 * M : 0.0) + A / 8.0 + rowb * c[cActivePins] +
-                (mode == kSym ? rowb * c[cActiveLinks] : 0.0) + M / 8.0;
+                8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) + A / 4.0 +
+                rowb * c[cActivePins] + (mode == kSym ? rowb * c[cActiveLinks] : 0.0) + M / 8.0;
             // hgx_atom_pull: inc_off + light inc_row + la bitmap + pulled rows + vis reads + lvl/vis writes
-            //                + ever/fa_next bitmaps
-            r->stats.bytes_kernel[HGX_K_ATOM_PULL] += 8.0 * (A + 1) + 4.0 * I_light + M / 8.0 +
-                                                      rowb * c[cIncLight] + rowb * c[cAccLight] +
-                                                      2.0 * rowb * c[cNewLight] + A / 4.0;
+            //                + ever/full/fa_next words
+            r->stats.bytes_kernel[HGX_K_ATOM_PULL] += (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) +
+                                                      M / 8.0 +
+                                                      rowb * c[cIncLight] + rowb * c[cVisLight] +
+                                                      2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
             if (g->n_chunks > 0) {
                 r->stats.bytes_kernel[HGX_K_PULL_HEAVY] += 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] +
                                                            rowb * g->n_chunks;
@@ -820,10 +1235,11 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
             }
             r->stats.launches[HGX_K_LINK_GATHER] += 1;
             r->stats.launches[HGX_K_ATOM_PULL] += 1;
+            if (d < 64) r->stats.level_new[d] += (int64_t)c[cNewAtoms];
         }
         r->batches.push_back(std::move(bt));
     }
-    if (tm.on) HGX_HIP(hipEventRecord(tm.end_all.a, g->stream));
+    if (tm.on) HGX_HIP(hipEventRecord(tm.all.b, g->stream));
     HGX_HIP(hipStreamSynchronize(g->stream));
     int nl = 1;
     for (auto& bt : r->batches) nl = std::max(nl, (int)bt.lvl.size());
@@ -832,9 +1248,9 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
     r->stats.n_batches = (int32_t)r->batches.size();
     if (tm.on) {
         float ms = 0;
-        HGX_HIP(hipEventElapsedTime(&ms, tm.begin_all.a, tm.end_all.a));
+        HGX_HIP(hipEventElapsedTime(&ms, tm.all.a, tm.all.b));
         r->stats.ms_total = ms;
-        for (int k = 0; k < HGX_K_COUNT; ++k) r->stats.ms_kernel[k] = tm.total(k);
+        tm.collect(r->stats);
     }
     guard.r = nullptr;
     *out = r;
@@ -920,7 +1336,7 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
     }
     int32_t* dres = (int32_t*)(tab + 2 * nl);
     HGX_HIP(hipMemcpyAsync(tab, h.data(), sizeof(void*) * 2 * nl, hipMemcpyHostToDevice, g->stream));
-    hgx_depth_probe<<<1, 64, 0, g->stream>>>(nl, (const uint32_t* const*)tab, (const u64* const*)(tab + nl), bt.W,
+    hgx_depth_probe<<<1, 64, 0, g->stream>>>(nl, (const u64* const*)tab, (const u64* const*)(tab + nl), bt.W,
                                              seed_index % 1024, atom, dres);
     HGX_CHECK_LAUNCH();
     HGX_HIP(hipMemcpyAsync(depth_out, dres, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));

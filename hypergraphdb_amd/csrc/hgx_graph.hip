@@ -59,16 +59,24 @@ __global__ void __launch_bounds__(256) k_pin_keys(int64_t M, const int64_t* __re
     if (dups) atomicAdd(n_dup, dups);
 }
 
-// inc_row[i] = low word; inc_off[a] = first i with key atom >= a.
-__global__ void __launch_bounds__(256) k_cut_rows(int64_t I, int64_t A, const uint64_t* __restrict__ keys,
-                                                  int32_t* __restrict__ inc_row,
-                                                  int64_t* __restrict__ inc_off) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= I;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t a = i < I ? (int64_t)(keys[i] >> 32) : A;
-        int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> 32) : -1;
-        if (i < I) inc_row[i] = (int32_t)(uint32_t)keys[i];
-        for (int64_t x = prev + 1; x <= a; ++x) inc_off[x] = i;
+// inc_row[i] = low word of key i.
+__global__ void __launch_bounds__(256) k_cut_rows(int64_t I, const uint64_t* __restrict__ keys,
+                                                  int32_t* __restrict__ inc_row) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x)
+        inc_row[i] = (int32_t)(uint32_t)keys[i];
+}
+
+// inc_off[a] = first i with (keys[i] >> 32) >= a  (binary search per atom; a in [0, A])
+__global__ void __launch_bounds__(256) k_row_offsets(int64_t I, int64_t A, const uint64_t* __restrict__ keys,
+                                                     int64_t* __restrict__ inc_off) {
+    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a <= A; a += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = I;
+        const uint64_t key = (uint64_t)a << 32;
+        while (lo < hi) {
+            int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        inc_off[a] = lo;
     }
 }
 
@@ -184,6 +192,13 @@ const char* hgx_version(void) { return "hgx 0.1.0 (gfx950)"; }
 
 const char* hgx_last_error(void) { return t_last_error.c_str(); }
 
+int hgx_device_synchronize(int32_t device) {
+    HGX_API_BEGIN
+    HGX_HIP(hipSetDevice(device));
+    HGX_HIP(hipDeviceSynchronize());
+    HGX_API_END
+}
+
 int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     HGX_API_BEGIN
     if (!d || !out) fail(HGX_E_INVALID, "hgx_graph_create: null argument");
@@ -271,7 +286,9 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
         HGX_HIP(hipStreamSynchronize(s));
         I = P - (int64_t)hdup;
         HGX_HIP(hipMalloc(&g->inc_row, sizeof(int32_t) * std::max<int64_t>(I, 1)));
-        k_cut_rows<<<grid_for(I + 1, 256), 256, 0, s>>>(I, A, sorted, g->inc_row, g->inc_off);
+        k_cut_rows<<<grid_for(I, 256), 256, 0, s>>>(I, sorted, g->inc_row);
+        HGX_CHECK_LAUNCH();
+        k_row_offsets<<<grid_for(A + 1, 256), 256, 0, s>>>(I, A, sorted, g->inc_off);
         HGX_CHECK_LAUNCH();
         HGX_HIP(hipStreamSynchronize(s));
         g->release(tmp, tmp_bytes);
@@ -347,6 +364,15 @@ int hgx_set_timing(hgx_graph* g, int32_t enabled) {
     if (!g) fail(HGX_E_INVALID, "null graph");
     std::lock_guard<std::mutex> lk(g->mu);
     g->timing = enabled != 0;
+    HGX_API_END
+}
+
+int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
+    HGX_API_BEGIN
+    if (!g) fail(HGX_E_INVALID, "null graph");
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (option == HGX_OPT_BFS_FLAGS) g->bfs_flags = (int32_t)value;
+    else fail(HGX_E_INVALID, "hgx_set_option: unknown option");
     HGX_API_END
 }
 

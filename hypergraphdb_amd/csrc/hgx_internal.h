@@ -83,6 +83,7 @@ struct hgx_graph {
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
+    int32_t bfs_flags = 0xE;        // HGX_OPT_BFS_FLAGS (see hgx.h)
 
     int64_t A = 0, M = 0, P = 0, I = 0;
     int32_t* link_atom = nullptr;

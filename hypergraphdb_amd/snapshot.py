@@ -126,6 +126,9 @@ class HyperGraphSnapshot:
     def set_timing(self, on=True):
         check(lib().hgx_set_timing(self.handle, 1 if on else 0))
 
+    def set_option(self, option, value):
+        check(lib().hgx_set_option(self.handle, int(option), int(value)))
+
     def close(self):
         if getattr(self, "_h", None) is not None:
             lib().hgx_graph_destroy(self._h)

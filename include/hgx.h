@@ -107,10 +107,14 @@ typedef struct hgx_bfs_stats {
     double  bytes_survey;
     double  traversed_edges;
     int64_t union_frontier[64];        /* |U_d| per expanded level (summed over batches)       */
+    double  level_ms[64];              /* device ms of all kernels of level d (timing enabled) */
+    int64_t level_new[64];             /* atoms with a new bit at level d+1 (summed over batches) */
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
 const char *hgx_last_error(void);
+/* hipDeviceSynchronize on one device (benchmark brackets; no graph needed). */
+int hgx_device_synchronize(int32_t device);
 
 /* device: HIP device ordinal to place the snapshot on. */
 int  hgx_graph_create(const hgx_graph_desc *desc, int32_t device, hgx_graph **out);
@@ -121,6 +125,13 @@ int  hgx_graph_degree(hgx_graph *g, const int32_t *atoms, int32_t n, int64_t *ou
 /* inc(atom) as link ATOM ids, ascending; *n_out = |inc(atom)| even when > cap. */
 int  hgx_graph_incidence(hgx_graph *g, int32_t atom, int32_t *out, int64_t cap, int64_t *n_out);
 int  hgx_set_timing(hgx_graph *g, int32_t enabled);
+/* Engine options (tuning / A-B experiments; defaults are the tuned values):
+ *   HGX_OPT_BFS_FLAGS: bit 0 = gather early exit, bit 1 = pull early exit,
+ *                      bit 2 = skip atoms / links already visited by every traversal,
+ *                      bit 3 = frontier-driven sparse levels (direction optimisation).
+ *                      Default 0xE. */
+#define HGX_OPT_BFS_FLAGS 1
+int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
 
 /* Batched multi-source BFS.  Seed i is HGBreadthFirstTraversal(seeds[i], gen, max_depth)
  * (max_depth HGX_UNBOUNDED = Integer.MAX_VALUE).  The result holds, per seed and per

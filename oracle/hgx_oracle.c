@@ -284,8 +284,18 @@ typedef void (*og_bfs_emit)(void *ctx, int32_t link, int32_t atom, int32_t dist)
 /* Returns the number of pairs returned by next(); *traversed = sum of |inc(v)| over
  * the atoms passed to advance() that were below maxDistance (the atoms whose
  * incidence set was iterated, :49-66). */
+static double og_now(void)
+{
+#ifdef _OPENMP
+    return omp_get_wtime();
+#else
+    return 0.0;
+#endif
+}
+
 static int64_t bfs_run(const og_graph *g, const og_algen *o, og_bfs_state *s, int32_t seed,
-                       int32_t max_dist, og_bfs_emit emit, void *ctx, int64_t *traversed)
+                       int32_t max_dist, og_bfs_emit emit, void *ctx, int64_t *traversed,
+                       double deadline)
 {
     int32_t maxd = max_dist < 0 ? INT_MAX : max_dist;
     uint32_t ep = ++s->epoch;
@@ -313,6 +323,7 @@ static int64_t bfs_run(const og_graph *g, const og_algen *o, og_bfs_state *s, in
         }
         /* next(): x = to_explore.remove(); examined.put(atom, TRUE); advance (:143-156) */
         if (head == tail) break;
+        if (deadline > 0 && (head & 1023) == 0 && og_now() > deadline) break;   /* bounded sample */
         int32_t l = s->q_link[head], a = s->q_atom[head], d = s->q_dist[head];
         head++;
         s->flag[a] = 1;
@@ -344,7 +355,7 @@ int64_t og_bfs(const og_graph *g, const og_algen *o, int32_t seed, int32_t max_d
     og_bfs_state s;
     if (bfs_state_init(&s, g->A)) { bfs_state_free(&s); return -1; }
     seq_ctx c = { out_link, out_atom, out_dist, cap, 0 };
-    bfs_run(g, o, &s, seed, max_dist, seq_emit, &c, traversed);
+    bfs_run(g, o, &s, seed, max_dist, seq_emit, &c, traversed, 0.0);
     bfs_state_free(&s);
     return c.n;
 }
@@ -359,8 +370,10 @@ static void cnt_emit(void *c, int32_t link, int32_t atom, int32_t dist)
 
 int og_bfs_many(const og_graph *g, const og_algen *o, const int32_t *seeds, int32_t n_seeds,
                 int32_t max_dist, int32_t max_levels, int64_t *counts, int64_t *traversed,
-                int32_t nthreads)
+                int32_t nthreads, double time_budget_s, double *elapsed_s)
 {
+    double t0 = og_now();
+    double deadline = time_budget_s > 0 ? t0 + time_budget_s : 0.0;
     for (int32_t i = 0; i < n_seeds; i++) if (seeds[i] < 0 || seeds[i] >= g->A) return -2;
     memset(counts, 0, sizeof(int64_t) * (size_t)n_seeds * (size_t)max_levels);
     int err = 0;
@@ -379,13 +392,14 @@ int og_bfs_many(const og_graph *g, const og_algen *o, const int32_t *seeds, int3
                 cnt_ctx c = { counts + (size_t)i * (size_t)max_levels, max_levels };
                 if (max_levels > 0) c.counts[0] = 1;
                 int64_t tr = 0;
-                bfs_run(g, o, &s, seeds[i], max_dist, cnt_emit, &c, &tr);
+                bfs_run(g, o, &s, seeds[i], max_dist, cnt_emit, &c, &tr, deadline);
                 if (traversed) traversed[i] = tr;
             }
         }
         bfs_state_free(&s);
     }
     (void)nthreads;
+    if (elapsed_s) *elapsed_s = og_now() - t0;
     return err ? -1 : 0;
 }
 

@@ -83,10 +83,13 @@ int64_t og_bfs(const og_graph *g, const og_algen *o, int32_t seed, int32_t max_d
 /* Many independent traversals (the CPU baseline): per seed, counts of atoms
  * returned at each distance 1..max_levels-1 (index 0 = the seed itself, always 1).
  * counts is [n_seeds * max_levels].  traversed[n_seeds] receives the hyperedge
- * TEPS numerator per seed.  nthreads <= 0: all cores (OpenMP). */
+ * TEPS numerator per seed.  nthreads <= 0: all cores (OpenMP).
+ * time_budget_s > 0 bounds the sample: a traversal still running that long after the
+ * call started stops (its counts/traversed are then partial); *elapsed_s receives the
+ * wall time of the call. */
 int og_bfs_many(const og_graph *g, const og_algen *o, const int32_t *seeds, int32_t n_seeds,
                 int32_t max_dist, int32_t max_levels, int64_t *counts, int64_t *traversed,
-                int32_t nthreads);
+                int32_t nthreads, double time_budget_s, double *elapsed_s);
 
 /* OrderedLinkCondition.satisfies on a link's target array
  * (C/query/OrderedLinkCondition.java:92-124); pattern entries < 0 are hg.anyHandle(). */

@@ -56,7 +56,7 @@ def lib():
                              i32p, i32p, i32p, C.c_int64, C.POINTER(C.c_int64)]
         L.og_bfs.restype = C.c_int64
         L.og_bfs_many.argtypes = [C.POINTER(OgGraph), C.POINTER(OgAlgen), i32p, C.c_int32, C.c_int32,
-                                  C.c_int32, i64p, i64p, C.c_int32]
+                                  C.c_int32, i64p, i64p, C.c_int32, C.c_double, C.POINTER(C.c_double)]
         L.og_bfs_many.restype = C.c_int
         L.og_ordered_link.argtypes = [i32p, C.c_int32, i32p, C.c_int32]
         L.og_ordered_link.restype = C.c_int
@@ -138,15 +138,21 @@ class OracleGraph:
             out.append(np.sort(a[d == k]))
         return out
 
-    def bfs_many(self, seeds, max_dist, max_levels, opts=None, nthreads=0):
+    def bfs_many(self, seeds, max_dist, max_levels, opts=None, nthreads=0, time_budget_s=0.0, timing=None):
+        """Per-seed level counts [n, max_levels] and TEPS numerators.  With time_budget_s > 0 the
+        traversals still running after that long stop early (bounded CPU-baseline sample); pass a
+        dict as ``timing`` to receive the elapsed wall time."""
         opts = opts or algen()
         seeds = np.ascontiguousarray(seeds, np.int32)
         counts = np.zeros(len(seeds) * max_levels, np.int64)
         trav = np.zeros(len(seeds), np.int64)
+        el = C.c_double(0)
         rc = lib().og_bfs_many(C.byref(self.g), C.byref(opts), seeds, len(seeds), int(max_dist),
-                               int(max_levels), counts, trav, int(nthreads))
+                               int(max_levels), counts, trav, int(nthreads), float(time_budget_s), C.byref(el))
         if rc != 0:
             raise RuntimeError(f"og_bfs_many failed {rc}")
+        if timing is not None:
+            timing["elapsed_s"] = el.value
         return counts.reshape(len(seeds), max_levels), trav
 
     def and_query(self, type_=-1, incident=(), pattern=None, zigzag=True):

@@ -223,3 +223,21 @@ def test_depth_of_and_errors():
         bfs_batch(snap, [g["num_atoms"]], 2)
     with pytest.raises(HGXError):
         res.visited(5, 0)
+
+
+@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE])
+def test_engine_option_matrix(flags):
+    """Every work-avoidance option (early exits, full-visited skipping, frontier-driven sparse
+    levels) returns the same per-depth sets; power-law hubs + random edge cases + ordered modes."""
+    from hypergraphdb_amd import _lib, synth
+    cases = []
+    rng = np.random.default_rng(77)
+    cases.append((K.random_graph(rng, 800, 2500, max_arity=7, n_types=3), K.ALGEN_MODES[0], -1, None))
+    cases.append((K.random_graph(rng, 800, 2500, max_arity=7, n_types=3), K.ALGEN_MODES[4], 1, 3))
+    cases.append((synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=12), K.ALGEN_MODES[0], -1, 3))
+    cases.append((synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=13), K.ALGEN_MODES[1], 2, None))
+    for g, mode, lt, maxd in cases:
+        snap, orc = snapshot(g), oracle(g)
+        snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
+        seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
+        check_batch(g, seeds, maxd, mode, lt, snap, orc)
