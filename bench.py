@@ -201,15 +201,20 @@ def main():
         snap3 = H.HyperGraphSnapshot(g3["num_atoms"], g3["link_atom"], g3["tgt_off"], g3["tgt_idx"],
                                      g3["link_type"], device=local)
         snap3.set_timing(True)
-        qs = [(int(Q["type"][i]), [int(Q["a"][i])], (int(Q["x"][i]), -1, int(Q["y"][i])))
-              for i in range(len(Q["type"]))]
+        from hypergraphdb_amd.query import pattern_batch_arrays
+        nq = len(Q["type"])
+        # hg.and(hg.type(T), hg.incident(a), hg.orderedLink(x, hg.anyHandle(), y)) as one packed batch
+        packed = (Q["type"], np.arange(nq + 1, dtype=np.int64), Q["a"], np.ones(nq, np.int32),
+                  np.arange(0, 3 * nq + 1, 3, dtype=np.int64),
+                  np.stack([Q["x"], np.full(nq, -1, np.int32), Q["y"]], 1).reshape(-1))
+        qs = range(nq)
         for _ in range(args.warmup):
-            H.pattern_batch(snap3, qs)
+            pattern_batch_arrays(snap3, *packed)
         ms, nres = [], 0
         barrier_sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            r = H.pattern_batch(snap3, qs)
+            r = pattern_batch_arrays(snap3, *packed)
             ms.append(r.ms)
             nres = int(r.offsets[-1])
         barrier_sync()

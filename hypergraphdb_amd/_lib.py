@@ -30,7 +30,7 @@ EXPORTED = (
     "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
-    "hgx_bfs_result_free", "hgx_pattern_batch", "hgx_query_result_offsets", "hgx_query_result_ids",
+    "hgx_bfs_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
 )
 
@@ -57,7 +57,9 @@ class BfsStats(C.Structure):
     _fields_ = [("n_levels_expanded", C.c_int32), ("n_batches", C.c_int32), ("ms_total", C.c_double),
                 ("ms_kernel", C.c_double * 4), ("launches", C.c_int64 * 4), ("bytes_kernel", C.c_double * 4),
                 ("bytes_survey", C.c_double), ("traversed_edges", C.c_double),
-                ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64)]
+                ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64),
+                ("level_bytes", C.c_double * 64), ("level_sparse", C.c_int32 * 64),
+                ("level_rows", (C.c_int64 * 8) * 64)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
@@ -68,6 +70,9 @@ class BfsStats(C.Structure):
         d["union_frontier"] = [int(x) for x in self.union_frontier[:n]]
         d["level_ms"] = [round(float(x), 4) for x in self.level_ms[:n]]
         d["level_new"] = [int(x) for x in self.level_new[:n]]
+        d["level_bytes"] = [float(x) for x in self.level_bytes[:n]]
+        d["level_sparse"] = [int(x) for x in self.level_sparse[:n]]
+        d["level_rows"] = [[int(v) for v in self.level_rows[i]] for i in range(n)]
         return d
 
 
@@ -114,6 +119,7 @@ def lib():
         "hgx_bfs_result_stats": ([vp, i32, C.POINTER(BfsStats)], C.c_int),
         "hgx_bfs_result_free": ([vp], None),
         "hgx_pattern_batch": ([vp, C.POINTER(AndQuery), i32, C.POINTER(vp)], C.c_int),
+        "hgx_pattern_batch_packed": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),
         "hgx_query_result_offsets": ([vp, vp], C.c_int),
         "hgx_query_result_ids": ([vp, vp], C.c_int),
         "hgx_query_result_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),

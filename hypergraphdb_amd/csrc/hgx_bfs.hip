@@ -132,6 +132,7 @@ enum Ctr {
     cNewAtoms,          // all new atoms of the level (early stop)
     cDirRows,           // ordered modes: target rows re-read in the pull
     cNewDeg,            // sum of |inc(v)| over the new atoms (next level's push volume)
+    cNewFull,           // atoms that became visited by every traversal
     cNum = 12
 };
 
@@ -180,16 +181,27 @@ __global__ void __launch_bounds__(256) hgx_link_gather(int64_t M, const int64_t*
                 bool all_full = true;
                 if constexpr (G >= 4) {
                     // lane `sub` loads target p+sub and checks its own bitmap bits; the group then
-                    // gathers the active rows (16 B per lane) via ballot + shuffle
+                    // gathers the active rows (16 B per lane) via ballot + shuffle.  The full bits of
+                    // all targets are known before any row is loaded: a link whose targets are all
+                    // visited by every traversal costs no row traffic.
                     const int base = lane & ~(G - 1);
+                    const u64 gmask = (1ull << G) - 1ull;
                     bool any_not_full = !skip_full;
+                    if (e - b > G && skip_full) {          // long rows: full bits first
+                        for (int64_t p = b; p < e && !any_not_full; p += G) {
+                            const int64_t q = p + sub;
+                            const int32_t myv = q < e ? tgt_idx[q] : -1;
+                            any_not_full |= ((__ballot(myv >= 0 && !bit(full, myv)) >> base) & gmask) != 0ull;
+                        }
+                    }
                     for (int64_t p = b; p < e; p += G) {
                         const int64_t q = p + sub;
                         const int32_t myv = q < e ? tgt_idx[q] : -1;
+                        if (e - b <= G && skip_full)
+                            any_not_full = ((__ballot(myv >= 0 && !bit(full, myv)) >> base) & gmask) != 0ull;
+                        if (!any_not_full) break;           // every target full: nobody pulls this row
                         const bool mya = myv >= 0 && bit(fa, myv);
-                        const bool mynf = myv >= 0 && skip_full && !bit(full, myv);
-                        const unsigned ga = (unsigned)((__ballot(mya) >> base) & ((1ull << G) - 1ull));
-                        any_not_full |= ((__ballot(mynf) >> base) & ((1ull << G) - 1ull)) != 0ull;
+                        const unsigned ga = (unsigned)((__ballot(mya) >> base) & gmask);
                         typename V::T r[G];
 #pragma unroll
                         for (int k = 0; k < G; ++k) {
@@ -199,10 +211,7 @@ __global__ void __launch_bounds__(256) hgx_link_gather(int64_t M, const int64_t*
 #pragma unroll
                         for (int k = 0; k < G; ++k) acc |= r[k];
                         nact += __popc(ga);
-                        if (early && p + G < e && group_all<G>(V::eq(acc, FULL))) {
-                            any_not_full = true;
-                            break;
-                        }
+                        if (early && p + G < e && group_all<G>(V::eq(acc, FULL))) break;
                     }
                     all_full = !any_not_full;
                 } else {
@@ -388,7 +397,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0;
+    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
         // sparse levels: only targets of active links (cand) can gain a bit
         const u64 cw = cand ? cand[tile] : ~0ull;
@@ -428,12 +437,14 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
             if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
             if (fullnew_w) full[tile] = full_w | fullnew_w;
             n_new += __popcll(new_w);
+            n_full += __popcll(fullnew_w);
         }
     }
     if (sub != 0) {
         n_inc = 0;
         n_vis = 0;
     }
+    wave_add(ctr + cNewFull, n_full);
     wave_add(ctr + cIncLight, n_inc);
     wave_add(ctr + cVisLight, n_vis);
     wave_add(ctr + cNewLight, n_new);
@@ -499,7 +510,7 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_acc = 0, n_new = 0, n_newdeg = 0;
+    u64 n_acc = 0, n_new = 0, n_newdeg = 0, n_full = 0;
     for (int64_t h = grp; h < H; h += ngrp) {
         const int64_t t = heavy_atom[h];
         typename V::T acc = V::ld(hubacc + h * W + sub * WPL);
@@ -518,9 +529,11 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
             if (!ev) set_bit(ever, t);
             if (becomes_full) set_bit(full, t);
             ++n_new;
+            n_full += becomes_full;
             n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
         }
     }
+    wave_add(ctr + cNewFull, n_full);
     wave_add(ctr + cAccHub, n_acc);
     wave_add(ctr + cNewHub, n_new);
     wave_add(ctr + cNewAtoms, n_new);
@@ -632,7 +645,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_vis = 0, n_new = 0, n_newdeg = 0;
+    u64 n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
         const u64 full_w = full[tile];
         const u64 cw = cand[tile] & ~full_w;
@@ -670,8 +683,10 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
             if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
             if (fullnew_w) full[tile] = full_w | fullnew_w;
             n_new += __popcll(new_w);
+            n_full += __popcll(fullnew_w);
         }
     }
+    wave_add(ctr + cNewFull, n_full);
     if (sub != 0) n_vis = 0;
     wave_add(ctr + cVisLight, n_vis);
     wave_add(ctr + cNewLight, n_new);
@@ -975,6 +990,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         HGX_HIP(hipStreamSynchronize(s));
     }
     const u64 sparse_limit = (u64)std::max<int64_t>(M / 16, 1024);
+    // Full-visited skipping costs two bitmap probes per pin; it pays once a sizeable share of the
+    // atoms is visited by every traversal (seeds that are full count from the start).
+    u64 full_total = 0;
 
     for (int32_t d = 0; d < maxd && d < max_levels_cap - 1; ++d) {
         u64* lvl = bt.lvl[d];
@@ -999,11 +1017,13 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }
         u64* lc = sparse ? lcand : nullptr;
         u64* cd = sparse ? cand : nullptr;
+        int lflags = g->bfs_flags;
+        if ((lflags & 16) && (int64_t)full_total * 16 < A) lflags &= ~4;   // adaptive full skip
 
         Events e1 = tm.start(kKindGather, d);
         hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
                                                                       want_type, fa, full, lvl, lf, la, c, fm,
-                                                                      g->bfs_flags, lc, cd);
+                                                                      lflags, lc, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
         if (sparse && MODE == kSym) {
@@ -1022,14 +1042,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         Events e2 = tm.start(kKindPull, d);
         hgx_atom_pull<W, MODE><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, g->tgt_off,
                                                            g->tgt_idx, fa, lvl, vis, ever, full, lvl_next, fa_next, c,
-                                                           fm, g->bfs_flags, cd);
+                                                           fm, lflags, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
         if (g->n_chunks > 0) {
             Events e3 = tm.start(kKindHeavy, d);
             hgx_atom_pull_heavy<W, MODE><<<(unsigned)g->n_chunks, block, 0, s>>>(
                 g->chunks, g->inc_row, la, lf, g->tgt_off, g->tgt_idx, fa, lvl, vis, ever, full, hubacc, c, fm,
-                g->bfs_flags, cd);
+                lflags, cd);
             HGX_CHECK_LAUNCH();
             tm.stop(e3);
             Events e4 = tm.start(kKindHub, d);
@@ -1044,6 +1064,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
         level_ctr.back()[cDirRows] = sparse ? 1 : 0;   // (host-side) mode of this level
         push_volume = h_new[cNewDeg];
+        full_total += h_new[cNewFull];
         if (h_new[cNewAtoms] == 0) {
             g->release(lvl_next, row_bytes);
             g->release(fa_next, bm_bytes);
@@ -1216,22 +1237,29 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
             const bool sparse_level = c[cDirRows] != 0;
             const double scan_links = sparse_level ? (double)c[cActiveLinks] : (double)M;
             const double scan_pins = sparse_level ? (double)c[cActivePins] : (double)P;
-            r->stats.bytes_kernel[HGX_K_LINK_GATHER] +=
-                8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) + A / 4.0 +
-                rowb * c[cActivePins] + (mode == kSym ? rowb * c[cActiveLinks] : 0.0) + M / 8.0;
+            const double b_gather = 8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) +
+                                    A / 4.0 + rowb * c[cActivePins] +
+                                    (mode == kSym ? rowb * c[cActiveLinks] : 0.0) + M / 8.0;
             // hgx_atom_pull: inc_off + light inc_row + la bitmap + pulled rows + vis reads + lvl/vis writes
-            //                + ever/full/fa_next words
-            r->stats.bytes_kernel[HGX_K_ATOM_PULL] += (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) +
-                                                      M / 8.0 +
-                                                      rowb * c[cIncLight] + rowb * c[cVisLight] +
-                                                      2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
-            if (g->n_chunks > 0) {
-                r->stats.bytes_kernel[HGX_K_PULL_HEAVY] += 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] +
-                                                           rowb * g->n_chunks;
-                r->stats.bytes_kernel[HGX_K_HUB_FINALIZE] += 4.0 * g->n_heavy + 2.0 * rowb * g->n_heavy +
-                                                             rowb * c[cAccHub] + 2.0 * rowb * c[cNewHub];
+            //                + ever/full/fa_next words (sparse levels: candidate words + pushed rows)
+            const double b_pull = (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) + M / 8.0 +
+                                  rowb * c[cIncLight] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] +
+                                  3.0 * A / 8.0;
+            r->stats.bytes_kernel[HGX_K_LINK_GATHER] += b_gather;
+            r->stats.bytes_kernel[HGX_K_ATOM_PULL] += b_pull;
+            double b_heavy = 0, b_hub = 0;
+            if (g->n_chunks > 0 && !sparse_level) {
+                b_heavy = 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
+                b_hub = 4.0 * g->n_heavy + 2.0 * rowb * g->n_heavy + rowb * c[cAccHub] + 2.0 * rowb * c[cNewHub];
+                r->stats.bytes_kernel[HGX_K_PULL_HEAVY] += b_heavy;
+                r->stats.bytes_kernel[HGX_K_HUB_FINALIZE] += b_hub;
                 r->stats.launches[HGX_K_PULL_HEAVY] += 1;
                 r->stats.launches[HGX_K_HUB_FINALIZE] += 1;
+            }
+            if (d < 64) {
+                for (int k = 0; k < 8; ++k) r->stats.level_rows[d][k] += (int64_t)c[k];
+                r->stats.level_bytes[d] += b_gather + b_pull + b_heavy + b_hub;
+                r->stats.level_sparse[d] = sparse_level ? 1 : 0;
             }
             r->stats.launches[HGX_K_LINK_GATHER] += 1;
             r->stats.launches[HGX_K_ATOM_PULL] += 1;

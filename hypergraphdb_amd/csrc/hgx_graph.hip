@@ -28,7 +28,7 @@ void graph_release(hgx_graph* g) {
     for (auto& b : g->pool) (void)hipFree(b.p);
     g->pool.clear();
     (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
-    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
+    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -57,6 +57,13 @@ __global__ void __launch_bounds__(256) k_pin_keys(int64_t M, const int64_t* __re
         }
     }
     if (dups) atomicAdd(n_dup, dups);
+}
+
+// inc_type[i] = link_type[inc_row[i]]
+__global__ void __launch_bounds__(256) k_inc_type(int64_t I, const int32_t* __restrict__ inc_row,
+                                                  const int32_t* __restrict__ link_type, int32_t* __restrict__ inc_type) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x)
+        inc_type[i] = link_type[inc_row[i]];
 }
 
 // inc_row[i] = low word of key i.
@@ -299,6 +306,11 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
         HGX_HIP(hipMemsetAsync(g->inc_off, 0, sizeof(int64_t) * (A + 1), s));
     }
     g->I = I;
+    HGX_HIP(hipMalloc(&g->inc_type, sizeof(int32_t) * std::max<int64_t>(I, 1)));
+    if (I > 0) {
+        k_inc_type<<<grid_for(I, 256), 256, 0, s>>>(I, g->inc_row, g->link_type, g->inc_type);
+        HGX_CHECK_LAUNCH();
+    }
 
     // heavy atoms + chunk table (load balance for power-law incidence rows)
     {

@@ -7,6 +7,7 @@
 //   link_type [M]   int32   type key of link row r
 //   inc_off   [A+1] int64   incidence row offsets
 //   inc_row   [I]   int32   incident LINK ROWS, ascending (row order == atom rank order)
+//   inc_type  [I]   int32   type key of inc_row[i] (denormalised for the pattern filter)
 // plus the heavy-atom chunk table used to balance power-law incidence rows.
 #pragma once
 
@@ -83,7 +84,7 @@ struct hgx_graph {
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
-    int32_t bfs_flags = 0xE;        // HGX_OPT_BFS_FLAGS (see hgx.h)
+    int32_t bfs_flags = 0x1E;       // HGX_OPT_BFS_FLAGS (see hgx.h)
 
     int64_t A = 0, M = 0, P = 0, I = 0;
     int32_t* link_atom = nullptr;
@@ -92,6 +93,7 @@ struct hgx_graph {
     int32_t* link_type = nullptr;
     int64_t* inc_off = nullptr;
     int32_t* inc_row = nullptr;
+    int32_t* inc_type = nullptr;    // [I] link_type[inc_row[i]]: streamed type filter of the query path
 
     int64_t n_heavy = 0;            // heavy atoms (deg > kHeavyDegree)
     int64_t I_heavy = 0;            // incidence entries of heavy atoms

@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const QPlan* __restrict__ plan, const int32_t* __restrict__ q_type, const int64_t* __restrict__ a_off,
     const int32_t* __restrict__ anchors, const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern,
     const int32_t* __restrict__ q_has_ordered, const int32_t* __restrict__ inc_row,
-    const int32_t* __restrict__ link_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+    const int32_t* __restrict__ inc_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
     int32_t* __restrict__ slots, int64_t* __restrict__ counts, u64* __restrict__ ctr) {
     const int lane = threadIdx.x & 63;
     const int64_t chunk = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -97,8 +97,9 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
         int32_t L = -1;
         if (ci < pl.n) {
             ++n_cand;
-            L = inc_row[pl.beg + ci];
-            if (T < 0 || link_type[L] == T) {
+            // streamed type filter (inc_type is link_type of the incidence entry), then the row
+            if (T < 0 || inc_type[pl.beg + ci] == T) {
+                L = inc_row[pl.beg + ci];
                 ++n_typed;
                 const int64_t b = tgt_off[L], e = tgt_off[L + 1];
                 n_ar += (u64)(e - b);
@@ -164,48 +165,118 @@ struct hgx_query_result {
     double ms_total = 0, ms_match = 0, bytes_match = 0;
 };
 
-extern "C" {
+namespace {
 
-int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t n, hgx_query_result** out) {
+// Normalised batch: ExpressionBasedQuery.expand (orderedLink adds incident(x) for each non-ANY x,
+// :730-737) + the toDNF HashSet dedupe (:100) -> per query: type, distinct anchors, pattern, nop.
+struct NormBatch {
+    std::vector<int32_t> q_type, q_nop, q_ord;
+    std::vector<int64_t> a_off, p_off;
+    std::vector<int32_t> anchors, pattern;
+};
+
+template <class Get>
+void normalise(hgx_graph* g, int32_t n, Get get, NormBatch& nb) {
+    nb.q_type.resize(n);
+    nb.q_nop.resize(n);
+    nb.q_ord.resize(n);
+    nb.a_off.assign(n + 1, 0);
+    nb.p_off.assign(n + 1, 0);
+    for (int32_t q = 0; q < n; ++q) {
+        int32_t type, n_inc, has_ord, n_pat;
+        const int32_t *inc, *pat;
+        get(q, type, n_inc, inc, has_ord, n_pat, pat);
+        if (n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
+            fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(q));
+        if (type < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type in query " + std::to_string(q));
+        nb.q_type[q] = type;
+        nb.q_ord[q] = has_ord ? 1 : 0;
+        const int32_t m = has_ord ? n_pat : 0;
+        if (m > kMaxPattern) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: ordered pattern too long");
+        const size_t a0 = nb.anchors.size();
+        auto add = [&](int32_t h) {
+            if (h < 0 || h >= g->A)
+                fail(HGX_E_INVALID, "hgx_pattern_batch: atom id out of range in query " + std::to_string(q));
+            for (size_t k = a0; k < nb.anchors.size(); ++k)
+                if (nb.anchors[k] == h) return;
+            nb.anchors.push_back(h);
+        };
+        for (int32_t i = 0; i < n_inc; ++i) add(inc[i]);
+        for (int32_t i = 0; i < m; ++i) {
+            if (pat[i] == HGX_ANY_HANDLE) continue;
+            if (pat[i] < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern id");
+            add(pat[i]);
+        }
+        if (nb.anchors.size() == a0)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(q) + " has no incidence anchor");
+        if ((int64_t)(nb.anchors.size() - a0) > kMaxAnchors)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: too many anchors");
+        // an empty OrderedLinkCondition gets QueryMetaData.EMPTY, lands in ORA and compiles to HGQuery.NOP
+        nb.q_nop[q] = (has_ord && m == 0) ? 1 : 0;
+        for (int32_t i = 0; i < m; ++i) nb.pattern.push_back(pat[i]);
+        nb.a_off[q + 1] = (int64_t)nb.anchors.size();
+        nb.p_off[q + 1] = (int64_t)nb.pattern.size();
+    }
+}
+
+int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out);
+
+}  // namespace
+
+extern "C" int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t n, hgx_query_result** out) {
     HGX_API_BEGIN
     if (!g || !out || n < 0 || (n > 0 && !qs)) fail(HGX_E_INVALID, "hgx_pattern_batch: bad argument");
     *out = nullptr;
-    // host-side normalisation (ExpressionBasedQuery.expand + toDNF dedupe)
-    std::vector<int32_t> q_type(n), q_nop(n), q_ord(n);
-    std::vector<int64_t> a_off(n + 1, 0), p_off(n + 1, 0);
-    std::vector<int32_t> anchors, pattern;
-    for (int32_t q = 0; q < n; ++q) {
-        const hgx_and_query& Q = qs[q];
-        if (Q.n_incident < 0 || Q.n_pattern < 0 || (Q.n_incident > 0 && !Q.incident) ||
-            (Q.n_pattern > 0 && !Q.pattern))
-            fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(q));
-        if (Q.type < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type in query " + std::to_string(q));
-        q_type[q] = Q.type;
-        q_ord[q] = Q.has_ordered ? 1 : 0;
-        const int32_t m = Q.has_ordered ? Q.n_pattern : 0;
-        if (m > kMaxPattern) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: ordered pattern too long");
-        size_t a0 = anchors.size();
-        auto add = [&](int32_t h) {
-            if (h < 0 || h >= g->A) fail(HGX_E_INVALID, "hgx_pattern_batch: atom id out of range in query " + std::to_string(q));
-            for (size_t k = a0; k < anchors.size(); ++k)
-                if (anchors[k] == h) return;
-            anchors.push_back(h);
-        };
-        for (int32_t i = 0; i < Q.n_incident; ++i) add(Q.incident[i]);
-        for (int32_t i = 0; i < m; ++i) {
-            if (Q.pattern[i] == HGX_ANY_HANDLE) continue;
-            if (Q.pattern[i] < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern id");
-            add(Q.pattern[i]);
-        }
-        if (anchors.size() == a0)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(q) + " has no incidence anchor");
-        if ((int64_t)(anchors.size() - a0) > kMaxAnchors) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: too many anchors");
-        // an empty OrderedLinkCondition gets QueryMetaData.EMPTY, lands in ORA and compiles to HGQuery.NOP
-        q_nop[q] = (Q.has_ordered && m == 0) ? 1 : 0;
-        for (int32_t i = 0; i < m; ++i) pattern.push_back(Q.pattern[i]);
-        a_off[q + 1] = (int64_t)anchors.size();
-        p_off[q + 1] = (int64_t)pattern.size();
-    }
+    NormBatch nb;
+    normalise(g, n,
+              [&](int32_t q, int32_t& t, int32_t& ni, const int32_t*& inc, int32_t& ho, int32_t& np,
+                  const int32_t*& pat) {
+                  t = qs[q].type;
+                  ni = qs[q].n_incident;
+                  inc = qs[q].incident;
+                  ho = qs[q].has_ordered;
+                  np = qs[q].n_pattern;
+                  pat = qs[q].pattern;
+              },
+              nb);
+    return run_batch(g, n, nb, out);
+    HGX_API_END
+}
+
+extern "C" int hgx_pattern_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off,
+                                        const int32_t* inc, const int32_t* has_ordered, const int64_t* pat_off,
+                                        const int32_t* pat, hgx_query_result** out) {
+    HGX_API_BEGIN
+    if (!g || !out || n < 0 || (n > 0 && (!type || !inc_off || !pat_off || !has_ordered)))
+        fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad argument");
+    *out = nullptr;
+    NormBatch nb;
+    normalise(g, n,
+              [&](int32_t q, int32_t& t, int32_t& ni, const int32_t*& ii, int32_t& ho, int32_t& np,
+                  const int32_t*& pp) {
+                  t = type[q];
+                  ni = (int32_t)(inc_off[q + 1] - inc_off[q]);
+                  ii = inc ? inc + inc_off[q] : nullptr;
+                  ho = has_ordered[q];
+                  np = (int32_t)(pat_off[q + 1] - pat_off[q]);
+                  pp = pat ? pat + pat_off[q] : nullptr;
+              },
+              nb);
+    return run_batch(g, n, nb, out);
+    HGX_API_END
+}
+
+namespace {
+
+int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
+    HGX_API_BEGIN
+    std::vector<int32_t>& q_type = nb.q_type;
+    std::vector<int32_t>& q_nop = nb.q_nop;
+    std::vector<int32_t>& q_ord = nb.q_ord;
+    std::vector<int64_t>& a_off = nb.a_off;
+    std::vector<int64_t>& p_off = nb.p_off;
+    std::vector<int32_t>& anchors = nb.anchors;
+    std::vector<int32_t>& pattern = nb.pattern;
     hgx_query_result* r = new hgx_query_result();
     struct Guard {
         hgx_query_result* r;
@@ -288,7 +359,7 @@ int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t n, hgx_quer
     if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
     if (n_chunks > 0) {
         hgx_pattern_match<<<(unsigned)ceil_div((int64_t)n_chunks * 64, 256), 256, 0, s>>>(
-            n_chunks, d_chq, d_choff, d_plan, d_type, d_aoff, d_anch, d_poff, d_pat, d_ord, g->inc_row, g->link_type,
+            n_chunks, d_chq, d_choff, d_plan, d_type, d_aoff, d_anch, d_poff, d_pat, d_ord, g->inc_row, g->inc_type,
             g->tgt_off, g->tgt_idx, d_slots, d_cnt, d_ctr);
         HGX_CHECK_LAUNCH();
     }
@@ -325,17 +396,21 @@ int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t n, hgx_quer
         r->ms_total = a;
         r->ms_match = b;
     }
-    // algorithmic bytes of hgx_pattern_match: plan + per candidate inc_row + link_type,
-    // per type-passing candidate its tgt_off pair and target row, 4 B per hit, 4 B per chunk count
+    // algorithmic bytes of hgx_pattern_match: per candidate inc_type (+ inc_row when the type
+    // passes), per type-passing candidate its tgt_off pair and target row, 4 B per hit, 8 B per chunk
     {
         double anchors_bytes = 4.0 * anchors.size() + 16.0 * anchors.size() + 4.0 * pattern.size();
-        r->bytes_match = 8.0 * (double)hctr[qCand] + 16.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
-                         4.0 * (double)hctr[qHits] + 4.0 * (double)n_chunks + anchors_bytes;
+        r->bytes_match = 4.0 * (double)hctr[qCand] + 20.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
+                         4.0 * (double)hctr[qHits] + 8.0 * (double)n_chunks + anchors_bytes;
     }
     guard.r = nullptr;
     *out = r;
     HGX_API_END
 }
+
+}  // namespace
+
+extern "C" {
 
 int hgx_query_result_offsets(const hgx_query_result* r, int64_t* offsets) {
     HGX_API_BEGIN

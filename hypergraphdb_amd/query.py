@@ -179,25 +179,15 @@ class QueryResult:
         return self.ids[self.offsets[q]:self.offsets[q + 1]]
 
 
-def pattern_batch(snapshot, queries) -> QueryResult:
-    """Evaluate many And{type?, incident*, orderedLink?} queries in one GPU launch sequence.
-    ``queries``: conditions or (type, incident, pattern) tuples."""
-    norm = [q if isinstance(q, tuple) else normalize(q) for q in queries]
-    n = len(norm)
-    keep = []
-    arr = (_lib.AndQuery * max(n, 1))()
-    empty = np.zeros(n, bool)
-    for i, (t, inc, pat) in enumerate(norm):
-        if t == "empty":
-            empty[i] = True
-            t, inc, pat = _lib.HGX_NO_TYPE, [], []
-            inc = [0]
-        ia = np.ascontiguousarray(list(inc) or [0], np.int32)
-        pa = np.ascontiguousarray(list(pat) if pat else [0], np.int32)
-        keep += [ia, pa]
-        arr[i] = _lib.AndQuery(int(t), len(inc), ptr(ia), int(pat is not None), len(pat or ()), ptr(pa))
+def pattern_batch_arrays(snapshot, q_type, inc_off, inc, has_ordered, pat_off, pat) -> QueryResult:
+    """Packed batch (hgx_pattern_batch_packed): query q = And(type(q_type[q]),
+    incident(inc[inc_off[q]:inc_off[q+1]]...), orderedLink(pat[pat_off[q]:pat_off[q+1]]) if has_ordered[q])."""
+    n = len(q_type)
+    arrs = [np.ascontiguousarray(q_type, np.int32), np.ascontiguousarray(inc_off, np.int64),
+            np.ascontiguousarray(inc, np.int32), np.ascontiguousarray(has_ordered, np.int32),
+            np.ascontiguousarray(pat_off, np.int64), np.ascontiguousarray(pat, np.int32)]
     h = C.c_void_p()
-    check(lib().hgx_pattern_batch(snapshot.handle, arr, n, C.byref(h)))
+    check(lib().hgx_pattern_batch_packed(snapshot.handle, n, *(a.ctypes.data for a in arrs), C.byref(h)))
     try:
         off = np.zeros(n + 1, np.int64)
         check(lib().hgx_query_result_offsets(h, ptr(off)))
@@ -207,12 +197,38 @@ def pattern_batch(snapshot, queries) -> QueryResult:
         check(lib().hgx_query_result_ms(h, C.byref(a), C.byref(b), C.byref(c)))
     finally:
         lib().hgx_query_result_free(h)
-    ids = ids[: int(off[-1])]
-    if empty.any():   # drop the placeholder queries' results
-        parts = [np.empty(0, np.int32) if empty[i] else ids[off[i]:off[i + 1]] for i in range(n)]
+    return QueryResult(off, ids[: int(off[-1])], {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+
+
+def pattern_batch(snapshot, queries) -> QueryResult:
+    """Evaluate many And{type?, incident*, orderedLink?} queries in one GPU launch sequence.
+    ``queries``: conditions or (type, incident, pattern) tuples (pattern None = no orderedLink)."""
+    norm = [q if isinstance(q, tuple) else normalize(q) for q in queries]
+    n = len(norm)
+    q_type = np.empty(n, np.int32)
+    has = np.zeros(n, np.int32)
+    inc_off = np.zeros(n + 1, np.int64)
+    pat_off = np.zeros(n + 1, np.int64)
+    inc, pat = [], []
+    empty = np.zeros(n, bool)
+    for i, (t, ic, pt) in enumerate(norm):
+        if t == "empty":                 # two different exact types: nothing satisfies both
+            empty[i] = True
+            t, ic, pt = _lib.HGX_NO_TYPE, [0], ()    # an empty orderedLink compiles to NOP
+        q_type[i] = t
+        inc.extend(ic)
+        inc_off[i + 1] = len(inc)
+        if pt is not None:
+            has[i] = 1
+            pat.extend(pt)
+        pat_off[i + 1] = len(pat)
+    r = pattern_batch_arrays(snapshot, q_type, inc_off, np.array(inc or [0], np.int32), has, pat_off,
+                             np.array(pat or [0], np.int32))
+    if empty.any():
+        parts = [np.empty(0, np.int32) if empty[i] else r[i] for i in range(n)]
         off = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64)
-        ids = np.concatenate(parts).astype(np.int32) if parts else ids
-    return QueryResult(off, ids, {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+        return QueryResult(off, np.concatenate(parts).astype(np.int32), r.ms)
+    return r
 
 
 class QueryMetaData:

@@ -109,6 +109,12 @@ typedef struct hgx_bfs_stats {
     int64_t union_frontier[64];        /* |U_d| per expanded level (summed over batches)       */
     double  level_ms[64];              /* device ms of all kernels of level d (timing enabled) */
     int64_t level_new[64];             /* atoms with a new bit at level d+1 (summed over batches) */
+    double  level_bytes[64];           /* algorithmic bytes of all kernels of level d          */
+    int32_t level_sparse[64];          /* 1 if level d ran frontier-driven (push)              */
+    /* per level, summed over batches: [0] lf rows written, [1] frontier rows gathered,
+     * [2] lf rows pulled (light), [3] vis rows read, [4] new light atoms, [5] lf rows pulled
+     * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
+    int64_t level_rows[64][8];
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
@@ -128,8 +134,9 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
 /* Engine options (tuning / A-B experiments; defaults are the tuned values):
  *   HGX_OPT_BFS_FLAGS: bit 0 = gather early exit, bit 1 = pull early exit,
  *                      bit 2 = skip atoms / links already visited by every traversal,
- *                      bit 3 = frontier-driven sparse levels (direction optimisation).
- *                      Default 0xE. */
+ *                      bit 3 = frontier-driven sparse levels (direction optimisation),
+ *                      bit 4 = apply bit 2 only once >= 1/16 of the atoms are fully visited.
+ *                      Default 0x1E. */
 #define HGX_OPT_BFS_FLAGS 1
 int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
 
@@ -161,6 +168,12 @@ void hgx_bfs_result_free(hgx_bfs_result *r);
  * AndToQuery, which scans the type index). */
 int  hgx_pattern_batch(hgx_graph *g, const hgx_and_query *queries, int32_t n,
                        hgx_query_result **out);
+/* The same batch as flat arrays (one call per batch from JNI / FFM): query q has type[q],
+ * incident anchors inc[inc_off[q] .. inc_off[q+1]), has_ordered[q], and ordered pattern
+ * pat[pat_off[q] .. pat_off[q+1]). */
+int  hgx_pattern_batch_packed(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off,
+                              const int32_t *inc, const int32_t *has_ordered, const int64_t *pat_off,
+                              const int32_t *pat, hgx_query_result **out);
 /* offsets[n+1]: results of query q are ids[offsets[q] .. offsets[q+1]). */
 int  hgx_query_result_offsets(const hgx_query_result *r, int64_t *offsets);
 int  hgx_query_result_ids(const hgx_query_result *r, int32_t *ids);

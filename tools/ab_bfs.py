@@ -49,11 +49,14 @@ def main():
         tot = sorted(s["ms_total"] for s in runs)
         k = {name: sorted(s["kernels"][name]["ms"] for s in runs)[len(runs) // 2] for name in runs[0]["kernels"]}
         lv = [round(sorted(s["level_ms"][d] for s in runs)[len(runs) // 2], 3) for d in range(len(runs[0]["level_ms"]))]
+        lgbs = [round(runs[0]["level_bytes"][d] / (lv[d] / 1e3) / 1e9, 0) if lv[d] > 0 else None for d in range(len(lv))]
         gbs = {name: round(runs[0]["kernels"][name]["bytes"] / (k[name] / 1e3) / 1e9, 1) if k[name] > 0 else None
                for name in k}
         table[f] = {"ms_total_median": round(tot[len(tot) // 2], 3), "ms_total_min": round(tot[0], 3),
-                    "kernel_ms": {n: round(v, 3) for n, v in k.items()}, "kernel_GBps": gbs, "level_ms": lv}
-        print(f"flags={f:#x} total {tot[len(tot) // 2]:.2f} ms (min {tot[0]:.2f})  levels {lv}  kernels "
+                    "kernel_ms": {n: round(v, 3) for n, v in k.items()}, "kernel_GBps": gbs, "level_ms": lv,
+                    "level_GBps": lgbs, "level_sparse": runs[0]["level_sparse"],
+                    "level_bytes": runs[0]["level_bytes"], "level_rows": runs[0]["level_rows"]}
+        print(f"flags={f:#x} total {tot[len(tot) // 2]:.2f} ms (min {tot[0]:.2f})  levels {lv} GB/s {lgbs}  kernels "
               f"{ {n: round(v, 2) for n, v in k.items()} }", flush=True)
     print(json.dumps({"level_new": ref_new, "variants": table}))
 
