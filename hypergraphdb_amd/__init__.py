@@ -8,6 +8,7 @@ This package is the host-side mirror of the reference interfaces on that path:
 """
 from ._lib import HGXError, HGXUnsupported, lib  # noqa: F401
 from .algorithms import (AtomTypeCondition, BfsResult, DefaultALGenerator, HGBreadthFirstTraversal,  # noqa: F401
+                         SequenceResult, bfs_sequence,
                          HGException, bfs_batch)
 from .query import GpuAndToQuery, HGQueryConfiguration, find_all, hg, pattern_batch  # noqa: F401
 from .snapshot import HyperGraphSnapshot, rank_handles  # noqa: F401

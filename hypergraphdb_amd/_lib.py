@@ -24,13 +24,15 @@ HGX_ANY_HANDLE = -1
 HGX_NO_TYPE = -1
 HGX_UNBOUNDED = -1
 HGX_OPT_BFS_FLAGS = 1
+HGX_OPT_SEQ_BUDGET = 2
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
     "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
-    "hgx_bfs_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_query_result_offsets", "hgx_query_result_ids",
+    "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
+    "hgx_seq_result_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
 )
 
@@ -118,6 +120,12 @@ def lib():
         "hgx_bfs_result_depth_of": ([vp, i32, i32, C.POINTER(i32)], C.c_int),
         "hgx_bfs_result_stats": ([vp, i32, C.POINTER(BfsStats)], C.c_int),
         "hgx_bfs_result_free": ([vp], None),
+        "hgx_bfs_sequence": ([vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
+        "hgx_seq_result_info": ([vp, C.POINTER(i32), C.POINTER(i64), C.POINTER(i32)], C.c_int),
+        "hgx_seq_result_offsets": ([vp, vp], C.c_int),
+        "hgx_seq_result_pairs": ([vp, vp, vp, vp], C.c_int),
+        "hgx_seq_result_stats": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
+        "hgx_seq_result_free": ([vp], None),
         "hgx_pattern_batch": ([vp, C.POINTER(AndQuery), i32, C.POINTER(vp)], C.c_int),
         "hgx_pattern_batch_packed": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),
         "hgx_query_result_offsets": ([vp, vp], C.c_int),

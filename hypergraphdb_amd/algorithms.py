@@ -139,27 +139,53 @@ def bfs_batch(snapshot, seeds, max_depth=None, generator: DefaultALGenerator | N
     return BfsResult(snapshot, h, s)
 
 
-def _reachable(mode, tg, v, t):
-    idx_v = [i for i, x in enumerate(tg) if x == v]
-    idx_t = [i for i, x in enumerate(tg) if x == t]
-    fv, lv, ft, lt = idx_v[0], idx_v[-1], idx_t[0], idx_t[-1]
-    return {0: True, 1: lt > fv, 2: ft < fv, 3: ft < lv, 4: lt > lv}[mode]
+class SequenceResult:
+    """Order-exact traversal result: per seed, the (link, atom) pairs next() returns, in order,
+    with each atom's distance (host arrays)."""
+
+    def __init__(self, handle, seeds):
+        self.seeds = np.asarray(seeds, np.int32)
+        try:
+            ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
+            check(lib().hgx_seq_result_info(handle, C.byref(ns), C.byref(npairs), C.byref(nl)))
+            self.n_seeds, self.n_levels = ns.value, nl.value
+            self.offsets = np.zeros(self.n_seeds + 1, np.int64)
+            check(lib().hgx_seq_result_offsets(handle, ptr(self.offsets)))
+            n = npairs.value
+            self.links = np.empty(max(n, 1), np.int32)
+            self.atoms = np.empty(max(n, 1), np.int32)
+            self.dists = np.empty(max(n, 1), np.int32)
+            check(lib().hgx_seq_result_pairs(handle, ptr(self.links), ptr(self.atoms), ptr(self.dists)))
+            self.links, self.atoms, self.dists = self.links[:n], self.atoms[:n], self.dists[:n]
+            ms, tr = C.c_double(), C.c_double()
+            check(lib().hgx_seq_result_stats(handle, C.byref(ms), C.byref(tr)))
+            self.ms_total, self.traversed_edges = ms.value, tr.value
+        finally:
+            lib().hgx_seq_result_free(handle)
+
+    def pairs(self, seed_index: int):
+        """(links, atoms, dists) of seed ``seed_index`` in next() order."""
+        a, b = self.offsets[seed_index], self.offsets[seed_index + 1]
+        return self.links[a:b], self.atoms[a:b], self.dists[a:b]
 
 
-def _mode(gen):
-    P, S, R, RS = gen.return_preceding, gen.return_succeeding, gen.reverse_order, gen.return_source
-    if not R:
-        return 1 if not P else (2 if (not S and not RS) else 0)
-    return 3 if not P else (4 if (not S and not RS) else 0)
+def bfs_sequence(snapshot, seeds, max_depth=None, generator: DefaultALGenerator | None = None) -> SequenceResult:
+    """The exact next() sequence of HGBreadthFirstTraversal(seeds[i], generator, max_depth) for
+    every i (FIFO order and discovering links as in the reference), computed on the GPU."""
+    gen = generator or DefaultALGenerator(snapshot)
+    opts = gen.options()
+    s = np.ascontiguousarray(seeds, np.int32)
+    md = _lib.HGX_UNBOUNDED if max_depth is None or max_depth >= 2**31 - 1 else int(max_depth)
+    h = C.c_void_p()
+    check(lib().hgx_bfs_sequence(snapshot.handle, ptr(s), len(s), md, C.byref(opts), C.byref(h)))
+    return SequenceResult(h, s)
 
 
 class HGBreadthFirstTraversal:
-    """HGTraversal over the GPU result for one start atom.
-
-    next() returns (link, atom) pairs by increasing distance, like the reference; within one
-    distance the atoms come in ascending handle order (the reference's FIFO order within a
-    level is not reproduced -- SURVEY.md 8(f) rank 3), and ``link`` is the smallest incident
-    link through which the atom is reachable from the previous level."""
+    """HGTraversal (C/algorithms/HGTraversal.java:36-63) for one start atom, backed by the GPU
+    order-exact traversal: next() returns the same (link, atom) pairs in the same order as
+    HGBreadthFirstTraversal.next() (:143-156), None once exhausted; isVisited(h) is true for the
+    start atom and for every atom already returned (:137-141); remove() is unsupported (:98-101)."""
 
     def __init__(self, start, adj_list_generator: DefaultALGenerator, max_distance=None):
         self.start = int(start)
@@ -169,26 +195,25 @@ class HGBreadthFirstTraversal:
         self.reset()
 
     def reset(self):
-        self._res = bfs_batch(self.snapshot, [self.start], self.max_distance, self.gen)
-        self._levels = self._res.levels(0)
-        self._depth = {self.start: 0}
-        for d, lv in enumerate(self._levels):
-            for a in lv.tolist():
-                self._depth[a] = d
-        self._returned = set()
-        self._queue = [(d, a) for d in range(1, len(self._levels)) for a in self._levels[d].tolist()]
+        seq = bfs_sequence(self.snapshot, [self.start], self.max_distance, self.gen)
+        self._links, self._atoms, self._dists = (x.tolist() for x in seq.pairs(0))
+        self._returned = {self.start}
         self._pos = 0
 
     def hasNext(self):
-        return self._pos < len(self._queue)
+        return self._pos < len(self._atoms)
 
     def next(self):
         if not self.hasNext():
             return None
-        d, a = self._queue[self._pos]
+        i = self._pos
         self._pos += 1
-        self._returned.add(a)
-        return (self._link_for(a, d), a)
+        self._returned.add(self._atoms[i])
+        return (self._links[i], self._atoms[i])
+
+    def distance(self):
+        """distance of the atom returned by the last next() (the queue entry's Integer)"""
+        return self._dists[self._pos - 1] if self._pos else 0
 
     def isVisited(self, handle):
         return int(handle) in self._returned
@@ -199,15 +224,3 @@ class HGBreadthFirstTraversal:
     def __iter__(self):
         while self.hasNext():
             yield self.next()
-
-    def _link_for(self, a, d):
-        snap, mode = self.snapshot, _mode(self.gen)
-        lt = self.gen.link_predicate.type if isinstance(self.gen.link_predicate, AtomTypeCondition) else None
-        for L in snap.incidence(a).tolist():
-            if lt is not None and snap.type_of(L) != lt:
-                continue
-            tg = snap.targets(L).tolist()
-            for v in tg:
-                if v != a and self._depth.get(v) == d - 1 and _reachable(mode, tg, v, a):
-                    return L
-        raise HGXError(_lib.HGX_E_DEVICE, f"no discovering link for atom {a}")

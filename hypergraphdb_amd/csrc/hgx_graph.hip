@@ -384,7 +384,10 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     if (!g) fail(HGX_E_INVALID, "null graph");
     std::lock_guard<std::mutex> lk(g->mu);
     if (option == HGX_OPT_BFS_FLAGS) g->bfs_flags = (int32_t)value;
-    else fail(HGX_E_INVALID, "hgx_set_option: unknown option");
+    else if (option == HGX_OPT_SEQ_BUDGET) {
+        if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
+        g->seq_budget_bytes = value;
+    } else fail(HGX_E_INVALID, "hgx_set_option: unknown option");
     HGX_API_END
 }
 

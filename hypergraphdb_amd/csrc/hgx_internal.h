@@ -85,6 +85,8 @@ struct hgx_graph {
     std::atomic<int> refs{1};
     bool timing = false;
     int32_t bfs_flags = 0x1E;       // HGX_OPT_BFS_FLAGS (see hgx.h)
+    int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
+    int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
 
     int64_t A = 0, M = 0, P = 0, I = 0;
     int32_t* link_atom = nullptr;

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import HGXUnsupported, check, lib, ptr
-from .algorithms import AtomTypeCondition, DefaultALGenerator, HGException, bfs_batch
+from .algorithms import AtomTypeCondition, DefaultALGenerator, HGException, bfs_sequence
 
 ANY = _lib.HGX_ANY_HANDLE
 
@@ -271,13 +271,11 @@ class HGQueryConfiguration:
 def find_all(snapshot, cond, config: HGQueryConfiguration | None = None):
     """hg.findAll(graph, cond) for the accelerated shapes."""
     if isinstance(cond, BFSCondition):
-        lp = cond.link_predicate
-        gen = DefaultALGenerator(snapshot, lp, None, *cond.flags)
-        res = bfs_batch(snapshot, [cond.start], cond.max_distance, gen)
-        try:
-            return sorted(int(a) for d in range(1, res.n_levels) for a in res.visited(0, d))
-        finally:
-            res.close()
+        # TraversalBasedQuery(traversal, ReturnType.targets) (ToQueryMap.java:313-319): the atoms
+        # in HGBreadthFirstTraversal.next() order
+        gen = DefaultALGenerator(snapshot, cond.link_predicate, None, *cond.flags)
+        seq = bfs_sequence(snapshot, [cond.start], cond.max_distance, gen)
+        return seq.pairs(0)[1].tolist()
     if isinstance(cond, MapCondition):
         return sorted({v for v in (cond.mapping(x) for x in find_all(snapshot, cond.cond, config)) if v is not None})
     if isinstance(cond, And):

@@ -138,6 +138,9 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 4 = apply bit 2 only once >= 1/16 of the atoms are fully visited.
  *                      Default 0x1E. */
 #define HGX_OPT_BFS_FLAGS 1
+/* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
+ * (seeds are processed in chunks that fit; default 16 GiB). */
+#define HGX_OPT_SEQ_BUDGET 2
 int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
 
 /* Batched multi-source BFS.  Seed i is HGBreadthFirstTraversal(seeds[i], gen, max_depth)
@@ -161,6 +164,22 @@ int  hgx_bfs_result_depth_of(hgx_bfs_result *r, int32_t seed_index, int32_t atom
 int  hgx_bfs_result_stats(hgx_bfs_result *r, int32_t with_accounting, hgx_bfs_stats *stats);
 void hgx_bfs_result_free(hgx_bfs_result *r);
 
+/* Order-exact traversal: for every seed the exact sequence of (link, atom) pairs that
+ * HGBreadthFirstTraversal(seeds[i], gen, max_depth).next() returns, in the reference's FIFO order
+ * (C/algorithms/HGBreadthFirstTraversal.java:49-66,143-156), plus the distance of each atom.
+ * The link of a pair is the link through which the atom was first discovered. */
+typedef struct hgx_seq_result hgx_seq_result;
+int  hgx_bfs_sequence(hgx_graph *g, const int32_t *seeds, int32_t n_seeds, int32_t max_depth,
+                      const hgx_algen_opts *opts, hgx_seq_result **out);
+/* n_pairs = total pairs over all seeds; n_levels = 1 + the largest distance returned. */
+int  hgx_seq_result_info(const hgx_seq_result *r, int32_t *n_seeds, int64_t *n_pairs, int32_t *n_levels);
+/* offsets[n_seeds+1]: seed i's pairs are [offsets[i], offsets[i+1]) of the pair arrays. */
+int  hgx_seq_result_offsets(const hgx_seq_result *r, int64_t *offsets);
+/* links / atoms / dists: n_pairs entries each (any may be NULL). */
+int  hgx_seq_result_pairs(const hgx_seq_result *r, int32_t *links, int32_t *atoms, int32_t *dists);
+/* device ms (timing enabled) and sum over seeds and expanded atoms of |inc(atom)|. */
+int  hgx_seq_result_stats(const hgx_seq_result *r, double *ms_total, double *traversed_edges);
+void hgx_seq_result_free(hgx_seq_result *r);
 /* Batched conjunctive pattern queries.  Result of query q = the link atoms L with
  * type(L) == type, every incident/pattern anchor in targets(L) and
  * OrderedLinkCondition(pattern) true on targets(L), ascending.  A query with no
