@@ -141,6 +141,17 @@ __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
+// Level counters are kept in kCtrShards replicas on lines of their own (one device-scope atomic
+// word saturates at ~90 adds/us; thousands of waves add to every counter each level).  Counter c
+// of shard k lives at base[k * kCtrStride + c]; the host sums the shards.
+constexpr int kCtrShards = 16, kCtrStride = 16, kCtrBlock = kCtrShards * kCtrStride;
+static_assert(cNum <= kCtrStride, "counter block");
+__device__ __forceinline__ void wave_add_sh(u64* ctr, u64 v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kCtrShards - 1));
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr + shard * kCtrStride, v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Link gather: lf[L] = OR_{v in targets(L), fa_d(v)} lvl_d[v]; la(L) set iff the row was written.
 // A wave owns 64 consecutive link rows (one la word); a G-lane group handles one row at a time.
@@ -254,8 +265,8 @@ __global__ void __launch_bounds__(256) hgx_link_gather(int64_t M, const int64_t*
         }
         if (lane == 0) la[tile] = word;
     }
-    wave_add(ctr + cActiveLinks, n_links);
-    wave_add(ctr + cActivePins, n_pins);
+    wave_add_sh(ctr + cActiveLinks, n_links);
+    wave_add_sh(ctr + cActivePins, n_pins);
 }
 
 // Ordered modes: the frontier rows of the co-targets of t in one link row that may yield t.
@@ -444,12 +455,12 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
         n_inc = 0;
         n_vis = 0;
     }
-    wave_add(ctr + cNewFull, n_full);
-    wave_add(ctr + cIncLight, n_inc);
-    wave_add(ctr + cVisLight, n_vis);
-    wave_add(ctr + cNewLight, n_new);
-    wave_add(ctr + cNewAtoms, n_new);
-    wave_add(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cIncLight, n_inc);
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
 }
 
 // Heavy atoms: one workgroup per chunk of <= kChunkEntries incidence entries; groups OR their
@@ -494,7 +505,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull_heavy(const HeavyChunk* __r
         if (r) atomicOr(hubacc + (int64_t)c.slot * W + j, r);
     }
     if (sub != 0) n_inc = 0;
-    wave_add(ctr + cIncHeavy, n_inc);
+    wave_add_sh(ctr + cIncHeavy, n_inc);
 }
 
 template <int W>
@@ -533,11 +544,11 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
             n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
         }
     }
-    wave_add(ctr + cNewFull, n_full);
-    wave_add(ctr + cAccHub, n_acc);
-    wave_add(ctr + cNewHub, n_new);
-    wave_add(ctr + cNewAtoms, n_new);
-    wave_add(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cAccHub, n_acc);
+    wave_add_sh(ctr + cNewHub, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
 }
 
 // Sparse levels: mark every (typed) link incident to a frontier atom.  One wave per frontier word:
@@ -686,12 +697,12 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
             n_full += __popcll(fullnew_w);
         }
     }
-    wave_add(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cNewFull, n_full);
     if (sub != 0) n_vis = 0;
-    wave_add(ctr + cVisLight, n_vis);
-    wave_add(ctr + cNewLight, n_new);
-    wave_add(ctr + cNewAtoms, n_new);
-    wave_add(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
 }
 
 // sum of |inc(v)| over the seed atoms (level-0 push volume)
@@ -946,15 +957,16 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* full = (u64*)g->alloc(bm_bytes);
     u64* la = (u64*)g->alloc(la_bytes);
     const int max_levels_cap = 4096;
-    u64* ctr = (u64*)g->alloc(sizeof(u64) * cNum * max_levels_cap);
+    u64* ctr = (u64*)g->alloc(sizeof(u64) * kCtrBlock * max_levels_cap);
     int32_t* d_atoms = (int32_t*)g->alloc(sizeof(int32_t) * seed_atoms.size());
     u64* d_rows = (u64*)g->alloc(sizeof(u64) * seed_rows.size());
-    u64* h_new = (u64*)g->pinned_buf(sizeof(u64) * cNum);
+    u64* h_sh = (u64*)g->pinned_buf(sizeof(u64) * kCtrBlock);
+    u64 h_new[cNum];
 
     HGX_HIP(hipMemsetAsync(ever, 0, bm_bytes, s));
     HGX_HIP(hipMemsetAsync(full, 0, bm_bytes, s));
     HGX_HIP(hipMemsetAsync(hubacc, 0, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W, s));
-    HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * cNum * max_levels_cap, s));
+    HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kCtrBlock * max_levels_cap, s));
     HGX_HIP(hipMemcpyAsync(d_atoms, seed_atoms.data(), sizeof(int32_t) * seed_atoms.size(), hipMemcpyHostToDevice, s));
     HGX_HIP(hipMemcpyAsync(d_rows, seed_rows.data(), sizeof(u64) * seed_rows.size(), hipMemcpyHostToDevice, s));
 
@@ -982,7 +994,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
     u64 push_volume = 0;
     if (sparse_ok) {
-        u64* dv = ctr + (size_t)(max_levels_cap - 1) * cNum;   // scratch slot
+        u64* dv = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock;   // scratch slot
         hgx_seed_degree<<<grid_for((int64_t)seed_atoms.size(), 256, 1 << 20), 256, 0, s>>>(
             (int32_t)seed_atoms.size(), d_atoms, g->inc_off, dv);
         HGX_CHECK_LAUNCH();
@@ -999,7 +1011,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64* fa = bt.fa[d];
         u64* lvl_next = (u64*)g->alloc(row_bytes);
         u64* fa_next = (u64*)g->alloc(bm_bytes);   // every word written by hgx_atom_pull
-        u64* c = ctr + (size_t)d * cNum;
+        u64* c = ctr + (size_t)d * kCtrBlock;
         const bool sparse = sparse_ok && push_volume < sparse_limit;
         if (sparse) {
             Events e0 = tm.start(kKindGather, d);
@@ -1059,8 +1071,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             tm.stop(e4);
         }
         }
-        HGX_HIP(hipMemcpyAsync(h_new, c, sizeof(u64) * cNum, hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipMemcpyAsync(h_sh, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
+        for (int k = 0; k < cNum; ++k) {
+            h_new[k] = 0;
+            for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += h_sh[sh * kCtrStride + k];
+        }
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
         level_ctr.back()[cDirRows] = sparse ? 1 : 0;   // (host-side) mode of this level
         push_volume = h_new[cNewDeg];
@@ -1081,7 +1097,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     g->release(la, la_bytes);
     if (lcand) g->release(lcand, la_bytes);
     if (cand) g->release(cand, bm_bytes);
-    g->release(ctr, sizeof(u64) * cNum * max_levels_cap);
+    g->release(ctr, sizeof(u64) * kCtrBlock * max_levels_cap);
     g->release(d_atoms, sizeof(int32_t) * seed_atoms.size());
     g->release(d_rows, sizeof(u64) * seed_rows.size());
 }

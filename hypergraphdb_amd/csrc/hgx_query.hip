@@ -71,7 +71,10 @@ __global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off
     for (int32_t c = chunk_off[q]; c < chunk_off[q + 1]; ++c) chunk_q[c] = q;
 }
 
-// One wave per chunk of kQChunk candidates of one query.
+// A wave per chunk of kQChunk candidates of one query (grid-stride over chunks; the counters are
+// summed in registers and added once per wave into sharded replicas).
+constexpr int kQShards = 16, kQStride = 16;
+
 __global__ void __launch_bounds__(256) hgx_pattern_match(
     int32_t n_chunks, const int32_t* __restrict__ chunk_q, const int32_t* __restrict__ chunk_off,
     const QPlan* __restrict__ plan, const int32_t* __restrict__ q_type, const int64_t* __restrict__ a_off,
@@ -80,59 +83,63 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const int32_t* __restrict__ inc_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
     int32_t* __restrict__ slots, int64_t* __restrict__ counts, u64* __restrict__ ctr) {
     const int lane = threadIdx.x & 63;
-    const int64_t chunk = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    if (chunk >= n_chunks) return;   // whole wave exits together
-    const int32_t q = chunk_q[chunk];
-    const QPlan pl = plan[q];
-    const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
-    const int32_t T = q_type[q];
-    const int64_t ab = a_off[q], na = a_off[q + 1] - ab;
-    const int64_t pb = p_off[q], np = p_off[q + 1] - pb;
-    const bool ordered = q_has_ordered[q] != 0;
-    int32_t written = 0;
-    u64 n_cand = 0, n_typed = 0, n_ar = 0;
-    for (int k = 0; k < kQChunk / 64; ++k) {
-        const int64_t ci = c0 + k * 64 + lane;
-        bool hit = false;
-        int32_t L = -1;
-        if (ci < pl.n) {
-            ++n_cand;
-            // streamed type filter (inc_type is link_type of the incidence entry), then the row
-            if (T < 0 || inc_type[pl.beg + ci] == T) {
-                L = inc_row[pl.beg + ci];
-                ++n_typed;
-                const int64_t b = tgt_off[L], e = tgt_off[L + 1];
-                n_ar += (u64)(e - b);
-                hit = true;
-                // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
-                for (int64_t j = 0; j < na && hit; ++j) {
-                    if (j == pl.amin) continue;
-                    const int32_t a = anchors[ab + j];
-                    bool found = false;
-                    for (int64_t i = b; i < e; ++i) found |= (tgt_idx[i] == a);
-                    hit = found;
-                }
-                // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
-                if (hit && ordered) {
-                    int64_t i = b, j = 0;
-                    while (i < e && j < np) {
-                        const int32_t pj = pattern[pb + j];
-                        if (pj < 0 || pj == tgt_idx[i]) ++j;
-                        ++i;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    u64 n_cand = 0, n_typed = 0, n_ar = 0, n_hits = 0;
+    for (int64_t chunk = wave; chunk < n_chunks; chunk += nwave) {
+        const int32_t q = chunk_q[chunk];
+        const QPlan pl = plan[q];
+        const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
+        const int32_t T = q_type[q];
+        const int64_t ab = a_off[q], na = a_off[q + 1] - ab;
+        const int64_t pb = p_off[q], np = p_off[q + 1] - pb;
+        const bool ordered = q_has_ordered[q] != 0;
+        int32_t written = 0;
+        for (int k = 0; k < kQChunk / 64; ++k) {
+            const int64_t ci = c0 + k * 64 + lane;
+            bool hit = false;
+            int32_t L = -1;
+            if (ci < pl.n) {
+                ++n_cand;
+                // streamed type filter (inc_type is link_type of the incidence entry), then the row
+                if (T < 0 || inc_type[pl.beg + ci] == T) {
+                    L = inc_row[pl.beg + ci];
+                    ++n_typed;
+                    const int64_t b = tgt_off[L], e = tgt_off[L + 1];
+                    n_ar += (u64)(e - b);
+                    hit = true;
+                    // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
+                    for (int64_t j = 0; j < na && hit; ++j) {
+                        if (j == pl.amin) continue;
+                        const int32_t a = anchors[ab + j];
+                        bool found = false;
+                        for (int64_t i = b; i < e; ++i) found |= (tgt_idx[i] == a);
+                        hit = found;
                     }
-                    hit = (j == np);
+                    // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
+                    if (hit && ordered) {
+                        int64_t i = b, j = 0;
+                        while (i < e && j < np) {
+                            const int32_t pj = pattern[pb + j];
+                            if (pj < 0 || pj == tgt_idx[i]) ++j;
+                            ++i;
+                        }
+                        hit = (j == np);
+                    }
                 }
             }
+            const u64 m = __ballot(hit);
+            if (hit) slots[chunk * kQChunk + written + __popcll(m & ((1ull << lane) - 1ull))] = L;
+            written += __popcll(m);
         }
-        const u64 m = __ballot(hit);
-        if (hit) slots[chunk * kQChunk + written + __popcll(m & ((1ull << lane) - 1ull))] = L;
-        written += __popcll(m);
+        if (lane == 0) counts[chunk] = written;
+        n_hits += (u64)written;
     }
-    if (lane == 0) counts[chunk] = written;
-    wave_add_q(ctr + qCand, n_cand);
-    wave_add_q(ctr + qTyped, n_typed);
-    wave_add_q(ctr + qArity, n_ar);
-    if (lane == 0) atomicAdd(ctr + qHits, (u64)written);
+    u64* c = ctr + (wave & (kQShards - 1)) * kQStride;
+    wave_add_q(c + qCand, n_cand);
+    wave_add_q(c + qTyped, n_typed);
+    wave_add_q(c + qArity, n_ar);
+    if (lane == 0 && n_hits) atomicAdd(c + qHits, n_hits);
 }
 
 // Copy each chunk's hits to its output position, mapping link rows to atom ids.
@@ -323,7 +330,7 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     QPlan* d_plan = (QPlan*)dalloc(sizeof(QPlan) * n);
     int32_t* d_nch = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
     int32_t* d_choff = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
-    u64* d_ctr = (u64*)dalloc(sizeof(u64) * qNum);
+    u64* d_ctr = (u64*)dalloc(sizeof(u64) * kQShards * kQStride);
     HGX_HIP(hipMemcpyAsync(d_type, q_type.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     HGX_HIP(hipMemcpyAsync(d_nop, q_nop.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     HGX_HIP(hipMemcpyAsync(d_ord, q_ord.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
@@ -333,7 +340,7 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
         HGX_HIP(hipMemcpyAsync(d_anch, anchors.data(), sizeof(int32_t) * anchors.size(), hipMemcpyHostToDevice, s));
     if (!pattern.empty())
         HGX_HIP(hipMemcpyAsync(d_pat, pattern.data(), sizeof(int32_t) * pattern.size(), hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * qNum, s));
+    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * kQShards * kQStride, s));
     HGX_HIP(hipMemsetAsync(d_nch + n, 0, sizeof(int32_t), s));
 
     if (g->timing) HGX_HIP(hipEventRecord(ev[0], s));
@@ -358,7 +365,7 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     HGX_CHECK_LAUNCH();
     if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
     if (n_chunks > 0) {
-        hgx_pattern_match<<<(unsigned)ceil_div((int64_t)n_chunks * 64, 256), 256, 0, s>>>(
+        hgx_pattern_match<<<grid_for((int64_t)n_chunks * 64, 256, 4096), 256, 0, s>>>(
             n_chunks, d_chq, d_choff, d_plan, d_type, d_aoff, d_anch, d_poff, d_pat, d_ord, g->inc_row, g->inc_type,
             g->tgt_off, g->tgt_idx, d_slots, d_cnt, d_ctr);
         HGX_CHECK_LAUNCH();
@@ -386,9 +393,11 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
         HGX_HIP(hipMemcpyAsync(r->ids.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, s));
     }
     if (g->timing) HGX_HIP(hipEventRecord(ev[3], s));
-    u64 hctr[qNum];
-    HGX_HIP(hipMemcpyAsync(hctr, d_ctr, sizeof(hctr), hipMemcpyDeviceToHost, s));
+    u64 hsh[kQShards * kQStride], hctr[qNum] = {0, 0, 0, 0};
+    HGX_HIP(hipMemcpyAsync(hsh, d_ctr, sizeof(hsh), hipMemcpyDeviceToHost, s));
     HGX_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < qNum; ++k)
+        for (int sh = 0; sh < kQShards; ++sh) hctr[k] += hsh[sh * kQStride + k];
     if (g->timing) {
         float a = 0, b = 0;
         HGX_HIP(hipEventElapsedTime(&a, ev[0], ev[3]));

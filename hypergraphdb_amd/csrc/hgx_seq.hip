@@ -124,42 +124,64 @@ __global__ void __launch_bounds__(256) hgx_seq_expand(ExpandArgs a) {
         }
         __syncthreads();
         const int64_t it = t0 + threadIdx.x;
-        if (it > t1) continue;
-        const int64_t i = seg_search(a.pre, s_lo, s_hi, it);
-        const int64_t j = it - a.pre[i];
-        const int32_t p = a.fr_atom[i];
-        const int64_t ii = a.inc_off[p] + j;
-        if (a.want_type >= 0 && a.inc_type[ii] != a.want_type) continue;   // linkPredicate (:300)
-        const int32_t L = a.inc_row[ii];
-        const int64_t b = a.tgt_off[L];
-        const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
-        if (n < a.min_arity) continue;                                      // minArity (:309)
-        const int32_t* tg = a.tgt_idx + b;
-        int32_t lo = 0, hi = n;                                             // yielded positions [lo, hi)
-        if (a.mode != sSym) {
-            int32_t fv = -1, lv = -1;
-            for (int32_t q = 0; q < n; ++q)
-                if (tg[q] == p) {
-                    if (fv < 0) fv = q;
-                    lv = q;
+        int32_t p = -1, lo = 0, cnt = 0, n = 0;
+        int64_t i = 0, j = 0, b = 0;
+        if (it <= t1) {
+            i = seg_search(a.pre, s_lo, s_hi, it);
+            j = it - a.pre[i];
+            p = a.fr_atom[i];
+            const int64_t ii = a.inc_off[p] + j;
+            if (a.want_type < 0 || a.inc_type[ii] == a.want_type) {              // linkPredicate (:300)
+                const int32_t L = a.inc_row[ii];
+                b = a.tgt_off[L];
+                n = (int32_t)(a.tgt_off[L + 1] - b);
+                if (n >= a.min_arity) {                                           // minArity (:309)
+                    int32_t hi = n;                                               // yielded positions [lo, hi)
+                    if (a.mode != sSym) {
+                        int32_t fv = -1, lv = -1;
+                        for (int32_t q = 0; q < n; ++q)
+                            if (a.tgt_idx[b + q] == p) {
+                                if (fv < 0) fv = q;
+                                lv = q;
+                            }
+                        if (a.mode == sAfterFirst) lo = fv + 1;
+                        else if (a.mode == sBeforeFirst) hi = fv;
+                        else if (a.mode == sBeforeLast) hi = lv;
+                        else lo = lv + 1;
+                    }
+                    cnt = hi > lo ? hi - lo : 0;
                 }
-            if (a.mode == sAfterFirst) lo = fv + 1;
-            else if (a.mode == sBeforeFirst) hi = fv;
-            else if (a.mode == sBeforeLast) hi = lv;
-            else lo = lv + 1;
+            }
         }
-        const int64_t sA = (int64_t)a.fr_seed[i] * a.A;
+        int32_t rounds = cnt;
+        for (int off = 32; off > 0; off >>= 1) rounds = max(rounds, __shfl_xor(rounds, off));
+        const int64_t sA = p >= 0 ? (int64_t)a.fr_seed[i] * a.A : 0;
         const u64 kb = ((a.e_base + (u64)i) << a.sh_e) | ((u64)j << a.sh_j);
-        for (int32_t q = lo; q < hi; ++q) {
-            const int32_t t = tg[q];
-            if (t == p) continue;                  // the expanded atom is examined already
-            const u64 k = kb | (u64)(a.rev ? n - 1 - q : q);
-            u64* slot = a.key + sA + t;
-            if (*slot <= k) continue;   // examined, or an earlier yield won
-            const u64 old = atomicMin(slot, k);
-            if (old == kNoKey) {
-                const u64 w = atomicAdd(a.list_n, 1ull);
-                if ((int64_t)w < a.cap) a.list[w] = sA + t;
+        // wave-uniform rounds so first discoveries are appended with one atomic per wave and round
+        for (int32_t r = 0; r < rounds; ++r) {
+            bool isnew = false;
+            int32_t t = 0;
+            if (r < cnt) {
+                const int32_t q = lo + r;
+                t = a.tgt_idx[b + q];
+                if (t != p) {                          // the expanded atom is examined already
+                    const u64 k = kb | (u64)(a.rev ? n - 1 - q : q);
+                    u64* slot = a.key + sA + t;
+                    if (*slot > k)                     // else: examined, or an earlier yield won
+                        isnew = atomicMin(slot, k) == kNoKey;
+                }
+            }
+            const u64 m = __ballot(isnew);
+            if (m) {
+                const int lane = threadIdx.x & 63;
+                const int leader = __ffsll((long long)m) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd(a.list_n, (u64)__popcll(m));
+                base = __shfl(base, leader);
+                if (isnew) {
+                    const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
+                    if ((int64_t)w < a.cap) a.list[w] = sA + t;
+                }
             }
         }
     }
