@@ -34,6 +34,8 @@ EXPORTED = (
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
     "hgx_seq_result_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
+    "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_free", "hgx_shard_graph_create",
+    "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
 )
 
 
@@ -61,11 +63,13 @@ class BfsStats(C.Structure):
                 ("bytes_survey", C.c_double), ("traversed_edges", C.c_double),
                 ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64),
                 ("level_bytes", C.c_double * 64), ("level_sparse", C.c_int32 * 64),
-                ("level_rows", (C.c_int64 * 8) * 64)]
+                ("level_rows", (C.c_int64 * 8) * 64), ("ms_exchange", C.c_double),
+                ("bytes_exchanged", C.c_double)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
-             "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges}
+             "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges,
+             "ms_exchange": self.ms_exchange, "bytes_exchanged": self.bytes_exchanged}
         d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
                             "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
         n = max(self.n_levels_expanded, 0)
@@ -132,6 +136,16 @@ def lib():
         "hgx_query_result_ids": ([vp, vp], C.c_int),
         "hgx_query_result_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         "hgx_query_result_free": ([vp], None),
+        "hgx_shard_build": ([C.POINTER(GraphDesc), i32, i32, C.POINTER(vp)], C.c_int),
+        "hgx_shard_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "hgx_shard_export": ([vp, vp, vp, vp, vp, vp, vp], C.c_int),
+        "hgx_shard_free": ([vp], None),
+        "hgx_shard_graph_create": ([vp, i32, C.POINTER(vp)], C.c_int),
+        "hgx_comm_rccl_unique_id": ([vp], C.c_int),
+        "hgx_comm_rccl_create": ([vp, i32, i32, i32, C.POINTER(vp)], C.c_int),
+        "hgx_comm_destroy": ([vp], None),
+        "hgx_pbfs_batch": ([vp, vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
+        "hgx_pbfs_batch_group": ([vp, i32, vp, i32, i32, C.POINTER(AlgenOpts), vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
 
 #include "hgx_internal.h"
 
@@ -848,6 +849,119 @@ __global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa,
     *out = d;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Partitioned BFS: per-level exchange of ghost rows.  After the local
+// expansion, the lvl_next row of a ghost holds the bits this shard discovered for an atom owned
+// elsewhere (ghost vis = bits already sent, so only news travel).  hgx_ghost_pack moves those rows
+// into per-owner send segments and clears the ghost frontier bits; the owner ORs the received rows
+// in with hgx_ghost_apply (new = row & ~vis), one launch per source segment so every atom appears
+// at most once per launch.
+// Record = (W + 1) u64: [global atom id, row words].
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ void __launch_bounds__(256) hgx_ghost_pack(int64_t A, u64* __restrict__ fa_next,
+                                                      const u64* __restrict__ own_bm,
+                                                      const int32_t* __restrict__ l2g, int32_t NP,
+                                                      const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
+                                                      const int64_t* __restrict__ seg_start, u64* __restrict__ send) {
+    constexpr int R = 64 / W;   // rows copied per wave iteration (W lanes per row)
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const u64 lt = (1ull << lane) - 1ull;
+    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+        const u64 f = fa_next[tile], own = own_bm[tile];
+        u64 gh = f & ~own;
+        if (gh == 0) continue;   // wave-uniform
+        const int64_t t = tile * 64 + lane;
+        const bool hit = (gh >> lane) & 1ull;
+        const int32_t gid = hit ? l2g[t] : 0;
+        const int dest = hit ? (int)(gid % NP) : -1;
+        int64_t slot = 0;
+        for (int d = 0; d < NP; ++d) {
+            const u64 m = __ballot(dest == d);
+            if (m == 0) continue;
+            const int leader = __ffsll((long long)m) - 1;
+            u64 base = 0;
+            if (lane == leader) base = atomicAdd(&cursor[d], (u64)__popcll(m));
+            base = __shfl(base, leader);
+            if (dest == d) slot = seg_start[d] + (int64_t)base + __popcll(m & lt);
+        }
+        const int k = lane / W, w = lane % W;
+        while (gh) {
+            u64 x = gh;
+            for (int i = 0; i < k && x; ++i) x &= x - 1ull;
+            const int src = x ? __ffsll((long long)x) - 1 : -1;
+            for (int i = 0; i < R && gh; ++i) gh &= gh - 1ull;
+            const int64_t s_slot = __shfl(slot, src < 0 ? 0 : src);
+            const int32_t s_gid = __shfl(gid, src < 0 ? 0 : src);
+            if (src >= 0) {
+                u64* rec = send + s_slot * (W + 1);
+                if (w == 0) rec[0] = (u64)(uint32_t)s_gid;
+                rec[1 + w] = lvl_next[(tile * 64 + src) * W + w];
+            }
+        }
+        if (lane == 0) fa_next[tile] = f & own;
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_ghost_apply(int64_t n, const u64* __restrict__ recv,
+                                                       const int32_t* __restrict__ own_l, int32_t NP,
+                                                       u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                       u64* __restrict__ vis, u64* __restrict__ ever,
+                                                       u64* __restrict__ full, FullMask fm) {
+    constexpr int R = 64 / W;
+    const int lane = threadIdx.x & 63, k = lane / W, w = lane % W;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const u64 FW = fm.w[w];
+    for (int64_t base = wave * R; base < n; base += nwave * R) {
+        const int64_t i = base + k;
+        const bool valid = i < n;
+        int64_t t = 0;
+        u64 r = 0;
+        if (valid) {
+            const u64* rec = recv + i * (W + 1);
+            t = own_l[(uint32_t)rec[0] / (uint32_t)NP];
+            r = rec[1 + w];
+        }
+        const bool ev = valid && bit(ever, t);
+        const u64 old = ev ? vis[t * W + w] : 0ull;
+        const u64 nw = r & ~old;
+        const bool any = group_any<W>(nw != 0ull);
+        const bool becomes_full = group_all<W>((old | nw) == FW);
+        if (valid && any) {
+            const bool was = bit(fa_next, t);
+            lvl_next[t * W + w] = was ? (lvl_next[t * W + w] | nw) : nw;
+            vis[t * W + w] = old | nw;
+            if (w == 0) {
+                if (!was) set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (becomes_full) set_bit(full, t);
+            }
+        }
+    }
+}
+
+// out[0] += |frontier|, out[1] += sum of |inc(v)| over the frontier (owned atoms only after the pack)
+__global__ void __launch_bounds__(256) hgx_frontier_stats(int64_t A, const u64* __restrict__ fa,
+                                                          const int64_t* __restrict__ inc_off, u64* __restrict__ out) {
+    u64 n = 0, deg = 0;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w * 64 < A;
+         w += (int64_t)gridDim.x * blockDim.x) {
+        u64 x = fa[w];
+        n += __popcll(x);
+        while (x) {
+            const int64_t v = w * 64 + __ffsll((long long)x) - 1;
+            x &= x - 1ull;
+            deg += (u64)(inc_off[v + 1] - inc_off[v]);
+        }
+    }
+    wave_add(out, n);
+    wave_add(out + 1, deg);
+}
+
 }  // namespace hgx
 
 using namespace hgx;
@@ -921,6 +1035,11 @@ struct Timer {
         for (auto& r : rec) {
             float ms = 0;
             HGX_HIP(hipEventElapsedTime(&ms, r.e.a, r.e.b));
+            if (r.kind == HGX_K_COUNT) {   // the partitioned exchange
+                st.ms_exchange += ms;
+                if (r.level < 64) st.level_ms[r.level] += ms;
+                continue;
+            }
             st.ms_kernel[r.kind] += ms;
             if (r.level < 64) st.level_ms[r.level] += ms;
         }
@@ -928,7 +1047,7 @@ struct Timer {
 };
 
 enum { kKindGather = HGX_K_LINK_GATHER, kKindPull = HGX_K_ATOM_PULL, kKindHeavy = HGX_K_PULL_HEAVY,
-       kKindHub = HGX_K_HUB_FINALIZE };
+       kKindHub = HGX_K_HUB_FINALIZE, kKindExchange = HGX_K_COUNT };
 
 FullMask full_mask(int S, int W) {
     FullMask fm;
@@ -939,10 +1058,104 @@ FullMask full_mask(int S, int W) {
     return fm;
 }
 
+// Per-batch buffers of the partitioned exchange (send segments per owner, receive area).
+struct Exchange {
+    hgx_graph* g;
+    Transport* tr;
+    int W;
+    int64_t rec_words;                  // W + 1
+    u64* send = nullptr;
+    u64* recv = nullptr;
+    u64* cursor = nullptr;              // [NP] device
+    u64* fstats = nullptr;              // [2] device
+    int64_t* seg_start = nullptr;       // [NP] device
+    int64_t send_recs = 0, recv_recs = 0;
+    std::vector<int64_t> recv_cnt_cap;  // per source part
+    double bytes_sent = 0;
+    Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w), rec_words(w + 1) {
+        ShardInfo& sh = *g->shard;
+        const int NP = sh.n_parts;
+        {   // how many of my atoms each part holds as ghosts (collective, once per batch)
+            std::vector<int64_t> all((size_t)NP * NP);
+            tr->allgather_i64(sh.ghost_count.data(), NP, all.data(), g->stream);
+            sh.recv_count.assign(NP, 0);
+            for (int p = 0; p < NP; ++p) sh.recv_count[p] = all[(size_t)p * NP + sh.part];
+        }
+        send_recs = sh.n_ghost;
+        recv_recs = 0;
+        for (int p = 0; p < NP; ++p) recv_recs += sh.recv_count[p];
+        send = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(send_recs, 1) * rec_words);
+        recv = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(recv_recs, 1) * rec_words);
+        cursor = (u64*)g->alloc(sizeof(u64) * (NP + 2));
+        fstats = cursor + NP;
+        seg_start = (int64_t*)g->alloc(sizeof(int64_t) * NP);
+        HGX_HIP(hipMemcpyAsync(seg_start, sh.ghost_start.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice,
+                               g->stream));
+    }
+    ~Exchange() {
+        const int NP = g->shard->n_parts;
+        g->release(send, sizeof(u64) * (size_t)std::max<int64_t>(send_recs, 1) * rec_words);
+        g->release(recv, sizeof(u64) * (size_t)std::max<int64_t>(recv_recs, 1) * rec_words);
+        g->release(cursor, sizeof(u64) * (NP + 2));
+        g->release(seg_start, sizeof(int64_t) * NP);
+    }
+    // Ship ghost rows to their owners and OR in what the other parts found for my atoms.  Returns
+    // the group-wide number of new atoms; *push_volume = sum of |inc| over my new frontier.
+    template <int Wt>
+    u64 level(u64* lvl_next, u64* fa_next, u64* vis, u64* ever, u64* full, const FullMask& fm, u64* push_volume) {
+        ShardInfo& sh = *g->shard;
+        const int NP = sh.n_parts, me = sh.part;
+        hipStream_t s = g->stream;
+        const int64_t A = g->A;
+        HGX_HIP(hipMemsetAsync(cursor, 0, sizeof(u64) * (NP + 2), s));
+        hgx_ghost_pack<Wt><<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(
+            A, fa_next, (const u64*)sh.own_bm, sh.l2g, NP, lvl_next, cursor, seg_start, send);
+        HGX_CHECK_LAUNCH();
+        std::vector<u64> cnt(NP);
+        HGX_HIP(hipMemcpyAsync(cnt.data(), cursor, sizeof(u64) * NP, hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        std::vector<int64_t> mine(NP), all((size_t)NP * NP);
+        for (int p = 0; p < NP; ++p) mine[p] = (int64_t)cnt[p];
+        tr->allgather_i64(mine.data(), NP, all.data(), s);
+        const int64_t rb = (int64_t)sizeof(u64) * rec_words;
+        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP), rcnt(NP);
+        int64_t ro = 0;
+        for (int p = 0; p < NP; ++p) {
+            soff[p] = sh.ghost_start[p] * rb;
+            sbytes[p] = mine[p] * rb;
+            rcnt[p] = all[(size_t)p * NP + me];
+            if (rcnt[p] > sh.recv_count[p]) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
+            roff[p] = ro * rb;
+            rbytes[p] = rcnt[p] * rb;
+            ro += rcnt[p];
+            bytes_sent += (double)sbytes[p];
+        }
+        tr->alltoallv(send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
+        for (int p = 0; p < NP; ++p) {
+            if (p == me || rcnt[p] == 0) continue;
+            hgx_ghost_apply<Wt><<<grid_for(ceil_div(rcnt[p], 64 / Wt) * 64, 256, 8192), 256, 0, s>>>(
+                rcnt[p], recv + roff[p] / (int64_t)sizeof(u64), sh.own_l, NP, lvl_next, fa_next, vis, ever, full, fm);
+            HGX_CHECK_LAUNCH();
+        }
+        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, g->inc_off, fstats);
+        HGX_CHECK_LAUNCH();
+        u64 fs[2];
+        HGX_HIP(hipMemcpyAsync(fs, fstats, sizeof(fs), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        *push_volume = fs[1];
+        int64_t nl = (int64_t)fs[0];
+        std::vector<int64_t> nall(NP);
+        tr->allgather_i64(&nl, 1, nall.data(), s);
+        u64 tot = 0;
+        for (int p = 0; p < NP; ++p) tot += (u64)nall[p];
+        return tot;
+    }
+};
+
 template <int W, int MODE>
 void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_depth, int32_t want_type,
                 const std::vector<int32_t>& seed_atoms, const std::vector<u64>& seed_rows, Timer& tm,
-                std::vector<std::vector<u64>>& level_ctr) {
+                std::vector<std::vector<u64>>& level_ctr, Transport* tr) {
     hipStream_t s = g->stream;
     const int64_t A = g->A, M = g->M;
     const size_t row_bytes = sizeof(u64) * (size_t)A * W;
@@ -989,6 +1202,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // Direction choice per level (Beamer-style): when the frontier's incidence volume
     // sum_{v in F} |inc(v)| is small, the level runs sparse -- candidate links are pushed from the
     // frontier atoms and only candidate tiles are gathered / pulled.  Otherwise every tile is scanned.
+    std::unique_ptr<Exchange> ex;
+    if (tr) ex.reset(new Exchange(g, tr, W));
     const bool sparse_ok = (g->bfs_flags & 8) != 0;
     u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
     u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
@@ -1071,11 +1286,21 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             tm.stop(e4);
         }
         }
+        u64 new_global = 0, part_push = 0;
+        if (ex) {
+            Events e5 = tm.start(kKindExchange, d);
+            new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push);
+            tm.stop(e5);
+        }
         HGX_HIP(hipMemcpyAsync(h_sh, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
         for (int k = 0; k < cNum; ++k) {
             h_new[k] = 0;
             for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += h_sh[sh * kCtrStride + k];
+        }
+        if (ex) {   // the group decides termination; the next level's push volume is my frontier's
+            h_new[cNewAtoms] = new_global;
+            h_new[cNewDeg] = part_push;
         }
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
         level_ctr.back()[cDirRows] = sparse ? 1 : 0;   // (host-side) mode of this level
@@ -1089,6 +1314,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         bt.lvl.push_back(lvl_next);
         bt.fa.push_back(fa_next);
     }
+    if (ex) res->stats.bytes_exchanged += ex->bytes_sent;
     g->release(vis, row_bytes);
     if (lf) g->release(lf, sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W);
     g->release(hubacc, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W);
@@ -1105,13 +1331,13 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
 template <int W>
 void run_mode(int mode, hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_depth, int32_t want_type,
               const std::vector<int32_t>& sa, const std::vector<u64>& sr, Timer& tm,
-              std::vector<std::vector<u64>>& lc) {
+              std::vector<std::vector<u64>>& lc, Transport* tr) {
     switch (mode) {
-        case kSym: run_levels<W, kSym>(g, res, bt, max_depth, want_type, sa, sr, tm, lc); break;
-        case kAfterFirst: run_levels<W, kAfterFirst>(g, res, bt, max_depth, want_type, sa, sr, tm, lc); break;
-        case kBeforeFirst: run_levels<W, kBeforeFirst>(g, res, bt, max_depth, want_type, sa, sr, tm, lc); break;
-        case kBeforeLast: run_levels<W, kBeforeLast>(g, res, bt, max_depth, want_type, sa, sr, tm, lc); break;
-        default: run_levels<W, kAfterLast>(g, res, bt, max_depth, want_type, sa, sr, tm, lc); break;
+        case kSym: run_levels<W, kSym>(g, res, bt, max_depth, want_type, sa, sr, tm, lc, tr); break;
+        case kAfterFirst: run_levels<W, kAfterFirst>(g, res, bt, max_depth, want_type, sa, sr, tm, lc, tr); break;
+        case kBeforeFirst: run_levels<W, kBeforeFirst>(g, res, bt, max_depth, want_type, sa, sr, tm, lc, tr); break;
+        case kBeforeLast: run_levels<W, kBeforeLast>(g, res, bt, max_depth, want_type, sa, sr, tm, lc, tr); break;
+        default: run_levels<W, kAfterLast>(g, res, bt, max_depth, want_type, sa, sr, tm, lc, tr); break;
     }
 }
 
@@ -1181,6 +1407,9 @@ void ensure_counts(hgx_bfs_result* r) {
     r->counts_ready = true;
 }
 
+void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
+                    const hgx_algen_opts* opts, hgx_bfs_result** out);
+
 }  // namespace
 
 extern "C" {
@@ -1190,18 +1419,51 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
     HGX_API_BEGIN
     if (!g || !out || n_seeds < 0 || (n_seeds > 0 && !seeds)) fail(HGX_E_INVALID, "hgx_bfs_batch: bad argument");
     *out = nullptr;
-    hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
+    if (g->shard) fail(HGX_E_INVALID, "hgx_bfs_batch: a partition shard needs hgx_pbfs_batch (a transport)");
     for (int32_t i = 0; i < n_seeds; ++i)
         if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_batch: seed out of range");
     if (max_depth < -1) fail(HGX_E_INVALID, "hgx_bfs_batch: bad max_depth");
+    bfs_batch_impl(g, nullptr, seeds, n_seeds, max_depth, opts, out);
+    HGX_API_END
+}
+
+}  // extern "C"
+
+// Partitioned batched BFS: seeds are GLOBAL atom ids; this shard seeds the ones it owns.
+void hgx::pbfs_run(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
+                   const hgx_algen_opts* opts, hgx_bfs_result** out) {
+    if (!g->shard) fail(HGX_E_INVALID, "hgx_pbfs_batch: not a partition shard");
+    const ShardInfo& sh = *g->shard;
+    if (tr->world != sh.n_parts || tr->rank != sh.part)
+        fail(HGX_E_INVALID, "hgx_pbfs_batch: transport rank/world does not match the shard's part/n_parts");
+    for (int32_t i = 0; i < n_seeds; ++i)
+        if (seeds[i] < 0 || seeds[i] >= sh.A_global) fail(HGX_E_INVALID, "hgx_pbfs_batch: seed out of range");
+    if (max_depth < -1) fail(HGX_E_INVALID, "hgx_pbfs_batch: bad max_depth");
+    bfs_batch_impl(g, tr, seeds, n_seeds, max_depth, opts, out);
+}
+
+namespace {
+
+void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
+                    const hgx_algen_opts* opts, hgx_bfs_result** out) {
+    hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
+    const ShardInfo* shp = g->shard;
     std::lock_guard<std::mutex> lk(g->mu);
     HGX_HIP(hipSetDevice(g->device));
     const int mode = mode_of(o);
 
     hgx_bfs_result* r = new hgx_bfs_result();
-    struct Guard {
+    struct Guard {   // error path: the graph mutex is held here, so release without re-locking
         hgx_bfs_result* r;
-        ~Guard() { if (r) hgx_bfs_result_free(r); }
+        ~Guard() {
+            if (!r) return;
+            for (auto& bt : r->batches) {
+                for (auto p : bt.lvl) r->g->release(p, r->row_bytes(bt));
+                for (auto p : bt.fa) r->g->release(p, r->bm_bytes());
+            }
+            r->g->refs.fetch_sub(1);   // the caller still holds its own reference
+            delete r;
+        }
     } guard{r};
     r->g = g;
     g->refs.fetch_add(1);
@@ -1220,7 +1482,12 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
         // unique seed atoms (ascending) and their rows
         std::map<int32_t, std::vector<u64>> rows;
         for (int32_t i = 0; i < bt.S; ++i) {
-            auto& row = rows[seeds[s0 + i]];
+            int32_t a = seeds[s0 + i];
+            if (shp) {   // a shard seeds only its own atoms (local id)
+                if (a % shp->n_parts != shp->part) continue;
+                a = shp->own_l_host[a / shp->n_parts];
+            }
+            auto& row = rows[a];
             if (row.empty()) row.assign(bt.W, 0ull);
             row[i >> 6] |= 1ull << (i & 63);
         }
@@ -1232,11 +1499,11 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
         }
         size_t before = level_ctr.size();
         switch (bt.W) {
-            case 1: run_mode<1>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
-            case 2: run_mode<2>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
-            case 4: run_mode<4>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
-            case 8: run_mode<8>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
-            default: run_mode<16>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr); break;
+            case 1: run_mode<1>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr, tr); break;
+            case 2: run_mode<2>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr, tr); break;
+            case 4: run_mode<4>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr, tr); break;
+            case 8: run_mode<8>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr, tr); break;
+            default: run_mode<16>(mode, g, r, bt, max_depth, o.link_type, sa, sr, tm, level_ctr, tr); break;
         }
         // algorithmic bytes of every launch of this batch
         const int64_t A = g->A, M = g->M, P = g->P, I = g->I;
@@ -1298,8 +1565,11 @@ int hgx_bfs_batch(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t m
     }
     guard.r = nullptr;
     *out = r;
-    HGX_API_END
 }
+
+}  // namespace
+
+extern "C" {
 
 int hgx_bfs_result_info(const hgx_bfs_result* r, int32_t* n_seeds, int32_t* n_levels) {
     HGX_API_BEGIN
@@ -1357,6 +1627,8 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
         HGX_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * k, hipMemcpyDeviceToHost, g->stream));
         HGX_HIP(hipStreamSynchronize(g->stream));
         g->release(dout, sizeof(int32_t) * k);
+        if (g->shard)   // local ids are in global order: the mapped list stays ascending
+            for (int64_t i = 0; i < k; ++i) out[i] = g->shard->l2g_host[out[i]];
     }
     g->release(dcnt, sizeof(int64_t) * nblk * 2);
     HGX_API_END
@@ -1367,6 +1639,12 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
     if (!r || !depth_out) fail(HGX_E_INVALID, "hgx_bfs_result_depth_of: bad argument");
     if (seed_index < 0 || seed_index >= r->n_seeds) fail(HGX_E_NOTFOUND, "no such seed index");
     hgx_graph* g = r->g;
+    if (g->shard) {   // global id of an atom this shard owns
+        const ShardInfo& sh = *g->shard;
+        if (atom < 0 || atom >= sh.A_global) fail(HGX_E_INVALID, "atom id out of range");
+        if (atom % sh.n_parts != sh.part) fail(HGX_E_NOTFOUND, "atom is owned by another part");
+        atom = sh.own_l_host[atom / sh.n_parts];
+    }
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "atom id out of range");
     std::lock_guard<std::mutex> lk(g->mu);
     HGX_HIP(hipSetDevice(g->device));

@@ -31,6 +31,10 @@ void graph_release(hgx_graph* g) {
     (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->stream) (void)hipStreamDestroy(g->stream);
+    if (g->shard) {
+        (void)hipFree(g->shard->l2g); (void)hipFree(g->shard->own_l); (void)hipFree(g->shard->own_bm);
+        delete g->shard;
+    }
     delete g;
 }
 
@@ -90,11 +94,11 @@ __global__ void __launch_bounds__(256) k_row_offsets(int64_t I, int64_t A, const
 __global__ void __launch_bounds__(256) k_validate(int64_t A, int64_t M, const int32_t* __restrict__ link_atom,
                                                   const int64_t* __restrict__ tgt_off,
                                                   const int32_t* __restrict__ tgt_idx, int64_t P,
-                                                  unsigned int* __restrict__ bad) {
+                                                  unsigned int* __restrict__ bad, int links_are_atoms) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M;
          r += (int64_t)gridDim.x * blockDim.x) {
         int32_t la = link_atom[r];
-        if (la < 0 || la >= A || (r > 0 && link_atom[r - 1] >= la)) atomicOr(bad, 1u);
+        if (la < 0 || (links_are_atoms && la >= A) || (r > 0 && link_atom[r - 1] >= la)) atomicOr(bad, 1u);
         if (tgt_off[r] > tgt_off[r + 1] || tgt_off[r + 1] > P) atomicOr(bad, 2u);
     }
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P;
@@ -210,7 +214,14 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     HGX_API_BEGIN
     if (!d || !out) fail(HGX_E_INVALID, "hgx_graph_create: null argument");
     *out = nullptr;
-    if (d->num_atoms < 0 || d->num_links < 0 || d->num_links > d->num_atoms)
+    *out = graph_create(d, device, true);
+    HGX_API_END
+}
+
+}  // extern "C"
+
+hgx_graph* hgx::graph_create(const hgx_graph_desc* d, int32_t device, bool links_are_atoms) {
+    if (d->num_atoms < 0 || d->num_links < 0 || (links_are_atoms && d->num_links > d->num_atoms))
         fail(HGX_E_INVALID, "hgx_graph_create: bad sizes");
     if (d->num_atoms >= (int64_t)INT32_MAX) fail(HGX_E_INVALID, "hgx_graph_create: more than 2^31-1 atoms");
     if (d->num_links > 0 && (!d->link_atom || !d->tgt_off || !d->tgt_idx))
@@ -257,7 +268,8 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     unsigned long long* ndup = (unsigned long long*)((char*)bad + 8);
     HGX_HIP(hipMemsetAsync(bad, 0, 16, s));
     if (M > 0) {
-        k_validate<<<grid_for(std::max(M, P), 256), 256, 0, s>>>(A, M, g->link_atom, g->tgt_off, g->tgt_idx, P, bad);
+        k_validate<<<grid_for(std::max(M, P), 256), 256, 0, s>>>(A, M, g->link_atom, g->tgt_off, g->tgt_idx, P, bad,
+                                                                 links_are_atoms ? 1 : 0);
         HGX_CHECK_LAUNCH();
     }
     unsigned int hbad = 0;
@@ -356,9 +368,10 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     }
     g->release(bad, 16);
     guard.g = nullptr;
-    *out = g;
-    HGX_API_END
+    return g;
 }
+
+extern "C" {
 
 void hgx_graph_destroy(hgx_graph* g) { graph_release(g); }
 
@@ -414,6 +427,7 @@ int hgx_graph_degree(hgx_graph* g, const int32_t* atoms, int32_t n, int64_t* out
 int hgx_graph_incidence(hgx_graph* g, int32_t atom, int32_t* out, int64_t cap, int64_t* n_out) {
     HGX_API_BEGIN
     if (!g || !n_out || (cap > 0 && !out)) fail(HGX_E_INVALID, "hgx_graph_incidence: bad argument");
+    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_graph_incidence: not available on a partition shard");
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "hgx_graph_incidence: atom id out of range");
     std::lock_guard<std::mutex> lk(g->mu);
     HGX_HIP(hipSetDevice(g->device));

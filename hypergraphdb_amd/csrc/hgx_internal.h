@@ -76,7 +76,44 @@ struct PoolBuf {
     size_t n;
 };
 
+// Hash partition of a snapshot over n_parts devices: owner(atom) =
+// atom % n_parts.  A shard's local atoms are its owned atoms plus its ghosts (atoms owned
+// elsewhere that are targets of a local link); local links are the links with at least one
+// owned target (their target rows are replicated on every shard that holds one).  Local ids are
+// assigned in global id order, so every ascending local list is an ascending global list.
+struct ShardInfo {
+    int32_t n_parts = 1, part = 0;
+    int64_t A_global = 0, n_owned = 0, n_ghost = 0;
+    std::vector<int32_t> l2g_host;       // [A_local] global id of local atom
+    std::vector<int32_t> own_l_host;     // [ceil((A_global - part) / n_parts)] local id of atom part + k*n_parts
+    std::vector<int64_t> ghost_count;    // [n_parts] ghosts owned by each part (0 for this part)
+    std::vector<int64_t> ghost_start;    // [n_parts + 1] prefix of ghost_count (send segments)
+    std::vector<int64_t> recv_count;     // [n_parts] atoms of this part held as ghosts by each part
+                                         // (filled on the first exchange; -1 = unknown)
+    int32_t* l2g = nullptr;              // device copies
+    int32_t* own_l = nullptr;
+    uint64_t* own_bm = nullptr;          // [A_local/64 + 2] bit set <=> local atom is owned
+};
+
+// Transport of the per-level frontier exchange: RCCL between processes (one GPU each) or an
+// in-process group of shard threads.  Every call is collective over the group.
+struct Transport {
+    int32_t world = 1, rank = 0;
+    virtual ~Transport() {}
+    // out[r * n + i] = in[i] of rank r (host buffers)
+    virtual void allgather_i64(const int64_t* in, int64_t n, int64_t* out, hipStream_t s) = 0;
+    // rank p receives send_bytes[p] bytes from send + send_off[p]; this rank receives recv_bytes[p]
+    // bytes from rank p at recv + recv_off[p] (device buffers, ordered on stream s)
+    virtual void alltoallv(const void* send, const int64_t* send_off, const int64_t* send_bytes, void* recv,
+                           const int64_t* recv_off, const int64_t* recv_bytes, hipStream_t s) = 0;
+    virtual const char* kind() const = 0;
+};
+
 }  // namespace hgx
+
+struct hgx_comm {
+    hgx::Transport* t = nullptr;
+};
 
 struct hgx_graph {
     int device = 0;
@@ -103,6 +140,8 @@ struct hgx_graph {
     int32_t* heavy_atom = nullptr;  // [n_heavy]
     hgx::HeavyChunk* chunks = nullptr;
 
+    hgx::ShardInfo* shard = nullptr;   // set for a partition shard (hgx_shard_graph_create)
+
     std::vector<hgx::PoolBuf> pool;  // free device buffers for reuse across batches
     void* pinned = nullptr;          // small pinned host staging area
     size_t pinned_bytes = 0;
@@ -114,6 +153,12 @@ struct hgx_graph {
 
 namespace hgx {
 void graph_release(hgx_graph* g);   // drop a reference; frees at zero
+// Upload + incidence build.  links_are_atoms = false for partition shards: link rows then carry
+// their global link atom ids (not local atoms) and are not validated against num_atoms.
+hgx_graph* graph_create(const hgx_graph_desc* d, int32_t device, bool links_are_atoms);
+// Partitioned batched BFS over one shard; tr is the group's transport (hgx_bfs.hip).
+void pbfs_run(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
+              const hgx_algen_opts* opts, hgx_bfs_result** out);
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int grid_for(int64_t work_items, int block, int max_blocks = 8192) {
     int64_t b = ceil_div(work_items > 0 ? work_items : 1, block);

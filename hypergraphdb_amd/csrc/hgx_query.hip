@@ -277,6 +277,7 @@ namespace {
 
 int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     HGX_API_BEGIN
+    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
     std::vector<int32_t>& q_type = nb.q_type;
     std::vector<int32_t>& q_nop = nb.q_nop;
     std::vector<int32_t>& q_ord = nb.q_ord;

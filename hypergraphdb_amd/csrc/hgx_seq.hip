@@ -266,6 +266,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     HGX_API_BEGIN
     if (!g || !out || n_seeds < 0 || (n_seeds > 0 && !seeds)) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad argument");
     *out = nullptr;
+    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: not available on a partition shard");
     hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
     for (int32_t i = 0; i < n_seeds; ++i)
         if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_sequence: seed out of range");

@@ -115,6 +115,10 @@ typedef struct hgx_bfs_stats {
      * [2] lf rows pulled (light), [3] vis rows read, [4] new light atoms, [5] lf rows pulled
      * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
     int64_t level_rows[64][8];
+    /* partitioned BFS (hgx_pbfs_batch): device ms of the per-level exchange (pack, transport,
+     * apply, frontier count) and the ghost-row bytes this part sent */
+    double  ms_exchange;
+    double  bytes_exchanged;
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
@@ -199,6 +203,52 @@ int  hgx_query_result_ids(const hgx_query_result *r, int32_t *ids);
 /* device milliseconds of the last pattern batch (timing enabled). */
 int  hgx_query_result_ms(const hgx_query_result *r, double *ms_total, double *ms_match, double *bytes_match);
 void hgx_query_result_free(hgx_query_result *r);
+
+/* ---------------------------------------------------------------------------------------------
+ * Hash-partitioned snapshot and BFS (config 4: graphs sharded over the GPUs of a node).
+ *
+ * Replaces the same HGBreadthFirstTraversal/DefaultALGenerator loop as hgx_bfs_batch
+ * (C/algorithms/HGBreadthFirstTraversal.java:49-66, C/algorithms/DefaultALGenerator.java:287-315)
+ * when the incidence index (HGStore.getIncidenceResultSet, C/HGStore.java:253) is split by atom
+ * over n_parts devices.  owner(atom) = atom % n_parts.  Part p holds the incidence rows of its
+ * atoms and the target rows of every link with at least one target it owns; each level it sends
+ * the rows it found for atoms owned elsewhere to their owners (one all-to-all per level).
+ * Results are bit-identical to hgx_bfs_batch on the whole graph.
+ * -------------------------------------------------------------------------------------------- */
+typedef struct hgx_shard hgx_shard;   /* host-side partition of one part */
+typedef struct hgx_comm hgx_comm;     /* the group's transport            */
+
+/* Build part `part` of n_parts from the whole snapshot (host only, no device work). */
+int  hgx_shard_build(const hgx_graph_desc *global, int32_t n_parts, int32_t part, hgx_shard **out);
+/* n_local = owned + ghost atoms; local links / pins = the replicated link rows of this part. */
+int  hgx_shard_info(const hgx_shard *s, int64_t *n_local, int64_t *n_owned, int64_t *n_local_links,
+                    int64_t *n_local_pins);
+/* Copies of the local tables (any pointer may be NULL): l2g[n_local] global id of each local atom
+ * (ascending); link_atom/link_type[n_local_links] global link atom id / type of each local link;
+ * tgt_off[n_local_links+1], tgt_idx[n_local_pins] targets in LOCAL ids; ghost_count[n_parts]. */
+int  hgx_shard_export(const hgx_shard *s, int32_t *l2g, int32_t *link_atom, int32_t *link_type,
+                      int64_t *tgt_off, int32_t *tgt_idx, int64_t *ghost_count);
+void hgx_shard_free(hgx_shard *s);
+/* Upload a part to a device (incidence build as in hgx_graph_create).  The result is an hgx_graph
+ * that only hgx_pbfs_batch (+ the hgx_bfs_result_* readers) accepts. */
+int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out);
+
+/* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
+ * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */
+int  hgx_comm_rccl_unique_id(uint8_t id[128]);
+int  hgx_comm_rccl_create(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, hgx_comm **out);
+void hgx_comm_destroy(hgx_comm *c);
+
+/* One part's share of a partitioned batched BFS (collective: every part calls it with the same
+ * seeds, depth and options).  seeds are GLOBAL atom ids.  The result reports this part's atoms:
+ * counts are partial (sum them over parts), visited lists hold global ids (disjoint over parts),
+ * depth_of accepts only atoms this part owns (else HGX_E_NOTFOUND). */
+int  hgx_pbfs_batch(hgx_graph *shard, hgx_comm *comm, const int32_t *seeds, int32_t n_seeds,
+                    int32_t max_depth, const hgx_algen_opts *opts, hgx_bfs_result **out);
+/* All parts in this process: shards[p] is part p (any devices, including one device for all);
+ * runs one host thread per part over an in-process transport.  outs[p] receives part p's result. */
+int  hgx_pbfs_batch_group(hgx_graph *const *shards, int32_t n_parts, const int32_t *seeds, int32_t n_seeds,
+                          int32_t max_depth, const hgx_algen_opts *opts, hgx_bfs_result **outs);
 
 #ifdef __cplusplus
 }
