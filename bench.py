@@ -115,6 +115,104 @@ def cpu_query_baseline(g, qs, budget_s):
             "seconds": round(elapsed, 2)}
 
 
+def _kernel_roof(stats_list):
+    tot = {}
+    for st in stats_list:
+        for k, v in st["kernels"].items():
+            t = tot.setdefault(k, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+            t["ms"] += v["ms"]
+            t["bytes"] += v["bytes"]
+            t["launches"] += v["launches"]
+    dom = max(tot, key=lambda k: tot[k]["ms"])
+    t = tot[dom]
+    ach = t["bytes"] / (t["ms"] / 1e3) / 1e9 if t["ms"] > 0 else 0.0
+    return {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(t["ms"] / max(t["launches"], 1), 4)}
+
+
+def run_config4(args, ctx, barrier_sync, result):
+    """Config 4 (1B incidences): (a) replicated -- every GPU holds the whole snapshot (compacted
+    one-part shard) and traverses 1024/N of the sources; (b) partitioned -- the snapshot is
+    hash-partitioned over the N GPUs and all 1024 sources run together with one RCCL all-to-all per
+    level.  Both are strong scaling (fixed graph, fixed 1024 sources).  Fills result[...] in place
+    so a watchdog can still report what finished."""
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd.partition import RcclComm, Shard, ShardSnapshot, pbfs_batch, pbfs_batch_group
+    rank, world, local = ctx.rank, ctx.world, ctx.device
+    t0 = time.time()
+    g = synth.config4(scale=args.c4_scale, n_sources=args.sources)
+    seeds = g["seeds"]
+    log(f"rank {rank}: config4 generated in {time.time() - t0:.1f}s: A={g['num_atoms']} P={len(g['tgt_idx'])}")
+    wl = (f"config4: 100M nodes / 200M links (1.0B incidences), Chung-Lu gamma 2.1, {args.sources}-source BFS "
+          f"depth {args.depth}" if args.c4_scale == 1.0 else f"config4 at scale {args.c4_scale}")
+
+    def timed(run, n_steps):
+        barrier_sync()
+        t1 = time.perf_counter()
+        st = []
+        for _ in range(n_steps):
+            r = run()
+            st.append(r.stats(accounting=False))
+            r.close()
+        barrier_sync()
+        return ctx.max(time.perf_counter() - t1), st
+
+    # (a) replicated snapshot, sources split over the ranks
+    t0 = time.time()
+    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], 1, 0)
+    snap = ShardSnapshot(sh, local)
+    log(f"rank {rank}: config4 replica (one part, {sh.n_local} atoms with incidence) on device in "
+        f"{time.time() - t0:.1f}s")
+    sh.close()
+    snap.set_timing(True)
+    mine = np.array_split(seeds, world)[rank]
+    for _ in range(max(args.warmup, 1)):
+        r = pbfs_batch_group([snap], mine, args.depth)
+        acct = r.parts[0].stats(accounting=True)
+        r.close()
+    dt, st = timed(lambda: pbfs_batch_group([snap], mine, args.depth).parts[0], args.steps)
+    edges = ctx.sum(acct["traversed_edges"] * args.steps)
+    result["replicated"] = {
+        "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl,
+        "parallelism": f"snapshot replicated, {args.sources} sources split over {world} GPU(s)",
+        "traversed_edges_per_step": edges / args.steps, "roofline": _kernel_roof(st)}
+    log(f"rank {rank}: config4 replicated {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step")
+    snap.close()
+    del snap
+    if world == 1:
+        result["partitioned"] = dict(result["replicated"], parallelism="one part (no exchange)")
+        return
+    # (b) hash partition over the ranks, RCCL all-to-all per level
+    t0 = time.time()
+    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world, rank)
+    info = {"local_atoms": sh.n_local, "local_links": sh.n_links, "local_pins": sh.n_pins}
+    snap = ShardSnapshot(sh, local)
+    sh.close()
+    del g
+    snap.set_timing(True)
+    comm = RcclComm.create(world, rank, local, broadcast=ctx.broadcast_bytes)
+    log(f"rank {rank}: config4 part {rank}/{world} on device + RCCL comm in {time.time() - t0:.1f}s {info}")
+    for _ in range(max(args.warmup, 1)):
+        r = pbfs_batch(snap, comm, seeds, args.depth)
+        acct = r.stats(accounting=True)
+        r.close()
+    dt, st = timed(lambda: pbfs_batch(snap, comm, seeds, args.depth), args.steps)
+    edges = ctx.sum(acct["traversed_edges"] * args.steps)
+    xbytes = ctx.sum(sum(s["bytes_exchanged"] for s in st)) / args.steps
+    xms = ctx.max(sum(s["ms_exchange"] for s in st) / args.steps)
+    result["partitioned"] = {
+        "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl,
+        "parallelism": f"hash partition over {world} GPUs (owner = atom % {world}), RCCL all-to-all per level",
+        "exchange_bytes_per_step": xbytes, "exchange_ms_per_step": round(xms, 3),
+        "rank0_part": info, "roofline": _kernel_roof(st)}
+    log(f"rank {rank}: config4 partitioned {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step, "
+        f"exchange {xbytes / 1e9:.2f} GB/step")
+    comm.close()
+    snap.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,6 +224,10 @@ def main():
     ap.add_argument("--no-queries", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work per metric")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (1B incidences) legs")
+    ap.add_argument("--c4-scale", type=float, default=1.0, help="fraction of the config-4 size")
+    ap.add_argument("--c4-timeout", type=float, default=420.0,
+                    help="seconds after which the config-4 legs are abandoned (the line is still printed)")
     args = ap.parse_args()
 
     from hypergraphdb_amd import dist as hdist
@@ -237,6 +339,7 @@ def main():
             pattern["cpu_baseline"] = cpu_query_baseline(g3, Q, args.cpu_budget)
             log(f"cpu pattern baseline {pattern['cpu_baseline']['value']:.1f} q/s")
 
+    line = None
     if rank == 0:
         line = {
             "metric": "hyperedge TEPS for batched multi-source BFS; pattern-match queries/sec",
@@ -259,6 +362,31 @@ def main():
                         for k, v in per_kernel.items()},
             "pattern": pattern,
         }
+
+    # ---------------- config 4: 1B incidences, replicated vs hash-partitioned ----------------
+    if not args.no_config4:
+        import threading
+        c4 = {}
+
+        def watchdog():   # a hung collective must not cost the whole line
+            log(f"rank {rank}: config4 legs exceeded {args.c4_timeout:.0f}s; reporting what finished")
+            if line is not None:
+                line["config4"] = dict(c4, error=f"abandoned after {args.c4_timeout:.0f}s")
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(args.c4_timeout, watchdog)
+        wd.daemon = True
+        wd.start()
+        try:
+            run_config4(args, ctx, barrier_sync, c4)
+        except Exception as e:   # report, keep the main line
+            log(f"rank {rank}: config4 failed: {e!r}")
+            c4["error"] = repr(e)
+        wd.cancel()
+        if line is not None:
+            line["config4"] = c4
+    if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
 

@@ -984,6 +984,7 @@ struct hgx_bfs_result {
     hgx_bfs_stats stats{};
     bool counts_ready = false;
     bool typed = false;
+    std::map<int32_t, int32_t> isolated;   // shards: seed index -> owned seed atom without incidence
     std::vector<int64_t> counts;   // [n_seeds * n_levels]
     size_t row_bytes(const BfsBatch& b) const { return sizeof(u64) * (size_t)g->A * b.W; }
     size_t bm_bytes() const { return sizeof(u64) * (size_t)(g->A / 64 + 2); }
@@ -1202,8 +1203,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // Direction choice per level (Beamer-style): when the frontier's incidence volume
     // sum_{v in F} |inc(v)| is small, the level runs sparse -- candidate links are pushed from the
     // frontier atoms and only candidate tiles are gathered / pulled.  Otherwise every tile is scanned.
-    std::unique_ptr<Exchange> ex;
-    if (tr) ex.reset(new Exchange(g, tr, W));
+    std::unique_ptr<Exchange> ex;   // one part: no ghosts, nothing to exchange
+    if (tr && tr->world > 1) ex.reset(new Exchange(g, tr, W));
     const bool sparse_ok = (g->bfs_flags & 8) != 0;
     u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
     u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
@@ -1403,6 +1404,7 @@ void ensure_counts(hgx_bfs_result* r) {
         }
     }
     g->release(dc, sizeof(u64) * 1025);
+    for (auto& kv : r->isolated) r->counts[(size_t)kv.first * r->n_levels] += 1;
     r->stats.traversed_edges = trav_total;
     r->counts_ready = true;
 }
@@ -1486,6 +1488,10 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             if (shp) {   // a shard seeds only its own atoms (local id)
                 if (a % shp->n_parts != shp->part) continue;
                 a = shp->own_l_host[a / shp->n_parts];
+                if (a < 0) {   // no incidence: V_0 = {seed} and nothing else (kept on the host)
+                    r->isolated[s0 + i] = seeds[s0 + i];
+                    continue;
+                }
             }
             auto& row = rows[a];
             if (row.empty()) row.assign(bt.W, 0ull);
@@ -1600,6 +1606,14 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
     const BfsBatch& bt = r->batches[seed_index / 1024];
     const int s = seed_index % 1024;
     *n_out = 0;
+    auto iso = r->isolated.find(seed_index);
+    if (iso != r->isolated.end()) {   // an isolated seed: only itself, at distance 0
+        if (depth == 0) {
+            *n_out = 1;
+            if (cap > 0) out[0] = iso->second;
+        }
+        return HGX_OK;
+    }
     if (depth >= (int32_t)bt.lvl.size()) return HGX_OK;
     const int nblk = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(g->A, 4096)));
     const int64_t span = ceil_div(std::max<int64_t>(g->A, 1), nblk);
@@ -1643,7 +1657,13 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
         const ShardInfo& sh = *g->shard;
         if (atom < 0 || atom >= sh.A_global) fail(HGX_E_INVALID, "atom id out of range");
         if (atom % sh.n_parts != sh.part) fail(HGX_E_NOTFOUND, "atom is owned by another part");
-        atom = sh.own_l_host[atom / sh.n_parts];
+        const int32_t loc = sh.own_l_host[atom / sh.n_parts];
+        if (loc < 0) {   // no incidence: reached only as its own seed
+            auto iso = r->isolated.find(seed_index);
+            *depth_out = (iso != r->isolated.end() && iso->second == atom) ? 0 : -1;
+            return HGX_OK;
+        }
+        atom = loc;
     }
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "atom id out of range");
     std::lock_guard<std::mutex> lk(g->mu);

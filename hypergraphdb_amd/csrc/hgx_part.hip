@@ -7,6 +7,8 @@
 //   * every atom it owns (the incidence rows of owned atoms are complete on p),
 //   * every link with at least one owned target (target rows replicated, at most arity copies),
 //   * the ghosts: atoms owned elsewhere that are targets of a local link.
+// Owned atoms with no incidence (no link targets them, e.g. the link atoms of config 4) get no
+// local id and no device rows: they are reachable only as seeds.
 // Local ids follow global id order, so ascending local lists are ascending global lists and the
 // on-device incidence build of hgx_graph_create applies unchanged.
 //
@@ -94,7 +96,8 @@ hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part) {
     for (int b : bad)
         if (b == 1) fail(HGX_E_INVALID, "hgx_shard_build: tgt_off not monotone");
         else if (b == 2) fail(HGX_E_INVALID, "hgx_shard_build: target id out of range");
-    for (int64_t a = part; a < A; a += NP) mark[a] = 1;
+    // Owned atoms that no link targets are left out of the local space: BFS can reach them only
+    // as seeds (V_0 = {seed}), which the result records on the host (bfs_batch_impl).
     parallel_for(M, [&](int64_t lo, int64_t hi, int) {
         for (int64_t r = lo; r < hi; ++r)
             if (loc[r])
@@ -135,7 +138,7 @@ hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part) {
     const int64_t AL = (int64_t)s->l2g.size();
     s->n_owned = A > part ? (A - part + NP - 1) / NP : 0;
     s->own_l.resize((size_t)s->n_owned);
-    for (int64_t k = 0; k < s->n_owned; ++k) s->own_l[k] = g2l[part + k * NP];
+    for (int64_t k = 0; k < s->n_owned; ++k) s->own_l[k] = g2l[part + k * NP];   // -1: isolated
     s->ghost_count.assign(NP, 0);
     for (int64_t i = 0; i < AL; ++i) {
         const int o = s->l2g[i] % NP;

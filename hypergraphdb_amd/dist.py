@@ -4,8 +4,8 @@ The batched BFS shards by SOURCE: every rank holds a replica of the snapshot (co
 CSR on a 288 GB device) and traverses its own batch of start atoms, so the data path has no
 collective.  Only the barrier and the max/sum of scalars cross processes, over a CPU gloo group
 (torch.distributed is plumbing here; torch's HIP runtime is never initialised, so libhgx drives the
-device alone).  The hash-partitioned config-4 path with a per-level RCCL all-to-all is the next
-step.
+device alone).  The hash-partitioned config-4 path runs its per-level all-to-all over RCCL inside
+libhgx (partition.RcclComm); only the 128-byte RCCL unique id crosses this gloo group.
 """
 from __future__ import annotations
 
@@ -38,6 +38,14 @@ class RankContext:
 
     def sum(self, x):
         return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist is not None else x
+
+    def broadcast_bytes(self, data: bytes) -> bytes:
+        """rank 0's bytes on every rank (the RCCL unique id travels over the gloo group)"""
+        if self.dist is None:
+            return data
+        obj = [data if self.rank == 0 else None]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
 
     def close(self):
         if self.dist is not None:

@@ -69,6 +69,16 @@ def config3(scale=1.0, n_queries=10_000):
     return g
 
 
+def config4(scale=1.0, n_sources=1024):
+    """100M nodes, 200M links, arity U{2..8} (P ~ 1.0B incidences), Chung-Lu gamma 2.1, seed 45;
+    1024 sources over nodes with deg >= 1 (seed 7); depth 4.  Hash-partitioned over the GPUs."""
+    n, m = max(int(100_000_000 * scale), 64), max(int(200_000_000 * scale), 64)
+    g = hypergraph(n, m, 2, 8, 2.1, 1, seed=45)
+    g["seeds"] = sources(g, n_sources, 7)
+    g["depth"] = 4
+    return g
+
+
 def config5(scale=1.0, n_sources=1024, subsumes_type=1, noise_type=2):
     """5M classes; class i > 0 gets 1-3 HGSubsumes(parent, i) links with preferential parents
     (seed 46) + 5M noise arity-2 links of another type; 1024 sources uniform over classes."""

@@ -118,6 +118,9 @@ def test_depth_of_and_errors():
     assert res.depth_of(0, n["n0"]) == 0
     assert res.depth_of(0, n["n1"]) == 1
     assert res.depth_of(1, n["n0"]) == -1
+    assert res.visited(1, 0).tolist() == [n["n10"]]     # isolated seed: no local id, V_0 = {seed}
+    assert res.depth_of(1, n["n10"]) == 0 and res.depth_of(0, n["n10"]) == -1
+    assert res.counts()[1].tolist() == [1] + [0] * (res.n_levels - 1)
     with pytest.raises(HGXError):                    # not owned by that part
         res.parts[1 - n["n0"] % 2].depth_of(0, n["n0"])
     with pytest.raises(HGXError):

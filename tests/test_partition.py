@@ -20,7 +20,7 @@ def _check_part(g, NP, p, d):
     off, tg = np.asarray(g["tgt_off"]), np.asarray(g["tgt_idx"])
     lt = np.zeros(len(g["link_atom"]), np.int32) if g.get("link_type") is None else np.asarray(g["link_type"])
     local_rows = [r for r in range(len(g["link_atom"])) if any(int(t) % NP == p for t in tg[off[r]:off[r + 1]])]
-    atoms = set(range(p, A, NP))
+    atoms = set()                                  # owned atoms without incidence get no local id
     for r in local_rows:
         atoms.update(int(t) for t in tg[off[r]:off[r + 1]])
     assert d["l2g"].tolist() == sorted(atoms)                  # local ids follow global order
@@ -47,7 +47,8 @@ def test_shard_tables_random_graph(NP):
         _check_part(g, NP, p, d)
         owned.extend(int(a) for a in d["l2g"] if a % NP == p)
         assert s.n_owned == len(range(p, g["num_atoms"], NP))
-    assert sorted(owned) == list(range(g["num_atoms"]))       # the parts own every atom exactly once
+    targets = sorted(set(np.asarray(g["tgt_idx"]).tolist()))
+    assert sorted(owned) == targets                # every atom with incidence is owned exactly once
     # every link is held by each part owning one of its targets (replication <= arity)
     row_of = {int(a): r for r, a in enumerate(g["link_atom"])}
     held = np.zeros(len(g["link_atom"]), np.int64)
@@ -105,7 +106,7 @@ def _rank_main(rank, world, port, q):
     dist.all_gather_object(views, mine)
     if rank == 0:
         owned = sorted(a for v in views for a in v["owned"])
-        ok = owned == list(range(g["num_atoms"]))
+        ok = owned == sorted(set(g["tgt_idx"].tolist()))
         # rank p's ghosts owned by r == atoms of r that p must receive rows for
         for p in range(world):
             for r in range(world):
