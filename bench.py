@@ -131,17 +131,20 @@ def _kernel_roof(stats_list):
 
 
 def run_config4(args, ctx, barrier_sync, result):
-    """Config 4 (1B incidences): (a) replicated -- every GPU holds the whole snapshot (compacted
-    one-part shard) and traverses 1024/N of the sources; (b) partitioned -- the snapshot is
-    hash-partitioned over the N GPUs and all 1024 sources run together with one RCCL all-to-all per
-    level.  Both are strong scaling (fixed graph, fixed 1024 sources).  Fills result[...] in place
-    so a watchdog can still report what finished."""
+    """Config 4 (1B incidences) in its two multi-GPU forms:
+      replicated  -- every GPU holds the whole snapshot (compacted one-part shard, ~16 GB of CSR)
+                     and runs its own 1024-source batch (weak scaling: throughput of the batch
+                     workload, no data-path collective);
+      partitioned -- the snapshot is hash-partitioned over the N GPUs (owner = atom % N) and the
+                     same 1024 sources run together, one RCCL all-to-all of ghost rows per level
+                     (strong scaling; the path for graphs beyond one GPU's 288 GB).
+    Fills result[...] in place so a watchdog can still report what finished."""
+    from hypergraphdb_amd import dist as hdist
     from hypergraphdb_amd import synth
     from hypergraphdb_amd.partition import RcclComm, Shard, ShardSnapshot, pbfs_batch, pbfs_batch_group
     rank, world, local = ctx.rank, ctx.world, ctx.device
     t0 = time.time()
     g = synth.config4(scale=args.c4_scale, n_sources=args.sources)
-    seeds = g["seeds"]
     log(f"rank {rank}: config4 generated in {time.time() - t0:.1f}s: A={g['num_atoms']} P={len(g['tgt_idx'])}")
     wl = (f"config4: 100M nodes / 200M links (1.0B incidences), Chung-Lu gamma 2.1, {args.sources}-source BFS "
           f"depth {args.depth}" if args.c4_scale == 1.0 else f"config4 at scale {args.c4_scale}")
@@ -157,7 +160,7 @@ def run_config4(args, ctx, barrier_sync, result):
         barrier_sync()
         return ctx.max(time.perf_counter() - t1), st
 
-    # (a) replicated snapshot, sources split over the ranks
+    # replicated snapshot, one 1024-source batch per GPU
     t0 = time.time()
     sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], 1, 0)
     snap = ShardSnapshot(sh, local)
@@ -165,7 +168,7 @@ def run_config4(args, ctx, barrier_sync, result):
         f"{time.time() - t0:.1f}s")
     sh.close()
     snap.set_timing(True)
-    mine = np.array_split(seeds, world)[rank]
+    mine = hdist.rank_sources(g, args.sources, rank)
     for _ in range(max(args.warmup, 1)):
         r = pbfs_batch_group([snap], mine, args.depth)
         acct = r.parts[0].stats(accounting=True)
@@ -173,17 +176,19 @@ def run_config4(args, ctx, barrier_sync, result):
     dt, st = timed(lambda: pbfs_batch_group([snap], mine, args.depth).parts[0], args.steps)
     edges = ctx.sum(acct["traversed_edges"] * args.steps)
     result["replicated"] = {
-        "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
-        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl,
-        "parallelism": f"snapshot replicated, {args.sources} sources split over {world} GPU(s)",
+        "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "weak",
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl, "n_gpus": world,
+        "parallelism": f"snapshot replicated on {world} GPU(s), {args.sources} sources per GPU",
         "traversed_edges_per_step": edges / args.steps, "roofline": _kernel_roof(st)}
     log(f"rank {rank}: config4 replicated {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step")
     snap.close()
     del snap
     if world == 1:
-        result["partitioned"] = dict(result["replicated"], parallelism="one part (no exchange)")
+        result["partitioned"] = dict(result["replicated"], scaling="strong",
+                                     parallelism="one part: the hash partition degenerates to the replica")
         return
-    # (b) hash partition over the ranks, RCCL all-to-all per level
+    # hash partition over the ranks, RCCL all-to-all per level, the same 1024 sources everywhere
+    seeds = g["seeds"]
     t0 = time.time()
     sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world, rank)
     info = {"local_atoms": sh.n_local, "local_links": sh.n_links, "local_pins": sh.n_pins}
@@ -203,7 +208,7 @@ def run_config4(args, ctx, barrier_sync, result):
     xms = ctx.max(sum(s["ms_exchange"] for s in st) / args.steps)
     result["partitioned"] = {
         "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
-        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl, "n_gpus": world,
         "parallelism": f"hash partition over {world} GPUs (owner = atom % {world}), RCCL all-to-all per level",
         "exchange_bytes_per_step": xbytes, "exchange_ms_per_step": round(xms, 3),
         "rank0_part": info, "roofline": _kernel_roof(st)}
@@ -211,6 +216,74 @@ def run_config4(args, ctx, barrier_sync, result):
         f"exchange {xbytes / 1e9:.2f} GB/step")
     comm.close()
     snap.close()
+
+
+def run_config5(args, ctx, barrier_sync):
+    """Config 5: hg.subsumed(G) / hg.subsumes(S) closures (unbounded BFS over HGSubsumes links only,
+    C/query/cond2qry/ToQueryMap.java:282-370) for 1024 classes of a 5M-class ontology, both
+    directions in one step.  Weak scaling: every GPU runs its own 1024 classes."""
+    import hypergraphdb_amd as H
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, synth
+    rank, world = ctx.rank, ctx.world
+    t0 = time.time()
+    g = synth.config5(scale=args.c5_scale, n_sources=args.sources)
+    if rank > 0:
+        g["seeds"] = synth.permutation_prefix(g["n_nodes"], args.sources, 47 + 1000 * rank)
+    snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"],
+                                device=ctx.device)
+    snap.set_timing(True)
+    T = g["subsumes_type"]
+    gens = [DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev) for rev in (False, True)]
+    log(f"rank {rank}: config5 ({g['n_nodes']} classes, {len(g['link_atom'])} links) ready in {time.time() - t0:.1f}s")
+    trav, closure = 0.0, 0
+    for _ in range(max(args.warmup, 1)):
+        for gen in gens:
+            r = H.bfs_batch(snap, g["seeds"], None, gen)
+            st = r.stats(accounting=True)
+            trav += st["traversed_edges"]
+            closure += int(r.counts()[:, 1:].sum())
+            r.close()
+    trav /= max(args.warmup, 1)
+    closure //= max(args.warmup, 1)
+    barrier_sync()
+    t1 = time.perf_counter()
+    sts = []
+    for _ in range(args.steps):
+        for gen in gens:
+            r = H.bfs_batch(snap, g["seeds"], None, gen)
+            sts.append(r.stats(accounting=False))
+            r.close()
+    barrier_sync()
+    dt = ctx.max(time.perf_counter() - t1)
+    edges = ctx.sum(trav * args.steps)
+    out = {"metric": "hyperedge TEPS (subsumption closures)", "value": edges / dt, "unit": "TEPS",
+           "closures_per_s": ctx.sum(2 * len(g["seeds"]) * args.steps) / dt, "scaling": "weak",
+           "ms_per_step": round(dt / args.steps * 1e3, 3), "levels": max(s["n_levels_expanded"] for s in sts),
+           "closure_atoms_per_step": closure,
+           "workload": (f"config5: {g['n_nodes']} classes, HGSubsumes DAG + noise links, {len(g['seeds'])} classes x "
+                        "{subsumed, subsumes}, unbounded depth"),
+           "roofline": _kernel_roof(sts)}
+    log(f"rank {rank}: config5 {out['value']:.3e} TEPS, {out['closures_per_s']:.1f} closures/s, "
+        f"{out['ms_per_step']} ms/step, {out['levels']} levels")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ctypes import OracleGraph, algen
+        threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+        tm, n, tr, el = {}, 0, 0, 0.0
+        for rev in (False, True):
+            batch = g["seeds"][: 4 * threads]
+            _, t_ = orc.bfs_many(batch, -1, 4096, algen(T, False, True, rev, False), nthreads=threads,
+                                 time_budget_s=args.cpu_budget / 2, timing=tm)
+            tr += int(t_.sum())
+            el += tm["elapsed_s"]
+            n += len(batch)
+        out["cpu_baseline"] = {"value": tr / el, "unit": "TEPS", "cores": threads, "kind": "port",
+                               "sample": f"{n} closures (C restatement of the subsumption BFS), {el:.1f}s",
+                               "seconds": round(el, 2)}
+        del orc
+    snap.close()
+    return out
 
 
 def main():
@@ -225,6 +298,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work per metric")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (1B incidences) legs")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 subsumption leg")
+    ap.add_argument("--c5-scale", type=float, default=1.0, help="fraction of the config-5 size")
     ap.add_argument("--c4-scale", type=float, default=1.0, help="fraction of the config-4 size")
     ap.add_argument("--c4-timeout", type=float, default=420.0,
                     help="seconds after which the config-4 legs are abandoned (the line is still printed)")
@@ -339,6 +414,11 @@ def main():
             pattern["cpu_baseline"] = cpu_query_baseline(g3, Q, args.cpu_budget)
             log(f"cpu pattern baseline {pattern['cpu_baseline']['value']:.1f} q/s")
 
+    # ---------------- config 5: subsumption closures ----------------
+    sub = None
+    if not args.no_config5:
+        sub = run_config5(args, ctx, barrier_sync)
+
     line = None
     if rank == 0:
         line = {
@@ -361,6 +441,7 @@ def main():
                             "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] > 0 else None}
                         for k, v in per_kernel.items()},
             "pattern": pattern,
+            "subsumption": sub,
         }
 
     # ---------------- config 4: 1B incidences, replicated vs hash-partitioned ----------------

@@ -120,6 +120,41 @@ template <int G> __device__ __forceinline__ u64 compress_groups(u64 b, int pos0)
     }
 }
 
+// Bitmap scans: a wave loads 64 consecutive words at once (one per lane) and visits only the
+// nonzero ones, so a sparse bitmap costs one coalesced load per 64 words instead of a serial
+// word-per-iteration loop.  body(word_index, word) runs wave-uniformly.
+template <class F>
+__device__ __forceinline__ void for_nonzero_words(const u64* __restrict__ bm, int64_t nwords, F body) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
+        const u64 x = base + lane < nwords ? bm[base + lane] : 0ull;
+        u64 m = __ballot(x != 0ull);
+        while (m) {
+            const int k = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            body(base + k, (u64)__shfl(x, k));
+        }
+    }
+}
+
+// For every set bit b of the wave-uniform word xw: op(b, w, payload of lane b) on W lanes
+// (w = 0..W-1), 64/W bits at a time.  The shuffle runs on every lane (a lane shuffling from an
+// inactive lane reads garbage on CDNA).
+template <class F>
+__device__ __forceinline__ void rows_of_word(u64 xw, int W, int32_t payload, F op) {
+    const int lane = threadIdx.x & 63, R = 64 / W, k = lane / W, wd = lane % W;
+    while (xw) {
+        u64 y = xw;
+        for (int i = 0; i < k && y; ++i) y &= y - 1ull;
+        const int b = y ? __ffsll((long long)y) - 1 : -1;
+        for (int i = 0; i < R && xw; ++i) xw &= xw - 1ull;
+        const int32_t pv = __shfl(payload, b < 0 ? 0 : b);
+        if (b >= 0) op(b, wd, pv);
+    }
+}
+
 // per-level counters (device): early stop + byte accounting
 enum Ctr {
     cActiveLinks = 0,   // lf rows written                                   (link gather)
@@ -134,7 +169,8 @@ enum Ctr {
     cDirRows,           // ordered modes: target rows re-read in the pull
     cNewDeg,            // sum of |inc(v)| over the new atoms (next level's push volume)
     cNewFull,           // atoms that became visited by every traversal
-    cNum = 12
+    cCand,              // frontier-push candidates finalised
+    cNum = 13
 };
 
 __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
@@ -599,25 +635,17 @@ __global__ void __launch_bounds__(256) hgx_frontier_links_heavy(const HeavyChunk
 __global__ void __launch_bounds__(256) hgx_push_zero(int64_t A, int W, const u64* __restrict__ cand,
                                                      const u64* __restrict__ full, u64* __restrict__ lvl_next) {
     const int lane = threadIdx.x & 63;
+    const int64_t nwords = (A + 63) / 64;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const int per = (64 / W) < 8 ? (64 / W) : 8;   // atoms zeroed per wave instruction
-    for (int64_t w = wave; w * 64 < A; w += nwave) {
-        u64 x = cand[w] & ~full[w];
-        while (x) {
-            int64_t t[8];
-            int n = 0;
-            while (x && n < per) {
-                t[n++] = w * 64 + __ffsll((long long)x) - 1;
-                x &= x - 1;
-            }
-            const int k = lane / W;
-            if (k < n) {
-                int64_t tk = t[0];
-                for (int q = 1; q < 8; ++q)
-                    if (q == k) tk = t[q];
-                lvl_next[tk * W + (lane % W)] = 0ull;
-            }
+    for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
+        const u64 x = base + lane < nwords ? cand[base + lane] & ~full[base + lane] : 0ull;
+        u64 m = __ballot(x != 0ull);
+        while (m) {
+            const int k = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int64_t t0 = (base + k) * 64;
+            rows_of_word((u64)__shfl(x, k), W, 0, [&](int b, int w, int32_t) { lvl_next[(t0 + b) * W + w] = 0ull; });
         }
     }
 }
@@ -656,50 +684,299 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t nwords = (A + 63) / 64;
     const typename V::T FULL = full_part<W>(fm, sub);
     u64 n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
-    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
-        const u64 full_w = full[tile];
-        const u64 cw = cand[tile] & ~full_w;
-        if (cw == 0) {
-            if (lane == 0) fa_next[tile] = 0;
-            continue;
-        }
-        const u64 ever_w = ever[tile];
-        u64 new_w = 0, fullnew_w = 0;
-        for (int j = 0; j < G; ++j) {
-            const int pos = j * PW + g;
-            const int64_t t = tile * 64 + pos;
-            bool isnew = false, becomes_full = false;
-            if (t < A && ((cw >> pos) & 1ull)) {
-                const typename V::T acc = V::ld(lvl_next + t * W + sub * WPL);
-                if (group_any<G>(V::nz(acc))) {
-                    const bool ev = (ever_w >> pos) & 1ull;
-                    const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
-                    n_vis += ev;
-                    const typename V::T nw = acc & ~old;
-                    if (group_any<G>(V::nz(nw))) {
-                        V::st(lvl_next + t * W + sub * WPL, nw);
-                        V::st(vis + t * W + sub * WPL, old | nw);
-                        isnew = true;
-                        becomes_full = group_all<G>(V::eq(old | nw, FULL));
-                        if (sub == 0) n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+    for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
+        const bool in = base + lane < nwords;
+        const u64 myfull = in ? full[base + lane] : 0ull;
+        const u64 mycw = in ? cand[base + lane] & ~myfull : 0ull;
+        if (in && mycw == 0ull) fa_next[base + lane] = 0ull;   // no candidate: empty frontier word
+        u64 m = __ballot(mycw != 0ull);
+        while (m) {
+            const int kk = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int64_t tile = base + kk;
+            const u64 cw = __shfl(mycw, kk), full_w = __shfl(myfull, kk);
+            const u64 ever_w = ever[tile];
+            u64 new_w = 0, fullnew_w = 0;
+            for (int j = 0; j < G; ++j) {
+                const int pos = j * PW + g;
+                const int64_t t = tile * 64 + pos;
+                bool isnew = false, becomes_full = false;
+                if (t < A && ((cw >> pos) & 1ull)) {
+                    const typename V::T acc = V::ld(lvl_next + t * W + sub * WPL);
+                    if (group_any<G>(V::nz(acc))) {
+                        const bool ev = (ever_w >> pos) & 1ull;
+                        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+                        n_vis += ev;
+                        const typename V::T nw = acc & ~old;
+                        if (group_any<G>(V::nz(nw))) {
+                            V::st(lvl_next + t * W + sub * WPL, nw);
+                            V::st(vis + t * W + sub * WPL, old | nw);
+                            isnew = true;
+                            becomes_full = group_all<G>(V::eq(old | nw, FULL));
+                            if (sub == 0) n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+                        }
                     }
                 }
+                new_w |= compress_groups<G>(__ballot(isnew), j * PW);
+                fullnew_w |= compress_groups<G>(__ballot(becomes_full), j * PW);
             }
-            new_w |= compress_groups<G>(__ballot(isnew), j * PW);
-            fullnew_w |= compress_groups<G>(__ballot(becomes_full), j * PW);
-        }
-        if (lane == 0) {
-            fa_next[tile] = new_w;
-            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
-            if (fullnew_w) full[tile] = full_w | fullnew_w;
-            n_new += __popcll(new_w);
-            n_full += __popcll(fullnew_w);
+            if (lane == 0) {
+                fa_next[tile] = new_w;
+                if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
+                if (fullnew_w) full[tile] = full_w | fullnew_w;
+                n_new += __popcll(new_w);
+                n_full += __popcll(fullnew_w);
+            }
         }
     }
     wave_add_sh(ctr + cNewFull, n_full);
     if (sub != 0) n_vis = 0;
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
+}
+
+// ---- sparse levels, ordered modes (hg.subsumed / hg.subsumes): frontier-driven push ------------
+// For every frontier atom v and incident (typed) link L, the targets DefaultALGenerator yields from
+// v by position (FTargetSetIterator / BTargetSetIterator,
+// C/algorithms/DefaultALGenerator.java:121-285) receive v's row.  Pass 0 marks the candidates,
+// pass 1 ORs the rows into their (zeroed) next-level rows with 64-bit atomics; hgx_push_finalize
+// then applies ~vis.  Work = sum over the frontier of |inc(v)| * arity, independent of |A| -- a
+// hub reached as a candidate is never scanned (the pull would scan all of its incidence row).
+template <int MODE>
+__device__ __forceinline__ bool yields(int pos, int fv, int lv) {
+    if constexpr (MODE == kSym) return true;   // every co-target (t != v is checked by the caller)
+    else if constexpr (MODE == kAfterFirst) return pos > fv;
+    else if constexpr (MODE == kBeforeFirst) return pos < fv;
+    else if constexpr (MODE == kBeforeLast) return pos < lv;
+    else return pos > lv;   // kAfterLast
+}
+
+// Per-wave LDS scratch of the frontier push: the yielded targets of one position step and the
+// nonzero words of the pushing atom's row.
+struct OPushLds {
+    int32_t tgt[64];
+    int32_t widx[16];
+    u64 wval[16];
+};
+
+// Links [start, hi) of frontier atom v (wave-uniform), lane l taking start + l, start + l + step, ...
+// Each lane reads its link's target row; position by position the wave ballots the yielded
+// targets and spreads the (target, nonzero word of v's row) pairs over the lanes: one 64-bit
+// atomicOr into the zero-invariant accumulator per pair and word, skipped when the bits are
+// already there (hub targets are hit by many pairs).  The first pair to reach a target sets its
+// candidate bit and appends it to the candidate list of the finalise.
+template <int W, int MODE>
+__device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi, int64_t step,
+                                            const int32_t* __restrict__ inc_row,
+                                            const int32_t* __restrict__ inc_type, int32_t want_type,
+                                            const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+                                            int nnz, OPushLds& sh, const u64* __restrict__ full,
+                                            u64* __restrict__ cand, int32_t* __restrict__ clist,
+                                            u64* __restrict__ n_clist, u64* __restrict__ acc, u64& n_links,
+                                            u64& n_pins, u64& n_pairs) {
+    const int lane = threadIdx.x & 63;
+    const u64 lt = (1ull << lane) - 1ull;
+    for (int64_t i0 = start; i0 < hi; i0 += step) {   // i0 is wave-uniform
+        const int64_t i = i0 + lane;
+        const bool have = i < hi && (want_type < 0 || inc_type[i] == want_type);
+        int64_t b = 0;
+        int n = 0, fv = -1, lv = -1;
+        if (have) {
+            const int32_t L = inc_row[i];
+            b = tgt_off[L];
+            n = (int)(tgt_off[L + 1] - b);
+            for (int p = 0; p < n; ++p)
+                if (tgt_idx[b + p] == v) {
+                    if (fv < 0) fv = p;
+                    lv = p;
+                }
+            ++n_links;
+            n_pins += (u64)n;
+        }
+        int nmax = n;
+        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        for (int p = 0; p < nmax; ++p) {
+            const int32_t t = p < n ? tgt_idx[b + p] : -1;
+            const bool elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
+            const u64 m = __ballot(elig);
+            if (m == 0ull) continue;
+            n_pairs += elig;
+            if (elig) sh.tgt[__popcll(m & lt)] = t;
+            __builtin_amdgcn_wave_barrier();
+            const int total = __popcll(m) * nnz;
+            for (int q0 = 0; q0 < total; q0 += 64) {   // wave-uniform trip count
+                const int q = q0 + lane;
+                bool fresh = false;
+                int32_t ts = 0;
+                if (q < total) {
+                    const int pr = q / nnz, wi = q - pr * nnz;
+                    ts = sh.tgt[pr];
+                    u64* a = acc + (int64_t)ts * W + sh.widx[wi];
+                    const u64 val = sh.wval[wi];
+                    if ((*a & val) != val) atomicOr(a, val);
+                    if (wi == 0) {
+                        const u64 cb = 1ull << (ts & 63);
+                        if (!(cand[ts >> 6] & cb)) fresh = !(atomicOr(&cand[ts >> 6], cb) & cb);
+                    }
+                }
+                const u64 fm = __ballot(fresh);
+                if (fm) {
+                    const int leader = __ffsll((long long)fm) - 1;
+                    u64 base = 0;
+                    if (lane == leader) base = atomicAdd(n_clist, (u64)__popcll(fm));
+                    base = __shfl(base, leader);
+                    if (fresh) clist[base + __popcll(fm & lt)] = ts;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// The nonzero words of v's row into the wave's LDS table; returns their count (wave-uniform).
+template <int W>
+__device__ __forceinline__ int row_words(const u64* __restrict__ lvl, int64_t v, OPushLds& sh) {
+    const int lane = threadIdx.x & 63;
+    const u64 x = lane < W ? lvl[v * W + lane] : 0ull;
+    const u64 nz = __ballot(x != 0ull);
+    if (x != 0ull) {
+        const int r = __popcll(nz & ((1ull << lane) - 1ull));
+        sh.widx[r] = lane;
+        sh.wval[r] = x;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return __popcll(nz);
+}
+
+// Light frontier atoms (0 < deg <= kHeavyDegree) appended to a list (order-free), so the push
+// kernels give one wave per atom whatever the bitmap's sparsity.
+__global__ void __launch_bounds__(256) hgx_frontier_list(int64_t A, const u64* __restrict__ fa,
+                                                         const int64_t* __restrict__ inc_off,
+                                                         int32_t* __restrict__ list, u64* __restrict__ n_list) {
+    const int lane = threadIdx.x & 63;
+    for_nonzero_words(fa, (A + 63) / 64, [&](int64_t w, u64 x) {
+        const int64_t v = w * 64 + lane;
+        bool take = (x >> lane) & 1ull;
+        if (take) {
+            const int64_t d = inc_off[v + 1] - inc_off[v];
+            take = d > 0 && d <= kHeavyDegree;
+        }
+        const u64 m = __ballot(take);
+        if (m == 0ull) return;
+        u64 base = 0;
+        if (lane == 0) base = atomicAdd(n_list, (u64)__popcll(m));
+        base = __shfl(base, 0);
+        if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)v;
+    });
+}
+
+template <int W, int MODE>
+__global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ list, const u64* __restrict__ n_list,
+                                                 const int64_t* __restrict__ inc_off,
+                                                 const int32_t* __restrict__ inc_row,
+                                                 const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                 const int64_t* __restrict__ tgt_off,
+                                                 const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
+                                                 const u64* __restrict__ full, u64* __restrict__ cand,
+                                                 int32_t* __restrict__ clist, u64* __restrict__ n_clist,
+                                                 u64* __restrict__ acc, u64* __restrict__ ctr) {
+    __shared__ OPushLds lds[4];
+    OPushLds& sh = lds[threadIdx.x >> 6];
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t n = (int64_t)*n_list;
+    u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    for (int64_t k = wave; k < n; k += nwave) {
+        const int32_t v = list[k];
+        const int nnz = row_words<W>(lvl, v, sh);
+        if (nnz == 0) continue;
+        opush_links<W, MODE>(v, inc_off[v], inc_off[v + 1], 64, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
+                             sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs);
+    }
+    wave_add_sh(ctr + cActiveLinks, n_links);
+    wave_add_sh(ctr + cActivePins, n_pins);
+    wave_add_sh(ctr + cIncLight, n_pairs);
+}
+
+template <int W, int MODE>
+__global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restrict__ chunks,
+                                                       const u64* __restrict__ fa,
+                                                       const int32_t* __restrict__ inc_row,
+                                                       const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                       const int64_t* __restrict__ tgt_off,
+                                                       const int32_t* __restrict__ tgt_idx,
+                                                       const u64* __restrict__ lvl, const u64* __restrict__ full,
+                                                       u64* __restrict__ cand, int32_t* __restrict__ clist,
+                                                       u64* __restrict__ n_clist, u64* __restrict__ acc,
+                                                       u64* __restrict__ ctr) {
+    __shared__ OPushLds lds[4];
+    const HeavyChunk c = chunks[blockIdx.x];
+    if (!bit(fa, c.atom)) return;   // block-uniform
+    const int wib = threadIdx.x >> 6;
+    OPushLds& sh = lds[wib];
+    const int nnz = row_words<W>(lvl, c.atom, sh);
+    if (nnz == 0) return;   // the same row for every wave of the block
+    u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    opush_links<W, MODE>(c.atom, c.beg + wib * 64, c.end, 256, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
+                         sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs);
+    wave_add_sh(ctr + cActiveLinks, n_links);
+    wave_add_sh(ctr + cActivePins, n_pins);
+    wave_add_sh(ctr + cIncLight, n_pairs);
+}
+
+// Finalise the candidates of a push level: new = acc & ~vis, the accumulator row is re-zeroed.
+// One G-lane group per candidate; fa_next (cleared beforehand) / ever / full bits by atomics.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __restrict__ clist,
+                                                              const u64* __restrict__ n_clist,
+                                                              const int64_t* __restrict__ inc_off,
+                                                              u64* __restrict__ acc, u64* __restrict__ vis,
+                                                              u64* __restrict__ ever, u64* __restrict__ full,
+                                                              u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                              u64* __restrict__ ctr, FullMask fm) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    typedef Vec<WPL> V;
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    const int64_t n = (int64_t)*n_clist;
+    u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    for (int64_t k0 = grp - (grp % (64 / G)); k0 < n; k0 += ngrp) {   // wave-uniform trip count
+        const int64_t k = k0 + (grp % (64 / G));
+        const bool valid = k < n;
+        const int64_t t = valid ? clist[k] : 0;
+        typename V::T a = valid ? V::ld(acc + t * W + sub * WPL) : V::zero();
+        if (valid) V::st(acc + t * W + sub * WPL, V::zero());
+        const bool ev = valid && bit(ever, t);
+        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const typename V::T nw = a & ~old;
+        const bool isnew = group_any<G>(V::nz(nw));
+        const bool becomes_full = group_all<G>(V::eq(old | nw, FULL));
+        if (valid && isnew) {
+            V::st(lvl_next + t * W + sub * WPL, nw);
+            V::st(vis + t * W + sub * WPL, old | nw);
+            if (sub == 0) {
+                set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (becomes_full) set_bit(full, t);
+                ++n_new;
+                n_full += becomes_full;
+                n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+            }
+        }
+        if (valid && sub == 0) {
+            ++n_cand;
+            n_vis += ev;
+        }
+    }
+    wave_add_sh(ctr + cCand, n_cand);
+    wave_add_sh(ctr + cNewFull, n_full);
     wave_add_sh(ctr + cVisLight, n_vis);
     wave_add_sh(ctr + cNewLight, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
@@ -1208,6 +1485,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const bool sparse_ok = (g->bfs_flags & 8) != 0;
     u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
     u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
+    const size_t flist_bytes = sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1);
+    int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
+    int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
     u64 push_volume = 0;
     if (sparse_ok) {
         u64* dv = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock;   // scratch slot
@@ -1229,6 +1509,49 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64* fa_next = (u64*)g->alloc(bm_bytes);   // every word written by hgx_atom_pull
         u64* c = ctr + (size_t)d * kCtrBlock;
         const bool sparse = sparse_ok && push_volume < sparse_limit;
+        int lflags = g->bfs_flags;
+        if ((lflags & 16) && (int64_t)full_total * 16 < A) lflags &= ~4;   // adaptive full skip
+        const bool opush = sparse && (MODE != kSym || (lflags & 32));
+        if (opush) {
+            // frontier-driven push (mark candidates, zero their rows, OR rows, finalise): the ordered
+            // modes always, the symmetric mode with HGX_OPT_BFS_FLAGS bit 5
+            Events e2 = tm.start(kKindPull, d);
+            if (!g->zacc_clean || g->zacc_bytes < row_bytes) {   // (re)establish the all-zero accumulator
+                if (g->zacc_bytes < row_bytes) {
+                    if (g->zacc) HGX_HIP(hipFree(g->zacc));
+                    g->zacc = nullptr;
+                    g->zacc_bytes = 0;
+                    HGX_HIP(hipMalloc(&g->zacc, row_bytes));
+                    g->zacc_bytes = row_bytes;
+                }
+                HGX_HIP(hipMemsetAsync(g->zacc, 0, g->zacc_bytes, s));
+            }
+            g->zacc_clean = false;   // until this level's finalise has run
+            u64* acc = (u64*)g->zacc;
+            HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
+            HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
+            u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slots
+            u64* n_clist = n_list + 1;
+            HGX_HIP(hipMemsetAsync(n_list, 0, 2 * sizeof(u64), s));
+            const int fgrid = grid_for(ceil_div(A, 64) * 64, 256, 4096);
+            hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, flist, n_list);
+            HGX_CHECK_LAUNCH();
+            const int lgrid = 2048;   // 8192 waves, grid-stride over the frontier list
+            hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(flist, n_list, g->inc_off, g->inc_row, g->inc_type, want_type,
+                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, clist, n_clist, acc, c);
+            HGX_CHECK_LAUNCH();
+            if (g->n_chunks > 0) {
+                hgx_opush_heavy<W, MODE><<<(unsigned)g->n_chunks, 256, 0, s>>>(
+                    g->chunks, fa, g->inc_row, g->inc_type, want_type, g->tgt_off, g->tgt_idx, lvl, full, cand, clist,
+                    n_clist, acc, c);
+                HGX_CHECK_LAUNCH();
+            }
+            hgx_push_finalize_list<W><<<4096, 256, 0, s>>>(clist, n_clist, g->inc_off, acc, vis, ever, full, lvl_next,
+                                                           fa_next, c, fm);
+            HGX_CHECK_LAUNCH();
+            g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
+            tm.stop(e2);
+        } else {
         if (sparse) {
             Events e0 = tm.start(kKindGather, d);
             HGX_HIP(hipMemsetAsync(lcand, 0, la_bytes, s));
@@ -1245,8 +1568,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }
         u64* lc = sparse ? lcand : nullptr;
         u64* cd = sparse ? cand : nullptr;
-        int lflags = g->bfs_flags;
-        if ((lflags & 16) && (int64_t)full_total * 16 < A) lflags &= ~4;   // adaptive full skip
 
         Events e1 = tm.start(kKindGather, d);
         hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
@@ -1287,6 +1608,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             tm.stop(e4);
         }
         }
+        }   // not an ordered push level
         u64 new_global = 0, part_push = 0;
         if (ex) {
             Events e5 = tm.start(kKindExchange, d);
@@ -1304,7 +1626,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             h_new[cNewDeg] = part_push;
         }
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
-        level_ctr.back()[cDirRows] = sparse ? 1 : 0;   // (host-side) mode of this level
+        level_ctr.back()[cDirRows] = sparse ? (opush ? 2 : 1) : 0;   // (host-side) kind of this level
         push_volume = h_new[cNewDeg];
         full_total += h_new[cNewFull];
         if (h_new[cNewAtoms] == 0) {
@@ -1324,6 +1646,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     g->release(la, la_bytes);
     if (lcand) g->release(lcand, la_bytes);
     if (cand) g->release(cand, bm_bytes);
+    if (flist) g->release(flist, flist_bytes);
+    if (clist) g->release(clist, flist_bytes);
     g->release(ctr, sizeof(u64) * kCtrBlock * max_levels_cap);
     g->release(d_atoms, sizeof(int32_t) * seed_atoms.size());
     g->release(d_rows, sizeof(u64) * seed_rows.size());
@@ -1526,14 +1850,22 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             const bool sparse_level = c[cDirRows] != 0;
             const double scan_links = sparse_level ? (double)c[cActiveLinks] : (double)M;
             const double scan_pins = sparse_level ? (double)c[cActivePins] : (double)P;
-            const double b_gather = 8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) +
+            double b_gather = 8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) +
                                     A / 4.0 + rowb * c[cActivePins] +
                                     (mode == kSym ? rowb * c[cActiveLinks] : 0.0) + M / 8.0;
             // hgx_atom_pull: inc_off + light inc_row + la bitmap + pulled rows + vis reads + lvl/vis writes
             //                + ever/full/fa_next words (sparse levels: candidate words + pushed rows)
-            const double b_pull = (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) + M / 8.0 +
+            double b_pull = (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) + M / 8.0 +
                                   rowb * c[cIncLight] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] +
                                   3.0 * A / 8.0;
+            const bool opush_level = c[cDirRows] == 2;
+            if (opush_level) {   // frontier push: no gather; two frontier passes + finalise
+                b_gather = 0.0;
+                // frontier scan + links (inc_row, inc_type, tgt_off pair) + pins + one word RMW per pair
+                // + candidates (acc read + re-zero) + vis reads + lvl/vis writes + cleared bitmaps
+                b_pull = 8.0 * (A / 64.0) + 24.0 * c[cActiveLinks] + 4.0 * c[cActivePins] + 16.0 * c[cIncLight] +
+                         2.0 * rowb * c[cCand] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] + 2.0 * A / 8.0;
+            }
             r->stats.bytes_kernel[HGX_K_LINK_GATHER] += b_gather;
             r->stats.bytes_kernel[HGX_K_ATOM_PULL] += b_pull;
             double b_heavy = 0, b_hub = 0;
@@ -1548,9 +1880,9 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             if (d < 64) {
                 for (int k = 0; k < 8; ++k) r->stats.level_rows[d][k] += (int64_t)c[k];
                 r->stats.level_bytes[d] += b_gather + b_pull + b_heavy + b_hub;
-                r->stats.level_sparse[d] = sparse_level ? 1 : 0;
+                r->stats.level_sparse[d] = (int32_t)c[cDirRows];
             }
-            r->stats.launches[HGX_K_LINK_GATHER] += 1;
+            if (!opush_level) r->stats.launches[HGX_K_LINK_GATHER] += 1;
             r->stats.launches[HGX_K_ATOM_PULL] += 1;
             if (d < 64) r->stats.level_new[d] += (int64_t)c[cNewAtoms];
         }

@@ -121,9 +121,14 @@ struct hgx_graph {
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
-    int32_t bfs_flags = 0x1E;       // HGX_OPT_BFS_FLAGS (see hgx.h)
+    int32_t bfs_flags = 0x3E;       // HGX_OPT_BFS_FLAGS (see hgx.h)
     int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
+    // Frontier-push accumulator rows (A x W words), all zero between levels: each push level ORs
+    // into it and its finalise re-zeroes exactly the rows it consumed (no per-level clear).
+    uint64_t* zacc = nullptr;
+    size_t zacc_bytes = 0;
+    bool zacc_clean = false;
 
     int64_t A = 0, M = 0, P = 0, I = 0;
     int32_t* link_atom = nullptr;

@@ -110,7 +110,7 @@ typedef struct hgx_bfs_stats {
     double  level_ms[64];              /* device ms of all kernels of level d (timing enabled) */
     int64_t level_new[64];             /* atoms with a new bit at level d+1 (summed over batches) */
     double  level_bytes[64];           /* algorithmic bytes of all kernels of level d          */
-    int32_t level_sparse[64];          /* 1 if level d ran frontier-driven (push)              */
+    int32_t level_sparse[64];          /* level d ran 0 = dense, 1 = frontier links + lf push, 2 = frontier push */
     /* per level, summed over batches: [0] lf rows written, [1] frontier rows gathered,
      * [2] lf rows pulled (light), [3] vis rows read, [4] new light atoms, [5] lf rows pulled
      * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
@@ -139,8 +139,10 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *   HGX_OPT_BFS_FLAGS: bit 0 = gather early exit, bit 1 = pull early exit,
  *                      bit 2 = skip atoms / links already visited by every traversal,
  *                      bit 3 = frontier-driven sparse levels (direction optimisation),
- *                      bit 4 = apply bit 2 only once >= 1/16 of the atoms are fully visited.
- *                      Default 0x1E. */
+ *                      bit 4 = apply bit 2 only once >= 1/16 of the atoms are fully visited,
+ *                      bit 5 = sparse levels of the symmetric mode push from the frontier atoms
+ *                              (the ordered modes always do).
+ *                      Default 0x3E. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
  * (seeds are processed in chunks that fit; default 16 GiB). */
