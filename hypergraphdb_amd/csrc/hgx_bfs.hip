@@ -500,6 +500,253 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
     wave_add_sh(ctr + cNewDeg, n_newdeg);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Dense levels, W >= 8 (G >= 4 lanes per row): the same gather / pull as above, restructured for
+// memory-level parallelism.  The kernels above walk one row per G-lane group through a chain of
+// dependent loads (offsets -> ids -> bitmap probes -> mask rows), one step of the chain in flight
+// per group; here a wave first loads the offsets of all 64 rows of its tile (one coalesced load),
+// then the ids of every row of the tile, then every probe, then the mask rows -- G independent
+// loads in flight per lane at each stage.  Tiles with no work (e.g. the link atoms' zero-degree
+// rows) cost one load.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool WRITE_LF>
+__global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t* __restrict__ tgt_off,
+                                                        const int32_t* __restrict__ tgt_idx,
+                                                        const int32_t* __restrict__ link_type, int32_t want_type,
+                                                        const u64* __restrict__ fa, const u64* __restrict__ full,
+                                                        const u64* __restrict__ lvl, u64* __restrict__ lf,
+                                                        u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm,
+                                                        int flags) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
+    static_assert(G >= 4, "gather2 needs G >= 4");
+    typedef Vec<WPL> V;
+    const bool early = flags & 1, skip_full = flags & 4;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
+    const u64 gmask = (1ull << G) - 1ull;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_links = 0, n_pins = 0;
+    for (int64_t tile = wave; tile * 64 < M; tile += nwave) {
+        const int64_t Lme = tile * 64 + lane;
+        int64_t bme = 0;
+        int nme = 0;
+        if (Lme < M && (want_type < 0 || link_type[Lme] == want_type)) {
+            bme = tgt_off[Lme];
+            nme = (int)(tgt_off[Lme + 1] - bme);
+        }
+        int32_t v[G];
+        int n[G];
+        int64_t bb[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            bb[j] = __shfl(bme, j * PW + g);
+            n[j] = __shfl(nme, j * PW + g);
+            v[j] = sub < n[j] ? tgt_idx[bb[j] + sub] : -1;
+        }
+        unsigned pa = 0, pnf = 0;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            if (v[j] >= 0) {
+                if (bit(fa, v[j])) pa |= 1u << j;
+                if (!skip_full || !bit(full, v[j])) pnf |= 1u << j;
+            }
+        u64 word = 0;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t L = tile * 64 + j * PW + g;
+            unsigned ga = (unsigned)((__ballot((pa >> j) & 1u) >> base) & gmask);
+            const bool any_nf0 = ((__ballot((pnf >> j) & 1u) >> base) & gmask) != 0ull;
+            typename V::T acc = V::zero();
+            int nact = 0;
+            bool act = false;
+            if (n[j] <= G) {
+                if (any_nf0 && ga) {   // group-uniform
+                    typename V::T r[G];
+#pragma unroll
+                    for (int k = 0; k < G; ++k) {
+                        const int32_t vk = __shfl(v[j], base + k);
+                        r[k] = ((ga >> k) & 1u) ? V::ld(lvl + (int64_t)vk * W + sub * WPL) : V::zero();
+                    }
+#pragma unroll
+                    for (int k = 0; k < G; ++k) acc |= r[k];
+                }
+                nact = __popc(ga);
+                act = nact > 0 && any_nf0;
+            } else {   // a row longer than G (rare): full bits first, then the rows with early exit
+                const int64_t b = bb[j], e = b + n[j];
+                bool any_not_full = !skip_full;
+                for (int64_t p = b; p < e && !any_not_full; p += G) {
+                    const int64_t q = p + sub;
+                    const int32_t myv = q < e ? tgt_idx[q] : -1;
+                    any_not_full |= ((__ballot(myv >= 0 && !bit(full, myv)) >> base) & gmask) != 0ull;
+                }
+                for (int64_t p = b; p < e && any_not_full; p += G) {
+                    const int64_t q = p + sub;
+                    const int32_t myv = q < e ? tgt_idx[q] : -1;
+                    const unsigned g2 = (unsigned)((__ballot(myv >= 0 && bit(fa, myv)) >> base) & gmask);
+                    typename V::T r[G];
+#pragma unroll
+                    for (int k = 0; k < G; ++k) {
+                        const int32_t vk = __shfl(myv, base + k);
+                        r[k] = ((g2 >> k) & 1u) ? V::ld(lvl + (int64_t)vk * W + sub * WPL) : V::zero();
+                    }
+#pragma unroll
+                    for (int k = 0; k < G; ++k) acc |= r[k];
+                    nact += __popc(g2);
+                    if (early && p + G < e && group_all<G>(V::eq(acc, FULL))) break;
+                }
+                act = nact > 0 && any_not_full;
+            }
+            if (act) {
+                if (WRITE_LF) V::st(lf + L * W + sub * WPL, acc);
+                if (sub == 0) {
+                    ++n_links;
+                    n_pins += nact;
+                }
+            }
+            word |= compress_groups<G>(__ballot(act), j * PW);
+        }
+        if (lane == 0) la[tile] = word;
+    }
+    wave_add_sh(ctr + cActiveLinks, n_links);
+    wave_add_sh(ctr + cActivePins, n_pins);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* __restrict__ inc_off,
+                                                      const int32_t* __restrict__ inc_row,
+                                                      const u64* __restrict__ la, const u64* __restrict__ lf,
+                                                      u64* __restrict__ vis, u64* __restrict__ ever,
+                                                      u64* __restrict__ full, u64* __restrict__ lvl_next,
+                                                      u64* __restrict__ fa_next, u64* __restrict__ ctr, FullMask fm,
+                                                      int flags) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
+    constexpr int JB = G >= 8 ? 4 : G;   // atoms of a group interleaved at once (register budget)
+    static_assert(G >= 4, "pull2 needs G >= 4");
+    typedef Vec<WPL> V;
+    const bool early = flags & 2, skip_full = flags & 4;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
+    const u64 gmask = (1ull << G) - 1ull;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+        const u64 ever_w = ever[tile], full_w = full[tile];
+        const int64_t tme = tile * 64 + lane;
+        int64_t bme = 0;
+        int dme = 0;
+        if (tme < A && !(skip_full && ((full_w >> lane) & 1ull))) {
+            bme = inc_off[tme];
+            const int64_t d = inc_off[tme + 1] - bme;
+            dme = (d > 0 && d <= kHeavyDegree) ? (int)d : 0;
+        }
+        if (__ballot(dme > 0) == 0ull) {   // nothing to pull in this tile
+            if (lane == 0) fa_next[tile] = 0ull;
+            continue;
+        }
+        u64 new_w = 0, fullnew_w = 0;
+        for (int j0 = 0; j0 < G; j0 += JB) {
+            int64_t bj[JB];
+            int dj[JB], dmax = 0;
+            typename V::T acc[JB], old[JB];
+            bool hv[JB], done[JB];
+#pragma unroll
+            for (int jj = 0; jj < JB; ++jj) {
+                const int src = (j0 + jj) * PW + g;
+                bj[jj] = __shfl(bme, src);
+                dj[jj] = __shfl(dme, src);
+                acc[jj] = V::zero();
+                old[jj] = V::zero();
+                hv[jj] = false;
+                done[jj] = dj[jj] == 0;
+                dmax = max(dmax, dj[jj]);
+            }
+            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, __shfl_xor(dmax, off));
+            for (int c0 = 0; c0 < dmax; c0 += G) {   // wave-uniform
+                int32_t myL[JB];
+#pragma unroll
+                for (int jj = 0; jj < JB; ++jj)
+                    myL[jj] = (!done[jj] && c0 + sub < dj[jj]) ? inc_row[bj[jj] + c0 + sub] : -1;
+                unsigned pa = 0;
+#pragma unroll
+                for (int jj = 0; jj < JB; ++jj)
+                    if (myL[jj] >= 0 && bit(la, myL[jj])) pa |= 1u << jj;
+#pragma unroll
+                for (int jj = 0; jj < JB; ++jj) {
+                    const unsigned ga = (unsigned)((__ballot((pa >> jj) & 1u) >> base) & gmask);
+                    if (ga) {   // group-uniform
+                        typename V::T r[G];
+#pragma unroll
+                        for (int k = 0; k < G; ++k) {
+                            const int32_t Lk = __shfl(myL[jj], base + k);
+                            r[k] = ((ga >> k) & 1u) ? V::ld(lf + (int64_t)Lk * W + sub * WPL) : V::zero();
+                        }
+#pragma unroll
+                        for (int k = 0; k < G; ++k) acc[jj] |= r[k];
+                        n_inc += __popc(ga);
+                    }
+                    if (done[jj]) continue;   // group-uniform from here on
+                    const int64_t t = tile * 64 + (j0 + jj) * PW + g;
+                    if (early) {
+                        if (!hv[jj] && group_any<G>(V::nz(acc[jj]))) {
+                            if ((ever_w >> ((j0 + jj) * PW + g)) & 1ull) {
+                                old[jj] = V::ld(vis + t * W + sub * WPL);
+                                ++n_vis;
+                            }
+                            hv[jj] = true;
+                        }
+                        if (hv[jj] && c0 + G < dj[jj] && group_all<G>(V::eq(acc[jj] | old[jj], FULL))) done[jj] = true;
+                    }
+                    if (c0 + G >= dj[jj]) done[jj] = true;
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < JB; ++jj) {
+                const int pos = (j0 + jj) * PW + g;
+                const int64_t t = tile * 64 + pos;
+                bool isnew = false, becomes_full = false;
+                if (dj[jj] > 0) {   // group-uniform
+                    if (!hv[jj] && group_any<G>(V::nz(acc[jj]))) {
+                        if ((ever_w >> pos) & 1ull) {
+                            old[jj] = V::ld(vis + t * W + sub * WPL);
+                            ++n_vis;
+                        }
+                    }
+                    const typename V::T nw = acc[jj] & ~old[jj];
+                    if (group_any<G>(V::nz(nw))) {
+                        V::st(lvl_next + t * W + sub * WPL, nw);
+                        V::st(vis + t * W + sub * WPL, old[jj] | nw);
+                        isnew = true;
+                        becomes_full = group_all<G>(V::eq(old[jj] | nw, FULL));
+                        if (sub == 0) n_newdeg += (u64)dj[jj];
+                    }
+                }
+                new_w |= compress_groups<G>(__ballot(isnew), pos - g);
+                fullnew_w |= compress_groups<G>(__ballot(becomes_full), pos - g);
+            }
+        }
+        if (lane == 0) {
+            fa_next[tile] = new_w;
+            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
+            if (fullnew_w) full[tile] = full_w | fullnew_w;
+            n_new += __popcll(new_w);
+            n_full += __popcll(fullnew_w);
+        }
+    }
+    if (sub != 0) {
+        n_inc = 0;
+        n_vis = 0;
+    }
+    wave_add_sh(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cIncLight, n_inc);
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
+}
+
 // Heavy atoms: one workgroup per chunk of <= kChunkEntries incidence entries; groups OR their
 // share (stopping early once every traversal is covered), the block reduces through LDS and ORs
 // the chunk result into hubacc[slot].  Hubs already visited by every traversal exit at once.
@@ -1569,10 +1816,17 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64* lc = sparse ? lcand : nullptr;
         u64* cd = sparse ? cand : nullptr;
 
+        const bool v2 = Lay<W>::G >= 4 && !sparse && !(lflags & 64);   // MLP-restructured dense kernels
         Events e1 = tm.start(kKindGather, d);
-        hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
-                                                                      want_type, fa, full, lvl, lf, la, c, fm,
-                                                                      lflags, lc, cd);
+        if constexpr (Lay<W>::G >= 4) {
+            if (v2)
+                hgx_link_gather2<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
+                    M, g->tgt_off, g->tgt_idx, g->link_type, want_type, fa, full, lvl, lf, la, c, fm, lflags);
+        }
+        if (!v2)
+            hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
+                                                                          want_type, fa, full, lvl, lf, la, c, fm,
+                                                                          lflags, lc, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
         if (sparse && MODE == kSym) {
@@ -1589,9 +1843,15 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             tm.stop(e2);
         } else {
         Events e2 = tm.start(kKindPull, d);
-        hgx_atom_pull<W, MODE><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, g->tgt_off,
-                                                           g->tgt_idx, fa, lvl, vis, ever, full, lvl_next, fa_next, c,
-                                                           fm, lflags, cd);
+        if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
+            if (v2)
+                hgx_atom_pull2<W><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever, full,
+                                                              lvl_next, fa_next, c, fm, lflags);
+        }
+        if (!(v2 && MODE == kSym))
+            hgx_atom_pull<W, MODE><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, g->tgt_off,
+                                                               g->tgt_idx, fa, lvl, vis, ever, full, lvl_next,
+                                                               fa_next, c, fm, lflags, cd);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
         if (g->n_chunks > 0) {

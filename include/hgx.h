@@ -141,7 +141,9 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 3 = frontier-driven sparse levels (direction optimisation),
  *                      bit 4 = apply bit 2 only once >= 1/16 of the atoms are fully visited,
  *                      bit 5 = sparse levels of the symmetric mode push from the frontier atoms
- *                              (the ordered modes always do).
+ *                              (the ordered modes always do),
+ *                      bit 6 = keep the one-row-at-a-time dense kernels for >= 512 sources
+ *                              (A/B only; the default uses the tile-staged ones).
  *                      Default 0x3E. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
