@@ -126,6 +126,7 @@ struct hgx_graph {
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
     // Frontier-push accumulator rows (A x W words), all zero between levels: each push level ORs
     // into it and its finalise re-zeroes exactly the rows it consumed (no per-level clear).
+    std::vector<int64_t> inc_off_host;   // host copy of inc_off (pattern planning), made on first use
     uint64_t* zacc = nullptr;
     size_t zacc_bytes = 0;
     bool zacc_clean = false;

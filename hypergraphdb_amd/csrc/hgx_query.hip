@@ -41,36 +41,6 @@ __device__ __forceinline__ void wave_add_q(u64* ctr, u64 v) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
-__global__ void __launch_bounds__(256) hgx_q_plan(int32_t n, const int64_t* __restrict__ inc_off,
-                                                  const int32_t* __restrict__ q_nop,
-                                                  const int64_t* __restrict__ a_off, const int32_t* __restrict__ anchors,
-                                                  QPlan* __restrict__ plan, int32_t* __restrict__ nchunks) {
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    QPlan p{0, 0, 0, 0};
-    if (!q_nop[q]) {
-        int64_t best = -1;
-        for (int64_t k = a_off[q]; k < a_off[q + 1]; ++k) {
-            int32_t a = anchors[k];
-            int64_t d = inc_off[a + 1] - inc_off[a];
-            if (best < 0 || d < best) {   // first smallest (AndToQuery sorts ORA by size)
-                best = d;
-                p.beg = inc_off[a];
-                p.amin = (int32_t)(k - a_off[q]);
-            }
-        }
-        p.n = best < 0 ? 0 : best;
-    }
-    plan[q] = p;
-    nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
-}
-
-__global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_q) {
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    for (int32_t c = chunk_off[q]; c < chunk_off[q + 1]; ++c) chunk_q[c] = q;
-}
-
 // A wave per chunk of kQChunk candidates of one query (grid-stride over chunks; the counters are
 // summed in registers and added once per wave into sharded replicas).
 constexpr int kQShards = 16, kQStride = 16;
@@ -82,6 +52,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const int32_t* __restrict__ q_has_ordered, const int32_t* __restrict__ inc_row,
     const int32_t* __restrict__ inc_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
     int32_t* __restrict__ slots, int64_t* __restrict__ counts, u64* __restrict__ ctr) {
+    constexpr int K = kQChunk / 64;   // candidates per lane, loaded stage by stage (K loads in flight)
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -94,42 +65,52 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
         const int64_t ab = a_off[q], na = a_off[q + 1] - ab;
         const int64_t pb = p_off[q], np = p_off[q + 1] - pb;
         const bool ordered = q_has_ordered[q] != 0;
-        int32_t written = 0;
-        for (int k = 0; k < kQChunk / 64; ++k) {
+        // stage 1: the streamed type column (inc_type = link_type of the incidence entry)
+        bool pass[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
             const int64_t ci = c0 + k * 64 + lane;
-            bool hit = false;
-            int32_t L = -1;
-            if (ci < pl.n) {
-                ++n_cand;
-                // streamed type filter (inc_type is link_type of the incidence entry), then the row
-                if (T < 0 || inc_type[pl.beg + ci] == T) {
-                    L = inc_row[pl.beg + ci];
-                    ++n_typed;
-                    const int64_t b = tgt_off[L], e = tgt_off[L + 1];
-                    n_ar += (u64)(e - b);
-                    hit = true;
-                    // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
-                    for (int64_t j = 0; j < na && hit; ++j) {
-                        if (j == pl.amin) continue;
-                        const int32_t a = anchors[ab + j];
-                        bool found = false;
-                        for (int64_t i = b; i < e; ++i) found |= (tgt_idx[i] == a);
-                        hit = found;
+            pass[k] = ci < pl.n && (T < 0 || inc_type[pl.beg + ci] == T);
+            n_cand += ci < pl.n;
+        }
+        // stage 2: link rows of the type-passing candidates; stage 3: their target offsets
+        int32_t L[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) L[k] = pass[k] ? inc_row[pl.beg + c0 + k * 64 + lane] : -1;
+        int64_t b[K], e[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            b[k] = L[k] >= 0 ? tgt_off[L[k]] : 0;
+            e[k] = L[k] >= 0 ? tgt_off[L[k] + 1] : 0;
+        }
+        int32_t written = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            bool hit = L[k] >= 0;
+            if (hit) {
+                ++n_typed;
+                n_ar += (u64)(e[k] - b[k]);
+                // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
+                for (int64_t j = 0; j < na && hit; ++j) {
+                    if (j == pl.amin) continue;
+                    const int32_t a = anchors[ab + j];
+                    bool found = false;
+                    for (int64_t i = b[k]; i < e[k]; ++i) found |= (tgt_idx[i] == a);
+                    hit = found;
+                }
+                // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
+                if (hit && ordered) {
+                    int64_t i = b[k], j = 0;
+                    while (i < e[k] && j < np) {
+                        const int32_t pj = pattern[pb + j];
+                        if (pj < 0 || pj == tgt_idx[i]) ++j;
+                        ++i;
                     }
-                    // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
-                    if (hit && ordered) {
-                        int64_t i = b, j = 0;
-                        while (i < e && j < np) {
-                            const int32_t pj = pattern[pb + j];
-                            if (pj < 0 || pj == tgt_idx[i]) ++j;
-                            ++i;
-                        }
-                        hit = (j == np);
-                    }
+                    hit = (j == np);
                 }
             }
             const u64 m = __ballot(hit);
-            if (hit) slots[chunk * kQChunk + written + __popcll(m & ((1ull << lane) - 1ull))] = L;
+            if (hit) slots[chunk * kQChunk + written + __popcll(m & ((1ull << lane) - 1ull))] = L[k];
             written += __popcll(m);
         }
         if (lane == 0) counts[chunk] = written;
@@ -278,13 +259,8 @@ namespace {
 int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     HGX_API_BEGIN
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
-    std::vector<int32_t>& q_type = nb.q_type;
-    std::vector<int32_t>& q_nop = nb.q_nop;
-    std::vector<int32_t>& q_ord = nb.q_ord;
-    std::vector<int64_t>& a_off = nb.a_off;
-    std::vector<int64_t>& p_off = nb.p_off;
-    std::vector<int32_t>& anchors = nb.anchors;
-    std::vector<int32_t>& pattern = nb.pattern;
+    const std::vector<int64_t>& a_off = nb.a_off;
+    const std::vector<int32_t>& anchors = nb.anchors;
     hgx_query_result* r = new hgx_query_result();
     struct Guard {
         hgx_query_result* r;
@@ -300,16 +276,66 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     std::lock_guard<std::mutex> lk(g->mu);
     HGX_HIP(hipSetDevice(g->device));
     hipStream_t s = g->stream;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    struct EvGuard {
-        hipEvent_t* e;
-        ~EvGuard() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
-    } evg{ev};
-    if (g->timing)
-        for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&ev[i]));
+    if (g->inc_off_host.empty()) {   // host copy of the incidence offsets: planning needs no device round trip
+        g->inc_off_host.resize((size_t)g->A + 1);
+        HGX_HIP(hipMemcpyAsync(g->inc_off_host.data(), g->inc_off, sizeof(int64_t) * (g->A + 1), hipMemcpyDeviceToHost,
+                               s));
+        HGX_HIP(hipStreamSynchronize(s));
+    }
+    // plan (AndToQuery orders the ORA inputs by size: the first smallest anchor set drives the scan)
+    std::vector<QPlan> plan(n);
+    std::vector<int32_t> choff(n + 1, 0);
+    const int64_t* io = g->inc_off_host.data();
+    int64_t total_ub = 0;
+    for (int32_t q = 0; q < n; ++q) {
+        QPlan p{0, 0, 0, 0};
+        if (!nb.q_nop[q]) {
+            int64_t best = -1;
+            for (int64_t k = a_off[q]; k < a_off[q + 1]; ++k) {
+                const int32_t a = anchors[k];
+                const int64_t d = io[a + 1] - io[a];
+                if (best < 0 || d < best) {
+                    best = d;
+                    p.beg = io[a];
+                    p.amin = (int32_t)(k - a_off[q]);
+                }
+            }
+            p.n = best < 0 ? 0 : best;
+        }
+        plan[q] = p;
+        total_ub += p.n;
+        const int64_t c = choff[q] + (p.n + kQChunk - 1) / kQChunk;
+        if (c > INT32_MAX / kQChunk) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
+        choff[q + 1] = (int32_t)c;
+    }
+    const int32_t n_chunks = choff[n], nc = std::max(n_chunks, 1);
+    std::vector<int32_t> chq((size_t)nc, 0);
+    for (int32_t q = 0; q < n; ++q)
+        for (int32_t c = choff[q]; c < choff[q + 1]; ++c) chq[c] = q;
 
-    // upload
-    const size_t nA = std::max<size_t>(anchors.size(), 1), nP = std::max<size_t>(pattern.size(), 1);
+    // one pinned staging buffer, one upload
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = (off + bytes + 15) & ~(size_t)15;
+        return o;
+    };
+    const size_t o_type = take(4 * (size_t)n), o_ord = take(4 * (size_t)n), o_aoff = take(8 * (size_t)(n + 1)),
+                 o_poff = take(8 * (size_t)(n + 1)), o_anch = take(4 * std::max<size_t>(anchors.size(), 1)),
+                 o_pat = take(4 * std::max<size_t>(nb.pattern.size(), 1)), o_plan = take(sizeof(QPlan) * n),
+                 o_choff = take(4 * (size_t)(n + 1)), o_chq = take(4 * (size_t)nc);
+    const size_t up_bytes = off;
+    char* h = (char*)g->pinned_buf(up_bytes);
+    std::memcpy(h + o_type, nb.q_type.data(), 4 * (size_t)n);
+    std::memcpy(h + o_ord, nb.q_ord.data(), 4 * (size_t)n);
+    std::memcpy(h + o_aoff, a_off.data(), 8 * (size_t)(n + 1));
+    std::memcpy(h + o_poff, nb.p_off.data(), 8 * (size_t)(n + 1));
+    if (!anchors.empty()) std::memcpy(h + o_anch, anchors.data(), 4 * anchors.size());
+    if (!nb.pattern.empty()) std::memcpy(h + o_pat, nb.pattern.data(), 4 * nb.pattern.size());
+    std::memcpy(h + o_plan, plan.data(), sizeof(QPlan) * n);
+    std::memcpy(h + o_choff, choff.data(), 4 * (size_t)(n + 1));
+    std::memcpy(h + o_chq, chq.data(), 4 * (size_t)nc);
+
     std::vector<std::pair<void*, size_t>> tmp;
     auto dalloc = [&](size_t bytes) {
         void* p = g->alloc(bytes);
@@ -321,49 +347,37 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
         std::vector<std::pair<void*, size_t>>* t;
         ~TmpGuard() { for (auto& x : *t) g->release(x.first, x.second); }
     } tg{g, &tmp};
-    int32_t* d_type = (int32_t*)dalloc(sizeof(int32_t) * n);
-    int32_t* d_nop = (int32_t*)dalloc(sizeof(int32_t) * n);
-    int32_t* d_ord = (int32_t*)dalloc(sizeof(int32_t) * n);
-    int64_t* d_aoff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
-    int64_t* d_poff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
-    int32_t* d_anch = (int32_t*)dalloc(sizeof(int32_t) * nA);
-    int32_t* d_pat = (int32_t*)dalloc(sizeof(int32_t) * nP);
-    QPlan* d_plan = (QPlan*)dalloc(sizeof(QPlan) * n);
-    int32_t* d_nch = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
-    int32_t* d_choff = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
-    u64* d_ctr = (u64*)dalloc(sizeof(u64) * kQShards * kQStride);
-    HGX_HIP(hipMemcpyAsync(d_type, q_type.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemcpyAsync(d_nop, q_nop.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemcpyAsync(d_ord, q_ord.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemcpyAsync(d_aoff, a_off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemcpyAsync(d_poff, p_off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s));
-    if (!anchors.empty())
-        HGX_HIP(hipMemcpyAsync(d_anch, anchors.data(), sizeof(int32_t) * anchors.size(), hipMemcpyHostToDevice, s));
-    if (!pattern.empty())
-        HGX_HIP(hipMemcpyAsync(d_pat, pattern.data(), sizeof(int32_t) * pattern.size(), hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * kQShards * kQStride, s));
-    HGX_HIP(hipMemsetAsync(d_nch + n, 0, sizeof(int32_t), s));
-
-    if (g->timing) HGX_HIP(hipEventRecord(ev[0], s));
-    hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, g->inc_off, d_nop, d_aoff, d_anch, d_plan, d_nch);
-    HGX_CHECK_LAUNCH();
-    size_t scan_bytes = 0;
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_nch, d_choff, n + 1, s));
-    void* d_scan = dalloc(scan_bytes);
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_nch, d_choff, n + 1, s));
-    int32_t n_chunks = 0;
-    HGX_HIP(hipMemcpyAsync(&n_chunks, d_choff + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HGX_HIP(hipStreamSynchronize(s));
-    if (n_chunks < 0) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
-    const int32_t nc = std::max(n_chunks, 1);
-    int32_t* d_chq = (int32_t*)dalloc(sizeof(int32_t) * nc);
+    char* d = (char*)dalloc(up_bytes);
     int32_t* d_slots = (int32_t*)dalloc(sizeof(int32_t) * (size_t)nc * kQChunk);
     int64_t* d_cnt = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
     int64_t* d_outoff = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
     int64_t* d_qoff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
+    u64* d_ctr = (u64*)dalloc(sizeof(u64) * kQShards * kQStride);
+    int32_t* d_out = (int32_t*)dalloc(sizeof(int32_t) * (size_t)std::max<int64_t>(total_ub, 1));
+    size_t scan_bytes = 0;
+    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_cnt, d_outoff, nc + 1, s));
+    void* d_scan = dalloc(scan_bytes);
+
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
+    } evg{ev};
+    if (g->timing)
+        for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&ev[i]));
+    if (g->timing) HGX_HIP(hipEventRecord(ev[0], s));
+    HGX_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * kQShards * kQStride, s));
     HGX_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * (nc + 1), s));
-    hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_chq);
-    HGX_CHECK_LAUNCH();
+    const int32_t* d_type = (const int32_t*)(d + o_type);
+    const int32_t* d_ord = (const int32_t*)(d + o_ord);
+    const int64_t* d_aoff = (const int64_t*)(d + o_aoff);
+    const int64_t* d_poff = (const int64_t*)(d + o_poff);
+    const int32_t* d_anch = (const int32_t*)(d + o_anch);
+    const int32_t* d_pat = (const int32_t*)(d + o_pat);
+    const QPlan* d_plan = (const QPlan*)(d + o_plan);
+    const int32_t* d_choff = (const int32_t*)(d + o_choff);
+    const int32_t* d_chq = (const int32_t*)(d + o_chq);
     if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
     if (n_chunks > 0) {
         hgx_pattern_match<<<grid_for((int64_t)n_chunks * 64, 256, 4096), 256, 0, s>>>(
@@ -372,30 +386,23 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
         HGX_CHECK_LAUNCH();
     }
     if (g->timing) HGX_HIP(hipEventRecord(ev[2], s));
-    // per-chunk hit counts -> exclusive output offsets
-    {
-        size_t sb = 0;
-        HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, d_cnt, d_outoff, nc + 1, s));
-        void* d_sc2 = dalloc(sb);
-        HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_sc2, sb, d_cnt, d_outoff, nc + 1, s));
-    }
-    int64_t total = 0;
-    HGX_HIP(hipMemcpyAsync(&total, d_outoff + n_chunks, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    // per-chunk hit counts -> exclusive output offsets -> per-query offsets; compaction into d_out
+    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_outoff, nc + 1, s));
     hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_outoff, d_qoff);
     HGX_CHECK_LAUNCH();
-    HGX_HIP(hipMemcpyAsync(r->offsets.data(), d_qoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
-    HGX_HIP(hipStreamSynchronize(s));
-    r->ids.resize((size_t)std::max<int64_t>(total, 0));
-    if (total > 0) {
-        int32_t* d_out = (int32_t*)dalloc(sizeof(int32_t) * total);
+    if (n_chunks > 0) {
         hgx_q_scatter<<<(unsigned)ceil_div((int64_t)n_chunks * 64, 256), 256, 0, s>>>(n_chunks, d_cnt, d_outoff,
                                                                                        d_slots, g->link_atom, d_out);
         HGX_CHECK_LAUNCH();
-        HGX_HIP(hipMemcpyAsync(r->ids.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, s));
     }
-    if (g->timing) HGX_HIP(hipEventRecord(ev[3], s));
     u64 hsh[kQShards * kQStride], hctr[qNum] = {0, 0, 0, 0};
+    HGX_HIP(hipMemcpyAsync(r->offsets.data(), d_qoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
     HGX_HIP(hipMemcpyAsync(hsh, d_ctr, sizeof(hsh), hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    const int64_t total = r->offsets[n];
+    r->ids.resize((size_t)std::max<int64_t>(total, 0));
+    if (total > 0) HGX_HIP(hipMemcpyAsync(r->ids.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, s));
+    if (g->timing) HGX_HIP(hipEventRecord(ev[3], s));
     HGX_HIP(hipStreamSynchronize(s));
     for (int k = 0; k < qNum; ++k)
         for (int sh = 0; sh < kQShards; ++sh) hctr[k] += hsh[sh * kQStride + k];
@@ -409,7 +416,7 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     // algorithmic bytes of hgx_pattern_match: per candidate inc_type (+ inc_row when the type
     // passes), per type-passing candidate its tgt_off pair and target row, 4 B per hit, 8 B per chunk
     {
-        double anchors_bytes = 4.0 * anchors.size() + 16.0 * anchors.size() + 4.0 * pattern.size();
+        double anchors_bytes = 4.0 * anchors.size() + 16.0 * anchors.size() + 4.0 * nb.pattern.size();
         r->bytes_match = 4.0 * (double)hctr[qCand] + 20.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
                          4.0 * (double)hctr[qHits] + 8.0 * (double)n_chunks + anchors_bytes;
     }
