@@ -10,7 +10,8 @@ from ._lib import HGXError, HGXUnsupported, lib  # noqa: F401
 from .algorithms import (AtomTypeCondition, BfsResult, DefaultALGenerator, HGBreadthFirstTraversal,  # noqa: F401
                          SequenceResult, bfs_sequence,
                          HGException, bfs_batch)
-from .query import GpuAndToQuery, HGQueryConfiguration, find_all, hg, pattern_batch  # noqa: F401
+from .query import (ArityCondition, GpuAndToQuery, HGQueryConfiguration, LinkCondition,  # noqa: F401
+                    PositionedIncidentCondition, TypePlusCondition, find_all, hg, pattern_batch)
 from .snapshot import HyperGraphSnapshot, rank_handles  # noqa: F401
 
 __version__ = "0.1.0"

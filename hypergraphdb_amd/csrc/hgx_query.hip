@@ -1,11 +1,15 @@
 // hgx_query.hip -- batched conjunctive pattern matching over typed hyperedges.
 //
-// Replaces, for And{AtomTypeCondition?, IncidentCondition*, OrderedLinkCondition?}:
-//   ExpressionBasedQuery.expand (C/query/cond2qry/ExpressionBasedQuery.java:730-737; orderedLink
-//   adds incident(x) for each non-ANY target) -> AndToQuery (C/query/cond2qry/AndToQuery.java:102-306):
-//   nested ZigZagIntersectionResult (C/query/impl/ZigZagIntersectionResult.java) over sorted
-//   incidence sets and the type index, then PredicateBasedFilter(OrderedLinkCondition)
-//   (C/query/impl/PredicateBasedFilter.java:67-86, C/query/OrderedLinkCondition.java:92-124).
+// Replaces, for And{type set?, IncidentCondition*, PositionedIncidentCondition*,
+// OrderedLinkCondition*, ArityCondition?}:
+//   ExpressionBasedQuery.expand (C/query/cond2qry/ExpressionBasedQuery.java:603-755: orderedLink and
+//   LinkCondition add incident(x) for each non-ANY target, :730-746; TypePlusCondition becomes an
+//   Or of its subtypes' AtomTypeConditions, :606-627) -> AndToQuery
+//   (C/query/cond2qry/AndToQuery.java:102-306): nested ZigZagIntersectionResult
+//   (C/query/impl/ZigZagIntersectionResult.java) over the sorted incidence sets, the type index and
+//   the position-filtered incidence sets of PositionedIncidentToQuery, then PredicateBasedFilter for
+//   OrderedLinkCondition (C/query/OrderedLinkCondition.java:92-124) and ArityCondition
+//   (C/query/ArityCondition.java:49-67).
 //
 // GPU formulation: L is in inc(a) <=> a is a target of L.  So the intersection of the anchor
 // incidence sets is the smallest anchor set filtered by "every other anchor is in targets(L)",
@@ -25,12 +29,25 @@ typedef unsigned long long u64;
 
 constexpr int kQChunk = 256;        // candidates per wave-chunk (4 per lane)
 constexpr int kMaxAnchors = 32;
-constexpr int kMaxPattern = 64;
+constexpr int kMaxPattern = 64;     // targets of one OrderedLinkCondition
+constexpr int kMaxPatterns = 16;    // OrderedLinkConditions in one And
+constexpr int kMaxPositioned = 16;  // PositionedIncidentConditions in one And
+constexpr int kMaxTypes = 1 << 16;  // types of one Or (TypePlusCondition)
 
 struct QPlan {
     int64_t beg;    // first incidence entry of the smallest anchor set
     int64_t n;      // its size (0: empty result)
     int32_t amin;   // index of that anchor inside the query's anchor list
+    int32_t pad;
+};
+
+// Per-query descriptor on the device (offsets into the flat arrays of the batch).
+struct QDesc {
+    int64_t a_beg, a_end;   // anchors
+    int64_t t_beg, t_end;   // types (ascending); empty = no type condition
+    int64_t s_beg, s_end;   // positioned conditions (4 ints each: target, lb, ub, complement)
+    int64_t r_beg, r_end;   // patterns (rows of p_off)
+    int32_t arity;          // -1 = no ArityCondition
     int32_t pad;
 };
 
@@ -41,17 +58,48 @@ __device__ __forceinline__ void wave_add_q(u64* ctr, u64 v) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
+// type in the ascending list types[b, e)?  (one compare for AtomTypeCondition, a binary search for
+// the subtype set of a TypePlusCondition)
+__device__ __forceinline__ bool type_in(int32_t t, const int32_t* __restrict__ types, int64_t b, int64_t e) {
+    if (e - b == 1) return types[b] == t;
+    while (b < e) {
+        const int64_t m = (b + e) >> 1;
+        const int32_t v = types[m];
+        if (v == t) return true;
+        if (v < t) b = m + 1; else e = m;
+    }
+    return false;
+}
+
+// PositionedIncidentCondition.satisfies on one target row (C/query/PositionedIncidentCondition.java:123-177)
+__device__ __forceinline__ bool positioned(const int32_t* __restrict__ row, int n, int32_t x, int32_t lb, int32_t ub,
+                                           bool complement) {
+    if (ub < 0) ub = n + ub;
+    if (lb < 0) lb = n + lb;
+    if (lb > ub || lb < 0 || ub < 0 || lb >= n || ub >= n) return false;
+    if (complement) {
+        for (int i = 0; i < lb; ++i)
+            if (row[i] == x) return true;
+        for (int i = ub + 1; i < n; ++i)
+            if (row[i] == x) return true;
+        return false;
+    }
+    for (int i = lb; i <= ub; ++i)
+        if (row[i] == x) return true;
+    return false;
+}
+
 // A wave per chunk of kQChunk candidates of one query (grid-stride over chunks; the counters are
 // summed in registers and added once per wave into sharded replicas).
 constexpr int kQShards = 16, kQStride = 16;
 
 __global__ void __launch_bounds__(256) hgx_pattern_match(
     int32_t n_chunks, const int32_t* __restrict__ chunk_q, const int32_t* __restrict__ chunk_off,
-    const QPlan* __restrict__ plan, const int32_t* __restrict__ q_type, const int64_t* __restrict__ a_off,
-    const int32_t* __restrict__ anchors, const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern,
-    const int32_t* __restrict__ q_has_ordered, const int32_t* __restrict__ inc_row,
-    const int32_t* __restrict__ inc_type, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
-    int32_t* __restrict__ slots, int64_t* __restrict__ counts, u64* __restrict__ ctr) {
+    const QPlan* __restrict__ plan, const QDesc* __restrict__ desc, const int32_t* __restrict__ anchors,
+    const int32_t* __restrict__ types, const int32_t* __restrict__ pos, const int64_t* __restrict__ p_off,
+    const int32_t* __restrict__ pattern, const int32_t* __restrict__ inc_row, const int32_t* __restrict__ inc_type,
+    const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx, int32_t* __restrict__ slots,
+    int64_t* __restrict__ counts, u64* __restrict__ ctr) {
     constexpr int K = kQChunk / 64;   // candidates per lane, loaded stage by stage (K loads in flight)
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -60,17 +108,15 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     for (int64_t chunk = wave; chunk < n_chunks; chunk += nwave) {
         const int32_t q = chunk_q[chunk];
         const QPlan pl = plan[q];
+        const QDesc d = desc[q];
         const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
-        const int32_t T = q_type[q];
-        const int64_t ab = a_off[q], na = a_off[q + 1] - ab;
-        const int64_t pb = p_off[q], np = p_off[q + 1] - pb;
-        const bool ordered = q_has_ordered[q] != 0;
+        const bool typed = d.t_end > d.t_beg;
         // stage 1: the streamed type column (inc_type = link_type of the incidence entry)
         bool pass[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t ci = c0 + k * 64 + lane;
-            pass[k] = ci < pl.n && (T < 0 || inc_type[pl.beg + ci] == T);
+            pass[k] = ci < pl.n && (!typed || type_in(inc_type[pl.beg + ci], types, d.t_beg, d.t_end));
             n_cand += ci < pl.n;
         }
         // stage 2: link rows of the type-passing candidates; stage 3: their target offsets
@@ -89,21 +135,30 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
             bool hit = L[k] >= 0;
             if (hit) {
                 ++n_typed;
-                n_ar += (u64)(e[k] - b[k]);
+                const int n = (int)(e[k] - b[k]);
+                n_ar += (u64)n;
+                const int32_t* row = tgt_idx + b[k];
+                // ArityCondition: layout.length == arity + 2
+                if (d.arity >= 0) hit = n == d.arity;
                 // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
-                for (int64_t j = 0; j < na && hit; ++j) {
-                    if (j == pl.amin) continue;
-                    const int32_t a = anchors[ab + j];
+                for (int64_t j = d.a_beg; j < d.a_end && hit; ++j) {
+                    if (j - d.a_beg == pl.amin) continue;
+                    const int32_t a = anchors[j];
                     bool found = false;
-                    for (int64_t i = b[k]; i < e[k]; ++i) found |= (tgt_idx[i] == a);
+                    for (int i = 0; i < n; ++i) found |= (row[i] == a);
                     hit = found;
                 }
+                // PositionedIncidentCondition (its ORA set: inc(target) filtered by the predicate)
+                for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
+                    hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
                 // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
-                if (hit && ordered) {
-                    int64_t i = b[k], j = 0;
-                    while (i < e[k] && j < np) {
+                for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
+                    const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
+                    int i = 0;
+                    int64_t j = 0;
+                    while (i < n && j < np) {
                         const int32_t pj = pattern[pb + j];
-                        if (pj < 0 || pj == tgt_idx[i]) ++j;
+                        if (pj < 0 || pj == row[i]) ++j;
                         ++i;
                     }
                     hit = (j == np);
@@ -155,55 +210,91 @@ struct hgx_query_result {
 
 namespace {
 
+// One query as handed over by any of the entry points.
+struct QueryIn {
+    int32_t n_types = 0;
+    const int32_t* types = nullptr;
+    int32_t n_inc = 0;
+    const int32_t* inc = nullptr;
+    int32_t n_pos = 0;
+    const int32_t* pos = nullptr;     // 4 ints each
+    int32_t n_pat = 0;                // OrderedLinkConditions
+    const int64_t* pat_off = nullptr; // [n_pat + 1] into pat
+    const int32_t* pat = nullptr;
+    int32_t arity = -1;
+};
+
 // Normalised batch: ExpressionBasedQuery.expand (orderedLink adds incident(x) for each non-ANY x,
-// :730-737) + the toDNF HashSet dedupe (:100) -> per query: type, distinct anchors, pattern, nop.
+// :730-737) + the toDNF HashSet dedupe (:100) -> per query: types, distinct anchors, positioned
+// conditions, patterns, arity, nop.
 struct NormBatch {
-    std::vector<int32_t> q_type, q_nop, q_ord;
-    std::vector<int64_t> a_off, p_off;
-    std::vector<int32_t> anchors, pattern;
+    std::vector<QDesc> desc;
+    std::vector<int32_t> nop;
+    std::vector<int32_t> anchors, types, pos, pattern;
+    std::vector<int64_t> p_off{0};
 };
 
 template <class Get>
 void normalise(hgx_graph* g, int32_t n, Get get, NormBatch& nb) {
-    nb.q_type.resize(n);
-    nb.q_nop.resize(n);
-    nb.q_ord.resize(n);
-    nb.a_off.assign(n + 1, 0);
-    nb.p_off.assign(n + 1, 0);
+    nb.desc.resize(n);
+    nb.nop.assign(n, 0);
     for (int32_t q = 0; q < n; ++q) {
-        int32_t type, n_inc, has_ord, n_pat;
-        const int32_t *inc, *pat;
-        get(q, type, n_inc, inc, has_ord, n_pat, pat);
-        if (n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
-            fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(q));
-        if (type < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type in query " + std::to_string(q));
-        nb.q_type[q] = type;
-        nb.q_ord[q] = has_ord ? 1 : 0;
-        const int32_t m = has_ord ? n_pat : 0;
-        if (m > kMaxPattern) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: ordered pattern too long");
-        const size_t a0 = nb.anchors.size();
+        QueryIn in;
+        get(q, in);
+        const std::string qs = std::to_string(q);
+        if (in.n_types < 0 || in.n_inc < 0 || in.n_pos < 0 || in.n_pat < 0 || (in.n_types > 0 && !in.types) ||
+            (in.n_inc > 0 && !in.inc) || (in.n_pos > 0 && !in.pos) || (in.n_pat > 0 && (!in.pat_off)) || in.arity < -1)
+            fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + qs);
+        if (in.n_types > kMaxTypes || in.n_pos > kMaxPositioned || in.n_pat > kMaxPatterns)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + qs + " exceeds the condition limits");
+        QDesc& d = nb.desc[q];
+        d.arity = in.arity;
+        // types: an Or of exact types (ascending, duplicates dropped)
+        d.t_beg = (int64_t)nb.types.size();
+        for (int32_t i = 0; i < in.n_types; ++i) {
+            if (in.types[i] < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type in query " + qs);
+            nb.types.push_back(in.types[i]);
+        }
+        std::sort(nb.types.begin() + d.t_beg, nb.types.end());
+        nb.types.erase(std::unique(nb.types.begin() + d.t_beg, nb.types.end()), nb.types.end());
+        d.t_end = (int64_t)nb.types.size();
+        // anchors
+        d.a_beg = (int64_t)nb.anchors.size();
         auto add = [&](int32_t h) {
-            if (h < 0 || h >= g->A)
-                fail(HGX_E_INVALID, "hgx_pattern_batch: atom id out of range in query " + std::to_string(q));
-            for (size_t k = a0; k < nb.anchors.size(); ++k)
+            if (h < 0 || h >= g->A) fail(HGX_E_INVALID, "hgx_pattern_batch: atom id out of range in query " + qs);
+            for (size_t k = (size_t)d.a_beg; k < nb.anchors.size(); ++k)
                 if (nb.anchors[k] == h) return;
             nb.anchors.push_back(h);
         };
-        for (int32_t i = 0; i < n_inc; ++i) add(inc[i]);
-        for (int32_t i = 0; i < m; ++i) {
-            if (pat[i] == HGX_ANY_HANDLE) continue;
-            if (pat[i] < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern id");
-            add(pat[i]);
+        for (int32_t i = 0; i < in.n_inc; ++i) add(in.inc[i]);
+        d.s_beg = (int64_t)nb.pos.size() / 4;
+        for (int32_t i = 0; i < in.n_pos; ++i) {   // its ORA set is inc(target): the target anchors the scan
+            add(in.pos[4 * i]);
+            for (int k = 0; k < 4; ++k) nb.pos.push_back(in.pos[4 * i + k]);
         }
-        if (nb.anchors.size() == a0)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(q) + " has no incidence anchor");
-        if ((int64_t)(nb.anchors.size() - a0) > kMaxAnchors)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: too many anchors");
-        // an empty OrderedLinkCondition gets QueryMetaData.EMPTY, lands in ORA and compiles to HGQuery.NOP
-        nb.q_nop[q] = (has_ord && m == 0) ? 1 : 0;
-        for (int32_t i = 0; i < m; ++i) nb.pattern.push_back(pat[i]);
-        nb.a_off[q + 1] = (int64_t)nb.anchors.size();
-        nb.p_off[q + 1] = (int64_t)nb.pattern.size();
+        d.s_end = (int64_t)nb.pos.size() / 4;
+        d.r_beg = (int64_t)nb.p_off.size() - 1;
+        for (int32_t r = 0; r < in.n_pat; ++r) {
+            const int64_t b = in.pat_off[r], m = in.pat_off[r + 1] - b;
+            if (m < 0 || (m > 0 && !in.pat)) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern in query " + qs);
+            if (m > kMaxPattern) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: ordered pattern too long");
+            // an empty OrderedLinkCondition gets QueryMetaData.EMPTY, lands in ORA and compiles to HGQuery.NOP
+            if (m == 0) nb.nop[q] = 1;
+            for (int64_t i = 0; i < m; ++i) {
+                const int32_t p = in.pat[b + i];
+                if (p != HGX_ANY_HANDLE) {
+                    if (p < 0) fail(HGX_E_INVALID, "hgx_pattern_batch: bad pattern id");
+                    add(p);
+                }
+                nb.pattern.push_back(p);
+            }
+            nb.p_off.push_back((int64_t)nb.pattern.size());
+        }
+        d.r_end = (int64_t)nb.p_off.size() - 1;
+        d.a_end = (int64_t)nb.anchors.size();
+        if (d.a_end == d.a_beg)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + qs + " has no incidence anchor");
+        if (d.a_end - d.a_beg > kMaxAnchors) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: too many anchors");
     }
 }
 
@@ -216,15 +307,18 @@ extern "C" int hgx_pattern_batch(hgx_graph* g, const hgx_and_query* qs, int32_t 
     if (!g || !out || n < 0 || (n > 0 && !qs)) fail(HGX_E_INVALID, "hgx_pattern_batch: bad argument");
     *out = nullptr;
     NormBatch nb;
+    std::vector<int64_t> one_off;
     normalise(g, n,
-              [&](int32_t q, int32_t& t, int32_t& ni, const int32_t*& inc, int32_t& ho, int32_t& np,
-                  const int32_t*& pat) {
-                  t = qs[q].type;
-                  ni = qs[q].n_incident;
-                  inc = qs[q].incident;
-                  ho = qs[q].has_ordered;
-                  np = qs[q].n_pattern;
-                  pat = qs[q].pattern;
+              [&](int32_t q, QueryIn& in) {
+                  if (qs[q].type < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type");
+                  in.n_types = qs[q].type >= 0 ? 1 : 0;
+                  in.types = &qs[q].type;
+                  in.n_inc = qs[q].n_incident;
+                  in.inc = qs[q].incident;
+                  one_off.assign({0, (int64_t)std::max(qs[q].n_pattern, 0)});
+                  in.n_pat = qs[q].has_ordered ? 1 : 0;
+                  in.pat_off = one_off.data();
+                  in.pat = qs[q].pattern;
               },
               nb);
     return run_batch(g, n, nb, out);
@@ -239,15 +333,46 @@ extern "C" int hgx_pattern_batch_packed(hgx_graph* g, int32_t n, const int32_t* 
         fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad argument");
     *out = nullptr;
     NormBatch nb;
+    std::vector<int64_t> one_off;
     normalise(g, n,
-              [&](int32_t q, int32_t& t, int32_t& ni, const int32_t*& ii, int32_t& ho, int32_t& np,
-                  const int32_t*& pp) {
-                  t = type[q];
-                  ni = (int32_t)(inc_off[q + 1] - inc_off[q]);
-                  ii = inc ? inc + inc_off[q] : nullptr;
-                  ho = has_ordered[q];
-                  np = (int32_t)(pat_off[q + 1] - pat_off[q]);
-                  pp = pat ? pat + pat_off[q] : nullptr;
+              [&](int32_t q, QueryIn& in) {
+                  if (type[q] < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type");
+                  in.n_types = type[q] >= 0 ? 1 : 0;
+                  in.types = type + q;
+                  in.n_inc = (int32_t)(inc_off[q + 1] - inc_off[q]);
+                  in.inc = inc ? inc + inc_off[q] : nullptr;
+                  one_off.assign({0, pat_off[q + 1] - pat_off[q]});
+                  in.n_pat = has_ordered[q] ? 1 : 0;
+                  in.pat_off = one_off.data();
+                  in.pat = pat ? pat + pat_off[q] : nullptr;
+              },
+              nb);
+    return run_batch(g, n, nb, out);
+    HGX_API_END
+}
+
+extern "C" int hgx_pattern_batch_ext(hgx_graph* g, int32_t n, const int64_t* type_off, const int32_t* types,
+                                     const int64_t* inc_off, const int32_t* inc, const int64_t* pos_off,
+                                     const int32_t* pos, const int64_t* pset_off, const int64_t* pat_off,
+                                     const int32_t* pat, const int32_t* arity, hgx_query_result** out) {
+    HGX_API_BEGIN
+    if (!g || !out || n < 0 || (n > 0 && (!type_off || !inc_off || !pos_off || !pset_off || !arity)))
+        fail(HGX_E_INVALID, "hgx_pattern_batch_ext: bad argument");
+    *out = nullptr;
+    NormBatch nb;
+    normalise(g, n,
+              [&](int32_t q, QueryIn& in) {
+                  in.n_types = (int32_t)(type_off[q + 1] - type_off[q]);
+                  in.types = types ? types + type_off[q] : nullptr;
+                  in.n_inc = (int32_t)(inc_off[q + 1] - inc_off[q]);
+                  in.inc = inc ? inc + inc_off[q] : nullptr;
+                  in.n_pos = (int32_t)(pos_off[q + 1] - pos_off[q]);
+                  in.pos = pos ? pos + 4 * pos_off[q] : nullptr;
+                  in.n_pat = (int32_t)(pset_off[q + 1] - pset_off[q]);
+                  if (in.n_pat > 0 && !pat_off) fail(HGX_E_INVALID, "hgx_pattern_batch_ext: null pat_off");
+                  in.pat_off = pat_off ? pat_off + pset_off[q] : nullptr;
+                  in.pat = pat;
+                  in.arity = arity[q];
               },
               nb);
     return run_batch(g, n, nb, out);
@@ -259,7 +384,6 @@ namespace {
 int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     HGX_API_BEGIN
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
-    const std::vector<int64_t>& a_off = nb.a_off;
     const std::vector<int32_t>& anchors = nb.anchors;
     hgx_query_result* r = new hgx_query_result();
     struct Guard {
@@ -289,15 +413,15 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     int64_t total_ub = 0;
     for (int32_t q = 0; q < n; ++q) {
         QPlan p{0, 0, 0, 0};
-        if (!nb.q_nop[q]) {
+        if (!nb.nop[q]) {
             int64_t best = -1;
-            for (int64_t k = a_off[q]; k < a_off[q + 1]; ++k) {
+            for (int64_t k = nb.desc[q].a_beg; k < nb.desc[q].a_end; ++k) {
                 const int32_t a = anchors[k];
                 const int64_t d = io[a + 1] - io[a];
                 if (best < 0 || d < best) {
                     best = d;
                     p.beg = io[a];
-                    p.amin = (int32_t)(k - a_off[q]);
+                    p.amin = (int32_t)(k - nb.desc[q].a_beg);
                 }
             }
             p.n = best < 0 ? 0 : best;
@@ -320,21 +444,25 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
         off = (off + bytes + 15) & ~(size_t)15;
         return o;
     };
-    const size_t o_type = take(4 * (size_t)n), o_ord = take(4 * (size_t)n), o_aoff = take(8 * (size_t)(n + 1)),
-                 o_poff = take(8 * (size_t)(n + 1)), o_anch = take(4 * std::max<size_t>(anchors.size(), 1)),
-                 o_pat = take(4 * std::max<size_t>(nb.pattern.size(), 1)), o_plan = take(sizeof(QPlan) * n),
+    auto bytes_of = [](const auto& v) { return sizeof(v[0]) * std::max<size_t>(v.size(), 1); };
+    const size_t o_desc = take(sizeof(QDesc) * n), o_anch = take(bytes_of(anchors)), o_types = take(bytes_of(nb.types)),
+                 o_pos = take(bytes_of(nb.pos)), o_poff = take(bytes_of(nb.p_off)),
+                 o_pat = take(bytes_of(nb.pattern)), o_plan = take(sizeof(QPlan) * n),
                  o_choff = take(4 * (size_t)(n + 1)), o_chq = take(4 * (size_t)nc);
     const size_t up_bytes = off;
     char* h = (char*)g->pinned_buf(up_bytes);
-    std::memcpy(h + o_type, nb.q_type.data(), 4 * (size_t)n);
-    std::memcpy(h + o_ord, nb.q_ord.data(), 4 * (size_t)n);
-    std::memcpy(h + o_aoff, a_off.data(), 8 * (size_t)(n + 1));
-    std::memcpy(h + o_poff, nb.p_off.data(), 8 * (size_t)(n + 1));
-    if (!anchors.empty()) std::memcpy(h + o_anch, anchors.data(), 4 * anchors.size());
-    if (!nb.pattern.empty()) std::memcpy(h + o_pat, nb.pattern.data(), 4 * nb.pattern.size());
-    std::memcpy(h + o_plan, plan.data(), sizeof(QPlan) * n);
-    std::memcpy(h + o_choff, choff.data(), 4 * (size_t)(n + 1));
-    std::memcpy(h + o_chq, chq.data(), 4 * (size_t)nc);
+    auto put = [&](size_t o, const auto& v) {
+        if (!v.empty()) std::memcpy(h + o, v.data(), sizeof(v[0]) * v.size());
+    };
+    put(o_desc, nb.desc);
+    put(o_anch, anchors);
+    put(o_types, nb.types);
+    put(o_pos, nb.pos);
+    put(o_poff, nb.p_off);
+    put(o_pat, nb.pattern);
+    put(o_plan, plan);
+    put(o_choff, choff);
+    put(o_chq, chq);
 
     std::vector<std::pair<void*, size_t>> tmp;
     auto dalloc = [&](size_t bytes) {
@@ -369,20 +497,14 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     HGX_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, s));
     HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * kQShards * kQStride, s));
     HGX_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * (nc + 1), s));
-    const int32_t* d_type = (const int32_t*)(d + o_type);
-    const int32_t* d_ord = (const int32_t*)(d + o_ord);
-    const int64_t* d_aoff = (const int64_t*)(d + o_aoff);
-    const int64_t* d_poff = (const int64_t*)(d + o_poff);
-    const int32_t* d_anch = (const int32_t*)(d + o_anch);
-    const int32_t* d_pat = (const int32_t*)(d + o_pat);
-    const QPlan* d_plan = (const QPlan*)(d + o_plan);
     const int32_t* d_choff = (const int32_t*)(d + o_choff);
-    const int32_t* d_chq = (const int32_t*)(d + o_chq);
     if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
     if (n_chunks > 0) {
         hgx_pattern_match<<<grid_for((int64_t)n_chunks * 64, 256, 4096), 256, 0, s>>>(
-            n_chunks, d_chq, d_choff, d_plan, d_type, d_aoff, d_anch, d_poff, d_pat, d_ord, g->inc_row, g->inc_type,
-            g->tgt_off, g->tgt_idx, d_slots, d_cnt, d_ctr);
+            n_chunks, (const int32_t*)(d + o_chq), d_choff, (const QPlan*)(d + o_plan), (const QDesc*)(d + o_desc),
+            (const int32_t*)(d + o_anch), (const int32_t*)(d + o_types), (const int32_t*)(d + o_pos),
+            (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_row, g->inc_type, g->tgt_off,
+            g->tgt_idx, d_slots, d_cnt, d_ctr);
         HGX_CHECK_LAUNCH();
     }
     if (g->timing) HGX_HIP(hipEventRecord(ev[2], s));
@@ -416,9 +538,10 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     // algorithmic bytes of hgx_pattern_match: per candidate inc_type (+ inc_row when the type
     // passes), per type-passing candidate its tgt_off pair and target row, 4 B per hit, 8 B per chunk
     {
-        double anchors_bytes = 4.0 * anchors.size() + 16.0 * anchors.size() + 4.0 * nb.pattern.size();
+        double cond_bytes = 20.0 * anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
+                            4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
         r->bytes_match = 4.0 * (double)hctr[qCand] + 20.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
-                         4.0 * (double)hctr[qHits] + 8.0 * (double)n_chunks + anchors_bytes;
+                         4.0 * (double)hctr[qHits] + 8.0 * (double)n_chunks + cond_bytes;
     }
     guard.r = nullptr;
     *out = r;

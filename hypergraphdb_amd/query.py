@@ -60,6 +60,71 @@ class OrderedLinkCondition:
         return f"orderedLink{self.targets}"
 
 
+class LinkCondition:
+    """hg.link(targets...): the link's targets include every given target
+    (C/query/LinkCondition.java:101-139); expand turns it into incident(target) for every non-ANY
+    target and drops it (C/query/cond2qry/ExpressionBasedQuery.java:739-746)."""
+
+    def __init__(self, *targets):
+        if len(targets) == 1 and isinstance(targets[0], (list, tuple, set)):
+            targets = tuple(targets[0])
+        self.targets = tuple(int(t) for t in targets)
+
+    def __repr__(self):
+        return f"links{self.targets}"
+
+
+class PositionedIncidentCondition:
+    """hg.incidentAt / hg.incidentNotAt (C/query/PositionedIncidentCondition.java:123-177): the
+    target sits at a position in [lower, upper] (negative = from the end), or outside it with
+    ``complement``."""
+
+    def __init__(self, target, lower, upper=None, complement=False):
+        self.target, self.lower = int(target), int(lower)
+        self.upper = self.lower if upper is None else int(upper)
+        self.complement = bool(complement)
+
+    def record(self):
+        return (self.target, self.lower, self.upper, int(self.complement))
+
+    def __repr__(self):
+        return f"incidentAt({self.target},{self.lower},{self.upper},{self.complement})"
+
+
+class ArityCondition:
+    """hg.arity(k) (C/query/ArityCondition.java:49-67): the link has exactly k targets."""
+
+    def __init__(self, arity):
+        self.arity = int(arity)
+
+    def __repr__(self):
+        return f"arity({self.arity})"
+
+
+class TypePlusCondition:
+    """hg.typePlus(base): the atom's type is the base or one of its subtypes
+    (C/query/TypePlusCondition.java:26-71); expand turns it into an Or of AtomTypeConditions
+    (ExpressionBasedQuery.java:606-627).  Here it carries the resulting set of type keys."""
+
+    def __init__(self, types):
+        self.types = frozenset(int(t) for t in types)
+
+    @classmethod
+    def from_subsumption(cls, snapshot, base_type_atom, subsumes_type, key_of_atom):
+        """The subtypes the way TypePlusCondition.fetchSubTypes finds them: a DefaultALGenerator
+        over HGSubsumes links (preceding=False, succeeding=True) from the base -- run as one GPU
+        traversal.  ``key_of_atom`` maps a type atom to the type key used in link_type."""
+        from .algorithms import bfs_batch
+        gen = DefaultALGenerator(snapshot, AtomTypeCondition(subsumes_type), None, False, True, False)
+        r = bfs_batch(snapshot, [int(base_type_atom)], None, gen)
+        atoms = [int(base_type_atom)] + [int(a) for d in range(1, r.n_levels) for a in r.visited(0, d)]
+        r.close()
+        return cls(key_of_atom[a] for a in atoms if a in key_of_atom)
+
+    def __repr__(self):
+        return f"typePlus{sorted(self.types)}"
+
+
 class And(list):
     def __repr__(self):
         return "and(" + ", ".join(map(repr, self)) + ")"
@@ -112,6 +177,26 @@ class hg:
         return ANY
 
     @staticmethod
+    def link(*targets):
+        return LinkCondition(*targets)
+
+    @staticmethod
+    def incidentAt(target, lower, upper=None):
+        return PositionedIncidentCondition(target, lower, upper, False)
+
+    @staticmethod
+    def incidentNotAt(target, lower, upper=None):
+        return PositionedIncidentCondition(target, lower, upper, True)
+
+    @staticmethod
+    def arity(k):
+        return ArityCondition(k)
+
+    @staticmethod
+    def typePlus(types):
+        return types if isinstance(types, TypePlusCondition) else TypePlusCondition(types)
+
+    @staticmethod
     def and_(*conds):
         return And(conds)
 
@@ -147,25 +232,47 @@ def _flatten(cond, out):
     return out
 
 
+_LEAVES = (AtomTypeCondition, TypePlusCondition, IncidentCondition, LinkCondition, PositionedIncidentCondition,
+           OrderedLinkCondition, ArityCondition)
+
+
 def normalize(cond):
-    """And{type?, incident*, orderedLink?} -> (type, incident list, pattern or None); raises
-    HGXUnsupported for any other shape (a Java shim delegates those to AndToQuery)."""
-    if isinstance(cond, (IncidentCondition, OrderedLinkCondition, AtomTypeCondition)):
+    """The accelerated And shapes after ExpressionBasedQuery.expand + toDNF, as a dict
+    {types (sorted list, [] = no type condition), inc, pos [(target, lb, ub, complement)],
+    patterns [tuple], arity (-1 = none)} -- or "empty" when the conjunction can match nothing
+    (two different exact types, two different arities).  Any other shape raises HGXUnsupported
+    (a Java shim delegates those to AndToQuery)."""
+    if isinstance(cond, _LEAVES):
         cond = And([cond])
     if not isinstance(cond, And):
         raise HGXUnsupported(_lib.HGX_E_UNSUPPORTED, f"not an And: {cond!r}")
     subs = _flatten(cond, [])
-    types = [c for c in subs if isinstance(c, AtomTypeCondition)]
-    incs = [c for c in subs if isinstance(c, IncidentCondition)]
-    ords = [c for c in subs if isinstance(c, OrderedLinkCondition)]
-    if len(types) + len(incs) + len(ords) != len(subs) or len(ords) > 1:
+    if not all(isinstance(c, _LEAVES) for c in subs):
         raise HGXUnsupported(_lib.HGX_E_UNSUPPORTED, f"shape not accelerated: {cond!r}")
-    tset = {t.type for t in types}
-    if len(tset) > 1:
-        return "empty", None, None       # two different exact types: nothing satisfies both
-    t = types[0].type if types else _lib.HGX_NO_TYPE
-    pattern = ords[0].targets if ords else None
-    return t, [c.target for c in incs], pattern
+    tset = None
+    for c in subs:   # every type condition must hold: intersect their type sets
+        if isinstance(c, AtomTypeCondition):
+            tset = {c.type} if tset is None else tset & {c.type}
+        elif isinstance(c, TypePlusCondition):
+            tset = set(c.types) if tset is None else tset & set(c.types)
+    arities = {c.arity for c in subs if isinstance(c, ArityCondition)}
+    if (tset is not None and not tset) or len(arities) > 1:
+        return "empty"
+    inc = [c.target for c in subs if isinstance(c, IncidentCondition)]
+    for c in subs:
+        if isinstance(c, LinkCondition):
+            inc.extend(t for t in c.targets if t != ANY)
+    return {"types": sorted(tset) if tset is not None else [], "inc": inc,
+            "pos": [c.record() for c in subs if isinstance(c, PositionedIncidentCondition)],
+            "patterns": [c.targets for c in subs if isinstance(c, OrderedLinkCondition)],
+            "arity": arities.pop() if arities else -1}
+
+
+def _from_tuple(q):
+    """legacy (type, incident, pattern-or-None) -> the normalised dict"""
+    t, inc, pat = q
+    return {"types": [] if t is None or t < 0 else [int(t)], "inc": list(inc), "pos": [],
+            "patterns": [] if pat is None else [tuple(pat)], "arity": -1}
 
 
 class QueryResult:
@@ -200,30 +307,63 @@ def pattern_batch_arrays(snapshot, q_type, inc_off, inc, has_ordered, pat_off, p
     return QueryResult(off, ids[: int(off[-1])], {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
 
 
+def pattern_batch_ext_arrays(snapshot, type_off, types, inc_off, inc, pos_off, pos, pset_off, pat_off, pat,
+                             arity) -> QueryResult:
+    """Flat batch for hgx_pattern_batch_ext (see include/hgx.h)."""
+    n = len(arity)
+    arrs = [np.ascontiguousarray(type_off, np.int64), np.ascontiguousarray(types, np.int32),
+            np.ascontiguousarray(inc_off, np.int64), np.ascontiguousarray(inc, np.int32),
+            np.ascontiguousarray(pos_off, np.int64), np.ascontiguousarray(pos, np.int32),
+            np.ascontiguousarray(pset_off, np.int64), np.ascontiguousarray(pat_off, np.int64),
+            np.ascontiguousarray(pat, np.int32), np.ascontiguousarray(arity, np.int32)]
+    h = C.c_void_p()
+    check(lib().hgx_pattern_batch_ext(snapshot.handle, n, *(a.ctypes.data for a in arrs), C.byref(h)))
+    try:
+        off = np.zeros(n + 1, np.int64)
+        check(lib().hgx_query_result_offsets(h, ptr(off)))
+        ids = np.zeros(max(int(off[-1]), 1), np.int32)
+        check(lib().hgx_query_result_ids(h, ptr(ids)))
+        a, b, c = C.c_double(), C.c_double(), C.c_double()
+        check(lib().hgx_query_result_ms(h, C.byref(a), C.byref(b), C.byref(c)))
+    finally:
+        lib().hgx_query_result_free(h)
+    return QueryResult(off, ids[: int(off[-1])], {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+
+
 def pattern_batch(snapshot, queries) -> QueryResult:
-    """Evaluate many And{type?, incident*, orderedLink?} queries in one GPU launch sequence.
-    ``queries``: conditions or (type, incident, pattern) tuples (pattern None = no orderedLink)."""
-    norm = [q if isinstance(q, tuple) else normalize(q) for q in queries]
+    """Evaluate many accelerated And queries in one GPU launch sequence.  ``queries``: conditions,
+    normalised dicts, or legacy (type, incident, pattern) tuples (pattern None = no orderedLink)."""
+    norm = []
+    for q in queries:
+        if isinstance(q, tuple):
+            q = _from_tuple(q)
+        elif not isinstance(q, dict) and q != "empty":
+            q = normalize(q)
+        norm.append(q)
     n = len(norm)
-    q_type = np.empty(n, np.int32)
-    has = np.zeros(n, np.int32)
-    inc_off = np.zeros(n + 1, np.int64)
-    pat_off = np.zeros(n + 1, np.int64)
-    inc, pat = [], []
+    type_off, inc_off, pos_off, pset_off = (np.zeros(n + 1, np.int64) for _ in range(4))
+    types, inc, pos, pat, pat_off = [], [], [], [], [0]
+    arity = np.full(n, -1, np.int32)
     empty = np.zeros(n, bool)
-    for i, (t, ic, pt) in enumerate(norm):
-        if t == "empty":                 # two different exact types: nothing satisfies both
+    for i, q in enumerate(norm):
+        if q == "empty":   # nothing can match: run a NOP (an empty orderedLink) on a valid anchor
             empty[i] = True
-            t, ic, pt = _lib.HGX_NO_TYPE, [0], ()    # an empty orderedLink compiles to NOP
-        q_type[i] = t
-        inc.extend(ic)
+            q = {"types": [], "inc": [0], "pos": [], "patterns": [()], "arity": -1}
+        types.extend(q["types"])
+        type_off[i + 1] = len(types)
+        inc.extend(q["inc"])
         inc_off[i + 1] = len(inc)
-        if pt is not None:
-            has[i] = 1
-            pat.extend(pt)
-        pat_off[i + 1] = len(pat)
-    r = pattern_batch_arrays(snapshot, q_type, inc_off, np.array(inc or [0], np.int32), has, pat_off,
-                             np.array(pat or [0], np.int32))
+        for rec in q["pos"]:
+            pos.extend(rec)
+        pos_off[i + 1] = len(pos) // 4
+        for p in q["patterns"]:
+            pat.extend(p)
+            pat_off.append(len(pat))
+        pset_off[i + 1] = len(pat_off) - 1
+        arity[i] = q["arity"]
+    r = pattern_batch_ext_arrays(snapshot, type_off, np.array(types or [0], np.int32), inc_off,
+                                 np.array(inc or [0], np.int32), pos_off, np.array(pos or [0], np.int32), pset_off,
+                                 np.array(pat_off, np.int64), np.array(pat or [0], np.int32), arity)
     if empty.any():
         parts = [np.empty(0, np.int32) if empty[i] else r[i] for i in range(n)]
         off = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64)

@@ -201,6 +201,23 @@ int  hgx_pattern_batch(hgx_graph *g, const hgx_and_query *queries, int32_t n,
 int  hgx_pattern_batch_packed(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off,
                               const int32_t *inc, const int32_t *has_ordered, const int64_t *pat_off,
                               const int32_t *pat, hgx_query_result **out);
+/* The And shapes beyond {type, incident, orderedLink} (flat arrays, one call per batch).  Query q is
+ *   And{ Or over types[type_off[q] .. type_off[q+1])        AtomTypeCondition (one type) or
+ *                                                          TypePlusCondition (base + subtypes, expanded to an
+ *                                                          Or, C/query/cond2qry/ExpressionBasedQuery.java:606-627);
+ *                                                          none = no type condition,
+ *        IncidentCondition(inc[inc_off[q] .. inc_off[q+1]))  (also LinkCondition targets, :739-746),
+ *        PositionedIncidentCondition(target, lb, ub, complement) for the 4-int records
+ *                 pos[4k .. 4k+4), k in [pos_off[q], pos_off[q+1])
+ *                 (C/query/PositionedIncidentCondition.java:123-177, PositionedIncidentToQuery.java),
+ *        OrderedLinkCondition(pat[pat_off[r] .. pat_off[r+1])) for r in [pset_off[q], pset_off[q+1]),
+ *        ArityCondition(arity[q]) unless arity[q] < 0 (C/query/ArityCondition.java:49-67) }.
+ * Every query needs an incidence anchor (an incident target, a non-ANY pattern target or a positioned
+ * target), else HGX_E_UNSUPPORTED for the batch.  Results as hgx_pattern_batch. */
+int  hgx_pattern_batch_ext(hgx_graph *g, int32_t n, const int64_t *type_off, const int32_t *types,
+                           const int64_t *inc_off, const int32_t *inc, const int64_t *pos_off, const int32_t *pos,
+                           const int64_t *pset_off, const int64_t *pat_off, const int32_t *pat,
+                           const int32_t *arity, hgx_query_result **out);
 /* offsets[n+1]: results of query q are ids[offsets[q] .. offsets[q+1]). */
 int  hgx_query_result_offsets(const hgx_query_result *r, int64_t *offsets);
 int  hgx_query_result_ids(const hgx_query_result *r, int32_t *ids);

@@ -739,6 +739,144 @@ int64_t og_and_query_sets(const og_graph *g, int32_t type, const int32_t *incide
     return and_query_impl(g, type, incident, n_incident, pattern, m, has_ordered, out, cap, 0);
 }
 
+/* ------------------------------------------------------------------------- */
+/* Extended And: TypePlus / Link / PositionedIncident / Arity / several orderedLinks */
+/* ------------------------------------------------------------------------- */
+
+int og_positioned(const int32_t *t, int32_t n, int32_t x, int32_t lb, int32_t ub, int32_t complement)
+{
+    /* C/query/PositionedIncidentCondition.java:146-176 */
+    if (ub < 0) ub = n + ub;
+    if (lb < 0) lb = n + lb;
+    if (lb > ub || lb < 0 || ub < 0 || lb >= n || ub >= n) return 0;
+    if (complement) {
+        for (int32_t i = 0; i < lb; i++) if (t[i] == x) return 1;
+        for (int32_t i = ub + 1; i < n; i++) if (t[i] == x) return 1;
+        return 0;
+    }
+    for (int32_t i = lb; i <= ub; i++) if (t[i] == x) return 1;
+    return 0;
+}
+
+typedef struct { const int32_t *a; int64_t n; int32_t *own; } ext_list;
+
+static int cmp_ext_list(const void *x, const void *y)
+{
+    const ext_list *a = (const ext_list *)x, *b = (const ext_list *)y;
+    return (a->n > b->n) - (a->n < b->n);
+}
+
+static int cmp_i32(const void *x, const void *y)
+{
+    int32_t a = *(const int32_t *)x, b = *(const int32_t *)y;
+    return (a > b) - (a < b);
+}
+
+static int64_t bsearch_i32(const int32_t *a, int64_t n, int32_t key)
+{
+    int64_t lo = 0, hi = n - 1;
+    while (lo <= hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1;
+        else if (a[mid] > key) hi = mid - 1;
+        else return mid;
+    }
+    return -1;
+}
+
+/* One And of the DNF (one type or none): the ascending intersection of its ORA sets
+ * (AndToQuery.java:164-217) filtered by its predicates (:277-293).  Appends to buf. */
+static int64_t ext_one_and(const og_graph *g, int32_t type, const int32_t *anchors, int32_t na,
+                           const int32_t *pos, int32_t n_pos, int32_t n_pat, const int64_t *pat_off,
+                           const int32_t *pat, int32_t arity, int32_t **buf, int64_t *bcap, int64_t nb)
+{
+    int32_t nl = na + n_pos + (type >= 0 ? 1 : 0);
+    ext_list *L = (ext_list *)calloc((size_t)(nl > 0 ? nl : 1), sizeof(ext_list));
+    int32_t k = 0;
+    if (type >= 0) {   /* the type index (links only) */
+        if (type < g->n_types) { L[k].a = g->type_atoms + g->type_off[type]; L[k].n = g->type_off[type + 1] - g->type_off[type]; }
+        k++;
+    }
+    for (int32_t i = 0; i < na; i++, k++) {
+        L[k].a = g->inc_atom + g->inc_off[anchors[i]];
+        L[k].n = g->inc_off[anchors[i] + 1] - g->inc_off[anchors[i]];
+    }
+    for (int32_t s = 0; s < n_pos; s++, k++) {   /* PositionedIncidentToQuery: inc(target) filtered */
+        int32_t x = pos[4 * s];
+        const int32_t *inc = g->inc_atom + g->inc_off[x];
+        int64_t m = g->inc_off[x + 1] - g->inc_off[x], c = 0;
+        int32_t *f = (int32_t *)malloc(sizeof(int32_t) * (size_t)(m > 0 ? m : 1));
+        for (int64_t i = 0; i < m; i++) {
+            int32_t row = g->atom_row[inc[i]];
+            if (og_positioned(g->tgt_idx + g->tgt_off[row], (int32_t)(g->tgt_off[row + 1] - g->tgt_off[row]), x,
+                              pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3]))
+                f[c++] = inc[i];
+        }
+        L[k].a = f; L[k].n = c; L[k].own = f;
+    }
+    qsort(L, (size_t)nl, sizeof(ext_list), cmp_ext_list);
+    for (int64_t i = 0; i < (nl > 0 ? L[0].n : 0); i++) {
+        int32_t h = L[0].a[i];
+        int ok = 1;
+        for (int32_t j = 1; j < nl && ok; j++) ok = bsearch_i32(L[j].a, L[j].n, h) >= 0;
+        if (!ok) continue;
+        int32_t row = g->atom_row[h];
+        const int32_t *t = g->tgt_idx + g->tgt_off[row];
+        int32_t ar = (int32_t)(g->tgt_off[row + 1] - g->tgt_off[row]);
+        if (arity >= 0 && ar != arity) continue;   /* ArityCondition: layout.length == arity + 2 */
+        for (int32_t r = 0; r < n_pat && ok; r++)
+            ok = og_ordered_link(t, ar, pat + pat_off[r], (int32_t)(pat_off[r + 1] - pat_off[r]));
+        if (!ok) continue;
+        if (nb >= *bcap) {
+            *bcap = *bcap * 2 + 64;
+            *buf = (int32_t *)realloc(*buf, sizeof(int32_t) * (size_t)*bcap);
+        }
+        (*buf)[nb++] = h;
+    }
+    for (int32_t j = 0; j < nl; j++) free(L[j].own);
+    free(L);
+    return nb;
+}
+
+int64_t og_and_query_ext(const og_graph *g, int32_t n_types, const int32_t *types, int32_t n_inc,
+                         const int32_t *inc, int32_t n_pos, const int32_t *pos, int32_t n_pat,
+                         const int64_t *pat_off, const int32_t *pat, int32_t arity, int32_t *out, int64_t cap)
+{
+    /* expand: incident targets, then every non-ANY pattern target (deduplicated) */
+    int64_t maxa = n_inc + (n_pat > 0 ? pat_off[n_pat] - pat_off[0] : 0) + 1;
+    int32_t *anchors = (int32_t *)malloc(sizeof(int32_t) * (size_t)maxa);
+    int32_t na = 0;
+    for (int64_t i = 0; i < maxa - 1; i++) {
+        int32_t h = i < n_inc ? inc[i] : pat[pat_off[0] + (i - n_inc)];
+        if (i >= n_inc && h < 0) continue;   /* anyHandle */
+        if (h < 0 || h >= g->A) { free(anchors); return -2; }
+        int dup = 0;
+        for (int32_t k = 0; k < na; k++) if (anchors[k] == h) { dup = 1; break; }
+        if (!dup) anchors[na++] = h;
+    }
+    for (int32_t s = 0; s < n_pos; s++)
+        if (pos[4 * s] < 0 || pos[4 * s] >= g->A) { free(anchors); return -2; }
+    if (na == 0 && n_pos == 0) { free(anchors); return -1; }
+    for (int32_t r = 0; r < n_pat; r++)
+        if (pat_off[r + 1] == pat_off[r]) { free(anchors); return 0; }   /* QueryMetaData.EMPTY -> NOP */
+    int32_t *buf = NULL;
+    int64_t bcap = 0, nb = 0;
+    if (n_types == 0) {
+        nb = ext_one_and(g, -1, anchors, na, pos, n_pos, n_pat, pat_off, pat, arity, &buf, &bcap, nb);
+    } else {
+        for (int32_t t = 0; t < n_types; t++) {   /* toDNF: one And per type of the Or, united */
+            int dup = 0;
+            for (int32_t u = 0; u < t; u++) if (types[u] == types[t]) dup = 1;
+            if (!dup) nb = ext_one_and(g, types[t], anchors, na, pos, n_pos, n_pat, pat_off, pat, arity, &buf, &bcap, nb);
+        }
+        if (nb > 1) qsort(buf, (size_t)nb, sizeof(int32_t), cmp_i32);
+    }
+    for (int64_t i = 0; i < nb && i < cap; i++) out[i] = buf[i];
+    free(buf);
+    free(anchors);
+    return nb;
+}
+
 int og_and_query_many(const og_graph *g, int32_t n, const int32_t *q_type,
                       const int64_t *q_inc_off, const int32_t *q_inc,
                       const int64_t *q_pat_off, const int32_t *q_pat, const int32_t *q_has_ordered,

@@ -114,6 +114,25 @@ int64_t og_and_query_sets(const og_graph *g, int32_t type, const int32_t *incide
                           const int32_t *pattern, int32_t m, int32_t has_ordered,
                           int32_t *out, int64_t cap);
 
+/* PositionedIncidentCondition.satisfies on a target array
+ * (C/query/PositionedIncidentCondition.java:123-177): x within [lb, ub] (negative bounds count
+ * from the end; complement = anywhere outside the range); invalid ranges never match. */
+int og_positioned(const int32_t *tgts, int32_t arity, int32_t x, int32_t lb, int32_t ub, int32_t complement);
+
+/* The extended And of hgx_pattern_batch_ext, restated with set semantics:
+ *   TypePlusCondition -> Or of AtomTypeConditions (ExpressionBasedQuery.java:606-627), distributed
+ *   over the And by toDNF -> one And per type, results united; LinkCondition / OrderedLinkCondition
+ *   targets -> IncidentConditions (:730-746); each And = intersection of its ORA sets (type index,
+ *   incidence sets, position-filtered incidence sets of PositionedIncidentToQuery) filtered by the
+ *   OrderedLinkCondition and ArityCondition predicates (AndToQuery.java:120-294).
+ * n_types == 0: no type condition.  pos: 4 ints per positioned condition (target, lb, ub,
+ * complement).  Pattern r is pat[pat_off[r] .. pat_off[r+1]), r < n_pat.  arity < 0: none.
+ * Returns the ascending result count (may exceed cap), -1 when there is no incidence anchor, -2 on a
+ * bad id. */
+int64_t og_and_query_ext(const og_graph *g, int32_t n_types, const int32_t *types, int32_t n_inc,
+                         const int32_t *inc, int32_t n_pos, const int32_t *pos, int32_t n_pat,
+                         const int64_t *pat_off, const int32_t *pat, int32_t arity, int32_t *out, int64_t cap);
+
 /* Batched pattern queries on all cores (CPU baseline).  Queries are packed:
  * q_type[n], q_inc_off[n+1] into q_inc, q_pat_off[n+1] into q_pat, q_has_ordered[n].
  * counts[n] receives result sizes; checksum receives the sum of result ids. */

@@ -67,6 +67,11 @@ def lib():
         L.og_and_query_many.argtypes = [C.POINTER(OgGraph), C.c_int32, i32p, i64p, i32p, i64p, i32p, i32p,
                                         i64p, C.POINTER(C.c_int64), C.c_int32]
         L.og_and_query_many.restype = C.c_int
+        L.og_positioned.argtypes = [i32p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+        L.og_positioned.restype = C.c_int
+        L.og_and_query_ext.argtypes = [C.POINTER(OgGraph), C.c_int32, i32p, C.c_int32, i32p, C.c_int32, i32p,
+                                       C.c_int32, i64p, i32p, C.c_int32, i32p, C.c_int64]
+        L.og_and_query_ext.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -170,6 +175,29 @@ class OracleGraph:
                 return out[:n]
             cap = n
 
+    def and_query_ext(self, types=(), incident=(), positioned=(), patterns=(), arity=-1):
+        """Extended And (see og_and_query_ext): positioned = [(target, lb, ub, complement)],
+        patterns = [tuple of ids, -1 = anyHandle].  None = not accelerated (no anchor)."""
+        ty = np.ascontiguousarray(list(types) or [0], np.int32)
+        ic = np.ascontiguousarray(list(incident) or [0], np.int32)
+        ps = np.ascontiguousarray([x for p in positioned for x in p] or [0], np.int32)
+        po = np.zeros(len(patterns) + 1, np.int64)
+        flat = []
+        for r, p in enumerate(patterns):
+            flat.extend(p)
+            po[r + 1] = len(flat)
+        pt = np.ascontiguousarray(flat or [0], np.int32)
+        cap = 1024
+        while True:
+            out = np.empty(cap, np.int32)
+            n = lib().og_and_query_ext(C.byref(self.g), len(types), ty, len(incident), ic, len(positioned), ps,
+                                       len(patterns), po, pt, int(arity), out, cap)
+            if n < 0:
+                return None if n == -1 else n
+            if n <= cap:
+                return out[:n]
+            cap = n
+
     def and_query_many(self, q_type, q_inc_off, q_inc, q_pat_off, q_pat, q_has_ordered, nthreads=0):
         n = len(q_type)
         counts = np.zeros(n, np.int64)
@@ -182,6 +210,11 @@ class OracleGraph:
                                      np.ascontiguousarray(q_has_ordered, np.int32), counts, C.byref(cs),
                                      int(nthreads))
         return counts, cs.value, rc
+
+
+def positioned(targets, x, lb, ub, complement=False):
+    t = np.ascontiguousarray(list(targets) or [0], np.int32)
+    return bool(lib().og_positioned(t, len(targets), int(x), int(lb), int(ub), int(bool(complement))))
 
 
 def ordered_link(targets, pattern):

@@ -230,6 +230,48 @@ def and_query(g, type_=None, incident=(), pattern=None):
     return res
 
 
+def positioned(targets, x, lb, ub, complement=False):
+    """PositionedIncidentCondition.satisfies (C/query/PositionedIncidentCondition.java:123-177)."""
+    n = len(targets)
+    if ub < 0:
+        ub += n
+    if lb < 0:
+        lb += n
+    if lb > ub or lb < 0 or ub < 0 or lb >= n or ub >= n:
+        return False
+    inside = [i for i in range(n) if targets[i] == x and lb <= i <= ub]
+    outside = [i for i in range(n) if targets[i] == x and not lb <= i <= ub]
+    return bool(outside) if complement else bool(inside)
+
+
+def and_query_ext(g, types=(), incident=(), positioned_=(), patterns=(), arity=None):
+    """Set semantics of the extended And: Or over types (TypePlusCondition), incident anchors (also
+    LinkCondition / orderedLink targets), position-filtered incidence sets, every orderedLink and
+    the arity as predicates.  None = not accelerated (no anchor)."""
+    anchors = []
+    for h in list(incident) + [p for pat in patterns for p in pat if p != ANY]:
+        if h not in anchors:
+            anchors.append(h)
+    if not anchors and not positioned_:
+        return None
+    if any(len(p) == 0 for p in patterns):
+        return []
+    sets = [set(g.inc[a]) for a in anchors]
+    for (x, lb, ub, c) in positioned_:
+        sets.append({l for l in g.inc[x] if positioned(g.targets(l), x, lb, ub, c)})
+    cand = set.intersection(*sets)
+    res = []
+    for l in sorted(cand):
+        if types and g.type_of(l) not in set(types):
+            continue
+        if arity is not None and arity >= 0 and len(g.targets(l)) != arity:
+            continue
+        if not all(ordered_link(g.targets(l), p) for p in patterns):
+            continue
+        res.append(l)
+    return res
+
+
 # ----------------------------------------------------------------------------
 # Closed-form neighbour rule used by the GPU kernels (see DESIGN.md section 3.2).
 # Tested exhaustively against AdjIterator above (tests/test_oracle.py).

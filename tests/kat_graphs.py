@@ -88,6 +88,26 @@ def compilation_graph():
     return b.arrays()
 
 
+def positioned_graph():
+    """TC/query/Queries.java:208-221 testPositionedLinkCondition: ten atoms A0..A9 and five plain
+    links over all of them in order (plus the queries graph's shape of an unrelated link)."""
+    b = Builder()
+    A = [b.node(f"A{i}") for i in range(10)]
+    for i in range(5):
+        b.link(f"L{i}", T_PLAIN, *A)
+    b.link("other", T_TESTLINK, A[3], A[0])
+    return b.arrays()
+
+
+def positioned_truth_table(g):
+    """(target, lower, upper, complement, contains all five links?, empty?) -- Queries.java:217-220,
+    plus the complement forms of hg.incidentNotAt."""
+    n = g["names"]
+    return [(n["A0"], 0, 0, False, True, False), (n["A9"], -1, -1, False, True, False),
+            (n["A5"], 3, 7, False, True, False), (n["A3"], -4, -1, False, False, True),
+            (n["A3"], -4, -1, True, True, False), (n["A5"], 3, 7, True, False, True)]
+
+
 def ordered_link_truth_table(g):
     """TC/query/Queries.java:178-206 on linkH = (n0, n1): (pattern, expected)."""
     n = g["names"]

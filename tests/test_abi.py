@@ -58,11 +58,19 @@ def test_handle_ranking_is_byte_order():
 def test_and_normalisation():
     from hypergraphdb_amd import HGXUnsupported, hg
     from hypergraphdb_amd.query import normalize
-    t, inc, pat = normalize(hg.and_(hg.type(3), hg.incident(5), hg.and_(hg.orderedLink(1, hg.anyHandle(), 2))))
-    assert t == 3 and inc == [5] and pat == (1, -1, 2)
+    q = normalize(hg.and_(hg.type(3), hg.incident(5), hg.and_(hg.orderedLink(1, hg.anyHandle(), 2))))
+    assert q == {"types": [3], "inc": [5], "pos": [], "patterns": [(1, -1, 2)], "arity": -1}
+    # several orderedLinks are predicates of one And; LinkCondition expands to incidents (ANY dropped)
+    q = normalize(hg.and_(hg.orderedLink(1), hg.orderedLink(2), hg.link(7, hg.anyHandle(), 8)))
+    assert q["patterns"] == [(1,), (2,)] and q["inc"] == [7, 8]
+    q = normalize(hg.and_(hg.incidentAt(4, -1), hg.incidentNotAt(5, 0, 2), hg.arity(3), hg.typePlus([2, 1])))
+    assert q["pos"] == [(4, -1, -1, 0), (5, 0, 2, 1)] and q["arity"] == 3 and q["types"] == [1, 2]
+    # every type condition must hold: typePlus sets intersect with exact types
+    assert normalize(hg.and_(hg.typePlus([1, 2]), hg.type(2), hg.incident(0)))["types"] == [2]
+    assert normalize(hg.and_(hg.type(1), hg.type(2), hg.incident(0))) == "empty"
+    assert normalize(hg.and_(hg.arity(1), hg.arity(2), hg.incident(0))) == "empty"
     with pytest.raises(HGXUnsupported):
-        normalize(hg.and_(hg.orderedLink(1), hg.orderedLink(2)))
-    assert normalize(hg.and_(hg.type(1), hg.type(2), hg.incident(0)))[0] == "empty"
+        normalize(hg.and_(hg.incident(1), hg.bfs(2)))
 
 
 def test_generator_deterministic_and_valid():

@@ -131,3 +131,92 @@ def test_unsupported_and_empty_shapes():
         pattern_batch(snap, [(-1, [], (-1, -1))])
     r = pattern_batch(snap, [(-1, [g["names"]["n0"]], ())])      # empty orderedLink -> NOP
     assert r[0].tolist() == []
+
+
+# --- extended And: PositionedIncident / Link / Arity / TypePlus / several orderedLinks ---------
+
+def test_positioned_kat_through_engine():
+    """TC/query/Queries.java:208-221 testPositionedLinkCondition (and hg.incidentNotAt)."""
+    from hypergraphdb_amd import find_all, hg
+    g = K.positioned_graph()
+    snap = snapshot(g)
+    links = {g["names"][f"L{i}"] for i in range(5)}
+    for x, lb, ub, comp, contains, empty in K.positioned_truth_table(g):
+        cond = hg.incidentNotAt(x, lb, ub) if comp else hg.incidentAt(x, lb, ub)
+        got = find_all(snap, cond)
+        assert (links <= set(got)) if contains else not (links & set(got)), (x, lb, ub, comp)
+        if empty:
+            assert got == []
+
+
+def test_link_arity_and_multiple_patterns():
+    from hypergraphdb_amd import find_all, hg
+    g = K.queries_graph()
+    snap, orc = snapshot(g), oracle(g)
+    n = g["names"]
+    assert find_all(snap, hg.and_(hg.link(n["n0"], n["n1"]), hg.arity(2))) == [n["linkH"]]
+    assert find_all(snap, hg.and_(hg.link(n["n0"], n["n1"]), hg.arity(3))) == []
+    assert find_all(snap, hg.and_(hg.incident(n["n2"]), hg.arity(3))) == [n["linkH1"]]
+    assert find_all(snap, hg.and_(hg.arity(2), hg.arity(3), hg.incident(n["n0"]))) == []
+    q = hg.and_(hg.orderedLink(n["n4"], hg.anyHandle(), n["n6"]), hg.orderedLink(n["n2"], n["linkH1"]))
+    assert find_all(snap, q) == [n["link5"]]
+    assert find_all(snap, q) == orc.and_query_ext([], [], [], [(n["n4"], -1, n["n6"]), (n["n2"], n["linkH1"])]).tolist()
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_ext_random_vs_oracle(case):
+    """Random extended Ands (type sets, incident, positioned, 0-2 orderedLinks, arity) on graphs with
+    links targeting links and repeated targets: identical ascending result sets."""
+    from hypergraphdb_amd import pattern_batch
+    rng = np.random.default_rng(1200 + case)
+    g = K.random_graph(rng, 300, 3000, max_arity=8, n_types=5, link_targets=case % 2 == 0)
+    snap, orc = snapshot(g), oracle(g)
+    A = g["num_atoms"]
+    qs, exp = [], []
+    while len(qs) < 2000:
+        types = sorted({int(t) for t in rng.integers(0, 5, int(rng.integers(0, 3)))})
+        inc = [int(x) for x in rng.integers(0, A, int(rng.integers(0, 3)))]
+        pos = [(int(rng.integers(0, A)), int(rng.integers(-5, 6)), int(rng.integers(-5, 6)), int(rng.integers(0, 2)))
+               for _ in range(int(rng.integers(0, 3)))]
+        pats = [tuple(int(x) if rng.random() < 0.6 else -1 for x in rng.integers(0, A, int(rng.integers(1, 4))))
+                for _ in range(int(rng.integers(0, 3)))]
+        ar = int(rng.integers(-1, 7))
+        e = orc.and_query_ext(types, inc, pos, pats, ar)
+        if e is None:
+            continue   # no incidence anchor: stays on AndToQuery (HGX_E_UNSUPPORTED)
+        qs.append({"types": types, "inc": inc, "pos": pos, "patterns": pats, "arity": ar})
+        exp.append(e.tolist())
+    r = pattern_batch(snap, qs)
+    for q in range(len(qs)):
+        assert r[q].tolist() == exp[q], qs[q]
+
+
+def test_type_plus_from_subsumption():
+    """hg.and(hg.typePlus(base), hg.incident(a)): the subtypes come from a GPU HGSubsumes closure
+    (TypePlusCondition.fetchSubTypes, C/query/TypePlusCondition.java:26-43)."""
+    from hypergraphdb_amd import find_all, hg
+    from hypergraphdb_amd.query import TypePlusCondition
+    from oracle_ctypes import algen
+    b = K.Builder()
+    S = 9                                             # HGSubsumes type key
+    tys = [b.node(f"T{i}") for i in range(6)]         # type atoms; key of T_i is i
+    for gen_, spec in ((0, 1), (0, 2), (1, 3), (3, 4)):
+        b.link(None, S, tys[gen_], tys[spec])         # HGSubsumes(general, specific)
+    x = [b.node(f"x{i}") for i in range(8)]
+    rng = np.random.default_rng(4)
+    for i in range(60):
+        t = int(rng.integers(0, 6))
+        b.link(None, t, *[int(v) for v in rng.choice(x, int(rng.integers(1, 5)), replace=False)])
+    g = b.arrays()
+    snap, orc = snapshot(g), oracle(g)
+    key_of = {tys[i]: i for i in range(6)}
+    tp = TypePlusCondition.from_subsumption(snap, tys[1], S, key_of)
+    assert tp.types == {1, 3, 4}
+    lv = orc.bfs_levels(tys[0], -1, algen(S, False, True, False, False))
+    assert TypePlusCondition.from_subsumption(snap, tys[0], S, key_of).types == {key_of[int(a)] for l in lv for a in l}
+    for a in x:
+        got = find_all(snap, hg.and_(hg.typePlus(tp), hg.incident(a)))
+        assert got == orc.and_query_ext(sorted(tp.types), [a]).tolist()
+        both = find_all(snap, hg.and_(hg.typePlus(tp), hg.type(3), hg.incident(a)))
+        assert both == orc.and_query_ext([3], [a]).tolist()
+        assert find_all(snap, hg.and_(hg.typePlus(tp), hg.type(2), hg.incident(a))) == []

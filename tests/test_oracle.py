@@ -213,3 +213,71 @@ def test_closed_form_neighbour_rule_exhaustive():
                     got.discard(v)
                     want = {t for t in atoms if t != v and pyref.reachable(m, list(tg), v, t)}
                     assert got == want, (tg, mode, v)
+
+
+# --- extended And: PositionedIncident / Link / Arity / TypePlus / several orderedLinks ---------
+
+def _ext_graphs():
+    g = K.positioned_graph()
+    rg = [K.random_graph(np.random.default_rng(s), 120, 300, max_arity=7, n_types=4) for s in (5, 6)]
+    return [g] + rg
+
+
+def test_positioned_kat_queries_java():
+    """TC/query/Queries.java:208-221 on both restatements."""
+    import pyref
+    g = K.positioned_graph()
+    orc, pgr = og(g), pg(g)
+    links = [g["names"][f"L{i}"] for i in range(5)]
+    for x, lb, ub, comp, contains, empty in K.positioned_truth_table(g):
+        got = orc.and_query_ext(positioned=[(x, lb, ub, int(comp))]).tolist()
+        assert got == pyref.and_query_ext(pgr, positioned_=[(x, lb, ub, comp)])
+        assert set(links) <= set(got) if contains else not (set(links) & set(got))
+        if empty:
+            assert got == []
+
+
+def test_positioned_predicate_exhaustive():
+    """og_positioned == pyref.positioned on every target array of arity <= 4 over 3 symbols."""
+    import itertools
+    import pyref
+    from oracle_ctypes import positioned
+    for n in range(0, 5):
+        for row in itertools.product(range(3), repeat=n):
+            for lb in range(-5, 5):
+                for ub in range(-5, 5):
+                    for c in (False, True):
+                        assert positioned(row, 1, lb, ub, c) == pyref.positioned(list(row), 1, lb, ub, c)
+
+
+def test_ext_queries_oracle_vs_pyref():
+    import pyref
+    for g in _ext_graphs():
+        orc, pgr = og(g), pg(g)
+        rng = np.random.default_rng(g["num_atoms"])
+        A = g["num_atoms"]
+        for _ in range(400):
+            types = sorted({int(t) for t in rng.integers(0, 4, int(rng.integers(0, 3)))})
+            inc = [int(x) for x in rng.integers(0, A, int(rng.integers(0, 3)))]
+            pos = [(int(rng.integers(0, A)), int(rng.integers(-4, 5)), int(rng.integers(-4, 5)), int(rng.integers(0, 2)))
+                   for _ in range(int(rng.integers(0, 3)))]
+            pats = [tuple(int(x) if rng.random() < 0.6 else -1 for x in rng.integers(0, A, int(rng.integers(1, 4))))
+                    for _ in range(int(rng.integers(0, 3)))]
+            ar = int(rng.integers(-1, 6))
+            a = orc.and_query_ext(types, inc, pos, pats, ar)
+            b = pyref.and_query_ext(pgr, types, inc, pos, pats, ar if ar >= 0 else None)
+            assert (a is None and b is None) or a.tolist() == b, (types, inc, pos, pats, ar)
+
+
+def test_ext_reduces_to_base_and():
+    """With one type and one pattern the extended And is the literal zig-zag And."""
+    for g in _ext_graphs():
+        orc = og(g)
+        rng = np.random.default_rng(3)
+        for _ in range(300):
+            t = int(rng.integers(-1, 4))
+            inc = [int(x) for x in rng.integers(0, g["num_atoms"], int(rng.integers(1, 3)))]
+            pat = tuple(int(x) if rng.random() < 0.6 else -1 for x in rng.integers(0, g["num_atoms"], 3))
+            a = orc.and_query_ext([] if t < 0 else [t], inc, [], [pat], -1)
+            b = orc.and_query(t, inc, pat)
+            assert a.tolist() == b.tolist()
