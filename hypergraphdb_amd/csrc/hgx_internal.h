@@ -139,6 +139,11 @@ struct hgx_graph {
     int64_t* inc_off = nullptr;
     int32_t* inc_row = nullptr;
     int32_t* inc_type = nullptr;    // [I] link_type[inc_row[i]]: streamed type filter of the query path
+    // Type-grouped incidence (built on the first pattern query): inside each atom's segment the link
+    // rows ordered by (type, row), so the links of one type incident to an atom are one contiguous,
+    // ascending range (found by binary search over inc_ts_type).
+    int32_t* inc_ts_row = nullptr;
+    int32_t* inc_ts_type = nullptr;
 
     int64_t n_heavy = 0;            // heavy atoms (deg > kHeavyDegree)
     int64_t I_heavy = 0;            // incidence entries of heavy atoms

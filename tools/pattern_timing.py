@@ -17,11 +17,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--calls", type=int, default=30)
+    ap.add_argument("--queries", type=int, default=10_000)
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
     from hypergraphdb_amd.query import pattern_batch_arrays
-    g = synth.config3(scale=args.scale, n_queries=10_000)
+    g = synth.config3(scale=args.scale, n_queries=args.queries)
     Q = g["queries"]
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     snap.set_timing(True)
@@ -37,7 +38,7 @@ def main():
         devs.append(r.ms["ms_total"])
     w, d = np.array(walls[3:]), np.array(devs[3:])
     print(f"wall ms: median {np.median(w):.3f} min {w.min():.3f} max {w.max():.3f}; "
-          f"device ms: median {np.median(d):.3f}; results {int(r.offsets[-1])}")
+          f"device ms: median {np.median(d):.3f}; match ms {r.ms['ms_match']:.3f}; results {int(r.offsets[-1])}")
     print("walls", [round(x, 3) for x in walls])
 
 
