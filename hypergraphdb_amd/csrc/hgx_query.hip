@@ -96,8 +96,11 @@ __device__ __forceinline__ bool positioned(const int32_t* __restrict__ row, int 
 // keeps the rows of one (atom, type) ascending.
 __global__ void __launch_bounds__(256) k_ts_keys(int64_t A, const int64_t* __restrict__ inc_off,
                                                  const int32_t* __restrict__ inc_type, u64* __restrict__ keys) {
-    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A; a += (int64_t)gridDim.x * blockDim.x)
-        for (int64_t i = inc_off[a]; i < inc_off[a + 1]; ++i) keys[i] = ((u64)a << 32) | (uint32_t)inc_type[i];
+    const int lane = threadIdx.x & 63;   // a wave per atom: hub rows are written 64 entries at a time
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t a = wave; a < A; a += nwave)
+        for (int64_t i = inc_off[a] + lane; i < inc_off[a + 1]; i += 64) keys[i] = ((u64)a << 32) | (uint32_t)inc_type[i];
 }
 
 __global__ void __launch_bounds__(256) k_low32(int64_t n, const u64* __restrict__ keys, int32_t* __restrict__ out) {
@@ -512,7 +515,7 @@ void ensure_type_grouped(hgx_graph* g) {
     u64* keys = (u64*)g->alloc(sizeof(u64) * I);
     u64* keys2 = (u64*)g->alloc(sizeof(u64) * I);
     int32_t* rows2 = (int32_t*)g->alloc(sizeof(int32_t) * I);
-    k_ts_keys<<<grid_for(g->A, 256), 256, 0, s>>>(g->A, g->inc_off, g->inc_type, keys);
+    k_ts_keys<<<grid_for(g->A * 64, 256, 16384), 256, 0, s>>>(g->A, g->inc_off, g->inc_type, keys);
     HGX_CHECK_LAUNCH();
     int end_bit = 64;
     {

@@ -22,10 +22,15 @@ import sys
 from collections import defaultdict
 
 
+# kernels that implement one engine kind (HGX_K_* of include/hgx.h): the tile-staged dense kernels
+# report under the kind's name so bench.py finds their PMC bytes
+KIND = {"hgx_link_gather2": "hgx_link_gather", "hgx_atom_pull2": "hgx_atom_pull"}
+
+
 def short(name):
     m = re.search(r"\b(hgx_[A-Za-z0-9_]+|k_[A-Za-z0-9_]+)\b", name)
     if m:
-        return m.group(1)
+        return KIND.get(m.group(1), m.group(1))
     if "radix_sort" in name:
         return "rocprim_radix_sort"
     if "scan" in name:
