@@ -12,6 +12,6 @@ from .algorithms import (AtomTypeCondition, BfsResult, DefaultALGenerator, HGBre
                          HGException, bfs_batch)
 from .query import (ArityCondition, GpuAndToQuery, HGQueryConfiguration, LinkCondition,  # noqa: F401
                     PositionedIncidentCondition, TypePlusCondition, find_all, hg, pattern_batch)
-from .snapshot import HyperGraphSnapshot, rank_handles  # noqa: F401
+from .snapshot import HyperGraphSnapshot, export_store, rank_handles, read_snapshot, write_snapshot  # noqa: F401
 
 __version__ = "0.1.0"

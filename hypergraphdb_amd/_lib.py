@@ -36,6 +36,8 @@ EXPORTED = (
     "hgx_query_result_ms", "hgx_query_result_free",
     "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_free", "hgx_shard_graph_create",
     "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
+    "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
+    "hgx_graph_update",
 )
 
 
@@ -147,6 +149,13 @@ def lib():
         "hgx_comm_destroy": ([vp], None),
         "hgx_pbfs_batch": ([vp, vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
         "hgx_pbfs_batch_group": ([vp, i32, vp, i32, i32, C.POINTER(AlgenOpts), vp], C.c_int),
+        "hgx_snapshot_write": ([C.c_char_p, C.POINTER(GraphDesc), vp, i32], C.c_int),
+        "hgx_snapshot_info": ([C.c_char_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i32),
+                               C.POINTER(i32)], C.c_int),
+        "hgx_snapshot_read": ([C.c_char_p, vp, vp, vp, vp, vp], C.c_int),
+        "hgx_graph_open": ([C.c_char_p, i32, C.POINTER(vp)], C.c_int),
+        "hgx_graph_export": ([vp, vp, vp, vp, vp], C.c_int),
+        "hgx_graph_update": ([vp, i64, i64, vp, vp, vp, vp, i64, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -10,6 +10,7 @@ C = core/src/java/org/hypergraphdb in the reference.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -38,32 +39,178 @@ def rank_handles(handles) -> dict:
     return ranks
 
 
+def _desc(num_atoms, link_atom, tgt_off, tgt_idx, link_type):
+    return _lib.GraphDesc(int(num_atoms), len(link_atom), ptr(link_atom), ptr(tgt_off), ptr(tgt_idx), ptr(link_type))
+
+
+def _export(h, with_targets=True):
+    """D2H of the device rows (hgx_graph_export) -> (num_atoms, link_atom, tgt_off, link_type[, tgt_idx])."""
+    a, m, i = C.c_int64(), C.c_int64(), C.c_int64()
+    check(lib().hgx_graph_info(h, C.byref(a), C.byref(m), C.byref(i)))
+    la = np.empty(m.value, np.int32)
+    off = np.empty(m.value + 1, np.int64)
+    ty = np.empty(m.value, np.int32)
+    check(lib().hgx_graph_export(h, ptr(la), ptr(off), None, ptr(ty)))
+    if not with_targets:
+        return a.value, la, off, ty
+    tg = np.empty(int(off[-1]), np.int32)
+    check(lib().hgx_graph_export(h, None, None, ptr(tg), None))
+    return a.value, la, off, ty, tg
+
+
+def _handle_table(handles, num_atoms):
+    if handles is None:
+        return None, 0
+    rows = [handle_bytes(h) for h in handles]
+    if len(rows) != num_atoms:
+        raise ValueError("the handle table needs one handle per atom rank")
+    width = len(rows[0]) if rows else 0
+    if any(len(r) != width for r in rows) or width > 64:
+        raise ValueError("handles must have one byte width (<= 64)")
+    return np.frombuffer(b"".join(rows), np.uint8).copy(), width
+
+
+def write_snapshot(path, num_atoms, link_atom, tgt_off, tgt_idx, link_type=None, handles=None):
+    """hgx_snapshot_write: the bipartite CSR (+ optional rank-ordered handle table) as a .hgcsr file."""
+    la = np.ascontiguousarray(link_atom, np.int32)
+    off = np.ascontiguousarray(tgt_off, np.int64)
+    tg = np.ascontiguousarray(tgt_idx, np.int32)
+    ty = None if link_type is None else np.ascontiguousarray(link_type, np.int32)
+    if len(off) != len(la) + 1:
+        raise ValueError("tgt_off must have num_links + 1 entries")
+    if len(off) and int(off[-1]) != len(tg) or (ty is not None and len(ty) != len(la)):
+        raise ValueError("tgt_idx / link_type sizes do not match tgt_off / link_atom")
+    tab, width = _handle_table(handles, int(num_atoms))
+    desc = _desc(num_atoms, la, off, tg, ty)
+    check(lib().hgx_snapshot_write(os.fsencode(path), C.byref(desc), ptr(tab), width))
+
+
+def read_snapshot(path) -> dict:
+    """hgx_snapshot_read (checksum-verified): num_atoms, link_atom, tgt_off, tgt_idx, link_type (None
+    when the file has none) and handles (uint8 [A, width] or None).  No device needed."""
+    a, m, p = C.c_int64(), C.c_int64(), C.c_int64()
+    hb, ht = C.c_int32(), C.c_int32()
+    bpath = os.fsencode(path)
+    check(lib().hgx_snapshot_info(bpath, C.byref(a), C.byref(m), C.byref(p), C.byref(hb), C.byref(ht)))
+    la = np.empty(m.value, np.int32)
+    off = np.empty(m.value + 1, np.int64)
+    tg = np.empty(p.value, np.int32)
+    ty = np.empty(m.value, np.int32)
+    hs = np.empty((a.value, hb.value), np.uint8) if hb.value else None
+    check(lib().hgx_snapshot_read(bpath, ptr(la), ptr(off), ptr(tg), ptr(ty), ptr(hs)))
+    return {"num_atoms": a.value, "link_atom": la, "tgt_off": off, "tgt_idx": tg,
+            "link_type": ty if ht.value else None, "handles": hs}
+
+
+def export_store(path, handles, layouts):
+    """The exporter in Python: rank the store's persistent handles, lay
+    the links out as rows and write the .hgcsr file with the handle table.  ``layouts`` as in
+    HyperGraphSnapshot.from_layouts.  Returns handle -> rank."""
+    ranks = rank_handles(handles)
+    la, off, tg, ty = _rows_from_layouts(ranks, layouts)
+    by_rank = [None] * len(ranks)
+    for h, r in ranks.items():
+        by_rank[r] = h
+    write_snapshot(path, len(ranks), la, off, tg, ty, by_rank)
+    return ranks
+
+
+def _rows_from_layouts(ranks, layouts):
+    links = sorted(layouts, key=lambda h: ranks[h])
+    link_atom = np.array([ranks[h] for h in links], np.int32)
+    off = np.zeros(len(links) + 1, np.int64)
+    tg = []
+    types = np.zeros(len(links), np.int32)
+    for r, h in enumerate(links):
+        t, targets = layouts[h]
+        types[r] = int(t)
+        tg.extend(ranks[x] for x in targets)
+        off[r + 1] = len(tg)
+    return link_atom, off, np.array(tg, np.int32), types
+
+
 class HyperGraphSnapshot:
     """A snapshot placed on one MI355X.  Atoms are ids 0..A-1 (rank order).  Link row r is atom
     ``link_atom[r]`` with targets ``tgt_idx[tgt_off[r]:tgt_off[r+1]]`` and type key ``link_type[r]``."""
 
     def __init__(self, num_atoms, link_atom, tgt_off, tgt_idx, link_type=None, device=0, keep_host=True):
-        self.A = int(num_atoms)
-        self.link_atom = np.ascontiguousarray(link_atom, np.int32)
-        self.tgt_off = np.ascontiguousarray(tgt_off, np.int64)
-        self.tgt_idx = np.ascontiguousarray(tgt_idx, np.int32)
-        self.link_type = None if link_type is None else np.ascontiguousarray(link_type, np.int32)
-        self.M = len(self.link_atom)
-        if len(self.tgt_off) != self.M + 1:
+        self._h = None
+        link_atom = np.ascontiguousarray(link_atom, np.int32)
+        tgt_off = np.ascontiguousarray(tgt_off, np.int64)
+        tgt_idx = np.ascontiguousarray(tgt_idx, np.int32)
+        link_type = None if link_type is None else np.ascontiguousarray(link_type, np.int32)
+        if len(tgt_off) != len(link_atom) + 1:
             raise ValueError("tgt_off must have num_links + 1 entries")
-        desc = _lib.GraphDesc(self.A, self.M, ptr(self.link_atom), ptr(self.tgt_off), ptr(self.tgt_idx),
-                              ptr(self.link_type))
+        desc = _desc(num_atoms, link_atom, tgt_off, tgt_idx, link_type)
         h = C.c_void_p()
         check(lib().hgx_graph_create(C.byref(desc), int(device), C.byref(h)))
+        self._attach(h, device, num_atoms, link_atom, tgt_off, tgt_idx, link_type, keep_host)
+
+    def _attach(self, h, device, num_atoms, link_atom, tgt_off, tgt_idx, link_type, keep_host):
         self._h = h
         self.device = device
+        self.A = int(num_atoms)
+        self.link_atom, self.tgt_off, self.tgt_idx, self.link_type = link_atom, tgt_off, tgt_idx, link_type
+        self.M = len(self.link_atom)
         a, m, i = C.c_int64(), C.c_int64(), C.c_int64()
         check(lib().hgx_graph_info(h, C.byref(a), C.byref(m), C.byref(i)))
         self.num_incidences = i.value
         self._row_of = None
+        self._keep_host = keep_host
         if not keep_host:
             # large benchmark graphs: the device copy is authoritative
             self.tgt_idx = None
+
+    # -- the snapshot on disk (.hgcsr, include/hgx.h) ------------------------------------------
+    @classmethod
+    def open(cls, path, device=0, keep_host=True):
+        """Map a .hgcsr file (hgx_graph_open) onto ``device``.  ``keep_host`` also reads the rows
+        into host arrays for targets()/type_of()."""
+        h = C.c_void_p()
+        check(lib().hgx_graph_open(os.fsencode(path), int(device), C.byref(h)))
+        snap = cls.__new__(cls)
+        snap._h = None
+        try:
+            if keep_host:
+                f = read_snapshot(path)
+                la, off, tg, ty = f["link_atom"], f["tgt_off"], f["tgt_idx"], f["link_type"]
+                n = f["num_atoms"]
+            else:
+                n, la, off, ty = _export(h, with_targets=False)
+                tg = None
+        except BaseException:
+            lib().hgx_graph_destroy(h)
+            raise
+        snap._attach(h, device, n, la, off, tg, ty, keep_host)
+        return snap
+
+    def save(self, path, handles=None):
+        """Write this snapshot as .hgcsr (rows exported from the device; ``handles``: optional
+        rank-ordered persistent handles stored as the handle table)."""
+        n, la, off, ty, tg = _export(self.handle, with_targets=True)
+        write_snapshot(path, n, la, off, tg, ty, handles)
+
+    def update(self, add=None, remove=(), num_atoms=None):
+        """Apply one batch of link events (hgx_graph_update): ``add`` = {link atom: (type key,
+        [target atoms])} for HGAtomAddedEvent, ``remove`` = link atoms for HGAtomRemovedEvent,
+        ``num_atoms`` = the grown rank space.  The host mirror is refreshed from the device."""
+        add = add or {}
+        keys = sorted(add)
+        la = np.array(keys, np.int32)
+        off = np.zeros(len(keys) + 1, np.int64)
+        tg, ty = [], np.zeros(len(keys), np.int32)
+        for r, k in enumerate(keys):
+            t, targets = add[k]
+            ty[r] = int(t)
+            tg.extend(int(x) for x in targets)
+            off[r + 1] = len(tg)
+        tg = np.array(tg, np.int32)
+        rm = np.ascontiguousarray(np.asarray(list(remove), np.int32))
+        A = self.A if num_atoms is None else int(num_atoms)
+        check(lib().hgx_graph_update(self.handle, A, len(keys), ptr(la), ptr(off), ptr(tg), ptr(ty), len(rm),
+                                     ptr(rm)))
+        n, la, off, ty, tg = _export(self.handle, with_targets=self._keep_host)
+        self._attach(self._h, self.device, n, la, off, tg, ty, self._keep_host)
 
     # -- construction from reference-side objects -------------------------------------------
     @classmethod
@@ -72,17 +219,8 @@ class HyperGraphSnapshot:
         handles])} = the store's link records [type, value, t0..] (C/HyperGraph.java:1603-1608).
         Returns (snapshot, ranks) where ranks maps handle -> atom id."""
         ranks = rank_handles(handles)
-        links = sorted(layouts, key=lambda h: ranks[h])
-        link_atom = np.array([ranks[h] for h in links], np.int32)
-        off = np.zeros(len(links) + 1, np.int64)
-        tg = []
-        types = np.zeros(len(links), np.int32)
-        for r, h in enumerate(links):
-            t, targets = layouts[h]
-            types[r] = int(t)
-            tg.extend(ranks[x] for x in targets)
-            off[r + 1] = len(tg)
-        snap = cls(len(ranks), link_atom, off, np.array(tg, np.int32), types, device=device)
+        link_atom, off, tg, types = _rows_from_layouts(ranks, layouts)
+        snap = cls(len(ranks), link_atom, off, tg, types, device=device)
         return snap, ranks
 
     # -- store reads -------------------------------------------------------------------------

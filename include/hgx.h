@@ -151,6 +151,42 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
 #define HGX_OPT_SEQ_BUDGET 2
 int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
 
+/* ---- the snapshot on disk (.hgcsr) and batched store updates ------------------------------------
+ * The exporter walks the store once -- atom handles from
+ * IndexScanQuery(indexByType) (C/query/cond2qry/ToQueryMap.java:101-113), link layouts from
+ * HGStore.getLink (C/HGStore.java:179-191) -- ranks the handles and writes the bipartite CSR with
+ * hgx_snapshot_write; a later process maps it with hgx_graph_open instead of re-walking the store.
+ * File layout (little-endian, 64-byte aligned sections): 64-byte header (magic "HGXCSR1\0",
+ * version 1, flags, num_atoms, num_links, num_pins, handle_bytes, checksum), link_atom i32[M],
+ * tgt_off i64[M+1], tgt_idx i32[P], link_type i32[M] (if present), handles u8[A*handle_bytes]
+ * (if present: the persistent handle bytes of every rank, so ranks map back to handles).
+ * The writer validates the rows like hgx_graph_create and replaces the file atomically. */
+int hgx_snapshot_write(const char *path, const hgx_graph_desc *desc, const uint8_t *handles,
+                       int32_t handle_bytes);
+/* Header fields without reading the sections (any output may be NULL). */
+int hgx_snapshot_info(const char *path, int64_t *num_atoms, int64_t *num_links, int64_t *num_pins,
+                      int32_t *handle_bytes, int32_t *has_types);
+/* Checksum-verified copy of the sections into caller buffers sized from hgx_snapshot_info (NULL
+ * skips a section; link_type is zero-filled when the file has none). */
+int hgx_snapshot_read(const char *path, int32_t *link_atom, int64_t *tgt_off, int32_t *tgt_idx,
+                      int32_t *link_type, uint8_t *handles);
+/* Map + verify the file and build the device snapshot (as hgx_graph_create). */
+int hgx_graph_open(const char *path, int32_t device, hgx_graph **out);
+/* D2H copy of the snapshot rows currently on the device (sizes from hgx_graph_info; num_pins =
+ * tgt_off[num_links]).  Any output may be NULL. */
+int hgx_graph_export(hgx_graph *g, int32_t *link_atom, int64_t *tgt_off, int32_t *tgt_idx, int32_t *link_type);
+/* Apply one batch of store events to a device snapshot: HGAtomAddedEvent for links (n_add rows in
+ * hgx_graph_desc form: link atom, offsets into add_tgt_idx, type) and HGAtomRemovedEvent for links
+ * (their atom ids) (C/event/HGAtomAddedEvent.java, C/event/HGAtomRemovedEvent.java; the store
+ * sides are HGStore.store/removeLink, C/HGStore.java:100-170).  New atoms extend the rank space
+ * to num_atoms (>= the current count; the exporter assigns new atoms ranks after the existing
+ * ones).  An added link must not exist yet; removing an absent link is a no-op, as a removal of a
+ * link already gone is in the store.  The incidence index is rebuilt from the merged rows (same
+ * device object, same handle).  Refused while a result of this graph is alive. */
+int hgx_graph_update(hgx_graph *g, int64_t num_atoms, int64_t n_add, const int32_t *add_link_atom,
+                     const int64_t *add_tgt_off, const int32_t *add_tgt_idx, const int32_t *add_link_type,
+                     int64_t n_remove, const int32_t *remove_link_atom);
+
 /* Batched multi-source BFS.  Seed i is HGBreadthFirstTraversal(seeds[i], gen, max_depth)
  * (max_depth HGX_UNBOUNDED = Integer.MAX_VALUE).  The result holds, per seed and per
  * distance d, the set V_d of atoms returned by next() at distance d (V_0 = {seed}),
