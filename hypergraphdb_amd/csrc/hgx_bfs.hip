@@ -32,6 +32,9 @@
 #include <map>
 #include <memory>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "hgx_internal.h"
 
 namespace hgx {
@@ -170,7 +173,9 @@ enum Ctr {
     cNewDeg,            // sum of |inc(v)| over the new atoms (next level's push volume)
     cNewFull,           // atoms that became visited by every traversal
     cCand,              // frontier-push candidates finalised
-    cNum = 13
+    cNewDegNF,          // sum of |inc(v)| over the new atoms not yet visited by every traversal
+    cNfRows,            // frontier rows read by the non-full pull
+    cNum = 15
 };
 
 __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
@@ -182,6 +187,8 @@ __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
 // word saturates at ~90 adds/us; thousands of waves add to every counter each level).  Counter c
 // of shard k lives at base[k * kCtrStride + c]; the host sums the shards.
 constexpr int kCtrShards = 16, kCtrStride = 16, kCtrBlock = kCtrShards * kCtrStride;
+// Internal per-level flag (above the HGX_OPT_BFS_FLAGS bits): dense level with every lf row written.
+constexpr int kAllRows = 1 << 16;
 static_assert(cNum <= kCtrStride, "counter block");
 __device__ __forceinline__ void wave_add_sh(u64* ctr, u64 v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -445,7 +452,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
         // sparse levels: only targets of active links (cand) can gain a bit
         const u64 cw = cand ? cand[tile] : ~0ull;
@@ -473,7 +480,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
                         V::st(vis + t * W + sub * WPL, old | nw);
                         isnew = true;
                         becomes_full = group_all<G>(V::eq(old | nw, FULL));
-                        if (sub == 0) n_newdeg += (u64)(e - b);
+                        if (sub == 0) { const u64 dg_ = (u64)(e - b); n_newdeg += dg_; if (!becomes_full) n_newdeg_nf += dg_; }
                     }
                 }
             }
@@ -498,6 +505,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
     wave_add_sh(ctr + cNewLight, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -520,7 +528,7 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
     static_assert(G >= 4, "gather2 needs G >= 4");
     typedef Vec<WPL> V;
-    const bool early = flags & 1, skip_full = flags & 4;
+    const bool early = flags & 1, skip_full = flags & 4, all_rows = flags & kAllRows;
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
     const u64 gmask = (1ull << G) - 1ull;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -604,6 +612,8 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
                     ++n_links;
                     n_pins += nact;
                 }
+            } else if (WRITE_LF && all_rows && L < M) {
+                V::st(lf + L * W + sub * WPL, V::zero());   // the pull reads every row unprobed
             }
             word |= compress_groups<G>(__ballot(act), j * PW);
         }
@@ -625,13 +635,13 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
     constexpr int JB = G >= 8 ? 4 : G;   // atoms of a group interleaved at once (register budget)
     static_assert(G >= 4, "pull2 needs G >= 4");
     typedef Vec<WPL> V;
-    const bool early = flags & 2, skip_full = flags & 4;
+    const bool early = flags & 2, skip_full = flags & 4, all_rows = flags & kAllRows;
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
     const u64 gmask = (1ull << G) - 1ull;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
         const u64 ever_w = ever[tile], full_w = full[tile];
         const int64_t tme = tile * 64 + lane;
@@ -672,7 +682,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                 unsigned pa = 0;
 #pragma unroll
                 for (int jj = 0; jj < JB; ++jj)
-                    if (myL[jj] >= 0 && bit(la, myL[jj])) pa |= 1u << jj;
+                    if (myL[jj] >= 0 && (all_rows || bit(la, myL[jj]))) pa |= 1u << jj;
 #pragma unroll
                 for (int jj = 0; jj < JB; ++jj) {
                     const unsigned ga = (unsigned)((__ballot((pa >> jj) & 1u) >> base) & gmask);
@@ -720,7 +730,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                         V::st(vis + t * W + sub * WPL, old[jj] | nw);
                         isnew = true;
                         becomes_full = group_all<G>(V::eq(old[jj] | nw, FULL));
-                        if (sub == 0) n_newdeg += (u64)dj[jj];
+                        if (sub == 0) { n_newdeg += (u64)dj[jj]; if (!becomes_full) n_newdeg_nf += (u64)dj[jj]; }
                     }
                 }
                 new_w |= compress_groups<G>(__ballot(isnew), pos - g);
@@ -745,6 +755,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
     wave_add_sh(ctr + cNewLight, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
 }
 
 // Heavy atoms: one workgroup per chunk of <= kChunkEntries incidence entries; groups OR their
@@ -805,7 +816,7 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_acc = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    u64 n_acc = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t h = grp; h < H; h += ngrp) {
         const int64_t t = heavy_atom[h];
         typename V::T acc = V::ld(hubacc + h * W + sub * WPL);
@@ -825,7 +836,7 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
             if (becomes_full) set_bit(full, t);
             ++n_new;
             n_full += becomes_full;
-            n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+            { const u64 dg_ = (u64)(inc_off[t + 1] - inc_off[t]); n_newdeg += dg_; if (!becomes_full) n_newdeg_nf += dg_; }
         }
     }
     wave_add_sh(ctr + cNewFull, n_full);
@@ -833,6 +844,7 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
     wave_add_sh(ctr + cNewHub, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
 }
 
 // Sparse levels: mark every (typed) link incident to a frontier atom.  One wave per frontier word:
@@ -933,7 +945,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t nwords = (A + 63) / 64;
     const typename V::T FULL = full_part<W>(fm, sub);
-    u64 n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    u64 n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
         const bool in = base + lane < nwords;
         const u64 myfull = in ? full[base + lane] : 0ull;
@@ -963,7 +975,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
                             V::st(vis + t * W + sub * WPL, old | nw);
                             isnew = true;
                             becomes_full = group_all<G>(V::eq(old | nw, FULL));
-                            if (sub == 0) n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+                            if (sub == 0) { const u64 dg_ = (u64)(inc_off[t + 1] - inc_off[t]); n_newdeg += dg_; if (!becomes_full) n_newdeg_nf += dg_; }
                         }
                     }
                 }
@@ -985,6 +997,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize(int64_t A, const int64_
     wave_add_sh(ctr + cNewLight, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
 }
 
 // ---- sparse levels, ordered modes (hg.subsumed / hg.subsumes): frontier-driven push ------------
@@ -1193,7 +1206,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
     const int64_t n = (int64_t)*n_clist;
-    u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_full = 0;
+    u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t k0 = grp - (grp % (64 / G)); k0 < n; k0 += ngrp) {   // wave-uniform trip count
         const int64_t k = k0 + (grp % (64 / G));
         const bool valid = k < n;
@@ -1214,7 +1227,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
                 if (becomes_full) set_bit(full, t);
                 ++n_new;
                 n_full += becomes_full;
-                n_newdeg += (u64)(inc_off[t + 1] - inc_off[t]);
+                { const u64 dg_ = (u64)(inc_off[t + 1] - inc_off[t]); n_newdeg += dg_; if (!becomes_full) n_newdeg_nf += dg_; }
             }
         }
         if (valid && sub == 0) {
@@ -1228,6 +1241,156 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
     wave_add_sh(ctr + cNewLight, n_new);
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Late dense levels (symmetric mode): once most atoms are visited by every traversal ("full"),
+// the few that are not pull straight from the frontier rows of their neighbours -- no link gather,
+// no lf rows.  Atom t's next row = OR over links L in inc(t) (type-filtered) of OR over targets u
+// of L in the frontier of lvl[u] (t's own row is a subset of vis[t] and masks out), minus vis[t].
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) hgx_nonfull_list(int64_t A, const u64* __restrict__ full,
+                                                        const int64_t* __restrict__ inc_off,
+                                                        int32_t* __restrict__ list, u64* __restrict__ n_list) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t w = wave; w * 64 < A; w += nwave) {
+        const int64_t v = w * 64 + lane;
+        bool take = v < A && !((full[w] >> lane) & 1ull);
+        if (take) take = inc_off[v + 1] > inc_off[v];
+        const u64 m = __ballot(take);
+        if (m == 0ull) continue;
+        u64 base = 0;
+        if (lane == 0) base = atomicAdd(n_list, (u64)__popcll(m));
+        base = __shfl(base, 0);
+        if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)v;
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_nf_pull(const int32_t* __restrict__ list, const u64* __restrict__ n_list,
+                                                   const int64_t* __restrict__ inc_off,
+                                                   const int32_t* __restrict__ inc_row,
+                                                   const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                   const int64_t* __restrict__ tgt_off,
+                                                   const int32_t* __restrict__ tgt_idx, const u64* __restrict__ fa,
+                                                   const u64* __restrict__ lvl, u64* __restrict__ vis,
+                                                   u64* __restrict__ ever, u64* __restrict__ full,
+                                                   u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                   u64* __restrict__ ctr, FullMask fm, int flags) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    static_assert(G >= 4, "nf pull needs G >= 4");
+    typedef Vec<WPL> V;
+    const bool early = flags & 2;
+    const int lane = threadIdx.x & 63, sub = lane & (G - 1), base = lane & ~(G - 1);
+    const u64 gmask = (1ull << G) - 1ull;
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    const int64_t n = (int64_t)*n_list;
+    u64 n_cand = 0, n_ent = 0, n_pins = 0, n_rows = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0,
+        n_full = 0;
+    for (int64_t k0 = grp - (grp % (64 / G)); k0 < n; k0 += ngrp) {   // wave-uniform trip count
+        const int64_t k = k0 + (grp % (64 / G));
+        if (k >= n) continue;   // group-uniform; no cross-group shuffles below
+        const int64_t t = list[k];
+        const int64_t b = inc_off[t], e = inc_off[t + 1];
+        const bool ev = bit(ever, t);
+        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        typename V::T acc = V::zero();
+        for (int64_t i0 = b; i0 < e; i0 += G) {   // group-uniform
+            const int64_t q = i0 + sub;
+            int32_t myL = q < e ? inc_row[q] : -1;
+            if (myL >= 0 && want_type >= 0 && inc_type[q] != want_type) myL = -1;
+            int64_t bme = 0;
+            int nme = 0;
+            if (myL >= 0) {
+                bme = tgt_off[myL];
+                nme = (int)(tgt_off[myL + 1] - bme);
+                ++n_ent;
+                n_pins += (u64)nme;
+            }
+            int32_t v[G];
+            int nn[G];
+            int64_t bb[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                bb[j] = __shfl(bme, base + j);
+                nn[j] = __shfl(nme, base + j);
+                v[j] = sub < nn[j] ? tgt_idx[bb[j] + sub] : -1;
+            }
+            unsigned pa = 0;
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if (v[j] >= 0 && bit(fa, v[j])) pa |= 1u << j;
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const unsigned ga = (unsigned)((__ballot((pa >> j) & 1u) >> base) & gmask);
+                if (ga) {   // group-uniform
+                    typename V::T r[G];
+#pragma unroll
+                    for (int kk = 0; kk < G; ++kk) {
+                        const int32_t vk = __shfl(v[j], base + kk);
+                        r[kk] = ((ga >> kk) & 1u) ? V::ld(lvl + (int64_t)vk * W + sub * WPL) : V::zero();
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < G; ++kk) acc |= r[kk];
+                    n_rows += __popc(ga);
+                }
+                if (nn[j] > G) {   // a link longer than G (rare): the rest of its targets
+                    for (int64_t p = bb[j] + G; p < bb[j] + nn[j]; p += G) {
+                        const int64_t qq = p + sub;
+                        const int32_t myv = qq < bb[j] + nn[j] ? tgt_idx[qq] : -1;
+                        const unsigned g2 = (unsigned)((__ballot(myv >= 0 && bit(fa, myv)) >> base) & gmask);
+                        typename V::T r[G];
+#pragma unroll
+                        for (int kk = 0; kk < G; ++kk) {
+                            const int32_t vk = __shfl(myv, base + kk);
+                            r[kk] = ((g2 >> kk) & 1u) ? V::ld(lvl + (int64_t)vk * W + sub * WPL) : V::zero();
+                        }
+#pragma unroll
+                        for (int kk = 0; kk < G; ++kk) acc |= r[kk];
+                        n_rows += __popc(g2);
+                    }
+                }
+            }
+            if (early && i0 + G < e && group_all<G>(V::eq(acc | old, FULL))) break;
+        }
+        const typename V::T nw = acc & ~old;
+        if (group_any<G>(V::nz(nw))) {
+            V::st(lvl_next + t * W + sub * WPL, nw);
+            V::st(vis + t * W + sub * WPL, old | nw);
+            const bool becomes_full = group_all<G>(V::eq(old | nw, FULL));
+            if (sub == 0) {
+                set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (becomes_full) set_bit(full, t);
+                ++n_new;
+                n_full += becomes_full;
+                const u64 dg = (u64)(e - b);
+                n_newdeg += dg;
+                if (!becomes_full) n_newdeg_nf += dg;
+            }
+        }
+        if (sub == 0) {
+            ++n_cand;
+            n_vis += ev;
+        }
+    }
+    if (sub != 0) n_rows = 0;   // n_ent / n_pins: each lane counted its own entry
+    wave_add_sh(ctr + cActiveLinks, n_ent);
+    wave_add_sh(ctr + cActivePins, n_pins);
+    wave_add_sh(ctr + cIncLight, n_ent);
+    wave_add_sh(ctr + cCand, n_cand);
+    wave_add_sh(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+    wave_add_sh(ctr + cNfRows, n_rows);
 }
 
 // sum of |inc(v)| over the seed atoms (level-0 push volume)
@@ -1572,7 +1735,8 @@ struct Timer {
 };
 
 enum { kKindGather = HGX_K_LINK_GATHER, kKindPull = HGX_K_ATOM_PULL, kKindHeavy = HGX_K_PULL_HEAVY,
-       kKindHub = HGX_K_HUB_FINALIZE, kKindExchange = HGX_K_COUNT };
+       kKindHub = HGX_K_HUB_FINALIZE, kKindPush = HGX_K_FRONTIER_PUSH, kKindNf = HGX_K_NF_PULL,
+       kKindExchange = HGX_K_COUNT };
 
 FullMask full_mask(int S, int W) {
     FullMask fm;
@@ -1735,7 +1899,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const size_t flist_bytes = sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1);
     int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
     int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
-    u64 push_volume = 0;
+    const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
+    const int64_t I_total = g->I;
+    int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
+    u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
     if (sparse_ok) {
         u64* dv = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock;   // scratch slot
         hgx_seed_degree<<<grid_for((int64_t)seed_atoms.size(), 256, 1 << 20), 256, 0, s>>>(
@@ -1743,6 +1910,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         HGX_CHECK_LAUNCH();
         HGX_HIP(hipMemcpyAsync(&push_volume, dv, sizeof(u64), hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
+        push_volume_nf = push_volume;
     }
     const u64 sparse_limit = (u64)std::max<int64_t>(M / 16, 1024);
     // Full-visited skipping costs two bitmap probes per pin; it pays once a sizeable share of the
@@ -1759,10 +1927,28 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         int lflags = g->bfs_flags;
         if ((lflags & 16) && (int64_t)full_total * 16 < A) lflags &= ~4;   // adaptive full skip
         const bool opush = sparse && (MODE != kSym || (lflags & 32));
-        if (opush) {
+        // late dense level with few atoms left unfull: those pull from the frontier directly
+        const bool nfp = !sparse && sparse_ok && MODE == kSym && Lay<W>::G >= 4 && !ex && (lflags & 256) &&
+                         (lflags & 4) && 4 * (int64_t)(I_total - full_deg_total) < I_total;
+        if (nfp) {
+            if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
+                Events e2 = tm.start(kKindNf, d);
+                HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
+                u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slot
+                HGX_HIP(hipMemsetAsync(n_list, 0, sizeof(u64), s));
+                hgx_nonfull_list<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, full, g->inc_off, clist,
+                                                                                         n_list);
+                HGX_CHECK_LAUNCH();
+                hgx_nf_pull<W><<<4096, 256, 0, s>>>(clist, n_list, g->inc_off, g->inc_row, g->inc_type, want_type,
+                                                    g->tgt_off, g->tgt_idx, fa, lvl, vis, ever, full, lvl_next, fa_next,
+                                                    c, fm, lflags);
+                HGX_CHECK_LAUNCH();
+                tm.stop(e2);
+            }
+        } else if (opush) {
             // frontier-driven push (mark candidates, zero their rows, OR rows, finalise): the ordered
             // modes always, the symmetric mode with HGX_OPT_BFS_FLAGS bit 5
-            Events e2 = tm.start(kKindPull, d);
+            Events e2 = tm.start(kKindPush, d);
             if (!g->zacc_clean || g->zacc_bytes < row_bytes) {   // (re)establish the all-zero accumulator
                 if (g->zacc_bytes < row_bytes) {
                     if (g->zacc) HGX_HIP(hipFree(g->zacc));
@@ -1817,6 +2003,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64* cd = sparse ? cand : nullptr;
 
         const bool v2 = Lay<W>::G >= 4 && !sparse && !(lflags & 64);   // MLP-restructured dense kernels
+        // A frontier whose incidence volume covers the links twice leaves few links inactive: the
+        // gather then writes a (zero) row for every link and the pull reads rows without probing la
+        // -- one dependent load fewer per incidence chunk (HGX_OPT_BFS_FLAGS bit 7).
+        if (v2 && (lflags & 128) && MODE == kSym && push_volume_nf >= 2 * (u64)M) lflags |= kAllRows;
         Events e1 = tm.start(kKindGather, d);
         if constexpr (Lay<W>::G >= 4) {
             if (v2)
@@ -1886,8 +2076,16 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             h_new[cNewDeg] = part_push;
         }
         level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
-        level_ctr.back()[cDirRows] = sparse ? (opush ? 2 : 1) : 0;   // (host-side) kind of this level
+        level_ctr.back()[cDirRows] = nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;   // (host-side) kind of this level
+        if (!ex) full_deg_total += (int64_t)(h_new[cNewDeg] - h_new[cNewDegNF]);   // incidence of atoms now full
+        if (trace)
+            std::fprintf(stderr, "[hgx bfs] level %d kind %d allrows %d active_links %llu new %llu push %llu push_nf %llu "
+                         "new_full %llu\n", d, nfp ? 3 : sparse ? (opush ? 2 : 1) : 0, (lflags & kAllRows) ? 1 : 0,
+                         (unsigned long long)h_new[cActiveLinks], (unsigned long long)h_new[cNewAtoms],
+                         (unsigned long long)h_new[cNewDeg], (unsigned long long)h_new[cNewDegNF],
+                         (unsigned long long)h_new[cNewFull]);
         push_volume = h_new[cNewDeg];
+        push_volume_nf = ex ? push_volume : h_new[cNewDegNF];
         full_total += h_new[cNewFull];
         if (h_new[cNewAtoms] == 0) {
             g->release(lvl_next, row_bytes);
@@ -2118,16 +2316,25 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             double b_pull = (sparse_level ? 8.0 * (A / 64.0) : 8.0 * (A + 1) + 4.0 * I_light) + M / 8.0 +
                                   rowb * c[cIncLight] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] +
                                   3.0 * A / 8.0;
-            const bool opush_level = c[cDirRows] == 2;
-            if (opush_level) {   // frontier push: no gather; two frontier passes + finalise
+            const bool opush_level = c[cDirRows] == 2 || c[cDirRows] == 3;
+            if (c[cDirRows] == 3) {   // non-full pull: no gather
+                b_gather = 0.0;
+                // full bitmap + inc_off of the listed atoms + list write/read + entries (inc_row, inc_type,
+                // tgt_off pair) + pins + frontier bitmap + frontier rows + vis reads + lvl/vis writes + bitmaps
+                b_pull = A / 8.0 + 24.0 * c[cCand] + 4.0 * A / 64.0 + (8.0 + (typed ? 4.0 : 0.0) + 16.0) * c[cIncLight] +
+                         4.0 * c[cActivePins] + A / 8.0 + rowb * c[cNfRows] + rowb * c[cVisLight] +
+                         2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
+            } else if (opush_level) {   // frontier push: no gather; two frontier passes + finalise
                 b_gather = 0.0;
                 // frontier scan + links (inc_row, inc_type, tgt_off pair) + pins + one word RMW per pair
                 // + candidates (acc read + re-zero) + vis reads + lvl/vis writes + cleared bitmaps
                 b_pull = 8.0 * (A / 64.0) + 24.0 * c[cActiveLinks] + 4.0 * c[cActivePins] + 16.0 * c[cIncLight] +
                          2.0 * rowb * c[cCand] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] + 2.0 * A / 8.0;
             }
+            const int pull_kind = c[cDirRows] == 3 ? HGX_K_NF_PULL : c[cDirRows] == 2 ? HGX_K_FRONTIER_PUSH
+                                                                                   : HGX_K_ATOM_PULL;
             r->stats.bytes_kernel[HGX_K_LINK_GATHER] += b_gather;
-            r->stats.bytes_kernel[HGX_K_ATOM_PULL] += b_pull;
+            r->stats.bytes_kernel[pull_kind] += b_pull;
             double b_heavy = 0, b_hub = 0;
             if (g->n_chunks > 0 && !sparse_level) {
                 b_heavy = 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
@@ -2143,7 +2350,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                 r->stats.level_sparse[d] = (int32_t)c[cDirRows];
             }
             if (!opush_level) r->stats.launches[HGX_K_LINK_GATHER] += 1;
-            r->stats.launches[HGX_K_ATOM_PULL] += 1;
+            r->stats.launches[pull_kind] += 1;
             if (d < 64) r->stats.level_new[d] += (int64_t)c[cNewAtoms];
         }
         r->batches.push_back(std::move(bt));

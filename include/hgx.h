@@ -96,7 +96,9 @@ typedef struct hgx_and_query {
 #define HGX_K_ATOM_PULL     1   /* hgx_atom_pull            */
 #define HGX_K_PULL_HEAVY    2   /* hgx_atom_pull_heavy      */
 #define HGX_K_HUB_FINALIZE  3   /* hgx_hub_finalize         */
-#define HGX_K_COUNT         4
+#define HGX_K_FRONTIER_PUSH 4   /* sparse levels: hgx_frontier_list, hgx_opush[_heavy], hgx_push_finalize_list */
+#define HGX_K_NF_PULL       5   /* late dense levels: hgx_nonfull_list, hgx_nf_pull                        */
+#define HGX_K_COUNT         6
 typedef struct hgx_bfs_stats {
     int32_t n_levels_expanded;
     int32_t n_batches;
@@ -110,7 +112,8 @@ typedef struct hgx_bfs_stats {
     double  level_ms[64];              /* device ms of all kernels of level d (timing enabled) */
     int64_t level_new[64];             /* atoms with a new bit at level d+1 (summed over batches) */
     double  level_bytes[64];           /* algorithmic bytes of all kernels of level d          */
-    int32_t level_sparse[64];          /* level d ran 0 = dense, 1 = frontier links + lf push, 2 = frontier push */
+    int32_t level_sparse[64];          /* level d ran 0 = dense, 1 = frontier links + lf push, 2 = frontier push,
+                                        * 3 = non-full pull */
     /* per level, summed over batches: [0] lf rows written, [1] frontier rows gathered,
      * [2] lf rows pulled (light), [3] vis rows read, [4] new light atoms, [5] lf rows pulled
      * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
@@ -143,8 +146,12 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 5 = sparse levels of the symmetric mode push from the frontier atoms
  *                              (the ordered modes always do),
  *                      bit 6 = keep the one-row-at-a-time dense kernels for >= 512 sources
- *                              (A/B only; the default uses the tile-staged ones).
- *                      Default 0x3E. */
+ *                              (A/B only; the default uses the tile-staged ones),
+ *                      bit 7 = dense levels whose frontier covers the links twice write every lf row
+ *                              and pull without the active-link probe,
+ *                      bit 8 = dense levels with < 1/4 of the incidence on atoms not yet visited by
+ *                              every traversal pull those atoms straight from the frontier rows.
+ *                      Default 0x1BE. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
  * (seeds are processed in chunks that fit; default 16 GiB). */

@@ -225,7 +225,7 @@ def test_depth_of_and_errors():
         res.visited(5, 0)
 
 
-@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40])
+@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6])
 def test_engine_option_matrix(flags):
     """Every work-avoidance option (early exits, full-visited skipping, frontier-driven sparse
     levels) returns the same per-depth sets; power-law hubs + random edge cases + ordered modes."""
@@ -236,8 +236,30 @@ def test_engine_option_matrix(flags):
     cases.append((K.random_graph(rng, 800, 2500, max_arity=7, n_types=3), K.ALGEN_MODES[4], 1, 3))
     cases.append((synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=12), K.ALGEN_MODES[0], -1, 3))
     cases.append((synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=13), K.ALGEN_MODES[1], 2, None))
-    for g, mode, lt, maxd in cases:
+    for i, (g, mode, lt, maxd) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
         snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
-        seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
+        seeds = rng.integers(0, g["num_atoms"], 1024 if i == 2 else 300).astype(np.int32)   # W = 16 and W < 16
         check_batch(g, seeds, maxd, mode, lt, snap, orc)
+
+
+@pytest.mark.parametrize("n_seeds,lt", [(1024, -1), (300, -1), (1024, 1)])
+def test_nonfull_pull_levels(n_seeds, lt):
+    """Late dense levels where most incidence sits on atoms visited by every traversal run the
+    non-full pull (level kind 3); per-depth sets stay identical to the oracle's, unbounded and
+    with a link type."""
+    from hypergraphdb_amd import bfs_batch, synth
+    g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=14)
+    snap, orc = snapshot(g), oracle(g)
+    # seeds with (typed) incidence: every traversal covers the same component, so atoms become full
+    off, tg = g["tgt_off"], g["tgt_idx"]
+    rows = np.nonzero(g["link_type"] == lt)[0] if lt >= 0 else np.arange(len(off) - 1)
+    has = np.zeros(g["num_atoms"], bool)
+    for r in rows:
+        has[tg[off[r]:off[r + 1]]] = True
+    seeds = np.random.default_rng(15).choice(np.nonzero(has)[0], n_seeds, replace=False).astype(np.int32)
+    res = bfs_batch(snap, seeds, None, gen(snap, K.ALGEN_MODES[0], lt))
+    kinds = res.stats(accounting=False)["level_sparse"]
+    res.close()
+    assert 3 in kinds, kinds
+    check_batch(g, seeds, None, K.ALGEN_MODES[0], lt, snap, orc)

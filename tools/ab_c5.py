@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-level breakdown of the config-5 subsumption closures (both directions).
 
-  python tools/ab_c5.py [--scale 1.0] [--flags 0x3E]
+  python tools/ab_c5.py [--scale 1.0] [--flags 0x1BE]
 """
 import argparse
 import json
@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--flags", default="0x3E")
+    ap.add_argument("--flags", default="0x1BE")
     ap.add_argument("--sources", type=int, default=1024)
     args = ap.parse_args()
     import hypergraphdb_amd as H
