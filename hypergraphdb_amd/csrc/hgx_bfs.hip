@@ -1250,22 +1250,54 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
 // no lf rows.  Atom t's next row = OR over links L in inc(t) (type-filtered) of OR over targets u
 // of L in the frontier of lvl[u] (t's own row is a subset of vis[t] and masks out), minus vis[t].
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) hgx_nonfull_list(int64_t A, const u64* __restrict__ full,
-                                                        const int64_t* __restrict__ inc_off,
-                                                        int32_t* __restrict__ list, u64* __restrict__ n_list) {
+// bit v of hasinc <=> inc(v) is non-empty (computed once per batch, for the non-full list)
+__global__ void __launch_bounds__(256) hgx_hasinc(int64_t A, const int64_t* __restrict__ inc_off,
+                                                  u64* __restrict__ hasinc) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t w = wave; w * 64 < A; w += nwave) {
         const int64_t v = w * 64 + lane;
-        bool take = v < A && !((full[w] >> lane) & 1ull);
-        if (take) take = inc_off[v + 1] > inc_off[v];
-        const u64 m = __ballot(take);
-        if (m == 0ull) continue;
-        u64 base = 0;
-        if (lane == 0) base = atomicAdd(n_list, (u64)__popcll(m));
-        base = __shfl(base, 0);
-        if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)v;
+        const u64 m = __ballot(v < A && inc_off[v + 1] > inc_off[v]);
+        if (lane == 0) hasinc[w] = m;
+    }
+}
+
+// Atoms with incidence not yet visited by every traversal, appended to a list (order-free).  A
+// thread owns one bitmap word; a block scans its 256 words' counts and claims its list range with
+// one atomic (a same-address atomic per wave would serialise on the counter).
+__global__ void __launch_bounds__(256) hgx_nonfull_list(int64_t A, const u64* __restrict__ full,
+                                                        const u64* __restrict__ hasinc, int32_t* __restrict__ list,
+                                                        u64* __restrict__ n_list) {
+    __shared__ int wsum[4];
+    __shared__ u64 sbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nw = (A + 63) / 64;
+    for (int64_t w0 = (int64_t)blockIdx.x * 256; w0 < nw; w0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        const int64_t w = w0 + threadIdx.x;
+        u64 x = w < nw ? (hasinc[w] & ~full[w]) : 0ull;   // hasinc is zero beyond A
+        const int c = __popcll(x);
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int k = 0; k < 4; ++k) {
+            before += k < wv ? wsum[k] : 0;
+            total += wsum[k];
+        }
+        if (threadIdx.x == 0) sbase = total ? atomicAdd(n_list, (u64)total) : 0ull;
+        __syncthreads();
+        u64 pos = sbase + (u64)(before + incl - c);
+        while (x) {
+            const int b = __ffsll((long long)x) - 1;
+            list[pos++] = (int32_t)(w * 64 + b);
+            x &= x - 1ull;
+        }
+        __syncthreads();   // wsum / sbase are rewritten by the next chunk
     }
 }
 
@@ -1900,6 +1932,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
     int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
+    u64* hasinc = nullptr;   // atoms with incidence (non-full pull levels), made on first use
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
     u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
@@ -1936,8 +1969,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
                 u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slot
                 HGX_HIP(hipMemsetAsync(n_list, 0, sizeof(u64), s));
-                hgx_nonfull_list<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, full, g->inc_off, clist,
-                                                                                         n_list);
+                if (!hasinc) {
+                    hasinc = (u64*)g->alloc(bm_bytes);
+                    hgx_hasinc<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, g->inc_off, hasinc);
+                    HGX_CHECK_LAUNCH();
+                }
+                hgx_nonfull_list<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, full, hasinc, clist, n_list);
                 HGX_CHECK_LAUNCH();
                 hgx_nf_pull<W><<<4096, 256, 0, s>>>(clist, n_list, g->inc_off, g->inc_row, g->inc_type, want_type,
                                                     g->tgt_off, g->tgt_idx, fa, lvl, vis, ever, full, lvl_next, fa_next,
@@ -2104,6 +2141,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     g->release(la, la_bytes);
     if (lcand) g->release(lcand, la_bytes);
     if (cand) g->release(cand, bm_bytes);
+    if (hasinc) g->release(hasinc, bm_bytes);
     if (flist) g->release(flist, flist_bytes);
     if (clist) g->release(clist, flist_bytes);
     g->release(ctr, sizeof(u64) * kCtrBlock * max_levels_cap);
