@@ -1250,7 +1250,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
 // no lf rows.  Atom t's next row = OR over links L in inc(t) (type-filtered) of OR over targets u
 // of L in the frontier of lvl[u] (t's own row is a subset of vis[t] and masks out), minus vis[t].
 // ---------------------------------------------------------------------------------------------
-// bit v of hasinc <=> inc(v) is non-empty (computed once per batch, for the non-full list)
+// bit v of hasinc <=> inc(v) is non-empty (computed once per snapshot, for the non-full list)
 __global__ void __launch_bounds__(256) hgx_hasinc(int64_t A, const int64_t* __restrict__ inc_off,
                                                   u64* __restrict__ hasinc) {
     const int lane = threadIdx.x & 63;
@@ -1932,7 +1932,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
     int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
-    u64* hasinc = nullptr;   // atoms with incidence (non-full pull levels), made on first use
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
     u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
@@ -1969,11 +1968,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
                 u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slot
                 HGX_HIP(hipMemsetAsync(n_list, 0, sizeof(u64), s));
-                if (!hasinc) {
-                    hasinc = (u64*)g->alloc(bm_bytes);
-                    hgx_hasinc<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, g->inc_off, hasinc);
+                if (!g->hasinc) {   // once per snapshot
+                    HGX_HIP(hipMalloc(&g->hasinc, sizeof(u64) * (size_t)(ceil_div(A, 64) + 1)));
+                    hgx_hasinc<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, g->inc_off, (u64*)g->hasinc);
                     HGX_CHECK_LAUNCH();
                 }
+                const u64* hasinc = (const u64*)g->hasinc;
                 hgx_nonfull_list<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, full, hasinc, clist, n_list);
                 HGX_CHECK_LAUNCH();
                 hgx_nf_pull<W><<<4096, 256, 0, s>>>(clist, n_list, g->inc_off, g->inc_row, g->inc_type, want_type,
@@ -2141,7 +2141,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     g->release(la, la_bytes);
     if (lcand) g->release(lcand, la_bytes);
     if (cand) g->release(cand, bm_bytes);
-    if (hasinc) g->release(hasinc, bm_bytes);
     if (flist) g->release(flist, flist_bytes);
     if (clist) g->release(clist, flist_bytes);
     g->release(ctr, sizeof(u64) * kCtrBlock * max_levels_cap);

@@ -30,6 +30,7 @@ void graph_release(hgx_graph* g) {
     (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
     (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->zacc) (void)hipFree(g->zacc);
+    if (g->hasinc) (void)hipFree(g->hasinc);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {

@@ -128,6 +128,7 @@ struct hgx_graph {
     // into it and its finalise re-zeroes exactly the rows it consumed (no per-level clear).
     std::vector<int64_t> inc_off_host;   // host copy of inc_off (pattern planning), made on first use
     uint64_t* zacc = nullptr;
+    uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
     size_t zacc_bytes = 0;
     bool zacc_clean = false;
 

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile_round.sh output directory into profiles/.
 
-  python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> [workload]
+  python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> [workload] [--until KERNEL]
+
+--until KERNEL keeps only the dispatches before the first launch of a kernel whose name contains
+KERNEL after the first BFS gather (bench.py runs config 2 first, then builds the config-3 snapshot:
+`--until k_validate` isolates the config-2 leg of the default bench command).
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
@@ -38,37 +42,60 @@ def short(name):
     return name.split("(")[0][-60:]
 
 
-def load_counter(path, counter):
+def cutoff(rows, until, after="hgx_link_gather"):
+    """Dispatch id of the first launch of `until` that follows a launch of `after` (None = keep
+    everything)."""
+    if not until:
+        return None
+    first = [int(r["Dispatch_Id"]) for r in rows if after in r["Kernel_Name"]]
+    if not first:
+        return None
+    ids = [int(r["Dispatch_Id"]) for r in rows if until in r["Kernel_Name"] and int(r["Dispatch_Id"]) > min(first)]
+    return min(ids) if ids else None
+
+
+def load_counter(path, counter, until=None):
     acc = defaultdict(list)
     if not os.path.exists(path):
         return acc
     with open(path) as f:
-        for row in csv.DictReader(f):
-            if row["Counter_Name"] == counter:
-                acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+        rows = list(csv.DictReader(f))
+    cut = cutoff(rows, until)
+    for row in rows:
+        if row["Counter_Name"] == counter and (cut is None or int(row["Dispatch_Id"]) < cut):
+            acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
     return acc
 
 
-def load_trace(path):
+def load_trace(path, until=None):
     acc = defaultdict(list)
     with open(path) as f:
-        for row in csv.DictReader(f):
+        rows = list(csv.DictReader(f))
+    cut = cutoff(rows, until)
+    for row in rows:
+        if cut is None or int(row["Dispatch_Id"]) < cut:
             acc[short(row["Kernel_Name"])].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
     return acc
 
 
 def main():
-    d, tag = sys.argv[1], sys.argv[2]
-    workload = sys.argv[3] if len(sys.argv) > 3 else "config2"
+    argv = sys.argv[1:]
+    until = None
+    if "--until" in argv:
+        k = argv.index("--until")
+        until = argv[k + 1]
+        del argv[k:k + 2]
+    d, tag = argv[0], argv[1]
+    workload = argv[2] if len(argv) > 2 else "config2"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"))
-    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until)
+    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until)
+    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until)
     rows, js = [], {"tag": tag, "workload": workload, "kernels": {},
                     "note": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE correction)"}
     for k in sorted(trace, key=lambda k: -sum(trace[k])):
@@ -87,6 +114,8 @@ def main():
         json.dump(js, f, indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary {tag} ({workload})\n\n")
+        if until:
+            f.write(f"Dispatches before the first `{until}` launch after the BFS only (the {workload} leg of the command).\n\n")
         f.write("Kernel trace: `rocprofv3 --kernel-trace --stats`; HBM bytes from separate `--pmc FETCH_SIZE` and\n"
                 "`--pmc WRITE_SIZE` passes, bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch.\n\n")
         f.write("| kernel | launches | total ms | avg ms | fetch B/launch | write B/launch | HBM GB/s |\n")
