@@ -32,6 +32,7 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->hasinc) (void)hipFree(g->hasinc);
     if (g->pinned) (void)hipHostFree(g->pinned);
+    if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {
         (void)hipFree(g->shard->l2g); (void)hipFree(g->shard->own_l); (void)hipFree(g->shard->own_bm);
@@ -193,6 +194,18 @@ void* hgx_graph::pinned_buf(size_t bytes) {
         pinned_bytes = n;
     }
     return pinned;
+}
+
+void* hgx_graph::mapped_buf(size_t bytes) {
+    if (bytes > mapped_bytes) {
+        if (mapped) (void)hipHostFree(mapped);
+        mapped = nullptr;
+        mapped_bytes = 0;
+        const size_t n = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+        HGX_HIP(hipHostMalloc(&mapped, n, hipHostMallocMapped));
+        mapped_bytes = n;
+    }
+    return mapped;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -157,10 +157,15 @@ struct hgx_graph {
     std::vector<hgx::PoolBuf> pool;  // free device buffers for reuse across batches
     void* pinned = nullptr;          // small pinned host staging area
     size_t pinned_bytes = 0;
+    void* mapped = nullptr;          // host-mapped result area the pattern kernels write into
+    size_t mapped_bytes = 0;
+    int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
+    int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
 
     void* alloc(size_t bytes);
     void release(void* p, size_t bytes);
     void* pinned_buf(size_t bytes);
+    void* mapped_buf(size_t bytes);
 };
 
 namespace hgx {

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 
 #include "hgx_internal.h"
 
@@ -36,6 +37,7 @@ constexpr int kMaxPattern = 64;     // targets of one OrderedLinkCondition
 constexpr int kMaxPatterns = 16;    // OrderedLinkConditions in one And
 constexpr int kMaxPositioned = 16;  // PositionedIncidentConditions in one And
 constexpr int kMaxTypes = 1 << 16;  // types of one Or (TypePlusCondition)
+constexpr int kQShards = 16, kQStride = 16;   // counter replicas of the match kernel
 
 struct QPlan {
     int64_t beg;    // first incidence entry of the smallest anchor set
@@ -109,52 +111,336 @@ __global__ void __launch_bounds__(256) k_low32(int64_t n, const u64* __restrict_
 }
 
 __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t b, int64_t e, int32_t v) {
-    while (b < e) {
-        const int64_t m = (b + e) >> 1;
-        if (a[m] < v) b = m + 1; else e = m;
+    // 8-ary steps while the range is long: 7 independent probes per step (log8 dependent loads
+    // instead of log2), then one step of 8 independent probes
+    while (e - b > 8) {
+        const int64_t step = (e - b) >> 3;
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) c += a[b + (j + 1) * step] < v;
+        const int64_t nb = c > 0 ? b + c * step + 1 : b;
+        e = c < 7 ? b + (c + 1) * step : e;
+        b = nb;
     }
-    return b;
+    {   // <= 8 left: independent probes
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c += (b + j < e) && a[b + j] < v;
+        return b + c;
+    }
 }
 
 // Plan per query (AndToQuery sorts the ORA inputs by size, :164-180): the anchor whose candidate
 // range is smallest drives the scan.  With exactly one type the candidate range of an anchor is
 // its type-T slice of the type-grouped incidence (the type index intersected for free); otherwise
 // its whole incidence row with the streamed type filter.  pad = 1 marks a type-grouped plan.
+// Plan of a query whose (distinct) anchors are in registers (na <= kRegAnchors).  The incidence
+// bounds of every anchor are loaded together and the anchor with the fewest incident links drives
+// the scan; with one type its type-T slice is found by an 8-ary search that brackets both bounds
+// (`single`, `single + 1`) with probes issued together -- a chain of ~log8(deg) dependent loads per
+// query.  (AndToQuery orders its ORA inputs by their size estimate; any anchor gives the same result
+// set, the smallest untyped one only bounds the candidates.)
+constexpr int kRegAnchors = 8;
+
+__device__ __forceinline__ QPlan plan_regs(const int32_t (&av)[kRegAnchors], int na, int32_t single,
+                                           const int64_t* __restrict__ inc_off, const int32_t* __restrict__ ts_type) {
+    int64_t lo[kRegAnchors], hi[kRegAnchors];
+#pragma unroll
+    for (int k = 0; k < kRegAnchors; ++k) {
+        lo[k] = k < na ? inc_off[av[k]] : 0;
+        hi[k] = k < na ? inc_off[av[k] + 1] : 0;
+    }
+    QPlan p{0, 0, 0, 0};
+    if (na == 0) return p;
+    int best = 0;
+#pragma unroll
+    for (int k = 1; k < kRegAnchors; ++k)
+        if (k < na && hi[k] - lo[k] < hi[best] - lo[best]) best = k;
+    int64_t b = 0, e = 0;
+#pragma unroll
+    for (int k = 0; k < kRegAnchors; ++k)
+        if (k == best) {
+            b = lo[k];
+            e = hi[k];
+        }
+    if (single >= 0) {
+        int64_t b1 = b, e1 = e, b2 = b, e2 = e;   // brackets of lower_bound(single), lower_bound(single + 1)
+        while (e1 - b1 > 8 || e2 - b2 > 8) {
+            const int64_t s1 = (e1 - b1) >> 3, s2 = (e2 - b2) >> 3;
+            int32_t p1[7], p2[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                p1[j] = ts_type[b1 + (j + 1) * s1];
+                p2[j] = ts_type[b2 + (j + 1) * s2];
+            }
+            if (e1 - b1 > 8) {
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) c += p1[j] < single;
+                const int64_t nb = c > 0 ? b1 + c * s1 + 1 : b1;
+                e1 = c < 7 ? b1 + (c + 1) * s1 : e1;
+                b1 = nb;
+            }
+            if (e2 - b2 > 8) {
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) c += p2[j] < single + 1;
+                const int64_t nb = c > 0 ? b2 + c * s2 + 1 : b2;
+                e2 = c < 7 ? b2 + (c + 1) * s2 : e2;
+                b2 = nb;
+            }
+        }
+        int32_t t1[8], t2[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            t1[j] = b1 + j < e1 ? ts_type[b1 + j] : INT32_MAX;
+            t2[j] = b2 + j < e2 ? ts_type[b2 + j] : INT32_MAX;
+        }
+        int c1 = 0, c2 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c1 += t1[j] < single;
+            c2 += t2[j] < single + 1;
+        }
+        b = b1 + c1;
+        e = b2 + c2;
+    }
+    p.beg = b;
+    p.n = e - b;
+    p.amin = best;
+    p.pad = single >= 0 ? 1 : 0;
+    return p;
+}
+
+__device__ __forceinline__ QPlan plan_query(const QDesc& d, bool nop, const int32_t* __restrict__ anchors,
+                                            const int32_t* __restrict__ types, const int64_t* __restrict__ inc_off,
+                                            const int32_t* __restrict__ ts_type) {
+    QPlan p{0, 0, 0, 0};
+    if (nop) return p;
+    const int32_t single = (d.t_end - d.t_beg == 1) ? types[d.t_beg] : -1;
+    int64_t best = -1;
+    for (int64_t k = d.a_beg; k < d.a_end; ++k) {
+        const int32_t a = anchors[k];
+        int64_t b = inc_off[a], e = inc_off[a + 1];
+        if (single >= 0) {
+            b = lower_bound_i32(ts_type, b, e, single);
+            e = lower_bound_i32(ts_type, b, e, single + 1);
+        }
+        if (best < 0 || e - b < best) {
+            best = e - b;
+            p.beg = b;
+            p.amin = (int32_t)(k - d.a_beg);
+        }
+    }
+    p.n = best < 0 ? 0 : best;
+    p.pad = single >= 0 ? 1 : 0;
+    return p;
+}
+
 __global__ void __launch_bounds__(256) hgx_q_plan(int32_t n, const QDesc* __restrict__ desc,
                                                   const int32_t* __restrict__ anchors, const int32_t* __restrict__ types,
                                                   const int32_t* __restrict__ nop, const int64_t* __restrict__ inc_off,
                                                   const int32_t* __restrict__ ts_type, QPlan* __restrict__ plan,
-                                                  int32_t* __restrict__ nchunks) {
+                                                  int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
     const QDesc d = desc[q];
-    QPlan p{0, 0, 0, 0};
-    if (!nop[q]) {
-        const int32_t single = (d.t_end - d.t_beg == 1) ? types[d.t_beg] : -1;
-        int64_t best = -1;
-        for (int64_t k = d.a_beg; k < d.a_end; ++k) {
-            const int32_t a = anchors[k];
-            int64_t b = inc_off[a], e = inc_off[a + 1];
-            if (single >= 0) {
-                b = lower_bound_i32(ts_type, b, e, single);
-                e = lower_bound_i32(ts_type, b, e, single + 1);
-            }
-            if (best < 0 || e - b < best) {
-                best = e - b;
-                p.beg = b;
-                p.amin = (int32_t)(k - d.a_beg);
-            }
-        }
-        p.n = best < 0 ? 0 : best;
-        p.pad = single >= 0 ? 1 : 0;
+    QPlan p;
+    if (d.a_end - d.a_beg <= kRegAnchors && !nop[q]) {
+        int32_t av[kRegAnchors];
+        const int na = (int)(d.a_end - d.a_beg);
+#pragma unroll
+        for (int k = 0; k < kRegAnchors; ++k) av[k] = k < na ? anchors[d.a_beg + k] : 0;
+        p = plan_regs(av, na, (d.t_end - d.t_beg == 1) ? types[d.t_beg] : -1, inc_off, ts_type);
+    } else {
+        p = plan_query(d, nop[q] != 0, anchors, types, inc_off, ts_type);
     }
     plan[q] = p;
     nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
+    ncand[q] = p.n;
 }
 
-__global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off, int32_t* __restrict__ chunk_q) {
+// Packed batch (hgx_pattern_batch_packed) normalised on the device, one thread per query:
+// ExpressionBasedQuery.expand adds incident(x) for every non-ANY target of the orderedLink (:730-737),
+// the toDNF HashSet drops duplicate anchors (:100).  The anchors of query q go to the fixed slot
+// inc_off[q] + pat_off[q] (room for all of them), its type is type[q], its pattern row q of pat_off,
+// so no scan is needed.  Bad queries are reported through err[0] (invalid) / err[1] (unsupported) as
+// the smallest offending query index; the plan is computed in the same pass.
+__global__ void __launch_bounds__(256) hgx_q_norm_packed(
+    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
+    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
+    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
+    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
+    int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand, int32_t* __restrict__ err) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
+    const int32_t tq = type[q];
+    const int64_t b = inc_off[q], e = inc_off[q + 1];
+    const bool ho = has_ordered[q] != 0;
+    const int64_t pb = pat_off[q], pe = pat_off[q + 1];
+    QDesc d;
+    d.a_beg = b + pb;
+    d.t_beg = q;
+    d.t_end = q + (tq >= 0 ? 1 : 0);
+    d.s_beg = d.s_end = 0;
+    d.r_beg = q;
+    d.r_end = q + (ho ? 1 : 0);
+    d.arity = -1;
+    d.pad = 0;
+    bool bad = tq < -1 || e < b || pe < pb, unsup = false;
+    int64_t na = 0;
+    int32_t av[kRegAnchors];   // the first kRegAnchors distinct anchors also stay in registers
+#pragma unroll
+    for (int k = 0; k < kRegAnchors; ++k) av[k] = -1;
+    auto add = [&](int32_t h) {
+        if (h < 0 || h >= A) {
+            bad = true;
+            return;
+        }
+        bool dup = false;
+#pragma unroll
+        for (int k = 0; k < kRegAnchors; ++k) dup |= av[k] == h;
+        for (int64_t k = kRegAnchors; k < na && !dup; ++k) dup = anchors[d.a_beg + k] == h;
+        if (dup) return;
+#pragma unroll
+        for (int k = 0; k < kRegAnchors; ++k)
+            if (k == na) av[k] = h;
+        anchors[d.a_beg + na++] = h;
+    };
+    if (!bad) {
+        for (int64_t i = b; i < e && !bad; ++i) add(inc[i]);
+        if (ho) {
+            if (pe - pb > kMaxPattern) unsup = true;
+            for (int64_t i = pb; i < pe && !bad; ++i)
+                if (pat[i] != HGX_ANY_HANDLE) add(pat[i]);
+        }
+    }
+    d.a_end = d.a_beg + na;
+    if (!bad && na == 0) unsup = true;
+    if (na > kMaxAnchors) unsup = true;
+    const bool isnop = ho && pe == pb;   // an empty OrderedLinkCondition compiles to HGQuery.NOP
+    if (bad) atomicMin(&err[0], q);
+    else if (unsup) atomicMin(&err[1], q);
+    desc[q] = d;
+    nop[q] = isnop ? 1 : 0;
+    QPlan p{0, 0, 0, 0};
+    if (!bad && !unsup && !isnop)
+        p = na <= kRegAnchors ? plan_regs(av, (int)na, tq, g_inc_off, ts_type)
+                              : plan_query(d, false, anchors, type, g_inc_off, ts_type);
+    plan[q] = p;
+    nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
+    ncand[q] = p.n;
+}
+
+// Small batches (n <= kSmallBatch): one workgroup scans the chunk counts and candidate counts, writes
+// the chunk -> query map and checks both totals against the workspace capacity.  stat[0] = total
+// chunks, stat[1] = total candidates, stat[2] = 1 on overflow (the match then sees no chunks).
+constexpr int kSmallBatch = 16384;   // <= 16 queries per thread of the scan block
+constexpr int kScanBlock = 1024;
+
+// Sum of a[b, e) with the loads of each 16-element step issued together (a plain loop waits on
+// every load before the next add).
+template <typename T>
+__device__ __forceinline__ T seg_sum(const T* __restrict__ a, int64_t b, int64_t e) {
+    T s = 0;
+    for (int64_t x = b; x < e; x += 16) {
+        T v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = x + j < e ? a[x + j] : (T)0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    return s;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* wsum, T& total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const T y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    T before = 0;
+    total = 0;
+    for (int k = 0; k < nw; ++k) {
+        before += k < wv ? wsum[k] : (T)0;
+        total += wsum[k];
+    }
+    __syncthreads();
+    return before + incl - v;
+}
+
+__global__ void __launch_bounds__(kScanBlock) hgx_q_scan_small(int32_t n, const int32_t* __restrict__ nch,
+                                                                const int64_t* __restrict__ ncand,
+                                                                int32_t* __restrict__ choff, int64_t* __restrict__ coff,
+                                                                int32_t* __restrict__ chq, int64_t cap_chunks,
+                                                                int64_t cap_cand, int64_t* __restrict__ stat,
+                                                                u64* __restrict__ ctr) {
+    __shared__ int32_t ws32[kScanBlock / 64];
+    __shared__ int64_t ws64[kScanBlock / 64];
+    if (threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;   // the match's counter shards
+    // thread t owns the contiguous queries [t*per, (t+1)*per): its loads are independent and in flight
+    // together, then one block scan of the per-thread sums
+    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kSmallBatch)
+    const int32_t q0 = threadIdx.x * per;
+    int32_t cv[16];
+    int64_t kv[16];
+    int32_t sc = 0;
+    int64_t sk = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {   // every load issued before any is used
+        const bool in = j < per && q0 + j < n;
+        cv[j] = in ? nch[q0 + j] : 0;
+        kv[j] = in ? ncand[q0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        sc += cv[j];
+        sk += kv[j];
+    }
+    int32_t tc;
+    int64_t tk;
+    int32_t ec = block_exclusive_scan<int32_t>(sc, ws32, tc);
+    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
+    const bool over = tc > cap_chunks || tk > cap_cand;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j < per && q0 + j < n) {
+            const int32_t q = q0 + j;
+            choff[q] = ec;
+            coff[q] = ek;
+            if (!over)
+                for (int32_t i = 0; i < cv[j]; ++i) chq[ec + i] = q;
+        }
+        ec += cv[j];
+        ek += kv[j];
+    }
+    if (threadIdx.x == 0) {
+        choff[n] = over ? 0 : tc;   // the match reads its chunk count here
+        coff[n] = tk;
+        stat[0] = tc;
+        stat[1] = tk;
+        stat[2] = over ? 1 : 0;
+    }
+}
+
+// Large batches: totals after the device scans, overflow check, chunk count for the match.
+__global__ void hgx_q_check(int32_t n, int32_t* __restrict__ choff, const int64_t* __restrict__ coff,
+                            int64_t cap_chunks, int64_t cap_cand, int64_t* __restrict__ stat) {
+    const int64_t c = choff[n], k = coff[n];
+    stat[0] = c;
+    stat[1] = k;
+    stat[2] = (c > cap_chunks || k > cap_cand) ? 1 : 0;
+    if (stat[2]) choff[n] = 0;
+}
+
+__global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ stat,
+                                int32_t* __restrict__ chunk_q) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n || stat[2]) return;   // nothing is matched after a workspace overflow
     for (int32_t c = chunk_off[q]; c < chunk_off[q + 1]; ++c) chunk_q[c] = q;
 }
 
@@ -167,7 +453,6 @@ __global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off
 //            target row, anchor / positioned / ordered / arity checks; hits are compacted in order.
 // The type filter passes ~1/T of the candidates, so stage 3 runs on full waves instead of lanes
 // idling behind failed type checks.  Hits of a chunk land in its own candidate range of slots.
-constexpr int kQShards = 16, kQStride = 16;
 constexpr int kPerLane = kQChunk / 64;
 
 __global__ void __launch_bounds__(256) hgx_pattern_match(
@@ -179,8 +464,10 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const int32_t* __restrict__ tgt_idx, int32_t* __restrict__ slots, int64_t* __restrict__ counts,
     u64* __restrict__ ctr) {
     __shared__ int32_t lds[4][kQChunk];
+    __shared__ int32_t lds_anch[4][kMaxAnchors];
     const int32_t n_chunks = *n_chunks_p;
     int32_t* list = lds[threadIdx.x >> 6];
+    int32_t* anch = lds_anch[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -229,7 +516,19 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
         pre -= cnt;
         for (unsigned m = passm; m; m &= m - 1u) list[pre++] = lane * kPerLane + __ffs(m) - 1;
         __builtin_amdgcn_wave_barrier();
-        // stage 3
+        // stage 3: the query's anchors go to LDS and a single short pattern to registers (wave-uniform
+        // values); a candidate's target row of <= 8 entries is loaded once into registers and every
+        // check runs on them -- three dependent loads per candidate (link row, offsets, targets)
+        const int na = (int)(d.a_end - d.a_beg);
+        if (lane < na && lane < kMaxAnchors) anch[lane] = anchors[d.a_beg + lane];
+        const bool one_pat = d.r_end - d.r_beg == 1;
+        const int64_t pb0 = one_pat ? p_off[d.r_beg] : 0;
+        const int np0 = one_pat ? (int)(p_off[d.r_beg + 1] - pb0) : 0;
+        const bool reg_pat = one_pat && np0 <= 8;
+        int32_t pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pv[k] = (reg_pat && k < np0) ? pattern[pb0 + k] : 0;
+        __builtin_amdgcn_wave_barrier();
         int32_t written = 0;
         int32_t* out = slots + cand_off[q] + c0;
         for (int base = 0; base < total; base += 64) {   // wave-uniform
@@ -245,28 +544,68 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
                 const int32_t* row = tgt_idx + b;
                 // ArityCondition: layout.length == arity + 2
                 if (d.arity >= 0) hit = n == d.arity;
-                // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
-                for (int64_t j = d.a_beg; j < d.a_end && hit; ++j) {
-                    if (j - d.a_beg == pl.amin) continue;
-                    const int32_t a = anchors[j];
-                    bool found = false;
-                    for (int i = 0; i < n; ++i) found |= (row[i] == a);
-                    hit = found;
-                }
-                // PositionedIncidentCondition (its ORA set: inc(target) filtered by the predicate)
-                for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
-                    hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
-                // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
-                for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
-                    const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
-                    int i = 0;
-                    int64_t j = 0;
-                    while (i < n && j < np) {
-                        const int32_t pj = pattern[pb + j];
-                        if (pj < 0 || pj == row[i]) ++j;
-                        ++i;
+                if (n <= 8) {
+                    int32_t tr[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
+                    // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
+                    for (int j = 0; j < na && hit; ++j) {
+                        if (j == pl.amin) continue;
+                        const int32_t a = anch[j];
+                        bool found = false;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) found |= (i < n) && tr[i] == a;
+                        hit = found;
                     }
-                    hit = (j == np);
+                    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
+                        hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
+                    if (hit && reg_pat) {   // OrderedLinkCondition.satisfies on registers
+                        int j = 0;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            int32_t pj = pv[0];
+#pragma unroll
+                            for (int k = 1; k < 8; ++k)
+                                if (j == k) pj = pv[k];
+                            if (i < n && j < np0 && (pj < 0 || pj == tr[i])) ++j;
+                        }
+                        hit = j == np0;
+                    } else {
+                        for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
+                            const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
+                            int i = 0;
+                            int64_t j = 0;
+                            while (i < n && j < np) {
+                                const int32_t pj = pattern[pb + j];
+                                if (pj < 0 || pj == row[i]) ++j;
+                                ++i;
+                            }
+                            hit = (j == np);
+                        }
+                    }
+                } else {
+                    for (int64_t j = d.a_beg; j < d.a_end && hit; ++j) {
+                        if (j - d.a_beg == pl.amin) continue;
+                        const int32_t a = anchors[j];
+                        bool found = false;
+                        for (int i = 0; i < n; ++i) found |= (row[i] == a);
+                        hit = found;
+                    }
+                    // PositionedIncidentCondition (its ORA set: inc(target) filtered by the predicate)
+                    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
+                        hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
+                    // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
+                    for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
+                        const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
+                        int i = 0;
+                        int64_t j = 0;
+                        while (i < n && j < np) {
+                            const int32_t pj = pattern[pb + j];
+                            if (pj < 0 || pj == row[i]) ++j;
+                            ++i;
+                        }
+                        hit = (j == np);
+                    }
                 }
             }
             const u64 m = __ballot(hit);
@@ -304,9 +643,98 @@ __global__ void __launch_bounds__(256) hgx_q_scatter(const int32_t* __restrict__
 }
 
 __global__ void hgx_q_offsets(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ out_off,
-                              int64_t* __restrict__ q_off) {
+                              const int64_t* __restrict__ stat, int64_t* __restrict__ q_off) {
     int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q <= n) q_off[q] = out_off[chunk_off[q]];
+    if (q <= n && !stat[2]) q_off[q] = out_off[chunk_off[q]];
+}
+
+// Small batches: one workgroup scans the per-chunk hit counts, writes the per-query offsets and sums
+// the counter shards (stat[3] = total hits); hgx_q_scatter then copies the hits, a wave per chunk
+// (a chunk loop inside one workgroup serialised ~5 dependent loads per chunk: 0.77 ms at 10K queries).
+__global__ void __launch_bounds__(kScanBlock) hgx_q_finish_small(
+    int32_t n, const int32_t* __restrict__ chunk_off, const int32_t* __restrict__ chunk_q,
+    const int64_t* __restrict__ cand_off, const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
+    const int32_t* __restrict__ link_atom, const u64* __restrict__ ctr, int64_t* __restrict__ outoff,
+    int64_t* __restrict__ q_off, int32_t* __restrict__ out, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
+    const int32_t* __restrict__ err) {
+    __shared__ int64_t ws[kScanBlock / 64];
+    if (stat[2]) {   // workspace overflow: nothing was matched, the host re-runs
+        if (threadIdx.x == 0) {
+            stat[3] = 0;
+            stat[4] = err ? err[0] : INT32_MAX;
+            stat[5] = err ? err[1] : INT32_MAX;
+        }
+        return;
+    }
+    const int32_t nc = chunk_off[n];
+    const int32_t per = (nc + kScanBlock - 1) / kScanBlock;
+    const int32_t c0 = threadIdx.x * per, c1 = min(nc, c0 + per);
+    int64_t tot, e;
+    if (per <= 16) {   // counts in registers: one round of loads
+        int64_t kv[16];
+        int64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) kv[j] = c0 + j < c1 ? counts[c0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += kv[j];
+        e = block_exclusive_scan<int64_t>(sum, ws, tot);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (c0 + j < c1) outoff[c0 + j] = e;
+            e += kv[j];
+        }
+    } else {
+        const int64_t sum = seg_sum<int64_t>(counts, c0, c1);
+        e = block_exclusive_scan<int64_t>(sum, ws, tot);
+        for (int32_t c = c0; c < c1; ++c) {
+            outoff[c] = e;
+            e += counts[c];
+        }
+    }
+    if (threadIdx.x == 0) {
+        outoff[nc] = tot;
+        stat[3] = tot;
+        stat[4] = err ? err[0] : INT32_MAX;
+        stat[5] = err ? err[1] : INT32_MAX;
+    }
+    __syncthreads();
+    {   // n <= kSmallBatch: <= 17 offsets per thread, both load rounds issued together
+        constexpr int R = kSmallBatch / kScanBlock + 1;
+        int32_t co[R];
+        int64_t ov[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int32_t q = threadIdx.x + j * kScanBlock;
+            co[j] = q <= n ? chunk_off[q] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) ov[j] = outoff[co[j]];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int32_t q = threadIdx.x + j * kScanBlock;
+            if (q <= n) q_off[q] = ov[j];
+        }
+    }
+    if (threadIdx.x < qNum) {
+        u64 v = 0;
+        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
+        ctr_out[threadIdx.x] = v;
+    }
+}
+
+__global__ void hgx_q_finish_stat(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ outoff,
+                                  const u64* __restrict__ ctr, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
+                                  const int32_t* __restrict__ err) {
+    if (threadIdx.x == 0) {
+        stat[3] = outoff[chunk_off[n]];
+        stat[4] = err ? err[0] : INT32_MAX;
+        stat[5] = err ? err[1] : INT32_MAX;
+    }
+    if (threadIdx.x < qNum) {
+        u64 v = 0;
+        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
+        ctr_out[threadIdx.x] = v;
+    }
 }
 
 }  // namespace hgx
@@ -421,6 +849,8 @@ void normalise(hgx_graph* g, int32_t n, Get get, NormBatch& nb) {
 }
 
 int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out);
+int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                     const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result** out);
 
 }  // namespace
 
@@ -454,24 +884,7 @@ extern "C" int hgx_pattern_batch_packed(hgx_graph* g, int32_t n, const int32_t* 
     if (!g || !out || n < 0 || (n > 0 && (!type || !inc_off || !pat_off || !has_ordered)))
         fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad argument");
     *out = nullptr;
-    NormBatch nb;
-    std::vector<int64_t> one_off;
-    const double t0 = now_ms();
-    normalise(g, n,
-              [&](int32_t q, QueryIn& in) {
-                  if (type[q] < HGX_NO_TYPE) fail(HGX_E_INVALID, "hgx_pattern_batch: bad type");
-                  in.n_types = type[q] >= 0 ? 1 : 0;
-                  in.types = type + q;
-                  in.n_inc = (int32_t)(inc_off[q + 1] - inc_off[q]);
-                  in.inc = inc ? inc + inc_off[q] : nullptr;
-                  one_off.assign({0, pat_off[q + 1] - pat_off[q]});
-                  in.n_pat = has_ordered[q] ? 1 : 0;
-                  in.pat_off = one_off.data();
-                  in.pat = pat ? pat + pat_off[q] : nullptr;
-              },
-              nb);
-    if (std::getenv("HGX_QUERY_PROFILE")) std::fprintf(stderr, "[hgx query] normalise %.3f ms\n", now_ms() - t0);
-    return run_batch(g, n, nb, out);
+    return run_batch_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, out);
     HGX_API_END
 }
 
@@ -542,186 +955,300 @@ void ensure_type_grouped(hgx_graph* g) {
     g->inc_ts_type = ts_type;
 }
 
-int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
-    HGX_API_BEGIN
-    const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
-    double t0 = now_ms();
-    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
-    const std::vector<int32_t>& anchors = nb.anchors;
-    hgx_query_result* r = new hgx_query_result();
-    struct Guard {
-        hgx_query_result* r;
-        ~Guard() { delete r; }
-    } guard{r};
-    r->n = n;
-    r->offsets.assign(n + 1, 0);
-    if (n == 0) {
-        guard.r = nullptr;
-        *out = r;
-        return HGX_OK;
-    }
-    std::lock_guard<std::mutex> lk(g->mu);
-    HGX_HIP(hipSetDevice(g->device));
-    hipStream_t s = g->stream;
-    if (g->inc_off_host.empty()) {   // host copy of the incidence offsets: buffer sizing needs no round trip
-        g->inc_off_host.resize((size_t)g->A + 1);
-        HGX_HIP(hipMemcpyAsync(g->inc_off_host.data(), g->inc_off, sizeof(int64_t) * (g->A + 1), hipMemcpyDeviceToHost,
-                               s));
-        HGX_HIP(hipStreamSynchronize(s));
-    }
-    ensure_type_grouped(g);
-    // Upper bounds from the untyped plan (the device plan can only shrink a query's range): the
-    // chunk count and each query's slot base in the flat candidate space.
-    std::vector<int64_t> cand_off(n + 1, 0);
-    const int64_t* io = g->inc_off_host.data();
-    int64_t nc_ub = 0;
-    for (int32_t q = 0; q < n; ++q) {
-        int64_t best = 0;
-        if (!nb.nop[q]) {
-            best = -1;
-            for (int64_t k = nb.desc[q].a_beg; k < nb.desc[q].a_end; ++k) {
-                const int32_t a = anchors[k];
-                const int64_t d = io[a + 1] - io[a];
-                if (best < 0 || d < best) best = d;
-            }
-        }
-        cand_off[q + 1] = cand_off[q] + best;
-        nc_ub += (best + kQChunk - 1) / kQChunk;
-    }
-    if (nc_ub > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
-    const double t_plan = now_ms();
-    const int64_t total_ub = cand_off[n];
-    const int32_t nc = (int32_t)std::max<int64_t>(nc_ub, 1);
+// Device arrays of one normalised batch (built by a front end) and the per-query plan.
+struct Front {
+    const QDesc* desc = nullptr;
+    const int32_t* anch = nullptr;
+    const int32_t* types = nullptr;
+    const int32_t* pos = nullptr;
+    const int64_t* poff = nullptr;
+    const int32_t* pat = nullptr;
+    QPlan* plan = nullptr;
+    int32_t* nch = nullptr;      // [n + 1]
+    int64_t* ncand = nullptr;    // [n + 1]
+    int32_t* err = nullptr;      // [2] device-side normalisation errors (packed front end), or null
+    double cond_bytes = 0;       // condition bytes read by the match (algorithmic accounting)
+};
 
-    // one pinned staging buffer, one upload
+// Buffers taken from the graph pool for one call, released on every exit path.
+struct Scratch {
+    hgx_graph* g;
+    std::vector<std::pair<void*, size_t>> t;
+    void* take(size_t bytes) {
+        void* p = g->alloc(bytes);
+        t.push_back({p, bytes});
+        return p;
+    }
+    ~Scratch() { for (auto& x : t) g->release(x.first, x.second); }
+};
+
+struct Events {
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool on = false;
+    void init(bool timing) {
+        on = timing;
+        if (on) for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&e[i]));
+    }
+    void rec(int i, hipStream_t s) { if (on) HGX_HIP(hipEventRecord(e[i], s)); }
+    ~Events() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
+};
+
+template <class T>
+size_t bytes_of(const std::vector<T>& v) { return sizeof(T) * std::max<size_t>(v.size(), 1); }
+
+// Pinned staging layout of one upload: put() reserves 16-byte aligned ranges.
+struct Upload {
     size_t off = 0;
-    auto take = [&](size_t bytes) {
+    size_t take(size_t bytes) {
         const size_t o = off;
-        off = (off + bytes + 15) & ~(size_t)15;
+        off = (off + std::max<size_t>(bytes, 1) + 15) & ~(size_t)15;
         return o;
-    };
-    auto bytes_of = [](const auto& v) { return sizeof(v[0]) * std::max<size_t>(v.size(), 1); };
-    const size_t o_desc = take(sizeof(QDesc) * n), o_anch = take(bytes_of(anchors)), o_types = take(bytes_of(nb.types)),
-                 o_pos = take(bytes_of(nb.pos)), o_poff = take(bytes_of(nb.p_off)),
-                 o_pat = take(bytes_of(nb.pattern)), o_nop = take(bytes_of(nb.nop)), o_coff = take(bytes_of(cand_off));
-    const size_t up_bytes = off;
-    char* h = (char*)g->pinned_buf(up_bytes);
+    }
+};
+
+// Front end for host-normalised batches (legacy / ext entry points).
+void front_host(hgx_graph* g, int32_t n, const NormBatch& nb, Scratch& sc, Events& ev, Front& f) {
+    hipStream_t s = g->stream;
+    Upload u;
+    const size_t o_desc = u.take(sizeof(QDesc) * n), o_anch = u.take(bytes_of(nb.anchors)),
+                 o_types = u.take(bytes_of(nb.types)), o_pos = u.take(bytes_of(nb.pos)),
+                 o_poff = u.take(bytes_of(nb.p_off)), o_pat = u.take(bytes_of(nb.pattern)),
+                 o_nop = u.take(bytes_of(nb.nop));
+    char* h = (char*)g->pinned_buf(u.off);
     auto put = [&](size_t o, const auto& v) {
         if (!v.empty()) std::memcpy(h + o, v.data(), sizeof(v[0]) * v.size());
     };
     put(o_desc, nb.desc);
-    put(o_anch, anchors);
+    put(o_anch, nb.anchors);
     put(o_types, nb.types);
     put(o_pos, nb.pos);
     put(o_poff, nb.p_off);
     put(o_pat, nb.pattern);
     put(o_nop, nb.nop);
-    put(o_coff, cand_off);
-    const double t_pack = now_ms();
+    char* d = (char*)sc.take(u.off);
+    f.plan = (QPlan*)sc.take(sizeof(QPlan) * n);
+    f.nch = (int32_t*)sc.take(sizeof(int32_t) * (n + 1));
+    f.ncand = (int64_t*)sc.take(sizeof(int64_t) * (n + 1));
+    ev.rec(0, s);
+    HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
+    f.desc = (const QDesc*)(d + o_desc);
+    f.anch = (const int32_t*)(d + o_anch);
+    f.types = (const int32_t*)(d + o_types);
+    f.pos = (const int32_t*)(d + o_pos);
+    f.poff = (const int64_t*)(d + o_poff);
+    f.pat = (const int32_t*)(d + o_pat);
+    hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop),
+                                                         g->inc_off, g->inc_ts_type, f.plan, f.nch, f.ncand);
+    HGX_CHECK_LAUNCH();
+    f.cond_bytes = 20.0 * nb.anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
+                   4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
+}
 
-    std::vector<std::pair<void*, size_t>> tmp;
-    auto dalloc = [&](size_t bytes) {
-        void* p = g->alloc(bytes);
-        tmp.push_back({p, bytes});
-        return p;
-    };
-    struct TmpGuard {
-        hgx_graph* g;
-        std::vector<std::pair<void*, size_t>>* t;
-        ~TmpGuard() { for (auto& x : *t) g->release(x.first, x.second); }
-    } tg{g, &tmp};
-    char* d = (char*)dalloc(up_bytes);
-    QPlan* d_plan = (QPlan*)dalloc(sizeof(QPlan) * n);
-    int32_t* d_nch = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
-    int32_t* d_choff = (int32_t*)dalloc(sizeof(int32_t) * (n + 1));
-    int32_t* d_chq = (int32_t*)dalloc(sizeof(int32_t) * nc);
-    int32_t* d_slots = (int32_t*)dalloc(sizeof(int32_t) * (size_t)std::max<int64_t>(total_ub, 1));
-    int64_t* d_cnt = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
-    int64_t* d_outoff = (int64_t*)dalloc(sizeof(int64_t) * (nc + 1));
-    int64_t* d_qoff = (int64_t*)dalloc(sizeof(int64_t) * (n + 1));
-    u64* d_ctr = (u64*)dalloc(sizeof(u64) * kQShards * kQStride);
-    int32_t* d_out = (int32_t*)dalloc(sizeof(int32_t) * (size_t)std::max<int64_t>(total_ub, 1));
-    size_t scan1 = 0, scan2 = 0;
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan1, d_nch, d_choff, n + 1, s));
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan2, d_cnt, d_outoff, nc + 1, s));
-    void* d_scan = dalloc(std::max(scan1, scan2));
-    size_t scan_bytes = std::max(scan1, scan2);
+// Front end for the packed batch: the raw arrays go up in one copy and are normalised + planned on
+// the device (hgx_q_norm_packed); the host only checks the offsets it needs to size the upload.
+void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                  const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, Scratch& sc, Events& ev,
+                  Front& f) {
+    hipStream_t s = g->stream;
+    const int64_t n_inc = inc_off[n] - inc_off[0], n_pat = pat_off[n] - pat_off[0];
+    if (inc_off[0] != 0 || pat_off[0] != 0 || n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
+        fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad offsets");
+    Upload u;
+    const size_t o_type = u.take(4 * (size_t)n), o_ioff = u.take(8 * (size_t)(n + 1)), o_inc = u.take(4 * (size_t)n_inc),
+                 o_ho = u.take(4 * (size_t)n), o_poff = u.take(8 * (size_t)(n + 1)), o_pat = u.take(4 * (size_t)n_pat),
+                 o_err = u.take(8);
+    char* h = (char*)g->pinned_buf(u.off);
+    const int32_t none[2] = {INT32_MAX, INT32_MAX};   // smallest bad query index, none yet
+    std::memcpy(h + o_err, none, 8);
+    std::memcpy(h + o_type, type, 4 * (size_t)n);
+    std::memcpy(h + o_ioff, inc_off, 8 * (size_t)(n + 1));
+    if (n_inc) std::memcpy(h + o_inc, inc, 4 * (size_t)n_inc);
+    std::memcpy(h + o_ho, has_ordered, 4 * (size_t)n);
+    std::memcpy(h + o_poff, pat_off, 8 * (size_t)(n + 1));
+    if (n_pat) std::memcpy(h + o_pat, pat, 4 * (size_t)n_pat);
+    char* d = (char*)sc.take(u.off);
+    QDesc* desc = (QDesc*)sc.take(sizeof(QDesc) * n);
+    int32_t* anch = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(n_inc + n_pat, 1));
+    int32_t* nop = (int32_t*)sc.take(4 * (size_t)n);
+    f.plan = (QPlan*)sc.take(sizeof(QPlan) * n);
+    f.nch = (int32_t*)sc.take(sizeof(int32_t) * (n + 1));
+    f.ncand = (int64_t*)sc.take(sizeof(int64_t) * (n + 1));
+    f.err = (int32_t*)(d + o_err);
+    ev.rec(0, s);
+    HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
+    hgx_q_norm_packed<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(
+        n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
+        (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
+        g->inc_ts_type, desc, anch, nop, f.plan, f.nch, f.ncand, f.err);
+    HGX_CHECK_LAUNCH();
+    f.desc = desc;
+    f.anch = anch;
+    f.types = (const int32_t*)(d + o_type);
+    f.pos = nullptr;
+    f.poff = (const int64_t*)(d + o_poff);
+    f.pat = (const int32_t*)(d + o_pat);
+    f.cond_bytes = 20.0 * (double)(n_inc + n_pat) + 4.0 * n + 4.0 * (double)n_pat + (double)sizeof(QDesc) * n;
+}
 
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    struct EvGuard {
-        hipEvent_t* e;
-        ~EvGuard() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
-    } evg{ev};
-    if (g->timing)
-        for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&ev[i]));
-    if (g->timing) HGX_HIP(hipEventRecord(ev[0], s));
-    HGX_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemsetAsync(d_ctr, 0, sizeof(u64) * kQShards * kQStride, s));
-    HGX_HIP(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * (nc + 1), s));
-    HGX_HIP(hipMemsetAsync(d_nch + n, 0, sizeof(int32_t), s));
-    const QDesc* d_desc = (const QDesc*)(d + o_desc);
-    const int32_t* d_anch = (const int32_t*)(d + o_anch);
-    const int32_t* d_types = (const int32_t*)(d + o_types);
-    const int64_t* d_coff = (const int64_t*)(d + o_coff);
-    // plan, chunk offsets and the chunk -> query map on the device: no host round trip before the match
-    hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_desc, d_anch, d_types, (const int32_t*)(d + o_nop),
-                                                         g->inc_off, g->inc_ts_type, d_plan, d_nch);
-    HGX_CHECK_LAUNCH();
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_nch, d_choff, n + 1, s));
-    hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_chq);
-    HGX_CHECK_LAUNCH();
-    const int32_t* d_nchunks = d_choff + n;
-    if (g->timing) HGX_HIP(hipEventRecord(ev[1], s));
-    hgx_pattern_match<<<grid_for((int64_t)nc * 64, 256, 4096), 256, 0, s>>>(
-        d_nchunks, d_chq, d_choff, d_coff, d_plan, d_desc, d_anch, d_types, (const int32_t*)(d + o_pos),
-        (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_row, g->inc_type, g->inc_ts_row, g->tgt_off,
-        g->tgt_idx, d_slots, d_cnt, d_ctr);
-    HGX_CHECK_LAUNCH();
-    if (g->timing) HGX_HIP(hipEventRecord(ev[2], s));
-    // per-chunk hit counts -> exclusive output offsets -> per-query offsets; compaction into d_out
-    HGX_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_outoff, nc + 1, s));
-    hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, d_choff, d_outoff, d_qoff);
-    HGX_CHECK_LAUNCH();
-    hgx_q_scatter<<<(unsigned)ceil_div((int64_t)nc * 64, 256), 256, 0, s>>>(d_nchunks, d_chq, d_choff, d_coff, d_cnt,
-                                                                            d_outoff, d_slots, g->link_atom, d_out);
-    HGX_CHECK_LAUNCH();
-    u64 hsh[kQShards * kQStride], hctr[qNum] = {0, 0, 0, 0};
-    int32_t n_chunks = 0;
-    HGX_HIP(hipMemcpyAsync(r->offsets.data(), d_qoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
-    HGX_HIP(hipMemcpyAsync(hsh, d_ctr, sizeof(hsh), hipMemcpyDeviceToHost, s));
-    HGX_HIP(hipMemcpyAsync(&n_chunks, d_nchunks, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HGX_HIP(hipStreamSynchronize(s));
-    const double t_sync1 = now_ms();
-    const int64_t total = r->offsets[n];
-    r->ids.resize((size_t)std::max<int64_t>(total, 0));
-    if (total > 0) HGX_HIP(hipMemcpyAsync(r->ids.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, s));
-    if (g->timing) HGX_HIP(hipEventRecord(ev[3], s));
-    HGX_HIP(hipStreamSynchronize(s));
-    if (prof)
-        std::fprintf(stderr, "[hgx query] n=%d plan %.3f pack %.3f device+sync %.3f ids %.3f ms\n", n, t_plan - t0,
-                     t_pack - t_plan, t_sync1 - t_pack, now_ms() - t_sync1);
-    for (int k = 0; k < qNum; ++k)
-        for (int sh = 0; sh < kQShards; ++sh) hctr[k] += hsh[sh * kQStride + k];
-    if (g->timing) {
-        float a = 0, b = 0;
-        HGX_HIP(hipEventElapsedTime(&a, ev[0], ev[3]));
-        HGX_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
-        r->ms_total = a;
-        r->ms_match = b;
+// Back end shared by every entry point: chunk tables, match, compaction into one result area that
+// goes back in one copy, one synchronisation.  The candidate / chunk workspace has a capacity kept on the graph;
+// a batch that exceeds it is detected on the device (nothing is matched), the capacity grows to the
+// reported totals and the back end runs again.
+void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
+              double t0) {
+    hipStream_t s = g->stream;
+    const bool small = n <= kSmallBatch;
+    if (g->q_cap_chunks < (int64_t)n + 64) g->q_cap_chunks = (int64_t)n + 64;
+    if (g->q_cap_cand < 16 * (int64_t)n + 4096) g->q_cap_cand = 16 * (int64_t)n + 4096;
+    for (int attempt = 0;; ++attempt) {
+        const int64_t capC = g->q_cap_chunks, capK = g->q_cap_cand;
+        if (capC > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
+        Scratch w{g, {}};
+        int32_t* choff = (int32_t*)w.take(sizeof(int32_t) * (n + 1));
+        int64_t* coff = (int64_t*)w.take(sizeof(int64_t) * (n + 1));
+        int32_t* chq = (int32_t*)w.take(sizeof(int32_t) * capC);
+        int32_t* slots = (int32_t*)w.take(sizeof(int32_t) * capK);
+        int64_t* cnt = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        int64_t* outoff = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        u64* ctr = (u64*)w.take(sizeof(u64) * kQShards * kQStride);
+        // result area (device, copied back in one piece): stat[8] | ctr[4] | q_off[n+1] | ids[capK]
+        // stat: [0] chunks [1] candidates [2] overflow [3] hits [4] invalid query [5] unsupported query
+        const size_t m_stat = 0, m_ctr = 64, m_qoff = 128;
+        const size_t m_ids = m_qoff + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
+        char* rd = (char*)w.take(m_ids + 4 * (size_t)capK);
+        int64_t* stat_d = (int64_t*)(rd + m_stat);
+        u64* ctr_d = (u64*)(rd + m_ctr);
+        int64_t* qoff_d = (int64_t*)(rd + m_qoff);
+        int32_t* ids_d = (int32_t*)(rd + m_ids);
+        if (!small) HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
+        // cnt needs no clearing: the match writes the count of every chunk below the chunk total
+        if (small) {
+            hgx_q_scan_small<<<1, kScanBlock, 0, s>>>(n, f.nch, f.ncand, choff, coff, chq, capC, capK, stat_d, ctr);
+            HGX_CHECK_LAUNCH();
+        } else {
+            HGX_HIP(hipMemsetAsync(f.nch + n, 0, sizeof(int32_t), s));
+            HGX_HIP(hipMemsetAsync(f.ncand + n, 0, sizeof(int64_t), s));
+            size_t b1 = 0, b2 = 0;
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, f.nch, choff, n + 1, s));
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, f.ncand, coff, n + 1, s));
+            size_t tb = std::max(b1, b2);
+            void* tmp = w.take(tb);
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, f.nch, choff, n + 1, s));
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, f.ncand, coff, n + 1, s));
+            hgx_q_check<<<1, 1, 0, s>>>(n, choff, coff, capC, capK, stat_d);
+            HGX_CHECK_LAUNCH();
+            hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, choff, stat_d, chq);
+            HGX_CHECK_LAUNCH();
+        }
+        const int32_t* d_nchunks = choff + n;   // 0 after an overflow
+        ev.rec(1, s);
+        hgx_pattern_match<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+            d_nchunks, chq, choff, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row,
+            g->inc_type, g->inc_ts_row, g->tgt_off, g->tgt_idx, slots, cnt, ctr);
+        HGX_CHECK_LAUNCH();
+        ev.rec(2, s);
+        if (small) {
+            hgx_q_finish_small<<<1, kScanBlock, 0, s>>>(n, choff, chq, coff, cnt, slots, g->link_atom, ctr, outoff,
+                                                        qoff_d, ids_d, stat_d, ctr_d, f.err);
+            HGX_CHECK_LAUNCH();
+            hgx_q_scatter<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(d_nchunks, chq, choff, coff, cnt, outoff,
+                                                                            slots, g->link_atom, ids_d);
+            HGX_CHECK_LAUNCH();
+        } else {
+            size_t tb = 0;
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, outoff, capC + 1, s));
+            void* tmp = w.take(tb);
+            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, outoff, capC + 1, s));
+            hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, choff, outoff, stat_d, qoff_d);
+            HGX_CHECK_LAUNCH();
+            hgx_q_scatter<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(d_nchunks, chq, choff, coff, cnt, outoff,
+                                                                            slots, g->link_atom, ids_d);
+            HGX_CHECK_LAUNCH();
+            hgx_q_finish_stat<<<1, 64, 0, s>>>(n, choff, outoff, ctr, stat_d, ctr_d, f.err);
+            HGX_CHECK_LAUNCH();
+        }
+        // one copy back: the head and as many ids as the last batches needed (a second copy if more)
+        const int64_t guess = std::min<int64_t>(capK, std::max<int64_t>(g->q_hits_guess, 1024));
+        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
+        HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
+        ev.rec(3, s);
+        HGX_HIP(hipStreamSynchronize(s));
+        const int64_t* stat = (const int64_t*)(hm + m_stat);
+        const u64* ctr_h = (const u64*)(hm + m_ctr);
+        const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
+        const int32_t* ids_h = (const int32_t*)(hm + m_ids);
+        if (stat[4] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(stat[4]));
+        if (stat[5] < n)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(stat[5]) +
+                                        " is not accelerated (no incidence anchor or condition limits)");
+        if (stat[2]) {   // workspace too small: grow to the reported totals and match again
+            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: workspace sizing failed");
+            g->q_cap_chunks = std::max<int64_t>(capC, stat[0] + stat[0] / 4 + 64);
+            g->q_cap_cand = std::max<int64_t>(capK, stat[1] + stat[1] / 4 + 4096);
+            continue;
+        }
+        const int64_t total = stat[3];
+        if (total > guess) {
+            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, ids_d + guess, 4 * (size_t)(total - guess),
+                                   hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+        }
+        g->q_hits_guess = total + total / 4;
+        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
+        r->ids.assign(ids_h, ids_h + total);
+        if (prof)
+            std::fprintf(stderr, "[hgx query] n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n", n,
+                         now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
+        if (ev.on) {
+            float a = 0, b = 0;
+            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
+            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
+            r->ms_total = a;
+            r->ms_match = b;
+        }
+        // algorithmic bytes of hgx_pattern_match: per streamed candidate its type (4 B; none in a
+        // type-grouped range), per examined candidate its link row, tgt_off pair and target row,
+        // 4 B per hit, per chunk its plan / descriptor, plus the conditions
+        r->bytes_match = 4.0 * (double)ctr_h[qCand] + 20.0 * (double)ctr_h[qTyped] + 4.0 * (double)ctr_h[qArity] +
+                         4.0 * (double)ctr_h[qHits] + (8.0 + sizeof(QPlan) + sizeof(QDesc)) * (double)stat[0] +
+                         f.cond_bytes;
+        return;
     }
-    // algorithmic bytes of hgx_pattern_match: per streamed candidate its type (4 B; none in a
-    // type-grouped range), per examined candidate its link row, tgt_off pair and target row, 4 B per
-    // hit, per chunk its plan / descriptor, plus the conditions
-    {
-        double cond_bytes = 20.0 * anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
-                            4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
-        r->bytes_match = 4.0 * (double)hctr[qCand] + 20.0 * (double)hctr[qTyped] + 4.0 * (double)hctr[qArity] +
-                         4.0 * (double)hctr[qHits] + (8.0 + sizeof(QPlan) + sizeof(QDesc)) * (double)n_chunks +
-                         cond_bytes;
+}
+
+template <class FrontFn>
+int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front) {
+    HGX_API_BEGIN
+    const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
+    const double t0 = now_ms();
+    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
+    std::unique_ptr<hgx_query_result> r(new hgx_query_result());
+    r->n = n;
+    r->offsets.assign(n + 1, 0);
+    if (n > 0) {
+        std::lock_guard<std::mutex> lk(g->mu);
+        HGX_HIP(hipSetDevice(g->device));
+        ensure_type_grouped(g);
+        Scratch sc{g, {}};
+        Events ev;
+        ev.init(g->timing);
+        Front f;
+        front(sc, ev, f);
+        back_end(g, n, f, sc, ev, r.get(), prof, t0);
     }
-    guard.r = nullptr;
-    *out = r;
+    *out = r.release();
     HGX_API_END
+}
+
+int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
+    return run_batch_with(g, n, out, [&](Scratch& sc, Events& ev, Front& f) { front_host(g, n, nb, sc, ev, f); });
+}
+
+int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                     const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result** out) {
+    return run_batch_with(g, n, out, [&](Scratch& sc, Events& ev, Front& f) {
+        front_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, sc, ev, f);
+    });
 }
 
 }  // namespace

@@ -220,3 +220,73 @@ def test_type_plus_from_subsumption():
         both = find_all(snap, hg.and_(hg.typePlus(tp), hg.type(3), hg.incident(a)))
         assert both == orc.and_query_ext([3], [a]).tolist()
         assert find_all(snap, hg.and_(hg.typePlus(tp), hg.type(2), hg.incident(a))) == []
+
+
+def _packed(qs):
+    """(type, [incident], pattern|None) list -> hgx_pattern_batch_packed arrays."""
+    t = np.array([q[0] for q in qs], np.int32)
+    inc_off = np.zeros(len(qs) + 1, np.int64)
+    pat_off = np.zeros(len(qs) + 1, np.int64)
+    inc, pat, ho = [], [], np.zeros(len(qs), np.int32)
+    for i, (_, a, p) in enumerate(qs):
+        inc += list(a)
+        inc_off[i + 1] = len(inc)
+        if p is not None:
+            ho[i] = 1
+            pat += list(p)
+        pat_off[i + 1] = len(pat)
+    return t, inc_off, np.array(inc, np.int32), ho, pat_off, np.array(pat, np.int32)
+
+
+def test_packed_large_batch_vs_oracle():
+    """A packed batch above the single-workgroup scan size (device scans + chunk map path),
+    normalised on the device, against the oracle."""
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    g = synth.config3(scale=0.01, n_queries=20000)
+    snap, orc = snapshot(g), oracle(g)
+    Q = g["queries"]
+    rng = np.random.default_rng(31)
+    qs = []
+    for i in range(20000):
+        if i % 4 == 3:   # untyped, two anchors, no pattern; or a repeated anchor (toDNF dedupe)
+            a = int(Q["a"][i])
+            qs.append((-1, [a, int(Q["x"][i]), a], None))
+        else:
+            qs.append((int(Q["type"][i]), [int(Q["a"][i])], (int(Q["x"][i]), -1, int(Q["y"][i]))))
+    r = pattern_batch_arrays(snap, *_packed(qs))
+    for q in rng.choice(len(qs), 3000, replace=False):
+        t, inc, pat = qs[q]
+        assert r[q].tolist() == orc.and_query(t, inc, pat).tolist(), qs[q]
+
+
+def test_packed_workspace_growth():
+    """Queries whose candidate ranges exceed the initial workspace are re-run with a grown one; the
+    next batch reuses it.  Anchored on the highest-degree atoms, untyped."""
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    g = synth.config3(scale=0.01, n_queries=10)
+    snap, orc = snapshot(g), oracle(g)
+    deg = np.diff(np.searchsorted(np.sort(g["tgt_idx"]), np.arange(g["num_atoms"] + 1)))
+    hubs = np.argsort(-deg)[:3]
+    assert deg[hubs[0]] > 16 * 3 + 4096
+    for rep in range(2):
+        qs = [(-1, [int(h)], None) for h in hubs]
+        r = pattern_batch_arrays(snap, *_packed(qs))
+        for q, (t, inc, pat) in enumerate(qs):
+            assert r[q].tolist() == orc.and_query(t, inc, pat).tolist()
+
+
+def test_packed_errors():
+    from hypergraphdb_amd import HGXError, HGXUnsupported, _lib
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    g = K.queries_graph()
+    snap = snapshot(g)
+    n0 = g["names"]["n0"]
+    with pytest.raises(HGXError) as e:          # atom id out of range
+        pattern_batch_arrays(snap, *_packed([(-1, [n0], None), (-1, [g["num_atoms"] + 5], None)]))
+    assert e.value.code == _lib.HGX_E_INVALID and "query 1" in str(e.value)
+    with pytest.raises(HGXUnsupported):         # no incidence anchor
+        pattern_batch_arrays(snap, *_packed([(-1, [n0], None), (K.T_TESTLINK, [], (-1, -1))]))
+    r = pattern_batch_arrays(snap, *_packed([(-1, [n0], ()), (-1, [n0], None)]))   # empty orderedLink: NOP
+    assert r[0].tolist() == [] and len(r[1]) > 0
