@@ -1018,11 +1018,28 @@ __device__ __forceinline__ bool yields(int pos, int fv, int lv) {
 
 // Per-wave LDS scratch of the frontier push: the yielded targets of one position step and the
 // nonzero words of the pushing atom's row.
+constexpr int kCBuf = 256;   // candidates staged per wave before one list append
+
 struct OPushLds {
     int32_t tgt[64];
     int32_t widx[16];
     u64 wval[16];
+    int32_t cbuf[kCBuf];     // fresh candidates not yet appended to the candidate list
 };
+
+// Append the wave's staged candidates with one atomic (a same-address atomic per ballot serialises
+// on the counter when thousands of waves find candidates).  Wave-uniform call, every lane active.
+__device__ __forceinline__ void cand_flush(OPushLds& sh, int& cc, int32_t* __restrict__ clist,
+                                           u64* __restrict__ n_clist) {
+    const int lane = threadIdx.x & 63;
+    if (cc == 0) return;
+    u64 base = 0;
+    if (lane == 0) base = atomicAdd(n_clist, (u64)cc);
+    base = __shfl(base, 0);
+    for (int i = lane; i < cc; i += 64) clist[base + i] = sh.cbuf[i];
+    __builtin_amdgcn_wave_barrier();
+    cc = 0;
+}
 
 // Links [start, hi) of frontier atom v (wave-uniform), lane l taking start + l, start + l + step, ...
 // Each lane reads its link's target row; position by position the wave ballots the yielded
@@ -1038,7 +1055,7 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
                                             int nnz, OPushLds& sh, const u64* __restrict__ full,
                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
                                             u64* __restrict__ n_clist, u64* __restrict__ acc, u64& n_links,
-                                            u64& n_pins, u64& n_pairs) {
+                                            u64& n_pins, u64& n_pairs, int& cc) {
     const int lane = threadIdx.x & 63;
     const u64 lt = (1ull << lane) - 1ull;
     for (int64_t i0 = start; i0 < hi; i0 += step) {   // i0 is wave-uniform
@@ -1085,12 +1102,12 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
                     }
                 }
                 const u64 fm = __ballot(fresh);
-                if (fm) {
-                    const int leader = __ffsll((long long)fm) - 1;
-                    u64 base = 0;
-                    if (lane == leader) base = atomicAdd(n_clist, (u64)__popcll(fm));
-                    base = __shfl(base, leader);
-                    if (fresh) clist[base + __popcll(fm & lt)] = ts;
+                if (fm) {   // wave-uniform: stage the fresh candidates in LDS
+                    const int nf = __popcll(fm);
+                    if (cc + nf > kCBuf) cand_flush(sh, cc, clist, n_clist);
+                    if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = ts;
+                    cc += nf;
+                    __builtin_amdgcn_wave_barrier();
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -1114,25 +1131,69 @@ __device__ __forceinline__ int row_words(const u64* __restrict__ lvl, int64_t v,
 }
 
 // Light frontier atoms (0 < deg <= kHeavyDegree) appended to a list (order-free), so the push
-// kernels give one wave per atom whatever the bitmap's sparsity.
+// kernels give one wave per atom whatever the bitmap's sparsity.  A thread owns one frontier word;
+// a block counts its words' atoms, claims its list range with one atomic, then writes them (a
+// per-wave atomic on the list counter serialised: 76 us per level on config 5's sparse frontiers).
 __global__ void __launch_bounds__(256) hgx_frontier_list(int64_t A, const u64* __restrict__ fa,
                                                          const int64_t* __restrict__ inc_off,
                                                          int32_t* __restrict__ list, u64* __restrict__ n_list) {
-    const int lane = threadIdx.x & 63;
-    for_nonzero_words(fa, (A + 63) / 64, [&](int64_t w, u64 x) {
-        const int64_t v = w * 64 + lane;
-        bool take = (x >> lane) & 1ull;
-        if (take) {
+    __shared__ int wsum[4];
+    __shared__ u64 sbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nw = (A + 63) / 64;
+    // the light atoms of word w
+    auto keep_of = [&](int64_t w) -> u64 {
+        if (w >= nw) return 0ull;
+        u64 x = fa[w], keep = 0ull;
+        for (u64 y = x; y; y &= y - 1ull) {
+            const int b = __ffsll((long long)y) - 1;
+            const int64_t v = w * 64 + b;
             const int64_t d = inc_off[v + 1] - inc_off[v];
-            take = d > 0 && d <= kHeavyDegree;
+            if (d > 0 && d <= kHeavyDegree) keep |= 1ull << b;
         }
-        const u64 m = __ballot(take);
-        if (m == 0ull) return;
-        u64 base = 0;
-        if (lane == 0) base = atomicAdd(n_list, (u64)__popcll(m));
-        base = __shfl(base, 0);
-        if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)v;
-    });
+        return keep;
+    };
+    auto block_scan = [&](int c, int& before, int& total) {
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        before = 0;
+        total = 0;
+        for (int k = 0; k < 4; ++k) {
+            before += k < wv ? wsum[k] : 0;
+            total += wsum[k];
+        }
+        __syncthreads();
+        before += incl - c;
+    };
+    // pass 1: the block's total over all its chunks -> one atomic
+    int mine = 0;
+    for (int64_t w0 = (int64_t)blockIdx.x * 256; w0 < nw; w0 += (int64_t)gridDim.x * 256)
+        mine += __popcll(keep_of(w0 + threadIdx.x));
+    int before, total;
+    block_scan(mine, before, total);
+    if (threadIdx.x == 0) sbase = total ? atomicAdd(n_list, (u64)total) : 0ull;
+    __syncthreads();
+    if (total == 0) return;   // block-uniform
+    // pass 2: positions in chunk order
+    u64 run = sbase;
+    for (int64_t w0 = (int64_t)blockIdx.x * 256; w0 < nw; w0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        const int64_t w = w0 + threadIdx.x;
+        u64 keep = keep_of(w);
+        int b4, t4;
+        block_scan(__popcll(keep), b4, t4);
+        u64 pos = run + (u64)b4;
+        while (keep) {
+            const int b = __ffsll((long long)keep) - 1;
+            list[pos++] = (int32_t)(w * 64 + b);
+            keep &= keep - 1ull;
+        }
+        run += (u64)t4;
+    }
 }
 
 template <int W, int MODE>
@@ -1151,13 +1212,15 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t n = (int64_t)*n_list;
     u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    int cc = 0;   // staged candidates (wave-uniform)
     for (int64_t k = wave; k < n; k += nwave) {
         const int32_t v = list[k];
         const int nnz = row_words<W>(lvl, v, sh);
         if (nnz == 0) continue;
         opush_links<W, MODE>(v, inc_off[v], inc_off[v + 1], 64, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
-                             sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs);
+                             sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, cc);
     }
+    cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
     wave_add_sh(ctr + cIncLight, n_pairs);
@@ -1182,8 +1245,10 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
     const int nnz = row_words<W>(lvl, c.atom, sh);
     if (nnz == 0) return;   // the same row for every wave of the block
     u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    int cc = 0;
     opush_links<W, MODE>(c.atom, c.beg + wib * 64, c.end, 256, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
-                         sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs);
+                         sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, cc);
+    cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
     wave_add_sh(ctr + cIncLight, n_pairs);
@@ -2003,7 +2068,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slots
             u64* n_clist = n_list + 1;
             HGX_HIP(hipMemsetAsync(n_list, 0, 2 * sizeof(u64), s));
-            const int fgrid = grid_for(ceil_div(A, 64) * 64, 256, 4096);
+            const int fgrid = grid_for(ceil_div(A, 64), 256, 256);   // <= 256 list atomics per level
             hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, flist, n_list);
             HGX_CHECK_LAUNCH();
             const int lgrid = 2048;   // 8192 waves, grid-stride over the frontier list
