@@ -175,7 +175,8 @@ enum Ctr {
     cCand,              // frontier-push candidates finalised
     cNewDegNF,          // sum of |inc(v)| over the new atoms not yet visited by every traversal
     cNfRows,            // frontier rows read by the non-full pull
-    cNum = 15
+    cScanned,           // incidence entries scanned by the frontier push (type + yield flag)
+    cNum = 16
 };
 
 __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
@@ -1016,15 +1017,57 @@ __device__ __forceinline__ bool yields(int pos, int fv, int lv) {
     else return pos > lv;   // kAfterLast
 }
 
+// Yield flags of incidence entry i = (v, L), bit MODE set <=> DefaultALGenerator in ordered mode
+// MODE can yield a target of L from v (a target other than v after / before v's first / last
+// position).  A frontier atom's push reads the target row of L only when the bit is
+// set: a hub's links where it sits at the far end (e.g. the parent end of its HGSubsumes links in
+// hg.subsumes) cost one byte each instead of two dependent row loads.  One wave per atom.
+__global__ void __launch_bounds__(256) hgx_inc_yield(int64_t A, const int64_t* __restrict__ inc_off,
+                                                     const int32_t* __restrict__ inc_row,
+                                                     const int64_t* __restrict__ tgt_off,
+                                                     const int32_t* __restrict__ tgt_idx, uint8_t* __restrict__ yf) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t v = wave; v < A; v += nwave) {
+        const int64_t e = inc_off[v + 1];
+        for (int64_t i = inc_off[v] + lane; i < e; i += 64) {
+            const int32_t L = inc_row[i];
+            const int64_t b = tgt_off[L];
+            const int n = (int)(tgt_off[L + 1] - b);
+            int fv = -1, lv = -1;
+            for (int p = 0; p < n; ++p)
+                if (tgt_idx[b + p] == v) {
+                    if (fv < 0) fv = p;
+                    lv = p;
+                }
+            bool after_first = false, before_last = false;
+            for (int p = 0; p < n; ++p) {
+                const bool other = tgt_idx[b + p] != v;
+                after_first |= other && p > fv;
+                before_last |= other && p < lv;
+            }
+            unsigned f = 0;
+            if (after_first) f |= 1u << kAfterFirst;
+            if (fv > 0) f |= 1u << kBeforeFirst;
+            if (before_last) f |= 1u << kBeforeLast;
+            if (lv >= 0 && lv < n - 1) f |= 1u << kAfterLast;
+            yf[i] = (uint8_t)f;
+        }
+    }
+}
+
 // Per-wave LDS scratch of the frontier push: the yielded targets of one position step and the
 // nonzero words of the pushing atom's row.
 constexpr int kCBuf = 256;   // candidates staged per wave before one list append
+constexpr int kEBuf = 256;   // filtered incidence entries staged per wave
 
 struct OPushLds {
     int32_t tgt[64];
     int32_t widx[16];
     u64 wval[16];
     int32_t cbuf[kCBuf];     // fresh candidates not yet appended to the candidate list
+    int32_t ent[kEBuf];      // incidence entries (relative to the range start) that pass type + yield
 };
 
 // Append the wave's staged candidates with one atomic (a same-address atomic per ballot serialises
@@ -1048,9 +1091,7 @@ __device__ __forceinline__ void cand_flush(OPushLds& sh, int& cc, int32_t* __res
 // already there (hub targets are hit by many pairs).  The first pair to reach a target sets its
 // candidate bit and appends it to the candidate list of the finalise.
 template <int W, int MODE>
-__device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi, int64_t step,
-                                            const int32_t* __restrict__ inc_row,
-                                            const int32_t* __restrict__ inc_type, int32_t want_type,
+__device__ __forceinline__ void opush_entry(int32_t v, int64_t i, bool have, const int32_t* __restrict__ inc_row,
                                             const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
                                             int nnz, OPushLds& sh, const u64* __restrict__ full,
                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
@@ -1058,61 +1099,122 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
                                             u64& n_pins, u64& n_pairs, int& cc) {
     const int lane = threadIdx.x & 63;
     const u64 lt = (1ull << lane) - 1ull;
-    for (int64_t i0 = start; i0 < hi; i0 += step) {   // i0 is wave-uniform
-        const int64_t i = i0 + lane;
-        const bool have = i < hi && (want_type < 0 || inc_type[i] == want_type);
-        int64_t b = 0;
-        int n = 0, fv = -1, lv = -1;
-        if (have) {
-            const int32_t L = inc_row[i];
-            b = tgt_off[L];
-            n = (int)(tgt_off[L + 1] - b);
-            for (int p = 0; p < n; ++p)
-                if (tgt_idx[b + p] == v) {
-                    if (fv < 0) fv = p;
-                    lv = p;
-                }
-            ++n_links;
-            n_pins += (u64)n;
-        }
-        int nmax = n;
-        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
-        for (int p = 0; p < nmax; ++p) {
-            const int32_t t = p < n ? tgt_idx[b + p] : -1;
-            const bool elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
-            const u64 m = __ballot(elig);
-            if (m == 0ull) continue;
-            n_pairs += elig;
-            if (elig) sh.tgt[__popcll(m & lt)] = t;
-            __builtin_amdgcn_wave_barrier();
-            const int total = __popcll(m) * nnz;
-            for (int q0 = 0; q0 < total; q0 += 64) {   // wave-uniform trip count
-                const int q = q0 + lane;
-                bool fresh = false;
-                int32_t ts = 0;
-                if (q < total) {
-                    const int pr = q / nnz, wi = q - pr * nnz;
-                    ts = sh.tgt[pr];
-                    u64* a = acc + (int64_t)ts * W + sh.widx[wi];
-                    const u64 val = sh.wval[wi];
-                    if ((*a & val) != val) atomicOr(a, val);
-                    if (wi == 0) {
-                        const u64 cb = 1ull << (ts & 63);
-                        if (!(cand[ts >> 6] & cb)) fresh = !(atomicOr(&cand[ts >> 6], cb) & cb);
-                    }
-                }
-                const u64 fm = __ballot(fresh);
-                if (fm) {   // wave-uniform: stage the fresh candidates in LDS
-                    const int nf = __popcll(fm);
-                    if (cc + nf > kCBuf) cand_flush(sh, cc, clist, n_clist);
-                    if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = ts;
-                    cc += nf;
-                    __builtin_amdgcn_wave_barrier();
+    int64_t b = 0;
+    int n = 0, fv = -1, lv = -1;
+    if (have) {
+        const int32_t L = inc_row[i];
+        b = tgt_off[L];
+        n = (int)(tgt_off[L + 1] - b);
+        for (int p = 0; p < n; ++p)
+            if (tgt_idx[b + p] == v) {
+                if (fv < 0) fv = p;
+                lv = p;
+            }
+        ++n_links;
+        n_pins += (u64)n;
+    }
+    int nmax = n;
+    for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+    for (int p = 0; p < nmax; ++p) {
+        const int32_t t = p < n ? tgt_idx[b + p] : -1;
+        const bool elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
+        const u64 m = __ballot(elig);
+        if (m == 0ull) continue;
+        n_pairs += elig;
+        if (elig) sh.tgt[__popcll(m & lt)] = t;
+        __builtin_amdgcn_wave_barrier();
+        const int total = __popcll(m) * nnz;
+        for (int q0 = 0; q0 < total; q0 += 64) {   // wave-uniform trip count
+            const int q = q0 + lane;
+            bool fresh = false;
+            int32_t ts = 0;
+            if (q < total) {
+                const int pr = q / nnz, wi = q - pr * nnz;
+                ts = sh.tgt[pr];
+                u64* a = acc + (int64_t)ts * W + sh.widx[wi];
+                const u64 val = sh.wval[wi];
+                if ((*a & val) != val) atomicOr(a, val);
+                if (wi == 0) {
+                    const u64 cb = 1ull << (ts & 63);
+                    if (!(cand[ts >> 6] & cb)) fresh = !(atomicOr(&cand[ts >> 6], cb) & cb);
                 }
             }
+            const u64 fm = __ballot(fresh);
+            if (fm) {   // wave-uniform: stage the fresh candidates in LDS
+                const int nf = __popcll(fm);
+                if (cc + nf > kCBuf) cand_flush(sh, cc, clist, n_clist);
+                if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = ts;
+                cc += nf;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Entries [start, hi) of frontier atom v (wave-uniform), lane l taking start + l, start + l + step, ...
+// Stage 1 streams the type column and the yield flags kUnroll chunks at a time (independent loads)
+// and compacts the passing entries into an LDS list; stage 2 runs the dependent chain (link row,
+// target offsets, target row, full bits, accumulator atomics) only for those, 64 per pass.  A hub's
+// links that cannot yield (most of them in hg.subsumes) thus cost streamed bytes, not round trips.
+template <int W, int MODE>
+__device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi, int64_t step,
+                                            const int32_t* __restrict__ inc_row,
+                                            const int32_t* __restrict__ inc_type, int32_t want_type,
+                                            const uint8_t* __restrict__ yf,
+                                            const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+                                            int nnz, OPushLds& sh, const u64* __restrict__ full,
+                                            u64* __restrict__ cand, int32_t* __restrict__ clist,
+                                            u64* __restrict__ n_clist, u64* __restrict__ acc, u64& n_links,
+                                            u64& n_pins, u64& n_pairs, u64& n_scan, int& cc) {
+    constexpr int kUnroll = 4;
+    const int lane = threadIdx.x & 63;
+    const u64 lt = (1ull << lane) - 1ull;
+    int ne = 0;   // staged entries (wave-uniform)
+    auto drain = [&]() {
+        for (int k0 = 0; k0 < ne; k0 += 64) {   // wave-uniform
+            const bool have = k0 + lane < ne;
+            const int64_t i = have ? start + sh.ent[k0 + lane] : 0;
+            opush_entry<W, MODE>(v, i, have, inc_row, tgt_off, tgt_idx, nnz, sh, full, cand, clist, n_clist, acc,
+                                 n_links, n_pins, n_pairs, cc);
+        }
+        __builtin_amdgcn_wave_barrier();
+        ne = 0;
+    };
+    for (int64_t i0 = start; i0 < hi; i0 += step * kUnroll) {   // i0 is wave-uniform
+        bool pass[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = i0 + u * step + lane;
+            pass[u] = i < hi;
+        }
+        if (want_type >= 0) {
+            int32_t ty[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) ty[u] = pass[u] ? inc_type[i0 + u * step + lane] : want_type;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ty[u] == want_type;
+        }
+        if constexpr (MODE != kSym) {
+            uint8_t f[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) f[u] = pass[u] ? yf[i0 + u * step + lane] : (uint8_t)0;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ((f[u] >> MODE) & 1u);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = i0 + u * step + lane;
+            n_scan += i < hi;
+            const u64 m = __ballot(pass[u]);
+            if (m == 0ull) continue;   // wave-uniform
+            if (ne + 64 > kEBuf) drain();
+            if (pass[u]) sh.ent[ne + __popcll(m & lt)] = (int32_t)(i - start);
+            ne += __popcll(m);
             __builtin_amdgcn_wave_barrier();
         }
     }
+    if (ne) drain();
 }
 
 // The nonzero words of v's row into the wave's LDS table; returns their count (wave-uniform).
@@ -1201,6 +1303,7 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
                                                  const int64_t* __restrict__ inc_off,
                                                  const int32_t* __restrict__ inc_row,
                                                  const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                 const uint8_t* __restrict__ yf,
                                                  const int64_t* __restrict__ tgt_off,
                                                  const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
                                                  const u64* __restrict__ full, u64* __restrict__ cand,
@@ -1211,19 +1314,21 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t n = (int64_t)*n_list;
-    u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
     int cc = 0;   // staged candidates (wave-uniform)
     for (int64_t k = wave; k < n; k += nwave) {
         const int32_t v = list[k];
+        if (v < 0) continue;   // a candidate list reused as the frontier list: not new / not light
         const int nnz = row_words<W>(lvl, v, sh);
         if (nnz == 0) continue;
-        opush_links<W, MODE>(v, inc_off[v], inc_off[v + 1], 64, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
-                             sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, cc);
+        opush_links<W, MODE>(v, inc_off[v], inc_off[v + 1], 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
+                             nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
     }
     cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
     wave_add_sh(ctr + cIncLight, n_pairs);
+    wave_add_sh(ctr + cScanned, n_scan);
 }
 
 template <int W, int MODE>
@@ -1231,6 +1336,7 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
                                                        const u64* __restrict__ fa,
                                                        const int32_t* __restrict__ inc_row,
                                                        const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                       const uint8_t* __restrict__ yf,
                                                        const int64_t* __restrict__ tgt_off,
                                                        const int32_t* __restrict__ tgt_idx,
                                                        const u64* __restrict__ lvl, const u64* __restrict__ full,
@@ -1244,26 +1350,28 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
     OPushLds& sh = lds[wib];
     const int nnz = row_words<W>(lvl, c.atom, sh);
     if (nnz == 0) return;   // the same row for every wave of the block
-    u64 n_links = 0, n_pins = 0, n_pairs = 0;
+    u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
     int cc = 0;
-    opush_links<W, MODE>(c.atom, c.beg + wib * 64, c.end, 256, inc_row, inc_type, want_type, tgt_off, tgt_idx, nnz,
-                         sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, cc);
+    opush_links<W, MODE>(c.atom, c.beg + wib * 64, c.end, 256, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
+                         nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
     cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
     wave_add_sh(ctr + cIncLight, n_pairs);
+    wave_add_sh(ctr + cScanned, n_scan);
 }
 
 // Finalise the candidates of a push level: new = acc & ~vis, the accumulator row is re-zeroed.
 // One G-lane group per candidate; fa_next (cleared beforehand) / ever / full bits by atomics.
 template <int W>
-__global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __restrict__ clist,
+__global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restrict__ clist,
                                                               const u64* __restrict__ n_clist,
                                                               const int64_t* __restrict__ inc_off,
-                                                              u64* __restrict__ acc, u64* __restrict__ vis,
+                                                              u64* __restrict__ acc, u64* __restrict__ cand,
+                                                              u64* __restrict__ vis,
                                                               u64* __restrict__ ever, u64* __restrict__ full,
                                                               u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
-                                                              u64* __restrict__ ctr, FullMask fm) {
+                                                              u64* __restrict__ ctr, FullMask fm, int relist) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
     const int sub = threadIdx.x & (G - 1);
@@ -1278,11 +1386,13 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
         const int64_t t = valid ? clist[k] : 0;
         typename V::T a = valid ? V::ld(acc + t * W + sub * WPL) : V::zero();
         if (valid) V::st(acc + t * W + sub * WPL, V::zero());
+        if (valid && sub == 0) cand[t >> 6] = 0ull;   // every candidate of the word is in the list
         const bool ev = valid && bit(ever, t);
         const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
         const typename V::T nw = a & ~old;
         const bool isnew = group_any<G>(V::nz(nw));
         const bool becomes_full = group_all<G>(V::eq(old | nw, FULL));
+        int64_t dg = 0;
         if (valid && isnew) {
             V::st(lvl_next + t * W + sub * WPL, nw);
             V::st(vis + t * W + sub * WPL, old | nw);
@@ -1292,9 +1402,13 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(const int32_t* __r
                 if (becomes_full) set_bit(full, t);
                 ++n_new;
                 n_full += becomes_full;
-                { const u64 dg_ = (u64)(inc_off[t + 1] - inc_off[t]); n_newdeg += dg_; if (!becomes_full) n_newdeg_nf += dg_; }
+                dg = inc_off[t + 1] - inc_off[t];
+                n_newdeg += (u64)dg;
+                if (!becomes_full) n_newdeg_nf += (u64)dg;
             }
         }
+        // the next push level's frontier list in place: the new light atoms, -1 elsewhere
+        if (relist && valid && sub == 0) clist[k] = (dg > 0 && dg <= kHeavyDegree) ? (int32_t)t : -1;
         if (valid && sub == 0) {
             ++n_cand;
             n_vis += ev;
@@ -1996,6 +2110,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const size_t flist_bytes = sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1);
     int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
     int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
+    // push levels: fl = this level's frontier list, cl = its candidates; the finalise turns cl into the
+    // next level's frontier list (chained), so consecutive push levels swap the two
+    int32_t *fl = flist, *cl = clist;
+    u64* n_fl = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 10;   // scratch slots
+    u64* n_cl = n_fl + 1;
+    bool chained = false, cand_clean = false;
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
@@ -2027,6 +2147,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         // late dense level with few atoms left unfull: those pull from the frontier directly
         const bool nfp = !sparse && sparse_ok && MODE == kSym && Lay<W>::G >= 4 && !ex && (lflags & 256) &&
                          (lflags & 4) && 4 * (int64_t)(I_total - full_deg_total) < I_total;
+        if (!opush) {   // the lists are reused as scratch; the sparse gather leaves candidate bits set
+            chained = false;
+            if (sparse) cand_clean = false;
+        }
         if (nfp) {
             if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
                 Events e2 = tm.start(kKindNf, d);
@@ -2063,28 +2187,42 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }
             g->zacc_clean = false;   // until this level's finalise has run
             u64* acc = (u64*)g->zacc;
-            HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
+            if (MODE != kSym && !g->inc_yf) {   // once per snapshot
+                HGX_HIP(hipMalloc(&g->inc_yf, std::max<int64_t>(g->I, 1)));
+                hgx_inc_yield<<<grid_for(A * 64, 256, 8192), 256, 0, s>>>(A, g->inc_off, g->inc_row, g->tgt_off,
+                                                                       g->tgt_idx, g->inc_yf);
+                HGX_CHECK_LAUNCH();
+            }
+            const uint8_t* yf = g->inc_yf;
+            if (!cand_clean) HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
             HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
-            u64* n_list = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slots
-            u64* n_clist = n_list + 1;
-            HGX_HIP(hipMemsetAsync(n_list, 0, 2 * sizeof(u64), s));
-            const int fgrid = grid_for(ceil_div(A, 64), 256, 256);   // <= 256 list atomics per level
-            hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, flist, n_list);
-            HGX_CHECK_LAUNCH();
+            HGX_HIP(hipMemsetAsync(n_cl, 0, sizeof(u64), s));
+            if (!chained) {   // the frontier list from the bitmap (else the last finalise left it in fl)
+                HGX_HIP(hipMemsetAsync(n_fl, 0, sizeof(u64), s));
+                const int fgrid = grid_for(ceil_div(A, 64), 256, 256);   // <= 256 list atomics per level
+                hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, fl, n_fl);
+                HGX_CHECK_LAUNCH();
+            }
             const int lgrid = 2048;   // 8192 waves, grid-stride over the frontier list
-            hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(flist, n_list, g->inc_off, g->inc_row, g->inc_type, want_type,
-                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, clist, n_clist, acc, c);
+            hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
+                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c);
             HGX_CHECK_LAUNCH();
             if (g->n_chunks > 0) {
                 hgx_opush_heavy<W, MODE><<<(unsigned)g->n_chunks, 256, 0, s>>>(
-                    g->chunks, fa, g->inc_row, g->inc_type, want_type, g->tgt_off, g->tgt_idx, lvl, full, cand, clist,
-                    n_clist, acc, c);
+                    g->chunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
+                    cl, n_cl, acc, c);
                 HGX_CHECK_LAUNCH();
             }
-            hgx_push_finalize_list<W><<<4096, 256, 0, s>>>(clist, n_clist, g->inc_off, acc, vis, ever, full, lvl_next,
-                                                           fa_next, c, fm);
+            // finalise; re-zeroes the accumulator rows and candidate words it consumed and, without a
+            // ghost exchange, rewrites the candidate list into the next level's frontier list
+            hgx_push_finalize_list<W><<<4096, 256, 0, s>>>(cl, n_cl, g->inc_off, acc, cand, vis, ever, full,
+                                                           lvl_next, fa_next, c, fm, ex ? 0 : 1);
             HGX_CHECK_LAUNCH();
             g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
+            cand_clean = true;
+            chained = !ex;
+            std::swap(fl, cl);
+            std::swap(n_fl, n_cl);
             tm.stop(e2);
         } else {
         if (sparse) {
@@ -2428,9 +2566,11 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                          2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
             } else if (opush_level) {   // frontier push: no gather; two frontier passes + finalise
                 b_gather = 0.0;
-                // frontier scan + links (inc_row, inc_type, tgt_off pair) + pins + one word RMW per pair
-                // + candidates (acc read + re-zero) + vis reads + lvl/vis writes + cleared bitmaps
-                b_pull = 8.0 * (A / 64.0) + 24.0 * c[cActiveLinks] + 4.0 * c[cActivePins] + 16.0 * c[cIncLight] +
+                // frontier scan + scanned entries (inc_type + yield flag) + links (inc_row, tgt_off pair) + pins
+                // + one word RMW per pair + candidates (acc read + re-zero) + vis reads + lvl/vis writes
+                // + cleared bitmaps
+                b_pull = 8.0 * (A / 64.0) + 5.0 * c[cScanned] + 20.0 * c[cActiveLinks] + 4.0 * c[cActivePins] +
+                         16.0 * c[cIncLight] +
                          2.0 * rowb * c[cCand] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] + 2.0 * A / 8.0;
             }
             const int pull_kind = c[cDirRows] == 3 ? HGX_K_NF_PULL : c[cDirRows] == 2 ? HGX_K_FRONTIER_PUSH

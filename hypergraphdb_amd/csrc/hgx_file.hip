@@ -331,6 +331,8 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->zacc = nullptr;
     if (g->hasinc) (void)hipFree(g->hasinc);
     g->hasinc = nullptr;
+    if (g->inc_yf) (void)hipFree(g->inc_yf);
+    g->inc_yf = nullptr;
     g->zacc_bytes = 0;
     g->zacc_clean = false;
     graph_release(fresh);   // frees the old arrays now held by `fresh`

@@ -31,6 +31,7 @@ void graph_release(hgx_graph* g) {
     (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->hasinc) (void)hipFree(g->hasinc);
+    if (g->inc_yf) (void)hipFree(g->inc_yf);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->stream) (void)hipStreamDestroy(g->stream);

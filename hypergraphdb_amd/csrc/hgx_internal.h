@@ -129,6 +129,7 @@ struct hgx_graph {
     std::vector<int64_t> inc_off_host;   // host copy of inc_off (pattern planning), made on first use
     uint64_t* zacc = nullptr;
     uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
+    uint8_t* inc_yf = nullptr;           // [I] ordered-mode yield flags per incidence (frontier push), made on first use
     size_t zacc_bytes = 0;
     bool zacc_clean = false;
 
