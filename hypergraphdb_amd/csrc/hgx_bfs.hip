@@ -1061,6 +1061,9 @@ __global__ void __launch_bounds__(256) hgx_inc_yield(int64_t A, const int64_t* _
 // nonzero words of the pushing atom's row.
 constexpr int kCBuf = 256;   // candidates staged per wave before one list append
 constexpr int kEBuf = 256;   // filtered incidence entries staged per wave
+// Frontier push load balance: an atom with more than kPushLight incidences is pushed by blocks of
+// four waves over kPushChunk-entry chunks (hgx_opush_heavy), the others by one wave each.
+constexpr int64_t kPushLight = 512, kPushChunk = 256;
 
 struct OPushLds {
     int32_t tgt[64];
@@ -1105,19 +1108,56 @@ __device__ __forceinline__ void opush_entry(int32_t v, int64_t i, bool have, con
         const int32_t L = inc_row[i];
         b = tgt_off[L];
         n = (int)(tgt_off[L + 1] - b);
+        ++n_links;
+        n_pins += (u64)n;
+    }
+    // A row of <= kRegRow targets is loaded once into registers (independent loads) and so are the
+    // full-bitmap words of its eligible targets; longer rows take the loop below.
+    constexpr int kRegRow = 8;
+    int32_t tr[kRegRow];
+    const bool reg = n <= kRegRow;
+#pragma unroll
+    for (int k = 0; k < kRegRow; ++k) tr[k] = (reg && k < n) ? tgt_idx[b + k] : -1;
+    if (reg) {
+#pragma unroll
+        for (int k = 0; k < kRegRow; ++k)
+            if (tr[k] == v) {
+                if (fv < 0) fv = k;
+                lv = k;
+            }
+    } else {
         for (int p = 0; p < n; ++p)
             if (tgt_idx[b + p] == v) {
                 if (fv < 0) fv = p;
                 lv = p;
             }
-        ++n_links;
-        n_pins += (u64)n;
+    }
+    unsigned em = 0;   // eligible register positions
+    if (reg) {
+        u64 fw[kRegRow];
+#pragma unroll
+        for (int k = 0; k < kRegRow; ++k) {
+            const bool e = tr[k] >= 0 && tr[k] != v && yields<MODE>(k, fv, lv);
+            fw[k] = e ? full[tr[k] >> 6] : ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kRegRow; ++k)
+            if (!((fw[k] >> (tr[k] & 63)) & 1ull)) em |= 1u << k;
     }
     int nmax = n;
     for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
     for (int p = 0; p < nmax; ++p) {
-        const int32_t t = p < n ? tgt_idx[b + p] : -1;
-        const bool elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
+        int32_t t = -1;
+        bool elig;
+        if (reg) {
+#pragma unroll
+            for (int k = 0; k < kRegRow; ++k)
+                if (k == p) t = tr[k];
+            elig = (em >> p) & 1u;
+        } else {
+            t = p < n ? tgt_idx[b + p] : -1;
+            elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
+        }
         const u64 m = __ballot(elig);
         if (m == 0ull) continue;
         n_pairs += elig;
@@ -1238,7 +1278,8 @@ __device__ __forceinline__ int row_words(const u64* __restrict__ lvl, int64_t v,
 // per-wave atomic on the list counter serialised: 76 us per level on config 5's sparse frontiers).
 __global__ void __launch_bounds__(256) hgx_frontier_list(int64_t A, const u64* __restrict__ fa,
                                                          const int64_t* __restrict__ inc_off,
-                                                         int32_t* __restrict__ list, u64* __restrict__ n_list) {
+                                                         int32_t* __restrict__ list, u64* __restrict__ n_list,
+                                                         int64_t light_max) {
     __shared__ int wsum[4];
     __shared__ u64 sbase;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1251,7 +1292,7 @@ __global__ void __launch_bounds__(256) hgx_frontier_list(int64_t A, const u64* _
             const int b = __ffsll((long long)y) - 1;
             const int64_t v = w * 64 + b;
             const int64_t d = inc_off[v + 1] - inc_off[v];
-            if (d > 0 && d <= kHeavyDegree) keep |= 1ull << b;
+            if (d > 0 && d <= light_max) keep |= 1ull << b;
         }
         return keep;
     };
@@ -1308,20 +1349,25 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
                                                  const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
                                                  const u64* __restrict__ full, u64* __restrict__ cand,
                                                  int32_t* __restrict__ clist, u64* __restrict__ n_clist,
-                                                 u64* __restrict__ acc, u64* __restrict__ ctr) {
+                                                 u64* __restrict__ acc, u64* __restrict__ ctr,
+                                                 u64* __restrict__ fa_next, int64_t n_words) {
     __shared__ OPushLds lds[4];
     OPushLds& sh = lds[threadIdx.x >> 6];
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    // the next frontier bitmap (set by the finalise) is cleared here instead of by a memset
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x)
+        fa_next[w] = 0ull;
     const int64_t n = (int64_t)*n_list;
     u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
     int cc = 0;   // staged candidates (wave-uniform)
     for (int64_t k = wave; k < n; k += nwave) {
         const int32_t v = list[k];
         if (v < 0) continue;   // a candidate list reused as the frontier list: not new / not light
+        const int64_t beg = inc_off[v], end = inc_off[v + 1];   // in flight with the row load
         const int nnz = row_words<W>(lvl, v, sh);
         if (nnz == 0) continue;
-        opush_links<W, MODE>(v, inc_off[v], inc_off[v + 1], 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
+        opush_links<W, MODE>(v, beg, end, 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
                              nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
     }
     cand_flush(sh, cc, clist, n_clist);
@@ -1371,7 +1417,8 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
                                                               u64* __restrict__ vis,
                                                               u64* __restrict__ ever, u64* __restrict__ full,
                                                               u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
-                                                              u64* __restrict__ ctr, FullMask fm, int relist) {
+                                                              u64* __restrict__ ctr, FullMask fm, int relist,
+                                                              u64* __restrict__ n_spent) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
     const int sub = threadIdx.x & (G - 1);
@@ -1379,6 +1426,8 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
     const int64_t n = (int64_t)*n_clist;
+    // the consumed frontier list's counter: zero for the next level's candidates (chained levels)
+    if (n_spent && blockIdx.x == 0 && threadIdx.x == 0) *n_spent = 0ull;
     u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t k0 = grp - (grp % (64 / G)); k0 < n; k0 += ngrp) {   // wave-uniform trip count
         const int64_t k = k0 + (grp % (64 / G));
@@ -1408,7 +1457,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
             }
         }
         // the next push level's frontier list in place: the new light atoms, -1 elsewhere
-        if (relist && valid && sub == 0) clist[k] = (dg > 0 && dg <= kHeavyDegree) ? (int32_t)t : -1;
+        if (relist && valid && sub == 0) clist[k] = (dg > 0 && dg <= kPushLight) ? (int32_t)t : -1;
         if (valid && sub == 0) {
             ++n_cand;
             n_vis += ev;
@@ -1949,6 +1998,66 @@ enum { kKindGather = HGX_K_LINK_GATHER, kKindPull = HGX_K_ATOM_PULL, kKindHeavy 
        kKindHub = HGX_K_HUB_FINALIZE, kKindPush = HGX_K_FRONTIER_PUSH, kKindNf = HGX_K_NF_PULL,
        kKindExchange = HGX_K_COUNT };
 
+// Atoms with more than thr incidences and their ranges (order-free compaction).
+__global__ void __launch_bounds__(256) hgx_push_heavy_find(int64_t A, const int64_t* __restrict__ inc_off,
+                                                           int64_t thr, int64_t* __restrict__ out,
+                                                           unsigned int* __restrict__ n) {
+    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A; a += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = inc_off[a], e = inc_off[a + 1];
+        if (e - b > thr) {
+            const unsigned k = atomicAdd(n, 1u);
+            out[3 * (int64_t)k] = a;
+            out[3 * (int64_t)k + 1] = b;
+            out[3 * (int64_t)k + 2] = e;
+        }
+    }
+}
+
+// The frontier push's chunk table (once per snapshot): kPushChunk-entry chunks of every atom with
+// more than kPushLight incidences, in atom order.
+void build_push_chunks(hgx_graph* g) {
+    hipStream_t s = g->stream;
+    const int64_t A = g->A;
+    // at most I / (kPushLight + 1) atoms have more than kPushLight incidences
+    const int64_t nmax = std::min<int64_t>(g->I / (kPushLight + 1) + 1, std::max<int64_t>(A, 1));
+    int64_t* dout = (int64_t*)g->alloc(sizeof(int64_t) * 3 * (size_t)nmax);
+    unsigned int* dn = (unsigned int*)g->alloc(16);
+    HGX_HIP(hipMemsetAsync(dn, 0, 4, s));
+    hgx_push_heavy_find<<<grid_for(A, 256, 4096), 256, 0, s>>>(A, g->inc_off, kPushLight, dout, dn);
+    HGX_CHECK_LAUNCH();
+    unsigned int nh = 0;
+    HGX_HIP(hipMemcpyAsync(&nh, dn, 4, hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> h(3 * (size_t)nh);
+    if (nh) HGX_HIP(hipMemcpyAsync(h.data(), dout, sizeof(int64_t) * 3 * nh, hipMemcpyDeviceToHost, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    g->release(dout, sizeof(int64_t) * 3 * (size_t)nmax);
+    g->release(dn, 16);
+    std::vector<size_t> ord(nh);
+    for (size_t i = 0; i < nh; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return h[3 * x] < h[3 * y]; });
+    std::vector<HeavyChunk> ch;
+    for (size_t i : ord)
+        for (int64_t b = h[3 * i + 1]; b < h[3 * i + 2]; b += kPushChunk)
+            ch.push_back({b, std::min(h[3 * i + 2], b + kPushChunk), (int32_t)h[3 * i], -1});
+    if (g->pchunks) HGX_HIP(hipFree(g->pchunks));
+    g->pchunks = nullptr;
+    HGX_HIP(hipMalloc(&g->pchunks, sizeof(HeavyChunk) * std::max<size_t>(ch.size(), 1)));
+    if (!ch.empty())
+        HGX_HIP(hipMemcpyAsync(g->pchunks, ch.data(), sizeof(HeavyChunk) * ch.size(), hipMemcpyHostToDevice, s));
+    HGX_HIP(hipStreamSynchronize(s));
+    g->n_pchunks = (int64_t)ch.size();
+}
+
+// End-of-level wait for the counter copy: a host spin on hipStreamQuery (the blocking wait adds
+// tens of microseconds per level, and unbounded traversals run tens of short levels).
+void level_sync(hipStream_t s) {
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    HGX_HIP(e);
+}
+
 FullMask full_mask(int S, int W) {
     FullMask fm;
     for (int w = 0; w < 16; ++w) {
@@ -2194,29 +2303,32 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 HGX_CHECK_LAUNCH();
             }
             const uint8_t* yf = g->inc_yf;
+            if (g->n_pchunks < 0) build_push_chunks(g);
+            // chained levels need no memset: the candidate words are zero-invariant, fa_next is cleared by
+            // hgx_opush and n_cl by the previous finalise
             if (!cand_clean) HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
-            HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
-            HGX_HIP(hipMemsetAsync(n_cl, 0, sizeof(u64), s));
             if (!chained) {   // the frontier list from the bitmap (else the last finalise left it in fl)
+                HGX_HIP(hipMemsetAsync(n_cl, 0, sizeof(u64), s));
                 HGX_HIP(hipMemsetAsync(n_fl, 0, sizeof(u64), s));
                 const int fgrid = grid_for(ceil_div(A, 64), 256, 256);   // <= 256 list atomics per level
-                hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, fl, n_fl);
+                hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, fl, n_fl, kPushLight);
                 HGX_CHECK_LAUNCH();
             }
             const int lgrid = 2048;   // 8192 waves, grid-stride over the frontier list
             hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
-                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c);
+                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
+                                                     fa_next, (int64_t)(bm_bytes / sizeof(u64)));
             HGX_CHECK_LAUNCH();
-            if (g->n_chunks > 0) {
-                hgx_opush_heavy<W, MODE><<<(unsigned)g->n_chunks, 256, 0, s>>>(
-                    g->chunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
+            if (g->n_pchunks > 0) {
+                hgx_opush_heavy<W, MODE><<<(unsigned)g->n_pchunks, 256, 0, s>>>(
+                    g->pchunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
                     cl, n_cl, acc, c);
                 HGX_CHECK_LAUNCH();
             }
             // finalise; re-zeroes the accumulator rows and candidate words it consumed and, without a
             // ghost exchange, rewrites the candidate list into the next level's frontier list
             hgx_push_finalize_list<W><<<4096, 256, 0, s>>>(cl, n_cl, g->inc_off, acc, cand, vis, ever, full,
-                                                           lvl_next, fa_next, c, fm, ex ? 0 : 1);
+                                                           lvl_next, fa_next, c, fm, ex ? 0 : 1, ex ? nullptr : n_fl);
             HGX_CHECK_LAUNCH();
             g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
             cand_clean = true;
@@ -2306,7 +2418,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             tm.stop(e5);
         }
         HGX_HIP(hipMemcpyAsync(h_sh, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
+        level_sync(s);
         for (int k = 0; k < cNum; ++k) {
             h_new[k] = 0;
             for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += h_sh[sh * kCtrStride + k];

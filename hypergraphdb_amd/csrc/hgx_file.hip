@@ -333,6 +333,9 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->hasinc = nullptr;
     if (g->inc_yf) (void)hipFree(g->inc_yf);
     g->inc_yf = nullptr;
+    if (g->pchunks) (void)hipFree(g->pchunks);
+    g->pchunks = nullptr;
+    g->n_pchunks = -1;
     g->zacc_bytes = 0;
     g->zacc_clean = false;
     graph_release(fresh);   // frees the old arrays now held by `fresh`

@@ -32,6 +32,7 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->hasinc) (void)hipFree(g->hasinc);
     if (g->inc_yf) (void)hipFree(g->inc_yf);
+    if (g->pchunks) (void)hipFree(g->pchunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->stream) (void)hipStreamDestroy(g->stream);

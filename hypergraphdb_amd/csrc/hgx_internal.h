@@ -130,6 +130,8 @@ struct hgx_graph {
     uint64_t* zacc = nullptr;
     uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
     uint8_t* inc_yf = nullptr;           // [I] ordered-mode yield flags per incidence (frontier push), made on first use
+    hgx::HeavyChunk* pchunks = nullptr;  // frontier push: kPushChunk-entry chunks of atoms with deg > kPushLight
+    int64_t n_pchunks = -1;              // -1 = not built yet
     size_t zacc_bytes = 0;
     bool zacc_clean = false;
 
