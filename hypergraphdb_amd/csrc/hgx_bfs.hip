@@ -2049,15 +2049,6 @@ void build_push_chunks(hgx_graph* g) {
     g->n_pchunks = (int64_t)ch.size();
 }
 
-// End-of-level wait for the counter copy: a host spin on hipStreamQuery (the blocking wait adds
-// tens of microseconds per level, and unbounded traversals run tens of short levels).
-void level_sync(hipStream_t s) {
-    hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
-    }
-    HGX_HIP(e);
-}
-
 FullMask full_mask(int S, int W) {
     FullMask fm;
     for (int w = 0; w < 16; ++w) {
@@ -2182,7 +2173,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* ctr = (u64*)g->alloc(sizeof(u64) * kCtrBlock * max_levels_cap);
     int32_t* d_atoms = (int32_t*)g->alloc(sizeof(int32_t) * seed_atoms.size());
     u64* d_rows = (u64*)g->alloc(sizeof(u64) * seed_rows.size());
-    u64* h_sh = (u64*)g->pinned_buf(sizeof(u64) * kCtrBlock);
+    u64* h_sh = (u64*)g->pinned_buf(sizeof(u64) * kCtrBlock * 2);   // two levels in flight
     u64 h_new[cNum];
 
     HGX_HIP(hipMemsetAsync(ever, 0, bm_bytes, s));
@@ -2243,13 +2234,73 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // atoms is visited by every traversal (seeds that are full count from the start).
     u64 full_total = 0;
 
-    for (int32_t d = 0; d < maxd && d < max_levels_cap - 1; ++d) {
-        u64* lvl = bt.lvl[d];
-        u64* fa = bt.fa[d];
+    struct Pend {
+        int32_t d = 0;
+        u64* lvl_next = nullptr;
+        u64* fa_next = nullptr;
+        int kind = 0, allrows = 0;
+        u64 new_global = 0, part_push = 0;
+        u64* h = nullptr;
+        hipEvent_t ev = nullptr;
+    } pend[2];
+    for (int k = 0; k < 2; ++k) {
+        pend[k].h = h_sh + (size_t)k * kCtrBlock;
+        HGX_HIP(hipEventCreateWithFlags(&pend[k].ev, hipEventDisableTiming));
+    }
+    int npend = 0;
+    bool stop = false;
+    u64* cur_lvl = bt.lvl[0];
+    u64* cur_fa = bt.fa[0];
+    const bool pipe_ok = sparse_ok && !ex && MODE != kSym && (g->bfs_flags & 512);
+    // End-of-level wait: a host spin (the blocking wait adds tens of microseconds per level, and
+    // unbounded traversals run tens of short levels).
+    auto wait_event = [](hipEvent_t ev) {
+        hipError_t e;
+        while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+        }
+        HGX_HIP(e);
+    };
+    // One level's counters -> host state; false once the level found no new atom (its rows released).
+    auto read_level = [&](Pend& p) -> bool {
+        wait_event(p.ev);
+        for (int k = 0; k < cNum; ++k) {
+            h_new[k] = 0;
+            for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += p.h[sh * kCtrStride + k];
+        }
+        if (ex) {   // the group decides termination; the next level's push volume is my frontier's
+            h_new[cNewAtoms] = p.new_global;
+            h_new[cNewDeg] = p.part_push;
+        }
+        level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
+        level_ctr.back()[cDirRows] = (u64)p.kind;   // (host-side) kind of this level
+        if (!ex) full_deg_total += (int64_t)(h_new[cNewDeg] - h_new[cNewDegNF]);   // incidence of atoms now full
+        if (trace)
+            std::fprintf(stderr, "[hgx bfs] level %d kind %d allrows %d active_links %llu new %llu push %llu push_nf %llu "
+                         "new_full %llu\n", p.d, p.kind, p.allrows,
+                         (unsigned long long)h_new[cActiveLinks], (unsigned long long)h_new[cNewAtoms],
+                         (unsigned long long)h_new[cNewDeg], (unsigned long long)h_new[cNewDegNF],
+                         (unsigned long long)h_new[cNewFull]);
+        push_volume = h_new[cNewDeg];
+        push_volume_nf = ex ? push_volume : h_new[cNewDegNF];
+        full_total += h_new[cNewFull];
+        if (h_new[cNewAtoms] == 0) {
+            g->release(p.lvl_next, row_bytes);
+            g->release(p.fa_next, bm_bytes);
+            return false;
+        }
+        bt.lvl.push_back(p.lvl_next);
+        bt.fa.push_back(p.fa_next);
+        return true;
+    };
+
+    for (int32_t d = 0; d < maxd && d < max_levels_cap - 1 && !stop; ++d) {
+        u64* lvl = cur_lvl;
+        u64* fa = cur_fa;
+        const bool spec = npend > 0;   // issued before the previous level's counters were read
         u64* lvl_next = (u64*)g->alloc(row_bytes);
         u64* fa_next = (u64*)g->alloc(bm_bytes);   // every word written by hgx_atom_pull
         u64* c = ctr + (size_t)d * kCtrBlock;
-        const bool sparse = sparse_ok && push_volume < sparse_limit;
+        const bool sparse = spec || (sparse_ok && push_volume < sparse_limit);
         int lflags = g->bfs_flags;
         if ((lflags & 16) && (int64_t)full_total * 16 < A) lflags &= ~4;   // adaptive full skip
         const bool opush = sparse && (MODE != kSym || (lflags & 32));
@@ -2417,36 +2468,41 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push);
             tm.stop(e5);
         }
-        HGX_HIP(hipMemcpyAsync(h_sh, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
-        level_sync(s);
-        for (int k = 0; k < cNum; ++k) {
-            h_new[k] = 0;
-            for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += h_sh[sh * kCtrStride + k];
+        Pend& pn = pend[d & 1];
+        pn.d = d;
+        pn.lvl_next = lvl_next;
+        pn.fa_next = fa_next;
+        pn.kind = nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;
+        pn.allrows = (lflags & kAllRows) ? 1 : 0;
+        pn.new_global = new_global;
+        pn.part_push = part_push;
+        HGX_HIP(hipMemcpyAsync(pn.h, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipEventRecord(pn.ev, s));
+        ++npend;
+        cur_lvl = lvl_next;
+        cur_fa = fa_next;
+        // Pipelined push levels: while this level runs, the next one is issued when it is surely a push
+        // level (frontier incidence volume < 1/4 of the sparse limit); an empty frontier costs it nothing
+        // but three near-empty launches, so the counters are read one level late.
+        for (;;) {
+            const bool can_spec = pipe_ok && npend == 1 && opush && push_volume * 4 < sparse_limit && d + 1 < maxd &&
+                                  d + 1 < max_levels_cap - 1;
+            if (npend == 0 || can_spec) break;
+            Pend& p = pend[(d - npend + 1) & 1];   // the oldest unread level
+            --npend;
+            if (!read_level(p)) {
+                stop = true;
+                for (; npend > 0; --npend) {   // a level issued after the last frontier: its rows are empty
+                    Pend& q = pend[(d - npend + 1) & 1];
+                    wait_event(q.ev);
+                    g->release(q.lvl_next, row_bytes);
+                    g->release(q.fa_next, bm_bytes);
+                }
+                break;
+            }
         }
-        if (ex) {   // the group decides termination; the next level's push volume is my frontier's
-            h_new[cNewAtoms] = new_global;
-            h_new[cNewDeg] = part_push;
-        }
-        level_ctr.push_back(std::vector<u64>(h_new, h_new + cNum));
-        level_ctr.back()[cDirRows] = nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;   // (host-side) kind of this level
-        if (!ex) full_deg_total += (int64_t)(h_new[cNewDeg] - h_new[cNewDegNF]);   // incidence of atoms now full
-        if (trace)
-            std::fprintf(stderr, "[hgx bfs] level %d kind %d allrows %d active_links %llu new %llu push %llu push_nf %llu "
-                         "new_full %llu\n", d, nfp ? 3 : sparse ? (opush ? 2 : 1) : 0, (lflags & kAllRows) ? 1 : 0,
-                         (unsigned long long)h_new[cActiveLinks], (unsigned long long)h_new[cNewAtoms],
-                         (unsigned long long)h_new[cNewDeg], (unsigned long long)h_new[cNewDegNF],
-                         (unsigned long long)h_new[cNewFull]);
-        push_volume = h_new[cNewDeg];
-        push_volume_nf = ex ? push_volume : h_new[cNewDegNF];
-        full_total += h_new[cNewFull];
-        if (h_new[cNewAtoms] == 0) {
-            g->release(lvl_next, row_bytes);
-            g->release(fa_next, bm_bytes);
-            break;
-        }
-        bt.lvl.push_back(lvl_next);
-        bt.fa.push_back(fa_next);
     }
+    for (int k = 0; k < 2; ++k) (void)hipEventDestroy(pend[k].ev);
     if (ex) res->stats.bytes_exchanged += ex->bytes_sent;
     g->release(vis, row_bytes);
     if (lf) g->release(lf, sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W);

@@ -121,7 +121,7 @@ struct hgx_graph {
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
-    int32_t bfs_flags = 0x1BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
+    int32_t bfs_flags = 0x3BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
     int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
     // Frontier-push accumulator rows (A x W words), all zero between levels: each push level ORs

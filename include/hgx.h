@@ -150,8 +150,10 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 7 = dense levels whose frontier covers the links twice write every lf row
  *                              and pull without the active-link probe,
  *                      bit 8 = dense levels with < 1/4 of the incidence on atoms not yet visited by
- *                              every traversal pull those atoms straight from the frontier rows.
- *                      Default 0x1BE. */
+ *                              every traversal pull those atoms straight from the frontier rows,
+ *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
+ *                              before this level's counters reach the host.
+ *                      Default 0x3BE. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
  * (seeds are processed in chunks that fit; default 16 GiB). */

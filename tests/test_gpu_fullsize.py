@@ -1,0 +1,136 @@
+"""GPU parity at BASELINE.json's full sizes (configs 2, 3 and 5; config 4 runs the same engine on
+a compacted shard and is covered at reduced size by test_gpu_partition.py).
+
+Where the C oracle finishes in seconds the check is exact (config 3: all 10,000 queries;
+config 5: every closure in both directions; config 2: every set up to depth 2 for a sample of
+sources, which a depth-4 traversal must reproduce since BFS levels do not depend on maxDistance
+beyond them, HGBreadthFirstTraversal.java:49-66).  Depths 3-4 of config 2 (≈4M atoms per source
+per level) are checked through size-independent properties: batch-order and batch-split
+invariance, single-source equality, and disjoint sorted levels."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle_ctypes import OracleGraph, algen
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def snapshot(g):
+    from hypergraphdb_amd import HyperGraphSnapshot
+    return HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g.get("link_type"))
+
+
+def oracle(g):
+    return OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g.get("link_type"))
+
+
+@pytest.fixture(scope="module")
+def config2():
+    from hypergraphdb_amd import synth
+    g = synth.config2()
+    snap = snapshot(g)
+    yield g, snap
+    snap.close()
+
+
+def test_config2_full_depth2_vs_oracle(config2):
+    """10M nodes / 40M links, 1024 sources, depth 4: levels 0-2 of 32 sources equal the oracle's
+    (counts), full sets for 3 of them."""
+    from hypergraphdb_amd import bfs_batch
+    g, snap = config2
+    res = bfs_batch(snap, g["seeds"], 4)
+    counts = res.counts()
+    assert counts.shape[0] == 1024 and np.all(counts[:, 0] == 1)
+    orc = oracle(g)
+    pick = np.arange(0, 1024, 32)
+    oc, _ = orc.bfs_many(g["seeds"][pick], 2, 3, nthreads=THREADS)
+    assert np.array_equal(counts[pick, :3], oc)
+    for i in (0, 511, 1023):
+        lv = orc.bfs_levels(int(g["seeds"][i]), 2)
+        for d_, exp in enumerate(lv):
+            assert np.array_equal(res.visited(i, d_), exp), (i, d_)
+    res.close()
+
+
+def test_config2_full_depth4_invariants(config2):
+    """Depth 4 at full size: the per-source sets do not depend on the source's bit lane or on the
+    batch it runs in (two reversed 512-source batches, single-source runs); every level is sorted,
+    duplicate-free and disjoint from the others; the start atom is level 0 only."""
+    from hypergraphdb_amd import bfs_batch
+    g, snap = config2
+    seeds = g["seeds"]
+    res = bfs_batch(snap, seeds, 4)
+    counts = res.counts()
+    assert counts[:, 1:].sum() > 0
+    for half in (slice(0, 512), slice(512, 1024)):
+        part = seeds[half][::-1].copy()
+        r2 = bfs_batch(snap, part, 4)
+        assert np.array_equal(r2.counts(), counts[half][::-1])
+        r2.close()
+    for i in (3, 700):
+        one = bfs_batch(snap, seeds[i:i + 1], 4)
+        seen = np.zeros(g["num_atoms"], np.int8)
+        for d_ in range(5):
+            a = res.visited(i, d_)
+            assert np.array_equal(one.visited(0, d_), a), (i, d_)
+            assert np.all(np.diff(a) > 0)
+            assert not seen[a].any()
+            seen[a] = 1
+            if d_ == 0:
+                assert a.tolist() == [int(seeds[i])]
+        one.close()
+    res.close()
+
+
+def test_config3_full_all_queries_vs_oracle():
+    """50M typed links, all 10,000 hg.and(type, incident, orderedLink(x, ANY, y)) queries of the
+    bench: per-query result counts and the id checksum equal the oracle's (literal ZigZag +
+    OrderedLinkCondition restatement); 300 sampled queries compared id by id (ascending)."""
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    g = synth.config3()
+    Q = g["queries"]
+    n = len(Q["type"])
+    snap = snapshot(g)
+    pat = np.stack([Q["x"], np.full(n, -1, np.int32), Q["y"]], 1).reshape(-1)
+    inc_off = np.arange(n + 1, dtype=np.int64)
+    pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
+    r = pattern_batch_arrays(snap, Q["type"], inc_off, Q["a"], np.ones(n, np.int32), pat_off, pat)
+    snap.close()
+    orc = oracle(g)
+    counts, checksum, rc = orc.and_query_many(Q["type"], inc_off, Q["a"], pat_off, pat, np.ones(n, np.int32),
+                                              nthreads=THREADS)
+    assert rc == 0
+    assert np.array_equal(np.diff(r.offsets), counts)
+    assert int(r.ids.astype(np.int64).sum()) == checksum
+    assert (counts > 0).sum() > 0.8 * n          # the sampled link matches its own query
+    for q in np.random.default_rng(5).choice(n, 300, replace=False):
+        exp = orc.and_query(int(Q["type"][q]), [int(Q["a"][q])], [int(Q["x"][q]), -1, int(Q["y"][q])])
+        assert r[q].tolist() == exp.tolist(), q
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_config5_full_closures_vs_oracle(reverse):
+    """5M classes, 1024 hg.subsumed / hg.subsumes closures, unbounded depth: every source's
+    per-depth counts equal the oracle's; full sets for 4 sources."""
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, bfs_batch, synth
+    g = synth.config5()
+    snap = snapshot(g)
+    T = g["subsumes_type"]
+    gen = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, reverse)
+    res = bfs_batch(snap, g["seeds"], None, gen)
+    counts = res.counts()
+    orc = oracle(g)
+    opts = algen(T, False, True, reverse, False)
+    oc, _ = orc.bfs_many(g["seeds"], -1, res.n_levels + 1, opts, nthreads=THREADS)
+    assert np.array_equal(counts, oc[:, :res.n_levels])
+    assert oc[:, res.n_levels:].sum() == 0
+    for i in (0, 100, 777, 1023):
+        lv = orc.bfs_levels(int(g["seeds"][i]), -1, opts)
+        for d_, exp in enumerate(lv):
+            assert np.array_equal(res.visited(i, d_), exp), (i, d_)
+    res.close()
+    snap.close()

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Per-level breakdown of the config-5 subsumption closures (both directions).
 
-  python tools/ab_c5.py [--scale 1.0] [--flags 0x1BE]
+  python tools/ab_c5.py [--scale 1.0] [--flags 0x3BE]
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -14,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--flags", default="0x1BE")
+    ap.add_argument("--flags", default="0x3BE")
     ap.add_argument("--sources", type=int, default=1024)
     args = ap.parse_args()
     import hypergraphdb_amd as H
@@ -30,7 +31,12 @@ def main():
                 r = H.bfs_batch(snap, g["seeds"], None, gen)
                 st = r.stats(accounting=True)
                 r.close()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                H.bfs_batch(snap, g["seeds"], None, gen).close()
+            wall = (time.perf_counter() - t0) / 5 * 1e3
             print(json.dumps({"flags": f, "reverse": rev, "ms_total": round(st["ms_total"], 3),
+                              "wall_ms": round(wall, 3),
                               "kernels": {k: round(v["ms"], 3) for k, v in st["kernels"].items()},
                               "level_ms": st["level_ms"], "level_new": st["level_new"],
                               "level_sparse": st["level_sparse"], "union_frontier": st["union_frontier"]}), flush=True)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-level row counters of the config-2 batched BFS (what each dense kernel read).
 
-  python tools/level_rows.py [--scale 1.0] [--flags 0x1BE]
+  python tools/level_rows.py [--scale 1.0] [--flags 0x3BE]
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ NAMES = ["active_links", "active_pins", "inc_light", "vis_light", "new_light", "
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--flags", default="0x1BE")
+    ap.add_argument("--flags", default="0x3BE")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import _lib, synth
