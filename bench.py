@@ -286,7 +286,31 @@ def run_config5(args, ctx, barrier_sync):
     return out
 
 
+_JSON_FD = None
+
+
+def claim_stdout():
+    """Native libraries write to fd 1 (gloo's peer-connection notes, RCCL's version banner): route
+    fd 1 to stderr for the whole run and keep the original stdout for the one JSON line."""
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(line):
+    data = (json.dumps(line) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+        return
+    sys.stdout.flush()
+    while data:
+        data = data[os.write(_JSON_FD, data):]
+
+
 def main():
+    claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -453,7 +477,7 @@ def main():
             log(f"rank {rank}: config4 legs exceeded {args.c4_timeout:.0f}s; reporting what finished")
             if line is not None:
                 line["config4"] = dict(c4, error=f"abandoned after {args.c4_timeout:.0f}s")
-                print(json.dumps(line), flush=True)
+                emit(line)
             os._exit(0)
 
         wd = threading.Timer(args.c4_timeout, watchdog)
@@ -468,7 +492,7 @@ def main():
         if line is not None:
             line["config4"] = c4
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     ctx.close()
 
 

@@ -27,6 +27,8 @@ void graph_release(hgx_graph* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     for (auto& b : g->pool) (void)hipFree(b.p);
     g->pool.clear();
+    for (auto e : g->ev_pool) (void)hipEventDestroy(e);
+    g->ev_pool.clear();
     (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
     (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->zacc) (void)hipFree(g->zacc);

@@ -121,6 +121,7 @@ struct hgx_graph {
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
+    std::vector<hipEvent_t> ev_pool;   // timing events reused across calls (taken under mu)
     int32_t bfs_flags = 0x3BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
     int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
