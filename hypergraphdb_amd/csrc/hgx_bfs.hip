@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
     wave_add_sh(ctr + cActivePins, n_pins);
 }
 
-template <int W>
+template <int W, int JBX = 2>
 __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* __restrict__ inc_off,
                                                       const int32_t* __restrict__ inc_row,
                                                       const u64* __restrict__ la, const u64* __restrict__ lf,
@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                                                       u64* __restrict__ fa_next, u64* __restrict__ ctr, FullMask fm,
                                                       int flags) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
-    constexpr int JB = G >= 8 ? 4 : G;   // atoms of a group interleaved at once (register budget)
+    constexpr int JB = G >= 8 ? JBX : G;   // atoms of a group interleaved at once (register budget)
     static_assert(G >= 4, "pull2 needs G >= 4");
     typedef Vec<WPL> V;
     const bool early = flags & 2, skip_full = flags & 4, all_rows = flags & kAllRows;
@@ -2426,8 +2426,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         Events e1 = tm.start(kKindGather, d);
         if constexpr (Lay<W>::G >= 4) {
             if (v2)
+            {
+                // Forcing more waves/SIMD (amdgpu_waves_per_eu) spills VGPRs: 4 waves ran 6% faster but 5
+                // waves returned wrong frontiers (spills around the group shuffles), so no variant ships.
                 hgx_link_gather2<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
                     M, g->tgt_off, g->tgt_idx, g->link_type, want_type, fa, full, lvl, lf, la, c, fm, lflags);
+            }
         }
         if (!v2)
             hgx_link_gather<W, MODE == kSym><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
@@ -2451,8 +2455,16 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         Events e2 = tm.start(kKindPull, d);
         if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
             if (v2)
-                hgx_atom_pull2<W><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever, full,
-                                                              lvl_next, fa_next, c, fm, lflags);
+            {
+                // two atoms of a group interleaved (152 VGPRs, 3 waves/SIMD): config 2 pull 5.73 -> 5.23 ms
+                // a step against four (184 VGPRs, 2 waves/SIMD); bit 11 = the four-atom variant (A/B)
+                if (lflags & 2048)
+                    hgx_atom_pull2<W, 4><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever,
+                                                                     full, lvl_next, fa_next, c, fm, lflags);
+                else
+                    hgx_atom_pull2<W, 2><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever,
+                                                                     full, lvl_next, fa_next, c, fm, lflags);
+            }
         }
         if (!(v2 && MODE == kSym))
             hgx_atom_pull<W, MODE><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, g->tgt_off,

@@ -152,7 +152,9 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 8 = dense levels with < 1/4 of the incidence on atoms not yet visited by
  *                              every traversal pull those atoms straight from the frontier rows,
  *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
- *                              before this level's counters reach the host.
+ *                              before this level's counters reach the host,
+ *                      bit 11 = the dense pull interleaves four atoms per lane group instead of two
+ *                              (A/B only).
  *                      Default 0x3BE. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays

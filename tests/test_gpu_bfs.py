@@ -225,7 +225,7 @@ def test_depth_of_and_errors():
         res.visited(5, 0)
 
 
-@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6, 0x3BE, 0x236])
+@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6, 0x3BE, 0x236, 0xBBE])
 def test_engine_option_matrix(flags):
     """Every work-avoidance option (early exits, full-visited skipping, frontier-driven sparse
     levels) returns the same per-depth sets; power-law hubs + random edge cases + ordered modes."""
