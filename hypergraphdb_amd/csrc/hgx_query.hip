@@ -469,12 +469,15 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     int32_t* list = lds[threadIdx.x >> 6];
     int32_t* anch = lds_anch[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform in scalar registers: the chunk, its query, plan and descriptor come through scalar
+    // loads and leave the VGPRs to the candidate pipeline (135 -> fewer VGPRs, more waves per SIMD)
+    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const u64 lt = (1ull << lane) - 1ull;
-    u64 n_cand = 0, n_typed = 0, n_ar = 0, n_hits = 0;
+    uint32_t n_cand = 0, n_typed = 0;   // <= 16 per lane and chunk: no overflow at <= 2^28 chunks a wave
+    u64 n_ar = 0, n_hits = 0;
     for (int64_t chunk = wave; chunk < n_chunks; chunk += nwave) {
-        const int32_t q = chunk_q[chunk];
+        const int32_t q = __builtin_amdgcn_readfirstlane(chunk_q[chunk]);
         const QPlan pl = plan[q];
         const QDesc d = desc[q];
         const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
@@ -503,7 +506,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
             }
         }
         if (typed)   // streamed type column entries (a type-grouped range streams none)
-            n_cand += (u64)(lane * kPerLane < nc ? (nc - lane * kPerLane < kPerLane ? nc - lane * kPerLane : kPerLane)
+            n_cand += (uint32_t)(lane * kPerLane < nc ? (nc - lane * kPerLane < kPerLane ? nc - lane * kPerLane : kPerLane)
                                                  : 0);
         // stage 2: ascending list of passing candidate indices (relative to the chunk)
         const int cnt = __popc(passm);
@@ -617,8 +620,8 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
         n_hits += (u64)written;
     }
     u64* c = ctr + (wave & (kQShards - 1)) * kQStride;
-    wave_add_q(c + qCand, n_cand);
-    wave_add_q(c + qTyped, n_typed);
+    wave_add_q(c + qCand, (u64)n_cand);
+    wave_add_q(c + qTyped, (u64)n_typed);
     wave_add_q(c + qArity, n_ar);
     if (lane == 0 && n_hits) atomicAdd(c + qHits, n_hits);
 }
