@@ -72,6 +72,7 @@ template <> struct Vec<1> {
     static __device__ __forceinline__ bool eq(T x, T y) { return x == y; }
     static __device__ __forceinline__ T ld(const u64* p) { return *p; }
     static __device__ __forceinline__ void st(u64* p, T x) { *p = x; }
+    static __device__ __forceinline__ void st_nt(u64* p, T x) { __builtin_nontemporal_store(x, p); }
 };
 template <> struct Vec<2> {
     typedef u64x2 T;
@@ -80,6 +81,7 @@ template <> struct Vec<2> {
     static __device__ __forceinline__ bool eq(T x, T y) { return x.x == y.x && x.y == y.y; }
     static __device__ __forceinline__ T ld(const u64* p) { return *reinterpret_cast<const u64x2*>(p); }
     static __device__ __forceinline__ void st(u64* p, T x) { *reinterpret_cast<u64x2*>(p) = x; }
+    static __device__ __forceinline__ void st_nt(u64* p, T x) { __builtin_nontemporal_store(x, reinterpret_cast<u64x2*>(p)); }
 };
 
 // Valid-source mask of a row (S need not be a multiple of 64 or a power of two).
@@ -190,6 +192,30 @@ __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
 constexpr int kCtrShards = 16, kCtrStride = 16, kCtrBlock = kCtrShards * kCtrStride;
 // Internal per-level flag (above the HGX_OPT_BFS_FLAGS bits): dense level with every lf row written.
 constexpr int kAllRows = 1 << 16;
+// Cache-policy A/B bits of HGX_OPT_BFS_FLAGS for the tile-staged dense kernels (gather2 / pull2).
+// None moved config 2 beyond noise (17.66 / 17.63 / 17.68 / 17.65 / 17.63 ms for none / 12 / 13 /
+// 14 / all three, profiles/r01i_ab_nt.log): the streamed columns and the written rows do not evict
+// the hub rows the Infinity Cache serves, so the default keeps the plain policy.
+constexpr int kNtIdx = 1 << 12;    // nontemporal loads of the streamed CSR columns (offsets, ids)
+constexpr int kNtLf = 1 << 13;     // nontemporal stores of the gather's lf rows
+constexpr int kNtOut = 1 << 14;    // nontemporal stores of the pull's lvl_next / vis rows
+// Heavy (hub) pull of the symmetric mode with two incidence chunks of a group in flight at once and
+// no la probe, in all-rows levels before the full-visited skip turns on (HGX_OPT_BFS_FLAGS bit 15,
+// A/B only, off by default).  Config 2: level 1 8.89 -> 8.60 ms but level 2 6.81 -> 7.04 ms (hub
+// pulls there exit early after a few chunks and the one-chunk pull_range exits sooner); with the
+// probe kept both levels were slower; neither the `ever` bit nor the full-skip state of the level
+// separates the two cases (profiles/r01i_ab_heavy*.log), so the default keeps pull_range.
+constexpr int kHeavyMlp2 = 1 << 15;
+
+template <typename T>
+__device__ __forceinline__ T ld_col(const T* p, bool nt) {
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename V>
+__device__ __forceinline__ void st_row(u64* p, typename V::T x, bool nt) {
+    if (nt) V::st_nt(p, x);
+    else V::st(p, x);
+}
 static_assert(cNum <= kCtrStride, "counter block");
 __device__ __forceinline__ void wave_add_sh(u64* ctr, u64 v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -530,6 +556,7 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
     static_assert(G >= 4, "gather2 needs G >= 4");
     typedef Vec<WPL> V;
     const bool early = flags & 1, skip_full = flags & 4, all_rows = flags & kAllRows;
+    const bool nt_idx = flags & kNtIdx, nt_lf = flags & kNtLf;
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
     const u64 gmask = (1ull << G) - 1ull;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -541,8 +568,8 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
         int64_t bme = 0;
         int nme = 0;
         if (Lme < M && (want_type < 0 || link_type[Lme] == want_type)) {
-            bme = tgt_off[Lme];
-            nme = (int)(tgt_off[Lme + 1] - bme);
+            bme = ld_col(tgt_off + Lme, nt_idx);
+            nme = (int)(ld_col(tgt_off + Lme + 1, nt_idx) - bme);
         }
         int32_t v[G];
         int n[G];
@@ -551,7 +578,7 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
         for (int j = 0; j < G; ++j) {
             bb[j] = __shfl(bme, j * PW + g);
             n[j] = __shfl(nme, j * PW + g);
-            v[j] = sub < n[j] ? tgt_idx[bb[j] + sub] : -1;
+            v[j] = sub < n[j] ? ld_col(tgt_idx + bb[j] + sub, nt_idx) : -1;
         }
         unsigned pa = 0, pnf = 0;
 #pragma unroll
@@ -608,13 +635,13 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
                 act = nact > 0 && any_not_full;
             }
             if (act) {
-                if (WRITE_LF) V::st(lf + L * W + sub * WPL, acc);
+                if (WRITE_LF) st_row<V>(lf + L * W + sub * WPL, acc, nt_lf);
                 if (sub == 0) {
                     ++n_links;
                     n_pins += nact;
                 }
             } else if (WRITE_LF && all_rows && L < M) {
-                V::st(lf + L * W + sub * WPL, V::zero());   // the pull reads every row unprobed
+                st_row<V>(lf + L * W + sub * WPL, V::zero(), nt_lf);   // the pull reads every row unprobed
             }
             word |= compress_groups<G>(__ballot(act), j * PW);
         }
@@ -637,6 +664,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
     static_assert(G >= 4, "pull2 needs G >= 4");
     typedef Vec<WPL> V;
     const bool early = flags & 2, skip_full = flags & 4, all_rows = flags & kAllRows;
+    const bool nt_idx = flags & kNtIdx, nt_out = flags & kNtOut;
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1);
     const u64 gmask = (1ull << G) - 1ull;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -649,8 +677,8 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
         int64_t bme = 0;
         int dme = 0;
         if (tme < A && !(skip_full && ((full_w >> lane) & 1ull))) {
-            bme = inc_off[tme];
-            const int64_t d = inc_off[tme + 1] - bme;
+            bme = ld_col(inc_off + tme, nt_idx);
+            const int64_t d = ld_col(inc_off + tme + 1, nt_idx) - bme;
             dme = (d > 0 && d <= kHeavyDegree) ? (int)d : 0;
         }
         if (__ballot(dme > 0) == 0ull) {   // nothing to pull in this tile
@@ -679,7 +707,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                 int32_t myL[JB];
 #pragma unroll
                 for (int jj = 0; jj < JB; ++jj)
-                    myL[jj] = (!done[jj] && c0 + sub < dj[jj]) ? inc_row[bj[jj] + c0 + sub] : -1;
+                    myL[jj] = (!done[jj] && c0 + sub < dj[jj]) ? ld_col(inc_row + bj[jj] + c0 + sub, nt_idx) : -1;
                 unsigned pa = 0;
 #pragma unroll
                 for (int jj = 0; jj < JB; ++jj)
@@ -727,8 +755,8 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                     }
                     const typename V::T nw = acc[jj] & ~old[jj];
                     if (group_any<G>(V::nz(nw))) {
-                        V::st(lvl_next + t * W + sub * WPL, nw);
-                        V::st(vis + t * W + sub * WPL, old[jj] | nw);
+                        st_row<V>(lvl_next + t * W + sub * WPL, nw, nt_out);
+                        st_row<V>(vis + t * W + sub * WPL, old[jj] | nw, nt_out);
                         isnew = true;
                         becomes_full = group_all<G>(V::eq(old[jj] | nw, FULL));
                         if (sub == 0) { n_newdeg += (u64)dj[jj]; if (!becomes_full) n_newdeg_nf += (u64)dj[jj]; }
@@ -757,6 +785,61 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+}
+
+// pull_range for the symmetric mode, G >= 4, restructured for memory-level parallelism: a group
+// loads U chunks of G incidence entries at once, probes their la bits together (no probe when every
+// lf row was written, kAllRows) and then issues all U*G lf row loads before ORing them.  The early
+// exit is tested every U*G entries; ORing rows past the point where acc | old covers FULL changes
+// nothing in acc & ~old, so the result is the same as pull_range's.
+template <int W, int U>
+__device__ __forceinline__ void pull_range_mlp(int64_t b, int64_t e, const int32_t* __restrict__ inc_row,
+                                               const u64* __restrict__ la, const u64* __restrict__ lf,
+                                               const u64* __restrict__ vis_row, bool have_vis,
+                                               typename Vec<Lay<W>::WPL>::T FULL, int sub,
+                                               typename Vec<Lay<W>::WPL>::T& acc, typename Vec<Lay<W>::WPL>::T& old,
+                                               bool& have_old, u64& n_inc, u64& n_vis, bool early, bool all_rows) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    static_assert(G >= 4, "pull_range_mlp needs G >= 4");
+    typedef Vec<WPL> V;
+    const int base = (threadIdx.x & 63) & ~(G - 1);
+    for (int64_t i = b; i < e; i += U * G) {
+        int32_t myL[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = i + u * G + sub;
+            myL[u] = q < e ? inc_row[q] : -1;
+        }
+        unsigned ga[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool mya = myL[u] >= 0 && (all_rows || bit(la, myL[u]));
+            ga[u] = (unsigned)((__ballot(mya) >> base) & ((1ull << G) - 1ull));
+        }
+        typename V::T r[U][G];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int32_t Lk = __shfl(myL[u], base + k);
+                r[u][k] = ((ga[u] >> k) & 1u) ? V::ld(lf + (int64_t)Lk * W + sub * WPL) : V::zero();
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) acc |= r[u][k];
+            n_inc += __popc(ga[u]);
+        }
+        if (!early) continue;
+        if (!have_old && group_any<G>(V::nz(acc))) {
+            if (have_vis) {
+                old = V::ld(vis_row + sub * WPL);
+                ++n_vis;
+            }
+            have_old = true;
+        }
+        if (have_old && i + U * G < e && group_all<G>(V::eq(acc | old, FULL))) break;
+    }
 }
 
 // Heavy atoms: one workgroup per chunk of <= kChunkEntries incidence entries; groups OR their
@@ -790,7 +873,15 @@ __global__ void __launch_bounds__(256) hgx_atom_pull_heavy(const HeavyChunk* __r
     u64 n_inc = 0, n_vis = 0;
     typename V::T acc = V::zero(), old = V::zero();
     bool have_old = false;
-    if (b < e)
+    bool done = false;
+    if constexpr (G >= 4 && MODE == kSym) {
+        if (b < e && (flags & kHeavyMlp2) && (flags & kAllRows) && !(flags & 4)) {   // block-uniform
+            pull_range_mlp<W, 2>(b, e, inc_row, la, lf, vis + (int64_t)c.atom * W, bit(ever, c.atom), FULL, sub, acc,
+                                 old, have_old, n_inc, n_vis, (flags & 2) != 0, true);
+            done = true;
+        }
+    }
+    if (b < e && !done)
         pull_range<W, MODE>(c.atom, b, e, inc_row, la, lf, tgt_off, tgt_idx, fa, lvl, vis + (int64_t)c.atom * W,
                             bit(ever, c.atom), FULL, sub, acc, old, have_old, n_inc, n_vis, (flags & 2) != 0);
     V::st(red + gi * W + sub * WPL, acc);

@@ -154,7 +154,11 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
  *                              before this level's counters reach the host,
  *                      bit 11 = the dense pull interleaves four atoms per lane group instead of two
- *                              (A/B only).
+ *                              (A/B only),
+ *                      bits 12 / 13 / 14 = nontemporal loads of the streamed CSR columns / stores of
+ *                              the gather's link rows / stores of the pull's atom rows (A/B only),
+ *                      bit 15 = the symmetric-mode hub pull keeps two incidence chunks in flight
+ *                              without the active-link probe in all-rows levels (A/B only).
  *                      Default 0x3BE. */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
