@@ -7,19 +7,29 @@ hgx_bfs_batch over the 1024 sources with the CSR resident in HBM (all per-depth 
 materialised on the device).  Secondary: config 3, one step = one hgx_pattern_batch of 10,000
 hg.and(hg.type(T), hg.incident(a), hg.orderedLink(x, ANY, y)) queries over 50M typed links.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the sources
-are independent units; every rank holds a replica of the snapshot and runs its own 1024-source
-batch (weak scaling, no data-path collective).  torch.distributed is used only for the barrier
-and the max-over-ranks of the elapsed time.
+A timed step ends with the result readout: the per-source, per-depth counts of every start atom
+(hgx_bfs_result_counts: one counting launch per level over the device rows + one D2H), as
+BASELINE.md section 2 times "to the last D2H of results".
+
+Multi-GPU: `python bench.py --gpus N` launches N ranks itself (one process per GPU, RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* set for each) unless it already runs under
+torch.distributed.run, in which case WORLD_SIZE must equal N.  Config 2: the sources are
+independent units; every rank holds a replica of the snapshot and runs its own 1024-source batch
+(weak scaling, no data-path collective).  Config 4: the same 1024 sources over a partitioned
+snapshot (strong scaling, RCCL exchange per level).  torch.distributed (gloo, CPU) carries only
+the barrier, the max/sum of scalars and the RCCL unique id.
 
 The CPU baseline is the C restatement of the reference path (oracle/, test infrastructure) timed
-on the host cores on a bounded sample of the same workload.
+on the host cores on a bounded sample of the same workload: 1 thread and all cores (the box's
+share), median of 5 runs after 1 warm-up, with the host's core count and CPU model.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,17 +45,31 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/pmc_<workload>.json,
-    written by tools/pmc_summary.py with the gfx950 FETCH_SIZE correction), or None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(p):
-        return None
+def _git_sha(path):
     try:
-        d = json.load(open(p))
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        return subprocess.run(["git", "-C", ROOT, "log", "-1", "--format=%h", "--", path], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
     except Exception:
         return None
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/pmc_<workload>.json,
+    written by tools/pmc_summary.py with the gfx950 FETCH_SIZE correction) and where it came from:
+    (bytes or None, "profiles/pmc_<workload>.json@<commit>").  Counters cannot be collected inside
+    this run (rocprofv3 --pmc needs its own pass), so the figure is the committed measurement of the
+    same kernel on the same workload, labelled as such."""
+    rel = os.path.join("profiles", f"pmc_{workload}.json")
+    p = os.path.join(ROOT, rel)
+    if not os.path.exists(p):
+        return None, None
+    try:
+        d = json.load(open(p))
+        v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None, None
+    sha = _git_sha(rel)
+    return v, f"{rel}@{sha}" if sha else rel
 
 
 def roofline(stats_list, workload):
@@ -60,59 +84,108 @@ def roofline(stats_list, workload):
     dom = max(tot, key=lambda k: tot[k]["ms"])
     t = tot[dom]
     achieved = t["bytes"] / (t["ms"] / 1e3) / 1e9 if t["ms"] > 0 else 0.0
-    traffic = pmc_traffic(dom, workload)
+    traffic, src = pmc_traffic(dom, workload)
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_from": src,
             "bytes_per_launch": t["bytes"] / max(t["launches"], 1),
             "avg_launch_ms": t["ms"] / max(t["launches"], 1), "launches": t["launches"]}, tot
 
 
+def host_info():
+    """nproc, the cores this process may use, and the lscpu model name (from /proc/cpuinfo)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "usable_cpus": usable, "cpu_model": model}
+
+
+def cpu_threads():
+    """All cores of the box's share: the GPU box exposes the whole machine to os.cpu_count() but a
+    one-GPU job owns 16 of them (OMP_NUM_THREADS is set to that share there)."""
+    env = os.environ.get("HGX_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    if env:
+        return max(1, int(env))
+    return max(1, min(16, host_info()["usable_cpus"]))
+
+
+def median_runs(run, reps=5):
+    """run() -> (units, seconds); one warm-up, then the median rate of `reps` runs."""
+    run()
+    rates = sorted(u / max(sec, 1e-9) for u, sec in (run() for _ in range(reps)))
+    return rates[len(rates) // 2], rates
+
+
+def cpu_leg(run_for_threads, unit, sample, kind="port"):
+    """The 1-thread and all-cores legs of one CPU baseline."""
+    info = host_info()
+    out = {"unit": unit, "kind": kind, "sample": sample, "repetitions": "median of 5 after 1 warm-up", **info}
+    nt = cpu_threads()
+    for tag, th in (("1t", 1), ("all", nt)):
+        med, rates = median_runs(lambda: run_for_threads(th))
+        out[f"value_{tag}"] = med
+        out[f"rates_{tag}"] = [round(r, 1) for r in rates]
+    out["value"] = out["value_all"]
+    out["cores"] = nt
+    return out
+
+
 def cpu_bfs_baseline(g, seeds, depth, budget_s):
-    """C restatement (oracle/) of HGBreadthFirstTraversal + DefaultALGenerator, OpenMP over seeds."""
+    """C restatement (oracle/) of HGBreadthFirstTraversal + DefaultALGenerator, one traversal per
+    thread, each stopped after budget_s: the edge rate of the reference path over the first budget_s
+    of each traversal (a bounded sample of the same workload)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_ctypes import OracleGraph
-    threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
     t0 = time.time()
     orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
-    log(f"cpu baseline: host snapshot built in {time.time() - t0:.1f}s; {threads} threads")
-    # one traversal per thread, each stopped after budget_s (a bounded sample of the same workload:
-    # the rate is the reference path's edge rate over the first budget_s of every traversal)
-    batch = np.asarray(seeds[:threads], np.int32)
-    tm = {}
-    _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads, time_budget_s=budget_s, timing=tm)
-    elapsed = tm["elapsed_s"]
-    trav = int(tr.sum())
+    log(f"cpu baseline: host snapshot built in {time.time() - t0:.1f}s")
+
+    def run(threads):
+        batch = np.asarray(seeds[:threads], np.int32)
+        tm = {}
+        _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads, time_budget_s=budget_s, timing=tm)
+        return int(tr.sum()), tm["elapsed_s"]
+
+    out = cpu_leg(run, "TEPS", f"config-2 sources seeds[:threads] (1 / all cores), depth {depth}, one traversal "
+                  f"per thread, each stopped after {budget_s:g}s (C restatement of HGBreadthFirstTraversal/"
+                  "DefaultALGenerator)")
     del orc
-    return {"value": trav / elapsed, "unit": "TEPS", "cores": threads, "kind": "port",
-            "sample": f"{len(batch)} of the {len(seeds)} config-2 sources, depth {depth}, one traversal per thread "
-                      f"(C restatement of HGBreadthFirstTraversal/DefaultALGenerator), each stopped after "
-                      f"{budget_s:.0f}s; {trav:.3e} hyperedges in {elapsed:.1f}s",
-            "seconds": round(elapsed, 2)}
+    return out
 
 
 def cpu_query_baseline(g, qs, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_ctypes import OracleGraph
-    threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
     orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
-    n_done, elapsed, i, step = 0, 0.0, 0, max(threads * 8, 64)
-    while elapsed < budget_s and i < len(qs["type"]):
-        sl = slice(i, i + step)
-        t = qs["type"][sl]
-        n = len(t)
-        inc_off = np.arange(n + 1, dtype=np.int64)
-        pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
-        pat = np.stack([qs["x"][sl], np.full(n, -1, np.int32), qs["y"][sl]], 1).reshape(-1)
-        t1 = time.time()
-        orc.and_query_many(t, inc_off, qs["a"][sl], pat_off, pat, np.ones(n, np.int32), nthreads=threads)
-        elapsed += time.time() - t1
-        n_done += n
-        i += step
+
+    def run(threads):
+        n_done, elapsed, i, step = 0, 0.0, 0, max(threads * 8, 64)
+        while elapsed < budget_s and i < len(qs["type"]):
+            sl = slice(i, i + step)
+            t = qs["type"][sl]
+            n = len(t)
+            inc_off = np.arange(n + 1, dtype=np.int64)
+            pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
+            pat = np.stack([qs["x"][sl], np.full(n, -1, np.int32), qs["y"][sl]], 1).reshape(-1)
+            t1 = time.time()
+            orc.and_query_many(t, inc_off, qs["a"][sl], pat_off, pat, np.ones(n, np.int32), nthreads=threads)
+            elapsed += time.time() - t1
+            n_done += n
+            i += step
+        return n_done, elapsed
+
+    out = cpu_leg(run, "queries/s", f"the config-3 queries in order until {budget_s:g}s per run (C restatement of "
+                  "AndToQuery + ZigZagIntersectionResult + OrderedLinkCondition)")
     del orc
-    return {"value": n_done / elapsed, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{n_done} of the {len(qs['type'])} config-3 queries (C restatement of AndToQuery + "
-                      f"ZigZagIntersectionResult + OrderedLinkCondition), {elapsed:.1f}s",
-            "seconds": round(elapsed, 2)}
+    return out
 
 
 def _kernel_roof(stats_list):
@@ -268,19 +341,20 @@ def run_config5(args, ctx, barrier_sync):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle_ctypes import OracleGraph, algen
-        threads = int(os.environ.get("HGX_CPU_THREADS", min(16, os.cpu_count() or 1)))
         orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
-        tm, n, tr, el = {}, 0, 0, 0.0
-        for rev in (False, True):
-            batch = g["seeds"]   # every closure of the step (bounded by the time budget)
-            _, t_ = orc.bfs_many(batch, -1, 4096, algen(T, False, True, rev, False), nthreads=threads,
-                                 time_budget_s=args.cpu_budget / 2, timing=tm)
-            tr += int(t_.sum())
-            el += tm["elapsed_s"]
-            n += len(batch)
-        out["cpu_baseline"] = {"value": tr / el, "unit": "TEPS", "cores": threads, "kind": "port",
-                               "sample": f"{n} closures (C restatement of the subsumption BFS), {el:.1f}s",
-                               "seconds": round(el, 2)}
+
+        def run(threads):
+            tm, tr, el = {}, 0, 0.0
+            for rev in (False, True):
+                _, t_ = orc.bfs_many(g["seeds"], -1, 4096, algen(T, False, True, rev, False), nthreads=threads,
+                                     time_budget_s=args.cpu_budget / 2, timing=tm)
+                tr += int(t_.sum())
+                el += tm["elapsed_s"]
+            return tr, el
+
+        out["cpu_baseline"] = cpu_leg(run, "TEPS", f"the {len(g['seeds'])} closures of each direction, every "
+                                      f"traversal stopped after {args.cpu_budget / 2:g}s (C restatement of the "
+                                      "subsumption BFS)")
         del orc
     snap.close()
     return out
@@ -309,7 +383,67 @@ def emit(line):
         data = data[os.write(_JSON_FD, data):]
 
 
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(argv):
+    """`bench.py --gpus N` outside torch.distributed.run: start N ranks of this script (one process
+    per GPU) and exit with the first failing rank's status.  Runs before anything touches a GPU.
+    Under torch.distributed.run (WORLD_SIZE set) nothing is launched, but WORLD_SIZE must equal N."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    a, _ = pre.parse_known_args(argv)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+            sys.exit(2)
+        return
+    if a.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if a.gpus == 1:
+        return
+    port = str(_free_port())
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        # rank 0 prints the JSON line on our stdout; the other ranks' stdout goes to stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in pending:   # a failed rank would leave the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    sys.exit(rc)
+
+
+def dry_run(args):
+    """CPU-side rehearsal of the launch: every rank joins the gloo group and reports; no GPU work."""
+    from hypergraphdb_amd import dist as hdist
+    ctx = hdist.init_from_env("gloo")
+    ranks = ctx.sum(1.0)
+    ctx.barrier()
+    if ctx.rank == 0:
+        emit({"dry_run": True, "n_gpus": ctx.world, "ranks_joined": int(ranks), "gpus_flag": args.gpus})
+    ctx.close()
+
+
 def main():
+    launch_ranks(sys.argv[1:])
     claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -320,21 +454,30 @@ def main():
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--no-queries", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work per metric")
+    ap.add_argument("--cpu-budget", type=float, default=2.0, help="seconds of CPU-baseline work per run")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (1B incidences) legs")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 subsumption leg")
     ap.add_argument("--c5-scale", type=float, default=1.0, help="fraction of the config-5 size")
     ap.add_argument("--c4-scale", type=float, default=1.0, help="fraction of the config-4 size")
     ap.add_argument("--c4-timeout", type=float, default=420.0,
                     help="seconds after which the config-4 legs are abandoned (the line is still printed)")
+    ap.add_argument("--dry-run", action="store_true", help="launch the ranks and join the group only (no GPU)")
     args = ap.parse_args()
+    if args.dry_run:
+        dry_run(args)
+        return
 
     from hypergraphdb_amd import dist as hdist
-    from hypergraphdb_amd._lib import device_synchronize
+    from hypergraphdb_amd._lib import device_count, device_synchronize
 
     # one process per GPU; only the barrier and scalar max/sum cross processes (gloo, CPU)
     ctx = hdist.init_from_env("gloo")
     rank, world, local = ctx.rank, ctx.world, ctx.device
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the group has {world} ranks")
+    ndev = device_count()
+    if local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} needs device {local} but {ndev} HIP device(s) are visible")
 
     def barrier_sync():
         ctx.barrier()
@@ -361,26 +504,38 @@ def main():
         res = H.bfs_batch(snap, g["seeds"], args.depth)
         if acct is None:
             acct = res.stats(accounting=True)     # TEPS numerator / |U_d| (deterministic per batch)
+            acct_visits = int(res.counts().sum())
             log(f"rank {rank}: levels |U_d|={acct['union_frontier']} traversed={acct['traversed_edges']:.3e}")
         res.close()
         log(f"rank {rank}: warmup {w} done")
     if acct is None:
         res = H.bfs_batch(snap, g["seeds"], args.depth)
         acct = res.stats(accounting=True)
+        acct_visits = int(res.counts().sum())
         res.close()
     stats = []
     barrier_sync()
     t0 = time.perf_counter()
+    readout = 0
     for _ in range(args.steps):
         res = H.bfs_batch(snap, g["seeds"], args.depth)
+        readout += int(res.counts().sum())   # the result readout: per-source per-depth counts (D2H)
         stats.append(res.stats(accounting=False))
         res.close()
     barrier_sync()
     dt = max_over_ranks(time.perf_counter() - t0)
+    assert readout == args.steps * acct_visits, "readout differs from the warm-up batch"
     edges_total = sum_over_ranks(acct["traversed_edges"] * args.steps)
     teps = edges_total / dt
     roof, per_kernel = roofline(stats, "config2")
     ms_dev = sum(s["ms_total"] for s in stats) / len(stats)
+    # step-level efficiency against the minimum-bytes model: every byte the
+    # traversal must move at least once, over the device time of the whole step
+    ach_min = acct["bytes_min"] / (ms_dev / 1e3) / 1e9 if ms_dev > 0 else 0.0
+    roof["min_bytes"] = {"model": "per level: CSR columns once (or the frontier's CSR slices) + one S/8-byte row "
+                                  "per frontier atom read and per new atom written; whole step, device time",
+                         "bytes_per_step": acct["bytes_min"], "achieved": round(ach_min, 1),
+                         "frac": round(ach_min / HBM_PEAK_GBS, 4)}
     log(f"rank {rank}: {args.steps} steps in {dt:.3f}s -> {teps:.3e} TEPS; device ms/step {ms_dev:.2f}; "
         f"dominant {roof['kernel']} {roof['achieved']} GB/s")
     snap.close()
@@ -389,7 +544,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_bfs_baseline(g, g["seeds"], args.depth, args.cpu_budget)
-        log(f"cpu baseline {cpu['value']:.3e} TEPS on {cpu['cores']} threads")
+        log(f"cpu baseline {cpu['value_1t']:.3e} TEPS on 1 thread, {cpu['value']:.3e} on {cpu['cores']} threads")
     del g
 
     # ---------------- config 3: pattern queries ----------------
@@ -430,7 +585,8 @@ def main():
                    "workload": "config3: 50M links over 10M nodes, arity 3-6, 64 types, 10K queries",
                    "roofline": {"bound": "hbm", "kernel": "hgx_pattern_match", "achieved": round(ach, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                "traffic": pmc_traffic("hgx_pattern_match", "config3"),
+                                "traffic": pmc_traffic("hgx_pattern_match", "config3")[0],
+                                "traffic_from": pmc_traffic("hgx_pattern_match", "config3")[1],
                                 "avg_launch_ms": round(mm, 4), "bytes_per_launch": bm}}
         log(f"rank {rank}: pattern {qps:.1f} q/s, match kernel {mm:.3f} ms")
         snap3.close()

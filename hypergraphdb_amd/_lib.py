@@ -25,10 +25,11 @@ HGX_NO_TYPE = -1
 HGX_UNBOUNDED = -1
 HGX_OPT_BFS_FLAGS = 1
 HGX_OPT_SEQ_BUDGET = 2
+HGX_OPT_RANKS_ORDERED = 3
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
-    "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
+    "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_device_count", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
@@ -67,12 +68,12 @@ class BfsStats(C.Structure):
                 ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64),
                 ("level_bytes", C.c_double * 64), ("level_sparse", C.c_int32 * 64),
                 ("level_rows", (C.c_int64 * 8) * 64), ("ms_exchange", C.c_double),
-                ("bytes_exchanged", C.c_double)]
+                ("bytes_exchanged", C.c_double), ("bytes_min", C.c_double)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
              "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges,
-             "ms_exchange": self.ms_exchange, "bytes_exchanged": self.bytes_exchanged}
+             "ms_exchange": self.ms_exchange, "bytes_exchanged": self.bytes_exchanged, "bytes_min": self.bytes_min}
         d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
                             "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
         n = max(self.n_levels_expanded, 0)
@@ -113,6 +114,7 @@ def lib():
         "hgx_version": ([], C.c_char_p),
         "hgx_last_error": ([], C.c_char_p),
         "hgx_device_synchronize": ([i32], C.c_int),
+        "hgx_device_count": ([C.POINTER(i32)], C.c_int),
         "hgx_graph_create": ([C.POINTER(GraphDesc), i32, C.POINTER(vp)], C.c_int),
         "hgx_graph_destroy": ([vp], None),
         "hgx_graph_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
@@ -176,6 +178,12 @@ def check(rc):
 
 def device_synchronize(device: int = 0):
     check(lib().hgx_device_synchronize(int(device)))
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    check(lib().hgx_device_count(C.byref(n)))
+    return n.value
 
 
 def ptr(a: np.ndarray):

@@ -1818,6 +1818,57 @@ __global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const u64* __r
         if (lc[j]) atomicAdd(&counts[j], (u64)lc[j]);
 }
 
+// Per-source counts of one level (the result readout of a batch): counts[w*64 + b] +=
+// |{v : fa(v), bit b of lvl[v][w]}|, reading only the rows of the level's atoms.  A wave takes 64
+// bitmap words at a time and visits the nonzero ones; the set bits of a word are spread over the
+// lanes W at a time (lane l always holds word l % W of its rows), each lane adding its row words
+// into K bit planes (a carry-save counter); the planes are folded once per lane at the end.  With
+// `own` the count covers only the atoms of that bitmap (a partition part's owned atoms).
+template <int W>
+__global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
+                                                      const u64* __restrict__ lvl, u64* __restrict__ counts) {
+    constexpr int K = 22;   // < 4M rows per lane: the grid keeps every lane far below
+    __shared__ unsigned int lc[W * 64];
+    for (int j = threadIdx.x; j < W * 64; j += 256) lc[j] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t nwords = (A + 63) / 64;
+    u64 c[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) c[k] = 0;
+    for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
+        const int64_t wi = base + lane;
+        const u64 x = wi < nwords ? (fa[wi] & (own ? own[wi] : ~0ull)) : 0ull;
+        u64 m = __ballot(x != 0ull);
+        while (m) {
+            const int k = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int64_t t0 = (base + k) * 64;
+            rows_of_word((u64)__shfl(x, k), W, 0, [&](int b, int w, int32_t) {
+                u64 carry = lvl[(t0 + b) * W + w];
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const u64 tq = c[q] & carry;
+                    c[q] ^= carry;
+                    carry = tq;
+                }
+            });
+        }
+    }
+    const int wd = lane % W;
+    for (int b = 0; b < 64; ++b) {
+        unsigned int n = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) n |= (unsigned int)((c[q] >> b) & 1ull) << q;
+        if (n) atomicAdd(&lc[wd * 64 + b], n);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < W * 64; j += 256)
+        if (lc[j]) atomicAdd(&counts[j], (u64)lc[j]);
+}
+
 // Compaction of {v : fa(v) && bit s of lvl[v]} in ascending order.  Pass 1 (write = false)
 // counts per block; pass 2 writes at the block's exclusive offset.  Each block owns the
 // contiguous atom range [blk*span, (blk+1)*span).
@@ -2020,7 +2071,7 @@ struct hgx_bfs_result {
     int32_t n_seeds = 0, n_levels = 0;
     std::vector<BfsBatch> batches;
     hgx_bfs_stats stats{};
-    bool counts_ready = false;
+    bool counts_ready = false, accounting_ready = false;
     bool typed = false;
     std::map<int32_t, int32_t> isolated;   // shards: seed index -> owned seed atom without incidence
     std::vector<int64_t> counts;   // [n_seeds * n_levels]
@@ -2675,45 +2726,99 @@ void count_level_dispatch(int W, hgx_graph* g, const u64* fa, const u64* lvl, u6
     }
 }
 
-// Fill res->counts, the TEPS numerator and the survey-model bytes (first call only).
+template <int W>
+void count_rows(hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, u64* counts) {
+    const int64_t nwords = ceil_div(std::max<int64_t>(g->A, 1), 64);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), 2048));
+    hgx_count_rows<W><<<grid, 256, 0, g->stream>>>(g->A, fa, own, lvl, counts);
+    HGX_CHECK_LAUNCH();
+}
+
+void count_rows_dispatch(int W, hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, u64* counts) {
+    switch (W) {
+        case 1: count_rows<1>(g, fa, own, lvl, counts); break;
+        case 2: count_rows<2>(g, fa, own, lvl, counts); break;
+        case 4: count_rows<4>(g, fa, own, lvl, counts); break;
+        case 8: count_rows<8>(g, fa, own, lvl, counts); break;
+        default: count_rows<16>(g, fa, own, lvl, counts); break;
+    }
+}
+
+// The result readout: res->counts (per seed, per depth) from the device rows -- one counting launch
+// per level into one device table, one D2H, one synchronisation (first call only).
 void ensure_counts(hgx_bfs_result* r) {
     if (r->counts_ready) return;
     hgx_graph* g = r->g;
     HGX_HIP(hipSetDevice(g->device));
     r->counts.assign((size_t)r->n_seeds * r->n_levels, 0);
+    size_t nslots = 0;
+    for (auto& bt : r->batches) nslots += bt.lvl.size();
+    const size_t bytes = sizeof(u64) * 1024 * std::max<size_t>(nslots, 1);
+    u64* dc = (u64*)g->alloc(bytes);
+    HGX_HIP(hipMemsetAsync(dc, 0, bytes, g->stream));
+    const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;
+    size_t k = 0;
+    for (auto& bt : r->batches)
+        for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) count_rows_dispatch(bt.W, g, bt.fa[d], own, bt.lvl[d], dc + k * 1024);
+    std::vector<u64> hc(1024 * std::max<size_t>(nslots, 1));
+    HGX_HIP(hipMemcpyAsync(hc.data(), dc, bytes, hipMemcpyDeviceToHost, g->stream));
+    HGX_HIP(hipStreamSynchronize(g->stream));
+    g->release(dc, bytes);
+    k = 0;
+    for (auto& bt : r->batches)
+        for (size_t d = 0; d < bt.lvl.size(); ++d, ++k)
+            for (int s = 0; s < bt.S; ++s) r->counts[(size_t)(bt.seed0 + s) * r->n_levels + d] = (int64_t)hc[k * 1024 + s];
+    for (auto& kv : r->isolated) r->counts[(size_t)kv.first * r->n_levels] += 1;
+    r->counts_ready = true;
+}
+
+// The TEPS numerator, the survey-model bytes, |U_d| and the minimum-bytes model (first call only;
+// reads every level and scans the links once per level -- not part of a timed step).
+void ensure_accounting(hgx_bfs_result* r) {
+    if (r->accounting_ready) return;
+    ensure_counts(r);
+    hgx_graph* g = r->g;
+    HGX_HIP(hipSetDevice(g->device));
     double trav_total = 0;
     u64* dc = (u64*)g->alloc(sizeof(u64) * (1024 + 1));
     std::vector<u64> hc(1025);
+    const double typed = r->typed ? 1.0 : 0.0;
+    const double dense_min = 8.0 * (g->A + 1) + 4.0 * g->I + 8.0 * (g->M + 1) + 4.0 * g->P;
     for (auto& bt : r->batches) {
         int nl = (int)bt.lvl.size();
+        const double mask = (double)((bt.S + 7) / 8);
+        std::vector<double> U(nl + 1, 0.0);
         for (int d = 0; d < nl; ++d) {
             HGX_HIP(hipMemsetAsync(dc, 0, sizeof(u64) * 1025, g->stream));
             count_level_dispatch(bt.W, g, bt.fa[d], bt.lvl[d], dc, dc + 1024);
             HGX_HIP(hipMemcpyAsync(hc.data(), dc, sizeof(u64) * 1025, hipMemcpyDeviceToHost, g->stream));
             HGX_HIP(hipStreamSynchronize(g->stream));
-            for (int s = 0; s < bt.S; ++s) r->counts[(size_t)(bt.seed0 + s) * r->n_levels + d] = (int64_t)hc[s];
+            HGX_HIP(hipMemsetAsync(dc, 0, sizeof(u64) * 4, g->stream));
+            hgx_level_survey<<<grid_for(std::max(g->A, g->M), 256, 8192), 256, 0, g->stream>>>(
+                g->A, g->M, bt.fa[d], g->tgt_off, g->tgt_idx, dc);
+            HGX_CHECK_LAUNCH();
+            u64 sv[3];
+            HGX_HIP(hipMemcpyAsync(sv, dc, sizeof(sv), hipMemcpyDeviceToHost, g->stream));
+            HGX_HIP(hipStreamSynchronize(g->stream));
+            U[d] = (double)sv[0];
             if (d < bt.n_expanded) {
                 trav_total += (double)hc[1024];
-                HGX_HIP(hipMemsetAsync(dc, 0, sizeof(u64) * 4, g->stream));
-                hgx_level_survey<<<grid_for(std::max(g->A, g->M), 256, 8192), 256, 0, g->stream>>>(
-                    g->A, g->M, bt.fa[d], g->tgt_off, g->tgt_idx, dc);
-                HGX_CHECK_LAUNCH();
-                u64 sv[3];
-                HGX_HIP(hipMemcpyAsync(sv, dc, sizeof(sv), hipMemcpyDeviceToHost, g->stream));
-                HGX_HIP(hipStreamSynchronize(g->stream));
-                const double U = (double)sv[0], sdeg = (double)sv[1], Pd = (double)sv[2];
-                const double typed = r->typed ? 1.0 : 0.0;
-                const double mask = (double)((bt.S + 7) / 8);
-                r->stats.bytes_survey += 16.0 * U + 4.0 * sdeg + (16.0 + 4.0 * typed) * sdeg + 4.0 * Pd +
-                                         mask * (U + 2.0 * Pd);
+                const double sdeg = (double)sv[1], Pd = (double)sv[2];
+                r->stats.bytes_survey += 16.0 * U[d] + 4.0 * sdeg + (16.0 + 4.0 * typed) * sdeg + 4.0 * Pd +
+                                         mask * (U[d] + 2.0 * Pd);
                 if (d < 64) r->stats.union_frontier[d] += (int64_t)sv[0];
+                // minimum bytes of the level: the CSR slices of the frontier (or every column once,
+                // whichever is less), one S/8-byte row per frontier atom read and per new atom written
+                const double sparse_min = 16.0 * U[d] + 4.0 * sdeg + (16.0 + 4.0 * typed) * sdeg + 4.0 * Pd;
+                r->stats.bytes_min += std::min(dense_min, sparse_min) + mask * U[d];
             }
         }
+        for (int d = 1; d < nl; ++d)
+            if (d <= bt.n_expanded) r->stats.bytes_min += mask * U[d];   // rows of the new atoms written
     }
     g->release(dc, sizeof(u64) * 1025);
-    for (auto& kv : r->isolated) r->counts[(size_t)kv.first * r->n_levels] += 1;
     r->stats.traversed_edges = trav_total;
-    r->counts_ready = true;
+    r->accounting_ready = true;
 }
 
 void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
@@ -3017,7 +3122,7 @@ int hgx_bfs_result_stats(hgx_bfs_result* r, int32_t with_accounting, hgx_bfs_sta
     HGX_API_BEGIN
     if (!r || !st) fail(HGX_E_INVALID, "hgx_bfs_result_stats: bad argument");
     std::lock_guard<std::mutex> lk(r->g->mu);
-    if (with_accounting) ensure_counts(r);
+    if (with_accounting) ensure_accounting(r);
     *st = r->stats;
     HGX_API_END
 }

@@ -8,9 +8,9 @@
 // changes (C/event; store side C/HGStore.java:100-170) by rebuilding the device index from the merged rows.
 //
 // Layout (little-endian), every section 64-byte aligned:
-//   header  64 B  magic "HGXCSR1\0", u32 version (1), u32 flags (bit 0 link_type, bit 1 handles),
+//   header  64 B  magic "HGXCSR1\0", u32 version (2), u32 flags (bit 0 link_type, bit 1 handles),
 //                 i64 num_atoms, i64 num_links, i64 num_pins, u32 handle_bytes, u32 reserved,
-//                 u64 checksum of the sections
+//                 u64 checksum of the header (checksum field zero) and the sections
 //   link_atom i32[M] | tgt_off i64[M+1] | tgt_idx i32[P] | link_type i32[M] (flag 0) |
 //   handles u8[A * handle_bytes] (flag 1: the persistent handle of every rank)
 #include <fcntl.h>
@@ -30,7 +30,7 @@ using namespace hgx;
 namespace {
 
 constexpr char kMagic[8] = {'H', 'G', 'X', 'C', 'S', 'R', '1', '\0'};
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;   // 2: the checksum also covers the header
 
 struct Header {
     char magic[8];
@@ -61,6 +61,16 @@ uint64_t mix(uint64_t h, const void* p, size_t n) {
         h = (h << 31) | (h >> 33);
     }
     return h;
+}
+
+// Checksum of a file: the header with its checksum field zeroed, then every section.  A corrupted
+// count or flag in the header fails verification even in a file without a handle table.
+uint64_t file_checksum(const Header& h, const void* const ptrs[5], const size_t lens[5]) {
+    Header z = h;
+    z.checksum = 0;
+    uint64_t c = mix(0x243F6A8885A308D3ull, &z, sizeof(z));
+    for (int k = 0; k < 5; ++k) c = mix(c, ptrs[k], lens[k]);
+    return c;
 }
 
 struct Sections {
@@ -116,9 +126,9 @@ std::unique_ptr<Mapped> map_file(const char* path, bool verify) {
     m->s = layout(h.num_atoms, h.num_links, h.num_pins, h.flags, h.handle_bytes);
     if (m->s.total > m->size) fail(HGX_E_INVALID, "hgcsr: truncated file");
     if (verify) {
-        uint64_t c = 0x243F6A8885A308D3ull;
-        for (int k = 0; k < 5; ++k) c = mix(c, m->at(k), m->s.len[k]);
-        if (c != h.checksum) fail(HGX_E_INVALID, "hgcsr: checksum mismatch");
+        const void* ptrs[5];
+        for (int k = 0; k < 5; ++k) ptrs[k] = m->at(k);
+        if (file_checksum(h, ptrs, m->s.len) != h.checksum) fail(HGX_E_INVALID, "hgcsr: checksum mismatch");
         const int64_t* off = (const int64_t*)m->at(1);
         if (off[0] != 0 || off[h.num_links] != h.num_pins) fail(HGX_E_INVALID, "hgcsr: inconsistent offsets");
     }
@@ -178,9 +188,7 @@ int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t*
         off = zero_off.data();
     }
     const void* ptrs[5] = {d->link_atom, off, d->tgt_idx, d->link_type, handles};
-    uint64_t c = 0x243F6A8885A308D3ull;
-    for (int k = 0; k < 5; ++k) c = mix(c, ptrs[k], s.len[k]);
-    h.checksum = c;
+    h.checksum = file_checksum(h, ptrs, s.len);
     const std::string tmp = std::string(path) + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) fail(HGX_E_DEVICE, std::string("hgx_snapshot_write: cannot create ") + tmp);
@@ -197,6 +205,8 @@ int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t*
         at = s.off[k] + s.len[k];
     }
     write_all(f, zeros, s.total - at);
+    // durable before it becomes visible under the final name
+    if (std::fflush(f) != 0 || fsync(fileno(f)) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: fsync failed");
     if (std::fclose(f) != 0) {
         closer.f = nullptr;
         fail(HGX_E_DEVICE, "hgx_snapshot_write: close failed");
@@ -296,12 +306,22 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
         ntg.insert(ntg.end(), add_tgt_idx + add_tgt_off[i], add_tgt_idx + add_tgt_off[i + 1]);
         noff.push_back((int64_t)ntg.size());
     };
+    for (size_t i = 1; i < add_order.size(); ++i)
+        if (add_link_atom[add_order[i]] == add_link_atom[add_order[i - 1]])
+            fail(HGX_E_INVALID, "hgx_graph_update: a link is added twice in one batch");
+    // Removals apply before additions: removing and adding the same link atom in one batch is a
+    // replace (HyperGraph.replace keeps the handle and rewrites type + targets, C/HyperGraph.java:
+    // 2100-2141, announced as HGAtomReplacedEvent); the new row takes the old row's rank slot.
     size_t ai = 0;
     for (int64_t r = 0; r < (int64_t)la.size(); ++r) {
         while (ai < add_order.size() && add_link_atom[add_order[ai]] < la[r]) push_new(add_order[ai++]);
-        if (ai < add_order.size() && add_link_atom[add_order[ai]] == la[r])
-            fail(HGX_E_INVALID, "hgx_graph_update: an added link already exists");
-        if (!std::binary_search(rm.begin(), rm.end(), la[r])) push_old(r);
+        const bool removed = std::binary_search(rm.begin(), rm.end(), la[r]);
+        if (ai < add_order.size() && add_link_atom[add_order[ai]] == la[r]) {
+            if (!removed) fail(HGX_E_INVALID, "hgx_graph_update: an added link already exists");
+            push_new(add_order[ai++]);   // replace
+            continue;
+        }
+        if (!removed) push_old(r);
     }
     while (ai < add_order.size()) push_new(add_order[ai++]);
     hgx_graph_desc d{num_atoms, (int64_t)nla.size(), nla.data(), noff.data(), ntg.data(), nty.data()};
@@ -325,6 +345,7 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     std::swap(g->n_chunks, fresh->n_chunks);
     std::swap(g->heavy_atom, fresh->heavy_atom);
     std::swap(g->chunks, fresh->chunks);
+    if (num_atoms > fresh->A) g->ranks_ordered = false;   // appended ranks (fresh->A = the old count)
     g->max_arity = g->max_deg = -1;
     g->inc_off_host.clear();
     if (g->zacc) (void)hipFree(g->zacc);

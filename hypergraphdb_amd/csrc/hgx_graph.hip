@@ -229,6 +229,15 @@ int hgx_device_synchronize(int32_t device) {
     HGX_API_END
 }
 
+int hgx_device_count(int32_t* n) {
+    HGX_API_BEGIN
+    if (!n) fail(HGX_E_INVALID, "hgx_device_count: null argument");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;   // no GPU / no driver: zero devices
+    *n = (int32_t)c;
+    HGX_API_END
+}
+
 int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     HGX_API_BEGIN
     if (!d || !out) fail(HGX_E_INVALID, "hgx_graph_create: null argument");
@@ -415,8 +424,13 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     HGX_API_BEGIN
     if (!g) fail(HGX_E_INVALID, "null graph");
     std::lock_guard<std::mutex> lk(g->mu);
-    if (option == HGX_OPT_BFS_FLAGS) g->bfs_flags = (int32_t)value;
-    else if (option == HGX_OPT_SEQ_BUDGET) {
+    if (option == HGX_OPT_BFS_FLAGS) {
+        // bits 16 and up are the engine's per-level internal flags (kAllRows, ...): never settable
+        if (value < 0 || value > 0xFFFF) fail(HGX_E_INVALID, "hgx_set_option: BFS flags outside bits 0-15");
+        g->bfs_flags = (int32_t)value;
+    } else if (option == HGX_OPT_RANKS_ORDERED) {
+        g->ranks_ordered = value != 0;
+    } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;
     } else fail(HGX_E_INVALID, "hgx_set_option: unknown option");

@@ -125,6 +125,10 @@ struct hgx_graph {
     int32_t bfs_flags = 0x3BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
     int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
+    // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
+    // that extends the rank space (appended ranks need not sort after the existing handles); the
+    // order-exact traversal refuses to run until the caller re-asserts it.
+    bool ranks_ordered = true;
     // Frontier-push accumulator rows (A x W words), all zero between levels: each push level ORs
     // into it and its finalise re-zeroes exactly the rows it consumed (no per-level clear).
     std::vector<int64_t> inc_off_host;   // host copy of inc_off (pattern planning), made on first use

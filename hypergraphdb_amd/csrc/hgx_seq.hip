@@ -267,6 +267,12 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     if (!g || !out || n_seeds < 0 || (n_seeds > 0 && !seeds)) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad argument");
     *out = nullptr;
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: not available on a partition shard");
+    // FIFO order and the discovering link follow the incidence order, i.e. rank order; after an
+    // update appended ranks whose handles may sort before existing ones that is not handle order
+    // (ADVICE r01), and no re-sort of the output can repair it.
+    if (!g->ranks_ordered)
+        fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: ranks were appended by hgx_graph_update and may not follow "
+                                "handle order (re-assert with HGX_OPT_RANKS_ORDERED or rebuild the snapshot)");
     hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
     for (int32_t i = 0; i < n_seeds; ++i)
         if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_sequence: seed out of range");

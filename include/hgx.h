@@ -23,7 +23,9 @@
  * Identity: every atom (node or link) is an int32 id = its rank in persistent-handle
  * byte order (C/handle/UUID.java:364-376; IntPersistentHandle via C/storage/BAUtils.java:55-80).
  * Rank order preserves every sorted list of the reference, so GPU result order is the
- * reference's result order.  The caller keeps the rank -> handle table.
+ * reference's result order -- for a snapshot whose ranks were assigned in handle order (see
+ * HGX_OPT_RANKS_ORDERED for snapshots grown by hgx_graph_update).  The caller keeps the
+ * rank -> handle table.
  */
 #ifndef HGX_H
 #define HGX_H
@@ -122,12 +124,18 @@ typedef struct hgx_bfs_stats {
      * apply, frontier count) and the ghost-row bytes this part sent */
     double  ms_exchange;
     double  bytes_exchanged;
+    /* minimum-bytes model of the whole batch (with accounting): per expanded level, the CSR slices
+     * of the frontier atoms or every CSR column once (whichever is less) + one S/8-byte row per
+     * frontier atom read + one per new atom written */
+    double  bytes_min;
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
 const char *hgx_last_error(void);
 /* hipDeviceSynchronize on one device (benchmark brackets; no graph needed). */
 int hgx_device_synchronize(int32_t device);
+/* Number of visible HIP devices (0 on a host without GPUs; never fails for that reason). */
+int hgx_device_count(int32_t *n);
 
 /* device: HIP device ordinal to place the snapshot on. */
 int  hgx_graph_create(const hgx_graph_desc *desc, int32_t device, hgx_graph **out);
@@ -164,6 +172,15 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
  * (seeds are processed in chunks that fit; default 16 GiB). */
 #define HGX_OPT_SEQ_BUDGET 2
+/* HGX_OPT_RANKS_ORDERED: 1 = the rank order equals the persistent-handle order (the default for a
+ * fresh snapshot).  An hgx_graph_update that extends the rank space sets it to 0: appended ranks
+ * sort after every existing rank, which is handle order only if the new handles sort after the old
+ * ones (true for IntHandleFactory's sequential handles, C/handle/IntHandleFactory.java:32-49; not
+ * for random UUIDs).  Result SETS stay correct (the shim re-sorts ids >= the old count by handle),
+ * but the FIFO order of hgx_bfs_sequence and its discovering links follow the incidence order and
+ * cannot be repaired afterwards, so hgx_bfs_sequence returns HGX_E_UNSUPPORTED until the caller
+ * re-asserts 1 (or re-exports the snapshot). */
+#define HGX_OPT_RANKS_ORDERED 3
 int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
 
 /* ---- the snapshot on disk (.hgcsr) and batched store updates ------------------------------------
@@ -210,7 +227,8 @@ int  hgx_bfs_batch(hgx_graph *g, const int32_t *seeds, int32_t n_seeds, int32_t 
                    const hgx_algen_opts *opts, hgx_bfs_result **out);
 /* n_levels = 1 + the largest distance reached by any seed. */
 int  hgx_bfs_result_info(const hgx_bfs_result *r, int32_t *n_seeds, int32_t *n_levels);
-/* counts[i * n_levels + d] = |V_d| of seed i. */
+/* counts[i * n_levels + d] = |V_d| of seed i: the batch's result readout (one counting launch per
+ * level over the device rows, one D2H; cheap enough to sit inside a timed step). */
 int  hgx_bfs_result_counts(hgx_bfs_result *r, int64_t *counts);
 /* V_d of seed i, ascending atom ids; *n_out = |V_d| even when > cap. */
 int  hgx_bfs_result_visited(hgx_bfs_result *r, int32_t seed_index, int32_t depth,

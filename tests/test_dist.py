@@ -62,3 +62,22 @@ def test_two_rank_gloo_sharding(tmp_path):
     from hypergraphdb_amd import synth
     g = synth.config2(scale=0.0005, n_sources=32)
     assert res[0]["seeds"] == g["seeds"].tolist()
+
+
+def test_bench_launches_its_ranks():
+    """`bench.py --gpus N` starts N ranks itself (one process per GPU) when not run under
+    torch.distributed.run; --dry-run joins the group without touching a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["ranks_joined"] == 2
+    # under a launcher, a world size that disagrees with --gpus is an error, not a silent 1-GPU run
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       env=dict(env, WORLD_SIZE="3", RANK="0"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr

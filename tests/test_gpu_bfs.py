@@ -225,7 +225,8 @@ def test_depth_of_and_errors():
         res.visited(5, 0)
 
 
-@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6, 0x3BE, 0x236, 0xBBE])
+@pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6, 0x3BE, 0x236, 0xBBE,
+                                   0x13BE, 0x23BE, 0x43BE, 0x73BE, 0x83BE, 0x83BA, 0xF3BA, 0x0BBE])
 def test_engine_option_matrix(flags):
     """Every work-avoidance option (early exits, full-visited skipping, frontier-driven sparse
     levels) returns the same per-depth sets; power-law hubs + random edge cases + ordered modes."""
@@ -241,6 +242,19 @@ def test_engine_option_matrix(flags):
         snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
         seeds = rng.integers(0, g["num_atoms"], 1024 if i == 2 else 300).astype(np.int32)   # W = 16 and W < 16
         check_batch(g, seeds, maxd, mode, lt, snap, orc)
+
+
+def test_engine_flags_reject_internal_bits():
+    """Bits 16+ are the engine's per-level internal flags (kAllRows): hgx_set_option refuses them
+    (-1 as 'everything on' used to switch the pull to the all-rows path)."""
+    from hypergraphdb_amd import HGXError, _lib
+    g = K.random_graph(np.random.default_rng(3), 50, 80)
+    snap = snapshot(g)
+    for bad in (-1, 1 << 16, 0x183BE):
+        with pytest.raises(HGXError, match="bits 0-15"):
+            snap.set_option(_lib.HGX_OPT_BFS_FLAGS, bad)
+    snap.set_option(_lib.HGX_OPT_BFS_FLAGS, 0xFFFF)
+    check_batch(g, np.arange(40, dtype=np.int32), None, K.ALGEN_MODES[0], -1, snap, oracle(g))
 
 
 @pytest.mark.parametrize("n_seeds,lt", [(1024, -1), (300, -1), (1024, 1)])

@@ -138,3 +138,48 @@ def test_update_errors():
     snap.update(remove=[la])                                 # the graph is unchanged by the failures
     assert snap.M == len(g["link_atom"]) - 1
     snap.close()
+
+
+def test_update_replace_rewrites_targets_and_type():
+    """HyperGraph.replace keeps the handle and rewrites type + targets (C/HyperGraph.java:2100-2141,
+    HGAtomReplacedEvent): the shim sends remove + add of the same link atom in one batch.  The new
+    row takes the old rank slot; BFS, incidence and pattern results equal a rebuilt snapshot."""
+    from hypergraphdb_amd import HyperGraphSnapshot
+    rng = np.random.default_rng(95)
+    g = K.random_graph(rng, 200, 600, max_arity=6)
+    snap = HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    rep = [int(x) for x in rng.choice(g["link_atom"], 40, replace=False)]
+    add = {a: (int(rng.integers(0, 3)), [int(x) for x in rng.integers(0, g["num_atoms"], int(rng.integers(0, 7)))
+                                         if x != a]) for a in rep}
+    g2 = merged(g, add, rep, g["num_atoms"])
+    snap.update(add=add, remove=rep)
+    assert snap.M == len(g["link_atom"])
+    for k in ("link_atom", "tgt_off", "tgt_idx", "link_type"):
+        np.testing.assert_array_equal(getattr(snap, k), g2[k], err_msg=k)
+    check_all(snap, g2, rng)
+    snap.close()
+
+
+def test_sequence_refused_after_appended_ranks():
+    """Appended ranks need not follow handle order, and the FIFO sequence cannot be repaired by a
+    re-sort: hgx_bfs_sequence is refused until the caller re-asserts the order."""
+    from hypergraphdb_amd import HGXError, HyperGraphSnapshot, bfs_sequence, _lib
+    from test_gpu_seq import check_seq
+    rng = np.random.default_rng(96)
+    g = K.random_graph(rng, 120, 300, max_arity=5)
+    snap = HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    A0 = g["num_atoms"]
+    add = {A0 + 1: (0, [3, 7, 11]), A0 + 4: (1, [A0, 2])}
+    snap.update(add=add, num_atoms=A0 + 6)
+    with pytest.raises(HGXError, match="appended") as e:
+        bfs_sequence(snap, [3], 3)
+    assert e.value.code == _lib.HGX_E_UNSUPPORTED
+    # IntHandleFactory handles are sequential: the appended ranks are in handle order -> re-assert
+    snap.set_option(_lib.HGX_OPT_RANKS_ORDERED, 1)
+    g2 = merged(g, add, [], A0 + 6)
+    for mode in ((True, True, False, False), (False, True, False, False)):
+        check_seq(g2, np.array([3, 7, A0], np.int32), None, mode, snap=snap)
+    # an update that does not grow the rank space keeps the order
+    snap.update(remove=[A0 + 1])
+    assert bfs_sequence(snap, [3], 2).n_seeds == 1
+    snap.close()

@@ -37,7 +37,7 @@ def test_header_layout(tmp_path):
     _write(p, g)
     raw = open(p, "rb").read(64)
     magic, ver, flags, A, M, P, hb, _res, _ck = struct.unpack("<8sIIqqqIIQ", raw[:56])
-    assert magic == b"HGXCSR1\0" and ver == 1 and flags == 1 and hb == 0
+    assert magic == b"HGXCSR1\0" and ver == 2 and flags == 1 and hb == 0
     assert (A, M, P) == (g["num_atoms"], len(g["link_atom"]), int(g["tgt_off"][-1]))
     # the link_atom section starts right after the header
     la = np.frombuffer(open(p, "rb").read()[64:64 + 4 * M], np.int32)
@@ -74,6 +74,18 @@ def test_corruption_is_detected(tmp_path):
     with pytest.raises(HGXError, match="checksum") as e:
         read_snapshot(q)
     assert e.value.code == _lib.HGX_E_INVALID
+    # a corrupted header count (num_atoms + 5: extra isolated atoms) in a file without a handle table
+    # is caught by the checksum, which covers the header
+    bad = bytearray(data)
+    bad[16:24] = struct.pack("<q", g["num_atoms"] + 5)
+    open(q, "wb").write(bytes(bad))
+    with pytest.raises(HGXError, match="checksum"):
+        read_snapshot(q)
+    bad = bytearray(data)
+    bad[44:48] = struct.pack("<I", 1)   # the reserved word
+    open(q, "wb").write(bytes(bad))
+    with pytest.raises(HGXError, match="checksum"):
+        read_snapshot(q)
     # bad magic, wrong version, truncation, missing file
     bad = bytearray(data)
     bad[0:1] = b"X"

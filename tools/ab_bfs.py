@@ -4,7 +4,8 @@
   python tools/ab_bfs.py --flags 0,2,4,6,7 --rounds 3 [--scale 1.0]
 
 For every flag setting (HGX_OPT_BFS_FLAGS) the same config-2 batch runs `rounds` times, interleaved;
-prints per-level device ms per kernel and checks that every variant yields identical level sizes.
+prints per-level device ms per kernel and checks that every variant yields identical results: the
+per-source per-depth counts of every seed and the visited sets of a sample of seeds.
 """
 import argparse
 import json
@@ -31,12 +32,20 @@ def main():
     snap.set_timing(True)
     flags = [int(f, 0) for f in args.flags.split(",")]
     res = {f: [] for f in flags}
-    ref_new = None
+    ref_new = ref_counts = ref_sets = None
+    sample = list(range(0, args.sources, max(1, args.sources // 8)))
     for r in range(args.rounds + 1):
         for f in flags:
             snap.set_option(_lib.HGX_OPT_BFS_FLAGS, f)
             out = H.bfs_batch(snap, g["seeds"], args.depth)
             st = out.stats(accounting=False)
+            if r == 0:   # identical results: counts of every seed, sets of the sampled seeds
+                counts = out.counts()
+                sets = [out.visited(i, d).tobytes() for i in sample for d in range(counts.shape[1])]
+                if ref_counts is None:
+                    ref_counts, ref_sets = counts, sets
+                assert counts.shape == ref_counts.shape and (counts == ref_counts).all(), (f, "per-source counts")
+                assert sets == ref_sets, (f, "visited sets")
             out.close()
             if ref_new is None:
                 ref_new = st["level_new"]
