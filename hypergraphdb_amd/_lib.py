@@ -26,6 +26,7 @@ HGX_UNBOUNDED = -1
 HGX_OPT_BFS_FLAGS = 1
 HGX_OPT_SEQ_BUDGET = 2
 HGX_OPT_RANKS_ORDERED = 3
+HGX_OPT_PART_SERIAL = 4
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
@@ -35,8 +36,9 @@ EXPORTED = (
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
     "hgx_seq_result_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_pattern_batch_ext", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
-    "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_free", "hgx_shard_graph_create",
-    "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
+    "hgx_partition_plan", "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_exchange_tables",
+    "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
+    "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
     "hgx_graph_update",
 )
@@ -68,7 +70,9 @@ class BfsStats(C.Structure):
                 ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64),
                 ("level_bytes", C.c_double * 64), ("level_sparse", C.c_int32 * 64),
                 ("level_rows", (C.c_int64 * 8) * 64), ("ms_exchange", C.c_double),
-                ("bytes_exchanged", C.c_double), ("bytes_min", C.c_double)]
+                ("bytes_exchanged", C.c_double), ("level_xbytes", C.c_double * 64),
+                ("level_xpair_max", C.c_double * 64), ("level_xms", C.c_double * 64),
+                ("xwords_nonzero", C.c_double), ("xwords_total", C.c_double), ("bytes_min", C.c_double)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
@@ -83,6 +87,10 @@ class BfsStats(C.Structure):
         d["level_bytes"] = [float(x) for x in self.level_bytes[:n]]
         d["level_sparse"] = [int(x) for x in self.level_sparse[:n]]
         d["level_rows"] = [[int(v) for v in self.level_rows[i]] for i in range(n)]
+        d["level_xbytes"] = [float(x) for x in self.level_xbytes[:n]]
+        d["level_xpair_max"] = [float(x) for x in self.level_xpair_max[:n]]
+        d["level_xms"] = [round(float(x), 4) for x in self.level_xms[:n]]
+        d["xwords_nonzero"], d["xwords_total"] = self.xwords_nonzero, self.xwords_total
         return d
 
 
@@ -142,7 +150,10 @@ def lib():
         "hgx_query_result_ids": ([vp, vp], C.c_int),
         "hgx_query_result_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         "hgx_query_result_free": ([vp], None),
-        "hgx_shard_build": ([C.POINTER(GraphDesc), i32, i32, C.POINTER(vp)], C.c_int),
+        "hgx_partition_plan": ([C.POINTER(GraphDesc), i32, vp], C.c_int),
+        "hgx_shard_build": ([C.POINTER(GraphDesc), i32, i32, vp, C.POINTER(vp)], C.c_int),
+        "hgx_shard_exchange_tables": ([vp, vp, vp, vp, vp, vp, vp], C.c_int),
+        "hgx_comm_host_create": ([i32, i32, vp, vp, vp, C.POINTER(vp)], C.c_int),
         "hgx_shard_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
         "hgx_shard_export": ([vp, vp, vp, vp, vp, vp, vp], C.c_int),
         "hgx_shard_free": ([vp], None),

@@ -1818,46 +1818,76 @@ __global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const u64* __r
         if (lc[j]) atomicAdd(&counts[j], (u64)lc[j]);
 }
 
+// Position of the n-th set bit (n < popcount(x)) of x: binary search over popcounts (6 steps).
+__device__ __forceinline__ int nth_set_bit(u64 x, int n) {
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half > 0; half >>= 1) {
+        const u64 lo = x & ((1ull << half) - 1ull);
+        const int c = __popcll(lo);
+        if (n >= c) {
+            n -= c;
+            x >>= half;
+            pos += half;
+        } else {
+            x = lo;
+        }
+    }
+    return pos;
+}
+
 // Per-source counts of one level (the result readout of a batch): counts[w*64 + b] +=
 // |{v : fa(v), bit b of lvl[v][w]}|, reading only the rows of the level's atoms.  A wave takes 64
 // bitmap words at a time and visits the nonzero ones; the set bits of a word are spread over the
-// lanes W at a time (lane l always holds word l % W of its rows), each lane adding its row words
-// into K bit planes (a carry-save counter); the planes are folded once per lane at the end.  With
-// `own` the count covers only the atoms of that bitmap (a partition part's owned atoms).
+// lanes W at a time (lane l always holds word l % W of its rows), U rows per lane in flight at once
+// (the loads are independent), each lane adding its row words into K bit planes (a carry-save
+// counter); the planes are folded once per lane at the end.  With `own` the count covers only the
+// atoms of that bitmap (a partition part's owned atoms).
 template <int W>
 __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
                                                       const u64* __restrict__ lvl, u64* __restrict__ counts) {
     constexpr int K = 22;   // < 4M rows per lane: the grid keeps every lane far below
+    constexpr int R = 64 / W, U = 4;
     __shared__ unsigned int lc[W * 64];
     for (int j = threadIdx.x; j < W * 64; j += 256) lc[j] = 0;
     __syncthreads();
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, k = lane / W, wd = lane % W;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t nwords = (A + 63) / 64;
     u64 c[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = 0;
+    for (int q = 0; q < K; ++q) c[q] = 0;
     for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
         const int64_t wi = base + lane;
         const u64 x = wi < nwords ? (fa[wi] & (own ? own[wi] : ~0ull)) : 0ull;
         u64 m = __ballot(x != 0ull);
         while (m) {
-            const int k = __ffsll((long long)m) - 1;
+            const int kw = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            const int64_t t0 = (base + k) * 64;
-            rows_of_word((u64)__shfl(x, k), W, 0, [&](int b, int w, int32_t) {
-                u64 carry = lvl[(t0 + b) * W + w];
+            const u64 xw = (u64)__shfl(x, kw);
+            const int64_t t0 = (base + kw) * 64;
+            const int n = __popcll(xw);
+            for (int r0 = 0; r0 < n; r0 += R * U) {   // wave-uniform
+                u64 v[U];
 #pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const u64 tq = c[q] & carry;
-                    c[q] ^= carry;
-                    carry = tq;
+                for (int u = 0; u < U; ++u) {
+                    const int j = r0 + u * R + k;
+                    v[u] = j < n ? lvl[(t0 + nth_set_bit(xw, j)) * W + wd] : 0ull;
                 }
-            });
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    u64 carry = v[u];
+#pragma unroll
+                    for (int q = 0; q < K; ++q) {
+                        const u64 tq = c[q] & carry;
+                        c[q] ^= carry;
+                        carry = tq;
+                    }
+                }
+            }
         }
     }
-    const int wd = lane % W;
     for (int b = 0; b < 64; ++b) {
         unsigned int n = 0;
 #pragma unroll
@@ -1873,7 +1903,8 @@ __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __re
 // counts per block; pass 2 writes at the block's exclusive offset.  Each block owns the
 // contiguous atom range [blk*span, (blk+1)*span).
 __global__ void __launch_bounds__(256) hgx_extract(int64_t A, int64_t span, int W, int s,
-                                                   const u64* __restrict__ fa, const u64* __restrict__ lvl,
+                                                   const u64* __restrict__ fa, const u64* __restrict__ own,
+                                                   const u64* __restrict__ lvl,
                                                    const int64_t* __restrict__ blk_off, int64_t* __restrict__ blk_cnt,
                                                    int32_t* __restrict__ out, int64_t cap, bool write) {
     __shared__ int64_t wave_tot[4];
@@ -1884,7 +1915,7 @@ __global__ void __launch_bounds__(256) hgx_extract(int64_t A, int64_t span, int 
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t base = lo; base < hi; base += 256) {
         int64_t v = base + threadIdx.x;
-        bool hit = v < hi && bit(fa, v) && ((lvl[v * W + (s >> 6)] >> (s & 63)) & 1ull);
+        bool hit = v < hi && bit(fa, v) && (!own || bit(own, v)) && ((lvl[v * W + (s >> 6)] >> (s & 63)) & 1ull);
         u64 m = __ballot(hit);
         int before = __popcll(m & ((1ull << lane) - 1ull));
         if (lane == 0) wave_tot[wid] = __popcll(m);
@@ -1939,108 +1970,175 @@ __global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Partitioned BFS: per-level exchange of ghost rows.  After the local
-// expansion, the lvl_next row of a ghost holds the bits this shard discovered for an atom owned
-// elsewhere (ghost vis = bits already sent, so only news travel).  hgx_ghost_pack moves those rows
-// into per-owner send segments and clears the ghost frontier bits; the owner ORs the received rows
-// in with hgx_ghost_apply (new = row & ~vis), one launch per source segment so every atom appears
-// at most once per launch.
-// Record = (W + 1) u64: [global atom id, row words].
+// Partitioned BFS (vertex cut): per-level exchange of S-bit rows.
+// After the local expansion a part holds, for every local atom with a frontier bit, the news its
+// own links produced (lvl_next; vis already ORed).  For a ghost that is a PARTIAL row:
+//   reduce    hgx_xr_pack ships ghost rows to their owners; hgx_xr_apply (one launch per source
+//             part, an atom appears at most once per source) ORs them in: new = row & ~vis;
+//   broadcast hgx_xb_pack ships every owned atom's final row to its other holders; hgx_xb_apply
+//             overwrites the holder's row (final is a superset of the partial) and ORs vis.
+// Record = [local id on the receiver, spare, W row words]: 16-byte aligned, one lane per record.
 // ---------------------------------------------------------------------------------------------
+constexpr int kRecHdr = 2;
+
+// Reserve one record slot per lane in its destination's segment (wave-aggregated atomics, one per
+// distinct destination of the wave).  dest < 0: no record.
+__device__ __forceinline__ int64_t reserve_slot(int dest, u64* __restrict__ cursor, const int64_t* __restrict__ seg_start) {
+    const int lane = threadIdx.x & 63;
+    const u64 lt = (1ull << lane) - 1ull;
+    u64 left = __ballot(dest >= 0);
+    int64_t slot = -1;
+    while (left) {
+        const int leader = __ffsll((long long)left) - 1;
+        const int d = __shfl(dest, leader);
+        const u64 m = __ballot(dest == d);
+        u64 base = 0;
+        if (lane == leader) base = atomicAdd(&cursor[d], (u64)__popcll(m));
+        base = __shfl(base, leader);
+        if (dest == d) slot = seg_start[d] + (int64_t)base + __popcll(m & lt);
+        left &= ~m;
+    }
+    return slot;
+}
+
 template <int W>
-__global__ void __launch_bounds__(256) hgx_ghost_pack(int64_t A, u64* __restrict__ fa_next,
-                                                      const u64* __restrict__ own_bm,
-                                                      const int32_t* __restrict__ l2g, int32_t NP,
-                                                      const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
-                                                      const int64_t* __restrict__ seg_start, u64* __restrict__ send) {
-    constexpr int R = 64 / W;   // rows copied per wave iteration (W lanes per row)
+__device__ __forceinline__ void write_record(u64* __restrict__ send, int64_t slot, int32_t lid, const u64* __restrict__ row) {
+    u64* rec = send + slot * (W + kRecHdr);
+    *reinterpret_cast<u64x2*>(rec) = u64x2{(u64)(uint32_t)lid, 0ull};
+#pragma unroll
+    for (int w = 0; w < W; w += 2) {
+        if constexpr (W == 1) rec[kRecHdr] = row[0];
+        else *reinterpret_cast<u64x2*>(rec + kRecHdr + w) = *reinterpret_cast<const u64x2*>(row + w);
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xr_pack(int64_t A, const u64* __restrict__ fa_next,
+                                                   const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
+                                                   const int32_t* __restrict__ xo_lid, const u64* __restrict__ lvl_next,
+                                                   u64* __restrict__ cursor, const int64_t* __restrict__ seg_start,
+                                                   u64* __restrict__ send, u64* __restrict__ nzw) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const u64 lt = (1ull << lane) - 1ull;
+    u64 nz = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
-        const u64 f = fa_next[tile], own = own_bm[tile];
-        u64 gh = f & ~own;
+        const u64 gh = fa_next[tile] & ~own_bm[tile];
         if (gh == 0) continue;   // wave-uniform
         const int64_t t = tile * 64 + lane;
         const bool hit = (gh >> lane) & 1ull;
-        const int32_t gid = hit ? l2g[t] : 0;
-        const int dest = hit ? (int)(gid % NP) : -1;
-        int64_t slot = 0;
-        for (int d = 0; d < NP; ++d) {
-            const u64 m = __ballot(dest == d);
-            if (m == 0) continue;
-            const int leader = __ffsll((long long)m) - 1;
-            u64 base = 0;
-            if (lane == leader) base = atomicAdd(&cursor[d], (u64)__popcll(m));
-            base = __shfl(base, leader);
-            if (dest == d) slot = seg_start[d] + (int64_t)base + __popcll(m & lt);
+        const int64_t slot = reserve_slot(hit ? xo_part[t] : -1, cursor, seg_start);
+        if (hit) {
+            const u64* row = lvl_next + t * W;
+            write_record<W>(send, slot, xo_lid[t], row);
+            for (int w = 0; w < W; ++w) nz += row[w] != 0ull;
         }
-        const int k = lane / W, w = lane % W;
-        while (gh) {
-            u64 x = gh;
-            for (int i = 0; i < k && x; ++i) x &= x - 1ull;
-            const int src = x ? __ffsll((long long)x) - 1 : -1;
-            for (int i = 0; i < R && gh; ++i) gh &= gh - 1ull;
-            const int64_t s_slot = __shfl(slot, src < 0 ? 0 : src);
-            const int32_t s_gid = __shfl(gid, src < 0 ? 0 : src);
-            if (src >= 0) {
-                u64* rec = send + s_slot * (W + 1);
-                if (w == 0) rec[0] = (u64)(uint32_t)s_gid;
-                rec[1 + w] = lvl_next[(tile * 64 + src) * W + w];
-            }
-        }
-        if (lane == 0) fa_next[tile] = f & own;
     }
+    wave_add(nzw, nz);
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) hgx_ghost_apply(int64_t n, const u64* __restrict__ recv,
-                                                       const int32_t* __restrict__ own_l, int32_t NP,
-                                                       u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
-                                                       u64* __restrict__ vis, u64* __restrict__ ever,
-                                                       u64* __restrict__ full, FullMask fm) {
-    constexpr int R = 64 / W;
-    const int lane = threadIdx.x & 63, k = lane / W, w = lane % W;
+__global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restrict__ fa_next,
+                                                   const u64* __restrict__ own_bm, const int64_t* __restrict__ bc_off,
+                                                   const int32_t* __restrict__ bc_part, const int32_t* __restrict__ bc_lid,
+                                                   const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
+                                                   const int64_t* __restrict__ seg_start, u64* __restrict__ send,
+                                                   u64* __restrict__ nzw) {
+    const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const u64 FW = fm.w[w];
-    for (int64_t base = wave * R; base < n; base += nwave * R) {
-        const int64_t i = base + k;
-        const bool valid = i < n;
-        int64_t t = 0;
-        u64 r = 0;
-        if (valid) {
-            const u64* rec = recv + i * (W + 1);
-            t = own_l[(uint32_t)rec[0] / (uint32_t)NP];
-            r = rec[1 + w];
+    u64 nz = 0;
+    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+        const u64 ow = fa_next[tile] & own_bm[tile];
+        if (ow == 0) continue;   // wave-uniform
+        const int64_t t = tile * 64 + lane;
+        const bool hit = (ow >> lane) & 1ull;
+        int64_t b = 0, n = 0;
+        if (hit) {
+            b = bc_off[t];
+            n = bc_off[t + 1] - b;
         }
-        const bool ev = valid && bit(ever, t);
-        const u64 old = ev ? vis[t * W + w] : 0ull;
-        const u64 nw = r & ~old;
-        const bool any = group_any<W>(nw != 0ull);
-        const bool becomes_full = group_all<W>((old | nw) == FW);
-        if (valid && any) {
-            const bool was = bit(fa_next, t);
-            lvl_next[t * W + w] = was ? (lvl_next[t * W + w] | nw) : nw;
-            vis[t * W + w] = old | nw;
-            if (w == 0) {
-                if (!was) set_bit(fa_next, t);
-                if (!ev) set_bit(ever, t);
-                if (becomes_full) set_bit(full, t);
+        int nmax = (int)n;
+        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        for (int k = 0; k < nmax; ++k) {   // wave-uniform: the k-th other holder of every lane's atom
+            const bool has = k < n;
+            const int64_t slot = reserve_slot(has ? bc_part[b + k] : -1, cursor, seg_start);
+            if (has) {
+                const u64* row = lvl_next + t * W;
+                write_record<W>(send, slot, bc_lid[b + k], row);
+                for (int w = 0; w < W; ++w) nz += row[w] != 0ull;
             }
         }
     }
+    wave_add(nzw, nz);
 }
 
-// out[0] += |frontier|, out[1] += sum of |inc(v)| over the frontier (owned atoms only after the pack)
+// reduce side: one source segment (every atom at most once)
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xr_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
+                                                    u64* __restrict__ fa_next, u64* __restrict__ vis,
+                                                    u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const u64* rec = recv + i * (W + kRecHdr);
+        const int64_t t = (int64_t)(uint32_t)rec[0];
+        const bool ev = bit(ever, t), was = bit(fa_next, t);
+        bool any = false, isfull = true;
+        u64* lv = lvl_next + t * W;
+        u64* vs = vis + t * W;
+        for (int w = 0; w < W; ++w) {
+            const u64 old = ev ? vs[w] : 0ull;
+            const u64 nw = rec[kRecHdr + w] & ~old;
+            any |= nw != 0ull;
+            isfull &= (old | nw) == fm.w[w];
+        }
+        if (!any) continue;
+        for (int w = 0; w < W; ++w) {
+            const u64 old = ev ? vs[w] : 0ull;
+            const u64 nw = rec[kRecHdr + w] & ~old;
+            lv[w] = was ? (lv[w] | nw) : nw;
+            vs[w] = old | nw;
+        }
+        if (!was) set_bit(fa_next, t);
+        if (!ev) set_bit(ever, t);
+        if (isfull) set_bit(full, t);
+    }
+}
+
+// broadcast side: every ghost receives exactly one record (from its owner)
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xb_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
+                                                    u64* __restrict__ fa_next, u64* __restrict__ vis,
+                                                    u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const u64* rec = recv + i * (W + kRecHdr);
+        const int64_t t = (int64_t)(uint32_t)rec[0];
+        const bool ev = bit(ever, t), was = bit(fa_next, t);
+        bool isfull = true;
+        u64* lv = lvl_next + t * W;
+        u64* vs = vis + t * W;
+        for (int w = 0; w < W; ++w) {
+            const u64 r = rec[kRecHdr + w];
+            const u64 v = (ev ? vs[w] : 0ull) | r;
+            lv[w] = r;
+            vs[w] = v;
+            isfull &= v == fm.w[w];
+        }
+        if (!was) set_bit(fa_next, t);
+        if (!ev) set_bit(ever, t);
+        if (isfull) set_bit(full, t);
+    }
+}
+
+// out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
+// over the whole local frontier (the next level's local push volume)
 __global__ void __launch_bounds__(256) hgx_frontier_stats(int64_t A, const u64* __restrict__ fa,
+                                                          const u64* __restrict__ own,
                                                           const int64_t* __restrict__ inc_off, u64* __restrict__ out) {
     u64 n = 0, deg = 0;
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w * 64 < A;
          w += (int64_t)gridDim.x * blockDim.x) {
         u64 x = fa[w];
-        n += __popcll(x);
+        n += __popcll(x & own[w]);
         while (x) {
             const int64_t v = w * 64 + __ffsll((long long)x) - 1;
             x &= x - 1ull;
@@ -2135,9 +2233,12 @@ struct Timer {
         for (auto& r : rec) {
             float ms = 0;
             HGX_HIP(hipEventElapsedTime(&ms, r.e.a, r.e.b));
-            if (r.kind == HGX_K_COUNT) {   // the partitioned exchange
+            if (r.kind == HGX_K_COUNT) {   // the partitioned exchange (pack / apply kernels)
                 st.ms_exchange += ms;
-                if (r.level < 64) st.level_ms[r.level] += ms;
+                if (r.level < 64) {
+                    st.level_ms[r.level] += ms;
+                    st.level_xms[r.level] += ms;
+                }
                 continue;
             }
             st.ms_kernel[r.kind] += ms;
@@ -2210,96 +2311,141 @@ FullMask full_mask(int S, int W) {
     return fm;
 }
 
-// Per-batch buffers of the partitioned exchange (send segments per owner, receive area).
+// Per-batch buffers of the partitioned exchange (vertex cut).  Segment
+// capacities are static: part q receives from me at most my ghosts owned by q (reduce) and my
+// owned atoms held by q (broadcast); symmetrically for what I receive.
 struct Exchange {
     hgx_graph* g;
     Transport* tr;
     int W;
-    int64_t rec_words;                  // W + 1
+    int64_t rec_words;                  // W + kRecHdr
+    int64_t cap_recs = 0;               // send / receive area capacity (records)
     u64* send = nullptr;
     u64* recv = nullptr;
-    u64* cursor = nullptr;              // [NP] device
-    u64* fstats = nullptr;              // [2] device
-    int64_t* seg_start = nullptr;       // [NP] device
-    int64_t send_recs = 0, recv_recs = 0;
-    std::vector<int64_t> recv_cnt_cap;  // per source part
-    double bytes_sent = 0;
-    Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w), rec_words(w + 1) {
+    u64* dctr = nullptr;                // [NP] cursors, [NP..NP+1] frontier stats, [NP+2] nonzero words
+    int64_t* seg = nullptr;             // [2 * NP] device: reduce / broadcast send segment starts
+    std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast), NP + 1 entries
+    double bytes_sent = 0, nz_words = 0, words = 0;
+    Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w), rec_words(w + kRecHdr) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts;
-        {   // how many of my atoms each part holds as ghosts (collective, once per batch)
-            std::vector<int64_t> all((size_t)NP * NP);
-            tr->allgather_i64(sh.ghost_count.data(), NP, all.data(), g->stream);
-            sh.recv_count.assign(NP, 0);
-            for (int p = 0; p < NP; ++p) sh.recv_count[p] = all[(size_t)p * NP + sh.part];
+        rseg.assign(NP + 1, 0);
+        bseg.assign(NP + 1, 0);
+        for (int q = 0; q < NP; ++q) {
+            rseg[q + 1] = rseg[q] + sh.ghost_count[q];
+            bseg[q + 1] = bseg[q] + sh.bc_count[q];
         }
-        send_recs = sh.n_ghost;
-        recv_recs = 0;
-        for (int p = 0; p < NP; ++p) recv_recs += sh.recv_count[p];
-        send = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(send_recs, 1) * rec_words);
-        recv = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(recv_recs, 1) * rec_words);
-        cursor = (u64*)g->alloc(sizeof(u64) * (NP + 2));
-        fstats = cursor + NP;
-        seg_start = (int64_t*)g->alloc(sizeof(int64_t) * NP);
-        HGX_HIP(hipMemcpyAsync(seg_start, sh.ghost_start.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice,
-                               g->stream));
+        cap_recs = std::max<int64_t>(std::max(rseg[NP], bseg[NP]), 1);
+        send = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
+        recv = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
+        dctr = (u64*)g->alloc(sizeof(u64) * (NP + 4));
+        seg = (int64_t*)g->alloc(sizeof(int64_t) * 2 * NP);
+        HGX_HIP(hipMemcpyAsync(seg, rseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
+        HGX_HIP(hipMemcpyAsync(seg + NP, bseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
     }
     ~Exchange() {
         const int NP = g->shard->n_parts;
-        g->release(send, sizeof(u64) * (size_t)std::max<int64_t>(send_recs, 1) * rec_words);
-        g->release(recv, sizeof(u64) * (size_t)std::max<int64_t>(recv_recs, 1) * rec_words);
-        g->release(cursor, sizeof(u64) * (NP + 2));
-        g->release(seg_start, sizeof(int64_t) * NP);
+        g->release(send, sizeof(u64) * (size_t)cap_recs * rec_words);
+        g->release(recv, sizeof(u64) * (size_t)cap_recs * rec_words);
+        g->release(dctr, sizeof(u64) * (NP + 4));
+        g->release(seg, sizeof(int64_t) * 2 * NP);
     }
-    // Ship ghost rows to their owners and OR in what the other parts found for my atoms.  Returns
-    // the group-wide number of new atoms; *push_volume = sum of |inc| over my new frontier.
+    // collective step: the part's device work is bracketed by compute_begin / compute_end
+    template <class F>
+    void coll(F f) {
+        tr->compute_end(g->stream);
+        f();
+        tr->compute_begin(g->stream);
+    }
+    // One exchange phase: counts -> all-to-all of the segments.  recv_cap[q] bounds what q sends me;
+    // returns the per-source receive counts and places source q's records at recv + rbase[q].
+    void ship(const std::vector<int64_t>& sbase, const std::vector<int64_t>& rbase, const std::vector<u64>& cnt,
+              std::vector<int64_t>& rcnt, double& pair_max) {
+        ShardInfo& sh = *g->shard;
+        const int NP = sh.n_parts, me = sh.part;
+        std::vector<int64_t> mine(NP), all((size_t)NP * NP);
+        for (int q = 0; q < NP; ++q) mine[q] = (int64_t)cnt[q];
+        coll([&] { tr->allgather_i64(mine.data(), NP, all.data(), g->stream); });
+        const int64_t rb = (int64_t)sizeof(u64) * rec_words;
+        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP);
+        rcnt.assign(NP, 0);
+        for (int q = 0; q < NP; ++q) {
+            soff[q] = sbase[q] * rb;
+            sbytes[q] = mine[q] * rb;
+            rcnt[q] = all[(size_t)q * NP + me];
+            if (rcnt[q] > rbase[q + 1] - rbase[q]) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
+            roff[q] = rbase[q] * rb;
+            rbytes[q] = rcnt[q] * rb;
+            bytes_sent += (double)sbytes[q];
+            pair_max = std::max(pair_max, (double)sbytes[q]);
+        }
+        coll([&] { tr->alltoallv(send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), g->stream); });
+    }
+    // Reduce + broadcast of one level.  Returns the group-wide number of new atoms; *push_volume =
+    // sum of |inc| over my (local) new frontier; *level_bytes / *pair_max: bytes I sent.
     template <int Wt>
-    u64 level(u64* lvl_next, u64* fa_next, u64* vis, u64* ever, u64* full, const FullMask& fm, u64* push_volume) {
+    u64 level(u64* lvl_next, u64* fa_next, u64* vis, u64* ever, u64* full, const FullMask& fm, u64* push_volume,
+              double* level_bytes, double* pair_max, Timer& tm, int d) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts, me = sh.part;
         hipStream_t s = g->stream;
         const int64_t A = g->A;
-        HGX_HIP(hipMemsetAsync(cursor, 0, sizeof(u64) * (NP + 2), s));
-        hgx_ghost_pack<Wt><<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(
-            A, fa_next, (const u64*)sh.own_bm, sh.l2g, NP, lvl_next, cursor, seg_start, send);
+        const int grid = grid_for(ceil_div(A, 64) * 64, 256, 4096);
+        const double before = bytes_sent;
+        *pair_max = 0;
+        std::vector<u64> cnt(NP + 4);
+        std::vector<int64_t> rcnt;
+        // reduce: partial rows of my ghosts -> their owners
+        Events e0 = tm.start(kKindExchange, d);
+        HGX_HIP(hipMemsetAsync(dctr, 0, sizeof(u64) * (NP + 4), s));
+        hgx_xr_pack<Wt><<<grid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_lid, lvl_next, dctr, seg, send,
+                                             dctr + NP + 2);
         HGX_CHECK_LAUNCH();
-        std::vector<u64> cnt(NP);
-        HGX_HIP(hipMemcpyAsync(cnt.data(), cursor, sizeof(u64) * NP, hipMemcpyDeviceToHost, s));
+        tm.stop(e0);
+        HGX_HIP(hipMemcpyAsync(cnt.data(), dctr, sizeof(u64) * (NP + 4), hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
-        std::vector<int64_t> mine(NP), all((size_t)NP * NP);
-        for (int p = 0; p < NP; ++p) mine[p] = (int64_t)cnt[p];
-        tr->allgather_i64(mine.data(), NP, all.data(), s);
-        const int64_t rb = (int64_t)sizeof(u64) * rec_words;
-        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP), rcnt(NP);
-        int64_t ro = 0;
-        for (int p = 0; p < NP; ++p) {
-            soff[p] = sh.ghost_start[p] * rb;
-            sbytes[p] = mine[p] * rb;
-            rcnt[p] = all[(size_t)p * NP + me];
-            if (rcnt[p] > sh.recv_count[p]) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
-            roff[p] = ro * rb;
-            rbytes[p] = rcnt[p] * rb;
-            ro += rcnt[p];
-            bytes_sent += (double)sbytes[p];
-        }
-        tr->alltoallv(send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
-        for (int p = 0; p < NP; ++p) {
-            if (p == me || rcnt[p] == 0) continue;
-            hgx_ghost_apply<Wt><<<grid_for(ceil_div(rcnt[p], 64 / Wt) * 64, 256, 8192), 256, 0, s>>>(
-                rcnt[p], recv + roff[p] / (int64_t)sizeof(u64), sh.own_l, NP, lvl_next, fa_next, vis, ever, full, fm);
+        nz_words += (double)cnt[NP + 2];
+        for (int q = 0; q < NP; ++q) words += (double)cnt[q] * Wt;
+        ship(rseg, bseg, cnt, rcnt, *pair_max);
+        Events e1 = tm.start(kKindExchange, d);
+        for (int q = 0; q < NP; ++q) {
+            if (q == me || rcnt[q] == 0) continue;
+            hgx_xr_apply<Wt><<<grid_for(rcnt[q], 256, 8192), 256, 0, s>>>(
+                rcnt[q], recv + bseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
         }
-        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, g->inc_off, fstats);
+        // broadcast: final rows of my owned atoms -> their other holders
+        HGX_HIP(hipMemsetAsync(dctr, 0, sizeof(u64) * (NP + 4), s));
+        hgx_xb_pack<Wt><<<grid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid, lvl_next, dctr,
+                                             seg + NP, send, dctr + NP + 2);
         HGX_CHECK_LAUNCH();
+        tm.stop(e1);
+        HGX_HIP(hipMemcpyAsync(cnt.data(), dctr, sizeof(u64) * (NP + 4), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        nz_words += (double)cnt[NP + 2];
+        for (int q = 0; q < NP; ++q) words += (double)cnt[q] * Wt;
+        ship(bseg, rseg, cnt, rcnt, *pair_max);
+        Events e2 = tm.start(kKindExchange, d);
+        for (int q = 0; q < NP; ++q) {
+            if (q == me || rcnt[q] == 0) continue;
+            hgx_xb_apply<Wt><<<grid_for(rcnt[q], 256, 8192), 256, 0, s>>>(
+                rcnt[q], recv + rseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
+            HGX_CHECK_LAUNCH();
+        }
+        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, g->inc_off,
+                                                                               dctr + NP);
+        HGX_CHECK_LAUNCH();
+        tm.stop(e2);
         u64 fs[2];
-        HGX_HIP(hipMemcpyAsync(fs, fstats, sizeof(fs), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipMemcpyAsync(fs, dctr + NP, sizeof(fs), hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
         *push_volume = fs[1];
+        *level_bytes = bytes_sent - before;
         int64_t nl = (int64_t)fs[0];
         std::vector<int64_t> nall(NP);
-        tr->allgather_i64(&nl, 1, nall.data(), s);
+        coll([&] { tr->allgather_i64(&nl, 1, nall.data(), s); });
         u64 tot = 0;
-        for (int p = 0; p < NP; ++p) tot += (u64)nall[p];
+        for (int q = 0; q < NP; ++q) tot += (u64)nall[q];
         return tot;
     }
 };
@@ -2314,6 +2460,18 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const size_t bm_bytes = res->bm_bytes();
     const size_t la_bytes = sizeof(u64) * (size_t)(M / 64 + 2);
     const FullMask fm = full_mask(bt.S, W);
+    // a partition part's device work runs between compute_begin / compute_end (the exchange releases
+    // it around each collective); the guard releases it on an error path too
+    struct Gate {
+        Transport* tr;
+        hipStream_t s;
+        explicit Gate(Transport* t, hipStream_t st) : tr(t), s(st) {
+            if (tr) tr->compute_begin(s);
+        }
+        ~Gate() {
+            if (tr) tr->compute_release(s);
+        }
+    } gate(tr, s);
 
     u64* vis = (u64*)g->alloc(row_bytes);
     u64* lf = (MODE == kSym) ? (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W) : nullptr;
@@ -2631,9 +2789,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }   // not an ordered push level
         u64 new_global = 0, part_push = 0;
         if (ex) {
-            Events e5 = tm.start(kKindExchange, d);
-            new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push);
-            tm.stop(e5);
+            double lb = 0, pm = 0;
+            new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push, &lb, &pm, tm, d);
+            if (d < 64) {
+                res->stats.level_xbytes[d] += lb;
+                res->stats.level_xpair_max[d] = std::max(res->stats.level_xpair_max[d], pm);
+            }
         }
         Pend& pn = pend[d & 1];
         pn.d = d;
@@ -2671,7 +2832,11 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }
     }
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(pend[k].ev);
-    if (ex) res->stats.bytes_exchanged += ex->bytes_sent;
+    if (ex) {
+        res->stats.bytes_exchanged += ex->bytes_sent;
+        res->stats.xwords_nonzero += ex->nz_words;
+        res->stats.xwords_total += ex->words;
+    }
     g->release(vis, row_bytes);
     if (lf) g->release(lf, sizeof(u64) * (size_t)std::max<int64_t>(M, 1) * W);
     g->release(hubacc, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W);
@@ -2729,7 +2894,7 @@ void count_level_dispatch(int W, hgx_graph* g, const u64* fa, const u64* lvl, u6
 template <int W>
 void count_rows(hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, u64* counts) {
     const int64_t nwords = ceil_div(std::max<int64_t>(g->A, 1), 64);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), 2048));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), 4096));
     hgx_count_rows<W><<<grid, 256, 0, g->stream>>>(g->A, fa, own, lvl, counts);
     HGX_CHECK_LAUNCH();
 }
@@ -2897,13 +3062,13 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         std::map<int32_t, std::vector<u64>> rows;
         for (int32_t i = 0; i < bt.S; ++i) {
             int32_t a = seeds[s0 + i];
-            if (shp) {   // a shard seeds only its own atoms (local id)
-                if (a % shp->n_parts != shp->part) continue;
-                a = shp->own_l_host[a / shp->n_parts];
-                if (a < 0) {   // no incidence: V_0 = {seed} and nothing else (kept on the host)
-                    r->isolated[s0 + i] = seeds[s0 + i];
+            if (shp) {   // every part holding the seed starts from it (its links are spread over them)
+                const int32_t l = shp->local_of(a);
+                if (l < 0) {   // not here; no incidence anywhere: V_0 = {seed}, recorded by part a % n_parts
+                    if (!shp->present(a) && a % shp->n_parts == shp->part) r->isolated[s0 + i] = seeds[s0 + i];
                     continue;
                 }
+                a = l;
             }
             auto& row = rows[a];
             if (row.empty()) row.assign(bt.W, 0ull);
@@ -3050,7 +3215,8 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
     const int64_t span = ceil_div(std::max<int64_t>(g->A, 1), nblk);
     int64_t* dcnt = (int64_t*)g->alloc(sizeof(int64_t) * nblk * 2);
     int64_t* doff = dcnt + nblk;
-    hgx_extract<<<nblk, 256, 0, g->stream>>>(g->A, span, bt.W, s, bt.fa[depth], bt.lvl[depth], doff, dcnt, nullptr,
+    const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;   // a part reports its owned atoms
+    hgx_extract<<<nblk, 256, 0, g->stream>>>(g->A, span, bt.W, s, bt.fa[depth], own, bt.lvl[depth], doff, dcnt, nullptr,
                                               0, false);
     HGX_CHECK_LAUNCH();
     std::vector<int64_t> hc(nblk), ho(nblk);
@@ -3066,7 +3232,7 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
     if (k > 0) {
         int32_t* dout = (int32_t*)g->alloc(sizeof(int32_t) * k);
         HGX_HIP(hipMemcpyAsync(doff, ho.data(), sizeof(int64_t) * nblk, hipMemcpyHostToDevice, g->stream));
-        hgx_extract<<<nblk, 256, 0, g->stream>>>(g->A, span, bt.W, s, bt.fa[depth], bt.lvl[depth], doff, dcnt, dout,
+        hgx_extract<<<nblk, 256, 0, g->stream>>>(g->A, span, bt.W, s, bt.fa[depth], own, bt.lvl[depth], doff, dcnt, dout,
                                                   k, true);
         HGX_CHECK_LAUNCH();
         HGX_HIP(hipMemcpyAsync(out, dout, sizeof(int32_t) * k, hipMemcpyDeviceToHost, g->stream));
@@ -3087,13 +3253,14 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
     if (g->shard) {   // global id of an atom this shard owns
         const ShardInfo& sh = *g->shard;
         if (atom < 0 || atom >= sh.A_global) fail(HGX_E_INVALID, "atom id out of range");
-        if (atom % sh.n_parts != sh.part) fail(HGX_E_NOTFOUND, "atom is owned by another part");
-        const int32_t loc = sh.own_l_host[atom / sh.n_parts];
-        if (loc < 0) {   // no incidence: reached only as its own seed
+        if (!sh.present(atom)) {   // no incidence anywhere: reached only as its own seed (part atom % n_parts)
+            if (atom % sh.n_parts != sh.part) fail(HGX_E_NOTFOUND, "atom is owned by another part");
             auto iso = r->isolated.find(seed_index);
             *depth_out = (iso != r->isolated.end() && iso->second == atom) ? 0 : -1;
             return HGX_OK;
         }
+        const int32_t loc = sh.local_of(atom);
+        if (loc < 0 || !sh.owns_local(loc)) fail(HGX_E_NOTFOUND, "atom is owned by another part");
         atom = loc;
     }
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "atom id out of range");

@@ -39,7 +39,8 @@ void graph_release(hgx_graph* g) {
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {
-        (void)hipFree(g->shard->l2g); (void)hipFree(g->shard->own_l); (void)hipFree(g->shard->own_bm);
+        (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);
+        (void)hipFree(g->shard->bc_off); (void)hipFree(g->shard->bc_part); (void)hipFree(g->shard->bc_lid);
         delete g->shard;
     }
     delete g;
@@ -430,6 +431,9 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         g->bfs_flags = (int32_t)value;
     } else if (option == HGX_OPT_RANKS_ORDERED) {
         g->ranks_ordered = value != 0;
+    } else if (option == HGX_OPT_PART_SERIAL) {
+        if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_PART_SERIAL applies to partition shards");
+        g->shard->serial = value != 0;
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;

@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <mutex>
@@ -76,27 +77,37 @@ struct PoolBuf {
     size_t n;
 };
 
-// Hash partition of a snapshot over n_parts devices: owner(atom) =
-// atom % n_parts.  A shard's local atoms are its owned atoms plus its ghosts (atoms owned
-// elsewhere that are targets of a local link); local links are the links with at least one
-// owned target (their target rows are replicated on every shard that holds one).  Local ids are
-// assigned in global id order, so every ascending local list is an ascending global list.
+// Vertex-cut partition of a snapshot over n_parts devices (hgx_part.hip):
+// every link row lives on one part; an atom is present (local) on every part holding one of its
+// links and owned by one of them.  Local ids are assigned in global id order, so every ascending
+// local list is an ascending global list.
 struct ShardInfo {
     int32_t n_parts = 1, part = 0;
-    int64_t A_global = 0, n_owned = 0, n_ghost = 0;
-    std::vector<int32_t> l2g_host;       // [A_local] global id of local atom
-    std::vector<int32_t> own_l_host;     // [ceil((A_global - part) / n_parts)] local id of atom part + k*n_parts
-    std::vector<int64_t> ghost_count;    // [n_parts] ghosts owned by each part (0 for this part)
-    std::vector<int64_t> ghost_start;    // [n_parts + 1] prefix of ghost_count (send segments)
-    std::vector<int64_t> recv_count;     // [n_parts] atoms of this part held as ghosts by each part
-                                         // (filled on the first exchange; -1 = unknown)
-    int32_t* l2g = nullptr;              // device copies
-    int32_t* own_l = nullptr;
-    uint64_t* own_bm = nullptr;          // [A_local/64 + 2] bit set <=> local atom is owned
+    int64_t A_global = 0, n_owned = 0;
+    std::vector<int32_t> l2g_host;       // [A_local] global id of local atom (ascending)
+    std::vector<uint64_t> present_host;  // [A_global/64 + 1] atoms present on some part
+    std::vector<uint64_t> own_bm_host;   // [A_local/64 + 2] bit set <=> local atom is owned here
+    std::vector<int64_t> ghost_count;    // [n_parts] my ghosts owned by part q = reduce records to q (max)
+    std::vector<int64_t> bc_count;       // [n_parts] my owned atoms held by part q = broadcast records to q (max)
+    bool serial = false;                 // in-process rehearsal: parts run their kernels one at a time
+    // device copies
+    uint64_t* own_bm = nullptr;          // [A_local/64 + 2]
+    int32_t* xo_part = nullptr;          // [A_local] ghost: owner part (-1 owned)
+    int32_t* xo_lid = nullptr;           // [A_local] ghost: its local id on the owner
+    int64_t* bc_off = nullptr;           // [A_local + 1] owned atom: its other holders ...
+    int32_t* bc_part = nullptr;          //   ... their parts
+    int32_t* bc_lid = nullptr;           //   ... and its local id there
+    // the global -> local id of an atom present here, or -1 (binary search of l2g_host)
+    int32_t local_of(int64_t v) const {
+        auto it = std::lower_bound(l2g_host.begin(), l2g_host.end(), (int32_t)v);
+        return (it != l2g_host.end() && *it == v) ? (int32_t)(it - l2g_host.begin()) : -1;
+    }
+    bool owns_local(int64_t l) const { return (own_bm_host[l >> 6] >> (l & 63)) & 1ull; }
+    bool present(int64_t v) const { return (present_host[v >> 6] >> (v & 63)) & 1ull; }
 };
 
-// Transport of the per-level frontier exchange: RCCL between processes (one GPU each) or an
-// in-process group of shard threads.  Every call is collective over the group.
+// Transport of the per-level frontier exchange: RCCL between processes (one GPU each), an
+// in-process group of shard threads, or host-staged callbacks.  Every call is collective.
 struct Transport {
     int32_t world = 1, rank = 0;
     virtual ~Transport() {}
@@ -106,6 +117,11 @@ struct Transport {
     // bytes from rank p at recv + recv_off[p] (device buffers, ordered on stream s)
     virtual void alltoallv(const void* send, const int64_t* send_off, const int64_t* send_bytes, void* recv,
                            const int64_t* recv_off, const int64_t* recv_bytes, hipStream_t s) = 0;
+    // brackets of a part's device work between two exchanges (the in-process rehearsal runs the
+    // parts' kernels one part at a time so their device times are clean)
+    virtual void compute_begin(hipStream_t) {}
+    virtual void compute_end(hipStream_t) {}
+    virtual void compute_release(hipStream_t) {}   // end of the work or an error path: give the gate back
     virtual const char* kind() const = 0;
 };
 

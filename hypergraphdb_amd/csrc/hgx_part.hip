@@ -1,25 +1,38 @@
-// hgx_part.hip -- hash partition of a snapshot over n_parts devices and the transports of the
-// partitioned BFS.
+// hgx_part.hip -- vertex-cut partition of a snapshot over n_parts devices and the transports of
+// the partitioned BFS.
 //
 // The reference keeps one incidence index per store (HGStore.getIncidenceResultSet,
-// C/HGStore.java:253; BJEStorageImplementation.java:405-439).  Config 4 (1B incidences) is split
-// by atom: owner(a) = a % n_parts.  Part p keeps
-//   * every atom it owns (the incidence rows of owned atoms are complete on p),
-//   * every link with at least one owned target (target rows replicated, at most arity copies),
-//   * the ghosts: atoms owned elsewhere that are targets of a local link.
-// Owned atoms with no incidence (no link targets them, e.g. the link atoms of config 4) get no
-// local id and no device rows: they are reachable only as seeds.
+// C/HGStore.java:253; BJEStorageImplementation.java:405-439) and walks it one atom at a time
+// (HGBreadthFirstTraversal.java:49-66).  Config 4 (1B incidences) is split by LINK: every link row
+// lives on exactly one part (its target row is stored once), so a part's gather and pull touch
+// 1/n_parts of the pins.  An atom is present on every part holding one of its links (its holders);
+// one holder owns it.  A BFS level then needs two exchanges of S-bit rows (hgx_bfs.hip, Exchange):
+//   reduce    each holder ships its partial news for an atom to the owner, which ORs them;
+//   broadcast the owner ships the atom's final news back to the other holders,
+// so every holder's frontier row and visited row stay identical to the whole-graph engine's.
+//
+// Placement (hgx_partition_plan): greedy streaming vertex cut -- a link goes to the part that
+// already holds the most of its targets, each target weighted 1/deg (low-degree atoms decide, hubs
+// are everywhere anyway), within a pin-balance cap.  Config 4 at 2-10% scale: 1.0 remote holder
+// per present atom against 2.0 for a random placement (tools/vcut_quality.py).  Decisions are taken in
+// batches of plan_batch(M) links against the hold state at the batch start, in kPlanChunks fixed
+// chunks, so the plan is deterministic whatever the thread count -- every rank of a multi-process
+// run computes the same plan from the same snapshot.
+// Owner of a present atom: one of its holders, chosen by a hash of its id (balances owned atoms).
 // Local ids follow global id order, so ascending local lists are ascending global lists and the
 // on-device incidence build of hgx_graph_create applies unchanged.
 //
-// Transports: RCCL (grouped ncclSend/ncclRecv over xGMI, one process per GPU) and an in-process
-// group (one host thread per part, device-to-device copies) used by hgx_pbfs_batch_group.
+// Transports: RCCL (grouped ncclSend/ncclRecv over xGMI, one process per GPU), an in-process
+// group (one host thread per part, device-to-device copies) used by hgx_pbfs_batch_group, and a
+// host-staged transport whose collectives are callbacks into the caller (e.g. a gloo group).
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <numeric>
 #include <thread>
 
 #include "hgx_internal.h"
@@ -29,9 +42,15 @@ using namespace hgx;
 struct hgx_shard {
     int32_t n_parts = 1, part = 0;
     int64_t A_global = 0, n_owned = 0;
-    std::vector<int32_t> l2g, own_l;
+    std::vector<int32_t> l2g;                 // [A_local] global id, ascending
     std::vector<int32_t> link_atom, link_type, tgt_idx;
-    std::vector<int64_t> tgt_off, ghost_count;
+    std::vector<int64_t> tgt_off;
+    std::vector<uint64_t> own_bm;             // [A_local/64 + 2] owned local atoms
+    std::vector<int32_t> xo_part, xo_lid;     // [A_local] ghosts: owner part / local id there (-1: owned)
+    std::vector<int64_t> bc_off;              // [A_local + 1] owned atoms: other holders
+    std::vector<int32_t> bc_part, bc_lid;     //   (part, local id there)
+    std::vector<int64_t> ghost_count, bc_count;   // [n_parts] reduce / broadcast records per peer
+    std::vector<uint64_t> present;            // [A_global/64 + 1] atoms present on some part
 };
 
 namespace {
@@ -41,7 +60,7 @@ int host_threads() {
     return (int)std::max(1u, std::min(n, 16u));
 }
 
-// fn(lo, hi) over [0, n) split into contiguous chunks, one per thread.
+// fn(lo, hi, t) over [0, n) split into contiguous chunks, one per thread.
 template <class F>
 void parallel_for(int64_t n, F fn) {
     const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 65536));
@@ -58,98 +77,300 @@ void parallel_for(int64_t n, F fn) {
     for (auto& x : th) x.join();
 }
 
-hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part) {
+// T worker threads started once; run(fn) executes fn(t) on every worker and returns when all are
+// done (a generation barrier), so thousands of short phases cost no thread launches.
+struct WorkerPool {
+    int T;
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv_go, cv_done;
+    std::function<void(int)> job;
+    int64_t gen = 0;
+    int running = 0;
+    bool quit = false;
+    explicit WorkerPool(int t) : T(t) {
+        for (int i = 0; i < T; ++i)
+            th.emplace_back([this, i] {
+                int64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> f;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv_go.wait(lk, [&] { return quit || gen != seen; });
+                        if (quit) return;
+                        seen = gen;
+                        f = job;
+                    }
+                    f(i);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--running == 0) cv_done.notify_all();
+                }
+            });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv_go.notify_all();
+        for (auto& x : th) x.join();
+    }
+    void run(std::function<void(int)> f) {
+        std::unique_lock<std::mutex> lk(mu);
+        job = std::move(f);
+        running = T;
+        ++gen;
+        cv_go.notify_all();
+        cv_done.wait(lk, [&] { return running == 0; });
+    }
+};
+
+void check_rows(const hgx_graph_desc* d) {
     const int64_t A = d->num_atoms, M = d->num_links;
-    if (A < 0 || M < 0 || A >= (int64_t)INT32_MAX) fail(HGX_E_INVALID, "hgx_shard_build: bad sizes");
-    if (M > 0 && (!d->tgt_off || !d->tgt_idx || !d->link_atom)) fail(HGX_E_INVALID, "hgx_shard_build: null link arrays");
-    if (NP < 1 || NP > 64 || part < 0 || part >= NP) fail(HGX_E_INVALID, "hgx_shard_build: bad part / n_parts (1..64)");
+    if (A < 0 || M < 0 || A >= (int64_t)INT32_MAX) fail(HGX_E_INVALID, "partition: bad sizes");
+    if (M > 0 && (!d->tgt_off || !d->tgt_idx || !d->link_atom)) fail(HGX_E_INVALID, "partition: null link arrays");
     const int64_t* off = d->tgt_off;
     const int32_t* tg = d->tgt_idx;
-    if (M > 0 && off[0] != 0) fail(HGX_E_INVALID, "hgx_shard_build: tgt_off[0] != 0");
+    if (M > 0 && off[0] != 0) fail(HGX_E_INVALID, "partition: tgt_off[0] != 0");
+    std::vector<int> bad(64, 0);
+    parallel_for(M, [&](int64_t lo, int64_t hi, int t) {
+        for (int64_t r = lo; r < hi; ++r) {
+            if (off[r + 1] < off[r]) {
+                bad[t] = 1;
+                continue;
+            }
+            for (int64_t p = off[r]; p < off[r + 1]; ++p)
+                if (tg[p] < 0 || tg[p] >= A) {
+                    bad[t] = 2;
+                    break;
+                }
+        }
+    });
+    for (int b : bad)
+        if (b == 1) fail(HGX_E_INVALID, "partition: tgt_off not monotone");
+        else if (b == 2) fail(HGX_E_INVALID, "partition: target id out of range");
+}
+
+// Links placed against one hold-state snapshot: M/512 clamped to [1K, 64K] (a function of M only,
+// so the plan stays deterministic); the first batch of a placement sees an empty state.
+inline int64_t plan_batch(int64_t M) { return std::min<int64_t>(std::max<int64_t>(M / 512, 1024), 1 << 16); }
+constexpr int kPlanChunks = 16;   // fixed chunks per batch (determinism)
+
+void plan_links(const hgx_graph_desc* d, int NP, int32_t* link_part, double slack) {
+    const int64_t A = d->num_atoms, M = d->num_links;
+    const int64_t* off = d->tgt_off;
+    const int32_t* tg = d->tgt_idx;
+    const int64_t P = M > 0 ? off[M] : 0;
+    if (NP == 1) {
+        std::fill(link_part, link_part + M, 0);
+        return;
+    }
+    std::vector<int32_t> deg((size_t)A, 0);
+    parallel_for(P, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t p = lo; p < hi; ++p) __atomic_fetch_add(&deg[tg[p]], 1, __ATOMIC_RELAXED);
+    });
+    std::vector<float> wt((size_t)A);
+    parallel_for(A, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t v = lo; v < hi; ++v) wt[v] = deg[v] > 0 ? 1.0f / (float)deg[v] : 0.0f;
+    });
+    std::vector<int32_t>().swap(deg);
+    std::vector<uint64_t> hold((size_t)A, 0);
+    std::vector<int64_t> load(NP, 0);
+    const int64_t cap = (int64_t)((1.0 + slack) * (double)P / NP) + 64;
+    std::vector<std::vector<int64_t>> delta(kPlanChunks, std::vector<int64_t>(NP, 0));
+    WorkerPool pool(std::min(host_threads(), kPlanChunks));
+    const int64_t batch = plan_batch(M);
+    for (int64_t b0 = 0; b0 < M; b0 += batch) {
+        const int64_t b1 = std::min(M, b0 + batch);
+        const int64_t per = (b1 - b0 + kPlanChunks - 1) / kPlanChunks;
+        // decide: every chunk reads the hold state of the batch start and its own load deltas
+        pool.run([&](int t) {
+            for (int c = t; c < kPlanChunks; c += pool.T) {
+                std::vector<int64_t>& dl = delta[c];
+                std::fill(dl.begin(), dl.end(), 0);
+                const int64_t lo = std::min(b1, b0 + c * per), hi = std::min(b1, lo + per);
+                float score[64];
+                for (int64_t L = lo; L < hi; ++L) {
+                    for (int q = 0; q < NP; ++q) score[q] = 0.0f;
+                    for (int64_t p = off[L]; p < off[L + 1]; ++p) {
+                        uint64_t m = hold[tg[p]];
+                        const float w = wt[tg[p]];
+                        while (m) {
+                            score[__builtin_ctzll(m)] += w;
+                            m &= m - 1;
+                        }
+                    }
+                    const int64_t n = off[L + 1] - off[L];
+                    int best = -1;
+                    for (int q = 0; q < NP; ++q) {
+                        if (load[q] + dl[q] + n > cap) continue;
+                        if (best < 0 || score[q] > score[best] ||
+                            (score[q] == score[best] && load[q] + dl[q] < load[best] + dl[best]))
+                            best = q;
+                    }
+                    if (best < 0) {   // every part at the cap: the least loaded
+                        best = 0;
+                        for (int q = 1; q < NP; ++q)
+                            if (load[q] + dl[q] < load[best] + dl[best]) best = q;
+                    }
+                    link_part[L] = best;
+                    dl[best] += n;
+                }
+            }
+        });
+        for (int c = 0; c < kPlanChunks; ++c)
+            for (int q = 0; q < NP; ++q) load[q] += delta[c][q];
+        // apply the batch's placements to the hold state
+        pool.run([&](int t) {
+            const int64_t per2 = (b1 - b0 + pool.T - 1) / pool.T;
+            const int64_t lo = std::min(b1, b0 + t * per2), hi = std::min(b1, lo + per2);
+            for (int64_t L = lo; L < hi; ++L) {
+                const uint64_t bitq = 1ull << link_part[L];
+                for (int64_t p = off[L]; p < off[L + 1]; ++p) {
+                    uint64_t* h = &hold[tg[p]];
+                    if (!(__atomic_load_n(h, __ATOMIC_RELAXED) & bitq)) __atomic_fetch_or(h, bitq, __ATOMIC_RELAXED);
+                }
+            }
+        });
+    }
+}
+
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// owner of a present atom: holder number mix(v) % |holders| in part order
+inline int owner_of(int64_t v, uint64_t hold) {
+    int k = (int)(mix64((uint64_t)v) % (uint64_t)__builtin_popcountll(hold));
+    while (k--) hold &= hold - 1;
+    return __builtin_ctzll(hold);
+}
+
+hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part, const int32_t* link_part) {
+    const int64_t A = d->num_atoms, M = d->num_links;
+    if (NP < 1 || NP > 64 || part < 0 || part >= NP) fail(HGX_E_INVALID, "hgx_shard_build: bad part / n_parts (1..64)");
+    if (M > 0 && !link_part) fail(HGX_E_INVALID, "hgx_shard_build: null link placement");
+    check_rows(d);
+    const int64_t* off = d->tgt_off;
+    const int32_t* tg = d->tgt_idx;
+    for (int64_t r = 0; r < M; ++r)
+        if (link_part[r] < 0 || link_part[r] >= NP) fail(HGX_E_INVALID, "hgx_shard_build: link placement out of range");
     std::unique_ptr<hgx_shard> s(new hgx_shard());
     s->n_parts = NP;
     s->part = part;
     s->A_global = A;
 
-    // 1. local links (an owned target) and the atoms they touch
-    std::vector<uint8_t> loc((size_t)M), mark((size_t)A, 0);
-    std::vector<int> bad(64, 0);
-    parallel_for(M, [&](int64_t lo, int64_t hi, int t) {
+    // 1. holders of every atom
+    std::vector<uint64_t> hold((size_t)A, 0);
+    parallel_for(M, [&](int64_t lo, int64_t hi, int) {
         for (int64_t r = lo; r < hi; ++r) {
-            const int64_t b = off[r], e = off[r + 1];
-            if (e < b) {
-                bad[t] = 1;
-                continue;
+            const uint64_t bq = 1ull << link_part[r];
+            for (int64_t p = off[r]; p < off[r + 1]; ++p) {
+                uint64_t* h = &hold[tg[p]];
+                if (!(__atomic_load_n(h, __ATOMIC_RELAXED) & bq)) __atomic_fetch_or(h, bq, __ATOMIC_RELAXED);
             }
-            bool any = false;
-            for (int64_t p = b; p < e; ++p) {
-                const int32_t v = tg[p];
-                if (v < 0 || v >= A) {
-                    bad[t] = 2;
-                    break;
-                }
-                any |= (v % NP) == part;
-            }
-            loc[r] = any;
         }
     });
-    for (int b : bad)
-        if (b == 1) fail(HGX_E_INVALID, "hgx_shard_build: tgt_off not monotone");
-        else if (b == 2) fail(HGX_E_INVALID, "hgx_shard_build: target id out of range");
-    // Owned atoms that no link targets are left out of the local space: BFS can reach them only
-    // as seeds (V_0 = {seed}), which the result records on the host (bfs_batch_impl).
-    parallel_for(M, [&](int64_t lo, int64_t hi, int) {
-        for (int64_t r = lo; r < hi; ++r)
-            if (loc[r])
-                for (int64_t p = off[r]; p < off[r + 1]; ++p) mark[tg[p]] = 1;   // benign same-value races
-    });
-
-    // 2. global -> local ids (prefix over the marks, in global order)
-    std::vector<int32_t> g2l((size_t)A);
-    {
-        const int T = host_threads();
-        std::vector<int64_t> cnt(T + 1, 0);
-        const int64_t per = (A + T - 1) / std::max(T, 1);
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t)
-            th.emplace_back([&, t] {
-                int64_t c = 0;
-                for (int64_t a = t * per; a < std::min(A, (t + 1) * per); ++a) c += mark[a];
-                cnt[t + 1] = c;
-            });
-        for (auto& x : th) x.join();
-        th.clear();
-        for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
-        s->l2g.resize((size_t)cnt[T]);
-        for (int t = 0; t < T; ++t)
-            th.emplace_back([&, t] {
-                int64_t k = cnt[t];
-                for (int64_t a = t * per; a < std::min(A, (t + 1) * per); ++a) {
-                    if (mark[a]) {
-                        g2l[a] = (int32_t)k;
-                        s->l2g[k++] = (int32_t)a;
-                    } else {
-                        g2l[a] = -1;
-                    }
+    // 2. per-part presence bitmaps and their block prefix counts: lid_q(v) in O(1)
+    const int64_t nw = A / 64 + 1;
+    std::vector<uint64_t> bm((size_t)NP * nw, 0);
+    std::vector<int32_t> cnt((size_t)NP * nw, 0);
+    s->present.assign((size_t)nw, 0);
+    parallel_for(nw, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t w = lo; w < hi; ++w) {
+            uint64_t pres = 0;
+            for (int64_t i = 0; i < 64 && w * 64 + i < A; ++i) {
+                uint64_t m = hold[w * 64 + i];
+                if (m) pres |= 1ull << i;
+                while (m) {
+                    bm[(size_t)__builtin_ctzll(m) * nw + w] |= 1ull << i;
+                    m &= m - 1;
                 }
-            });
-        for (auto& x : th) x.join();
-    }
-    const int64_t AL = (int64_t)s->l2g.size();
-    s->n_owned = A > part ? (A - part + NP - 1) / NP : 0;
-    s->own_l.resize((size_t)s->n_owned);
-    for (int64_t k = 0; k < s->n_owned; ++k) s->own_l[k] = g2l[part + k * NP];   // -1: isolated
-    s->ghost_count.assign(NP, 0);
+            }
+            s->present[w] = pres;
+        }
+    });
+    parallel_for(NP, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t q = lo; q < hi; ++q) {
+            int64_t run = 0;
+            for (int64_t w = 0; w < nw; ++w) {
+                cnt[(size_t)q * nw + w] = (int32_t)run;
+                run += __builtin_popcountll(bm[(size_t)q * nw + w]);
+            }
+        }
+    });
+    auto lid = [&](int q, int64_t v) -> int32_t {
+        const int64_t w = v >> 6;
+        return cnt[(size_t)q * nw + w] + __builtin_popcountll(bm[(size_t)q * nw + w] & ((1ull << (v & 63)) - 1ull));
+    };
+    // 3. local atoms of this part (ascending global ids) and their exchange partners
+    int64_t AL = 0;
+    for (int64_t w = 0; w < nw; ++w) AL += __builtin_popcountll(bm[(size_t)part * nw + w]);
+    s->l2g.resize((size_t)AL);
+    parallel_for(nw, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t w = lo; w < hi; ++w) {
+            uint64_t m = bm[(size_t)part * nw + w];
+            int64_t k = cnt[(size_t)part * nw + w];
+            while (m) {
+                s->l2g[k++] = (int32_t)(w * 64 + __builtin_ctzll(m));
+                m &= m - 1;
+            }
+        }
+    });
+    s->own_bm.assign((size_t)(AL / 64 + 2), 0);
+    s->xo_part.assign((size_t)AL, -1);
+    s->xo_lid.assign((size_t)AL, -1);
+    s->bc_off.assign((size_t)AL + 1, 0);
+    std::vector<int32_t> nbc((size_t)AL, 0);
+    parallel_for(AL, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {
+            const int64_t v = s->l2g[i];
+            const uint64_t h = hold[v];
+            const int o = owner_of(v, h);
+            if (o == part) nbc[i] = __builtin_popcountll(h) - 1;
+            else {
+                s->xo_part[i] = o;
+                s->xo_lid[i] = lid(o, v);
+            }
+        }
+    });
     for (int64_t i = 0; i < AL; ++i) {
-        const int o = s->l2g[i] % NP;
-        if (o != part) s->ghost_count[o]++;
+        s->bc_off[i + 1] = s->bc_off[i] + nbc[i];
+        if (s->xo_part[i] < 0) s->own_bm[i >> 6] |= 1ull << (i & 63);
     }
+    s->bc_part.resize((size_t)s->bc_off[AL]);
+    s->bc_lid.resize((size_t)s->bc_off[AL]);
+    parallel_for(AL, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {
+            if (!nbc[i]) continue;
+            const int64_t v = s->l2g[i];
+            uint64_t m = hold[v] & ~(1ull << part);
+            int64_t k = s->bc_off[i];
+            while (m) {
+                const int q = __builtin_ctzll(m);
+                m &= m - 1;
+                s->bc_part[k] = q;
+                s->bc_lid[k++] = lid(q, v);
+            }
+        }
+    });
+    s->ghost_count.assign(NP, 0);
+    s->bc_count.assign(NP, 0);
+    for (int64_t i = 0; i < AL; ++i)
+        if (s->xo_part[i] >= 0) s->ghost_count[s->xo_part[i]]++;
+    for (int32_t q : s->bc_part) s->bc_count[q]++;
+    s->n_owned = AL - std::accumulate(s->ghost_count.begin(), s->ghost_count.end(), (int64_t)0);
 
-    // 3. local link rows (ascending global row order) with targets in local ids
+    // 4. local link rows (ascending global row order) with targets in local ids
     std::vector<int64_t> lrow;
     lrow.reserve((size_t)(M / std::max(NP, 1) + 16));
     for (int64_t r = 0; r < M; ++r)
-        if (loc[r]) lrow.push_back(r);
+        if (link_part[r] == part) lrow.push_back(r);
     const int64_t ML = (int64_t)lrow.size();
     s->tgt_off.resize((size_t)ML + 1);
     s->link_atom.resize((size_t)ML);
@@ -163,7 +384,7 @@ hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part) {
             s->link_atom[i] = d->link_atom[r];
             s->link_type[i] = d->link_type ? d->link_type[r] : 0;
             int64_t o = s->tgt_off[i];
-            for (int64_t p = off[r]; p < off[r + 1]; ++p) s->tgt_idx[o++] = g2l[tg[p]];
+            for (int64_t p = off[r]; p < off[r + 1]; ++p) s->tgt_idx[o++] = lid(part, tg[p]);
         }
     });
     return s.release();
@@ -223,6 +444,8 @@ struct RcclTransport : Transport {
 // failing part releases the others instead of leaving them waiting.
 struct LocalHub {
     int world;
+    bool serial = false;   // rehearsal: one part's device work at a time (clean per-part device times)
+    std::mutex gate;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -257,6 +480,26 @@ struct LocalTransport : Transport {
     std::shared_ptr<LocalHub> hub;
     int device = 0;
     const char* kind() const override { return "local"; }
+    bool held = false;
+    void compute_begin(hipStream_t) override {
+        if (hub->serial && !held) {
+            hub->gate.lock();
+            held = true;
+        }
+    }
+    void compute_end(hipStream_t s) override {
+        if (!held) return;
+        hipError_t e = hipStreamSynchronize(s);   // this part's kernels have finished
+        held = false;
+        hub->gate.unlock();
+        HGX_HIP(e);
+    }
+    void compute_release(hipStream_t s) override {
+        if (!held) return;
+        (void)hipStreamSynchronize(s);
+        held = false;
+        hub->gate.unlock();
+    }
     void allgather_i64(const int64_t* in, int64_t n, int64_t* out, hipStream_t) override {
         hub->ag_in[rank] = in;
         hub->barrier();
@@ -285,15 +528,75 @@ struct LocalTransport : Transport {
     }
 };
 
+// Host-staged transport: the collectives are the caller's callbacks on host buffers (e.g. a
+// torch.distributed gloo group); device segments are staged through pinned host memory.  Used to
+// run the partitioned BFS between processes without RCCL (tests on one GPU).
+struct HostTransport : Transport {
+    hgx_host_allgather_fn ag = nullptr;
+    hgx_host_alltoallv_fn a2a = nullptr;
+    void* user = nullptr;
+    void* hs = nullptr;
+    void* hr = nullptr;
+    size_t hs_n = 0, hr_n = 0;
+    ~HostTransport() override {
+        if (hs) (void)hipHostFree(hs);
+        if (hr) (void)hipHostFree(hr);
+    }
+    const char* kind() const override { return "host"; }
+    static void grow(void*& p, size_t& n, size_t need) {
+        if (need <= n) return;
+        if (p) HGX_HIP(hipHostFree(p));
+        p = nullptr;
+        n = 0;
+        HGX_HIP(hipHostMalloc(&p, need));
+        n = need;
+    }
+    void allgather_i64(const int64_t* in, int64_t n, int64_t* out, hipStream_t) override {
+        if (ag(user, in, n, out) != 0) fail(HGX_E_DEVICE, "host transport: all-gather callback failed");
+    }
+    void alltoallv(const void* send, const int64_t* send_off, const int64_t* send_bytes, void* recv,
+                   const int64_t* recv_off, const int64_t* recv_bytes, hipStream_t s) override {
+        size_t sn = 1, rn = 1;
+        for (int p = 0; p < world; ++p) {
+            sn = std::max(sn, (size_t)(send_off[p] + send_bytes[p]));
+            rn = std::max(rn, (size_t)(recv_off[p] + recv_bytes[p]));
+        }
+        grow(hs, hs_n, sn);
+        grow(hr, hr_n, rn);
+        for (int p = 0; p < world; ++p)
+            if (send_bytes[p] > 0)
+                HGX_HIP(hipMemcpyAsync((char*)hs + send_off[p], (const char*)send + send_off[p], (size_t)send_bytes[p],
+                                       hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipStreamSynchronize(s));
+        if (a2a(user, hs, send_off, send_bytes, hr, recv_off, recv_bytes) != 0)
+            fail(HGX_E_DEVICE, "host transport: all-to-all callback failed");
+        for (int p = 0; p < world; ++p)
+            if (recv_bytes[p] > 0)
+                HGX_HIP(hipMemcpyAsync((char*)recv + recv_off[p], (const char*)hr + recv_off[p], (size_t)recv_bytes[p],
+                                       hipMemcpyHostToDevice, s));
+        HGX_HIP(hipStreamSynchronize(s));
+    }
+};
+
 }  // namespace
 
 extern "C" {
 
-int hgx_shard_build(const hgx_graph_desc* global, int32_t n_parts, int32_t part, hgx_shard** out) {
+int hgx_partition_plan(const hgx_graph_desc* global, int32_t n_parts, int32_t* link_part) {
+    HGX_API_BEGIN
+    if (!global || (global->num_links > 0 && !link_part)) fail(HGX_E_INVALID, "hgx_partition_plan: null argument");
+    if (n_parts < 1 || n_parts > 64) fail(HGX_E_INVALID, "hgx_partition_plan: n_parts must be 1..64");
+    check_rows(global);
+    plan_links(global, n_parts, link_part, 0.02);
+    HGX_API_END
+}
+
+int hgx_shard_build(const hgx_graph_desc* global, int32_t n_parts, int32_t part, const int32_t* link_part,
+                    hgx_shard** out) {
     HGX_API_BEGIN
     if (!global || !out) fail(HGX_E_INVALID, "hgx_shard_build: null argument");
     *out = nullptr;
-    *out = shard_build(global, n_parts, part);
+    *out = shard_build(global, n_parts, part, link_part);
     HGX_API_END
 }
 
@@ -321,6 +624,20 @@ int hgx_shard_export(const hgx_shard* s, int32_t* l2g, int32_t* link_atom, int32
     HGX_API_END
 }
 
+int hgx_shard_exchange_tables(const hgx_shard* s, int32_t* xo_part, int32_t* xo_lid, int64_t* bc_off,
+                              int32_t* bc_part, int32_t* bc_lid, int64_t* bc_count) {
+    HGX_API_BEGIN
+    if (!s) fail(HGX_E_INVALID, "null shard");
+    const size_t AL = s->l2g.size();
+    if (xo_part) std::memcpy(xo_part, s->xo_part.data(), sizeof(int32_t) * AL);
+    if (xo_lid) std::memcpy(xo_lid, s->xo_lid.data(), sizeof(int32_t) * AL);
+    if (bc_off) std::memcpy(bc_off, s->bc_off.data(), sizeof(int64_t) * (AL + 1));
+    if (bc_part) std::memcpy(bc_part, s->bc_part.data(), sizeof(int32_t) * s->bc_part.size());
+    if (bc_lid) std::memcpy(bc_lid, s->bc_lid.data(), sizeof(int32_t) * s->bc_lid.size());
+    if (bc_count) std::memcpy(bc_count, s->bc_count.data(), sizeof(int64_t) * s->bc_count.size());
+    HGX_API_END
+}
+
 void hgx_shard_free(hgx_shard* s) { delete s; }
 
 int hgx_shard_graph_create(const hgx_shard* s, int32_t device, hgx_graph** out) {
@@ -341,22 +658,23 @@ int hgx_shard_graph_create(const hgx_shard* s, int32_t device, hgx_graph** out) 
     sh->A_global = s->A_global;
     sh->n_owned = s->n_owned;
     sh->l2g_host = s->l2g;
-    sh->own_l_host = s->own_l;
+    sh->present_host = s->present;
+    sh->own_bm_host = s->own_bm;
     sh->ghost_count = s->ghost_count;
-    sh->ghost_start.assign(s->n_parts + 1, 0);
-    for (int p = 0; p < s->n_parts; ++p) sh->ghost_start[p + 1] = sh->ghost_start[p] + s->ghost_count[p];
-    sh->n_ghost = sh->ghost_start[s->n_parts];
-    std::vector<uint64_t> own((size_t)(AL / 64 + 2), 0);
-    for (int64_t i = 0; i < AL; ++i)
-        if (s->l2g[i] % s->n_parts == s->part) own[i >> 6] |= 1ull << (i & 63);
-    HGX_HIP(hipMalloc(&sh->l2g, sizeof(int32_t) * std::max<int64_t>(AL, 1)));
-    HGX_HIP(hipMalloc(&sh->own_l, sizeof(int32_t) * std::max<int64_t>(s->n_owned, 1)));
-    HGX_HIP(hipMalloc(&sh->own_bm, sizeof(uint64_t) * own.size()));
-    if (AL) HGX_HIP(hipMemcpyAsync(sh->l2g, s->l2g.data(), sizeof(int32_t) * AL, hipMemcpyHostToDevice, g->stream));
-    if (s->n_owned)
-        HGX_HIP(hipMemcpyAsync(sh->own_l, s->own_l.data(), sizeof(int32_t) * s->n_owned, hipMemcpyHostToDevice,
-                               g->stream));
-    HGX_HIP(hipMemcpyAsync(sh->own_bm, own.data(), sizeof(uint64_t) * own.size(), hipMemcpyHostToDevice, g->stream));
+    sh->bc_count = s->bc_count;
+    auto up = [&](auto*& dst, const auto& v, size_t min_n) {
+        using T = typename std::remove_reference<decltype(v)>::type::value_type;
+        const size_t n = std::max(v.size(), min_n);
+        HGX_HIP(hipMalloc(&dst, sizeof(T) * std::max<size_t>(n, 1)));
+        if (!v.empty())
+            HGX_HIP(hipMemcpyAsync(dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, g->stream));
+    };
+    up(sh->own_bm, s->own_bm, 1);
+    up(sh->xo_part, s->xo_part, 1);
+    up(sh->xo_lid, s->xo_lid, 1);
+    up(sh->bc_off, s->bc_off, 1);
+    up(sh->bc_part, s->bc_part, 1);
+    up(sh->bc_lid, s->bc_lid, 1);
     HGX_HIP(hipStreamSynchronize(g->stream));
     guard.g = nullptr;
     *out = g;
@@ -391,6 +709,24 @@ int hgx_comm_rccl_create(const uint8_t id[128], int32_t world, int32_t rank, int
     HGX_API_END
 }
 
+int hgx_comm_host_create(int32_t world, int32_t rank, hgx_host_allgather_fn allgather, hgx_host_alltoallv_fn alltoallv,
+                         void* user, hgx_comm** out) {
+    HGX_API_BEGIN
+    if (!out || !allgather || !alltoallv || world < 1 || rank < 0 || rank >= world)
+        fail(HGX_E_INVALID, "hgx_comm_host_create: bad argument");
+    *out = nullptr;
+    std::unique_ptr<HostTransport> t(new HostTransport());
+    t->world = world;
+    t->rank = rank;
+    t->ag = allgather;
+    t->a2a = alltoallv;
+    t->user = user;
+    hgx_comm* c = new hgx_comm();
+    c->t = t.release();
+    *out = c;
+    HGX_API_END
+}
+
 void hgx_comm_destroy(hgx_comm* c) {
     if (!c) return;
     delete c->t;
@@ -418,6 +754,7 @@ int hgx_pbfs_batch_group(hgx_graph* const* shards, int32_t n_parts, const int32_
             fail(HGX_E_INVALID, "hgx_pbfs_batch_group: shards[p] must be part p of n_parts");
     }
     auto hub = std::make_shared<LocalHub>(n_parts);
+    for (int p = 0; p < n_parts; ++p) hub->serial |= shards[p]->shard->serial;
     std::vector<std::unique_ptr<LocalTransport>> tr(n_parts);
     for (int p = 0; p < n_parts; ++p) {
         tr[p].reset(new LocalTransport());

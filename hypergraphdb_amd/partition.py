@@ -1,16 +1,20 @@
-"""Hash-partitioned snapshot and BFS over several GPUs (config 4).
+"""Partitioned snapshot and BFS over several GPUs (config 4).
 
 The reference's incidence index (HGStore.getIncidenceResultSet, C/HGStore.java:253) is split by
-atom: owner(atom) = atom % n_parts.  Part p holds the incidence rows of its atoms and the target
-rows of every link with an owned target; each BFS level it sends the rows it discovered for atoms
-owned elsewhere to their owners (one all-to-all per level: RCCL between processes, device copies
-inside one process).  Results are identical to ``bfs_batch`` on the whole snapshot
-(HGBreadthFirstTraversal + DefaultALGenerator, C/algorithms/HGBreadthFirstTraversal.java:49-66).
+LINK (vertex cut): every link row lives on one part (partition_plan: greedy placement next to the
+low-degree targets it shares), an atom is present on every part holding one of its links and owned
+by one of them.  Each BFS level every part expands its own links, ships its partial news for atoms
+owned elsewhere to their owners (reduce) and the owners ship the final news back (broadcast): RCCL
+between processes, device copies inside one process, or host-staged callbacks (a gloo group).
+Results are identical to ``bfs_batch`` on the whole snapshot (HGBreadthFirstTraversal +
+DefaultALGenerator, C/algorithms/HGBreadthFirstTraversal.java:49-66).
 
-  Shard.build(graph arrays, n_parts, part)      host partition (C ABI hgx_shard_build)
+  partition_plan(graph arrays, n_parts)         link placement (C ABI hgx_partition_plan)
+  Shard.build(graph arrays, n_parts, part, plan) host partition (hgx_shard_build)
   ShardSnapshot(shard, device)                  one part on one device
   pbfs_batch_group(shard_snapshots, seeds, d)   every part in this process (one thread per part)
-  RcclComm.create(ctx, device) + pbfs_batch     one part per process over RCCL
+  RcclComm.create(...) + pbfs_batch             one part per process over RCCL
+  HostComm.gloo(...) + pbfs_batch               one part per process over a torch.distributed group
   PartitionedBfsResult                          the union of the parts' results
 """
 from __future__ import annotations
@@ -24,6 +28,21 @@ from ._lib import check, lib, ptr
 from .algorithms import BfsResult, DefaultALGenerator
 
 
+def _desc(num_atoms, link_atom, tgt_off, tgt_idx, link_type):
+    arrs = (np.ascontiguousarray(link_atom, np.int32), np.ascontiguousarray(tgt_off, np.int64),
+            np.ascontiguousarray(tgt_idx, np.int32),
+            None if link_type is None else np.ascontiguousarray(link_type, np.int32))
+    return _lib.GraphDesc(int(num_atoms), len(arrs[0]), ptr(arrs[0]), ptr(arrs[1]), ptr(arrs[2]), ptr(arrs[3])), arrs
+
+
+def partition_plan(num_atoms, link_atom, tgt_off, tgt_idx, link_type, n_parts) -> np.ndarray:
+    """link_part[r] = the part that stores link row r (deterministic for a snapshot)."""
+    desc, keep = _desc(num_atoms, link_atom, tgt_off, tgt_idx, link_type)
+    out = np.zeros(max(len(keep[0]), 1), np.int32)
+    check(lib().hgx_partition_plan(C.byref(desc), int(n_parts), ptr(out)))
+    return out[: len(keep[0])]
+
+
 class Shard:
     """Host-side partition of one part (no device work)."""
 
@@ -35,15 +54,30 @@ class Shard:
         self.n_local, self.n_owned, self.n_links, self.n_pins = a.value, o.value, m.value, p.value
 
     @classmethod
-    def build(cls, num_atoms, link_atom, tgt_off, tgt_idx, link_type, n_parts, part):
-        link_atom = np.ascontiguousarray(link_atom, np.int32)
-        tgt_off = np.ascontiguousarray(tgt_off, np.int64)
-        tgt_idx = np.ascontiguousarray(tgt_idx, np.int32)
-        lt = None if link_type is None else np.ascontiguousarray(link_type, np.int32)
-        desc = _lib.GraphDesc(int(num_atoms), len(link_atom), ptr(link_atom), ptr(tgt_off), ptr(tgt_idx), ptr(lt))
+    def build(cls, num_atoms, link_atom, tgt_off, tgt_idx, link_type, n_parts, part, plan=None):
+        """plan: link_part from partition_plan (computed here when None)."""
+        if plan is None:
+            plan = partition_plan(num_atoms, link_atom, tgt_off, tgt_idx, link_type, n_parts)
+        plan = np.ascontiguousarray(plan, np.int32)
+        desc, keep = _desc(num_atoms, link_atom, tgt_off, tgt_idx, link_type)
         h = C.c_void_p()
-        check(lib().hgx_shard_build(C.byref(desc), int(n_parts), int(part), C.byref(h)))
+        check(lib().hgx_shard_build(C.byref(desc), int(n_parts), int(part), ptr(plan), C.byref(h)))
         return cls(h, int(n_parts), int(part))
+
+    def exchange_tables(self) -> dict:
+        """xo_part / xo_lid (owner and the atom's local id there, -1 for owned atoms), bc_off /
+        bc_part / bc_lid (each owned atom's other holders and its local id on each), bc_count."""
+        n = self.n_local
+        d = {"xo_part": np.empty(max(n, 1), np.int32), "xo_lid": np.empty(max(n, 1), np.int32),
+             "bc_off": np.empty(n + 1, np.int64), "bc_count": np.empty(self.n_parts, np.int64)}
+        check(lib().hgx_shard_exchange_tables(self._h, ptr(d["xo_part"]), ptr(d["xo_lid"]), ptr(d["bc_off"]), None,
+                                              None, ptr(d["bc_count"])))
+        m = int(d["bc_off"][-1])
+        d["bc_part"], d["bc_lid"] = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.int32)
+        check(lib().hgx_shard_exchange_tables(self._h, None, None, None, ptr(d["bc_part"]), ptr(d["bc_lid"]), None))
+        d["xo_part"], d["xo_lid"] = d["xo_part"][:n], d["xo_lid"][:n]
+        d["bc_part"], d["bc_lid"] = d["bc_part"][:m], d["bc_lid"][:m]
+        return d
 
     def export(self) -> dict:
         """The local tables (l2g, link_atom, link_type, tgt_off, tgt_idx in local ids, ghost_count)."""
@@ -92,6 +126,10 @@ class ShardSnapshot:
     def set_option(self, option, value):
         check(lib().hgx_set_option(self.handle, int(option), int(value)))
 
+    def set_serial(self, on=True):
+        """In-process rehearsal: the group runs its parts' device work one part at a time."""
+        self.set_option(_lib.HGX_OPT_PART_SERIAL, 1 if on else 0)
+
     def close(self):
         if getattr(self, "_h", None) is not None:
             lib().hgx_graph_destroy(self._h)
@@ -124,6 +162,99 @@ class RcclComm:
         h = C.c_void_p()
         check(lib().hgx_comm_rccl_create(buf, int(world), int(rank), int(device), C.byref(h)))
         return cls(h, world, rank)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().hgx_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_AG = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64))
+_A2A = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_void_p,
+                   C.POINTER(C.c_int64), C.POINTER(C.c_int64))
+
+
+class HostComm:
+    """Host-staged transport (hgx_comm_host_create): libhgx stages the exchange segments through
+    pinned host memory and calls ``allgather(in_array) -> out_array`` and
+    ``alltoallv(send_bytes_per_peer: list[bytes]) -> list[bytes]`` (Python callables) for the
+    collectives.  HostComm.gloo(group) wires them to a torch.distributed (gloo) group."""
+
+    def __init__(self, world, rank, allgather, alltoallv):
+        self.world, self.rank = world, rank
+        self._ag_py, self._a2a_py = allgather, alltoallv
+
+        def ag(_user, inp, n, out):
+            try:
+                a = np.ctypeslib.as_array(inp, (n,)).copy()
+                res = np.asarray(self._ag_py(a), np.int64).reshape(-1)
+                np.ctypeslib.as_array(out, (n * world,))[:] = res
+                return 0
+            except Exception:   # noqa: BLE001 -- reported as a transport failure
+                return 1
+
+        def a2a(_user, send, soff, sbytes, recv, roff, rbytes):
+            try:
+                so = np.ctypeslib.as_array(soff, (world,))
+                sb = np.ctypeslib.as_array(sbytes, (world,))
+                ro = np.ctypeslib.as_array(roff, (world,))
+                rb = np.ctypeslib.as_array(rbytes, (world,))
+                parts = [C.string_at(send + int(so[p]), int(sb[p])) if sb[p] > 0 else b"" for p in range(world)]
+                got = self._a2a_py(parts)
+                for p in range(world):
+                    if len(got[p]) != int(rb[p]):
+                        return 2
+                    if rb[p] > 0:
+                        C.memmove(recv + int(ro[p]), got[p], int(rb[p]))
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+
+        self._cb = (_AG(ag), _A2A(a2a))   # keep the trampolines alive
+        h = C.c_void_p()
+        check(lib().hgx_comm_host_create(int(world), int(rank), C.cast(self._cb[0], C.c_void_p),
+                                         C.cast(self._cb[1], C.c_void_p), None, C.byref(h)))
+        self._h = h
+
+    @classmethod
+    def gloo(cls, dist, world, rank):
+        """Collectives over an initialised torch.distributed (gloo) default group."""
+        import torch
+
+        def allgather(a):
+            t = torch.from_numpy(a)
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return np.concatenate([o.numpy() for o in out])
+
+        def alltoallv(parts):
+            sizes = torch.tensor([len(b) for b in parts], dtype=torch.int64)
+            allsz = [torch.empty_like(sizes) for _ in range(world)]
+            dist.all_gather(allsz, sizes)
+            recv_sz = [int(allsz[q][rank]) for q in range(world)]
+            reqs, bufs = [], [None] * world
+            for q in range(world):
+                if q == rank:
+                    bufs[q] = parts[q]
+                    continue
+                if len(parts[q]):
+                    reqs.append(dist.isend(torch.frombuffer(bytearray(parts[q]), dtype=torch.uint8), q))
+                if recv_sz[q]:
+                    bufs[q] = torch.empty(recv_sz[q], dtype=torch.uint8)
+                    reqs.append(dist.irecv(bufs[q], q))
+                else:
+                    bufs[q] = b""
+            for r in reqs:
+                r.wait()
+            return [b if isinstance(b, bytes) else b.numpy().tobytes() for b in bufs]
+
+        return cls(world, rank, allgather, alltoallv)
 
     def close(self):
         if getattr(self, "_h", None) is not None:
@@ -182,8 +313,14 @@ class PartitionedBfsResult:
         return np.sort(np.concatenate([p.visited(seed_index, depth) for p in self.parts]))
 
     def depth_of(self, seed_index, atom) -> int:
-        p = self.parts[int(atom) % len(self.parts)]
-        return p.depth_of(seed_index, atom)
+        """Asked of the owner part (the others answer HGX_E_NOTFOUND)."""
+        for p in self.parts:
+            try:
+                return p.depth_of(seed_index, atom)
+            except _lib.HGXError as e:
+                if e.code != _lib.HGX_E_NOTFOUND:
+                    raise
+        raise _lib.HGXError(_lib.HGX_E_NOTFOUND, f"no part owns atom {atom}")
 
     def stats(self, accounting=True) -> list:
         return [p.stats(accounting) for p in self.parts]

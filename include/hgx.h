@@ -121,9 +121,13 @@ typedef struct hgx_bfs_stats {
      * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
     int64_t level_rows[64][8];
     /* partitioned BFS (hgx_pbfs_batch): device ms of the per-level exchange (pack, transport,
-     * apply, frontier count) and the ghost-row bytes this part sent */
+     * apply, frontier count) and the row bytes this part sent (reduce + broadcast) */
     double  ms_exchange;
     double  bytes_exchanged;
+    double  level_xbytes[64];          /* bytes this part sent at level d                      */
+    double  level_xpair_max[64];       /* the largest of those per destination part at level d */
+    double  level_xms[64];             /* device ms of the exchange kernels of level d (timing on) */
+    double  xwords_nonzero, xwords_total;   /* row words shipped: nonzero / all (compression headroom) */
     /* minimum-bytes model of the whole batch (with accounting): per expanded level, the CSR slices
      * of the frontier atoms or every CSR column once (whichever is less) + one S/8-byte row per
      * frontier atom read + one per new atom written */
@@ -295,44 +299,69 @@ int  hgx_query_result_ms(const hgx_query_result *r, double *ms_total, double *ms
 void hgx_query_result_free(hgx_query_result *r);
 
 /* ---------------------------------------------------------------------------------------------
- * Hash-partitioned snapshot and BFS (config 4: graphs sharded over the GPUs of a node).
+ * Partitioned snapshot and BFS (config 4: graphs sharded over the GPUs of a node).
  *
  * Replaces the same HGBreadthFirstTraversal/DefaultALGenerator loop as hgx_bfs_batch
  * (C/algorithms/HGBreadthFirstTraversal.java:49-66, C/algorithms/DefaultALGenerator.java:287-315)
- * when the incidence index (HGStore.getIncidenceResultSet, C/HGStore.java:253) is split by atom
- * over n_parts devices.  owner(atom) = atom % n_parts.  Part p holds the incidence rows of its
- * atoms and the target rows of every link with at least one target it owns; each level it sends
- * the rows it found for atoms owned elsewhere to their owners (one all-to-all per level).
- * Results are bit-identical to hgx_bfs_batch on the whole graph.
+ * when the incidence index (HGStore.getIncidenceResultSet, C/HGStore.java:253) is split over
+ * n_parts devices.  Vertex cut: every link row lives on exactly one part (link_part[r]); an atom is
+ * present on every part that holds one of its links and is owned by one of them.  Each level every
+ * part expands its own links, ships its partial news for atoms owned elsewhere to their owners
+ * (reduce) and each owner ships the final news back to the other holders (broadcast).  Results are
+ * bit-identical to hgx_bfs_batch on the whole graph.
  * -------------------------------------------------------------------------------------------- */
 typedef struct hgx_shard hgx_shard;   /* host-side partition of one part */
 typedef struct hgx_comm hgx_comm;     /* the group's transport            */
 
-/* Build part `part` of n_parts from the whole snapshot (host only, no device work). */
-int  hgx_shard_build(const hgx_graph_desc *global, int32_t n_parts, int32_t part, hgx_shard **out);
-/* n_local = owned + ghost atoms; local links / pins = the replicated link rows of this part. */
+/* Link placement over n_parts (1..64): greedy streaming vertex cut (a link goes to the part that
+ * already holds most of its low-degree targets, within a 2% pin-balance cap).  Deterministic: every
+ * rank computes the same link_part[num_links] from the same snapshot.  Host only. */
+int  hgx_partition_plan(const hgx_graph_desc *global, int32_t n_parts, int32_t *link_part);
+/* Build part `part` of n_parts for a placement (host only, no device work). */
+int  hgx_shard_build(const hgx_graph_desc *global, int32_t n_parts, int32_t part, const int32_t *link_part,
+                     hgx_shard **out);
+/* n_local = atoms present on this part (owned + ghosts); local links / pins = this part's link rows. */
 int  hgx_shard_info(const hgx_shard *s, int64_t *n_local, int64_t *n_owned, int64_t *n_local_links,
                     int64_t *n_local_pins);
 /* Copies of the local tables (any pointer may be NULL): l2g[n_local] global id of each local atom
  * (ascending); link_atom/link_type[n_local_links] global link atom id / type of each local link;
- * tgt_off[n_local_links+1], tgt_idx[n_local_pins] targets in LOCAL ids; ghost_count[n_parts]. */
+ * tgt_off[n_local_links+1], tgt_idx[n_local_pins] targets in LOCAL ids; ghost_count[n_parts] = my
+ * ghosts owned by each part. */
 int  hgx_shard_export(const hgx_shard *s, int32_t *l2g, int32_t *link_atom, int32_t *link_type,
                       int64_t *tgt_off, int32_t *tgt_idx, int64_t *ghost_count);
+/* The exchange tables: xo_part/xo_lid[n_local] = owner part and the atom's local id there (-1 for
+ * owned atoms); bc_off[n_local+1] / bc_part / bc_lid = for each owned atom its other holders and
+ * its local id on each (bc_off[n_local] entries); bc_count[n_parts] = entries per part. */
+int  hgx_shard_exchange_tables(const hgx_shard *s, int32_t *xo_part, int32_t *xo_lid, int64_t *bc_off,
+                               int32_t *bc_part, int32_t *bc_lid, int64_t *bc_count);
 void hgx_shard_free(hgx_shard *s);
 /* Upload a part to a device (incidence build as in hgx_graph_create).  The result is an hgx_graph
- * that only hgx_pbfs_batch (+ the hgx_bfs_result_* readers) accepts. */
+ * that only hgx_pbfs_batch / hgx_pbfs_batch_group (+ the hgx_bfs_result_* readers) accept.
+ * hgx_set_option(shard_graph, HGX_OPT_PART_SERIAL, 1) makes an in-process group run its parts'
+ * device work one part at a time (clean per-part device times for a one-GPU rehearsal). */
 int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out);
+#define HGX_OPT_PART_SERIAL 4
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
  * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */
 int  hgx_comm_rccl_unique_id(uint8_t id[128]);
 int  hgx_comm_rccl_create(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, hgx_comm **out);
+/* Host-staged transport: the collectives are callbacks on HOST buffers (return 0 on success).
+ * allgather: out[r*n + i] = in[i] of rank r.  alltoallv: rank p receives send_bytes[p] bytes of
+ * send + send_off[p]; this rank receives recv_bytes[p] bytes from rank p into recv + recv_off[p]. */
+typedef int (*hgx_host_allgather_fn)(void *user, const int64_t *in, int64_t n, int64_t *out);
+typedef int (*hgx_host_alltoallv_fn)(void *user, const void *send, const int64_t *send_off,
+                                     const int64_t *send_bytes, void *recv, const int64_t *recv_off,
+                                     const int64_t *recv_bytes);
+int  hgx_comm_host_create(int32_t world, int32_t rank, hgx_host_allgather_fn allgather,
+                          hgx_host_alltoallv_fn alltoallv, void *user, hgx_comm **out);
 void hgx_comm_destroy(hgx_comm *c);
 
 /* One part's share of a partitioned batched BFS (collective: every part calls it with the same
- * seeds, depth and options).  seeds are GLOBAL atom ids.  The result reports this part's atoms:
- * counts are partial (sum them over parts), visited lists hold global ids (disjoint over parts),
- * depth_of accepts only atoms this part owns (else HGX_E_NOTFOUND). */
+ * seeds, depth and options).  seeds are GLOBAL atom ids.  The result reports this part's OWNED
+ * atoms: counts are partial (sum them over parts), visited lists hold global ids (disjoint over
+ * parts), depth_of accepts only atoms this part owns (else HGX_E_NOTFOUND); the TEPS numerator of
+ * the stats sums over parts to the whole graph's. */
 int  hgx_pbfs_batch(hgx_graph *shard, hgx_comm *comm, const int32_t *seeds, int32_t n_seeds,
                     int32_t max_depth, const hgx_algen_opts *opts, hgx_bfs_result **out);
 /* All parts in this process: shards[p] is part p (any devices, including one device for all);
