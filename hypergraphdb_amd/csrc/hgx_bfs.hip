@@ -206,6 +206,7 @@ constexpr int kNtOut = 1 << 14;    // nontemporal stores of the pull's lvl_next 
 // probe kept both levels were slower; neither the `ever` bit nor the full-skip state of the level
 // separates the two cases (profiles/r01i_ab_heavy*.log), so the default keeps pull_range.
 constexpr int kHeavyMlp2 = 1 << 15;
+constexpr int kGatherO5 = 1 << 10;   // diagnostic: the dense gather built at 5 waves/SIMD (spills)
 
 template <typename T>
 __device__ __forceinline__ T ld_col(const T* p, bool nt) {
@@ -545,13 +546,12 @@ __global__ void __launch_bounds__(256) hgx_atom_pull(int64_t A, const int64_t* _
 // rows) cost one load.
 // ---------------------------------------------------------------------------------------------
 template <int W, bool WRITE_LF>
-__global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t* __restrict__ tgt_off,
-                                                        const int32_t* __restrict__ tgt_idx,
-                                                        const int32_t* __restrict__ link_type, int32_t want_type,
-                                                        const u64* __restrict__ fa, const u64* __restrict__ full,
-                                                        const u64* __restrict__ lvl, u64* __restrict__ lf,
-                                                        u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm,
-                                                        int flags) {
+__device__ __forceinline__ void gather2_body(int64_t M, const int64_t* __restrict__ tgt_off,
+                                             const int32_t* __restrict__ tgt_idx,
+                                             const int32_t* __restrict__ link_type, int32_t want_type,
+                                             const u64* __restrict__ fa, const u64* __restrict__ full,
+                                             const u64* __restrict__ lvl, u64* __restrict__ lf,
+                                             u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm, int flags) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
     static_assert(G >= 4, "gather2 needs G >= 4");
     typedef Vec<WPL> V;
@@ -649,6 +649,29 @@ __global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t
     }
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
+}
+
+template <int W, bool WRITE_LF>
+__global__ void __launch_bounds__(256) hgx_link_gather2(int64_t M, const int64_t* __restrict__ tgt_off,
+                                                        const int32_t* __restrict__ tgt_idx,
+                                                        const int32_t* __restrict__ link_type, int32_t want_type,
+                                                        const u64* __restrict__ fa, const u64* __restrict__ full,
+                                                        const u64* __restrict__ lvl, u64* __restrict__ lf,
+                                                        u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm,
+                                                        int flags) {
+    gather2_body<W, WRITE_LF>(M, tgt_off, tgt_idx, link_type, want_type, fa, full, lvl, lf, la, ctr, fm, flags);
+}
+
+// Diagnostic only (HGX_OPT_BFS_FLAGS bit 10, A/B): the same gather forced to 5 waves/SIMD, which
+// makes the compiler spill ~47 VGPRs per lane to scratch (round 1 saw wrong
+// level sizes from such a build; tools/ab_bfs.py compares its per-source results with the default).
+template <int W, bool WRITE_LF>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5)))
+hgx_link_gather2_o5(int64_t M, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+                    const int32_t* __restrict__ link_type, int32_t want_type, const u64* __restrict__ fa,
+                    const u64* __restrict__ full, const u64* __restrict__ lvl, u64* __restrict__ lf,
+                    u64* __restrict__ la, u64* __restrict__ ctr, FullMask fm, int flags) {
+    gather2_body<W, WRITE_LF>(M, tgt_off, tgt_idx, link_type, want_type, fa, full, lvl, lf, la, ctr, fm, flags);
 }
 
 template <int W, int JBX = 2>
@@ -1981,35 +2004,75 @@ __global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa,
 // ---------------------------------------------------------------------------------------------
 constexpr int kRecHdr = 2;
 
-// Reserve one record slot per lane in its destination's segment (wave-aggregated atomics, one per
-// distinct destination of the wave).  dest < 0: no record.
-__device__ __forceinline__ int64_t reserve_slot(int dest, u64* __restrict__ cursor, const int64_t* __restrict__ seg_start) {
-    const int lane = threadIdx.x & 63;
-    const u64 lt = (1ull << lane) - 1ull;
-    u64 left = __ballot(dest >= 0);
-    int64_t slot = -1;
-    while (left) {
-        const int leader = __ffsll((long long)left) - 1;
-        const int d = __shfl(dest, leader);
-        const u64 m = __ballot(dest == d);
-        u64 base = 0;
-        if (lane == leader) base = atomicAdd(&cursor[d], (u64)__popcll(m));
-        base = __shfl(base, leader);
-        if (dest == d) slot = seg_start[d] + (int64_t)base + __popcll(m & lt);
-        left &= ~m;
-    }
-    return slot;
+// Record slots are reserved per BLOCK: a block walks a contiguous range of tiles twice -- pass 1
+// counts its records per destination in LDS, one global atomic per destination claims the block's
+// range (cursors kCurStride words apart, each on its own cache line), pass 2 writes the records at
+// LDS-counted offsets.  One atomic per wave per destination (7 cursors on one line) serialised to
+// ~25 ms a level at config-4 scale.
+constexpr int kCurStride = 16;
+constexpr int kMaxParts = 64;
+
+struct PackLds {
+    unsigned int cnt[kMaxParts];
+    unsigned long long base[kMaxParts];
+};
+
+// per-lane destination of record k of this lane's atom, -1 = none
+__device__ __forceinline__ int64_t block_slot(int dest, PackLds& sh, const int64_t* __restrict__ seg_start) {
+    if (dest < 0) return -1;
+    const unsigned int off = atomicAdd(&sh.cnt[dest], 1u);
+    return seg_start[dest] + (int64_t)sh.base[dest] + off;
 }
 
+// Header of a record: the receiver's local id (16-byte store; two 8-byte stores when W == 1 and
+// the record is only 8-byte aligned).
 template <int W>
-__device__ __forceinline__ void write_record(u64* __restrict__ send, int64_t slot, int32_t lid, const u64* __restrict__ row) {
-    u64* rec = send + slot * (W + kRecHdr);
-    *reinterpret_cast<u64x2*>(rec) = u64x2{(u64)(uint32_t)lid, 0ull};
-#pragma unroll
-    for (int w = 0; w < W; w += 2) {
-        if constexpr (W == 1) rec[kRecHdr] = row[0];
-        else *reinterpret_cast<u64x2*>(rec + kRecHdr + w) = *reinterpret_cast<const u64x2*>(row + w);
+__device__ __forceinline__ void write_header(u64* rec, int32_t lid) {
+    if constexpr (((W + kRecHdr) & 1) == 0) {
+        *reinterpret_cast<u64x2*>(rec) = u64x2{(u64)(uint32_t)lid, 0ull};
+    } else {
+        rec[0] = (u64)(uint32_t)lid;
+        rec[1] = 0ull;
     }
+}
+
+// Copy the rows of the set bits of hits (atoms t0 + b) into their records: one G-lane group per
+// row, 16 bytes per lane (a row is one coalesced 128-byte access at W = 16).  slot / lid come from
+// lane b.  Wave-uniform call.
+template <int W>
+__device__ __forceinline__ u64 copy_rows(u64 hits, int64_t t0, int64_t slot, int32_t lid, const u64* __restrict__ lvl,
+                                         u64* __restrict__ send) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
+    typedef Vec<WPL> V;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int n = __popcll(hits);
+    u64 nz = 0;
+    for (int r0 = 0; r0 < n; r0 += PER) {   // wave-uniform
+        const int j = r0 + g;
+        const int b = j < n ? nth_set_bit(hits, j) : 0;
+        const int64_t s_slot = __shfl(slot, b);
+        const int32_t s_lid = __shfl(lid, b);
+        if (j < n) {
+            const typename V::T row = V::ld(lvl + (t0 + b) * W + sub * WPL);
+            u64* rec = send + s_slot * (W + kRecHdr);
+            if (sub == 0) write_header<W>(rec, s_lid);
+            if constexpr (WPL == 1) {
+                rec[kRecHdr + sub] = row;
+                nz += row != 0ull;
+            } else {
+                *reinterpret_cast<u64x2*>(rec + kRecHdr + sub * WPL) = row;
+                nz += (row.x != 0ull) + (row.y != 0ull);
+            }
+        }
+    }
+    return nz;
+}
+
+// The tiles of block b: [b * per, min((b + 1) * per, ntiles)).
+__device__ __forceinline__ void block_tiles(int64_t ntiles, int64_t& lo, int64_t& hi) {
+    const int64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    lo = (int64_t)blockIdx.x * per;
+    hi = lo + per < ntiles ? lo + per : ntiles;
 }
 
 template <int W>
@@ -2017,22 +2080,32 @@ __global__ void __launch_bounds__(256) hgx_xr_pack(int64_t A, const u64* __restr
                                                    const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
                                                    const int32_t* __restrict__ xo_lid, const u64* __restrict__ lvl_next,
                                                    u64* __restrict__ cursor, const int64_t* __restrict__ seg_start,
-                                                   u64* __restrict__ send, u64* __restrict__ nzw) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+                                                   u64* __restrict__ send, u64* __restrict__ nzw, int NP) {
+    __shared__ PackLds sh;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t lo, hi;
+    block_tiles((A + 63) / 64, lo, hi);
+    for (int d = threadIdx.x; d < NP; d += 256) sh.cnt[d] = 0;
+    __syncthreads();
+    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 1: counts per destination
+        const u64 gh = fa_next[tile] & ~own_bm[tile];
+        if ((gh >> lane) & 1ull) atomicAdd(&sh.cnt[xo_part[tile * 64 + lane]], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < NP; d += 256) {
+        const unsigned int c = sh.cnt[d];
+        sh.base[d] = c ? atomicAdd(&cursor[d * kCurStride], (u64)c) : 0ull;
+        sh.cnt[d] = 0;
+    }
+    __syncthreads();
     u64 nz = 0;
-    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2: the records
         const u64 gh = fa_next[tile] & ~own_bm[tile];
         if (gh == 0) continue;   // wave-uniform
         const int64_t t = tile * 64 + lane;
         const bool hit = (gh >> lane) & 1ull;
-        const int64_t slot = reserve_slot(hit ? xo_part[t] : -1, cursor, seg_start);
-        if (hit) {
-            const u64* row = lvl_next + t * W;
-            write_record<W>(send, slot, xo_lid[t], row);
-            for (int w = 0; w < W; ++w) nz += row[w] != 0ull;
-        }
+        const int64_t slot = block_slot(hit ? xo_part[t] : -1, sh, seg_start);
+        nz += copy_rows<W>(gh, tile * 64, slot, hit ? xo_lid[t] : 0, lvl_next, send);
     }
     wave_add(nzw, nz);
 }
@@ -2043,89 +2116,86 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
                                                    const int32_t* __restrict__ bc_part, const int32_t* __restrict__ bc_lid,
                                                    const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
                                                    const int64_t* __restrict__ seg_start, u64* __restrict__ send,
-                                                   u64* __restrict__ nzw) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+                                                   u64* __restrict__ nzw, int NP) {
+    __shared__ PackLds sh;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t lo, hi;
+    block_tiles((A + 63) / 64, lo, hi);
+    for (int d = threadIdx.x; d < NP; d += 256) sh.cnt[d] = 0;
+    __syncthreads();
+    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 1
+        const u64 ow = fa_next[tile] & own_bm[tile];
+        if ((ow >> lane) & 1ull) {
+            const int64_t t = tile * 64 + lane;
+            for (int64_t e = bc_off[t]; e < bc_off[t + 1]; ++e) atomicAdd(&sh.cnt[bc_part[e]], 1u);
+        }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < NP; d += 256) {
+        const unsigned int c = sh.cnt[d];
+        sh.base[d] = c ? atomicAdd(&cursor[d * kCurStride], (u64)c) : 0ull;
+        sh.cnt[d] = 0;
+    }
+    __syncthreads();
     u64 nz = 0;
-    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
+    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2
         const u64 ow = fa_next[tile] & own_bm[tile];
         if (ow == 0) continue;   // wave-uniform
         const int64_t t = tile * 64 + lane;
         const bool hit = (ow >> lane) & 1ull;
-        int64_t b = 0, n = 0;
+        int64_t b = 0;
+        int n = 0;
         if (hit) {
             b = bc_off[t];
-            n = bc_off[t + 1] - b;
+            n = (int)(bc_off[t + 1] - b);
         }
-        int nmax = (int)n;
+        int nmax = n;
         for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
         for (int k = 0; k < nmax; ++k) {   // wave-uniform: the k-th other holder of every lane's atom
             const bool has = k < n;
-            const int64_t slot = reserve_slot(has ? bc_part[b + k] : -1, cursor, seg_start);
-            if (has) {
-                const u64* row = lvl_next + t * W;
-                write_record<W>(send, slot, bc_lid[b + k], row);
-                for (int w = 0; w < W; ++w) nz += row[w] != 0ull;
-            }
+            const int64_t slot = block_slot(has ? bc_part[b + k] : -1, sh, seg_start);
+            nz += copy_rows<W>(__ballot(has), tile * 64, slot, has ? bc_lid[b + k] : 0, lvl_next, send);
         }
     }
     wave_add(nzw, nz);
 }
 
-// reduce side: one source segment (every atom at most once)
-template <int W>
-__global__ void __launch_bounds__(256) hgx_xr_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
-                                                    u64* __restrict__ fa_next, u64* __restrict__ vis,
-                                                    u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const u64* rec = recv + i * (W + kRecHdr);
-        const int64_t t = (int64_t)(uint32_t)rec[0];
-        const bool ev = bit(ever, t), was = bit(fa_next, t);
-        bool any = false, isfull = true;
-        u64* lv = lvl_next + t * W;
-        u64* vs = vis + t * W;
-        for (int w = 0; w < W; ++w) {
-            const u64 old = ev ? vs[w] : 0ull;
-            const u64 nw = rec[kRecHdr + w] & ~old;
-            any |= nw != 0ull;
-            isfull &= (old | nw) == fm.w[w];
+// Apply n received records, one G-lane group each.  REDUCE: OR a partial row into an owned atom
+// (new = row & ~vis; a source sends an atom at most once, so one launch per source segment);
+// BROADCAST: a ghost's final row replaces the partial one (each ghost gets exactly one record).
+template <int W, bool REDUCE>
+__global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
+                                                   u64* __restrict__ fa_next, u64* __restrict__ vis,
+                                                   u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
+    typedef Vec<WPL> V;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    for (int64_t base = wave * PER; base < n; base += nwave * PER) {   // wave-uniform
+        const int64_t i = base + g;
+        const bool valid = i < n;
+        const u64* rec = recv + (valid ? i : 0) * (W + kRecHdr);
+        const int64_t t = valid ? (int64_t)(uint32_t)rec[0] : 0;
+        const typename V::T row = valid ? V::ld(rec + kRecHdr + sub * WPL) : V::zero();
+        const bool ev = valid && bit(ever, t);
+        const bool was = valid && bit(fa_next, t);
+        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const typename V::T nw = REDUCE ? (row & ~old) : row;
+        const bool any = group_any<G>(V::nz(nw));
+        const bool isfull = group_all<G>(V::eq(old | nw, FULL));
+        if (valid && (any || !REDUCE)) {
+            typename V::T lv = nw;
+            if (REDUCE && was) lv = V::ld(lvl_next + t * W + sub * WPL) | nw;
+            V::st(lvl_next + t * W + sub * WPL, lv);
+            V::st(vis + t * W + sub * WPL, old | nw);
+            if (sub == 0) {
+                if (!was) set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (isfull) set_bit(full, t);
+            }
         }
-        if (!any) continue;
-        for (int w = 0; w < W; ++w) {
-            const u64 old = ev ? vs[w] : 0ull;
-            const u64 nw = rec[kRecHdr + w] & ~old;
-            lv[w] = was ? (lv[w] | nw) : nw;
-            vs[w] = old | nw;
-        }
-        if (!was) set_bit(fa_next, t);
-        if (!ev) set_bit(ever, t);
-        if (isfull) set_bit(full, t);
-    }
-}
-
-// broadcast side: every ghost receives exactly one record (from its owner)
-template <int W>
-__global__ void __launch_bounds__(256) hgx_xb_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
-                                                    u64* __restrict__ fa_next, u64* __restrict__ vis,
-                                                    u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const u64* rec = recv + i * (W + kRecHdr);
-        const int64_t t = (int64_t)(uint32_t)rec[0];
-        const bool ev = bit(ever, t), was = bit(fa_next, t);
-        bool isfull = true;
-        u64* lv = lvl_next + t * W;
-        u64* vs = vis + t * W;
-        for (int w = 0; w < W; ++w) {
-            const u64 r = rec[kRecHdr + w];
-            const u64 v = (ev ? vs[w] : 0ull) | r;
-            lv[w] = r;
-            vs[w] = v;
-            isfull &= v == fm.w[w];
-        }
-        if (!was) set_bit(fa_next, t);
-        if (!ev) set_bit(ever, t);
-        if (isfull) set_bit(full, t);
     }
 }
 
@@ -2338,7 +2408,7 @@ struct Exchange {
         cap_recs = std::max<int64_t>(std::max(rseg[NP], bseg[NP]), 1);
         send = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
         recv = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
-        dctr = (u64*)g->alloc(sizeof(u64) * (NP + 4));
+        dctr = (u64*)g->alloc(sizeof(u64) * (NP * kCurStride + 4));
         seg = (int64_t*)g->alloc(sizeof(int64_t) * 2 * NP);
         HGX_HIP(hipMemcpyAsync(seg, rseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
         HGX_HIP(hipMemcpyAsync(seg + NP, bseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
@@ -2347,7 +2417,7 @@ struct Exchange {
         const int NP = g->shard->n_parts;
         g->release(send, sizeof(u64) * (size_t)cap_recs * rec_words);
         g->release(recv, sizeof(u64) * (size_t)cap_recs * rec_words);
-        g->release(dctr, sizeof(u64) * (NP + 4));
+        g->release(dctr, sizeof(u64) * (NP * kCurStride + 4));
         g->release(seg, sizeof(int64_t) * 2 * NP);
     }
     // collective step: the part's device work is bracketed by compute_begin / compute_end
@@ -2391,53 +2461,59 @@ struct Exchange {
         hipStream_t s = g->stream;
         const int64_t A = g->A;
         const int grid = grid_for(ceil_div(A, 64) * 64, 256, 4096);
+        const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(A, 64) / 4 + 1, 2048));
         const double before = bytes_sent;
         *pair_max = 0;
-        std::vector<u64> cnt(NP + 4);
+        const size_t cbytes = sizeof(u64) * (NP * kCurStride + 4);
+        u64* xs = dctr + NP * kCurStride;   // [0..1] frontier stats, [2] nonzero words
+        std::vector<u64> hc(NP * kCurStride + 4), cnt(NP);
         std::vector<int64_t> rcnt;
+        auto read_counts = [&]() {
+            HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+            for (int q = 0; q < NP; ++q) {
+                cnt[q] = hc[(size_t)q * kCurStride];
+                words += (double)cnt[q] * Wt;
+            }
+            nz_words += (double)hc[(size_t)NP * kCurStride + 2];
+        };
         // reduce: partial rows of my ghosts -> their owners
         Events e0 = tm.start(kKindExchange, d);
-        HGX_HIP(hipMemsetAsync(dctr, 0, sizeof(u64) * (NP + 4), s));
-        hgx_xr_pack<Wt><<<grid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_lid, lvl_next, dctr, seg, send,
-                                             dctr + NP + 2);
+        HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+        hgx_xr_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_lid, lvl_next, dctr,
+                                              seg, send, xs + 2, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e0);
-        HGX_HIP(hipMemcpyAsync(cnt.data(), dctr, sizeof(u64) * (NP + 4), hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
-        nz_words += (double)cnt[NP + 2];
-        for (int q = 0; q < NP; ++q) words += (double)cnt[q] * Wt;
+        read_counts();
         ship(rseg, bseg, cnt, rcnt, *pair_max);
         Events e1 = tm.start(kKindExchange, d);
         for (int q = 0; q < NP; ++q) {
             if (q == me || rcnt[q] == 0) continue;
-            hgx_xr_apply<Wt><<<grid_for(rcnt[q], 256, 8192), 256, 0, s>>>(
+            hgx_x_apply<Wt, true><<<grid_for(ceil_div(rcnt[q], 64 / Lay<Wt>::G) * 64, 256, 8192), 256, 0, s>>>(
                 rcnt[q], recv + bseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
         }
         // broadcast: final rows of my owned atoms -> their other holders
-        HGX_HIP(hipMemsetAsync(dctr, 0, sizeof(u64) * (NP + 4), s));
-        hgx_xb_pack<Wt><<<grid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid, lvl_next, dctr,
-                                             seg + NP, send, dctr + NP + 2);
+        HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+        hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
+                                              lvl_next, dctr, seg + NP, send, xs + 2, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
-        HGX_HIP(hipMemcpyAsync(cnt.data(), dctr, sizeof(u64) * (NP + 4), hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
-        nz_words += (double)cnt[NP + 2];
-        for (int q = 0; q < NP; ++q) words += (double)cnt[q] * Wt;
+        read_counts();
         ship(bseg, rseg, cnt, rcnt, *pair_max);
         Events e2 = tm.start(kKindExchange, d);
         for (int q = 0; q < NP; ++q) {
             if (q == me || rcnt[q] == 0) continue;
-            hgx_xb_apply<Wt><<<grid_for(rcnt[q], 256, 8192), 256, 0, s>>>(
+            hgx_x_apply<Wt, false><<<grid_for(ceil_div(rcnt[q], 64 / Lay<Wt>::G) * 64, 256, 8192), 256, 0, s>>>(
                 rcnt[q], recv + rseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
         }
-        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, g->inc_off,
-                                                                               dctr + NP);
+        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm,
+                                                                               g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
         u64 fs[2];
-        HGX_HIP(hipMemcpyAsync(fs, dctr + NP, sizeof(fs), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipMemcpyAsync(fs, xs, sizeof(fs), hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
         *push_volume = fs[1];
         *level_bytes = bytes_sent - before;
@@ -2727,10 +2803,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         if constexpr (Lay<W>::G >= 4) {
             if (v2)
             {
-                // Forcing more waves/SIMD (amdgpu_waves_per_eu) spills VGPRs: 4 waves ran 6% faster but 5
-                // waves returned wrong frontiers (spills around the group shuffles), so no variant ships.
-                hgx_link_gather2<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
-                    M, g->tgt_off, g->tgt_idx, g->link_type, want_type, fa, full, lvl, lf, la, c, fm, lflags);
+                if (lflags & kGatherO5)   // diagnostic A/B (bit 10)
+                    hgx_link_gather2_o5<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
+                        M, g->tgt_off, g->tgt_idx, g->link_type, want_type, fa, full, lvl, lf, la, c, fm, lflags);
+                else
+                    hgx_link_gather2<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
+                        M, g->tgt_off, g->tgt_idx, g->link_type, want_type, fa, full, lvl, lf, la, c, fm, lflags);
             }
         }
         if (!v2)

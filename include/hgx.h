@@ -165,6 +165,7 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                              every traversal pull those atoms straight from the frontier rows,
  *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
  *                              before this level's counters reach the host,
+ *                      bit 10 = the dense gather built for 5 waves/SIMD (spills VGPRs; diagnostic A/B only),
  *                      bit 11 = the dense pull interleaves four atoms per lane group instead of two
  *                              (A/B only),
  *                      bits 12 / 13 / 14 = nontemporal loads of the streamed CSR columns / stores of
