@@ -205,16 +205,17 @@ def _kernel_roof(stats_list):
 
 def run_config4(args, ctx, barrier_sync, result):
     """Config 4 (1B incidences) in its two multi-GPU forms:
-      replicated  -- every GPU holds the whole snapshot (compacted one-part shard, ~16 GB of CSR)
-                     and runs its own 1024-source batch (weak scaling: throughput of the batch
-                     workload, no data-path collective);
-      partitioned -- the snapshot is hash-partitioned over the N GPUs (owner = atom % N) and the
-                     same 1024 sources run together, one RCCL all-to-all of ghost rows per level
-                     (strong scaling; the path for graphs beyond one GPU's 288 GB).
+      replicated  -- every GPU holds the whole snapshot (one-part shard, ~16 GB of CSR) and runs its
+                     own 1024-source batch (weak scaling: throughput of the batch workload, no
+                     data-path collective);
+      partitioned -- the snapshot is split over the N GPUs as a vertex cut (every link on one part,
+                     hgx_partition_plan) and the same 1024 sources run together: per level each part
+                     expands its own links, then reduce + broadcast of the new rows over RCCL
+                     (strong scaling; hgx_pbfs_batch).
     Fills result[...] in place so a watchdog can still report what finished."""
     from hypergraphdb_amd import dist as hdist
     from hypergraphdb_amd import synth
-    from hypergraphdb_amd.partition import RcclComm, Shard, ShardSnapshot, pbfs_batch, pbfs_batch_group
+    from hypergraphdb_amd.partition import RcclComm, Shard, ShardSnapshot, partition_plan, pbfs_batch, pbfs_batch_group
     rank, world, local = ctx.rank, ctx.world, ctx.device
     t0 = time.time()
     g = synth.config4(scale=args.c4_scale, n_sources=args.sources)
@@ -228,6 +229,7 @@ def run_config4(args, ctx, barrier_sync, result):
         st = []
         for _ in range(n_steps):
             r = run()
+            r.counts()   # the readout
             st.append(r.stats(accounting=False))
             r.close()
         barrier_sync()
@@ -235,7 +237,8 @@ def run_config4(args, ctx, barrier_sync, result):
 
     # replicated snapshot, one 1024-source batch per GPU
     t0 = time.time()
-    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], 1, 0)
+    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], 1, 0,
+                     np.zeros(len(g["link_atom"]), np.int32))
     snap = ShardSnapshot(sh, local)
     log(f"rank {rank}: config4 replica (one part, {sh.n_local} atoms with incidence) on device in "
         f"{time.time() - t0:.1f}s")
@@ -258,16 +261,19 @@ def run_config4(args, ctx, barrier_sync, result):
     del snap
     if world == 1:
         result["partitioned"] = dict(result["replicated"], scaling="strong",
-                                     parallelism="one part: the hash partition degenerates to the replica")
+                                     parallelism="one part: the partition degenerates to the replica")
         return
-    # hash partition over the ranks, RCCL all-to-all per level, the same 1024 sources everywhere
+    # vertex cut over the ranks (every rank computes the same plan), RCCL reduce + broadcast per level
     seeds = g["seeds"]
     t0 = time.time()
-    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world, rank)
-    info = {"local_atoms": sh.n_local, "local_links": sh.n_links, "local_pins": sh.n_pins}
+    plan = partition_plan(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world)
+    t_plan = time.time() - t0
+    sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world, rank, plan)
+    info = {"local_atoms": sh.n_local, "owned_atoms": sh.n_owned, "local_links": sh.n_links, "local_pins": sh.n_pins,
+            "plan_s": round(t_plan, 1)}
     snap = ShardSnapshot(sh, local)
     sh.close()
-    del g
+    del g, plan
     snap.set_timing(True)
     comm = RcclComm.create(world, rank, local, broadcast=ctx.broadcast_bytes)
     log(f"rank {rank}: config4 part {rank}/{world} on device + RCCL comm in {time.time() - t0:.1f}s {info}")
@@ -276,14 +282,15 @@ def run_config4(args, ctx, barrier_sync, result):
         acct = r.stats(accounting=True)
         r.close()
     dt, st = timed(lambda: pbfs_batch(snap, comm, seeds, args.depth), args.steps)
-    edges = ctx.sum(acct["traversed_edges"] * args.steps)
+    edges = ctx.sum(acct["traversed_edges"]) * args.steps   # parts' shares sum to the whole batch's numerator
     xbytes = ctx.sum(sum(s["bytes_exchanged"] for s in st)) / args.steps
     xms = ctx.max(sum(s["ms_exchange"] for s in st) / args.steps)
     result["partitioned"] = {
         "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
         "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl, "n_gpus": world,
-        "parallelism": f"hash partition over {world} GPUs (owner = atom % {world}), RCCL all-to-all per level",
-        "exchange_bytes_per_step": xbytes, "exchange_ms_per_step": round(xms, 3),
+        "parallelism": f"vertex cut over {world} GPUs (links placed by hgx_partition_plan), RCCL reduce + "
+                       "broadcast of new rows per level, the same sources on every part",
+        "exchange_bytes_per_step": xbytes, "exchange_kernels_ms_per_step": round(xms, 3),
         "rank0_part": info, "roofline": _kernel_roof(st)}
     log(f"rank {rank}: config4 partitioned {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step, "
         f"exchange {xbytes / 1e9:.2f} GB/step")

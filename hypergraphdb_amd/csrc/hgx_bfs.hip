@@ -2137,24 +2137,52 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
         sh.cnt[d] = 0;
     }
     __syncthreads();
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
+    typedef Vec<WPL> V;
+    const int g = lane / G, sub = lane & (G - 1), gbase = lane & ~(G - 1);
     u64 nz = 0;
-    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2
+    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2: one G-lane group per atom
         const u64 ow = fa_next[tile] & own_bm[tile];
         if (ow == 0) continue;   // wave-uniform
         const int64_t t = tile * 64 + lane;
-        const bool hit = (ow >> lane) & 1ull;
         int64_t b = 0;
         int n = 0;
-        if (hit) {
+        if ((ow >> lane) & 1ull) {
             b = bc_off[t];
             n = (int)(bc_off[t + 1] - b);
         }
-        int nmax = n;
-        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
-        for (int k = 0; k < nmax; ++k) {   // wave-uniform: the k-th other holder of every lane's atom
-            const bool has = k < n;
-            const int64_t slot = block_slot(has ? bc_part[b + k] : -1, sh, seg_start);
-            nz += copy_rows<W>(__ballot(has), tile * 64, slot, has ? bc_lid[b + k] : 0, lvl_next, send);
+        const u64 hits = __ballot(n > 0);   // owned atoms with news that other parts hold
+        const int nh = __popcll(hits);
+        for (int r0 = 0; r0 < nh; r0 += PER) {   // wave-uniform
+            const int j = r0 + g;
+            const int bsel = j < nh ? nth_set_bit(hits, j) : 0;
+            const int64_t sb = __shfl(b, bsel);
+            const int sn = j < nh ? __shfl(n, bsel) : 0;
+            int emax = sn;
+            for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
+            const typename V::T row = sn > 0 ? V::ld(lvl_next + (tile * 64 + bsel) * W + sub * WPL) : V::zero();
+            if (sn > 0) {
+                if constexpr (WPL == 1) nz += row != 0ull;
+                else nz += (row.x != 0ull) + (row.y != 0ull);
+            }
+            for (int e = 0; e < emax; ++e) {   // wave-uniform: the e-th other holder of each group's atom
+                const bool has = e < sn;
+                int q = 0;
+                int32_t lid = 0;
+                if (has) {
+                    q = bc_part[sb + e];
+                    lid = bc_lid[sb + e];
+                }
+                int64_t s0 = 0;
+                if (has && sub == 0) s0 = seg_start[q] + (int64_t)sh.base[q] + atomicAdd(&sh.cnt[q], 1u);
+                const int64_t slot = __shfl(s0, gbase);
+                if (has) {
+                    u64* rec = send + slot * (W + kRecHdr);
+                    if (sub == 0) write_header<W>(rec, lid);
+                    if constexpr (WPL == 1) rec[kRecHdr + sub] = row;
+                    else *reinterpret_cast<u64x2*>(rec + kRecHdr + sub * WPL) = row;
+                }
+            }
         }
     }
     wave_add(nzw, nz);
@@ -2200,21 +2228,18 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
 }
 
 // out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
-// over the whole local frontier (the next level's local push volume)
+// over the whole local frontier (the next level's local push volume).  A wave visits the nonzero
+// frontier words; the degrees of a word's atoms come from one coalesced pair of offset loads.
 __global__ void __launch_bounds__(256) hgx_frontier_stats(int64_t A, const u64* __restrict__ fa,
                                                           const u64* __restrict__ own,
                                                           const int64_t* __restrict__ inc_off, u64* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
     u64 n = 0, deg = 0;
-    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w * 64 < A;
-         w += (int64_t)gridDim.x * blockDim.x) {
-        u64 x = fa[w];
-        n += __popcll(x & own[w]);
-        while (x) {
-            const int64_t v = w * 64 + __ffsll((long long)x) - 1;
-            x &= x - 1ull;
-            deg += (u64)(inc_off[v + 1] - inc_off[v]);
-        }
-    }
+    for_nonzero_words(fa, (A + 63) / 64, [&](int64_t w, u64 x) {
+        const int64_t v = w * 64 + lane;
+        if ((x >> lane) & 1ull) deg += (u64)(inc_off[v + 1] - inc_off[v]);
+        if (lane == 0) n += __popcll(x & own[w]);
+    });
     wave_add(out, n);
     wave_add(out + 1, deg);
 }
@@ -2508,8 +2533,8 @@ struct Exchange {
                 rcnt[q], recv + rseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
         }
-        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm,
-                                                                               g->inc_off, xs);
+        hgx_frontier_stats<<<grid_for(ceil_div(A, 64 * 64) * 64, 256, 1024), 256, 0, s>>>(
+            A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
         u64 fs[2];
