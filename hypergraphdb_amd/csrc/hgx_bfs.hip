@@ -2156,8 +2156,11 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
         for (int r0 = 0; r0 < nh; r0 += PER) {   // wave-uniform
             const int j = r0 + g;
             const int bsel = j < nh ? nth_set_bit(hits, j) : 0;
+            // shuffles at wave-uniform points only: a source lane that is inactive during a
+            // ds_bpermute yields garbage, and lane bsel's own group may be past nh
             const int64_t sb = __shfl(b, bsel);
-            const int sn = j < nh ? __shfl(n, bsel) : 0;
+            const int sn_src = __shfl(n, bsel);
+            const int sn = j < nh ? sn_src : 0;
             int emax = sn;
             for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
             const typename V::T row = sn > 0 ? V::ld(lvl_next + (tile * 64 + bsel) * W + sub * WPL) : V::zero();

@@ -1258,6 +1258,13 @@ int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t
 
 extern "C" {
 
+int hgx_query_result_count(const hgx_query_result* r, int64_t* n_queries) {
+    HGX_API_BEGIN
+    if (!r || !n_queries) fail(HGX_E_INVALID, "hgx_query_result_count: bad argument");
+    *n_queries = (int64_t)r->offsets.size() - 1;
+    HGX_API_END
+}
+
 int hgx_query_result_offsets(const hgx_query_result* r, int64_t* offsets) {
     HGX_API_BEGIN
     if (!r || !offsets) fail(HGX_E_INVALID, "hgx_query_result_offsets: bad argument");

@@ -292,6 +292,8 @@ int  hgx_pattern_batch_ext(hgx_graph *g, int32_t n, const int64_t *type_off, con
                            const int64_t *inc_off, const int32_t *inc, const int64_t *pos_off, const int32_t *pos,
                            const int64_t *pset_off, const int64_t *pat_off, const int32_t *pat,
                            const int32_t *arity, hgx_query_result **out);
+/* n = the number of queries of the batch (the size of offsets is n + 1). */
+int  hgx_query_result_count(const hgx_query_result *r, int64_t *n_queries);
 /* offsets[n+1]: results of query q are ids[offsets[q] .. offsets[q+1]). */
 int  hgx_query_result_offsets(const hgx_query_result *r, int64_t *offsets);
 int  hgx_query_result_ids(const hgx_query_result *r, int32_t *ids);
