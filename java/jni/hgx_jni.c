@@ -457,5 +457,172 @@ JNIEXPORT jlong JFN(pbfsBatch)(JNIEnv *e, jclass k, jlong shard, jlong comm, jin
     return (jlong)(intptr_t)res;
 }
 
+JNIEXPORT jlongArray JFN(shardInfo)(JNIEnv *e, jclass k, jlong sh) {
+    int64_t v[4];
+    int rc = hgx_shard_info((const hgx_shard *)(intptr_t)sh, &v[0], &v[1], &v[2], &v[3]);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    return new_longs(e, v, 4);
+}
+
+JNIEXPORT jintArray JFN(shardLocalAtoms)(JNIEnv *e, jclass k, jlong sh) {
+    const hgx_shard *s = (const hgx_shard *)(intptr_t)sh;
+    int64_t nl = 0;
+    int rc = hgx_shard_info(s, &nl, NULL, NULL, NULL);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int32_t *l2g = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nl > 0 ? nl : 1));
+    rc = l2g ? hgx_shard_export(s, l2g, NULL, NULL, NULL, NULL, NULL) : HGX_E_NOMEM;
+    jintArray out = rc ? NULL : new_ints(e, l2g, (jsize)nl);
+    free(l2g);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+JNIEXPORT jintArray JFN(shardOwners)(JNIEnv *e, jclass k, jlong sh) {
+    const hgx_shard *s = (const hgx_shard *)(intptr_t)sh;
+    int64_t nl = 0;
+    int rc = hgx_shard_info(s, &nl, NULL, NULL, NULL);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int32_t *xo = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nl > 0 ? nl : 1));
+    rc = xo ? hgx_shard_exchange_tables(s, xo, NULL, NULL, NULL, NULL, NULL) : HGX_E_NOMEM;
+    jintArray out = rc ? NULL : new_ints(e, xo, (jsize)nl);
+    free(xo);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+JNIEXPORT jlongArray JFN(pbfsBatchGroup)(JNIEnv *e, jclass k, jlongArray shards, jintArray seeds, jint maxDepth,
+                                         jint linkType, jboolean p, jboolean s, jboolean r, jboolean src) {
+    pin_t sh = pin_long(e, shards), sd = pin_int(e, seeds);
+    hgx_algen_opts o = opts_of(linkType, p, s, r, src);
+    const jsize np = sh.n;
+    hgx_graph **gs = (hgx_graph **)malloc(sizeof(hgx_graph *) * (size_t)(np > 0 ? np : 1));
+    hgx_bfs_result **outs = (hgx_bfs_result **)calloc((size_t)(np > 0 ? np : 1), sizeof(hgx_bfs_result *));
+    int rc = (!gs || !outs) ? HGX_E_NOMEM : HGX_OK;
+    for (jsize i = 0; !rc && i < np; i++) gs[i] = (hgx_graph *)(intptr_t)((const jlong *)sh.p)[i];
+    if (!rc) rc = hgx_pbfs_batch_group(gs, np, (const int32_t *)sd.p, sd.n, maxDepth, &o, outs);
+    jlongArray out = NULL;
+    if (!rc) {
+        int64_t *h = (int64_t *)malloc(sizeof(int64_t) * (size_t)(np > 0 ? np : 1));
+        if (h) {
+            for (jsize i = 0; i < np; i++) h[i] = (int64_t)(intptr_t)outs[i];
+            out = new_longs(e, h, np);
+            free(h);
+        } else {
+            for (jsize i = 0; i < np; i++) hgx_bfs_result_free(outs[i]);
+            rc = HGX_E_NOMEM;
+        }
+    }
+    unpin(e, &sh);
+    unpin(e, &sd);
+    free(gs);
+    free(outs);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+static jarray new_doubles(JNIEnv *e, const double *v, jsize n) {
+    jarray a = (*e)->NewDoubleArray(e, n);
+    if (a && n) (*e)->SetDoubleArrayRegion(e, a, 0, n, v);
+    return a;
+}
+
+JNIEXPORT void JFN(setTiming)(JNIEnv *e, jclass k, jlong g, jboolean on) {
+    int rc = hgx_set_timing((hgx_graph *)(intptr_t)g, on ? 1 : 0);
+    if (rc) throw_rc(e, rc);
+}
+
+JNIEXPORT jarray JFN(bfsStats)(JNIEnv *e, jclass k, jlong r, jboolean accounting) {
+    hgx_bfs_stats st;
+    int rc = hgx_bfs_result_stats((hgx_bfs_result *)(intptr_t)r, accounting ? 1 : 0, &st);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    double v[5] = {st.ms_total, st.traversed_edges, st.bytes_min, st.ms_exchange, st.bytes_exchanged};
+    return new_doubles(e, v, 5);
+}
+
+JNIEXPORT jarray JFN(seqStats)(JNIEnv *e, jclass k, jlong sq) {
+    double v[2] = {0, 0};
+    int rc = hgx_seq_result_stats((const hgx_seq_result *)(intptr_t)sq, &v[0], &v[1]);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    return new_doubles(e, v, 2);
+}
+
+JNIEXPORT jarray JFN(queryMs)(JNIEnv *e, jclass k, jlong q) {
+    double v[3] = {0, 0, 0};
+    int rc = hgx_query_result_ms((const hgx_query_result *)(intptr_t)q, &v[0], &v[1], &v[2]);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    return new_doubles(e, v, 3);
+}
+
+/* which: 0 link_atom, 1 tgt_idx */
+static jintArray export_ints(JNIEnv *e, jlong gh, int which) {
+    hgx_graph *g = (hgx_graph *)(intptr_t)gh;
+    int64_t A = 0, M = 0, I = 0;
+    int rc = hgx_graph_info(g, &A, &M, &I);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int64_t *off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(M + 1));
+    rc = off ? hgx_graph_export(g, NULL, off, NULL, NULL) : HGX_E_NOMEM;
+    int64_t n = rc ? 0 : (which == 0 ? M : off[M]);
+    free(off);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    rc = buf ? hgx_graph_export(g, which == 0 ? buf : NULL, NULL, which == 1 ? buf : NULL, NULL) : HGX_E_NOMEM;
+    jintArray out = rc ? NULL : new_ints(e, buf, (jsize)n);
+    free(buf);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+JNIEXPORT jintArray JFN(graphExportLinks)(JNIEnv *e, jclass k, jlong g) { return export_ints(e, g, 0); }
+JNIEXPORT jintArray JFN(graphExportTargets)(JNIEnv *e, jclass k, jlong g) { return export_ints(e, g, 1); }
+
+JNIEXPORT jlongArray JFN(graphExportOffsets)(JNIEnv *e, jclass k, jlong gh) {
+    hgx_graph *g = (hgx_graph *)(intptr_t)gh;
+    int64_t A = 0, M = 0, I = 0;
+    int rc = hgx_graph_info(g, &A, &M, &I);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int64_t *off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(M + 1));
+    rc = off ? hgx_graph_export(g, NULL, off, NULL, NULL) : HGX_E_NOMEM;
+    jlongArray out = rc ? NULL : new_longs(e, off, (jsize)(M + 1));
+    free(off);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+JNIEXPORT jlong JFN(patternBatchStructs)(JNIEnv *e, jclass k, jlong g, jintArray type, jlongArray incOff,
+                                         jintArray inc, jintArray hasOrdered, jlongArray patOff, jintArray pat) {
+    pin_t ty = pin_int(e, type), io = pin_long(e, incOff), ic = pin_int(e, inc), ho = pin_int(e, hasOrdered),
+          po = pin_long(e, patOff), pt = pin_int(e, pat);
+    const jsize n = ty.n;
+    hgx_and_query *qs = (hgx_and_query *)malloc(sizeof(hgx_and_query) * (size_t)(n > 0 ? n : 1));
+    hgx_query_result *q = NULL;
+    int rc = !qs ? HGX_E_NOMEM : (io.n != n + 1 || po.n != n + 1 || ho.n != n) ? HGX_E_INVALID : HGX_OK;
+    for (jsize i = 0; !rc && i < n; i++) {
+        const int64_t *iof = (const int64_t *)io.p, *pof = (const int64_t *)po.p;
+        qs[i].type = ((const int32_t *)ty.p)[i];
+        qs[i].n_incident = (int32_t)(iof[i + 1] - iof[i]);
+        qs[i].incident = (const int32_t *)ic.p + iof[i];
+        qs[i].has_ordered = ((const int32_t *)ho.p)[i];
+        qs[i].n_pattern = (int32_t)(pof[i + 1] - pof[i]);
+        qs[i].pattern = (const int32_t *)pt.p + pof[i];
+    }
+    if (!rc) rc = hgx_pattern_batch((hgx_graph *)(intptr_t)g, qs, n, &q);
+    unpin(e, &ty); unpin(e, &io); unpin(e, &ic); unpin(e, &ho); unpin(e, &po); unpin(e, &pt);
+    free(qs);
+    if (rc) { throw_rc(e, rc); return 0; }
+    return (jlong)(intptr_t)q;
+}
+
+JNIEXPORT jint JFN(deviceCount)(JNIEnv *e, jclass k) {
+    int32_t n = 0;
+    int rc = hgx_device_count(&n);
+    if (rc) throw_rc(e, rc);
+    return n;
+}
+
+JNIEXPORT void JFN(deviceSynchronize)(JNIEnv *e, jclass k, jint device) {
+    int rc = hgx_device_synchronize(device);
+    if (rc) throw_rc(e, rc);
+}
+
 JNIEXPORT jstring JFN(lastError)(JNIEnv *e, jclass k) { return (*e)->NewStringUTF(e, hgx_last_error()); }
 JNIEXPORT jstring JFN(version)(JNIEnv *e, jclass k) { return (*e)->NewStringUTF(e, hgx_version()); }

@@ -1,0 +1,178 @@
+/*
+ * HGGpuTraversal.java -- drop-in HGTraversal (core/.../algorithms/HGTraversal.java:36-63) whose
+ * next() sequence is computed on the GPU: the exact (link, atom) pairs of
+ * HGBreadthFirstTraversal(start, DefaultALGenerator, maxDistance).next() in the reference's FIFO
+ * order, including the link through which each atom was first discovered
+ * (core/.../algorithms/HGBreadthFirstTraversal.java:49-66,143-156) -- hgx_bfs_sequence.
+ *
+ * Accelerated generators: DefaultALGenerator (core/.../algorithms/DefaultALGenerator.java) with
+ *   linkPredicate  == null or an AtomTypeCondition (getters :517-592),
+ *   siblingPredicate == null, and any of the four booleans.
+ * Anything else -- another HGALGenerator, a sibling predicate, another link predicate, or an engine
+ * status HGX_E_UNSUPPORTED -- runs the reference HGBreadthFirstTraversal unchanged.
+ *
+ * The batch form (bfsBatch) is what TraversalBasedQuery (core/.../query/impl/TraversalBasedQuery.java:
+ * 47-71) and the subsumption translators (core/.../query/cond2qry/ToQueryMap.java:282-370) need: the
+ * per-depth visited sets of many start atoms at once (hgx_bfs_batch).
+ *
+ * UNVERIFIED: written against the cited reference interfaces; no JDK exists in this build image.
+ */
+package org.hypergraphdb.gpu;
+
+import java.util.ArrayList;
+import java.util.HashSet;
+import java.util.List;
+import java.util.NoSuchElementException;
+import java.util.Set;
+
+import org.hypergraphdb.HGHandle;
+import org.hypergraphdb.HyperGraph;
+import org.hypergraphdb.algorithms.DefaultALGenerator;
+import org.hypergraphdb.algorithms.HGALGenerator;
+import org.hypergraphdb.algorithms.HGBreadthFirstTraversal;
+import org.hypergraphdb.algorithms.HGTraversal;
+import org.hypergraphdb.query.AtomTypeCondition;
+import org.hypergraphdb.util.Pair;
+
+public class HGGpuTraversal implements HGTraversal
+{
+    private final HGGpuSnapshot snap;
+    private final HGHandle start;
+    private final HGALGenerator gen;
+    private final int maxDistance;
+    private HGTraversal cpu;              // the reference traversal when the generator is not accelerated
+    private int[] links, atoms;           // the next() sequence (ranks)
+    private int pos;
+    private final Set<HGHandle> visited = new HashSet<HGHandle>();
+
+    public HGGpuTraversal(HGGpuSnapshot snap, HGHandle start, HGALGenerator gen)
+    {
+        this(snap, start, gen, Integer.MAX_VALUE);
+    }
+
+    public HGGpuTraversal(HGGpuSnapshot snap, HGHandle start, HGALGenerator gen, int maxDistance)
+    {
+        this.snap = snap;
+        this.start = start;
+        this.gen = gen;
+        this.maxDistance = maxDistance;
+        if (options(snap, gen) == null)
+            cpu = new HGBreadthFirstTraversal(start, gen, maxDistance);
+    }
+
+    /**
+     * The engine options of a generator: {link type key or NO_TYPE, preceding, succeeding, reverse,
+     * source}, or null when the generator is not accelerated.  An AtomTypeCondition on a type no
+     * stored link has yields type key -2 (nothing matches: only the start atom is reachable).
+     */
+    static int[] options(HGGpuSnapshot snap, HGALGenerator g)
+    {
+        if (!(g instanceof DefaultALGenerator)) return null;
+        DefaultALGenerator d = (DefaultALGenerator)g;
+        if (d.getSiblingPredicate() != null) return null;
+        int type = Hgx.NO_TYPE;
+        if (d.getLinkPredicate() != null)
+        {
+            if (!(d.getLinkPredicate() instanceof AtomTypeCondition)) return null;
+            HGHandle th = ((AtomTypeCondition)d.getLinkPredicate()).getTypeHandle(snap.getGraph());
+            if (th == null) return null;
+            int k = snap.typeKeyOrNone(th);
+            type = k >= 0 ? k : Integer.MAX_VALUE;   // no stored link of that type: a key nothing carries
+        }
+        return new int[] {type, d.isReturnPreceeding() ? 1 : 0, d.isReturnSucceeding() ? 1 : 0,
+                          d.isReverseOrder() ? 1 : 0, d.isReturnSource() ? 1 : 0};
+    }
+
+    private static int depth(int maxDistance) { return maxDistance == Integer.MAX_VALUE ? Hgx.UNBOUNDED : maxDistance; }
+
+    private void init()
+    {
+        if (links != null || cpu != null) return;
+        snap.sync();
+        int[] o = options(snap, gen);
+        long s;
+        try
+        {
+            s = Hgx.bfsSequence(snap.native_(), new int[] {snap.rank(start)}, depth(maxDistance), o[0], o[1] != 0,
+                                o[2] != 0, o[3] != 0, o[4] != 0);
+        }
+        catch (UnsupportedOperationException e)
+        {   // e.g. ranks appended out of handle order since the export: keep the reference traversal
+            cpu = new HGBreadthFirstTraversal(start, gen, maxDistance);
+            return;
+        }
+        try
+        {
+            links = Hgx.seqLinks(s);
+            atoms = Hgx.seqAtoms(s);
+        }
+        finally
+        {
+            Hgx.seqFree(s);
+        }
+        visited.add(start);   // examined.put(start, TRUE) at init (HGBreadthFirstTraversal.java:42-46)
+    }
+
+    public boolean hasNext()
+    {
+        init();
+        if (cpu != null) return cpu.hasNext();
+        return pos < atoms.length;
+    }
+
+    public Pair<HGHandle, HGHandle> next()
+    {
+        init();
+        if (cpu != null) return cpu.next();
+        if (pos >= atoms.length) throw new NoSuchElementException();
+        HGHandle a = snap.handle(atoms[pos]);
+        Pair<HGHandle, HGHandle> p = new Pair<HGHandle, HGHandle>(snap.handle(links[pos]), a);
+        pos++;
+        visited.add(a);   // visited once returned (HGTraversal.isVisited contract)
+        return p;
+    }
+
+    public boolean isVisited(HGHandle handle)
+    {
+        init();
+        if (cpu != null) return cpu.isVisited(handle);
+        return visited.contains(handle);
+    }
+
+    public void remove() { throw new UnsupportedOperationException(); }   // HGBreadthFirstTraversal.java:98-101
+
+    /**
+     * Per-depth visited sets of many traversals at once: result[i][d] = the atoms the traversal
+     * from starts[i] returns at distance d (result[i][0] = {starts[i]}), each in handle order.
+     * Returns null when the generator is not accelerated (the caller keeps the reference path).
+     */
+    public static List<HGHandle[][]> bfsBatch(HGGpuSnapshot snap, HGHandle[] starts, HGALGenerator gen,
+                                              int maxDistance)
+    {
+        int[] o = options(snap, gen);
+        if (o == null) return null;
+        snap.sync();
+        int[] seeds = new int[starts.length];
+        for (int i = 0; i < starts.length; i++)
+            seeds[i] = snap.rank(starts[i]);
+        long r = Hgx.bfsBatch(snap.native_(), seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0,
+                              o[4] != 0);
+        try
+        {
+            int levels = Hgx.bfsInfo(r)[1];
+            List<HGHandle[][]> out = new ArrayList<HGHandle[][]>(starts.length);
+            for (int i = 0; i < starts.length; i++)
+            {
+                HGHandle[][] byDepth = new HGHandle[levels][];
+                for (int d = 0; d < levels; d++)
+                    byDepth[d] = snap.handles(Hgx.bfsVisited(r, i, d));
+                out.add(byDepth);
+            }
+            return out;
+        }
+        finally
+        {
+            Hgx.bfsFree(r);
+        }
+    }
+}

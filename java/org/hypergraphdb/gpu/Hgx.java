@@ -74,6 +74,25 @@ final class Hgx
     static native long pbfsBatch(long shard, long comm, int[] seeds, int maxDepth, int linkType, boolean preceding,
                                  boolean succeeding, boolean reverse, boolean source);
 
+    static native long[] shardInfo(long s);                     // {n_local, n_owned, n_local_links, n_local_pins}
+    static native int[] shardLocalAtoms(long s);                // l2g: global id of each local atom
+    static native int[] shardOwners(long s);                    // owner part of each local atom (-1 = here)
+    static native long[] pbfsBatchGroup(long[] shards, int[] seeds, int maxDepth, int linkType, boolean preceding,
+                                        boolean succeeding, boolean reverse, boolean source);   // one result per part
+
+    // ---- timing / statistics / device -------------------------------------------------------
+    static native void setTiming(long g, boolean on);
+    static native double[] bfsStats(long r, boolean accounting); // {ms_total, traversed_edges, bytes_min, ms_exchange, bytes_exchanged}
+    static native double[] seqStats(long s);                    // {ms_total, traversed_edges}
+    static native double[] queryMs(long q);                     // {ms_total, ms_match, bytes_match}
+    static native long[] graphExportOffsets(long g);            // tgt_off of the device snapshot (D2H)
+    static native int[] graphExportTargets(long g);             // tgt_idx
+    static native int[] graphExportLinks(long g);               // link_atom
+    static native long patternBatchStructs(long g, int[] type, long[] incOff, int[] inc, int[] hasOrdered,
+                                           long[] patOff, int[] pat);   // the hgx_and_query[] form
+    static native int deviceCount();
+    static native void deviceSynchronize(int device);
+
     static native String lastError();
     static native String version();
 }

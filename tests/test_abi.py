@@ -98,3 +98,36 @@ def test_generator_ontology_shape():
     sub = g["link_type"] == g["subsumes_type"]
     assert (tg[sub, 0] < tg[sub, 1]).all()          # parents have lower ids (a DAG)
     assert (tg[:, 0] != tg[:, 1]).all()
+
+
+JAVA = os.path.join(ROOT, "java")
+
+
+def test_jni_shim_compiles():
+    """java/jni/hgx_jni.c type-checks against include/hgx.h (a minimal jni.h stands in for the JDK's:
+    no JDK in this image).  Catches ABI drift between the C ABI and the JNI shim."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    assert gcc
+    r = subprocess.run([gcc, "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "tests", "jni_stub"),
+                        "-I", os.path.join(ROOT, "include"), os.path.join(JAVA, "jni", "hgx_jni.c")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_every_java_native_has_a_body_and_every_abi_entry_a_java_caller():
+    """Hgx.java's natives <-> hgx_jni.c's JNI functions, and every hgx_* entry point of include/hgx.h
+    is called by the shim (hgx_comm_host_create excepted: its collectives are host callbacks, and
+    the JNI contract has no callbacks into the JVM)."""
+    import re
+    java = open(os.path.join(JAVA, "org", "hypergraphdb", "gpu", "Hgx.java")).read()
+    jni = open(os.path.join(JAVA, "jni", "hgx_jni.c")).read()
+    natives = set(re.findall(r"static native [\w\[\]<>]+ (\w+)\(", java))
+    bodies = set(re.findall(r"JNIEXPORT [\w ]+ JFN\((\w+)\)", jni))
+    assert natives == bodies, (sorted(natives - bodies), sorted(bodies - natives))
+    header = open(os.path.join(ROOT, "include", "hgx.h")).read()
+    entries = set(re.findall(r"^\s*(?:int|void|const char \*)\s+\*?(hgx_\w+)\(", header, re.M))
+    called = set(re.findall(r"\b(hgx_\w+)\(", jni))
+    missing = sorted(entries - called - {"hgx_comm_host_create"})
+    assert not missing, missing
