@@ -580,6 +580,13 @@ struct HostTransport : Transport {
 
 }  // namespace
 
+// copy a host table to a caller buffer (an empty table copies nothing: memcpy from a null data()
+// would be undefined even at size 0)
+template <class T>
+static void copy_out(T* dst, const std::vector<T>& v) {
+    if (dst && !v.empty()) std::memcpy(dst, v.data(), sizeof(T) * v.size());
+}
+
 extern "C" {
 
 int hgx_partition_plan(const hgx_graph_desc* global, int32_t n_parts, int32_t* link_part) {
@@ -615,12 +622,12 @@ int hgx_shard_export(const hgx_shard* s, int32_t* l2g, int32_t* link_atom, int32
                      int32_t* tgt_idx, int64_t* ghost_count) {
     HGX_API_BEGIN
     if (!s) fail(HGX_E_INVALID, "null shard");
-    if (l2g) std::memcpy(l2g, s->l2g.data(), sizeof(int32_t) * s->l2g.size());
-    if (link_atom) std::memcpy(link_atom, s->link_atom.data(), sizeof(int32_t) * s->link_atom.size());
-    if (link_type) std::memcpy(link_type, s->link_type.data(), sizeof(int32_t) * s->link_type.size());
-    if (tgt_off) std::memcpy(tgt_off, s->tgt_off.data(), sizeof(int64_t) * s->tgt_off.size());
-    if (tgt_idx) std::memcpy(tgt_idx, s->tgt_idx.data(), sizeof(int32_t) * s->tgt_idx.size());
-    if (ghost_count) std::memcpy(ghost_count, s->ghost_count.data(), sizeof(int64_t) * s->ghost_count.size());
+    copy_out(l2g, s->l2g);
+    copy_out(link_atom, s->link_atom);
+    copy_out(link_type, s->link_type);
+    copy_out(tgt_off, s->tgt_off);
+    copy_out(tgt_idx, s->tgt_idx);
+    copy_out(ghost_count, s->ghost_count);
     HGX_API_END
 }
 
@@ -628,13 +635,12 @@ int hgx_shard_exchange_tables(const hgx_shard* s, int32_t* xo_part, int32_t* xo_
                               int32_t* bc_part, int32_t* bc_lid, int64_t* bc_count) {
     HGX_API_BEGIN
     if (!s) fail(HGX_E_INVALID, "null shard");
-    const size_t AL = s->l2g.size();
-    if (xo_part) std::memcpy(xo_part, s->xo_part.data(), sizeof(int32_t) * AL);
-    if (xo_lid) std::memcpy(xo_lid, s->xo_lid.data(), sizeof(int32_t) * AL);
-    if (bc_off) std::memcpy(bc_off, s->bc_off.data(), sizeof(int64_t) * (AL + 1));
-    if (bc_part) std::memcpy(bc_part, s->bc_part.data(), sizeof(int32_t) * s->bc_part.size());
-    if (bc_lid) std::memcpy(bc_lid, s->bc_lid.data(), sizeof(int32_t) * s->bc_lid.size());
-    if (bc_count) std::memcpy(bc_count, s->bc_count.data(), sizeof(int64_t) * s->bc_count.size());
+    copy_out(xo_part, s->xo_part);
+    copy_out(xo_lid, s->xo_lid);
+    copy_out(bc_off, s->bc_off);
+    copy_out(bc_part, s->bc_part);
+    copy_out(bc_lid, s->bc_lid);
+    copy_out(bc_count, s->bc_count);
     HGX_API_END
 }
 

@@ -1,0 +1,30 @@
+"""Host code under AddressSanitizer + UBSan (VERDICT r1 'what's missing' 6).
+
+`make -C hypergraphdb_amd/csrc sanitize` compiles the engine's sources with the sanitizers on the
+host side (device code unchanged), plus the synthetic generator and the oracle, and links them
+into tests/native/host_check.cc's driver: the .hgcsr writer/reader (with every header-byte
+corruption and every truncation step), the descriptor validation, the vertex-cut planner and
+shard builder for 1..8 parts (table consistency) and the oracle restatements.  No GPU is used.
+The driver runs as its own executable (the sanitizer runtimes are linked into it, nothing is
+preloaded into Python)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "hypergraphdb_amd", "csrc")
+
+
+@pytest.mark.timeout(1200)
+def test_host_code_under_asan_ubsan(tmp_path):
+    b = subprocess.run(["make", "-C", CSRC, "sanitize", "-j8"], capture_output=True, text=True, timeout=1100)
+    assert b.returncode == 0, b.stdout[-3000:] + b.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([os.path.join(CSRC, "build", "san", "host_check"), str(tmp_path)], capture_output=True,
+                       text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "host_check: all checks passed" in out
+    assert "runtime error" not in out and "AddressSanitizer" not in out, out[-4000:]
