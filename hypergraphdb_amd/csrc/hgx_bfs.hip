@@ -1996,76 +1996,84 @@ __global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa,
 // Partitioned BFS (vertex cut): per-level exchange of S-bit rows.
 // After the local expansion a part holds, for every local atom with a frontier bit, the news its
 // own links produced (lvl_next; vis already ORed).  For a ghost that is a PARTIAL row:
-//   reduce    hgx_xr_pack ships ghost rows to their owners; hgx_xr_apply (one launch per source
-//             part, an atom appears at most once per source) ORs them in: new = row & ~vis;
-//   broadcast hgx_xb_pack ships every owned atom's final row to its other holders; hgx_xb_apply
+//   reduce    hgx_xr_pack ships ghost rows to their owners; hgx_x_apply<REDUCE> (one launch per
+//             source part, an atom appears at most once per source) ORs them in: new = row & ~vis;
+//   broadcast hgx_xb_pack ships every owned atom's final row to its other holders; hgx_x_apply
 //             overwrites the holder's row (final is a superset of the partial) and ORs vis.
-// Record = [local id on the receiver, spare, W row words]: 16-byte aligned, one lane per record.
+// Records are compressed to the row's nonzero 64-bit words (about half of them at config 4): a
+// 16-byte header {local id on the receiver, word mask, payload offset} in the header stream and
+// the nonzero words, in word order, at the payload offset of the payload stream.  Both streams are
+// segmented by destination part and shipped by one all-to-all each.
 // ---------------------------------------------------------------------------------------------
-constexpr int kRecHdr = 2;
 
-// Record slots are reserved per BLOCK: a block walks a contiguous range of tiles twice -- pass 1
-// counts its records per destination in LDS, one global atomic per destination claims the block's
-// range (cursors kCurStride words apart, each on its own cache line), pass 2 writes the records at
-// LDS-counted offsets.  One atomic per wave per destination (7 cursors on one line) serialised to
-// ~25 ms a level at config-4 scale.
-constexpr int kCurStride = 16;
+// Slots are reserved per BLOCK: a block walks a contiguous range of tiles twice -- pass 1 loads the
+// rows and counts its records and payload words per destination in LDS, one global atomic per
+// destination and stream claims the block's ranges (cursors kCurStride words apart, each pair on a
+// line of its own), pass 2 loads the rows again and writes the records at LDS-counted offsets.  One
+// atomic per wave per destination (7 cursors on one line) serialised to ~25 ms a level at config-4
+// scale.
+constexpr int kCurStride = 16;   // cursor q: [q * kCurStride] records, [q * kCurStride + 8] words
 constexpr int kMaxParts = 64;
 
 struct PackLds {
-    unsigned int cnt[kMaxParts];
-    unsigned long long base[kMaxParts];
+    unsigned int rec[kMaxParts];
+    unsigned int wrd[kMaxParts];
+    unsigned long long base_r[kMaxParts];
+    unsigned long long base_w[kMaxParts];
+    unsigned long long slot[kMaxParts];   // pass 2: records | words << 32 handed out so far
 };
 
-// per-lane destination of record k of this lane's atom, -1 = none
-__device__ __forceinline__ int64_t block_slot(int dest, PackLds& sh, const int64_t* __restrict__ seg_start) {
-    if (dest < 0) return -1;
-    const unsigned int off = atomicAdd(&sh.cnt[dest], 1u);
-    return seg_start[dest] + (int64_t)sh.base[dest] + off;
-}
-
-// Header of a record: the receiver's local id (16-byte store; two 8-byte stores when W == 1 and
-// the record is only 8-byte aligned).
+// Word-nonzero mask of the row of this lane's G-lane group (bit w = row word w != 0).  Wave-uniform.
 template <int W>
-__device__ __forceinline__ void write_header(u64* rec, int32_t lid) {
-    if constexpr (((W + kRecHdr) & 1) == 0) {
-        *reinterpret_cast<u64x2*>(rec) = u64x2{(u64)(uint32_t)lid, 0ull};
+__device__ __forceinline__ uint32_t group_mask(typename Vec<Lay<W>::WPL>::T row) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    const int gbase = (threadIdx.x & 63) & ~(G - 1);
+    if constexpr (WPL == 1) {
+        return (uint32_t)((__ballot(row != 0ull) >> gbase) & ((1ull << G) - 1ull));
     } else {
-        rec[0] = (u64)(uint32_t)lid;
-        rec[1] = 0ull;
+        const uint32_t m0 = (uint32_t)((__ballot(row.x != 0ull) >> gbase) & ((1ull << G) - 1ull));
+        const uint32_t m1 = (uint32_t)((__ballot(row.y != 0ull) >> gbase) & ((1ull << G) - 1ull));
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) m |= (((m0 >> k) & 1u) << (2 * k)) | (((m1 >> k) & 1u) << (2 * k + 1));
+        return m;
     }
 }
 
-// Copy the rows of the set bits of hits (atoms t0 + b) into their records: one G-lane group per
-// row, 16 bytes per lane (a row is one coalesced 128-byte access at W = 16).  slot / lid come from
-// lane b.  Wave-uniform call.
+// Write one record: the group's leader the header, every lane its words (dense: all W words, mask
+// all ones -- a block whose rows are mostly nonzero skips the counting pass's row loads).
 template <int W>
-__device__ __forceinline__ u64 copy_rows(u64 hits, int64_t t0, int64_t slot, int32_t lid, const u64* __restrict__ lvl,
-                                         u64* __restrict__ send) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
+__device__ __forceinline__ void put_record(u64* __restrict__ hdr, u64* __restrict__ pay, int64_t slot, int64_t woff,
+                                           int32_t lid, uint32_t mask, typename Vec<Lay<W>::WPL>::T row, bool dense) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
-    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
-    const int n = __popcll(hits);
-    u64 nz = 0;
-    for (int r0 = 0; r0 < n; r0 += PER) {   // wave-uniform
-        const int j = r0 + g;
-        const int b = j < n ? nth_set_bit(hits, j) : 0;
-        const int64_t s_slot = __shfl(slot, b);
-        const int32_t s_lid = __shfl(lid, b);
-        if (j < n) {
-            const typename V::T row = V::ld(lvl + (t0 + b) * W + sub * WPL);
-            u64* rec = send + s_slot * (W + kRecHdr);
-            if (sub == 0) write_header<W>(rec, s_lid);
-            if constexpr (WPL == 1) {
-                rec[kRecHdr + sub] = row;
-                nz += row != 0ull;
-            } else {
-                *reinterpret_cast<u64x2*>(rec + kRecHdr + sub * WPL) = row;
-                nz += (row.x != 0ull) + (row.y != 0ull);
-            }
-        }
+    const int sub = (threadIdx.x & 63) & (G - 1);
+    if (sub == 0)
+        *reinterpret_cast<u64x2*>(hdr + 2 * slot) = u64x2{(u64)(uint32_t)lid | ((u64)mask << 32), (u64)woff};
+    if (dense) {
+        V::st(pay + woff + sub * WPL, row);
+    } else if constexpr (WPL == 1) {
+        if (row != 0ull) pay[woff + __popc(mask & ((1u << sub) - 1u))] = row;
+    } else {
+        const int w0 = sub * 2;
+        const int64_t p0 = woff + __popc(mask & ((1u << w0) - 1u));
+        if (row.x != 0ull) pay[p0] = row.x;
+        if (row.y != 0ull) pay[p0 + (row.x != 0ull)] = row.y;
     }
-    return nz;
+}
+
+constexpr uint32_t full_word_mask(int W) { return W >= 32 ? 0xffffffffu : ((1u << W) - 1u); }
+
+// A block packs dense (all W words per record, no row loads while counting) when the rows of its
+// sample -- the first tile of each of its waves -- have more than 70% nonzero words.  Wave-uniform.
+__device__ __forceinline__ void sample_add(unsigned int* samp, bool leader, uint32_t mask) {
+    if (leader) {
+        atomicAdd(&samp[0], (unsigned int)__popc(mask));
+        atomicAdd(&samp[1], 1u);
+    }
+}
+__device__ __forceinline__ bool sample_dense(const unsigned int* samp, int W) {
+    return samp[1] > 0 && (u64)samp[0] * 10ull > (u64)samp[1] * (u64)W * 7ull;
 }
 
 // The tiles of block b: [b * per, min((b + 1) * per, ntiles)).
@@ -2075,129 +2083,228 @@ __device__ __forceinline__ void block_tiles(int64_t ntiles, int64_t& lo, int64_t
     hi = lo + per < ntiles ? lo + per : ntiles;
 }
 
+__device__ __forceinline__ void pack_reserve(PackLds& sh, u64* __restrict__ cursor, int NP) {
+    for (int d = threadIdx.x; d < NP; d += 256) {
+        const unsigned int r = sh.rec[d], w = sh.wrd[d];
+        sh.base_r[d] = r ? atomicAdd(&cursor[d * kCurStride], (u64)r) : 0ull;
+        sh.base_w[d] = w ? atomicAdd(&cursor[d * kCurStride + 8], (u64)w) : 0ull;
+        sh.slot[d] = 0ull;
+    }
+}
+
+// The tiles of this wave in its block's range (lo + wv, lo + wv + 4, ...) whose word of fa & own
+// (OWNED) or fa & ~own is nonzero: 64 tile words per coalesced load, body(tile, word) runs
+// wave-uniformly on the nonzero ones.  first_only stops after the first (the density sample).
+template <bool OWNED, class F>
+__device__ __forceinline__ void for_wave_tiles(int64_t lo, int64_t hi, const u64* __restrict__ fa,
+                                               const u64* __restrict__ own, bool first_only, F body) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t b = lo + wv; b < hi; b += 4 * 64) {
+        const int64_t tile = b + 4 * (int64_t)lane;
+        u64 x = 0;
+        if (tile < hi) {
+            const u64 f = fa[tile], o = own[tile];
+            x = OWNED ? (f & o) : (f & ~o);
+        }
+        u64 m = __ballot(x != 0ull);
+        while (m) {
+            const int k = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            body(b + 4 * (int64_t)k, (u64)__shfl(x, k));
+            if (first_only) return;
+        }
+    }
+}
+
+// Reduce pack: one record per ghost with news, to its owner.  seg_h / seg_p: the destination
+// segments' starts in the header (records) and payload (words) streams.  A wave loads U rows per
+// group at once (the row loads are the latency chain of the kernel).
 template <int W>
 __global__ void __launch_bounds__(256) hgx_xr_pack(int64_t A, const u64* __restrict__ fa_next,
                                                    const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
                                                    const int32_t* __restrict__ xo_lid, const u64* __restrict__ lvl_next,
-                                                   u64* __restrict__ cursor, const int64_t* __restrict__ seg_start,
-                                                   u64* __restrict__ send, u64* __restrict__ nzw, int NP) {
+                                                   u64* __restrict__ cursor, const int64_t* __restrict__ seg_h,
+                                                   const int64_t* __restrict__ seg_p, u64* __restrict__ hdr,
+                                                   u64* __restrict__ pay, u64* __restrict__ nzw, int NP) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G, U = 4;
+    constexpr uint32_t FULLM = full_word_mask(W);
+    typedef Vec<WPL> V;
     __shared__ PackLds sh;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ unsigned int samp[2];
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), gbase = lane & ~(G - 1);
     int64_t lo, hi;
     block_tiles((A + 63) / 64, lo, hi);
-    for (int d = threadIdx.x; d < NP; d += 256) sh.cnt[d] = 0;
+    for (int d = threadIdx.x; d < NP; d += 256) sh.rec[d] = sh.wrd[d] = 0;
+    if (threadIdx.x < 2) samp[threadIdx.x] = 0;
     __syncthreads();
-    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 1: counts per destination
-        const u64 gh = fa_next[tile] & ~own_bm[tile];
-        if ((gh >> lane) & 1ull) atomicAdd(&sh.cnt[xo_part[tile * 64 + lane]], 1u);
+    for (int pass = -1; pass < 2; ++pass) {   // density sample, counts, records
+        const bool dense = pass >= 0 && sample_dense(samp, W);
+        const bool load = !(pass == 0 && dense);
+        u64 nz = 0;
+        for_wave_tiles<false>(lo, hi, fa_next, own_bm, pass < 0, [&](int64_t tile, u64 gh) {
+            const int n = __popcll(gh);
+            for (int r0 = 0; r0 < n; r0 += PER * U) {   // wave-uniform
+                typename V::T row[U];
+                int64_t t[U];
+                int q[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = r0 + u * PER + g;
+                    t[u] = tile * 64 + (j < n ? nth_set_bit(gh, j) : 0);
+                    row[u] = (load && j < n) ? V::ld(lvl_next + t[u] * W + sub * WPL) : V::zero();
+                    q[u] = (pass >= 0 && j < n) ? xo_part[t[u]] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (r0 + u * PER < n) {   // wave-uniform
+                        const bool ok = r0 + u * PER + g < n;
+                        const uint32_t nzm = group_mask<W>(row[u]);
+                        const uint32_t mask = dense ? FULLM : nzm;
+                        if (pass < 0) {
+                            sample_add(samp, ok && sub == 0, nzm);
+                        } else if (pass == 0) {
+                            if (ok && sub == 0) {
+                                atomicAdd(&sh.rec[q[u]], 1u);
+                                atomicAdd(&sh.wrd[q[u]], (unsigned int)__popc(mask));
+                            }
+                        } else {
+                            u64 pk = 0;
+                            if (ok && sub == 0) pk = atomicAdd(&sh.slot[q[u]], 1ull | ((u64)__popc(mask) << 32));
+                            pk = __shfl(pk, gbase);   // wave-uniform point
+                            if (ok) {
+                                const int64_t slot = seg_h[q[u]] + (int64_t)sh.base_r[q[u]] + (int64_t)(pk & 0xffffffffull);
+                                const int64_t woff = (int64_t)sh.base_w[q[u]] + (int64_t)(pk >> 32);
+                                put_record<W>(hdr, pay + seg_p[q[u]], slot, woff, xo_lid[t[u]], mask, row[u], dense);
+                                if (sub == 0) nz += (u64)__popc(nzm);
+                            }
+                        }
+                    }
+                }
+            }
+        });
+        __syncthreads();
+        if (pass == 0) {
+            pack_reserve(sh, cursor, NP);
+            __syncthreads();
+        } else if (pass == 1) {
+            wave_add(nzw, nz);
+        }
     }
-    __syncthreads();
-    for (int d = threadIdx.x; d < NP; d += 256) {
-        const unsigned int c = sh.cnt[d];
-        sh.base[d] = c ? atomicAdd(&cursor[d * kCurStride], (u64)c) : 0ull;
-        sh.cnt[d] = 0;
-    }
-    __syncthreads();
-    u64 nz = 0;
-    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2: the records
-        const u64 gh = fa_next[tile] & ~own_bm[tile];
-        if (gh == 0) continue;   // wave-uniform
-        const int64_t t = tile * 64 + lane;
-        const bool hit = (gh >> lane) & 1ull;
-        const int64_t slot = block_slot(hit ? xo_part[t] : -1, sh, seg_start);
-        nz += copy_rows<W>(gh, tile * 64, slot, hit ? xo_lid[t] : 0, lvl_next, send);
-    }
-    wave_add(nzw, nz);
 }
 
+// Broadcast pack: one record per (owned atom with news, other holder).
 template <int W>
 __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restrict__ fa_next,
                                                    const u64* __restrict__ own_bm, const int64_t* __restrict__ bc_off,
                                                    const int32_t* __restrict__ bc_part, const int32_t* __restrict__ bc_lid,
                                                    const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
-                                                   const int64_t* __restrict__ seg_start, u64* __restrict__ send,
-                                                   u64* __restrict__ nzw, int NP) {
+                                                   const int64_t* __restrict__ seg_h, const int64_t* __restrict__ seg_p,
+                                                   u64* __restrict__ hdr, u64* __restrict__ pay, u64* __restrict__ nzw,
+                                                   int NP) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G, U = 2;
+    constexpr uint32_t FULLM = full_word_mask(W);
+    typedef Vec<WPL> V;
     __shared__ PackLds sh;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ unsigned int samp[2];
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), gbase = lane & ~(G - 1);
     int64_t lo, hi;
     block_tiles((A + 63) / 64, lo, hi);
-    for (int d = threadIdx.x; d < NP; d += 256) sh.cnt[d] = 0;
+    for (int d = threadIdx.x; d < NP; d += 256) sh.rec[d] = sh.wrd[d] = 0;
+    if (threadIdx.x < 2) samp[threadIdx.x] = 0;
     __syncthreads();
-    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 1
-        const u64 ow = fa_next[tile] & own_bm[tile];
-        if ((ow >> lane) & 1ull) {
+    for (int pass = -1; pass < 2; ++pass) {   // density sample, counts, records
+        const bool dense = pass >= 0 && sample_dense(samp, W);
+        const bool load = !(pass == 0 && dense);
+        u64 nz = 0;
+        bool sampled = false;
+        for_wave_tiles<true>(lo, hi, fa_next, own_bm, false, [&](int64_t tile, u64 ow) {
+            if (pass < 0 && sampled) return;
             const int64_t t = tile * 64 + lane;
-            for (int64_t e = bc_off[t]; e < bc_off[t + 1]; ++e) atomicAdd(&sh.cnt[bc_part[e]], 1u);
-        }
-    }
-    __syncthreads();
-    for (int d = threadIdx.x; d < NP; d += 256) {
-        const unsigned int c = sh.cnt[d];
-        sh.base[d] = c ? atomicAdd(&cursor[d * kCurStride], (u64)c) : 0ull;
-        sh.cnt[d] = 0;
-    }
-    __syncthreads();
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
-    typedef Vec<WPL> V;
-    const int g = lane / G, sub = lane & (G - 1), gbase = lane & ~(G - 1);
-    u64 nz = 0;
-    for (int64_t tile = lo + wv; tile < hi; tile += 4) {   // pass 2: one G-lane group per atom
-        const u64 ow = fa_next[tile] & own_bm[tile];
-        if (ow == 0) continue;   // wave-uniform
-        const int64_t t = tile * 64 + lane;
-        int64_t b = 0;
-        int n = 0;
-        if ((ow >> lane) & 1ull) {
-            b = bc_off[t];
-            n = (int)(bc_off[t + 1] - b);
-        }
-        const u64 hits = __ballot(n > 0);   // owned atoms with news that other parts hold
-        const int nh = __popcll(hits);
-        for (int r0 = 0; r0 < nh; r0 += PER) {   // wave-uniform
-            const int j = r0 + g;
-            const int bsel = j < nh ? nth_set_bit(hits, j) : 0;
-            // shuffles at wave-uniform points only: a source lane that is inactive during a
-            // ds_bpermute yields garbage, and lane bsel's own group may be past nh
-            const int64_t sb = __shfl(b, bsel);
-            const int sn_src = __shfl(n, bsel);
-            const int sn = j < nh ? sn_src : 0;
-            int emax = sn;
-            for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
-            const typename V::T row = sn > 0 ? V::ld(lvl_next + (tile * 64 + bsel) * W + sub * WPL) : V::zero();
-            if (sn > 0) {
-                if constexpr (WPL == 1) nz += row != 0ull;
-                else nz += (row.x != 0ull) + (row.y != 0ull);
+            int64_t b = 0;
+            int n = 0;
+            if ((ow >> lane) & 1ull) {
+                b = bc_off[t];
+                n = (int)(bc_off[t + 1] - b);
             }
-            for (int e = 0; e < emax; ++e) {   // wave-uniform: the e-th other holder of each group's atom
-                const bool has = e < sn;
-                int q = 0;
-                int32_t lid = 0;
-                if (has) {
-                    q = bc_part[sb + e];
-                    lid = bc_lid[sb + e];
+            const u64 hits = __ballot(n > 0);   // owned atoms with news that other parts hold
+            const int nh = __popcll(hits);
+            if (nh == 0) return;   // wave-uniform
+            sampled = true;
+            for (int r0 = 0; r0 < nh; r0 += PER * U) {   // wave-uniform
+                typename V::T row[U];
+                int64_t sb[U];
+                int sn[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = r0 + u * PER + g;
+                    const int bsel = j < nh ? nth_set_bit(hits, j) : 0;
+                    // shuffles at wave-uniform points only: a source lane that is inactive during a
+                    // ds_bpermute yields garbage, and lane bsel's own group may be past nh
+                    sb[u] = __shfl(b, bsel);
+                    const int sn_src = __shfl(n, bsel);
+                    sn[u] = j < nh ? sn_src : 0;
+                    row[u] = (load && sn[u] > 0) ? V::ld(lvl_next + (tile * 64 + bsel) * W + sub * WPL) : V::zero();
                 }
-                int64_t s0 = 0;
-                if (has && sub == 0) s0 = seg_start[q] + (int64_t)sh.base[q] + atomicAdd(&sh.cnt[q], 1u);
-                const int64_t slot = __shfl(s0, gbase);
-                if (has) {
-                    u64* rec = send + slot * (W + kRecHdr);
-                    if (sub == 0) write_header<W>(rec, lid);
-                    if constexpr (WPL == 1) rec[kRecHdr + sub] = row;
-                    else *reinterpret_cast<u64x2*>(rec + kRecHdr + sub * WPL) = row;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (r0 + u * PER < nh) {   // wave-uniform
+                        const uint32_t nzm = group_mask<W>(row[u]);
+                        const uint32_t mask = dense ? FULLM : nzm;
+                        const unsigned int nnz = (unsigned int)__popc(mask);
+                        if (pass < 0) {
+                            sample_add(samp, sn[u] > 0 && sub == 0, nzm);
+                        } else if (pass == 0) {
+                            if (sub == 0)
+                                for (int e = 0; e < sn[u]; ++e) {
+                                    const int q = bc_part[sb[u] + e];
+                                    atomicAdd(&sh.rec[q], 1u);
+                                    atomicAdd(&sh.wrd[q], nnz);
+                                }
+                        } else {
+                            if (sn[u] > 0 && sub == 0) nz += (u64)__popc(nzm);
+                            int emax = sn[u];
+                            for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
+                            for (int e = 0; e < emax; ++e) {   // wave-uniform: the e-th other holder
+                                const bool has = e < sn[u];
+                                int q = 0;
+                                int32_t lid = 0;
+                                if (has) {
+                                    q = bc_part[sb[u] + e];
+                                    lid = bc_lid[sb[u] + e];
+                                }
+                                u64 pk = 0;
+                                if (has && sub == 0) pk = atomicAdd(&sh.slot[q], 1ull | ((u64)nnz << 32));
+                                pk = __shfl(pk, gbase);
+                                if (has) {
+                                    const int64_t slot = seg_h[q] + (int64_t)sh.base_r[q] + (int64_t)(pk & 0xffffffffull);
+                                    const int64_t woff = (int64_t)sh.base_w[q] + (int64_t)(pk >> 32);
+                                    put_record<W>(hdr, pay + seg_p[q], slot, woff, lid, mask, row[u], dense);
+                                }
+                            }
+                        }
+                    }
                 }
             }
+        });
+        __syncthreads();
+        if (pass == 0) {
+            pack_reserve(sh, cursor, NP);
+            __syncthreads();
+        } else if (pass == 1) {
+            wave_add(nzw, nz);
         }
     }
-    wave_add(nzw, nz);
 }
 
-// Apply n received records, one G-lane group each.  REDUCE: OR a partial row into an owned atom
-// (new = row & ~vis; a source sends an atom at most once, so one launch per source segment);
-// BROADCAST: a ghost's final row replaces the partial one (each ghost gets exactly one record).
+// Apply n received records (headers hdr, payload pay of one source), one G-lane group each.
+// REDUCE: OR a partial row into an owned atom (new = row & ~vis; a source sends an atom at most
+// once, so one launch per source segment); BROADCAST: a ghost's final row replaces the partial one
+// (each ghost gets exactly one record).
 template <int W, bool REDUCE>
-__global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restrict__ recv, u64* __restrict__ lvl_next,
-                                                   u64* __restrict__ fa_next, u64* __restrict__ vis,
-                                                   u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+__global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restrict__ hdr, const u64* __restrict__ pay,
+                                                   u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                   u64* __restrict__ vis, u64* __restrict__ ever, u64* __restrict__ full,
+                                                   FullMask fm) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
     typedef Vec<WPL> V;
     const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
@@ -2207,18 +2314,34 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
     for (int64_t base = wave * PER; base < n; base += nwave * PER) {   // wave-uniform
         const int64_t i = base + g;
         const bool valid = i < n;
-        const u64* rec = recv + (valid ? i : 0) * (W + kRecHdr);
-        const int64_t t = valid ? (int64_t)(uint32_t)rec[0] : 0;
-        const typename V::T row = valid ? V::ld(rec + kRecHdr + sub * WPL) : V::zero();
+        const u64x2 h = valid ? *reinterpret_cast<const u64x2*>(hdr + 2 * i) : u64x2{0ull, 0ull};
+        const int64_t t = (int64_t)(uint32_t)h.x;
+        const uint32_t mask = (uint32_t)(h.x >> 32);
+        typename V::T row = V::zero();
+        if (valid) {
+            if constexpr (WPL == 1) {
+                if ((mask >> sub) & 1u) row = pay[h.y + __popc(mask & ((1u << sub) - 1u))];
+            } else {
+                const int w0 = sub * 2;
+                const int64_t p0 = (int64_t)h.y + __popc(mask & ((1u << w0) - 1u));
+                const bool b0 = (mask >> w0) & 1u, b1 = (mask >> (w0 + 1)) & 1u;
+                row.x = b0 ? pay[p0] : 0ull;
+                row.y = b1 ? pay[p0 + b0] : 0ull;
+            }
+        }
+        // the bitmap words and both rows are loaded at once (the rows of an atom not yet reached
+        // or without news this level are read and discarded: one round trip instead of two)
         const bool ev = valid && bit(ever, t);
         const bool was = valid && bit(fa_next, t);
-        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const typename V::T vis0 = valid ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const typename V::T lv0 = (REDUCE && valid) ? V::ld(lvl_next + t * W + sub * WPL) : V::zero();
+        const typename V::T old = ev ? vis0 : V::zero();
         const typename V::T nw = REDUCE ? (row & ~old) : row;
         const bool any = group_any<G>(V::nz(nw));
         const bool isfull = group_all<G>(V::eq(old | nw, FULL));
         if (valid && (any || !REDUCE)) {
             typename V::T lv = nw;
-            if (REDUCE && was) lv = V::ld(lvl_next + t * W + sub * WPL) | nw;
+            if (REDUCE && was) lv = lv0 | nw;
             V::st(lvl_next + t * W + sub * WPL, lv);
             V::st(vis + t * W + sub * WPL, old | nw);
             if (sub == 0) {
@@ -2411,20 +2534,22 @@ FullMask full_mask(int S, int W) {
 
 // Per-batch buffers of the partitioned exchange (vertex cut).  Segment
 // capacities are static: part q receives from me at most my ghosts owned by q (reduce) and my
-// owned atoms held by q (broadcast); symmetrically for what I receive.
+// owned atoms held by q (broadcast); symmetrically for what I receive.  A segment of cap records
+// has cap 16-byte headers and at most cap * W payload words.
 struct Exchange {
     hgx_graph* g;
     Transport* tr;
     int W;
-    int64_t rec_words;                  // W + kRecHdr
     int64_t cap_recs = 0;               // send / receive area capacity (records)
-    u64* send = nullptr;
-    u64* recv = nullptr;
-    u64* dctr = nullptr;                // [NP] cursors, [NP..NP+1] frontier stats, [NP+2] nonzero words
-    int64_t* seg = nullptr;             // [2 * NP] device: reduce / broadcast send segment starts
-    std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast), NP + 1 entries
+    u64* send_h = nullptr;              // header streams (2 words per record)
+    u64* recv_h = nullptr;
+    u64* send_p = nullptr;              // payload streams (W words per record at most)
+    u64* recv_p = nullptr;
+    u64* dctr = nullptr;                // [NP * kCurStride] cursors, then frontier stats [0..1], nonzero words [2]
+    int64_t* seg = nullptr;             // [4 * NP] device: reduce h / p, broadcast h / p segment starts
+    std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast; records), NP + 1 entries
     double bytes_sent = 0, nz_words = 0, words = 0;
-    Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w), rec_words(w + kRecHdr) {
+    Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts;
         rseg.assign(NP + 1, 0);
@@ -2434,19 +2559,31 @@ struct Exchange {
             bseg[q + 1] = bseg[q] + sh.bc_count[q];
         }
         cap_recs = std::max<int64_t>(std::max(rseg[NP], bseg[NP]), 1);
-        send = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
-        recv = (u64*)g->alloc(sizeof(u64) * (size_t)cap_recs * rec_words);
+        if (cap_recs >= ((int64_t)1 << 32)) fail(HGX_E_INVALID, "partitioned BFS: exchange segment above 2^32 records");
+        send_h = (u64*)g->alloc(sizeof(u64) * 2 * (size_t)cap_recs);
+        recv_h = (u64*)g->alloc(sizeof(u64) * 2 * (size_t)cap_recs);
+        send_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
+        recv_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
         dctr = (u64*)g->alloc(sizeof(u64) * (NP * kCurStride + 4));
-        seg = (int64_t*)g->alloc(sizeof(int64_t) * 2 * NP);
-        HGX_HIP(hipMemcpyAsync(seg, rseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
-        HGX_HIP(hipMemcpyAsync(seg + NP, bseg.data(), sizeof(int64_t) * NP, hipMemcpyHostToDevice, g->stream));
+        seg = (int64_t*)g->alloc(sizeof(int64_t) * 4 * NP);
+        std::vector<int64_t> hs(4 * (size_t)NP);
+        for (int q = 0; q < NP; ++q) {
+            hs[q] = rseg[q];
+            hs[NP + q] = rseg[q] * W;
+            hs[2 * NP + q] = bseg[q];
+            hs[3 * NP + q] = bseg[q] * W;
+        }
+        HGX_HIP(hipMemcpyAsync(seg, hs.data(), sizeof(int64_t) * 4 * NP, hipMemcpyHostToDevice, g->stream));
+        HGX_HIP(hipStreamSynchronize(g->stream));   // hs is a local
     }
     ~Exchange() {
         const int NP = g->shard->n_parts;
-        g->release(send, sizeof(u64) * (size_t)cap_recs * rec_words);
-        g->release(recv, sizeof(u64) * (size_t)cap_recs * rec_words);
+        g->release(send_h, sizeof(u64) * 2 * (size_t)cap_recs);
+        g->release(recv_h, sizeof(u64) * 2 * (size_t)cap_recs);
+        g->release(send_p, sizeof(u64) * W * (size_t)cap_recs);
+        g->release(recv_p, sizeof(u64) * W * (size_t)cap_recs);
         g->release(dctr, sizeof(u64) * (NP * kCurStride + 4));
-        g->release(seg, sizeof(int64_t) * 2 * NP);
+        g->release(seg, sizeof(int64_t) * 4 * NP);
     }
     // collective step: the part's device work is bracketed by compute_begin / compute_end
     template <class F>
@@ -2455,32 +2592,47 @@ struct Exchange {
         f();
         tr->compute_begin(g->stream);
     }
-    // One exchange phase: counts -> all-to-all of the segments.  recv_cap[q] bounds what q sends me;
-    // returns the per-source receive counts and places source q's records at recv + rbase[q].
+    // One exchange phase: counts -> all-to-all of the header and payload segments.  sbase / rbase:
+    // segment starts (records) of what I send / receive; rbase[q+1] - rbase[q] bounds what q sends
+    // me.  Returns the per-source record counts; source q's records land at recv_h + 2 * rbase[q],
+    // its payload at recv_p + W * rbase[q].  *pair_max: the largest bytes I send one peer.
     void ship(const std::vector<int64_t>& sbase, const std::vector<int64_t>& rbase, const std::vector<u64>& cnt,
-              std::vector<int64_t>& rcnt, double& pair_max) {
+              const std::vector<u64>& wcnt, std::vector<int64_t>& rcnt, double* pair_max) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts, me = sh.part;
-        std::vector<int64_t> mine(NP), all((size_t)NP * NP);
-        for (int q = 0; q < NP; ++q) mine[q] = (int64_t)cnt[q];
-        coll([&] { tr->allgather_i64(mine.data(), NP, all.data(), g->stream); });
-        const int64_t rb = (int64_t)sizeof(u64) * rec_words;
-        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP);
-        rcnt.assign(NP, 0);
+        std::vector<int64_t> mine(2 * (size_t)NP), all((size_t)NP * 2 * NP);
         for (int q = 0; q < NP; ++q) {
-            soff[q] = sbase[q] * rb;
-            sbytes[q] = mine[q] * rb;
-            rcnt[q] = all[(size_t)q * NP + me];
-            if (rcnt[q] > rbase[q + 1] - rbase[q]) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
-            roff[q] = rbase[q] * rb;
-            rbytes[q] = rcnt[q] * rb;
-            bytes_sent += (double)sbytes[q];
-            pair_max = std::max(pair_max, (double)sbytes[q]);
+            mine[q] = (int64_t)cnt[q];
+            mine[NP + q] = (int64_t)wcnt[q];
         }
-        coll([&] { tr->alltoallv(send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), g->stream); });
+        coll([&] { tr->allgather_i64(mine.data(), 2 * NP, all.data(), g->stream); });
+        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP), psoff(NP), psbytes(NP), proff(NP),
+            prbytes(NP);
+        rcnt.assign(NP, 0);
+        *pair_max = 0;
+        for (int q = 0; q < NP; ++q) {
+            const int64_t rr = all[(size_t)q * 2 * NP + me], rw = all[(size_t)q * 2 * NP + NP + me];
+            if (rr > rbase[q + 1] - rbase[q] || rw > rr * W) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
+            rcnt[q] = rr;
+            soff[q] = sbase[q] * 16;
+            sbytes[q] = mine[q] * 16;
+            roff[q] = rbase[q] * 16;
+            rbytes[q] = rr * 16;
+            psoff[q] = sbase[q] * W * 8;
+            psbytes[q] = mine[NP + q] * 8;
+            proff[q] = rbase[q] * W * 8;
+            prbytes[q] = rw * 8;
+            bytes_sent += (double)(sbytes[q] + psbytes[q]);
+            *pair_max = std::max(*pair_max, (double)(sbytes[q] + psbytes[q]));
+        }
+        coll([&] {
+            tr->alltoallv(send_h, soff.data(), sbytes.data(), recv_h, roff.data(), rbytes.data(), g->stream);
+            tr->alltoallv(send_p, psoff.data(), psbytes.data(), recv_p, proff.data(), prbytes.data(), g->stream);
+        });
     }
     // Reduce + broadcast of one level.  Returns the group-wide number of new atoms; *push_volume =
-    // sum of |inc| over my (local) new frontier; *level_bytes / *pair_max: bytes I sent.
+    // sum of |inc| over my (local) new frontier; *level_bytes: bytes I sent; *pair_max: the sum over
+    // the level's two phases of the largest bytes I send one peer (the phases run one after the other).
     template <int Wt>
     u64 level(u64* lvl_next, u64* fa_next, u64* vis, u64* ever, u64* full, const FullMask& fm, u64* push_volume,
               double* level_bytes, double* pair_max, Timer& tm, int d) {
@@ -2488,54 +2640,57 @@ struct Exchange {
         const int NP = sh.n_parts, me = sh.part;
         hipStream_t s = g->stream;
         const int64_t A = g->A;
-        const int grid = grid_for(ceil_div(A, 64) * 64, 256, 4096);
         const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(A, 64) / 4 + 1, 2048));
         const double before = bytes_sent;
-        *pair_max = 0;
         const size_t cbytes = sizeof(u64) * (NP * kCurStride + 4);
         u64* xs = dctr + NP * kCurStride;   // [0..1] frontier stats, [2] nonzero words
-        std::vector<u64> hc(NP * kCurStride + 4), cnt(NP);
+        std::vector<u64> hc(NP * kCurStride + 4), cnt(NP), wcnt(NP);
         std::vector<int64_t> rcnt;
         auto read_counts = [&]() {
             HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
             HGX_HIP(hipStreamSynchronize(s));
             for (int q = 0; q < NP; ++q) {
                 cnt[q] = hc[(size_t)q * kCurStride];
+                wcnt[q] = hc[(size_t)q * kCurStride + 8];
                 words += (double)cnt[q] * Wt;
             }
             nz_words += (double)hc[(size_t)NP * kCurStride + 2];
         };
+        auto apply = [&](bool reduce, const std::vector<int64_t>& rbase) {
+            for (int q = 0; q < NP; ++q) {
+                if (q == me || rcnt[q] == 0) continue;
+                const int grid = grid_for(ceil_div(rcnt[q], 64 / Lay<Wt>::G) * 64, 256, 8192);
+                const u64* h = recv_h + 2 * rbase[q];
+                const u64* p = recv_p + (size_t)Wt * rbase[q];
+                if (reduce)
+                    hgx_x_apply<Wt, true><<<grid, 256, 0, s>>>(rcnt[q], h, p, lvl_next, fa_next, vis, ever, full, fm);
+                else
+                    hgx_x_apply<Wt, false><<<grid, 256, 0, s>>>(rcnt[q], h, p, lvl_next, fa_next, vis, ever, full, fm);
+                HGX_CHECK_LAUNCH();
+            }
+        };
+        double pm_r = 0, pm_b = 0;
         // reduce: partial rows of my ghosts -> their owners
         Events e0 = tm.start(kKindExchange, d);
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
         hgx_xr_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_lid, lvl_next, dctr,
-                                              seg, send, xs + 2, NP);
+                                              seg, seg + NP, send_h, send_p, xs + 2, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e0);
         read_counts();
-        ship(rseg, bseg, cnt, rcnt, *pair_max);
+        ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r);
         Events e1 = tm.start(kKindExchange, d);
-        for (int q = 0; q < NP; ++q) {
-            if (q == me || rcnt[q] == 0) continue;
-            hgx_x_apply<Wt, true><<<grid_for(ceil_div(rcnt[q], 64 / Lay<Wt>::G) * 64, 256, 8192), 256, 0, s>>>(
-                rcnt[q], recv + bseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
-            HGX_CHECK_LAUNCH();
-        }
+        apply(true, bseg);
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
         hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
-                                              lvl_next, dctr, seg + NP, send, xs + 2, NP);
+                                              lvl_next, dctr, seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs + 2, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
         read_counts();
-        ship(bseg, rseg, cnt, rcnt, *pair_max);
+        ship(bseg, rseg, cnt, wcnt, rcnt, &pm_b);
         Events e2 = tm.start(kKindExchange, d);
-        for (int q = 0; q < NP; ++q) {
-            if (q == me || rcnt[q] == 0) continue;
-            hgx_x_apply<Wt, false><<<grid_for(ceil_div(rcnt[q], 64 / Lay<Wt>::G) * 64, 256, 8192), 256, 0, s>>>(
-                rcnt[q], recv + rseg[q] * rec_words, lvl_next, fa_next, vis, ever, full, fm);
-            HGX_CHECK_LAUNCH();
-        }
+        apply(false, rseg);
         hgx_frontier_stats<<<grid_for(ceil_div(A, 64 * 64) * 64, 256, 1024), 256, 0, s>>>(
             A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
@@ -2545,6 +2700,7 @@ struct Exchange {
         HGX_HIP(hipStreamSynchronize(s));
         *push_volume = fs[1];
         *level_bytes = bytes_sent - before;
+        *pair_max = pm_r + pm_b;
         int64_t nl = (int64_t)fs[0];
         std::vector<int64_t> nall(NP);
         coll([&] { tr->allgather_i64(&nl, 1, nall.data(), s); });

@@ -513,16 +513,30 @@ struct LocalTransport : Transport {
         hub->send_off[rank] = send_off;
         hub->dev[rank] = device;
         hub->barrier();
-        for (int p = 0; p < world; ++p) {
-            if (recv_bytes[p] <= 0) continue;
-            const char* src = (const char*)hub->send[p] + hub->send_off[p][rank];
-            char* dst = (char*)recv + recv_off[p];
-            if (hub->dev[p] == device)
-                HGX_HIP(hipMemcpyAsync(dst, src, (size_t)recv_bytes[p], hipMemcpyDeviceToDevice, s));
-            else
-                HGX_HIP(hipMemcpyPeerAsync(dst, device, src, hub->dev[p], (size_t)recv_bytes[p], s));
+        {
+            // rehearsal: the copies (the modelled link traffic) run under the gate too, so no
+            // part's kernels overlap another part's copies; the gate is given back before the barrier
+            struct Ungate {
+                LocalHub* h;
+                ~Ungate() {
+                    if (h) h->gate.unlock();
+                }
+            } ungate{nullptr};
+            if (hub->serial) {
+                hub->gate.lock();
+                ungate.h = hub.get();
+            }
+            for (int p = 0; p < world; ++p) {
+                if (recv_bytes[p] <= 0) continue;
+                const char* src = (const char*)hub->send[p] + hub->send_off[p][rank];
+                char* dst = (char*)recv + recv_off[p];
+                if (hub->dev[p] == device)
+                    HGX_HIP(hipMemcpyAsync(dst, src, (size_t)recv_bytes[p], hipMemcpyDeviceToDevice, s));
+                else
+                    HGX_HIP(hipMemcpyPeerAsync(dst, device, src, hub->dev[p], (size_t)recv_bytes[p], s));
+            }
+            HGX_HIP(hipStreamSynchronize(s));
         }
-        HGX_HIP(hipStreamSynchronize(s));
         hub->barrier();   // every part has pulled its segments: send buffers may be reused
         (void)send_bytes;
     }

@@ -125,7 +125,8 @@ typedef struct hgx_bfs_stats {
     double  ms_exchange;
     double  bytes_exchanged;
     double  level_xbytes[64];          /* bytes this part sent at level d                      */
-    double  level_xpair_max[64];       /* the largest of those per destination part at level d */
+    double  level_xpair_max[64];       /* sum over the level's two exchange phases (reduce,     */
+                                       /* broadcast) of the largest bytes sent to one part      */
     double  level_xms[64];             /* device ms of the exchange kernels of level d (timing on) */
     double  xwords_nonzero, xwords_total;   /* row words shipped: nonzero / all (compression headroom) */
     /* minimum-bytes model of the whole batch (with accounting): per expanded level, the CSR slices
