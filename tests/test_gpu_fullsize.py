@@ -4,8 +4,10 @@ a compacted shard and is covered at reduced size by test_gpu_partition.py).
 Where the C oracle finishes in seconds the check is exact (config 3: all 10,000 queries;
 config 5: every closure in both directions; config 2: every set up to depth 2 for a sample of
 sources, which a depth-4 traversal must reproduce since BFS levels do not depend on maxDistance
-beyond them, HGBreadthFirstTraversal.java:49-66).  Depths 3-4 of config 2 (≈4M atoms per source
-per level) are checked through size-independent properties: batch-order and batch-split
+beyond them, HGBreadthFirstTraversal.java:49-66).  Depths 3-4 of config 2 (about 4M atoms per
+source per level) are compared with the oracle for 16 sources (per-depth counts; one traversal
+per oracle thread, so 16 sources cost about one traversal's time) and the full sets of one of
+them, and checked through size-independent properties over all 1024: batch-order and batch-split
 invariance, single-source equality, and disjoint sorted levels."""
 import os
 
@@ -52,6 +54,27 @@ def test_config2_full_depth2_vs_oracle(config2):
         lv = orc.bfs_levels(int(g["seeds"][i]), 2)
         for d_, exp in enumerate(lv):
             assert np.array_equal(res.visited(i, d_), exp), (i, d_)
+    res.close()
+
+
+@pytest.mark.timeout(900)
+def test_config2_full_depth4_vs_oracle(config2):
+    """Depth 4 at full size against the oracle: per-depth counts of 16 sources spread over the
+    batch (all 5 levels, about 2e8 traversed incidences each) and the complete sets of one."""
+    from hypergraphdb_amd import bfs_batch
+    g, snap = config2
+    res = bfs_batch(snap, g["seeds"], 4)
+    counts = res.counts()
+    orc = oracle(g)
+    pick = np.linspace(0, 1023, 16).astype(np.int64)
+    oc, _ = orc.bfs_many(g["seeds"][pick], 4, 5, nthreads=THREADS)
+    assert np.array_equal(counts[pick, :5], oc)
+    assert oc[:, 3:].sum() > 0
+    i = int(pick[5])
+    lv = orc.bfs_levels(int(g["seeds"][i]), 4)
+    assert len(lv) == 5
+    for d_, exp in enumerate(lv):
+        assert np.array_equal(res.visited(i, d_), exp), (i, d_)
     res.close()
 
 
