@@ -1859,18 +1859,29 @@ __device__ __forceinline__ int nth_set_bit(u64 x, int n) {
     return pos;
 }
 
-// Per-source counts of one level (the result readout of a batch): counts[w*64 + b] +=
+// Per-source counts of one level (the result readout of a batch): the count of source w*64 + b =
 // |{v : fa(v), bit b of lvl[v][w]}|, reading only the rows of the level's atoms.  A wave takes 64
 // bitmap words at a time and visits the nonzero ones; the set bits of a word are spread over the
-// lanes W at a time (lane l always holds word l % W of its rows), U rows per lane in flight at once
-// (the loads are independent), each lane adding its row words into K bit planes (a carry-save
-// counter); the planes are folded once per lane at the end.  With `own` the count covers only the
-// atoms of that bitmap (a partition part's owned atoms).
+// lanes W at a time (lane l always holds word l % W of its rows), U = 8 rows per lane in flight at
+// once.  A lane adds its 8 words with a carry-save (Harley-Seal) tree -- ones, twos, fours, and the
+// eights carried into K vertical planes, stopping once no lane carries -- about 12 VALU ops a word
+// instead of a 3K-op ripple per word (the ripple made the kernel ALU-bound at 1.8 TB/s).  The
+// planes are folded once per lane; each block stores its 1024 partial counts (no global atomics:
+// thousands of blocks adding to the same 1024 words serialised), hgx_count_reduce sums them.  With
+// `own` only the atoms of that bitmap count (a partition part's owned atoms).
+__device__ __forceinline__ void csa(u64& h, u64& l, u64 a, u64 b, u64 c) {
+    const u64 u = a ^ b;
+    h = (a & b) | (u & c);
+    l = u ^ c;
+}
+
+constexpr int kCountBlocks = 2048;
+
 template <int W>
 __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
-                                                      const u64* __restrict__ lvl, u64* __restrict__ counts) {
-    constexpr int K = 22;   // < 4M rows per lane: the grid keeps every lane far below
-    constexpr int R = 64 / W, U = 4;
+                                                      const u64* __restrict__ lvl, uint32_t* __restrict__ partial) {
+    constexpr int K = 22;   // planes of the eights: < 2^25 rows per lane
+    constexpr int R = 64 / W, U = 8;
     __shared__ unsigned int lc[W * 64];
     for (int j = threadIdx.x; j < W * 64; j += 256) lc[j] = 0;
     __syncthreads();
@@ -1878,6 +1889,7 @@ __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __re
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t nwords = (A + 63) / 64;
+    u64 ones = 0, twos = 0, fours = 0;
     u64 c[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) c[q] = 0;
@@ -1898,28 +1910,58 @@ __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __re
                     const int j = r0 + u * R + k;
                     v[u] = j < n ? lvl[(t0 + nth_set_bit(xw, j)) * W + wd] : 0ull;
                 }
+                u64 t2a, t2b, t4a, t4b, t8;
+                csa(t2a, ones, ones, v[0], v[1]);
+                csa(t2b, ones, ones, v[2], v[3]);
+                csa(t4a, twos, twos, t2a, t2b);
+                csa(t2a, ones, ones, v[4], v[5]);
+                csa(t2b, ones, ones, v[6], v[7]);
+                csa(t4b, twos, twos, t2a, t2b);
+                csa(t8, fours, fours, t4a, t4b);
+                u64 carry = t8;
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    u64 carry = v[u];
-#pragma unroll
-                    for (int q = 0; q < K; ++q) {
-                        const u64 tq = c[q] & carry;
-                        c[q] ^= carry;
-                        carry = tq;
-                    }
+                for (int q = 0; q < K; ++q) {
+                    if (__ballot(carry != 0ull) == 0ull) break;   // wave-uniform
+                    const u64 tq = c[q] & carry;
+                    c[q] ^= carry;
+                    carry = tq;
                 }
             }
         }
     }
     for (int b = 0; b < 64; ++b) {
-        unsigned int n = 0;
+        unsigned int n = (unsigned int)((ones >> b) & 1ull) | ((unsigned int)((twos >> b) & 1ull) << 1) |
+                         ((unsigned int)((fours >> b) & 1ull) << 2);
 #pragma unroll
-        for (int q = 0; q < K; ++q) n |= (unsigned int)((c[q] >> b) & 1ull) << q;
+        for (int q = 0; q < K; ++q) n += (unsigned int)((c[q] >> b) & 1ull) << (q + 3);
         if (n) atomicAdd(&lc[wd * 64 + b], n);
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < W * 64; j += 256)
-        if (lc[j]) atomicAdd(&counts[j], (u64)lc[j]);
+    for (int j = threadIdx.x; j < W * 64; j += 256) partial[(int64_t)blockIdx.x * (W * 64) + j] = lc[j];
+}
+
+// counts[l][j] = sum over the blocks of the partial counts of level slot l (one launch for every
+// level of the readout): a thread per (slot, source), the block partials read with 8 loads in flight.
+__global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t* __restrict__ nblk,
+                                                        const int32_t* __restrict__ width,
+                                                        const int64_t* __restrict__ poff,
+                                                        const uint32_t* __restrict__ partial, u64* __restrict__ counts) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nslot * 1024) return;
+    const int sl = (int)(i / 1024), j = (int)(i % 1024);
+    const int wj = width[sl];
+    if (j >= wj) return;
+    const uint32_t* p = partial + poff[sl] + j;
+    const int nb = nblk[sl];
+    u64 sum = 0;
+    for (int b0 = 0; b0 < nb; b0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = b0 + u < nb ? p[(int64_t)(b0 + u) * wj] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    counts[(int64_t)sl * 1024 + j] = sum;
 }
 
 // Compaction of {v : fa(v) && bit s of lvl[v]} in ascending order.  Pass 1 (write = false)
@@ -3153,26 +3195,26 @@ void count_level_dispatch(int W, hgx_graph* g, const u64* fa, const u64* lvl, u6
     }
 }
 
-template <int W>
-void count_rows(hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, u64* counts) {
-    const int64_t nwords = ceil_div(std::max<int64_t>(g->A, 1), 64);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), 4096));
-    hgx_count_rows<W><<<grid, 256, 0, g->stream>>>(g->A, fa, own, lvl, counts);
+int count_grid(int64_t A) {
+    const int64_t nwords = ceil_div(std::max<int64_t>(A, 1), 64);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), kCountBlocks));
+}
+
+void count_rows_dispatch(int W, hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, uint32_t* partial) {
+    const int grid = count_grid(g->A);
+    hipStream_t s = g->stream;
+    switch (W) {
+        case 1: hgx_count_rows<1><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
+        case 2: hgx_count_rows<2><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
+        case 4: hgx_count_rows<4><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
+        case 8: hgx_count_rows<8><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
+        default: hgx_count_rows<16><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
+    }
     HGX_CHECK_LAUNCH();
 }
 
-void count_rows_dispatch(int W, hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, u64* counts) {
-    switch (W) {
-        case 1: count_rows<1>(g, fa, own, lvl, counts); break;
-        case 2: count_rows<2>(g, fa, own, lvl, counts); break;
-        case 4: count_rows<4>(g, fa, own, lvl, counts); break;
-        case 8: count_rows<8>(g, fa, own, lvl, counts); break;
-        default: count_rows<16>(g, fa, own, lvl, counts); break;
-    }
-}
-
 // The result readout: res->counts (per seed, per depth) from the device rows -- one counting launch
-// per level into one device table, one D2H, one synchronisation (first call only).
+// per level (block partials), one reduce launch, one D2H, one synchronisation (first call only).
 void ensure_counts(hgx_bfs_result* r) {
     if (r->counts_ready) return;
     hgx_graph* g = r->g;
@@ -3180,17 +3222,46 @@ void ensure_counts(hgx_bfs_result* r) {
     r->counts.assign((size_t)r->n_seeds * r->n_levels, 0);
     size_t nslots = 0;
     for (auto& bt : r->batches) nslots += bt.lvl.size();
+    const int grid = count_grid(g->A);
+    std::vector<int32_t> meta(2 * std::max<size_t>(nslots, 1), 0);   // [nblk | width]
+    std::vector<int64_t> poff(std::max<size_t>(nslots, 1), 0);
+    int64_t ptot = 0;
+    {
+        size_t k = 0;
+        for (auto& bt : r->batches)
+            for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) {
+                meta[k] = grid;
+                meta[nslots + k] = bt.W * 64;
+                poff[k] = ptot;
+                ptot += (int64_t)grid * bt.W * 64;
+            }
+    }
     const size_t bytes = sizeof(u64) * 1024 * std::max<size_t>(nslots, 1);
+    const size_t pbytes = sizeof(uint32_t) * (size_t)std::max<int64_t>(ptot, 1);
+    const size_t mbytes = sizeof(int32_t) * meta.size() + sizeof(int64_t) * poff.size();
     u64* dc = (u64*)g->alloc(bytes);
-    HGX_HIP(hipMemsetAsync(dc, 0, bytes, g->stream));
+    uint32_t* dp = (uint32_t*)g->alloc(pbytes);
+    char* dm = (char*)g->alloc(mbytes);
+    char* hm = (char*)g->pinned_buf(mbytes);
+    std::memcpy(hm, meta.data(), sizeof(int32_t) * meta.size());
+    std::memcpy(hm + sizeof(int32_t) * meta.size(), poff.data(), sizeof(int64_t) * poff.size());
+    HGX_HIP(hipMemcpyAsync(dm, hm, mbytes, hipMemcpyHostToDevice, g->stream));
     const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;
     size_t k = 0;
     for (auto& bt : r->batches)
-        for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) count_rows_dispatch(bt.W, g, bt.fa[d], own, bt.lvl[d], dc + k * 1024);
+        for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) count_rows_dispatch(bt.W, g, bt.fa[d], own, bt.lvl[d], dp + poff[k]);
+    if (nslots) {
+        hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024, 256), 256, 0, g->stream>>>(
+            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots,
+            (const int64_t*)(dm + sizeof(int32_t) * meta.size()), dp, dc);
+        HGX_CHECK_LAUNCH();
+    }
     std::vector<u64> hc(1024 * std::max<size_t>(nslots, 1));
     HGX_HIP(hipMemcpyAsync(hc.data(), dc, bytes, hipMemcpyDeviceToHost, g->stream));
     HGX_HIP(hipStreamSynchronize(g->stream));
     g->release(dc, bytes);
+    g->release(dp, pbytes);
+    g->release(dm, mbytes);
     k = 0;
     for (auto& bt : r->batches)
         for (size_t d = 0; d < bt.lvl.size(); ++d, ++k)
