@@ -27,6 +27,7 @@ HGX_OPT_BFS_FLAGS = 1
 HGX_OPT_SEQ_BUDGET = 2
 HGX_OPT_RANKS_ORDERED = 3
 HGX_OPT_PART_SERIAL = 4
+HGX_OPT_QUERY_FUSED = 5
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (

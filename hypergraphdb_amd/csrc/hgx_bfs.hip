@@ -674,7 +674,7 @@ hgx_link_gather2_o5(int64_t M, const int64_t* __restrict__ tgt_off, const int32_
     gather2_body<W, WRITE_LF>(M, tgt_off, tgt_idx, link_type, want_type, fa, full, lvl, lf, la, ctr, fm, flags);
 }
 
-template <int W, int JBX = 2>
+template <int W, int JBX, bool SORT>
 __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* __restrict__ inc_off,
                                                       const int32_t* __restrict__ inc_row,
                                                       const u64* __restrict__ la, const u64* __restrict__ lf,
@@ -708,17 +708,34 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
             if (lane == 0) fa_next[tile] = 0ull;
             continue;
         }
+        // SORT (A/B, bit 11): the atoms of the tile go to the (j0, group) slots in descending degree
+        // order, so the JB * PW atoms interleaved together have similar degrees (the wave-uniform chunk
+        // loop runs to the largest degree among them; unsorted, power-law degrees leave ~40% of the
+        // lane slots idle on config 2).  Bitonic sort of (degree << 6 | lane) over the wave; slot i
+        // takes the atom at lane key[i] & 63.  Unsorted, slot i is lane i.
+        uint32_t key = ((uint32_t)dme << 6) | (uint32_t)lane;
+        if constexpr (SORT) {
+#pragma unroll
+            for (int k2 = 2; k2 <= 64; k2 <<= 1) {
+#pragma unroll
+                for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+                    const uint32_t other = (uint32_t)__shfl_xor((int)key, j2);
+                    const bool up = ((lane & k2) == 0) == ((lane & j2) == 0);   // keep the larger key here
+                    key = up ? max(key, other) : min(key, other);
+                }
+            }
+        }
         u64 new_w = 0, fullnew_w = 0;
         for (int j0 = 0; j0 < G; j0 += JB) {
             int64_t bj[JB];
-            int dj[JB], dmax = 0;
+            int dj[JB], sl[JB], dmax = 0;
             typename V::T acc[JB], old[JB];
             bool hv[JB], done[JB];
 #pragma unroll
             for (int jj = 0; jj < JB; ++jj) {
-                const int src = (j0 + jj) * PW + g;
-                bj[jj] = __shfl(bme, src);
-                dj[jj] = __shfl(dme, src);
+                sl[jj] = SORT ? (int)((uint32_t)__shfl((int)key, (j0 + jj) * PW + g) & 63u) : (j0 + jj) * PW + g;
+                bj[jj] = __shfl(bme, sl[jj]);
+                dj[jj] = __shfl(dme, sl[jj]);
                 acc[jj] = V::zero();
                 old[jj] = V::zero();
                 hv[jj] = false;
@@ -750,10 +767,10 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                         n_inc += __popc(ga);
                     }
                     if (done[jj]) continue;   // group-uniform from here on
-                    const int64_t t = tile * 64 + (j0 + jj) * PW + g;
+                    const int64_t t = tile * 64 + sl[jj];
                     if (early) {
                         if (!hv[jj] && group_any<G>(V::nz(acc[jj]))) {
-                            if ((ever_w >> ((j0 + jj) * PW + g)) & 1ull) {
+                            if ((ever_w >> sl[jj]) & 1ull) {
                                 old[jj] = V::ld(vis + t * W + sub * WPL);
                                 ++n_vis;
                             }
@@ -766,7 +783,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
             }
 #pragma unroll
             for (int jj = 0; jj < JB; ++jj) {
-                const int pos = (j0 + jj) * PW + g;
+                const int pos = sl[jj];
                 const int64_t t = tile * 64 + pos;
                 bool isnew = false, becomes_full = false;
                 if (dj[jj] > 0) {   // group-uniform
@@ -785,9 +802,16 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                         if (sub == 0) { n_newdeg += (u64)dj[jj]; if (!becomes_full) n_newdeg_nf += (u64)dj[jj]; }
                     }
                 }
-                new_w |= compress_groups<G>(__ballot(isnew), pos - g);
-                fullnew_w |= compress_groups<G>(__ballot(becomes_full), pos - g);
+                if (sub == 0) {   // the atom's own bit (slots are permuted: no ballot compression)
+                    new_w |= (u64)isnew << pos;
+                    fullnew_w |= (u64)becomes_full << pos;
+                }
             }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            new_w |= (u64)__shfl_xor((long long)new_w, off);
+            fullnew_w |= (u64)__shfl_xor((long long)fullnew_w, off);
         }
         if (lane == 0) {
             fa_next[tile] = new_w;
@@ -3061,13 +3085,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             if (v2)
             {
                 // two atoms of a group interleaved (152 VGPRs, 3 waves/SIMD): config 2 pull 5.73 -> 5.23 ms
-                // a step against four (184 VGPRs, 2 waves/SIMD); bit 11 = the four-atom variant (A/B)
+                // a step against four (184 VGPRs, 2 waves/SIMD, dropped in r02); bit 11 = the tile's atoms
+                // placed in descending degree order (A/B)
                 if (lflags & 2048)
-                    hgx_atom_pull2<W, 4><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever,
-                                                                     full, lvl_next, fa_next, c, fm, lflags);
+                    hgx_atom_pull2<W, 2, true><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
+                                                                           ever, full, lvl_next, fa_next, c, fm, lflags);
                 else
-                    hgx_atom_pull2<W, 2><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis, ever,
-                                                                     full, lvl_next, fa_next, c, fm, lflags);
+                    hgx_atom_pull2<W, 2, false><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
+                                                                            ever, full, lvl_next, fa_next, c, fm, lflags);
             }
         }
         if (!(v2 && MODE == kSym))

@@ -434,6 +434,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     } else if (option == HGX_OPT_PART_SERIAL) {
         if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_PART_SERIAL applies to partition shards");
         g->shard->serial = value != 0;
+    } else if (option == HGX_OPT_QUERY_FUSED) {
+        g->q_fused = value != 0;
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;

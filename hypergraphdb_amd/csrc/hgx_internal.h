@@ -42,6 +42,26 @@ void set_last_error(const std::string& msg);
 #define HGX_CHECK_LAUNCH() HGX_HIP(hipGetLastError())
 
 #define HGX_API_BEGIN try {
+// As HGX_API_END without the final `return HGX_OK` (a body that falls through to more code).
+#define HGX_API_END_NORETURN                                                                    \
+    }                                                                                           \
+    catch (const ::hgx::Error& e) {                                                             \
+        ::hgx::set_last_error(e.msg);                                                           \
+        return e.code;                                                                          \
+    }                                                                                           \
+    catch (const std::bad_alloc&) {                                                             \
+        ::hgx::set_last_error("host allocation failed");                                        \
+        return HGX_E_NOMEM;                                                                     \
+    }                                                                                           \
+    catch (const std::exception& e) {                                                           \
+        ::hgx::set_last_error(e.what());                                                        \
+        return HGX_E_DEVICE;                                                                    \
+    }                                                                                           \
+    catch (...) {                                                                               \
+        ::hgx::set_last_error("unknown error");                                                 \
+        return HGX_E_DEVICE;                                                                    \
+    }
+
 #define HGX_API_END                                                                             \
     }                                                                                           \
     catch (const ::hgx::Error& e) {                                                             \
@@ -185,6 +205,9 @@ struct hgx_graph {
     size_t mapped_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
+    bool q_fused = true;                        // HGX_OPT_QUERY_FUSED: small packed batches in one launch
+    int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
+    int64_t q_chunk_guess = 0;                  // fused pattern path: chunk area of the chunked queries
 
     void* alloc(size_t bytes);
     void release(void* p, size_t bytes);

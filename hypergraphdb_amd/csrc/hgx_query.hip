@@ -740,6 +740,550 @@ __global__ void hgx_q_finish_stat(int32_t n, const int32_t* __restrict__ chunk_o
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Fused small-batch path of hgx_pattern_batch_packed (two launches instead of five plus a copy):
+//   hgx_q_fused      one wavefront per query runs ExpressionBasedQuery.expand + the toDNF duplicate
+//                    drop on its anchors (lanes compare in first-occurrence order), the plan (the
+//                    anchor with the fewest incident links, AndToQuery's size order :164-180; with a
+//                    type its type-T slice found by 64 probes a round), and the match (64 candidates
+//                    at a time, the checks of hgx_pattern_match stage 3).  Up to kFusedHold hits go
+//                    to the query's own slot as atom ids; a query with more claims a range of an
+//                    overflow area (one atomic) and writes them there in a second match pass.
+//                    A query with more than kInline candidates (41 of the 10K bench queries, up to
+//                    16K candidates) is normalised into a BigQ record instead: one wave walking 16K
+//                    candidates alone kept the whole launch at 0.38 ms.
+//   hgx_q_fused_big  the records' candidates in kInline chunks, a wave per chunk, hits into the
+//                    chunk's own range.
+//   hgx_q_fused_out  one workgroup scans the per-query counts and copies every query's hits to its
+//                    place in the mapped result area (offsets, ids, status), so nothing is copied
+//                    back after the kernels.
+// A single-launch variant that placed the hits through a decoupled look-back over the previous
+// queries' counts took 35 ms for 10K queries: thousands of waves spun on acquire loads (each an L1
+// invalidate) while the prefix crawled from query 0.
+// ---------------------------------------------------------------------------------------------
+constexpr int kFusedMax = 16384;   // batches up to this size take the fused kernels
+constexpr int kFusedHold = 64;     // hits a query keeps in its own slot
+constexpr int kInline = 1024;      // candidates a query's own wave matches; larger ones go to chunks
+constexpr int kMaxBig = 1024;      // chunked queries per batch (more: the batch takes the general path)
+constexpr int qProbe = qNum;       // counter slot: type-slice probes
+
+// A query with more than kInline candidates, normalised by its wave for the chunk kernel.
+struct BigQ {
+    int32_t q, amin, na, np;
+    int64_t cb, ce;
+    int32_t anch[kMaxAnchors];
+    int32_t pat[kMaxPattern];
+};
+
+struct FusedHead {       // head of the mapped result area (written by hgx_q_fused_out)
+    int64_t total;       // hits of the batch
+    int32_t err[3];      // smallest invalid / unsupported query; [2] = 1 if a query needs the general path
+    int32_t ovf;         // 1: the overflow area was too small (the batch runs again with a larger one)
+    int64_t ovf_need;    // overflow entries the batch claimed
+    int32_t chunk_need;  // > 0: the chunk area was too small for this many chunks (run again)
+    int32_t pad2;
+    u64 ctr[qNum + 1];   // candidates, -, arity sum, hits, probes
+};
+
+// Candidate checks of one link row L (every anchor but amin among its targets, every ordered
+// pattern a greedy subsequence): the logic of hgx_pattern_match stage 3 for the packed shapes.
+__device__ __forceinline__ bool fused_check(int32_t L, const int64_t* __restrict__ tgt_off,
+                                            const int32_t* __restrict__ tgt_idx, const int32_t* anch, int na,
+                                            int amin, const int32_t* spat, int np, bool reg_pat,
+                                            const int32_t (&pv)[8], u64& n_ar) {
+    const int64_t b = tgt_off[L];
+    const int n = (int)(tgt_off[L + 1] - b);
+    n_ar += (u64)n;
+    const int32_t* row = tgt_idx + b;
+    bool hit = true;
+    if (n <= 8) {
+        int32_t tr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
+        for (int j = 0; j < na && hit; ++j) {
+            if (j == amin) continue;
+            const int32_t a = anch[j];
+            bool found = false;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) found |= (i < n) && tr[i] == a;
+            hit = found;
+        }
+        if (hit && reg_pat) {
+            int j = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                int32_t pj = pv[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k)
+                    if (j == k) pj = pv[k];
+                if (i < n && j < np && (pj < 0 || pj == tr[i])) ++j;
+            }
+            hit = j == np;
+        } else if (hit && np > 0) {
+            int i = 0, j = 0;
+            while (i < n && j < np) {
+                const int32_t pj = spat[j];
+                if (pj < 0 || pj == row[i]) ++j;
+                ++i;
+            }
+            hit = j == np;
+        }
+        return hit;
+    }
+    for (int j = 0; j < na && hit; ++j) {
+        if (j == amin) continue;
+        const int32_t a = anch[j];
+        bool found = false;
+        for (int i = 0; i < n && !found; ++i) found = row[i] == a;
+        hit = found;
+    }
+    if (hit && np > 0) {
+        int i = 0, j = 0;
+        while (i < n && j < np) {
+            const int32_t pj = spat[j];
+            if (pj < 0 || pj == row[i]) ++j;
+            ++i;
+        }
+        hit = j == np;
+    }
+    return hit;
+}
+
+// lower_bound(v1) and lower_bound(v2) (v1 < v2) in the ascending a[b, e), the bounds of a type slice.
+// A range of <= 64 entries is read in one coalesced load; a longer one is narrowed 16x a round by 16
+// strided probes (16 lines, one dependent load a round).  While both bounds share their range (the
+// first round) one probe set serves both.
+__device__ __forceinline__ void slice_bounds(const int32_t* __restrict__ a, int32_t v1, int32_t v2, int64_t b,
+                                             int64_t e, int64_t& r1, int64_t& r2, u64& probes) {
+    const int lane = threadIdx.x & 63;
+    int64_t b1 = b, e1 = e, b2 = b, e2 = e;
+    r1 = -1;
+    r2 = -1;
+    auto narrow = [&](int64_t& bb, int64_t& ee, int64_t st, int c, int64_t& r) {
+        if (st == 1 || c == 0) {
+            r = bb + (st == 1 ? c : 0);
+            return;
+        }
+        const int64_t nb = bb + (int64_t)(c - 1) * st + 1;
+        ee = bb + (int64_t)c * st < ee ? bb + (int64_t)c * st : ee;
+        bb = nb;
+    };
+    while (r1 < 0 || r2 < 0) {   // wave-uniform
+        if (r1 < 0 && r2 < 0 && b1 == b2 && e1 == e2) {   // shared range
+            const int64_t span = e1 - b1;
+            const int np = span <= 64 ? 64 : 16;
+            const int64_t st = span <= 64 ? 1 : (span + 15) / 16;
+            const int64_t p = b1 + (int64_t)lane * st;
+            const bool in = lane < np && p < e1;
+            const int32_t x = in ? a[p] : INT32_MAX;
+            const int c1 = __popcll(__ballot(in && x < v1)), c2 = __popcll(__ballot(in && x < v2));
+            probes += (u64)__popcll(__ballot(in));
+            narrow(b1, e1, st, c1, r1);
+            narrow(b2, e2, st, c2, r2);
+            continue;
+        }
+        // separate ranges: lanes 0-31 serve bound 1, lanes 32-63 bound 2
+        const bool hi = lane >= 32;
+        const int l = lane & 31;
+        const int64_t bb = hi ? b2 : b1, ee = hi ? e2 : e1;
+        const bool live = hi ? r2 < 0 : r1 < 0;
+        const int64_t span = ee - bb;
+        const int np = span <= 32 ? 32 : 16;
+        const int64_t st = span <= 32 ? 1 : (span + 15) / 16;
+        const int64_t p = bb + (int64_t)l * st;
+        const bool in = live && l < np && p < ee;
+        const int32_t x = in ? a[p] : INT32_MAX;
+        const u64 m = __ballot(in && x < (hi ? v2 : v1));
+        probes += (u64)__popcll(__ballot(in));
+        const int64_t st1 = __shfl(st, 0), st2 = __shfl(st, 32);
+        if (r1 < 0) narrow(b1, e1, st1, __popcll(m & 0xffffffffull), r1);
+        if (r2 < 0) narrow(b2, e2, st2, __popcll(m >> 32), r2);
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_q_fused(
+    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
+    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
+    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ inc_row,
+    const int32_t* __restrict__ ts_type, const int32_t* __restrict__ ts_row, const int64_t* __restrict__ tgt_off,
+    const int32_t* __restrict__ tgt_idx, const int32_t* __restrict__ link_atom, int32_t* __restrict__ dstat,
+    u64* __restrict__ dctr, int64_t* __restrict__ counts, int32_t* __restrict__ slots, int64_t* __restrict__ ovf_pos,
+    int64_t* __restrict__ ovf_claim, int32_t* __restrict__ ovf, int64_t ovf_cap, BigQ* __restrict__ big,
+    int32_t* __restrict__ big_n) {
+    __shared__ int32_t s_anch[4][kMaxAnchors];
+    __shared__ int32_t s_pat[4][kMaxPattern];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wv));
+    if (q >= n) return;   // whole wave
+    int32_t* anch = s_anch[wv];
+    int32_t* spat = s_pat[wv];
+    const u64 lt = (1ull << lane) - 1ull;
+    // 1. the query, expanded: orderedLink targets become incident anchors (:730-737), duplicates
+    //    dropped in first-occurrence order (:100)
+    const int32_t tq = type[q];
+    const int64_t ib = inc_off[q], ie = inc_off[q + 1];
+    const bool ho = has_ordered[q] != 0;
+    const int64_t pb = pat_off[q], pe = pat_off[q + 1];
+    bool bad = tq < -1 || ie < ib || pe < pb;
+    bool unsup = false, legacy = false;
+    const int ni = bad ? 0 : (int)min<int64_t>(ie - ib, 65);
+    const int np = (bad || !ho) ? 0 : (int)min<int64_t>(pe - pb, kMaxPattern + 1);
+    if (ni > 64) legacy = true;   // long anchor lists take the general path (host fallback)
+    if (np > kMaxPattern) unsup = true;
+    const bool use = !legacy && !unsup;
+    const bool e0 = use && lane < ni, e1 = use && lane < np;
+    const int32_t v0 = e0 ? inc[ib + lane] : -2, v1 = e1 ? pat[pb + lane] : -2;
+    if (__ballot((e0 && (v0 < 0 || v0 >= A)) || (e1 && v1 != HGX_ANY_HANDLE && (v1 < 0 || v1 >= A)))) bad = true;
+    bool a0 = e0, a1 = e1 && v1 != HGX_ANY_HANDLE;
+    const int kmax = ni > np ? ni : np;
+    for (int k = 0; k < kmax; ++k) {   // wave-uniform
+        const int32_t x0 = __shfl(v0, k), x1 = __shfl(v1, k);
+        const bool k0 = k < ni, k1 = k < np && x1 != HGX_ANY_HANDLE;
+        if (k0 && k < lane && x0 == v0) a0 = false;
+        if ((k0 && x0 == v1) || (k1 && k < lane && x1 == v1)) a1 = false;
+    }
+    const u64 m0 = __ballot(a0), m1 = __ballot(a1);
+    const int n0 = __popcll(m0), na = n0 + __popcll(m1);
+    if (!bad && use && (na == 0 || na > kMaxAnchors)) unsup = true;
+    const bool isnop = ho && pe == pb;   // an empty OrderedLinkCondition compiles to HGQuery.NOP
+    const bool run = !bad && !unsup && !legacy && !isnop;
+    if (run) {
+        if (a0) anch[__popcll(m0 & lt)] = v0;
+        if (a1) anch[n0 + __popcll(m1 & lt)] = v1;
+        if (e1) spat[lane] = v1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        if (bad) atomicMin(&dstat[0], q);
+        else if (unsup) atomicMin(&dstat[1], q);
+        else if (legacy) atomicMax(&dstat[2], 1);
+    }
+    // 2. plan
+    int64_t cb = 0, ce = 0;
+    int amin = 0;
+    u64 probes = 0;
+    if (run) {
+        const int32_t a = lane < na ? anch[lane] : 0;
+        const int64_t lo = lane < na ? g_inc_off[a] : 0, hi = lane < na ? g_inc_off[a + 1] : 0;
+        int64_t best = lane < na ? hi - lo : INT64_MAX;
+        int bi = lane;
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t os = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bi, off);
+            if (os < best || (os == best && oi < bi)) {
+                best = os;
+                bi = oi;
+            }
+        }
+        amin = __builtin_amdgcn_readfirstlane(bi);
+        cb = __shfl(lo, amin);
+        ce = __shfl(hi, amin);
+        if (tq >= 0) {   // the type-T slice of the grouped incidence
+            int64_t r1, r2;
+            slice_bounds(ts_type, tq, tq + 1, cb, ce, r1, r2, probes);
+            cb = r1;
+            ce = r2;
+        }
+    }
+    // 3. match: candidates 64 at a time, ascending; the first kFusedHold hits go to the slot
+    const int32_t* rows = tq >= 0 ? ts_row : inc_row;
+    const bool reg_pat = np <= 8;
+    int32_t pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv[k] = __shfl(v1, k);   // the pattern in registers (np <= 8)
+    if (run && ce - cb > kInline) {   // hand the query to the chunk kernel
+        int k = 0;
+        if (lane == 0) k = atomicAdd(big_n, 1);
+        k = __shfl(k, 0);
+        if (k < kMaxBig) {
+            BigQ* bq = big + k;
+            if (lane == 0) {
+                bq->q = q;
+                bq->amin = amin;
+                bq->na = na;
+                bq->np = np;
+                bq->cb = cb;
+                bq->ce = ce;
+            }
+            if (lane < na) bq->anch[lane] = anch[lane];
+            if (lane < np) bq->pat[lane] = spat[lane];
+            if (lane == 0) ovf_pos[q] = -(int64_t)(k + 1);
+        } else if (lane == 0) {
+            atomicMax(&dstat[2], 1);   // too many: the batch takes the general path
+        }
+        if (lane == 0) {
+            counts[q] = 0;   // the chunk kernel adds the query's hits
+            u64* c = dctr + (q & (kQShards - 1)) * kQStride;
+            atomicAdd(c + qCand, (u64)(ce - cb));
+            if (probes) atomicAdd(c + qProbe, probes);
+        }
+        return;
+    }
+    const int64_t nc = run ? ce - cb : 0;
+    if (lane == 0) ovf_pos[q] = 0;   // not chunked (an overflow range replaces it below)
+    int32_t* slot = slots + (int64_t)q * kFusedHold;
+    int64_t hits = 0;
+    u64 n_ar = 0;
+    for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
+        bool hit = false;
+        int32_t L = 0;
+        if (i0 + lane < nc) {
+            L = rows[cb + i0 + lane];
+            hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, reg_pat, pv, n_ar);
+        }
+        const u64 m = __ballot(hit);
+        const int64_t r = hits + __popcll(m & lt);
+        if (hit && r < kFusedHold) slot[r] = link_atom[L];
+        hits += __popcll(m);
+    }
+    if (hits > kFusedHold) {   // a second pass into a claimed overflow range
+        int64_t base = 0;
+        if (lane == 0) base = (int64_t)atomicAdd((unsigned long long*)ovf_claim, (unsigned long long)hits);
+        base = __shfl(base, 0);
+        if (lane == 0) ovf_pos[q] = base;
+        if (base + hits <= ovf_cap) {
+            int64_t w = 0;
+            u64 dummy = 0;
+            for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
+                bool hit = false;
+                int32_t L = 0;
+                if (i0 + lane < nc) {
+                    L = rows[cb + i0 + lane];
+                    hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, reg_pat, pv, dummy);
+                }
+                const u64 m = __ballot(hit);
+                if (hit) ovf[base + w + __popcll(m & lt)] = link_atom[L];
+                w += __popcll(m);
+            }
+        }
+    }
+    if (lane == 0) counts[q] = hits;
+    u64* c = dctr + (q & (kQShards - 1)) * kQStride;
+    for (int off = 32; off > 0; off >>= 1) n_ar += __shfl_xor(n_ar, off);
+    if (lane == 0) {
+        if (nc) atomicAdd(c + qCand, (u64)nc);
+        if (n_ar) atomicAdd(c + qArity, n_ar);
+        if (hits) atomicAdd(c + qHits, (u64)hits);
+        if (probes) atomicAdd(c + qProbe, probes);
+    }
+}
+
+// Chunks of the BigQ records: chunk c of record k covers candidates [cb + j * kInline, +kInline) with
+// j = c - chunk_off[k].  Each workgroup rebuilds the chunk offsets of the records in LDS, its waves
+// grid-stride over the chunks; a chunk's hits (atom ids, ascending) go to big_hits[c * kInline ...],
+// their number to chunk_cnt[c] and into the query's count.
+__device__ __forceinline__ int big_chunk_offsets(const BigQ* __restrict__ big, int nb, int32_t* coff) {
+    // coff[k] = first chunk of record k (nb <= kMaxBig); returns the chunk total.  256 threads.
+    __shared__ int32_t wsum[4];
+    const int per = (nb + 255) / 256;   // <= 4
+    const int k0 = threadIdx.x * per;
+    int32_t cv[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cv[j] = (j < per && k0 + j < nb) ? (int32_t)((big[k0 + j].ce - big[k0 + j].cb + kInline - 1) / kInline) : 0;
+        sum += cv[j];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < 4; ++w) {
+        before += w < wv ? wsum[w] : 0;
+        total += wsum[w];
+    }
+    int e = before + incl - sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < per && k0 + j < nb) coff[k0 + j] = e;
+        e += cv[j];
+    }
+    if (threadIdx.x == 0) coff[nb] = total;
+    __syncthreads();
+    return total;
+}
+
+__global__ void __launch_bounds__(256) hgx_q_fused_big(const BigQ* __restrict__ big, const int32_t* __restrict__ big_n,
+                                                       const int32_t* __restrict__ inc_row,
+                                                       const int32_t* __restrict__ ts_row,
+                                                       const int32_t* __restrict__ type,
+                                                       const int64_t* __restrict__ tgt_off,
+                                                       const int32_t* __restrict__ tgt_idx,
+                                                       const int32_t* __restrict__ link_atom, int64_t* __restrict__ counts,
+                                                       int32_t* __restrict__ big_hits, int32_t* __restrict__ chunk_cnt,
+                                                       int32_t chunk_cap, int32_t* __restrict__ dstat,
+                                                       u64* __restrict__ dctr) {
+    __shared__ int32_t coff[kMaxBig + 1];
+    __shared__ int32_t s_anch[4][kMaxAnchors];
+    __shared__ int32_t s_pat[4][kMaxPattern];
+    const int nb = min(*big_n, kMaxBig);
+    if (nb == 0) return;   // block-uniform
+    const int total = big_chunk_offsets(big, nb, coff);
+    if (total > chunk_cap) {   // too small a chunk area: the host runs the batch again with a larger one
+        if (blockIdx.x == 0 && threadIdx.x == 0) dstat[3] = total;
+        return;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u64 lt = (1ull << lane) - 1ull;
+    int32_t* anch = s_anch[wv];
+    int32_t* spat = s_pat[wv];
+    u64 n_ar = 0;
+    for (int c = blockIdx.x * 4 + wv; c < total; c += gridDim.x * 4) {   // wave-uniform
+        int lo = 0, hi = nb;   // the record k with coff[k] <= c < coff[k + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (coff[mid] <= c) lo = mid; else hi = mid;
+        }
+        const BigQ* bq = big + lo;
+        const int q = bq->q, amin = bq->amin, na = bq->na, np = bq->np;
+        const int64_t b0 = bq->cb + (int64_t)(c - coff[lo]) * kInline;
+        const int64_t nc = min<int64_t>(kInline, bq->ce - b0);
+        if (lane < na) anch[lane] = bq->anch[lane];
+        const int32_t pvl = lane < np ? bq->pat[lane] : -2;
+        if (lane < np) spat[lane] = pvl;
+        __builtin_amdgcn_wave_barrier();
+        int32_t pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pv[k] = __shfl(pvl, k);
+        const int32_t* rows = type[q] >= 0 ? ts_row : inc_row;
+        int32_t* out = big_hits + (int64_t)c * kInline;
+        int64_t hits = 0;
+        for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
+            bool hit = false;
+            int32_t L = 0;
+            if (i0 + lane < nc) {
+                L = rows[b0 + i0 + lane];
+                hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, np <= 8, pv, n_ar);
+            }
+            const u64 m = __ballot(hit);
+            if (hit) out[hits + __popcll(m & lt)] = link_atom[L];
+            hits += __popcll(m);
+        }
+        if (lane == 0) {
+            chunk_cnt[c] = (int32_t)hits;
+            if (hits) atomicAdd((unsigned long long*)&counts[q], (unsigned long long)hits);
+            if (hits) atomicAdd(dctr + (q & (kQShards - 1)) * kQStride + qHits, (u64)hits);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int off = 32; off > 0; off >>= 1) n_ar += __shfl_xor(n_ar, off);
+    if (lane == 0 && n_ar) atomicAdd(dctr + qArity, n_ar);
+}
+
+// One workgroup: exclusive scan of the per-query hit counts into the mapped offsets, every query's
+// hits copied from its slot (or its overflow range) to the mapped ids, and the batch status.
+__global__ void __launch_bounds__(kScanBlock) hgx_q_fused_out(int32_t n, const int64_t* __restrict__ counts,
+                                                             const int32_t* __restrict__ slots,
+                                                             const int64_t* __restrict__ ovf_pos,
+                                                             const int64_t* __restrict__ ovf_claim,
+                                                             const int32_t* __restrict__ ovf, int64_t ovf_cap,
+                                                             const BigQ* __restrict__ big,
+                                                             const int32_t* __restrict__ big_n,
+                                                             const int32_t* __restrict__ big_hits,
+                                                             const int32_t* __restrict__ chunk_cnt,
+                                                             const int32_t* __restrict__ dstat,
+                                                             const u64* __restrict__ dctr, FusedHead* __restrict__ head,
+                                                             int64_t* __restrict__ out_off, int32_t* __restrict__ out_ids,
+                                                             int64_t cap) {
+    __shared__ int64_t ws64[kScanBlock / 64];
+    __shared__ int64_t qstart[kMaxBig];
+    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kFusedMax)
+    const int32_t q0 = threadIdx.x * per;
+    int64_t cv[16];
+    int64_t sk = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        cv[j] = (j < per && q0 + j < n) ? counts[q0 + j] : 0;
+        sk += cv[j];
+    }
+    int64_t tk;
+    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
+    const int64_t ovf_need = *ovf_claim;
+    const bool ovf_bad = ovf_need > ovf_cap;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j < per && q0 + j < n) {
+            const int32_t q = q0 + j;
+            out_off[q] = ek;
+            const int64_t h = cv[j];
+            const int64_t op = ovf_pos[q];
+            if (op < 0) {
+                qstart[-op - 1] = ek;   // a chunked query: placed below
+            } else if (tk <= cap && !ovf_bad) {
+                const int32_t* src = h <= kFusedHold ? slots + (int64_t)q * kFusedHold : ovf + op;
+                for (int64_t i = 0; i < h; ++i) out_ids[ek + i] = src[i];
+            }
+        }
+        ek += cv[j];
+    }
+    // chunked queries: each chunk's place = its query's start + the hits of the query's earlier chunks
+    // (a scan of the chunk counts); then the chunks are copied one after the other by the whole block
+    const int nb = min(*big_n, kMaxBig);
+    if (nb > 0 && tk <= cap && !ovf_bad && dstat[3] == 0) {   // block-uniform
+        __shared__ int32_t coff[kMaxBig + 1];
+        __shared__ int64_t cex[kScanBlock];
+        __shared__ int64_t cstart[kScanBlock];
+        // chunk offsets of the records (1024 threads: one record each)
+        int32_t nck = 0;
+        if ((int)threadIdx.x < nb) nck = (int32_t)((big[threadIdx.x].ce - big[threadIdx.x].cb + kInline - 1) / kInline);
+        int64_t tch;
+        const int64_t ech = block_exclusive_scan<int64_t>((int64_t)nck, ws64, tch);
+        if ((int)threadIdx.x < nb) coff[threadIdx.x] = (int32_t)ech;
+        if (threadIdx.x == 0) coff[nb] = (int32_t)tch;
+        __syncthreads();
+        for (int64_t c0 = 0; c0 < tch; c0 += kScanBlock) {   // block-uniform: kScanBlock chunks at a time
+            const int64_t c = c0 + threadIdx.x;
+            int64_t cnt = c < tch ? chunk_cnt[c] : 0;
+            int64_t tot;
+            const int64_t ex = block_exclusive_scan<int64_t>(cnt, ws64, tot);   // over this window
+            int k = 0;
+            if (c < tch) {
+                int lo = 0, hi = nb;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (coff[mid] <= c) lo = mid; else hi = mid;
+                }
+                k = lo;
+            }
+            cex[threadIdx.x] = ex;
+            __syncthreads();
+            if (c < tch) {
+                // hits of the record's earlier chunks: those inside this window + those before it
+                const int64_t first = coff[k];
+                int64_t before = ex - (first >= c0 ? cex[first - c0] : 0);
+                if (first < c0) {   // the record started in an earlier window: add its earlier chunks
+                    for (int64_t e = first; e < c0; ++e) before += chunk_cnt[e];
+                }
+                cstart[threadIdx.x] = qstart[k] + before;
+            }
+            __syncthreads();
+            for (int64_t cc = c0; cc < c0 + kScanBlock && cc < tch; ++cc) {   // block-uniform
+                const int64_t cn = chunk_cnt[cc], st = cstart[cc - c0];
+                for (int64_t i = threadIdx.x; i < cn; i += kScanBlock) out_ids[st + i] = big_hits[cc * kInline + i];
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        out_off[n] = tk;
+        head->total = tk;
+        for (int i = 0; i < 3; ++i) head->err[i] = dstat[i];
+        head->chunk_need = dstat[3];
+        head->ovf = ovf_bad ? 1 : 0;
+        head->ovf_need = ovf_need;
+    }
+    if (threadIdx.x <= qNum) {
+        u64 t = 0;
+        for (int sh = 0; sh < kQShards; ++sh) t += dctr[sh * kQStride + threadIdx.x];
+        head->ctr[threadIdx.x] = t;
+    }
+}
+
 }  // namespace hgx
 
 using namespace hgx;
@@ -1219,6 +1763,121 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
     }
 }
 
+
+// The fused path of hgx_pattern_batch_packed (batches of <= kFusedMax queries): the raw arrays go up
+// in one pinned copy together with the zeroed status / counter words, hgx_q_fused + hgx_q_fused_out,
+// one synchronisation; offsets and ids are read from the mapped result area.  Returns false when a
+// query needs the general path (more than 64 incident entries), which the caller then runs.
+bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                      const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result* r,
+                      bool prof, double t0) {
+    hipStream_t s = g->stream;
+    const int64_t n_inc = inc_off[n] - inc_off[0], n_pat = pat_off[n] - pat_off[0];
+    if (inc_off[0] != 0 || pat_off[0] != 0 || n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
+        fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad offsets");
+    Upload u;
+    const size_t o_type = u.take(4 * (size_t)n), o_ioff = u.take(8 * (size_t)(n + 1)), o_inc = u.take(4 * (size_t)n_inc),
+                 o_ho = u.take(4 * (size_t)n), o_poff = u.take(8 * (size_t)(n + 1)), o_pat = u.take(4 * (size_t)n_pat),
+                 o_stat = u.take(32), o_ctr = u.take(sizeof(u64) * kQShards * kQStride),
+                 o_ovfn = u.take(8);   // the overflow claim counter
+    char* h = (char*)g->pinned_buf(u.off);
+    // status: [0] invalid query, [1] unsupported query, [2] general path needed, [3] chunks needed
+    // beyond the chunk area, [4] chunked queries (claim counter)
+    const int32_t st0[8] = {INT32_MAX, INT32_MAX, 0, 0, 0, 0, 0, 0};
+    std::memcpy(h + o_stat, st0, 32);
+    std::memset(h + o_ctr, 0, sizeof(u64) * kQShards * kQStride + 8);
+    std::memcpy(h + o_type, type, 4 * (size_t)n);
+    std::memcpy(h + o_ioff, inc_off, 8 * (size_t)(n + 1));
+    if (n_inc) std::memcpy(h + o_inc, inc, 4 * (size_t)n_inc);
+    std::memcpy(h + o_ho, has_ordered, 4 * (size_t)n);
+    std::memcpy(h + o_poff, pat_off, 8 * (size_t)(n + 1));
+    if (n_pat) std::memcpy(h + o_pat, pat, 4 * (size_t)n_pat);
+    Scratch sc{g, {}};
+    char* d = (char*)sc.take(u.off);
+    int64_t* counts = (int64_t*)sc.take(sizeof(int64_t) * (size_t)n);
+    int32_t* slots = (int32_t*)sc.take(sizeof(int32_t) * (size_t)n * kFusedHold);
+    int64_t* ovf_pos = (int64_t*)sc.take(sizeof(int64_t) * (size_t)n);
+    BigQ* big = (BigQ*)sc.take(sizeof(BigQ) * kMaxBig);
+    int32_t* big_n = (int32_t*)(d + o_stat) + 4;
+    int64_t* ovf_claim = (int64_t*)(d + o_ovfn);   // zeroed by the upload
+    Events ev;
+    ev.init(g->timing);
+    ev.rec(0, s);
+    HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
+    for (int attempt = 0;; ++attempt) {
+        const int64_t cap = std::max<int64_t>(g->q_hits_guess, 4096);
+        const int64_t ovf_cap = std::max<int64_t>(g->q_ovf_guess, 1 << 16);
+        const int32_t chunk_cap = (int32_t)std::max<int64_t>(g->q_chunk_guess, 1024);
+        Scratch w{g, {}};
+        int32_t* ovf = (int32_t*)w.take(sizeof(int32_t) * (size_t)ovf_cap);
+        int32_t* big_hits = (int32_t*)w.take(sizeof(int32_t) * (size_t)chunk_cap * kInline);
+        int32_t* chunk_cnt = (int32_t*)w.take(sizeof(int32_t) * (size_t)chunk_cap);
+        const size_t m_off = (sizeof(FusedHead) + 15) & ~(size_t)15;
+        const size_t m_ids = m_off + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
+        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)cap);
+        char* dm = nullptr;
+        HGX_HIP(hipHostGetDevicePointer((void**)&dm, hm, 0));
+        if (attempt > 0)   // fresh status and counter words
+            HGX_HIP(hipMemcpyAsync(d + o_stat, h + o_stat, o_ovfn + 8 - o_stat, hipMemcpyHostToDevice, s));
+        ev.rec(1, s);
+        hgx_q_fused<<<(unsigned)ceil_div(n, 4), 256, 0, s>>>(
+            n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
+            (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
+            g->inc_row, g->inc_ts_type, g->inc_ts_row, g->tgt_off, g->tgt_idx, g->link_atom, (int32_t*)(d + o_stat),
+            (u64*)(d + o_ctr), counts, slots, ovf_pos, ovf_claim, ovf, ovf_cap, big, big_n);
+        HGX_CHECK_LAUNCH();
+        hgx_q_fused_big<<<512, 256, 0, s>>>(big, big_n, g->inc_row, g->inc_ts_row, (const int32_t*)(d + o_type),
+                                            g->tgt_off, g->tgt_idx, g->link_atom, counts, big_hits, chunk_cnt, chunk_cap,
+                                            (int32_t*)(d + o_stat), (u64*)(d + o_ctr));
+        HGX_CHECK_LAUNCH();
+        ev.rec(2, s);
+        hgx_q_fused_out<<<1, kScanBlock, 0, s>>>(n, counts, slots, ovf_pos, ovf_claim, ovf, ovf_cap, big, big_n,
+                                                 big_hits, chunk_cnt, (const int32_t*)(d + o_stat),
+                                                 (const u64*)(d + o_ctr), (FusedHead*)dm, (int64_t*)(dm + m_off),
+                                                 (int32_t*)(dm + m_ids), cap);
+        HGX_CHECK_LAUNCH();
+        ev.rec(3, s);
+        HGX_HIP(hipStreamSynchronize(s));
+        const FusedHead* hd = (const FusedHead*)hm;
+        if (hd->err[0] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(hd->err[0]));
+        if (hd->err[1] < n)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(hd->err[1]) +
+                                        " is not accelerated (no incidence anchor or condition limits)");
+        if (hd->err[2]) return false;
+        const int64_t total = hd->total;
+        if (total > cap || hd->ovf || hd->chunk_need > 0) {   // an area was too small: grow it and run again
+            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: result sizing failed");
+            g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
+            g->q_ovf_guess = std::max<int64_t>(g->q_ovf_guess, hd->ovf_need + hd->ovf_need / 4);
+            g->q_chunk_guess = std::max<int64_t>(g->q_chunk_guess, (int64_t)hd->chunk_need + hd->chunk_need / 4);
+            continue;
+        }
+        g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
+        const int64_t* qoff = (const int64_t*)(hm + m_off);
+        const int32_t* ids = (const int32_t*)(hm + m_ids);
+        std::memcpy(r->offsets.data(), qoff, sizeof(int64_t) * (n + 1));
+        r->ids.assign(ids, ids + total);
+        if (prof)
+            std::fprintf(stderr, "[hgx query] fused n=%d host+device %.3f ms (candidates %llu, hits %lld)\n", n,
+                         now_ms() - t0, (unsigned long long)hd->ctr[qCand], (long long)total);
+        if (ev.on) {
+            float a = 0, b = 0;
+            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
+            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
+            r->ms_total = a;
+            r->ms_match = b;
+        }
+        // algorithmic bytes of hgx_q_fused: per query its fields (4 + 16 + 4 + 16 B), its anchor /
+        // pattern entries and 16 B of incidence bounds per entry (an upper bound of the distinct
+        // anchors), 4 B per type-slice probe; per candidate its link row, tgt_off pair and target row;
+        // per hit the link atom read and the id written; the per-query count
+        r->bytes_match = 40.0 * n + 20.0 * (double)(n_inc + n_pat) + 4.0 * (double)hd->ctr[qProbe] +
+                         20.0 * (double)hd->ctr[qCand] + 4.0 * (double)hd->ctr[qArity] + 8.0 * (double)hd->ctr[qHits] +
+                         8.0 * n;
+        return true;
+    }
+}
+
 template <class FrontFn>
 int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front) {
     HGX_API_BEGIN
@@ -1249,6 +1908,26 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
 
 int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
                      const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result** out) {
+    if (n > 0 && n <= kFusedMax && g->q_fused && !g->shard) {
+        HGX_API_BEGIN
+        const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
+        const double t0 = now_ms();
+        std::unique_ptr<hgx_query_result> r(new hgx_query_result());
+        r->n = n;
+        r->offsets.assign(n + 1, 0);
+        bool done;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            HGX_HIP(hipSetDevice(g->device));
+            ensure_type_grouped(g);
+            done = run_fused_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, r.get(), prof, t0);
+        }
+        if (done) {
+            *out = r.release();
+            return HGX_OK;
+        }
+        HGX_API_END_NORETURN
+    }
     return run_batch_with(g, n, out, [&](Scratch& sc, Events& ev, Front& f) {
         front_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, sc, ev, f);
     });

@@ -167,8 +167,8 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
  *                              before this level's counters reach the host,
  *                      bit 10 = the dense gather built for 5 waves/SIMD (spills VGPRs; diagnostic A/B only),
- *                      bit 11 = the dense pull interleaves four atoms per lane group instead of two
- *                              (A/B only),
+ *                      bit 11 = the dense pull places a tile's atoms on its lane groups in
+ *                              descending degree order (A/B only),
  *                      bits 12 / 13 / 14 = nontemporal loads of the streamed CSR columns / stores of
  *                              the gather's link rows / stores of the pull's atom rows (A/B only),
  *                      bit 15 = the symmetric-mode hub pull keeps two incidence chunks in flight
@@ -345,6 +345,10 @@ void hgx_shard_free(hgx_shard *s);
  * device work one part at a time (clean per-part device times for a one-GPU rehearsal). */
 int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out);
 #define HGX_OPT_PART_SERIAL 4
+/* HGX_OPT_QUERY_FUSED: 1 (default) = hgx_pattern_batch_packed runs batches of <= 16384 queries in
+ * two fused launches (a wavefront per query: expand, plan, match; then one workgroup places the hits
+ * in the mapped result area); 0 = the general five-launch path for every batch (A/B). */
+#define HGX_OPT_QUERY_FUSED 5
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
  * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */

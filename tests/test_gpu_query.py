@@ -290,3 +290,59 @@ def test_packed_errors():
         pattern_batch_arrays(snap, *_packed([(-1, [n0], None), (K.T_TESTLINK, [], (-1, -1))]))
     r = pattern_batch_arrays(snap, *_packed([(-1, [n0], ()), (-1, [n0], None)]))   # empty orderedLink: NOP
     assert r[0].tolist() == [] and len(r[1]) > 0
+
+
+def _same(r1, r2, n):
+    assert np.array_equal(r1.offsets, r2.offsets)
+    for q in range(n):
+        assert r1[q].tolist() == r2[q].tolist(), q
+
+
+def test_fused_packed_path_vs_general_and_oracle():
+    """Batches of <= 16384 packed queries run in one fused launch (a wave per query, look-back output
+    offsets).  Against the general five-launch path (HGX_OPT_QUERY_FUSED = 0) and the oracle: typed
+    orderedLink queries, untyped multi-anchor queries with repeated anchors, hub anchors with
+    thousands of hits (the second match pass and the result-area growth), empty orderedLinks (NOP),
+    several batches in a row (look-back epochs), and a batch with a 70-entry anchor list (the
+    fused kernel hands the batch to the general path)."""
+    from hypergraphdb_amd import _lib, synth
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    g = synth.config3(scale=0.01, n_queries=6000)
+    snap, orc = snapshot(g), oracle(g)
+    Q = g["queries"]
+    deg = np.diff(np.searchsorted(np.sort(g["tgt_idx"]), np.arange(g["num_atoms"] + 1)))
+    hubs = [int(h) for h in np.argsort(-deg)[:4]]
+    rng = np.random.default_rng(77)
+    qs = []
+    for i in range(6000):
+        k = i % 10
+        if k < 6:
+            qs.append((int(Q["type"][i]), [int(Q["a"][i])], (int(Q["x"][i]), -1, int(Q["y"][i]))))
+        elif k < 8:
+            a = int(Q["a"][i])
+            qs.append((-1, [a, int(Q["x"][i]), a], None))
+        elif k == 8:
+            qs.append((int(Q["type"][i]), [hubs[i % 4]], None) if i % 20 == 8 else (-1, [int(Q["a"][i])], ()))
+        else:
+            qs.append((-1, [hubs[(i // 10) % 4]], (int(Q["x"][i]),)))
+    arrs = _packed(qs)
+    for rep in range(2):
+        snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
+        fused = pattern_batch_arrays(snap, *arrs)
+        snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 0)
+        general = pattern_batch_arrays(snap, *arrs)
+        _same(fused, general, len(qs))
+    assert max(len(fused[q]) for q in range(len(qs))) > 64
+    for q in rng.choice(len(qs), 600, replace=False):
+        t, inc, pat = qs[q]
+        assert fused[q].tolist() == orc.and_query(t, inc, pat).tolist(), qs[q]
+    # a 70-entry anchor list: the whole batch goes to the general path, same results
+    long_q = (-1, [int(Q["a"][0])] * 70, None)
+    arrs2 = _packed(qs[:100] + [long_q])
+    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
+    r1 = pattern_batch_arrays(snap, *arrs2)
+    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 0)
+    r2 = pattern_batch_arrays(snap, *arrs2)
+    _same(r1, r2, 101)
+    assert r1[100].tolist() == orc.and_query(-1, [int(Q["a"][0])], None).tolist()
+    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
