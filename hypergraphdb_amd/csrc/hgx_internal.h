@@ -205,7 +205,7 @@ struct hgx_graph {
     size_t mapped_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
-    bool q_fused = true;                        // HGX_OPT_QUERY_FUSED: small packed batches in one launch
+    bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels
     int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
     int64_t q_chunk_guess = 0;                  // fused pattern path: chunk area of the chunked queries
 

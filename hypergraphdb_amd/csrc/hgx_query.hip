@@ -31,7 +31,9 @@ namespace hgx {
 
 typedef unsigned long long u64;
 
-constexpr int kQChunk = 1024;       // candidates per wave-chunk (16 per lane)
+constexpr int kQChunk = 256;        // candidates per wave-chunk (4 per lane): with 1024 the 41 config-3
+                                    // queries above 1024 candidates kept the match at ~30 us of
+                                    // dependent loads per chunk
 constexpr int kMaxAnchors = 32;
 constexpr int kMaxPattern = 64;     // targets of one OrderedLinkCondition
 constexpr int kMaxPatterns = 16;    // OrderedLinkConditions in one And
@@ -764,7 +766,7 @@ __global__ void hgx_q_finish_stat(int32_t n, const int32_t* __restrict__ chunk_o
 // ---------------------------------------------------------------------------------------------
 constexpr int kFusedMax = 16384;   // batches up to this size take the fused kernels
 constexpr int kFusedHold = 64;     // hits a query keeps in its own slot
-constexpr int kInline = 1024;      // candidates a query's own wave matches; larger ones go to chunks
+constexpr int kInline = 256;       // candidates a query's own wave matches; larger ones go to chunks
 constexpr int kMaxBig = 1024;      // chunked queries per batch (more: the batch takes the general path)
 constexpr int qProbe = qNum;       // counter slot: type-slice probes
 
@@ -1814,9 +1816,11 @@ bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_
         int32_t* chunk_cnt = (int32_t*)w.take(sizeof(int32_t) * (size_t)chunk_cap);
         const size_t m_off = (sizeof(FusedHead) + 15) & ~(size_t)15;
         const size_t m_ids = m_off + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
+        // result area on the device, copied back in one piece with as many ids as recent batches
+        // needed (the kernel writing small host-mapped words one by one over PCIe was slower)
+        char* dm = (char*)w.take(m_ids + 4 * (size_t)cap);
         char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)cap);
-        char* dm = nullptr;
-        HGX_HIP(hipHostGetDevicePointer((void**)&dm, hm, 0));
+        const int64_t guess = std::min<int64_t>(cap, std::max<int64_t>(g->q_hits_guess, 1024));
         if (attempt > 0)   // fresh status and counter words
             HGX_HIP(hipMemcpyAsync(d + o_stat, h + o_stat, o_ovfn + 8 - o_stat, hipMemcpyHostToDevice, s));
         ev.rec(1, s);
@@ -1836,6 +1840,7 @@ bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_
                                                  (const u64*)(d + o_ctr), (FusedHead*)dm, (int64_t*)(dm + m_off),
                                                  (int32_t*)(dm + m_ids), cap);
         HGX_CHECK_LAUNCH();
+        HGX_HIP(hipMemcpyAsync(hm, dm, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
         ev.rec(3, s);
         HGX_HIP(hipStreamSynchronize(s));
         const FusedHead* hd = (const FusedHead*)hm;
@@ -1846,11 +1851,18 @@ bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_
         if (hd->err[2]) return false;
         const int64_t total = hd->total;
         if (total > cap || hd->ovf || hd->chunk_need > 0) {   // an area was too small: grow it and run again
-            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: result sizing failed");
+            // (a chunk-area overflow leaves the chunked queries' hits out of the total, so growing the
+            // chunk area can take one more round to size the result area)
+            if (attempt > 1) fail(HGX_E_DEVICE, "hgx_pattern_batch: result sizing failed");
             g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
             g->q_ovf_guess = std::max<int64_t>(g->q_ovf_guess, hd->ovf_need + hd->ovf_need / 4);
             g->q_chunk_guess = std::max<int64_t>(g->q_chunk_guess, (int64_t)hd->chunk_need + hd->chunk_need / 4);
             continue;
+        }
+        if (total > guess) {
+            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, dm + m_ids + 4 * (size_t)guess,
+                                   4 * (size_t)(total - guess), hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
         }
         g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
         const int64_t* qoff = (const int64_t*)(hm + m_off);

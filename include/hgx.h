@@ -345,9 +345,10 @@ void hgx_shard_free(hgx_shard *s);
  * device work one part at a time (clean per-part device times for a one-GPU rehearsal). */
 int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out);
 #define HGX_OPT_PART_SERIAL 4
-/* HGX_OPT_QUERY_FUSED: 1 (default) = hgx_pattern_batch_packed runs batches of <= 16384 queries in
- * two fused launches (a wavefront per query: expand, plan, match; then one workgroup places the hits
- * in the mapped result area); 0 = the general five-launch path for every batch (A/B). */
+/* HGX_OPT_QUERY_FUSED (A/B, default 0): 1 = hgx_pattern_batch_packed runs batches of <= 16384
+ * queries in three fused launches (a wavefront per query expands, plans and matches; a chunk kernel
+ * takes queries above 256 candidates; one workgroup places the hits).  Measured slower than the
+ * general path on config 3 (0.318 vs 0.211 ms wall, profiles/r02v_pattern_ab.log), kept for A/B. */
 #define HGX_OPT_QUERY_FUSED 5
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
