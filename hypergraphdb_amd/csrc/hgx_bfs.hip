@@ -224,6 +224,25 @@ __device__ __forceinline__ void wave_add_sh(u64* ctr, u64 v) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr + shard * kCtrStride, v);
 }
 
+// Block-wide sum of v added into shard (blockIdx.x % kStatShards) of counter c: stats[shard *
+// kStatStride + c].  Every thread of the block calls it.  One device atomic per block spread over 16
+// lines: thousands of waves adding into one word serialise at ~90 adds/us (a 4096-wave kernel spent
+// ~90 us there per counter).
+constexpr int kStatShards = 16, kStatStride = 16;
+__device__ __forceinline__ void block_add_sh(u64* stats, int c, u64 v) {
+    __shared__ u64 part[16];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) part[wv] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 t = 0;
+        for (int w = 0; w < nw; ++w) t += part[w];
+        if (t) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + c, t);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Link gather: lf[L] = OR_{v in targets(L), fa_d(v)} lvl_d[v]; la(L) set iff the row was written.
 // A wave owns 64 consecutive link rows (one la word); a G-lane group handles one row at a time.
@@ -681,7 +700,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                                                       u64* __restrict__ vis, u64* __restrict__ ever,
                                                       u64* __restrict__ full, u64* __restrict__ lvl_next,
                                                       u64* __restrict__ fa_next, u64* __restrict__ ctr, FullMask fm,
-                                                      int flags) {
+                                                      int flags, const u64* __restrict__ own) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PW = Lay<W>::PER_WAVE;
     constexpr int JB = G >= 8 ? JBX : G;   // atoms of a group interleaved at once (register budget)
     static_assert(G >= 4, "pull2 needs G >= 4");
@@ -696,6 +715,9 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
     u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
         const u64 ever_w = ever[tile], full_w = full[tile];
+        // partition part: a ghost's new row is partial and its vis / ever are rewritten by the
+        // broadcast of the owner's final row (hgx_x_apply), so the pull writes neither for ghosts
+        const u64 own_w = own ? own[tile] : ~0ull;
         const int64_t tme = tile * 64 + lane;
         int64_t bme = 0;
         int dme = 0;
@@ -796,7 +818,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                     const typename V::T nw = acc[jj] & ~old[jj];
                     if (group_any<G>(V::nz(nw))) {
                         st_row<V>(lvl_next + t * W + sub * WPL, nw, nt_out);
-                        st_row<V>(vis + t * W + sub * WPL, old[jj] | nw, nt_out);
+                        if ((own_w >> pos) & 1ull) st_row<V>(vis + t * W + sub * WPL, old[jj] | nw, nt_out);
                         isnew = true;
                         becomes_full = group_all<G>(V::eq(old[jj] | nw, FULL));
                         if (sub == 0) { n_newdeg += (u64)dj[jj]; if (!becomes_full) n_newdeg_nf += (u64)dj[jj]; }
@@ -815,7 +837,7 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
         }
         if (lane == 0) {
             fa_next[tile] = new_w;
-            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
+            if (new_w & own_w & ~ever_w) ever[tile] = ever_w | (new_w & own_w);
             if (fullnew_w) full[tile] = full_w | fullnew_w;
             n_new += __popcll(new_w);
             n_full += __popcll(fullnew_w);
@@ -2078,7 +2100,7 @@ __global__ void hgx_depth_probe(int32_t nlev, const u64* const* __restrict__ fa,
 // line of its own), pass 2 loads the rows again and writes the records at LDS-counted offsets.  One
 // atomic per wave per destination (7 cursors on one line) serialised to ~25 ms a level at config-4
 // scale.
-constexpr int kCurStride = 16;   // cursor q: [q * kCurStride] records, [q * kCurStride + 8] words
+constexpr int kCurStride = 32;   // cursor q: [q * kCurStride] records, [q * kCurStride + 16] words (own lines)
 constexpr int kMaxParts = 64;
 
 struct PackLds {
@@ -2153,7 +2175,7 @@ __device__ __forceinline__ void pack_reserve(PackLds& sh, u64* __restrict__ curs
     for (int d = threadIdx.x; d < NP; d += 256) {
         const unsigned int r = sh.rec[d], w = sh.wrd[d];
         sh.base_r[d] = r ? atomicAdd(&cursor[d * kCurStride], (u64)r) : 0ull;
-        sh.base_w[d] = w ? atomicAdd(&cursor[d * kCurStride + 8], (u64)w) : 0ull;
+        sh.base_w[d] = w ? atomicAdd(&cursor[d * kCurStride + 16], (u64)w) : 0ull;
         sh.slot[d] = 0ull;
     }
 }
@@ -2253,7 +2275,7 @@ __global__ void __launch_bounds__(256) hgx_xr_pack(int64_t A, const u64* __restr
             pack_reserve(sh, cursor, NP);
             __syncthreads();
         } else if (pass == 1) {
-            wave_add(nzw, nz);
+            block_add_sh(nzw, 2, nz);
         }
     }
 }
@@ -2319,25 +2341,29 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
                         const unsigned int nnz = (unsigned int)__popc(mask);
                         if (pass < 0) {
                             sample_add(samp, sn[u] > 0 && sub == 0, nzm);
-                        } else if (pass == 0) {
-                            if (sub == 0)
-                                for (int e = 0; e < sn[u]; ++e) {
-                                    const int q = bc_part[sb[u] + e];
-                                    atomicAdd(&sh.rec[q], 1u);
-                                    atomicAdd(&sh.wrd[q], nnz);
+                            continue;
+                        }
+                        if (pass == 1 && sn[u] > 0 && sub == 0) nz += (u64)__popc(nzm);
+                        int emax = sn[u];
+                        for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
+                        // the atom's other holders, G at a time: lane sub of the group loads entry e0 + sub
+                        // (independent loads instead of one dependent load per holder)
+                        for (int e0 = 0; e0 < emax; e0 += G) {   // wave-uniform
+                            const bool mine = e0 + sub < sn[u];
+                            const int hq = mine ? bc_part[sb[u] + e0 + sub] : 0;
+                            const int32_t hl = mine ? bc_lid[sb[u] + e0 + sub] : 0;
+                            if (pass == 0) {
+                                if (mine) {
+                                    atomicAdd(&sh.rec[hq], 1u);
+                                    atomicAdd(&sh.wrd[hq], nnz);
                                 }
-                        } else {
-                            if (sn[u] > 0 && sub == 0) nz += (u64)__popc(nzm);
-                            int emax = sn[u];
-                            for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
-                            for (int e = 0; e < emax; ++e) {   // wave-uniform: the e-th other holder
-                                const bool has = e < sn[u];
-                                int q = 0;
-                                int32_t lid = 0;
-                                if (has) {
-                                    q = bc_part[sb[u] + e];
-                                    lid = bc_lid[sb[u] + e];
-                                }
+                                continue;
+                            }
+                            const int kmax = min(G, emax - e0);
+                            for (int k = 0; k < kmax; ++k) {   // wave-uniform: holder e0 + k of each group's atom
+                                const int q = __shfl(hq, gbase + k);
+                                const int32_t lid = __shfl(hl, gbase + k);
+                                const bool has = e0 + k < sn[u];
                                 u64 pk = 0;
                                 if (has && sub == 0) pk = atomicAdd(&sh.slot[q], 1ull | ((u64)nnz << 32));
                                 pk = __shfl(pk, gbase);
@@ -2357,7 +2383,7 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
             pack_reserve(sh, cursor, NP);
             __syncthreads();
         } else if (pass == 1) {
-            wave_add(nzw, nz);
+            block_add_sh(nzw, 2, nz);
         }
     }
 }
@@ -2432,8 +2458,8 @@ __global__ void __launch_bounds__(256) hgx_frontier_stats(int64_t A, const u64* 
         if ((x >> lane) & 1ull) deg += (u64)(inc_off[v + 1] - inc_off[v]);
         if (lane == 0) n += __popcll(x & own[w]);
     });
-    wave_add(out, n);
-    wave_add(out + 1, deg);
+    block_add_sh(out, 0, n);
+    block_add_sh(out, 1, deg);
 }
 
 }  // namespace hgx
@@ -2611,7 +2637,8 @@ struct Exchange {
     u64* recv_h = nullptr;
     u64* send_p = nullptr;              // payload streams (W words per record at most)
     u64* recv_p = nullptr;
-    u64* dctr = nullptr;                // [NP * kCurStride] cursors, then frontier stats [0..1], nonzero words [2]
+    u64* dctr = nullptr;                // [NP * kCurStride] cursors, then kStatShards x kStatStride stats:
+                                        // [0] owned new atoms, [1] push volume, [2] nonzero words
     int64_t* seg = nullptr;             // [4 * NP] device: reduce h / p, broadcast h / p segment starts
     std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast; records), NP + 1 entries
     double bytes_sent = 0, nz_words = 0, words = 0;
@@ -2630,7 +2657,7 @@ struct Exchange {
         recv_h = (u64*)g->alloc(sizeof(u64) * 2 * (size_t)cap_recs);
         send_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
         recv_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
-        dctr = (u64*)g->alloc(sizeof(u64) * (NP * kCurStride + 4));
+        dctr = (u64*)g->alloc(sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride));
         seg = (int64_t*)g->alloc(sizeof(int64_t) * 4 * NP);
         std::vector<int64_t> hs(4 * (size_t)NP);
         for (int q = 0; q < NP; ++q) {
@@ -2648,7 +2675,7 @@ struct Exchange {
         g->release(recv_h, sizeof(u64) * 2 * (size_t)cap_recs);
         g->release(send_p, sizeof(u64) * W * (size_t)cap_recs);
         g->release(recv_p, sizeof(u64) * W * (size_t)cap_recs);
-        g->release(dctr, sizeof(u64) * (NP * kCurStride + 4));
+        g->release(dctr, sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride));
         g->release(seg, sizeof(int64_t) * 4 * NP);
     }
     // collective step: the part's device work is bracketed by compute_begin / compute_end
@@ -2708,19 +2735,24 @@ struct Exchange {
         const int64_t A = g->A;
         const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(A, 64) / 4 + 1, 2048));
         const double before = bytes_sent;
-        const size_t cbytes = sizeof(u64) * (NP * kCurStride + 4);
-        u64* xs = dctr + NP * kCurStride;   // [0..1] frontier stats, [2] nonzero words
-        std::vector<u64> hc(NP * kCurStride + 4), cnt(NP), wcnt(NP);
+        const size_t cbytes = sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride);
+        u64* xs = dctr + NP * kCurStride;   // sharded stats (see dctr)
+        std::vector<u64> hc(NP * kCurStride + kStatShards * kStatStride), cnt(NP), wcnt(NP);
+        auto stat_sum = [&](int c) {
+            u64 t = 0;
+            for (int k = 0; k < kStatShards; ++k) t += hc[(size_t)NP * kCurStride + k * kStatStride + c];
+            return t;
+        };
         std::vector<int64_t> rcnt;
         auto read_counts = [&]() {
             HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
             HGX_HIP(hipStreamSynchronize(s));
             for (int q = 0; q < NP; ++q) {
                 cnt[q] = hc[(size_t)q * kCurStride];
-                wcnt[q] = hc[(size_t)q * kCurStride + 8];
+                wcnt[q] = hc[(size_t)q * kCurStride + 16];
                 words += (double)cnt[q] * Wt;
             }
-            nz_words += (double)hc[(size_t)NP * kCurStride + 2];
+            nz_words += (double)stat_sum(2);
         };
         auto apply = [&](bool reduce, const std::vector<int64_t>& rbase) {
             for (int q = 0; q < NP; ++q) {
@@ -2740,7 +2772,7 @@ struct Exchange {
         Events e0 = tm.start(kKindExchange, d);
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
         hgx_xr_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_lid, lvl_next, dctr,
-                                              seg, seg + NP, send_h, send_p, xs + 2, NP);
+                                              seg, seg + NP, send_h, send_p, xs, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e0);
         read_counts();
@@ -2750,7 +2782,7 @@ struct Exchange {
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
         hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
-                                              lvl_next, dctr, seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs + 2, NP);
+                                              lvl_next, dctr, seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
         read_counts();
@@ -2761,9 +2793,9 @@ struct Exchange {
             A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
-        u64 fs[2];
-        HGX_HIP(hipMemcpyAsync(fs, xs, sizeof(fs), hipMemcpyDeviceToHost, s));
+        HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
+        const u64 fs[2] = {stat_sum(0), stat_sum(1)};
         *push_volume = fs[1];
         *level_bytes = bytes_sent - before;
         *pair_max = pm_r + pm_b;
@@ -2786,6 +2818,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const size_t bm_bytes = res->bm_bytes();
     const size_t la_bytes = sizeof(u64) * (size_t)(M / 64 + 2);
     const FullMask fm = full_mask(bt.S, W);
+    const u64* own_bm = g->shard ? (const u64*)g->shard->own_bm : nullptr;   // partition part: owned atoms
     // a partition part's device work runs between compute_begin / compute_end (the exchange releases
     // it around each collective); the guard releases it on an error path too
     struct Gate {
@@ -3089,10 +3122,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 // placed in descending degree order (A/B)
                 if (lflags & 2048)
                     hgx_atom_pull2<W, 2, true><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
-                                                                           ever, full, lvl_next, fa_next, c, fm, lflags);
+                                                                           ever, full, lvl_next, fa_next, c, fm, lflags,
+                                                                           own_bm);
                 else
                     hgx_atom_pull2<W, 2, false><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
-                                                                            ever, full, lvl_next, fa_next, c, fm, lflags);
+                                                                            ever, full, lvl_next, fa_next, c, fm, lflags,
+                                                                            own_bm);
             }
         }
         if (!(v2 && MODE == kSym))
