@@ -693,8 +693,8 @@ hgx_link_gather2_o5(int64_t M, const int64_t* __restrict__ tgt_off, const int32_
     gather2_body<W, WRITE_LF>(M, tgt_off, tgt_idx, link_type, want_type, fa, full, lvl, lf, la, ctr, fm, flags);
 }
 
-template <int W, int JBX, bool SORT>
-__global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* __restrict__ inc_off,
+template <int W, int JBX, bool SORT, int KR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KR < Lay<W>::G ? 4 : 1, 8))) hgx_atom_pull2(int64_t A, const int64_t* __restrict__ inc_off,
                                                       const int32_t* __restrict__ inc_row,
                                                       const u64* __restrict__ la, const u64* __restrict__ lf,
                                                       u64* __restrict__ vis, u64* __restrict__ ever,
@@ -778,14 +778,18 @@ __global__ void __launch_bounds__(256) hgx_atom_pull2(int64_t A, const int64_t* 
                 for (int jj = 0; jj < JB; ++jj) {
                     const unsigned ga = (unsigned)((__ballot((pa >> jj) & 1u) >> base) & gmask);
                     if (ga) {   // group-uniform
-                        typename V::T r[G];
+                        // KR of the G rows in flight at once (KR < G: fewer VGPRs, more waves/SIMD)
 #pragma unroll
-                        for (int k = 0; k < G; ++k) {
-                            const int32_t Lk = __shfl(myL[jj], base + k);
-                            r[k] = ((ga >> k) & 1u) ? V::ld(lf + (int64_t)Lk * W + sub * WPL) : V::zero();
+                        for (int k0 = 0; k0 < G; k0 += KR) {
+                            typename V::T r[KR];
+#pragma unroll
+                            for (int k = 0; k < KR; ++k) {
+                                const int32_t Lk = __shfl(myL[jj], base + k0 + k);
+                                r[k] = ((ga >> (k0 + k)) & 1u) ? V::ld(lf + (int64_t)Lk * W + sub * WPL) : V::zero();
+                            }
+#pragma unroll
+                            for (int k = 0; k < KR; ++k) acc[jj] |= r[k];
                         }
-#pragma unroll
-                        for (int k = 0; k < G; ++k) acc[jj] |= r[k];
                         n_inc += __popc(ga);
                     }
                     if (done[jj]) continue;   // group-uniform from here on
@@ -1986,28 +1990,33 @@ __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __re
     for (int j = threadIdx.x; j < W * 64; j += 256) partial[(int64_t)blockIdx.x * (W * 64) + j] = lc[j];
 }
 
-// counts[l][j] = sum over the blocks of the partial counts of level slot l (one launch for every
-// level of the readout): a thread per (slot, source), the block partials read with 8 loads in flight.
+// counts[l][j] += the partial counts of level slot l over one range of kReduceSpan blocks (one launch
+// for every level of the readout; counts zeroed first): a thread per (slot, source, block range), the
+// partials read 8 loads in flight.  One thread per (slot, source) walking all 2048 blocks took ~0.18 ms.
+constexpr int kReduceSpan = 128;
 __global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t* __restrict__ nblk,
                                                         const int32_t* __restrict__ width,
                                                         const int64_t* __restrict__ poff,
                                                         const uint32_t* __restrict__ partial, u64* __restrict__ counts) {
+    constexpr int NR = kCountBlocks / kReduceSpan;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= (int64_t)nslot * 1024) return;
-    const int sl = (int)(i / 1024), j = (int)(i % 1024);
+    if (i >= (int64_t)nslot * 1024 * NR) return;
+    const int r = (int)(i % NR);
+    const int64_t sj = i / NR;
+    const int sl = (int)(sj / 1024), j = (int)(sj % 1024);
     const int wj = width[sl];
     if (j >= wj) return;
     const uint32_t* p = partial + poff[sl] + j;
-    const int nb = nblk[sl];
+    const int b0 = r * kReduceSpan, b1 = min(nblk[sl], b0 + kReduceSpan);
     u64 sum = 0;
-    for (int b0 = 0; b0 < nb; b0 += 8) {
+    for (int b = b0; b < b1; b += 8) {
         uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = b0 + u < nb ? p[(int64_t)(b0 + u) * wj] : 0u;
+        for (int u = 0; u < 8; ++u) v[u] = b + u < b1 ? p[(int64_t)(b + u) * wj] : 0u;
 #pragma unroll
         for (int u = 0; u < 8; ++u) sum += v[u];
     }
-    counts[(int64_t)sl * 1024 + j] = sum;
+    if (sum) atomicAdd(&counts[(int64_t)sl * 1024 + j], sum);
 }
 
 // Compaction of {v : fa(v) && bit s of lvl[v]} in ascending order.  Pass 1 (write = false)
@@ -2446,18 +2455,28 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
 }
 
 // out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
-// over the whole local frontier (the next level's local push volume).  A wave visits the nonzero
-// frontier words; the degrees of a word's atoms come from one coalesced pair of offset loads.
+// over the whole local frontier (the next level's local push volume).  A thread per bitmap word; the
+// degrees of a run of consecutive frontier atoms are one difference of incidence offsets, so a
+// dense word costs two loads (a wave walking its nonzero words one after the other took ~50 us of
+// dependent loads even on a near-empty level).
 __global__ void __launch_bounds__(256) hgx_frontier_stats(int64_t A, const u64* __restrict__ fa,
                                                           const u64* __restrict__ own,
                                                           const int64_t* __restrict__ inc_off, u64* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (A + 63) / 64;
     u64 n = 0, deg = 0;
-    for_nonzero_words(fa, (A + 63) / 64, [&](int64_t w, u64 x) {
-        const int64_t v = w * 64 + lane;
-        if ((x >> lane) & 1ull) deg += (u64)(inc_off[v + 1] - inc_off[v]);
-        if (lane == 0) n += __popcll(x & own[w]);
-    });
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x) {
+        u64 x = fa[w];
+        if (!x) continue;
+        n += __popcll(x & own[w]);
+        const int64_t base = w * 64;
+        while (x) {
+            const int a0 = __ffsll((long long)x) - 1;
+            const u64 rest = ~(x >> a0);
+            const int r = rest ? __ffsll((long long)rest) - 1 : 64 - a0;   // run length
+            deg += (u64)(inc_off[base + a0 + r] - inc_off[base + a0]);
+            x &= (r + a0 >= 64) ? 0ull : (~0ull << (a0 + r));
+        }
+    }
     block_add_sh(out, 0, n);
     block_add_sh(out, 1, deg);
 }
@@ -2789,7 +2808,7 @@ struct Exchange {
         ship(bseg, rseg, cnt, wcnt, rcnt, &pm_b);
         Events e2 = tm.start(kKindExchange, d);
         apply(false, rseg);
-        hgx_frontier_stats<<<grid_for(ceil_div(A, 64 * 64) * 64, 256, 1024), 256, 0, s>>>(
+        hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
             A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
@@ -3118,16 +3137,15 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             if (v2)
             {
                 // two atoms of a group interleaved (152 VGPRs, 3 waves/SIMD): config 2 pull 5.73 -> 5.23 ms
-                // a step against four (184 VGPRs, 2 waves/SIMD, dropped in r02); bit 11 = the tile's atoms
-                // placed in descending degree order (A/B)
+                // a step against four (184 VGPRs, 2 waves/SIMD, dropped in r02); a tile's atoms placed in
+                // descending degree order (5.20 -> 5.13 ms, profiles/r02r_ab_pull_sort.log).  Bit 11 (A/B):
+                // half of a group's rows in flight at once (fewer VGPRs, more waves per SIMD).
                 if (lflags & 2048)
-                    hgx_atom_pull2<W, 2, true><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
-                                                                           ever, full, lvl_next, fa_next, c, fm, lflags,
-                                                                           own_bm);
+                    hgx_atom_pull2<W, 2, true, Lay<W>::G / 2><<<pull_grid, block, 0, s>>>(
+                        A, g->inc_off, g->inc_row, la, lf, vis, ever, full, lvl_next, fa_next, c, fm, lflags, own_bm);
                 else
-                    hgx_atom_pull2<W, 2, false><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, la, lf, vis,
-                                                                            ever, full, lvl_next, fa_next, c, fm, lflags,
-                                                                            own_bm);
+                    hgx_atom_pull2<W, 2, true, Lay<W>::G><<<pull_grid, block, 0, s>>>(
+                        A, g->inc_off, g->inc_row, la, lf, vis, ever, full, lvl_next, fa_next, c, fm, lflags, own_bm);
             }
         }
         if (!(v2 && MODE == kSym))
@@ -3310,8 +3328,10 @@ void ensure_counts(hgx_bfs_result* r) {
     size_t k = 0;
     for (auto& bt : r->batches)
         for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) count_rows_dispatch(bt.W, g, bt.fa[d], own, bt.lvl[d], dp + poff[k]);
+    HGX_HIP(hipMemsetAsync(dc, 0, bytes, g->stream));
     if (nslots) {
-        hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024, 256), 256, 0, g->stream>>>(
+        hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024 * (kCountBlocks / kReduceSpan), 256), 256, 0,
+                           g->stream>>>(
             (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots,
             (const int64_t*)(dm + sizeof(int32_t) * meta.size()), dp, dc);
         HGX_CHECK_LAUNCH();

@@ -167,8 +167,8 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bit 9 = ordered-mode push levels are pipelined: the next level is issued
  *                              before this level's counters reach the host,
  *                      bit 10 = the dense gather built for 5 waves/SIMD (spills VGPRs; diagnostic A/B only),
- *                      bit 11 = the dense pull places a tile's atoms on its lane groups in
- *                              descending degree order (A/B only),
+ *                      bit 11 = the dense pull keeps half of a lane group's rows in flight at
+ *                              once (fewer VGPRs, more waves per SIMD; A/B only),
  *                      bits 12 / 13 / 14 = nontemporal loads of the streamed CSR columns / stores of
  *                              the gather's link rows / stores of the pull's atom rows (A/B only),
  *                      bit 15 = the symmetric-mode hub pull keeps two incidence chunks in flight
