@@ -25,7 +25,6 @@
 //   * a pull stops as soon as acc | vis covers every traversal, a gather as soon as acc does.
 // Bitmaps are 64-bit words owned by one wavefront each (a wave processes 64 consecutive rows), so
 // they are written with plain stores -- no per-row atomics.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>

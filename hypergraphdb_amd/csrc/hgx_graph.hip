@@ -5,7 +5,8 @@
 //  -> BJEStorageImplementation.getIncidenceResultSet storage/bdb-je/.../BJEStorageImplementation.java:405-439)
 // with one device-resident CSR built once per snapshot: pins are keyed (target << 32 | link row),
 // radix-sorted on the GPU, de-duplicated (putNoDupData, :300-307) and cut into rows.
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -322,13 +323,10 @@ hgx_graph* hgx::graph_create(const hgx_graph_desc* d, int32_t device, bool links
             end_bit = 32 + ab;            // UINT64_MAX sentinels still sort last
             if (end_bit > 64) end_bit = 64;
         }
-        size_t tmp_bytes = 0;
-        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, sorted, (int)0, 0, end_bit, s));
-        // hipcub takes int num_items: sort in one call when it fits, else fail loudly.
-        if (P > (int64_t)INT32_MAX) fail(HGX_E_UNSUPPORTED, "hgx_graph_create: more than 2^31-1 pins per device");
-        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, sorted, (int)P, 0, end_bit, s));
+        size_t tmp_bytes = 0;   // rocPRIM takes 64-bit sizes: no 2^31-1 pin limit
+        HGX_HIP(rocprim::radix_sort_keys(nullptr, tmp_bytes, keys, sorted, (size_t)P, 0u, (unsigned)end_bit, s));
         void* tmp = g->alloc(tmp_bytes);
-        HGX_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, sorted, (int)P, 0, end_bit, s));
+        HGX_HIP(rocprim::radix_sort_keys(tmp, tmp_bytes, keys, sorted, (size_t)P, 0u, (unsigned)end_bit, s));
         unsigned long long hdup = 0;
         HGX_HIP(hipMemcpyAsync(&hdup, ndup, sizeof(hdup), hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));

@@ -16,7 +16,8 @@
 // which reads one short target row per candidate instead of zig-zag probes.  Candidates are
 // visited in ascending order, so the result is ascending like the reference's.  A candidate
 // failing the type filter (one 4-byte read) never touches its target row.
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -97,14 +98,22 @@ __device__ __forceinline__ bool positioned(const int32_t* __restrict__ row, int 
 }
 
 // Keys of the type-grouped incidence: (atom << 32 | type), value = link row; a stable radix sort
-// keeps the rows of one (atom, type) ascending.
-__global__ void __launch_bounds__(256) k_ts_keys(int64_t A, const int64_t* __restrict__ inc_off,
+// keeps the rows of one (atom, type) ascending.  The owning atom of every entry comes from a max-scan
+// over markers (atom + 1 at the first entry of each non-empty row), so the keys are written a thread
+// per entry: the first version walked each row with one wavefront and a 1M-entry hub kept one wave
+// busy for ~15 ms (36 ms for config 3).
+__global__ void __launch_bounds__(256) k_ts_mark(int64_t A, const int64_t* __restrict__ inc_off,
+                                                 int32_t* __restrict__ mark) {
+    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A; a += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = inc_off[a];
+        if (inc_off[a + 1] > b) mark[b] = (int32_t)(a + 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ts_keys(int64_t I, const int32_t* __restrict__ atom1,
                                                  const int32_t* __restrict__ inc_type, u64* __restrict__ keys) {
-    const int lane = threadIdx.x & 63;   // a wave per atom: hub rows are written 64 entries at a time
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t a = wave; a < A; a += nwave)
-        for (int64_t i = inc_off[a] + lane; i < inc_off[a + 1]; i += 64) keys[i] = ((u64)a << 32) | (uint32_t)inc_type[i];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x)
+        keys[i] = ((u64)(uint32_t)(atom1[i] - 1) << 32) | (uint32_t)inc_type[i];
 }
 
 __global__ void __launch_bounds__(256) k_low32(int64_t n, const u64* __restrict__ keys, int32_t* __restrict__ out) {
@@ -1473,12 +1482,26 @@ void ensure_type_grouped(hgx_graph* g) {
     if (g->inc_ts_row || g->I == 0) return;
     hipStream_t s = g->stream;
     const int64_t I = g->I;
-    if (I > (int64_t)INT32_MAX) fail(HGX_E_UNSUPPORTED, "type-grouped incidence: more than 2^31-1 entries");
     u64* keys = (u64*)g->alloc(sizeof(u64) * I);
     u64* keys2 = (u64*)g->alloc(sizeof(u64) * I);
     int32_t* rows2 = (int32_t*)g->alloc(sizeof(int32_t) * I);
-    k_ts_keys<<<grid_for(g->A * 64, 256, 16384), 256, 0, s>>>(g->A, g->inc_off, g->inc_type, keys);
-    HGX_CHECK_LAUNCH();
+    {   // owning atom of every entry: markers, max-scan, keys
+        int32_t* mark = (int32_t*)g->alloc(sizeof(int32_t) * I);
+        int32_t* atom1 = (int32_t*)g->alloc(sizeof(int32_t) * I);
+        HGX_HIP(hipMemsetAsync(mark, 0, sizeof(int32_t) * I, s));
+        k_ts_mark<<<grid_for(g->A, 256, 65536), 256, 0, s>>>(g->A, g->inc_off, mark);
+        HGX_CHECK_LAUNCH();
+        size_t sb = 0;
+        HGX_HIP(rocprim::inclusive_scan(nullptr, sb, mark, atom1, (size_t)I, rocprim::maximum<int32_t>(), s));
+        void* st = g->alloc(sb);
+        HGX_HIP(rocprim::inclusive_scan(st, sb, mark, atom1, (size_t)I, rocprim::maximum<int32_t>(), s));
+        k_ts_keys<<<grid_for(I, 256, 65536), 256, 0, s>>>(I, atom1, g->inc_type, keys);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipStreamSynchronize(s));
+        g->release(st, sb);
+        g->release(mark, sizeof(int32_t) * I);
+        g->release(atom1, sizeof(int32_t) * I);
+    }
     int end_bit = 64;
     {
         int ab = 1;
@@ -1486,9 +1509,9 @@ void ensure_type_grouped(hgx_graph* g) {
         end_bit = std::min(64, 32 + ab);
     }
     size_t tb = 0;
-    HGX_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys2, g->inc_row, rows2, (int)I, 0, end_bit, s));
+    HGX_HIP(rocprim::radix_sort_pairs(nullptr, tb, keys, keys2, g->inc_row, rows2, (size_t)I, 0u, (unsigned)end_bit, s));
     void* tmp = g->alloc(tb);
-    HGX_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, g->inc_row, rows2, (int)I, 0, end_bit, s));
+    HGX_HIP(rocprim::radix_sort_pairs(tmp, tb, keys, keys2, g->inc_row, rows2, (size_t)I, 0u, (unsigned)end_bit, s));
     int32_t *ts_row = nullptr, *ts_type = nullptr;
     HGX_HIP(hipMalloc(&ts_row, sizeof(int32_t) * I));
     HGX_HIP(hipMalloc(&ts_type, sizeof(int32_t) * I));
@@ -1678,12 +1701,12 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
             HGX_HIP(hipMemsetAsync(f.nch + n, 0, sizeof(int32_t), s));
             HGX_HIP(hipMemsetAsync(f.ncand + n, 0, sizeof(int64_t), s));
             size_t b1 = 0, b2 = 0;
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, f.nch, choff, n + 1, s));
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, f.ncand, coff, n + 1, s));
+            HGX_HIP(rocprim::exclusive_scan(nullptr, b1, f.nch, choff, (int32_t)0, (size_t)n + 1, rocprim::plus<int32_t>(), s));
+            HGX_HIP(rocprim::exclusive_scan(nullptr, b2, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
             size_t tb = std::max(b1, b2);
             void* tmp = w.take(tb);
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, f.nch, choff, n + 1, s));
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, f.ncand, coff, n + 1, s));
+            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.nch, choff, (int32_t)0, (size_t)n + 1, rocprim::plus<int32_t>(), s));
+            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
             hgx_q_check<<<1, 1, 0, s>>>(n, choff, coff, capC, capK, stat_d);
             HGX_CHECK_LAUNCH();
             hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, choff, stat_d, chq);
@@ -1705,9 +1728,9 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
             HGX_CHECK_LAUNCH();
         } else {
             size_t tb = 0;
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, outoff, capC + 1, s));
+            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
             void* tmp = w.take(tb);
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, outoff, capC + 1, s));
+            HGX_HIP(rocprim::exclusive_scan(tmp, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
             hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, choff, outoff, stat_d, qoff_d);
             HGX_CHECK_LAUNCH();
             hgx_q_scatter<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(d_nchunks, chq, choff, coff, cnt, outoff,

@@ -19,8 +19,9 @@
 //
 // Data-parallel structure per level:  flat incidence items (entry, j) of the frontier
 // -> hgx_seq_expand (one item per lane, block-local entry search) -> gather final keys ->
-// hipcub radix sort by key -> hgx_seq_decode (next frontier + (link, atom) pairs).
-#include <hipcub/hipcub.hpp>
+// rocPRIM radix sort by key -> hgx_seq_decode (next frontier + (link, atom) pairs).
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -329,7 +330,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     }
     DevBuf<u64> key(g), knew(g), ksort(g);
     DevBuf<int32_t> fa(g), fs(g), na(g), ns(g), olink(g), dseeds(g);
-    DevBuf<int64_t> pre(g), list(g), lsort(g);
+    DevBuf<int64_t> pre(g), pre_in(g), list(g), lsort(g);
     DevBuf<u64> cnt(g);
     DevBuf<char> tmp(g);
     u64* h_cnt = (u64*)g->pinned_buf(64);
@@ -350,11 +351,13 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         for (int32_t d = 0; F > 0 && d < maxd; ++d) {
             // degree prefix over the frontier entries
             int64_t* dpre = pre.get(F + 1);
-            k_seq_degree<<<grid_for(F + 1, 256), 256, 0, st>>>(F, cur_a, g->inc_off, dpre);
+            int64_t* ddeg = pre_in.get(F + 1);
+            k_seq_degree<<<grid_for(F + 1, 256), 256, 0, st>>>(F, cur_a, g->inc_off, ddeg);
             HGX_CHECK_LAUNCH();
             size_t tb = 0;
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, dpre, dpre, (int)(F + 1), st));
-            HGX_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.get(tb), tb, dpre, dpre, (int)(F + 1), st));
+            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, ddeg, dpre, (int64_t)0, (size_t)F + 1, rocprim::plus<int64_t>(), st));
+            HGX_HIP(rocprim::exclusive_scan(tmp.get(tb), tb, ddeg, dpre, (int64_t)0, (size_t)F + 1, rocprim::plus<int64_t>(),
+                                            st));
             HGX_HIP(hipMemcpyAsync(&h_cnt[0], dpre + F, sizeof(int64_t), hipMemcpyDeviceToHost, st));
             HGX_HIP(hipStreamSynchronize(st));
             const int64_t T = (int64_t)h_cnt[0];
@@ -374,7 +377,6 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             if (nn > cap) fail(HGX_E_DEVICE, "hgx_bfs_sequence: discovery list overflow");
             e_base += (u64)F;
             if (nn == 0) break;
-            if (nn > (int64_t)INT32_MAX) fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: level larger than 2^31-1");
             // order the discoveries by stream key
             u64* dk = knew.get(nn);
             u64* dks = ksort.get(nn);
@@ -383,8 +385,8 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             HGX_CHECK_LAUNCH();
             const int end_bit = std::min(64, sh_e + bitlen(e_base));
             tb = 0;
-            HGX_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dks, dlist, dls, (int)nn, 0, end_bit, st));
-            HGX_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(tb), tb, dk, dks, dlist, dls, (int)nn, 0, end_bit, st));
+            HGX_HIP(rocprim::radix_sort_pairs(nullptr, tb, dk, dks, dlist, dls, (size_t)nn, 0u, (unsigned)end_bit, st));
+            HGX_HIP(rocprim::radix_sort_pairs(tmp.get(tb), tb, dk, dks, dlist, dls, (size_t)nn, 0u, (unsigned)end_bit, st));
             int32_t* nxa = na.get(nn);
             int32_t* nxs = ns.get(nn);
             int32_t* ol = olink.get(nn);

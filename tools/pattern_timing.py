@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--queries", type=int, default=10_000)
-    ap.add_argument("--fused", default="1", help="HGX_OPT_QUERY_FUSED values to compare, interleaved (e.g. 1,0)")
+    ap.add_argument("--fused", default="0", help="HGX_OPT_QUERY_FUSED values to compare, interleaved (e.g. 1,0)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
