@@ -524,12 +524,21 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     readout = 0
+    phase = {"bfs_batch": 0.0, "readout": 0.0, "stats+close": 0.0}   # host wall split of the steps
     for _ in range(args.steps):
+        ta = time.perf_counter()
         res = H.bfs_batch(snap, g["seeds"], args.depth)
+        tb = time.perf_counter()
         readout += int(res.counts().sum())   # the result readout: per-source per-depth counts (D2H)
+        tc = time.perf_counter()
         stats.append(res.stats(accounting=False))
         res.close()
+        phase["bfs_batch"] += tb - ta
+        phase["readout"] += tc - tb
+        phase["stats+close"] += time.perf_counter() - tc
     barrier_sync()
+    log(f"rank {rank}: host wall per step (ms): " +
+        ", ".join(f"{k} {v / max(args.steps, 1) * 1e3:.3f}" for k, v in phase.items()))
     dt = max_over_ranks(time.perf_counter() - t0)
     assert readout == args.steps * acct_visits, "readout differs from the warm-up batch"
     edges_total = sum_over_ranks(acct["traversed_edges"] * args.steps)

@@ -28,6 +28,10 @@ HGX_OPT_SEQ_BUDGET = 2
 HGX_OPT_RANKS_ORDERED = 3
 HGX_OPT_PART_SERIAL = 4
 HGX_OPT_QUERY_FUSED = 5
+HGX_OPT_QUERY_INLINE = 6
+HGX_OPT_PUSH_BATCH = 7
+HGX_OPT_PART_EXCHANGE = 8
+HGX_OPT_QUERY_FLAT = 9
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (

@@ -1540,6 +1540,287 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
     wave_add_sh(ctr + cScanned, n_scan);
 }
 
+// Flattened frontier push (HGX_OPT_PUSH_BATCH = K > 0): a wave takes K consecutive list atoms at
+// once and expands their incidence entries into one stream (a wave prefix sum over the degrees, an
+// entry's atom found by a binary search over the prefix in LDS), so its lanes carry the entries of
+// many atoms instead of the few of one.  Stage 1 prefilters type + yield flags (kUnroll passes in
+// flight), stage 2 runs the entry chain (link row, target offsets, <= 8 targets in registers, full
+// bits) for the passing entries 64 at a time and stages the eligible (target, source) pairs in LDS,
+// stage 3 ORs each pair's source row into the target's accumulator row, one G-lane group per pair
+// (16-byte loads of the source row; a word is ORed only when it is nonzero and missing).  With one
+// wave per atom, a config-5 level of ~30K atoms of degree ~4 kept 2048 waves on ~15 sequential
+// dependent chains each, with ~4 of 64 lanes busy.
+constexpr int kFlatMax = 64;     // atoms per batch at most (one per lane)
+constexpr int kPairBuf = 512;    // (target, source) pairs staged per wave
+
+struct FlatLds {
+    int32_t v[kFlatMax];
+    int64_t beg[kFlatMax];
+    int32_t pre[kFlatMax + 1];   // inclusive prefix of the batch's degrees, pre[0] = 0
+    int32_t ej[kEBuf];           // passing entries: batch slot of the atom
+    int64_t ei[kEBuf];           //                  incidence entry
+    int32_t pt[kPairBuf];        // pairs: target
+    int32_t ps[kPairBuf];        //        source atom
+    int32_t cbuf[kCBuf];         // fresh candidates not yet appended
+};
+
+__device__ __forceinline__ void flat_cand_flush(FlatLds& sh, int& cc, int32_t* __restrict__ clist,
+                                                u64* __restrict__ n_clist) {
+    const int lane = threadIdx.x & 63;
+    if (cc == 0) return;
+    u64 base = 0;
+    if (lane == 0) base = atomicAdd(n_clist, (u64)cc);
+    base = __shfl(base, 0);
+    for (int i = lane; i < cc; i += 64) clist[base + i] = sh.cbuf[i];
+    __builtin_amdgcn_wave_barrier();
+    cc = 0;
+}
+
+// Stage 3: OR the source row of every staged pair into its target's accumulator row; the first
+// pair to reach a target sets its candidate bit and stages it for the candidate list.
+template <int W>
+__device__ __forceinline__ void flat_pairs(FlatLds& sh, int& np, int& cc, const u64* __restrict__ lvl,
+                                           u64* __restrict__ acc, u64* __restrict__ cand,
+                                           int32_t* __restrict__ clist, u64* __restrict__ n_clist) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
+    typedef Vec<WPL> V;
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const u64 lt = (1ull << lane) - 1ull;
+    __builtin_amdgcn_wave_barrier();
+    for (int p0 = 0; p0 < np; p0 += PER) {   // wave-uniform
+        const int p = p0 + g;
+        const bool ok = p < np;
+        const int32_t t = ok ? sh.pt[p] : 0;
+        const int32_t src = ok ? sh.ps[p] : 0;
+        bool fresh = false;
+        if (ok) {
+            const typename V::T row = V::ld(lvl + (int64_t)src * W + sub * WPL);
+            u64* a = acc + (int64_t)t * W + sub * WPL;
+            if constexpr (WPL == 1) {
+                if (row != 0ull && (*a & row) != row) atomicOr(a, row);
+            } else {
+                if (V::nz(row)) {
+                    const typename V::T cur = V::ld(a);
+                    if (row.x != 0ull && (cur.x & row.x) != row.x) atomicOr(a, row.x);
+                    if (row.y != 0ull && (cur.y & row.y) != row.y) atomicOr(a + 1, row.y);
+                }
+            }
+            if (sub == 0) {
+                const u64 cb = 1ull << (t & 63);
+                if (!(cand[t >> 6] & cb)) fresh = !(atomicOr(&cand[t >> 6], cb) & cb);
+            }
+        }
+        const u64 fm = __ballot(fresh);
+        if (fm) {   // wave-uniform
+            const int nf = __popcll(fm);
+            if (cc + nf > kCBuf) flat_cand_flush(sh, cc, clist, n_clist);
+            if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = t;
+            cc += nf;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    np = 0;
+}
+
+// Stage 2 for up to 64 staged entries: the generator's eligible targets of each entry's link, as
+// (target, source) pairs.
+template <int W, int MODE>
+__device__ __forceinline__ void flat_entries(FlatLds& sh, int ne, int& np, int& cc,
+                                             const int32_t* __restrict__ inc_row, const int64_t* __restrict__ tgt_off,
+                                             const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
+                                             const u64* __restrict__ full, u64* __restrict__ acc,
+                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
+                                             u64* __restrict__ n_clist, u64& n_links, u64& n_pins, u64& n_pairs) {
+    const int lane = threadIdx.x & 63;
+    const u64 lt = (1ull << lane) - 1ull;
+    constexpr int kRegRow = 8;
+    __builtin_amdgcn_wave_barrier();
+    for (int k0 = 0; k0 < ne; k0 += 64) {   // wave-uniform
+        const bool have = k0 + lane < ne;
+        int32_t v = -1;
+        int64_t b = 0;
+        int n = 0;
+        if (have) {
+            v = sh.v[sh.ej[k0 + lane]];
+            const int32_t L = inc_row[sh.ei[k0 + lane]];
+            b = tgt_off[L];
+            n = (int)(tgt_off[L + 1] - b);
+            ++n_links;
+            n_pins += (u64)n;
+        }
+        int32_t tr[kRegRow];
+        const bool reg = n <= kRegRow;
+#pragma unroll
+        for (int k = 0; k < kRegRow; ++k) tr[k] = (reg && k < n) ? tgt_idx[b + k] : -1;
+        int fv = -1, lv = -1;
+        if (reg) {
+#pragma unroll
+            for (int k = 0; k < kRegRow; ++k)
+                if (tr[k] == v) {
+                    if (fv < 0) fv = k;
+                    lv = k;
+                }
+        } else {
+            for (int p = 0; p < n; ++p)
+                if (tgt_idx[b + p] == v) {
+                    if (fv < 0) fv = p;
+                    lv = p;
+                }
+        }
+        unsigned em = 0;   // eligible register positions
+        if (reg) {
+            u64 fw[kRegRow];
+#pragma unroll
+            for (int k = 0; k < kRegRow; ++k) {
+                const bool e = tr[k] >= 0 && tr[k] != v && yields<MODE>(k, fv, lv);
+                fw[k] = e ? full[tr[k] >> 6] : ~0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < kRegRow; ++k)
+                if (!((fw[k] >> (tr[k] & 63)) & 1ull)) em |= 1u << k;
+        }
+        int nmax = n;
+        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        for (int p = 0; p < nmax; ++p) {   // wave-uniform
+            int32_t t = -1;
+            bool elig;
+            if (reg) {
+#pragma unroll
+                for (int k = 0; k < kRegRow; ++k)
+                    if (k == p) t = tr[k];
+                elig = (em >> p) & 1u;
+            } else {
+                t = p < n ? tgt_idx[b + p] : -1;
+                elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
+            }
+            const u64 m = __ballot(elig);
+            if (m == 0ull) continue;   // wave-uniform
+            if (np + 64 > kPairBuf) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
+            n_pairs += elig;
+            if (elig) {
+                const int q = np + __popcll(m & lt);
+                sh.pt[q] = t;
+                sh.ps[q] = v;
+            }
+            np += __popcll(m);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int W, int MODE>
+__global__ void __launch_bounds__(256) hgx_opush_flat(const int32_t* __restrict__ list, const u64* __restrict__ n_list,
+                                                      int K, const int64_t* __restrict__ inc_off,
+                                                      const int32_t* __restrict__ inc_row,
+                                                      const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                      const uint8_t* __restrict__ yf,
+                                                      const int64_t* __restrict__ tgt_off,
+                                                      const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
+                                                      const u64* __restrict__ full, u64* __restrict__ cand,
+                                                      int32_t* __restrict__ clist, u64* __restrict__ n_clist,
+                                                      u64* __restrict__ acc, u64* __restrict__ ctr,
+                                                      u64* __restrict__ fa_next, int64_t n_words) {
+    constexpr int kUnroll = 4;
+    __shared__ FlatLds lds[4];
+    FlatLds& sh = lds[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const u64 lt = (1ull << lane) - 1ull;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x)
+        fa_next[w] = 0ull;
+    const int64_t n = (int64_t)*n_list;
+    u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
+    int cc = 0, np = 0;   // staged candidates / pairs (wave-uniform)
+    for (int64_t k0 = wave * K; k0 < n; k0 += nwave * K) {   // wave-uniform
+        const int64_t k = k0 + lane;
+        int32_t v = -1;
+        if (lane < K && k < n) v = list[k];
+        int64_t beg = 0;
+        int deg = 0;
+        if (v >= 0) {
+            beg = inc_off[v];
+            deg = (int)(inc_off[v + 1] - beg);
+        }
+        int incl = deg;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const int E = __shfl(incl, 63);
+        if (E == 0) continue;   // wave-uniform
+        sh.v[lane] = v;
+        sh.beg[lane] = beg;
+        sh.pre[lane + 1] = incl;
+        if (lane == 0) sh.pre[0] = 0;
+        __builtin_amdgcn_wave_barrier();
+        int ne = 0;   // staged passing entries (wave-uniform)
+        for (int e0 = 0; e0 < E; e0 += 64 * kUnroll) {   // wave-uniform
+            int jj[kUnroll];
+            int64_t ii[kUnroll];
+            bool pass[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int e = e0 + u * 64 + lane;
+                pass[u] = e < E;
+                int lo = 0, hi = 63;   // the batch slot j with pre[j] <= e < pre[j + 1]
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sh.pre[mid] <= e) lo = mid; else hi = mid - 1;
+                }
+                jj[u] = lo;
+                ii[u] = pass[u] ? sh.beg[lo] + (e - sh.pre[lo]) : 0;
+            }
+            if (want_type >= 0) {
+                int32_t ty[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) ty[u] = pass[u] ? inc_type[ii[u]] : want_type;
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ty[u] == want_type;
+            }
+            if constexpr (MODE != kSym) {
+                uint8_t f[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) f[u] = pass[u] ? yf[ii[u]] : (uint8_t)0;
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ((f[u] >> MODE) & 1u);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                n_scan += e0 + u * 64 + lane < E;
+                const u64 m = __ballot(pass[u]);
+                if (m == 0ull) continue;   // wave-uniform
+                if (ne + 64 > kEBuf) {
+                    flat_entries<W, MODE>(sh, ne, np, cc, inc_row, tgt_off, tgt_idx, lvl, full, acc, cand, clist,
+                                          n_clist, n_links, n_pins, n_pairs);
+                    ne = 0;
+                }
+                if (pass[u]) {
+                    const int q = ne + __popcll(m & lt);
+                    sh.ej[q] = jj[u];
+                    sh.ei[q] = ii[u];
+                }
+                ne += __popcll(m);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (ne)
+            flat_entries<W, MODE>(sh, ne, np, cc, inc_row, tgt_off, tgt_idx, lvl, full, acc, cand, clist, n_clist,
+                                  n_links, n_pins, n_pairs);
+        // the batch's atoms leave sh.v / sh.beg for the next batch: drain the pairs first (they only
+        // keep target / source ids, but the next batch's stage 2 would append behind them: fine) --
+        // pairs stay staged across batches and drain when full or at the end
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (np) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
+    flat_cand_flush(sh, cc, clist, n_clist);
+    wave_add_sh(ctr + cActiveLinks, n_links);
+    wave_add_sh(ctr + cActivePins, n_pins);
+    wave_add_sh(ctr + cIncLight, n_pairs);
+    wave_add_sh(ctr + cScanned, n_scan);
+}
+
 template <int W, int MODE>
 __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restrict__ chunks,
                                                        const u64* __restrict__ fa,
@@ -2453,6 +2734,147 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Static-slot exchange of a dense level (HGX_OPT_PART_EXCHANGE).  When most ghosts have news, the
+// records' headers, the counting passes and the count round trips cost more than they save: every
+// ghost ships its whole row (zero without news) to a fixed slot of its owner's segment (xo_slot),
+// and the owner, which finds its holders' slots through its broadcast table (bc_slot, the same
+// ascending order on both sides), ORs them in, finishes the atom and writes the final row straight
+// into each holder's broadcast slot -- the reduce apply and the broadcast pack in one pass.  Three
+// launches a level (ghost pack, owner, ghost apply) instead of two three-pass packs and one apply
+// launch per source part and phase.
+// ---------------------------------------------------------------------------------------------
+constexpr int kXsU = 4;   // atoms per lane group in flight
+
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xs_gpack(int64_t A, const u64* __restrict__ fa_next,
+                                                    const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
+                                                    const int32_t* __restrict__ xo_slot,
+                                                    const u64* __restrict__ lvl_next, const int64_t* __restrict__ seg_w,
+                                                    u64* __restrict__ pay) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    typedef Vec<WPL> V;
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    for (int64_t t0 = grp; t0 < A; t0 += ngrp * kXsU) {
+        int64_t dst[kXsU];
+        typename V::T row[kXsU];
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {
+            const int64_t t = t0 + u * ngrp;
+            dst[u] = -1;
+            row[u] = V::zero();
+            if (t < A && !bit(own_bm, t)) {
+                const int32_t q = xo_part[t];
+                dst[u] = seg_w[q] + (int64_t)xo_slot[t] * W + sub * WPL;
+                if (bit(fa_next, t)) row[u] = V::ld(lvl_next + t * W + sub * WPL);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u)
+            if (dst[u] >= 0) V::st(pay + dst[u], row[u]);
+    }
+}
+
+// Owner pass: reduce the holders' slots into an owned atom (new = row & ~vis), then write its final
+// news (zero when none) into every holder's broadcast slot.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xs_owner(int64_t A, const u64* __restrict__ own_bm,
+                                                    const int64_t* __restrict__ bc_off, const int32_t* __restrict__ bc_part,
+                                                    const int32_t* __restrict__ bc_slot, const u64* __restrict__ recv,
+                                                    u64* __restrict__ send, const int64_t* __restrict__ seg_w,
+                                                    u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                    u64* __restrict__ vis, u64* __restrict__ ever, u64* __restrict__ full,
+                                                    FullMask fm) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    typedef Vec<WPL> V;
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    // the trip count is the same for every lane of a wave (ballots below)
+    for (int64_t t0 = grp - (grp % (64 / G)); t0 < A; t0 += ngrp) {
+        const int64_t t = t0 + (grp % (64 / G));
+        int64_t b = 0;
+        int nb = 0;
+        if (t < A && bit(own_bm, t)) {
+            b = bc_off[t];
+            nb = (int)(bc_off[t + 1] - b);
+        }
+        typename V::T acc = V::zero();
+        for (int k = 0; k < nb; ++k)   // group-uniform; the holders' slots are independent loads
+            acc |= V::ld(recv + seg_w[bc_part[b + k]] + (int64_t)bc_slot[b + k] * W + sub * WPL);
+        const bool valid = nb > 0;
+        const bool ev = valid && bit(ever, t);
+        const bool was = valid && bit(fa_next, t);
+        const typename V::T vis0 = valid ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const typename V::T lv0 = was ? V::ld(lvl_next + t * W + sub * WPL) : V::zero();
+        const typename V::T old = ev ? vis0 : V::zero();
+        const typename V::T nw = acc & ~old;
+        const bool any = group_any<G>(V::nz(nw));
+        const bool isfull = group_all<G>(V::eq(old | nw, FULL));
+        typename V::T fin = lv0;
+        if (valid && any) {
+            fin = lv0 | nw;
+            V::st(lvl_next + t * W + sub * WPL, fin);
+            V::st(vis + t * W + sub * WPL, old | nw);
+            if (sub == 0) {
+                if (!was) set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (isfull) set_bit(full, t);
+            }
+        }
+        for (int k = 0; k < nb; ++k)
+            V::st(send + seg_w[bc_part[b + k]] + (int64_t)bc_slot[b + k] * W + sub * WPL, fin);
+    }
+}
+
+// Ghost apply: the owner's final row (zero: no news) replaces the ghost's partial one.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xs_gapply(int64_t A, const u64* __restrict__ own_bm,
+                                                     const int32_t* __restrict__ xo_part,
+                                                     const int32_t* __restrict__ xo_slot, const u64* __restrict__ recv,
+                                                     const int64_t* __restrict__ seg_w, u64* __restrict__ lvl_next,
+                                                     u64* __restrict__ fa_next, u64* __restrict__ vis,
+                                                     u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    typedef Vec<WPL> V;
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    for (int64_t t0 = grp - (grp % (64 / G)); t0 < A; t0 += ngrp) {
+        const int64_t t = t0 + (grp % (64 / G));
+        const bool valid = t < A && !bit(own_bm, t);
+        typename V::T row = V::zero();
+        if (valid) row = V::ld(recv + seg_w[xo_part[t]] + (int64_t)xo_slot[t] * W + sub * WPL);
+        const bool ev = valid && bit(ever, t);
+        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        const bool any = group_any<G>(V::nz(row));
+        const bool isfull = group_all<G>(V::eq(old | row, FULL));
+        if (valid && any) {
+            V::st(lvl_next + t * W + sub * WPL, row);
+            V::st(vis + t * W + sub * WPL, old | row);
+            if (sub == 0) {
+                if (!bit(fa_next, t)) set_bit(fa_next, t);
+                if (!ev) set_bit(ever, t);
+                if (isfull) set_bit(full, t);
+            }
+        }
+    }
+}
+
+// out[3] += ghosts with news (fa_next & ~own): the exchange-mode decision of a level.
+__global__ void __launch_bounds__(256) hgx_ghost_news(int64_t A, const u64* __restrict__ fa,
+                                                      const u64* __restrict__ own, u64* __restrict__ out) {
+    const int64_t nwords = (A + 63) / 64;
+    u64 n = 0;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x)
+        n += __popcll(fa[w] & ~own[w]);
+    block_add_sh(out, 3, n);
+}
+
 // out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
 // over the whole local frontier (the next level's local push volume).  A thread per bitmap word; the
 // degrees of a run of consecutive frontier atoms are one difference of incidence offsets, so a
@@ -2660,6 +3082,7 @@ struct Exchange {
     int64_t* seg = nullptr;             // [4 * NP] device: reduce h / p, broadcast h / p segment starts
     std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast; records), NP + 1 entries
     double bytes_sent = 0, nz_words = 0, words = 0;
+    int static_levels = 0;              // levels exchanged through the static slots
     Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts;
@@ -2786,6 +3209,54 @@ struct Exchange {
             }
         };
         double pm_r = 0, pm_b = 0;
+        // exchange mode of the level (group-wide): static slots when at least half of the group's
+        // ghosts have news, compressed records otherwise (HGX_OPT_PART_EXCHANGE forces one)
+        bool stat_mode = sh.xmode == 2;
+        if (sh.xmode == 0) {
+            HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+            hgx_ghost_news<<<grid_for(ceil_div(A, 64), 256, 1024), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, xs);
+            HGX_CHECK_LAUNCH();
+            HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+            int64_t mine2[2] = {(int64_t)stat_sum(3), rseg[NP]};
+            std::vector<int64_t> all2(2 * (size_t)NP);
+            coll([&] { tr->allgather_i64(mine2, 2, all2.data(), s); });
+            int64_t news = 0, ghosts = 0;
+            for (int q = 0; q < NP; ++q) {
+                news += all2[2 * (size_t)q];
+                ghosts += all2[2 * (size_t)q + 1];
+            }
+            stat_mode = ghosts > 0 && 2 * news >= ghosts;
+        }
+        if (stat_mode) {
+            static_levels += 1;
+            // reduce: every ghost's row (zero without news) -> its slot at the owner
+            const int sgrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 8192);
+            Events e0 = tm.start(kKindExchange, d);
+            hgx_xs_gpack<Wt><<<sgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, lvl_next,
+                                                   seg + NP, send_p);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e0);
+            ship_static(rseg, sh.ghost_count, bseg, sh.bc_count, &pm_r);
+            // owners: reduce + finish + broadcast slots; then every ghost takes its final row
+            const int ogrid = grid_for(A * Lay<Wt>::G, 256, 8192);
+            Events e1 = tm.start(kKindExchange, d);
+            hgx_xs_owner<Wt><<<ogrid, 256, 0, s>>>(A, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_slot, recv_p,
+                                                   send_p, seg + 3 * NP, lvl_next, fa_next, vis, ever, full, fm);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e1);
+            ship_static(bseg, sh.bc_count, rseg, sh.ghost_count, &pm_b);
+            Events e2 = tm.start(kKindExchange, d);
+            hgx_xs_gapply<Wt><<<ogrid, 256, 0, s>>>(A, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, recv_p, seg + NP,
+                                                    lvl_next, fa_next, vis, ever, full, fm);
+            HGX_CHECK_LAUNCH();
+            HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+            hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
+                A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e2);
+            return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
+        }
         // reduce: partial rows of my ghosts -> their owners
         Events e0 = tm.start(kKindExchange, d);
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
@@ -2811,18 +3282,45 @@ struct Exchange {
             A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
+        return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
+    }
+    // the level's statistics back to the host, the group's new-atom total
+    template <class SS>
+    u64 finish_level(std::vector<u64>& hc, size_t cbytes, SS& stat_sum, u64* push_volume, double* level_bytes,
+                     double* pair_max, double before, double pm) {
+        const int NP = g->shard->n_parts;
+        hipStream_t s = g->stream;
         HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
         HGX_HIP(hipStreamSynchronize(s));
         const u64 fs[2] = {stat_sum(0), stat_sum(1)};
         *push_volume = fs[1];
         *level_bytes = bytes_sent - before;
-        *pair_max = pm_r + pm_b;
+        *pair_max = pm;
         int64_t nl = (int64_t)fs[0];
         std::vector<int64_t> nall(NP);
         coll([&] { tr->allgather_i64(&nl, 1, nall.data(), s); });
         u64 tot = 0;
         for (int q = 0; q < NP; ++q) tot += (u64)nall[q];
         return tot;
+    }
+    // One static-slot phase: scnt[q] full rows from my segment sbase[q] to q, rcnt[q] from q into
+    // rbase[q] (sizes known on both sides: no count exchange).
+    void ship_static(const std::vector<int64_t>& sbase, const std::vector<int64_t>& scnt,
+                     const std::vector<int64_t>& rbase, const std::vector<int64_t>& rcnt, double* pair_max) {
+        const int NP = g->shard->n_parts;
+        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP);
+        *pair_max = 0;
+        for (int q = 0; q < NP; ++q) {
+            soff[q] = sbase[q] * W * 8;
+            sbytes[q] = scnt[q] * W * 8;
+            roff[q] = rbase[q] * W * 8;
+            rbytes[q] = rcnt[q] * W * 8;
+            bytes_sent += (double)sbytes[q];
+            words += (double)scnt[q] * W;
+            nz_words += (double)scnt[q] * W;   // static slots: every word counts as shipped
+            *pair_max = std::max(*pair_max, (double)sbytes[q]);
+        }
+        coll([&] { tr->alltoallv(send_p, soff.data(), sbytes.data(), recv_p, roff.data(), rbytes.data(), g->stream); });
     }
 };
 
@@ -3056,9 +3554,15 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // 19-113 us against 30-142 us with 8192 waves (the launch of mostly idle workgroups and
             // the candidate-append contention) and 20-171 us with 1024 waves
             const int lgrid = 512;
-            hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
-                                                     g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
-                                                     fa_next, (int64_t)(bm_bytes / sizeof(u64)));
+            if (g->push_batch > 0)   // flattened: K atoms per wave batch (HGX_OPT_PUSH_BATCH)
+                hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->push_batch, g->inc_off, g->inc_row,
+                                                              g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl,
+                                                              full, cand, cl, n_cl, acc, c, fa_next,
+                                                              (int64_t)(bm_bytes / sizeof(u64)));
+            else
+                hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
+                                                         g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
+                                                         fa_next, (int64_t)(bm_bytes / sizeof(u64)));
             HGX_CHECK_LAUNCH();
             if (g->n_pchunks > 0) {
                 hgx_opush_heavy<W, MODE><<<(unsigned)g->n_pchunks, 256, 0, s>>>(

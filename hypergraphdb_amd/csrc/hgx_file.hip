@@ -340,6 +340,7 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     std::swap(g->inc_type, fresh->inc_type);
     std::swap(g->inc_ts_row, fresh->inc_ts_row);
     std::swap(g->inc_ts_type, fresh->inc_ts_type);
+    std::swap(g->inc_ts_tgt, fresh->inc_ts_tgt);
     std::swap(g->n_heavy, fresh->n_heavy);
     std::swap(g->I_heavy, fresh->I_heavy);
     std::swap(g->n_chunks, fresh->n_chunks);

@@ -31,7 +31,7 @@ void graph_release(hgx_graph* g) {
     for (auto e : g->ev_pool) (void)hipEventDestroy(e);
     g->ev_pool.clear();
     (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
-    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
+    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->inc_ts_tgt); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->hasinc) (void)hipFree(g->hasinc);
     if (g->inc_yf) (void)hipFree(g->inc_yf);
@@ -42,6 +42,7 @@ void graph_release(hgx_graph* g) {
     if (g->shard) {
         (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);
         (void)hipFree(g->shard->bc_off); (void)hipFree(g->shard->bc_part); (void)hipFree(g->shard->bc_lid);
+        (void)hipFree(g->shard->xo_slot); (void)hipFree(g->shard->bc_slot);
         delete g->shard;
     }
     delete g;
@@ -434,6 +435,17 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         g->shard->serial = value != 0;
     } else if (option == HGX_OPT_QUERY_FUSED) {
         g->q_fused = value != 0;
+    } else if (option == HGX_OPT_QUERY_INLINE) {
+        g->q_inline = value != 0;
+    } else if (option == HGX_OPT_PART_EXCHANGE) {
+        if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_PART_EXCHANGE applies to partition shards");
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: exchange mode outside 0..2");
+        g->shard->xmode = (int32_t)value;
+    } else if (option == HGX_OPT_QUERY_FLAT) {
+        g->q_flat = value != 0;
+    } else if (option == HGX_OPT_PUSH_BATCH) {
+        if (value < 0 || value > 64) fail(HGX_E_INVALID, "hgx_set_option: push batch outside 0..64");
+        g->push_batch = (int32_t)value;
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;

@@ -117,6 +117,12 @@ struct ShardInfo {
     int64_t* bc_off = nullptr;           // [A_local + 1] owned atom: its other holders ...
     int32_t* bc_part = nullptr;          //   ... their parts
     int32_t* bc_lid = nullptr;           //   ... and its local id there
+    // Static exchange slots (dense levels): the j-th of my ghosts owned by q (ascending ids) sends to
+    // slot j of q's receive segment from me, and q's j-th owned atom held by me (ascending ids: the
+    // same atom) answers in slot j of my receive segment from q.
+    int32_t* xo_slot = nullptr;          // [A_local] ghost: its slot in the (me -> owner) segment
+    int32_t* bc_slot = nullptr;          // [bc entries] its slot in the (me -> holder) segment
+    int32_t xmode = 0;                   // HGX_OPT_PART_EXCHANGE: 0 auto, 1 compressed records, 2 static slots
     // the global -> local id of an atom present here, or -1 (binary search of l2g_host)
     int32_t local_of(int64_t v) const {
         auto it = std::lower_bound(l2g_host.begin(), l2g_host.end(), (int32_t)v);
@@ -189,6 +195,12 @@ struct hgx_graph {
     // ascending range (found by binary search over inc_ts_type).
     int32_t* inc_ts_row = nullptr;
     int32_t* inc_ts_type = nullptr;
+    // Inline target rows of the type-grouped incidence (HGX_OPT_QUERY_INLINE, built with it): entry i
+    // holds the <= 8 targets of link inc_ts_row[i] in 32 bytes (-1 padded; slot 0 = -2 for a link of
+    // arity > 8, which the match reads through tgt_off).  A typed candidate then costs one streamed
+    // 32-byte record instead of two dependent random rows.
+    int32_t* inc_ts_tgt = nullptr;
+    bool q_inline = true;
 
     int64_t n_heavy = 0;            // heavy atoms (deg > kHeavyDegree)
     int64_t I_heavy = 0;            // incidence entries of heavy atoms
@@ -205,6 +217,8 @@ struct hgx_graph {
     size_t mapped_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
+    int32_t push_batch = 16;                    // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
+    bool q_flat = true;                         // HGX_OPT_QUERY_FLAT: a lane per candidate over the batch's flat candidate space
     bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels
     int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
     int64_t q_chunk_guess = 0;                  // fused pattern path: chunk area of the chunked queries

@@ -59,7 +59,7 @@ struct QDesc {
     int32_t pad;
 };
 
-enum QCtr { qCand = 0, qTyped, qArity, qHits, qNum = 4 };
+enum QCtr { qCand = 0, qTyped, qArity, qHits, qInline, qNum = 5 };
 
 __device__ __forceinline__ void wave_add_q(u64* ctr, u64 v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -97,6 +97,18 @@ __device__ __forceinline__ bool positioned(const int32_t* __restrict__ row, int 
     return false;
 }
 
+// The same on a target row held in registers (n <= 8): unrolled, no indexed register access.
+__device__ __forceinline__ bool positioned_regs(const int32_t (&tr)[8], int n, int32_t x, int32_t lb, int32_t ub,
+                                                bool complement) {
+    if (ub < 0) ub = n + ub;
+    if (lb < 0) lb = n + lb;
+    if (lb > ub || lb < 0 || ub < 0 || lb >= n || ub >= n) return false;
+    bool f = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f |= (i < n) && ((i >= lb && i <= ub) != complement) && tr[i] == x;
+    return f;
+}
+
 // Keys of the type-grouped incidence: (atom << 32 | type), value = link row; a stable radix sort
 // keeps the rows of one (atom, type) ascending.  The owning atom of every entry comes from a max-scan
 // over markers (atom + 1 at the first entry of each non-empty row), so the keys are written a thread
@@ -119,6 +131,24 @@ __global__ void __launch_bounds__(256) k_ts_keys(int64_t I, const int32_t* __res
 __global__ void __launch_bounds__(256) k_low32(int64_t n, const u64* __restrict__ keys, int32_t* __restrict__ out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = (int32_t)(uint32_t)keys[i];
+}
+
+// Inline target rows of the type-grouped incidence: one thread per entry writes the <= 8 targets of
+// its link as two 16-byte stores (-1 padded; slot 0 = -2 marks arity > 8).
+__global__ void __launch_bounds__(256) k_ts_inline(int64_t I, const int32_t* __restrict__ ts_row,
+                                                   const int64_t* __restrict__ tgt_off,
+                                                   const int32_t* __restrict__ tgt_idx, int4* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t L = ts_row[i];
+        const int64_t b = tgt_off[L];
+        const int n = (int)(tgt_off[L + 1] - b);
+        int32_t t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = k < n ? tgt_idx[b + k] : -1;
+        if (n > 8) t[0] = -2;
+        out[2 * i] = make_int4(t[0], t[1], t[2], t[3]);
+        out[2 * i + 1] = make_int4(t[4], t[5], t[6], t[7]);
+    }
 }
 
 __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t b, int64_t e, int32_t v) {
@@ -472,8 +502,8 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const int32_t* __restrict__ anchors, const int32_t* __restrict__ types, const int32_t* __restrict__ pos,
     const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern, const int32_t* __restrict__ inc_row,
     const int32_t* __restrict__ inc_type, const int32_t* __restrict__ inc_ts_row, const int64_t* __restrict__ tgt_off,
-    const int32_t* __restrict__ tgt_idx, int32_t* __restrict__ slots, int64_t* __restrict__ counts,
-    u64* __restrict__ ctr) {
+    const int32_t* __restrict__ tgt_idx, const int4* __restrict__ ts_tgt, int32_t* __restrict__ slots,
+    int64_t* __restrict__ counts, u64* __restrict__ ctr) {
     __shared__ int32_t lds[4][kQChunk];
     __shared__ int32_t lds_anch[4][kMaxAnchors];
     const int32_t n_chunks = *n_chunks_p;
@@ -486,6 +516,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const u64 lt = (1ull << lane) - 1ull;
     uint32_t n_cand = 0, n_typed = 0;   // <= 16 per lane and chunk: no overflow at <= 2^28 chunks a wave
+    uint32_t n_inl = 0;                 // candidates served by an inline target record
     u64 n_ar = 0, n_hits = 0;
     for (int64_t chunk = wave; chunk < n_chunks; chunk += nwave) {
         const int32_t q = __builtin_amdgcn_readfirstlane(chunk_q[chunk]);
@@ -495,6 +526,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
         const int64_t nc = pl.n - c0 < kQChunk ? pl.n - c0 : kQChunk;   // candidates of this chunk
         const bool typed = d.t_end > d.t_beg && !pl.pad;   // a type-grouped range is all of type T
         const int32_t* rows = pl.pad ? inc_ts_row : inc_row;
+        const int4* inl = pl.pad ? ts_tgt : nullptr;   // wave-uniform: inline records of a type-grouped range
         // stage 1: lane l owns candidates [l*kPerLane, (l+1)*kPerLane) of the chunk
         unsigned passm = 0;
         const int64_t cb = c0 + lane * kPerLane;
@@ -550,18 +582,35 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
             bool hit = idx < total;
             int32_t L = -1;
             if (hit) {
-                L = rows[pl.beg + c0 + list[idx]];
+                const int64_t ci = pl.beg + c0 + list[idx];
+                L = rows[ci];
                 ++n_typed;
-                const int64_t b = tgt_off[L];
-                const int n = (int)(tgt_off[L + 1] - b);
-                n_ar += (u64)n;
-                const int32_t* row = tgt_idx + b;
+                int32_t tr[8];
+                int n;
+                const int32_t* row = nullptr;   // the target row in memory (links not served inline)
+                bool have = false;
+                if (inl) {   // one streamed 32-byte record: the link's targets inline (issued with L)
+                    const int4 r0 = inl[2 * ci], r1 = inl[2 * ci + 1];
+                    tr[0] = r0.x; tr[1] = r0.y; tr[2] = r0.z; tr[3] = r0.w;
+                    tr[4] = r1.x; tr[5] = r1.y; tr[6] = r1.z; tr[7] = r1.w;
+                    have = tr[0] != -2;
+                }
+                if (have) {
+                    n = 0;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) n += tr[i] >= 0;
+                    ++n_inl;
+                } else {
+                    const int64_t b = tgt_off[L];
+                    n = (int)(tgt_off[L + 1] - b);
+                    row = tgt_idx + b;
+                    n_ar += (u64)n;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
+                }
                 // ArityCondition: layout.length == arity + 2
                 if (d.arity >= 0) hit = n == d.arity;
                 if (n <= 8) {
-                    int32_t tr[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
                     // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
                     for (int j = 0; j < na && hit; ++j) {
                         if (j == pl.amin) continue;
@@ -572,7 +621,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
                         hit = found;
                     }
                     for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
-                        hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
+                        hit = positioned_regs(tr, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
                     if (hit && reg_pat) {   // OrderedLinkCondition.satisfies on registers
                         int j = 0;
 #pragma unroll
@@ -585,15 +634,15 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
                         }
                         hit = j == np0;
                     } else {
-                        for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
+                        for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {   // greedy subsequence on registers
                             const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
-                            int i = 0;
                             int64_t j = 0;
-                            while (i < n && j < np) {
-                                const int32_t pj = pattern[pb + j];
-                                if (pj < 0 || pj == row[i]) ++j;
-                                ++i;
-                            }
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                if (i < n && j < np) {
+                                    const int32_t pj = pattern[pb + j];
+                                    if (pj < 0 || pj == tr[i]) ++j;
+                                }
                             hit = (j == np);
                         }
                     }
@@ -634,7 +683,353 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
     wave_add_q(c + qCand, (u64)n_cand);
     wave_add_q(c + qTyped, (u64)n_typed);
     wave_add_q(c + qArity, n_ar);
+    wave_add_q(c + qInline, (u64)n_inl);
     if (lane == 0 && n_hits) atomicAdd(c + qHits, n_hits);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Flat match (default; HGX_OPT_QUERY_FLAT = 0 keeps the per-query chunks above).  The candidates of
+// the batch form one flat space (query q owns [coff[q], coff[q+1])) cut into chunks of 64: a wave
+// takes a chunk and each lane one candidate, whatever query it belongs to.  Half of the config-3
+// queries have one candidate: with a wave per query chunk the batch was ~11K waves each running a
+// chain of ~6 dependent loads for a handful of live lanes; flat it is ~4K full waves.  A lane finds
+// its query in the chunk's window of coff (LDS), loads that query's plan / descriptor and checks
+// its candidate on registers (inline record or target row).  Hits are compacted per chunk (flat
+// order = query order, ascending candidates) and the chunk's hit mask gives every query its output
+// offset: q_off[q] = outoff[coff[q] / 64] + popc(hitmask & bits below coff[q] % 64).
+// ---------------------------------------------------------------------------------------------
+constexpr int kFlatChunk = 64;
+
+__global__ void __launch_bounds__(kScanBlock) hgx_q_scan_flat(int32_t n, const int64_t* __restrict__ ncand,
+                                                               int64_t* __restrict__ coff, int32_t* __restrict__ chq,
+                                                               int32_t* __restrict__ n_chunks_out, int64_t cap_chunks,
+                                                               int64_t cap_cand, int64_t* __restrict__ stat,
+                                                               u64* __restrict__ ctr) {
+    __shared__ int64_t ws64[kScanBlock / 64];
+    if (threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;
+    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kSmallBatch)
+    const int32_t q0 = threadIdx.x * per;
+    int64_t kv[16];
+    int64_t sk = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) kv[j] = (j < per && q0 + j < n) ? ncand[q0 + j] : 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sk += kv[j];
+    int64_t tk;
+    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
+    const int64_t tc = (tk + kFlatChunk - 1) / kFlatChunk;
+    const bool over = tc > cap_chunks || tk > cap_cand;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j < per && q0 + j < n) {
+            const int32_t q = q0 + j;
+            coff[q] = ek;
+            if (!over)   // the chunks whose first candidate is one of q's
+                for (int64_t c = (ek + kFlatChunk - 1) / kFlatChunk; c * kFlatChunk < ek + kv[j]; ++c) chq[c] = q;
+        }
+        ek += kv[j];
+    }
+    if (threadIdx.x == 0) {
+        coff[n] = tk;
+        *n_chunks_out = over ? 0 : (int32_t)tc;
+        stat[0] = tc;
+        stat[1] = tk;
+        stat[2] = over ? 1 : 0;
+    }
+}
+
+// Large batches: coff from a device scan; the chunk count / overflow check, then a thread per query
+// writes the chunk -> first query map.
+__global__ void hgx_q_check_flat(int32_t n, const int64_t* __restrict__ coff, int32_t* __restrict__ n_chunks_out,
+                                 int64_t cap_chunks, int64_t cap_cand, int64_t* __restrict__ stat) {
+    const int64_t k = coff[n], c = (k + kFlatChunk - 1) / kFlatChunk;
+    stat[0] = c;
+    stat[1] = k;
+    stat[2] = (c > cap_chunks || k > cap_cand) ? 1 : 0;
+    *n_chunks_out = stat[2] ? 0 : (int32_t)c;
+}
+
+__global__ void hgx_q_chunk_map_flat(int32_t n, const int64_t* __restrict__ coff, const int64_t* __restrict__ stat,
+                                     int32_t* __restrict__ chq) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n || stat[2]) return;
+    const int64_t b = coff[q], e = coff[q + 1];
+    for (int64_t c = (b + kFlatChunk - 1) / kFlatChunk; c * kFlatChunk < e; ++c) chq[c] = q;
+}
+
+// One candidate against its query's conditions (the target row in registers, n <= 8).
+__device__ __forceinline__ bool check_regs(const int32_t (&tr)[8], int n, const QDesc& d, int amin,
+                                           const int32_t* __restrict__ anchors, const int32_t* __restrict__ pos,
+                                           const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern) {
+    bool hit = d.arity < 0 || n == d.arity;
+    const int na = (int)(d.a_end - d.a_beg);
+    for (int j = 0; j < na && hit; ++j) {   // IncidentCondition of every other anchor
+        if (j == amin) continue;
+        const int32_t a = anchors[d.a_beg + j];
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) found |= (i < n) && tr[i] == a;
+        hit = found;
+    }
+    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
+        hit = positioned_regs(tr, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
+    for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {   // OrderedLinkCondition: greedy subsequence
+        const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
+        int64_t j = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i < n && j < np) {
+                const int32_t pj = pattern[pb + j];
+                if (pj < 0 || pj == tr[i]) ++j;
+            }
+        hit = (j == np);
+    }
+    return hit;
+}
+
+// The same on a target row in memory (links of arity > 8).
+__device__ __forceinline__ bool check_mem(const int32_t* __restrict__ row, int n, const QDesc& d, int amin,
+                                          const int32_t* __restrict__ anchors, const int32_t* __restrict__ pos,
+                                          const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern) {
+    bool hit = d.arity < 0 || n == d.arity;
+    for (int64_t j = d.a_beg; j < d.a_end && hit; ++j) {
+        if (j - d.a_beg == amin) continue;
+        const int32_t a = anchors[j];
+        bool found = false;
+        for (int i = 0; i < n && !found; ++i) found = row[i] == a;
+        hit = found;
+    }
+    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
+        hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
+    for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
+        const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
+        int i = 0;
+        int64_t j = 0;
+        while (i < n && j < np) {
+            const int32_t pj = pattern[pb + j];
+            if (pj < 0 || pj == row[i]) ++j;
+            ++i;
+        }
+        hit = (j == np);
+    }
+    return hit;
+}
+
+__global__ void __launch_bounds__(256) hgx_pattern_match_flat(
+    const int32_t* __restrict__ n_chunks_p, int32_t n, const int32_t* __restrict__ chq, const int64_t* __restrict__ coff,
+    const QPlan* __restrict__ plan, const QDesc* __restrict__ desc, const int32_t* __restrict__ anchors,
+    const int32_t* __restrict__ types, const int32_t* __restrict__ pos, const int64_t* __restrict__ p_off,
+    const int32_t* __restrict__ pattern, const int32_t* __restrict__ inc_row, const int32_t* __restrict__ inc_type,
+    const int32_t* __restrict__ inc_ts_row, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
+    const int4* __restrict__ ts_tgt, int32_t* __restrict__ slots, int64_t* __restrict__ counts,
+    u64* __restrict__ hitmask, u64* __restrict__ ctr) {
+    __shared__ int64_t win[4][kFlatChunk + 1];
+    int64_t* cw = win[threadIdx.x >> 6];
+    const int32_t n_chunks = *n_chunks_p;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const u64 lt = (1ull << lane) - 1ull;
+    const int64_t total = coff[n];
+    u64 n_cand = 0, n_typed = 0, n_ar = 0, n_hits = 0, n_inl = 0;
+    for (int64_t k = wave; k < n_chunks; k += nwave) {
+        const int32_t q0 = __builtin_amdgcn_readfirstlane(chq[k]);
+        // the chunk's window of query offsets: queries q0 .. q0 + 64
+        cw[lane] = q0 + lane <= n ? coff[q0 + lane] : INT64_MAX;
+        if (lane == 0) cw[kFlatChunk] = q0 + kFlatChunk <= n ? coff[q0 + kFlatChunk] : INT64_MAX;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t f = k * kFlatChunk + lane;
+        const bool valid = f < total;
+        int32_t q = q0;
+        if (valid) {
+            if (cw[kFlatChunk] <= f) {   // more than 64 queries in the chunk (empty ones): search coff
+                int32_t lo = q0, hi = n - 1;
+                while (lo < hi) {
+                    const int32_t mid = (lo + hi + 1) >> 1;
+                    if (coff[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                q = lo;
+            } else {
+                int lo = 0, hi = kFlatChunk - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (cw[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                q = q0 + lo;
+            }
+        }
+        bool hit = false;
+        int32_t L = -1;
+        if (valid) {
+            const QPlan pl = plan[q];
+            const QDesc d = desc[q];
+            const int64_t ci = pl.beg + (f - coff[q]);
+            const bool typed = d.t_end > d.t_beg && !pl.pad;
+            hit = true;
+            if (typed) {
+                ++n_cand;
+                hit = type_in(inc_type[ci], types, d.t_beg, d.t_end);
+            }
+            if (hit) {
+                L = (pl.pad ? inc_ts_row : inc_row)[ci];
+                ++n_typed;
+                int32_t tr[8];
+                bool have = false;
+                if (pl.pad && ts_tgt) {
+                    const int4 r0 = ts_tgt[2 * ci], r1 = ts_tgt[2 * ci + 1];
+                    tr[0] = r0.x; tr[1] = r0.y; tr[2] = r0.z; tr[3] = r0.w;
+                    tr[4] = r1.x; tr[5] = r1.y; tr[6] = r1.z; tr[7] = r1.w;
+                    have = tr[0] != -2;
+                }
+                int nt = 0;
+                if (have) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) nt += tr[i] >= 0;
+                    ++n_inl;
+                    hit = check_regs(tr, nt, d, pl.amin, anchors, pos, p_off, pattern);
+                } else {
+                    const int64_t b = tgt_off[L];
+                    nt = (int)(tgt_off[L + 1] - b);
+                    n_ar += (u64)nt;
+                    if (nt <= 8) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) tr[i] = i < nt ? tgt_idx[b + i] : -1;
+                        hit = check_regs(tr, nt, d, pl.amin, anchors, pos, p_off, pattern);
+                    } else {
+                        hit = check_mem(tgt_idx + b, nt, d, pl.amin, anchors, pos, p_off, pattern);
+                    }
+                }
+            }
+        }
+        const u64 m = __ballot(hit);
+        if (hit) slots[k * kFlatChunk + __popcll(m & lt)] = L;
+        if (lane == 0) {
+            counts[k] = __popcll(m);
+            hitmask[k] = m;
+        }
+        n_hits += hit;
+        __builtin_amdgcn_wave_barrier();
+    }
+    u64* c = ctr + (wave & (kQShards - 1)) * kQStride;
+    wave_add_q(c + qCand, n_cand);
+    wave_add_q(c + qTyped, n_typed);
+    wave_add_q(c + qArity, n_ar);
+    wave_add_q(c + qInline, n_inl);
+    wave_add_q(c + qHits, n_hits);
+}
+
+// Small flat batches: one workgroup scans the chunk hit counts, writes every query's offset from the
+// hit masks and sums the counter shards; hgx_q_scatter_flat then copies the hits, a wave per chunk.
+__global__ void __launch_bounds__(kScanBlock) hgx_q_finish_flat(
+    int32_t n, const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ coff,
+    const int64_t* __restrict__ counts, const u64* __restrict__ hitmask, const u64* __restrict__ ctr,
+    int64_t* __restrict__ outoff, int64_t* __restrict__ q_off, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
+    const int32_t* __restrict__ err) {
+    __shared__ int64_t ws[kScanBlock / 64];
+    if (stat[2]) {   // workspace overflow: nothing was matched, the host re-runs
+        if (threadIdx.x == 0) {
+            stat[3] = 0;
+            stat[4] = err ? err[0] : INT32_MAX;
+            stat[5] = err ? err[1] : INT32_MAX;
+        }
+        return;
+    }
+    const int32_t nc = *n_chunks_p;
+    const int32_t per = (nc + kScanBlock - 1) / kScanBlock;
+    const int32_t c0 = threadIdx.x * per, c1 = min(nc, c0 + per);
+    int64_t tot, e;
+    if (per <= 16) {
+        int64_t kv[16];
+        int64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) kv[j] = c0 + j < c1 ? counts[c0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += kv[j];
+        e = block_exclusive_scan<int64_t>(sum, ws, tot);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (c0 + j < c1) outoff[c0 + j] = e;
+            e += kv[j];
+        }
+    } else {
+        const int64_t sum = seg_sum<int64_t>(counts, c0, c1);
+        e = block_exclusive_scan<int64_t>(sum, ws, tot);
+        for (int32_t c = c0; c < c1; ++c) {
+            outoff[c] = e;
+            e += counts[c];
+        }
+    }
+    if (threadIdx.x == 0) {
+        outoff[nc] = tot;
+        stat[3] = tot;
+        stat[4] = err ? err[0] : INT32_MAX;
+        stat[5] = err ? err[1] : INT32_MAX;
+    }
+    __syncthreads();
+    {   // n <= kSmallBatch: <= 17 queries per thread, the load rounds issued together
+        constexpr int R = kSmallBatch / kScanBlock + 1;
+        int64_t cf[R], ov[R];
+        u64 hm[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int32_t q = threadIdx.x + j * kScanBlock;
+            cf[j] = q <= n ? coff[q] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int64_t k = cf[j] / kFlatChunk;
+            ov[j] = outoff[k];
+            hm[j] = k < nc ? hitmask[k] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int32_t q = threadIdx.x + j * kScanBlock;
+            const int b = (int)(cf[j] % kFlatChunk);
+            if (q <= n) q_off[q] = ov[j] + __popcll(hm[j] & ((1ull << b) - 1ull));
+        }
+    }
+    if (threadIdx.x < qNum) {
+        u64 v = 0;
+        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
+        ctr_out[threadIdx.x] = v;
+    }
+}
+
+// Large flat batches: every query's offset from the scanned chunk counts and the hit masks.
+__global__ void hgx_q_offsets_flat(int32_t n, const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ coff,
+                                   const int64_t* __restrict__ outoff, const u64* __restrict__ hitmask,
+                                   const int64_t* __restrict__ stat, int64_t* __restrict__ q_off) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > n || stat[2]) return;
+    const int64_t cf = coff[q], k = cf / kFlatChunk;
+    const u64 hm = k < *n_chunks_p ? hitmask[k] : 0ull;
+    q_off[q] = outoff[k] + __popcll(hm & ((1ull << (cf % kFlatChunk)) - 1ull));
+}
+
+__global__ void __launch_bounds__(256) hgx_q_scatter_flat(const int32_t* __restrict__ n_chunks_p,
+                                                          const int64_t* __restrict__ counts,
+                                                          const int64_t* __restrict__ out_off,
+                                                          const int32_t* __restrict__ slots,
+                                                          const int32_t* __restrict__ link_atom, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (k >= *n_chunks_p) return;
+    if (lane < counts[k]) out[out_off[k] + lane] = link_atom[slots[k * kFlatChunk + lane]];
+}
+
+__global__ void hgx_q_finish_stat_flat(const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ outoff,
+                                       const u64* __restrict__ ctr, int64_t* __restrict__ stat,
+                                       u64* __restrict__ ctr_out, const int32_t* __restrict__ err) {
+    if (threadIdx.x == 0) {
+        stat[3] = stat[2] ? 0 : outoff[*n_chunks_p];
+        stat[4] = err ? err[0] : INT32_MAX;
+        stat[5] = err ? err[1] : INT32_MAX;
+    }
+    if (threadIdx.x < qNum) {
+        u64 v = 0;
+        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
+        ctr_out[threadIdx.x] = v;
+    }
 }
 
 // Copy each chunk's hits to its output position, mapping link rows to atom ids.
@@ -1527,6 +1922,25 @@ void ensure_type_grouped(hgx_graph* g) {
     g->inc_ts_type = ts_type;
 }
 
+// Inline target records of the type-grouped incidence (32 B per entry), built after the index when
+// HGX_OPT_QUERY_INLINE is on and the device has room for them (a quarter of the free memory at most).
+void ensure_ts_inline(hgx_graph* g) {
+    if (!g->q_inline || g->inc_ts_tgt || !g->inc_ts_row || g->I == 0) return;
+    const size_t bytes = (size_t)32 * (size_t)g->I;
+    size_t free_b = 0, total_b = 0;
+    HGX_HIP(hipMemGetInfo(&free_b, &total_b));
+    if (bytes > free_b / 4) {
+        g->q_inline = false;   // no room: the match reads target rows through tgt_off
+        return;
+    }
+    int4* t = nullptr;
+    HGX_HIP(hipMalloc(&t, bytes));
+    k_ts_inline<<<grid_for(g->I, 256, 65536), 256, 0, g->stream>>>(g->I, g->inc_ts_row, g->tgt_off, g->tgt_idx, t);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipStreamSynchronize(g->stream));
+    g->inc_ts_tgt = (int32_t*)t;
+}
+
 // Device arrays of one normalised batch (built by a front end) and the per-query plan.
 struct Front {
     const QDesc* desc = nullptr;
@@ -1662,12 +2076,135 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
     f.cond_bytes = 20.0 * (double)(n_inc + n_pat) + 4.0 * n + 4.0 * (double)n_pat + (double)sizeof(QDesc) * n;
 }
 
+// Flat back end (HGX_OPT_QUERY_FLAT, default): the candidates of the batch in chunks of 64, a wave
+// per chunk and a lane per candidate (hgx_pattern_match_flat); the rest as back_end below.
+void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
+                   double t0) {
+    (void)sc;
+    hipStream_t s = g->stream;
+    const bool small = n <= kSmallBatch;
+    if (g->q_cap_chunks < (int64_t)n / 4 + 64) g->q_cap_chunks = (int64_t)n / 4 + 64;
+    if (g->q_cap_cand < 16 * (int64_t)n + 4096) g->q_cap_cand = 16 * (int64_t)n + 4096;
+    for (int attempt = 0;; ++attempt) {
+        const int64_t capC = std::max<int64_t>(g->q_cap_chunks, ceil_div(g->q_cap_cand, kFlatChunk)), capK = g->q_cap_cand;
+        if (capC > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
+        Scratch w{g, {}};
+        int64_t* coff = (int64_t*)w.take(sizeof(int64_t) * (n + 1));
+        int32_t* chq = (int32_t*)w.take(sizeof(int32_t) * capC);
+        int32_t* nch = (int32_t*)w.take(sizeof(int32_t) * 4);
+        int32_t* slots = (int32_t*)w.take(sizeof(int32_t) * capC * kFlatChunk);
+        int64_t* cnt = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        u64* hmask = (u64*)w.take(sizeof(u64) * (capC + 1));
+        int64_t* outoff = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        u64* ctr = (u64*)w.take(sizeof(u64) * kQShards * kQStride);
+        const size_t m_stat = 0, m_ctr = 64, m_qoff = 128;
+        const size_t m_ids = m_qoff + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
+        char* rd = (char*)w.take(m_ids + 4 * (size_t)capK);
+        int64_t* stat_d = (int64_t*)(rd + m_stat);
+        u64* ctr_d = (u64*)(rd + m_ctr);
+        int64_t* qoff_d = (int64_t*)(rd + m_qoff);
+        int32_t* ids_d = (int32_t*)(rd + m_ids);
+        if (small) {
+            hgx_q_scan_flat<<<1, kScanBlock, 0, s>>>(n, f.ncand, coff, chq, nch, capC, capK, stat_d, ctr);
+            HGX_CHECK_LAUNCH();
+        } else {
+            HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
+            HGX_HIP(hipMemsetAsync(f.ncand + n, 0, sizeof(int64_t), s));
+            size_t tb = 0;
+            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
+            void* tmp = w.take(tb);
+            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
+            hgx_q_check_flat<<<1, 1, 0, s>>>(n, coff, nch, capC, capK, stat_d);
+            HGX_CHECK_LAUNCH();
+            hgx_q_chunk_map_flat<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, coff, stat_d, chq);
+            HGX_CHECK_LAUNCH();
+        }
+        ev.rec(1, s);
+        hgx_pattern_match_flat<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+            nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
+            g->inc_ts_row, g->tgt_off, g->tgt_idx, g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt,
+            hmask, ctr);
+        HGX_CHECK_LAUNCH();
+        ev.rec(2, s);
+        if (small) {
+            hgx_q_finish_flat<<<1, kScanBlock, 0, s>>>(n, nch, coff, cnt, hmask, ctr, outoff, qoff_d, stat_d, ctr_d,
+                                                        f.err);
+            HGX_CHECK_LAUNCH();
+        } else {
+            size_t tb = 0;
+            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
+            void* tmp = w.take(tb);
+            HGX_HIP(hipMemsetAsync(cnt + capC, 0, sizeof(int64_t), s));
+            HGX_HIP(rocprim::exclusive_scan(tmp, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
+            hgx_q_offsets_flat<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, nch, coff, outoff, hmask, stat_d, qoff_d);
+            HGX_CHECK_LAUNCH();
+        }
+        hgx_q_scatter_flat<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(nch, cnt, outoff, slots, g->link_atom,
+                                                                              ids_d);
+        HGX_CHECK_LAUNCH();
+        if (!small) {
+            hgx_q_finish_stat_flat<<<1, 64, 0, s>>>(nch, outoff, ctr, stat_d, ctr_d, f.err);
+            HGX_CHECK_LAUNCH();
+        }
+        const int64_t guess = std::min<int64_t>(capK, std::max<int64_t>(g->q_hits_guess, 1024));
+        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
+        HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
+        ev.rec(3, s);
+        HGX_HIP(hipStreamSynchronize(s));
+        const int64_t* stat = (const int64_t*)(hm + m_stat);
+        const u64* ctr_h = (const u64*)(hm + m_ctr);
+        const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
+        const int32_t* ids_h = (const int32_t*)(hm + m_ids);
+        if (stat[4] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(stat[4]));
+        if (stat[5] < n)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(stat[5]) +
+                                        " is not accelerated (no incidence anchor or condition limits)");
+        if (stat[2]) {   // workspace too small: grow to the reported totals and match again
+            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: workspace sizing failed");
+            g->q_cap_chunks = std::max<int64_t>(capC, stat[0] + stat[0] / 4 + 64);
+            g->q_cap_cand = std::max<int64_t>(capK, stat[1] + stat[1] / 4 + 4096);
+            continue;
+        }
+        const int64_t total = stat[3];
+        if (total > guess) {
+            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, ids_d + guess, 4 * (size_t)(total - guess),
+                                   hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+        }
+        g->q_hits_guess = total + total / 4;
+        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
+        r->ids.assign(ids_h, ids_h + total);
+        if (prof)
+            std::fprintf(stderr, "[hgx query] flat n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n",
+                         n, now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
+        if (ev.on) {
+            float a = 0, b = 0;
+            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
+            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
+            r->ms_total = a;
+            r->ms_match = b;
+        }
+        // algorithmic bytes of hgx_pattern_match_flat: per chunk its first query and its window of
+        // query offsets; per candidate its query's plan + descriptor (once per query) and, when its
+        // range is not type-grouped, its type; per examined candidate its link row and its inline
+        // record or tgt_off pair + target row; per chunk its count and hit mask; 4 B per hit; the
+        // conditions
+        r->bytes_match = (4.0 + 8.0 * (kFlatChunk + 1) + 16.0) * (double)stat[0] +
+                         (double)(sizeof(QPlan) + sizeof(QDesc)) * n + 4.0 * (double)ctr_h[qCand] +
+                         4.0 * (double)ctr_h[qTyped] + 32.0 * (double)ctr_h[qInline] +
+                         16.0 * ((double)ctr_h[qTyped] - (double)ctr_h[qInline]) + 4.0 * (double)ctr_h[qArity] +
+                         4.0 * (double)ctr_h[qHits] + f.cond_bytes;
+        return;
+    }
+}
+
 // Back end shared by every entry point: chunk tables, match, compaction into one result area that
 // goes back in one copy, one synchronisation.  The candidate / chunk workspace has a capacity kept on the graph;
 // a batch that exceeds it is detected on the device (nothing is matched), the capacity grows to the
 // reported totals and the back end runs again.
 void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
               double t0) {
+    if (g->q_flat) return back_end_flat(g, n, f, sc, ev, r, prof, t0);
     hipStream_t s = g->stream;
     const bool small = n <= kSmallBatch;
     if (g->q_cap_chunks < (int64_t)n + 64) g->q_cap_chunks = (int64_t)n + 64;
@@ -1716,7 +2253,8 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
         ev.rec(1, s);
         hgx_pattern_match<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
             d_nchunks, chq, choff, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row,
-            g->inc_type, g->inc_ts_row, g->tgt_off, g->tgt_idx, slots, cnt, ctr);
+            g->inc_type, g->inc_ts_row, g->tgt_off, g->tgt_idx,
+            g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt, ctr);
         HGX_CHECK_LAUNCH();
         ev.rec(2, s);
         if (small) {
@@ -1779,11 +2317,13 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
             r->ms_match = b;
         }
         // algorithmic bytes of hgx_pattern_match: per streamed candidate its type (4 B; none in a
-        // type-grouped range), per examined candidate its link row, tgt_off pair and target row,
-        // 4 B per hit, per chunk its plan / descriptor, plus the conditions
-        r->bytes_match = 4.0 * (double)ctr_h[qCand] + 20.0 * (double)ctr_h[qTyped] + 4.0 * (double)ctr_h[qArity] +
-                         4.0 * (double)ctr_h[qHits] + (8.0 + sizeof(QPlan) + sizeof(QDesc)) * (double)stat[0] +
-                         f.cond_bytes;
+        // type-grouped range), per examined candidate its link row (4 B) and either its 32-byte inline
+        // record or its tgt_off pair and target row, 4 B per hit, per chunk its plan / descriptor, plus
+        // the conditions
+        r->bytes_match = 4.0 * (double)ctr_h[qCand] + 4.0 * (double)ctr_h[qTyped] +
+                         32.0 * (double)ctr_h[qInline] + 16.0 * ((double)ctr_h[qTyped] - (double)ctr_h[qInline]) +
+                         4.0 * (double)ctr_h[qArity] + 4.0 * (double)ctr_h[qHits] +
+                         (8.0 + sizeof(QPlan) + sizeof(QDesc)) * (double)stat[0] + f.cond_bytes;
         return;
     }
 }
@@ -1926,6 +2466,7 @@ int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn fron
         std::lock_guard<std::mutex> lk(g->mu);
         HGX_HIP(hipSetDevice(g->device));
         ensure_type_grouped(g);
+        ensure_ts_inline(g);
         Scratch sc{g, {}};
         Events ev;
         ev.init(g->timing);

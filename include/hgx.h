@@ -350,6 +350,22 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * takes queries above 256 candidates; one workgroup places the hits).  Measured slower than the
  * general path on config 3 (0.318 vs 0.211 ms wall, profiles/r02v_pattern_ab.log), kept for A/B. */
 #define HGX_OPT_QUERY_FUSED 5
+/* HGX_OPT_QUERY_INLINE (default 1): the type-grouped incidence index carries each link's <= 8
+ * targets inline (32 bytes per incidence entry, built with the index on the first pattern query),
+ * so a typed candidate is one streamed record instead of two dependent random rows.  0 = read the
+ * target rows through tgt_off (A/B; also what a snapshot too large for the extra bytes gets). */
+#define HGX_OPT_QUERY_INLINE 6
+/* HGX_OPT_PUSH_BATCH (default 16, 0..64): frontier-push levels give each wavefront K frontier atoms
+ * at once and spread their incidence entries over its lanes; 0 = one wavefront per atom (A/B). */
+#define HGX_OPT_PUSH_BATCH 7
+/* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value):
+ * 0 = per level, static-slot rows when at least half of the group's ghosts have news (dense levels),
+ * compressed records otherwise; 1 = always compressed records; 2 = always static slots. */
+#define HGX_OPT_PART_EXCHANGE 8
+/* HGX_OPT_QUERY_FLAT (default 1): pattern batches match over the batch's flat candidate space, a
+ * wavefront per 64 candidates and a lane per candidate whatever query it belongs to; 0 = a
+ * wavefront per chunk of one query's candidates (A/B). */
+#define HGX_OPT_QUERY_FLAT 9
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
  * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */

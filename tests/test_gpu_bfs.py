@@ -277,3 +277,29 @@ def test_nonfull_pull_levels(n_seeds, lt):
     res.close()
     assert 3 in kinds, kinds
     check_batch(g, seeds, None, K.ALGEN_MODES[0], lt, snap, orc)
+
+
+@pytest.mark.parametrize("batch", [0, 1, 7, 16, 64])
+def test_push_batch_all_modes(batch):
+    """HGX_OPT_PUSH_BATCH: the frontier push with K atoms per wavefront batch (their incidence
+    entries spread over the lanes, eligible (target, source) pairs staged in LDS) and with one atom
+    per wavefront (0) give the oracle's per-depth sets in every generator mode: power-law hubs
+    (heavy chunks next to the flattened light atoms), typed links, long rows (> 8 targets),
+    links targeting links, 300 and 1024 seeds."""
+    from hypergraphdb_amd import _lib, synth
+    rng = np.random.default_rng(91)
+    cases = [(K.random_graph(rng, 600, 2500, max_arity=12, n_types=3), -1, None, 300),
+             (synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=17), 1, None, 1024),
+             (synth.config5(scale=0.001, n_sources=300), None, None, 300)]
+    for gi, (g, lt, maxd, ns) in enumerate(cases):
+        snap, orc = snapshot(g), oracle(g)
+        snap.set_option(_lib.HGX_OPT_PUSH_BATCH, batch)
+        if gi == 2:
+            lt = int(g["subsumes_type"])
+            modes = [(False, True, False, False), (False, True, True, False)]
+            seeds = np.asarray(g["seeds"], np.int32)
+        else:
+            modes = K.ALGEN_MODES[::2] if gi == 0 else K.ALGEN_MODES[1::3]
+            seeds = rng.integers(0, g["num_atoms"], ns).astype(np.int32)
+        for mode in modes:
+            check_batch(g, seeds, maxd, mode, lt, snap, orc)

@@ -26,7 +26,7 @@ def parts(g, NP, device=0):
     return out
 
 
-def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=None):
+def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=None, xmode=None):
     from hypergraphdb_amd import _lib, bfs_batch
     from hypergraphdb_amd.partition import pbfs_batch_group
     snap = snapshot(g)
@@ -34,6 +34,9 @@ def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=
     if flags is not None:
         for s in sh:
             s.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
+    if xmode is not None:
+        for s in sh:
+            s.set_option(_lib.HGX_OPT_PART_EXCHANGE, xmode)
     ref = bfs_batch(snap, seeds, maxd, gen(snap, mode, lt))
     res = pbfs_batch_group(sh, seeds, maxd, gen(None, mode, lt))
     rc, pc = ref.counts(), res.counts()
@@ -256,3 +259,22 @@ def test_two_processes_gloo_transport():
     c = np.array(views[0]["4"][0]) + np.array(views[1]["4"][0])
     assert np.array_equal(c, oc[:, : c.shape[1]])
     assert all(p.exitcode == 0 for p in ps)
+
+
+@pytest.mark.parametrize("xmode", [1, 2])
+def test_exchange_modes(xmode):
+    """HGX_OPT_PART_EXCHANGE forced to compressed records (1) or static slots (2) on every level:
+    every generator mode family, typed links, power-law hubs, 2 / 3 / 8 parts, identical to the
+    whole-snapshot engine and the oracle (the default chooses per level)."""
+    from hypergraphdb_amd import synth
+    rng = np.random.default_rng(60 + xmode)
+    g = K.random_graph(rng, 1500, 2500, max_arity=7, n_types=3)
+    seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
+    for NP in (2, 3, 8):
+        compare(g, NP, seeds, None, xmode=xmode)
+    compare(g, 3, seeds, 3, K.ALGEN_MODES[1], 1, xmode=xmode)
+    compare(g, 3, seeds, None, K.ALGEN_MODES[6], 2, xmode=xmode)
+    h = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=21)
+    hs = rng.integers(0, h["num_atoms"], 1024).astype(np.int32)
+    st = compare(h, 4, hs, 4, xmode=xmode)
+    assert all(s["bytes_exchanged"] > 0 for s in st)

@@ -346,3 +346,75 @@ def test_fused_packed_path_vs_general_and_oracle():
     _same(r1, r2, 101)
     assert r1[100].tolist() == orc.and_query(-1, [int(Q["a"][0])], None).tolist()
     snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
+
+
+@pytest.mark.parametrize("case", range(2))
+def test_inline_records_vs_tgt_rows_and_oracle(case):
+    """HGX_OPT_QUERY_INLINE: typed candidates read their link's targets from the 32-byte inline record
+    of the type-grouped index (links of arity > 8 fall back to tgt_off).  Single-type extended Ands
+    (positioned, several orderedLinks, arity) on links of arity 0-12: inline on, inline off and the
+    oracle give identical ascending result sets."""
+    from hypergraphdb_amd import _lib, pattern_batch
+    rng = np.random.default_rng(1500 + case)
+    g = K.random_graph(rng, 300, 3000, max_arity=12, n_types=4, link_targets=case == 0)
+    snap, orc = snapshot(g), oracle(g)
+    A = g["num_atoms"]
+    qs, exp = [], []
+    while len(qs) < 2000:
+        types = [int(rng.integers(0, 4))]
+        inc = [int(x) for x in rng.integers(0, A, int(rng.integers(1, 3)))]
+        pos = [(int(rng.integers(0, A)), int(rng.integers(-9, 10)), int(rng.integers(-9, 10)), int(rng.integers(0, 2)))
+               for _ in range(int(rng.integers(0, 2)))]
+        pats = [tuple(int(x) if rng.random() < 0.6 else -1 for x in rng.integers(0, A, int(rng.integers(1, 5))))
+                for _ in range(int(rng.integers(0, 3)))]
+        ar = int(rng.integers(-1, 13))
+        e = orc.and_query_ext(types, inc, pos, pats, ar)
+        if e is None:
+            continue
+        qs.append({"types": types, "inc": inc, "pos": pos, "patterns": pats, "arity": ar})
+        exp.append(e.tolist())
+    # plain typed queries too (the packed entry point, registers-only pattern path)
+    plain = [(int(rng.integers(0, 4)), [int(rng.integers(0, A))],
+              tuple(int(x) if rng.random() < 0.7 else -1 for x in rng.integers(0, A, int(rng.integers(1, 6)))))
+             for _ in range(2000)]
+    plain_exp = [orc.and_query(t, i, p).tolist() for t, i, p in plain]
+    for inline in (1, 0, 1):
+        snap.set_option(_lib.HGX_OPT_QUERY_INLINE, inline)
+        r = pattern_batch(snap, qs)
+        for q in range(len(qs)):
+            assert r[q].tolist() == exp[q], (inline, qs[q])
+        r = pattern_batch(snap, plain)
+        for q in range(len(plain)):
+            assert r[q].tolist() == plain_exp[q], (inline, plain[q])
+
+
+def test_flat_and_chunked_match_paths():
+    """HGX_OPT_QUERY_FLAT: the flat match (a lane per candidate over the batch's candidate space,
+    per-chunk hit masks for the query offsets) and the per-query chunks give the oracle's results:
+    batches with long runs of queries without candidates (a chunk window of more than 64 queries),
+    empty orderedLinks, untyped and typed queries, and a batch above 16384 queries (device scans)."""
+    from hypergraphdb_amd import _lib, pattern_batch
+    rng = np.random.default_rng(1700)
+    g = K.random_graph(rng, 400, 4000, max_arity=8, n_types=3, link_targets=True)
+    snap, orc = snapshot(g), oracle(g)
+    A = g["num_atoms"]
+    isolated = [a for a in range(A) if orc.and_query(-1, [a], None).size == 0][:5]
+    assert isolated
+    qs = []
+    for i in range(20000):
+        r = rng.random()
+        if r < 0.3:   # no candidates: an anchor without incidence, or an empty orderedLink
+            qs.append((-1, [isolated[i % len(isolated)]], None) if i % 3 else (-1, [int(rng.integers(0, A))], ()))
+        else:
+            t = int(rng.integers(-1, 3))
+            pat = None if rng.random() < 0.5 else tuple(int(x) if rng.random() < 0.7 else -1
+                                                        for x in rng.integers(0, A, int(rng.integers(1, 4))))
+            qs.append((t, [int(rng.integers(0, A))], pat))
+    for lo, hi in ((0, 3000), (3000, 3300), (0, 20000)):
+        sub = qs[lo:hi]
+        exp = [orc.and_query(t, i, p).tolist() for t, i, p in sub]
+        for flat in (1, 0):
+            snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
+            r = pattern_batch(snap, sub)
+            for q in range(len(sub)):
+                assert r[q].tolist() == exp[q], (flat, lo + q, sub[q])

@@ -17,14 +17,16 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--flags", default="0x3BE")
     ap.add_argument("--sources", type=int, default=1024)
+    ap.add_argument("--push", default="16", help="HGX_OPT_PUSH_BATCH values (0 = one wavefront per atom)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, synth
     g = synth.config5(scale=args.scale, n_sources=args.sources)
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     snap.set_timing(True)
-    for f in args.flags.split(","):
+    for f, pb in [(f, pb) for f in args.flags.split(",") for pb in args.push.split(",")]:
         snap.set_option(_lib.HGX_OPT_BFS_FLAGS, int(f, 0))
+        snap.set_option(_lib.HGX_OPT_PUSH_BATCH, int(pb))
         for rev in (False, True):
             gen = DefaultALGenerator(snap, AtomTypeCondition(g["subsumes_type"]), None, False, True, rev)
             for _ in range(2):
@@ -35,7 +37,7 @@ def main():
             for _ in range(5):
                 H.bfs_batch(snap, g["seeds"], None, gen).close()
             wall = (time.perf_counter() - t0) / 5 * 1e3
-            print(json.dumps({"flags": f, "reverse": rev, "ms_total": round(st["ms_total"], 3),
+            print(json.dumps({"flags": f, "push_batch": int(pb), "reverse": rev, "ms_total": round(st["ms_total"], 3),
                               "wall_ms": round(wall, 3),
                               "kernels": {k: round(v["ms"], 3) for k, v in st["kernels"].items()},
                               "level_ms": st["level_ms"], "level_new": st["level_new"],

@@ -34,14 +34,16 @@ def main():
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--out", default="")
+    ap.add_argument("--xmode", type=int, nargs="+", default=[0],
+                    help="HGX_OPT_PART_EXCHANGE values to measure at NP > 1 (0 auto, 1 records, 2 static slots)")
     args = ap.parse_args()
-    from hypergraphdb_amd import synth
+    from hypergraphdb_amd import _lib, synth
     from hypergraphdb_amd.partition import Shard, ShardSnapshot, partition_plan, pbfs_batch_group
     t0 = time.time()
     g = synth.config4(scale=args.scale, n_sources=args.sources)
     print(f"config4 x{args.scale}: A={g['num_atoms']} P={len(g['tgt_idx'])} in {time.time() - t0:.1f}s", flush=True)
     rows = []
-    ref_counts, ref_ms = None, None
+    state = {"ref_counts": None, "ref_ms": None}
     for NP in args.parts:
         t0 = time.time()
         plan = partition_plan(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], NP)
@@ -58,13 +60,30 @@ def main():
                 snaps[-1].set_serial(True)
         build_s = time.time() - t0
         print(f"{NP} parts: plan {plan_s:.1f}s, built in {build_s:.1f}s", flush=True)
+        for xmode in (args.xmode if NP > 1 else [0]):
+            for sn in snaps:
+                if NP > 1:
+                    sn.set_option(_lib.HGX_OPT_PART_EXCHANGE, xmode)
+            measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state)
+        for s in snaps:
+            s.close()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"scale": args.scale, "sources": args.sources, "depth": args.depth,
+                       "xgmi_link_GBps": XGMI_LINK_GBS, "rows": rows}, f, indent=1)
+
+
+def measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state):
+    from hypergraphdb_amd.partition import pbfs_batch_group
+    if True:
         r = pbfs_batch_group(snaps, g["seeds"], args.depth)
         counts = r.counts()
         st0 = r.stats(accounting=True)
         r.close()
-        if ref_counts is None:
-            ref_counts = counts
-        assert np.array_equal(counts, ref_counts), f"{NP} parts differ from {args.parts[0]}"
+        if state["ref_counts"] is None:
+            state["ref_counts"] = counts
+        assert np.array_equal(counts, state["ref_counts"]), f"{NP} parts (xmode {xmode}) differ from {args.parts[0]}"
+        ref_ms = state["ref_ms"]
         sts = []
         for _ in range(args.steps):
             r = pbfs_batch_group(snaps, g["seeds"], args.depth)
@@ -102,8 +121,8 @@ def main():
                                               if ss[0]["xwords_total"] else None),
                         "traversed_edges": st0[p]["traversed_edges"], **info[p]})
         if NP == 1:
-            ref_ms = per[0]["device_ms"]
-        row = {"parts": NP, "plan_s": round(plan_s, 1), "build_s": round(build_s, 1),
+            ref_ms = state["ref_ms"] = per[0]["device_ms"]
+        row = {"parts": NP, "xmode": xmode, "plan_s": round(plan_s, 1), "build_s": round(build_s, 1),
                "traversed_edges": sum(x["traversed_edges"] for x in per),
                "max_part_device_ms": round(max(x["device_ms"] for x in per), 3),
                "model_step_ms": round(model_ms, 3),
@@ -112,12 +131,6 @@ def main():
                "exchange_bytes_total": sum(x["bytes_exchanged"] for x in per), "levels": levels, "per_part": per}
         rows.append(row)
         print(json.dumps({k: v for k, v in row.items() if k not in ("per_part",)}), flush=True)
-        for s in snaps:
-            s.close()
-    if args.out:
-        with open(args.out, "w") as f:
-            json.dump({"scale": args.scale, "sources": args.sources, "depth": args.depth,
-                       "xgmi_link_GBps": XGMI_LINK_GBS, "rows": rows}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--queries", type=int, default=10_000)
     ap.add_argument("--fused", default="0", help="HGX_OPT_QUERY_FUSED values to compare, interleaved (e.g. 1,0)")
+    ap.add_argument("--inline", default="1", help="HGX_OPT_QUERY_INLINE values to compare, interleaved (e.g. 1,0)")
+    ap.add_argument("--flat", default="1", help="HGX_OPT_QUERY_FLAT values to compare, interleaved (e.g. 1,0)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
@@ -32,27 +34,33 @@ def main():
               np.arange(0, 3 * nq + 1, 3, dtype=np.int64),
               np.stack([Q["x"], np.full(nq, -1, np.int32), Q["y"]], 1).reshape(-1))
     from hypergraphdb_amd import _lib
-    opts = [int(x) for x in args.fused.split(",")]
+    opts = [(int(f), int(i), int(fl)) for f in args.fused.split(",") for i in args.inline.split(",")
+            for fl in args.flat.split(",")]
     walls = {o: [] for o in opts}
     devs = {o: [] for o in opts}
     match = {o: [] for o in opts}
+    gbs = {o: [] for o in opts}
     ref = None
     for i in range(args.calls):
         for o in opts:
-            snap.set_option(_lib.HGX_OPT_QUERY_FUSED, o)
+            snap.set_option(_lib.HGX_OPT_QUERY_FUSED, o[0])
+            snap.set_option(_lib.HGX_OPT_QUERY_INLINE, o[1])
+            snap.set_option(_lib.HGX_OPT_QUERY_FLAT, o[2])
             t0 = time.perf_counter()
             r = pattern_batch_arrays(snap, *packed)
             walls[o].append((time.perf_counter() - t0) * 1e3)
             devs[o].append(r.ms["ms_total"])
             match[o].append(r.ms["ms_match"])
+            gbs[o].append(r.ms["bytes_match"] / max(r.ms["ms_match"], 1e-9) / 1e6)
             if ref is None:
                 ref = (r.offsets.copy(), r.ids.copy())
             elif i < 2:
                 assert np.array_equal(ref[0], r.offsets) and np.array_equal(ref[1], r.ids), "paths differ"
     for o in opts:
         w, d, m = np.array(walls[o][3:]), np.array(devs[o][3:]), np.array(match[o][3:])
-        print(f"fused={o} wall ms: median {np.median(w):.3f} min {w.min():.3f} max {w.max():.3f}; "
-              f"device ms: median {np.median(d):.3f}; match ms median {np.median(m):.3f}; results {int(r.offsets[-1])}")
+        print(f"fused,inline,flat={o} wall ms: median {np.median(w):.3f} min {w.min():.3f} max {w.max():.3f}; "
+              f"device ms: median {np.median(d):.3f}; match ms median {np.median(m):.3f} "
+              f"({np.median(gbs[o][3:]):.1f} GB/s algorithmic); results {int(r.offsets[-1])}")
         print("walls", [round(x, 3) for x in walls[o]])
 
 
