@@ -189,6 +189,7 @@ __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
 // word saturates at ~90 adds/us; thousands of waves add to every counter each level).  Counter c
 // of shard k lives at base[k * kCtrStride + c]; the host sums the shards.
 constexpr int kCtrShards = 16, kCtrStride = 16, kCtrBlock = kCtrShards * kCtrStride;
+constexpr int kHostSlot = 32;   // u64 words of one level's counters in mapped host memory (cNum + sequence)
 // Internal per-level flag (above the HGX_OPT_BFS_FLAGS bits): dense level with every lf row written.
 constexpr int kAllRows = 1 << 16;
 // Cache-policy A/B bits of HGX_OPT_BFS_FLAGS for the tile-staged dense kernels (gather2 / pull2).
@@ -1513,7 +1514,9 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
                                                  const u64* __restrict__ full, u64* __restrict__ cand,
                                                  int32_t* __restrict__ clist, u64* __restrict__ n_clist,
                                                  u64* __restrict__ acc, u64* __restrict__ ctr,
-                                                 u64* __restrict__ fa_next, int64_t n_words) {
+                                                 u64* __restrict__ fa_next, int64_t n_words,
+                                                 const HeavyChunk* __restrict__ chunks, int64_t n_chunks,
+                                                 const u64* __restrict__ fa) {
     __shared__ OPushLds lds[4];
     OPushLds& sh = lds[threadIdx.x >> 6];
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1521,9 +1524,20 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
     // the next frontier bitmap (set by the finalise) is cleared here instead of by a memset
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x)
         fa_next[w] = 0ull;
-    const int64_t n = (int64_t)*n_list;
     u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
     int cc = 0;   // staged candidates (wave-uniform)
+    // hub chunks first (the hgx_opush_heavy launch folded in: one launch less per level): a block per
+    // kPushChunk-entry chunk of a frontier hub, its four waves striding over the chunk
+    for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {   // block-uniform
+        const HeavyChunk c = chunks[ch];
+        if (!bit(fa, c.atom)) continue;
+        const int nnz = row_words<W>(lvl, c.atom, sh);
+        if (nnz == 0) continue;
+        opush_links<W, MODE>(c.atom, c.beg + (threadIdx.x >> 6) * 64, c.end, 256, inc_row, inc_type, want_type, yf,
+                             tgt_off, tgt_idx, nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs,
+                             n_scan, cc);
+    }
+    const int64_t n = (int64_t)*n_list;
     for (int64_t k = wave; k < n; k += nwave) {
         const int32_t v = list[k];
         if (v < 0) continue;   // a candidate list reused as the frontier list: not new / not light
@@ -1851,6 +1865,34 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
     wave_add_sh(ctr + cScanned, n_scan);
 }
 
+// The level's counters straight to host memory (no copy in the stream between two levels): the last
+// block to finish sums the shards (device-scope atomic reads), stores the totals into the mapped
+// host slot, then the sequence number the host spins on.  Every thread of every block calls it.
+__device__ __forceinline__ void level_counters_out(u64* __restrict__ ctr, u64* __restrict__ ticket,
+                                                   u64* __restrict__ hout, u64 seq) {
+    __shared__ bool last;
+    __syncthreads();   // the block's counter atomics are issued
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(ticket, 1ull) == (u64)gridDim.x - 1ull;
+    }
+    __syncthreads();
+    if (!last) return;   // block-uniform
+    __threadfence();
+    if (threadIdx.x < cNum) {
+        u64 v = 0;
+        for (int k = 0; k < kCtrShards; ++k) v += atomicAdd(ctr + k * kCtrStride + threadIdx.x, 0ull);
+        __hip_atomic_store(hout + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *ticket = 0ull;
+        __threadfence_system();
+        __hip_atomic_store(hout + cNum, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Finalise the candidates of a push level: new = acc & ~vis, the accumulator row is re-zeroed.
 // One G-lane group per candidate; fa_next (cleared beforehand) / ever / full bits by atomics.
 template <int W>
@@ -1862,7 +1904,8 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
                                                               u64* __restrict__ ever, u64* __restrict__ full,
                                                               u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
                                                               u64* __restrict__ ctr, FullMask fm, int relist,
-                                                              u64* __restrict__ n_spent) {
+                                                              u64* __restrict__ n_spent, u64* __restrict__ ticket,
+                                                              u64* __restrict__ hout, u64 seq) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
     const int sub = threadIdx.x & (G - 1);
@@ -1914,6 +1957,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+    if (hout) level_counters_out(ctr, ticket, hout, seq);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2208,8 +2252,30 @@ __device__ __forceinline__ void csa(u64& h, u64& l, u64 a, u64 b, u64 c) {
 constexpr int kCountBlocks = 2048;
 
 template <int W>
+__device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
+                                                const u64* __restrict__ lvl, uint32_t* __restrict__ partial);
+
+template <int W>
 __global__ void __launch_bounds__(256) hgx_count_rows(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
                                                       const u64* __restrict__ lvl, uint32_t* __restrict__ partial) {
+    count_rows_body<W>(A, fa, own, lvl, partial);
+}
+
+// Every level of one batch in one launch (blockIdx.y = level slot): a traversal of tens of short
+// levels (config 5) paid one launch per level for its readout.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_count_rows_multi(int64_t A, const u64* const* __restrict__ fa_p,
+                                                            const u64* __restrict__ own,
+                                                            const u64* const* __restrict__ lvl_p,
+                                                            const int64_t* __restrict__ poff, int slot0,
+                                                            uint32_t* __restrict__ partial) {
+    const int sl = slot0 + (int)blockIdx.y;
+    count_rows_body<W>(A, fa_p[sl], own, lvl_p[sl], partial + poff[sl]);
+}
+
+template <int W>
+__device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
+                                                const u64* __restrict__ lvl, uint32_t* __restrict__ partial) {
     constexpr int K = 22;   // planes of the eights: < 2^25 rows per lane
     constexpr int R = 64 / W, U = 8;
     __shared__ unsigned int lc[W * 64];
@@ -2744,43 +2810,56 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
 // launches a level (ghost pack, owner, ghost apply) instead of two three-pass packs and one apply
 // launch per source part and phase.
 // ---------------------------------------------------------------------------------------------
-constexpr int kXsU = 4;   // atoms per lane group in flight
+constexpr int kXsU = 4;   // atoms per lane group in flight (each stage's loads issued together)
+
+// the part's segment starts (payload words) in LDS: one table lookup per record instead of a global
+// load on the dependent chain
+__device__ __forceinline__ void load_seg(int64_t* sw, const int64_t* __restrict__ seg_w, int NP) {
+    for (int q = threadIdx.x; q < NP; q += blockDim.x) sw[q] = seg_w[q];
+    __syncthreads();
+}
 
 template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_gpack(int64_t A, const u64* __restrict__ fa_next,
+__global__ void __launch_bounds__(256) hgx_xs_gpack(int64_t A, int NP, const u64* __restrict__ fa_next,
                                                     const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
                                                     const int32_t* __restrict__ xo_slot,
                                                     const u64* __restrict__ lvl_next, const int64_t* __restrict__ seg_w,
                                                     u64* __restrict__ pay) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
+    __shared__ int64_t sw[kMaxParts];
+    load_seg(sw, seg_w, NP);
     const int sub = threadIdx.x & (G - 1);
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     for (int64_t t0 = grp; t0 < A; t0 += ngrp * kXsU) {
-        int64_t dst[kXsU];
+        bool gh[kXsU], nw[kXsU];
+        int32_t q[kXsU], sl[kXsU];
         typename V::T row[kXsU];
 #pragma unroll
         for (int u = 0; u < kXsU; ++u) {
             const int64_t t = t0 + u * ngrp;
-            dst[u] = -1;
-            row[u] = V::zero();
-            if (t < A && !bit(own_bm, t)) {
-                const int32_t q = xo_part[t];
-                dst[u] = seg_w[q] + (int64_t)xo_slot[t] * W + sub * WPL;
-                if (bit(fa_next, t)) row[u] = V::ld(lvl_next + t * W + sub * WPL);
-            }
+            const bool in = t < A;
+            const u64 ow = in ? own_bm[t >> 6] : ~0ull, fw = in ? fa_next[t >> 6] : 0ull;
+            gh[u] = in && !((ow >> (t & 63)) & 1ull);
+            nw[u] = gh[u] && ((fw >> (t & 63)) & 1ull);
+            q[u] = gh[u] ? xo_part[t] : 0;
+            sl[u] = gh[u] ? xo_slot[t] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kXsU; ++u)
-            if (dst[u] >= 0) V::st(pay + dst[u], row[u]);
+            row[u] = nw[u] ? V::ld(lvl_next + (t0 + u * ngrp) * W + sub * WPL) : V::zero();
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u)
+            if (gh[u]) V::st(pay + sw[q[u]] + (int64_t)sl[u] * W + sub * WPL, row[u]);
     }
 }
 
 // Owner pass: reduce the holders' slots into an owned atom (new = row & ~vis), then write its final
-// news (zero when none) into every holder's broadcast slot.
+// news (zero when none) into every holder's broadcast slot.  kXsU atoms per group in flight, the
+// first two holders of each in registers (a present atom has 1.95 holders on config 4 at 8 parts).
 template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_owner(int64_t A, const u64* __restrict__ own_bm,
+__global__ void __launch_bounds__(256) hgx_xs_owner(int64_t A, int NP, const u64* __restrict__ own_bm,
                                                     const int64_t* __restrict__ bc_off, const int32_t* __restrict__ bc_part,
                                                     const int32_t* __restrict__ bc_slot, const u64* __restrict__ recv,
                                                     u64* __restrict__ send, const int64_t* __restrict__ seg_w,
@@ -2789,50 +2868,75 @@ __global__ void __launch_bounds__(256) hgx_xs_owner(int64_t A, const u64* __rest
                                                     FullMask fm) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
+    __shared__ int64_t sw[kMaxParts];
+    load_seg(sw, seg_w, NP);
     const int sub = threadIdx.x & (G - 1);
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
     // the trip count is the same for every lane of a wave (ballots below)
-    for (int64_t t0 = grp - (grp % (64 / G)); t0 < A; t0 += ngrp) {
-        const int64_t t = t0 + (grp % (64 / G));
-        int64_t b = 0;
-        int nb = 0;
-        if (t < A && bit(own_bm, t)) {
-            b = bc_off[t];
-            nb = (int)(bc_off[t + 1] - b);
+    const int64_t gw = grp % (64 / G);
+    for (int64_t t0 = grp - gw; t0 < A; t0 += ngrp * kXsU) {
+        int64_t b[kXsU], d0[kXsU], d1[kXsU];
+        int nb[kXsU];
+        bool ev[kXsU], was[kXsU];
+        typename V::T acc[kXsU], vis0[kXsU], lv0[kXsU];
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {   // stage 1: ownership, holder range, bitmap words
+            const int64_t t = t0 + gw + u * ngrp;
+            const bool in = t < A;
+            const u64 ow = in ? own_bm[t >> 6] : 0ull;
+            const bool mine = in && ((ow >> (t & 63)) & 1ull);
+            b[u] = mine ? bc_off[t] : 0;
+            const int64_t e = mine ? bc_off[t + 1] : 0;
+            nb[u] = (int)(e - b[u]);
+            const u64 evw = mine ? ever[t >> 6] : 0ull, faw = mine ? fa_next[t >> 6] : 0ull;
+            ev[u] = nb[u] > 0 && ((evw >> (t & 63)) & 1ull);
+            was[u] = nb[u] > 0 && ((faw >> (t & 63)) & 1ull);
         }
-        typename V::T acc = V::zero();
-        for (int k = 0; k < nb; ++k)   // group-uniform; the holders' slots are independent loads
-            acc |= V::ld(recv + seg_w[bc_part[b + k]] + (int64_t)bc_slot[b + k] * W + sub * WPL);
-        const bool valid = nb > 0;
-        const bool ev = valid && bit(ever, t);
-        const bool was = valid && bit(fa_next, t);
-        const typename V::T vis0 = valid ? V::ld(vis + t * W + sub * WPL) : V::zero();
-        const typename V::T lv0 = was ? V::ld(lvl_next + t * W + sub * WPL) : V::zero();
-        const typename V::T old = ev ? vis0 : V::zero();
-        const typename V::T nw = acc & ~old;
-        const bool any = group_any<G>(V::nz(nw));
-        const bool isfull = group_all<G>(V::eq(old | nw, FULL));
-        typename V::T fin = lv0;
-        if (valid && any) {
-            fin = lv0 | nw;
-            V::st(lvl_next + t * W + sub * WPL, fin);
-            V::st(vis + t * W + sub * WPL, old | nw);
-            if (sub == 0) {
-                if (!was) set_bit(fa_next, t);
-                if (!ev) set_bit(ever, t);
-                if (isfull) set_bit(full, t);
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {   // stage 2: the first two holders' slots, the atom's rows
+            const int64_t t = t0 + gw + u * ngrp;
+            d0[u] = nb[u] > 0 ? sw[bc_part[b[u]]] + (int64_t)bc_slot[b[u]] * W + sub * WPL : -1;
+            d1[u] = nb[u] > 1 ? sw[bc_part[b[u] + 1]] + (int64_t)bc_slot[b[u] + 1] * W + sub * WPL : -1;
+            vis0[u] = ev[u] ? V::ld(vis + t * W + sub * WPL) : V::zero();
+            lv0[u] = was[u] ? V::ld(lvl_next + t * W + sub * WPL) : V::zero();
+        }
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {   // stage 3: the holders' partial rows
+            acc[u] = d0[u] >= 0 ? V::ld(recv + d0[u]) : V::zero();
+            if (d1[u] >= 0) acc[u] |= V::ld(recv + d1[u]);
+            for (int k = 2; k < nb[u]; ++k)   // rare: a third holder and more
+                acc[u] |= V::ld(recv + sw[bc_part[b[u] + k]] + (int64_t)bc_slot[b[u] + k] * W + sub * WPL);
+        }
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {   // stage 4: finish the atom, write the broadcast slots
+            const int64_t t = t0 + gw + u * ngrp;
+            const typename V::T nw = acc[u] & ~vis0[u];
+            const bool any = group_any<G>(V::nz(nw));
+            const bool isfull = group_all<G>(V::eq(vis0[u] | nw, FULL));
+            typename V::T fin = lv0[u];
+            if (nb[u] > 0 && any) {
+                fin = lv0[u] | nw;
+                V::st(lvl_next + t * W + sub * WPL, fin);
+                V::st(vis + t * W + sub * WPL, vis0[u] | nw);
+                if (sub == 0) {
+                    if (!was[u]) set_bit(fa_next, t);
+                    if (!ev[u]) set_bit(ever, t);
+                    if (isfull) set_bit(full, t);
+                }
             }
+            if (d0[u] >= 0) V::st(send + d0[u], fin);
+            if (d1[u] >= 0) V::st(send + d1[u], fin);
+            for (int k = 2; k < nb[u]; ++k)
+                V::st(send + sw[bc_part[b[u] + k]] + (int64_t)bc_slot[b[u] + k] * W + sub * WPL, fin);
         }
-        for (int k = 0; k < nb; ++k)
-            V::st(send + seg_w[bc_part[b + k]] + (int64_t)bc_slot[b + k] * W + sub * WPL, fin);
     }
 }
 
 // Ghost apply: the owner's final row (zero: no news) replaces the ghost's partial one.
 template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_gapply(int64_t A, const u64* __restrict__ own_bm,
+__global__ void __launch_bounds__(256) hgx_xs_gapply(int64_t A, int NP, const u64* __restrict__ own_bm,
                                                      const int32_t* __restrict__ xo_part,
                                                      const int32_t* __restrict__ xo_slot, const u64* __restrict__ recv,
                                                      const int64_t* __restrict__ seg_w, u64* __restrict__ lvl_next,
@@ -2840,39 +2944,81 @@ __global__ void __launch_bounds__(256) hgx_xs_gapply(int64_t A, const u64* __res
                                                      u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
+    __shared__ int64_t sw[kMaxParts];
+    load_seg(sw, seg_w, NP);
     const int sub = threadIdx.x & (G - 1);
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
-    for (int64_t t0 = grp - (grp % (64 / G)); t0 < A; t0 += ngrp) {
-        const int64_t t = t0 + (grp % (64 / G));
-        const bool valid = t < A && !bit(own_bm, t);
-        typename V::T row = V::zero();
-        if (valid) row = V::ld(recv + seg_w[xo_part[t]] + (int64_t)xo_slot[t] * W + sub * WPL);
-        const bool ev = valid && bit(ever, t);
-        const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
-        const bool any = group_any<G>(V::nz(row));
-        const bool isfull = group_all<G>(V::eq(old | row, FULL));
-        if (valid && any) {
-            V::st(lvl_next + t * W + sub * WPL, row);
-            V::st(vis + t * W + sub * WPL, old | row);
-            if (sub == 0) {
-                if (!bit(fa_next, t)) set_bit(fa_next, t);
-                if (!ev) set_bit(ever, t);
-                if (isfull) set_bit(full, t);
+    const int64_t gw = grp % (64 / G);
+    for (int64_t t0 = grp - gw; t0 < A; t0 += ngrp * kXsU) {
+        bool gh[kXsU], ev[kXsU], was[kXsU];
+        int64_t src[kXsU];
+        typename V::T row[kXsU], old[kXsU];
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {
+            const int64_t t = t0 + gw + u * ngrp;
+            const bool in = t < A;
+            const u64 ow = in ? own_bm[t >> 6] : ~0ull;
+            gh[u] = in && !((ow >> (t & 63)) & 1ull);
+            src[u] = gh[u] ? sw[xo_part[t]] + (int64_t)xo_slot[t] * W + sub * WPL : -1;
+            const u64 evw = gh[u] ? ever[t >> 6] : 0ull, faw = gh[u] ? fa_next[t >> 6] : 0ull;
+            ev[u] = gh[u] && ((evw >> (t & 63)) & 1ull);
+            was[u] = gh[u] && ((faw >> (t & 63)) & 1ull);
+        }
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {
+            const int64_t t = t0 + gw + u * ngrp;
+            row[u] = src[u] >= 0 ? V::ld(recv + src[u]) : V::zero();
+            old[u] = ev[u] ? V::ld(vis + t * W + sub * WPL) : V::zero();
+        }
+#pragma unroll
+        for (int u = 0; u < kXsU; ++u) {
+            const int64_t t = t0 + gw + u * ngrp;
+            const bool any = group_any<G>(V::nz(row[u]));
+            const bool isfull = group_all<G>(V::eq(old[u] | row[u], FULL));
+            if (gh[u] && any) {
+                V::st(lvl_next + t * W + sub * WPL, row[u]);
+                V::st(vis + t * W + sub * WPL, old[u] | row[u]);
+                if (sub == 0) {
+                    if (!was[u]) set_bit(fa_next, t);
+                    if (!ev[u]) set_bit(ever, t);
+                    if (isfull) set_bit(full, t);
+                }
             }
         }
     }
 }
 
-// out[3] += ghosts with news (fa_next & ~own): the exchange-mode decision of a level.
+// The exchange-mode decision of a level: out[3] += ghosts with news (fa_next & ~own), a thread per
+// bitmap word; on a 1/16 sample of the atoms (one G-lane group each) out[4] += nonzero row words of
+// the ghosts with news and out[5] += those ghosts -- the compressed records' density estimate.
+template <int W>
 __global__ void __launch_bounds__(256) hgx_ghost_news(int64_t A, const u64* __restrict__ fa,
-                                                      const u64* __restrict__ own, u64* __restrict__ out) {
+                                                      const u64* __restrict__ own, const u64* __restrict__ lvl,
+                                                      u64* __restrict__ out) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
+    typedef Vec<WPL> V;
     const int64_t nwords = (A + 63) / 64;
-    u64 n = 0;
+    u64 n = 0, nzw = 0, rows = 0;
     for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x)
         n += __popcll(fa[w] & ~own[w]);
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
+    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
+    for (int64_t i = grp; i * 16 < A; i += ngrp) {
+        const int64_t t = i * 16 + (i & 15);
+        const bool take = t < A && bit(fa, t) && !bit(own, t);
+        if (take) {
+            const typename V::T r = V::ld(lvl + t * W + sub * WPL);
+            if constexpr (WPL == 1) nzw += r != 0ull;
+            else nzw += (u64)(r.x != 0ull) + (u64)(r.y != 0ull);
+            rows += sub == 0;
+        }
+    }
     block_add_sh(out, 3, n);
+    block_add_sh(out, 4, nzw);
+    block_add_sh(out, 5, rows);
 }
 
 // out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
@@ -2942,10 +3088,12 @@ struct Timer {
     struct Rec {
         int kind, level;
         Events e;
+        bool own_a;   // false: e.a is the previous record's e.b (chained levels, one event per boundary)
     };
     std::vector<Rec> rec;
     Events all{};
     bool on;
+    hipEvent_t chain = nullptr;   // the last stop event when nothing was enqueued after it
     explicit Timer(hgx_graph* gg) : g(gg), on(gg->timing) {
         if (on) {
             HGX_HIP(hipEventCreate(&all.a));
@@ -2954,7 +3102,7 @@ struct Timer {
     }
     ~Timer() {   // events go back to the graph's pool (the caller holds g->mu)
         for (auto& r : rec) {
-            g->ev_pool.push_back(r.e.a);
+            if (r.own_a) g->ev_pool.push_back(r.e.a);
             g->ev_pool.push_back(r.e.b);
         }
         if (all.a) (void)hipEventDestroy(all.a);
@@ -2972,16 +3120,33 @@ struct Timer {
     }
     Events start(int kind, int level) {
         Events e{};
+        chain = nullptr;
         if (!on) return e;
         e.a = take();
         e.b = take();
         HGX_HIP(hipEventRecord(e.a, g->stream));
-        rec.push_back({kind, level, e});
+        rec.push_back({kind, level, e, true});
         return e;
     }
     void stop(const Events& e) {
         if (on) HGX_HIP(hipEventRecord(e.b, g->stream));
     }
+    // Consecutive push levels: a level starts at the previous level's stop event when nothing was
+    // enqueued in between (an event record between two kernels costs several microseconds of idle
+    // queue on a level of a few tens of microseconds).
+    Events start_chained(int kind, int level) {
+        if (!on || !chain) return start(kind, level);
+        Events e{chain, take()};
+        rec.push_back({kind, level, e, false});
+        chain = nullptr;
+        return e;
+    }
+    void stop_chained(const Events& e) {
+        if (!on) return;
+        HGX_HIP(hipEventRecord(e.b, g->stream));
+        chain = e.b;
+    }
+    void break_chain() { chain = nullptr; }
     void collect(hgx_bfs_stats& st) {
         for (auto& r : rec) {
             float ms = 0;
@@ -3212,43 +3377,51 @@ struct Exchange {
         // exchange mode of the level (group-wide): static slots when at least half of the group's
         // ghosts have news, compressed records otherwise (HGX_OPT_PART_EXCHANGE forces one)
         bool stat_mode = sh.xmode == 2;
-        if (sh.xmode == 0) {
+        if (sh.xmode == 0) {   // bytes of each format: static = every ghost's row, records = the ghosts
+                               // with news (16-byte header + their nonzero words, from a 1/16 sample)
+            Events eg = tm.start(kKindExchange, d);
             HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
-            hgx_ghost_news<<<grid_for(ceil_div(A, 64), 256, 1024), 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, xs);
+            hgx_ghost_news<Wt><<<grid_for(ceil_div(A, 16) * Lay<Wt>::G, 256, 2048), 256, 0, s>>>(
+                A, fa_next, (const u64*)sh.own_bm, lvl_next, xs);
             HGX_CHECK_LAUNCH();
+            tm.stop(eg);
             HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
             HGX_HIP(hipStreamSynchronize(s));
-            int64_t mine2[2] = {(int64_t)stat_sum(3), rseg[NP]};
-            std::vector<int64_t> all2(2 * (size_t)NP);
-            coll([&] { tr->allgather_i64(mine2, 2, all2.data(), s); });
-            int64_t news = 0, ghosts = 0;
+            int64_t mine2[4] = {(int64_t)stat_sum(3), rseg[NP], (int64_t)stat_sum(4), (int64_t)stat_sum(5)};
+            std::vector<int64_t> all2(4 * (size_t)NP);
+            coll([&] { tr->allgather_i64(mine2, 4, all2.data(), s); });
+            double news = 0, ghosts = 0, nzw = 0, rows = 0;
             for (int q = 0; q < NP; ++q) {
-                news += all2[2 * (size_t)q];
-                ghosts += all2[2 * (size_t)q + 1];
+                news += (double)all2[4 * (size_t)q];
+                ghosts += (double)all2[4 * (size_t)q + 1];
+                nzw += (double)all2[4 * (size_t)q + 2];
+                rows += (double)all2[4 * (size_t)q + 3];
             }
-            stat_mode = ghosts > 0 && 2 * news >= ghosts;
+            const double nzfrac = rows > 0 ? nzw / (rows * Wt) : 1.0;
+            const double rec_bytes = news * (16.0 + 8.0 * Wt * nzfrac), static_bytes = ghosts * 8.0 * Wt;
+            stat_mode = ghosts > 0 && static_bytes <= rec_bytes;
         }
         if (stat_mode) {
             static_levels += 1;
             // reduce: every ghost's row (zero without news) -> its slot at the owner
-            const int sgrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 8192);
+            const int sgrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 4096);
             Events e0 = tm.start(kKindExchange, d);
-            hgx_xs_gpack<Wt><<<sgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, lvl_next,
-                                                   seg + NP, send_p);
+            hgx_xs_gpack<Wt><<<sgrid, 256, 0, s>>>(A, NP, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot,
+                                                   lvl_next, seg + NP, send_p);
             HGX_CHECK_LAUNCH();
             tm.stop(e0);
             ship_static(rseg, sh.ghost_count, bseg, sh.bc_count, &pm_r);
             // owners: reduce + finish + broadcast slots; then every ghost takes its final row
-            const int ogrid = grid_for(A * Lay<Wt>::G, 256, 8192);
+            const int ogrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 4096);
             Events e1 = tm.start(kKindExchange, d);
-            hgx_xs_owner<Wt><<<ogrid, 256, 0, s>>>(A, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_slot, recv_p,
-                                                   send_p, seg + 3 * NP, lvl_next, fa_next, vis, ever, full, fm);
+            hgx_xs_owner<Wt><<<ogrid, 256, 0, s>>>(A, NP, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_slot,
+                                                   recv_p, send_p, seg + 3 * NP, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
             tm.stop(e1);
             ship_static(bseg, sh.bc_count, rseg, sh.ghost_count, &pm_b);
             Events e2 = tm.start(kKindExchange, d);
-            hgx_xs_gapply<Wt><<<ogrid, 256, 0, s>>>(A, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, recv_p, seg + NP,
-                                                    lvl_next, fa_next, vis, ever, full, fm);
+            hgx_xs_gapply<Wt><<<ogrid, 256, 0, s>>>(A, NP, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, recv_p,
+                                                    seg + NP, lvl_next, fa_next, vis, ever, full, fm);
             HGX_CHECK_LAUNCH();
             HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
             hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
@@ -3400,6 +3573,13 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     int32_t *fl = flist, *cl = clist;
     u64* n_fl = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 10;   // scratch slots
     u64* n_cl = n_fl + 1;
+    u64* ticket = n_fl + 2;   // the finalise's last-block ticket (re-zeroed by that block)
+    if (!g->ctr_host) {       // two level slots of mapped, coherent host memory (once per graph)
+        void* hp = nullptr;
+        HGX_HIP(hipHostMalloc(&hp, sizeof(u64) * 2 * kHostSlot, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, sizeof(u64) * 2 * kHostSlot);
+        g->ctr_host = (u64*)hp;
+    }
     bool chained = false, cand_clean = false;
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
     const int64_t I_total = g->I;
@@ -3427,6 +3607,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64 new_global = 0, part_push = 0;
         u64* h = nullptr;
         hipEvent_t ev = nullptr;
+        bool flag = false;    // counters in slot[0..cNum) once slot[cNum] == seq (mapped host memory)
+        u64 seq = 0;
+        u64* slot = nullptr;
     } pend[2];
     for (int k = 0; k < 2; ++k) {
         pend[k].h = h_sh + (size_t)k * kCtrBlock;
@@ -3447,10 +3630,22 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     };
     // One level's counters -> host state; false once the level found no new atom (its rows released).
     auto read_level = [&](Pend& p) -> bool {
-        wait_event(p.ev);
-        for (int k = 0; k < cNum; ++k) {
-            h_new[k] = 0;
-            for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += p.h[sh * kCtrStride + k];
+        if (p.flag) {   // spin on the sequence word; a stream that finished or failed without it is an error
+            for (unsigned spin = 0; __atomic_load_n(p.slot + cNum, __ATOMIC_ACQUIRE) != p.seq; ++spin) {
+                if ((spin & 1023u) != 1023u) continue;   // the stream is asked every 1024 polls
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipErrorNotReady) continue;
+                if (e != hipSuccess) HGX_HIP(e);
+                if (__atomic_load_n(p.slot + cNum, __ATOMIC_ACQUIRE) != p.seq)
+                    fail(HGX_E_DEVICE, "batched BFS: level counters never arrived");
+            }
+            for (int k = 0; k < cNum; ++k) h_new[k] = __atomic_load_n(p.slot + k, __ATOMIC_RELAXED);
+        } else {
+            wait_event(p.ev);
+            for (int k = 0; k < cNum; ++k) {
+                h_new[k] = 0;
+                for (int sh = 0; sh < kCtrShards; ++sh) h_new[k] += p.h[sh * kCtrStride + k];
+            }
         }
         if (ex) {   // the group decides termination; the next level's push volume is my frontier's
             h_new[cNewAtoms] = p.new_global;
@@ -3481,6 +3676,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     for (int32_t d = 0; d < maxd && d < max_levels_cap - 1 && !stop; ++d) {
         u64* lvl = cur_lvl;
         u64* fa = cur_fa;
+        bool flag_level = false;   // counters written by the finalise into mapped host memory
+        u64 flag_seq = 0;
+        u64* flag_slot = nullptr;
         const bool spec = npend > 0;   // issued before the previous level's counters were read
         u64* lvl_next = (u64*)g->alloc(row_bytes);
         u64* fa_next = (u64*)g->alloc(bm_bytes);   // every word written by hgx_atom_pull
@@ -3519,7 +3717,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         } else if (opush) {
             // frontier-driven push (mark candidates, zero their rows, OR rows, finalise): the ordered
             // modes always, the symmetric mode with HGX_OPT_BFS_FLAGS bit 5
-            Events e2 = tm.start(kKindPush, d);
+            const bool pre_work = !g->zacc_clean || g->zacc_bytes < row_bytes || (MODE != kSym && !g->inc_yf) ||
+                                  g->n_pchunks < 0 || !cand_clean || !chained;
+            if (pre_work) tm.break_chain();
             if (!g->zacc_clean || g->zacc_bytes < row_bytes) {   // (re)establish the all-zero accumulator
                 if (g->zacc_bytes < row_bytes) {
                     if (g->zacc) HGX_HIP(hipFree(g->zacc));
@@ -3554,17 +3754,20 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // 19-113 us against 30-142 us with 8192 waves (the launch of mostly idle workgroups and
             // the candidate-append contention) and 20-171 us with 1024 waves
             const int lgrid = 512;
-            if (g->push_batch > 0)   // flattened: K atoms per wave batch (HGX_OPT_PUSH_BATCH)
+            Events e2 = tm.start_chained(kKindPush, d);
+            const bool flat = g->push_batch > 0;
+            if (flat)   // flattened: K atoms per wave batch (HGX_OPT_PUSH_BATCH)
                 hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->push_batch, g->inc_off, g->inc_row,
                                                               g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl,
                                                               full, cand, cl, n_cl, acc, c, fa_next,
                                                               (int64_t)(bm_bytes / sizeof(u64)));
-            else
+            else   // hub chunks in the same launch
                 hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
                                                          g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
-                                                         fa_next, (int64_t)(bm_bytes / sizeof(u64)));
+                                                         fa_next, (int64_t)(bm_bytes / sizeof(u64)), g->pchunks,
+                                                         g->n_pchunks, fa);
             HGX_CHECK_LAUNCH();
-            if (g->n_pchunks > 0) {
+            if (flat && g->n_pchunks > 0) {
                 hgx_opush_heavy<W, MODE><<<(unsigned)g->n_pchunks, 256, 0, s>>>(
                     g->pchunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
                     cl, n_cl, acc, c);
@@ -3572,15 +3775,24 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }
             // finalise; re-zeroes the accumulator rows and candidate words it consumed and, without a
             // ghost exchange, rewrites the candidate list into the next level's frontier list
+            // without an exchange the level's counters go straight to mapped host memory (no copy in the
+            // stream between this level and the next)
+            if (!ex) {
+                flag_level = true;
+                flag_seq = ++g->ctr_seq;
+                flag_slot = g->ctr_host + (size_t)(d & 1) * kHostSlot;
+                __atomic_store_n(flag_slot + cNum, (u64)0, __ATOMIC_RELEASE);
+            }
             hgx_push_finalize_list<W><<<512, 256, 0, s>>>(cl, n_cl, g->inc_off, acc, cand, vis, ever, full,
-                                                           lvl_next, fa_next, c, fm, ex ? 0 : 1, ex ? nullptr : n_fl);
+                                                           lvl_next, fa_next, c, fm, ex ? 0 : 1, ex ? nullptr : n_fl,
+                                                           ticket, flag_level ? flag_slot : nullptr, flag_seq);
             HGX_CHECK_LAUNCH();
             g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
             cand_clean = true;
             chained = !ex;
             std::swap(fl, cl);
             std::swap(n_fl, n_cl);
-            tm.stop(e2);
+            tm.stop_chained(e2);
         } else {
         if (sparse) {
             Events e0 = tm.start(kKindGather, d);
@@ -3689,8 +3901,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         pn.allrows = (lflags & kAllRows) ? 1 : 0;
         pn.new_global = new_global;
         pn.part_push = part_push;
-        HGX_HIP(hipMemcpyAsync(pn.h, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipEventRecord(pn.ev, s));
+        pn.flag = flag_level;
+        pn.seq = flag_seq;
+        pn.slot = flag_slot;
+        if (!flag_level) {
+            tm.break_chain();
+            HGX_HIP(hipMemcpyAsync(pn.h, c, sizeof(u64) * kCtrBlock, hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipEventRecord(pn.ev, s));
+        }
         ++npend;
         cur_lvl = lvl_next;
         cur_fa = fa_next;
@@ -3708,7 +3926,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 stop = true;
                 for (; npend > 0; --npend) {   // a level issued after the last frontier: its rows are empty
                     Pend& q = pend[(d - npend + 1) & 1];
-                    wait_event(q.ev);
+                    if (q.flag) HGX_HIP(hipStreamSynchronize(s));
+                    else wait_event(q.ev);
                     g->release(q.lvl_next, row_bytes);
                     g->release(q.fa_next, bm_bytes);
                 }
@@ -3781,18 +4000,6 @@ int count_grid(int64_t A) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), kCountBlocks));
 }
 
-void count_rows_dispatch(int W, hgx_graph* g, const u64* fa, const u64* own, const u64* lvl, uint32_t* partial) {
-    const int grid = count_grid(g->A);
-    hipStream_t s = g->stream;
-    switch (W) {
-        case 1: hgx_count_rows<1><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
-        case 2: hgx_count_rows<2><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
-        case 4: hgx_count_rows<4><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
-        case 8: hgx_count_rows<8><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
-        default: hgx_count_rows<16><<<grid, 256, 0, s>>>(g->A, fa, own, lvl, partial); break;
-    }
-    HGX_CHECK_LAUNCH();
-}
 
 // The result readout: res->counts (per seed, per depth) from the device rows -- one counting launch
 // per level (block partials), one reduce launch, one D2H, one synchronisation (first call only).
@@ -3806,6 +4013,7 @@ void ensure_counts(hgx_bfs_result* r) {
     const int grid = count_grid(g->A);
     std::vector<int32_t> meta(2 * std::max<size_t>(nslots, 1), 0);   // [nblk | width]
     std::vector<int64_t> poff(std::max<size_t>(nslots, 1), 0);
+    std::vector<const u64*> fap(std::max<size_t>(nslots, 1), nullptr), lvp(std::max<size_t>(nslots, 1), nullptr);
     int64_t ptot = 0;
     {
         size_t k = 0;
@@ -3814,33 +4022,59 @@ void ensure_counts(hgx_bfs_result* r) {
                 meta[k] = grid;
                 meta[nslots + k] = bt.W * 64;
                 poff[k] = ptot;
+                fap[k] = bt.fa[d];
+                lvp[k] = bt.lvl[d];
                 ptot += (int64_t)grid * bt.W * 64;
             }
     }
     const size_t bytes = sizeof(u64) * 1024 * std::max<size_t>(nslots, 1);
     const size_t pbytes = sizeof(uint32_t) * (size_t)std::max<int64_t>(ptot, 1);
-    const size_t mbytes = sizeof(int32_t) * meta.size() + sizeof(int64_t) * poff.size();
+    const size_t o_poff = (sizeof(int32_t) * meta.size() + 15) & ~(size_t)15;
+    const size_t o_fap = o_poff + sizeof(int64_t) * poff.size();
+    const size_t o_lvp = o_fap + sizeof(u64*) * fap.size();
+    const size_t mbytes = o_lvp + sizeof(u64*) * lvp.size();
     u64* dc = (u64*)g->alloc(bytes);
     uint32_t* dp = (uint32_t*)g->alloc(pbytes);
     char* dm = (char*)g->alloc(mbytes);
-    char* hm = (char*)g->pinned_buf(mbytes);
+    // one pinned region: the launch metadata going up, the counts coming back (a copy into pageable
+    // memory is staged through a bounce buffer)
+    const size_t o_back = (mbytes + 255) & ~(size_t)255;
+    char* hm = (char*)g->pinned_buf(o_back + bytes);
     std::memcpy(hm, meta.data(), sizeof(int32_t) * meta.size());
-    std::memcpy(hm + sizeof(int32_t) * meta.size(), poff.data(), sizeof(int64_t) * poff.size());
+    std::memcpy(hm + o_poff, poff.data(), sizeof(int64_t) * poff.size());
+    std::memcpy(hm + o_fap, fap.data(), sizeof(u64*) * fap.size());
+    std::memcpy(hm + o_lvp, lvp.data(), sizeof(u64*) * lvp.size());
     HGX_HIP(hipMemcpyAsync(dm, hm, mbytes, hipMemcpyHostToDevice, g->stream));
     const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;
     size_t k = 0;
-    for (auto& bt : r->batches)
-        for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) count_rows_dispatch(bt.W, g, bt.fa[d], own, bt.lvl[d], dp + poff[k]);
+    for (auto& bt : r->batches) {   // one launch per batch: blockIdx.y = its level slots
+        const int nl = (int)bt.lvl.size();
+        if (nl > 0) {
+            const dim3 gr((unsigned)grid, (unsigned)nl);
+            const u64* const* fa_d = (const u64* const*)(dm + o_fap);
+            const u64* const* lv_d = (const u64* const*)(dm + o_lvp);
+            const int64_t* po_d = (const int64_t*)(dm + o_poff);
+            hipStream_t s = g->stream;
+            switch (bt.W) {
+                case 1: hgx_count_rows_multi<1><<<gr, 256, 0, s>>>(g->A, fa_d, own, lv_d, po_d, (int)k, dp); break;
+                case 2: hgx_count_rows_multi<2><<<gr, 256, 0, s>>>(g->A, fa_d, own, lv_d, po_d, (int)k, dp); break;
+                case 4: hgx_count_rows_multi<4><<<gr, 256, 0, s>>>(g->A, fa_d, own, lv_d, po_d, (int)k, dp); break;
+                case 8: hgx_count_rows_multi<8><<<gr, 256, 0, s>>>(g->A, fa_d, own, lv_d, po_d, (int)k, dp); break;
+                default: hgx_count_rows_multi<16><<<gr, 256, 0, s>>>(g->A, fa_d, own, lv_d, po_d, (int)k, dp); break;
+            }
+            HGX_CHECK_LAUNCH();
+        }
+        k += (size_t)nl;
+    }
     HGX_HIP(hipMemsetAsync(dc, 0, bytes, g->stream));
     if (nslots) {
         hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024 * (kCountBlocks / kReduceSpan), 256), 256, 0,
                            g->stream>>>(
-            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots,
-            (const int64_t*)(dm + sizeof(int32_t) * meta.size()), dp, dc);
+            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots, (const int64_t*)(dm + o_poff), dp, dc);
         HGX_CHECK_LAUNCH();
     }
-    std::vector<u64> hc(1024 * std::max<size_t>(nslots, 1));
-    HGX_HIP(hipMemcpyAsync(hc.data(), dc, bytes, hipMemcpyDeviceToHost, g->stream));
+    const u64* hc = (const u64*)(hm + o_back);
+    HGX_HIP(hipMemcpyAsync(hm + o_back, dc, bytes, hipMemcpyDeviceToHost, g->stream));
     HGX_HIP(hipStreamSynchronize(g->stream));
     g->release(dc, bytes);
     g->release(dp, pbytes);

@@ -37,6 +37,7 @@ void graph_release(hgx_graph* g) {
     if (g->inc_yf) (void)hipFree(g->inc_yf);
     if (g->pchunks) (void)hipFree(g->pchunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
+    if (g->ctr_host) (void)hipHostFree(g->ctr_host);
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {

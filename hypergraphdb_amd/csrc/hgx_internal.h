@@ -175,6 +175,8 @@ struct hgx_graph {
     // into it and its finalise re-zeroes exactly the rows it consumed (no per-level clear).
     std::vector<int64_t> inc_off_host;   // host copy of inc_off (pattern planning), made on first use
     uint64_t* zacc = nullptr;
+    unsigned long long* ctr_host = nullptr;   // push levels' counters, written by the finalise (mapped host memory)
+    unsigned long long ctr_seq = 0;          // sequence numbers of those writes
     uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
     uint8_t* inc_yf = nullptr;           // [I] ordered-mode yield flags per incidence (frontier push), made on first use
     hgx::HeavyChunk* pchunks = nullptr;  // frontier push: kPushChunk-entry chunks of atoms with deg > kPushLight
@@ -217,7 +219,7 @@ struct hgx_graph {
     size_t mapped_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
-    int32_t push_batch = 16;                    // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
+    int32_t push_batch = 0;                     // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
     bool q_flat = true;                         // HGX_OPT_QUERY_FLAT: a lane per candidate over the batch's flat candidate space
     bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels
     int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
