@@ -100,6 +100,24 @@ __device__ __forceinline__ typename Vec<Lay<W>::WPL>::T full_part(const FullMask
 __device__ __forceinline__ bool bit(const u64* __restrict__ bm, int64_t i) { return (bm[i >> 6] >> (i & 63)) & 1ull; }
 __device__ __forceinline__ void set_bit(u64* bm, int64_t i) { atomicOr(&bm[i >> 6], 1ull << (i & 63)); }
 
+// position of the n-th (0-based) set bit of x (n < popcount(x)): a binary descent over the halves
+__device__ __forceinline__ int nth_set_bit(u64 x, int n) {
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half > 0; half >>= 1) {
+        const u64 lo = x & ((1ull << half) - 1ull);
+        const int c = __popcll(lo);
+        if (n >= c) {
+            n -= c;
+            x >>= half;
+            pos += half;
+        } else {
+            x = lo;
+        }
+    }
+    return pos;
+}
+
 // true if predicate holds on any / every lane of this lane's G-lane group (groups are G-aligned).
 template <int G> __device__ __forceinline__ bool group_any(bool p) {
     if constexpr (G == 1) {
@@ -1567,6 +1585,8 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
 constexpr int kFlatMax = 64;     // atoms per batch at most (one per lane)
 constexpr int kPairBuf = 512;    // (target, source) pairs staged per wave
 
+constexpr int kFlatRows = 16;   // batch atoms whose row words sit in LDS (K is clamped to this)
+
 struct FlatLds {
     int32_t v[kFlatMax];
     int64_t beg[kFlatMax];
@@ -1574,8 +1594,11 @@ struct FlatLds {
     int32_t ej[kEBuf];           // passing entries: batch slot of the atom
     int64_t ei[kEBuf];           //                  incidence entry
     int32_t pt[kPairBuf];        // pairs: target
-    int32_t ps[kPairBuf];        //        source atom
+    int32_t ps[kPairBuf];        //        batch slot of the source atom
     int32_t cbuf[kCBuf];         // fresh candidates not yet appended
+    uint32_t wmask[kFlatRows];   // nonzero words of each batch atom's row
+    u64 wval[kFlatRows * 16];    // the batch atoms' rows (W words each)
+    int32_t ppre[65];            // pair drain: exclusive prefix of the pairs' nonzero words
 };
 
 __device__ __forceinline__ void flat_cand_flush(FlatLds& sh, int& cc, int32_t* __restrict__ clist,
@@ -1590,50 +1613,63 @@ __device__ __forceinline__ void flat_cand_flush(FlatLds& sh, int& cc, int32_t* _
     cc = 0;
 }
 
-// Stage 3: OR the source row of every staged pair into its target's accumulator row; the first
-// pair to reach a target sets its candidate bit and stages it for the candidate list.
+// Stage 3: OR the source row of every staged pair into its target's accumulator row, one lane per
+// (pair, nonzero word of the source's row) -- the rows of a push level are sparse (one or two nonzero
+// words of 16 on config 5), so the words come from the batch's LDS row table and a wave pass covers
+// 64 of them; the first word of a pair sets the target's candidate bit and stages it.
 template <int W>
 __device__ __forceinline__ void flat_pairs(FlatLds& sh, int& np, int& cc, const u64* __restrict__ lvl,
                                            u64* __restrict__ acc, u64* __restrict__ cand,
                                            int32_t* __restrict__ clist, u64* __restrict__ n_clist) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
-    typedef Vec<WPL> V;
-    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int lane = threadIdx.x & 63;
     const u64 lt = (1ull << lane) - 1ull;
+    (void)lvl;
     __builtin_amdgcn_wave_barrier();
-    for (int p0 = 0; p0 < np; p0 += PER) {   // wave-uniform
-        const int p = p0 + g;
-        const bool ok = p < np;
-        const int32_t t = ok ? sh.pt[p] : 0;
-        const int32_t src = ok ? sh.ps[p] : 0;
-        bool fresh = false;
-        if (ok) {
-            const typename V::T row = V::ld(lvl + (int64_t)src * W + sub * WPL);
-            u64* a = acc + (int64_t)t * W + sub * WPL;
-            if constexpr (WPL == 1) {
-                if (row != 0ull && (*a & row) != row) atomicOr(a, row);
-            } else {
-                if (V::nz(row)) {
-                    const typename V::T cur = V::ld(a);
-                    if (row.x != 0ull && (cur.x & row.x) != row.x) atomicOr(a, row.x);
-                    if (row.y != 0ull && (cur.y & row.y) != row.y) atomicOr(a + 1, row.y);
+    for (int p0 = 0; p0 < np; p0 += 64) {   // wave-uniform
+        const int p = p0 + lane;
+        const uint32_t wm = p < np ? sh.wmask[sh.ps[p]] : 0u;
+        const int cnt = __popc(wm);
+        int incl = cnt;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const int T = __shfl(incl, 63);
+        sh.ppre[lane] = incl - cnt;
+        if (lane == 63) sh.ppre[64] = incl;
+        __builtin_amdgcn_wave_barrier();
+        for (int q0 = 0; q0 < T; q0 += 64) {   // wave-uniform
+            const int q = q0 + lane;
+            bool fresh = false;
+            int32_t t = 0;
+            if (q < T) {
+                int lo = 0, hi = 63;   // the pair holding item q
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sh.ppre[mid] <= q) lo = mid; else hi = mid - 1;
+                }
+                const int pp = p0 + lo, j = sh.ps[pp], r = q - sh.ppre[lo];
+                t = sh.pt[pp];
+                const int w = nth_set_bit((u64)sh.wmask[j], r);
+                const u64 val = sh.wval[j * W + w];
+                u64* a = acc + (int64_t)t * W + w;
+                if ((*a & val) != val) atomicOr(a, val);
+                if (r == 0) {
+                    const u64 cb = 1ull << (t & 63);
+                    if (!(cand[t >> 6] & cb)) fresh = !(atomicOr(&cand[t >> 6], cb) & cb);
                 }
             }
-            if (sub == 0) {
-                const u64 cb = 1ull << (t & 63);
-                if (!(cand[t >> 6] & cb)) fresh = !(atomicOr(&cand[t >> 6], cb) & cb);
+            const u64 fm = __ballot(fresh);
+            if (fm) {   // wave-uniform
+                const int nf = __popcll(fm);
+                if (cc + nf > kCBuf) flat_cand_flush(sh, cc, clist, n_clist);
+                if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = t;
+                cc += nf;
+                __builtin_amdgcn_wave_barrier();
             }
         }
-        const u64 fm = __ballot(fresh);
-        if (fm) {   // wave-uniform
-            const int nf = __popcll(fm);
-            if (cc + nf > kCBuf) flat_cand_flush(sh, cc, clist, n_clist);
-            if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = t;
-            cc += nf;
-            __builtin_amdgcn_wave_barrier();
-        }
+        __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
     np = 0;
 }
 
@@ -1652,11 +1688,12 @@ __device__ __forceinline__ void flat_entries(FlatLds& sh, int ne, int& np, int& 
     __builtin_amdgcn_wave_barrier();
     for (int k0 = 0; k0 < ne; k0 += 64) {   // wave-uniform
         const bool have = k0 + lane < ne;
-        int32_t v = -1;
+        int32_t v = -1, slot = 0;
         int64_t b = 0;
         int n = 0;
         if (have) {
-            v = sh.v[sh.ej[k0 + lane]];
+            slot = sh.ej[k0 + lane];
+            v = sh.v[slot];
             const int32_t L = inc_row[sh.ei[k0 + lane]];
             b = tgt_off[L];
             n = (int)(tgt_off[L + 1] - b);
@@ -1715,7 +1752,7 @@ __device__ __forceinline__ void flat_entries(FlatLds& sh, int ne, int& np, int& 
             if (elig) {
                 const int q = np + __popcll(m & lt);
                 sh.pt[q] = t;
-                sh.ps[q] = v;
+                sh.ps[q] = slot;
             }
             np += __popcll(m);
         }
@@ -1768,6 +1805,16 @@ __global__ void __launch_bounds__(256) hgx_opush_flat(const int32_t* __restrict_
         sh.beg[lane] = beg;
         sh.pre[lane + 1] = incl;
         if (lane == 0) sh.pre[0] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (int i0 = 0; i0 < K * W; i0 += 64) {   // the batch atoms' rows and their nonzero-word masks
+            const int i = i0 + lane, sl = i / W;
+            const int32_t sv = i < K * W ? sh.v[sl] : -1;
+            const u64 x = sv >= 0 ? lvl[(int64_t)sv * W + (i % W)] : 0ull;
+            if (i < K * W) sh.wval[i] = x;
+            const u64 nzb = __ballot(x != 0ull);
+            if (i < K * W && i % W == 0)
+                sh.wmask[sl] = (uint32_t)((nzb >> (lane - (lane % W))) & ((W >= 32) ? 0xffffffffull : ((1ull << W) - 1ull)));
+        }
         __builtin_amdgcn_wave_barrier();
         int ne = 0;   // staged passing entries (wave-uniform)
         for (int e0 = 0; e0 < E; e0 += 64 * kUnroll) {   // wave-uniform
@@ -1822,9 +1869,8 @@ __global__ void __launch_bounds__(256) hgx_opush_flat(const int32_t* __restrict_
         if (ne)
             flat_entries<W, MODE>(sh, ne, np, cc, inc_row, tgt_off, tgt_idx, lvl, full, acc, cand, clist, n_clist,
                                   n_links, n_pins, n_pairs);
-        // the batch's atoms leave sh.v / sh.beg for the next batch: drain the pairs first (they only
-        // keep target / source ids, but the next batch's stage 2 would append behind them: fine) --
-        // pairs stay staged across batches and drain when full or at the end
+        // the pairs point into this batch's row table: drain them before the next batch replaces it
+        if (np) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
         __builtin_amdgcn_wave_barrier();
     }
     if (np) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
@@ -1905,9 +1951,17 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
                                                               u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
                                                               u64* __restrict__ ctr, FullMask fm, int relist,
                                                               u64* __restrict__ n_spent, u64* __restrict__ ticket,
-                                                              u64* __restrict__ hout, u64 seq) {
+                                                              u64* __restrict__ hout, u64 seq,
+                                                              u64* __restrict__ lcount) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
+    // lcount: the next level's per-source counts, accumulated here (a push level's new rows are sparse:
+    // one LDS add per set bit, one global add per nonzero source per block) instead of a readout pass
+    __shared__ uint32_t lc[W * 64];
+    if (lcount) {
+        for (int j = threadIdx.x; j < W * 64; j += blockDim.x) lc[j] = 0u;
+        __syncthreads();
+    }
     const int sub = threadIdx.x & (G - 1);
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
@@ -1932,6 +1986,14 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
         if (valid && isnew) {
             V::st(lvl_next + t * W + sub * WPL, nw);
             V::st(vis + t * W + sub * WPL, old | nw);
+            if (lcount) {
+                if constexpr (WPL == 1) {
+                    for (u64 m = nw; m; m &= m - 1ull) atomicAdd(&lc[sub * 64 + __ffsll((long long)m) - 1], 1u);
+                } else {
+                    for (u64 m = nw.x; m; m &= m - 1ull) atomicAdd(&lc[sub * 128 + __ffsll((long long)m) - 1], 1u);
+                    for (u64 m = nw.y; m; m &= m - 1ull) atomicAdd(&lc[sub * 128 + 64 + __ffsll((long long)m) - 1], 1u);
+                }
+            }
             if (sub == 0) {
                 set_bit(fa_next, t);
                 if (!ev) set_bit(ever, t);
@@ -1957,6 +2019,11 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+    if (lcount) {
+        __syncthreads();
+        for (int j = threadIdx.x; j < W * 64; j += blockDim.x)
+            if (lc[j]) atomicAdd(lcount + j, (u64)lc[j]);
+    }
     if (hout) level_counters_out(ctr, ticket, hout, seq);
 }
 
@@ -2216,22 +2283,6 @@ __global__ void __launch_bounds__(256) hgx_level_count(int64_t A, const u64* __r
 }
 
 // Position of the n-th set bit (n < popcount(x)) of x: binary search over popcounts (6 steps).
-__device__ __forceinline__ int nth_set_bit(u64 x, int n) {
-    int pos = 0;
-#pragma unroll
-    for (int half = 32; half > 0; half >>= 1) {
-        const u64 lo = x & ((1ull << half) - 1ull);
-        const int c = __popcll(lo);
-        if (n >= c) {
-            n -= c;
-            x >>= half;
-            pos += half;
-        } else {
-            x = lo;
-        }
-    }
-    return pos;
-}
 
 // Per-source counts of one level (the result readout of a batch): the count of source w*64 + b =
 // |{v : fa(v), bit b of lvl[v][w]}|, reading only the rows of the level's atoms.  A wave takes 64
@@ -2270,6 +2321,7 @@ __global__ void __launch_bounds__(256) hgx_count_rows_multi(int64_t A, const u64
                                                             const int64_t* __restrict__ poff, int slot0,
                                                             uint32_t* __restrict__ partial) {
     const int sl = slot0 + (int)blockIdx.y;
+    if (!fa_p[sl]) return;   // counted by its push finalise
     count_rows_body<W>(A, fa_p[sl], own, lvl_p[sl], partial + poff[sl]);
 }
 
@@ -2343,6 +2395,7 @@ constexpr int kReduceSpan = 128;
 __global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t* __restrict__ nblk,
                                                         const int32_t* __restrict__ width,
                                                         const int64_t* __restrict__ poff,
+                                                        const u64* const* __restrict__ direct,
                                                         const uint32_t* __restrict__ partial, u64* __restrict__ counts) {
     constexpr int NR = kCountBlocks / kReduceSpan;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -2354,7 +2407,7 @@ __global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t
     if (j >= wj) return;
     const uint32_t* p = partial + poff[sl] + j;
     const int b0 = r * kReduceSpan, b1 = min(nblk[sl], b0 + kReduceSpan);
-    u64 sum = 0;
+    u64 sum = (r == 0 && direct[sl]) ? direct[sl][j] : 0ull;   // a push level's counts from its finalise
     for (int b = b0; b < b1; b += 8) {
         uint32_t v[8];
 #pragma unroll
@@ -3056,11 +3109,15 @@ using namespace hgx;
 // Host orchestration
 // ---------------------------------------------------------------------------------------------
 
+constexpr int kDirectLevels = 256;   // levels whose push-level counts the finalise accumulates
+
 struct BfsBatch {
     int32_t seed0 = 0, S = 0, W = 0;
     int32_t n_expanded = 0;       // levels whose frontier was expanded (advance() iterated)
     std::vector<u64*> lvl;        // per level, A*W words (rows valid where fa bit set)
     std::vector<u64*> fa;         // per level, A bits
+    u64* pcnt = nullptr;          // [kDirectLevels][1024] per-source counts of push levels (whole graph)
+    std::vector<char> direct;     // direct[d]: level d's counts are in pcnt (no counting pass)
 };
 
 struct hgx_bfs_result {
@@ -3536,6 +3593,11 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
 
     HGX_HIP(hipMemsetAsync(ever, 0, bm_bytes, s));
     HGX_HIP(hipMemsetAsync(full, 0, bm_bytes, s));
+    if (!tr) {   // per-source counts of push levels, accumulated by their finalise (readout without a pass)
+        bt.pcnt = (u64*)g->alloc(sizeof(u64) * 1024 * kDirectLevels);
+        HGX_HIP(hipMemsetAsync(bt.pcnt, 0, sizeof(u64) * 1024 * kDirectLevels, s));
+        bt.direct.assign(kDirectLevels, 0);
+    }
     HGX_HIP(hipMemsetAsync(hubacc, 0, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W, s));
     HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kCtrBlock * max_levels_cap, s));
     HGX_HIP(hipMemcpyAsync(d_atoms, seed_atoms.data(), sizeof(int32_t) * seed_atoms.size(), hipMemcpyHostToDevice, s));
@@ -3756,8 +3818,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             const int lgrid = 512;
             Events e2 = tm.start_chained(kKindPush, d);
             const bool flat = g->push_batch > 0;
-            if (flat)   // flattened: K atoms per wave batch (HGX_OPT_PUSH_BATCH)
-                hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->push_batch, g->inc_off, g->inc_row,
+            if (flat)   // flattened: K <= kFlatRows atoms per wave batch (HGX_OPT_PUSH_BATCH)
+                hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, std::min(g->push_batch, kFlatRows), g->inc_off, g->inc_row,
                                                               g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl,
                                                               full, cand, cl, n_cl, acc, c, fa_next,
                                                               (int64_t)(bm_bytes / sizeof(u64)));
@@ -3783,9 +3845,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 flag_slot = g->ctr_host + (size_t)(d & 1) * kHostSlot;
                 __atomic_store_n(flag_slot + cNum, (u64)0, __ATOMIC_RELEASE);
             }
+            u64* lcount = nullptr;   // the new level's counts accumulated by the finalise (no exchange)
+            if (!ex && bt.pcnt && d + 1 < kDirectLevels) {
+                lcount = bt.pcnt + (size_t)(d + 1) * 1024;
+                bt.direct[d + 1] = 1;
+            }
             hgx_push_finalize_list<W><<<512, 256, 0, s>>>(cl, n_cl, g->inc_off, acc, cand, vis, ever, full,
                                                            lvl_next, fa_next, c, fm, ex ? 0 : 1, ex ? nullptr : n_fl,
-                                                           ticket, flag_level ? flag_slot : nullptr, flag_seq);
+                                                           ticket, flag_level ? flag_slot : nullptr, flag_seq, lcount);
             HGX_CHECK_LAUNCH();
             g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
             cand_clean = true;
@@ -4013,18 +4080,21 @@ void ensure_counts(hgx_bfs_result* r) {
     const int grid = count_grid(g->A);
     std::vector<int32_t> meta(2 * std::max<size_t>(nslots, 1), 0);   // [nblk | width]
     std::vector<int64_t> poff(std::max<size_t>(nslots, 1), 0);
-    std::vector<const u64*> fap(std::max<size_t>(nslots, 1), nullptr), lvp(std::max<size_t>(nslots, 1), nullptr);
+    std::vector<const u64*> fap(std::max<size_t>(nslots, 1), nullptr), lvp(std::max<size_t>(nslots, 1), nullptr),
+        dirp(std::max<size_t>(nslots, 1), nullptr);
     int64_t ptot = 0;
     {
         size_t k = 0;
         for (auto& bt : r->batches)
             for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) {
-                meta[k] = grid;
+                const bool dir = d < bt.direct.size() && bt.direct[d];   // counted by the push finalise
+                meta[k] = dir ? 0 : grid;
                 meta[nslots + k] = bt.W * 64;
                 poff[k] = ptot;
-                fap[k] = bt.fa[d];
+                fap[k] = dir ? nullptr : bt.fa[d];
                 lvp[k] = bt.lvl[d];
-                ptot += (int64_t)grid * bt.W * 64;
+                dirp[k] = dir ? bt.pcnt + d * 1024 : nullptr;
+                if (!dir) ptot += (int64_t)grid * bt.W * 64;
             }
     }
     const size_t bytes = sizeof(u64) * 1024 * std::max<size_t>(nslots, 1);
@@ -4032,7 +4102,8 @@ void ensure_counts(hgx_bfs_result* r) {
     const size_t o_poff = (sizeof(int32_t) * meta.size() + 15) & ~(size_t)15;
     const size_t o_fap = o_poff + sizeof(int64_t) * poff.size();
     const size_t o_lvp = o_fap + sizeof(u64*) * fap.size();
-    const size_t mbytes = o_lvp + sizeof(u64*) * lvp.size();
+    const size_t o_dir = o_lvp + sizeof(u64*) * lvp.size();
+    const size_t mbytes = o_dir + sizeof(u64*) * dirp.size();
     u64* dc = (u64*)g->alloc(bytes);
     uint32_t* dp = (uint32_t*)g->alloc(pbytes);
     char* dm = (char*)g->alloc(mbytes);
@@ -4044,6 +4115,7 @@ void ensure_counts(hgx_bfs_result* r) {
     std::memcpy(hm + o_poff, poff.data(), sizeof(int64_t) * poff.size());
     std::memcpy(hm + o_fap, fap.data(), sizeof(u64*) * fap.size());
     std::memcpy(hm + o_lvp, lvp.data(), sizeof(u64*) * lvp.size());
+    std::memcpy(hm + o_dir, dirp.data(), sizeof(u64*) * dirp.size());
     HGX_HIP(hipMemcpyAsync(dm, hm, mbytes, hipMemcpyHostToDevice, g->stream));
     const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;
     size_t k = 0;
@@ -4070,7 +4142,8 @@ void ensure_counts(hgx_bfs_result* r) {
     if (nslots) {
         hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024 * (kCountBlocks / kReduceSpan), 256), 256, 0,
                            g->stream>>>(
-            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots, (const int64_t*)(dm + o_poff), dp, dc);
+            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots, (const int64_t*)(dm + o_poff),
+            (const u64* const*)(dm + o_dir), dp, dc);
         HGX_CHECK_LAUNCH();
     }
     const u64* hc = (const u64*)(hm + o_back);
@@ -4189,6 +4262,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             for (auto& bt : r->batches) {
                 for (auto p : bt.lvl) r->g->release(p, r->row_bytes(bt));
                 for (auto p : bt.fa) r->g->release(p, r->bm_bytes());
+                if (bt.pcnt) r->g->release(bt.pcnt, sizeof(u64) * 1024 * kDirectLevels);
             }
             r->g->refs.fetch_sub(1);   // the caller still holds its own reference
             delete r;
@@ -4453,6 +4527,7 @@ void hgx_bfs_result_free(hgx_bfs_result* r) {
         for (auto& bt : r->batches) {
             for (auto p : bt.lvl) g->release(p, r->row_bytes(bt));
             for (auto p : bt.fa) g->release(p, r->bm_bytes());
+            if (bt.pcnt) g->release(bt.pcnt, sizeof(u64) * 1024 * kDirectLevels);
         }
     }
     delete r;

@@ -122,7 +122,7 @@ struct ShardInfo {
     // same atom) answers in slot j of my receive segment from q.
     int32_t* xo_slot = nullptr;          // [A_local] ghost: its slot in the (me -> owner) segment
     int32_t* bc_slot = nullptr;          // [bc entries] its slot in the (me -> holder) segment
-    int32_t xmode = 0;                   // HGX_OPT_PART_EXCHANGE: 0 auto, 1 compressed records, 2 static slots
+    int32_t xmode = 1;                   // HGX_OPT_PART_EXCHANGE: 1 compressed records (default), 2 static slots, 0 per level
     // the global -> local id of an atom present here, or -1 (binary search of l2g_host)
     int32_t local_of(int64_t v) const {
         auto it = std::lower_bound(l2g_host.begin(), l2g_host.end(), (int32_t)v);

@@ -360,8 +360,10 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * ms per direction at K = 16 against 1.74 / 2.08 with one wavefront per atom, the default 0). */
 #define HGX_OPT_PUSH_BATCH 7
 /* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value):
- * 0 = per level, static-slot rows when at least half of the group's ghosts have news (dense levels),
- * compressed records otherwise; 1 = always compressed records; 2 = always static slots. */
+ * 1 = compressed records (default); 2 = static slots (every ghost's whole row to a fixed slot of its
+ * owner, the owner's final row back); 0 = per level, the format a sampled density estimate says moves
+ * fewer bytes.  A/B on full config 4 at 8 parts: 34.0 / 42.8 / 35.5 ms per part a step
+ * (profiles/r02ze_part_c4x1.json) -- the static kernels touch every ghost and owned atom. */
 #define HGX_OPT_PART_EXCHANGE 8
 /* HGX_OPT_QUERY_FLAT (default 1): pattern batches match over the batch's flat candidate space, a
  * wavefront per 64 candidates and a lane per candidate whatever query it belongs to; 0 = a
