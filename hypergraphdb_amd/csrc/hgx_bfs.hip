@@ -2328,7 +2328,9 @@ __global__ void __launch_bounds__(256) hgx_count_rows_multi(int64_t A, const u64
 template <int W>
 __device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict__ fa, const u64* __restrict__ own,
                                                 const u64* __restrict__ lvl, uint32_t* __restrict__ partial) {
-    constexpr int K = 22;   // planes of the eights: < 2^25 rows per lane
+    // planes of the eights: K = 8 holds < 2^11 rows per lane, flushed into the block's LDS counts before
+    // they can overflow (22 planes kept 44 VGPRs live for the whole kernel: 120 VGPRs, 4 waves/SIMD)
+    constexpr int K = 8;
     constexpr int R = 64 / W, U = 8;
     __shared__ unsigned int lc[W * 64];
     for (int j = threadIdx.x; j < W * 64; j += 256) lc[j] = 0;
@@ -2341,6 +2343,20 @@ __device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict
     u64 c[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) c[q] = 0;
+    int since = 0;   // rows per lane added since the last flush (wave-uniform)
+    auto flush = [&]() {
+        for (int b = 0; b < 64; ++b) {
+            unsigned int n = (unsigned int)((ones >> b) & 1ull) | ((unsigned int)((twos >> b) & 1ull) << 1) |
+                             ((unsigned int)((fours >> b) & 1ull) << 2);
+#pragma unroll
+            for (int q = 0; q < K; ++q) n += (unsigned int)((c[q] >> b) & 1ull) << (q + 3);
+            if (n) atomicAdd(&lc[wd * 64 + b], n);
+        }
+        ones = twos = fours = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) c[q] = 0;
+        since = 0;
+    };
     for (int64_t base = wave * 64; base < nwords; base += nwave * 64) {
         const int64_t wi = base + lane;
         const u64 x = wi < nwords ? (fa[wi] & (own ? own[wi] : ~0ull)) : 0ull;
@@ -2374,16 +2390,12 @@ __device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict
                     c[q] ^= carry;
                     carry = tq;
                 }
+                since += U;
+                if (since > (8 << K) - 2 * U) flush();   // wave-uniform
             }
         }
     }
-    for (int b = 0; b < 64; ++b) {
-        unsigned int n = (unsigned int)((ones >> b) & 1ull) | ((unsigned int)((twos >> b) & 1ull) << 1) |
-                         ((unsigned int)((fours >> b) & 1ull) << 2);
-#pragma unroll
-        for (int q = 0; q < K; ++q) n += (unsigned int)((c[q] >> b) & 1ull) << (q + 3);
-        if (n) atomicAdd(&lc[wd * 64 + b], n);
-    }
+    flush();
     __syncthreads();
     for (int j = threadIdx.x; j < W * 64; j += 256) partial[(int64_t)blockIdx.x * (W * 64) + j] = lc[j];
 }
