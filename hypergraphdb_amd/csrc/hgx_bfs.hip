@@ -2361,37 +2361,46 @@ __device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict
         const int64_t wi = base + lane;
         const u64 x = wi < nwords ? (fa[wi] & (own ? own[wi] : ~0ull)) : 0ull;
         u64 m = __ballot(x != 0ull);
-        while (m) {
-            const int kw = __ffsll((long long)m) - 1;
+        auto add8 = [&](const u64 (&v)[U]) {   // 8 row words into the carry-save planes
+            u64 t2a, t2b, t4a, t4b, t8;
+            csa(t2a, ones, ones, v[0], v[1]);
+            csa(t2b, ones, ones, v[2], v[3]);
+            csa(t4a, twos, twos, t2a, t2b);
+            csa(t2a, ones, ones, v[4], v[5]);
+            csa(t2b, ones, ones, v[6], v[7]);
+            csa(t4b, twos, twos, t2a, t2b);
+            csa(t8, fours, fours, t4a, t4b);
+            u64 carry = t8;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                if (__ballot(carry != 0ull) == 0ull) break;   // wave-uniform
+                const u64 tq = c[q] & carry;
+                c[q] ^= carry;
+                carry = tq;
+            }
+        };
+        while (m) {   // two nonzero words at a time: their row loads in flight together
+            const int kw1 = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            const u64 xw = (u64)__shfl(x, kw);
-            const int64_t t0 = (base + kw) * 64;
-            const int n = __popcll(xw);
-            for (int r0 = 0; r0 < n; r0 += R * U) {   // wave-uniform
-                u64 v[U];
+            const int kw2 = m ? __ffsll((long long)m) - 1 : -1;
+            if (m) m &= m - 1ull;
+            const u64 xw1 = (u64)__shfl(x, kw1);
+            const u64 s2 = (u64)__shfl(x, kw2 < 0 ? 0 : kw2);
+            const u64 xw2 = kw2 < 0 ? 0ull : s2;
+            const int64_t t1 = (base + kw1) * 64, t2 = (base + (kw2 < 0 ? 0 : kw2)) * 64;
+            const int n1 = __popcll(xw1), n2 = __popcll(xw2), nm = n1 > n2 ? n1 : n2;
+            for (int r0 = 0; r0 < nm; r0 += R * U) {   // wave-uniform
+                u64 v1[U], v2[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int j = r0 + u * R + k;
-                    v[u] = j < n ? lvl[(t0 + nth_set_bit(xw, j)) * W + wd] : 0ull;
+                    v1[u] = j < n1 ? lvl[(t1 + nth_set_bit(xw1, j)) * W + wd] : 0ull;
+                    v2[u] = j < n2 ? lvl[(t2 + nth_set_bit(xw2, j)) * W + wd] : 0ull;
                 }
-                u64 t2a, t2b, t4a, t4b, t8;
-                csa(t2a, ones, ones, v[0], v[1]);
-                csa(t2b, ones, ones, v[2], v[3]);
-                csa(t4a, twos, twos, t2a, t2b);
-                csa(t2a, ones, ones, v[4], v[5]);
-                csa(t2b, ones, ones, v[6], v[7]);
-                csa(t4b, twos, twos, t2a, t2b);
-                csa(t8, fours, fours, t4a, t4b);
-                u64 carry = t8;
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    if (__ballot(carry != 0ull) == 0ull) break;   // wave-uniform
-                    const u64 tq = c[q] & carry;
-                    c[q] ^= carry;
-                    carry = tq;
-                }
-                since += U;
-                if (since > (8 << K) - 2 * U) flush();   // wave-uniform
+                add8(v1);
+                add8(v2);
+                since += 2 * U;
+                if (since > (8 << K) - 4 * U) flush();   // wave-uniform
             }
         }
     }
