@@ -3839,6 +3839,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             const int lgrid = 512;
             Events e2 = tm.start_chained(kKindPush, d);
             const bool flat = g->push_batch > 0;
+            // hub chunks inside hgx_opush while there are few of them (config 5: ~350 chunks, one launch
+            // less per level); a block per chunk in hgx_opush_heavy when there are many (config 2:
+            // ~380K chunks of 26K hubs: folded into 512 blocks the seed level took 0.58 ms against 0.41)
+            const bool fold = !flat && g->n_pchunks <= 8 * lgrid;
             if (flat)   // flattened: K <= kFlatRows atoms per wave batch (HGX_OPT_PUSH_BATCH)
                 hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, std::min(g->push_batch, kFlatRows), g->inc_off, g->inc_row,
                                                               g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl,
@@ -3848,9 +3852,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
                                                          g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
                                                          fa_next, (int64_t)(bm_bytes / sizeof(u64)), g->pchunks,
-                                                         g->n_pchunks, fa);
+                                                         fold ? g->n_pchunks : 0, fa);
             HGX_CHECK_LAUNCH();
-            if (flat && g->n_pchunks > 0) {
+            if (!fold && g->n_pchunks > 0) {
                 hgx_opush_heavy<W, MODE><<<(unsigned)g->n_pchunks, 256, 0, s>>>(
                     g->pchunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
                     cl, n_cl, acc, c);
