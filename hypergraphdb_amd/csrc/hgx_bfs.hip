@@ -2415,9 +2415,9 @@ __device__ __forceinline__ void count_rows_body(int64_t A, const u64* __restrict
 constexpr int kReduceSpan = 128;
 __global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t* __restrict__ nblk,
                                                         const int32_t* __restrict__ width,
-                                                        const int64_t* __restrict__ poff,
+                                                        const uint32_t* const* __restrict__ pp,
                                                         const u64* const* __restrict__ direct,
-                                                        const uint32_t* __restrict__ partial, u64* __restrict__ counts) {
+                                                        u64* __restrict__ counts) {
     constexpr int NR = kCountBlocks / kReduceSpan;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= (int64_t)nslot * 1024 * NR) return;
@@ -2426,7 +2426,7 @@ __global__ void __launch_bounds__(256) hgx_count_reduce(int nslot, const int32_t
     const int sl = (int)(sj / 1024), j = (int)(sj % 1024);
     const int wj = width[sl];
     if (j >= wj) return;
-    const uint32_t* p = partial + poff[sl] + j;
+    const uint32_t* p = pp[sl] + j;
     const int b0 = r * kReduceSpan, b1 = min(nblk[sl], b0 + kReduceSpan);
     u64 sum = (r == 0 && direct[sl]) ? direct[sl][j] : 0ull;   // a push level's counts from its finalise
     for (int b = b0; b < b1; b += 8) {
@@ -3130,6 +3130,12 @@ using namespace hgx;
 // Host orchestration
 // ---------------------------------------------------------------------------------------------
 
+// blocks of a counting pass (a wave per 64 bitmap words at least, kCountBlocks at most)
+inline int count_grid(int64_t A) {
+    const int64_t nwords = ceil_div(std::max<int64_t>(A, 1), 64);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), kCountBlocks));
+}
+
 constexpr int kDirectLevels = 256;   // levels whose push-level counts the finalise accumulates
 
 struct BfsBatch {
@@ -3139,6 +3145,11 @@ struct BfsBatch {
     std::vector<u64*> fa;         // per level, A bits
     u64* pcnt = nullptr;          // [kDirectLevels][1024] per-source counts of push levels (whole graph)
     std::vector<char> direct;     // direct[d]: level d's counts are in pcnt (no counting pass)
+    // counting launched on g->stream2 as soon as a level is final, next to the following levels
+    // (cpart[d]: its block partials, cgrid blocks of W*64 words; null = counted at readout)
+    std::vector<uint32_t*> cpart;
+    int cgrid = 0;
+    size_t cpart_bytes = 0;
 };
 
 struct hgx_bfs_result {
@@ -3633,6 +3644,32 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                                                               full, fm);
         HGX_CHECK_LAUNCH();
     }
+    // Readout counting next to the traversal (A/B, HGX_COUNT_EAGER=1): a level's rows are final once
+    // it is produced, so its counting pass can run on a second stream while the following levels run.
+    // Measured slower on config 2 (19.36 against 18.66 ms for traversal + readout,
+    // profiles/r02zj_readout_*.log): the passes share HBM and CUs with the dense levels and delay
+    // them by more than they save.  Default: counted at readout time.  Push levels count their news
+    // in their finalise and need no pass either way.
+    const bool eager = !tr && !g->shard && std::getenv("HGX_COUNT_EAGER") && std::getenv("HGX_COUNT_EAGER")[0] == '1';
+    if (eager && !g->stream2) {
+        HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
+        HGX_HIP(hipEventCreateWithFlags(&g->ev_count, hipEventDisableTiming));
+    }
+    auto count_now = [&](size_t lev, hipEvent_t after) {   // level lev of bt: its counting pass on stream2
+        if (!eager) return;
+        if (lev < bt.direct.size() && bt.direct[lev]) return;
+        if (bt.cpart.size() <= lev) bt.cpart.resize(lev + 1, nullptr);
+        bt.cgrid = count_grid(A);
+        bt.cpart_bytes = sizeof(uint32_t) * (size_t)bt.cgrid * W * 64;
+        bt.cpart[lev] = (uint32_t*)g->alloc(bt.cpart_bytes);
+        HGX_HIP(hipStreamWaitEvent(g->stream2, after, 0));
+        hgx_count_rows<W><<<bt.cgrid, 256, 0, g->stream2>>>(A, bt.fa[lev], nullptr, bt.lvl[lev], bt.cpart[lev]);
+        HGX_CHECK_LAUNCH();
+    };
+    if (eager) {
+        HGX_HIP(hipEventRecord(g->ev_count, s));
+        count_now(0, g->ev_count);
+    }
 
     const int block = 256;
     const int gather_grid = grid_for(ceil_div(M, 64) * 64, block, 256 * 16);
@@ -3753,6 +3790,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }
         bt.lvl.push_back(p.lvl_next);
         bt.fa.push_back(p.fa_next);
+        if (!p.flag) count_now(bt.lvl.size() - 1, p.ev);   // p.ev follows the level's kernels
         return true;
     };
 
@@ -4087,10 +4125,6 @@ void count_level_dispatch(int W, hgx_graph* g, const u64* fa, const u64* lvl, u6
     }
 }
 
-int count_grid(int64_t A) {
-    const int64_t nwords = ceil_div(std::max<int64_t>(A, 1), 64);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nwords, 64 * 4), kCountBlocks));
-}
 
 
 // The result readout: res->counts (per seed, per depth) from the device rows -- one counting launch
@@ -4108,18 +4142,23 @@ void ensure_counts(hgx_bfs_result* r) {
     std::vector<const u64*> fap(std::max<size_t>(nslots, 1), nullptr), lvp(std::max<size_t>(nslots, 1), nullptr),
         dirp(std::max<size_t>(nslots, 1), nullptr);
     int64_t ptot = 0;
+    bool any_early = false;
+    std::vector<const uint32_t*> early_p(std::max<size_t>(nslots, 1), nullptr), partp(std::max<size_t>(nslots, 1), nullptr);
     {
         size_t k = 0;
         for (auto& bt : r->batches)
             for (size_t d = 0; d < bt.lvl.size(); ++d, ++k) {
                 const bool dir = d < bt.direct.size() && bt.direct[d];   // counted by the push finalise
-                meta[k] = dir ? 0 : grid;
+                const bool early = d < bt.cpart.size() && bt.cpart[d];   // counted next to the traversal
+                any_early |= early;
+                meta[k] = dir ? 0 : early ? bt.cgrid : grid;
                 meta[nslots + k] = bt.W * 64;
                 poff[k] = ptot;
-                fap[k] = dir ? nullptr : bt.fa[d];
+                fap[k] = (dir || early) ? nullptr : bt.fa[d];
                 lvp[k] = bt.lvl[d];
                 dirp[k] = dir ? bt.pcnt + d * 1024 : nullptr;
-                if (!dir) ptot += (int64_t)grid * bt.W * 64;
+                early_p[k] = early ? bt.cpart[d] : nullptr;
+                if (!dir && !early) ptot += (int64_t)grid * bt.W * 64;
             }
     }
     const size_t bytes = sizeof(u64) * 1024 * std::max<size_t>(nslots, 1);
@@ -4128,9 +4167,11 @@ void ensure_counts(hgx_bfs_result* r) {
     const size_t o_fap = o_poff + sizeof(int64_t) * poff.size();
     const size_t o_lvp = o_fap + sizeof(u64*) * fap.size();
     const size_t o_dir = o_lvp + sizeof(u64*) * lvp.size();
-    const size_t mbytes = o_dir + sizeof(u64*) * dirp.size();
+    const size_t o_pp = o_dir + sizeof(u64*) * dirp.size();
+    const size_t mbytes = o_pp + sizeof(uint32_t*) * partp.size();
     u64* dc = (u64*)g->alloc(bytes);
     uint32_t* dp = (uint32_t*)g->alloc(pbytes);
+    for (size_t k = 0; k < nslots; ++k) partp[k] = early_p[k] ? early_p[k] : dp + poff[k];
     char* dm = (char*)g->alloc(mbytes);
     // one pinned region: the launch metadata going up, the counts coming back (a copy into pageable
     // memory is staged through a bounce buffer)
@@ -4141,6 +4182,7 @@ void ensure_counts(hgx_bfs_result* r) {
     std::memcpy(hm + o_fap, fap.data(), sizeof(u64*) * fap.size());
     std::memcpy(hm + o_lvp, lvp.data(), sizeof(u64*) * lvp.size());
     std::memcpy(hm + o_dir, dirp.data(), sizeof(u64*) * dirp.size());
+    std::memcpy(hm + o_pp, partp.data(), sizeof(uint32_t*) * partp.size());
     HGX_HIP(hipMemcpyAsync(dm, hm, mbytes, hipMemcpyHostToDevice, g->stream));
     const u64* own = g->shard ? (const u64*)g->shard->own_bm : nullptr;
     size_t k = 0;
@@ -4164,11 +4206,15 @@ void ensure_counts(hgx_bfs_result* r) {
         k += (size_t)nl;
     }
     HGX_HIP(hipMemsetAsync(dc, 0, bytes, g->stream));
+    if (any_early) {   // the passes already launched on stream2 come first
+        HGX_HIP(hipEventRecord(g->ev_count, g->stream2));
+        HGX_HIP(hipStreamWaitEvent(g->stream, g->ev_count, 0));
+    }
     if (nslots) {
         hgx_count_reduce<<<(unsigned)ceil_div((int64_t)nslots * 1024 * (kCountBlocks / kReduceSpan), 256), 256, 0,
                            g->stream>>>(
-            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots, (const int64_t*)(dm + o_poff),
-            (const u64* const*)(dm + o_dir), dp, dc);
+            (int)nslots, (const int32_t*)dm, (const int32_t*)dm + nslots, (const uint32_t* const*)(dm + o_pp),
+            (const u64* const*)(dm + o_dir), dc);
         HGX_CHECK_LAUNCH();
     }
     const u64* hc = (const u64*)(hm + o_back);
@@ -4177,6 +4223,11 @@ void ensure_counts(hgx_bfs_result* r) {
     g->release(dc, bytes);
     g->release(dp, pbytes);
     g->release(dm, mbytes);
+    for (auto& bt : r->batches) {   // stream2's passes were ordered before the synchronised reduce
+        for (auto& p : bt.cpart)
+            if (p) g->release(p, bt.cpart_bytes);
+        bt.cpart.clear();
+    }
     k = 0;
     for (auto& bt : r->batches)
         for (size_t d = 0; d < bt.lvl.size(); ++d, ++k)
@@ -4284,10 +4335,13 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         hgx_bfs_result* r;
         ~Guard() {
             if (!r) return;
+            if (r->g->stream2) (void)hipStreamSynchronize(r->g->stream2);   // counting passes read the rows
             for (auto& bt : r->batches) {
                 for (auto p : bt.lvl) r->g->release(p, r->row_bytes(bt));
                 for (auto p : bt.fa) r->g->release(p, r->bm_bytes());
                 if (bt.pcnt) r->g->release(bt.pcnt, sizeof(u64) * 1024 * kDirectLevels);
+                for (auto p : bt.cpart)
+                    if (p) r->g->release(p, bt.cpart_bytes);
             }
             r->g->refs.fetch_sub(1);   // the caller still holds its own reference
             delete r;
@@ -4549,10 +4603,13 @@ void hgx_bfs_result_free(hgx_bfs_result* r) {
     if (g) {
         std::lock_guard<std::mutex> lk(g->mu);
         (void)hipSetDevice(g->device);
+        if (g->stream2) (void)hipStreamSynchronize(g->stream2);   // counting passes may still read the rows
         for (auto& bt : r->batches) {
             for (auto p : bt.lvl) g->release(p, r->row_bytes(bt));
             for (auto p : bt.fa) g->release(p, r->bm_bytes());
             if (bt.pcnt) g->release(bt.pcnt, sizeof(u64) * 1024 * kDirectLevels);
+            for (auto p : bt.cpart)
+                if (p) g->release(p, bt.cpart_bytes);
         }
     }
     delete r;

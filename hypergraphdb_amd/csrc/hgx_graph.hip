@@ -39,6 +39,9 @@ void graph_release(hgx_graph* g) {
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
     if (g->mapped) (void)hipHostFree(g->mapped);
+    if (g->stream2) (void)hipStreamSynchronize(g->stream2);
+    if (g->ev_count) (void)hipEventDestroy(g->ev_count);
+    if (g->stream2) (void)hipStreamDestroy(g->stream2);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {
         (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);

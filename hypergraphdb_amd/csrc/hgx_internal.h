@@ -160,6 +160,8 @@ struct hgx_comm {
 struct hgx_graph {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;      // readout counting next to the traversal (made on first use)
+    hipEvent_t ev_count = nullptr;      //   and its ordering event
     std::mutex mu;
     std::atomic<int> refs{1};
     bool timing = false;
