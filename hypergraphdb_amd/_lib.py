@@ -32,6 +32,7 @@ HGX_OPT_QUERY_INLINE = 6
 HGX_OPT_PUSH_BATCH = 7
 HGX_OPT_PART_EXCHANGE = 8
 HGX_OPT_QUERY_FLAT = 9
+HGX_OPT_CODED = 10
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (

@@ -35,6 +35,8 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->hasinc) (void)hipFree(g->hasinc);
     if (g->inc_yf) (void)hipFree(g->inc_yf);
+    if (g->fcode) (void)hipFree(g->fcode);
+    if (g->lcode) (void)hipFree(g->lcode);
     if (g->pchunks) (void)hipFree(g->pchunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
@@ -447,6 +449,9 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         g->shard->xmode = (int32_t)value;
     } else if (option == HGX_OPT_QUERY_FLAT) {
         g->q_flat = value != 0;
+    } else if (option == HGX_OPT_CODED) {
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: coded mode outside 0..2");
+        g->coded = (int32_t)value;
     } else if (option == HGX_OPT_PUSH_BATCH) {
         if (value < 0 || value > 64) fail(HGX_E_INVALID, "hgx_set_option: push batch outside 0..64");
         g->push_batch = (int32_t)value;

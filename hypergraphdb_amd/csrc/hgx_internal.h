@@ -221,6 +221,9 @@ struct hgx_graph {
     size_t mapped_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
+    int32_t coded = 0;                          // HGX_OPT_CODED: 0 off (default), 1 auto, 2 always when codes exist
+    unsigned long long* fcode = nullptr;        // [A] codes of a push level's new rows (coded next level)
+    unsigned long long* lcode = nullptr;        // [M] codes of a coded level's link rows
     int32_t push_batch = 0;                     // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
     bool q_flat = true;                         // HGX_OPT_QUERY_FLAT: a lane per candidate over the batch's flat candidate space
     bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels

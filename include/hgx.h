@@ -369,6 +369,10 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * wavefront per 64 candidates and a lane per candidate whatever query it belongs to; 0 = a
  * wavefront per chunk of one query's candidates (A/B). */
 #define HGX_OPT_QUERY_FLAT 9
+/* HGX_OPT_CODED (symmetric mode; default 1): a dense level right after a push level whose new rows
+ * carry <= 3 source bits on average moves rows of <= 6 bits as 64-bit codes (six 10-bit source ids)
+ * instead of 128-byte rows; 2 = whenever the push level wrote codes (tests), 0 = off. */
+#define HGX_OPT_CODED 10
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
  * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */
