@@ -357,6 +357,10 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->inc_yf = nullptr;
     if (g->pchunks) (void)hipFree(g->pchunks);
     g->pchunks = nullptr;
+    if (g->fcode) (void)hipFree(g->fcode);   // coded-level scratch, sized by the old A / M
+    g->fcode = nullptr;
+    if (g->lcode) (void)hipFree(g->lcode);
+    g->lcode = nullptr;
     g->n_pchunks = -1;
     g->zacc_bytes = 0;
     g->zacc_clean = false;

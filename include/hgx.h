@@ -355,9 +355,10 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * so a typed candidate is one streamed record instead of two dependent random rows.  0 = read the
  * target rows through tgt_off (A/B; also what a snapshot too large for the extra bytes gets). */
 #define HGX_OPT_QUERY_INLINE 6
-/* HGX_OPT_PUSH_BATCH (default 0, 0..64): K > 0 = frontier-push levels give each wavefront K frontier
- * atoms at once and spread their incidence entries over its lanes (A/B: config 5 measured 1.79 / 2.53
- * ms per direction at K = 16 against 1.74 / 2.08 with one wavefront per atom, the default 0). */
+/* HGX_OPT_PUSH_BATCH (default 0, 0..64; K above 16 runs as 16): K > 0 = frontier-push levels give
+ * each wavefront K frontier atoms at once and spread their incidence entries over its lanes (A/B:
+ * config 5 measured 1.65-1.67 / 2.15-2.48 ms per direction for K = 4-16 against 1.71 / 2.05 with one
+ * wavefront per atom, the default 0; profiles/r02zg_c5_push_ab.jsonl). */
 #define HGX_OPT_PUSH_BATCH 7
 /* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value):
  * 1 = compressed records (default); 2 = static slots (every ghost's whole row to a fixed slot of its
