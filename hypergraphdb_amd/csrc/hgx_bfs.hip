@@ -2408,8 +2408,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
     if (fcode) wave_add_sh(ctr + cNewBits, n_bits);
-    if (lcount) {
-        __syncthreads();
+    if (lcount && __syncthreads_or(n_new != 0)) {   // blocks that found no new atom skip the flush
         for (int j = threadIdx.x; j < W * 64; j += blockDim.x)
             if (lc[j]) atomicAdd(lcount + j, (u64)lc[j]);
     }
