@@ -4741,6 +4741,33 @@ void hgx::pbfs_run(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_
     for (int32_t i = 0; i < n_seeds; ++i)
         if (seeds[i] < 0 || seeds[i] >= sh.A_global) fail(HGX_E_INVALID, "hgx_pbfs_batch: seed out of range");
     if (max_depth < -1) fail(HGX_E_INVALID, "hgx_pbfs_batch: bad max_depth");
+    // The call is collective: every part must run the same exchange format (each mode issues a
+    // different sequence of collectives) on the same seeds, depth and generator.  One all-gather
+    // before any exchange; every part sees the same table, so a mismatch fails on all of them.
+    {
+        hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
+        uint64_t h = 1469598103934665603ull;   // FNV-1a over seeds + depth + generator flags
+        auto mix = [&](uint64_t v) {
+            for (int b = 0; b < 8; ++b) h = (h ^ ((v >> (8 * b)) & 0xff)) * 1099511628211ull;
+        };
+        for (int32_t i = 0; i < n_seeds; ++i) mix((uint32_t)seeds[i]);
+        mix((uint32_t)max_depth);
+        mix((uint32_t)o.link_type);
+        mix(o.return_preceding | o.return_succeeding << 1 | o.reverse_order << 2 | o.return_source << 3);
+        const int NP = sh.n_parts;
+        int64_t mine[3] = {sh.xmode, n_seeds, (int64_t)h};
+        std::vector<int64_t> all(3 * (size_t)NP);
+        HGX_HIP(hipSetDevice(g->device));
+        tr->allgather_i64(mine, 3, all.data(), g->stream);
+        for (int q = 0; q < NP; ++q) {
+            if (all[3 * (size_t)q] != mine[0])
+                fail(HGX_E_INVALID, "hgx_pbfs_batch: HGX_OPT_PART_EXCHANGE differs between the parts of the group (part " +
+                                        std::to_string(q) + ")");
+            if (all[3 * (size_t)q + 1] != mine[1] || all[3 * (size_t)q + 2] != mine[2])
+                fail(HGX_E_INVALID, "hgx_pbfs_batch: the parts were called with different seeds, depth or generator (part " +
+                                        std::to_string(q) + ")");
+        }
+    }
     bfs_batch_impl(g, tr, seeds, n_seeds, max_depth, opts, out);
 }
 

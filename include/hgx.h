@@ -356,11 +356,14 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * target rows through tgt_off (A/B; also what a snapshot too large for the extra bytes gets). */
 #define HGX_OPT_QUERY_INLINE 6
 /* HGX_OPT_PUSH_BATCH (default 0, 0..64; K above 16 runs as 16): K > 0 = frontier-push levels give
- * each wavefront K frontier atoms at once and spread their incidence entries over its lanes (A/B:
- * config 5 measured 1.65-1.67 / 2.15-2.48 ms per direction for K = 4-16 against 1.71 / 2.05 with one
- * wavefront per atom, the default 0; profiles/r02zg_c5_push_ab.jsonl). */
+ * each wavefront K frontier atoms at once and spread their incidence entries over its lanes (A/B,
+ * config 5 wall ms per direction subsumed / subsumes, profiles/r02zg_c5_push_ab.jsonl: K = 4, 8, 16
+ * 1.68 / 2.15, 1.65 / 2.17, 1.67 / 2.48 against 1.71 / 2.05 with one wavefront per atom -- 2-4%
+ * faster on subsumed, 5-21% slower on subsumes, slower on the sum; the default stays 0). */
 #define HGX_OPT_PUSH_BATCH 7
-/* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value):
+/* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value -- the
+ * partitioned BFS checks it collectively before any exchange and fails with HGX_E_INVALID on every
+ * part when they differ):
  * 1 = compressed records (default); 2 = static slots (every ghost's whole row to a fixed slot of its
  * owner, the owner's final row back); 0 = per level, the format a sampled density estimate says moves
  * fewer bytes.  A/B on full config 4 at 8 parts: 34.0 / 42.8 / 35.5 ms per part a step
@@ -370,9 +373,10 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * wavefront per 64 candidates and a lane per candidate whatever query it belongs to; 0 = a
  * wavefront per chunk of one query's candidates (A/B). */
 #define HGX_OPT_QUERY_FLAT 9
-/* HGX_OPT_CODED (symmetric mode; default 1): a dense level right after a push level whose new rows
- * carry <= 3 source bits on average moves rows of <= 6 bits as 64-bit codes (six 10-bit source ids)
- * instead of 128-byte rows; 2 = whenever the push level wrote codes (tests), 0 = off. */
+/* HGX_OPT_CODED (symmetric mode; default 0 = off, A/B): 1 = a dense level right after a push level
+ * whose new rows carry <= 3 source bits on average moves rows of <= 6 bits as 64-bit codes (six 10-bit
+ * source ids) instead of 128-byte rows; 2 = whenever the push level wrote codes (tests).  Exact, but
+ * measured slower on config 2's level 1 (16.0 vs 9.0 ms, profiles/r02zn_*_c2_levels.log). */
 #define HGX_OPT_CODED 10
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and

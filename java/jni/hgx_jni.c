@@ -2,7 +2,11 @@
  * hgx_jni.c -- JNI shim between org.hypergraphdb.gpu.Hgx (java/org/hypergraphdb/gpu/Hgx.java) and
  * the C ABI of libhgx.so (include/hgx.h).  Arrays in, handles (jlong) out; a nonzero status becomes
  * an exception: HGX_E_UNSUPPORTED -> java.lang.UnsupportedOperationException (the Java caller keeps
- * the reference class), anything else -> org.hypergraphdb.HGException with hgx_last_error().
+ * the reference class), HGX_E_NOMEM -> OutOfMemoryError, anything else -> org.hypergraphdb.HGException
+ * with hgx_last_error().  Arguments the shim itself rejects (inconsistent array lengths, offset tables
+ * that would reach past their data array) throw java.lang.IllegalArgumentException with the shim's own
+ * message, before the engine is called: the C ABI cannot see Java array lengths and would read past
+ * the pinned array.  A result too large for one Java array throws UnsupportedOperationException.
  * Primitive arrays are pinned with Get<T>ArrayElements and released with JNI_ABORT (the ABI
  * deep-copies every input); no pointer into the JVM heap outlives a call, and nothing calls back
  * into the JVM (ownership).
@@ -11,11 +15,13 @@
  *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
  *       java/jni/hgx_jni.c -Lhypergraphdb_amd -lhgx -Wl,-rpath,'$ORIGIN' -o libhgx_jni.so
  *
- * UNVERIFIED on a JVM: no JDK exists in this build image.  The C is
- * type-checked here against a minimal JNI declaration set (tests/test_abi.py::test_jni_shim_compiles),
- * never linked against a JVM or run.
+ * No JDK exists in this build image.  The shim is executed instead through a
+ * test JNIEnv (tests/native/fake_jni.c: arrays as heap objects, copy-mode pinning, exceptions
+ * recorded, JNI-call discipline checked) -- tests/test_jni.py drives every native on the CPU and
+ * tests/test_gpu_jni.py on the GPU against the oracle.
  */
 #include <jni.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -23,35 +29,49 @@
 
 #define JFN(name) JNICALL Java_org_hypergraphdb_gpu_Hgx_##name
 
-static void throw_rc(JNIEnv *e, int rc) {
-    const char *cls = rc == HGX_E_UNSUPPORTED ? "java/lang/UnsupportedOperationException"
-                    : rc == HGX_E_NOMEM       ? "java/lang/OutOfMemoryError"
-                                              : "org/hypergraphdb/HGException";
-    jclass c = (*e)->FindClass(e, cls);
-    if (c) (*e)->ThrowNew(e, c, hgx_last_error());
-}
+/* the largest element count of one Java array (VMs reserve a few header words below INT_MAX) */
+#define HGX_JARRAY_MAX ((int64_t)0x7fffffff - 8)
 
-static void throw_msg(JNIEnv *e, const char *msg) {
-    jclass c = (*e)->FindClass(e, "java/lang/IllegalArgumentException");
+static void throw_class(JNIEnv *e, const char *cls, const char *msg) {
+    jclass c = (*e)->FindClass(e, cls);
     if (c) (*e)->ThrowNew(e, c, msg);
 }
 
-/* Pinned views of Java arrays (NULL array -> NULL pointer, length 0). */
+static void throw_rc(JNIEnv *e, int rc) {
+    throw_class(e, rc == HGX_E_UNSUPPORTED ? "java/lang/UnsupportedOperationException"
+                   : rc == HGX_E_NOMEM     ? "java/lang/OutOfMemoryError"
+                                           : "org/hypergraphdb/HGException",
+                hgx_last_error());
+}
+
+static void throw_msg(JNIEnv *e, const char *msg) { throw_class(e, "java/lang/IllegalArgumentException", msg); }
+
+/* A result of n elements must fit one Java array. */
+static int fits_jarray(JNIEnv *e, int64_t n, const char *what) {
+    if (n >= 0 && n <= HGX_JARRAY_MAX) return 1;
+    char m[160];
+    snprintf(m, sizeof m, "%s: %lld elements do not fit one Java array", what, (long long)n);
+    throw_class(e, "java/lang/UnsupportedOperationException", m);
+    return 0;
+}
+
+/* Pinned views of Java arrays (NULL array -> NULL pointer, length 0).  A pin after a failed one
+ * (OutOfMemoryError pending) is skipped: no JNI call but Release* may run with an exception pending. */
 typedef struct { jarray a; void *p; jsize n; int kind; } pin_t;   /* kind: 0 int, 1 long, 2 byte */
 
 static pin_t pin_int(JNIEnv *e, jintArray a) {
     pin_t r = {a, NULL, 0, 0};
-    if (a) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetIntArrayElements(e, a, NULL); }
+    if (a && !(*e)->ExceptionCheck(e)) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetIntArrayElements(e, a, NULL); }
     return r;
 }
 static pin_t pin_long(JNIEnv *e, jlongArray a) {
     pin_t r = {a, NULL, 0, 1};
-    if (a) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetLongArrayElements(e, a, NULL); }
+    if (a && !(*e)->ExceptionCheck(e)) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetLongArrayElements(e, a, NULL); }
     return r;
 }
 static pin_t pin_byte(JNIEnv *e, jbyteArray a) {
     pin_t r = {a, NULL, 0, 2};
-    if (a) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetByteArrayElements(e, a, NULL); }
+    if (a && !(*e)->ExceptionCheck(e)) { r.n = (*e)->GetArrayLength(e, a); r.p = (*e)->GetByteArrayElements(e, a, NULL); }
     return r;
 }
 static void unpin(JNIEnv *e, pin_t *x) {
@@ -61,15 +81,68 @@ static void unpin(JNIEnv *e, pin_t *x) {
     else (*e)->ReleaseByteArrayElements(e, (jbyteArray)x->a, (jbyte *)x->p, JNI_ABORT);
     x->p = NULL;
 }
+/* a pin of a non-null array whose elements could not be obtained (the VM has thrown OutOfMemoryError) */
+static int pin_failed(const pin_t *x) { return x->a && !x->p; }
 
-static jintArray new_ints(JNIEnv *e, const int32_t *v, jsize n) {
-    jintArray a = (*e)->NewIntArray(e, n);
-    if (a && n) (*e)->SetIntArrayRegion(e, a, 0, n, (const jint *)v);
+/* ---- argument checks (each throws IllegalArgumentException and returns 0 on failure) ----------- */
+
+static int check_len(JNIEnv *e, const pin_t *x, int64_t want, const char *name) {
+    if (pin_failed(x)) return 0;   /* OutOfMemoryError already pending */
+    if ((int64_t)x->n == want) return 1;
+    char m[200];
+    snprintf(m, sizeof m, "%s: length %lld, expected %lld", name, (long long)x->n, (long long)want);
+    throw_msg(e, m);
+    return 0;
+}
+
+/* An offsets table of n1 entries into a data array of data_len elements (stride elements per offset
+ * unit): off[0] = 0, never decreasing, off[n1-1] * stride <= data_len.  Every slice the engine reads
+ * then lies inside the pinned data array. */
+static int check_offsets(JNIEnv *e, const pin_t *off, int64_t n1, int64_t data_len, int64_t stride,
+                         const char *name) {
+    if (!check_len(e, off, n1, name)) return 0;
+    const int64_t *o = (const int64_t *)off->p;
+    char m[200];
+    if (n1 == 0) return 1;
+    if (!o) { snprintf(m, sizeof m, "%s: null", name); throw_msg(e, m); return 0; }
+    if (o[0] != 0) {
+        snprintf(m, sizeof m, "%s[0] = %lld, expected 0", name, (long long)o[0]);
+        throw_msg(e, m);
+        return 0;
+    }
+    for (int64_t i = 1; i < n1; i++)
+        if (o[i] < o[i - 1]) {
+            snprintf(m, sizeof m, "%s decreases at index %lld", name, (long long)i);
+            throw_msg(e, m);
+            return 0;
+        }
+    if (o[n1 - 1] > data_len / stride) {
+        snprintf(m, sizeof m, "%s ends at %lld, beyond its data array (%lld elements)", name, (long long)o[n1 - 1],
+                 (long long)data_len);
+        throw_msg(e, m);
+        return 0;
+    }
+    return 1;
+}
+
+static int check_not_null(JNIEnv *e, const void *p, const char *name) {
+    if (p) return 1;
+    char m[120];
+    snprintf(m, sizeof m, "%s is null", name);
+    throw_class(e, "java/lang/NullPointerException", m);
+    return 0;
+}
+
+static jintArray new_ints(JNIEnv *e, const int32_t *v, int64_t n) {
+    if (!fits_jarray(e, n, "int[] result")) return NULL;
+    jintArray a = (*e)->NewIntArray(e, (jsize)n);
+    if (a && n) (*e)->SetIntArrayRegion(e, a, 0, (jsize)n, (const jint *)v);
     return a;
 }
-static jlongArray new_longs(JNIEnv *e, const int64_t *v, jsize n) {
-    jlongArray a = (*e)->NewLongArray(e, n);
-    if (a && n) (*e)->SetLongArrayRegion(e, a, 0, n, (const jlong *)v);
+static jlongArray new_longs(JNIEnv *e, const int64_t *v, int64_t n) {
+    if (!fits_jarray(e, n, "long[] result")) return NULL;
+    jlongArray a = (*e)->NewLongArray(e, (jsize)n);
+    if (a && n) (*e)->SetLongArrayRegion(e, a, 0, (jsize)n, (const jlong *)v);
     return a;
 }
 
@@ -84,25 +157,34 @@ static hgx_graph_desc desc_of(jlong numAtoms, pin_t *la, pin_t *off, pin_t *tg, 
     return d;
 }
 
+/* The snapshot rows of hgx_graph_desc: tgtOff has M+1 entries ending within tgtIdx, linkType is null
+ * or has M entries. */
+static int check_rows(JNIEnv *e, const pin_t *la, const pin_t *off, const pin_t *tg, const pin_t *ty) {
+    if (pin_failed(la) || pin_failed(tg)) return 0;
+    return check_offsets(e, off, (int64_t)la->n + 1, tg->n, 1, "tgtOff") &&
+           (!ty->a || check_len(e, ty, la->n, "linkType"));
+}
+
 /* ---- snapshot ------------------------------------------------------------------------------ */
 
 JNIEXPORT jlong JFN(graphCreate)(JNIEnv *e, jclass k, jlong numAtoms, jintArray linkAtom, jlongArray tgtOff,
                                  jintArray tgtIdx, jintArray linkType, jint device) {
     pin_t la = pin_int(e, linkAtom), off = pin_long(e, tgtOff), tg = pin_int(e, tgtIdx), ty = pin_int(e, linkType);
     hgx_graph *g = NULL;
-    int rc;
-    if (off.n != la.n + 1 || (ty.a && ty.n != la.n)) rc = HGX_E_INVALID;
-    else {
+    int ok = check_rows(e, &la, &off, &tg, &ty), rc = HGX_OK;
+    if (ok) {
         hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
         rc = hgx_graph_create(&d, device, &g);
     }
     unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty);
-    if (rc) { throw_rc(e, rc); return 0; }
-    return (jlong)(intptr_t)g;
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)g : 0;
 }
 
 JNIEXPORT jlong JFN(graphOpen)(JNIEnv *e, jclass k, jstring path, jint device) {
+    if (!check_not_null(e, path, "path")) return 0;
     const char *p = (*e)->GetStringUTFChars(e, path, NULL);
+    if (!p) return 0;
     hgx_graph *g = NULL;
     int rc = hgx_graph_open(p, device, &g);
     (*e)->ReleaseStringUTFChars(e, path, p);
@@ -124,21 +206,26 @@ JNIEXPORT void JFN(graphUpdate)(JNIEnv *e, jclass k, jlong g, jlong numAtoms, ji
                                 jintArray removeLinkAtom) {
     pin_t la = pin_int(e, addLinkAtom), off = pin_long(e, addTgtOff), tg = pin_int(e, addTgtIdx),
           ty = pin_int(e, addLinkType), rm = pin_int(e, removeLinkAtom);
-    int rc = (la.n && off.n != la.n + 1) ? HGX_E_INVALID
-           : hgx_graph_update((hgx_graph *)(intptr_t)g, numAtoms, la.n, (const int32_t *)la.p, (const int64_t *)off.p,
+    /* no additions: addTgtOff may be null or {0} */
+    int ok = !pin_failed(&rm) && (la.n == 0 && off.n <= 1 ? (off.n == 0 || check_offsets(e, &off, 1, tg.n, 1, "addTgtOff"))
+                                                         : check_rows(e, &la, &off, &tg, &ty));
+    int rc = HGX_OK;
+    if (ok)
+        rc = hgx_graph_update((hgx_graph *)(intptr_t)g, numAtoms, la.n, (const int32_t *)la.p, (const int64_t *)off.p,
                               (const int32_t *)tg.p, (const int32_t *)ty.p, rm.n, (const int32_t *)rm.p);
     unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty); unpin(e, &rm);
-    if (rc) throw_rc(e, rc);
+    if (ok && rc) throw_rc(e, rc);
 }
 
 JNIEXPORT jintArray JFN(incidence)(JNIEnv *e, jclass k, jlong g, jint atom) {
     int64_t n = 0;
     int rc = hgx_graph_incidence((hgx_graph *)(intptr_t)g, atom, NULL, 0, &n);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, n, "incidence")) return NULL;
     int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-    if (!buf) { throw_rc(e, HGX_E_NOMEM); return NULL; }
+    if (!buf) { throw_class(e, "java/lang/OutOfMemoryError", "incidence buffer"); return NULL; }
     rc = hgx_graph_incidence((hgx_graph *)(intptr_t)g, atom, buf, n, &n);
-    jintArray out = rc ? NULL : new_ints(e, buf, (jsize)n);
+    jintArray out = rc ? NULL : new_ints(e, buf, n);
     free(buf);
     if (rc) throw_rc(e, rc);
     return out;
@@ -146,6 +233,7 @@ JNIEXPORT jintArray JFN(incidence)(JNIEnv *e, jclass k, jlong g, jint atom) {
 
 JNIEXPORT jlongArray JFN(degree)(JNIEnv *e, jclass k, jlong g, jintArray atoms) {
     pin_t a = pin_int(e, atoms);
+    if (pin_failed(&a)) return NULL;
     int64_t *deg = (int64_t *)malloc(sizeof(int64_t) * (size_t)(a.n > 0 ? a.n : 1));
     int rc = deg ? hgx_graph_degree((hgx_graph *)(intptr_t)g, (const int32_t *)a.p, a.n, deg) : HGX_E_NOMEM;
     jlongArray out = rc ? NULL : new_longs(e, deg, a.n);
@@ -163,19 +251,32 @@ JNIEXPORT void JFN(setOption)(JNIEnv *e, jclass k, jlong g, jint option, jlong v
 JNIEXPORT void JFN(snapshotWrite)(JNIEnv *e, jclass k, jstring path, jlong numAtoms, jintArray linkAtom,
                                   jlongArray tgtOff, jintArray tgtIdx, jintArray linkType, jbyteArray handles,
                                   jint handleBytes) {
+    if (!check_not_null(e, path, "path")) return;
     pin_t la = pin_int(e, linkAtom), off = pin_long(e, tgtOff), tg = pin_int(e, tgtIdx), ty = pin_int(e, linkType),
           hb = pin_byte(e, handles);
-    const char *p = (*e)->GetStringUTFChars(e, path, NULL);
-    hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
-    int rc = (off.n != la.n + 1) ? HGX_E_INVALID
-           : hgx_snapshot_write(p, &d, (const uint8_t *)hb.p, hb.p ? handleBytes : 0);
-    (*e)->ReleaseStringUTFChars(e, path, p);
+    int ok = check_rows(e, &la, &off, &tg, &ty) && !pin_failed(&hb), rc = HGX_OK;
+    if (ok && hb.a && (handleBytes <= 0 || numAtoms < 0 || (int64_t)hb.n != numAtoms * (int64_t)handleBytes)) {
+        char m[200];
+        snprintf(m, sizeof m, "handles: length %lld, expected numAtoms * handleBytes = %lld", (long long)hb.n,
+                 (long long)numAtoms * (long long)handleBytes);
+        throw_msg(e, m);
+        ok = 0;
+    }
+    const char *p = ok ? (*e)->GetStringUTFChars(e, path, NULL) : NULL;
+    if (ok && !p) ok = 0;
+    if (ok) {
+        hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
+        rc = hgx_snapshot_write(p, &d, (const uint8_t *)hb.p, hb.p ? handleBytes : 0);
+        (*e)->ReleaseStringUTFChars(e, path, p);
+    }
     unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty); unpin(e, &hb);
-    if (rc) throw_rc(e, rc);
+    if (ok && rc) throw_rc(e, rc);
 }
 
 JNIEXPORT jlongArray JFN(snapshotInfo)(JNIEnv *e, jclass k, jstring path) {
+    if (!check_not_null(e, path, "path")) return NULL;
     const char *p = (*e)->GetStringUTFChars(e, path, NULL);
+    if (!p) return NULL;
     int64_t v[5] = {0, 0, 0, 0, 0};
     int32_t hb = 0, ht = 0;
     int rc = hgx_snapshot_info(p, &v[0], &v[1], &v[2], &hb, &ht);
@@ -187,22 +288,30 @@ JNIEXPORT jlongArray JFN(snapshotInfo)(JNIEnv *e, jclass k, jstring path) {
 }
 
 JNIEXPORT jbyteArray JFN(snapshotHandles)(JNIEnv *e, jclass k, jstring path) {
+    if (!check_not_null(e, path, "path")) return NULL;
     const char *p = (*e)->GetStringUTFChars(e, path, NULL);
+    if (!p) return NULL;
     int64_t A = 0;
     int32_t hb = 0;
     int rc = hgx_snapshot_info(p, &A, NULL, NULL, &hb, NULL);
     jbyteArray out = NULL;
+    int thrown = 0;
     if (!rc && hb > 0) {
-        uint8_t *buf = (uint8_t *)malloc((size_t)A * (size_t)hb);
-        rc = buf ? hgx_snapshot_read(p, NULL, NULL, NULL, NULL, buf) : HGX_E_NOMEM;
-        if (!rc) {
-            out = (*e)->NewByteArray(e, (jsize)(A * hb));
-            if (out) (*e)->SetByteArrayRegion(e, out, 0, (jsize)(A * hb), (const jbyte *)buf);
+        const int64_t bytes = A * (int64_t)hb;
+        if (!fits_jarray(e, bytes, "snapshot handle table")) {
+            thrown = 1;
+        } else {
+            uint8_t *buf = (uint8_t *)malloc((size_t)(bytes > 0 ? bytes : 1));
+            rc = buf ? hgx_snapshot_read(p, NULL, NULL, NULL, NULL, buf) : HGX_E_NOMEM;
+            if (!rc) {
+                out = (*e)->NewByteArray(e, (jsize)bytes);
+                if (out && bytes) (*e)->SetByteArrayRegion(e, out, 0, (jsize)bytes, (const jbyte *)buf);
+            }
+            free(buf);
         }
-        free(buf);
     }
     (*e)->ReleaseStringUTFChars(e, path, p);
-    if (rc) throw_rc(e, rc);
+    if (rc && !thrown) throw_rc(e, rc);
     return out;
 }
 
@@ -221,6 +330,7 @@ static hgx_algen_opts opts_of(jint linkType, jboolean p, jboolean s, jboolean r,
 JNIEXPORT jlong JFN(bfsBatch)(JNIEnv *e, jclass k, jlong g, jintArray seeds, jint maxDepth, jint linkType,
                               jboolean p, jboolean s, jboolean r, jboolean src) {
     pin_t sd = pin_int(e, seeds);
+    if (pin_failed(&sd)) return 0;
     hgx_algen_opts o = opts_of(linkType, p, s, r, src);
     hgx_bfs_result *res = NULL;
     int rc = hgx_bfs_batch((hgx_graph *)(intptr_t)g, (const int32_t *)sd.p, sd.n, maxDepth, &o, &res);
@@ -240,9 +350,11 @@ JNIEXPORT jlongArray JFN(bfsCounts)(JNIEnv *e, jclass k, jlong r) {
     int32_t ns = 0, nl = 0;
     int rc = hgx_bfs_result_info((const hgx_bfs_result *)(intptr_t)r, &ns, &nl);
     if (rc) { throw_rc(e, rc); return NULL; }
-    int64_t *c = (int64_t *)malloc(sizeof(int64_t) * ((size_t)ns * nl + 1));
+    const int64_t n = (int64_t)ns * nl;
+    if (!fits_jarray(e, n, "bfsCounts")) return NULL;
+    int64_t *c = (int64_t *)malloc(sizeof(int64_t) * ((size_t)n + 1));
     rc = c ? hgx_bfs_result_counts((hgx_bfs_result *)(intptr_t)r, c) : HGX_E_NOMEM;
-    jlongArray out = rc ? NULL : new_longs(e, c, ns * nl);
+    jlongArray out = rc ? NULL : new_longs(e, c, n);
     free(c);
     if (rc) throw_rc(e, rc);
     return out;
@@ -253,9 +365,10 @@ JNIEXPORT jintArray JFN(bfsVisited)(JNIEnv *e, jclass k, jlong r, jint seedIndex
     hgx_bfs_result *res = (hgx_bfs_result *)(intptr_t)r;
     int rc = hgx_bfs_result_visited(res, seedIndex, depth, NULL, 0, &n);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, n, "bfsVisited")) return NULL;
     int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     rc = buf ? hgx_bfs_result_visited(res, seedIndex, depth, buf, n, &n) : HGX_E_NOMEM;
-    jintArray out = rc ? NULL : new_ints(e, buf, (jsize)n);
+    jintArray out = rc ? NULL : new_ints(e, buf, n);
     free(buf);
     if (rc) throw_rc(e, rc);
     return out;
@@ -275,6 +388,7 @@ JNIEXPORT void JFN(bfsFree)(JNIEnv *e, jclass k, jlong r) { hgx_bfs_result_free(
 JNIEXPORT jlong JFN(bfsSequence)(JNIEnv *e, jclass k, jlong g, jintArray seeds, jint maxDepth, jint linkType,
                                  jboolean p, jboolean s, jboolean r, jboolean src) {
     pin_t sd = pin_int(e, seeds);
+    if (pin_failed(&sd)) return 0;
     hgx_algen_opts o = opts_of(linkType, p, s, r, src);
     hgx_seq_result *res = NULL;
     int rc = hgx_bfs_sequence((hgx_graph *)(intptr_t)g, (const int32_t *)sd.p, sd.n, maxDepth, &o, &res);
@@ -291,7 +405,7 @@ JNIEXPORT jlongArray JFN(seqOffsets)(JNIEnv *e, jclass k, jlong sq) {
     if (rc) { throw_rc(e, rc); return NULL; }
     int64_t *off = (int64_t *)malloc(sizeof(int64_t) * ((size_t)ns + 1));
     rc = off ? hgx_seq_result_offsets(s, off) : HGX_E_NOMEM;
-    jlongArray out = rc ? NULL : new_longs(e, off, ns + 1);
+    jlongArray out = rc ? NULL : new_longs(e, off, (int64_t)ns + 1);
     free(off);
     if (rc) throw_rc(e, rc);
     return out;
@@ -304,10 +418,11 @@ static jintArray seq_column(JNIEnv *e, jlong sq, int which) {
     int64_t np = 0;
     int rc = hgx_seq_result_info(s, &ns, &np, &nl);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, np, "sequence pairs")) return NULL;
     int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(np > 0 ? np : 1));
-    if (!buf) { throw_rc(e, HGX_E_NOMEM); return NULL; }
+    if (!buf) { throw_class(e, "java/lang/OutOfMemoryError", "sequence buffer"); return NULL; }
     rc = hgx_seq_result_pairs(s, which == 0 ? buf : NULL, which == 1 ? buf : NULL, which == 2 ? buf : NULL);
-    jintArray out = rc ? NULL : new_ints(e, buf, (jsize)np);
+    jintArray out = rc ? NULL : new_ints(e, buf, np);
     free(buf);
     if (rc) throw_rc(e, rc);
     return out;
@@ -320,18 +435,28 @@ JNIEXPORT void JFN(seqFree)(JNIEnv *e, jclass k, jlong s) { hgx_seq_result_free(
 
 /* ---- conjunctive pattern batches ------------------------------------------------------------- */
 
+/* The packed batch: n = type.length queries, incOff / patOff of n+1 entries into inc / pat,
+ * hasOrdered of n entries. */
+static int check_packed(JNIEnv *e, const pin_t *ty, const pin_t *io, const pin_t *ic, const pin_t *ho,
+                        const pin_t *po, const pin_t *pt) {
+    if (pin_failed(ty) || pin_failed(ic) || pin_failed(pt)) return 0;
+    return check_offsets(e, io, (int64_t)ty->n + 1, ic->n, 1, "incOff") && check_len(e, ho, ty->n, "hasOrdered") &&
+           check_offsets(e, po, (int64_t)ty->n + 1, pt->n, 1, "patOff");
+}
+
 JNIEXPORT jlong JFN(patternBatch)(JNIEnv *e, jclass k, jlong g, jintArray type, jlongArray incOff, jintArray inc,
                                   jintArray hasOrdered, jlongArray patOff, jintArray pat) {
     pin_t ty = pin_int(e, type), io = pin_long(e, incOff), ic = pin_int(e, inc), ho = pin_int(e, hasOrdered),
           po = pin_long(e, patOff), pt = pin_int(e, pat);
     hgx_query_result *q = NULL;
-    int rc = (io.n != ty.n + 1 || po.n != ty.n + 1 || ho.n != ty.n) ? HGX_E_INVALID
-           : hgx_pattern_batch_packed((hgx_graph *)(intptr_t)g, ty.n, (const int32_t *)ty.p, (const int64_t *)io.p,
+    int ok = check_packed(e, &ty, &io, &ic, &ho, &po, &pt), rc = HGX_OK;
+    if (ok)
+        rc = hgx_pattern_batch_packed((hgx_graph *)(intptr_t)g, ty.n, (const int32_t *)ty.p, (const int64_t *)io.p,
                                       (const int32_t *)ic.p, (const int32_t *)ho.p, (const int64_t *)po.p,
                                       (const int32_t *)pt.p, &q);
     unpin(e, &ty); unpin(e, &io); unpin(e, &ic); unpin(e, &ho); unpin(e, &po); unpin(e, &pt);
-    if (rc) { throw_rc(e, rc); return 0; }
-    return (jlong)(intptr_t)q;
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)q : 0;
 }
 
 JNIEXPORT jlong JFN(patternBatchExt)(JNIEnv *e, jclass k, jlong g, jlongArray typeOff, jintArray types,
@@ -342,15 +467,27 @@ JNIEXPORT jlong JFN(patternBatchExt)(JNIEnv *e, jclass k, jlong g, jlongArray ty
           pt = pin_int(e, pat), ar = pin_int(e, arity);
     const jsize n = ar.n;
     hgx_query_result *q = NULL;
-    int rc = (to.n != n + 1 || io.n != n + 1 || po.n != n + 1 || so.n != n + 1) ? HGX_E_INVALID
-           : hgx_pattern_batch_ext((hgx_graph *)(intptr_t)g, n, (const int64_t *)to.p, (const int32_t *)ty.p,
+    int rc = HGX_OK;
+    /* psetOff indexes the orderedLink patterns, each of which is a slice of pat through patOff
+     * (psetOff[n] + 1 entries); a positioned record is 4 ints of pos */
+    int ok = !pin_failed(&ar) && !pin_failed(&ty) && !pin_failed(&ic) && !pin_failed(&ps) && !pin_failed(&pt) &&
+             check_offsets(e, &to, (int64_t)n + 1, ty.n, 1, "typeOff") &&
+             check_offsets(e, &io, (int64_t)n + 1, ic.n, 1, "incOff") &&
+             check_offsets(e, &po, (int64_t)n + 1, ps.n, 4, "posOff") &&
+             check_offsets(e, &so, (int64_t)n + 1, pa.n > 0 ? (int64_t)pa.n - 1 : 0, 1, "psetOff");
+    if (ok) {
+        const int64_t nsets = so.n ? ((const int64_t *)so.p)[n] : 0;
+        ok = (nsets == 0 && pa.n == 0) || check_offsets(e, &pa, nsets + 1, pt.n, 1, "patOff");
+    }
+    if (ok)
+        rc = hgx_pattern_batch_ext((hgx_graph *)(intptr_t)g, n, (const int64_t *)to.p, (const int32_t *)ty.p,
                                    (const int64_t *)io.p, (const int32_t *)ic.p, (const int64_t *)po.p,
                                    (const int32_t *)ps.p, (const int64_t *)so.p, (const int64_t *)pa.p,
                                    (const int32_t *)pt.p, (const int32_t *)ar.p, &q);
     unpin(e, &to); unpin(e, &ty); unpin(e, &io); unpin(e, &ic); unpin(e, &po);
     unpin(e, &ps); unpin(e, &so); unpin(e, &pa); unpin(e, &pt); unpin(e, &ar);
-    if (rc) { throw_rc(e, rc); return 0; }
-    return (jlong)(intptr_t)q;
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)q : 0;
 }
 
 JNIEXPORT jlongArray JFN(queryOffsets)(JNIEnv *e, jclass k, jlong qr) {
@@ -358,9 +495,10 @@ JNIEXPORT jlongArray JFN(queryOffsets)(JNIEnv *e, jclass k, jlong qr) {
     int64_t count = 0;
     int rc = hgx_query_result_count(q, &count);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, count + 1, "queryOffsets")) return NULL;
     int64_t *off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(count + 1));
     rc = off ? hgx_query_result_offsets(q, off) : HGX_E_NOMEM;
-    jlongArray out = rc ? NULL : new_longs(e, off, (jsize)(count + 1));
+    jlongArray out = rc ? NULL : new_longs(e, off, count + 1);
     free(off);
     if (rc) throw_rc(e, rc);
     return out;
@@ -377,9 +515,10 @@ JNIEXPORT jintArray JFN(queryIds)(JNIEnv *e, jclass k, jlong qr) {
         free(off);
     }
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, total, "queryIds")) return NULL;
     int32_t *ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)(total > 0 ? total : 1));
     rc = ids ? hgx_query_result_ids(q, ids) : HGX_E_NOMEM;
-    jintArray out = rc ? NULL : new_ints(e, ids, (jsize)total);
+    jintArray out = rc ? NULL : new_ints(e, ids, total);
     free(ids);
     if (rc) throw_rc(e, rc);
     return out;
@@ -392,13 +531,18 @@ JNIEXPORT void JFN(queryFree)(JNIEnv *e, jclass k, jlong q) { hgx_query_result_f
 JNIEXPORT jintArray JFN(partitionPlan)(JNIEnv *e, jclass k, jlong numAtoms, jintArray linkAtom, jlongArray tgtOff,
                                        jintArray tgtIdx, jintArray linkType, jint nParts) {
     pin_t la = pin_int(e, linkAtom), off = pin_long(e, tgtOff), tg = pin_int(e, tgtIdx), ty = pin_int(e, linkType);
-    int32_t *plan = (int32_t *)malloc(sizeof(int32_t) * (size_t)(la.n > 0 ? la.n : 1));
-    hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
-    int rc = !plan ? HGX_E_NOMEM : (off.n != la.n + 1) ? HGX_E_INVALID : hgx_partition_plan(&d, nParts, plan);
-    jintArray out = rc ? NULL : new_ints(e, plan, la.n);
+    int ok = check_rows(e, &la, &off, &tg, &ty), rc = HGX_OK;
+    int32_t *plan = NULL;
+    jintArray out = NULL;
+    if (ok) {
+        plan = (int32_t *)malloc(sizeof(int32_t) * (size_t)(la.n > 0 ? la.n : 1));
+        hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
+        rc = !plan ? HGX_E_NOMEM : hgx_partition_plan(&d, nParts, plan);
+        if (!rc) out = new_ints(e, plan, la.n);
+    }
     unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty);
     free(plan);
-    if (rc) throw_rc(e, rc);
+    if (ok && rc) throw_rc(e, rc);
     return out;
 }
 
@@ -406,13 +550,15 @@ JNIEXPORT jlong JFN(shardBuild)(JNIEnv *e, jclass k, jlong numAtoms, jintArray l
                                 jintArray tgtIdx, jintArray linkType, jint nParts, jint part, jintArray plan) {
     pin_t la = pin_int(e, linkAtom), off = pin_long(e, tgtOff), tg = pin_int(e, tgtIdx), ty = pin_int(e, linkType),
           pl = pin_int(e, plan);
-    hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
     hgx_shard *s = NULL;
-    int rc = (off.n != la.n + 1 || pl.n != la.n) ? HGX_E_INVALID
-           : hgx_shard_build(&d, nParts, part, (const int32_t *)pl.p, &s);
+    int ok = check_rows(e, &la, &off, &tg, &ty) && check_len(e, &pl, la.n, "plan"), rc = HGX_OK;
+    if (ok) {
+        hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
+        rc = hgx_shard_build(&d, nParts, part, (const int32_t *)pl.p, &s);
+    }
     unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty); unpin(e, &pl);
-    if (rc) { throw_rc(e, rc); return 0; }
-    return (jlong)(intptr_t)s;
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)s : 0;
 }
 
 JNIEXPORT void JFN(shardFree)(JNIEnv *e, jclass k, jlong s) { hgx_shard_free((hgx_shard *)(intptr_t)s); }
@@ -448,6 +594,7 @@ JNIEXPORT void JFN(commDestroy)(JNIEnv *e, jclass k, jlong c) { hgx_comm_destroy
 JNIEXPORT jlong JFN(pbfsBatch)(JNIEnv *e, jclass k, jlong shard, jlong comm, jintArray seeds, jint maxDepth,
                                jint linkType, jboolean p, jboolean s, jboolean r, jboolean src) {
     pin_t sd = pin_int(e, seeds);
+    if (pin_failed(&sd)) return 0;
     hgx_algen_opts o = opts_of(linkType, p, s, r, src);
     hgx_bfs_result *res = NULL;
     int rc = hgx_pbfs_batch((hgx_graph *)(intptr_t)shard, (hgx_comm *)(intptr_t)comm, (const int32_t *)sd.p, sd.n,
@@ -469,9 +616,10 @@ JNIEXPORT jintArray JFN(shardLocalAtoms)(JNIEnv *e, jclass k, jlong sh) {
     int64_t nl = 0;
     int rc = hgx_shard_info(s, &nl, NULL, NULL, NULL);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, nl, "shardLocalAtoms")) return NULL;
     int32_t *l2g = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nl > 0 ? nl : 1));
     rc = l2g ? hgx_shard_export(s, l2g, NULL, NULL, NULL, NULL, NULL) : HGX_E_NOMEM;
-    jintArray out = rc ? NULL : new_ints(e, l2g, (jsize)nl);
+    jintArray out = rc ? NULL : new_ints(e, l2g, nl);
     free(l2g);
     if (rc) throw_rc(e, rc);
     return out;
@@ -482,9 +630,10 @@ JNIEXPORT jintArray JFN(shardOwners)(JNIEnv *e, jclass k, jlong sh) {
     int64_t nl = 0;
     int rc = hgx_shard_info(s, &nl, NULL, NULL, NULL);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, nl, "shardOwners")) return NULL;
     int32_t *xo = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nl > 0 ? nl : 1));
     rc = xo ? hgx_shard_exchange_tables(s, xo, NULL, NULL, NULL, NULL, NULL) : HGX_E_NOMEM;
-    jintArray out = rc ? NULL : new_ints(e, xo, (jsize)nl);
+    jintArray out = rc ? NULL : new_ints(e, xo, nl);
     free(xo);
     if (rc) throw_rc(e, rc);
     return out;
@@ -495,28 +644,35 @@ JNIEXPORT jlongArray JFN(pbfsBatchGroup)(JNIEnv *e, jclass k, jlongArray shards,
     pin_t sh = pin_long(e, shards), sd = pin_int(e, seeds);
     hgx_algen_opts o = opts_of(linkType, p, s, r, src);
     const jsize np = sh.n;
-    hgx_graph **gs = (hgx_graph **)malloc(sizeof(hgx_graph *) * (size_t)(np > 0 ? np : 1));
-    hgx_bfs_result **outs = (hgx_bfs_result **)calloc((size_t)(np > 0 ? np : 1), sizeof(hgx_bfs_result *));
-    int rc = (!gs || !outs) ? HGX_E_NOMEM : HGX_OK;
-    for (jsize i = 0; !rc && i < np; i++) gs[i] = (hgx_graph *)(intptr_t)((const jlong *)sh.p)[i];
-    if (!rc) rc = hgx_pbfs_batch_group(gs, np, (const int32_t *)sd.p, sd.n, maxDepth, &o, outs);
+    int ok = !pin_failed(&sh) && !pin_failed(&sd) && check_not_null(e, sh.a, "shards");
+    hgx_graph **gs = NULL;
+    hgx_bfs_result **outs = NULL;
+    int rc = HGX_OK;
     jlongArray out = NULL;
-    if (!rc) {
-        int64_t *h = (int64_t *)malloc(sizeof(int64_t) * (size_t)(np > 0 ? np : 1));
-        if (h) {
-            for (jsize i = 0; i < np; i++) h[i] = (int64_t)(intptr_t)outs[i];
-            out = new_longs(e, h, np);
-            free(h);
-        } else {
-            for (jsize i = 0; i < np; i++) hgx_bfs_result_free(outs[i]);
-            rc = HGX_E_NOMEM;
+    if (ok) {
+        gs = (hgx_graph **)malloc(sizeof(hgx_graph *) * (size_t)(np > 0 ? np : 1));
+        outs = (hgx_bfs_result **)calloc((size_t)(np > 0 ? np : 1), sizeof(hgx_bfs_result *));
+        rc = (!gs || !outs) ? HGX_E_NOMEM : HGX_OK;
+        for (jsize i = 0; !rc && i < np; i++) gs[i] = (hgx_graph *)(intptr_t)((const jlong *)sh.p)[i];
+        if (!rc) rc = hgx_pbfs_batch_group(gs, np, (const int32_t *)sd.p, sd.n, maxDepth, &o, outs);
+        if (!rc) {
+            int64_t *h = (int64_t *)malloc(sizeof(int64_t) * (size_t)(np > 0 ? np : 1));
+            if (h) {
+                for (jsize i = 0; i < np; i++) h[i] = (int64_t)(intptr_t)outs[i];
+                out = new_longs(e, h, np);
+                free(h);
+            }
+            if (!out) {   /* the results cannot reach Java: free them (OutOfMemoryError pending or NOMEM) */
+                for (jsize i = 0; i < np; i++) hgx_bfs_result_free(outs[i]);
+                if (!h) rc = HGX_E_NOMEM;
+            }
         }
     }
     unpin(e, &sh);
     unpin(e, &sd);
     free(gs);
     free(outs);
-    if (rc) throw_rc(e, rc);
+    if (ok && rc) throw_rc(e, rc);
     return out;
 }
 
@@ -564,9 +720,10 @@ static jintArray export_ints(JNIEnv *e, jlong gh, int which) {
     int64_t n = rc ? 0 : (which == 0 ? M : off[M]);
     free(off);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, n, which == 0 ? "graphExportLinks" : "graphExportTargets")) return NULL;
     int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     rc = buf ? hgx_graph_export(g, which == 0 ? buf : NULL, NULL, which == 1 ? buf : NULL, NULL) : HGX_E_NOMEM;
-    jintArray out = rc ? NULL : new_ints(e, buf, (jsize)n);
+    jintArray out = rc ? NULL : new_ints(e, buf, n);
     free(buf);
     if (rc) throw_rc(e, rc);
     return out;
@@ -580,9 +737,10 @@ JNIEXPORT jlongArray JFN(graphExportOffsets)(JNIEnv *e, jclass k, jlong gh) {
     int64_t A = 0, M = 0, I = 0;
     int rc = hgx_graph_info(g, &A, &M, &I);
     if (rc) { throw_rc(e, rc); return NULL; }
+    if (!fits_jarray(e, M + 1, "graphExportOffsets")) return NULL;
     int64_t *off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(M + 1));
     rc = off ? hgx_graph_export(g, NULL, off, NULL, NULL) : HGX_E_NOMEM;
-    jlongArray out = rc ? NULL : new_longs(e, off, (jsize)(M + 1));
+    jlongArray out = rc ? NULL : new_longs(e, off, M + 1);
     free(off);
     if (rc) throw_rc(e, rc);
     return out;
@@ -593,23 +751,27 @@ JNIEXPORT jlong JFN(patternBatchStructs)(JNIEnv *e, jclass k, jlong g, jintArray
     pin_t ty = pin_int(e, type), io = pin_long(e, incOff), ic = pin_int(e, inc), ho = pin_int(e, hasOrdered),
           po = pin_long(e, patOff), pt = pin_int(e, pat);
     const jsize n = ty.n;
-    hgx_and_query *qs = (hgx_and_query *)malloc(sizeof(hgx_and_query) * (size_t)(n > 0 ? n : 1));
     hgx_query_result *q = NULL;
-    int rc = !qs ? HGX_E_NOMEM : (io.n != n + 1 || po.n != n + 1 || ho.n != n) ? HGX_E_INVALID : HGX_OK;
-    for (jsize i = 0; !rc && i < n; i++) {
-        const int64_t *iof = (const int64_t *)io.p, *pof = (const int64_t *)po.p;
-        qs[i].type = ((const int32_t *)ty.p)[i];
-        qs[i].n_incident = (int32_t)(iof[i + 1] - iof[i]);
-        qs[i].incident = (const int32_t *)ic.p + iof[i];
-        qs[i].has_ordered = ((const int32_t *)ho.p)[i];
-        qs[i].n_pattern = (int32_t)(pof[i + 1] - pof[i]);
-        qs[i].pattern = (const int32_t *)pt.p + pof[i];
+    int ok = check_packed(e, &ty, &io, &ic, &ho, &po, &pt), rc = HGX_OK;
+    hgx_and_query *qs = NULL;
+    if (ok) {   /* the offsets are checked: every slice below lies inside inc / pat */
+        qs = (hgx_and_query *)malloc(sizeof(hgx_and_query) * (size_t)(n > 0 ? n : 1));
+        rc = qs ? HGX_OK : HGX_E_NOMEM;
+        for (jsize i = 0; !rc && i < n; i++) {
+            const int64_t *iof = (const int64_t *)io.p, *pof = (const int64_t *)po.p;
+            qs[i].type = ((const int32_t *)ty.p)[i];
+            qs[i].n_incident = (int32_t)(iof[i + 1] - iof[i]);
+            qs[i].incident = (const int32_t *)ic.p + iof[i];
+            qs[i].has_ordered = ((const int32_t *)ho.p)[i];
+            qs[i].n_pattern = (int32_t)(pof[i + 1] - pof[i]);
+            qs[i].pattern = (const int32_t *)pt.p + pof[i];
+        }
+        if (!rc) rc = hgx_pattern_batch((hgx_graph *)(intptr_t)g, qs, n, &q);
     }
-    if (!rc) rc = hgx_pattern_batch((hgx_graph *)(intptr_t)g, qs, n, &q);
     unpin(e, &ty); unpin(e, &io); unpin(e, &ic); unpin(e, &ho); unpin(e, &po); unpin(e, &pt);
     free(qs);
-    if (rc) { throw_rc(e, rc); return 0; }
-    return (jlong)(intptr_t)q;
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)q : 0;
 }
 
 JNIEXPORT jint JFN(deviceCount)(JNIEnv *e, jclass k) {

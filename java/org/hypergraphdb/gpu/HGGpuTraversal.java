@@ -22,7 +22,6 @@ package org.hypergraphdb.gpu;
 import java.util.ArrayList;
 import java.util.HashSet;
 import java.util.List;
-import java.util.NoSuchElementException;
 import java.util.Set;
 
 import org.hypergraphdb.HGHandle;
@@ -31,13 +30,16 @@ import org.hypergraphdb.algorithms.DefaultALGenerator;
 import org.hypergraphdb.algorithms.HGALGenerator;
 import org.hypergraphdb.algorithms.HGBreadthFirstTraversal;
 import org.hypergraphdb.algorithms.HGTraversal;
+import org.hypergraphdb.HGQuery.hg;
 import org.hypergraphdb.query.AtomTypeCondition;
 import org.hypergraphdb.util.Pair;
+import org.hypergraphdb.util.Ref;
 
 public class HGGpuTraversal implements HGTraversal
 {
     private final HGGpuSnapshot snap;
-    private final HGHandle start;
+    private final Ref<HGHandle> startRef;
+    private HGHandle start;
     private final HGALGenerator gen;
     private final int maxDistance;
     private HGTraversal cpu;              // the reference traversal when the generator is not accelerated
@@ -52,8 +54,24 @@ public class HGGpuTraversal implements HGTraversal
 
     public HGGpuTraversal(HGGpuSnapshot snap, HGHandle start, HGALGenerator gen, int maxDistance)
     {
+        this(snap, hg.constant(start), gen, maxDistance);
+    }
+
+    public HGGpuTraversal(HGGpuSnapshot snap, Ref<HGHandle> start, HGALGenerator gen)
+    {
+        this(snap, start, gen, Integer.MAX_VALUE);
+    }
+
+    /**
+     * The reference resolves the start reference in its constructor (HGBreadthFirstTraversal.java:
+     * 122-128 calls init(), :42-47), i.e. when ToQueryMap's translators build the query; so does this
+     * class.  The GPU call itself is deferred to the first hasNext() / next() / isVisited().
+     */
+    public HGGpuTraversal(HGGpuSnapshot snap, Ref<HGHandle> start, HGALGenerator gen, int maxDistance)
+    {
         this.snap = snap;
-        this.start = start;
+        this.startRef = start;
+        this.start = start.get();
         this.gen = gen;
         this.maxDistance = maxDistance;
         if (options(snap, gen) == null)
@@ -120,11 +138,12 @@ public class HGGpuTraversal implements HGTraversal
         return pos < atoms.length;
     }
 
+    /** The next (link, atom) pair, or null when the traversal is exhausted (HGBreadthFirstTraversal.java:143-156). */
     public Pair<HGHandle, HGHandle> next()
     {
         init();
         if (cpu != null) return cpu.next();
-        if (pos >= atoms.length) throw new NoSuchElementException();
+        if (pos >= atoms.length) return null;
         HGHandle a = snap.handle(atoms[pos]);
         Pair<HGHandle, HGHandle> p = new Pair<HGHandle, HGHandle>(snap.handle(links[pos]), a);
         pos++;
@@ -140,6 +159,52 @@ public class HGGpuTraversal implements HGTraversal
     }
 
     public void remove() { throw new UnsupportedOperationException(); }   // HGBreadthFirstTraversal.java:98-101
+
+    /** Restart from the (re-resolved) start atom (HGBreadthFirstTraversal.java:158-163). */
+    public void reset()
+    {
+        start = startRef.get();
+        links = atoms = null;
+        pos = 0;
+        visited.clear();
+        if (cpu != null)
+            cpu = new HGBreadthFirstTraversal(startRef, gen, maxDistance);
+    }
+
+    /**
+     * The next() atoms of many traversals at once, each in the reference's FIFO order: result[i] =
+     * the atoms HGBreadthFirstTraversal(starts[i], gen, maxDistance) returns (one hgx_bfs_sequence
+     * call for all starts).  Returns null when the generator is not accelerated.
+     */
+    public static HGHandle[][] sequences(HGGpuSnapshot snap, HGHandle[] starts, HGALGenerator gen, int maxDistance)
+    {
+        int[] o = options(snap, gen);
+        if (o == null) return null;
+        snap.sync();
+        int[] seeds = new int[starts.length];
+        for (int i = 0; i < starts.length; i++)
+            seeds[i] = snap.rank(starts[i]);
+        long s = Hgx.bfsSequence(snap.native_(), seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0,
+                                 o[4] != 0);
+        try
+        {
+            long[] off = Hgx.seqOffsets(s);
+            int[] atoms = Hgx.seqAtoms(s);
+            HGHandle[][] out = new HGHandle[starts.length][];
+            for (int i = 0; i < starts.length; i++)
+            {
+                HGHandle[] row = new HGHandle[(int)(off[i + 1] - off[i])];
+                for (int k = 0; k < row.length; k++)
+                    row[k] = snap.handle(atoms[(int)off[i] + k]);   // FIFO order: no re-sort
+                out[i] = row;
+            }
+            return out;
+        }
+        finally
+        {
+            Hgx.seqFree(s);
+        }
+    }
 
     /**
      * Per-depth visited sets of many traversals at once: result[i][d] = the atoms the traversal

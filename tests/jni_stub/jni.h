@@ -39,5 +39,6 @@ struct JNINativeInterface_ {
     const char *(*GetStringUTFChars)(JNIEnv *, jstring, jboolean *);
     void (*ReleaseStringUTFChars)(JNIEnv *, jstring, const char *);
     jstring (*NewStringUTF)(JNIEnv *, const char *);
+    jboolean (*ExceptionCheck)(JNIEnv *);
 };
 #endif
