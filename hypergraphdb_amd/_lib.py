@@ -33,6 +33,7 @@ HGX_OPT_PUSH_BATCH = 7
 HGX_OPT_PART_EXCHANGE = 8
 HGX_OPT_QUERY_FLAT = 9
 HGX_OPT_CODED = 10
+HGX_OPT_QUERY_COALESCE = 11
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
@@ -46,7 +47,7 @@ EXPORTED = (
     "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
     "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
-    "hgx_graph_update",
+    "hgx_graph_update", "hgx_query_coalesce_stats",
 )
 
 
@@ -177,6 +178,7 @@ def lib():
         "hgx_graph_open": ([C.c_char_p, i32, C.POINTER(vp)], C.c_int),
         "hgx_graph_export": ([vp, vp, vp, vp, vp], C.c_int),
         "hgx_graph_update": ([vp, i64, i64, vp, vp, vp, vp, i64, vp], C.c_int),
+        "hgx_query_coalesce_stats": ([vp, C.POINTER(i64), C.POINTER(i64)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

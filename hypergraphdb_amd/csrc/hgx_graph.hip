@@ -41,6 +41,7 @@ void graph_release(hgx_graph* g) {
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
     if (g->mapped) (void)hipHostFree(g->mapped);
+    if (g->zc_in) (void)hipHostFree(g->zc_in);
     if (g->stream2) (void)hipStreamSynchronize(g->stream2);
     if (g->ev_count) (void)hipEventDestroy(g->ev_count);
     if (g->stream2) (void)hipStreamDestroy(g->stream2);
@@ -219,6 +220,19 @@ void* hgx_graph::mapped_buf(size_t bytes) {
         mapped_bytes = n;
     }
     return mapped;
+}
+
+void* hgx_graph::zc_in_buf(size_t bytes) {
+    if (bytes > zc_in_bytes) {
+        if (zc_in) (void)hipHostFree(zc_in);
+        zc_in = zc_in_dev = nullptr;
+        zc_in_bytes = 0;
+        const size_t n = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+        HGX_HIP(hipHostMalloc(&zc_in, n, hipHostMallocMapped | hipHostMallocCoherent));
+        zc_in_bytes = n;
+        HGX_HIP(hipHostGetDevicePointer(&zc_in_dev, zc_in, 0));
+    }
+    return zc_in;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -448,7 +462,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: exchange mode outside 0..2");
         g->shard->xmode = (int32_t)value;
     } else if (option == HGX_OPT_QUERY_FLAT) {
-        g->q_flat = value != 0;
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: query flat mode outside 0..2");
+        g->q_flat = (int32_t)value;
     } else if (option == HGX_OPT_CODED) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: coded mode outside 0..2");
         g->coded = (int32_t)value;
@@ -458,6 +473,10 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;
+    } else if (option == HGX_OPT_QUERY_COALESCE) {
+        if (value < 0 || value > (1 << 24)) fail(HGX_E_INVALID, "hgx_set_option: coalesce cap outside 0..2^24");
+        g->q_coalesce = value != 0;
+        if (value > 1) g->q_coalesce_max = value;
     } else fail(HGX_E_INVALID, "hgx_set_option: unknown option");
     HGX_API_END
 }

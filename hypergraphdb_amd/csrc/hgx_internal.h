@@ -15,7 +15,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -151,6 +153,33 @@ struct Transport {
     virtual const char* kind() const = 0;
 };
 
+// Cross-thread coalescing of pattern batches (hgx_pattern_batch_packed, HGX_OPT_QUERY_COALESCE):
+// a caller that finds the graph's device busy queues its batch; whoever runs next takes every queued
+// batch (FIFO, up to a query cap) and runs them as ONE device batch, then splits the result.  The
+// reference's usage is many threads each executing small compiled queries
+// (TC/query/QueryCompilation.java:76-122); one device batch per caller would serialise them on the
+// per-graph mutex at the full fixed cost of a batch each.
+struct PackedReq {
+    int32_t n = 0;
+    const int32_t* type = nullptr;
+    const int64_t* inc_off = nullptr;
+    const int32_t* inc = nullptr;
+    const int32_t* has_ordered = nullptr;
+    const int64_t* pat_off = nullptr;
+    const int32_t* pat = nullptr;
+    hgx_query_result* r = nullptr;   // set when done and rc == HGX_OK
+    int rc = HGX_OK;
+    std::string err;
+    bool done = false;
+};
+struct QueryCombiner {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<PackedReq*> pending;
+    bool busy = false;
+    int64_t batches = 0, requests = 0;   // device batches run / caller batches served (statistics)
+};
+
 }  // namespace hgx
 
 struct hgx_comm {
@@ -219,21 +248,29 @@ struct hgx_graph {
     size_t pinned_bytes = 0;
     void* mapped = nullptr;          // host-mapped result area the pattern kernels write into
     size_t mapped_bytes = 0;
+    void* zc_in = nullptr;           // fine-grained pinned staging the pattern front kernel reads directly
+    void* zc_in_dev = nullptr;       //   (its device address)
+    size_t zc_in_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
     int32_t coded = 0;                          // HGX_OPT_CODED: 0 off (default), 1 auto, 2 always when codes exist
     unsigned long long* fcode = nullptr;        // [A] codes of a push level's new rows (coded next level)
     unsigned long long* lcode = nullptr;        // [M] codes of a coded level's link rows
     int32_t push_batch = 0;                     // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
-    bool q_flat = true;                         // HGX_OPT_QUERY_FLAT: a lane per candidate over the batch's flat candidate space
+    int32_t q_flat = 2;                         // HGX_OPT_QUERY_FLAT: 2 single-pass (front-scan + match with look-back),
+                                                //   1 flat match + separate scan / finish / scatter, 0 per-query chunks
     bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels
     int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
     int64_t q_chunk_guess = 0;                  // fused pattern path: chunk area of the chunked queries
+    int32_t q_coalesce = 1;                     // HGX_OPT_QUERY_COALESCE: concurrent packed batches share device batches
+    int64_t q_coalesce_max = 1 << 16;           //   at most this many queries per coalesced device batch
+    hgx::QueryCombiner qcomb;
 
     void* alloc(size_t bytes);
     void release(void* p, size_t bytes);
     void* pinned_buf(size_t bytes);
     void* mapped_buf(size_t bytes);
+    void* zc_in_buf(size_t bytes);   // host pointer; zc_in_dev is the kernels' view of it
 };
 
 namespace hgx {

@@ -307,14 +307,11 @@ __global__ void __launch_bounds__(256) hgx_q_plan(int32_t n, const QDesc* __rest
 // inc_off[q] + pat_off[q] (room for all of them), its type is type[q], its pattern row q of pat_off,
 // so no scan is needed.  Bad queries are reported through err[0] (invalid) / err[1] (unsupported) as
 // the smallest offending query index; the plan is computed in the same pass.
-__global__ void __launch_bounds__(256) hgx_q_norm_packed(
-    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
+__device__ __forceinline__ QPlan norm_query(
+    int32_t q, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
     const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
     const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
-    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
-    int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand, int32_t* __restrict__ err) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
+    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, int& status) {
     const int32_t tq = type[q];
     const int64_t b = inc_off[q], e = inc_off[q + 1];
     const bool ho = has_ordered[q] != 0;
@@ -360,14 +357,28 @@ __global__ void __launch_bounds__(256) hgx_q_norm_packed(
     if (!bad && na == 0) unsup = true;
     if (na > kMaxAnchors) unsup = true;
     const bool isnop = ho && pe == pb;   // an empty OrderedLinkCondition compiles to HGQuery.NOP
-    if (bad) atomicMin(&err[0], q);
-    else if (unsup) atomicMin(&err[1], q);
+    status = bad ? 1 : unsup ? 2 : 0;   // the caller reports the smallest offending query
     desc[q] = d;
     nop[q] = isnop ? 1 : 0;
     QPlan p{0, 0, 0, 0};
     if (!bad && !unsup && !isnop)
         p = na <= kRegAnchors ? plan_regs(av, (int)na, tq, g_inc_off, ts_type)
                               : plan_query(d, false, anchors, type, g_inc_off, ts_type);
+    return p;
+}
+
+__global__ void __launch_bounds__(256) hgx_q_norm_packed(
+    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
+    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
+    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
+    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
+    int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand, int32_t* __restrict__ err) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    int st = 0;
+    const QPlan p = norm_query(q, A, type, inc_off, inc, has_ordered, pat_off, pat, g_inc_off, ts_type, desc, anchors,
+                               nop, st);
+    if (st) atomicMin(&err[st - 1], q);
     plan[q] = p;
     nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
     ncand[q] = p.n;
@@ -1029,6 +1040,243 @@ __global__ void hgx_q_finish_stat_flat(const int32_t* __restrict__ n_chunks_p, c
         u64 v = 0;
         for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
         ctr_out[threadIdx.x] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-pass flat pipeline (HGX_OPT_QUERY_FLAT = 2, the default): five back-to-back kernels, no
+// single-workgroup pass, no copy engine and no host round trip inside a batch.
+//   hgx_q_norm_sp / hgx_q_plan_sp -- a thread per query: normalise + plan (packed batches, reading the
+//        caller's arrays straight from the pinned staging area and keeping device copies of the
+//        type and pattern columns the match reads) or plan (host-normalised batches); per block of 256
+//        queries the candidate total and the smallest bad / unsupported query;
+//   hgx_q_scan_sp   -- a block of 256 queries sums the candidate totals of the blocks before it (one
+//        load per thread), scans its own queries, writes their candidate offsets and the chunk -> first
+//        query map; the last block checks the workspace and publishes the chunk count and statuses;
+//   hgx_pattern_match_flat -- unchanged (a lane per candidate, per-chunk hit masks);
+//   hgx_q_place     -- a block of 256 chunks sums the hit counts of the chunks before it (redundantly:
+//        at most a few loads per thread), scans its own, and copies each chunk's hits as atom ids
+//        into the mapped result area;
+//   hgx_q_offsets_flat -- every query's result offset from its first chunk's offset and hit mask.
+// Replaces norm + the one-workgroup scan (15 + 20 us on the config-3 batch), the one-workgroup finish
+// + scatter (17 + 4 us) and the two copies (14 + 7 us, plus ~9 us of dispatch gap after each).
+// Tried first: a decoupled look-back (blocks publishing prefixes through device-scope atomics) in
+// the scan and in the match itself: 27 and 58 us -- each look-back step is a device-scope atomic
+// round trip (the XCDs' L2 caches are not coherent with each other, so a plain store is not seen by
+// a wave on another XCD, and a release store writes back the whole L2), so the redundant prefix sums
+// that need no communication inside a kernel are faster.
+constexpr int kSpBlock = 256;
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* wsum) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    T t = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += wsum[k];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ int32_t block_min(int32_t v, int32_t* wmin) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int32_t t = INT32_MAX;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t = min(t, wmin[k]);
+    __syncthreads();
+    return t;
+}
+
+// Packed batch: the inputs are the caller's arrays in the pinned staging area (read over the host
+// link, no copy); the type, pattern-offset and pattern columns the match reads per candidate are
+// copied to device memory.  blk[3b] = candidates of block b, blk[3b+1] / blk[3b+2] = its smallest
+// bad / unsupported query (INT32_MAX: none).
+__global__ void __launch_bounds__(kSpBlock) hgx_q_norm_sp(
+    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
+    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
+    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
+    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
+    int32_t* __restrict__ d_type, int64_t* __restrict__ d_poff, int32_t* __restrict__ d_pat, int64_t* __restrict__ ncand,
+    int64_t* __restrict__ blk) {
+    __shared__ int64_t ws[kSpBlock / 64];
+    __shared__ int32_t wm[kSpBlock / 64];
+    const int64_t q = (int64_t)blockIdx.x * kSpBlock + threadIdx.x;
+    QPlan p{0, 0, 0, 0};
+    int32_t bad = INT32_MAX, uns = INT32_MAX;
+    if (q < n) {
+        int st = 0;
+        p = norm_query((int32_t)q, A, type, inc_off, inc, has_ordered, pat_off, pat, g_inc_off, ts_type, desc, anchors,
+                       nop, st);
+        if (st == 1) bad = (int32_t)q;
+        if (st == 2) uns = (int32_t)q;
+        plan[q] = p;
+        ncand[q] = p.n;
+        d_type[q] = type[q];
+        const int64_t pb = pat_off[q], pe = pat_off[q + 1];
+        d_poff[q] = pb;
+        if (q == n - 1) d_poff[n] = pe;
+        for (int64_t i = pb; i < pe; ++i) d_pat[i] = pat[i];
+    }
+    const int64_t tot = block_sum<int64_t>(p.n, ws);
+    bad = block_min(bad, wm);
+    uns = block_min(uns, wm);
+    if (threadIdx.x == 0) {
+        blk[3 * blockIdx.x] = tot;
+        blk[3 * blockIdx.x + 1] = bad;
+        blk[3 * blockIdx.x + 2] = uns;
+    }
+}
+
+// Host-normalised batch (legacy / ext entry points): the plan of hgx_q_plan + the block totals.
+__global__ void __launch_bounds__(kSpBlock) hgx_q_plan_sp(int32_t n, const QDesc* __restrict__ desc,
+                                                         const int32_t* __restrict__ anchors,
+                                                         const int32_t* __restrict__ types,
+                                                         const int32_t* __restrict__ nop, const int64_t* __restrict__ inc_off,
+                                                         const int32_t* __restrict__ ts_type, QPlan* __restrict__ plan,
+                                                         int64_t* __restrict__ ncand, int64_t* __restrict__ blk) {
+    __shared__ int64_t ws[kSpBlock / 64];
+    const int64_t q = (int64_t)blockIdx.x * kSpBlock + threadIdx.x;
+    QPlan p{0, 0, 0, 0};
+    if (q < n) {
+        const QDesc d = desc[q];
+        if (d.a_end - d.a_beg <= kRegAnchors && !nop[q]) {
+            int32_t av[kRegAnchors];
+            const int na = (int)(d.a_end - d.a_beg);
+#pragma unroll
+            for (int k = 0; k < kRegAnchors; ++k) av[k] = k < na ? anchors[d.a_beg + k] : 0;
+            p = plan_regs(av, na, (d.t_end - d.t_beg == 1) ? types[d.t_beg] : -1, inc_off, ts_type);
+        } else {
+            p = plan_query(d, nop[q] != 0, anchors, types, inc_off, ts_type);
+        }
+        plan[q] = p;
+        ncand[q] = p.n;
+    }
+    const int64_t tot = block_sum<int64_t>(p.n, ws);
+    if (threadIdx.x == 0) {
+        blk[3 * blockIdx.x] = tot;
+        blk[3 * blockIdx.x + 1] = INT32_MAX;
+        blk[3 * blockIdx.x + 2] = INT32_MAX;
+    }
+}
+
+// Candidate offsets: block b = queries [256 b, 256 b + 256).  stat (mapped result area): [0] chunks,
+// [1] candidates, [2] workspace overflow (the match then sees no chunks), [4] / [5] smallest bad /
+// unsupported query.
+__global__ void __launch_bounds__(kSpBlock) hgx_q_scan_sp(int32_t n, const int64_t* __restrict__ ncand,
+                                                         const int64_t* __restrict__ blk, int64_t* __restrict__ coff,
+                                                         int32_t* __restrict__ chq, int32_t* __restrict__ n_chunks_out,
+                                                         int64_t cap_chunks, int64_t cap_cand, int64_t* __restrict__ stat,
+                                                         u64* __restrict__ ctr) {
+    __shared__ int64_t ws[kSpBlock / 64];
+    __shared__ int32_t wm[kSpBlock / 64];
+    const int b = blockIdx.x, nb = gridDim.x;
+    const bool last = b == nb - 1;
+    const int64_t q = (int64_t)b * kSpBlock + threadIdx.x;
+    const int64_t c = q < n ? ncand[q] : 0;   // issued before the block totals are summed
+    // the candidates of the blocks before this one (the last block: of all blocks, + the statuses)
+    int64_t before = 0;
+    int32_t bad = INT32_MAX, uns = INT32_MAX;
+    for (int j = threadIdx.x; j < (last ? nb : b); j += kSpBlock) {
+        const int64_t t = blk[3 * j];
+        if (j < b) before += t;
+        if (last) {
+            bad = min(bad, (int32_t)blk[3 * j + 1]);
+            uns = min(uns, (int32_t)blk[3 * j + 2]);
+        }
+    }
+    const int64_t pre = block_sum<int64_t>(before, ws);
+    int64_t btot;
+    const int64_t ex = pre + block_exclusive_scan<int64_t>(c, ws, btot);
+    if (q < n) {
+        coff[q] = ex;
+        // the chunks whose first candidate is one of q's (beyond the workspace: overflow, re-run)
+        for (int64_t k = (ex + kFlatChunk - 1) / kFlatChunk; k * kFlatChunk < ex + c && k < cap_chunks; ++k)
+            chq[k] = (int32_t)q;
+    }
+    if (b == 0 && threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;   // the match's counter shards
+    if (last) {
+        bad = block_min(bad, wm);
+        uns = block_min(uns, wm);
+        if (threadIdx.x == 0) {
+            const int64_t tk = pre + btot, tc = (tk + kFlatChunk - 1) / kFlatChunk;
+            const bool over = tc > cap_chunks || tk > cap_cand;
+            coff[n] = tk;
+            *n_chunks_out = over ? 0 : (int32_t)tc;
+            stat[0] = tc;
+            stat[1] = tk;
+            stat[2] = over ? 1 : 0;
+            stat[4] = bad;
+            stat[5] = uns;
+        }
+    }
+}
+
+// Placement: block b = chunks [64 b, 64 b + 64): wave 0 scans their hit counts (after summing the
+// counts of the chunks before the block), then each wave places the hits of 16 chunks with all 16 slot
+// loads, then all 16 link-atom loads, in flight (two dependent rounds instead of one per chunk).
+// outoff[n_chunks] = total hits; the block holding the last chunk (block 0 when there is none)
+// publishes the hit total and the summed counter shards.
+constexpr int kPlaceChunks = 64;
+__global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n_chunks_p,
+                                                  const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
+                                                  const int32_t* __restrict__ link_atom, int64_t* __restrict__ outoff,
+                                                  int32_t* __restrict__ ids, int64_t* __restrict__ stat,
+                                                  const u64* __restrict__ ctr, u64* __restrict__ ctr_out) {
+    __shared__ int64_t ws[4], c_off[kPlaceChunks];
+    __shared__ int32_t c_cnt[kPlaceChunks];
+    const int32_t nc = *n_chunks_p;
+    const int64_t k0 = (int64_t)blockIdx.x * kPlaceChunks;
+    if (k0 > 0 && k0 >= nc) return;   // beyond the chunks (block 0 always runs: it publishes an empty result)
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t k = k0 + lane;
+    const int32_t cnt = wv == 0 && k < nc ? (int32_t)counts[k] : 0;   // issued before the prefix loads
+    int64_t before = 0;   // hit counts of the chunks before this block, eight loads in flight per thread
+    for (int64_t j = threadIdx.x; j < k0; j += 8 * 256) {
+        int64_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = j + u * 256 < k0 ? counts[j + u * 256] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) before += v[u];
+    }
+    const int64_t pre = block_sum<int64_t>(before, ws);
+    if (wv == 0) {
+        int64_t incl = cnt;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const int64_t ex = pre + incl - cnt;
+        if (k < nc) outoff[k] = ex;
+        c_off[lane] = ex;
+        c_cnt[lane] = cnt;
+        if (lane == 63) ws[0] = pre + incl;   // total through this block
+    }
+    __syncthreads();
+    int32_t row[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int cc = wv * 16 + u;
+        row[u] = lane < c_cnt[cc] ? slots[(k0 + cc) * kFlatChunk + lane] : -1;
+    }
+    int32_t at[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) at[u] = row[u] >= 0 ? link_atom[row[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+        if (row[u] >= 0) ids[c_off[wv * 16 + u] + lane] = at[u];
+    const bool holds_last = nc == 0 ? blockIdx.x == 0 : (nc - 1) / kPlaceChunks == (int32_t)blockIdx.x;
+    if (holds_last) {
+        if (threadIdx.x == 0) {
+            const int64_t tot = ws[0];
+            outoff[nc] = tot;
+            stat[3] = stat[2] ? 0 : tot;
+        }
+        if (threadIdx.x < qNum) {
+            u64 v = 0;
+            for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
+            ctr_out[threadIdx.x] = v;
+        }
     }
 }
 
@@ -1954,6 +2202,7 @@ struct Front {
     int64_t* ncand = nullptr;    // [n + 1]
     int32_t* err = nullptr;      // [2] device-side normalisation errors (packed front end), or null
     double cond_bytes = 0;       // condition bytes read by the match (algorithmic accounting)
+    int64_t* blk = nullptr;      // single-pass pipeline: [3 per block of 256 queries] candidates, bad, unsupported
 };
 
 // Buffers taken from the graph pool for one call, released on every exit path.
@@ -2023,6 +2272,15 @@ void front_host(hgx_graph* g, int32_t n, const NormBatch& nb, Scratch& sc, Event
     f.pos = (const int32_t*)(d + o_pos);
     f.poff = (const int64_t*)(d + o_poff);
     f.pat = (const int32_t*)(d + o_pat);
+    f.cond_bytes = 20.0 * nb.anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
+                   4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
+    if (g->q_flat == 2) {   // single-pass pipeline: the plan + per-block candidate totals
+        f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
+        hgx_q_plan_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
+            n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop), g->inc_off, g->inc_ts_type, f.plan, f.ncand, f.blk);
+        HGX_CHECK_LAUNCH();
+        return;
+    }
     hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop),
                                                          g->inc_off, g->inc_ts_type, f.plan, f.nch, f.ncand);
     HGX_CHECK_LAUNCH();
@@ -2043,7 +2301,8 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
     const size_t o_type = u.take(4 * (size_t)n), o_ioff = u.take(8 * (size_t)(n + 1)), o_inc = u.take(4 * (size_t)n_inc),
                  o_ho = u.take(4 * (size_t)n), o_poff = u.take(8 * (size_t)(n + 1)), o_pat = u.take(4 * (size_t)n_pat),
                  o_err = u.take(8);
-    char* h = (char*)g->pinned_buf(u.off);
+    const bool sp = g->q_flat == 2;   // single-pass: the front kernel reads the staging area in place
+    char* h = sp ? (char*)g->zc_in_buf(u.off) : (char*)g->pinned_buf(u.off);
     const int32_t none[2] = {INT32_MAX, INT32_MAX};   // smallest bad query index, none yet
     std::memcpy(h + o_err, none, 8);
     std::memcpy(h + o_type, type, 4 * (size_t)n);
@@ -2052,7 +2311,7 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
     std::memcpy(h + o_ho, has_ordered, 4 * (size_t)n);
     std::memcpy(h + o_poff, pat_off, 8 * (size_t)(n + 1));
     if (n_pat) std::memcpy(h + o_pat, pat, 4 * (size_t)n_pat);
-    char* d = (char*)sc.take(u.off);
+    char* d = sp ? (char*)g->zc_in_dev : (char*)sc.take(u.off);
     QDesc* desc = (QDesc*)sc.take(sizeof(QDesc) * n);
     int32_t* anch = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(n_inc + n_pat, 1));
     int32_t* nop = (int32_t*)sc.take(4 * (size_t)n);
@@ -2061,6 +2320,25 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
     f.ncand = (int64_t*)sc.take(sizeof(int64_t) * (n + 1));
     f.err = (int32_t*)(d + o_err);
     ev.rec(0, s);
+    f.cond_bytes = 20.0 * (double)(n_inc + n_pat) + 4.0 * n + 4.0 * (double)n_pat + (double)sizeof(QDesc) * n;
+    if (sp) {   // normalise + plan straight from the staging area; device copies of the match's columns
+        int32_t* dty = (int32_t*)sc.take(4 * (size_t)n);
+        int64_t* dpo = (int64_t*)sc.take(8 * (size_t)(n + 1));
+        int32_t* dpa = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(n_pat, 1));
+        f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
+        hgx_q_norm_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
+            n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
+            (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
+            g->inc_ts_type, desc, anch, nop, f.plan, dty, dpo, dpa, f.ncand, f.blk);
+        HGX_CHECK_LAUNCH();
+        f.desc = desc;
+        f.anch = anch;
+        f.types = dty;
+        f.pos = nullptr;
+        f.poff = dpo;
+        f.pat = dpa;
+        return;
+    }
     HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
     hgx_q_norm_packed<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(
         n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
@@ -2073,10 +2351,95 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
     f.pos = nullptr;
     f.poff = (const int64_t*)(d + o_poff);
     f.pat = (const int32_t*)(d + o_pat);
-    f.cond_bytes = 20.0 * (double)(n_inc + n_pat) + 4.0 * n + 4.0 * (double)n_pat + (double)sizeof(QDesc) * n;
 }
 
-// Flat back end (HGX_OPT_QUERY_FLAT, default): the candidates of the batch in chunks of 64, a wave
+// Single-pass back end (HGX_OPT_QUERY_FLAT = 2, default): scan + match + placement + offsets after the
+// front kernel, results written by the kernels into mapped host memory, one synchronisation.
+void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
+                 double t0) {
+    (void)sc;
+    hipStream_t s = g->stream;
+    if (g->q_cap_chunks < (int64_t)n / 4 + 64) g->q_cap_chunks = (int64_t)n / 4 + 64;
+    if (g->q_cap_cand < 16 * (int64_t)n + 4096) g->q_cap_cand = 16 * (int64_t)n + 4096;
+    const int nblk = (int)ceil_div(n, kSpBlock);
+    for (int attempt = 0;; ++attempt) {
+        const int64_t capC = std::max<int64_t>(g->q_cap_chunks, ceil_div(g->q_cap_cand, kFlatChunk)), capK = g->q_cap_cand;
+        if (capC > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
+        Scratch w{g, {}};
+        int64_t* coff = (int64_t*)w.take(sizeof(int64_t) * (n + 1));
+        int32_t* chq = (int32_t*)w.take(sizeof(int32_t) * capC);
+        int32_t* nch = (int32_t*)w.take(sizeof(int32_t) * 4);
+        int32_t* slots = (int32_t*)w.take(sizeof(int32_t) * capC * kFlatChunk);
+        int64_t* cnt = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        u64* hmask = (u64*)w.take(sizeof(u64) * (capC + 1));
+        int64_t* outoff = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
+        u64* ctr = (u64*)w.take(sizeof(u64) * kQShards * kQStride);
+        // result area in mapped host memory, written by the kernels (no copy back):
+        // stat[8] | ctr[4] | q_off[n+1] | ids[capK]
+        const size_t m_stat = 0, m_ctr = 64, m_qoff = 128;
+        const size_t m_ids = m_qoff + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
+        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
+        void* hmd = nullptr;
+        HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
+        char* rd = (char*)hmd;
+        int64_t* stat_d = (int64_t*)(rd + m_stat);
+        u64* ctr_d = (u64*)(rd + m_ctr);
+        int64_t* qoff_d = (int64_t*)(rd + m_qoff);
+        int32_t* ids_d = (int32_t*)(rd + m_ids);
+        hgx_q_scan_sp<<<nblk, kSpBlock, 0, s>>>(n, f.ncand, f.blk, coff, chq, nch, capC, capK, stat_d, ctr);
+        HGX_CHECK_LAUNCH();
+        ev.rec(1, s);
+        hgx_pattern_match_flat<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+            nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
+            g->inc_ts_row, g->tgt_off, g->tgt_idx, g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt,
+            hmask, ctr);
+        HGX_CHECK_LAUNCH();
+        ev.rec(2, s);
+        hgx_q_place<<<(unsigned)std::max<int64_t>(1, ceil_div(capC, kPlaceChunks)), 256, 0, s>>>(
+            nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d);
+        HGX_CHECK_LAUNCH();
+        hgx_q_offsets_flat<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, nch, coff, outoff, hmask, stat_d, qoff_d);
+        HGX_CHECK_LAUNCH();
+        ev.rec(3, s);
+        HGX_HIP(hipStreamSynchronize(s));
+        const int64_t* stat = (const int64_t*)(hm + m_stat);
+        const u64* ctr_h = (const u64*)(hm + m_ctr);
+        const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
+        const int32_t* ids_h = (const int32_t*)(hm + m_ids);
+        if (stat[4] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(stat[4]));
+        if (stat[5] < n)
+            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(stat[5]) +
+                                        " is not accelerated (no incidence anchor or condition limits)");
+        if (stat[2]) {   // workspace too small: grow to the reported totals and match again
+            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: workspace sizing failed");
+            g->q_cap_chunks = std::max<int64_t>(capC, stat[0] + stat[0] / 4 + 64);
+            g->q_cap_cand = std::max<int64_t>(capK, stat[1] + stat[1] / 4 + 4096);
+            continue;
+        }
+        const int64_t total = stat[3];
+        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
+        r->ids.assign(ids_h, ids_h + total);
+        if (prof)
+            std::fprintf(stderr, "[hgx query] single-pass n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n",
+                         n, now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
+        if (ev.on) {
+            float a = 0, b = 0;
+            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
+            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
+            r->ms_total = a;
+            r->ms_match = b;
+        }
+        // algorithmic bytes of hgx_pattern_match_flat (as back_end_flat)
+        r->bytes_match = (4.0 + 8.0 * (kFlatChunk + 1) + 16.0) * (double)stat[0] +
+                         (double)(sizeof(QPlan) + sizeof(QDesc)) * n + 4.0 * (double)ctr_h[qCand] +
+                         4.0 * (double)ctr_h[qTyped] + 32.0 * (double)ctr_h[qInline] +
+                         16.0 * ((double)ctr_h[qTyped] - (double)ctr_h[qInline]) + 4.0 * (double)ctr_h[qArity] +
+                         4.0 * (double)ctr_h[qHits] + f.cond_bytes;
+        return;
+    }
+}
+
+// Flat back end (HGX_OPT_QUERY_FLAT = 1, A/B): the candidates of the batch in chunks of 64, a wave
 // per chunk and a lane per candidate (hgx_pattern_match_flat); the rest as back_end below.
 void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
                    double t0) {
@@ -2204,6 +2567,7 @@ void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, h
 // reported totals and the back end runs again.
 void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
               double t0) {
+    if (f.blk) return back_end_sp(g, n, f, sc, ev, r, prof, t0);
     if (g->q_flat) return back_end_flat(g, n, f, sc, ev, r, prof, t0);
     hipStream_t s = g->stream;
     const bool small = n <= kSmallBatch;
@@ -2482,8 +2846,159 @@ int run_batch(hgx_graph* g, int32_t n, NormBatch& nb, hgx_query_result** out) {
     return run_batch_with(g, n, out, [&](Scratch& sc, Events& ev, Front& f) { front_host(g, n, nb, sc, ev, f); });
 }
 
+int run_batch_packed_direct(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                            const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat,
+                            hgx_query_result** out);
+
+// One caller batch of the combiner run on its own: the result, or the status and this thread's
+// error message handed to the waiting caller.
+void serve_one(hgx_graph* g, PackedReq* q) {
+    hgx_query_result* r = nullptr;
+    q->rc = run_batch_packed_direct(g, q->n, q->type, q->inc_off, q->inc, q->has_ordered, q->pat_off, q->pat, &r);
+    if (q->rc == HGX_OK) q->r = r;
+    else q->err = hgx_last_error();
+}
+
+// The offsets of a caller batch are what the merge relies on (the device checks everything else).
+bool mergeable(const PackedReq* q) {
+    if (q->n <= 0 || q->inc_off[0] != 0 || q->pat_off[0] != 0) return false;
+    const int64_t ni = q->inc_off[q->n], np = q->pat_off[q->n];
+    return ni >= 0 && np >= 0 && (ni == 0 || q->inc) && (np == 0 || q->pat);
+}
+
+// Serve a group of queued caller batches: those that can merge run as ONE device batch (their
+// arrays concatenated, offsets rebased) whose result is split back per caller; a merged run that
+// reports a bad or unsupported query is re-run caller by caller, so every caller gets exactly the
+// result or error of a separate call.  Never throws (statuses go to the requests).
+void serve_group(hgx_graph* g, const std::vector<PackedReq*>& grp) {
+    std::vector<PackedReq*> m;
+    for (PackedReq* q : grp) {
+        if (grp.size() > 1 && mergeable(q)) m.push_back(q);
+        else serve_one(g, q);
+    }
+    if (m.empty()) return;
+    if (m.size() == 1) {
+        serve_one(g, m[0]);
+        return;
+    }
+    int rc = HGX_OK;
+    std::string err;
+    try {
+        int64_t N = 0, NI = 0, NP = 0;
+        for (PackedReq* q : m) {
+            N += q->n;
+            NI += q->inc_off[q->n];
+            NP += q->pat_off[q->n];
+        }
+        std::vector<int32_t> type((size_t)N), ho((size_t)N), inc((size_t)std::max<int64_t>(NI, 1)),
+            pat((size_t)std::max<int64_t>(NP, 1));
+        std::vector<int64_t> io((size_t)N + 1), po((size_t)N + 1);
+        int64_t b = 0, bi = 0, bp = 0;
+        for (PackedReq* q : m) {
+            std::memcpy(&type[b], q->type, 4 * (size_t)q->n);
+            std::memcpy(&ho[b], q->has_ordered, 4 * (size_t)q->n);
+            for (int32_t k = 0; k < q->n; ++k) {
+                io[b + k] = bi + q->inc_off[k];
+                po[b + k] = bp + q->pat_off[k];
+            }
+            if (q->inc_off[q->n]) std::memcpy(&inc[bi], q->inc, 4 * (size_t)q->inc_off[q->n]);
+            if (q->pat_off[q->n]) std::memcpy(&pat[bp], q->pat, 4 * (size_t)q->pat_off[q->n]);
+            b += q->n;
+            bi += q->inc_off[q->n];
+            bp += q->pat_off[q->n];
+        }
+        io[N] = bi;
+        po[N] = bp;
+        hgx_query_result* all = nullptr;
+        rc = run_batch_packed_direct(g, (int32_t)N, type.data(), io.data(), inc.data(), ho.data(), po.data(), pat.data(),
+                                     &all);
+        if (rc == HGX_OK) {
+            std::unique_ptr<hgx_query_result> keep(all);
+            int64_t q0 = 0;
+            for (PackedReq* q : m) {
+                std::unique_ptr<hgx_query_result> r(new hgx_query_result());
+                r->n = q->n;
+                r->offsets.resize((size_t)q->n + 1);
+                const int64_t base = all->offsets[(size_t)q0];
+                for (int32_t k = 0; k <= q->n; ++k) r->offsets[(size_t)k] = all->offsets[(size_t)(q0 + k)] - base;
+                r->ids.assign(all->ids.begin() + base, all->ids.begin() + all->offsets[(size_t)(q0 + q->n)]);
+                r->ms_total = all->ms_total;
+                r->ms_match = all->ms_match;
+                r->bytes_match = all->bytes_match;
+                q->r = r.release();
+                q->rc = HGX_OK;
+                q0 += q->n;
+            }
+            return;
+        }
+        err = hgx_last_error();
+    } catch (const std::bad_alloc&) {
+        rc = HGX_E_NOMEM;
+        err = "host allocation failed";
+    } catch (const std::exception& e) {
+        rc = HGX_E_DEVICE;
+        err = e.what();
+    }
+    if (rc == HGX_E_INVALID || rc == HGX_E_UNSUPPORTED) {   // a query-specific status: whose query?
+        for (PackedReq* q : m) serve_one(g, q);
+        return;
+    }
+    for (PackedReq* q : m) {
+        q->rc = rc;
+        q->err = err;
+    }
+}
+
 int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
                      const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result** out) {
+    if (n <= 0 || !g->q_coalesce || g->q_fused || g->shard)
+        return run_batch_packed_direct(g, n, type, inc_off, inc, has_ordered, pat_off, pat, out);
+    PackedReq me;
+    me.n = n;
+    me.type = type;
+    me.inc_off = inc_off;
+    me.inc = inc;
+    me.has_ordered = has_ordered;
+    me.pat_off = pat_off;
+    me.pat = pat;
+    QueryCombiner& c = g->qcomb;
+    std::unique_lock<std::mutex> lk(c.mu);
+    c.pending.push_back(&me);
+    while (!me.done) {
+        if (c.busy) {
+            c.cv.wait(lk);
+            continue;
+        }
+        // run the queue's head group: FIFO, up to the query cap (a batch above the cap runs alone)
+        c.busy = true;
+        std::vector<PackedReq*> grp;
+        int64_t tot = 0;
+        while (!c.pending.empty() && (grp.empty() || tot + c.pending.front()->n <= g->q_coalesce_max)) {
+            grp.push_back(c.pending.front());
+            tot += c.pending.front()->n;
+            c.pending.pop_front();
+        }
+        lk.unlock();
+        serve_group(g, grp);
+        lk.lock();
+        for (PackedReq* q : grp) q->done = true;
+        c.batches += 1;
+        c.requests += (int64_t)grp.size();
+        c.busy = false;
+        c.cv.notify_all();
+    }
+    lk.unlock();
+    if (me.rc != HGX_OK) {
+        set_last_error(me.err);
+        return me.rc;
+    }
+    *out = me.r;
+    return HGX_OK;
+}
+
+int run_batch_packed_direct(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                            const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat,
+                            hgx_query_result** out) {
     if (n > 0 && n <= kFusedMax && g->q_fused && !g->shard) {
         HGX_API_BEGIN
         const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
@@ -2544,5 +3059,14 @@ int hgx_query_result_ms(const hgx_query_result* r, double* ms_total, double* ms_
 }
 
 void hgx_query_result_free(hgx_query_result* r) { delete r; }
+
+int hgx_query_coalesce_stats(hgx_graph* g, int64_t* device_batches, int64_t* caller_batches) {
+    HGX_API_BEGIN
+    if (!g) fail(HGX_E_INVALID, "null graph");
+    std::lock_guard<std::mutex> lk(g->qcomb.mu);
+    if (device_batches) *device_batches = g->qcomb.batches;
+    if (caller_batches) *caller_batches = g->qcomb.requests;
+    HGX_API_END
+}
 
 }  // extern "C"

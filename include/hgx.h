@@ -369,15 +369,28 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * fewer bytes.  A/B on full config 4 at 8 parts: 34.0 / 42.8 / 35.5 ms per part a step
  * (profiles/r02ze_part_c4x1.json) -- the static kernels touch every ghost and owned atom. */
 #define HGX_OPT_PART_EXCHANGE 8
-/* HGX_OPT_QUERY_FLAT (default 1): pattern batches match over the batch's flat candidate space, a
- * wavefront per 64 candidates and a lane per candidate whatever query it belongs to; 0 = a
- * wavefront per chunk of one query's candidates (A/B). */
+/* HGX_OPT_QUERY_FLAT (default 2): pattern batches match over the batch's flat candidate space, a
+ * wavefront per 64 candidates and a lane per candidate whatever query it belongs to.  2 = single pass:
+ * two kernels per batch (normalise + plan + candidate scan with a decoupled look-back; match + hit
+ * offsets with a decoupled look-back + result placement); 1 = the same match with a separate
+ * single-workgroup scan, finish and scatter (A/B); 0 = a wavefront per chunk of one query's
+ * candidates (A/B). */
 #define HGX_OPT_QUERY_FLAT 9
 /* HGX_OPT_CODED (symmetric mode; default 0 = off, A/B): 1 = a dense level right after a push level
  * whose new rows carry <= 3 source bits on average moves rows of <= 6 bits as 64-bit codes (six 10-bit
  * source ids) instead of 128-byte rows; 2 = whenever the push level wrote codes (tests).  Exact, but
  * measured slower on config 2's level 1 (16.0 vs 9.0 ms, profiles/r02zn_*_c2_levels.log). */
 #define HGX_OPT_CODED 10
+/* HGX_OPT_QUERY_COALESCE (default 1 = on): concurrent hgx_pattern_batch_packed calls on one graph
+ * share device batches.  A caller that finds the device busy queues its batch; the next caller to
+ * run takes every queued batch (FIFO, up to 65536 queries; a value > 1 sets that cap) and runs them
+ * as ONE batch, then splits the result -- the reference's usage is many threads each executing small
+ * compiled queries (QueryCompilation.java:76-122).  Results and errors are exactly those of separate
+ * calls (a batch whose merged run reports a bad or unsupported query is re-run on its own).  0 = off. */
+#define HGX_OPT_QUERY_COALESCE 11
+/* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
+ * and caller batches they served (caller / device = the mean coalescing factor). */
+int  hgx_query_coalesce_stats(hgx_graph *g, int64_t *device_batches, int64_t *caller_batches);
 
 /* RCCL transport between processes (one GPU each): rank 0 calls hgx_comm_rccl_unique_id and
  * broadcasts the 128 bytes out of band; every rank then calls hgx_comm_rccl_create. */

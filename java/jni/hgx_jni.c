@@ -526,6 +526,13 @@ JNIEXPORT jintArray JFN(queryIds)(JNIEnv *e, jclass k, jlong qr) {
 
 JNIEXPORT void JFN(queryFree)(JNIEnv *e, jclass k, jlong q) { hgx_query_result_free((hgx_query_result *)(intptr_t)q); }
 
+JNIEXPORT jlongArray JFN(queryCoalesceStats)(JNIEnv *e, jclass k, jlong g) {
+    int64_t v[2] = {0, 0};
+    int rc = hgx_query_coalesce_stats((hgx_graph *)(intptr_t)g, &v[0], &v[1]);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    return new_longs(e, v, 2);
+}
+
 /* ---- partitioned snapshot -------------------------------------------------------------------- */
 
 JNIEXPORT jintArray JFN(partitionPlan)(JNIEnv *e, jclass k, jlong numAtoms, jintArray linkAtom, jlongArray tgtOff,

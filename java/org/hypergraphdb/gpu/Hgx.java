@@ -18,7 +18,7 @@ final class Hgx
     static final int NO_TYPE = -1, ANY_HANDLE = -1, UNBOUNDED = -1;
     static final int OPT_BFS_FLAGS = 1, OPT_SEQ_BUDGET = 2, OPT_RANKS_ORDERED = 3, OPT_PART_SERIAL = 4;
     static final int OPT_QUERY_FUSED = 5, OPT_QUERY_INLINE = 6, OPT_PUSH_BATCH = 7, OPT_PART_EXCHANGE = 8,
-                     OPT_QUERY_FLAT = 9, OPT_CODED = 10;   // include/hgx.h
+                     OPT_QUERY_FLAT = 9, OPT_CODED = 10, OPT_QUERY_COALESCE = 11;   // include/hgx.h
 
     // ---- snapshot (hgx_graph_create / open / destroy / update / info) ---------------------------
     static native long graphCreate(long numAtoms, int[] linkAtom, long[] tgtOff, int[] tgtIdx, int[] linkType,
@@ -62,6 +62,7 @@ final class Hgx
     static native long[] queryOffsets(long q);                  // [n + 1]
     static native int[] queryIds(long q);
     static native void queryFree(long q);
+    static native long[] queryCoalesceStats(long g);            // {device batches, caller batches}
 
     // ---- partitioned snapshot (config 4: one part per GPU / JVM) -----------------------------
     static native int[] partitionPlan(long numAtoms, int[] linkAtom, long[] tgtOff, int[] tgtIdx, int[] linkType,

@@ -6,7 +6,7 @@ pinning and pending exceptions, and checks the JNI discipline on every call.  Th
 HGGpuSnapshot / HGGpuTraversal / GpuAndToQuery / GpuTraversalToQuery take (java/org/hypergraphdb/gpu):
 the results are compared with the C oracle (oracle/hgx_oracle.c, the restatement of
 HGBreadthFirstTraversal / DefaultALGenerator / AndToQuery), bit-exact.  The last test checks that
-all 52 natives were called."""
+all 53 natives were called."""
 import numpy as np
 import pytest
 
@@ -343,6 +343,45 @@ def test_partitioned_natives_vs_oracle(jni, graph):
         jni.graphDestroy(gp)
 
 
+def test_concurrent_single_queries_coalesce(jni, graph, gh):
+    """20 'Java threads' (one JNIEnv each) issue single And queries at once, the usage of
+    TC/query/QueryCompilation.java:76-122: every result equals the oracle's, and the engine served them
+    with fewer device batches than calls (HGX_OPT_QUERY_COALESCE; queryCoalesceStats)."""
+    import threading
+    g, orc = graph
+    qs = pattern_queries(g, np.random.default_rng(21), 400)
+    exp = [orc.and_query(t, a, p) for t, a, p in qs]
+    b0 = jni.queryCoalesceStats(gh)
+    errors = []
+
+    def worker(t):
+        j = Jni()
+        try:
+            for i in range(t, len(qs), 20):
+                q = j.patternBatch(gh, *packed([qs[i]]))
+                try:
+                    ids = j.queryIds(q)
+                    if not np.array_equal(ids, exp[i]):
+                        errors.append((t, i))
+                finally:
+                    j.queryFree(q)
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+        finally:
+            j.close()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(20)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+    b1 = jni.queryCoalesceStats(gh)
+    dev, calls = int(b1[0] - b0[0]), int(b1[1] - b0[1])
+    assert calls == len(qs)
+    assert dev < calls, (dev, calls)
+
+
 def test_engine_errors_become_exceptions(jni, gh):
     with pytest.raises(JavaException) as ei:
         jni.bfsBatch(gh, np.array([10 ** 8], np.int32), 2, -1, True, True, False, False)
@@ -351,8 +390,8 @@ def test_engine_errors_become_exceptions(jni, gh):
     assert jni.lastError() == ei.value.msg
 
 
-def test_all_52_natives_were_executed(jni):
+def test_all_natives_were_executed(jni):
     """Runs last (file order): every native declared in Hgx.java has been called on the GPU."""
     missing = sorted(set(java_natives()) - jni.called)
     assert not missing, missing
-    assert len(jni.called) == 52
+    assert len(jni.called) == 53

@@ -279,3 +279,26 @@ def test_exchange_modes(xmode):
     hs = rng.integers(0, h["num_atoms"], 1024).astype(np.int32)
     st = compare(h, 4, hs, 4, xmode=xmode)
     assert all(s["bytes_exchanged"] > 0 for s in st)
+
+
+def test_mismatched_exchange_mode_is_rejected_on_every_part():
+    """every part of a group must run the same exchange format (each issues a different
+    sequence of collectives).  The partitioned BFS all-gathers the mode (and the call's seeds, depth
+    and generator) before any exchange and fails with HGX_E_INVALID on every part -- no hang, no
+    out-of-bounds read of a peer's buffers -- and the group still works once the parts agree."""
+    from hypergraphdb_amd import HGXError, _lib
+    from hypergraphdb_amd.partition import pbfs_batch_group
+    rng = np.random.default_rng(77)
+    g = K.random_graph(rng, 400, 700, max_arity=6, n_types=2)
+    sh = parts(g, 3)
+    sh[1].set_option(_lib.HGX_OPT_PART_EXCHANGE, 2)
+    with pytest.raises(HGXError) as ei:
+        pbfs_batch_group(sh, [0, 1, 2], 3)
+    assert ei.value.code == _lib.HGX_E_INVALID and "HGX_OPT_PART_EXCHANGE" in str(ei.value)
+    sh[1].set_option(_lib.HGX_OPT_PART_EXCHANGE, 1)
+    res = pbfs_batch_group(sh, [0, 1, 2], 3)
+    orc = oracle(g)
+    for i, s in enumerate((0, 1, 2)):
+        exp = orc.bfs_levels(s, 3)
+        assert res.counts()[i, :len(exp)].tolist() == [len(x) for x in exp]
+    res.close()

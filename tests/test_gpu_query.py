@@ -389,7 +389,8 @@ def test_inline_records_vs_tgt_rows_and_oracle(case):
 
 
 def test_flat_and_chunked_match_paths():
-    """HGX_OPT_QUERY_FLAT: the flat match (a lane per candidate over the batch's candidate space,
+    """HGX_OPT_QUERY_FLAT: the single-pass pipeline (2: front-scan and match kernels with decoupled
+    look-backs), the flat match (a lane per candidate over the batch's candidate space,
     per-chunk hit masks for the query offsets) and the per-query chunks give the oracle's results:
     batches with long runs of queries without candidates (a chunk window of more than 64 queries),
     empty orderedLinks, untyped and typed queries, and a batch above 16384 queries (device scans)."""
@@ -413,8 +414,62 @@ def test_flat_and_chunked_match_paths():
     for lo, hi in ((0, 3000), (3000, 3300), (0, 20000)):
         sub = qs[lo:hi]
         exp = [orc.and_query(t, i, p).tolist() for t, i, p in sub]
-        for flat in (1, 0):
+        for flat in (2, 1, 0):
             snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
             r = pattern_batch(snap, sub)
             for q in range(len(sub)):
                 assert r[q].tolist() == exp[q], (flat, lo + q, sub[q])
+
+
+def test_single_pass_packed_batches_all_sizes():
+    """The single-pass pipeline on the packed entry (device normalisation in the front-scan kernel):
+    batch sizes 1..70000 (1 to 274 front blocks; chunk counts from 0 to thousands, so both look-backs
+    run across many predecessors), batches whose queries all have no candidate, the workspace-growth
+    re-run, and the same results as the flat (1) and per-query (0) paths."""
+    from hypergraphdb_amd import _lib
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    rng = np.random.default_rng(1900)
+    g = K.random_graph(rng, 3000, 30000, max_arity=8, n_types=4, link_targets=True)
+    snap, orc = snapshot(g), oracle(g)
+    A = g["num_atoms"]
+    off, tg, lt = g["tgt_off"], g["tgt_idx"], g["link_type"]
+
+    def batch(n):
+        ty, inc, pat, po, ho = [], [], [], [0], []
+        for _ in range(n):
+            r = int(rng.integers(0, len(off) - 1))
+            t = tg[off[r]:off[r + 1]]
+            a = int(t[int(rng.integers(0, len(t)))]) if len(t) and rng.random() < 0.8 else int(rng.integers(0, A))
+            ty.append(int(lt[r]) if rng.random() < 0.6 else -1)
+            inc.append(a)
+            if len(t) >= 3 and rng.random() < 0.5:
+                pat += [int(t[0]), -1, int(t[2])]
+                ho.append(1)
+            else:
+                ho.append(0)
+            po.append(len(pat))
+        return (np.array(ty, np.int32), np.arange(n + 1, dtype=np.int64), np.array(inc, np.int32),
+                np.array(ho, np.int32), np.array(po, np.int64), np.array(pat, np.int32))
+
+    for n in (1, 2, 63, 255, 256, 257, 1000, 5000, 70000):
+        b = batch(n)
+        ref = None
+        for flat in (2, 1, 0):
+            snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
+            r = pattern_batch_arrays(snap, *b)
+            if ref is None:
+                ref = r
+                if n <= 5000:
+                    for q in range(n):
+                        p = b[5][b[4][q]:b[4][q + 1]].tolist() if b[3][q] else None
+                        e = orc.and_query(int(b[0][q]), [int(b[2][q])], p)
+                        assert r.ids[r.offsets[q]:r.offsets[q + 1]].tolist() == e.tolist(), (n, q)
+            else:
+                assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), (n, flat)
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
+    # every query without candidates (isolated anchors): zero chunks, all offsets 0
+    isolated = np.array([a for a in range(A) if orc.and_query(-1, [a], None).size == 0][:50], np.int32)
+    n = len(isolated)
+    r = pattern_batch_arrays(snap, np.full(n, -1, np.int32), np.arange(n + 1, dtype=np.int64), isolated,
+                             np.zeros(n, np.int32), np.zeros(n + 1, np.int64), np.zeros(0, np.int32))
+    assert r.offsets.tolist() == [0] * (n + 1)

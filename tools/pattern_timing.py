@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--queries", type=int, default=10_000)
     ap.add_argument("--fused", default="0", help="HGX_OPT_QUERY_FUSED values to compare, interleaved (e.g. 1,0)")
     ap.add_argument("--inline", default="1", help="HGX_OPT_QUERY_INLINE values to compare, interleaved (e.g. 1,0)")
-    ap.add_argument("--flat", default="1", help="HGX_OPT_QUERY_FLAT values to compare, interleaved (e.g. 1,0)")
+    ap.add_argument("--flat", default="2", help="HGX_OPT_QUERY_FLAT values to compare, interleaved (e.g. 2,1,0)")
+    ap.add_argument("--no-timing", action="store_true", help="no device events (wall time without their gaps)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
@@ -28,7 +29,7 @@ def main():
     g = synth.config3(scale=args.scale, n_queries=args.queries)
     Q = g["queries"]
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
-    snap.set_timing(True)
+    snap.set_timing(not args.no_timing)
     nq = len(Q["type"])
     packed = (Q["type"], np.arange(nq + 1, dtype=np.int64), Q["a"], np.ones(nq, np.int32),
               np.arange(0, 3 * nq + 1, 3, dtype=np.int64),
