@@ -85,8 +85,11 @@ def roofline(stats_list, workload):
     t = tot[dom]
     achieved = t["bytes"] / (t["ms"] / 1e3) / 1e9 if t["ms"] > 0 else 0.0
     traffic, src = pmc_traffic(dom, workload)
+    avg_s = t["ms"] / max(t["launches"], 1) / 1e3
+    # the counter-based fraction: PMC HBM bytes per launch / this run's average launch time / peak
+    frac_pmc = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_s > 0 else None
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_from": src,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "frac_pmc": frac_pmc, "traffic": traffic, "traffic_from": src,
             "bytes_per_launch": t["bytes"] / max(t["launches"], 1),
             "avg_launch_ms": t["ms"] / max(t["launches"], 1), "launches": t["launches"]}, tot
 
@@ -109,8 +112,8 @@ def host_info():
 
 
 def cpu_threads():
-    """All cores of the box's share: the GPU box exposes the whole machine to os.cpu_count() but a
-    one-GPU job owns 16 of them (OMP_NUM_THREADS is set to that share there)."""
+    """The CPU share of this job: the GPU box exposes the whole machine to os.cpu_count() (256 CPUs on
+    an 8-GPU node) but a one-GPU job owns 16 of them (OMP_NUM_THREADS is set to that share there)."""
     env = os.environ.get("HGX_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
     if env:
         return max(1, int(env))
@@ -125,16 +128,22 @@ def median_runs(run, reps=5):
 
 
 def cpu_leg(run_for_threads, unit, sample, kind="port"):
-    """The 1-thread and all-cores legs of one CPU baseline."""
+    """The 1-thread leg and the job's-CPU-share leg (cpu_threads() threads) of one CPU baseline.  `value`
+    and `cores` are the share leg as run; `value_linear_usable_cpus` = the 1-thread rate x every CPU the
+    process may use, a linear-scaling ceiling for a run on the whole machine (not measured: the box
+    gives a one-GPU job 16 CPUs)."""
     info = host_info()
     out = {"unit": unit, "kind": kind, "sample": sample, "repetitions": "median of 5 after 1 warm-up", **info}
     nt = cpu_threads()
-    for tag, th in (("1t", 1), ("all", nt)):
+    for tag, th in (("1t", 1), (f"{nt}t", nt)):
         med, rates = median_runs(lambda: run_for_threads(th))
         out[f"value_{tag}"] = med
         out[f"rates_{tag}"] = [round(r, 1) for r in rates]
-    out["value"] = out["value_all"]
+    out["value"] = out[f"value_{nt}t"]
     out["cores"] = nt
+    out["cores_note"] = (f"{nt} threads = the CPU share of this job (OMP_NUM_THREADS / HGX_CPU_THREADS, else min(16, "
+                         "usable CPUs)); usable_cpus is the whole machine")
+    out["value_linear_usable_cpus"] = out["value_1t"] * info["usable_cpus"]
     return out
 
 
@@ -154,7 +163,7 @@ def cpu_bfs_baseline(g, seeds, depth, budget_s):
         _, tr = orc.bfs_many(batch, depth, depth + 1, nthreads=threads, time_budget_s=budget_s, timing=tm)
         return int(tr.sum()), tm["elapsed_s"]
 
-    out = cpu_leg(run, "TEPS", f"config-2 sources seeds[:threads] (1 / all cores), depth {depth}, one traversal "
+    out = cpu_leg(run, "TEPS", f"config-2 sources seeds[:threads] (1 thread / the job's CPU share), depth {depth}, one traversal "
                   f"per thread, each stopped after {budget_s:g}s (C restatement of HGBreadthFirstTraversal/"
                   "DefaultALGenerator)")
     del orc
@@ -313,41 +322,67 @@ def run_config5(args, ctx, barrier_sync):
                                 device=ctx.device)
     snap.set_timing(True)
     T = g["subsumes_type"]
-    gens = [DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev) for rev in (False, True)]
+    # the two directions of a step run side by side: hg.subsumed on the snapshot, hg.subsumes on an
+    # execution context of it (hgx_graph_context: same device arrays, its own stream and scratch), each
+    # driven by its own host thread -- one direction's levels are a few tens of microseconds of
+    # latency-bound kernels that leave most of the GPU idle
+    views = [snap, snap.context()]
+    gens = [DefaultALGenerator(v, AtomTypeCondition(T), None, False, True, rev) for v, rev in zip(views, (False, True))]
     log(f"rank {rank}: config5 ({g['n_nodes']} classes, {len(g['link_atom'])} links) ready in {time.time() - t0:.1f}s")
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(1)
+
+    def direction(k, accounting=False):
+        r = H.bfs_batch(views[k], g["seeds"], None, gens[k])
+        n = int(r.counts()[:, 1:].sum())   # the result readout: per-class closure sizes per depth (D2H)
+        st = r.stats(accounting=accounting)
+        r.close()
+        return n, st
+
+    def step(accounting=False, concurrent=True):
+        if not concurrent:
+            return [direction(0, accounting), direction(1, accounting)]
+        f = pool.submit(direction, 1, accounting)
+        a = direction(0, accounting)
+        return [a, f.result()]
+
     trav, closure = 0.0, 0
     for _ in range(max(args.warmup, 1)):
-        for gen in gens:
-            r = H.bfs_batch(snap, g["seeds"], None, gen)
-            st = r.stats(accounting=True)
+        for n, st in step(accounting=True):
             trav += st["traversed_edges"]
-            closure += int(r.counts()[:, 1:].sum())
-            r.close()
+            closure += n
     trav /= max(args.warmup, 1)
     closure //= max(args.warmup, 1)
+    # the same step with the directions one after the other (reported next to the timed line)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(concurrent=False)
+    seq_ms = (time.perf_counter() - t1) / args.steps * 1e3
     barrier_sync()
     t1 = time.perf_counter()
     sts = []
     readout = 0
     for _ in range(args.steps):
-        for gen in gens:
-            r = H.bfs_batch(snap, g["seeds"], None, gen)
-            readout += int(r.counts()[:, 1:].sum())   # the result readout: per-class closure sizes per depth (D2H)
-            sts.append(r.stats(accounting=False))
-            r.close()
+        for n, st in step():
+            readout += n
+            sts.append(st)
     barrier_sync()
     dt = ctx.max(time.perf_counter() - t1)
+    pool.shutdown()
+    views[1].close()
     assert readout == closure * args.steps, "config-5 readout differs from the warm-up closures"
     edges = ctx.sum(trav * args.steps)
     out = {"metric": "hyperedge TEPS (subsumption closures)", "value": edges / dt, "unit": "TEPS",
            "closures_per_s": ctx.sum(2 * len(g["seeds"]) * args.steps) / dt, "scaling": "weak",
            "ms_per_step": round(dt / args.steps * 1e3, 3), "levels": max(s["n_levels_expanded"] for s in sts),
+           "directions": "concurrent: hg.subsumed on the snapshot, hg.subsumes on an execution context of it",
+           "ms_per_step_directions_serial": round(seq_ms, 3),
            "closure_atoms_per_step": closure,
            "workload": (f"config5: {g['n_nodes']} classes, HGSubsumes DAG + noise links, {len(g['seeds'])} classes x "
                         "{subsumed, subsumes}, unbounded depth"),
            "roofline": _kernel_roof(sts)}
     log(f"rank {rank}: config5 {out['value']:.3e} TEPS, {out['closures_per_s']:.1f} closures/s, "
-        f"{out['ms_per_step']} ms/step, {out['levels']} levels")
+        f"{out['ms_per_step']} ms/step ({seq_ms:.3f} with the directions one after the other), {out['levels']} levels")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle_ctypes import OracleGraph, algen

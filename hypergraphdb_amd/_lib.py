@@ -37,7 +37,7 @@ HGX_OPT_QUERY_COALESCE = 11
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (
-    "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_device_count", "hgx_graph_create", "hgx_graph_destroy", "hgx_graph_info",
+    "hgx_version", "hgx_last_error", "hgx_device_synchronize", "hgx_device_count", "hgx_graph_create", "hgx_graph_context", "hgx_graph_destroy", "hgx_graph_info",
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
@@ -131,6 +131,7 @@ def lib():
         "hgx_device_synchronize": ([i32], C.c_int),
         "hgx_device_count": ([C.POINTER(i32)], C.c_int),
         "hgx_graph_create": ([C.POINTER(GraphDesc), i32, C.POINTER(vp)], C.c_int),
+        "hgx_graph_context": ([vp, C.POINTER(vp)], C.c_int),
         "hgx_graph_destroy": ([vp], None),
         "hgx_graph_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
         "hgx_graph_degree": ([vp, vp, i32, vp], C.c_int),

@@ -2295,12 +2295,12 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
 // block to finish sums the shards (device-scope atomic reads), stores the totals into the mapped
 // host slot, then the sequence number the host spins on.  Every thread of every block calls it.
 __device__ __forceinline__ void level_counters_out(u64* __restrict__ ctr, u64* __restrict__ ticket,
-                                                   u64* __restrict__ hout, u64 seq) {
+                                                   u64* __restrict__ hout, u64 seq, unsigned nblocks) {
     __shared__ bool last;
     __syncthreads();   // the block's counter atomics are issued
     if (threadIdx.x == 0) {
         __threadfence();
-        last = atomicAdd(ticket, 1ull) == (u64)gridDim.x - 1ull;
+        last = atomicAdd(ticket, 1ull) == (u64)nblocks - 1ull;
     }
     __syncthreads();
     if (!last) return;   // block-uniform
@@ -2335,6 +2335,13 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
                                                               u64* __restrict__ lcount, u64* __restrict__ fcode) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
+    const int64_t n = (int64_t)*n_clist;
+    // Blocks past the list leave at once and take no ticket: the grid is sized for the largest lists
+    // (512 blocks), a config-5 level lists a few thousand candidates (32 a block per pass at W = 16),
+    // and 512 same-address ticket atomics serialise for several microseconds a level.
+    const unsigned nactive =
+        (unsigned)max((int64_t)1, min((int64_t)gridDim.x, (n + (int64_t)(blockDim.x / G) - 1) / (int64_t)(blockDim.x / G)));
+    if (blockIdx.x >= nactive) return;   // block-uniform
     // lcount: the next level's per-source counts, accumulated here (a push level's new rows are sparse:
     // one LDS add per set bit, one global add per nonzero source per block) instead of a readout pass
     __shared__ uint32_t lc[W * 64];
@@ -2346,7 +2353,6 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
     const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
     const typename V::T FULL = full_part<W>(fm, sub);
-    const int64_t n = (int64_t)*n_clist;
     // the consumed frontier list's counter: zero for the next level's candidates (chained levels)
     if (n_spent && blockIdx.x == 0 && threadIdx.x == 0) *n_spent = 0ull;
     u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0, n_bits = 0;
@@ -2412,7 +2418,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
         for (int j = threadIdx.x; j < W * 64; j += blockDim.x)
             if (lc[j]) atomicAdd(lcount + j, (u64)lc[j]);
     }
-    if (hout) level_counters_out(ctr, ticket, hout, seq);
+    if (hout) level_counters_out(ctr, ticket, hout, seq, nactive);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2596,12 +2602,23 @@ __global__ void __launch_bounds__(256) hgx_nf_pull(const int32_t* __restrict__ l
     wave_add_sh(ctr + cNfRows, n_rows);
 }
 
-// sum of |inc(v)| over the seed atoms (level-0 push volume)
-__global__ void hgx_seed_degree(int32_t n, const int32_t* __restrict__ atoms, const int64_t* __restrict__ inc_off,
-                                u64* __restrict__ out) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    u64 d = k < n ? (u64)(inc_off[atoms[k] + 1] - inc_off[atoms[k]]) : 0ull;
-    wave_add(out, d);
+// The seeds' incidence volume (the level-0 direction choice) straight into mapped host memory: one
+// block sums the degrees, stores the total, then the sequence number the host spins on (a
+// device-to-host copy and a stream synchronisation cost ~40 us before the first level).
+__global__ void __launch_bounds__(256) hgx_seed_degree_host(int32_t n, const int32_t* __restrict__ atoms,
+                                                            const int64_t* __restrict__ inc_off,
+                                                            u64* __restrict__ hout, u64 seq) {
+    __shared__ u64 part[4];
+    u64 d = 0;
+    for (int k = threadIdx.x; k < n; k += 256) d += (u64)(inc_off[atoms[k] + 1] - inc_off[atoms[k]]);
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(hout, part[0] + part[1] + part[2] + part[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(hout + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Level 0: seed rows.  rows[i*W ..] is the mask row of unique seed atom atoms[i].
@@ -4082,24 +4099,33 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* n_fl = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 10;   // scratch slots
     u64* n_cl = n_fl + 1;
     u64* ticket = n_fl + 2;   // the finalise's last-block ticket (re-zeroed by that block)
-    if (!g->ctr_host) {       // two level slots of mapped, coherent host memory (once per graph)
-        void* hp = nullptr;
-        HGX_HIP(hipHostMalloc(&hp, sizeof(u64) * 2 * kHostSlot, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(hp, 0, sizeof(u64) * 2 * kHostSlot);
+    if (!g->ctr_host) {       // two level slots + the seed-volume slot of mapped, coherent host memory
+        void* hp = nullptr;  // (once per graph)
+        HGX_HIP(hipHostMalloc(&hp, sizeof(u64) * 3 * kHostSlot, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, sizeof(u64) * 3 * kHostSlot);
         g->ctr_host = (u64*)hp;
     }
+    if (!g->pend_ev[0])   // the two in-flight levels' events (once per graph)
+        for (int k = 0; k < 2; ++k) HGX_HIP(hipEventCreateWithFlags(&g->pend_ev[k], hipEventDisableTiming));
     bool chained = false, cand_clean = false;
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
     u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
     if (sparse_ok) {
-        u64* dv = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock;   // scratch slot
-        hgx_seed_degree<<<grid_for((int64_t)seed_atoms.size(), 256, 1 << 20), 256, 0, s>>>(
-            (int32_t)seed_atoms.size(), d_atoms, g->inc_off, dv);
+        u64* slot = g->ctr_host + 2 * kHostSlot;
+        const u64 seq = ++g->ctr_seq;
+        __atomic_store_n(slot + 1, (u64)0, __ATOMIC_RELEASE);
+        hgx_seed_degree_host<<<1, 256, 0, s>>>((int32_t)seed_atoms.size(), d_atoms, g->inc_off, slot, seq);
         HGX_CHECK_LAUNCH();
-        HGX_HIP(hipMemcpyAsync(&push_volume, dv, sizeof(u64), hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
+        for (unsigned spin = 0; __atomic_load_n(slot + 1, __ATOMIC_ACQUIRE) != seq; ++spin) {
+            if ((spin & 1023u) != 1023u) continue;   // the stream is asked every 1024 polls
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) HGX_HIP(e);
+            if (__atomic_load_n(slot + 1, __ATOMIC_ACQUIRE) != seq) fail(HGX_E_DEVICE, "batched BFS: seed volume never arrived");
+        }
+        push_volume = __atomic_load_n(slot, __ATOMIC_RELAXED);
         push_volume_nf = push_volume;
     }
     const u64 sparse_limit = (u64)std::max<int64_t>(M / 16, 1024);
@@ -4122,7 +4148,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     } pend[2];
     for (int k = 0; k < 2; ++k) {
         pend[k].h = h_sh + (size_t)k * kCtrBlock;
-        HGX_HIP(hipEventCreateWithFlags(&pend[k].ev, hipEventDisableTiming));
+        pend[k].ev = g->pend_ev[k];
     }
     int npend = 0;
     bool stop = false;
@@ -4489,7 +4515,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }
         }
     }
-    for (int k = 0; k < 2; ++k) (void)hipEventDestroy(pend[k].ev);
     if (ex) {
         res->stats.bytes_exchanged += ex->bytes_sent;
         res->stats.xwords_nonzero += ex->nz_words;
@@ -5079,3 +5104,24 @@ void hgx_bfs_result_free(hgx_bfs_result* r) {
 }
 
 }  // extern "C"
+
+// The read-only tables the BFS otherwise builds on first use -- the has-incidence bitmap (non-full
+// pull levels), the ordered-mode yield flags and the frontier-push chunk table -- built now on the
+// snapshot so that its execution contexts (hgx_graph_context) share one copy.  Caller holds g->mu.
+void hgx::bfs_shared_tables(hgx_graph* g) {
+    hipStream_t s = g->stream;
+    const int64_t A = g->A;
+    if (!g->hasinc) {
+        HGX_HIP(hipMalloc(&g->hasinc, sizeof(u64) * (size_t)(ceil_div(A, 64) + 1)));
+        hgx_hasinc<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, g->inc_off, (u64*)g->hasinc);
+        HGX_CHECK_LAUNCH();
+    }
+    if (!g->inc_yf) {
+        HGX_HIP(hipMalloc(&g->inc_yf, std::max<int64_t>(g->I, 1)));
+        hgx_inc_yield<<<grid_for(A * 64, 256, 8192), 256, 0, s>>>(A, g->inc_off, g->inc_row, g->tgt_off, g->tgt_idx,
+                                                               g->inc_yf);
+        HGX_CHECK_LAUNCH();
+    }
+    if (g->n_pchunks < 0) build_push_chunks(g);
+    HGX_HIP(hipStreamSynchronize(s));
+}

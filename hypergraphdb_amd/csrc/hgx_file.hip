@@ -279,7 +279,9 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_graph_update: not available on a partition shard");
     if (num_atoms < g->A) fail(HGX_E_INVALID, "hgx_graph_update: atoms cannot disappear from the id space");
     std::lock_guard<std::mutex> lk(g->mu);
-    if (g->refs.load() > 1) fail(HGX_E_INVALID, "hgx_graph_update: results of this graph are still alive");
+    if (g->base) fail(HGX_E_INVALID, "hgx_graph_update: apply store events to the snapshot, not to one of its contexts");
+    if (g->refs.load() > 1)
+        fail(HGX_E_INVALID, "hgx_graph_update: results or execution contexts of this graph are still alive");
     HGX_HIP(hipSetDevice(g->device));
     std::vector<int32_t> la, tg, ty;
     std::vector<int64_t> off;

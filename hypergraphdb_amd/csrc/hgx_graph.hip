@@ -30,14 +30,20 @@ void graph_release(hgx_graph* g) {
     g->pool.clear();
     for (auto e : g->ev_pool) (void)hipEventDestroy(e);
     g->ev_pool.clear();
-    (void)hipFree(g->link_atom); (void)hipFree(g->tgt_off); (void)hipFree(g->tgt_idx); (void)hipFree(g->link_type);
-    (void)hipFree(g->inc_off); (void)hipFree(g->inc_row); (void)hipFree(g->inc_type); (void)hipFree(g->inc_ts_row); (void)hipFree(g->inc_ts_type); (void)hipFree(g->inc_ts_tgt); (void)hipFree(g->heavy_atom); (void)hipFree(g->chunks);
+    for (auto e : g->pend_ev)
+        if (e) (void)hipEventDestroy(e);
+    // a context (hgx_graph_context) frees what it built itself, never an array borrowed from its base
+    hgx_graph* const b = g->base;
+#define HGX_FREE_OWN(f) \
+    if (g->f && (!b || (const void*)g->f != (const void*)b->f)) (void)hipFree(g->f)
+    HGX_FREE_OWN(link_atom); HGX_FREE_OWN(tgt_off); HGX_FREE_OWN(tgt_idx); HGX_FREE_OWN(link_type);
+    HGX_FREE_OWN(inc_off); HGX_FREE_OWN(inc_row); HGX_FREE_OWN(inc_type); HGX_FREE_OWN(inc_ts_row);
+    HGX_FREE_OWN(inc_ts_type); HGX_FREE_OWN(inc_ts_tgt); HGX_FREE_OWN(heavy_atom); HGX_FREE_OWN(chunks);
+    HGX_FREE_OWN(hasinc); HGX_FREE_OWN(inc_yf); HGX_FREE_OWN(pchunks);
+#undef HGX_FREE_OWN
     if (g->zacc) (void)hipFree(g->zacc);
-    if (g->hasinc) (void)hipFree(g->hasinc);
-    if (g->inc_yf) (void)hipFree(g->inc_yf);
     if (g->fcode) (void)hipFree(g->fcode);
     if (g->lcode) (void)hipFree(g->lcode);
-    if (g->pchunks) (void)hipFree(g->pchunks);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
     if (g->mapped) (void)hipHostFree(g->mapped);
@@ -53,6 +59,7 @@ void graph_release(hgx_graph* g) {
         delete g->shard;
     }
     delete g;
+    if (b) graph_release(b);   // the context's reference on its snapshot
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -266,6 +273,44 @@ int hgx_graph_create(const hgx_graph_desc* d, int32_t device, hgx_graph** out) {
     if (!d || !out) fail(HGX_E_INVALID, "hgx_graph_create: null argument");
     *out = nullptr;
     *out = graph_create(d, device, true);
+    HGX_API_END
+}
+
+int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
+    HGX_API_BEGIN
+    if (!g || !out) fail(HGX_E_INVALID, "hgx_graph_context: null argument");
+    *out = nullptr;
+    if (g->base) g = g->base;   // a context of a context is another context of the snapshot
+    if (g->shard)
+        fail(HGX_E_UNSUPPORTED, "hgx_graph_context: a partition shard runs one collective traversal at a time");
+    std::lock_guard<std::mutex> lk(g->mu);
+    HGX_HIP(hipSetDevice(g->device));
+    bfs_shared_tables(g);   // built once on the snapshot, read by every context
+    hgx_graph* c = new hgx_graph();
+    c->base = g;
+    g->refs.fetch_add(1);
+    struct Guard {
+        hgx_graph* c;
+        ~Guard() { if (c) graph_release(c); }
+    } guard{c};
+    c->device = g->device;
+    HGX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // the snapshot (borrowed)
+    c->A = g->A; c->M = g->M; c->P = g->P; c->I = g->I;
+    c->link_atom = g->link_atom; c->tgt_off = g->tgt_off; c->tgt_idx = g->tgt_idx; c->link_type = g->link_type;
+    c->inc_off = g->inc_off; c->inc_row = g->inc_row; c->inc_type = g->inc_type;
+    c->inc_ts_row = g->inc_ts_row; c->inc_ts_type = g->inc_ts_type; c->inc_ts_tgt = g->inc_ts_tgt;
+    c->n_heavy = g->n_heavy; c->I_heavy = g->I_heavy; c->n_chunks = g->n_chunks;
+    c->heavy_atom = g->heavy_atom; c->chunks = g->chunks;
+    c->hasinc = g->hasinc; c->inc_yf = g->inc_yf; c->pchunks = g->pchunks; c->n_pchunks = g->n_pchunks;
+    c->max_arity = g->max_arity; c->max_deg = g->max_deg;
+    // the snapshot's options at this point (set separately on the context afterwards)
+    c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
+    c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline; c->coded = g->coded;
+    c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused;
+    c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
+    guard.c = nullptr;
+    *out = c;
     HGX_API_END
 }
 

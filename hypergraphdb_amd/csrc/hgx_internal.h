@@ -187,6 +187,10 @@ struct hgx_comm {
 };
 
 struct hgx_graph {
+    // Execution context (hgx_graph_context): the snapshot's arrays are borrowed from base (which this
+    // context holds a reference on); the stream, lock, scratch pool, accumulator, counters and host
+    // staging are its own, so traversals on two contexts of one snapshot run side by side.
+    hgx_graph* base = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;      // readout counting next to the traversal (made on first use)
@@ -208,6 +212,7 @@ struct hgx_graph {
     uint64_t* zacc = nullptr;
     unsigned long long* ctr_host = nullptr;   // push levels' counters, written by the finalise (mapped host memory)
     unsigned long long ctr_seq = 0;          // sequence numbers of those writes
+    hipEvent_t pend_ev[2] = {nullptr, nullptr};   // the batched BFS's two in-flight level events
     uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
     uint8_t* inc_yf = nullptr;           // [I] ordered-mode yield flags per incidence (frontier push), made on first use
     hgx::HeavyChunk* pchunks = nullptr;  // frontier push: kPushChunk-entry chunks of atoms with deg > kPushLight
@@ -275,6 +280,9 @@ struct hgx_graph {
 
 namespace hgx {
 void graph_release(hgx_graph* g);   // drop a reference; frees at zero
+// Builds the BFS's first-use read-only tables (has-incidence bitmap, yield flags, push chunks) on g
+// (hgx_bfs.hip; caller holds g->mu).
+void bfs_shared_tables(hgx_graph* g);
 // Upload + incidence build.  links_are_atoms = false for partition shards: link rows then carry
 // their global link atom ids (not local atoms) and are not validated against num_atoms.
 hgx_graph* graph_create(const hgx_graph_desc* d, int32_t device, bool links_are_atoms);

@@ -203,7 +203,9 @@ void plan_links(const hgx_graph_desc* d, int NP, int32_t* link_part, double slac
                     const int64_t n = off[L + 1] - off[L];
                     int best = -1;
                     for (int q = 0; q < NP; ++q) {
-                        if (load[q] + dl[q] + n > cap) continue;
+                        // each chunk of the batch may fill 1/kPlanChunks of a part's room under the cap
+                        // (the chunks decide concurrently against the batch-start loads)
+                        if ((dl[q] + n) * kPlanChunks > cap - load[q]) continue;
                         if (best < 0 || score[q] > score[best] ||
                             (score[q] == score[best] && load[q] + dl[q] < load[best] + dl[best]))
                             best = q;

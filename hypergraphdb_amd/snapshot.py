@@ -261,6 +261,19 @@ class HyperGraphSnapshot:
         check(lib().hgx_graph_degree(self.handle, ptr(a), len(a), ptr(out)))
         return out
 
+    def context(self):
+        """An execution context of this snapshot (hgx_graph_context): shares the device arrays, has its
+        own stream, lock and scratch, so traversals on it run next to the ones on this snapshot (e.g.
+        from another thread).  Store reads go to the same host mirror."""
+        h = C.c_void_p()
+        check(lib().hgx_graph_context(self.handle, C.byref(h)))
+        ctx = type(self).__new__(type(self))
+        ctx._h = None
+        ctx._attach(h, self.device, self.A, self.link_atom, self.tgt_off, self.tgt_idx, self.link_type,
+                    self._keep_host)
+        ctx._row_of = self._row_of
+        return ctx
+
     def set_timing(self, on=True):
         check(lib().hgx_set_timing(self.handle, 1 if on else 0))
 

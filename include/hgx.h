@@ -4,7 +4,8 @@
  * Plain pointers and sizes only; no C++ or torch types.  Every entry point returns an
  * int status (HGX_OK = 0) and never throws or aborts across the ABI; the message of the
  * last failure on the calling thread is hgx_last_error().  All entry points are
- * thread-safe (one mutex per graph; calls on one graph are serialised).
+ * thread-safe (one mutex per graph; calls on one graph are serialised -- use one execution
+ * context per concurrent caller, hgx_graph_context, to run them side by side).
  *
  * Reference interfaces replaced (paths relative to the reference root,
  * C = core/src/java/org/hypergraphdb):
@@ -145,6 +146,15 @@ int hgx_device_count(int32_t *n);
 /* device: HIP device ordinal to place the snapshot on. */
 int  hgx_graph_create(const hgx_graph_desc *desc, int32_t device, hgx_graph **out);
 void hgx_graph_destroy(hgx_graph *g);
+/* An execution context of g's snapshot: an hgx_graph that borrows the device arrays (no copy) but has
+ * its own stream, lock, scratch pool, push accumulator, level counters and host staging, so
+ * traversals and pattern batches on different contexts of one snapshot run concurrently on the device
+ * (e.g. the hg.subsumed and hg.subsumes closures of one step, or the pool threads of
+ * TC/query/QueryCompilation.java:76-122).  It takes the snapshot's options at the time of the call;
+ * hgx_set_option / hgx_set_timing on it apply to it alone.  Release it with hgx_graph_destroy; it keeps
+ * the snapshot alive, and hgx_graph_update is refused while a context exists.  Not for partition
+ * shards (HGX_E_UNSUPPORTED). */
+int  hgx_graph_context(hgx_graph *g, hgx_graph **out);
 int  hgx_graph_info(const hgx_graph *g, int64_t *num_atoms, int64_t *num_links, int64_t *num_incidences);
 /* |inc(atom)| for n atoms (HyperGraph.getIncidenceSet(h).size()). */
 int  hgx_graph_degree(hgx_graph *g, const int32_t *atoms, int32_t n, int64_t *out_deg);

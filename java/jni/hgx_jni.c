@@ -194,6 +194,13 @@ JNIEXPORT jlong JFN(graphOpen)(JNIEnv *e, jclass k, jstring path, jint device) {
 
 JNIEXPORT void JFN(graphDestroy)(JNIEnv *e, jclass k, jlong g) { hgx_graph_destroy((hgx_graph *)(intptr_t)g); }
 
+JNIEXPORT jlong JFN(graphContext)(JNIEnv *e, jclass k, jlong g) {
+    hgx_graph *c = NULL;
+    int rc = hgx_graph_context((hgx_graph *)(intptr_t)g, &c);
+    if (rc) { throw_rc(e, rc); return 0; }
+    return (jlong)(intptr_t)c;
+}
+
 JNIEXPORT jlongArray JFN(graphInfo)(JNIEnv *e, jclass k, jlong g) {
     int64_t v[3];
     int rc = hgx_graph_info((hgx_graph *)(intptr_t)g, &v[0], &v[1], &v[2]);

@@ -19,6 +19,7 @@
  */
 package org.hypergraphdb.gpu;
 
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.Arrays;
 import java.util.Comparator;
@@ -65,6 +66,8 @@ public final class HGGpuSnapshot implements AutoCloseable
     private int orderedPrefix;                        // ranks below this are in handle order
     private final List<HGPersistentHandle> pendingAdd = new ArrayList<HGPersistentHandle>();
     private final List<HGPersistentHandle> pendingRemove = new ArrayList<HGPersistentHandle>();
+    private final ArrayDeque<Long> idleContexts = new ArrayDeque<Long>();   // hgx_graph_context handles
+    private int busyContexts;
     private final HGListener listener = new HGListener() {
         public Result handle(HyperGraph graph, HGEvent event)
         {
@@ -231,6 +234,16 @@ public final class HGGpuSnapshot implements AutoCloseable
     public synchronized void sync()
     {
         if (pendingAdd.isEmpty() && pendingRemove.isEmpty()) return;
+        while (busyContexts > 0)   // hgx_graph_update is refused while an execution context exists
+        {
+            try { wait(); }
+            catch (InterruptedException e)
+            {
+                Thread.currentThread().interrupt();
+                throw new HGException("interrupted while GPU traversals finish", e);
+            }
+        }
+        dropIdleContexts();
         int before = byRank.size();
         HGPersistentHandle maxOld = before > 0 ? byRank.get(orderedPrefix - 1) : null;
         boolean ordered = true;
@@ -285,6 +298,35 @@ public final class HGGpuSnapshot implements AutoCloseable
         return out;
     }
 
+    /**
+     * An execution context of the device snapshot for one traversal call (hgx_graph_context: the same
+     * device arrays, its own stream, lock and scratch), so traversals issued by several threads run
+     * side by side on the GPU instead of queueing on the snapshot's lock.  Pending store events are
+     * applied first.  Give it back with releaseContext (contexts are pooled).
+     */
+    synchronized long acquireContext()
+    {
+        sync();
+        busyContexts++;
+        Long c = idleContexts.poll();
+        if (c != null) return c;
+        try { return Hgx.graphContext(g); }
+        catch (RuntimeException e) { busyContexts--; notifyAll(); throw e; }
+    }
+
+    synchronized void releaseContext(long c)
+    {
+        busyContexts--;
+        idleContexts.push(c);
+        notifyAll();
+    }
+
+    private void dropIdleContexts()
+    {
+        for (Long c : idleContexts) Hgx.graphDestroy(c);
+        idleContexts.clear();
+    }
+
     public HyperGraph getGraph() { return graph; }
     public int getDevice() { return device; }
     long native_() { return g; }
@@ -296,6 +338,7 @@ public final class HGGpuSnapshot implements AutoCloseable
             graph.getEventManager().removeListener(HGAtomAddedEvent.class, listener);
             graph.getEventManager().removeListener(HGAtomRemovedEvent.class, listener);
             graph.getEventManager().removeListener(HGAtomReplacedEvent.class, listener);
+            dropIdleContexts();   // a context still in use keeps the device snapshot alive until released
             Hgx.graphDestroy(g);
             g = 0;
         }

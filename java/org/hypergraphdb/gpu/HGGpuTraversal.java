@@ -106,18 +106,22 @@ public class HGGpuTraversal implements HGTraversal
     private void init()
     {
         if (links != null || cpu != null) return;
-        snap.sync();
         int[] o = options(snap, gen);
         long s;
+        long ctx = snap.acquireContext();   // its own stream: traversals of other threads run alongside
         try
         {
-            s = Hgx.bfsSequence(snap.native_(), new int[] {snap.rank(start)}, depth(maxDistance), o[0], o[1] != 0,
+            s = Hgx.bfsSequence(ctx, new int[] {snap.rank(start)}, depth(maxDistance), o[0], o[1] != 0,
                                 o[2] != 0, o[3] != 0, o[4] != 0);
         }
         catch (UnsupportedOperationException e)
         {   // e.g. ranks appended out of handle order since the export: keep the reference traversal
             cpu = new HGBreadthFirstTraversal(start, gen, maxDistance);
             return;
+        }
+        finally
+        {
+            snap.releaseContext(ctx);   // the sequence result is host data
         }
         try
         {
@@ -180,12 +184,19 @@ public class HGGpuTraversal implements HGTraversal
     {
         int[] o = options(snap, gen);
         if (o == null) return null;
-        snap.sync();
-        int[] seeds = new int[starts.length];
-        for (int i = 0; i < starts.length; i++)
-            seeds[i] = snap.rank(starts[i]);
-        long s = Hgx.bfsSequence(snap.native_(), seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0,
-                                 o[4] != 0);
+        long ctx = snap.acquireContext();   // applies pending store events: ranks after it
+        long s;
+        try
+        {
+            int[] seeds = new int[starts.length];
+            for (int i = 0; i < starts.length; i++)
+                seeds[i] = snap.rank(starts[i]);
+            s = Hgx.bfsSequence(ctx, seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0, o[4] != 0);
+        }
+        finally
+        {
+            snap.releaseContext(ctx);
+        }
         try
         {
             long[] off = Hgx.seqOffsets(s);
@@ -216,12 +227,20 @@ public class HGGpuTraversal implements HGTraversal
     {
         int[] o = options(snap, gen);
         if (o == null) return null;
-        snap.sync();
-        int[] seeds = new int[starts.length];
-        for (int i = 0; i < starts.length; i++)
-            seeds[i] = snap.rank(starts[i]);
-        long r = Hgx.bfsBatch(snap.native_(), seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0,
-                              o[4] != 0);
+        long ctx = snap.acquireContext();   // applies pending store events: ranks after it
+        long r;
+        try
+        {
+            int[] seeds = new int[starts.length];
+            for (int i = 0; i < starts.length; i++)
+                seeds[i] = snap.rank(starts[i]);
+            r = Hgx.bfsBatch(ctx, seeds, depth(maxDistance), o[0], o[1] != 0, o[2] != 0, o[3] != 0, o[4] != 0);
+        }
+        catch (RuntimeException e)
+        {
+            snap.releaseContext(ctx);
+            throw e;
+        }
         try
         {
             int levels = Hgx.bfsInfo(r)[1];
@@ -238,6 +257,7 @@ public class HGGpuTraversal implements HGTraversal
         finally
         {
             Hgx.bfsFree(r);
+            snap.releaseContext(ctx);
         }
     }
 }

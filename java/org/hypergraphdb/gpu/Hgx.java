@@ -25,6 +25,7 @@ final class Hgx
                                    int device);
     static native long graphOpen(String path, int device);
     static native void graphDestroy(long g);
+    static native long graphContext(long g);                     // hgx_graph_context: one per concurrent caller
     static native long[] graphInfo(long g);                      // {num_atoms, num_links, num_incidences}
     static native void graphUpdate(long g, long numAtoms, int[] addLinkAtom, long[] addTgtOff, int[] addTgtIdx,
                                    int[] addLinkType, int[] removeLinkAtom);
