@@ -1819,6 +1819,20 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
     if (ne) drain();
 }
 
+// The nonzero words of a row (lane w holds word w, already loaded) into the wave's LDS table; returns
+// their count (wave-uniform).
+__device__ __forceinline__ int row_words_of(u64 x, OPushLds& sh) {
+    const int lane = threadIdx.x & 63;
+    const u64 nz = __ballot(x != 0ull);
+    if (x != 0ull) {
+        const int r = __popcll(nz & ((1ull << lane) - 1ull));
+        sh.widx[r] = lane;
+        sh.wval[r] = x;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return __popcll(nz);
+}
+
 // The nonzero words of v's row into the wave's LDS table; returns their count (wave-uniform).
 template <int W>
 __device__ __forceinline__ int row_words(const u64* __restrict__ lvl, int64_t v, OPushLds& sh) {
@@ -1936,14 +1950,41 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
                              n_scan, cc);
     }
     const int64_t n = (int64_t)*n_list;
-    for (int64_t k = wave; k < n; k += nwave) {
-        const int32_t v = list[k];
-        if (v < 0) continue;   // a candidate list reused as the frontier list: not new / not light
-        const int64_t beg = inc_off[v], end = inc_off[v + 1];   // in flight with the row load
-        const int nnz = row_words<W>(lvl, v, sh);
-        if (nnz == 0) continue;
-        opush_links<W, MODE>(v, beg, end, 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
-                             nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
+    // A wave pushes the atoms k, k + nwave, ... of the list one after the other; the list entry, the
+    // incidence range and the row of the NEXT atom (three dependent round trips of every atom) are
+    // loaded while this one is pushed.  A list entry < 0: a candidate list reused as the frontier list
+    // (not new / not light).
+    const int lane = threadIdx.x & 63;
+    auto list_at = [&](int64_t k) -> int32_t { return k < n ? list[k] : -1; };
+    int64_t k = wave;
+    int32_t v = list_at(k), vn = list_at(k + nwave);
+    int64_t beg = 0, end = 0;
+    u64 x = 0ull;
+    if (v >= 0) {
+        beg = inc_off[v];
+        end = inc_off[v + 1];
+        x = lane < W ? lvl[(int64_t)v * W + lane] : 0ull;
+    }
+    for (; k < n; k += nwave) {   // wave-uniform
+        const int32_t vnn = list_at(k + 2 * nwave);
+        int64_t nbeg = 0, nend = 0;
+        u64 nx = 0ull;
+        if (vn >= 0) {
+            nbeg = inc_off[vn];
+            nend = inc_off[vn + 1];
+            nx = lane < W ? lvl[(int64_t)vn * W + lane] : 0ull;
+        }
+        if (v >= 0) {
+            const int nnz = row_words_of(x, sh);
+            if (nnz)
+                opush_links<W, MODE>(v, beg, end, 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx, nnz, sh,
+                                     full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
+        }
+        v = vn;
+        vn = vnn;
+        beg = nbeg;
+        end = nend;
+        x = nx;
     }
     cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);

@@ -2217,15 +2217,30 @@ struct Scratch {
     ~Scratch() { for (auto& x : t) g->release(x.first, x.second); }
 };
 
+// Timing events of one batch, taken from the graph's pool and given back (an event create + destroy
+// per batch costs more host time than the batch's match kernel).  The caller holds g->mu.
 struct Events {
+    hgx_graph* g = nullptr;
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
     bool on = false;
-    void init(bool timing) {
-        on = timing;
-        if (on) for (int i = 0; i < 4; ++i) HGX_HIP(hipEventCreate(&e[i]));
+    void init(hgx_graph* gg) {
+        g = gg;
+        on = gg->timing;
+        if (!on) return;
+        for (int i = 0; i < 4; ++i) {
+            if (!g->ev_pool.empty()) {
+                e[i] = g->ev_pool.back();
+                g->ev_pool.pop_back();
+            } else {
+                HGX_HIP(hipEventCreate(&e[i]));
+            }
+        }
     }
     void rec(int i, hipStream_t s) { if (on) HGX_HIP(hipEventRecord(e[i], s)); }
-    ~Events() { for (int i = 0; i < 4; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
+    ~Events() {
+        for (int i = 0; i < 4; ++i)
+            if (e[i]) g->ev_pool.push_back(e[i]);
+    }
 };
 
 template <class T>
@@ -2730,7 +2745,7 @@ bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_
     int32_t* big_n = (int32_t*)(d + o_stat) + 4;
     int64_t* ovf_claim = (int64_t*)(d + o_ovfn);   // zeroed by the upload
     Events ev;
-    ev.init(g->timing);
+    ev.init(g);
     ev.rec(0, s);
     HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
     for (int attempt = 0;; ++attempt) {
@@ -2833,7 +2848,7 @@ int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn fron
         ensure_ts_inline(g);
         Scratch sc{g, {}};
         Events ev;
-        ev.init(g->timing);
+        ev.init(g);
         Front f;
         front(sc, ev, f);
         back_end(g, n, f, sc, ev, r.get(), prof, t0);

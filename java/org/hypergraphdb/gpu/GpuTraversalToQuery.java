@@ -27,7 +27,7 @@
  *
  * Many traversals at once: executeBatch(...) runs every start atom of a list of conditions in ONE
  * hgx_bfs_sequence call (the engine's unit of work is a batch: a single seed pays the whole fixed
- * launch and copy cost, profiles/r03*_single_latency.json).
+ * launch and copy cost, profiles/r03d_single_latency.json).
  *
  * Executed through the JNI shim by tests/test_gpu_jni.py (fake JNIEnv); the Java itself is not
  * compiled here: no JDK exists in this build image.
