@@ -239,10 +239,10 @@ def run_config4(args, ctx, barrier_sync, result):
         for _ in range(n_steps):
             r = run()
             r.counts()   # the readout
-            st.append(r.stats(accounting=False))
+            st.append(r.stats(accounting=False, raw=True))
             r.close()
         barrier_sync()
-        return ctx.max(time.perf_counter() - t1), st
+        return ctx.max(time.perf_counter() - t1), [x.as_dict() for x in st]
 
     # replicated snapshot, one 1024-source batch per GPU
     t0 = time.time()
@@ -335,7 +335,7 @@ def run_config5(args, ctx, barrier_sync):
     def direction(k, accounting=False):
         r = H.bfs_batch(views[k], g["seeds"], None, gens[k])
         n = int(r.counts()[:, 1:].sum())   # the result readout: per-class closure sizes per depth (D2H)
-        st = r.stats(accounting=accounting)
+        st = r.stats(accounting=accounting, raw=not accounting)   # raw structs: converted after the timed loop
         r.close()
         return n, st
 
@@ -368,6 +368,7 @@ def run_config5(args, ctx, barrier_sync):
             sts.append(st)
     barrier_sync()
     dt = ctx.max(time.perf_counter() - t1)
+    sts = [x.as_dict() for x in sts]
     pool.shutdown()
     views[1].close()
     assert readout == closure * args.steps, "config-5 readout differs from the warm-up closures"
@@ -569,7 +570,7 @@ def main():
         tb = time.perf_counter()
         readout += int(res.counts().sum())   # the result readout: per-source per-depth counts (D2H)
         tc = time.perf_counter()
-        stats.append(res.stats(accounting=False))
+        stats.append(res.stats(accounting=False, raw=True))
         res.close()
         phase["bfs_batch"] += tb - ta
         phase["readout"] += tc - tb
@@ -578,6 +579,7 @@ def main():
     log(f"rank {rank}: host wall per step (ms): " +
         ", ".join(f"{k} {v / max(args.steps, 1) * 1e3:.3f}" for k, v in phase.items()))
     dt = max_over_ranks(time.perf_counter() - t0)
+    stats = [x.as_dict() for x in stats]
     assert readout == args.steps * acct_visits, "readout differs from the warm-up batch"
     edges_total = sum_over_ranks(acct["traversed_edges"] * args.steps)
     teps = edges_total / dt

@@ -109,12 +109,13 @@ class BfsResult:
         check(lib().hgx_bfs_result_depth_of(self._h, int(seed_index), int(atom), C.byref(d)))
         return d.value
 
-    def stats(self, accounting=True) -> dict:
+    def stats(self, accounting=True, raw=False):
         """Kernel timings (timing enabled), algorithmic bytes; with ``accounting`` also the
-        TEPS numerator, |U_d| and the SURVEY.md 8(d) bytes (runs the accounting kernels)."""
+        TEPS numerator, |U_d| and the SURVEY.md 8(d) bytes (runs the accounting kernels).
+        ``raw``: the hgx_bfs_stats struct itself (``.as_dict()`` later, outside a timed loop)."""
         s = _lib.BfsStats()
         check(lib().hgx_bfs_result_stats(self._h, 1 if accounting else 0, C.byref(s)))
-        return s.as_dict()
+        return s if raw else s.as_dict()
 
     def close(self):
         if self._h is not None:

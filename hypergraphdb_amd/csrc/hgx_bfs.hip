@@ -3583,6 +3583,41 @@ inline int count_grid(int64_t A) {
 }
 
 constexpr int kDirectLevels = 256;   // levels whose push-level counts the finalise accumulates
+constexpr int kZeroLevels = 64;      // level counter blocks / count rows cleared per launch
+
+// Up to kZeroParts device ranges cleared by one launch (a traversal's prologue cleared six buffers
+// with six fill launches, each a few microseconds of device time and a gap).
+constexpr int kZeroParts = 8;
+struct ZeroSpans {
+    u64* p[kZeroParts];
+    int64_t n[kZeroParts];   // words
+    int k;
+};
+__global__ void __launch_bounds__(256) hgx_zero_multi(ZeroSpans z) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+    for (int j = 0; j < z.k; ++j) {
+        u64x2* p = reinterpret_cast<u64x2*>(z.p[j]);
+        const int64_t n2 = z.n[j] >> 1;
+        for (int64_t i = t; i < n2; i += nt) p[i] = u64x2{0ull, 0ull};
+        if ((z.n[j] & 1) && t == 0) z.p[j][z.n[j] - 1] = 0ull;
+    }
+}
+struct ZeroList {
+    ZeroSpans z{};
+    int64_t most = 0;
+    void add(void* p, size_t bytes) {
+        if (z.k == kZeroParts) fail(HGX_E_DEVICE, "ZeroList: too many spans");
+        z.p[z.k] = (u64*)p;
+        z.n[z.k] = (int64_t)(bytes / sizeof(u64));
+        most = std::max(most, z.n[z.k]);
+        ++z.k;
+    }
+    void launch(hipStream_t s) {
+        if (z.k == 0) return;
+        hgx_zero_multi<<<grid_for(std::max<int64_t>(most / 2, 1), 256, 2048), 256, 0, s>>>(z);
+        HGX_CHECK_LAUNCH();
+    }
+};
 
 struct BfsBatch {
     int32_t seed0 = 0, S = 0, W = 0;
@@ -3783,9 +3818,11 @@ struct Exchange {
     std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast; records), NP + 1 entries
     double bytes_sent = 0, nz_words = 0, words = 0;
     int static_levels = 0;              // levels exchanged through the static slots
+    u64* hpin = nullptr;                // pinned landing area of the cursor / stats read-backs
     Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts;
+        HGX_HIP(hipHostMalloc(&hpin, sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride), hipHostMallocDefault));
         rseg.assign(NP + 1, 0);
         bseg.assign(NP + 1, 0);
         for (int q = 0; q < NP; ++q) {
@@ -3810,7 +3847,14 @@ struct Exchange {
         HGX_HIP(hipMemcpyAsync(seg, hs.data(), sizeof(int64_t) * 4 * NP, hipMemcpyHostToDevice, g->stream));
         HGX_HIP(hipStreamSynchronize(g->stream));   // hs is a local
     }
+    // cursor / stats words back to the host (pinned copy, polled: no staging, no sleeping wait)
+    void read_back(std::vector<u64>& hc, size_t cbytes) {
+        HGX_HIP(hipMemcpyAsync(hpin, dctr, cbytes, hipMemcpyDeviceToHost, g->stream));
+        spin_sync(g->stream);
+        std::memcpy(hc.data(), hpin, cbytes);
+    }
     ~Exchange() {
+        if (hpin) (void)hipHostFree(hpin);
         const int NP = g->shard->n_parts;
         g->release(send_h, sizeof(u64) * 2 * (size_t)cap_recs);
         g->release(recv_h, sizeof(u64) * 2 * (size_t)cap_recs);
@@ -3886,8 +3930,7 @@ struct Exchange {
         };
         std::vector<int64_t> rcnt;
         auto read_counts = [&]() {
-            HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
-            HGX_HIP(hipStreamSynchronize(s));
+            read_back(hc, cbytes);
             for (int q = 0; q < NP; ++q) {
                 cnt[q] = hc[(size_t)q * kCurStride];
                 wcnt[q] = hc[(size_t)q * kCurStride + 16];
@@ -3920,8 +3963,7 @@ struct Exchange {
                 A, fa_next, (const u64*)sh.own_bm, lvl_next, xs);
             HGX_CHECK_LAUNCH();
             tm.stop(eg);
-            HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
-            HGX_HIP(hipStreamSynchronize(s));
+            read_back(hc, cbytes);
             int64_t mine2[4] = {(int64_t)stat_sum(3), rseg[NP], (int64_t)stat_sum(4), (int64_t)stat_sum(5)};
             std::vector<int64_t> all2(4 * (size_t)NP);
             coll([&] { tr->allgather_i64(mine2, 4, all2.data(), s); });
@@ -3998,8 +4040,7 @@ struct Exchange {
                      double* pair_max, double before, double pm) {
         const int NP = g->shard->n_parts;
         hipStream_t s = g->stream;
-        HGX_HIP(hipMemcpyAsync(hc.data(), dctr, cbytes, hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
+        read_back(hc, cbytes);
         const u64 fs[2] = {stat_sum(0), stat_sum(1)};
         *push_volume = fs[1];
         *level_bytes = bytes_sent - before;
@@ -4066,24 +4107,35 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     u64* ctr = (u64*)g->alloc(sizeof(u64) * kCtrBlock * max_levels_cap);
     int32_t* d_atoms = (int32_t*)g->alloc(sizeof(int32_t) * seed_atoms.size());
     u64* d_rows = (u64*)g->alloc(sizeof(u64) * seed_rows.size());
-    u64* h_sh = (u64*)g->pinned_buf(sizeof(u64) * kCtrBlock * 2);   // two levels in flight
+    // one pinned region: two levels' counters in flight, then the seed atoms and rows going up (a copy
+    // from pageable memory is staged by the runtime and holds the host)
+    const size_t o_atoms = sizeof(u64) * kCtrBlock * 2;
+    const size_t o_rows = (o_atoms + sizeof(int32_t) * seed_atoms.size() + 15) & ~(size_t)15;
+    char* hp = (char*)g->pinned_buf(o_rows + sizeof(u64) * seed_rows.size());
+    u64* h_sh = (u64*)hp;
     u64 h_new[cNum];
+    std::memcpy(hp + o_atoms, seed_atoms.data(), sizeof(int32_t) * seed_atoms.size());
+    std::memcpy(hp + o_rows, seed_rows.data(), sizeof(u64) * seed_rows.size());
 
-    HGX_HIP(hipMemsetAsync(ever, 0, bm_bytes, s));
-    HGX_HIP(hipMemsetAsync(full, 0, bm_bytes, s));
-    if (!tr) {   // per-source counts of push levels, accumulated by their finalise (readout without a pass)
-        bt.pcnt = (u64*)g->alloc(sizeof(u64) * 1024 * kDirectLevels);
-        HGX_HIP(hipMemsetAsync(bt.pcnt, 0, sizeof(u64) * 1024 * kDirectLevels, s));
-        bt.direct.assign(kDirectLevels, 0);
-    }
-    HGX_HIP(hipMemsetAsync(hubacc, 0, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W, s));
-    HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kCtrBlock * max_levels_cap, s));
-    HGX_HIP(hipMemcpyAsync(d_atoms, seed_atoms.data(), sizeof(int32_t) * seed_atoms.size(), hipMemcpyHostToDevice, s));
-    HGX_HIP(hipMemcpyAsync(d_rows, seed_rows.data(), sizeof(u64) * seed_rows.size(), hipMemcpyHostToDevice, s));
-
+    // the prologue's buffers cleared by one launch; level counter blocks (and push-level count rows)
+    // are cleared kZeroLevels at a time as the traversal reaches them
     bt.lvl.push_back((u64*)g->alloc(row_bytes));
     bt.fa.push_back((u64*)g->alloc(bm_bytes));
-    HGX_HIP(hipMemsetAsync(bt.fa[0], 0, bm_bytes, s));
+    ZeroList z{};
+    z.add(ever, bm_bytes);
+    z.add(full, bm_bytes);
+    z.add(bt.fa[0], bm_bytes);
+    z.add(hubacc, sizeof(u64) * (size_t)std::max<int64_t>(g->n_heavy, 1) * W);
+    z.add(ctr, sizeof(u64) * kCtrBlock * kZeroLevels);
+    z.add(ctr + (size_t)(max_levels_cap - 1) * kCtrBlock, sizeof(u64) * kCtrBlock);   // scratch slots
+    if (!tr) {   // per-source counts of push levels, accumulated by their finalise (readout without a pass)
+        bt.pcnt = (u64*)g->alloc(sizeof(u64) * 1024 * kDirectLevels);
+        z.add(bt.pcnt, sizeof(u64) * 1024 * kZeroLevels);
+        bt.direct.assign(kDirectLevels, 0);
+    }
+    z.launch(s);
+    HGX_HIP(hipMemcpyAsync(d_atoms, hp + o_atoms, sizeof(int32_t) * seed_atoms.size(), hipMemcpyHostToDevice, s));
+    HGX_HIP(hipMemcpyAsync(d_rows, hp + o_rows, sizeof(u64) * seed_rows.size(), hipMemcpyHostToDevice, s));
     {
         int n = (int)seed_atoms.size();
         hgx_seed<W><<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, d_atoms, d_rows, bt.lvl[0], vis, bt.fa[0], ever,
@@ -4256,6 +4308,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     };
 
     for (int32_t d = 0; d < maxd && d < max_levels_cap - 1 && !stop; ++d) {
+        if ((d + 1) % kZeroLevels == 0) {   // the next kZeroLevels counter blocks / count rows
+            ZeroList zl{};
+            const int64_t b0 = d + 1, b1 = std::min<int64_t>(b0 + kZeroLevels, max_levels_cap - 1);
+            zl.add(ctr + (size_t)b0 * kCtrBlock, sizeof(u64) * kCtrBlock * (size_t)(b1 - b0));
+            if (bt.pcnt && b0 < kDirectLevels)
+                zl.add(bt.pcnt + (size_t)b0 * 1024, sizeof(u64) * 1024 * (size_t)(std::min<int64_t>(b1, kDirectLevels) - b0));
+            zl.launch(s);
+        }
         u64* lvl = cur_lvl;
         u64* fa = cur_fa;
         bool codes_written = false;   // this level's finalise wrote the codes of its new rows
@@ -4547,7 +4607,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 stop = true;
                 for (; npend > 0; --npend) {   // a level issued after the last frontier: its rows are empty
                     Pend& q = pend[(d - npend + 1) & 1];
-                    if (q.flag) HGX_HIP(hipStreamSynchronize(s));
+                    if (q.flag) spin_sync(s);
                     else wait_event(q.ev);
                     g->release(q.lvl_next, row_bytes);
                     g->release(q.fa_next, bm_bytes);
@@ -4624,6 +4684,40 @@ void ensure_counts(hgx_bfs_result* r) {
     hgx_graph* g = r->g;
     HGX_HIP(hipSetDevice(g->device));
     r->counts.assign((size_t)r->n_seeds * r->n_levels, 0);
+    // Traversals made of push levels (config 5's closures): every level past the seeds was counted by
+    // its push finalise, and level 0 of a whole-graph batch is {seed} (count 1 each) -- the readout is
+    // one copy of the count rows, no counting pass and no reduce launch.
+    bool all_direct = !g->shard;
+    size_t rows = 0;
+    for (auto& bt : r->batches) {
+        all_direct = all_direct && bt.cpart.empty() && bt.pcnt;
+        for (size_t d = 1; all_direct && d < bt.lvl.size(); ++d) all_direct = d < bt.direct.size() && bt.direct[d];
+        rows += bt.lvl.empty() ? 0 : bt.lvl.size() - 1;
+    }
+    if (all_direct) {
+        u64* hc = (u64*)g->pinned_buf(sizeof(u64) * 1024 * std::max<size_t>(rows, 1));
+        size_t o = 0;
+        for (auto& bt : r->batches) {
+            const size_t nl = bt.lvl.size();
+            if (nl > 1)
+                HGX_HIP(hipMemcpyAsync(hc + o * 1024, bt.pcnt + 1024, sizeof(u64) * 1024 * (nl - 1), hipMemcpyDeviceToHost,
+                                       g->stream));
+            o += nl > 0 ? nl - 1 : 0;
+        }
+        spin_sync(g->stream);
+        o = 0;
+        for (auto& bt : r->batches) {
+            const size_t nl = bt.lvl.size();
+            for (int s = 0; s < bt.S; ++s) {
+                int64_t* c = &r->counts[(size_t)(bt.seed0 + s) * r->n_levels];
+                if (nl > 0) c[0] = 1;   // V_0 = {seed}
+                for (size_t d = 1; d < nl; ++d) c[d] = (int64_t)hc[(o + d - 1) * 1024 + s];
+            }
+            o += nl > 0 ? nl - 1 : 0;
+        }
+        r->counts_ready = true;
+        return;
+    }
     size_t nslots = 0;
     for (auto& bt : r->batches) nslots += bt.lvl.size();
     const int grid = count_grid(g->A);
@@ -4709,7 +4803,7 @@ void ensure_counts(hgx_bfs_result* r) {
     }
     const u64* hc = (const u64*)(hm + o_back);
     HGX_HIP(hipMemcpyAsync(hm + o_back, dc, bytes, hipMemcpyDeviceToHost, g->stream));
-    HGX_HIP(hipStreamSynchronize(g->stream));
+    spin_sync(g->stream);
     g->release(dc, bytes);
     g->release(dp, pbytes);
     g->release(dm, mbytes);
@@ -4878,8 +4972,9 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         bt.seed0 = s0;
         bt.S = std::min<int32_t>(1024, n_seeds - s0);
         bt.W = words_for(bt.S);
-        // unique seed atoms (ascending) and their rows
-        std::map<int32_t, std::vector<u64>> rows;
+        // unique seed atoms (ascending) and their rows: (atom, source bit) pairs sorted by atom
+        std::vector<std::pair<int32_t, int32_t>> at;
+        at.reserve((size_t)bt.S);
         for (int32_t i = 0; i < bt.S; ++i) {
             int32_t a = seeds[s0 + i];
             if (shp) {   // every part holding the seed starts from it (its links are spread over them)
@@ -4890,15 +4985,19 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                 }
                 a = l;
             }
-            auto& row = rows[a];
-            if (row.empty()) row.assign(bt.W, 0ull);
-            row[i >> 6] |= 1ull << (i & 63);
+            at.emplace_back(a, i);
         }
+        std::sort(at.begin(), at.end());
         std::vector<int32_t> sa;
         std::vector<u64> sr;
-        for (auto& kv : rows) {
-            sa.push_back(kv.first);
-            sr.insert(sr.end(), kv.second.begin(), kv.second.end());
+        sa.reserve(at.size());
+        sr.reserve(at.size() * (size_t)bt.W);
+        for (size_t k = 0; k < at.size(); ++k) {
+            if (k == 0 || at[k].first != at[k - 1].first) {
+                sa.push_back(at[k].first);
+                sr.insert(sr.end(), (size_t)bt.W, 0ull);
+            }
+            sr[(sa.size() - 1) * (size_t)bt.W + (at[k].second >> 6)] |= 1ull << (at[k].second & 63);
         }
         size_t before = level_ctr.size();
         switch (bt.W) {
@@ -4984,7 +5083,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         r->batches.push_back(std::move(bt));
     }
     if (tm.on) HGX_HIP(hipEventRecord(tm.all.b, g->stream));
-    HGX_HIP(hipStreamSynchronize(g->stream));
+    spin_sync(g->stream);
     int nl = 1;
     for (auto& bt : r->batches) nl = std::max(nl, (int)bt.lvl.size());
     r->n_levels = nl;

@@ -290,6 +290,14 @@ hgx_graph* graph_create(const hgx_graph_desc* d, int32_t device, bool links_are_
 void pbfs_run(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
               const hgx_algen_opts* opts, hgx_bfs_result** out);
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+// Waits for the work enqueued on s by polling: hipStreamSynchronize sleeps and wakes tens of
+// microseconds after the last kernel, a cost per call of the short pattern batches.
+inline void spin_sync(hipStream_t s) {
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    HGX_HIP(e);
+}
 inline int grid_for(int64_t work_items, int block, int max_blocks = 8192) {
     int64_t b = ceil_div(work_items > 0 ? work_items : 1, block);
     return (int)(b < max_blocks ? b : max_blocks);

@@ -2416,7 +2416,7 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
         hgx_q_offsets_flat<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, nch, coff, outoff, hmask, stat_d, qoff_d);
         HGX_CHECK_LAUNCH();
         ev.rec(3, s);
-        HGX_HIP(hipStreamSynchronize(s));
+        spin_sync(s);
         const int64_t* stat = (const int64_t*)(hm + m_stat);
         const u64* ctr_h = (const u64*)(hm + m_ctr);
         const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
@@ -2528,7 +2528,7 @@ void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, h
         char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
         HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
         ev.rec(3, s);
-        HGX_HIP(hipStreamSynchronize(s));
+        spin_sync(s);
         const int64_t* stat = (const int64_t*)(hm + m_stat);
         const u64* ctr_h = (const u64*)(hm + m_ctr);
         const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
@@ -2661,7 +2661,7 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
         char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
         HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
         ev.rec(3, s);
-        HGX_HIP(hipStreamSynchronize(s));
+        spin_sync(s);
         const int64_t* stat = (const int64_t*)(hm + m_stat);
         const u64* ctr_h = (const u64*)(hm + m_ctr);
         const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);

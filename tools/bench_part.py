@@ -7,9 +7,12 @@ Per level it reports, over the parts: the largest per-part device time (local ex
 apply kernels of the exchange), the bytes each part ships, and the largest bytes one part sends to
 ONE peer (an all-to-all over xGMI runs its 7 peer links in parallel, each at ~153 GB/s:
 MI355X_MICROARCH / SURVEY.md 5).  The modelled NP-GPU level time is
-    max_p device_ms(p) + max_pair_bytes / 153 GB/s
+    max_p device_ms(p) + max_pair_bytes / 153 GB/s + host round trips x --sync-us
 (no overlap of exchange and compute assumed), summed over the levels; the 1-part run is the
-replica on one GPU.  Counts of every source must equal the replica's.
+replica on one GPU.  Host round trips of a level (compressed records): the two count read-backs,
+the two count all-gathers and the termination all-gather (5; the all-to-alls are ordered on the
+stream without a host wait); --sync-us prices one (a small RCCL collective or a read-back at 8
+ranks, default 40 us).  Counts of every source must equal the replica's.
 
   python tools/bench_part.py --scale 0.25 --parts 1 8 --out gpurun_out/part.json
 """
@@ -34,6 +37,7 @@ def main():
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--out", default="")
+    ap.add_argument("--sync-us", type=float, default=40.0, help="price of one host round trip of the exchange")
     ap.add_argument("--xmode", type=int, nargs="+", default=[0],
                     help="HGX_OPT_PART_EXCHANGE values to measure at NP > 1 (0 auto, 1 records, 2 static slots)")
     args = ap.parse_args()
@@ -70,7 +74,7 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"scale": args.scale, "sources": args.sources, "depth": args.depth,
-                       "xgmi_link_GBps": XGMI_LINK_GBS, "rows": rows}, f, indent=1)
+                       "xgmi_link_GBps": XGMI_LINK_GBS, "host_sync_us": args.sync_us, "rows": rows}, f, indent=1)
 
 
 def measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state):
@@ -101,9 +105,11 @@ def measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state):
             pm = max(max((s[p]["level_xpair_max"][d] for s in sts if d < len(s[p]["level_xpair_max"])), default=0)
                      for p in range(NP))
             link_ms = pm / (XGMI_LINK_GBS * 1e9) * 1e3
+            sync_ms = (5 * args.sync_us / 1e3) if NP > 1 else 0.0
             levels.append({"max_part_device_ms": round(max(dev), 3), "max_part_exchange_kernels_ms": round(max(xms), 3),
                            "bytes_per_part_max": max(xb), "max_pair_bytes": pm, "max_pair_link_ms": round(link_ms, 3),
-                           "model_level_ms": round(max(dev) + link_ms, 3),
+                           "host_sync_ms": round(sync_ms, 3),
+                           "model_level_ms": round(max(dev) + link_ms + sync_ms, 3),
                            "exchange_below_compute": link_ms < max(dev) - max(xms)})
         model_ms = sum(lv["model_level_ms"] for lv in levels)
         per = []

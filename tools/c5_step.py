@@ -37,7 +37,7 @@ def main():
     def direction(k):
         r = H.bfs_batch(views[k], g["seeds"], None, gens[k])
         n = int(r.counts()[:, 1:].sum())
-        st = r.stats(accounting=False)
+        st = r.stats(accounting=False, raw=True)
         r.close()
         return n, st
 
@@ -63,9 +63,9 @@ def main():
         assert closures == ref, "closure sizes differ between modes"
         key = "concurrent" if conc else "serial"
         out[key] = {"ms_per_step": round(ms, 4), "closure_atoms": closures,
-                    "levels": [st["n_levels_expanded"] for _, st in res[0]]}
+                    "levels": [st.n_levels_expanded for _, st in res[0]]}
         if args.timing:
-            out[key]["device_ms"] = [round(st["ms_total"], 4) for _, st in res[-1]]
+            out[key]["device_ms"] = [round(st.ms_total, 4) for _, st in res[-1]]
         print(f"[c5] {key}: {ms:.3f} ms/step", file=sys.stderr, flush=True)
     pool.shutdown()
     views[1].close()
