@@ -1,5 +1,6 @@
-"""GPU parity at BASELINE.json's full sizes (configs 2, 3 and 5; config 4 runs the same engine on
-a compacted shard and is covered at reduced size by test_gpu_partition.py).
+"""GPU parity at BASELINE.json's full sizes (configs 2, 3, 4 and 5; config 4's 8-part vertex cut
+against its one-part replica at full size, against the oracle at reduced size in
+test_gpu_partition.py).
 
 Where the C oracle finishes in seconds the check is exact (config 3: all 10,000 queries;
 config 5: every closure in both directions; config 2: every set up to depth 2 for a sample of
@@ -157,3 +158,43 @@ def test_config5_full_closures_vs_oracle(reverse):
             assert np.array_equal(res.visited(i, d_), exp), (i, d_)
     res.close()
     snap.close()
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_eight_parts_vs_replica():
+    """Config 4 at full size (100M nodes / 200M links, 1.0B incidences, 1024 sources, depth 4): the
+    8-part vertex cut (hgx_pbfs_batch_group, in-process transport on one GPU) gives every source's
+    per-depth counts of the whole graph run as ONE part (the replica), and the parts' TEPS numerators
+    sum to the replica's.  The oracle is too slow at this size; it pins the same
+    code at 0.2% scale (test_gpu_partition.py::test_config4_eight_parts_vs_oracle)."""
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd.partition import Shard, ShardSnapshot, partition_plan, pbfs_batch_group
+    g = synth.config4()
+    seeds = np.asarray(g["seeds"], np.int32)
+    args = (g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    sh = Shard.build(*args, 1, 0, np.zeros(len(g["link_atom"]), np.int32))
+    rep = ShardSnapshot(sh, 0)
+    sh.close()
+    r = pbfs_batch_group([rep], seeds, 4)
+    ref = r.counts()
+    ref_tr = r.stats(accounting=True)[0]["traversed_edges"]
+    r.close()
+    rep.close()
+    assert ref.shape == (1024, 5) and np.all(ref[:, 0] == 1) and ref[:, 4].sum() > 0
+    plan = partition_plan(*args, 8)
+    parts = []
+    try:
+        for p in range(8):
+            s = Shard.build(*args, 8, p, plan)
+            parts.append(ShardSnapshot(s, 0))
+            s.close()
+        del g, args, plan
+        r = pbfs_batch_group(parts, seeds, 4)
+        got = r.counts()
+        tr = sum(x["traversed_edges"] for x in r.stats(accounting=True))
+        r.close()
+        assert np.array_equal(got, ref)
+        assert tr == ref_tr
+    finally:
+        for x in parts:
+            x.close()

@@ -8,6 +8,8 @@ its readout), the two directions one after the other and side by side on two exe
 """
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 import time
@@ -23,19 +25,24 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="both", choices=("both", "serial", "concurrent"))
     ap.add_argument("--timing", action="store_true", help="device events per level (adds event records)")
+    ap.add_argument("--split", type=int, default=1,
+                    help="concurrent mode: each direction's sources in this many batches, each on its own context")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, synth
     g = synth.config5(scale=args.scale, n_sources=1024)
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     snap.set_timing(args.timing)
-    views = [snap, snap.context()]
+    K = max(1, args.split)
+    views = [snap] + [snap.context() for _ in range(2 * K - 1)]
     T = g["subsumes_type"]
-    gens = [DefaultALGenerator(v, AtomTypeCondition(T), None, False, True, rev) for v, rev in zip(views, (False, True))]
-    pool = ThreadPoolExecutor(1)
+    # job j: direction j % 2 (subsumed / subsumes), source batch j // 2 of K
+    gens = [DefaultALGenerator(v, AtomTypeCondition(T), None, False, True, bool(j % 2)) for j, v in enumerate(views)]
+    parts = np.array_split(np.asarray(g["seeds"], np.int32), K)
+    pool = ThreadPoolExecutor(2 * K - 1)
 
-    def direction(k):
-        r = H.bfs_batch(views[k], g["seeds"], None, gens[k])
+    def job(j, seeds=None):
+        r = H.bfs_batch(views[j], parts[j // 2] if seeds is None else seeds, None, gens[j])
         n = int(r.counts()[:, 1:].sum())
         st = r.stats(accounting=False, raw=True)
         r.close()
@@ -43,12 +50,13 @@ def main():
 
     def step(concurrent):
         if not concurrent:
-            return [direction(0), direction(1)]
-        f = pool.submit(direction, 1)
-        a = direction(0)
-        return [a, f.result()]
+            return [job(0, g["seeds"]), job(1, g["seeds"])]
+        fs = [pool.submit(job, j) for j in range(1, 2 * K)]
+        res = [job(0)] + [f.result() for f in fs]
+        # per direction: closure atoms summed over the source batches, the batches' stats
+        return [(sum(res[j][0] for j in range(d, 2 * K, 2)), res[d][1]) for d in (0, 1)]
 
-    out = {"tool": "tools/c5_step.py", "scale": args.scale, "steps": args.steps}
+    out = {"tool": "tools/c5_step.py", "scale": args.scale, "steps": args.steps, "split": K}
     modes = {"both": (False, True), "serial": (False,), "concurrent": (True,)}[args.mode]
     ref = None
     for conc in modes:
@@ -68,7 +76,8 @@ def main():
             out[key]["device_ms"] = [round(st.ms_total, 4) for _, st in res[-1]]
         print(f"[c5] {key}: {ms:.3f} ms/step", file=sys.stderr, flush=True)
     pool.shutdown()
-    views[1].close()
+    for v in views[1:]:
+        v.close()
     snap.close()
     print(json.dumps(out))
 
