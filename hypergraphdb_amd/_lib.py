@@ -47,7 +47,8 @@ EXPORTED = (
     "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
     "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
-    "hgx_graph_update", "hgx_query_coalesce_stats",
+    "hgx_graph_update", "hgx_query_coalesce_stats", "hgx_query_set_create", "hgx_pattern_batch_set",
+    "hgx_query_set_free",
 )
 
 
@@ -180,6 +181,9 @@ def lib():
         "hgx_graph_export": ([vp, vp, vp, vp, vp], C.c_int),
         "hgx_graph_update": ([vp, i64, i64, vp, vp, vp, vp, i64, vp], C.c_int),
         "hgx_query_coalesce_stats": ([vp, C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "hgx_query_set_create": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),
+        "hgx_pattern_batch_set": ([vp, vp, C.POINTER(vp)], C.c_int),
+        "hgx_query_set_free": ([vp], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1949,6 +1949,16 @@ struct hgx_query_result {
     double ms_total = 0, ms_match = 0, bytes_match = 0;
 };
 
+// A packed batch resident in device memory (hgx_query_set_create), in the staging layout of the
+// packed front end.
+struct hgx_query_set {
+    int device = 0;
+    int32_t n = 0;
+    size_t o_type = 0, o_ioff = 0, o_inc = 0, o_ho = 0, o_poff = 0, o_pat = 0, o_err = 0, bytes = 0;
+    int64_t n_inc = 0, n_pat = 0;
+    char* dev = nullptr;
+};
+
 namespace {
 
 double now_ms() {
@@ -2303,47 +2313,65 @@ void front_host(hgx_graph* g, int32_t n, const NormBatch& nb, Scratch& sc, Event
                    4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
 }
 
-// Front end for the packed batch: the raw arrays go up in one copy and are normalised + planned on
-// the device (hgx_q_norm_packed); the host only checks the offsets it needs to size the upload.
-void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
-                  const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, Scratch& sc, Events& ev,
+// Layout of a packed batch in one staging area (pinned, mapped or device): its columns at 16-byte
+// aligned offsets, plus the 8-byte error slot of the legacy front kernel.
+struct PackedLayout {
+    size_t o_type = 0, o_ioff = 0, o_inc = 0, o_ho = 0, o_poff = 0, o_pat = 0, o_err = 0, bytes = 0;
+    int64_t n_inc = 0, n_pat = 0;
+};
+
+PackedLayout packed_layout(int32_t n, const int32_t* inc, const int64_t* inc_off, const int32_t* pat,
+                           const int64_t* pat_off, const char* who) {
+    PackedLayout l;
+    l.n_inc = inc_off[n] - inc_off[0];
+    l.n_pat = pat_off[n] - pat_off[0];
+    if (inc_off[0] != 0 || pat_off[0] != 0 || l.n_inc < 0 || l.n_pat < 0 || (l.n_inc > 0 && !inc) || (l.n_pat > 0 && !pat))
+        fail(HGX_E_INVALID, std::string(who) + ": bad offsets");
+    Upload u;
+    l.o_type = u.take(4 * (size_t)n);
+    l.o_ioff = u.take(8 * (size_t)(n + 1));
+    l.o_inc = u.take(4 * (size_t)l.n_inc);
+    l.o_ho = u.take(4 * (size_t)n);
+    l.o_poff = u.take(8 * (size_t)(n + 1));
+    l.o_pat = u.take(4 * (size_t)l.n_pat);
+    l.o_err = u.take(8);
+    l.bytes = u.off;
+    return l;
+}
+
+void packed_fill(char* h, const PackedLayout& l, int32_t n, const int32_t* type, const int64_t* inc_off,
+                 const int32_t* inc, const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat) {
+    const int32_t none[2] = {INT32_MAX, INT32_MAX};   // smallest bad query index, none yet
+    std::memcpy(h + l.o_err, none, 8);
+    std::memcpy(h + l.o_type, type, 4 * (size_t)n);
+    std::memcpy(h + l.o_ioff, inc_off, 8 * (size_t)(n + 1));
+    if (l.n_inc) std::memcpy(h + l.o_inc, inc, 4 * (size_t)l.n_inc);
+    std::memcpy(h + l.o_ho, has_ordered, 4 * (size_t)n);
+    std::memcpy(h + l.o_poff, pat_off, 8 * (size_t)(n + 1));
+    if (l.n_pat) std::memcpy(h + l.o_pat, pat, 4 * (size_t)l.n_pat);
+}
+
+// Normalise + plan a packed batch the device can read at d (the mapped staging area, a device copy of
+// the pinned staging, or a query set resident in HBM).  sp: the single-pass front kernel.
+void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d, bool sp, Scratch& sc, Events& ev,
                   Front& f) {
     hipStream_t s = g->stream;
-    const int64_t n_inc = inc_off[n] - inc_off[0], n_pat = pat_off[n] - pat_off[0];
-    if (inc_off[0] != 0 || pat_off[0] != 0 || n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
-        fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad offsets");
-    Upload u;
-    const size_t o_type = u.take(4 * (size_t)n), o_ioff = u.take(8 * (size_t)(n + 1)), o_inc = u.take(4 * (size_t)n_inc),
-                 o_ho = u.take(4 * (size_t)n), o_poff = u.take(8 * (size_t)(n + 1)), o_pat = u.take(4 * (size_t)n_pat),
-                 o_err = u.take(8);
-    const bool sp = g->q_flat == 2;   // single-pass: the front kernel reads the staging area in place
-    char* h = sp ? (char*)g->zc_in_buf(u.off) : (char*)g->pinned_buf(u.off);
-    const int32_t none[2] = {INT32_MAX, INT32_MAX};   // smallest bad query index, none yet
-    std::memcpy(h + o_err, none, 8);
-    std::memcpy(h + o_type, type, 4 * (size_t)n);
-    std::memcpy(h + o_ioff, inc_off, 8 * (size_t)(n + 1));
-    if (n_inc) std::memcpy(h + o_inc, inc, 4 * (size_t)n_inc);
-    std::memcpy(h + o_ho, has_ordered, 4 * (size_t)n);
-    std::memcpy(h + o_poff, pat_off, 8 * (size_t)(n + 1));
-    if (n_pat) std::memcpy(h + o_pat, pat, 4 * (size_t)n_pat);
-    char* d = sp ? (char*)g->zc_in_dev : (char*)sc.take(u.off);
     QDesc* desc = (QDesc*)sc.take(sizeof(QDesc) * n);
-    int32_t* anch = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(n_inc + n_pat, 1));
+    int32_t* anch = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(l.n_inc + l.n_pat, 1));
     int32_t* nop = (int32_t*)sc.take(4 * (size_t)n);
     f.plan = (QPlan*)sc.take(sizeof(QPlan) * n);
     f.nch = (int32_t*)sc.take(sizeof(int32_t) * (n + 1));
     f.ncand = (int64_t*)sc.take(sizeof(int64_t) * (n + 1));
-    f.err = (int32_t*)(d + o_err);
-    ev.rec(0, s);
-    f.cond_bytes = 20.0 * (double)(n_inc + n_pat) + 4.0 * n + 4.0 * (double)n_pat + (double)sizeof(QDesc) * n;
-    if (sp) {   // normalise + plan straight from the staging area; device copies of the match's columns
+    f.err = (int32_t*)(d + l.o_err);
+    f.cond_bytes = 20.0 * (double)(l.n_inc + l.n_pat) + 4.0 * n + 4.0 * (double)l.n_pat + (double)sizeof(QDesc) * n;
+    if (sp) {   // normalise + plan straight from d; device copies of the match's columns
         int32_t* dty = (int32_t*)sc.take(4 * (size_t)n);
         int64_t* dpo = (int64_t*)sc.take(8 * (size_t)(n + 1));
-        int32_t* dpa = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(n_pat, 1));
+        int32_t* dpa = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(l.n_pat, 1));
         f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
         hgx_q_norm_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
-            n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
-            (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
+            n, g->A, (const int32_t*)(d + l.o_type), (const int64_t*)(d + l.o_ioff), (const int32_t*)(d + l.o_inc),
+            (const int32_t*)(d + l.o_ho), (const int64_t*)(d + l.o_poff), (const int32_t*)(d + l.o_pat), g->inc_off,
             g->inc_ts_type, desc, anch, nop, f.plan, dty, dpo, dpa, f.ncand, f.blk);
         HGX_CHECK_LAUNCH();
         f.desc = desc;
@@ -2354,18 +2382,33 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
         f.pat = dpa;
         return;
     }
-    HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
     hgx_q_norm_packed<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(
-        n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
-        (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
+        n, g->A, (const int32_t*)(d + l.o_type), (const int64_t*)(d + l.o_ioff), (const int32_t*)(d + l.o_inc),
+        (const int32_t*)(d + l.o_ho), (const int64_t*)(d + l.o_poff), (const int32_t*)(d + l.o_pat), g->inc_off,
         g->inc_ts_type, desc, anch, nop, f.plan, f.nch, f.ncand, f.err);
     HGX_CHECK_LAUNCH();
     f.desc = desc;
     f.anch = anch;
-    f.types = (const int32_t*)(d + o_type);
+    f.types = (const int32_t*)(d + l.o_type);
     f.pos = nullptr;
-    f.poff = (const int64_t*)(d + o_poff);
-    f.pat = (const int32_t*)(d + o_pat);
+    f.poff = (const int64_t*)(d + l.o_poff);
+    f.pat = (const int32_t*)(d + l.o_pat);
+}
+
+// Front end for the packed batch: the raw arrays go into one staging area (the single-pass kernel reads
+// it in place through the mapping; otherwise one copy up) and are normalised + planned on the device.
+void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                  const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, Scratch& sc, Events& ev,
+                  Front& f) {
+    hipStream_t s = g->stream;
+    const PackedLayout l = packed_layout(n, inc, inc_off, pat, pat_off, "hgx_pattern_batch_packed");
+    const bool sp = g->q_flat == 2;   // single-pass: the front kernel reads the staging area in place
+    char* h = sp ? (char*)g->zc_in_buf(l.bytes) : (char*)g->pinned_buf(l.bytes);
+    packed_fill(h, l, n, type, inc_off, inc, has_ordered, pat_off, pat);
+    char* d = sp ? (char*)g->zc_in_dev : (char*)sc.take(l.bytes);
+    ev.rec(0, s);
+    if (!sp) HGX_HIP(hipMemcpyAsync(d, h, l.bytes, hipMemcpyHostToDevice, s));
+    front_device(g, n, l, d, sp, sc, ev, f);
 }
 
 // Single-pass back end (HGX_OPT_QUERY_FLAT = 2, default): scan + match + placement + offsets after the
@@ -3082,6 +3125,70 @@ int hgx_query_coalesce_stats(hgx_graph* g, int64_t* device_batches, int64_t* cal
     if (device_batches) *device_batches = g->qcomb.batches;
     if (caller_batches) *caller_batches = g->qcomb.requests;
     HGX_API_END
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Query sets: a packed batch uploaded once and run many times with its arrays resident in HBM (a
+// fixed set of compiled queries re-executed by the application's threads, QueryCompilation.java:
+// 76-122; the bench's config-3 step with its inputs in HBM).  The run is the packed path's front
+// kernel reading the set instead of the pinned staging area, then the same back end.
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int hgx_query_set_create(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
+                         const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_set** out) {
+    HGX_API_BEGIN
+    if (!g || !out || n <= 0 || !type || !inc_off || !pat_off || !has_ordered)
+        fail(HGX_E_INVALID, "hgx_query_set_create: bad argument");
+    *out = nullptr;
+    const PackedLayout l = packed_layout(n, inc, inc_off, pat, pat_off, "hgx_query_set_create");
+    std::vector<char> h(l.bytes);
+    packed_fill(h.data(), l, n, type, inc_off, inc, has_ordered, pat_off, pat);
+    std::unique_ptr<hgx_query_set> qs(new hgx_query_set());
+    qs->device = g->device;
+    qs->n = n;
+    qs->o_type = l.o_type; qs->o_ioff = l.o_ioff; qs->o_inc = l.o_inc; qs->o_ho = l.o_ho;
+    qs->o_poff = l.o_poff; qs->o_pat = l.o_pat; qs->o_err = l.o_err; qs->bytes = l.bytes;
+    qs->n_inc = l.n_inc; qs->n_pat = l.n_pat;
+    HGX_HIP(hipSetDevice(g->device));
+    HGX_HIP(hipMalloc(&qs->dev, l.bytes));
+    if (hipMemcpy(qs->dev, h.data(), l.bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(qs->dev);
+        fail(HGX_E_DEVICE, "hgx_query_set_create: upload failed");
+    }
+    *out = qs.release();
+    HGX_API_END
+}
+
+int hgx_pattern_batch_set(hgx_graph* g, const hgx_query_set* qs, hgx_query_result** out) {
+    HGX_API_BEGIN
+    if (!g || !qs || !out) fail(HGX_E_INVALID, "hgx_pattern_batch_set: bad argument");
+    if (qs->device != g->device) fail(HGX_E_INVALID, "hgx_pattern_batch_set: the set lives on another device");
+    *out = nullptr;
+    PackedLayout l;
+    l.o_type = qs->o_type; l.o_ioff = qs->o_ioff; l.o_inc = qs->o_inc; l.o_ho = qs->o_ho;
+    l.o_poff = qs->o_poff; l.o_pat = qs->o_pat; l.o_err = qs->o_err; l.bytes = qs->bytes;
+    l.n_inc = qs->n_inc; l.n_pat = qs->n_pat;
+    return run_batch_with(g, qs->n, out, [&](Scratch& sc, Events& ev, Front& f) {
+        const bool sp = g->q_flat == 2;
+        ev.rec(0, g->stream);
+        if (!sp) {   // the legacy front kernel reports into the set's error slot: reset it
+            int32_t* none = (int32_t*)g->pinned_buf(8);
+            none[0] = none[1] = INT32_MAX;
+            HGX_HIP(hipMemcpyAsync(qs->dev + l.o_err, none, 8, hipMemcpyHostToDevice, g->stream));
+        }
+        front_device(g, qs->n, l, qs->dev, sp, sc, ev, f);
+    });
+    HGX_API_END
+}
+
+void hgx_query_set_free(hgx_query_set* qs) {
+    if (!qs) return;
+    (void)hipSetDevice(qs->device);
+    if (qs->dev) (void)hipFree(qs->dev);
+    delete qs;
 }
 
 }  // extern "C"

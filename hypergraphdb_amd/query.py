@@ -286,6 +286,52 @@ class QueryResult:
         return self.ids[self.offsets[q]:self.offsets[q + 1]]
 
 
+def _read_result(h, n) -> QueryResult:
+    try:
+        off = np.empty(n + 1, np.int64)
+        check(lib().hgx_query_result_offsets(h, ptr(off)))
+        ids = np.empty(max(int(off[-1]), 1), np.int32)
+        check(lib().hgx_query_result_ids(h, ptr(ids)))
+        a, b, c = C.c_double(), C.c_double(), C.c_double()
+        check(lib().hgx_query_result_ms(h, C.byref(a), C.byref(b), C.byref(c)))
+    finally:
+        lib().hgx_query_result_free(h)
+    return QueryResult(off, ids[: int(off[-1])], {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+
+
+class QuerySet:
+    """A packed batch resident in device memory (hgx_query_set_create): uploaded once, run many times
+    (``run(snapshot)``) without moving the queries again -- a fixed set of compiled queries re-executed
+    by an application (TC/query/QueryCompilation.java:76-122)."""
+
+    def __init__(self, snapshot, q_type, inc_off, inc, has_ordered, pat_off, pat):
+        self._h = None
+        arrs = [np.ascontiguousarray(q_type, np.int32), np.ascontiguousarray(inc_off, np.int64),
+                np.ascontiguousarray(inc, np.int32), np.ascontiguousarray(has_ordered, np.int32),
+                np.ascontiguousarray(pat_off, np.int64), np.ascontiguousarray(pat, np.int32)]
+        self.n = len(arrs[0])
+        h = C.c_void_p()
+        check(lib().hgx_query_set_create(snapshot.handle, self.n, *(a.ctypes.data for a in arrs), C.byref(h)))
+        self._h = h
+
+    def run(self, snapshot) -> QueryResult:
+        """hgx_pattern_batch_set on ``snapshot`` (or an execution context of it)."""
+        h = C.c_void_p()
+        check(lib().hgx_pattern_batch_set(snapshot.handle, self._h, C.byref(h)))
+        return _read_result(h, self.n)
+
+    def close(self):
+        if self._h is not None:
+            lib().hgx_query_set_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def pattern_batch_arrays(snapshot, q_type, inc_off, inc, has_ordered, pat_off, pat) -> QueryResult:
     """Packed batch (hgx_pattern_batch_packed): query q = And(type(q_type[q]),
     incident(inc[inc_off[q]:inc_off[q+1]]...), orderedLink(pat[pat_off[q]:pat_off[q+1]]) if has_ordered[q])."""
@@ -295,16 +341,7 @@ def pattern_batch_arrays(snapshot, q_type, inc_off, inc, has_ordered, pat_off, p
             np.ascontiguousarray(pat_off, np.int64), np.ascontiguousarray(pat, np.int32)]
     h = C.c_void_p()
     check(lib().hgx_pattern_batch_packed(snapshot.handle, n, *(a.ctypes.data for a in arrs), C.byref(h)))
-    try:
-        off = np.zeros(n + 1, np.int64)
-        check(lib().hgx_query_result_offsets(h, ptr(off)))
-        ids = np.zeros(max(int(off[-1]), 1), np.int32)
-        check(lib().hgx_query_result_ids(h, ptr(ids)))
-        a, b, c = C.c_double(), C.c_double(), C.c_double()
-        check(lib().hgx_query_result_ms(h, C.byref(a), C.byref(b), C.byref(c)))
-    finally:
-        lib().hgx_query_result_free(h)
-    return QueryResult(off, ids[: int(off[-1])], {"ms_total": a.value, "ms_match": b.value, "bytes_match": c.value})
+    return _read_result(h, n)
 
 
 def pattern_batch_ext_arrays(snapshot, type_off, types, inc_off, inc, pos_off, pos, pset_off, pat_off, pat,

@@ -286,6 +286,18 @@ int  hgx_pattern_batch(hgx_graph *g, const hgx_and_query *queries, int32_t n,
 int  hgx_pattern_batch_packed(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off,
                               const int32_t *inc, const int32_t *has_ordered, const int64_t *pat_off,
                               const int32_t *pat, hgx_query_result **out);
+/* A packed batch resident in device memory: uploaded once (validated like hgx_pattern_batch_packed)
+ * and run any number of times without moving the queries again -- an application re-running a fixed
+ * set of compiled queries (the reference compiles a query once and executes it repeatedly,
+ * TC/query/QueryCompilation.java:76-122), and the bench's config-3 step with its inputs resident in
+ * HBM.  The set belongs to the device of g; it may be run on any graph or execution context of that
+ * device.  Results as hgx_pattern_batch. */
+typedef struct hgx_query_set hgx_query_set;
+int  hgx_query_set_create(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off, const int32_t *inc,
+                          const int32_t *has_ordered, const int64_t *pat_off, const int32_t *pat,
+                          hgx_query_set **out);
+int  hgx_pattern_batch_set(hgx_graph *g, const hgx_query_set *qs, hgx_query_result **out);
+void hgx_query_set_free(hgx_query_set *qs);
 /* The And shapes beyond {type, incident, orderedLink} (flat arrays, one call per batch).  Query q is
  *   And{ Or over types[type_off[q] .. type_off[q+1])        AtomTypeCondition (one type) or
  *                                                          TypePlusCondition (base + subtypes, expanded to an

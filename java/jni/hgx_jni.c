@@ -466,6 +466,30 @@ JNIEXPORT jlong JFN(patternBatch)(JNIEnv *e, jclass k, jlong g, jintArray type, 
     return ok && !rc ? (jlong)(intptr_t)q : 0;
 }
 
+JNIEXPORT jlong JFN(querySetCreate)(JNIEnv *e, jclass k, jlong g, jintArray type, jlongArray incOff, jintArray inc,
+                                    jintArray hasOrdered, jlongArray patOff, jintArray pat) {
+    pin_t ty = pin_int(e, type), io = pin_long(e, incOff), ic = pin_int(e, inc), ho = pin_int(e, hasOrdered),
+          po = pin_long(e, patOff), pt = pin_int(e, pat);
+    hgx_query_set *qs = NULL;
+    int ok = check_packed(e, &ty, &io, &ic, &ho, &po, &pt), rc = HGX_OK;
+    if (ok)
+        rc = hgx_query_set_create((hgx_graph *)(intptr_t)g, ty.n, (const int32_t *)ty.p, (const int64_t *)io.p,
+                                  (const int32_t *)ic.p, (const int32_t *)ho.p, (const int64_t *)po.p,
+                                  (const int32_t *)pt.p, &qs);
+    unpin(e, &ty); unpin(e, &io); unpin(e, &ic); unpin(e, &ho); unpin(e, &po); unpin(e, &pt);
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)qs : 0;
+}
+
+JNIEXPORT jlong JFN(patternBatchSet)(JNIEnv *e, jclass k, jlong g, jlong set) {
+    hgx_query_result *q = NULL;
+    int rc = hgx_pattern_batch_set((hgx_graph *)(intptr_t)g, (const hgx_query_set *)(intptr_t)set, &q);
+    if (rc) { throw_rc(e, rc); return 0; }
+    return (jlong)(intptr_t)q;
+}
+
+JNIEXPORT void JFN(querySetFree)(JNIEnv *e, jclass k, jlong set) { hgx_query_set_free((hgx_query_set *)(intptr_t)set); }
+
 JNIEXPORT jlong JFN(patternBatchExt)(JNIEnv *e, jclass k, jlong g, jlongArray typeOff, jintArray types,
                                      jlongArray incOff, jintArray inc, jlongArray posOff, jintArray pos,
                                      jlongArray psetOff, jlongArray patOff, jintArray pat, jintArray arity) {

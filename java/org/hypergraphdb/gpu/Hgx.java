@@ -58,6 +58,10 @@ final class Hgx
     // ---- conjunctive pattern batches (hgx_pattern_batch_packed / _ext + readers) -------------
     static native long patternBatch(long g, int[] type, long[] incOff, int[] inc, int[] hasOrdered, long[] patOff,
                                     int[] pat);
+    static native long querySetCreate(long g, int[] type, long[] incOff, int[] inc, int[] hasOrdered, long[] patOff,
+                                      int[] pat);                // hgx_query_set_create: a batch resident in HBM
+    static native long patternBatchSet(long g, long set);       // hgx_pattern_batch_set
+    static native void querySetFree(long set);
     static native long patternBatchExt(long g, long[] typeOff, int[] types, long[] incOff, int[] inc, long[] posOff,
                                        int[] pos, long[] psetOff, long[] patOff, int[] pat, int[] arity);
     static native long[] queryOffsets(long q);                  // [n + 1]

@@ -6,7 +6,7 @@ pinning and pending exceptions, and checks the JNI discipline on every call.  Th
 HGGpuSnapshot / HGGpuTraversal / GpuAndToQuery / GpuTraversalToQuery take (java/org/hypergraphdb/gpu):
 the results are compared with the C oracle (oracle/hgx_oracle.c, the restatement of
 HGBreadthFirstTraversal / DefaultALGenerator / AndToQuery), bit-exact.  The last test checks that
-all 54 natives were called."""
+all 57 natives were called."""
 import numpy as np
 import pytest
 
@@ -201,6 +201,19 @@ def test_pattern_batches_vs_oracle(jni, graph, gh):
         finally:
             jni.queryFree(q)
     jni.setTiming(gh, False)
+    # a resident query set (querySetCreate / patternBatchSet / querySetFree), run twice
+    qset = jni.querySetCreate(gh, *args)
+    try:
+        for _ in range(2):
+            q = jni.patternBatchSet(gh, qset)
+            try:
+                off, ids = jni.queryOffsets(q), jni.queryIds(q)
+                for i, e in enumerate(exp):
+                    assert np.array_equal(ids[off[i]:off[i + 1]], e), ("set", i)
+            finally:
+                jni.queryFree(q)
+    finally:
+        jni.querySetFree(qset)
     # no incidence anchor: the engine refuses, the Java side keeps AndToQuery
     with pytest.raises(JavaException) as ei:
         jni.patternBatch(gh, np.array([1], np.int32), np.zeros(2, np.int64), np.zeros(0, np.int32),
@@ -419,4 +432,4 @@ def test_all_natives_were_executed(jni):
     """Runs last (file order): every native declared in Hgx.java has been called on the GPU."""
     missing = sorted(set(java_natives()) - jni.called)
     assert not missing, missing
-    assert len(jni.called) == 54
+    assert len(jni.called) == 57

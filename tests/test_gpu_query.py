@@ -473,3 +473,38 @@ def test_single_pass_packed_batches_all_sizes():
     r = pattern_batch_arrays(snap, np.full(n, -1, np.int32), np.arange(n + 1, dtype=np.int64), isolated,
                              np.zeros(n, np.int32), np.zeros(n + 1, np.int64), np.zeros(0, np.int32))
     assert r.offsets.tolist() == [0] * (n + 1)
+
+
+def test_query_set_resident_batches():
+    """hgx_query_set_create + hgx_pattern_batch_set: a packed batch uploaded once and run repeatedly,
+    in every front-end mode, on the snapshot and on an execution context of it, equals the packed
+    call (and the oracle); bad offsets are refused at creation."""
+    from hypergraphdb_amd import HGXError, _lib
+    from hypergraphdb_amd.query import QuerySet, pattern_batch_arrays
+    from hypergraphdb_amd import synth
+    g = synth.config3(scale=0.002, n_queries=3000)
+    snap, orc = snapshot(g), oracle(g)
+    Q = g["queries"]
+    nq = len(Q["type"])
+    packed = (Q["type"], np.arange(nq + 1, dtype=np.int64), Q["a"], np.ones(nq, np.int32),
+              np.arange(0, 3 * nq + 1, 3, dtype=np.int64),
+              np.stack([Q["x"], np.full(nq, -1, np.int32), Q["y"]], 1).reshape(-1))
+    ref = pattern_batch_arrays(snap, *packed)
+    for q in range(0, nq, 101):
+        assert ref[q].tolist() == orc.and_query(int(Q["type"][q]), [int(Q["a"][q])],
+                                                (int(Q["x"][q]), -1, int(Q["y"][q]))).tolist()
+    qs = QuerySet(snap, *packed)
+    ctx = snap.context()
+    for flat in (2, 1, 0):
+        for target in (snap, ctx):
+            target.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
+            for _ in range(2):
+                r = qs.run(target)
+                assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), (flat, target is ctx)
+    qs.close()
+    bad = list(packed)
+    bad[1] = np.arange(1, nq + 2, dtype=np.int64)   # inc_off[0] != 0
+    with pytest.raises(HGXError):
+        QuerySet(snap, *bad)
+    ctx.close()
+    snap.close()
