@@ -2131,8 +2131,25 @@ namespace {
 
 // Type-grouped incidence index, once per snapshot (a stable radix sort of (atom, type) keys with
 // the link row as value keeps each (atom, type) slice ascending).
+void ensure_ts_inline(hgx_graph* g);
+
 void ensure_type_grouped(hgx_graph* g) {
     if (g->inc_ts_row || g->I == 0) return;
+    if (g->base) {   // an execution context: the snapshot builds the index once and every context borrows it
+        hgx_graph* b = g->base;
+        {
+            std::lock_guard<std::mutex> lk(b->mu);   // lock order: context, then its snapshot (never the reverse)
+            HGX_HIP(hipSetDevice(b->device));
+            ensure_type_grouped(b);
+            if (g->q_inline) ensure_ts_inline(b);
+            HGX_HIP(hipStreamSynchronize(b->stream));
+        }
+        g->inc_ts_row = b->inc_ts_row;
+        g->inc_ts_type = b->inc_ts_type;
+        g->inc_ts_tgt = b->inc_ts_tgt;
+        if (!b->inc_ts_tgt) g->q_inline = false;
+        return;
+    }
     hipStream_t s = g->stream;
     const int64_t I = g->I;
     u64* keys = (u64*)g->alloc(sizeof(u64) * I);

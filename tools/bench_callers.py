@@ -33,7 +33,8 @@ def callers():
     vp = C.c_void_p
     L.hgxc_pattern_threads.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp,
                                        C.POINTER(C.c_double)]
-    L.hgxc_sequence_threads.argtypes = [vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, vp, C.POINTER(C.c_double)]
+    L.hgxc_sequence_threads.argtypes = [vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, vp, C.POINTER(C.c_double),
+                                        C.c_int32]
     return L
 
 
@@ -61,18 +62,18 @@ def pattern_leg(L, snap, packed, n, threads, per_call, expect):
             "hits_match_batch": ok}
 
 
-def seq_leg(L, snap, seeds, depth, opts, threads):
+def seq_leg(L, snap, seeds, depth, opts, threads, contexts=0):
     from hypergraphdb_amd._lib import AlgenOpts
     o = AlgenOpts(*opts)
     pairs = np.zeros(len(seeds), np.int64)
     sec = C.c_double()
     s = np.ascontiguousarray(seeds, np.int32)
     rc = L.hgxc_sequence_threads(snap.handle, threads, len(s), ptr(s), depth, C.cast(C.pointer(o), C.c_void_p),
-                                 ptr(pairs), C.byref(sec))
+                                 ptr(pairs), C.byref(sec), contexts)
     if rc != 0:
         from hypergraphdb_amd._lib import lib
         raise RuntimeError(f"hgxc_sequence_threads rc={rc}: {lib().hgx_last_error().decode()}")
-    return {"threads": threads, "seeds": len(s), "seconds": round(sec.value, 5),
+    return {"threads": threads, "contexts": bool(contexts), "seeds": len(s), "seconds": round(sec.value, 5),
             "traversals_per_s": round(len(s) / sec.value, 1),
             "ms_per_traversal_per_caller": round(sec.value / len(s) * threads * 1e3, 4),
             "pairs": int(pairs.sum())}, pairs
@@ -132,10 +133,13 @@ def main():
             seq_leg(L, snap, seeds[:8], depth, opts, 1)   # warm-up (index + yield flags on first use)
             one, p1 = seq_leg(L, snap, seeds, depth, opts, 1)
             many, pm = seq_leg(L, snap, seeds, depth, opts, args.threads)
-            one["pairs_match_many"] = bool(np.array_equal(p1, pm))
-            out[f"{name}_sequence"] = {"single_seed_1_caller": one, f"single_seed_{args.threads}_callers": many}
+            manyc, pc = seq_leg(L, snap, seeds, depth, opts, args.threads, contexts=1)
+            one["pairs_match_many"] = bool(np.array_equal(p1, pm) and np.array_equal(p1, pc))
+            out[f"{name}_sequence"] = {"single_seed_1_caller": one, f"single_seed_{args.threads}_callers": many,
+                                       f"single_seed_{args.threads}_callers_own_contexts": manyc}
             log(f"{name} sequence: 1 caller {one['ms_per_traversal_per_caller']} ms per traversal; "
-                f"{args.threads} callers {many['traversals_per_s']:.0f} traversals/s")
+                f"{args.threads} callers {many['traversals_per_s']:.0f} traversals/s on one graph, "
+                f"{manyc['traversals_per_s']:.0f} on their own contexts")
             snap.close()
             del g
     js = json.dumps(out, indent=1)

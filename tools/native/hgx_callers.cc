@@ -6,7 +6,7 @@
 // hgxc_pattern_threads: thread t issues the packed queries t*per_call, (t+T)*per_call, ... in calls of
 // per_call queries each (per_call = 1: single And queries); per-query hit counts go to hits[].
 // hgxc_sequence_threads: thread t issues hgx_bfs_sequence for single seeds t, t+T, ...; per-seed pair
-// counts go to pairs[].  Both return the wall seconds from the start barrier to the last call's end.
+// counts go to pairs[] (contexts != 0: each thread on its own execution context of the graph).  Both return the wall seconds from the start barrier to the last call's end.
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -80,14 +80,26 @@ int hgxc_pattern_threads(hgx_graph* g, int32_t threads, int32_t n, const int32_t
 }
 
 int hgxc_sequence_threads(hgx_graph* g, int32_t threads, int32_t n, const int32_t* seeds, int32_t max_depth,
-                          const hgx_algen_opts* opts, int64_t* pairs, double* seconds) {
+                          const hgx_algen_opts* opts, int64_t* pairs, double* seconds, int32_t contexts) {
     if (!g || threads < 1 || n < 1 || !seeds || !seconds) return HGX_E_INVALID;
-    return run_threads(
+    // contexts != 0: every thread runs on its own execution context of g (hgx_graph_context, made before
+    // the start barrier), as HGGpuSnapshot.acquireContext gives each Java caller one
+    std::vector<hgx_graph*> ctx((size_t)threads, g);
+    if (contexts)
+        for (int t = 0; t < threads; ++t) {
+            const int rc = hgx_graph_context(g, &ctx[(size_t)t]);
+            if (rc != HGX_OK) {
+                for (int k = 0; k < t; ++k) hgx_graph_destroy(ctx[(size_t)k]);
+                return rc;
+            }
+        }
+    const int rc_all = run_threads(
         threads,
         [&](int t) -> int {
+            hgx_graph* gt = ctx[(size_t)t];
             for (int32_t i = t; i < n; i += threads) {
                 hgx_seq_result* r = nullptr;
-                int rc = hgx_bfs_sequence(g, seeds + i, 1, max_depth, opts, &r);
+                int rc = hgx_bfs_sequence(gt, seeds + i, 1, max_depth, opts, &r);
                 if (rc != HGX_OK) return rc;
                 int32_t ns = 0, nl = 0;
                 int64_t np = 0;
@@ -99,6 +111,9 @@ int hgxc_sequence_threads(hgx_graph* g, int32_t threads, int32_t n, const int32_
             return HGX_OK;
         },
         seconds);
+    if (contexts)
+        for (hgx_graph* c : ctx) hgx_graph_destroy(c);
+    return rc_all;
 }
 
 }  // extern "C"
