@@ -3912,8 +3912,11 @@ struct Exchange {
     // sum of |inc| over my (local) new frontier; *level_bytes: bytes I sent; *pair_max: the sum over
     // the level's two phases of the largest bytes I send one peer (the phases run one after the other).
     template <int Wt>
+    // last: the traversal's final level (depth limit reached): the owners still need their ghosts'
+    // news (the result counts and lists are the owners'), but no later level reads a ghost's row, so
+    // the broadcast phase (pack, transfer, apply) is skipped.
     u64 level(u64* lvl_next, u64* fa_next, u64* vis, u64* ever, u64* full, const FullMask& fm, u64* push_volume,
-              double* level_bytes, double* pair_max, Timer& tm, int d) {
+              double* level_bytes, double* pair_max, Timer& tm, int d, bool last) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts, me = sh.part;
         hipStream_t s = g->stream;
@@ -4018,6 +4021,14 @@ struct Exchange {
         ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r);
         Events e1 = tm.start(kKindExchange, d);
         apply(true, bseg);
+        if (last) {   // no broadcast after the final level
+            HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+            hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
+                A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e1);
+            return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r);
+        }
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
         hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
@@ -4567,7 +4578,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64 new_global = 0, part_push = 0;
         if (ex) {
             double lb = 0, pm = 0;
-            new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push, &lb, &pm, tm, d);
+            new_global = ex->template level<W>(lvl_next, fa_next, vis, ever, full, fm, &part_push, &lb, &pm, tm, d,
+                                               d + 1 >= maxd);
             if (d < 64) {
                 res->stats.level_xbytes[d] += lb;
                 res->stats.level_xpair_max[d] = std::max(res->stats.level_xpair_max[d], pm);

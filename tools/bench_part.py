@@ -10,8 +10,9 @@ MI355X_MICROARCH / SURVEY.md 5).  The modelled NP-GPU level time is
     max_p device_ms(p) + max_pair_bytes / 153 GB/s + host round trips x --sync-us
 (no overlap of exchange and compute assumed), summed over the levels; the 1-part run is the
 replica on one GPU.  Host round trips of a level (compressed records): the two count read-backs,
-the two count all-gathers and the termination all-gather (5; the all-to-alls are ordered on the
-stream without a host wait); --sync-us prices one (a small RCCL collective or a read-back at 8
+the two count all-gathers and the termination all-gather (5; 3 at the final level of a depth-limited
+traversal, which has no broadcast phase; the all-to-alls are ordered on the stream without a host
+wait); --sync-us prices one (a small RCCL collective or a read-back at 8
 ranks, default 40 us).  Counts of every source must equal the replica's.
 
   python tools/bench_part.py --scale 0.25 --parts 1 8 --out gpurun_out/part.json
@@ -105,7 +106,9 @@ def measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state):
             pm = max(max((s[p]["level_xpair_max"][d] for s in sts if d < len(s[p]["level_xpair_max"])), default=0)
                      for p in range(NP))
             link_ms = pm / (XGMI_LINK_GBS * 1e9) * 1e3
-            sync_ms = (5 * args.sync_us / 1e3) if NP > 1 else 0.0
+            # the final level of a depth-limited traversal has no broadcast phase: 3 round trips
+            trips = 3 if d == args.depth - 1 else 5
+            sync_ms = (trips * args.sync_us / 1e3) if NP > 1 else 0.0
             levels.append({"max_part_device_ms": round(max(dev), 3), "max_part_exchange_kernels_ms": round(max(xms), 3),
                            "bytes_per_part_max": max(xb), "max_pair_bytes": pm, "max_pair_link_ms": round(link_ms, 3),
                            "host_sync_ms": round(sync_ms, 3),
