@@ -4408,7 +4408,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // 2048 waves grid-striding over the frontier list: config 5 levels of 20 to 35K atoms measured
             // 19-113 us against 30-142 us with 8192 waves (the launch of mostly idle workgroups and
             // the candidate-append contention) and 20-171 us with 1024 waves
-            const int lgrid = 512;
+            static const int kPushGrid = [] {   // HGX_PUSH_GRID: A/B override of the push grid (blocks)
+                const char* e = std::getenv("HGX_PUSH_GRID");
+                const int v = e ? std::atoi(e) : 0;
+                return v >= 64 && v <= 8192 ? v : 512;
+            }();
+            const int lgrid = kPushGrid;
             Events e2 = tm.start_chained(kKindPush, d);
             const bool flat = g->push_batch > 0;
             // hub chunks inside hgx_opush while there are few of them (config 5: ~350 chunks, one launch
