@@ -34,6 +34,7 @@ HGX_OPT_PART_EXCHANGE = 8
 HGX_OPT_QUERY_FLAT = 9
 HGX_OPT_CODED = 10
 HGX_OPT_QUERY_COALESCE = 11
+HGX_OPT_PUSH_INLINE = 12
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (

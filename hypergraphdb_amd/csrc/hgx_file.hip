@@ -359,6 +359,9 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->inc_yf = nullptr;
     if (g->pchunks) (void)hipFree(g->pchunks);
     g->pchunks = nullptr;
+    if (g->inc_tgt) (void)hipFree(g->inc_tgt);   // inline target records of the old incidence
+    g->inc_tgt = nullptr;
+    g->inc_tgt_tried = false;
     if (g->fcode) (void)hipFree(g->fcode);   // coded-level scratch, sized by the old A / M
     g->fcode = nullptr;
     if (g->lcode) (void)hipFree(g->lcode);

@@ -410,6 +410,13 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * compiled queries (QueryCompilation.java:76-122).  Results and errors are exactly those of separate
  * calls (a batch whose merged run reports a bad or unsupported query is re-run on its own).  0 = off. */
 #define HGX_OPT_QUERY_COALESCE 11
+/* HGX_OPT_PUSH_INLINE (A/B, default 0): 1 = frontier-push levels read each incidence entry's link
+ * targets from inline 32-byte records in incidence order (built on the first push level with the
+ * option on: 32 bytes per incidence entry, skipped when that exceeds a quarter of the free HBM) -- one
+ * load at the entry's own position instead of three dependent ones.  Measured no faster on config 5
+ * (2.14-2.25 against 2.16-2.17 ms per concurrent step, profiles/r03n_c5.log: the rows of a graph that
+ * size are cache hits), so the default saves the memory. */
+#define HGX_OPT_PUSH_INLINE 12
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */
 int  hgx_query_coalesce_stats(hgx_graph *g, int64_t *device_batches, int64_t *caller_batches);

@@ -305,6 +305,32 @@ def test_push_batch_all_modes(batch):
             check_batch(g, seeds, maxd, mode, lt, snap, orc)
 
 
+@pytest.mark.parametrize("inline", [1, 0])
+def test_push_inline_records_all_modes(inline):
+    """HGX_OPT_PUSH_INLINE: the frontier push reading each incidence entry's targets from the inline
+    32-byte records (1) or through tgt_off (0) gives the oracle's per-depth sets in every generator
+    mode: rows longer than 8 targets (the records' fallback), typed links, power-law hubs (chunked
+    push), links targeting links, and the config-5 ontology in both subsumption directions."""
+    from hypergraphdb_amd import _lib, synth
+    rng = np.random.default_rng(93)
+    cases = [(K.random_graph(rng, 600, 2500, max_arity=12, n_types=3), -1, None, 300),
+             (synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=19), 1, 3, 1024),
+             (synth.config5(scale=0.002, n_sources=500), None, None, 500)]
+    for gi, (g, lt, maxd, ns) in enumerate(cases):
+        snap, orc = snapshot(g), oracle(g)
+        snap.set_option(_lib.HGX_OPT_PUSH_INLINE, inline)
+        if gi == 2:
+            lt = int(g["subsumes_type"])
+            modes = [(False, True, False, False), (False, True, True, False)]
+            seeds = np.asarray(g["seeds"], np.int32)
+        else:
+            modes = K.ALGEN_MODES[::2] if gi == 0 else K.ALGEN_MODES[1::3]
+            seeds = rng.integers(0, g["num_atoms"], ns).astype(np.int32)
+        for mode in modes:
+            check_batch(g, seeds, maxd, mode, lt, snap, orc)
+        snap.close()
+
+
 @pytest.mark.parametrize("coded", [2, 0])
 def test_coded_levels(coded):
     """HGX_OPT_CODED: a dense level after a push level moves rows of <= 6 source bits as 64-bit codes
