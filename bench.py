@@ -353,11 +353,15 @@ def run_config5(args, ctx, barrier_sync):
             closure += n
     trav /= max(args.warmup, 1)
     closure //= max(args.warmup, 1)
-    # the same step with the directions one after the other (reported next to the timed line)
+    # the same step with the directions one after the other (reported next to the timed line, with the
+    # push kernels' roofline when they run alone: side by side they share the CUs and each launch lasts
+    # longer)
     t1 = time.perf_counter()
+    seq_sts = []
     for _ in range(args.steps):
-        step(concurrent=False)
+        seq_sts += [st for _, st in step(concurrent=False)]
     seq_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    seq_sts = [x.as_dict() for x in seq_sts]
     barrier_sync()
     t1 = time.perf_counter()
     sts = []
@@ -381,7 +385,8 @@ def run_config5(args, ctx, barrier_sync):
            "closure_atoms_per_step": closure,
            "workload": (f"config5: {g['n_nodes']} classes, HGSubsumes DAG + noise links, {len(g['seeds'])} classes x "
                         "{subsumed, subsumes}, unbounded depth"),
-           "roofline": _kernel_roof(sts)}
+           "roofline": _kernel_roof(sts),
+           "roofline_directions_serial": _kernel_roof(seq_sts)}
     log(f"rank {rank}: config5 {out['value']:.3e} TEPS, {out['closures_per_s']:.1f} closures/s, "
         f"{out['ms_per_step']} ms/step ({seq_ms:.3f} with the directions one after the other), {out['levels']} levels")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
