@@ -49,7 +49,7 @@ EXPORTED = (
     "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
     "hgx_graph_update", "hgx_query_coalesce_stats", "hgx_query_set_create", "hgx_pattern_batch_set",
-    "hgx_query_set_free",
+    "hgx_query_set_free", "hgx_pattern_batch_set_into",
 )
 
 
@@ -185,6 +185,7 @@ def lib():
         "hgx_query_set_create": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),
         "hgx_pattern_batch_set": ([vp, vp, C.POINTER(vp)], C.c_int),
         "hgx_query_set_free": ([vp], None),
+        "hgx_pattern_batch_set_into": ([vp, vp, vp, vp, i64, C.POINTER(i64), vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1947,6 +1947,11 @@ struct hgx_query_result {
     std::vector<int64_t> offsets;
     std::vector<int32_t> ids;
     double ms_total = 0, ms_match = 0, bytes_match = 0;
+    // caller buffers (hgx_pattern_batch_set_into): the single-pass back end copies the offsets and,
+    // when they fit, the ids straight from the mapped result area into them
+    int64_t* ext_off = nullptr;
+    int32_t* ext_ids = nullptr;
+    int64_t ext_cap = 0, n_hits = 0;
 };
 
 // A packed batch resident in device memory (hgx_query_set_create), in the staging layout of the
@@ -2492,8 +2497,14 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
             continue;
         }
         const int64_t total = stat[3];
-        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
-        r->ids.assign(ids_h, ids_h + total);
+        r->n_hits = total;
+        if (r->ext_off) {   // caller buffers: no result vectors
+            std::memcpy(r->ext_off, qoff_h, sizeof(int64_t) * (n + 1));
+            if (total <= r->ext_cap && total > 0) std::memcpy(r->ext_ids, ids_h, sizeof(int32_t) * total);
+        } else {
+            std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
+            r->ids.assign(ids_h, ids_h + total);
+        }
         if (prof)
             std::fprintf(stderr, "[hgx query] single-pass n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n",
                          n, now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
@@ -2893,14 +2904,20 @@ bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_
 }
 
 template <class FrontFn>
-int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front) {
+int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front, hgx_query_result* into = nullptr) {
     HGX_API_BEGIN
     const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
     const double t0 = now_ms();
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
-    std::unique_ptr<hgx_query_result> r(new hgx_query_result());
+    std::unique_ptr<hgx_query_result> own;
+    hgx_query_result* r = into;
+    if (!r) {
+        own.reset(new hgx_query_result());
+        r = own.get();
+    }
     r->n = n;
-    r->offsets.assign(n + 1, 0);
+    // the single-pass back end writes caller buffers directly; the other back ends fill the vectors
+    if (!r->ext_off || g->q_flat != 2) r->offsets.assign(n + 1, 0);
     if (n > 0) {
         std::lock_guard<std::mutex> lk(g->mu);
         HGX_HIP(hipSetDevice(g->device));
@@ -2911,9 +2928,9 @@ int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn fron
         ev.init(g);
         Front f;
         front(sc, ev, f);
-        back_end(g, n, f, sc, ev, r.get(), prof, t0);
+        back_end(g, n, f, sc, ev, r, prof, t0);
     }
-    *out = r.release();
+    if (out) *out = own.release();
     HGX_API_END
 }
 
@@ -3198,6 +3215,54 @@ int hgx_pattern_batch_set(hgx_graph* g, const hgx_query_set* qs, hgx_query_resul
         }
         front_device(g, qs->n, l, qs->dev, sp, sc, ev, f);
     });
+    HGX_API_END
+}
+
+int hgx_pattern_batch_set_into(hgx_graph* g, const hgx_query_set* qs, int64_t* offsets, int32_t* ids, int64_t ids_cap,
+                                int64_t* n_ids, double* timing) {
+    HGX_API_BEGIN
+    if (!g || !qs || !offsets || !n_ids || ids_cap < 0 || (ids_cap > 0 && !ids))
+        fail(HGX_E_INVALID, "hgx_pattern_batch_set_into: bad argument");
+    if (qs->device != g->device) fail(HGX_E_INVALID, "hgx_pattern_batch_set_into: the set lives on another device");
+    if (qs->n == 0) {
+        offsets[0] = 0;
+        *n_ids = 0;
+        if (timing) timing[0] = timing[1] = timing[2] = 0.0;
+        return HGX_OK;
+    }
+    PackedLayout l;
+    l.o_type = qs->o_type; l.o_ioff = qs->o_ioff; l.o_inc = qs->o_inc; l.o_ho = qs->o_ho;
+    l.o_poff = qs->o_poff; l.o_pat = qs->o_pat; l.o_err = qs->o_err; l.bytes = qs->bytes;
+    l.n_inc = qs->n_inc; l.n_pat = qs->n_pat;
+    hgx_query_result r;
+    r.ext_off = offsets;
+    r.ext_ids = ids;
+    r.ext_cap = ids_cap;
+    const int rc = run_batch_with(
+        g, qs->n, nullptr,
+        [&](Scratch& sc, Events& ev, Front& f) {
+            const bool sp = g->q_flat == 2;
+            ev.rec(0, g->stream);
+            if (!sp) {
+                int32_t* none = (int32_t*)g->pinned_buf(8);
+                none[0] = none[1] = INT32_MAX;
+                HGX_HIP(hipMemcpyAsync(qs->dev + l.o_err, none, 8, hipMemcpyHostToDevice, g->stream));
+            }
+            front_device(g, qs->n, l, qs->dev, sp, sc, ev, f);
+        },
+        &r);
+    if (rc != HGX_OK) return rc;
+    if (g->q_flat != 2) {   // the other back ends filled the vectors
+        std::memcpy(offsets, r.offsets.data(), sizeof(int64_t) * r.offsets.size());
+        r.n_hits = (int64_t)r.ids.size();
+        if (r.n_hits <= ids_cap && r.n_hits > 0) std::memcpy(ids, r.ids.data(), sizeof(int32_t) * r.n_hits);
+    }
+    *n_ids = r.n_hits;
+    if (timing) {
+        timing[0] = r.ms_total;
+        timing[1] = r.ms_match;
+        timing[2] = r.bytes_match;
+    }
     HGX_API_END
 }
 

@@ -320,6 +320,23 @@ class QuerySet:
         check(lib().hgx_pattern_batch_set(snapshot.handle, self._h, C.byref(h)))
         return _read_result(h, self.n)
 
+    def run_into(self, snapshot, offsets: np.ndarray, ids: np.ndarray, timing: np.ndarray | None = None) -> int:
+        """hgx_pattern_batch_set_into: the results into caller arrays (``offsets``: int64[n + 1],
+        ``ids``: int32); returns the number of hits.  ``ids`` holds them only when that number fits
+        (``offsets`` is always filled, so a caller can size ``ids`` and run again).  ``timing``
+        (float64[3], optional): device ms of the batch, ms and algorithmic bytes of the match kernel."""
+        if timing is not None and (timing.dtype != np.float64 or timing.size < 3 or not timing.flags.c_contiguous):
+            raise ValueError("timing must be a contiguous float64 array of 3 entries")
+        if offsets.dtype != np.int64 or offsets.size < self.n + 1 or not offsets.flags.c_contiguous:
+            raise ValueError(f"offsets must be a contiguous int64 array of at least {self.n + 1} entries")
+        if ids.dtype != np.int32 or not ids.flags.c_contiguous:
+            raise ValueError("ids must be a contiguous int32 array")
+        n_ids = C.c_int64()
+        check(lib().hgx_pattern_batch_set_into(snapshot.handle, self._h, offsets.ctypes.data, ids.ctypes.data,
+                                               ids.size, C.byref(n_ids),
+                                               None if timing is None else timing.ctypes.data))
+        return n_ids.value
+
     def close(self):
         if self._h is not None:
             lib().hgx_query_set_free(self._h)

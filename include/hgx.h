@@ -297,6 +297,13 @@ int  hgx_query_set_create(hgx_graph *g, int32_t n, const int32_t *type, const in
                           const int32_t *has_ordered, const int64_t *pat_off, const int32_t *pat,
                           hgx_query_set **out);
 int  hgx_pattern_batch_set(hgx_graph *g, const hgx_query_set *qs, hgx_query_result **out);
+/* The same run with the results written into caller buffers (no result object): offsets[n + 1] always,
+ * ids when the hits fit in ids_cap; *n_ids = the number of hits (call again with a larger buffer when
+ * it exceeds ids_cap).  The single-pass back end copies straight from the mapped result area.
+ * timing (optional, double[3]): what hgx_query_ms reports for a result object -- device ms of the batch,
+ * ms of the match kernel, its algorithmic bytes (zeros unless hgx_set_timing is on). */
+int  hgx_pattern_batch_set_into(hgx_graph *g, const hgx_query_set *qs, int64_t *offsets, int32_t *ids, int64_t ids_cap,
+                                int64_t *n_ids, double *timing);
 void hgx_query_set_free(hgx_query_set *qs);
 /* The And shapes beyond {type, incident, orderedLink} (flat arrays, one call per batch).  Query q is
  *   And{ Or over types[type_off[q] .. type_off[q+1])        AtomTypeCondition (one type) or

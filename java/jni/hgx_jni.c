@@ -81,6 +81,14 @@ static void unpin(JNIEnv *e, pin_t *x) {
     else (*e)->ReleaseByteArrayElements(e, (jbyteArray)x->a, (jbyte *)x->p, JNI_ABORT);
     x->p = NULL;
 }
+/* an output array: its elements are copied back into the Java array (mode 0) */
+static void unpin_out(JNIEnv *e, pin_t *x) {
+    if (!x->a || !x->p) return;
+    if (x->kind == 0) (*e)->ReleaseIntArrayElements(e, (jintArray)x->a, (jint *)x->p, 0);
+    else if (x->kind == 1) (*e)->ReleaseLongArrayElements(e, (jlongArray)x->a, (jlong *)x->p, 0);
+    else (*e)->ReleaseByteArrayElements(e, (jbyteArray)x->a, (jbyte *)x->p, 0);
+    x->p = NULL;
+}
 /* a pin of a non-null array whose elements could not be obtained (the VM has thrown OutOfMemoryError) */
 static int pin_failed(const pin_t *x) { return x->a && !x->p; }
 
@@ -489,6 +497,21 @@ JNIEXPORT jlong JFN(patternBatchSet)(JNIEnv *e, jclass k, jlong g, jlong set) {
 }
 
 JNIEXPORT void JFN(querySetFree)(JNIEnv *e, jclass k, jlong set) { hgx_query_set_free((hgx_query_set *)(intptr_t)set); }
+
+/* The set's results into caller arrays: offsets (n + 1 entries) always, ids when they fit; returns the
+ * number of hits (a larger ids array and a second call when it exceeds ids.length). */
+JNIEXPORT jlong JFN(patternBatchSetInto)(JNIEnv *e, jclass k, jlong g, jlong set, jlongArray offsets, jintArray ids) {
+    if (!check_not_null(e, offsets, "offsets")) return 0;
+    pin_t off = pin_long(e, offsets), id = pin_int(e, ids);
+    int64_t n_ids = 0;
+    int rc = HGX_OK, ok = !pin_failed(&off) && !pin_failed(&id);
+    if (ok)
+        rc = hgx_pattern_batch_set_into((hgx_graph *)(intptr_t)g, (const hgx_query_set *)(intptr_t)set,
+                                        (int64_t *)off.p, (int32_t *)id.p, (int64_t)id.n, &n_ids, NULL);
+    unpin_out(e, &off); unpin_out(e, &id);
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)n_ids : 0;
+}
 
 JNIEXPORT jlong JFN(patternBatchExt)(JNIEnv *e, jclass k, jlong g, jlongArray typeOff, jintArray types,
                                      jlongArray incOff, jintArray inc, jlongArray posOff, jintArray pos,

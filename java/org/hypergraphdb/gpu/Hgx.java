@@ -62,6 +62,7 @@ final class Hgx
                                       int[] pat);                // hgx_query_set_create: a batch resident in HBM
     static native long patternBatchSet(long g, long set);       // hgx_pattern_batch_set
     static native void querySetFree(long set);
+    static native long patternBatchSetInto(long g, long set, long[] offsets, int[] ids);   // -> hits
     static native long patternBatchExt(long g, long[] typeOff, int[] types, long[] incOff, int[] inc, long[] posOff,
                                        int[] pos, long[] psetOff, long[] patOff, int[] pat, int[] arity);
     static native long[] queryOffsets(long q);                  // [n + 1]

@@ -5,7 +5,8 @@
 passes exactly the Java argument list the declaration has (a drifted declaration fails to bind).
 Each call:
   - converts Python arguments to Java objects (numpy / lists -> int[] / long[] / byte[], str -> String,
-    None -> null);
+    None -> null); a writable contiguous numpy array of the Java element type gets back what the native
+    committed to its Java copy (Java arrays are passed by reference);
   - calls `Java_org_hypergraphdb_gpu_Hgx_<name>(env, clazz, ...)`;
   - checks the JNI discipline the fake env records (pins all released, inputs unmodified, no JNI call
     with an exception pending);
@@ -145,8 +146,14 @@ class Jni:
                 jargs.append(self._to_java(t, v))
         self.called.add(name)
         r = self._fn(name)(self.env, None, *jargs)
-        for t, o in zip(params, jargs):   # the "Java" inputs go out of scope
+        for t, v, o in zip(params, args, jargs):   # the "Java" inputs go out of scope
             if t not in _SCALAR and o:
+                if t in _KIND and isinstance(v, np.ndarray) and v.size and v.flags.writeable and \
+                        v.flags.c_contiguous and v.dtype == _KIND[t][1]:
+                    # Java arrays are passed by reference: what the native committed is the caller's
+                    v[...] = np.ctypeslib.as_array(
+                        C.cast(self.L.fj_data(o), C.POINTER(np.ctypeslib.as_ctypes_type(v.dtype))), (v.size,)
+                    ).reshape(v.shape)
                 self.L.fj_release(self.env, o)
         L = self.L
         pins = L.fj_outstanding_pins(self.env)

@@ -6,7 +6,7 @@ pinning and pending exceptions, and checks the JNI discipline on every call.  Th
 HGGpuSnapshot / HGGpuTraversal / GpuAndToQuery / GpuTraversalToQuery take (java/org/hypergraphdb/gpu):
 the results are compared with the C oracle (oracle/hgx_oracle.c, the restatement of
 HGBreadthFirstTraversal / DefaultALGenerator / AndToQuery), bit-exact.  The last test checks that
-all 57 natives were called."""
+all 58 natives were called."""
 import numpy as np
 import pytest
 
@@ -212,6 +212,19 @@ def test_pattern_batches_vs_oracle(jni, graph, gh):
                     assert np.array_equal(ids[off[i]:off[i + 1]], e), ("set", i)
             finally:
                 jni.queryFree(q)
+        # into caller arrays (patternBatchSetInto): exact fit, then an ids array one short
+        total = sum(len(e) for e in exp)
+        off = np.zeros(len(exp) + 1, np.int64)
+        ids = np.full(total, -1, np.int32)
+        assert jni.patternBatchSetInto(gh, qset, off, ids) == total
+        for i, e in enumerate(exp):
+            assert np.array_equal(ids[off[i]:off[i + 1]], e), ("set into", i)
+        short = np.full(max(total - 1, 0), -1, np.int32)
+        off[:] = 0
+        assert jni.patternBatchSetInto(gh, qset, off, short) == total
+        assert off[-1] == total and (short == -1).all()
+        with pytest.raises(JavaException):
+            jni.patternBatchSetInto(gh, qset, None, ids)
     finally:
         jni.querySetFree(qset)
     # no incidence anchor: the engine refuses, the Java side keeps AndToQuery
@@ -432,4 +445,4 @@ def test_all_natives_were_executed(jni):
     """Runs last (file order): every native declared in Hgx.java has been called on the GPU."""
     missing = sorted(set(java_natives()) - jni.called)
     assert not missing, missing
-    assert len(jni.called) == 57
+    assert len(jni.called) == 58

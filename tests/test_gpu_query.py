@@ -478,7 +478,8 @@ def test_single_pass_packed_batches_all_sizes():
 def test_query_set_resident_batches():
     """hgx_query_set_create + hgx_pattern_batch_set: a packed batch uploaded once and run repeatedly,
     in every front-end mode, on the snapshot and on an execution context of it, equals the packed
-    call (and the oracle); bad offsets are refused at creation."""
+    call (and the oracle), also into caller buffers (hgx_pattern_batch_set_into); bad offsets are
+    refused at creation."""
     from hypergraphdb_amd import HGXError, _lib
     from hypergraphdb_amd.query import QuerySet, pattern_batch_arrays
     from hypergraphdb_amd import synth
@@ -501,6 +502,22 @@ def test_query_set_resident_batches():
             for _ in range(2):
                 r = qs.run(target)
                 assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), (flat, target is ctx)
+            # caller buffers (hgx_pattern_batch_set_into): exact fit, then too small (offsets and the
+            # count still come back, the ids array is left alone)
+            total = int(ref.offsets[-1])
+            off = np.full(nq + 1, -7, np.int64)
+            ids = np.full(total + 3, -7, np.int32)
+            tm = np.full(3, -1.0)
+            assert qs.run_into(target, off, ids, tm) == total
+            assert np.array_equal(off, ref.offsets) and np.array_equal(ids[:total], ref.ids)
+            assert (tm >= 0).all()
+            assert (ids[total:] == -7).all()
+            off[:] = -7
+            small = np.full(max(total - 1, 0), -7, np.int32)
+            assert qs.run_into(target, off, small) == total
+            assert np.array_equal(off, ref.offsets) and (small == -7).all()
+    with pytest.raises(ValueError):
+        qs.run_into(snap, np.zeros(nq, np.int64), np.zeros(8, np.int32))
     qs.close()
     bad = list(packed)
     bad[1] = np.arange(1, nq + 2, dtype=np.int64)   # inc_off[0] != 0

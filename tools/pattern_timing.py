@@ -22,10 +22,12 @@ def main():
     ap.add_argument("--inline", default="1", help="HGX_OPT_QUERY_INLINE values to compare, interleaved (e.g. 1,0)")
     ap.add_argument("--flat", default="2", help="HGX_OPT_QUERY_FLAT values to compare, interleaved (e.g. 2,1,0)")
     ap.add_argument("--no-timing", action="store_true", help="no device events (wall time without their gaps)")
+    ap.add_argument("--resident", action="store_true",
+                    help="run the batch as a resident query set (hgx_query_set_create + hgx_pattern_batch_set)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import synth
-    from hypergraphdb_amd.query import pattern_batch_arrays
+    from hypergraphdb_amd.query import QuerySet, pattern_batch_arrays
     g = synth.config3(scale=args.scale, n_queries=args.queries)
     Q = g["queries"]
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
@@ -42,13 +44,16 @@ def main():
     match = {o: [] for o in opts}
     gbs = {o: [] for o in opts}
     ref = None
+    qset = None
     for i in range(args.calls):
         for o in opts:
             snap.set_option(_lib.HGX_OPT_QUERY_FUSED, o[0])
             snap.set_option(_lib.HGX_OPT_QUERY_INLINE, o[1])
             snap.set_option(_lib.HGX_OPT_QUERY_FLAT, o[2])
+            if args.resident and qset is None:
+                qset = QuerySet(snap, *packed)
             t0 = time.perf_counter()
-            r = pattern_batch_arrays(snap, *packed)
+            r = qset.run(snap) if args.resident else pattern_batch_arrays(snap, *packed)
             walls[o].append((time.perf_counter() - t0) * 1e3)
             devs[o].append(r.ms["ms_total"])
             match[o].append(r.ms["ms_match"])
@@ -57,6 +62,19 @@ def main():
                 ref = (r.offsets.copy(), r.ids.copy())
             elif i < 2:
                 assert np.array_equal(ref[0], r.offsets) and np.array_equal(ref[1], r.ids), "paths differ"
+    if args.resident:
+        # the same set into caller buffers (hgx_pattern_batch_set_into): no result object per batch
+        off = np.zeros(len(ref[0]), np.int64)
+        ids = np.zeros(len(ref[1]) + 1, np.int32)
+        wi = []
+        for i in range(args.calls):
+            t0 = time.perf_counter()
+            n = qset.run_into(snap, off, ids)
+            wi.append((time.perf_counter() - t0) * 1e3)
+            assert n == len(ref[1]) and np.array_equal(off, ref[0]) and np.array_equal(ids[:n], ref[1])
+        w = np.array(wi[3:])
+        print(f"into caller buffers (flat={opts[-1][2]}) wall ms: median {np.median(w):.3f} min {w.min():.3f} "
+              f"max {w.max():.3f}")
     for o in opts:
         w, d, m = np.array(walls[o][3:]), np.array(devs[o][3:]), np.array(match[o][3:])
         print(f"fused,inline,flat={o} wall ms: median {np.median(w):.3f} min {w.min():.3f} max {w.max():.3f}; "
