@@ -3282,6 +3282,99 @@ __global__ void __launch_bounds__(256) hgx_xb_pack(int64_t A, const u64* __restr
     }
 }
 
+// Broadcast pack of a dense level over the broadcast entries (bc_atom / bc_part / bc_lid, grouped by
+// owned atom): one dense record per (owned atom with news, other holder), 64 entries per wave step.
+// Slots are ranked inside the wave by ballots -- one LDS atomic per wave and destination, none per
+// record -- so a wave's records are contiguous in each destination segment, and every lane group
+// writes a record (hgx_xb_pack walks atoms and idles the groups whose atom has fewer holders than
+// the wave's most-held atom).  Two passes: counts, records.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xb_pack_flat(int64_t E, const int32_t* __restrict__ bc_atom,
+                                                        const int32_t* __restrict__ bc_part,
+                                                        const int32_t* __restrict__ bc_lid, const u64* __restrict__ fa_next,
+                                                        const u64* __restrict__ lvl_next, u64* __restrict__ cursor,
+                                                        const int64_t* __restrict__ seg_h, const int64_t* __restrict__ seg_p,
+                                                        u64* __restrict__ hdr, u64* __restrict__ pay, u64* __restrict__ nzw,
+                                                        int NP) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G, U = 2;
+    constexpr uint32_t FULLM = full_word_mask(W);
+    typedef Vec<WPL> V;
+    __shared__ PackLds sh;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane / G, sub = lane & (G - 1);
+    const u64 lt = (1ull << lane) - 1ull;
+    int64_t lo, hi;
+    block_tiles((E + 63) / 64, lo, hi);
+    for (int d = threadIdx.x; d < NP; d += 256) sh.rec[d] = sh.slot[d] = 0;
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        u64 nz = 0;
+        for (int64_t c = lo + wv; c < hi; c += 4) {   // wave-uniform
+            const int64_t e = c * 64 + lane;
+            int32_t t = 0, q = -1, lid = 0;
+            if (e < E) {
+                t = bc_atom[e];
+                if (bit(fa_next, t)) {
+                    q = bc_part[e];
+                    lid = bc_lid[e];
+                }
+            }
+            const u64 news = __ballot(q >= 0);
+            if (!news) continue;   // wave-uniform
+            int64_t local = 0;     // this lane's record: its rank among the block's records to q
+            for (int d = 0; d < NP; ++d) {   // wave-uniform
+                const u64 m = __ballot(q == d);
+                if (!m) continue;
+                unsigned long long b = 0;
+                if (lane == 0) {
+                    if (pass == 0) atomicAdd(&sh.rec[d], (unsigned int)__popcll(m));
+                    else b = atomicAdd(&sh.slot[d], (unsigned long long)__popcll(m));
+                }
+                b = __shfl(b, 0);
+                if (q == d) local = (int64_t)b + __popcll(m & lt);
+            }
+            if (pass == 0) continue;
+            const int n = __popcll(news);
+            for (int r0 = 0; r0 < n; r0 += PER * U) {   // wave-uniform
+                typename V::T row[U];
+                int64_t lc[U];
+                int qq[U];
+                int32_t ll[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = r0 + u * PER + g;
+                    const int src = j < n ? nth_set_bit(news, j) : 0;
+                    const int32_t ts = __shfl(t, src);
+                    qq[u] = __shfl(q, src);
+                    ll[u] = __shfl(lid, src);
+                    lc[u] = (int64_t)__shfl((long long)local, src);
+                    row[u] = j < n ? V::ld(lvl_next + (int64_t)ts * W + sub * WPL) : V::zero();
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (r0 + u * PER < n) {   // wave-uniform
+                        const uint32_t nzm = group_mask<W>(row[u]);
+                        if (r0 + u * PER + g < n) {
+                            const int d = qq[u];
+                            put_record<W>(hdr, pay + seg_p[d], seg_h[d] + (int64_t)sh.base_r[d] + lc[u],
+                                          (int64_t)sh.base_w[d] + lc[u] * W, ll[u], FULLM, row[u], true);
+                            if (sub == 0) nz += (u64)__popc(nzm);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (pass == 0) {
+            for (int d = threadIdx.x; d < NP; d += 256) sh.wrd[d] = sh.rec[d] * (unsigned int)W;
+            __syncthreads();
+            pack_reserve(sh, cursor, NP);
+            __syncthreads();
+        } else {
+            block_add_sh(nzw, 2, nz);
+        }
+    }
+}
+
 // Apply n received records (headers hdr, payload pay of one source), one G-lane group each.
 // REDUCE: OR a partial row into an owned atom (new = row & ~vis; a source sends an atom at most
 // once, so one launch per source segment); BROADCAST: a ghost's final row replaces the partial one
@@ -4070,6 +4163,18 @@ struct Exchange {
         HGX_CHECK_LAUNCH();
         tm.stop(e0);
         read_counts();
+        // a dense level (at least half of my ghosts with news, rows > 70% nonzero words) packs its
+        // broadcast over the entries (hgx_xb_pack_flat); HGX_XB_FLAT=0 keeps the atom walk on every
+        // level, 2 takes the entries on every level (A/B and tests)
+        u64 sent_r = 0, sent_w = 0;
+        for (int q = 0; q < NP; ++q) {
+            sent_r += cnt[q];
+            sent_w += wcnt[q];
+        }
+        const char* fe = std::getenv("HGX_XB_FLAT");
+        const int flat_opt = fe ? std::atoi(fe) : 1;
+        const bool flat = bseg[NP] > 0 && (flat_opt == 2 || (flat_opt == 1 && sent_r * 2 >= (u64)rseg[NP] &&
+                                                             sent_w * 10 > sent_r * (u64)Wt * 7));
         ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r);
         Events e1 = tm.start(kKindExchange, d);
         apply(true, bseg);
@@ -4083,8 +4188,15 @@ struct Exchange {
         }
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
-        hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
-                                              lvl_next, dctr, seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs, NP);
+        if (flat) {
+            const int64_t E = bseg[NP];
+            const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E, 64) / 4 + 1, 2048));
+            hgx_xb_pack_flat<Wt><<<fgrid, 256, 0, s>>>(E, sh.bc_atom, sh.bc_part, sh.bc_lid, fa_next, lvl_next, dctr,
+                                                       seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs, NP);
+        } else {
+            hgx_xb_pack<Wt><<<pgrid, 256, 0, s>>>(A, fa_next, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_lid,
+                                                  lvl_next, dctr, seg + 2 * NP, seg + 3 * NP, send_h, send_p, xs, NP);
+        }
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
         read_counts();

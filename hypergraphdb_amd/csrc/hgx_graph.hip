@@ -56,6 +56,7 @@ void graph_release(hgx_graph* g) {
         (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);
         (void)hipFree(g->shard->bc_off); (void)hipFree(g->shard->bc_part); (void)hipFree(g->shard->bc_lid);
         (void)hipFree(g->shard->xo_slot); (void)hipFree(g->shard->bc_slot);
+        (void)hipFree(g->shard->bc_atom);
         delete g->shard;
     }
     delete g;

@@ -124,6 +124,7 @@ struct ShardInfo {
     // same atom) answers in slot j of my receive segment from q.
     int32_t* xo_slot = nullptr;          // [A_local] ghost: its slot in the (me -> owner) segment
     int32_t* bc_slot = nullptr;          // [bc entries] its slot in the (me -> holder) segment
+    int32_t* bc_atom = nullptr;          // [bc entries] the owned atom of the entry (flat broadcast pack)
     int32_t xmode = 1;                   // HGX_OPT_PART_EXCHANGE: 1 compressed records (default), 2 static slots, 0 per level
     // the global -> local id of an atom present here, or -1 (binary search of l2g_host)
     int32_t local_of(int64_t v) const {

@@ -261,6 +261,26 @@ def test_two_processes_gloo_transport():
     assert all(p.exitcode == 0 for p in ps)
 
 
+@pytest.mark.parametrize("flat", ["0", "1", "2"])
+def test_broadcast_pack_forms(flat, monkeypatch):
+    """The broadcast pack walks owned atoms (HGX_XB_FLAT=0), takes the broadcast entries on dense
+    levels (1, the default) or on every level (2): identical results to the whole-snapshot engine and
+    the oracle on 2, 3 and 8 parts, dense (1024 sources on a power-law hypergraph) and sparse levels."""
+    from hypergraphdb_amd import synth
+    monkeypatch.setenv("HGX_XB_FLAT", flat)
+    rng = np.random.default_rng(90)
+    g = K.random_graph(rng, 1500, 2500, max_arity=7, n_types=3)
+    seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
+    for NP in (3, 8):
+        compare(g, NP, seeds, None)
+    compare(g, 3, seeds, None, K.ALGEN_MODES[6], 2)
+    h = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=23)
+    hs = rng.integers(0, h["num_atoms"], 1024).astype(np.int32)
+    for NP in (2, 8):
+        st = compare(h, NP, hs, 4)
+        assert all(s["bytes_exchanged"] > 0 for s in st)
+
+
 @pytest.mark.parametrize("xmode", [0, 2])
 def test_exchange_modes(xmode):
     """HGX_OPT_PART_EXCHANGE = static slots on every level (2) or chosen per level by the sampled
