@@ -81,7 +81,8 @@ class BfsStats(C.Structure):
                 ("level_rows", (C.c_int64 * 8) * 64), ("ms_exchange", C.c_double),
                 ("bytes_exchanged", C.c_double), ("level_xbytes", C.c_double * 64),
                 ("level_xpair_max", C.c_double * 64), ("level_xms", C.c_double * 64),
-                ("xwords_nonzero", C.c_double), ("xwords_total", C.c_double), ("bytes_min", C.c_double)]
+                ("xwords_nonzero", C.c_double), ("xwords_total", C.c_double), ("bytes_min", C.c_double),
+                ("level_xtrips", C.c_int32 * 64)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
@@ -99,6 +100,7 @@ class BfsStats(C.Structure):
         d["level_xbytes"] = [float(x) for x in self.level_xbytes[:n]]
         d["level_xpair_max"] = [float(x) for x in self.level_xpair_max[:n]]
         d["level_xms"] = [round(float(x), 4) for x in self.level_xms[:n]]
+        d["level_xtrips"] = [int(x) for x in self.level_xtrips[:n]]
         d["xwords_nonzero"], d["xwords_total"] = self.xwords_nonzero, self.xwords_total
         return d
 

@@ -3375,6 +3375,61 @@ __global__ void __launch_bounds__(256) hgx_xb_pack_flat(int64_t E, const int32_t
     }
 }
 
+// Broadcast of a level on which (nearly) every ghost of the group has news: every broadcast entry
+// writes a dense record at its static slot (bc_slot: the holder's ghosts of this owner in ascending
+// order, so the holder knows every segment's size) -- mask all ones with news, 0 without (the holder
+// skips it).  One pass, no counting, no LDS atomics; the phase needs no count read-back and no count
+// all-gather.  U entries per lane group in flight.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_xb_pack_static(int64_t E, int NP, const int32_t* __restrict__ bc_atom,
+                                                          const int32_t* __restrict__ bc_part,
+                                                          const int32_t* __restrict__ bc_lid,
+                                                          const int32_t* __restrict__ bc_slot,
+                                                          const u64* __restrict__ fa_next, const u64* __restrict__ lvl_next,
+                                                          const int64_t* __restrict__ seg_h,
+                                                          const int64_t* __restrict__ seg_p, u64* __restrict__ hdr,
+                                                          u64* __restrict__ pay, u64* __restrict__ nzw) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G, U = 4;
+    constexpr uint32_t FULLM = full_word_mask(W);
+    typedef Vec<WPL> V;
+    __shared__ int64_t sh_h[kMaxParts], sh_p[kMaxParts];
+    for (int q = threadIdx.x; q < NP; q += blockDim.x) {
+        sh_h[q] = seg_h[q];
+        sh_p[q] = seg_p[q];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    u64 nz = 0;
+    for (int64_t base = wave * PER * U; base < E; base += nwave * PER * U) {   // wave-uniform
+        typename V::T row[U];
+        int32_t q[U], lid[U], slot[U];
+        bool ok[U], news[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = base + u * PER + g;
+            ok[u] = e < E;
+            const int32_t t = ok[u] ? bc_atom[e] : 0;
+            q[u] = ok[u] ? bc_part[e] : 0;
+            lid[u] = ok[u] ? bc_lid[e] : 0;
+            slot[u] = ok[u] ? bc_slot[e] : 0;
+            news[u] = ok[u] && bit(fa_next, t);
+            row[u] = news[u] ? V::ld(lvl_next + (int64_t)t * W + sub * WPL) : V::zero();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t nzm = group_mask<W>(row[u]);
+            if (ok[u]) {
+                put_record<W>(hdr, pay + sh_p[q[u]], sh_h[q[u]] + slot[u], (int64_t)slot[u] * W, lid[u],
+                              news[u] ? FULLM : 0u, row[u], true);
+                if (sub == 0) nz += (u64)__popc(nzm);
+            }
+        }
+    }
+    block_add_sh(nzw, 2, nz);
+}
+
 // Apply n received records (headers hdr, payload pay of one source), one G-lane group each.
 // REDUCE: OR a partial row into an owned atom (new = row & ~vis; a source sends an atom at most
 // once, so one launch per source segment); BROADCAST: a ghost's final row replaces the partial one
@@ -3418,7 +3473,7 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
         const typename V::T nw = REDUCE ? (row & ~old) : row;
         const bool any = group_any<G>(V::nz(nw));
         const bool isfull = group_all<G>(V::eq(old | nw, FULL));
-        if (valid && (any || !REDUCE)) {
+        if (valid && (REDUCE ? any : mask != 0u)) {   // a static broadcast record without news has mask 0
             typename V::T lv = nw;
             if (REDUCE && was) lv = lv0 | nw;
             V::st(lvl_next + t * W + sub * WPL, lv);
@@ -3993,7 +4048,9 @@ struct Exchange {
         HGX_HIP(hipStreamSynchronize(g->stream));   // hs is a local
     }
     // cursor / stats words back to the host (pinned copy, polled: no staging, no sleeping wait)
+    int trips = 0;                      // host round trips of the current level (read-backs, count all-gathers)
     void read_back(std::vector<u64>& hc, size_t cbytes) {
+        ++trips;
         HGX_HIP(hipMemcpyAsync(hpin, dctr, cbytes, hipMemcpyDeviceToHost, g->stream));
         spin_sync(g->stream);
         std::memcpy(hc.data(), hpin, cbytes);
@@ -4019,22 +4076,36 @@ struct Exchange {
     // segment starts (records) of what I send / receive; rbase[q+1] - rbase[q] bounds what q sends
     // me.  Returns the per-source record counts; source q's records land at recv_h + 2 * rbase[q],
     // its payload at recv_p + W * rbase[q].  *pair_max: the largest bytes I send one peer.
+    // *group (optional): the group's records, words and ghosts (every part gets the same numbers).
     void ship(const std::vector<int64_t>& sbase, const std::vector<int64_t>& rbase, const std::vector<u64>& cnt,
-              const std::vector<u64>& wcnt, std::vector<int64_t>& rcnt, double* pair_max) {
+              const std::vector<u64>& wcnt, std::vector<int64_t>& rcnt, double* pair_max, double* group = nullptr) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts, me = sh.part;
-        std::vector<int64_t> mine(2 * (size_t)NP), all((size_t)NP * 2 * NP);
+        const int K = 2 * NP + 1;   // records and words to every part, then my ghost count
+        std::vector<int64_t> mine((size_t)K), all((size_t)NP * K);
         for (int q = 0; q < NP; ++q) {
             mine[q] = (int64_t)cnt[q];
             mine[NP + q] = (int64_t)wcnt[q];
         }
-        coll([&] { tr->allgather_i64(mine.data(), 2 * NP, all.data(), g->stream); });
+        mine[2 * NP] = rseg[NP];
+        ++trips;
+        coll([&] { tr->allgather_i64(mine.data(), K, all.data(), g->stream); });
+        if (group) {
+            group[0] = group[1] = group[2] = 0;
+            for (int p = 0; p < NP; ++p) {
+                for (int q = 0; q < NP; ++q) {
+                    group[0] += (double)all[(size_t)p * K + q];
+                    group[1] += (double)all[(size_t)p * K + NP + q];
+                }
+                group[2] += (double)all[(size_t)p * K + 2 * NP];
+            }
+        }
         std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP), psoff(NP), psbytes(NP), proff(NP),
             prbytes(NP);
         rcnt.assign(NP, 0);
         *pair_max = 0;
         for (int q = 0; q < NP; ++q) {
-            const int64_t rr = all[(size_t)q * 2 * NP + me], rw = all[(size_t)q * 2 * NP + NP + me];
+            const int64_t rr = all[(size_t)q * K + me], rw = all[(size_t)q * K + NP + me];
             if (rr > rbase[q + 1] - rbase[q] || rw > rr * W) fail(HGX_E_DEVICE, "partitioned BFS: receive overflow");
             rcnt[q] = rr;
             soff[q] = sbase[q] * 16;
@@ -4068,6 +4139,7 @@ struct Exchange {
         const int64_t A = g->A;
         const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(A, 64) / 4 + 1, 2048));
         const double before = bytes_sent;
+        trips = 0;
         const size_t cbytes = sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride);
         u64* xs = dctr + NP * kCurStride;   // sharded stats (see dctr)
         std::vector<u64> hc(NP * kCurStride + kStatShards * kStatStride), cnt(NP), wcnt(NP);
@@ -4114,6 +4186,7 @@ struct Exchange {
             read_back(hc, cbytes);
             int64_t mine2[4] = {(int64_t)stat_sum(3), rseg[NP], (int64_t)stat_sum(4), (int64_t)stat_sum(5)};
             std::vector<int64_t> all2(4 * (size_t)NP);
+            ++trips;
             coll([&] { tr->allgather_i64(mine2, 4, all2.data(), s); });
             double news = 0, ghosts = 0, nzw = 0, rows = 0;
             for (int q = 0; q < NP; ++q) {
@@ -4175,7 +4248,17 @@ struct Exchange {
         const int flat_opt = fe ? std::atoi(fe) : 1;
         const bool flat = bseg[NP] > 0 && (flat_opt == 2 || (flat_opt == 1 && sent_r * 2 >= (u64)rseg[NP] &&
                                                              sent_w * 10 > sent_r * (u64)Wt * 7));
-        ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r);
+        double grp[3];
+        ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r, grp);
+        // static broadcast (group-wide choice from the all-gathered reduce counts, so every part
+        // agrees): at least 85% of the group's ghosts had news and their rows were > 70% nonzero
+        // words -- shipping a record for every entry then costs < 18% more bytes than the news alone
+        // and saves the counting pass and the phase's count round trips.  HGX_XB_STATIC=0 never,
+        // 2 on every level (A/B and tests).
+        const char* se = std::getenv("HGX_XB_STATIC");
+        const int static_opt = se ? std::atoi(se) : 1;
+        const bool bstatic = static_opt == 2 || (static_opt == 1 && grp[2] > 0 && grp[0] >= 0.85 * grp[2] &&
+                                                 grp[1] * 10.0 > grp[0] * Wt * 7.0);
         Events e1 = tm.start(kKindExchange, d);
         apply(true, bseg);
         if (last) {   // no broadcast after the final level
@@ -4188,6 +4271,28 @@ struct Exchange {
         }
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
+        if (bstatic) {
+            const int64_t E = bseg[NP];
+            if (E > 0) {
+                const int sgrid = grid_for(ceil_div(E, 4) * Lay<Wt>::G, 256, 4096);
+                hgx_xb_pack_static<Wt><<<sgrid, 256, 0, s>>>(E, NP, sh.bc_atom, sh.bc_part, sh.bc_lid, sh.bc_slot,
+                                                             fa_next, lvl_next, seg + 2 * NP, seg + 3 * NP, send_h,
+                                                             send_p, xs);
+                HGX_CHECK_LAUNCH();
+            }
+            tm.stop(e1);
+            ship_known(bseg, sh.bc_count, rseg, sh.ghost_count, &pm_b);
+            rcnt.assign(sh.ghost_count.begin(), sh.ghost_count.end());
+            Events e2 = tm.start(kKindExchange, d);
+            apply(false, rseg);
+            hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
+                A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
+            HGX_CHECK_LAUNCH();
+            tm.stop(e2);
+            const u64 tot = finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
+            nz_words += (double)stat_sum(2);
+            return tot;
+        }
         if (flat) {
             const int64_t E = bseg[NP];
             const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E, 64) / 4 + 1, 2048));
@@ -4222,10 +4327,37 @@ struct Exchange {
         *pair_max = pm;
         int64_t nl = (int64_t)fs[0];
         std::vector<int64_t> nall(NP);
+        ++trips;
         coll([&] { tr->allgather_i64(&nl, 1, nall.data(), s); });
         u64 tot = 0;
         for (int q = 0; q < NP; ++q) tot += (u64)nall[q];
         return tot;
+    }
+    // A record phase whose sizes both sides know (static broadcast): scnt[q] records (headers and W
+    // words each) from my segments sbase[q] to q, rcnt[q] from q into rbase[q].  No count exchange.
+    void ship_known(const std::vector<int64_t>& sbase, const std::vector<int64_t>& scnt,
+                    const std::vector<int64_t>& rbase, const std::vector<int64_t>& rcnt, double* pair_max) {
+        const int NP = g->shard->n_parts;
+        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP), psoff(NP), psbytes(NP), proff(NP),
+            prbytes(NP);
+        *pair_max = 0;
+        for (int q = 0; q < NP; ++q) {
+            soff[q] = sbase[q] * 16;
+            sbytes[q] = scnt[q] * 16;
+            roff[q] = rbase[q] * 16;
+            rbytes[q] = rcnt[q] * 16;
+            psoff[q] = sbase[q] * W * 8;
+            psbytes[q] = scnt[q] * W * 8;
+            proff[q] = rbase[q] * W * 8;
+            prbytes[q] = rcnt[q] * W * 8;
+            bytes_sent += (double)(sbytes[q] + psbytes[q]);
+            words += (double)scnt[q] * W;
+            *pair_max = std::max(*pair_max, (double)(sbytes[q] + psbytes[q]));
+        }
+        coll([&] {
+            tr->alltoallv(send_h, soff.data(), sbytes.data(), recv_h, roff.data(), rbytes.data(), g->stream);
+            tr->alltoallv(send_p, psoff.data(), psbytes.data(), recv_p, proff.data(), prbytes.data(), g->stream);
+        });
     }
     // One static-slot phase: scnt[q] full rows from my segment sbase[q] to q, rcnt[q] from q into
     // rbase[q] (sizes known on both sides: no count exchange).
@@ -4754,6 +4886,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             if (d < 64) {
                 res->stats.level_xbytes[d] += lb;
                 res->stats.level_xpair_max[d] = std::max(res->stats.level_xpair_max[d], pm);
+                res->stats.level_xtrips[d] = std::max(res->stats.level_xtrips[d], (int32_t)ex->trips);
             }
         }
         Pend& pn = pend[d & 1];

@@ -134,6 +134,9 @@ typedef struct hgx_bfs_stats {
      * of the frontier atoms or every CSR column once (whichever is less) + one S/8-byte row per
      * frontier atom read + one per new atom written */
     double  bytes_min;
+    /* partitioned BFS: host round trips of level d's exchange (count / statistics read-backs and
+     * count all-gathers; the row transfers are not counted), the largest over the parts' batches */
+    int32_t level_xtrips[64];
 } hgx_bfs_stats;
 
 const char *hgx_version(void);

@@ -261,13 +261,17 @@ def test_two_processes_gloo_transport():
     assert all(p.exitcode == 0 for p in ps)
 
 
-@pytest.mark.parametrize("flat", ["0", "1", "2"])
-def test_broadcast_pack_forms(flat, monkeypatch):
+@pytest.mark.parametrize("flat,static", [("0", "0"), ("1", "0"), ("2", "0"), ("1", "1"), ("0", "2")])
+def test_broadcast_pack_forms(flat, static, monkeypatch):
     """The broadcast pack walks owned atoms (HGX_XB_FLAT=0), takes the broadcast entries on dense
-    levels (1, the default) or on every level (2): identical results to the whole-snapshot engine and
-    the oracle on 2, 3 and 8 parts, dense (1024 sources on a power-law hypergraph) and sparse levels."""
+    levels (1, the default) or on every level (2); with HGX_XB_STATIC every broadcast entry ships a
+    record at its static slot (mask 0 without news) on the levels where the group's ghosts nearly all
+    had news (1, the default) or on every level (2): identical results to the whole-snapshot engine
+    and the oracle on 2, 3 and 8 parts, dense (1024 sources on a power-law hypergraph) and sparse
+    levels."""
     from hypergraphdb_amd import synth
     monkeypatch.setenv("HGX_XB_FLAT", flat)
+    monkeypatch.setenv("HGX_XB_STATIC", static)
     rng = np.random.default_rng(90)
     g = K.random_graph(rng, 1500, 2500, max_arity=7, n_types=3)
     seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
@@ -279,6 +283,15 @@ def test_broadcast_pack_forms(flat, monkeypatch):
     for NP in (2, 8):
         st = compare(h, NP, hs, 4)
         assert all(s["bytes_exchanged"] > 0 for s in st)
+        # host round trips of level 0 (not the final level): counted records in both phases take 6,
+        # a static broadcast 4; the final level (no broadcast) 4
+        for s in st:
+            if static == "2":
+                assert s["level_xtrips"][0] == 4, s["level_xtrips"]
+            elif static == "0":
+                assert s["level_xtrips"][0] == 6, s["level_xtrips"]
+            if len(s["level_xtrips"]) == 4:
+                assert s["level_xtrips"][3] == 4, s["level_xtrips"]
 
 
 @pytest.mark.parametrize("xmode", [0, 2])

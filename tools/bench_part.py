@@ -9,11 +9,12 @@ ONE peer (an all-to-all over xGMI runs its 7 peer links in parallel, each at ~15
 MI355X_MICROARCH / SURVEY.md 5).  The modelled NP-GPU level time is
     max_p device_ms(p) + max_pair_bytes / 153 GB/s + host round trips x --sync-us
 (no overlap of exchange and compute assumed), summed over the levels; the 1-part run is the
-replica on one GPU.  Host round trips of a level (compressed records): the two count read-backs,
-the two count all-gathers and the termination all-gather (5; 3 at the final level of a depth-limited
+replica on one GPU.  Host round trips of a level: what the engine counted (stats level_xtrips:
+the count and statistics read-backs and the count / termination all-gathers -- 6 with counted
+records in both phases, 4 with a static broadcast or at the final level of a depth-limited
 traversal, which has no broadcast phase; the all-to-alls are ordered on the stream without a host
-wait); --sync-us prices one (a small RCCL collective or a read-back at 8
-ranks, default 40 us).  Counts of every source must equal the replica's.
+wait); --sync-us prices one (a small RCCL collective or a read-back at 8 ranks, default 40 us).
+Counts of every source must equal the replica's.
 
   python tools/bench_part.py --scale 0.25 --parts 1 8 --out gpurun_out/part.json
 """
@@ -106,10 +107,14 @@ def measure(args, g, snaps, NP, xmode, plan_s, build_s, info, rows, state):
             pm = max(max((s[p]["level_xpair_max"][d] for s in sts if d < len(s[p]["level_xpair_max"])), default=0)
                      for p in range(NP))
             link_ms = pm / (XGMI_LINK_GBS * 1e9) * 1e3
-            # the final level of a depth-limited traversal has no broadcast phase: 3 round trips
-            trips = 3 if d == args.depth - 1 else 5
+            # the level's host round trips as the engine counted them (count / statistics read-backs and
+            # count all-gathers: 6 with counted records in both phases, 4 with a static broadcast or on
+            # the final level of a depth-limited traversal, which has no broadcast phase)
+            trips = max((s[p].get("level_xtrips", [0] * nlev)[d] for s in sts for p in range(NP)
+                         if d < len(s[p].get("level_xtrips", []))), default=0)
             sync_ms = (trips * args.sync_us / 1e3) if NP > 1 else 0.0
             levels.append({"max_part_device_ms": round(max(dev), 3), "max_part_exchange_kernels_ms": round(max(xms), 3),
+                           "host_trips": trips,
                            "bytes_per_part_max": max(xb), "max_pair_bytes": pm, "max_pair_link_ms": round(link_ms, 3),
                            "host_sync_ms": round(sync_ms, 3),
                            "model_level_ms": round(max(dev) + link_ms + sync_ms, 3),
