@@ -356,17 +356,18 @@ def run_config5(args, ctx, barrier_sync):
     # the same step with the directions one after the other (reported next to the timed line, with the
     # push kernels' roofline when they run alone: side by side they share the CUs and each launch lasts
     # longer)
+    n5 = max(args.steps, 20)   # a step is ~2 ms: at least 20 of them
     t1 = time.perf_counter()
     seq_sts = []
-    for _ in range(args.steps):
+    for _ in range(n5):
         seq_sts += [st for _, st in step(concurrent=False)]
-    seq_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    seq_ms = (time.perf_counter() - t1) / n5 * 1e3
     seq_sts = [x.as_dict() for x in seq_sts]
     barrier_sync()
     t1 = time.perf_counter()
     sts = []
     readout = 0
-    for _ in range(args.steps):
+    for _ in range(n5):
         for n, st in step():
             readout += n
             sts.append(st)
@@ -375,11 +376,11 @@ def run_config5(args, ctx, barrier_sync):
     sts = [x.as_dict() for x in sts]
     pool.shutdown()
     views[1].close()
-    assert readout == closure * args.steps, "config-5 readout differs from the warm-up closures"
-    edges = ctx.sum(trav * args.steps)
+    assert readout == closure * n5, "config-5 readout differs from the warm-up closures"
+    edges = ctx.sum(trav * n5)
     out = {"metric": "hyperedge TEPS (subsumption closures)", "value": edges / dt, "unit": "TEPS",
-           "closures_per_s": ctx.sum(2 * len(g["seeds"]) * args.steps) / dt, "scaling": "weak",
-           "ms_per_step": round(dt / args.steps * 1e3, 3), "levels": max(s["n_levels_expanded"] for s in sts),
+           "closures_per_s": ctx.sum(2 * len(g["seeds"]) * n5) / dt, "scaling": "weak", "steps": n5,
+           "ms_per_step": round(dt / n5 * 1e3, 3), "levels": max(s["n_levels_expanded"] for s in sts),
            "directions": "concurrent: hg.subsumed on the snapshot, hg.subsumes on an execution context of it",
            "ms_per_step_directions_serial": round(seq_ms, 3),
            "closure_atoms_per_step": closure,
@@ -633,39 +634,41 @@ def main():
         r0 = qset.run(snap3)
         q_off = np.zeros(nq + 1, np.int64)
         q_ids = np.zeros(max(1, int(r0.offsets[-1])), np.int32)
-        tim = np.zeros((args.steps, 3), np.float64)
-        for _ in range(args.warmup):
+        # a step is ~0.1 ms: at least 50 of them, so the timer and the barriers are not a share of it
+        n3 = max(args.steps, 50)
+        tim = np.zeros((n3, 3), np.float64)
+        for _ in range(max(args.warmup, 3)):
             qset.run_into(snap3, q_off, q_ids, tim[0])
         nres = 0
         barrier_sync()
         t0 = time.perf_counter()
-        for i in range(args.steps):
+        for i in range(n3):
             nres = qset.run_into(snap3, q_off, q_ids, tim[i])
         barrier_sync()
+        dtq = max_over_ranks(time.perf_counter() - t0)
         if nres > len(q_ids) or not np.array_equal(q_off, r0.offsets) or not np.array_equal(q_ids[:nres], r0.ids):
             raise RuntimeError("config3: the timed batches differ from the first run")
         ms = [{"ms_total": t[0], "ms_match": t[1], "bytes_match": t[2]} for t in tim]
-        dtq = max_over_ranks(time.perf_counter() - t0)
-        qps = sum_over_ranks(len(qs) * args.steps) / dtq
+        qps = sum_over_ranks(len(qs) * n3) / dtq
         qset.close()
         # the same batch handed over in host memory each step (hgx_pattern_batch_packed: the queries
         # cross PCIe inside the step) -- the PCIe-inclusive rate, reported beside the line
         for _ in range(args.warmup):
             pattern_batch_arrays(snap3, *packed)
         t1 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(n3):
             pattern_batch_arrays(snap3, *packed)
         dtp = time.perf_counter() - t1
         mm = sum(m["ms_match"] for m in ms) / len(ms)
         bm = sum(m["bytes_match"] for m in ms) / len(ms)
         ach = bm / (mm / 1e3) / 1e9 if mm > 0 else 0.0
         pattern = {"metric": "pattern-match queries/sec", "value": round(qps, 1), "unit": "queries/s",
-                   "ms_per_step": round(dtq / args.steps * 1e3, 3), "queries_per_step": len(qs),
+                   "ms_per_step": round(dtq / n3 * 1e3, 3), "steps": n3, "queries_per_step": len(qs),
                    "results_per_step": nres,
                    "inputs": "the 10K packed queries resident in HBM (hgx_query_set_create before the timed steps)",
                    "results": "offsets + ids into preallocated host arrays each step (hgx_pattern_batch_set_into)",
-                   "pcie_inclusive": {"value": round(len(qs) * args.steps / dtp, 1), "unit": "queries/s",
-                                      "ms_per_step": round(dtp / args.steps * 1e3, 3),
+                   "pcie_inclusive": {"value": round(len(qs) * n3 / dtp, 1), "unit": "queries/s",
+                                      "ms_per_step": round(dtp / n3 * 1e3, 3),
                                       "path": "hgx_pattern_batch_packed: host arrays staged and read over PCIe each step"},
                    "workload": "config3: 50M links over 10M nodes, arity 3-6, 64 types, 10K queries",
                    "roofline": {"bound": "hbm", "kernel": "hgx_pattern_match_flat", "achieved": round(ach, 1),
@@ -673,7 +676,7 @@ def main():
                                 "traffic": pmc_traffic("hgx_pattern_match_flat", "config3")[0],
                                 "traffic_from": pmc_traffic("hgx_pattern_match_flat", "config3")[1],
                                 "avg_launch_ms": round(mm, 4), "bytes_per_launch": bm}}
-        log(f"rank {rank}: pattern {qps:.1f} q/s ({len(qs) * args.steps / dtp:.1f} with the queries crossing PCIe each "
+        log(f"rank {rank}: pattern {qps:.1f} q/s ({len(qs) * n3 / dtp:.1f} with the queries crossing PCIe each "
             f"step), match kernel {mm:.3f} ms")
         snap3.close()
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
