@@ -4428,7 +4428,14 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // are cleared kZeroLevels at a time as the traversal reaches them
     bt.lvl.push_back((u64*)g->alloc(row_bytes));
     bt.fa.push_back((u64*)g->alloc(bm_bytes));
+    const bool sparse_ok = (g->bfs_flags & 8) != 0;
+    u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
+    u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
+    const size_t flist_bytes = sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1);
+    int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
+    int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
     ZeroList z{};
+    if (cand) z.add(cand, bm_bytes);   // the first push level's candidate words (no memset of their own)
     z.add(ever, bm_bytes);
     z.add(full, bm_bytes);
     z.add(bt.fa[0], bm_bytes);
@@ -4487,12 +4494,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // frontier atoms and only candidate tiles are gathered / pulled.  Otherwise every tile is scanned.
     std::unique_ptr<Exchange> ex;   // one part: no ghosts, nothing to exchange
     if (tr && tr->world > 1) ex.reset(new Exchange(g, tr, W));
-    const bool sparse_ok = (g->bfs_flags & 8) != 0;
-    u64* lcand = sparse_ok ? (u64*)g->alloc(la_bytes) : nullptr;
-    u64* cand = sparse_ok ? (u64*)g->alloc(bm_bytes) : nullptr;
-    const size_t flist_bytes = sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1);
-    int32_t* flist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // frontier list (push levels)
-    int32_t* clist = sparse_ok ? (int32_t*)g->alloc(flist_bytes) : nullptr;   // push candidates
     // push levels: fl = this level's frontier list, cl = its candidates; the finalise turns cl into the
     // next level's frontier list (chained), so consecutive push levels swap the two
     int32_t *fl = flist, *cl = clist;
@@ -4507,7 +4508,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     }
     if (!g->pend_ev[0])   // the two in-flight levels' events (once per graph)
         for (int k = 0; k < 2; ++k) HGX_HIP(hipEventCreateWithFlags(&g->pend_ev[k], hipEventDisableTiming));
-    bool chained = false, cand_clean = false;
+    // cand was cleared by the prologue launch, and so were the scratch slots n_fl / n_cl (until a level
+    // uses them): the first push level issues no memset (each costs a host API call, ~20 us between
+    // the prologue's device operations on config 5)
+    bool chained = false, cand_clean = cand != nullptr, scratch_clean = true;
     const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
@@ -4625,6 +4629,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         }
         u64* lvl = cur_lvl;
         u64* fa = cur_fa;
+        const bool scratch_zero = scratch_clean;   // first level: n_fl / n_cl still zero from the prologue
+        scratch_clean = false;
         bool codes_written = false;   // this level's finalise wrote the codes of its new rows
         bool coded = false;
         bool flag_level = false;   // counters written by the finalise into mapped host memory
@@ -4697,8 +4703,10 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // hgx_opush and n_cl by the previous finalise
             if (!cand_clean) HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
             if (!chained) {   // the frontier list from the bitmap (else the last finalise left it in fl)
-                HGX_HIP(hipMemsetAsync(n_cl, 0, sizeof(u64), s));
-                HGX_HIP(hipMemsetAsync(n_fl, 0, sizeof(u64), s));
+                if (!scratch_zero) {
+                    HGX_HIP(hipMemsetAsync(n_cl, 0, sizeof(u64), s));
+                    HGX_HIP(hipMemsetAsync(n_fl, 0, sizeof(u64), s));
+                }
                 const int fgrid = grid_for(ceil_div(A, 64), 256, 256);   // <= 256 list atomics per level
                 hgx_frontier_list<<<fgrid, 256, 0, s>>>(A, fa, g->inc_off, fl, n_fl, kPushLight);
                 HGX_CHECK_LAUNCH();
