@@ -1044,20 +1044,22 @@ __global__ void hgx_q_finish_stat_flat(const int32_t* __restrict__ n_chunks_p, c
 }
 
 // ---------------------------------------------------------------------------------------------
-// Single-pass flat pipeline (HGX_OPT_QUERY_FLAT = 2, the default): five back-to-back kernels, no
+// Single-pass flat pipeline (HGX_OPT_QUERY_FLAT = 2, the default): four back-to-back kernels, no
 // single-workgroup pass, no copy engine and no host round trip inside a batch.
 //   hgx_q_norm_sp / hgx_q_plan_sp -- a thread per query: normalise + plan (packed batches, reading the
 //        caller's arrays straight from the pinned staging area and keeping device copies of the
 //        type and pattern columns the match reads) or plan (host-normalised batches); per block of 256
 //        queries the candidate total and the smallest bad / unsupported query;
 //   hgx_q_scan_sp   -- a block of 256 queries sums the candidate totals of the blocks before it (one
-//        load per thread), scans its own queries, writes their candidate offsets and the chunk -> first
-//        query map; the last block checks the workspace and publishes the chunk count and statuses;
+//        load per thread), scans its own queries, writes their candidate offsets, the chunk -> first
+//        query map and the chunk -> first query at or past its start; the last block checks the
+//        workspace and publishes the chunk count and statuses;
 //   hgx_pattern_match_flat -- unchanged (a lane per candidate, per-chunk hit masks);
 //   hgx_q_place     -- a block of 256 chunks sums the hit counts of the chunks before it (redundantly:
 //        at most a few loads per thread), scans its own, and copies each chunk's hits as atom ids
-//        into the mapped result area;
-//   hgx_q_offsets_flat -- every query's result offset from its first chunk's offset and hit mask.
+//        into the mapped result area, then the result offsets of the queries starting in its chunks
+//        (from its chunk offsets and their hit masks; a separate hgx_q_offsets_flat launch until
+//        round 3 -- one launch and one dispatch gap fewer).
 // Replaces norm + the one-workgroup scan (15 + 20 us on the config-3 batch), the one-workgroup finish
 // + scatter (17 + 4 us) and the two copies (14 + 7 us, plus ~9 us of dispatch gap after each).
 // Tried first: a decoupled look-back (blocks publishing prefixes through device-scope atomics) in
@@ -1222,8 +1224,10 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
                                                   const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
                                                   const int32_t* __restrict__ link_atom, int64_t* __restrict__ outoff,
                                                   int32_t* __restrict__ ids, int64_t* __restrict__ stat,
-                                                  const u64* __restrict__ ctr, u64* __restrict__ ctr_out) {
-    __shared__ int64_t ws[4], c_off[kPlaceChunks];
+                                                  const u64* __restrict__ ctr, u64* __restrict__ ctr_out, int32_t n,
+                                                  const int32_t* __restrict__ chq, const int64_t* __restrict__ coff,
+                                                  const u64* __restrict__ hitmask, int64_t* __restrict__ q_off) {
+    __shared__ int64_t ws[4], c_off[kPlaceChunks], qb[2];
     __shared__ int32_t c_cnt[kPlaceChunks];
     const int32_t nc = *n_chunks_p;
     const int64_t k0 = (int64_t)blockIdx.x * kPlaceChunks;
@@ -1231,6 +1235,36 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t k = k0 + lane;
     const int32_t cnt = wv == 0 && k < nc ? (int32_t)counts[k] : 0;   // issued before the prefix loads
+    const bool holds_last = nc == 0 ? blockIdx.x == 0 : (nc - 1) / kPlaceChunks == (int32_t)blockIdx.x;
+    // The queries whose first candidate lies in this block's chunks, [qb[0], qb[1]) (the block of the last
+    // chunk: through n), whose result offsets the block writes below.  Boundary kb -> the first query
+    // with a candidate offset >= kb * kFlatChunk: one past chunk kb's owner chq[kb] unless the owner's
+    // candidates start exactly there, then at or before it (zero-candidate queries share that offset:
+    // 64 at a time, one ballot).  Waves 2 and 3 find the two boundaries while wave 0 sums the counts.
+    if (wv >= 2) {
+        const int e = wv - 2;
+        const int64_t kb = k0 + e * kPlaceChunks;
+        int64_t res = 0;
+        if (e == 1 && holds_last) {
+            res = (int64_t)n + 1;
+        } else if (kb > 0 && !stat[2]) {
+            const int64_t target = kb * kFlatChunk;
+            const int64_t q0 = chq[kb];
+            if (coff[q0] < target) {
+                res = q0 + 1;
+            } else {
+                for (int64_t hi = q0;; hi -= 64) {   // wave-uniform; coff[hi] >= target
+                    const int64_t j = hi - 64 + lane;
+                    const u64 m = __ballot(j < 0 || coff[j < 0 ? 0 : j] < target);
+                    if (m) {
+                        res = hi - 64 + (63 - __clzll((long long)m)) + 1;
+                        break;
+                    }
+                }
+            }
+        }
+        if (lane == 0) qb[e] = res;
+    }
     int64_t before = 0;   // hit counts of the chunks before this block, eight loads in flight per thread
     for (int64_t j = threadIdx.x; j < k0; j += 8 * 256) {
         int64_t v[8];
@@ -1265,7 +1299,15 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
 #pragma unroll
     for (int u = 0; u < 16; ++u)
         if (row[u] >= 0) ids[c_off[wv * 16 + u] + lane] = at[u];
-    const bool holds_last = nc == 0 ? blockIdx.x == 0 : (nc - 1) / kPlaceChunks == (int32_t)blockIdx.x;
+    // the result offsets of the queries starting in this block's chunks, from the chunk offsets in LDS
+    // and the chunk's hit mask (the offsets launch folded in)
+    if (!stat[2]) {
+        for (int64_t q = qb[0] + threadIdx.x; q < qb[1]; q += 256) {
+            const int64_t cf = coff[q], kq = cf / kFlatChunk, lc = kq - k0;
+            const u64 hm = kq < nc ? hitmask[kq] : 0ull;
+            q_off[q] = (lc < kPlaceChunks ? c_off[lc] : ws[0]) + __popcll(hm & ((1ull << (cf % kFlatChunk)) - 1ull));
+        }
+    }
     if (holds_last) {
         if (threadIdx.x == 0) {
             const int64_t tot = ws[0];
@@ -2476,9 +2518,7 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
         HGX_CHECK_LAUNCH();
         ev.rec(2, s);
         hgx_q_place<<<(unsigned)std::max<int64_t>(1, ceil_div(capC, kPlaceChunks)), 256, 0, s>>>(
-            nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d);
-        HGX_CHECK_LAUNCH();
-        hgx_q_offsets_flat<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, nch, coff, outoff, hmask, stat_d, qoff_d);
+            nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d, n, chq, coff, hmask, qoff_d);
         HGX_CHECK_LAUNCH();
         ev.rec(3, s);
         spin_sync(s);
