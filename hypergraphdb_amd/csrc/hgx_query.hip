@@ -1055,7 +1055,7 @@ __global__ void hgx_q_finish_stat_flat(const int32_t* __restrict__ n_chunks_p, c
 //        query map and the chunk -> first query at or past its start; the last block checks the
 //        workspace and publishes the chunk count and statuses;
 //   hgx_pattern_match_flat -- unchanged (a lane per candidate, per-chunk hit masks);
-//   hgx_q_place     -- a block of 256 chunks sums the hit counts of the chunks before it (redundantly:
+//   hgx_q_place     -- a block of 64 chunks sums the hit counts of the chunks before it (redundantly:
 //        at most a few loads per thread), scans its own, and copies each chunk's hits as atom ids
 //        into the mapped result area, then the result offsets of the queries starting in its chunks
 //        (from its chunk offsets and their hit masks; a separate hgx_q_offsets_flat launch until
