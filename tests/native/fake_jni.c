@@ -80,7 +80,7 @@ static struct _jobject *new_obj(fj_env *f, int kind, int64_t n) {
     struct _jobject *o = (struct _jobject *)calloc(1, sizeof *o);
     o->kind = kind;
     o->n = n;
-    o->data = calloc((size_t)(n > 0 ? n : 1) + (kind == K_STRING), k_elem[kind]);
+    o->data = calloc((size_t)(n > 0 ? n : 1) + (kind == K_STRING || kind == K_CLASS), k_elem[kind]);   /* names: + NUL */
     o->next = f->objs;
     f->objs = o;
     return o;
