@@ -525,3 +525,59 @@ def test_query_set_resident_batches():
         QuerySet(snap, *bad)
     ctx.close()
     snap.close()
+
+
+def test_placement_query_ranges_at_block_starts():
+    """The placement kernel writes the result offsets of the queries starting in its 64 chunks (4096
+    candidates): its query range starts one past the owner of the candidate before the block, or --
+    when a query's candidates begin exactly at the block start -- at the first of the candidate-free
+    queries before it (a ballot over 64 queries at a time).  Untyped one-anchor queries have exactly
+    deg(anchor) candidates, so the batch is built to put a query start exactly on block starts, after
+    runs of 1, 63, 64, 65, 130 and 300 candidate-free queries, with such runs at the batch's head and
+    tail too; single-pass results equal the oracle's and the flat path's offsets."""
+    from hypergraphdb_amd import _lib
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    N, S = 2000, 50                      # node atoms (deg(v) = v % 98), sink atoms
+    link_atom, tgt_off, tgt_idx = [], [0], []
+    for v in range(N):
+        for j in range(v % 98):
+            link_atom.append(N + S + len(link_atom))
+            tgt_idx += [v, N + (v * 7 + j) % S]
+            tgt_off.append(len(tgt_idx))
+    M = len(link_atom)
+    g = {"num_atoms": N + S + M, "link_atom": np.array(link_atom, np.int32), "tgt_off": np.array(tgt_off, np.int64),
+         "tgt_idx": np.array(tgt_idx, np.int32), "link_type": np.ones(M, np.int32)}
+    snap, orc = snapshot(g), oracle(g)
+    by_deg = {}
+    for v in range(N):
+        by_deg.setdefault(v % 98, []).append(v)
+    iso = by_deg[0]
+    anchors, total, block = [], 0, 64 * 64
+    anchors += [iso[i % len(iso)] for i in range(150)]
+    rng = np.random.default_rng(2024)
+    for run in (1, 63, 64, 65, 130, 300, 7):
+        target = (total // block + 2) * block   # fill to a block start exactly, then the run
+        while total < target:
+            d = min(97, target - total, int(rng.integers(20, 98)))
+            anchors.append(by_deg[d][int(rng.integers(0, len(by_deg[d])))])
+            total += d
+        anchors += [iso[i % len(iso)] for i in range(run)]
+    for _ in range(40):
+        d = int(rng.integers(1, 98))
+        anchors.append(by_deg[d][0])
+    anchors += [iso[i % len(iso)] for i in range(150)]
+    n = len(anchors)
+    b = (np.full(n, -1, np.int32), np.arange(n + 1, dtype=np.int64), np.array(anchors, np.int32),
+         np.zeros(n, np.int32), np.zeros(n + 1, np.int64), np.zeros(0, np.int32))
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
+    r2 = pattern_batch_arrays(snap, *b)
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 1)
+    r1 = pattern_batch_arrays(snap, *b)
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
+    assert np.array_equal(r2.offsets, r1.offsets) and np.array_equal(r2.ids, r1.ids)
+    cache = {}
+    for q, a in enumerate(anchors):
+        if a not in cache:
+            cache[a] = orc.and_query(-1, [a], None).tolist()
+        assert r2.ids[r2.offsets[q]:r2.offsets[q + 1]].tolist() == cache[a], (q, a)
+    assert r2.offsets[-1] == sum(a % 98 for a in anchors)
