@@ -581,3 +581,8 @@ def test_placement_query_ranges_at_block_starts():
             cache[a] = orc.and_query(-1, [a], None).tolist()
         assert r2.ids[r2.offsets[q]:r2.offsets[q + 1]].tolist() == cache[a], (q, a)
     assert r2.offsets[-1] == sum(a % 98 for a in anchors)
+    # every query's hits are its candidates here, so the offsets show the alignment the batch was built for:
+    # a query with candidates starting exactly on a block start right after a candidate-free run
+    aligned = [q for q in range(1, n) if anchors[q] % 98 and anchors[q - 1] % 98 == 0 and r2.offsets[q] > 0
+               and r2.offsets[q] % block == 0]
+    assert len(aligned) >= 6, aligned
