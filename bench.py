@@ -232,13 +232,15 @@ def run_config4(args, ctx, barrier_sync, result):
     wl = (f"config4: 100M nodes / 200M links (1.0B incidences), Chung-Lu gamma 2.1, {args.sources}-source BFS "
           f"depth {args.depth}" if args.c4_scale == 1.0 else f"config4 at scale {args.c4_scale}")
 
+    last = {}
+
     def timed(run, n_steps):
         barrier_sync()
         t1 = time.perf_counter()
         st = []
         for _ in range(n_steps):
             r = run()
-            r.counts()   # the readout
+            last["counts"] = r.counts()   # the readout (the last step's counts are checked below)
             st.append(r.stats(accounting=False, raw=True))
             r.close()
         barrier_sync()
@@ -254,10 +256,14 @@ def run_config4(args, ctx, barrier_sync, result):
     sh.close()
     snap.set_timing(True)
     mine = hdist.rank_sources(g, args.sources, rank)
+    ref_counts = None   # rank 0's replica batch runs g["seeds"]: the partitioned leg's expected counts
     for _ in range(max(args.warmup, 1)):
         r = pbfs_batch_group([snap], mine, args.depth)
         acct = r.parts[0].stats(accounting=True)
+        if ref_counts is None:
+            ref_counts = r.parts[0].counts()
         r.close()
+    ref_edges = acct["traversed_edges"] if rank == 0 else 0.0
     dt, st = timed(lambda: pbfs_batch_group([snap], mine, args.depth).parts[0], args.steps)
     edges = ctx.sum(acct["traversed_edges"] * args.steps)
     result["replicated"] = {
@@ -270,7 +276,8 @@ def run_config4(args, ctx, barrier_sync, result):
     del snap
     if world == 1:
         result["partitioned"] = dict(result["replicated"], scaling="strong",
-                                     parallelism="one part: the partition degenerates to the replica")
+                                     parallelism="one part: the partition degenerates to the replica",
+                                     parity="n/a: one part is the replica")
         return
     # vertex cut over the ranks (every rank computes the same plan), RCCL reduce + broadcast per level
     seeds = g["seeds"]
@@ -284,23 +291,55 @@ def run_config4(args, ctx, barrier_sync, result):
     sh.close()
     del g, plan
     snap.set_timing(True)
-    comm = RcclComm.create(world, rank, local, broadcast=ctx.broadcast_bytes)
-    log(f"rank {rank}: config4 part {rank}/{world} on device + RCCL comm in {time.time() - t0:.1f}s {info}")
+    # RCCL between the ranks; HGX_BENCH_C4_TRANSPORT=host stages the exchange through the gloo group
+    # (hgx_comm_host_create), which lets a test run the N > 1 leg as two ranks on one GPU
+    if os.environ.get("HGX_BENCH_C4_TRANSPORT", "rccl") == "host":
+        from hypergraphdb_amd.partition import HostComm
+        comm = HostComm.gloo(ctx.dist, world, rank)
+    else:
+        comm = RcclComm.create(world, rank, local, broadcast=ctx.broadcast_bytes)
+    log(f"rank {rank}: config4 part {rank}/{world} on device + {type(comm).__name__} in {time.time() - t0:.1f}s {info}")
     for _ in range(max(args.warmup, 1)):
         r = pbfs_batch(snap, comm, seeds, args.depth)
         acct = r.stats(accounting=True)
         r.close()
     dt, st = timed(lambda: pbfs_batch(snap, comm, seeds, args.depth), args.steps)
-    edges = ctx.sum(acct["traversed_edges"]) * args.steps   # parts' shares sum to the whole batch's numerator
+    edges_part = ctx.sum(acct["traversed_edges"])
+    edges = edges_part * args.steps   # parts' shares sum to the whole batch's numerator
     xbytes = ctx.sum(sum(s["bytes_exchanged"] for s in st)) / args.steps
     xms = ctx.max(sum(s["ms_exchange"] for s in st) / args.steps)
+    # self-check, outside the timed region: the parts' per-source per-depth counts of the last timed
+    # step, summed over the ranks, must equal the replica's counts of the same sources (rank 0 ran
+    # them on the whole snapshot above), and so must the TEPS numerator
+    pc = last["counts"]
+    width = max(pc.shape[1], ref_counts.shape[1] if rank == 0 else 0)
+    width = int(ctx.max(width))
+    padded = np.zeros((len(seeds), width), np.int64)
+    padded[:, : pc.shape[1]] = pc
+    total = ctx.sum_array(padded)
+    if os.environ.get("HGX_BENCH_INJECT_MISMATCH") == "1":   # test hook: the check must catch this
+        total[0, 1] += 1
+    ok = 1.0
+    if rank == 0:
+        ref = np.zeros((len(seeds), width), np.int64)
+        ref[:, : ref_counts.shape[1]] = ref_counts
+        ok = float(np.array_equal(total, ref) and edges_part == ref_edges)
+    ok = ctx.sum(ok if rank == 0 else 0.0) == 1.0
+    log(f"rank {rank}: config4 partitioned parity against the replica: {'ok' if ok else 'MISMATCH'}")
     result["partitioned"] = {
         "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "strong",
         "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl, "n_gpus": world,
-        "parallelism": f"vertex cut over {world} GPUs (links placed by hgx_partition_plan), RCCL reduce + "
-                       "broadcast of new rows per level, the same sources on every part",
+        "parallelism": f"vertex cut over {world} GPUs (links placed by hgx_partition_plan), "
+                       f"{'RCCL' if isinstance(comm, RcclComm) else 'host-staged gloo'} reduce + broadcast of new "
+                       "rows per level, the same sources on every part",
         "exchange_bytes_per_step": xbytes, "exchange_kernels_ms_per_step": round(xms, 3),
+        "parity": ok,
+        "parity_check": ("the last timed step's per-source per-depth counts summed over the parts == the replica's "
+                         "counts of the same sources on the whole snapshot (rank 0), and the summed TEPS numerator == "
+                         "the replica's; checked after the timed steps"),
         "rank0_part": info, "roofline": _kernel_roof(st)}
+    if not ok:
+        result["error"] = "partitioned counts differ from the replica's"
     log(f"rank {rank}: config4 partitioned {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step, "
         f"exchange {xbytes / 1e9:.2f} GB/step")
     comm.close()
@@ -374,6 +413,7 @@ def run_config5(args, ctx, barrier_sync):
     barrier_sync()
     dt = ctx.max(time.perf_counter() - t1)
     sts = [x.as_dict() for x in sts]
+    drop = None if args.no_dropin else dropin_config5(args, ctx, barrier_sync, g, views, gens, pool)
     pool.shutdown()
     views[1].close()
     assert readout == closure * n5, "config-5 readout differs from the warm-up closures"
@@ -407,8 +447,141 @@ def run_config5(args, ctx, barrier_sync):
         out["cpu_baseline"] = cpu_leg(run, "TEPS", f"the {len(g['seeds'])} closures of each direction, every "
                                       f"traversal stopped after {args.cpu_budget / 2:g}s (C restatement of the "
                                       "subsumption BFS)")
+        # the drop-in's unit of work on the CPU: one order-exact traversal (the oracle's FIFO
+        # HGBreadthFirstTraversal, every pair materialised) at a time on one thread, the same seeds as the
+        # GPU's single-seed calls
+        n1 = len(drop["single"]["seeds"]) if drop else 0
+        for rev, name in ((False, "subsumed"), (True, "subsumes")) if drop else ():
+            lat = []
+            for sd in drop["single"]["seeds"]:
+                t1 = time.perf_counter()
+                orc.bfs(int(sd), -1, algen(T, False, True, rev, False))
+                lat.append(time.perf_counter() - t1)
+            lat.sort()
+            drop["single"][name]["cpu_ms_median"] = round(lat[n1 // 2] * 1e3, 4)
+            drop["single"][name]["cpu_ms_p90"] = round(lat[int(n1 * 0.9)] * 1e3, 4)
+        if drop:
+            drop["single"]["cpu"] = ("C restatement of HGBreadthFirstTraversal + DefaultALGenerator (oracle/), one "
+                                     "traversal per call on 1 thread, pairs materialised")
+            drop["cpu_baseline"] = {"same_as": "subsumption.cpu_baseline",
+                                    "note": "the batched sequence step traverses exactly the set step's closures "
+                                            "(same seeds, same FIFO traversal); the CPU restatement's rate is that "
+                                            "leg's"}
         del orc
+    if drop:
+        drop["single"]["seeds"] = len(drop["single"]["seeds"])
+    out["dropin"] = drop
     snap.close()
+    return out
+
+
+def dropin_config5(args, ctx, barrier_sync, g, views, gens, pool):
+    """What the Java drop-ins run for hg.subsumed(G) / hg.subsumes(S) (GpuTraversalToQuery ->
+    HGGpuTraversal -> hgx_bfs_sequence, C/query/cond2qry/ToQueryMap.java:282-312,340-370): the
+    order-exact FIFO sequence of every closure, pairs and distances into host arrays.  Batched: the
+    1024 closures of each direction per step (directions on two execution contexts, as the set step);
+    single: one traversal per call, the drop-in's shape (HGGpuTraversal.next() on one start atom)."""
+    import hypergraphdb_amd as H
+    rank = ctx.rank
+
+    def direction(k):
+        r = H.bfs_sequence(views[k], g["seeds"], None, gens[k])   # readout: the result arrays on the host
+        return r
+
+    def step():
+        f = pool.submit(direction, 1)
+        a = direction(0)
+        return [a, f.result()]
+
+    ref = step()
+    pairs = sum(int(r.offsets[-1]) for r in ref)
+    n5 = max(args.steps, 10)
+    barrier_sync()
+    t1 = time.perf_counter()
+    got = []
+    for _ in range(n5):
+        got = step()
+    barrier_sync()
+    dt = ctx.max(time.perf_counter() - t1)
+    for a, b in zip(got, ref):
+        if not (np.array_equal(a.offsets, b.offsets) and np.array_equal(a.atoms, b.atoms) and
+                np.array_equal(a.links, b.links)):
+            raise RuntimeError("dropin: a timed sequence step differs from the first")
+    # roofline of the workgroup-per-seed kernel, each direction alone (launch device time by HIP events)
+    roofs = {}
+    for k, name in ((0, "subsumed"), (1, "subsumes")):
+        ms, by = 0.0, 0.0
+        for _ in range(5):
+            r = direction(k)
+            ms += r.ms_block
+            by += r.bytes_block
+        ach = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        roofs[name] = {"bound": "hbm", "kernel": "hgx_seq_block", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(ms / 5, 4),
+                       "bytes_per_launch": by / 5, "seeds_workgroup_engine": r.n_block,
+                       "seeds_level_engine": r.n_level,
+                       "ms_per_call": round(r.ms_total, 4)}
+    # single-seed calls: the first 200 classes, one traversal per call, each direction
+    single = {"seeds": [int(x) for x in g["seeds"][:200]]}
+    for k, name in ((0, "subsumed"), (1, "subsumes")):
+        lat = []
+        for sd in single["seeds"]:
+            t1 = time.perf_counter()
+            H.bfs_sequence(views[k], [sd], None, gens[k])
+            lat.append(time.perf_counter() - t1)
+        lat.sort()
+        n1 = len(lat)
+        single[name] = {"ms_median": round(lat[n1 // 2] * 1e3, 4), "ms_p90": round(lat[int(n1 * 0.9)] * 1e3, 4),
+                        "ms_max": round(lat[-1] * 1e3, 4)}
+    out = {"metric": "order-exact closures/s (hgx_bfs_sequence: the HGTraversal drop-in)",
+           "value": ctx.sum(2 * len(g["seeds"]) * n5) / dt, "unit": "closures/s", "steps": n5,
+           "ms_per_step": round(dt / n5 * 1e3, 3), "pairs_per_step": pairs,
+           "traversed_items_per_step": sum(r.traversed_edges for r in ref),
+           "step": "hgx_bfs_sequence of the 1024 classes per direction, the directions on two execution contexts; "
+                   "every (link, atom, distance) pair in host arrays",
+           "roofline": roofs["subsumes"], "roofline_subsumed": roofs["subsumed"], "single": single}
+    log(f"rank {rank}: dropin config5 {out['value']:.1f} closures/s, {out['ms_per_step']} ms/step; single-seed "
+        f"subsumed {single['subsumed']['ms_median']} ms, subsumes {single['subsumes']['ms_median']} ms (median)")
+    return out
+
+
+def dropin_config2(args, ctx, snap, g):
+    """The order-exact sequence engine on config 2: 64 of the bench's sources to depth 2 in one
+    hgx_bfs_sequence call (each traversal returns ~4.5M pairs, so the workgroup engine hands them all
+    to the level-synchronous one), pairs into host arrays.  TEPS = traversed incidence items / time."""
+    import hypergraphdb_amd as H
+    seeds = np.asarray(g["seeds"][:64], np.int32)
+    r = H.bfs_sequence(snap, seeds, 2)
+    pairs, trav = int(r.offsets[-1]), r.traversed_edges
+    del r
+    steps = 2
+    t1 = time.perf_counter()
+    ms_dev = 0.0
+    for _ in range(steps):
+        r = H.bfs_sequence(snap, seeds, 2)
+        ms_dev += r.ms_total
+        if int(r.offsets[-1]) != pairs:
+            raise RuntimeError("dropin config2: a timed step differs from the first")
+        del r
+    dt = time.perf_counter() - t1
+    out = {"metric": "hyperedge TEPS of the order-exact sequence", "value": ctx.sum(trav * steps) / ctx.max(dt),
+           "unit": "TEPS", "seeds": len(seeds), "depth": 2, "steps": steps, "ms_per_step": round(dt / steps * 1e3, 2),
+           "device_ms_per_step": round(ms_dev / steps, 2), "pairs_per_step": pairs, "traversed_items_per_step": trav}
+    log(f"rank {ctx.rank}: dropin config2 {out['value']:.3e} TEPS, {out['ms_per_step']} ms/step, {pairs} pairs")
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ctypes import OracleGraph
+        orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+
+        def run(threads):
+            tm = {}
+            _, tr = orc.bfs_many(seeds[: max(threads, 4)], 2, 3, nthreads=threads, time_budget_s=args.cpu_budget,
+                                 timing=tm)
+            return int(tr.sum()), tm["elapsed_s"]
+
+        out["cpu_baseline"] = cpu_leg(run, "TEPS", f"the first max(threads, 4) of the 64 seeds to depth 2, each "
+                                      f"traversal stopped after {args.cpu_budget:g}s (C restatement)")
+        del orc
     return out
 
 
@@ -509,6 +682,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=2.0, help="seconds of CPU-baseline work per run")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (1B incidences) legs")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 subsumption leg")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the order-exact sequence (drop-in) legs")
     ap.add_argument("--c5-scale", type=float, default=1.0, help="fraction of the config-5 size")
     ap.add_argument("--c4-scale", type=float, default=1.0, help="fraction of the config-4 size")
     ap.add_argument("--c4-timeout", type=float, default=420.0,
@@ -600,6 +774,7 @@ def main():
                          "frac": round(ach_min / HBM_PEAK_GBS, 4)}
     log(f"rank {rank}: {args.steps} steps in {dt:.3f}s -> {teps:.3e} TEPS; device ms/step {ms_dev:.2f}; "
         f"dominant {roof['kernel']} {roof['achieved']} GB/s")
+    drop2 = None if args.no_dropin else dropin_config2(args, ctx, snap, g)
     snap.close()
     del snap
 
@@ -711,19 +886,24 @@ def main():
                         for k, v in per_kernel.items()},
             "pattern": pattern,
             "subsumption": sub,
+            "dropin": None if args.no_dropin else {
+                "what": "hgx_bfs_sequence, the order-exact FIFO next() sequence the Java drop-ins run "
+                        "(HGGpuTraversal; hg.subsumed / hg.subsumes through GpuTraversalToQuery)",
+                "config5": sub.pop("dropin") if sub else None, "config2": drop2},
         }
 
     # ---------------- config 4: 1B incidences, replicated vs hash-partitioned ----------------
+    rc = 0
     if not args.no_config4:
         import threading
         c4 = {}
 
-        def watchdog():   # a hung collective must not cost the whole line
+        def watchdog():   # a hung collective must not cost the whole line, but the run has failed
             log(f"rank {rank}: config4 legs exceeded {args.c4_timeout:.0f}s; reporting what finished")
             if line is not None:
                 line["config4"] = dict(c4, error=f"abandoned after {args.c4_timeout:.0f}s")
                 emit(line)
-            os._exit(0)
+            os._exit(3)
 
         wd = threading.Timer(args.c4_timeout, watchdog)
         wd.daemon = True
@@ -736,9 +916,13 @@ def main():
         wd.cancel()
         if line is not None:
             line["config4"] = c4
+        if "error" in c4:   # a failed or mismatching config-4 leg fails the run (after the line is out)
+            rc = 3
     if rank == 0:
         emit(line)
     ctx.close()
+    if rc:
+        sys.exit(rc)
 
 
 if __name__ == "__main__":

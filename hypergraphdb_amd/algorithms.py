@@ -161,6 +161,11 @@ class SequenceResult:
             ms, tr = C.c_double(), C.c_double()
             check(lib().hgx_seq_result_stats(handle, C.byref(ms), C.byref(tr)))
             self.ms_total, self.traversed_edges = ms.value, tr.value
+            nb, nl, mb, bb = C.c_int32(), C.c_int32(), C.c_double(), C.c_double()
+            check(lib().hgx_seq_result_engine_stats(handle, C.byref(nb), C.byref(nl), C.byref(mb), C.byref(bb)))
+            # seeds finished by the workgroup-per-seed engine / the level-synchronous reruns, and the
+            # workgroup launches' device ms and algorithmic bytes
+            self.n_block, self.n_level, self.ms_block, self.bytes_block = nb.value, nl.value, mb.value, bb.value
         finally:
             lib().hgx_seq_result_free(handle)
 

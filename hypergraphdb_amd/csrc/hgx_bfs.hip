@@ -3999,6 +3999,32 @@ FullMask full_mask(int S, int W) {
     return fm;
 }
 
+// The exchange's count vectors, gathered on the device (Transport::allgather_dev: RCCL all-gathers
+// them without a host copy in between).  Reduce / broadcast phase: [records to q (NP), words to q (NP),
+// my ghosts, nonzero words shipped]; end of level: [owned new atoms, push volume, nonzero words].
+__global__ void k_x_counts(int NP, const u64* __restrict__ dctr, int64_t ghosts, int64_t* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < NP) {
+        out[t] = (int64_t)dctr[(size_t)t * kCurStride];
+        out[NP + t] = (int64_t)dctr[(size_t)t * kCurStride + 16];
+    }
+    if (t == 0) {
+        const u64* xs = dctr + (size_t)NP * kCurStride;
+        u64 z = 0;
+        for (int k = 0; k < kStatShards; ++k) z += xs[k * kStatStride + 2];
+        out[2 * NP] = ghosts;
+        out[2 * NP + 1] = (int64_t)z;
+    }
+}
+__global__ void k_x_finish(const u64* __restrict__ xs, int64_t* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < 3) {
+        u64 v = 0;
+        for (int k = 0; k < kStatShards; ++k) v += xs[k * kStatStride + t];
+        out[t] = (int64_t)v;
+    }
+}
+
 // Per-batch buffers of the partitioned exchange (vertex cut).  Segment
 // capacities are static: part q receives from me at most my ghosts owned by q (reduce) and my
 // owned atoms held by q (broadcast); symmetrically for what I receive.  A segment of cap records
@@ -4019,10 +4045,13 @@ struct Exchange {
     double bytes_sent = 0, nz_words = 0, words = 0;
     int static_levels = 0;              // levels exchanged through the static slots
     u64* hpin = nullptr;                // pinned landing area of the cursor / stats read-backs
+    int64_t* dvec = nullptr;            // [2 * NP + 2] device count vector of the next all-gather
+    int64_t* gpin = nullptr;            // [(2 * NP + 2) * NP] pinned landing area of the gathered vectors
     Exchange(hgx_graph* gg, Transport* t, int w) : g(gg), tr(t), W(w) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts;
         HGX_HIP(hipHostMalloc(&hpin, sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride), hipHostMallocDefault));
+        HGX_HIP(hipHostMalloc(&gpin, sizeof(int64_t) * (2 * NP + 2) * NP, hipHostMallocDefault));
         rseg.assign(NP + 1, 0);
         bseg.assign(NP + 1, 0);
         for (int q = 0; q < NP; ++q) {
@@ -4036,6 +4065,7 @@ struct Exchange {
         send_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
         recv_p = (u64*)g->alloc(sizeof(u64) * W * (size_t)cap_recs);
         dctr = (u64*)g->alloc(sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride));
+        dvec = (int64_t*)g->alloc(sizeof(int64_t) * (2 * NP + 2));
         seg = (int64_t*)g->alloc(sizeof(int64_t) * 4 * NP);
         std::vector<int64_t> hs(4 * (size_t)NP);
         for (int q = 0; q < NP; ++q) {
@@ -4057,7 +4087,9 @@ struct Exchange {
     }
     ~Exchange() {
         if (hpin) (void)hipHostFree(hpin);
+        if (gpin) (void)hipHostFree(gpin);
         const int NP = g->shard->n_parts;
+        g->release(dvec, sizeof(int64_t) * (2 * NP + 2));
         g->release(send_h, sizeof(u64) * 2 * (size_t)cap_recs);
         g->release(recv_h, sizeof(u64) * 2 * (size_t)cap_recs);
         g->release(send_p, sizeof(u64) * W * (size_t)cap_recs);
@@ -4077,19 +4109,31 @@ struct Exchange {
     // me.  Returns the per-source record counts; source q's records land at recv_h + 2 * rbase[q],
     // its payload at recv_p + W * rbase[q].  *pair_max: the largest bytes I send one peer.
     // *group (optional): the group's records, words and ghosts (every part gets the same numbers).
-    void ship(const std::vector<int64_t>& sbase, const std::vector<int64_t>& rbase, const std::vector<u64>& cnt,
-              const std::vector<u64>& wcnt, std::vector<int64_t>& rcnt, double* pair_max, double* group = nullptr) {
+    // The count vectors of a record phase (k_x_counts after the phase's pack), gathered from every
+    // part: all[p * K ..] is part p's (K = 2 NP + 2); my records / words per destination go to cnt /
+    // wcnt.  RCCL gathers them on the device: one host round trip instead of a read-back plus a
+    // host all-gather.
+    void gather_counts(std::vector<int64_t>& all, std::vector<u64>& cnt, std::vector<u64>& wcnt) {
         ShardInfo& sh = *g->shard;
         const int NP = sh.n_parts, me = sh.part;
-        const int K = 2 * NP + 1;   // records and words to every part, then my ghost count
-        std::vector<int64_t> mine((size_t)K), all((size_t)NP * K);
+        const int K = 2 * NP + 2;
+        all.assign((size_t)NP * K, 0);
+        k_x_counts<<<1, 64, 0, g->stream>>>(NP, dctr, rseg[NP], dvec);
+        HGX_CHECK_LAUNCH();
+        coll([&] { trips += tr->allgather_dev(dvec, K, all.data(), g->stream, gpin); });
         for (int q = 0; q < NP; ++q) {
-            mine[q] = (int64_t)cnt[q];
-            mine[NP + q] = (int64_t)wcnt[q];
+            cnt[q] = (u64)all[(size_t)me * K + q];
+            wcnt[q] = (u64)all[(size_t)me * K + NP + q];
+            words += (double)cnt[q] * W;
         }
-        mine[2 * NP] = rseg[NP];
-        ++trips;
-        coll([&] { tr->allgather_i64(mine.data(), K, all.data(), g->stream); });
+        nz_words += (double)all[(size_t)me * K + 2 * NP + 1];
+    }
+    void ship(const std::vector<int64_t>& sbase, const std::vector<int64_t>& rbase, const std::vector<int64_t>& all,
+              std::vector<int64_t>& rcnt, double* pair_max, double* group = nullptr) {
+        ShardInfo& sh = *g->shard;
+        const int NP = sh.n_parts, me = sh.part;
+        const int K = 2 * NP + 2;   // records and words to every part, my ghost count, nonzero words
+        const int64_t* mine = all.data() + (size_t)me * K;
         if (group) {
             group[0] = group[1] = group[2] = 0;
             for (int p = 0; p < NP; ++p) {
@@ -4149,15 +4193,6 @@ struct Exchange {
             return t;
         };
         std::vector<int64_t> rcnt;
-        auto read_counts = [&]() {
-            read_back(hc, cbytes);
-            for (int q = 0; q < NP; ++q) {
-                cnt[q] = hc[(size_t)q * kCurStride];
-                wcnt[q] = hc[(size_t)q * kCurStride + 16];
-                words += (double)cnt[q] * Wt;
-            }
-            nz_words += (double)stat_sum(2);
-        };
         auto apply = [&](bool reduce, const std::vector<int64_t>& rbase) {
             for (int q = 0; q < NP; ++q) {
                 if (q == me || rcnt[q] == 0) continue;
@@ -4226,7 +4261,7 @@ struct Exchange {
                 A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
             HGX_CHECK_LAUNCH();
             tm.stop(e2);
-            return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
+            return finish_level(push_volume, level_bytes, pair_max, before, pm_r + pm_b);
         }
         // reduce: partial rows of my ghosts -> their owners
         Events e0 = tm.start(kKindExchange, d);
@@ -4235,7 +4270,8 @@ struct Exchange {
                                               seg, seg + NP, send_h, send_p, xs, NP);
         HGX_CHECK_LAUNCH();
         tm.stop(e0);
-        read_counts();
+        std::vector<int64_t> all;
+        gather_counts(all, cnt, wcnt);
         // a dense level (at least half of my ghosts with news, rows > 70% nonzero words) packs its
         // broadcast over the entries (hgx_xb_pack_flat); HGX_XB_FLAT=0 keeps the atom walk on every
         // level, 2 takes the entries on every level (A/B and tests)
@@ -4249,7 +4285,7 @@ struct Exchange {
         const bool flat = bseg[NP] > 0 && (flat_opt == 2 || (flat_opt == 1 && sent_r * 2 >= (u64)rseg[NP] &&
                                                              sent_w * 10 > sent_r * (u64)Wt * 7));
         double grp[3];
-        ship(rseg, bseg, cnt, wcnt, rcnt, &pm_r, grp);
+        ship(rseg, bseg, all, rcnt, &pm_r, grp);
         // static broadcast (group-wide choice from the all-gathered reduce counts, so every part
         // agrees): at least 85% of the group's ghosts had news and their rows were > 70% nonzero
         // words -- shipping a record for every entry then costs < 18% more bytes than the news alone
@@ -4267,7 +4303,7 @@ struct Exchange {
                 A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
             HGX_CHECK_LAUNCH();
             tm.stop(e1);
-            return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r);
+            return finish_level(push_volume, level_bytes, pair_max, before, pm_r);
         }
         // broadcast: final rows of my owned atoms -> their other holders
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
@@ -4289,9 +4325,7 @@ struct Exchange {
                 A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
             HGX_CHECK_LAUNCH();
             tm.stop(e2);
-            const u64 tot = finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
-            nz_words += (double)stat_sum(2);
-            return tot;
+            return finish_level(push_volume, level_bytes, pair_max, before, pm_r + pm_b, true);
         }
         if (flat) {
             const int64_t E = bseg[NP];
@@ -4304,33 +4338,33 @@ struct Exchange {
         }
         HGX_CHECK_LAUNCH();
         tm.stop(e1);
-        read_counts();
-        ship(bseg, rseg, cnt, wcnt, rcnt, &pm_b);
+        gather_counts(all, cnt, wcnt);
+        ship(bseg, rseg, all, rcnt, &pm_b);
         Events e2 = tm.start(kKindExchange, d);
         apply(false, rseg);
         hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
             A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
         HGX_CHECK_LAUNCH();
         tm.stop(e2);
-        return finish_level(hc, cbytes, stat_sum, push_volume, level_bytes, pair_max, before, pm_r + pm_b);
+        return finish_level(push_volume, level_bytes, pair_max, before, pm_r + pm_b);
     }
     // the level's statistics back to the host, the group's new-atom total
-    template <class SS>
-    u64 finish_level(std::vector<u64>& hc, size_t cbytes, SS& stat_sum, u64* push_volume, double* level_bytes,
-                     double* pair_max, double before, double pm) {
-        const int NP = g->shard->n_parts;
+    // (gathered on the device like the record counts; add_nz: count the nonzero words the level's
+    // static broadcast shipped)
+    u64 finish_level(u64* push_volume, double* level_bytes, double* pair_max, double before, double pm,
+                     bool add_nz = false) {
+        const int NP = g->shard->n_parts, me = g->shard->part;
         hipStream_t s = g->stream;
-        read_back(hc, cbytes);
-        const u64 fs[2] = {stat_sum(0), stat_sum(1)};
-        *push_volume = fs[1];
+        k_x_finish<<<1, 64, 0, s>>>(dctr + (size_t)NP * kCurStride, dvec);
+        HGX_CHECK_LAUNCH();
+        std::vector<int64_t> all(3 * (size_t)NP);
+        coll([&] { trips += tr->allgather_dev(dvec, 3, all.data(), s, gpin); });
+        *push_volume = (u64)all[(size_t)me * 3 + 1];
+        if (add_nz) nz_words += (double)all[(size_t)me * 3 + 2];
         *level_bytes = bytes_sent - before;
         *pair_max = pm;
-        int64_t nl = (int64_t)fs[0];
-        std::vector<int64_t> nall(NP);
-        ++trips;
-        coll([&] { tr->allgather_i64(&nl, 1, nall.data(), s); });
         u64 tot = 0;
-        for (int q = 0; q < NP; ++q) tot += (u64)nall[q];
+        for (int q = 0; q < NP; ++q) tot += (u64)all[(size_t)q * 3];
         return tot;
     }
     // A record phase whose sizes both sides know (static broadcast): scnt[q] records (headers and W
@@ -4690,7 +4724,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             g->zacc_clean = false;   // until this level's finalise has run
             u64* acc = (u64*)g->zacc;
             if (MODE != kSym && !g->inc_yf) {   // once per snapshot
-                HGX_HIP(hipMalloc(&g->inc_yf, std::max<int64_t>(g->I, 1)));
+                HGX_HIP(hipMalloc(&g->inc_yf, (size_t)g->I + 64));
                 hgx_inc_yield<<<grid_for(A * 64, 256, 8192), 256, 0, s>>>(A, g->inc_off, g->inc_row, g->tgt_off,
                                                                        g->tgt_idx, g->inc_yf);
                 HGX_CHECK_LAUNCH();
@@ -5580,13 +5614,17 @@ void hgx::bfs_shared_tables(hgx_graph* g) {
         hgx_hasinc<<<grid_for(ceil_div(A, 64) * 64, 256, 4096), 256, 0, s>>>(A, g->inc_off, (u64*)g->hasinc);
         HGX_CHECK_LAUNCH();
     }
-    if (!g->inc_yf) {
-        HGX_HIP(hipMalloc(&g->inc_yf, std::max<int64_t>(g->I, 1)));
-        hgx_inc_yield<<<grid_for(A * 64, 256, 8192), 256, 0, s>>>(A, g->inc_off, g->inc_row, g->tgt_off, g->tgt_idx,
-                                                               g->inc_yf);
-        HGX_CHECK_LAUNCH();
-    }
+    if (!g->inc_yf) ensure_inc_yield(g);
     if (g->n_pchunks < 0) build_push_chunks(g);
     if (g->push_inline && !g->inc_tgt_tried) build_inc_targets(g);
     HGX_HIP(hipStreamSynchronize(s));
+}
+
+void hgx::ensure_inc_yield(hgx_graph* g) {
+    if (g->inc_yf) return;
+    HGX_HIP(hipMalloc(&g->inc_yf, (size_t)g->I + 64));   // + padding: 16-byte loads of the last entries
+    HGX_HIP(hipMemsetAsync(g->inc_yf + g->I, 0, 64, g->stream));
+    hgx_inc_yield<<<grid_for(g->A * 64, 256, 8192), 256, 0, g->stream>>>(g->A, g->inc_off, g->inc_row, g->tgt_off,
+                                                                         g->tgt_idx, g->inc_yf);
+    HGX_CHECK_LAUNCH();
 }

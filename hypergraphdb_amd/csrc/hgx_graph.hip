@@ -44,6 +44,8 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->fcode) (void)hipFree(g->fcode);
     if (g->lcode) (void)hipFree(g->lcode);
+    for (auto& b : g->seq_hbufs) (void)hipHostFree(b.p);
+    g->seq_hbufs.clear();
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
     if (g->mapped) (void)hipHostFree(g->mapped);
@@ -308,6 +310,7 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     c->max_arity = g->max_arity; c->max_deg = g->max_deg;
     // the snapshot's options at this point (set separately on the context afterwards)
     c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
+    c->seq_engine = g->seq_engine;
     c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline; c->coded = g->coded;
     c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused; c->push_inline = g->push_inline;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
@@ -520,6 +523,9 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;
+    } else if (option == HGX_OPT_SEQ_ENGINE) {
+        if (value < 0 || value > 1) fail(HGX_E_INVALID, "hgx_set_option: sequence engine outside 0..1");
+        g->seq_engine = (int32_t)value;
     } else if (option == HGX_OPT_PUSH_INLINE) {
         g->push_inline = value != 0;
     } else if (option == HGX_OPT_QUERY_COALESCE) {

@@ -142,6 +142,11 @@ struct Transport {
     virtual ~Transport() {}
     // out[r * n + i] = in[i] of rank r (host buffers)
     virtual void allgather_i64(const int64_t* in, int64_t n, int64_t* out, hipStream_t s) = 0;
+    // The same for a DEVICE input written by work ordered on s: out (host) = every rank's n values;
+    // pin = pinned host scratch of n * world int64.  Returns the host round trips it took.  The
+    // default reads the values back and runs the host all-gather (two); RCCL gathers on the device
+    // and reads the gathered block back once (hgx_part.hip).
+    virtual int allgather_dev(const int64_t* din, int64_t n, int64_t* out, hipStream_t s, int64_t* pin);
     // rank p receives send_bytes[p] bytes from send + send_off[p]; this rank receives recv_bytes[p]
     // bytes from rank p at recv + recv_off[p] (device buffers, ordered on stream s)
     virtual void alltoallv(const void* send, const int64_t* send_off, const int64_t* send_bytes, void* recv,
@@ -201,8 +206,11 @@ struct hgx_graph {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;   // timing events reused across calls (taken under mu)
     int32_t bfs_flags = 0x3BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
-    int64_t seq_budget_bytes = (int64_t)16 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
+    int64_t seq_budget_bytes = (int64_t)48 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
+    int32_t seq_engine = 0;                         // HGX_OPT_SEQ_ENGINE: 0 workgroup per seed (+ fallback), 1 level-synchronous
+    std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
+    std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
     // order-exact traversal refuses to run until the caller re-asserts it.
@@ -294,6 +302,9 @@ hgx_graph* graph_create(const hgx_graph_desc* d, int32_t device, bool links_are_
 void pbfs_run(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
               const hgx_algen_opts* opts, hgx_bfs_result** out);
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+// Builds the ordered-mode yield flags (hgx_inc_yield, one byte per incidence entry + 64 bytes of
+// padding for 16-byte vector loads) on g if absent; caller holds g->mu (hgx_bfs.hip).
+void ensure_inc_yield(hgx_graph* g);
 // Waits for the work enqueued on s by polling: hipStreamSynchronize sleeps and wakes tens of
 // microseconds after the last kernel, a cost per call of the short pattern batches.
 inline void spin_sync(hipStream_t s) {

@@ -402,6 +402,17 @@ hgx_shard* shard_build(const hgx_graph_desc* d, int32_t NP, int32_t part, const 
         if (r_ != ncclSuccess) ::hgx::fail(HGX_E_DEVICE, std::string(#x) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
+}  // namespace
+
+int hgx::Transport::allgather_dev(const int64_t* din, int64_t n, int64_t* out, hipStream_t s, int64_t* pin) {
+    HGX_HIP(hipMemcpyAsync(pin, din, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+    spin_sync(s);
+    allgather_i64(pin, n, out, s);
+    return 2;
+}
+
+namespace {
+
 struct RcclTransport : Transport {
     ncclComm_t comm = nullptr;
     int device = 0;
@@ -423,7 +434,22 @@ struct RcclTransport : Transport {
         HGX_HIP(hipMemcpyAsync(scratch + (int64_t)rank * n, in, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
         HGX_NCCL(ncclAllGather(scratch + (int64_t)rank * n, scratch, (size_t)n, ncclInt64, comm, s));
         HGX_HIP(hipMemcpyAsync(out, scratch, sizeof(int64_t) * need, hipMemcpyDeviceToHost, s));
-        HGX_HIP(hipStreamSynchronize(s));
+        spin_sync(s);
+    }
+    // the counts never leave the device before the gather: one collective, one read-back
+    int allgather_dev(const int64_t* din, int64_t n, int64_t* out, hipStream_t s, int64_t* pin) override {
+        const int64_t need = n * world;
+        if (need > scratch_n) {
+            if (scratch) HGX_HIP(hipFree(scratch));
+            scratch = nullptr;
+            HGX_HIP(hipMalloc(&scratch, sizeof(int64_t) * need));
+            scratch_n = need;
+        }
+        HGX_NCCL(ncclAllGather(din, scratch, (size_t)n, ncclInt64, comm, s));
+        HGX_HIP(hipMemcpyAsync(pin, scratch, sizeof(int64_t) * need, hipMemcpyDeviceToHost, s));
+        spin_sync(s);
+        std::memcpy(out, pin, sizeof(int64_t) * need);
+        return 1;
     }
     void alltoallv(const void* send, const int64_t* send_off, const int64_t* send_bytes, void* recv,
                    const int64_t* recv_off, const int64_t* recv_bytes, hipStream_t s) override {

@@ -9,17 +9,22 @@
 //     (FIFO rank e of the expanded atom, index j of the link in inc(parent), yield rank k in the link)
 // (DefaultALGenerator.getNextLink walks inc(src) ascending, :287-315; FTargetSetIterator yields
 // positions ascending, BTargetSetIterator descending, :121-285).  The triple is packed into one
-// 64-bit key and every candidate does an atomicMin on key[seed][t]; the winning key names the
-// discovering link, and sorting the level's discoveries by key gives the next FIFO segment.
+// integer key and every candidate lowers the key of its target with an atomicMin; the winning key
+// names the discovering link, and ordering the level's discoveries by key gives the next FIFO segment.
 //
-// e counts frontier entries across all levels of the batch (seed-major inside a level), so a key
-// from an earlier level is always smaller than any key of the current one: key[] doubles as the
-// 'examined' map, and a plain load filters the candidates that are already visited before any
-// atomic is issued.
+// Two engines share that rule:
+//   * workgroup per seed (default, hgx_seq_block): the whole traversal of one start atom inside one
+//     workgroup, examined set / frontier / ranks in LDS, no host round trip per level -- the shape of
+//     the drop-in's calls (one HGGpuTraversal or one hg.subsumed closure at a time);
+//   * level-synchronous (fallback for traversals larger than a workgroup holds, HGX_OPT_SEQ_ENGINE 1):
+//     flat incidence items (entry, j) of the frontier -> hgx_seq_expand (one item per lane,
+//     block-local entry search, atomicMin on key[seed][atom]) -> gather final keys -> rocPRIM radix
+//     sort by key -> hgx_seq_decode (next frontier + (link, atom) pairs).
 //
-// Data-parallel structure per level:  flat incidence items (entry, j) of the frontier
-// -> hgx_seq_expand (one item per lane, block-local entry search) -> gather final keys ->
-// rocPRIM radix sort by key -> hgx_seq_decode (next frontier + (link, atom) pairs).
+// Level-synchronous keys: e counts frontier entries across all levels of the batch (seed-major
+// inside a level), so a key from an earlier level is always smaller than any key of the current one:
+// key[] doubles as the 'examined' map, and a plain load filters the candidates that are already
+// visited before any atomic is issued.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -194,7 +199,9 @@ __global__ void __launch_bounds__(256) k_seq_gather_keys(int64_t n, const int64_
         out[i] = key[list[i]];
 }
 
-// Sorted discoveries -> next frontier (seed-major FIFO) and the returned (link, atom) pairs.
+// Sorted discoveries -> next frontier (seed-major FIFO) and the returned (link, atom) pairs, the
+// pairs written straight into mapped host memory (out_link / out_atom), plus each chunk seed's range
+// of the level: [first[s], last[s]) (the level is seed-major: the key's entry rank e is).
 __global__ void __launch_bounds__(256) hgx_seq_decode(int64_t n, const u64* __restrict__ skey,
                                                       const int64_t* __restrict__ sflat, u64 e_base, int32_t sh_e,
                                                       int32_t sh_j, u64 jmask, int64_t A,
@@ -204,15 +211,20 @@ __global__ void __launch_bounds__(256) hgx_seq_decode(int64_t n, const u64* __re
                                                       const int32_t* __restrict__ inc_row,
                                                       const int32_t* __restrict__ link_atom,
                                                       int32_t* __restrict__ nx_atom, int32_t* __restrict__ nx_seed,
-                                                      int32_t* __restrict__ out_link) {
+                                                      int32_t* __restrict__ out_link, int32_t* __restrict__ out_atom,
+                                                      int64_t* __restrict__ first, int64_t* __restrict__ last) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const u64 k = skey[i];
         const int64_t fi = (int64_t)((k >> sh_e) - e_base);
         const int64_t j = (int64_t)((k >> sh_j) & jmask);
         const int32_t p = fr_atom[fi], s = fr_seed[fi];
+        const int32_t t = (int32_t)(sflat[i] - (int64_t)s * A);
         out_link[i] = link_atom[inc_row[inc_off[p] + j]];
-        nx_atom[i] = (int32_t)(sflat[i] - (int64_t)s * A);
+        out_atom[i] = t;
+        nx_atom[i] = t;
         nx_seed[i] = s;
+        if (i == 0 || (int32_t)(sflat[i - 1] / A) != s) first[s] = i;
+        if (i == n - 1 || (int32_t)(sflat[i + 1] / A) != s) last[s] = i + 1;
     }
 }
 
@@ -223,6 +235,460 @@ __global__ void k_seq_seed_keys(int32_t B, const int32_t* __restrict__ seeds, in
         key[(int64_t)i * A + seeds[i]] = 0ull;   // examined.put(start, TRUE) (:42-46)
         fr_atom[i] = seeds[i];
         fr_seed[i] = i;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Workgroup-per-seed engine (HGX_OPT_SEQ_ENGINE 0, the default).
+//
+// The drop-in (HGGpuTraversal.next(), hg.subsumed / hg.subsumes through TraversalBasedQuery) asks for
+// one traversal at a time, and the closures it asks for are small: config 5's hg.subsumes closures
+// hold <= 1265 atoms over ~15 levels, hg.subsumed ones a median of 1.  The level-synchronous engine
+// below pays ~8 launches and 2 host round trips per level for those.  Here one workgroup runs one
+// seed's whole traversal with its state in LDS:
+//   - an open-addressing hash (kSbHash slots) of the examined atoms: atom id + a 64-bit value
+//     ((key + 1) << 32 | discovering link atom id) lowered with atomicMin by every yield of the
+//     level; 0 marks an atom examined at an earlier level, so the min never displaces it;
+//   - the frontier table: atom, incidence start, degree prefix and 16-byte segment prefix;
+//   - a staging area of candidate incidence items (their flat item index), re-used as the rank
+//     bitmap or the sort buffer at the end of a level.
+// Stream order is the reference's: key = (flat item index it, yield rank k), it = (FIFO entry,
+// index of the link in inc(entry)) flattened in order, k = position rank in the link (descending in
+// reverse mode) -- the same lexicographic triple as the level-synchronous engine's
+// (DefaultALGenerator.getNextLink :287-315; F/BTargetSetIterator :121-285).
+// A level: (1) the frontier's incidence is streamed 16 entries per lane (one 16-byte load of the
+// ordered-mode yield flags, hgx_inc_yield; the symmetric mode stages every entry) and the entries
+// that can yield are staged; (2) each staged entry reads its link's type, targets and atom id, and
+// every yielded target not examined yet takes part in the atomicMin; (3) the new atoms are ranked by
+// their keys (a bitmap over the level's key space + a popcount prefix, or a bitonic sort when the key
+// space is wider than the staging area); rank r is the r-th pair of the level and the r-th entry of
+// the next frontier.  Pairs go straight into mapped host memory.  A seed whose traversal needs more
+// than kSbPairs pairs (or a level wider than a 32-bit key) reports -1 and reruns on the
+// level-synchronous engine.
+constexpr int kSbThreads = 512;
+constexpr int kSbWaves = kSbThreads / 64;
+constexpr int kSbHash = 4096;                       // hash slots (power of two)
+constexpr int kSbDisc = kSbHash / 2 - 1;            // examined atoms incl. the seed (load <= 1/2)
+constexpr int kSbPairs = kSbDisc - 1;               // pairs one seed may return
+constexpr int kSbFront = 2048;                      // frontier entries (>= kSbPairs)
+constexpr int kSbCand = 16384;                      // staged candidate items
+constexpr int kSbRound = kSbThreads * 16;           // items one staging step may add
+constexpr int kSbU = 4;                             // 16-byte segments a lane loads at once
+constexpr int kSbInline = 32;                       // seeds passed in the kernel arguments
+constexpr int kSbChunk = 1024;                      // seeds per launch (mapped output per launch)
+
+struct SbArgs {
+    int32_t n;                                      // seeds of this launch
+    const int32_t* seeds;                           // device seeds (n > kSbInline)
+    int32_t seed_inline[kSbInline];
+    const int64_t* inc_off;
+    const int32_t* inc_row;
+    const int32_t* inc_type;
+    const uint8_t* yf;                              // ordered-mode yield flags; null in the symmetric mode
+    const int64_t* tgt_off;
+    const int32_t* tgt_idx;
+    const int32_t* link_atom;
+    int32_t want_type, min_arity, mode, rev, kbits, maxd;
+    int64_t t_limit;                                // largest item count of a level with 32-bit keys
+    int32_t* out_link;                              // [n * kSbPairs] (mapped host memory)
+    int32_t* out_atom;
+    int32_t* out_dist;
+    int64_t* meta;                                  // [3 n]: pairs (-1 = fall back), traversed items, bytes
+};
+
+struct SbShared {
+    int32_t h_atom[kSbHash];
+    u64 h_val[kSbHash];
+    int64_t e_fb[kSbFront];                         // frontier entry: first incidence position
+    int32_t e_atom[kSbFront];
+    int32_t e_dp[kSbFront + 1];                     // degree prefix (flat item index of the entry's first item)
+    int32_t e_sp[kSbFront + 1];                     // 16-byte segment prefix
+    union {
+        int32_t cand[kSbCand];                      // staged items
+        u64 bm[kSbCand / 2];                        // rank bitmap over the level's key space
+        struct {
+            u64 key[kSbFront];
+            int32_t pay[kSbFront];
+        } srt;                                      // bitonic sort buffer
+    } u;
+    int64_t wsum[kSbWaves];
+    int32_t cp[kSbThreads];                         // rank bitmap: popcount prefix of each thread's words
+    int64_t T, S;
+    int32_t cand_n, n_disc, ovf;
+};
+
+// exclusive block scan (every thread calls it); *total = the block sum
+__device__ __forceinline__ int64_t sb_scan(SbShared& sm, int64_t v, int64_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) sm.wsum[w] = x;
+    __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSbWaves; ++k) {
+        const int64_t t = sm.wsum[k];
+        base += k < w ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// last index i in [0, n) with pre[i] <= x (pre non-decreasing, pre[0] <= x)
+__device__ __forceinline__ int sb_search(const int32_t* pre, int n, int64_t x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t sb_hash(int32_t t) { return ((uint32_t)t * 0x9E3779B1u) >> 20; }
+
+// Examined-set insert: the first arrival claims a slot (one reservation each, so the table never
+// fills), then the value is lowered to val unless the atom was examined at an earlier level.
+__device__ __forceinline__ void sb_insert(SbShared& sm, int32_t t, u64 val) {
+    uint32_t h = sb_hash(t);
+    for (;;) {
+        int32_t a = sm.h_atom[h];
+        if (a == t) break;
+        if (a == -1) {
+            if (atomicAdd(&sm.n_disc, 1) >= kSbDisc) {
+                sm.ovf = 1;
+                return;
+            }
+            a = atomicCAS(&sm.h_atom[h], -1, t);
+            if (a == -1 || a == t) break;
+        }
+        h = (h + 1) & (kSbHash - 1);
+    }
+    if (sm.h_val[h] > val) atomicMin(&sm.h_val[h], val);
+}
+
+// Frontier table of e_atom[0, F): incidence start, degree and segment prefixes, sm.T / sm.S.
+__device__ void sb_frontier(SbShared& sm, const SbArgs& a, int F) {
+    const int tid = threadIdx.x;
+    int64_t dg[4], sg[4], ds = 0, ss = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid * 4 + k;
+        dg[k] = sg[k] = 0;
+        if (i < F) {
+            const int32_t p = sm.e_atom[i];
+            const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
+            sm.e_fb[i] = b;
+            dg[k] = e - b;
+            sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+        }
+        ds += dg[k];
+        ss += sg[k];
+    }
+    int64_t T, S;
+    int64_t dp = sb_scan(sm, ds, &T);
+    int64_t sp = sb_scan(sm, ss, &S);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid * 4 + k;
+        if (i < F) {
+            sm.e_dp[i] = (int32_t)dp;   // exact whenever T <= t_limit (checked by the level)
+            sm.e_sp[i] = (int32_t)sp;
+        }
+        dp += dg[k];
+        sp += sg[k];
+    }
+    if (tid == 0) {
+        sm.e_dp[F] = (int32_t)(T < INT32_MAX ? T : INT32_MAX);
+        sm.e_sp[F] = (int32_t)(S < INT32_MAX ? S : INT32_MAX);
+        sm.T = T;
+        sm.S = S;
+    }
+    __syncthreads();
+}
+
+// Staged items -> yields -> examined-set inserts.
+// nbytes: the thread's algorithmic bytes (the type, row, target-offset, link-id and target loads).
+__device__ void sb_process(SbShared& sm, const SbArgs& a, int F, int cn, int64_t& nbytes) {
+    for (int c = threadIdx.x; c < cn; c += kSbThreads) {
+        const int32_t it = sm.u.cand[c];
+        const int i = sb_search(sm.e_dp, F, it);
+        const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
+        const int32_t p = sm.e_atom[i];
+        const int32_t L = a.inc_row[ii];
+        const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
+        nbytes += a.want_type >= 0 ? 8 : 4;
+        if (a.want_type >= 0 && ty != a.want_type) continue;                     // linkPredicate (:300)
+        const int64_t b = a.tgt_off[L];
+        const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
+        const int32_t la = a.link_atom[L];
+        nbytes += 20 + 4 * (int64_t)n;
+        if (n < a.min_arity) continue;                                           // minArity (:309)
+        const u64 kb = ((u64)(uint32_t)it << a.kbits) + 1ull;
+        const u64 lw = (u64)(uint32_t)la;
+        if (n <= 8) {
+            int32_t tg[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[b + q] : -1;
+            int32_t lo = 0, hi = n;
+            if (a.mode != sSym) {
+                int32_t fv = -1, lv = -1;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (tg[q] == p) {
+                        if (fv < 0) fv = q;
+                        lv = q;
+                    }
+                if (a.mode == sAfterFirst) lo = fv + 1;
+                else if (a.mode == sBeforeFirst) hi = fv;
+                else if (a.mode == sBeforeLast) hi = lv;
+                else lo = lv + 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q >= lo && q < hi && tg[q] != p)
+                    sb_insert(sm, tg[q], ((kb + (u64)(a.rev ? n - 1 - q : q)) << 32) | lw);
+        } else {
+            int32_t lo = 0, hi = n;
+            if (a.mode != sSym) {
+                int32_t fv = -1, lv = -1;
+                for (int32_t q = 0; q < n; ++q)
+                    if (a.tgt_idx[b + q] == p) {
+                        if (fv < 0) fv = q;
+                        lv = q;
+                    }
+                if (a.mode == sAfterFirst) lo = fv + 1;
+                else if (a.mode == sBeforeFirst) hi = fv;
+                else if (a.mode == sBeforeLast) hi = lv;
+                else lo = lv + 1;
+            }
+            for (int32_t q = lo; q < hi; ++q) {
+                const int32_t t = a.tgt_idx[b + q];
+                if (t != p) sb_insert(sm, t, ((kb + (u64)(a.rev ? n - 1 - q : q)) << 32) | lw);
+            }
+        }
+    }
+}
+
+__device__ void sb_bitonic(SbShared& sm, int N2) {
+    for (int k = 2; k <= N2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < N2 / 2; i += kSbThreads) {
+                const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo | j;
+                const bool up = (lo & k) == 0;
+                const u64 x = sm.u.srt.key[lo], y = sm.u.srt.key[hi];
+                if ((x > y) == up) {
+                    sm.u.srt.key[lo] = y;
+                    sm.u.srt.key[hi] = x;
+                    const int32_t t = sm.u.srt.pay[lo];
+                    sm.u.srt.pay[lo] = sm.u.srt.pay[hi];
+                    sm.u.srt.pay[hi] = t;
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// New atom in hash slot sl has rank r of its level: pair r of the level, entry r of the next frontier.
+__device__ __forceinline__ void sb_emit(SbShared& sm, const SbArgs& a, int64_t o, int r, int sl, int32_t dist) {
+    const int32_t t = sm.h_atom[sl];
+    const u64 v = sm.h_val[sl];
+    a.out_link[o + r] = (int32_t)(uint32_t)v;
+    a.out_atom[o + r] = t;
+    a.out_dist[o + r] = dist;
+    sm.e_atom[r] = t;
+    sm.h_val[sl] = 0ull;   // examined from now on
+}
+
+__device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int32_t seed = a.n <= kSbInline ? a.seed_inline[si] : a.seeds[si];
+    for (int i = tid; i < kSbHash; i += kSbThreads) {
+        sm.h_atom[i] = -1;
+        sm.h_val[i] = ~0ull;
+    }
+    if (tid == 0) {
+        sm.cand_n = 0;
+        sm.n_disc = 1;
+        sm.ovf = 0;
+        sm.e_atom[0] = seed;
+    }
+    __syncthreads();
+    if (tid == 0) {   // examined.put(start, TRUE) (HGBreadthFirstTraversal.java:42-46)
+        const uint32_t h = sb_hash(seed);
+        sm.h_atom[h] = seed;
+        sm.h_val[h] = 0ull;
+    }
+    sb_frontier(sm, a, 1);
+    const int64_t obase = (int64_t)si * kSbPairs;
+    int F = 1;
+    int64_t trav = 0, out_n = 0, nbytes = 0;
+    bool ovf = false;
+    for (int32_t d = 0; d < a.maxd && F > 0; ++d) {
+        const int64_t T = sm.T, S = sm.S;
+        trav += T;
+        nbytes += tid == 0 ? 16 * (int64_t)F + (a.yf ? T : 0) : 0;   // frontier offsets, streamed yield flags
+        if (T == 0) break;
+        if (T > a.t_limit) {
+            ovf = true;
+            break;
+        }
+        // (1) stream the frontier's incidence, stage the entries that can yield: kSbU segments per lane
+        // loaded at once, staged one segment at a time (a stage flushes through (2) when full)
+        bool stop = false;
+        for (int64_t sb = 0; sb < S && !stop; sb += (int64_t)kSbThreads * kSbU) {
+            uint4 v[kSbU];
+            int64_t lo_[kSbU], hi_[kSbU], ad_[kSbU], it_[kSbU];
+#pragma unroll
+            for (int u = 0; u < kSbU; ++u) {
+                const int64_t s = sb + (int64_t)u * kSbThreads + tid;
+                v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                lo_[u] = hi_[u] = ad_[u] = it_[u] = 0;
+                if (s < S) {
+                    const int i = sb_search(sm.e_sp, F, s);
+                    lo_[u] = sm.e_fb[i];
+                    hi_[u] = lo_[u] + (sm.e_dp[i + 1] - sm.e_dp[i]);
+                    ad_[u] = ((lo_[u] >> 4) + (s - sm.e_sp[i])) << 4;
+                    it_[u] = sm.e_dp[i] + (ad_[u] - lo_[u]);
+                    if (a.yf) v[u] = *(const uint4*)(a.yf + ad_[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kSbU; ++u) {
+                const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t mask = 0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t pos = ad_[u] + q;
+                    const bool y = a.yf ? ((wv[q >> 2] >> (8 * (q & 3) + a.mode)) & 1u) != 0 : true;
+                    if (pos >= lo_[u] && pos < hi_[u] && y) mask |= 1u << q;
+                }
+                const int cnt = __popc(mask);
+                int x = cnt;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+                const int wtot = __shfl(x, 63);
+                int base = 0;
+                if (lane == 63 && wtot) base = atomicAdd(&sm.cand_n, wtot);
+                base = __shfl(base, 63);
+                int o = base + x - cnt;
+                while (mask) {
+                    const int q = __ffs(mask) - 1;
+                    mask &= mask - 1;
+                    sm.u.cand[o++] = (int32_t)(it_[u] + q);
+                }
+                __syncthreads();
+                const int cn = sm.cand_n;
+                const bool last = sb + (int64_t)(u + 1) * kSbThreads >= S;
+                if (cn > 0 && (cn > kSbCand - kSbRound || last)) {
+                    // (2) the staged entries' links and yields
+                    sb_process(sm, a, F, cn, nbytes);
+                    __syncthreads();
+                    if (tid == 0) sm.cand_n = 0;
+                    __syncthreads();
+                    if (sm.ovf) stop = true;
+                }
+                if (last || stop) break;
+            }
+        }
+        if (sm.ovf) {
+            ovf = true;
+            break;
+        }
+        // (3) rank the level's new atoms by key
+        uint32_t nm = 0;
+#pragma unroll
+        for (int k = 0; k < kSbHash / kSbThreads; ++k) {
+            const int sl = tid * (kSbHash / kSbThreads) + k;
+            if (sm.h_atom[sl] != -1 && sm.h_val[sl] != 0ull) nm |= 1u << k;
+        }
+        int64_t n_new;
+        const int64_t off = sb_scan(sm, __popc(nm), &n_new);
+        if (n_new == 0) break;
+        const int32_t dist = d + 1;
+        const uint64_t nbits = (uint64_t)T << a.kbits;
+        if (nbits <= (uint64_t)kSbCand * 32) {   // bitmap over the key space + popcount prefix
+            const int W = (int)((nbits + 63) >> 6);
+            for (int w = tid; w < W; w += kSbThreads) sm.u.bm[w] = 0ull;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kSbHash / kSbThreads; ++k)
+                if ((nm >> k) & 1u) {
+                    const u64 key = (sm.h_val[tid * (kSbHash / kSbThreads) + k] >> 32) - 1ull;
+                    atomicOr(&sm.u.bm[key >> 6], 1ull << (key & 63));
+                }
+            __syncthreads();
+            const int cw = (W + kSbThreads - 1) / kSbThreads;
+            const int w0 = min(W, tid * cw), w1 = min(W, w0 + cw);
+            int c = 0;
+            for (int w = w0; w < w1; ++w) c += __popcll(sm.u.bm[w]);
+            int64_t tot;
+            const int64_t pre = sb_scan(sm, c, &tot);
+            sm.cp[tid] = (int32_t)pre;
+            __syncthreads();
+            int rk[kSbHash / kSbThreads];
+#pragma unroll
+            for (int k = 0; k < kSbHash / kSbThreads; ++k) {
+                rk[k] = 0;
+                if ((nm >> k) & 1u) {
+                    const u64 key = (sm.h_val[tid * (kSbHash / kSbThreads) + k] >> 32) - 1ull;
+                    const int w = (int)(key >> 6), ch = w / cw;
+                    int r = sm.cp[ch];
+                    for (int x2 = ch * cw; x2 < w; ++x2) r += __popcll(sm.u.bm[x2]);
+                    rk[k] = r + __popcll(sm.u.bm[w] & ((1ull << (key & 63)) - 1ull));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kSbHash / kSbThreads; ++k)
+                if ((nm >> k) & 1u) sb_emit(sm, a, obase + out_n, rk[k], tid * (kSbHash / kSbThreads) + k, dist);
+        } else {   // bitonic sort of the (value, slot) pairs
+            int N2 = 1;
+            while (N2 < n_new) N2 <<= 1;
+            int o = (int)off;
+#pragma unroll
+            for (int k = 0; k < kSbHash / kSbThreads; ++k)
+                if ((nm >> k) & 1u) {
+                    const int sl = tid * (kSbHash / kSbThreads) + k;
+                    sm.u.srt.key[o] = sm.h_val[sl];
+                    sm.u.srt.pay[o++] = sl;
+                }
+            for (int r = (int)n_new + tid; r < N2; r += kSbThreads) {
+                sm.u.srt.key[r] = ~0ull;
+                sm.u.srt.pay[r] = -1;
+            }
+            __syncthreads();
+            sb_bitonic(sm, N2);
+            for (int r = tid; r < n_new; r += kSbThreads) sb_emit(sm, a, obase + out_n, r, sm.u.srt.pay[r], dist);
+        }
+        __syncthreads();
+        out_n += n_new;
+        nbytes += tid == 0 ? 12 * n_new : 0;   // the pairs written
+        F = (int)n_new;
+        sb_frontier(sm, a, F);
+    }
+    int64_t tb;
+    sb_scan(sm, nbytes, &tb);
+    if (tid == 0) {
+        a.meta[3 * (int64_t)si] = ovf ? -1 : out_n;
+        a.meta[3 * (int64_t)si + 1] = trav;
+        a.meta[3 * (int64_t)si + 2] = tb;
+    }
+}
+
+__global__ void __launch_bounds__(kSbThreads) hgx_seq_block(SbArgs a) {
+    __shared__ SbShared sm;
+    for (int si = blockIdx.x; si < a.n; si += gridDim.x) {
+        sb_run(sm, a, si);
+        __syncthreads();
     }
 }
 
@@ -247,55 +713,50 @@ template <class T> struct DevBuf {
     }
 };
 
-}  // namespace
-}  // namespace hgx
-
-using namespace hgx;
-
-struct hgx_seq_result {
-    int32_t n_seeds = 0;
-    int32_t n_levels = 0;           // 1 + deepest distance returned by any seed
-    std::vector<int64_t> off;       // [n_seeds + 1]
-    std::vector<int32_t> link, atom, dist;
-    double ms_total = 0, traversed = 0;
+// Where the pairs of a seed live: segments of mapped host buffers (dist = nullptr: every pair of the
+// segment has distance dist_c).
+struct Seg {
+    const int32_t *link, *atom, *dist;
+    int64_t n;
+    int32_t dist_c;
 };
 
-extern "C" {
+// The level-synchronous engine's output: per seed its segments (one per level it reached), the
+// mapped buffers they live in (the result owns them), traversed items, deepest distance.
+struct SeqOut {
+    std::vector<std::vector<Seg>> segs;   // [n seeds]
+    std::vector<PoolBuf> bufs;
+    double traversed = 0;
+    int32_t deepest = 0;
+};
 
-int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
-                     const hgx_algen_opts* opts, hgx_seq_result** out) {
-    HGX_API_BEGIN
-    if (!g || !out || n_seeds < 0 || (n_seeds > 0 && !seeds)) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad argument");
-    *out = nullptr;
-    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: not available on a partition shard");
-    // FIFO order and the discovering link follow the incidence order, i.e. rank order; after an
-    // update appended ranks whose handles may sort before existing ones that is not handle order
-    // (ADVICE r01), and no re-sort of the output can repair it.
-    if (!g->ranks_ordered)
-        fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: ranks were appended by hgx_graph_update and may not follow "
-                                "handle order (re-assert with HGX_OPT_RANKS_ORDERED or rebuild the snapshot)");
-    hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
-    for (int32_t i = 0; i < n_seeds; ++i)
-        if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_sequence: seed out of range");
-    if (max_depth < -1) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad max_depth");
-    std::lock_guard<std::mutex> lk(g->mu);
-    HGX_HIP(hipSetDevice(g->device));
+PoolBuf take_host_buf(hgx_graph* g, size_t bytes);
+
+// Key widths of the level-synchronous engine and the block engine's yield rank (once per snapshot).
+void seq_maxes(hgx_graph* g) {
+    if (g->max_deg >= 0) return;
+    hipStream_t st = g->stream;
+    u64* d = (u64*)g->alloc(16);
+    HGX_HIP(hipMemsetAsync(d, 0, 16, st));
+    k_seq_maxes<<<grid_for(std::max(g->M, g->A), 256), 256, 0, st>>>(g->M, g->tgt_off, g->A, g->inc_off, d);
+    HGX_CHECK_LAUNCH();
+    u64* h = (u64*)g->pinned_buf(16);
+    HGX_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, st));
+    HGX_HIP(hipStreamSynchronize(st));
+    g->release(d, 16);
+    g->max_arity = (int64_t)h[0];
+    g->max_deg = (int64_t)h[1];
+}
+
+// The level-synchronous engine: every level of a chunk of seeds is degree prefix -> expand (one
+// incidence item per lane, atomicMin of stream keys on key[seed][atom]) -> sort of the level's
+// discoveries by key -> decode.  Any traversal size; two host round trips per level.  Caller holds
+// g->mu, g's device is current.
+void seq_levels(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t maxd, const hgx_algen_opts& o,
+                SeqOut& out) {
     hipStream_t st = g->stream;
     const int64_t A = g->A;
-    const int32_t maxd = max_depth < 0 ? INT32_MAX : max_depth;
-
-    if (g->max_deg < 0) {                       // key widths, once per snapshot
-        u64* d = (u64*)g->alloc(16);
-        HGX_HIP(hipMemsetAsync(d, 0, 16, st));
-        k_seq_maxes<<<grid_for(std::max(g->M, A), 256), 256, 0, st>>>(g->M, g->tgt_off, A, g->inc_off, d);
-        HGX_CHECK_LAUNCH();
-        u64 h[2];
-        HGX_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, st));
-        HGX_HIP(hipStreamSynchronize(st));
-        g->release(d, 16);
-        g->max_arity = (int64_t)h[0];
-        g->max_deg = (int64_t)h[1];
-    }
+    seq_maxes(g);
     const int sh_j = bitlen(g->max_arity > 0 ? (u64)(g->max_arity - 1) : 0);
     const int bits_j = bitlen(g->max_deg > 0 ? (u64)(g->max_deg - 1) : 0);
     const int sh_e = sh_j + bits_j;
@@ -306,30 +767,16 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     while (B > 1 && (bitlen((u64)B * (u64)(A + 1)) + sh_e > 64 || B * A * 40 > budget)) B = (B + 1) / 2;
     if (bitlen((u64)B * (u64)(A + 1)) + sh_e > 64)
         fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: stream keys exceed 64 bits for this graph");
-
-    hgx_seq_result* r = new hgx_seq_result();
-    struct Guard {
-        hgx_seq_result* r;
-        ~Guard() { delete r; }
-    } guard{r};
-    r->n_seeds = n_seeds;
-    r->off.assign((size_t)n_seeds + 1, 0);
-    // per level: (seed slot, link, atom) host copies, assembled seed-major at the end
+    out.segs.assign((size_t)n_seeds, {});
+    // per level of a chunk: the mapped buffer [first nb int64][last nb int64][link nn][atom nn]
     struct Level {
-        int64_t chunk0;
+        int64_t chunk0, nb, nn;
         int32_t depth;
-        std::vector<int32_t> seed, link, atom;
+        char* h;
     };
     std::vector<Level> levels;
-
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (g->timing) {
-        HGX_HIP(hipEventCreate(&ev0));
-        HGX_HIP(hipEventCreate(&ev1));
-        HGX_HIP(hipEventRecord(ev0, st));
-    }
     DevBuf<u64> key(g), knew(g), ksort(g);
-    DevBuf<int32_t> fa(g), fs(g), na(g), ns(g), olink(g), dseeds(g);
+    DevBuf<int32_t> fa(g), fs(g), na(g), ns(g), dseeds(g);
     DevBuf<int64_t> pre(g), pre_in(g), list(g), lsort(g);
     DevBuf<u64> cnt(g);
     DevBuf<char> tmp(g);
@@ -359,9 +806,9 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             HGX_HIP(rocprim::exclusive_scan(tmp.get(tb), tb, ddeg, dpre, (int64_t)0, (size_t)F + 1, rocprim::plus<int64_t>(),
                                             st));
             HGX_HIP(hipMemcpyAsync(&h_cnt[0], dpre + F, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipStreamSynchronize(st));
+            spin_sync(st);
             const int64_t T = (int64_t)h_cnt[0];
-            r->traversed += (double)T;
+            out.traversed += (double)T;
             if (T == 0) break;
             const int64_t cap = std::min<int64_t>(nb * A, T * std::max<int64_t>(g->max_arity, 1));
             int64_t* dlist = list.get(cap);
@@ -372,7 +819,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             hgx_seq_expand<<<grid_for(ceil_div(T, 256) * 256, 256, 16384), 256, 0, st>>>(ea);
             HGX_CHECK_LAUNCH();
             HGX_HIP(hipMemcpyAsync(&h_cnt[1], dcnt, sizeof(u64), hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipStreamSynchronize(st));
+            spin_sync(st);
             const int64_t nn = (int64_t)h_cnt[1];
             if (nn > cap) fail(HGX_E_DEVICE, "hgx_bfs_sequence: discovery list overflow");
             e_base += (u64)F;
@@ -389,21 +836,19 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             HGX_HIP(rocprim::radix_sort_pairs(tmp.get(tb), tb, dk, dks, dlist, dls, (size_t)nn, 0u, (unsigned)end_bit, st));
             int32_t* nxa = na.get(nn);
             int32_t* nxs = ns.get(nn);
-            int32_t* ol = olink.get(nn);
+            const size_t hbytes = 16 * (size_t)nb + 8 * (size_t)nn;
+            PoolBuf hb = take_host_buf(g, hbytes);
+            out.bufs.push_back(hb);
+            std::memset(hb.p, 0, 16 * (size_t)nb);   // seeds the level does not reach: empty ranges
+            void* dv = nullptr;
+            HGX_HIP(hipHostGetDevicePointer(&dv, hb.p, 0));
+            int64_t* dfirst = (int64_t*)dv;
+            int32_t* dlink = (int32_t*)(dfirst + 2 * nb);
             hgx_seq_decode<<<grid_for(nn, 256), 256, 0, st>>>(nn, dks, dls, e_base - (u64)F, sh_e, sh_j, jmask, A,
                                                               cur_a, cur_s, g->inc_off, g->inc_row, g->link_atom,
-                                                              nxa, nxs, ol);
+                                                              nxa, nxs, dlink, dlink + nn, dfirst, dfirst + nb);
             HGX_CHECK_LAUNCH();
-            Level lv;
-            lv.chunk0 = c0;
-            lv.depth = d + 1;
-            lv.seed.resize(nn);
-            lv.link.resize(nn);
-            lv.atom.resize(nn);
-            HGX_HIP(hipMemcpyAsync(lv.seed.data(), nxs, sizeof(int32_t) * nn, hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipMemcpyAsync(lv.link.data(), ol, sizeof(int32_t) * nn, hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipMemcpyAsync(lv.atom.data(), nxa, sizeof(int32_t) * nn, hipMemcpyDeviceToHost, st));
-            levels.push_back(std::move(lv));
+            levels.push_back({c0, nb, nn, d + 1, (char*)hb.p});
             deepest = std::max(deepest, d + 1);
             // the new level becomes the frontier (swap buffers)
             std::swap(fa.p, na.p);
@@ -415,32 +860,239 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             F = nn;
         }
     }
-    if (g->timing) HGX_HIP(hipEventRecord(ev1, st));
-    HGX_HIP(hipStreamSynchronize(st));
+    spin_sync(st);
+    // per seed, its segment of every level it reached (levels in order)
+    for (auto& lv : levels) {
+        const int64_t* first = (const int64_t*)lv.h;
+        const int64_t* last = first + lv.nb;
+        const int32_t* lk = (const int32_t*)(first + 2 * lv.nb);
+        const int32_t* at = lk + lv.nn;
+        for (int64_t s = 0; s < lv.nb; ++s) {
+            const int64_t n = last[s] - first[s];
+            if (n > 0) out.segs[(size_t)(lv.chunk0 + s)].push_back({lk + first[s], at + first[s], nullptr, n, lv.depth});
+        }
+    }
+    out.deepest = deepest;
+}
+
+// A mapped host buffer of the graph's result pool (best fit within 8x), or a new one.
+PoolBuf take_host_buf(hgx_graph* g, size_t bytes) {
+    {
+        std::lock_guard<std::mutex> lk(g->seq_mu);
+        size_t best = (size_t)-1;
+        for (size_t i = 0; i < g->seq_hbufs.size(); ++i) {
+            const size_t n = g->seq_hbufs[i].n;
+            if (n >= bytes && n <= std::max<size_t>(8 * bytes, (size_t)1 << 20) &&
+                (best == (size_t)-1 || n < g->seq_hbufs[best].n))
+                best = i;
+        }
+        if (best != (size_t)-1) {
+            PoolBuf b = g->seq_hbufs[best];
+            g->seq_hbufs.erase(g->seq_hbufs.begin() + best);
+            return b;
+        }
+    }
+    void* p = nullptr;
+    HGX_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped));
+    return PoolBuf{p, bytes};
+}
+
+}  // namespace
+}  // namespace hgx
+
+using namespace hgx;
+
+// Per seed, where its pairs live: a region of a mapped buffer the workgroup engine wrote, or one
+// segment per level of the level-synchronous run's mapped buffers.  The result keeps a reference on
+// its graph so the mapped buffers go back to the graph's pool when it is freed.
+struct hgx_seq_result {
+    int32_t n_seeds = 0;
+    int32_t n_levels = 0;           // 1 + deepest distance returned by any seed
+    std::vector<int64_t> off;       // [n_seeds + 1]
+    std::vector<Seg> blk;           // [n_seeds] the workgroup engine's region (n < 0: level engine)
+    std::vector<PoolBuf> hbufs;     // mapped buffers of the workgroup launches (owned until free)
+    SeqOut lev;                     // the level-synchronous engine's seeds (indexed by rerun order)
+    std::vector<int32_t> lev_of;    // [n_seeds] index into lev.segs, or -1
+    hgx_graph* g = nullptr;
+    double ms_total = 0, traversed = 0;
+    double ms_block = 0, bytes_block = 0;   // the workgroup engine's launches: device ms, algorithmic bytes
+    int32_t n_block = 0, n_level = 0;       // seeds finished by each engine
+    ~hgx_seq_result() {
+        if (!g) return;
+        {
+            std::lock_guard<std::mutex> lk(g->seq_mu);
+            for (auto& b : hbufs) g->seq_hbufs.push_back(b);
+            for (auto& b : lev.bufs) g->seq_hbufs.push_back(b);
+        }
+        hbufs.clear();
+        lev.bufs.clear();
+        graph_release(g);
+    }
+};
+
+extern "C" {
+
+int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth,
+                     const hgx_algen_opts* opts, hgx_seq_result** out) {
+    HGX_API_BEGIN
+    if (!g || !out || n_seeds < 0 || (n_seeds > 0 && !seeds)) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad argument");
+    *out = nullptr;
+    if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: not available on a partition shard");
+    // FIFO order and the discovering link follow the incidence order, i.e. rank order; after an
+    // update appended ranks whose handles may sort before existing ones that is not handle order
+    // (ADVICE r01), and no re-sort of the output can repair it.
+    if (!g->ranks_ordered)
+        fail(HGX_E_UNSUPPORTED, "hgx_bfs_sequence: ranks were appended by hgx_graph_update and may not follow "
+                                "handle order (re-assert with HGX_OPT_RANKS_ORDERED or rebuild the snapshot)");
+    hgx_algen_opts o = opts ? *opts : hgx_algen_opts{HGX_NO_TYPE, 1, 1, 0, 0};
+    for (int32_t i = 0; i < n_seeds; ++i)
+        if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_sequence: seed out of range");
+    if (max_depth < -1) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad max_depth");
+    std::lock_guard<std::mutex> lk(g->mu);
+    HGX_HIP(hipSetDevice(g->device));
+    hipStream_t st = g->stream;
+    const int32_t maxd = max_depth < 0 ? INT32_MAX : max_depth;
+    const int mode = seq_mode(o);
+
+    hgx_seq_result* r = new hgx_seq_result();
+    struct Guard {
+        hgx_seq_result* r;
+        ~Guard() { delete r; }
+    } guard{r};
+    r->g = g;
+    g->refs.fetch_add(1);
+    r->n_seeds = n_seeds;
+    r->blk.assign((size_t)n_seeds, Seg{nullptr, nullptr, nullptr, -1, 0});
+    r->lev_of.assign((size_t)n_seeds, -1);
+    std::vector<int64_t> cnt((size_t)n_seeds, 0);
+    seq_maxes(g);
+    if (mode != sSym) ensure_inc_yield(g);
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (g->timing) {
+        HGX_HIP(hipEventCreate(&ev0));
+        HGX_HIP(hipEventCreate(&ev1));
+        HGX_HIP(hipEventRecord(ev0, st));
+    }
+    std::vector<int32_t> rerun;   // seed indices for the level-synchronous engine
+    int32_t deepest = 0;
+    if (g->seq_engine == 0 && n_seeds > 0) {
+        const int kbits = bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
+        SbArgs a{};
+        a.inc_off = g->inc_off;
+        a.inc_row = g->inc_row;
+        a.inc_type = g->inc_type;
+        a.yf = mode != sSym ? g->inc_yf : nullptr;
+        a.tgt_off = g->tgt_off;
+        a.tgt_idx = g->tgt_idx;
+        a.link_atom = g->link_atom;
+        a.want_type = o.link_type;
+        a.min_arity = o.return_source ? 1 : 2;
+        a.mode = mode;
+        a.rev = o.reverse_order ? 1 : 0;
+        a.kbits = kbits;
+        a.maxd = maxd;
+        a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
+        const size_t per_seed = (size_t)kSbPairs * 12 + 24;
+        int32_t* dseeds = nullptr;
+        size_t dseeds_n = 0;
+        if (n_seeds > kSbInline) {
+            dseeds_n = sizeof(int32_t) * (size_t)n_seeds;
+            dseeds = (int32_t*)g->alloc(dseeds_n);
+            int32_t* hs = (int32_t*)g->pinned_buf(dseeds_n);
+            std::memcpy(hs, seeds, dseeds_n);
+            HGX_HIP(hipMemcpyAsync(dseeds, hs, dseeds_n, hipMemcpyHostToDevice, st));
+        }
+        struct Chunk {
+            int64_t c0, nb;
+            char* h;
+        };
+        std::vector<Chunk> chunks;
+        for (int64_t c0 = 0; c0 < n_seeds; c0 += kSbChunk) {
+            const int64_t nb = std::min<int64_t>(kSbChunk, n_seeds - c0);
+            PoolBuf hb = take_host_buf(g, per_seed * (size_t)nb);
+            r->hbufs.push_back(hb);
+            char* h = (char*)hb.p;
+            void* dv = nullptr;
+            HGX_HIP(hipHostGetDevicePointer(&dv, h, 0));
+            char* d = (char*)dv;
+            // layout: meta [3 nb] int64 | link [nb * kSbPairs] | atom [..] | dist [..]
+            a.n = (int32_t)nb;
+            a.meta = (int64_t*)d;
+            a.out_link = (int32_t*)(d + 24 * nb);
+            a.out_atom = a.out_link + nb * kSbPairs;
+            a.out_dist = a.out_atom + nb * kSbPairs;
+            if (n_seeds <= kSbInline) {
+                for (int64_t i = 0; i < nb; ++i) a.seed_inline[i] = seeds[c0 + i];
+                a.seeds = nullptr;
+            } else {
+                a.seeds = dseeds + c0;
+            }
+            hgx_seq_block<<<(unsigned)nb, kSbThreads, 0, st>>>(a);
+            HGX_CHECK_LAUNCH();
+            chunks.push_back({c0, nb, h});
+        }
+        hipEvent_t evb = nullptr;
+        if (g->timing) {
+            HGX_HIP(hipEventCreate(&evb));
+            HGX_HIP(hipEventRecord(evb, st));
+        }
+        spin_sync(st);
+        if (evb) {
+            float ms = 0;
+            HGX_HIP(hipEventElapsedTime(&ms, ev0, evb));
+            r->ms_block = ms;
+            (void)hipEventDestroy(evb);
+        }
+        if (dseeds) g->release(dseeds, dseeds_n);
+        for (auto& c : chunks) {
+            const int64_t* meta = (const int64_t*)c.h;
+            const int32_t* lk_ = (const int32_t*)(c.h + 24 * c.nb);
+            const int32_t* at = lk_ + c.nb * kSbPairs;
+            const int32_t* ds = at + c.nb * kSbPairs;
+            for (int64_t i = 0; i < c.nb; ++i) {
+                const int64_t np = meta[3 * i];
+                const int64_t si = c.c0 + i;
+                r->bytes_block += (double)meta[3 * i + 2];
+                if (np < 0) {
+                    rerun.push_back((int32_t)si);
+                    continue;
+                }
+                cnt[si] = np;
+                r->traversed += (double)meta[3 * i + 1];
+                r->blk[si] = {lk_ + i * kSbPairs, at + i * kSbPairs, ds + i * kSbPairs, np, 0};
+                if (np > 0) deepest = std::max(deepest, ds[i * kSbPairs + np - 1]);
+            }
+        }
+    } else {
+        for (int32_t i = 0; i < n_seeds; ++i) rerun.push_back(i);
+    }
+    r->n_level = (int32_t)rerun.size();
+    r->n_block = n_seeds - r->n_level;
+    if (!rerun.empty()) {
+        std::vector<int32_t> rs(rerun.size());
+        for (size_t k = 0; k < rerun.size(); ++k) rs[k] = seeds[rerun[k]];
+        seq_levels(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev);
+        r->traversed += r->lev.traversed;
+        deepest = std::max(deepest, r->lev.deepest);
+        for (size_t k = 0; k < rerun.size(); ++k) {
+            int64_t n = 0;
+            for (const Seg& sg : r->lev.segs[k]) n += sg.n;
+            cnt[rerun[k]] = n;
+            r->lev_of[rerun[k]] = (int32_t)k;
+        }
+    }
+    if (g->timing) {
+        HGX_HIP(hipEventRecord(ev1, st));
+        HGX_HIP(hipEventSynchronize(ev1));
         float ms = 0;
         HGX_HIP(hipEventElapsedTime(&ms, ev0, ev1));
         r->ms_total = ms;
         (void)hipEventDestroy(ev0);
         (void)hipEventDestroy(ev1);
     }
-    // assemble: seed-major, then distance, then FIFO order
-    std::vector<int64_t>& off = r->off;
-    for (auto& lv : levels)
-        for (int32_t s : lv.seed) off[(size_t)(lv.chunk0 + s) + 1]++;
-    for (int32_t i = 0; i < n_seeds; ++i) off[i + 1] += off[i];
-    const int64_t total = off[n_seeds];
-    r->link.resize(total);
-    r->atom.resize(total);
-    r->dist.resize(total);
-    std::vector<int64_t> pos(off.begin(), off.end() - 1);
-    for (auto& lv : levels)
-        for (size_t i = 0; i < lv.seed.size(); ++i) {
-            const int64_t q = pos[(size_t)(lv.chunk0 + lv.seed[i])]++;
-            r->link[q] = lv.link[i];
-            r->atom[q] = lv.atom[i];
-            r->dist[q] = lv.depth;
-        }
+    r->off.assign((size_t)n_seeds + 1, 0);
+    for (int32_t i = 0; i < n_seeds; ++i) r->off[i + 1] = r->off[i] + cnt[i];
     r->n_levels = deepest + 1;
     guard.r = nullptr;
     *out = r;
@@ -466,10 +1118,26 @@ int hgx_seq_result_offsets(const hgx_seq_result* r, int64_t* offsets) {
 int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms, int32_t* dists) {
     HGX_API_BEGIN
     if (!r) fail(HGX_E_INVALID, "null result");
-    const size_t n = r->link.size();
-    if (links && n) std::memcpy(links, r->link.data(), sizeof(int32_t) * n);
-    if (atoms && n) std::memcpy(atoms, r->atom.data(), sizeof(int32_t) * n);
-    if (dists && n) std::memcpy(dists, r->dist.data(), sizeof(int32_t) * n);
+    auto put = [&](int64_t b, const Seg& s) {
+        if (s.n <= 0) return;
+        if (links) std::memcpy(links + b, s.link, sizeof(int32_t) * s.n);
+        if (atoms) std::memcpy(atoms + b, s.atom, sizeof(int32_t) * s.n);
+        if (dists) {
+            if (s.dist) std::memcpy(dists + b, s.dist, sizeof(int32_t) * s.n);
+            else std::fill(dists + b, dists + b + s.n, s.dist_c);
+        }
+    };
+    for (int32_t i = 0; i < r->n_seeds; ++i) {
+        int64_t b = r->off[i];
+        if (r->lev_of[i] < 0) {
+            put(b, r->blk[i]);
+            continue;
+        }
+        for (const Seg& s : r->lev.segs[(size_t)r->lev_of[i]]) {
+            put(b, s);
+            b += s.n;
+        }
+    }
     HGX_API_END
 }
 
@@ -478,6 +1146,17 @@ int hgx_seq_result_stats(const hgx_seq_result* r, double* ms_total, double* trav
     if (!r) fail(HGX_E_INVALID, "null result");
     if (ms_total) *ms_total = r->ms_total;
     if (traversed_edges) *traversed_edges = r->traversed;
+    HGX_API_END
+}
+
+int hgx_seq_result_engine_stats(const hgx_seq_result* r, int32_t* n_block, int32_t* n_level, double* ms_block,
+                                 double* bytes_block) {
+    HGX_API_BEGIN
+    if (!r) fail(HGX_E_INVALID, "null result");
+    if (n_block) *n_block = r->n_block;
+    if (n_level) *n_level = r->n_level;
+    if (ms_block) *ms_block = r->ms_block;
+    if (bytes_block) *bytes_block = r->bytes_block;
     HGX_API_END
 }
 

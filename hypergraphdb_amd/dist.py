@@ -39,6 +39,17 @@ class RankContext:
     def sum(self, x):
         return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist is not None else x
 
+    def sum_array(self, a):
+        """Element-wise int64 sum of a numpy array over the ranks (every rank gets the sum)."""
+        import numpy as np
+        a = np.ascontiguousarray(a, np.int64)
+        if self.dist is None:
+            return a.copy()
+        import torch
+        t = torch.from_numpy(a.copy())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.numpy()
+
     def broadcast_bytes(self, data: bytes) -> bytes:
         """rank 0's bytes on every rank (the RCCL unique id travels over the gloo group)"""
         if self.dist is None:

@@ -188,8 +188,8 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                              without the active-link probe in all-rows levels (A/B only).
  *                      Default 0x3BE. */
 #define HGX_OPT_BFS_FLAGS 1
-/* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal may use for its per-seed key arrays
- * (seeds are processed in chunks that fit; default 16 GiB). */
+/* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal's level-synchronous engine may use for
+ * its per-seed key arrays (seeds are processed in chunks that fit; default 48 GiB). */
 #define HGX_OPT_SEQ_BUDGET 2
 /* HGX_OPT_RANKS_ORDERED: 1 = the rank order equals the persistent-handle order (the default for a
  * fresh snapshot).  An hgx_graph_update that extends the rank space sets it to 0: appended ranks
@@ -275,6 +275,13 @@ int  hgx_seq_result_offsets(const hgx_seq_result *r, int64_t *offsets);
 int  hgx_seq_result_pairs(const hgx_seq_result *r, int32_t *links, int32_t *atoms, int32_t *dists);
 /* device ms (timing enabled) and sum over seeds and expanded atoms of |inc(atom)|. */
 int  hgx_seq_result_stats(const hgx_seq_result *r, double *ms_total, double *traversed_edges);
+/* Which engine finished the seeds (HGX_OPT_SEQ_ENGINE): seeds done by the workgroup-per-seed engine /
+ * by the level-synchronous one (the overflow reruns), the device ms of the workgroup launches (from the
+ * call's first operation to their end; timing enabled) and their algorithmic bytes (streamed yield
+ * flags, the staged entries' type / row / target-offset / link-id / target loads, frontier offsets,
+ * pairs written).  Any output may be NULL. */
+int  hgx_seq_result_engine_stats(const hgx_seq_result *r, int32_t *n_block, int32_t *n_level, double *ms_block,
+                                 double *bytes_block);
 void hgx_seq_result_free(hgx_seq_result *r);
 /* Batched conjunctive pattern queries.  Result of query q = the link atoms L with
  * type(L) == type, every incident/pattern anchor in targets(L) and
@@ -427,6 +434,12 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * (2.14-2.25 against 2.16-2.17 ms per concurrent step, profiles/r03n_c5.log: the rows of a graph that
  * size are cache hits), so the default saves the memory. */
 #define HGX_OPT_PUSH_INLINE 12
+/* HGX_OPT_SEQ_ENGINE (default 0): how hgx_bfs_sequence runs.  0 = one workgroup per seed with the
+ * whole traversal in LDS (hash of the examined atoms, frontier and discovery ranks on chip, pairs
+ * written into mapped host memory; one launch per 1024 seeds, no host round trip per level), seeds
+ * whose traversal outgrows the workgroup's 2046 pairs rerun on the level-synchronous engine;
+ * 1 = every seed on the level-synchronous engine (A/B and tests). */
+#define HGX_OPT_SEQ_ENGINE 13
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */
 int  hgx_query_coalesce_stats(hgx_graph *g, int64_t *device_batches, int64_t *caller_batches);

@@ -120,3 +120,72 @@ def test_traversal_iterator_matches_reference_order():
     assert tr.next() is None
     tr.reset()
     assert tr.hasNext() == (len(a) > 0)
+
+
+def _seq(snap, seeds, maxd, g_, engine):
+    from hypergraphdb_amd import _lib, bfs_sequence
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, engine)
+    try:
+        return bfs_sequence(snap, seeds, maxd, g_)
+    finally:
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_workgroup_and_level_engines_agree(case):
+    """The workgroup-per-seed engine (default) and the level-synchronous engine return identical
+    sequences, links, distances and traversal counts -- over graphs whose closures stay inside one
+    workgroup and graphs whose hubs push some seeds over its 2046 pairs (those rerun on the
+    level-synchronous engine)."""
+    from hypergraphdb_amd import synth
+    rng = np.random.default_rng(40 + case)
+    if case < 2:
+        g = K.random_graph(rng, 3000, 2000, max_arity=9, link_targets=True, n_types=3)
+    else:
+        g = synth.hypergraph(6000, 9000, 2, 6, 2.1, 2, seed=70 + case)
+    snap = snapshot(g)
+    seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
+    for mi, mode in enumerate(K.ALGEN_MODES):
+        lt = [-1, 0, 1][mi % 3] if case % 2 == 0 else -1
+        for maxd in (None, 2):
+            a = _seq(snap, seeds, maxd, gen(snap, mode, lt), 0)
+            b = _seq(snap, seeds, maxd, gen(snap, mode, lt), 1)
+            assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd)
+            assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd)
+            assert np.array_equal(a.dists, b.dists), (case, mi, maxd)
+            assert a.traversed_edges == b.traversed_edges and a.n_levels == b.n_levels
+    snap.close()
+
+
+def test_workgroup_engine_overflow_mixed_with_small_seeds_vs_oracle():
+    """A batch mixing seeds whose traversal exceeds the workgroup's pairs (hub neighbourhoods) with
+    tiny ones, checked seed by seed against the oracle."""
+    from hypergraphdb_amd import synth
+    g = synth.hypergraph(20000, 30000, 2, 5, 2.0, 1, seed=5)
+    snap, orc = snapshot(g), oracle(g)
+    deg = np.diff(np.searchsorted(np.sort(g["tgt_idx"]), np.arange(g["num_atoms"] + 1)))
+    hubs = np.argsort(-deg)[:3].astype(np.int32)
+    seeds = np.concatenate([hubs, np.arange(19990, 20000, dtype=np.int32), hubs[:1]])
+    res = check_seq(g, seeds, 3, K.ALGEN_MODES[0], -1, snap, orc)
+    assert (np.diff(res.offsets) > 2046).any() and (np.diff(res.offsets) <= 2046).any()
+
+
+def test_config5_closures_sequence_vs_oracle():
+    """Config 5 (5M classes, full size): hg.subsumed / hg.subsumes as order-exact sequences for 128
+    classes of the bench's 1024 against the oracle, pair by pair; the batch of 1024 equals the
+    concatenation of single-seed calls (the drop-in issues one traversal per HGGpuTraversal)."""
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, bfs_sequence, synth
+    g = synth.config5()
+    snap, orc = snapshot(g), oracle(g)
+    T = g["subsumes_type"]
+    for rev in (False, True):
+        gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
+        res = bfs_sequence(snap, g["seeds"], None, gen_)
+        for i in range(0, 1024, 8):
+            l_, a, d, _ = orc.bfs(int(g["seeds"][i]), -1, algen(T, False, True, rev, False))
+            gl, ga, gd = res.pairs(i)
+            assert np.array_equal(ga, a) and np.array_equal(gl, l_) and np.array_equal(gd, d), (rev, i)
+        for i in (0, 1, 511, 1023):
+            one = bfs_sequence(snap, g["seeds"][i:i + 1], None, gen_)
+            assert all(np.array_equal(x, y) for x, y in zip(one.pairs(0), res.pairs(i))), (rev, i)
+    snap.close()

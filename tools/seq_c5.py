@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Order-exact traversal (hgx_bfs_sequence, what HGGpuTraversal.next() and the hg.subsumed /
+hg.subsumes drop-ins run) on config 5: batched 1024-closure calls and single-seed latency per
+direction, for the workgroup-per-seed engine (HGX_OPT_SEQ_ENGINE 0) and the level-synchronous one (1).
+
+  python tools/seq_c5.py [--scale 1.0] [--single 200] [--engines 0,1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--single", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--engines", default="0,1")
+    args = ap.parse_args()
+    import hypergraphdb_amd as H
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_sequence, synth
+    g = synth.config5(scale=args.scale)
+    snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    snap.set_timing(True)
+    T = g["subsumes_type"]
+    out = {"workload": f"config5 scale {args.scale}", "seeds": len(g["seeds"]), "engines": {}}
+    for eng in [int(x) for x in args.engines.split(",")]:
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, eng)
+        e = {}
+        for rev, name in ((False, "subsumed"), (True, "subsumes")):
+            gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
+            bfs_sequence(snap, g["seeds"], None, gen_)   # warm-up (tables, buffers)
+            walls, devs = [], []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                r = bfs_sequence(snap, g["seeds"], None, gen_)
+                walls.append(time.perf_counter() - t0)
+                devs.append(r.ms_total)
+            pairs = int(r.offsets[-1])
+            singles = []
+            for s in g["seeds"][: args.single]:
+                t0 = time.perf_counter()
+                bfs_sequence(snap, [s], None, gen_)
+                singles.append(time.perf_counter() - t0)
+            singles.sort()
+            e[name] = {"batch_wall_ms": round(float(np.median(walls)) * 1e3, 3),
+                       "batch_device_ms": round(float(np.median(devs)), 3), "pairs": pairs,
+                       "traversed_items": r.traversed_edges,
+                       "single_ms_median": round(singles[len(singles) // 2] * 1e3, 4),
+                       "single_ms_p90": round(singles[int(len(singles) * 0.9)] * 1e3, 4),
+                       "single_ms_max": round(singles[-1] * 1e3, 4)}
+            print(f"engine {eng} {name}: {e[name]}", file=sys.stderr, flush=True)
+        out["engines"][str(eng)] = e
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
