@@ -2928,8 +2928,8 @@ __global__ void __launch_bounds__(256) hgx_extract(int64_t A, int64_t span, int 
         int64_t wbase = run;
         for (int k = 0; k < wid; ++k) wbase += wave_tot[k];
         if (write && hit) {
-            int64_t pos = wbase + before;
-            if (pos < cap) out[pos] = (int32_t)v;
+            int64_t pos = wbase + before;   // (blk_off may start below 0: a range read from a later position)
+            if (pos >= 0 && pos < cap) out[pos] = (int32_t)v;
         }
         __syncthreads();
         if (threadIdx.x == 0) run += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
@@ -5480,8 +5480,14 @@ int hgx_bfs_result_counts(hgx_bfs_result* r, int64_t* counts) {
 
 int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth, int32_t* out, int64_t cap,
                            int64_t* n_out) {
+    return hgx_bfs_result_visited_range(r, seed_index, depth, 0, out, cap, n_out);
+}
+
+int hgx_bfs_result_visited_range(hgx_bfs_result* r, int32_t seed_index, int32_t depth, int64_t first, int32_t* out,
+                                 int64_t cap, int64_t* n_out) {
     HGX_API_BEGIN
-    if (!r || !n_out || (cap > 0 && !out)) fail(HGX_E_INVALID, "hgx_bfs_result_visited: bad argument");
+    if (!r || !n_out || (cap > 0 && !out) || first < 0 || cap < 0)
+        fail(HGX_E_INVALID, "hgx_bfs_result_visited: bad argument");
     if (seed_index < 0 || seed_index >= r->n_seeds) fail(HGX_E_NOTFOUND, "no such seed index");
     if (depth < 0) fail(HGX_E_NOTFOUND, "no such depth");
     hgx_graph* g = r->g;
@@ -5494,7 +5500,7 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
     if (iso != r->isolated.end()) {   // an isolated seed: only itself, at distance 0
         if (depth == 0) {
             *n_out = 1;
-            if (cap > 0) out[0] = iso->second;
+            if (cap > 0 && first == 0) out[0] = iso->second;
         }
         return HGX_OK;
     }
@@ -5512,11 +5518,11 @@ int hgx_bfs_result_visited(hgx_bfs_result* r, int32_t seed_index, int32_t depth,
     HGX_HIP(hipStreamSynchronize(g->stream));
     int64_t tot = 0;
     for (int i = 0; i < nblk; ++i) {
-        ho[i] = tot;
+        ho[i] = tot - first;   // positions relative to the range's first entry
         tot += hc[i];
     }
     *n_out = tot;
-    int64_t k = std::min(tot, cap);
+    int64_t k = std::min(std::max<int64_t>(tot - first, 0), cap);
     if (k > 0) {
         int32_t* dout = (int32_t*)g->alloc(sizeof(int32_t) * k);
         HGX_HIP(hipMemcpyAsync(doff, ho.data(), sizeof(int64_t) * nblk, hipMemcpyHostToDevice, g->stream));

@@ -155,12 +155,33 @@ void download(hgx_graph* g, std::vector<int32_t>& la, std::vector<int64_t>& off,
 
 }  // namespace
 
+// A streaming .hgcsr writer: the rows at begin, the handle table in any number of pieces (an exporter
+// walking a store larger than one Java array never holds the whole table), the checksum run alongside;
+// end patches the header and renames the file into place, abort removes the partial file.
+struct hgx_snapshot_writer {
+    std::string path, tmp;
+    FILE* f = nullptr;
+    Header h{};
+    Sections s;
+    uint64_t c = 0;           // running checksum
+    uint8_t carry[8] = {0};   // handle bytes of a partial checksum word
+    size_t carry_n = 0;
+    int64_t ranks = 0;        // handles written so far
+    bool failed = false;
+    ~hgx_snapshot_writer() {
+        if (f) std::fclose(f);
+        if (!tmp.empty()) std::remove(tmp.c_str());
+    }
+};
+
 extern "C" {
 
-int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t* handles, int32_t handle_bytes) {
+int hgx_snapshot_writer_begin(const char* path, const hgx_graph_desc* d, int32_t handle_bytes,
+                              hgx_snapshot_writer** out) {
     HGX_API_BEGIN
-    if (!path || !d || handle_bytes < 0 || handle_bytes > 64 || (handle_bytes > 0 && !handles))
+    if (!path || !d || !out || handle_bytes < 0 || handle_bytes > 64)
         fail(HGX_E_INVALID, "hgx_snapshot_write: bad argument");
+    *out = nullptr;
     const int64_t A = d->num_atoms, M = d->num_links;
     if (A < 0 || M < 0 || M > A || (M > 0 && (!d->link_atom || !d->tgt_off || !d->tgt_idx)))
         fail(HGX_E_INVALID, "hgx_snapshot_write: bad snapshot");
@@ -172,7 +193,8 @@ int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t*
             fail(HGX_E_INVALID, "hgx_snapshot_write: link rows not ascending / offsets not monotone");
     for (int64_t p = 0; p < P; ++p)
         if (d->tgt_idx[p] < 0 || d->tgt_idx[p] >= A) fail(HGX_E_INVALID, "hgx_snapshot_write: target out of range");
-    Header h{};
+    std::unique_ptr<hgx_snapshot_writer> w(new hgx_snapshot_writer());
+    Header& h = w->h;
     std::memcpy(h.magic, kMagic, 8);
     h.version = kVersion;
     h.flags = (d->link_type ? 1u : 0u) | (handle_bytes > 0 ? 2u : 0u);
@@ -180,40 +202,100 @@ int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t*
     h.num_links = M;
     h.num_pins = P;
     h.handle_bytes = (uint32_t)handle_bytes;
-    const Sections s = layout(A, M, P, h.flags, h.handle_bytes);
-    std::vector<int64_t> zero_off;
-    const int64_t* off = d->tgt_off;
-    if (M == 0) {
-        zero_off.assign(1, 0);
-        off = zero_off.data();
-    }
-    const void* ptrs[5] = {d->link_atom, off, d->tgt_idx, d->link_type, handles};
-    h.checksum = file_checksum(h, ptrs, s.len);
-    const std::string tmp = std::string(path) + ".tmp";
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) fail(HGX_E_DEVICE, std::string("hgx_snapshot_write: cannot create ") + tmp);
-    struct Closer {
-        FILE* f;
-        ~Closer() { if (f) std::fclose(f); }
-    } closer{f};
-    write_all(f, &h, sizeof(h));
+    h.checksum = 0;
+    w->s = layout(A, M, P, h.flags, h.handle_bytes);
+    w->path = path;
+    w->tmp = w->path + ".tmp";
+    w->f = std::fopen(w->tmp.c_str(), "wb");
+    if (!w->f) fail(HGX_E_DEVICE, std::string("hgx_snapshot_write: cannot create ") + w->tmp);
+    // the header (its checksum patched in at the end), then the four row sections; the checksum runs
+    // over the header with a zero checksum field and then every section in order (file_checksum)
+    write_all(w->f, &h, sizeof(h));
+    w->c = mix(0x243F6A8885A308D3ull, &h, sizeof(h));
+    const int64_t zero_off = 0;
+    const void* ptrs[4] = {d->link_atom, M ? (const void*)d->tgt_off : (const void*)&zero_off, d->tgt_idx, d->link_type};
     size_t at = sizeof(Header);
     static const char zeros[64] = {0};
-    for (int k = 0; k < 5; ++k) {
-        write_all(f, zeros, s.off[k] - at);
-        write_all(f, ptrs[k], s.len[k]);
-        at = s.off[k] + s.len[k];
+    for (int k = 0; k < 4; ++k) {
+        write_all(w->f, zeros, w->s.off[k] - at);
+        write_all(w->f, ptrs[k], w->s.len[k]);
+        w->c = mix(w->c, ptrs[k], w->s.len[k]);
+        at = w->s.off[k] + w->s.len[k];
     }
-    write_all(f, zeros, s.total - at);
-    // durable before it becomes visible under the final name
-    if (std::fflush(f) != 0 || fsync(fileno(f)) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: fsync failed");
-    if (std::fclose(f) != 0) {
-        closer.f = nullptr;
-        fail(HGX_E_DEVICE, "hgx_snapshot_write: close failed");
-    }
-    closer.f = nullptr;
-    if (std::rename(tmp.c_str(), path) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: rename failed");
+    write_all(w->f, zeros, w->s.off[4] - at);
+    *out = w.release();
     HGX_API_END
+}
+
+int hgx_snapshot_writer_handles(hgx_snapshot_writer* w, const uint8_t* handles, int64_t n_ranks) {
+    HGX_API_BEGIN
+    if (!w || n_ranks < 0 || (n_ranks > 0 && !handles) || w->failed)
+        fail(HGX_E_INVALID, "hgx_snapshot_writer_handles: bad argument");
+    const size_t hb = w->h.handle_bytes;
+    if (n_ranks > 0 && hb == 0) fail(HGX_E_INVALID, "hgx_snapshot_writer_handles: the snapshot has no handle table");
+    if (n_ranks > w->h.num_atoms - w->ranks) fail(HGX_E_INVALID, "hgx_snapshot_writer_handles: more ranks than num_atoms");
+    const size_t n = (size_t)n_ranks * hb;
+    try {
+        write_all(w->f, handles, n);
+    } catch (...) {
+        w->failed = true;
+        throw;
+    }
+    // streamed checksum: whole 8-byte words, a partial one carried to the next call (zero-padded at the end)
+    size_t i = 0;
+    while (i < n && w->carry_n > 0 && w->carry_n < 8) w->carry[w->carry_n++] = handles[i++];
+    if (w->carry_n == 8) {
+        w->c = mix(w->c, w->carry, 8);
+        w->carry_n = 0;
+    }
+    const size_t whole = (n - i) & ~(size_t)7;
+    w->c = mix(w->c, handles + i, whole);
+    i += whole;
+    while (i < n) w->carry[w->carry_n++] = handles[i++];
+    w->ranks += n_ranks;
+    HGX_API_END
+}
+
+int hgx_snapshot_writer_end(hgx_snapshot_writer* w) {
+    HGX_API_BEGIN
+    if (!w) fail(HGX_E_INVALID, "hgx_snapshot_writer_end: null writer");
+    std::unique_ptr<hgx_snapshot_writer> own(w);
+    if (w->failed) fail(HGX_E_DEVICE, "hgx_snapshot_write: an earlier write failed");
+    if (w->h.handle_bytes > 0 && w->ranks != w->h.num_atoms)
+        fail(HGX_E_INVALID, "hgx_snapshot_writer_end: " + std::to_string(w->ranks) + " of " +
+                                std::to_string(w->h.num_atoms) + " handles written");
+    if (w->carry_n) w->c = mix(w->c, w->carry, w->carry_n);
+    static const char zeros[64] = {0};
+    write_all(w->f, zeros, w->s.total - (w->s.off[4] + w->s.len[4]));
+    w->h.checksum = w->c;
+    if (std::fseek(w->f, 0, SEEK_SET) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: seek failed");
+    write_all(w->f, &w->h, sizeof(Header));
+    // durable before it becomes visible under the final name
+    if (std::fflush(w->f) != 0 || fsync(fileno(w->f)) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: fsync failed");
+    FILE* f = w->f;
+    w->f = nullptr;
+    if (std::fclose(f) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: close failed");
+    if (std::rename(w->tmp.c_str(), w->path.c_str()) != 0) fail(HGX_E_DEVICE, "hgx_snapshot_write: rename failed");
+    w->tmp.clear();
+    HGX_API_END
+}
+
+void hgx_snapshot_writer_abort(hgx_snapshot_writer* w) { delete w; }
+
+int hgx_snapshot_write(const char* path, const hgx_graph_desc* d, const uint8_t* handles, int32_t handle_bytes) {
+    if (handle_bytes > 0 && !handles) {
+        set_last_error("hgx_snapshot_write: bad argument");
+        return HGX_E_INVALID;
+    }
+    hgx_snapshot_writer* w = nullptr;
+    int rc = hgx_snapshot_writer_begin(path, d, handle_bytes, &w);
+    if (rc) return rc;
+    if (handle_bytes > 0) rc = hgx_snapshot_writer_handles(w, handles, d->num_atoms);
+    if (rc) {
+        hgx_snapshot_writer_abort(w);
+        return rc;
+    }
+    return hgx_snapshot_writer_end(w);
 }
 
 int hgx_snapshot_info(const char* path, int64_t* num_atoms, int64_t* num_links, int64_t* num_pins,
@@ -238,6 +320,18 @@ int hgx_snapshot_read(const char* path, int32_t* link_atom, int64_t* tgt_off, in
     for (int k = 0; k < 5; ++k)
         if (dst[k] && m->s.len[k]) std::memcpy(dst[k], m->at(k), m->s.len[k]);
     if (link_type && !(m->h.flags & 1)) std::memset(link_type, 0, 4 * (size_t)m->h.num_links);
+    HGX_API_END
+}
+
+int hgx_snapshot_read_handles(const char* path, int64_t first_rank, int64_t n, int32_t verify, uint8_t* out) {
+    HGX_API_BEGIN
+    if (!path || n < 0 || first_rank < 0 || (n > 0 && !out)) fail(HGX_E_INVALID, "hgx_snapshot_read_handles: bad argument");
+    auto m = map_file(path, verify != 0);
+    if (!(m->h.flags & 2)) fail(HGX_E_NOTFOUND, "hgx_snapshot_read_handles: the file has no handle table");
+    if (first_rank > m->h.num_atoms || n > m->h.num_atoms - first_rank)
+        fail(HGX_E_INVALID, "hgx_snapshot_read_handles: ranks outside [0, num_atoms)");
+    const size_t hb = m->h.handle_bytes;
+    if (n) std::memcpy(out, m->at(4) + (size_t)first_rank * hb, (size_t)n * hb);
     HGX_API_END
 }
 

@@ -1220,13 +1220,60 @@ __global__ void __launch_bounds__(kSpBlock) hgx_q_scan_sp(int32_t n, const int64
 // outoff[n_chunks] = total hits; the block holding the last chunk (block 0 when there is none)
 // publishes the hit total and the summed counter shards.
 constexpr int kPlaceChunks = 64;
+// Above this many placement blocks the prefix of the chunk hit counts before each block comes from
+// a two-launch scan (hgx_q_place_bsum + hgx_q_place_bscan) instead of each block summing every chunk
+// before it, which grows with the square of the chunk count.
+constexpr int64_t kPlaceDirectBlocks = 256;
+
+// bsum[b] = hit count of placement block b's chunks (one thread per block).
+__global__ void __launch_bounds__(256) hgx_q_place_bsum(const int32_t* __restrict__ n_chunks_p,
+                                                       const int64_t* __restrict__ counts, int64_t nbp,
+                                                       int64_t* __restrict__ bsum) {
+    const int32_t nc = *n_chunks_p;
+    for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nbp; b += (int64_t)gridDim.x * blockDim.x) {
+        int64_t v = 0;
+        const int64_t k0 = b * kPlaceChunks, k1 = min<int64_t>(nc, k0 + kPlaceChunks);
+        for (int64_t k = k0; k < k1; ++k) v += counts[k];
+        bsum[b] = v;
+    }
+}
+
+// In-place exclusive scan of bsum[0, nbp) by one workgroup (1024 entries a round, carried).
+__global__ void __launch_bounds__(1024) hgx_q_place_bscan(int64_t nbp, int64_t* __restrict__ bsum) {
+    __shared__ int64_t wsum[16];
+    __shared__ int64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t b0 = 0; b0 < nbp; b0 += 1024) {
+        const int64_t b = b0 + threadIdx.x;
+        const int64_t v = b < nbp ? bsum[b] : 0;
+        int64_t x = v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int64_t base = carry, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            base += k < w ? wsum[k] : 0;
+            tot += wsum[k];
+        }
+        if (b < nbp) bsum[b] = base + x - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += tot;
+        __syncthreads();
+    }
+}
 __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n_chunks_p,
                                                   const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
                                                   const int32_t* __restrict__ link_atom, int64_t* __restrict__ outoff,
                                                   int32_t* __restrict__ ids, int64_t* __restrict__ stat,
                                                   const u64* __restrict__ ctr, u64* __restrict__ ctr_out, int32_t n,
                                                   const int32_t* __restrict__ chq, const int64_t* __restrict__ coff,
-                                                  const u64* __restrict__ hitmask, int64_t* __restrict__ q_off) {
+                                                  const u64* __restrict__ hitmask, int64_t* __restrict__ q_off,
+                                                  const int64_t* __restrict__ bpre) {
     __shared__ int64_t ws[4], c_off[kPlaceChunks], qb[2];
     __shared__ int32_t c_cnt[kPlaceChunks];
     const int32_t nc = *n_chunks_p;
@@ -1266,12 +1313,16 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
         if (lane == 0) qb[e] = res;
     }
     int64_t before = 0;   // hit counts of the chunks before this block, eight loads in flight per thread
-    for (int64_t j = threadIdx.x; j < k0; j += 8 * 256) {
-        int64_t v[8];
+    if (!bpre) {          // (large batches: the scanned block sums instead)
+        for (int64_t j = threadIdx.x; j < k0; j += 8 * 256) {
+            int64_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = j + u * 256 < k0 ? counts[j + u * 256] : 0;
+            for (int u = 0; u < 8; ++u) v[u] = j + u * 256 < k0 ? counts[j + u * 256] : 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) before += v[u];
+            for (int u = 0; u < 8; ++u) before += v[u];
+        }
+    } else if (threadIdx.x == 0) {
+        before = bpre[blockIdx.x];
     }
     const int64_t pre = block_sum<int64_t>(before, ws);
     if (wv == 0) {
@@ -2391,6 +2442,11 @@ PackedLayout packed_layout(int32_t n, const int32_t* inc, const int64_t* inc_off
     l.n_pat = pat_off[n] - pat_off[0];
     if (inc_off[0] != 0 || pat_off[0] != 0 || l.n_inc < 0 || l.n_pat < 0 || (l.n_inc > 0 && !inc) || (l.n_pat > 0 && !pat))
         fail(HGX_E_INVALID, std::string(who) + ": bad offsets");
+    // every query's slices inside the columns: the device front end copies pat[pat_off[q] ..
+    // pat_off[q+1]) and the anchors into fixed slots sized from these offsets
+    for (int32_t q = 0; q < n; ++q)
+        if (inc_off[q + 1] < inc_off[q] || pat_off[q + 1] < pat_off[q])
+            fail(HGX_E_INVALID, std::string(who) + ": offsets decrease at query " + std::to_string(q));
     Upload u;
     l.o_type = u.take(4 * (size_t)n);
     l.o_ioff = u.take(8 * (size_t)(n + 1));
@@ -2517,8 +2573,17 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
             hmask, ctr);
         HGX_CHECK_LAUNCH();
         ev.rec(2, s);
-        hgx_q_place<<<(unsigned)std::max<int64_t>(1, ceil_div(capC, kPlaceChunks)), 256, 0, s>>>(
-            nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d, n, chq, coff, hmask, qoff_d);
+        const int64_t nbp = std::max<int64_t>(1, ceil_div(capC, kPlaceChunks));
+        int64_t* bpre = nullptr;
+        if (nbp > kPlaceDirectBlocks) {
+            bpre = (int64_t*)w.take(sizeof(int64_t) * (nbp + 1));
+            hgx_q_place_bsum<<<grid_for(nbp, 256, 4096), 256, 0, s>>>(nch, cnt, nbp, bpre);
+            HGX_CHECK_LAUNCH();
+            hgx_q_place_bscan<<<1, 1024, 0, s>>>(nbp, bpre);
+            HGX_CHECK_LAUNCH();
+        }
+        hgx_q_place<<<(unsigned)nbp, 256, 0, s>>>(nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d,
+                                                  n, chq, coff, hmask, qoff_d, bpre);
         HGX_CHECK_LAUNCH();
         ev.rec(3, s);
         spin_sync(s);
@@ -3096,14 +3161,46 @@ int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t
     QueryCombiner& c = g->qcomb;
     std::unique_lock<std::mutex> lk(c.mu);
     c.pending.push_back(&me);
+    // an exception below (allocation) must not leave this stack request queued for another caller
+    struct Unqueue {
+        QueryCombiner& c;
+        PackedReq* me;
+        std::unique_lock<std::mutex>& lk;
+        ~Unqueue() {
+            if (!lk.owns_lock()) lk.lock();
+            auto it = std::find(c.pending.begin(), c.pending.end(), me);
+            if (it != c.pending.end()) c.pending.erase(it);
+        }
+    } unqueue{c, &me, lk};
     while (!me.done) {
         if (c.busy) {
             c.cv.wait(lk);
             continue;
         }
         // run the queue's head group: FIFO, up to the query cap (a batch above the cap runs alone)
-        c.busy = true;
         std::vector<PackedReq*> grp;
+        grp.reserve(c.pending.size());   // the only allocation: before the combiner is marked busy
+        c.busy = true;
+        // whatever happens while the group runs, its members end done (an unserved one with an error),
+        // the combiner is released and the waiting callers are woken
+        struct Release {
+            QueryCombiner& c;
+            std::vector<PackedReq*>& grp;
+            std::unique_lock<std::mutex>& lk;
+            bool served = false;
+            ~Release() {
+                if (!lk.owns_lock()) lk.lock();
+                for (PackedReq* q : grp) {
+                    if (!served && q->rc == HGX_OK && !q->r) {
+                        q->rc = HGX_E_DEVICE;
+                        q->err = "hgx_pattern_batch_packed: the coalesced batch failed";
+                    }
+                    q->done = true;
+                }
+                c.busy = false;
+                c.cv.notify_all();
+            }
+        } release{c, grp, lk};
         int64_t tot = 0;
         while (!c.pending.empty() && (grp.empty() || tot + c.pending.front()->n <= g->q_coalesce_max)) {
             grp.push_back(c.pending.front());
@@ -3113,11 +3210,9 @@ int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t
         lk.unlock();
         serve_group(g, grp);
         lk.lock();
-        for (PackedReq* q : grp) q->done = true;
         c.batches += 1;
         c.requests += (int64_t)grp.size();
-        c.busy = false;
-        c.cv.notify_all();
+        release.served = true;
     }
     lk.unlock();
     if (me.rc != HGX_OK) {
@@ -3303,6 +3398,13 @@ int hgx_pattern_batch_set_into(hgx_graph* g, const hgx_query_set* qs, int64_t* o
         timing[1] = r.ms_match;
         timing[2] = r.bytes_match;
     }
+    HGX_API_END
+}
+
+int hgx_query_set_info(const hgx_query_set* qs, int32_t* n_queries) {
+    HGX_API_BEGIN
+    if (!qs || !n_queries) fail(HGX_E_INVALID, "hgx_query_set_info: null argument");
+    *n_queries = qs->n;
     HGX_API_END
 }
 

@@ -1141,6 +1141,43 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
     HGX_API_END
 }
 
+int hgx_seq_result_pairs_range(const hgx_seq_result* r, int64_t first, int64_t n, int32_t* links, int32_t* atoms,
+                               int32_t* dists, int64_t* n_out) {
+    HGX_API_BEGIN
+    if (!r || first < 0 || n < 0) fail(HGX_E_INVALID, "hgx_seq_result_pairs_range: bad argument");
+    const int64_t total = r->off.back();
+    const int64_t hi = std::min(total, first + std::min(n, total));
+    if (n_out) *n_out = std::max<int64_t>(hi - first, 0);
+    // copy the overlap of every segment with [first, hi)
+    auto put = [&](int64_t b, const Seg& s) {
+        const int64_t lo_ = std::max(b, first), hi_ = std::min(b + s.n, hi);
+        if (hi_ <= lo_) return;
+        const int64_t k = hi_ - lo_, so = lo_ - b, o = lo_ - first;
+        if (links) std::memcpy(links + o, s.link + so, sizeof(int32_t) * k);
+        if (atoms) std::memcpy(atoms + o, s.atom + so, sizeof(int32_t) * k);
+        if (dists) {
+            if (s.dist) std::memcpy(dists + o, s.dist + so, sizeof(int32_t) * k);
+            else std::fill(dists + o, dists + o + k, s.dist_c);
+        }
+    };
+    if (hi > first) {
+        // the first seed whose pairs reach past `first`
+        int32_t i0 = (int32_t)(std::upper_bound(r->off.begin(), r->off.end(), first) - r->off.begin()) - 1;
+        for (int32_t i = std::max(i0, 0); i < r->n_seeds && r->off[i] < hi; ++i) {
+            int64_t b = r->off[i];
+            if (r->lev_of[i] < 0) {
+                put(b, r->blk[i]);
+                continue;
+            }
+            for (const Seg& sg : r->lev.segs[(size_t)r->lev_of[i]]) {
+                put(b, sg);
+                b += sg.n;
+            }
+        }
+    }
+    HGX_API_END
+}
+
 int hgx_seq_result_stats(const hgx_seq_result* r, double* ms_total, double* traversed_edges) {
     HGX_API_BEGIN
     if (!r) fail(HGX_E_INVALID, "null result");

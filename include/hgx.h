@@ -214,6 +214,17 @@ int  hgx_set_option(hgx_graph *g, int32_t option, int64_t value);
  * The writer validates the rows like hgx_graph_create and replaces the file atomically. */
 int hgx_snapshot_write(const char *path, const hgx_graph_desc *desc, const uint8_t *handles,
                        int32_t handle_bytes);
+/* The same file written in pieces: begin writes the header and the row sections, handles appends
+ * n_ranks handles (rank order; call it until num_atoms handles are written, or never for
+ * handle_bytes 0), end writes the checksum and replaces the file atomically; abort (or a failed end)
+ * removes the partial file.  For exporters whose handle table does not fit one buffer (a Java byte[]
+ * stops at 2^31 bytes: 134M 16-byte UUIDs; config 4 has 300M atoms). */
+typedef struct hgx_snapshot_writer hgx_snapshot_writer;
+int  hgx_snapshot_writer_begin(const char *path, const hgx_graph_desc *desc, int32_t handle_bytes,
+                               hgx_snapshot_writer **out);
+int  hgx_snapshot_writer_handles(hgx_snapshot_writer *w, const uint8_t *handles, int64_t n_ranks);
+int  hgx_snapshot_writer_end(hgx_snapshot_writer *w);   /* frees w */
+void hgx_snapshot_writer_abort(hgx_snapshot_writer *w);
 /* Header fields without reading the sections (any output may be NULL). */
 int hgx_snapshot_info(const char *path, int64_t *num_atoms, int64_t *num_links, int64_t *num_pins,
                       int32_t *handle_bytes, int32_t *has_types);
@@ -221,6 +232,11 @@ int hgx_snapshot_info(const char *path, int64_t *num_atoms, int64_t *num_links, 
  * skips a section; link_type is zero-filled when the file has none). */
 int hgx_snapshot_read(const char *path, int32_t *link_atom, int64_t *tgt_off, int32_t *tgt_idx,
                       int32_t *link_type, uint8_t *handles);
+/* Handles of ranks [first_rank, first_rank + n) (n * handle_bytes bytes) from the file's handle table,
+ * for readers that cannot hold the whole table at once (a Java byte[] stops at 2^31 bytes: 134M
+ * 16-byte UUID handles).  verify = 1 also checks the whole file's checksum (once, on the first range);
+ * HGX_E_NOTFOUND when the file has no handle table, HGX_E_INVALID for ranks outside [0, num_atoms). */
+int hgx_snapshot_read_handles(const char *path, int64_t first_rank, int64_t n, int32_t verify, uint8_t *out);
 /* Map + verify the file and build the device snapshot (as hgx_graph_create). */
 int hgx_graph_open(const char *path, int32_t device, hgx_graph **out);
 /* D2H copy of the snapshot rows currently on the device (sizes from hgx_graph_info; num_pins =
@@ -252,6 +268,10 @@ int  hgx_bfs_result_counts(hgx_bfs_result *r, int64_t *counts);
 /* V_d of seed i, ascending atom ids; *n_out = |V_d| even when > cap. */
 int  hgx_bfs_result_visited(hgx_bfs_result *r, int32_t seed_index, int32_t depth,
                             int32_t *out, int64_t cap, int64_t *n_out);
+/* The same list from position first on: out[0, min(cap, *n_out - first)) = V_d[first, ...); *n_out = |V_d|
+ * (paged readers of sets larger than one Java array). */
+int  hgx_bfs_result_visited_range(hgx_bfs_result *r, int32_t seed_index, int32_t depth, int64_t first,
+                                  int32_t *out, int64_t cap, int64_t *n_out);
 /* isVisited after draining (C/algorithms/HGBreadthFirstTraversal.java:137-141):
  * *depth_out = distance of atom from seed i, or -1 when never reached. */
 int  hgx_bfs_result_depth_of(hgx_bfs_result *r, int32_t seed_index, int32_t atom, int32_t *depth_out);
@@ -273,6 +293,10 @@ int  hgx_seq_result_info(const hgx_seq_result *r, int32_t *n_seeds, int64_t *n_p
 int  hgx_seq_result_offsets(const hgx_seq_result *r, int64_t *offsets);
 /* links / atoms / dists: n_pairs entries each (any may be NULL). */
 int  hgx_seq_result_pairs(const hgx_seq_result *r, int32_t *links, int32_t *atoms, int32_t *dists);
+/* Pairs [first, first + n) of the flattened pair arrays (paged readers; n may run past the end: only
+ * the pairs that exist are copied, *n_out says how many). */
+int  hgx_seq_result_pairs_range(const hgx_seq_result *r, int64_t first, int64_t n, int32_t *links, int32_t *atoms,
+                                int32_t *dists, int64_t *n_out);
 /* device ms (timing enabled) and sum over seeds and expanded atoms of |inc(atom)|. */
 int  hgx_seq_result_stats(const hgx_seq_result *r, double *ms_total, double *traversed_edges);
 /* Which engine finished the seeds (HGX_OPT_SEQ_ENGINE): seeds done by the workgroup-per-seed engine /
@@ -301,7 +325,9 @@ int  hgx_pattern_batch_packed(hgx_graph *g, int32_t n, const int32_t *type, cons
  * set of compiled queries (the reference compiles a query once and executes it repeatedly,
  * TC/query/QueryCompilation.java:76-122), and the bench's config-3 step with its inputs resident in
  * HBM.  The set belongs to the device of g; it may be run on any graph or execution context of that
- * device.  Results as hgx_pattern_batch. */
+ * device.  Results as hgx_pattern_batch.  With HGX_OPT_QUERY_FLAT 0 or 1 (A/B paths) the set's error slot
+ * lives in the set itself, so one set must not run on two graphs / contexts at the same time there;
+ * the default single-pass path (2) keeps every per-run word in the running graph's scratch. */
 typedef struct hgx_query_set hgx_query_set;
 int  hgx_query_set_create(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off, const int32_t *inc,
                           const int32_t *has_ordered, const int64_t *pat_off, const int32_t *pat,
@@ -314,6 +340,8 @@ int  hgx_pattern_batch_set(hgx_graph *g, const hgx_query_set *qs, hgx_query_resu
  * ms of the match kernel, its algorithmic bytes (zeros unless hgx_set_timing is on). */
 int  hgx_pattern_batch_set_into(hgx_graph *g, const hgx_query_set *qs, int64_t *offsets, int32_t *ids, int64_t ids_cap,
                                 int64_t *n_ids, double *timing);
+/* The number of queries of a set (the size of a run's offsets is n_queries + 1). */
+int  hgx_query_set_info(const hgx_query_set *qs, int32_t *n_queries);
 void hgx_query_set_free(hgx_query_set *qs);
 /* The And shapes beyond {type, incident, orderedLink} (flat arrays, one call per batch).  Query q is
  *   And{ Or over types[type_off[q] .. type_off[q+1])        AtomTypeCondition (one type) or

@@ -330,6 +330,100 @@ JNIEXPORT jbyteArray JFN(snapshotHandles)(JNIEnv *e, jclass k, jstring path) {
     return out;
 }
 
+/* The file's checksum over every section (hgx_snapshot_read with no outputs maps and verifies). */
+JNIEXPORT void JFN(snapshotVerify)(JNIEnv *e, jclass k, jstring path) {
+    if (!check_not_null(e, path, "path")) return;
+    const char *p = (*e)->GetStringUTFChars(e, path, NULL);
+    if (!p) return;
+    int rc = hgx_snapshot_read(p, NULL, NULL, NULL, NULL, NULL);
+    (*e)->ReleaseStringUTFChars(e, path, p);
+    if (rc) throw_rc(e, rc);
+}
+
+/* Handles of ranks [first, first + n) (n * handle_bytes bytes): the reader of tables beyond one Java
+ * array (300M 16-byte handles = 4.8 GB); the caller verifies the file once with snapshotVerify. */
+JNIEXPORT jbyteArray JFN(snapshotHandlesRange)(JNIEnv *e, jclass k, jstring path, jlong first, jlong n) {
+    if (!check_not_null(e, path, "path")) return NULL;
+    if (first < 0 || n < 0) { throw_msg(e, "snapshotHandlesRange: negative first or n"); return NULL; }
+    const char *p = (*e)->GetStringUTFChars(e, path, NULL);
+    if (!p) return NULL;
+    int64_t A = 0;
+    int32_t hb = 0;
+    int rc = hgx_snapshot_info(p, &A, NULL, NULL, &hb, NULL), thrown = 0;
+    jbyteArray out = NULL;
+    if (!rc && hb <= 0) rc = HGX_E_NOTFOUND;
+    if (!rc && (first > A || n > A - first)) {
+        char m[200];
+        snprintf(m, sizeof m, "snapshotHandlesRange: ranks [%lld, %lld) outside [0, %lld)", (long long)first,
+                 (long long)(first + n), (long long)A);
+        throw_msg(e, m);
+        thrown = 1;
+    }
+    if (!rc && !thrown) {
+        const int64_t bytes = n * (int64_t)hb;
+        if (!fits_jarray(e, bytes, "snapshot handle range")) {
+            thrown = 1;
+        } else {
+            uint8_t *buf = (uint8_t *)malloc((size_t)(bytes > 0 ? bytes : 1));
+            rc = buf ? hgx_snapshot_read_handles(p, first, n, 0, buf) : HGX_E_NOMEM;
+            if (!rc) {
+                out = (*e)->NewByteArray(e, (jsize)bytes);
+                if (out && bytes) (*e)->SetByteArrayRegion(e, out, 0, (jsize)bytes, (const jbyte *)buf);
+            }
+            free(buf);
+        }
+    }
+    (*e)->ReleaseStringUTFChars(e, path, p);
+    if (rc && !thrown) throw_rc(e, rc);
+    return out;
+}
+
+/* Streaming writer (hgx_snapshot_writer_*): the rows at begin, the handle table in pieces of whole
+ * handles, end = checksum + atomic replace.  The exporter of a store larger than one Java array. */
+JNIEXPORT jlong JFN(snapshotWriterBegin)(JNIEnv *e, jclass k, jstring path, jlong numAtoms, jintArray linkAtom,
+                                         jlongArray tgtOff, jintArray tgtIdx, jintArray linkType, jint handleBytes) {
+    if (!check_not_null(e, path, "path")) return 0;
+    pin_t la = pin_int(e, linkAtom), off = pin_long(e, tgtOff), tg = pin_int(e, tgtIdx), ty = pin_int(e, linkType);
+    int ok = check_rows(e, &la, &off, &tg, &ty), rc = HGX_OK;
+    hgx_snapshot_writer *w = NULL;
+    const char *p = ok ? (*e)->GetStringUTFChars(e, path, NULL) : NULL;
+    if (ok && !p) ok = 0;
+    if (ok) {
+        hgx_graph_desc d = desc_of(numAtoms, &la, &off, &tg, &ty);
+        rc = hgx_snapshot_writer_begin(p, &d, handleBytes, &w);
+        (*e)->ReleaseStringUTFChars(e, path, p);
+    }
+    unpin(e, &la); unpin(e, &off); unpin(e, &tg); unpin(e, &ty);
+    if (ok && rc) throw_rc(e, rc);
+    return ok && !rc ? (jlong)(intptr_t)w : 0;
+}
+
+/* handles.length must be a whole number of handles (checked by the engine against num_atoms). */
+JNIEXPORT void JFN(snapshotWriterHandles)(JNIEnv *e, jclass k, jlong w, jbyteArray handles, jint handleBytes) {
+    if (!check_not_null(e, handles, "handles")) return;
+    if (handleBytes <= 0) { throw_msg(e, "snapshotWriterHandles: handleBytes <= 0"); return; }
+    pin_t hb = pin_byte(e, handles);
+    if (pin_failed(&hb)) return;
+    int rc = HGX_OK, ok = 1;
+    if (hb.n % handleBytes) {
+        throw_msg(e, "snapshotWriterHandles: not a whole number of handles");
+        ok = 0;
+    }
+    if (ok) rc = hgx_snapshot_writer_handles((hgx_snapshot_writer *)(intptr_t)w, (const uint8_t *)hb.p,
+                                             (int64_t)hb.n / handleBytes);
+    unpin(e, &hb);
+    if (ok && rc) throw_rc(e, rc);
+}
+
+JNIEXPORT void JFN(snapshotWriterEnd)(JNIEnv *e, jclass k, jlong w) {
+    int rc = hgx_snapshot_writer_end((hgx_snapshot_writer *)(intptr_t)w);
+    if (rc) throw_rc(e, rc);
+}
+
+JNIEXPORT void JFN(snapshotWriterAbort)(JNIEnv *e, jclass k, jlong w) {
+    hgx_snapshot_writer_abort((hgx_snapshot_writer *)(intptr_t)w);
+}
+
 /* ---- batched BFS ----------------------------------------------------------------------------- */
 
 static hgx_algen_opts opts_of(jint linkType, jboolean p, jboolean s, jboolean r, jboolean src) {
@@ -384,6 +478,21 @@ JNIEXPORT jintArray JFN(bfsVisited)(JNIEnv *e, jclass k, jlong r, jint seedIndex
     int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     rc = buf ? hgx_bfs_result_visited(res, seedIndex, depth, buf, n, &n) : HGX_E_NOMEM;
     jintArray out = rc ? NULL : new_ints(e, buf, n);
+    free(buf);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
+/* V_d[first, first + max) of seed seedIndex: the paged reader of sets beyond one Java array. */
+JNIEXPORT jintArray JFN(bfsVisitedRange)(JNIEnv *e, jclass k, jlong r, jint seedIndex, jint depth, jlong first,
+                                         jint max) {
+    if (first < 0 || max < 0) { throw_msg(e, "bfsVisitedRange: negative first or max"); return NULL; }
+    int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(max > 0 ? max : 1));
+    if (!buf) { throw_class(e, "java/lang/OutOfMemoryError", "visited page"); return NULL; }
+    int64_t n = 0;
+    int rc = hgx_bfs_result_visited_range((hgx_bfs_result *)(intptr_t)r, seedIndex, depth, first, buf, max, &n);
+    const int64_t got = n > first ? (n - first < max ? n - first : max) : 0;
+    jintArray out = rc ? NULL : new_ints(e, buf, got);
     free(buf);
     if (rc) throw_rc(e, rc);
     return out;
@@ -448,6 +557,21 @@ JNIEXPORT jintArray JFN(seqAtoms)(JNIEnv *e, jclass k, jlong s) { return seq_col
 JNIEXPORT jintArray JFN(seqDists)(JNIEnv *e, jclass k, jlong s) { return seq_column(e, s, 2); }
 JNIEXPORT void JFN(seqFree)(JNIEnv *e, jclass k, jlong s) { hgx_seq_result_free((hgx_seq_result *)(intptr_t)s); }
 
+/* Pairs [first, first + max) of one column (0 links, 1 atoms, 2 distances): the paged reader of
+ * sequences beyond one Java array. */
+JNIEXPORT jintArray JFN(seqRange)(JNIEnv *e, jclass k, jlong sq, jint which, jlong first, jint max) {
+    if (first < 0 || max < 0 || which < 0 || which > 2) { throw_msg(e, "seqRange: bad argument"); return NULL; }
+    int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(max > 0 ? max : 1));
+    if (!buf) { throw_class(e, "java/lang/OutOfMemoryError", "sequence page"); return NULL; }
+    int64_t got = 0;
+    int rc = hgx_seq_result_pairs_range((const hgx_seq_result *)(intptr_t)sq, first, max, which == 0 ? buf : NULL,
+                                        which == 1 ? buf : NULL, which == 2 ? buf : NULL, &got);
+    jintArray out = rc ? NULL : new_ints(e, buf, got);
+    free(buf);
+    if (rc) throw_rc(e, rc);
+    return out;
+}
+
 /* ---- conjunctive pattern batches ------------------------------------------------------------- */
 
 /* The packed batch: n = type.length queries, incOff / patOff of n+1 entries into inc / pat,
@@ -502,9 +626,12 @@ JNIEXPORT void JFN(querySetFree)(JNIEnv *e, jclass k, jlong set) { hgx_query_set
  * number of hits (a larger ids array and a second call when it exceeds ids.length). */
 JNIEXPORT jlong JFN(patternBatchSetInto)(JNIEnv *e, jclass k, jlong g, jlong set, jlongArray offsets, jintArray ids) {
     if (!check_not_null(e, offsets, "offsets")) return 0;
+    int32_t nq = 0;   /* the engine writes nq + 1 offsets: a shorter array is refused before the call */
+    int rc = hgx_query_set_info((const hgx_query_set *)(intptr_t)set, &nq);
+    if (rc) { throw_rc(e, rc); return 0; }
     pin_t off = pin_long(e, offsets), id = pin_int(e, ids);
     int64_t n_ids = 0;
-    int rc = HGX_OK, ok = !pin_failed(&off) && !pin_failed(&id);
+    int ok = !pin_failed(&off) && !pin_failed(&id) && check_len(e, &off, (int64_t)nq + 1, "offsets");
     if (ok)
         rc = hgx_pattern_batch_set_into((hgx_graph *)(intptr_t)g, (const hgx_query_set *)(intptr_t)set,
                                         (int64_t *)off.p, (int32_t *)id.p, (int64_t)id.n, &n_ids, NULL);
@@ -761,6 +888,14 @@ JNIEXPORT jarray JFN(seqStats)(JNIEnv *e, jclass k, jlong sq) {
     int rc = hgx_seq_result_stats((const hgx_seq_result *)(intptr_t)sq, &v[0], &v[1]);
     if (rc) { throw_rc(e, rc); return NULL; }
     return new_doubles(e, v, 2);
+}
+
+JNIEXPORT jlongArray JFN(seqEngineStats)(JNIEnv *e, jclass k, jlong sq) {
+    int32_t nb = 0, nl = 0;
+    int rc = hgx_seq_result_engine_stats((const hgx_seq_result *)(intptr_t)sq, &nb, &nl, NULL, NULL);
+    if (rc) { throw_rc(e, rc); return NULL; }
+    int64_t v[2] = {nb, nl};
+    return new_longs(e, v, 2);
 }
 
 JNIEXPORT jarray JFN(queryMs)(JNIEnv *e, jclass k, jlong q) {

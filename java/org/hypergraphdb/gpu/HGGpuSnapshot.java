@@ -127,10 +127,19 @@ public final class HGGpuSnapshot implements AutoCloseable
         int hb = (int)info[3];
         if (hb <= 0)
             throw new HGException("hgcsr file " + path + " has no handle table");
-        byte[] table = Hgx.snapshotHandles(path);
-        for (int r = 0; r < info[0]; r++)
-            s.appendRank(graph.getHandleFactory().makeHandle(table, r * hb));
-        s.orderedPrefix = (int)info[0];
+        // the handle table by ranges (a config-4 store: 300M 16-byte handles = 4.8 GB, beyond one
+        // byte[]); the whole file's checksum is verified once first
+        Hgx.snapshotVerify(path);
+        final long A = info[0];
+        final long step = Math.max(1, TABLE_CHUNK_BYTES / hb);
+        for (long r0 = 0; r0 < A; r0 += step)
+        {
+            long n = Math.min(step, A - r0);
+            byte[] table = Hgx.snapshotHandlesRange(path, r0, n);
+            for (int k = 0; k < n; k++)
+                s.appendRank(graph.getHandleFactory().makeHandle(table, k * hb));
+        }
+        s.orderedPrefix = (int)A;
         s.g = Hgx.graphOpen(path, device);
         for (int r = 0; r < s.byRank.size(); r++)                 // type keys of the stored links
         {
@@ -145,12 +154,33 @@ public final class HGGpuSnapshot implements AutoCloseable
     public synchronized void save(String path)
     {
         Rows r = rowsOf(byRank);
-        int hb = byRank.isEmpty() ? 0 : byRank.get(0).toByteArray().length;
-        byte[] table = new byte[byRank.size() * hb];
-        for (int i = 0; i < byRank.size(); i++)
-            System.arraycopy(byRank.get(i).toByteArray(), 0, table, i * hb, hb);
-        Hgx.snapshotWrite(path, byRank.size(), r.linkAtom, r.tgtOff, r.tgtIdx, r.linkType, table, hb);
+        final int hb = byRank.isEmpty() ? 0 : byRank.get(0).toByteArray().length;
+        // streamed: the rows, then the handle table in pieces of TABLE_CHUNK_BYTES (long arithmetic: the
+        // table of a 300M-atom store is 4.8 GB, beyond one byte[] and beyond int byte offsets)
+        long w = Hgx.snapshotWriterBegin(path, byRank.size(), r.linkAtom, r.tgtOff, r.tgtIdx, r.linkType, hb);
+        boolean ended = false;   // end frees the writer whether or not it succeeds
+        try
+        {
+            final int per = hb > 0 ? (int)Math.max(1, TABLE_CHUNK_BYTES / hb) : 0;
+            for (int i0 = 0; hb > 0 && i0 < byRank.size(); i0 += per)
+            {
+                int n = Math.min(per, byRank.size() - i0);
+                byte[] chunk = new byte[n * hb];   // n * hb <= TABLE_CHUNK_BYTES
+                for (int k = 0; k < n; k++)
+                    System.arraycopy(byRank.get(i0 + k).toByteArray(), 0, chunk, k * hb, hb);
+                Hgx.snapshotWriterHandles(w, chunk, hb);
+            }
+            ended = true;
+            Hgx.snapshotWriterEnd(w);
+        }
+        finally
+        {
+            if (!ended) Hgx.snapshotWriterAbort(w);   // removes the partial file
+        }
     }
+
+    /** Bytes of handle table per native read / write (well below the 2^31 limit of one byte[]). */
+    static final long TABLE_CHUNK_BYTES = 1L << 28;
 
     private void register()
     {
@@ -211,6 +241,9 @@ public final class HGGpuSnapshot implements AutoCloseable
             targets.add(t);
             pins += t.length;
         }
+        if (pins > Integer.MAX_VALUE - 8)   // one int[] of targets: 2^31 pins (config 4 has 1.0e9)
+            throw new HGException("snapshot: " + pins + " link targets exceed one Java array; export it with "
+                                  + "the native exporter (hgx_snapshot_writer_*) instead");
         Rows r = new Rows();
         r.linkAtom = new int[la.size()];
         r.linkType = new int[la.size()];

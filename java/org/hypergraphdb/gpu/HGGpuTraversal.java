@@ -101,6 +101,9 @@ public class HGGpuTraversal implements HGTraversal
                           d.isReverseOrder() ? 1 : 0, d.isReturnSource() ? 1 : 0};
     }
 
+    /** Entries per native read of a large result (sequence columns, visited sets). */
+    static final int PAGE = 1 << 24;
+
     private static int depth(int maxDistance) { return maxDistance == Integer.MAX_VALUE ? Hgx.UNBOUNDED : maxDistance; }
 
     private void init()
@@ -199,14 +202,19 @@ public class HGGpuTraversal implements HGTraversal
         }
         try
         {
+            // the pairs of all starts may exceed one Java array (2^31): read each start's atoms by pages
+            // of the flattened sequence (seqRange), never the whole column at once
             long[] off = Hgx.seqOffsets(s);
-            int[] atoms = Hgx.seqAtoms(s);
             HGHandle[][] out = new HGHandle[starts.length][];
             for (int i = 0; i < starts.length; i++)
             {
-                HGHandle[] row = new HGHandle[(int)(off[i + 1] - off[i])];
-                for (int k = 0; k < row.length; k++)
-                    row[k] = snap.handle(atoms[(int)off[i] + k]);   // FIFO order: no re-sort
+                HGHandle[] row = new HGHandle[(int)(off[i + 1] - off[i])];   // one traversal <= num_atoms < 2^31
+                for (int k = 0; k < row.length; )
+                {
+                    int[] page = Hgx.seqRange(s, 1, off[i] + k, Math.min(row.length - k, PAGE));
+                    for (int a : page)
+                        row[k++] = snap.handle(a);   // FIFO order: no re-sort
+                }
                 out[i] = row;
             }
             return out;
@@ -249,7 +257,17 @@ public class HGGpuTraversal implements HGTraversal
             {
                 HGHandle[][] byDepth = new HGHandle[levels][];
                 for (int d = 0; d < levels; d++)
-                    byDepth[d] = snap.handles(Hgx.bfsVisited(r, i, d));
+                {
+                    // paged: the first page also reports nothing about the total, so read until short
+                    List<HGHandle> set = new ArrayList<HGHandle>();
+                    for (long first = 0; ; first += PAGE)
+                    {
+                        int[] page = Hgx.bfsVisitedRange(r, i, d, first, PAGE);
+                        for (HGHandle h : snap.handles(page)) set.add(h);
+                        if (page.length < PAGE) break;
+                    }
+                    byDepth[d] = set.toArray(new HGHandle[set.size()]);
+                }
                 out.add(byDepth);
             }
             return out;

@@ -18,7 +18,8 @@ final class Hgx
     static final int NO_TYPE = -1, ANY_HANDLE = -1, UNBOUNDED = -1;
     static final int OPT_BFS_FLAGS = 1, OPT_SEQ_BUDGET = 2, OPT_RANKS_ORDERED = 3, OPT_PART_SERIAL = 4;
     static final int OPT_QUERY_FUSED = 5, OPT_QUERY_INLINE = 6, OPT_PUSH_BATCH = 7, OPT_PART_EXCHANGE = 8,
-                     OPT_QUERY_FLAT = 9, OPT_CODED = 10, OPT_QUERY_COALESCE = 11, OPT_PUSH_INLINE = 12;   // include/hgx.h
+                     OPT_QUERY_FLAT = 9, OPT_CODED = 10, OPT_QUERY_COALESCE = 11, OPT_PUSH_INLINE = 12,
+                     OPT_SEQ_ENGINE = 13;   // include/hgx.h
 
     // ---- snapshot (hgx_graph_create / open / destroy / update / info) ---------------------------
     static native long graphCreate(long numAtoms, int[] linkAtom, long[] tgtOff, int[] tgtIdx, int[] linkType,
@@ -36,6 +37,14 @@ final class Hgx
                                      int[] linkType, byte[] handles, int handleBytes);
     static native long[] snapshotInfo(String path);             // {num_atoms, num_links, num_pins, handle_bytes, has_types}
     static native byte[] snapshotHandles(String path);          // rank-ordered handle bytes (or null)
+    static native void snapshotVerify(String path);             // whole-file checksum (throws on mismatch)
+    static native byte[] snapshotHandlesRange(String path, long first, long n);   // ranks [first, first + n)
+    // streaming writer (hgx_snapshot_writer_*): handle tables beyond one byte[]
+    static native long snapshotWriterBegin(String path, long numAtoms, int[] linkAtom, long[] tgtOff, int[] tgtIdx,
+                                           int[] linkType, int handleBytes);
+    static native void snapshotWriterHandles(long w, byte[] handles, int handleBytes);
+    static native void snapshotWriterEnd(long w);               // checksum + atomic replace; frees w
+    static native void snapshotWriterAbort(long w);
 
     // ---- batched BFS (hgx_bfs_batch + readers) ----------------------------------------------
     static native long bfsBatch(long g, int[] seeds, int maxDepth, int linkType, boolean preceding,
@@ -43,6 +52,7 @@ final class Hgx
     static native int[] bfsInfo(long r);                        // {n_seeds, n_levels}
     static native long[] bfsCounts(long r);                     // [n_seeds * n_levels]
     static native int[] bfsVisited(long r, int seedIndex, int depth);
+    static native int[] bfsVisitedRange(long r, int seedIndex, int depth, long first, int max);   // paged
     static native int bfsDepthOf(long r, int seedIndex, int atom);
     static native void bfsFree(long r);
 
@@ -54,6 +64,8 @@ final class Hgx
     static native int[] seqAtoms(long s);
     static native int[] seqDists(long s);
     static native void seqFree(long s);
+    static native int[] seqRange(long s, int which, long first, int max);   // 0 links / 1 atoms / 2 dists, paged
+    static native long[] seqEngineStats(long s);                // {workgroup seeds, level-synchronous seeds}
 
     // ---- conjunctive pattern batches (hgx_pattern_batch_packed / _ext + readers) -------------
     static native long patternBatch(long g, int[] type, long[] incOff, int[] inc, int[] hasOrdered, long[] patOff,

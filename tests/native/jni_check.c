@@ -42,6 +42,12 @@ jlong JN(graphCreate)(JNIEnv *, jclass, jlong, jintArray, jlongArray, jintArray,
 void JN(snapshotWrite)(JNIEnv *, jclass, jstring, jlong, jintArray, jlongArray, jintArray, jintArray, jbyteArray, jint);
 jlongArray JN(snapshotInfo)(JNIEnv *, jclass, jstring);
 jbyteArray JN(snapshotHandles)(JNIEnv *, jclass, jstring);
+void JN(snapshotVerify)(JNIEnv *, jclass, jstring);
+jbyteArray JN(snapshotHandlesRange)(JNIEnv *, jclass, jstring, jlong, jlong);
+jlong JN(snapshotWriterBegin)(JNIEnv *, jclass, jstring, jlong, jintArray, jlongArray, jintArray, jintArray, jint);
+void JN(snapshotWriterHandles)(JNIEnv *, jclass, jlong, jbyteArray, jint);
+void JN(snapshotWriterEnd)(JNIEnv *, jclass, jlong);
+void JN(snapshotWriterAbort)(JNIEnv *, jclass, jlong);
 jintArray JN(partitionPlan)(JNIEnv *, jclass, jlong, jintArray, jlongArray, jintArray, jintArray, jint);
 jlong JN(shardBuild)(JNIEnv *, jclass, jlong, jintArray, jlongArray, jintArray, jintArray, jint, jint, jintArray);
 void JN(shardFree)(JNIEnv *, jclass, jlong);
@@ -233,11 +239,107 @@ static void check_argument_errors(void) {
     CHECK(strcmp(cls, "java/lang/IllegalArgumentException") == 0, "patternBatch threw %s", cls);
 }
 
+/* Handle tables beyond one Java array: a sparse 300M-atom file with 16-byte handles (4.8 GB of table,
+ * config 4's size) read by ranges, the whole-table reader refused; the streamed writer in pieces whose
+ * sizes carry partial checksum words, identical to snapshotWrite's file, and its refusals. */
+static void check_large_tables(const char *dir) {
+    char path[512];
+    snprintf(path, sizeof path, "%s/jni_check_big.hgcsr", dir);
+    const int64_t BA = 300000000, HB = 16;
+    unsigned char hdr[64] = {0};
+    memcpy(hdr, "HGXCSR1", 8);
+    const uint32_t ver = 2, flags = 2, hb32 = (uint32_t)HB;
+    memcpy(hdr + 8, &ver, 4);
+    memcpy(hdr + 12, &flags, 4);
+    memcpy(hdr + 16, &BA, 8);
+    memcpy(hdr + 40, &hb32, 4);
+    FILE *f = fopen(path, "wb");
+    CHECK(f != NULL, "create %s", path);
+    if (!f) return;
+    fwrite(hdr, 1, 64, f);
+    const long total = (long)(((128 + BA * HB + 63) / 64) * 64);   /* handles at 128 (hgx_file.hip layout) */
+    CHECK(fseek(f, total - 1, SEEK_SET) == 0 && fputc(0, f) == 0, "extend the file (sparse)");
+    fclose(f);
+    jstring p = (jstring)fj_new_string(E, path);
+    JN(snapshotHandles)(E, NULL, p);
+    const char *cls = settle("snapshotHandles(4.8 GB)");
+    CHECK(strcmp(cls, "java/lang/UnsupportedOperationException") == 0, "whole 4.8 GB table threw '%s'", cls);
+    const int64_t firsts[3] = {0, BA / 2, BA - 1000};
+    for (int i = 0; i < 3; i++) {
+        jbyteArray r = JN(snapshotHandlesRange)(E, NULL, p, firsts[i], 1000);
+        cls = settle("snapshotHandlesRange");
+        CHECK(cls[0] == 0 && r && fj_length(r) == 1000 * HB, "range at %lld threw '%s'", (long long)firsts[i], cls);
+    }
+    JN(snapshotHandlesRange)(E, NULL, p, BA - 10, 11);
+    cls = settle("snapshotHandlesRange(past the end)");
+    CHECK(strcmp(cls, "java/lang/IllegalArgumentException") == 0, "range past the end threw '%s'", cls);
+    JN(snapshotVerify)(E, NULL, p);   /* the synthetic header carries no checksum */
+    cls = settle("snapshotVerify(synthetic)");
+    CHECK(strcmp(cls, "org/hypergraphdb/HGException") == 0, "verify threw '%s'", cls);
+    remove(path);
+    /* streamed writer == snapshotWrite, pieces of 1, 5 and A - 6 four-byte handles */
+    char ref[512], out[512];
+    snprintf(ref, sizeof ref, "%s/jni_check_ref.hgcsr", dir);
+    snprintf(out, sizeof out, "%s/jni_check_stream.hgcsr", dir);
+    int8_t handles[A * 4];
+    for (int i = 0; i < A * 4; i++) handles[i] = (int8_t)(i * 11 + 1);
+    jstring pr = (jstring)fj_new_string(E, ref), po = (jstring)fj_new_string(E, out);
+    JN(snapshotWrite)(E, NULL, pr, A, ints(LA, M), longs(OFF, M + 1), ints(TG, 16), ints(TY, M),
+                      (jbyteArray)fj_new_array(E, K_BYTE, handles, A * 4), 4);
+    settle("snapshotWrite(ref)");
+    jlong w = JN(snapshotWriterBegin)(E, NULL, po, A, ints(LA, M), longs(OFF, M + 1), ints(TG, 16), ints(TY, M), 4);
+    cls = settle("snapshotWriterBegin");
+    CHECK(cls[0] == 0 && w != 0, "writer begin threw '%s'", cls);
+    const int cuts[4] = {0, 1, 6, A};
+    for (int i = 0; i < 3; i++) {
+        JN(snapshotWriterHandles)(E, NULL, w, (jbyteArray)fj_new_array(E, K_BYTE, handles + 4 * cuts[i],
+                                                                    4 * (cuts[i + 1] - cuts[i])), 4);
+        cls = settle("snapshotWriterHandles");
+        CHECK(cls[0] == 0, "writer piece %d threw '%s'", i, cls);
+    }
+    JN(snapshotWriterEnd)(E, NULL, w);
+    settle("snapshotWriterEnd");
+    FILE *a = fopen(ref, "rb"), *b = fopen(out, "rb");
+    CHECK(a && b, "open written files");
+    if (a && b) {
+        int same = 1, ca, cb;
+        do {
+            ca = fgetc(a);
+            cb = fgetc(b);
+            same &= ca == cb;
+        } while (ca != EOF && cb != EOF);
+        CHECK(same, "streamed file differs from snapshotWrite's");
+    }
+    if (a) fclose(a);
+    if (b) fclose(b);
+    JN(snapshotVerify)(E, NULL, po);
+    cls = settle("snapshotVerify(streamed)");
+    CHECK(cls[0] == 0, "verify of the streamed file threw '%s'", cls);
+    /* a short table: end refuses (and frees the writer); half a handle: refused; abort */
+    w = JN(snapshotWriterBegin)(E, NULL, po, A, ints(LA, M), longs(OFF, M + 1), ints(TG, 16), ints(TY, M), 4);
+    settle("snapshotWriterBegin(2)");
+    JN(snapshotWriterHandles)(E, NULL, w, (jbyteArray)fj_new_array(E, K_BYTE, handles, 6), 4);
+    cls = settle("snapshotWriterHandles(half a handle)");
+    CHECK(strcmp(cls, "java/lang/IllegalArgumentException") == 0, "half a handle threw '%s'", cls);
+    JN(snapshotWriterHandles)(E, NULL, w, (jbyteArray)fj_new_array(E, K_BYTE, handles, 8), 4);
+    settle("snapshotWriterHandles(2 of A)");
+    JN(snapshotWriterEnd)(E, NULL, w);
+    cls = settle("snapshotWriterEnd(short)");
+    CHECK(strcmp(cls, "org/hypergraphdb/HGException") == 0, "short table end threw '%s'", cls);
+    w = JN(snapshotWriterBegin)(E, NULL, po, A, ints(LA, M), longs(OFF, M + 1), ints(TG, 16), ints(TY, M), 4);
+    settle("snapshotWriterBegin(3)");
+    JN(snapshotWriterAbort)(E, NULL, w);
+    settle("snapshotWriterAbort");
+    remove(ref);
+    remove(out);
+}
+
 int main(int argc, char **argv) {
     const char *dir = argc > 1 ? argv[1] : ".";
     E = fj_env_new();
     check_version_and_nulls();
     check_snapshot_file(dir);
+    check_large_tables(dir);
     check_partition();
     check_argument_errors();
     fj_env_free(E);

@@ -6,7 +6,7 @@ pinning and pending exceptions, and checks the JNI discipline on every call.  Th
 HGGpuSnapshot / HGGpuTraversal / GpuAndToQuery / GpuTraversalToQuery take (java/org/hypergraphdb/gpu):
 the results are compared with the C oracle (oracle/hgx_oracle.c, the restatement of
 HGBreadthFirstTraversal / DefaultALGenerator / AndToQuery), bit-exact.  The last test checks that
-all 58 natives were called."""
+all 67 natives were called."""
 import numpy as np
 import pytest
 
@@ -95,6 +95,9 @@ def test_bfs_batch_every_mode_vs_oracle(jni, graph, gh, mi):
                 assert counts[i, d] == len(exp), (i, d)
                 if i % 9 == 0:
                     assert np.array_equal(jni.bfsVisited(r, i, d), exp), (i, d)
+                    # paged reads (bfsVisitedRange): pages of 3 reassemble the set
+                    pages = [jni.bfsVisitedRange(r, i, d, f, 3) for f in range(0, len(exp) + 3, 3)]
+                    assert np.array_equal(np.concatenate(pages), exp), (i, d)
             if i % 9 == 0:
                 for d, lvl in enumerate(lv):
                     for a in lvl[:3]:
@@ -147,6 +150,12 @@ def test_bfs_sequence_order_exact(jni, graph, gh):
                 sl = slice(int(off[i]), int(off[i + 1]))
                 assert np.array_equal(atoms[sl], a) and np.array_equal(links[sl], l) and np.array_equal(dists[sl], d)
             assert jni.seqStats(s)[1] == float(trav)
+            # paged column reads (seqRange) across seed boundaries, and the engine split
+            for which, col in ((0, links), (1, atoms), (2, dists)):
+                got = np.concatenate([jni.seqRange(s, which, f, 5) for f in range(0, len(col) + 5, 5)])
+                assert np.array_equal(got, col), which
+            nb, nl = jni.seqEngineStats(s).tolist()
+            assert nb + nl == len(seeds)
         finally:
             jni.seqFree(s)
 
@@ -225,6 +234,13 @@ def test_pattern_batches_vs_oracle(jni, graph, gh):
         assert off[-1] == total and (short == -1).all()
         with pytest.raises(JavaException):
             jni.patternBatchSetInto(gh, qset, None, ids)
+        # an offsets array shorter than the set's n + 1 is refused before the engine writes into it
+        # (the engine always writes n + 1 offsets)
+        guard = np.full(len(exp) + 8, -7, np.int64)
+        with pytest.raises(JavaException) as ei:
+            jni.patternBatchSetInto(gh, qset, guard[: len(exp)], ids)
+        assert ei.value.cls == "java.lang.IllegalArgumentException"
+        assert (guard == -7).all()
     finally:
         jni.querySetFree(qset)
     # no incidence anchor: the engine refuses, the Java side keeps AndToQuery
@@ -288,6 +304,17 @@ def test_snapshot_file_open_update(jni, graph, tmp_path):
     jni.snapshotWrite(p, *rows(g), handles, 4)
     assert jni.snapshotInfo(p).tolist() == [A, len(g["link_atom"]), len(g["tgt_idx"]), 4, 1]
     assert np.array_equal(jni.snapshotHandles(p), handles)
+    # the streamed writer (the exporter of tables beyond one byte[]) and the ranged reader
+    p2 = str(tmp_path / "g2.hgcsr")
+    w = jni.snapshotWriterBegin(p2, *rows(g), 4)
+    jni.snapshotWriterHandles(w, handles[:4 * 5].copy(), 4)
+    jni.snapshotWriterHandles(w, handles[4 * 5:].copy(), 4)
+    jni.snapshotWriterEnd(w)
+    assert open(p2, "rb").read() == open(p, "rb").read()
+    jni.snapshotVerify(p2)
+    assert np.array_equal(jni.snapshotHandlesRange(p2, 3, 9), handles[12:48])
+    w = jni.snapshotWriterBegin(str(tmp_path / "g3.hgcsr"), *rows(g), 4)
+    jni.snapshotWriterAbort(w)
     h = jni.graphOpen(p, 0)
     try:
         assert jni.graphInfo(h).tolist()[:2] == [A, len(g["link_atom"])]

@@ -586,3 +586,38 @@ def test_placement_query_ranges_at_block_starts():
     aligned = [q for q in range(1, n) if anchors[q] % 98 and anchors[q - 1] % 98 == 0 and r2.offsets[q] > 0
                and r2.offsets[q] % block == 0]
     assert len(aligned) >= 6, aligned
+
+
+def test_large_candidate_batch_placement_prefix():
+    """A batch whose candidate space spans more than 256 placement blocks (> 16384 chunks of 64
+    candidates) takes the scanned block prefix in the placement (hgx_q_place_bsum / _bscan) instead of
+    every block summing all chunks before it (quadratic); results equal the flat path's (1)
+    and the oracle's for a sample, and the timing of both paths is printed for the crossover."""
+    import time
+    from hypergraphdb_amd import _lib
+    from hypergraphdb_amd.query import pattern_batch_arrays
+    from hypergraphdb_amd import synth
+    g = synth.hypergraph(2000, 400000, 2, 5, 1.6, 2, seed=11)
+    snap, orc = snapshot(g), oracle(g)
+    deg = np.bincount(g["tgt_idx"], minlength=g["num_atoms"])
+    hubs = np.argsort(-deg)[:64].astype(np.int32)
+    rng = np.random.default_rng(5)
+    nq = 6000
+    anchors = hubs[rng.integers(0, len(hubs), nq)]
+    types = np.where(rng.random(nq) < 0.5, -1, rng.integers(0, 2, nq)).astype(np.int32)
+    args = (types, np.arange(nq + 1, dtype=np.int64), anchors, np.zeros(nq, np.int32),
+            np.zeros(nq + 1, np.int64), np.zeros(0, np.int32))
+    assert int(sum(deg[anchors])) > 64 * 64 * 260   # > 260 placement blocks of candidates
+    out = {}
+    for flat in (2, 1):
+        snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
+        pattern_batch_arrays(snap, *args)
+        t0 = time.perf_counter()
+        r = pattern_batch_arrays(snap, *args)
+        out[flat] = (r, time.perf_counter() - t0)
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
+    print(f"large batch: single-pass {out[2][1] * 1e3:.3f} ms, flat {out[1][1] * 1e3:.3f} ms")
+    a, b = out[2][0], out[1][0]
+    assert np.array_equal(a.offsets, b.offsets) and np.array_equal(a.ids, b.ids)
+    for q in range(0, nq, 97):
+        assert a[q].tolist() == orc.and_query(int(types[q]), [int(anchors[q])], None).tolist(), q

@@ -28,9 +28,9 @@ def small_graph(seed=3, N=300, M=500):
 
 
 def test_every_native_binds(jni):
-    """Hgx.java's 58 declarations resolve to symbols of the shim with the declared arity."""
+    """Hgx.java's 67 declarations resolve to symbols of the shim with the declared arity."""
     nat = java_natives()
-    assert len(nat) == 58
+    assert len(nat) == 67
     for name in nat:
         jni._fn(name)
 
@@ -72,6 +72,93 @@ def test_snapshot_file_roundtrip(jni, tmp_path):
     with pytest.raises(JavaException) as ei:
         jni.snapshotInfo(str(tmp_path / "missing.hgcsr"))
     assert ei.value.cls == "org.hypergraphdb.HGException"
+
+
+def test_snapshot_ranged_handles_and_streamed_writer(jni, tmp_path):
+    """The readers / writer of handle tables beyond one Java array: snapshotHandlesRange returns any
+    slice of the table (after one snapshotVerify), snapshotWriter* streams the table in pieces (odd
+    piece sizes of 4-byte handles carry partial checksum words across calls) and writes a file
+    byte-identical to snapshotWrite's; a short table, an abort or ranks outside the table are refused
+    and leave no file behind."""
+    g = small_graph()
+    A = g["num_atoms"]
+    rows = (g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
+    handles = ((np.arange(A * 4) * 13 + 5) % 251).astype(np.int8)
+    ref = str(tmp_path / "ref.hgcsr")
+    jni.snapshotWrite(ref, A, *rows, handles, 4)
+    jni.snapshotVerify(ref)
+    for first, n in ((0, A), (0, 1), (7, 100), (A - 3, 3), (A, 0)):
+        assert np.array_equal(jni.snapshotHandlesRange(ref, first, n), handles[4 * first:4 * (first + n)])
+    for first, n in ((A - 2, 3), (A + 1, 0), (-1, 2)):
+        with pytest.raises(JavaException) as ei:
+            jni.snapshotHandlesRange(ref, first, n)
+        assert ei.value.cls == "java.lang.IllegalArgumentException"
+    out = str(tmp_path / "streamed.hgcsr")
+    w = jni.snapshotWriterBegin(out, A, *rows, 4)
+    cuts = [0, 1, 4, 11, A // 2, A]
+    for a, b in zip(cuts, cuts[1:]):
+        jni.snapshotWriterHandles(w, handles[4 * a:4 * b].copy(), 4)
+    jni.snapshotWriterEnd(w)
+    assert open(out, "rb").read() == open(ref, "rb").read()
+    jni.snapshotVerify(out)
+    # a table one handle short: end refuses and removes the partial file
+    bad = str(tmp_path / "short.hgcsr")
+    w = jni.snapshotWriterBegin(bad, A, *rows, 4)
+    jni.snapshotWriterHandles(w, handles[: 4 * (A - 1)].copy(), 4)
+    with pytest.raises(JavaException):
+        jni.snapshotWriterEnd(w)
+    assert not os.path.exists(bad) and not os.path.exists(bad + ".tmp")
+    w = jni.snapshotWriterBegin(bad, A, *rows, 4)
+    with pytest.raises(JavaException):   # more handles than atoms
+        jni.snapshotWriterHandles(w, np.zeros(4 * (A + 1), np.int8), 4)
+    with pytest.raises(JavaException):   # not a whole number of handles
+        jni.snapshotWriterHandles(w, np.zeros(6, np.int8), 4)
+    jni.snapshotWriterAbort(w)
+    assert not os.path.exists(bad) and not os.path.exists(bad + ".tmp")
+    # a corrupted byte fails the verification but not the unverified ranged read
+    data = bytearray(open(ref, "rb").read())
+    data[-1] ^= 0x5A
+    cor = str(tmp_path / "corrupt.hgcsr")
+    open(cor, "wb").write(bytes(data))
+    with pytest.raises(JavaException):
+        jni.snapshotVerify(cor)
+    assert len(jni.snapshotHandlesRange(cor, 0, 2)) == 8
+
+
+def synthetic_header_file(path, A, hb):
+    """A sparse .hgcsr of A atoms, no links and an all-zero handle table of A * hb bytes (header only
+    written; the checksum field is left 0, so only unverified readers accept it)."""
+    import struct
+    hdr = struct.pack("<8sIIqqqIIQ8s", b"HGXCSR1\0", 2, 2, A, 0, 0, hb, 0, 0, b"\0" * 8)
+    assert len(hdr) == 64
+    tgt_off_at = 64                      # link_atom [0] at 64, tgt_off [1 x i64] at 64
+    tbl_at = ((tgt_off_at + 8 + 63) // 64) * 64 + 0   # tgt_idx [0], link_type absent, then handles
+    total = ((tbl_at + A * hb + 63) // 64) * 64
+    with open(path, "wb") as f:
+        f.write(hdr)
+        f.truncate(total)                # sparse: no page of the table is ever written
+    return tbl_at, total
+
+
+def test_ranged_reader_of_a_300m_atom_table(jni, tmp_path):
+    """A 300M-atom store with 16-byte UUID handles (4.8 GB of table, config 4's size): the whole-table
+    reader throws cleanly (beyond one Java array), the ranged reader returns any slice of it."""
+    A, hb = 300_000_000, 16
+    p = str(tmp_path / "big.hgcsr")
+    synthetic_header_file(p, A, hb)
+    assert jni.snapshotInfo(p).tolist() == [A, 0, 0, hb, 0]
+    with pytest.raises(JavaException) as ei:
+        jni.snapshotHandles(p)
+    assert ei.value.cls == "java.lang.UnsupportedOperationException"
+    for first in (0, A // 2, A - 1000):
+        page = jni.snapshotHandlesRange(p, first, 1000)
+        assert len(page) == 1000 * hb and not page.any()
+    with pytest.raises(JavaException) as ei:
+        jni.snapshotHandlesRange(p, A - 10, 11)
+    assert ei.value.cls == "java.lang.IllegalArgumentException"
+    with pytest.raises(JavaException) as ei:   # 2^27 handles = 2 GiB: not one Java array
+        jni.snapshotHandlesRange(p, 0, 1 << 27)
+    assert ei.value.cls == "java.lang.UnsupportedOperationException"
 
 
 def test_partition_natives_match_the_abi(jni):
