@@ -50,7 +50,9 @@ EXPORTED = (
     "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
     "hgx_graph_update", "hgx_query_coalesce_stats", "hgx_query_set_create", "hgx_pattern_batch_set",
-    "hgx_query_set_free", "hgx_pattern_batch_set_into",
+    "hgx_query_set_free", "hgx_pattern_batch_set_into", "hgx_query_set_info", "hgx_snapshot_read_handles",
+    "hgx_snapshot_writer_begin", "hgx_snapshot_writer_handles", "hgx_snapshot_writer_end", "hgx_snapshot_writer_abort",
+    "hgx_bfs_result_visited_range", "hgx_seq_result_pairs_range",
 )
 
 
