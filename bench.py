@@ -68,7 +68,9 @@ def pmc_traffic(kernel, workload):
         v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None, None
-    sha = _git_sha(rel)
+    # the commit the passes measured, written into the file by tools/pmc_summary.py (a GPU lease has
+    # no .git); the file's own last commit otherwise
+    sha = d.get("commit") or _git_sha(rel)
     return v, f"{rel}@{sha}" if sha else rel
 
 
@@ -147,7 +149,7 @@ def cpu_leg(run_for_threads, unit, sample, kind="port"):
     return out
 
 
-def cpu_bfs_baseline(g, seeds, depth, budget_s):
+def cpu_bfs_baseline(g, seeds, depth, budget_s, full_traversals=True):
     """C restatement (oracle/) of HGBreadthFirstTraversal + DefaultALGenerator, one traversal per
     thread, each stopped after budget_s: the edge rate of the reference path over the first budget_s
     of each traversal (a bounded sample of the same workload)."""
@@ -166,6 +168,18 @@ def cpu_bfs_baseline(g, seeds, depth, budget_s):
     out = cpu_leg(run, "TEPS", f"config-2 sources seeds[:threads] (1 thread / the job's CPU share), depth {depth}, one traversal "
                   f"per thread, each stopped after {budget_s:g}s (C restatement of HGBreadthFirstTraversal/"
                   "DefaultALGenerator)")
+    # the 2-s prefix of a traversal is its hub-heavy start; a second sample runs one COMPLETE depth-4
+    # traversal per thread of the job's share (one run: ~1 min of CPU work)
+    if full_traversals:
+        nt = cpu_threads()
+        tm = {}
+        _, tr = orc.bfs_many(np.asarray(seeds[:nt], np.int32), depth, depth + 1, nthreads=nt, timing=tm)
+        out["complete_traversals"] = {"threads": nt, "traversals": nt, "seconds": round(tm["elapsed_s"], 2),
+                                      "traversed_edges": int(tr.sum()), "value": int(tr.sum()) / tm["elapsed_s"],
+                                      "unit": "TEPS", "sample": f"seeds[:{nt}], one complete depth-{depth} traversal per "
+                                                                "thread, one run"}
+        log(f"cpu baseline: {nt} complete traversals {out['complete_traversals']['value']:.3e} TEPS "
+            f"({tm['elapsed_s']:.1f}s)")
     del orc
     return out
 
@@ -175,24 +189,22 @@ def cpu_query_baseline(g, qs, budget_s):
     from oracle_ctypes import OracleGraph
     orc = OracleGraph(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
 
-    def run(threads):
-        n_done, elapsed, i, step = 0, 0.0, 0, max(threads * 8, 64)
-        while elapsed < budget_s and i < len(qs["type"]):
-            sl = slice(i, i + step)
-            t = qs["type"][sl]
-            n = len(t)
-            inc_off = np.arange(n + 1, dtype=np.int64)
-            pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
-            pat = np.stack([qs["x"][sl], np.full(n, -1, np.int32), qs["y"][sl]], 1).reshape(-1)
-            t1 = time.time()
-            orc.and_query_many(t, inc_off, qs["a"][sl], pat_off, pat, np.ones(n, np.int32), nthreads=threads)
-            elapsed += time.time() - t1
-            n_done += n
-            i += step
-        return n_done, elapsed
+    # the whole 10K batch in ONE parallel region with dynamic scheduling (og_and_query_many: schedule
+    # dynamic, 4), timed to its completion -- per-slice calls each waited for their slowest hub query
+    n = len(qs["type"])
+    inc_off = np.arange(n + 1, dtype=np.int64)
+    pat_off = np.arange(0, 3 * n + 1, 3, dtype=np.int64)
+    pat = np.stack([qs["x"], np.full(n, -1, np.int32), qs["y"]], 1).reshape(-1)
+    ho = np.ones(n, np.int32)
 
-    out = cpu_leg(run, "queries/s", f"the config-3 queries in order until {budget_s:g}s per run (C restatement of "
-                  "AndToQuery + ZigZagIntersectionResult + OrderedLinkCondition)")
+    def run(threads):
+        t1 = time.perf_counter()
+        orc.and_query_many(qs["type"], inc_off, qs["a"], pat_off, pat, ho, nthreads=threads)
+        return n, time.perf_counter() - t1
+
+    out = cpu_leg(run, "queries/s", f"the {n} config-3 queries as one batch, one OpenMP region with dynamic "
+                  "scheduling, to completion (C restatement of AndToQuery + ZigZagIntersectionResult + "
+                  "OrderedLinkCondition)")
     del orc
     return out
 

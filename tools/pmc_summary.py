@@ -22,6 +22,7 @@ import json
 import os
 import re
 import shutil
+import subprocess
 import sys
 from collections import defaultdict
 
@@ -96,7 +97,19 @@ def main():
     trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until)
     fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until)
     write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until)
-    rows, js = [], {"tag": tag, "workload": workload, "kernels": {},
+    # the commit of the code the passes measured (this script runs in the repository right after the
+    # gpurun call that took them); bench.py copies it into the line's traffic_from, so the provenance
+    # survives a GPU lease without .git
+    try:
+        commit = subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                text=True, timeout=10).stdout.strip() or None
+        dirty = bool(subprocess.run(["git", "-C", root, "status", "--porcelain", "--untracked-files=no", "--",
+                                     "hypergraphdb_amd", "include"], capture_output=True, text=True,
+                                    timeout=10).stdout.strip())
+    except Exception:
+        commit, dirty = None, None
+    rows, js = [], {"tag": tag, "workload": workload, "kernels": {}, "commit": commit,
+                    "commit_dirty": dirty,
                     "note": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE correction)"}
     for k in sorted(trace, key=lambda k: -sum(trace[k])):
         t = trace[k]
