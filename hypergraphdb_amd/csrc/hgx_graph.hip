@@ -48,6 +48,7 @@ void graph_release(hgx_graph* g) {
     g->seq_hbufs.clear();
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->ctr_host) (void)hipHostFree(g->ctr_host);
+    if (g->seq_flag) (void)hipHostFree(g->seq_flag);
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->zc_in) (void)hipHostFree(g->zc_in);
     if (g->stream2) (void)hipStreamSynchronize(g->stream2);
@@ -524,7 +525,7 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;
     } else if (option == HGX_OPT_SEQ_ENGINE) {
-        if (value < 0 || value > 1) fail(HGX_E_INVALID, "hgx_set_option: sequence engine outside 0..1");
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: sequence engine outside 0..2");
         g->seq_engine = (int32_t)value;
     } else if (option == HGX_OPT_PUSH_INLINE) {
         g->push_inline = value != 0;

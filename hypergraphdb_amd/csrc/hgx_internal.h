@@ -208,7 +208,11 @@ struct hgx_graph {
     int32_t bfs_flags = 0x3BE;      // HGX_OPT_BFS_FLAGS (see hgx.h)
     int64_t seq_budget_bytes = (int64_t)48 << 30;   // HGX_OPT_SEQ_BUDGET: order-exact traversal working set
     int64_t max_arity = -1, max_deg = -1;           // lazily computed (order-exact stream keys)
-    int32_t seq_engine = 0;                         // HGX_OPT_SEQ_ENGINE: 0 workgroup per seed (+ fallback), 1 level-synchronous
+    int32_t seq_engine = 0;                         // HGX_OPT_SEQ_ENGINE: 0 workgroup per seed (+ level engine), 1 key-array
+                                                    //   level engine only, 2 level engine (hgx_ls_*) only
+    unsigned long long* seq_flag = nullptr;         // mapped coherent words: level sizes of the level engine
+    unsigned long long seq_flag_seq = 0;            //   (their sequence numbers)
+    int64_t ls_cap = 0, ls_wcap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update

@@ -29,6 +29,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -692,6 +693,372 @@ __global__ void __launch_bounds__(kSbThreads) hgx_seq_block(SbArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Level-synchronous engine (the traversals a workgroup cannot hold: more than kSbPairs pairs).
+//
+// Per level six kernels with fixed grids that read every size from device memory, so the host never
+// waits inside a level; it enqueues level d+1 before it polls level d's frontier size from mapped
+// memory (a finished traversal costs one level of no-op launches):
+//   hgx_ls_degree   frontier entries -> incidence start + degree; block sums over contiguous entry
+//                   ranges; records where each seed's pairs of the previous level start (runs)
+//   hgx_ls_prefix   degree prefix (blocks scan the block sums redundantly) + the tile -> first-entry
+//                   table of the level's flat item space; T, key-space width, capacity checks
+//   hgx_ls_expand   256-item tiles: entry by a short search inside the tile's entry range, yield
+//                   flags, link predicate, targets, position rule; atomicMin of
+//                   ((it << kbits | k) + 1) << 32 | link atom on key[seed][target]; first touch
+//                   appends (seed, target) to the level's discoveries; zeroes the rank bitmap
+//   hgx_ls_bits     one bit per discovery at its key in a bitmap over the level's key space
+//   hgx_ls_wprefix  popcount prefix of the bitmap words, per contiguous word range
+//   hgx_ls_emit     rank = popcount prefix below the key: pair `rank` of the level (link, atom),
+//                   entry `rank` of the next frontier, key[seed][atom] = 0 (examined)
+// The key order is (entry, link index, yield rank), i.e. the reference's stream order (the file
+// header); the level's pairs are seed-major because the frontier is.
+constexpr int kLsG = 1024;              // blocks of the range kernels (contiguous ranges: prefix-able)
+constexpr int64_t kLsTile = 256;        // items per expand tile
+constexpr int kLsSlots = 4;             // per-level counter slots (ring); slot words:
+enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5 };
+constexpr int kLsSlotWords = 8;
+constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2;
+constexpr int kLsCtlWords = kLsStatus + 8;
+
+struct LsArgs {
+    int64_t A;
+    const int64_t* inc_off;
+    const int32_t* inc_row;
+    const int32_t* inc_type;
+    const uint8_t* yf;                  // ordered-mode yield flags (null in the symmetric mode)
+    const int64_t* tgt_off;
+    const int32_t* tgt_idx;
+    const int32_t* link_atom;
+    int32_t want_type, min_arity, mode, rev, kbits;
+    int64_t t_limit;                    // largest item count of a level with 32-bit keys
+    u64* key;                           // [nb * A]: ~0 fresh, 0 examined, else this level's best value
+    int64_t cap;                        // frontier / discovery / output capacity (entries)
+    int64_t wcap, tcap, rcap;           // bitmap words, tiles, runs
+    int64_t* ctl;                       // kLsCtlWords
+    int32_t* fa[2];                     // frontier atom / seed (double-buffered)
+    int32_t* fs[2];
+    int64_t* fbase;                     // [cap] incidence start of entry i
+    int64_t* deg;                       // [cap] degree of entry i
+    int64_t* pre;                       // [cap + 1] exclusive degree prefix
+    int64_t* tile;                      // [tcap] first entry of each item tile
+    int64_t* bsum;                      // [kLsG] block sums (entries, then bitmap words)
+    int64_t* disc;                      // [cap] the level's discoveries: seed * A + atom
+    u64* bm;                            // [wcap] rank bitmap
+    uint32_t* wpre;                     // [wcap] popcount prefix of word w inside its block's range
+    int32_t* out_link;                  // [cap] pairs, level-major (device)
+    int32_t* out_atom;
+    int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
+    u64* hflag;                         // mapped coherent host words: {n, status, seq}
+};
+
+__device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
+
+__device__ __forceinline__ int64_t ls_block_sum(int64_t v, int64_t* ws) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const int64_t t = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    return t;
+}
+
+// exclusive scan over the 256 threads of a block; *tot = the block sum
+__device__ __forceinline__ int64_t ls_block_scan(int64_t v, int64_t* ws, int64_t* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    int64_t base = 0;
+    for (int k = 0; k < w; ++k) base += ws[k];
+    *tot = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    return base + x - v;
+}
+
+// exclusive prefix of bsum[0, kLsG) into LDS (every block, redundantly); returns the total
+__device__ __forceinline__ int64_t ls_block_offsets(const int64_t* __restrict__ bsum, int64_t* off, int64_t* ws) {
+    constexpr int per = kLsG / 256;
+    int64_t v[per], s = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        v[k] = bsum[threadIdx.x * per + k];
+        s += v[k];
+    }
+    int64_t tot;
+    int64_t b = ls_block_scan(s, ws, &tot);
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        off[threadIdx.x * per + k] = b;
+        b += v[k];
+    }
+    __syncthreads();
+    return tot;
+}
+
+__device__ __forceinline__ int64_t ls_lo(int64_t n, int b) { return n * b / kLsG; }   // n < 2^53
+
+__global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_t runs_only) {
+    __shared__ int64_t ws[4];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int64_t F = sl[lsF], out0 = sl[lsOut];
+    const int cur = d & 1;
+    const int32_t* fa = a.fa[cur];
+    const int32_t* fs = a.fs[cur];
+    const int64_t lo = ls_lo(F, blockIdx.x), hi = ls_lo(F, blockIdx.x + 1);
+    int64_t sum = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const int32_t s = fs[i];
+        if (d > 0 && (i == 0 || fs[i - 1] != s)) {   // where seed s's pairs of distance d start
+            const int64_t r = atomicAdd((unsigned long long*)&a.ctl[kLsRuns], 1ull);
+            if (r < a.rcap) {
+                a.runs[3 * r] = d;
+                a.runs[3 * r + 1] = s;
+                a.runs[3 * r + 2] = out0 + i;
+            } else {
+                atomicOr((unsigned long long*)&a.ctl[kLsStatus], 2ull);   // more runs than rcap
+            }
+        }
+        if (runs_only) continue;
+        const int32_t p = fa[i];
+        const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
+        a.fbase[i] = b;
+        a.deg[i] = e - b;
+        sum += e - b;
+    }
+    if (runs_only) return;
+    sum = ls_block_sum(sum, ws);
+    if (threadIdx.x == 0) a.bsum[blockIdx.x] = sum;
+    if (blockIdx.x == 0 && threadIdx.x < kLsSlotWords && threadIdx.x != lsF && threadIdx.x != lsOut)
+        a.ctl[((d + 1) % kLsSlots) * kLsSlotWords + threadIdx.x] = 0;   // the next level's slot counters
+}
+
+__global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
+    __shared__ int64_t ws[4], off[kLsG];
+    int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int64_t F = sl[lsF];
+    const int64_t T = ls_block_offsets(a.bsum, off, ws);
+    const int64_t lo = ls_lo(F, blockIdx.x), hi = ls_lo(F, blockIdx.x + 1);
+    // contiguous pieces per thread: local sums, block scan, then the prefix written in order
+    const int64_t piece = (hi - lo + 255) / 256, p0 = lo + threadIdx.x * piece, p1 = min(hi, p0 + piece);
+    int64_t s = 0;
+    for (int64_t i = p0; i < p1; ++i) s += a.deg[i];
+    int64_t tot;
+    int64_t run = off[blockIdx.x] + ls_block_scan(s, ws, &tot);
+    for (int64_t i = p0; i < p1; ++i) {
+        const int64_t dg = a.deg[i];
+        a.pre[i] = run;
+        // the tiles whose first item lies in this entry's items
+        for (int64_t k = (run + kLsTile - 1) / kLsTile; k * kLsTile < run + dg; ++k)
+            if (k < a.tcap) a.tile[k] = i;
+        run += dg;
+    }
+    if (blockIdx.x == kLsG - 1 && threadIdx.x == 0) {
+        a.pre[F] = T;
+        sl[lsT] = T;
+        const int64_t W = (int64_t)((((u64)T << a.kbits) + 63ull) >> 6);
+        sl[lsW] = W;
+        sl[lsTiles] = (T + kLsTile - 1) / kLsTile;
+        atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
+        int64_t st = 0;
+        if (T > a.t_limit) st |= 16;   // keys wider than 32 bits: the key-array engine takes the chunk
+        if (W > a.wcap) st |= 4;
+        if (sl[lsTiles] > a.tcap) st |= 8;
+        if (st) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)st);
+    }
+}
+
+// last index i in [lo, hi] with pre[i] <= x
+__device__ __forceinline__ int64_t ls_search(const int64_t* __restrict__ pre, int64_t lo, int64_t hi, int64_t x) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int64_t F = sl[lsF], T = sl[lsT], W = sl[lsW], nt = sl[lsTiles];
+    int64_t* dn = (int64_t*)(a.ctl + (d % kLsSlots) * kLsSlotWords + lsN);
+    const int cur = d & 1;
+    const int32_t* fa = a.fa[cur];
+    const int32_t* fs = a.fs[cur];
+    for (int64_t w = blockIdx.x * 256ll + threadIdx.x; w < W; w += (int64_t)gridDim.x * 256) a.bm[w] = 0ull;
+    const int lane = threadIdx.x & 63;
+    for (int64_t k = blockIdx.x; k < nt; k += gridDim.x) {
+        const int64_t e0 = a.tile[k], e1 = k + 1 < nt ? a.tile[k + 1] : F - 1;
+        const int64_t it = k * kLsTile + threadIdx.x;
+        bool live = it < T;
+        int64_t i = 0, j = 0, ii = 0;
+        int32_t p = -1, n = 0, la = 0, lo = 0, hi = 0;
+        int64_t b = 0;
+        if (live) {
+            i = ls_search(a.pre, e0, e1, it);
+            j = it - a.pre[i];
+            p = fa[i];
+            ii = a.fbase[i] + j;
+            if (a.yf && !((a.yf[ii] >> a.mode) & 1u)) live = false;                 // nothing to yield
+        }
+        if (live) {
+            const int32_t L = a.inc_row[ii];
+            const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
+            if (a.want_type >= 0 && ty != a.want_type) live = false;             // linkPredicate (:300)
+            b = a.tgt_off[L];
+            n = (int32_t)(a.tgt_off[L + 1] - b);
+            la = a.link_atom[L];
+            if (n < a.min_arity) live = false;                                    // minArity (:309)
+        }
+        if (live) {
+            hi = n;
+            if (a.mode != sSym) {
+                int32_t fv = -1, lv = -1;
+                for (int32_t q = 0; q < n; ++q)
+                    if (a.tgt_idx[b + q] == p) {
+                        if (fv < 0) fv = q;
+                        lv = q;
+                    }
+                if (a.mode == sAfterFirst) lo = fv + 1;
+                else if (a.mode == sBeforeFirst) hi = fv;
+                else if (a.mode == sBeforeLast) hi = lv;
+                else lo = lv + 1;
+            }
+        }
+        const int32_t cnt = live && hi > lo ? hi - lo : 0;
+        int32_t rounds = cnt;
+        for (int off = 32; off > 0; off >>= 1) rounds = max(rounds, __shfl_xor(rounds, off));
+        const int64_t sA = live ? (int64_t)fs[i] * a.A : 0;
+        const u64 kb = ((u64)it << a.kbits) + 1ull;
+        for (int32_t r = 0; r < rounds; ++r) {   // wave-uniform rounds: one append atomic per wave and round
+            bool isnew = false;
+            int32_t t = 0;
+            if (r < cnt) {
+                const int32_t q = lo + r;
+                t = a.tgt_idx[b + q];
+                if (t != p) {
+                    const u64 v = ((kb + (u64)(a.rev ? n - 1 - q : q)) << 32) | (u64)(uint32_t)la;
+                    u64* slot = a.key + sA + t;
+                    if (*slot > v) isnew = atomicMin(slot, v) == kNoKey;
+                }
+            }
+            const u64 m = __ballot(isnew);
+            if (m) {
+                const int leader = __ffsll((long long)m) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd((unsigned long long*)dn, (u64)__popcll(m));
+                base = __shfl(base, leader);
+                if (isnew) {
+                    const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
+                    if ((int64_t)w < a.cap) a.disc[w] = sA + t;
+                    else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap
+                }
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int64_t n = sl[lsN];
+    for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
+        const u64 kk = (a.key[a.disc[x]] >> 32) - 1ull;
+        atomicOr(&a.bm[kk >> 6], 1ull << (kk & 63));
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_ls_wprefix(LsArgs a, int32_t d) {
+    __shared__ int64_t ws[4];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int64_t W = sl[lsW];
+    const int64_t lo = ls_lo(W, blockIdx.x), hi = ls_lo(W, blockIdx.x + 1);
+    const int64_t piece = (hi - lo + 255) / 256, p0 = lo + threadIdx.x * piece, p1 = min(hi, p0 + piece);
+    int64_t s = 0;
+    for (int64_t w = p0; w < p1; ++w) s += __popcll(a.bm[w]);
+    int64_t tot;
+    int64_t run = ls_block_scan(s, ws, &tot);
+    for (int64_t w = p0; w < p1; ++w) {
+        a.wpre[w] = (uint32_t)run;
+        run += __popcll(a.bm[w]);
+    }
+    if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq) {
+    __shared__ int64_t ws[4], off[kLsG];
+    int64_t* sl = ls_slot(a, d);
+    int64_t status = a.ctl[kLsStatus];
+    const int64_t W = sl[lsW], out0 = sl[lsOut];
+    int64_t n = sl[lsN];
+    if (!status && (n > a.cap || out0 + n > a.cap)) status = 1;   // the pairs outgrow the output (every block agrees)
+    if (status) n = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (status) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)status);
+        int64_t* nx = a.ctl + ((d + 1) % kLsSlots) * kLsSlotWords;
+        nx[lsF] = n;
+        nx[lsOut] = out0 + n;
+        __hip_atomic_store(a.hflag, (u64)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.hflag + 1, (u64)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(a.hflag + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (n == 0) return;
+    ls_block_offsets(a.bsum, off, ws);
+    const int nx = (d + 1) & 1;
+    for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
+        const int64_t sa = a.disc[x];
+        const u64 v = a.key[sa];
+        const u64 kk = (v >> 32) - 1ull;
+        const int64_t w = (int64_t)(kk >> 6);
+        int b = (int)(w * kLsG / W);   // the block whose word range holds w
+        while (b + 1 < kLsG && ls_lo(W, b + 1) <= w) ++b;
+        while (b > 0 && ls_lo(W, b) > w) --b;
+        const int64_t r = off[b] + a.wpre[w] + __popcll(a.bm[w] & ((1ull << (kk & 63)) - 1ull));
+        const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
+        a.out_link[out0 + r] = (int32_t)(uint32_t)v;
+        a.out_atom[out0 + r] = t;
+        a.fa[nx][r] = t;
+        a.fs[nx][r] = s;
+        a.key[sa] = 0ull;   // examined from now on
+    }
+}
+
+__global__ void hgx_ls_seed(LsArgs a, int32_t nb, const int32_t* __restrict__ seeds) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb) {
+        a.key[(int64_t)i * a.A + seeds[i]] = 0ull;   // examined.put(start, TRUE) (:42-46)
+        a.fa[0][i] = seeds[i];
+        a.fs[0][i] = i;
+    }
+    if (i == 0) {
+        a.ctl[lsF] = nb;
+        a.ctl[lsOut] = 0;
+    }
+}
+
+// Device buffers of one call, given back to the graph's pool at scope exit.
+struct SeqScratch {
+    hgx_graph* g;
+    std::vector<std::pair<void*, size_t>> t;
+    void* take(size_t bytes) {
+        void* p = g->alloc(bytes);
+        t.push_back({p, bytes});
+        return p;
+    }
+    ~SeqScratch() {
+        for (auto& x : t) g->release(x.first, x.second);
+    }
+};
+
 template <class T> struct DevBuf {
     hgx_graph* g;
     T* p = nullptr;
@@ -897,6 +1264,188 @@ PoolBuf take_host_buf(hgx_graph* g, size_t bytes) {
     return PoolBuf{p, bytes};
 }
 
+// The level-synchronous engine (hgx_ls_* kernels) over a chunk of seeds; false when a capacity it
+// cannot grow was exceeded (level keys wider than 32 bits): the caller then runs the key-array engine.
+bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t maxd, const hgx_algen_opts& o,
+                       SeqOut& out, int64_t seed0) {
+    hipStream_t st = g->stream;
+    const int64_t A = g->A;
+    const int mode = seq_mode(o);
+    const int kbits = bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
+    if (!g->seq_flag) {   // mapped, coherent: the emit kernel's level sizes (once per graph)
+        void* hp = nullptr;
+        HGX_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, 64);
+        g->seq_flag = (u64*)hp;
+    }
+    u64* hflag_d = nullptr;
+    HGX_HIP(hipHostGetDevicePointer((void**)&hflag_d, g->seq_flag, 0));
+    const int64_t full = (int64_t)nb * A;
+    // starting capacities (grown x4 on overflow and kept on the graph); HGX_LS_SMALL (tests) starts
+    // them tiny so that every growth path runs
+    const bool small = std::getenv("HGX_LS_SMALL") != nullptr;
+    for (int attempt = 0;; ++attempt) {
+        const int64_t cap = std::min(full, std::max<int64_t>(g->ls_cap, small ? 64 : (int64_t)1 << 20));
+        const int64_t wcap = std::max<int64_t>(g->ls_wcap, small ? 16 : (int64_t)1 << 18);
+        const int64_t tcap = std::max<int64_t>(g->ls_tcap, small ? 8 : (int64_t)1 << 16);
+        const int64_t rcap = std::max<int64_t>(g->ls_rcap, small ? 4 : (int64_t)1 << 14);
+        LsArgs a{};
+        a.A = A;
+        a.inc_off = g->inc_off;
+        a.inc_row = g->inc_row;
+        a.inc_type = g->inc_type;
+        a.yf = mode != sSym ? g->inc_yf : nullptr;
+        a.tgt_off = g->tgt_off;
+        a.tgt_idx = g->tgt_idx;
+        a.link_atom = g->link_atom;
+        a.want_type = o.link_type;
+        a.min_arity = o.return_source ? 1 : 2;
+        a.mode = mode;
+        a.rev = o.reverse_order ? 1 : 0;
+        a.kbits = kbits;
+        a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
+        a.cap = cap;
+        a.wcap = wcap;
+        a.tcap = tcap;
+        a.rcap = rcap;
+        a.hflag = hflag_d;
+        SeqScratch w{g, {}};
+        a.key = (u64*)w.take(sizeof(u64) * (size_t)full);
+        a.ctl = (int64_t*)w.take(sizeof(int64_t) * kLsCtlWords);
+        for (int k = 0; k < 2; ++k) {
+            a.fa[k] = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
+            a.fs[k] = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
+        }
+        a.fbase = (int64_t*)w.take(sizeof(int64_t) * (size_t)std::max<int64_t>(cap, nb));
+        a.deg = (int64_t*)w.take(sizeof(int64_t) * (size_t)std::max<int64_t>(cap, nb));
+        a.pre = (int64_t*)w.take(sizeof(int64_t) * (size_t)(std::max<int64_t>(cap, nb) + 1));
+        a.tile = (int64_t*)w.take(sizeof(int64_t) * (size_t)tcap);
+        a.bsum = (int64_t*)w.take(sizeof(int64_t) * kLsG);
+        a.disc = (int64_t*)w.take(sizeof(int64_t) * (size_t)cap);
+        a.bm = (u64*)w.take(sizeof(u64) * (size_t)wcap);
+        a.wpre = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)wcap);
+        a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
+        a.out_atom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
+        a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
+        int32_t* dseeds = (int32_t*)w.take(sizeof(int32_t) * (size_t)nb);
+        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)nb);
+        std::memcpy(hs, seeds, sizeof(int32_t) * (size_t)nb);
+        HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)nb, hipMemcpyHostToDevice, st));
+        HGX_HIP(hipMemsetAsync(a.key, 0xFF, sizeof(u64) * (size_t)full, st));
+        HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(int64_t) * kLsCtlWords, st));
+        hgx_ls_seed<<<grid_for(nb, 256), 256, 0, st>>>(a, nb, dseeds);
+        HGX_CHECK_LAUNCH();
+        const u64 base = g->seq_flag_seq;
+        auto enqueue = [&](int32_t d) {
+            const int eg = 2048;   // grid of the grid-stride kernels
+            hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d, 0);
+            hgx_ls_prefix<<<kLsG, 256, 0, st>>>(a, d);
+            hgx_ls_expand<<<eg, 256, 0, st>>>(a, d);
+            hgx_ls_bits<<<eg, 256, 0, st>>>(a, d);
+            hgx_ls_wprefix<<<kLsG, 256, 0, st>>>(a, d);
+            hgx_ls_emit<<<eg, 256, 0, st>>>(a, d, base + (u64)d + 1);
+            HGX_CHECK_LAUNCH();
+        };
+        int64_t total = 0, status = 0;
+        int32_t dw = 0, enq = 0;
+        if (maxd > 0) {
+            enqueue(0);
+            enq = 1;
+        }
+        while (dw < enq) {
+            if (enq < maxd && enq == dw + 1) enqueue(enq++);   // one level ahead of the host
+            const u64 want = base + (u64)dw + 1;
+            for (unsigned spin = 0; __atomic_load_n(g->seq_flag + 2, __ATOMIC_ACQUIRE) != want; ++spin) {
+                if ((spin & 1023u) != 1023u) continue;   // the stream is asked every 1024 polls
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipErrorNotReady) continue;
+                if (e != hipSuccess) HGX_HIP(e);
+                if (__atomic_load_n(g->seq_flag + 2, __ATOMIC_ACQUIRE) != want)
+                    fail(HGX_E_DEVICE, "hgx_bfs_sequence: a level's size never arrived");
+            }
+            const int64_t n = (int64_t)__atomic_load_n(g->seq_flag, __ATOMIC_RELAXED);
+            status = (int64_t)__atomic_load_n(g->seq_flag + 1, __ATOMIC_RELAXED);
+            if (status) break;
+            total += n;
+            ++dw;
+            if (n == 0) break;
+            if (dw == maxd) {   // depth limit: the last level's pairs still need their runs
+                hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, dw, 1);
+                HGX_CHECK_LAUNCH();
+            }
+        }
+        g->seq_flag_seq = base + (u64)enq + 2;
+        std::vector<int64_t> ctl(kLsCtlWords);
+        HGX_HIP(hipMemcpyAsync(ctl.data(), a.ctl, sizeof(int64_t) * kLsCtlWords, hipMemcpyDeviceToHost, st));
+        spin_sync(st);
+        status |= ctl[kLsStatus];
+        if (status) {
+            if (status & 16) return false;   // 32-bit level keys do not fit
+            if (attempt > 16) fail(HGX_E_DEVICE, "hgx_bfs_sequence: level-synchronous capacities did not converge");
+            if (status & 1) g->ls_cap = std::min(full, cap * 4);
+            if (status & 2) g->ls_rcap = rcap * 4;
+            if (status & 4) g->ls_wcap = wcap * 4;
+            if (status & 8) g->ls_tcap = tcap * 4;
+            continue;   // rerun the chunk with the grown capacities (kept on the graph)
+        }
+        const int64_t nruns = ctl[kLsRuns];
+        out.traversed += (double)ctl[kLsTrav];
+        PoolBuf hb = take_host_buf(g, 8 * (size_t)std::max<int64_t>(total, 1) + 24 * (size_t)std::max<int64_t>(nruns, 1));
+        out.bufs.push_back(hb);
+        int32_t* hl = (int32_t*)hb.p;
+        int32_t* ha = hl + total;
+        int64_t* hr = (int64_t*)(ha + total + (total & 1));
+        if (total) {
+            HGX_HIP(hipMemcpyAsync(hl, a.out_link, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
+            HGX_HIP(hipMemcpyAsync(ha, a.out_atom, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
+        }
+        if (nruns) HGX_HIP(hipMemcpyAsync(hr, a.runs, sizeof(int64_t) * 3 * (size_t)nruns, hipMemcpyDeviceToHost, st));
+        spin_sync(st);
+        // runs partition [0, total) in pair order; each seed's runs in distance order are its pairs
+        std::vector<int64_t> ord((size_t)nruns);
+        for (int64_t k = 0; k < nruns; ++k) ord[k] = k;
+        std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return hr[3 * x + 2] < hr[3 * y + 2]; });
+        std::vector<std::vector<std::pair<int64_t, int64_t>>> per((size_t)nb);   // (distance, run)
+        for (int64_t k = 0; k < nruns; ++k) per[(size_t)hr[3 * ord[k] + 1]].push_back({hr[3 * ord[k]], k});
+        for (int32_t s = 0; s < nb; ++s) {
+            std::sort(per[s].begin(), per[s].end());
+            for (auto& dk : per[s]) {
+                const int64_t k = dk.second, b = hr[3 * ord[k] + 2];
+                const int64_t e = k + 1 < nruns ? hr[3 * ord[k + 1] + 2] : total;
+                out.segs[(size_t)(seed0 + s)].push_back({hl + b, ha + b, nullptr, e - b, (int32_t)dk.first});
+                out.deepest = std::max(out.deepest, (int32_t)dk.first);
+            }
+        }
+        return true;
+    }
+}
+
+// The level-synchronous engines over any number of seeds: chunks whose key arrays fit the budget,
+// hgx_ls_* first, the key-array engine (seq_levels) for a chunk whose level keys exceed 32 bits.
+void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t maxd, const hgx_algen_opts& o,
+                    SeqOut& out, bool v2) {
+    if (!v2) {
+        seq_levels(g, seeds, n_seeds, maxd, o, out);
+        return;
+    }
+    out.segs.assign((size_t)n_seeds, {});
+    const int64_t A = std::max<int64_t>(g->A, 1);
+    int64_t B = std::max<int64_t>(1, std::min<int64_t>(n_seeds, 1024));
+    while (B > 1 && B * A * 24 > g->seq_budget_bytes) B = (B + 1) / 2;
+    for (int64_t c0 = 0; c0 < n_seeds; c0 += B) {
+        const int32_t nb = (int32_t)std::min<int64_t>(B, n_seeds - c0);
+        if (!seq_levels2_chunk(g, seeds + c0, nb, maxd, o, out, c0)) {
+            SeqOut one;
+            seq_levels(g, seeds + c0, nb, maxd, o, one);
+            out.traversed += one.traversed;
+            out.deepest = std::max(out.deepest, one.deepest);
+            for (int32_t s = 0; s < nb; ++s) out.segs[(size_t)(c0 + s)] = std::move(one.segs[s]);
+            for (auto& b : one.bufs) out.bufs.push_back(b);
+            one.bufs.clear();
+        }
+    }
+}
+
 }  // namespace
 }  // namespace hgx
 
@@ -1072,7 +1621,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     if (!rerun.empty()) {
         std::vector<int32_t> rs(rerun.size());
         for (size_t k = 0; k < rerun.size(); ++k) rs[k] = seeds[rerun[k]];
-        seq_levels(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev);
+        seq_levels_all(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev, g->seq_engine != 1);
         r->traversed += r->lev.traversed;
         deepest = std::max(deepest, r->lev.deepest);
         for (size_t k = 0; k < rerun.size(); ++k) {

@@ -465,8 +465,11 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
 /* HGX_OPT_SEQ_ENGINE (default 0): how hgx_bfs_sequence runs.  0 = one workgroup per seed with the
  * whole traversal in LDS (hash of the examined atoms, frontier and discovery ranks on chip, pairs
  * written into mapped host memory; one launch per 1024 seeds, no host round trip per level), seeds
- * whose traversal outgrows the workgroup's 2046 pairs rerun on the level-synchronous engine;
- * 1 = every seed on the level-synchronous engine (A/B and tests). */
+ * whose traversal outgrows the workgroup's 2046 pairs rerun on the level-synchronous engine (six
+ * fixed-grid kernels a level that read every size from device memory; the host polls each level's
+ * size one level behind; discoveries ranked by a bitmap over the level's key space);
+ * 1 = every seed on the round-1 key-array engine (rocPRIM sort, two host round trips a level; A/B);
+ * 2 = every seed on the level-synchronous engine (tests). */
 #define HGX_OPT_SEQ_ENGINE 13
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */

@@ -133,10 +133,10 @@ def _seq(snap, seeds, maxd, g_, engine):
 
 @pytest.mark.parametrize("case", range(4))
 def test_workgroup_and_level_engines_agree(case):
-    """The workgroup-per-seed engine (default) and the level-synchronous engine return identical
-    sequences, links, distances and traversal counts -- over graphs whose closures stay inside one
-    workgroup and graphs whose hubs push some seeds over its 2046 pairs (those rerun on the
-    level-synchronous engine)."""
+    """The workgroup-per-seed engine (default), the level-synchronous hgx_ls_* engine (2) and the
+    round-1 key-array engine (1) return identical sequences, links, distances and traversal counts --
+    over graphs whose closures stay inside one workgroup and graphs whose hubs push some seeds over its
+    2046 pairs (those rerun on the level-synchronous engine)."""
     from hypergraphdb_amd import synth
     rng = np.random.default_rng(40 + case)
     if case < 2:
@@ -149,11 +149,12 @@ def test_workgroup_and_level_engines_agree(case):
         lt = [-1, 0, 1][mi % 3] if case % 2 == 0 else -1
         for maxd in (None, 2):
             a = _seq(snap, seeds, maxd, gen(snap, mode, lt), 0)
-            b = _seq(snap, seeds, maxd, gen(snap, mode, lt), 1)
-            assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd)
-            assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd)
-            assert np.array_equal(a.dists, b.dists), (case, mi, maxd)
-            assert a.traversed_edges == b.traversed_edges and a.n_levels == b.n_levels
+            for eng in (1, 2):
+                b = _seq(snap, seeds, maxd, gen(snap, mode, lt), eng)
+                assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd, eng)
+                assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd, eng)
+                assert np.array_equal(a.dists, b.dists), (case, mi, maxd, eng)
+                assert a.traversed_edges == b.traversed_edges and a.n_levels == b.n_levels, eng
     snap.close()
 
 
@@ -189,3 +190,22 @@ def test_config5_closures_sequence_vs_oracle():
             one = bfs_sequence(snap, g["seeds"][i:i + 1], None, gen_)
             assert all(np.array_equal(x, y) for x, y in zip(one.pairs(0), res.pairs(i))), (rev, i)
     snap.close()
+
+
+def test_level_engine_capacity_growth_and_depth_limits():
+    """The level-synchronous engine grows its capacities (discoveries, bitmap words, tiles, runs)
+    from small starting values on a graph whose levels exceed them, then stays exact; every depth
+    limit 0..4 and unbounded, against the oracle."""
+    import os
+    from hypergraphdb_amd import _lib, synth
+    g = synth.hypergraph(30000, 60000, 2, 6, 2.0, 1, seed=13)
+    os.environ["HGX_LS_SMALL"] = "1"
+    try:
+        snap, orc = snapshot(g), oracle(g)
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
+        seeds = np.array([0, 1, 2, 29999, 15000, 0], np.int32)
+        for maxd in (0, 1, 2, 3, 4, None):
+            check_seq(g, seeds, maxd, K.ALGEN_MODES[maxd % 3 if maxd else 0], -1, snap, orc)
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+    finally:
+        del os.environ["HGX_LS_SMALL"]
