@@ -713,7 +713,7 @@ __global__ void __launch_bounds__(kSbThreads) hgx_seq_block(SbArgs a) {
 //                   entry `rank` of the next frontier, key[seed][atom] = 0 (examined)
 // The key order is (entry, link index, yield rank), i.e. the reference's stream order (the file
 // header); the level's pairs are seed-major because the frontier is.
-constexpr int kLsG = 1024;              // blocks of the range kernels (contiguous ranges: prefix-able)
+constexpr int kLsG = 256;               // blocks of the range kernels (contiguous ranges: prefix-able)
 constexpr int64_t kLsTile = 256;        // items per expand tile
 constexpr int kLsSlots = 4;             // per-level counter slots (ring); slot words:
 enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5 };
@@ -749,7 +749,7 @@ struct LsArgs {
     int32_t* out_link;                  // [cap] pairs, level-major (device)
     int32_t* out_atom;
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
-    u64* hflag;                         // mapped coherent host words: {n, status, seq}
+    u64* hflag;                         // mapped coherent host words: {n, status, seq} x 2 (level parity)
 };
 
 __device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
@@ -806,7 +806,8 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
     __shared__ int64_t ws[4];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
-    const int64_t F = sl[lsF], out0 = sl[lsOut];
+    // this frontier = the previous level's pairs, which sit at [Out_d - F, Out_d) of the output
+    const int64_t F = sl[lsF], out0 = sl[lsOut] - F;
     const int cur = d & 1;
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
@@ -1006,10 +1007,13 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
         int64_t* nx = a.ctl + ((d + 1) % kLsSlots) * kLsSlotWords;
         nx[lsF] = n;
         nx[lsOut] = out0 + n;
-        __hip_atomic_store(a.hflag, (u64)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(a.hflag + 1, (u64)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // two host slots by level parity: the host reads level d while level d+1 may already be
+        // publishing (it never enqueues level d+2 before it has read level d)
+        u64* hf = a.hflag + 4 * (d & 1);
+        __hip_atomic_store(hf, (u64)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hf + 1, (u64)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
-        __hip_atomic_store(a.hflag + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hf + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (n == 0) return;
     ls_block_offsets(a.bsum, off, ws);
@@ -1337,13 +1341,14 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         HGX_CHECK_LAUNCH();
         const u64 base = g->seq_flag_seq;
         auto enqueue = [&](int32_t d) {
-            const int eg = 2048;   // grid of the grid-stride kernels
+            // grids: thousands of idle workgroups cost ~10 us a launch on small levels;
+            // the expand's tiles are the only work that needs more than a block per CU
             hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d, 0);
             hgx_ls_prefix<<<kLsG, 256, 0, st>>>(a, d);
-            hgx_ls_expand<<<eg, 256, 0, st>>>(a, d);
-            hgx_ls_bits<<<eg, 256, 0, st>>>(a, d);
+            hgx_ls_expand<<<1024, 256, 0, st>>>(a, d);
+            hgx_ls_bits<<<512, 256, 0, st>>>(a, d);
             hgx_ls_wprefix<<<kLsG, 256, 0, st>>>(a, d);
-            hgx_ls_emit<<<eg, 256, 0, st>>>(a, d, base + (u64)d + 1);
+            hgx_ls_emit<<<512, 256, 0, st>>>(a, d, base + (u64)d + 1);
             HGX_CHECK_LAUNCH();
         };
         int64_t total = 0, status = 0;
@@ -1355,16 +1360,17 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         while (dw < enq) {
             if (enq < maxd && enq == dw + 1) enqueue(enq++);   // one level ahead of the host
             const u64 want = base + (u64)dw + 1;
-            for (unsigned spin = 0; __atomic_load_n(g->seq_flag + 2, __ATOMIC_ACQUIRE) != want; ++spin) {
+            const u64* hf = g->seq_flag + 4 * (dw & 1);
+            for (unsigned spin = 0; __atomic_load_n(hf + 2, __ATOMIC_ACQUIRE) != want; ++spin) {
                 if ((spin & 1023u) != 1023u) continue;   // the stream is asked every 1024 polls
                 const hipError_t e = hipStreamQuery(st);
                 if (e == hipErrorNotReady) continue;
                 if (e != hipSuccess) HGX_HIP(e);
-                if (__atomic_load_n(g->seq_flag + 2, __ATOMIC_ACQUIRE) != want)
+                if (__atomic_load_n(hf + 2, __ATOMIC_ACQUIRE) != want)
                     fail(HGX_E_DEVICE, "hgx_bfs_sequence: a level's size never arrived");
             }
-            const int64_t n = (int64_t)__atomic_load_n(g->seq_flag, __ATOMIC_RELAXED);
-            status = (int64_t)__atomic_load_n(g->seq_flag + 1, __ATOMIC_RELAXED);
+            const int64_t n = (int64_t)__atomic_load_n(hf, __ATOMIC_RELAXED);
+            status = (int64_t)__atomic_load_n(hf + 1, __ATOMIC_RELAXED);
             if (status) break;
             total += n;
             ++dw;
@@ -1390,7 +1396,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         }
         const int64_t nruns = ctl[kLsRuns];
         out.traversed += (double)ctl[kLsTrav];
-        PoolBuf hb = take_host_buf(g, 8 * (size_t)std::max<int64_t>(total, 1) + 24 * (size_t)std::max<int64_t>(nruns, 1));
+        // [links total][atoms total][pad to 8 bytes][runs 3 x nruns]
+        PoolBuf hb = take_host_buf(g, 8 * (size_t)total + 8 + 24 * (size_t)std::max<int64_t>(nruns, 1));
         out.bufs.push_back(hb);
         int32_t* hl = (int32_t*)hb.p;
         int32_t* ha = hl + total;
@@ -1405,6 +1412,18 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         std::vector<int64_t> ord((size_t)nruns);
         for (int64_t k = 0; k < nruns; ++k) ord[k] = k;
         std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return hr[3 * x + 2] < hr[3 * y + 2]; });
+        // the runs must tile [0, total) exactly (one per seed and level with pairs)
+        for (int64_t k = 0; k < nruns; ++k) {
+            const int64_t b = hr[3 * ord[k] + 2], e = k + 1 < nruns ? hr[3 * ord[k + 1] + 2] : total;
+            const int64_t sd = hr[3 * ord[k] + 1];
+            if ((k == 0 && b != 0) || e <= b || sd < 0 || sd >= nb)
+                fail(HGX_E_DEVICE, "hgx_bfs_sequence: level engine runs inconsistent (run " + std::to_string(k) + " of " +
+                                       std::to_string(nruns) + ": start " + std::to_string(b) + " end " +
+                                       std::to_string(e) + " seed " + std::to_string(sd) + " distance " +
+                                       std::to_string(hr[3 * ord[k]]) + ", pairs " + std::to_string(total) + ")");
+        }
+        if (nruns == 0 && total != 0)
+            fail(HGX_E_DEVICE, "hgx_bfs_sequence: level engine pairs without runs (" + std::to_string(total) + ")");
         std::vector<std::vector<std::pair<int64_t, int64_t>>> per((size_t)nb);   // (distance, run)
         for (int64_t k = 0; k < nruns; ++k) per[(size_t)hr[3 * ord[k] + 1]].push_back({hr[3 * ord[k]], k});
         for (int32_t s = 0; s < nb; ++s) {

@@ -472,4 +472,4 @@ def test_all_natives_were_executed(jni):
     """Runs last (file order): every native declared in Hgx.java has been called on the GPU."""
     missing = sorted(set(java_natives()) - jni.called)
     assert not missing, missing
-    assert len(jni.called) == 58
+    assert len(jni.called) == 67
