@@ -3809,6 +3809,11 @@ struct hgx_bfs_result {
     bool typed = false;
     std::map<int32_t, int32_t> isolated;   // shards: seed index -> owned seed atom without incidence
     std::vector<int64_t> counts;   // [n_seeds * n_levels]
+    // Seeds finished by the workgroup engine (HGX_OPT_BFS_BLOCK); the batches then hold only the
+    // others, compacted: orig[k] = seed index of batch seed k, compact[i] = k (-1: a workgroup seed).
+    std::unique_ptr<hgx::BlockSet> blk;
+    std::vector<int32_t> orig, compact;
+    int32_t orig_of(int32_t k) const { return orig.empty() ? k : orig[k]; }
     size_t row_bytes(const BfsBatch& b) const { return sizeof(u64) * (size_t)g->A * b.W; }
     size_t bm_bytes() const { return sizeof(u64) * (size_t)(g->A / 64 + 2); }
 };
@@ -5042,6 +5047,19 @@ void ensure_counts(hgx_bfs_result* r) {
     hgx_graph* g = r->g;
     HGX_HIP(hipSetDevice(g->device));
     r->counts.assign((size_t)r->n_seeds * r->n_levels, 0);
+    if (r->blk) {   // the workgroup engine's seeds: V_0 = {seed}, then the level counts it wrote
+        const BlockSet& b = *r->blk;
+        for (int32_t i = 0; i < r->n_seeds; ++i) {
+            if (b.pairs[i] < 0) continue;
+            int64_t* c = &r->counts[(size_t)i * r->n_levels];
+            c[0] = 1;
+            for (int32_t d = 0; d < b.levels[i]; ++d) c[d + 1] = b.lcnt[i][d];
+        }
+        if (r->batches.empty()) {
+            r->counts_ready = true;
+            return;
+        }
+    }
     // Traversals made of push levels (config 5's closures): every level past the seeds was counted by
     // its push finalise, and level 0 of a whole-graph batch is {seed} (count 1 each) -- the readout is
     // one copy of the count rows, no counting pass and no reduce launch.
@@ -5067,7 +5085,7 @@ void ensure_counts(hgx_bfs_result* r) {
         for (auto& bt : r->batches) {
             const size_t nl = bt.lvl.size();
             for (int s = 0; s < bt.S; ++s) {
-                int64_t* c = &r->counts[(size_t)(bt.seed0 + s) * r->n_levels];
+                int64_t* c = &r->counts[(size_t)r->orig_of(bt.seed0 + s) * r->n_levels];
                 if (nl > 0) c[0] = 1;   // V_0 = {seed}
                 for (size_t d = 1; d < nl; ++d) c[d] = (int64_t)hc[(o + d - 1) * 1024 + s];
             }
@@ -5173,7 +5191,8 @@ void ensure_counts(hgx_bfs_result* r) {
     k = 0;
     for (auto& bt : r->batches)
         for (size_t d = 0; d < bt.lvl.size(); ++d, ++k)
-            for (int s = 0; s < bt.S; ++s) r->counts[(size_t)(bt.seed0 + s) * r->n_levels + d] = (int64_t)hc[k * 1024 + s];
+            for (int s = 0; s < bt.S; ++s)
+                r->counts[(size_t)r->orig_of(bt.seed0 + s) * r->n_levels + d] = (int64_t)hc[k * 1024 + s];
     for (auto& kv : r->isolated) r->counts[(size_t)kv.first * r->n_levels] += 1;
     r->counts_ready = true;
 }
@@ -5223,6 +5242,9 @@ void ensure_accounting(hgx_bfs_result* r) {
             if (d <= bt.n_expanded) r->stats.bytes_min += mask * U[d];   // rows of the new atoms written
     }
     g->release(dc, sizeof(u64) * 1025);
+    // the workgroup engine's seeds counted their own items (|U_d|, the survey and minimum-bytes
+    // models above cover the rows engine's seeds only)
+    if (r->blk) trav_total += r->blk->traversed;
     r->stats.traversed_edges = trav_total;
     r->accounting_ready = true;
 }
@@ -5312,6 +5334,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                 for (auto p : bt.cpart)
                     if (p) r->g->release(p, bt.cpart_bytes);
             }
+            if (r->blk) block_release(r->g, *r->blk);
             r->g->refs.fetch_sub(1);   // the caller still holds its own reference
             delete r;
         }
@@ -5325,6 +5348,27 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
     if (tm.on) HGX_HIP(hipEventRecord(tm.all.a, g->stream));
     std::vector<std::vector<u64>> level_ctr;
     int max_expanded = 0;
+    // Whole-graph batches: every seed first runs in one workgroup (hgx_bfs_block); the rows engine
+    // below takes the seeds that outgrew it, compacted.
+    std::vector<int32_t> rseeds;
+    if (!shp && !tr && g->bfs_block && n_seeds > 0) {
+        r->blk.reset(new BlockSet());
+        bfs_block(g, seeds, n_seeds, max_depth, o, *r->blk);
+        const BlockSet& b = *r->blk;
+        max_expanded = b.expanded;
+        r->stats.ms_block = b.ms;
+        r->stats.bytes_block = b.bytes;
+        r->stats.block_seeds = n_seeds - (int64_t)b.rerun.size();
+        r->stats.block_rerun = (int64_t)b.rerun.size();
+        r->compact.assign((size_t)n_seeds, -1);
+        for (size_t k = 0; k < b.rerun.size(); ++k) {
+            r->compact[b.rerun[k]] = (int32_t)k;
+            r->orig.push_back(b.rerun[k]);
+            rseeds.push_back(seeds[b.rerun[k]]);
+        }
+        seeds = rseeds.data();
+        n_seeds = (int32_t)rseeds.size();
+    }
     for (int32_t s0 = 0; s0 < n_seeds; s0 += 1024) {
         BfsBatch bt;
         bt.seed0 = s0;
@@ -5444,6 +5488,8 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
     spin_sync(g->stream);
     int nl = 1;
     for (auto& bt : r->batches) nl = std::max(nl, (int)bt.lvl.size());
+    if (r->blk)
+        for (int32_t lv : r->blk->levels) nl = std::max(nl, lv + 1);
     r->n_levels = nl;
     r->stats.n_levels_expanded = max_expanded;
     r->stats.n_batches = (int32_t)r->batches.size();
@@ -5492,10 +5538,29 @@ int hgx_bfs_result_visited_range(hgx_bfs_result* r, int32_t seed_index, int32_t 
     if (depth < 0) fail(HGX_E_NOTFOUND, "no such depth");
     hgx_graph* g = r->g;
     std::lock_guard<std::mutex> lk(g->mu);
+    *n_out = 0;
+    if (r->blk && r->blk->pairs[seed_index] >= 0) {   // a workgroup seed: its level, sorted on the host
+        const BlockSet& b = *r->blk;
+        if (depth > b.levels[seed_index]) return HGX_OK;
+        if (depth == 0) {
+            *n_out = 1;
+            if (cap > 0 && first == 0) out[0] = b.seeds[seed_index];
+            return HGX_OK;
+        }
+        int64_t beg = 0;
+        for (int32_t d = 0; d < depth - 1; ++d) beg += b.lcnt[seed_index][d];
+        const int64_t n = b.lcnt[seed_index][depth - 1];
+        std::vector<int32_t> v(b.atoms[seed_index] + beg, b.atoms[seed_index] + beg + n);
+        std::sort(v.begin(), v.end());
+        *n_out = n;
+        const int64_t k = std::min(std::max<int64_t>(n - first, 0), cap);
+        if (k > 0) std::memcpy(out, v.data() + first, sizeof(int32_t) * (size_t)k);
+        return HGX_OK;
+    }
     HGX_HIP(hipSetDevice(g->device));
+    if (r->blk) seed_index = r->compact[seed_index];
     const BfsBatch& bt = r->batches[seed_index / 1024];
     const int s = seed_index % 1024;
-    *n_out = 0;
     auto iso = r->isolated.find(seed_index);
     if (iso != r->isolated.end()) {   // an isolated seed: only itself, at distance 0
         if (depth == 0) {
@@ -5559,7 +5624,24 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
     }
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "atom id out of range");
     std::lock_guard<std::mutex> lk(g->mu);
+    if (r->blk && r->blk->pairs[seed_index] >= 0) {   // a workgroup seed: scan its levels
+        const BlockSet& b = *r->blk;
+        *depth_out = -1;
+        if (b.seeds[seed_index] == atom) {
+            *depth_out = 0;
+            return HGX_OK;
+        }
+        int64_t k = 0;
+        for (int32_t d = 0; d < b.levels[seed_index] && *depth_out < 0; ++d)
+            for (int64_t e = k + b.lcnt[seed_index][d]; k < e; ++k)
+                if (b.atoms[seed_index][k] == atom) {
+                    *depth_out = d + 1;
+                    break;
+                }
+        return HGX_OK;
+    }
     HGX_HIP(hipSetDevice(g->device));
+    if (r->blk) seed_index = r->compact[seed_index];
     const BfsBatch& bt = r->batches[seed_index / 1024];
     const int nl = (int)bt.lvl.size();
     void** tab = (void**)g->alloc(sizeof(void*) * 2 * nl + sizeof(int32_t) * 4);
@@ -5602,6 +5684,7 @@ void hgx_bfs_result_free(hgx_bfs_result* r) {
             for (auto p : bt.cpart)
                 if (p) g->release(p, bt.cpart_bytes);
         }
+        if (r->blk) block_release(g, *r->blk);
     }
     delete r;
     if (g) graph_release(g);

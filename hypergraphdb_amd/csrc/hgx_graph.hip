@@ -312,6 +312,7 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     // the snapshot's options at this point (set separately on the context afterwards)
     c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
     c->seq_engine = g->seq_engine;
+    c->bfs_block = g->bfs_block;
     c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline; c->coded = g->coded;
     c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused; c->push_inline = g->push_inline;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
@@ -527,6 +528,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     } else if (option == HGX_OPT_SEQ_ENGINE) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: sequence engine outside 0..2");
         g->seq_engine = (int32_t)value;
+    } else if (option == HGX_OPT_BFS_BLOCK) {
+        g->bfs_block = value != 0;
     } else if (option == HGX_OPT_PUSH_INLINE) {
         g->push_inline = value != 0;
     } else if (option == HGX_OPT_QUERY_COALESCE) {

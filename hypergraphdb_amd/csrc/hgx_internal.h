@@ -215,6 +215,7 @@ struct hgx_graph {
     int64_t ls_cap = 0, ls_wcap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
+    int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
     // order-exact traversal refuses to run until the caller re-asserts it.
@@ -309,6 +310,25 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Builds the ordered-mode yield flags (hgx_inc_yield, one byte per incidence entry + 64 bytes of
 // padding for 16-byte vector loads) on g if absent; caller holds g->mu (hgx_bfs.hip).
 void ensure_inc_yield(hgx_graph* g);
+// The set-mode workgroup engine's part of one hgx_bfs_batch (hgx_seq.hip, HGX_OPT_BFS_BLOCK): per seed
+// V_1, V_2, ... one after the other (atoms) and |V_d| (lcnt[d - 1]) in mapped host buffers the
+// result owns; the seeds whose traversal outgrew a workgroup are listed in rerun (the batched engine
+// runs them).
+struct BlockSet {
+    std::vector<PoolBuf> bufs;
+    std::vector<int32_t> seeds;                 // [n seeds] the start atoms (V_0)
+    std::vector<const int32_t*> atoms, lcnt;   // [n seeds] (nullptr: rerun)
+    std::vector<int32_t> pairs, levels;         // [n seeds] atoms past V_0 (-1: rerun), levels with news
+    std::vector<int32_t> rerun;                 // seed indices, ascending
+    double traversed = 0, ms = 0, bytes = 0;   // items of the finished seeds; device ms; algorithmic bytes
+    int32_t expanded = 0;                       // most levels expanded by one finished seed
+};
+// Runs every seed on the workgroup engine (caller holds g->mu, g's device current; max_depth -1 =
+// unbounded); returns when the seeds are done.
+void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
+               BlockSet& out);
+// Hands the result's mapped buffers back to the graph's pool.
+void block_release(hgx_graph* g, BlockSet& b);
 // Waits for the work enqueued on s by polling: hipStreamSynchronize sleeps and wakes tens of
 // microseconds after the last kernel, a cost per call of the short pattern batches.
 inline void spin_sync(hipStream_t s) {

@@ -711,6 +711,61 @@ __global__ void __launch_bounds__(256) hgx_pattern_match(
 // ---------------------------------------------------------------------------------------------
 constexpr int kFlatChunk = 64;
 
+// Derived flat index (single-pass pipeline, at most kDerivedBlocks front blocks): the query offsets
+// and the chunk owners come from the front kernel's block totals and in-block prefixes instead of a
+// scan kernel.  Every workgroup of the match and of the placement sums the block totals itself into
+// LDS (a few dozen values), so no launch sits between the front kernel and the match:
+//   coff(q) = bp[q / 256] + lpre[q],  bp[b] = candidates of the front blocks before b.
+// A chunk's owner (the last query whose candidates start at or before the chunk's first candidate)
+// is found by a search over bp in LDS and one 256-entry window of lpre (a ballot per 64 entries).
+constexpr int kDerivedBlocks = 256;
+
+struct DIdx {
+    const int64_t* bp;     // LDS [nb + 1]
+    const int64_t* lpre;   // [n]
+    int32_t nb, n;
+    __device__ __forceinline__ int64_t coff(int64_t q) const { return q >= n ? bp[nb] : bp[q >> 8] + lpre[q]; }
+};
+
+// bp[0..nb] from blk (whole workgroup, 256 threads, nb <= 256); ends with a barrier.
+__device__ __forceinline__ void didx_load(int64_t* bp, int64_t* ws, const int64_t* __restrict__ blk, int32_t nb) {
+    const int64_t v = (int)threadIdx.x < nb ? blk[3 * threadIdx.x] : 0;
+    int64_t tot;
+    const int64_t ex = block_exclusive_scan<int64_t>(v, ws, tot);
+    if ((int)threadIdx.x < nb) bp[threadIdx.x] = ex;
+    if (threadIdx.x == 0) bp[nb] = tot;
+    __syncthreads();
+}
+
+// Last query q with coff(q) <= x (strict: < x), -1 when there is none.  x is wave-uniform; the whole
+// wave takes part and gets the same answer.
+__device__ __forceinline__ int64_t didx_last(const DIdx& ix, int64_t x, bool strict) {
+    int lo = 0, hi = ix.nb - 1, b = -1;   // last front block whose first query qualifies
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool ok = strict ? ix.bp[mid] < x : ix.bp[mid] <= x;
+        if (ok) {
+            b = mid;
+            lo = mid + 1;
+        } else {
+            hi = mid - 1;
+        }
+    }
+    if (b < 0) return -1;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = (int64_t)b * 256, t = x - ix.bp[b];
+    int64_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t q = base + i * 64 + lane;
+        v[i] = q < ix.n ? ix.lpre[q] : INT64_MAX;
+    }
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c += __popcll(__ballot(strict ? v[i] < t : v[i] <= t));
+    return base + c - 1;   // lpre is non-decreasing inside the block and lpre[base] = 0 qualifies
+}
+
 __global__ void __launch_bounds__(kScanBlock) hgx_q_scan_flat(int32_t n, const int64_t* __restrict__ ncand,
                                                                int64_t* __restrict__ coff, int32_t* __restrict__ chq,
                                                                int32_t* __restrict__ n_chunks_out, int64_t cap_chunks,
@@ -826,6 +881,8 @@ __device__ __forceinline__ bool check_mem(const int32_t* __restrict__ row, int n
     return hit;
 }
 
+// D: the derived flat index (blk / lpre / nb; n_chunks_p, chq and coff unused), else the scanned one.
+template <bool D>
 __global__ void __launch_bounds__(256) hgx_pattern_match_flat(
     const int32_t* __restrict__ n_chunks_p, int32_t n, const int32_t* __restrict__ chq, const int64_t* __restrict__ coff,
     const QPlan* __restrict__ plan, const QDesc* __restrict__ desc, const int32_t* __restrict__ anchors,
@@ -833,21 +890,34 @@ __global__ void __launch_bounds__(256) hgx_pattern_match_flat(
     const int32_t* __restrict__ pattern, const int32_t* __restrict__ inc_row, const int32_t* __restrict__ inc_type,
     const int32_t* __restrict__ inc_ts_row, const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
     const int4* __restrict__ ts_tgt, int32_t* __restrict__ slots, int64_t* __restrict__ counts,
-    u64* __restrict__ hitmask, u64* __restrict__ ctr) {
+    u64* __restrict__ hitmask, u64* __restrict__ ctr, const int64_t* __restrict__ blk, const int64_t* __restrict__ lpre,
+    int32_t nb, int64_t cap_chunks, int64_t cap_cand) {
     __shared__ int64_t win[4][kFlatChunk + 1];
+    __shared__ int64_t bp[D ? kDerivedBlocks + 1 : 1], ws[4];
     int64_t* cw = win[threadIdx.x >> 6];
-    const int32_t n_chunks = *n_chunks_p;
+    DIdx ix{bp, lpre, nb, n};
+    int64_t total;
+    int32_t n_chunks;
+    if (D) {
+        didx_load(bp, ws, blk, nb);
+        total = bp[nb];
+        const int64_t tc = (total + kFlatChunk - 1) / kFlatChunk;
+        n_chunks = (tc > cap_chunks || total > cap_cand) ? 0 : (int32_t)tc;
+    } else {
+        n_chunks = *n_chunks_p;
+        total = coff[n];
+    }
+    auto qoff = [&](int64_t q) -> int64_t { return D ? ix.coff(q) : coff[q]; };
     const int lane = threadIdx.x & 63;
     const int64_t wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const u64 lt = (1ull << lane) - 1ull;
-    const int64_t total = coff[n];
     u64 n_cand = 0, n_typed = 0, n_ar = 0, n_hits = 0, n_inl = 0;
     for (int64_t k = wave; k < n_chunks; k += nwave) {
-        const int32_t q0 = __builtin_amdgcn_readfirstlane(chq[k]);
+        const int32_t q0 = __builtin_amdgcn_readfirstlane(D ? (int32_t)didx_last(ix, k * kFlatChunk, false) : chq[k]);
         // the chunk's window of query offsets: queries q0 .. q0 + 64
-        cw[lane] = q0 + lane <= n ? coff[q0 + lane] : INT64_MAX;
-        if (lane == 0) cw[kFlatChunk] = q0 + kFlatChunk <= n ? coff[q0 + kFlatChunk] : INT64_MAX;
+        cw[lane] = q0 + lane <= n ? qoff(q0 + lane) : INT64_MAX;
+        if (lane == 0) cw[kFlatChunk] = q0 + kFlatChunk <= n ? qoff(q0 + kFlatChunk) : INT64_MAX;
         __builtin_amdgcn_wave_barrier();
         const int64_t f = k * kFlatChunk + lane;
         const bool valid = f < total;
@@ -857,7 +927,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match_flat(
                 int32_t lo = q0, hi = n - 1;
                 while (lo < hi) {
                     const int32_t mid = (lo + hi + 1) >> 1;
-                    if (coff[mid] <= f) lo = mid; else hi = mid - 1;
+                    if (qoff(mid) <= f) lo = mid; else hi = mid - 1;
                 }
                 q = lo;
             } else {
@@ -874,7 +944,7 @@ __global__ void __launch_bounds__(256) hgx_pattern_match_flat(
         if (valid) {
             const QPlan pl = plan[q];
             const QDesc d = desc[q];
-            const int64_t ci = pl.beg + (f - coff[q]);
+            const int64_t ci = pl.beg + (f - qoff(q));
             const bool typed = d.t_end > d.t_beg && !pl.pad;
             hit = true;
             if (typed) {
@@ -1100,10 +1170,11 @@ __global__ void __launch_bounds__(kSpBlock) hgx_q_norm_sp(
     const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
     QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
     int32_t* __restrict__ d_type, int64_t* __restrict__ d_poff, int32_t* __restrict__ d_pat, int64_t* __restrict__ ncand,
-    int64_t* __restrict__ blk) {
+    int64_t* __restrict__ blk, int64_t* __restrict__ lpre, u64* __restrict__ ctr) {
     __shared__ int64_t ws[kSpBlock / 64];
     __shared__ int32_t wm[kSpBlock / 64];
     const int64_t q = (int64_t)blockIdx.x * kSpBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;   // the match's counter shards
     QPlan p{0, 0, 0, 0};
     int32_t bad = INT32_MAX, uns = INT32_MAX;
     if (q < n) {
@@ -1120,7 +1191,9 @@ __global__ void __launch_bounds__(kSpBlock) hgx_q_norm_sp(
         if (q == n - 1) d_poff[n] = pe;
         for (int64_t i = pb; i < pe; ++i) d_pat[i] = pat[i];
     }
-    const int64_t tot = block_sum<int64_t>(p.n, ws);
+    int64_t tot;
+    const int64_t lp = block_exclusive_scan<int64_t>(p.n, ws, tot);
+    if (q < n) lpre[q] = lp;
     bad = block_min(bad, wm);
     uns = block_min(uns, wm);
     if (threadIdx.x == 0) {
@@ -1136,9 +1209,11 @@ __global__ void __launch_bounds__(kSpBlock) hgx_q_plan_sp(int32_t n, const QDesc
                                                          const int32_t* __restrict__ types,
                                                          const int32_t* __restrict__ nop, const int64_t* __restrict__ inc_off,
                                                          const int32_t* __restrict__ ts_type, QPlan* __restrict__ plan,
-                                                         int64_t* __restrict__ ncand, int64_t* __restrict__ blk) {
+                                                         int64_t* __restrict__ ncand, int64_t* __restrict__ blk,
+                                                         int64_t* __restrict__ lpre, u64* __restrict__ ctr) {
     __shared__ int64_t ws[kSpBlock / 64];
     const int64_t q = (int64_t)blockIdx.x * kSpBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;
     QPlan p{0, 0, 0, 0};
     if (q < n) {
         const QDesc d = desc[q];
@@ -1154,7 +1229,9 @@ __global__ void __launch_bounds__(kSpBlock) hgx_q_plan_sp(int32_t n, const QDesc
         plan[q] = p;
         ncand[q] = p.n;
     }
-    const int64_t tot = block_sum<int64_t>(p.n, ws);
+    int64_t tot;
+    const int64_t lp = block_exclusive_scan<int64_t>(p.n, ws, tot);
+    if (q < n) lpre[q] = lp;
     if (threadIdx.x == 0) {
         blk[3 * blockIdx.x] = tot;
         blk[3 * blockIdx.x + 1] = INT32_MAX;
@@ -1266,6 +1343,10 @@ __global__ void __launch_bounds__(1024) hgx_q_place_bscan(int64_t nbp, int64_t* 
         __syncthreads();
     }
 }
+// D: the derived flat index (blk / lpre / nb; n_chunks_p, chq and coff unused; the block holding the last
+// chunk also publishes the chunk / candidate totals, the overflow flag and the bad / unsupported
+// queries), else the scanned one.
+template <bool D>
 __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n_chunks_p,
                                                   const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
                                                   const int32_t* __restrict__ link_atom, int64_t* __restrict__ outoff,
@@ -1273,10 +1354,26 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
                                                   const u64* __restrict__ ctr, u64* __restrict__ ctr_out, int32_t n,
                                                   const int32_t* __restrict__ chq, const int64_t* __restrict__ coff,
                                                   const u64* __restrict__ hitmask, int64_t* __restrict__ q_off,
-                                                  const int64_t* __restrict__ bpre) {
+                                                  const int64_t* __restrict__ bpre, const int64_t* __restrict__ blk,
+                                                  const int64_t* __restrict__ lpre, int32_t nb, int64_t cap_chunks,
+                                                  int64_t cap_cand) {
     __shared__ int64_t ws[4], c_off[kPlaceChunks], qb[2];
     __shared__ int32_t c_cnt[kPlaceChunks];
-    const int32_t nc = *n_chunks_p;
+    __shared__ int64_t bp[D ? kDerivedBlocks + 1 : 1];
+    __shared__ int32_t wm[4];
+    DIdx ix{bp, lpre, nb, n};
+    int32_t nc;
+    bool over;
+    if (D) {
+        didx_load(bp, ws, blk, nb);
+        const int64_t tk = bp[nb], tc = (tk + kFlatChunk - 1) / kFlatChunk;
+        over = tc > cap_chunks || tk > cap_cand;
+        nc = over ? 0 : (int32_t)tc;
+    } else {
+        nc = *n_chunks_p;
+        over = stat[2] != 0;
+    }
+    auto qoff = [&](int64_t q) -> int64_t { return D ? ix.coff(q) : coff[q]; };
     const int64_t k0 = (int64_t)blockIdx.x * kPlaceChunks;
     if (k0 > 0 && k0 >= nc) return;   // beyond the chunks (block 0 always runs: it publishes an empty result)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1294,18 +1391,22 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
         int64_t res = 0;
         if (e == 1 && holds_last) {
             res = (int64_t)n + 1;
-        } else if (kb > 0 && !stat[2]) {
+        } else if (kb > 0 && !over) {
             const int64_t target = kb * kFlatChunk;
-            const int64_t q0 = chq[kb];
-            if (coff[q0] < target) {
-                res = q0 + 1;
+            if (D) {
+                res = didx_last(ix, target, true) + 1;
             } else {
-                for (int64_t hi = q0;; hi -= 64) {   // wave-uniform; coff[hi] >= target
-                    const int64_t j = hi - 64 + lane;
-                    const u64 m = __ballot(j < 0 || coff[j < 0 ? 0 : j] < target);
-                    if (m) {
-                        res = hi - 64 + (63 - __clzll((long long)m)) + 1;
-                        break;
+                const int64_t q0 = chq[kb];
+                if (coff[q0] < target) {
+                    res = q0 + 1;
+                } else {
+                    for (int64_t hi = q0;; hi -= 64) {   // wave-uniform; coff[hi] >= target
+                        const int64_t j = hi - 64 + lane;
+                        const u64 m = __ballot(j < 0 || coff[j < 0 ? 0 : j] < target);
+                        if (m) {
+                            res = hi - 64 + (63 - __clzll((long long)m)) + 1;
+                            break;
+                        }
                     }
                 }
             }
@@ -1352,18 +1453,35 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
         if (row[u] >= 0) ids[c_off[wv * 16 + u] + lane] = at[u];
     // the result offsets of the queries starting in this block's chunks, from the chunk offsets in LDS
     // and the chunk's hit mask (the offsets launch folded in)
-    if (!stat[2]) {
+    if (!over) {
         for (int64_t q = qb[0] + threadIdx.x; q < qb[1]; q += 256) {
-            const int64_t cf = coff[q], kq = cf / kFlatChunk, lc = kq - k0;
+            const int64_t cf = qoff(q), kq = cf / kFlatChunk, lc = kq - k0;
             const u64 hm = kq < nc ? hitmask[kq] : 0ull;
             q_off[q] = (lc < kPlaceChunks ? c_off[lc] : ws[0]) + __popcll(hm & ((1ull << (cf % kFlatChunk)) - 1ull));
         }
     }
     if (holds_last) {
+        if (D) {   // the scan kernel's statistics: totals, overflow, smallest bad / unsupported query
+            int32_t bad = INT32_MAX, uns = INT32_MAX;
+            for (int j = threadIdx.x; j < nb; j += 256) {
+                bad = min(bad, (int32_t)blk[3 * j + 1]);
+                uns = min(uns, (int32_t)blk[3 * j + 2]);
+            }
+            bad = block_min(bad, wm);
+            uns = block_min(uns, wm);
+            if (threadIdx.x == 0) {
+                const int64_t tk = bp[nb];
+                stat[0] = (tk + kFlatChunk - 1) / kFlatChunk;
+                stat[1] = tk;
+                stat[2] = over ? 1 : 0;
+                stat[4] = bad;
+                stat[5] = uns;
+            }
+        }
         if (threadIdx.x == 0) {
             const int64_t tot = ws[0];
             outoff[nc] = tot;
-            stat[3] = stat[2] ? 0 : tot;
+            stat[3] = over ? 0 : tot;
         }
         if (threadIdx.x < qNum) {
             u64 v = 0;
@@ -2328,6 +2446,8 @@ struct Front {
     int32_t* err = nullptr;      // [2] device-side normalisation errors (packed front end), or null
     double cond_bytes = 0;       // condition bytes read by the match (algorithmic accounting)
     int64_t* blk = nullptr;      // single-pass pipeline: [3 per block of 256 queries] candidates, bad, unsupported
+    int64_t* lpre = nullptr;     //   [n] candidates of the queries before q in its block of 256
+    u64* ctr = nullptr;          //   the match's counter shards, zeroed by the front kernel
 };
 
 // Buffers taken from the graph pool for one call, released on every exit path.
@@ -2416,8 +2536,11 @@ void front_host(hgx_graph* g, int32_t n, const NormBatch& nb, Scratch& sc, Event
                    4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
     if (g->q_flat == 2) {   // single-pass pipeline: the plan + per-block candidate totals
         f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
+        f.lpre = (int64_t*)sc.take(sizeof(int64_t) * (size_t)std::max(n, 1));
+        f.ctr = (u64*)sc.take(sizeof(u64) * kQShards * kQStride);
         hgx_q_plan_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
-            n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop), g->inc_off, g->inc_ts_type, f.plan, f.ncand, f.blk);
+            n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop), g->inc_off, g->inc_ts_type, f.plan, f.ncand, f.blk,
+            f.lpre, f.ctr);
         HGX_CHECK_LAUNCH();
         return;
     }
@@ -2489,10 +2612,12 @@ void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d,
         int64_t* dpo = (int64_t*)sc.take(8 * (size_t)(n + 1));
         int32_t* dpa = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(l.n_pat, 1));
         f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
+        f.lpre = (int64_t*)sc.take(sizeof(int64_t) * (size_t)std::max(n, 1));
+        f.ctr = (u64*)sc.take(sizeof(u64) * kQShards * kQStride);
         hgx_q_norm_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
             n, g->A, (const int32_t*)(d + l.o_type), (const int64_t*)(d + l.o_ioff), (const int32_t*)(d + l.o_inc),
             (const int32_t*)(d + l.o_ho), (const int64_t*)(d + l.o_poff), (const int32_t*)(d + l.o_pat), g->inc_off,
-            g->inc_ts_type, desc, anch, nop, f.plan, dty, dpo, dpa, f.ncand, f.blk);
+            g->inc_ts_type, desc, anch, nop, f.plan, dty, dpo, dpa, f.ncand, f.blk, f.lpre, f.ctr);
         HGX_CHECK_LAUNCH();
         f.desc = desc;
         f.anch = anch;
@@ -2564,27 +2689,48 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
         u64* ctr_d = (u64*)(rd + m_ctr);
         int64_t* qoff_d = (int64_t*)(rd + m_qoff);
         int32_t* ids_d = (int32_t*)(rd + m_ids);
-        hgx_q_scan_sp<<<nblk, kSpBlock, 0, s>>>(n, f.ncand, f.blk, coff, chq, nch, capC, capK, stat_d, ctr);
-        HGX_CHECK_LAUNCH();
-        ev.rec(1, s);
-        hgx_pattern_match_flat<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
-            nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
-            g->inc_ts_row, g->tgt_off, g->tgt_idx, g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt,
-            hmask, ctr);
-        HGX_CHECK_LAUNCH();
-        ev.rec(2, s);
         const int64_t nbp = std::max<int64_t>(1, ceil_div(capC, kPlaceChunks));
-        int64_t* bpre = nullptr;
-        if (nbp > kPlaceDirectBlocks) {
-            bpre = (int64_t*)w.take(sizeof(int64_t) * (nbp + 1));
-            hgx_q_place_bsum<<<grid_for(nbp, 256, 4096), 256, 0, s>>>(nch, cnt, nbp, bpre);
+        // derived flat index: no scan launch between the front kernel and the match (its counter shards
+        // were zeroed by the front kernel; a re-run after a workspace overflow zeroes them here)
+        const bool derived = f.lpre && nblk <= kDerivedBlocks && nbp <= kPlaceDirectBlocks;
+        const int4* tt = g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr;
+        if (derived) {
+            ctr = f.ctr;
+            if (attempt > 0) HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
+            ev.rec(1, s);
+            hgx_pattern_match_flat<true><<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+                nullptr, n, nullptr, nullptr, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row,
+                g->inc_type, g->inc_ts_row, g->tgt_off, g->tgt_idx, tt, slots, cnt, hmask, ctr, f.blk, f.lpre, nblk, capC,
+                capK);
             HGX_CHECK_LAUNCH();
-            hgx_q_place_bscan<<<1, 1024, 0, s>>>(nbp, bpre);
+            ev.rec(2, s);
+            hgx_q_place<true><<<(unsigned)nbp, 256, 0, s>>>(nullptr, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr,
+                                                            ctr_d, n, nullptr, nullptr, hmask, qoff_d, nullptr, f.blk,
+                                                            f.lpre, nblk, capC, capK);
             HGX_CHECK_LAUNCH();
         }
-        hgx_q_place<<<(unsigned)nbp, 256, 0, s>>>(nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr, ctr_d,
-                                                  n, chq, coff, hmask, qoff_d, bpre);
-        HGX_CHECK_LAUNCH();
+        if (!derived) {
+            hgx_q_scan_sp<<<nblk, kSpBlock, 0, s>>>(n, f.ncand, f.blk, coff, chq, nch, capC, capK, stat_d, ctr);
+            HGX_CHECK_LAUNCH();
+            ev.rec(1, s);
+            hgx_pattern_match_flat<false><<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+                nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
+                g->inc_ts_row, g->tgt_off, g->tgt_idx, tt, slots, cnt, hmask, ctr, nullptr, nullptr, 0, 0, 0);
+            HGX_CHECK_LAUNCH();
+            ev.rec(2, s);
+            int64_t* bpre = nullptr;
+            if (nbp > kPlaceDirectBlocks) {
+                bpre = (int64_t*)w.take(sizeof(int64_t) * (nbp + 1));
+                hgx_q_place_bsum<<<grid_for(nbp, 256, 4096), 256, 0, s>>>(nch, cnt, nbp, bpre);
+                HGX_CHECK_LAUNCH();
+                hgx_q_place_bscan<<<1, 1024, 0, s>>>(nbp, bpre);
+                HGX_CHECK_LAUNCH();
+            }
+            hgx_q_place<false><<<(unsigned)nbp, 256, 0, s>>>(nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr,
+                                                             ctr_d, n, chq, coff, hmask, qoff_d, bpre, nullptr, nullptr,
+                                                             0, 0, 0);
+            HGX_CHECK_LAUNCH();
+        }
         ev.rec(3, s);
         spin_sync(s);
         const int64_t* stat = (const int64_t*)(hm + m_stat);
@@ -2674,10 +2820,10 @@ void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, h
             HGX_CHECK_LAUNCH();
         }
         ev.rec(1, s);
-        hgx_pattern_match_flat<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
+        hgx_pattern_match_flat<false><<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
             nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
             g->inc_ts_row, g->tgt_off, g->tgt_idx, g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt,
-            hmask, ctr);
+            hmask, ctr, nullptr, nullptr, 0, 0, 0);
         HGX_CHECK_LAUNCH();
         ev.rec(2, s);
         if (small) {

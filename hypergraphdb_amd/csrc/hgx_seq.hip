@@ -694,6 +694,352 @@ __global__ void __launch_bounds__(kSbThreads) hgx_seq_block(SbArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Set-mode workgroup engine (hgx_bfs_batch, HGX_OPT_BFS_BLOCK): the per-depth visited sets V_d of
+// one seed inside one workgroup -- the batched engine's result for a traversal that stays small
+// (config 5: 1018 of 1024 hg.subsumed closures and every hg.subsumes closure hold <= 1265 atoms, but
+// reach 21-24 levels deep, and the batched engine pays two launches and a host turn-around per level
+// for every level of the deepest one).  Same yields as the order-exact engine above (the generator's
+// link predicate, minimum arity, position rule and yield flags), without the ranking: a set needs no
+// FIFO order, so the first arrival that claims an atom's hash slot makes it a member of the next
+// level, and the level is the claimed slots.  LDS per workgroup ~37 KB (four workgroups per CU, 16
+// waves): a hash of 2048 slots holding <= 1535 atoms, a 1024-entry frontier table and a 2048-item
+// staging area; a seed that outgrows any of them (or meets a frontier of more than kBbItemLimit
+// incidence entries) reports -1 and runs on the batched engine.
+constexpr int kBbThreads = 256;
+constexpr int kBbWaves = kBbThreads / 64;
+constexpr int kBbHash = 2048;
+constexpr int kBbDisc = 1535;                        // examined atoms incl. the seed (load <= 3/4)
+constexpr int kBbPairs = kBbDisc - 1;                // atoms one seed may return past V_0
+constexpr int kBbFront = 1024;
+constexpr int kBbCand = 2048;
+constexpr int kBbU = 2;
+constexpr int64_t kBbItemLimit = (int64_t)1 << 22;
+constexpr int kBbChunk = 4096;                       // seeds per launch (mapped output per launch)
+
+struct BbArgs {
+    int32_t n;
+    const int32_t* seeds;                            // device seeds (n > kSbInline)
+    int32_t seed_inline[kSbInline];
+    const int64_t* inc_off;
+    const int32_t* inc_row;
+    const int32_t* inc_type;
+    const uint8_t* yf;                               // ordered-mode yield flags; null in the symmetric mode
+    const int64_t* tgt_off;
+    const int32_t* tgt_idx;
+    int32_t want_type, min_arity, mode, maxd;
+    int32_t* out_atom;                               // [n * kBbPairs] (mapped host memory)
+    int32_t* out_cnt;                                // [n * kBbPairs]: |V_{d+1}| at d
+    int64_t* meta;                                   // [4 n]: atoms (-1 = rerun), traversed items, bytes,
+                                                     //        levels with news | levels expanded << 32
+};
+
+struct BbShared {
+    int32_t h_atom[kBbHash];
+    uint32_t h_new[kBbHash / 32];                    // slot claimed at the current level
+    int64_t e_fb[kBbFront];
+    int32_t e_atom[kBbFront];
+    int32_t e_dp[kBbFront + 1];
+    int32_t e_sp[kBbFront + 1];
+    int32_t cand[kBbCand];
+    int64_t wsum[kBbWaves];
+    int64_t T, S;
+    int32_t cand_n, n_disc, ovf;
+};
+
+__device__ __forceinline__ int64_t bb_scan(BbShared& sm, int64_t v, int64_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) sm.wsum[w] = x;
+    __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kBbWaves; ++k) {
+        const int64_t t = sm.wsum[k];
+        base += k < w ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+__device__ __forceinline__ uint32_t bb_hash(int32_t t) { return ((uint32_t)t * 0x9E3779B1u) >> 21; }
+
+// Examined-set insert: a slot is reserved before it is claimed and the reservation is returned when
+// another lane claims it first, so the table never holds more than kBbDisc atoms.
+__device__ __forceinline__ void bb_insert(BbShared& sm, int32_t t) {
+    uint32_t h = bb_hash(t);
+    for (;;) {
+        int32_t x = sm.h_atom[h];
+        if (x == t) return;
+        if (x == -1) {
+            if (atomicAdd(&sm.n_disc, 1) >= kBbDisc) {
+                sm.ovf = 1;
+                return;
+            }
+            x = atomicCAS(&sm.h_atom[h], -1, t);
+            if (x == -1) {
+                atomicOr(&sm.h_new[h >> 5], 1u << (h & 31));
+                return;
+            }
+            atomicSub(&sm.n_disc, 1);
+            if (x == t) return;
+        }
+        h = (h + 1) & (kBbHash - 1);
+    }
+}
+
+__device__ void bb_frontier(BbShared& sm, const BbArgs& a, int F) {
+    const int tid = threadIdx.x;
+    constexpr int K = kBbFront / kBbThreads;
+    int64_t dg[K], sg[K], ds = 0, ss = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = tid * K + k;
+        dg[k] = sg[k] = 0;
+        if (i < F) {
+            const int32_t p = sm.e_atom[i];
+            const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
+            sm.e_fb[i] = b;
+            dg[k] = e - b;
+            sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+        }
+        ds += dg[k];
+        ss += sg[k];
+    }
+    int64_t T, S;
+    int64_t dp = bb_scan(sm, ds, &T);
+    int64_t sp = bb_scan(sm, ss, &S);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = tid * K + k;
+        if (i < F) {
+            sm.e_dp[i] = (int32_t)dp;   // exact whenever T <= kBbItemLimit (checked by the level)
+            sm.e_sp[i] = (int32_t)sp;
+        }
+        dp += dg[k];
+        sp += sg[k];
+    }
+    if (tid == 0) {
+        sm.e_dp[F] = (int32_t)(T < INT32_MAX ? T : INT32_MAX);
+        sm.e_sp[F] = (int32_t)(S < INT32_MAX ? S : INT32_MAX);
+        sm.T = T;
+        sm.S = S;
+    }
+    __syncthreads();
+}
+
+// Staged items -> the generator's yields -> examined-set inserts (as sb_process, no keys).
+__device__ void bb_process(BbShared& sm, const BbArgs& a, int F, int cn, int64_t& nbytes) {
+    for (int c = threadIdx.x; c < cn; c += kBbThreads) {
+        const int32_t it = sm.cand[c];
+        const int i = sb_search(sm.e_dp, F, it);
+        const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
+        const int32_t p = sm.e_atom[i];
+        const int32_t L = a.inc_row[ii];
+        nbytes += a.want_type >= 0 ? 8 : 4;
+        if (a.want_type >= 0 && a.inc_type[ii] != a.want_type) continue;   // linkPredicate (:300)
+        const int64_t b = a.tgt_off[L];
+        const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
+        nbytes += 16 + 4 * (int64_t)n;
+        if (n < a.min_arity) continue;                                       // minArity (:309)
+        if (n <= 8) {
+            int32_t tg[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[b + q] : -1;
+            int32_t lo = 0, hi = n;
+            if (a.mode != sSym) {
+                int32_t fv = -1, lv = -1;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (tg[q] == p) {
+                        if (fv < 0) fv = q;
+                        lv = q;
+                    }
+                if (a.mode == sAfterFirst) lo = fv + 1;
+                else if (a.mode == sBeforeFirst) hi = fv;
+                else if (a.mode == sBeforeLast) hi = lv;
+                else lo = lv + 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q >= lo && q < hi && tg[q] != p) bb_insert(sm, tg[q]);
+        } else {
+            int32_t lo = 0, hi = n;
+            if (a.mode != sSym) {
+                int32_t fv = -1, lv = -1;
+                for (int32_t q = 0; q < n; ++q)
+                    if (a.tgt_idx[b + q] == p) {
+                        if (fv < 0) fv = q;
+                        lv = q;
+                    }
+                if (a.mode == sAfterFirst) lo = fv + 1;
+                else if (a.mode == sBeforeFirst) hi = fv;
+                else if (a.mode == sBeforeLast) hi = lv;
+                else lo = lv + 1;
+            }
+            for (int32_t q = lo; q < hi; ++q) {
+                const int32_t t = a.tgt_idx[b + q];
+                if (t != p) bb_insert(sm, t);
+            }
+        }
+    }
+}
+
+__device__ void bb_run(BbShared& sm, const BbArgs& a, int si) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int32_t seed = a.n <= kSbInline ? a.seed_inline[si] : a.seeds[si];
+    for (int i = tid; i < kBbHash; i += kBbThreads) sm.h_atom[i] = -1;
+    if (tid < kBbHash / 32) sm.h_new[tid] = 0u;
+    if (tid == 0) {
+        sm.cand_n = 0;
+        sm.n_disc = 1;
+        sm.ovf = 0;
+        sm.e_atom[0] = seed;
+    }
+    __syncthreads();
+    if (tid == 0) sm.h_atom[bb_hash(seed)] = seed;   // examined.put(start, TRUE) (HGBreadthFirstTraversal.java:42-46)
+    bb_frontier(sm, a, 1);
+    const int64_t obase = (int64_t)si * kBbPairs;
+    int F = 1;
+    int64_t trav = 0, out_n = 0, nbytes = 0, n_lev = 0, n_exp = 0;
+    bool ovf = false;
+    for (int32_t d = 0; d < a.maxd && F > 0; ++d) {
+        const int64_t T = sm.T, S = sm.S;
+        trav += T;
+        n_exp = d + 1;
+        nbytes += tid == 0 ? 16 * (int64_t)F + (a.yf ? T : 0) : 0;   // frontier offsets, streamed yield flags
+        if (T == 0) break;
+        if (T > kBbItemLimit) {
+            ovf = true;
+            break;
+        }
+        // (1) stream the frontier's incidence and stage the entries that can yield; a lane keeps the
+        // entries that did not fit the staging area and stages them after the next flush through (2)
+        bool stop = false;
+        for (int64_t sb = 0; sb < S && !stop; sb += (int64_t)kBbThreads * kBbU) {
+            uint4 v[kBbU];
+            int64_t lo_[kBbU], hi_[kBbU], ad_[kBbU], it_[kBbU];
+#pragma unroll
+            for (int u = 0; u < kBbU; ++u) {
+                const int64_t s = sb + (int64_t)u * kBbThreads + tid;
+                v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                lo_[u] = hi_[u] = ad_[u] = it_[u] = 0;
+                if (s < S) {
+                    const int i = sb_search(sm.e_sp, F, s);
+                    lo_[u] = sm.e_fb[i];
+                    hi_[u] = lo_[u] + (sm.e_dp[i + 1] - sm.e_dp[i]);
+                    ad_[u] = ((lo_[u] >> 4) + (s - sm.e_sp[i])) << 4;
+                    it_[u] = sm.e_dp[i] + (ad_[u] - lo_[u]);
+                    if (a.yf) v[u] = *(const uint4*)(a.yf + ad_[u]);
+                }
+            }
+            for (int u = 0; u < kBbU; ++u) {
+                const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t mask = 0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t pos = ad_[u] + q;
+                    const bool y = a.yf ? ((wv[q >> 2] >> (8 * (q & 3) + a.mode)) & 1u) != 0 : true;
+                    if (pos >= lo_[u] && pos < hi_[u] && y) mask |= 1u << q;
+                }
+                const bool last = sb + (int64_t)(u + 1) * kBbThreads >= S;
+                for (;;) {
+                    const int cnt = __popc(mask);
+                    int x = cnt;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const int y = __shfl_up(x, off);
+                        if (lane >= off) x += y;
+                    }
+                    const int wtot = __shfl(x, 63);
+                    int base = 0;
+                    if (lane == 63 && wtot) base = atomicAdd(&sm.cand_n, wtot);
+                    base = __shfl(base, 63);
+                    int o = base + x - cnt;
+                    for (uint32_t m = mask; m; m &= m - 1, ++o) {
+                        const int q = __ffs(m) - 1;
+                        if (o < kBbCand) {
+                            sm.cand[o] = (int32_t)(it_[u] + q);
+                            mask &= ~(1u << q);
+                        }
+                    }
+                    __syncthreads();
+                    const int staged = sm.cand_n;
+                    const bool more = __syncthreads_or(mask != 0u) != 0;
+                    const int cn = min(staged, kBbCand);
+                    if (cn > 0 && (more || last || cn > kBbCand / 2)) {
+                        // (2) the staged entries' links and yields
+                        bb_process(sm, a, F, cn, nbytes);
+                        __syncthreads();
+                        if (tid == 0) sm.cand_n = 0;
+                        __syncthreads();
+                        if (sm.ovf) {
+                            stop = true;
+                            break;
+                        }
+                    }
+                    if (!more) break;
+                }
+                if (last || stop) break;
+            }
+        }
+        __syncthreads();
+        if (sm.ovf) {
+            ovf = true;
+            break;
+        }
+        // (3) the claimed slots are V_{d+1}: the next frontier, appended to the seed's output
+        constexpr int K = kBbHash / kBbThreads;
+        const uint32_t nm = (sm.h_new[tid * K / 32] >> ((tid * K) & 31)) & ((1u << K) - 1u);
+        int64_t n_new;
+        int o = (int)bb_scan(sm, __popc(nm), &n_new);
+        if (n_new == 0) break;
+        if (n_new > kBbFront) {
+            ovf = true;
+            break;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if ((nm >> k) & 1u) {
+                const int32_t t = sm.h_atom[tid * K + k];
+                sm.e_atom[o] = t;
+                a.out_atom[obase + out_n + o] = t;
+                ++o;
+            }
+        __syncthreads();
+        if (tid < kBbHash / 32) sm.h_new[tid] = 0u;
+        if (tid == 0) a.out_cnt[obase + d] = (int32_t)n_new;
+        out_n += n_new;
+        n_lev = d + 1;
+        nbytes += tid == 0 ? 4 * n_new + 4 : 0;   // the atoms and the level count written
+        F = (int)n_new;
+        bb_frontier(sm, a, F);
+    }
+    int64_t tb;
+    bb_scan(sm, nbytes, &tb);
+    if (tid == 0) {
+        a.meta[4 * (int64_t)si] = ovf ? -1 : out_n;
+        a.meta[4 * (int64_t)si + 1] = trav;
+        a.meta[4 * (int64_t)si + 2] = tb;
+        a.meta[4 * (int64_t)si + 3] = n_lev | (n_exp << 32);
+    }
+}
+
+__global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
+    __shared__ BbShared sm;
+    for (int si = blockIdx.x; si < a.n; si += gridDim.x) {
+        bb_run(sm, a, si);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Level-synchronous engine (the traversals a workgroup cannot hold: more than kSbPairs pairs).
 //
 // Per level six kernels with fixed grids that read every size from device memory, so the host never
@@ -1466,6 +1812,108 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 }
 
 }  // namespace
+
+void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
+               BlockSet& out) {
+    hipStream_t st = g->stream;
+    const int mode = seq_mode(o);
+    if (mode != sSym) ensure_inc_yield(g);
+    out.seeds.assign(seeds, seeds + n_seeds);
+    out.atoms.assign((size_t)n_seeds, nullptr);
+    out.lcnt.assign((size_t)n_seeds, nullptr);
+    out.pairs.assign((size_t)n_seeds, -1);
+    out.levels.assign((size_t)n_seeds, 0);
+    BbArgs a{};
+    a.inc_off = g->inc_off;
+    a.inc_row = g->inc_row;
+    a.inc_type = g->inc_type;
+    a.yf = mode != sSym ? g->inc_yf : nullptr;
+    a.tgt_off = g->tgt_off;
+    a.tgt_idx = g->tgt_idx;
+    a.want_type = o.link_type;
+    a.min_arity = o.return_source ? 1 : 2;
+    a.mode = mode;
+    a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
+    const size_t per_seed = (size_t)kBbPairs * 8 + 32;
+    int32_t* dseeds = nullptr;
+    size_t dseeds_n = 0;
+    if (n_seeds > kSbInline) {
+        dseeds_n = sizeof(int32_t) * (size_t)n_seeds;
+        dseeds = (int32_t*)g->alloc(dseeds_n);
+        int32_t* hs = (int32_t*)g->pinned_buf(dseeds_n);
+        std::memcpy(hs, seeds, dseeds_n);
+        HGX_HIP(hipMemcpyAsync(dseeds, hs, dseeds_n, hipMemcpyHostToDevice, st));
+    }
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (g->timing) {
+        HGX_HIP(hipEventCreate(&ev[0]));
+        HGX_HIP(hipEventCreate(&ev[1]));
+        HGX_HIP(hipEventRecord(ev[0], st));
+    }
+    struct Chunk {
+        int64_t c0, nb;
+        char* h;
+    };
+    std::vector<Chunk> chunks;
+    for (int64_t c0 = 0; c0 < n_seeds; c0 += kBbChunk) {
+        const int64_t nb = std::min<int64_t>(kBbChunk, n_seeds - c0);
+        PoolBuf hb = take_host_buf(g, per_seed * (size_t)nb);
+        out.bufs.push_back(hb);
+        void* dv = nullptr;
+        HGX_HIP(hipHostGetDevicePointer(&dv, hb.p, 0));
+        char* d = (char*)dv;
+        // layout: meta [4 nb] int64 | atoms [nb * kBbPairs] | level counts [nb * kBbPairs]
+        a.n = (int32_t)nb;
+        a.meta = (int64_t*)d;
+        a.out_atom = (int32_t*)(d + 32 * nb);
+        a.out_cnt = a.out_atom + nb * kBbPairs;
+        if (n_seeds <= kSbInline) {
+            for (int64_t i = 0; i < nb; ++i) a.seed_inline[i] = seeds[c0 + i];
+            a.seeds = nullptr;
+        } else {
+            a.seeds = dseeds + c0;
+        }
+        hgx_bfs_block<<<(unsigned)nb, kBbThreads, 0, st>>>(a);
+        HGX_CHECK_LAUNCH();
+        chunks.push_back({c0, nb, (char*)hb.p});
+    }
+    if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+    spin_sync(st);
+    if (ev[1]) {
+        float ms = 0;
+        HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        out.ms = ms;
+        (void)hipEventDestroy(ev[0]);
+        (void)hipEventDestroy(ev[1]);
+    }
+    if (dseeds) g->release(dseeds, dseeds_n);
+    for (auto& c : chunks) {
+        const int64_t* meta = (const int64_t*)c.h;
+        const int32_t* at = (const int32_t*)(c.h + 32 * c.nb);
+        const int32_t* lc = at + c.nb * kBbPairs;
+        for (int64_t i = 0; i < c.nb; ++i) {
+            const int64_t si = c.c0 + i;
+            out.bytes += (double)meta[4 * i + 2];
+            if (meta[4 * i] < 0) {
+                out.rerun.push_back((int32_t)si);
+                continue;
+            }
+            out.pairs[si] = (int32_t)meta[4 * i];
+            out.levels[si] = (int32_t)(meta[4 * i + 3] & 0xFFFFFFFF);
+            out.expanded = std::max(out.expanded, (int32_t)(meta[4 * i + 3] >> 32));
+            out.traversed += (double)meta[4 * i + 1];
+            out.atoms[si] = at + i * kBbPairs;
+            out.lcnt[si] = lc + i * kBbPairs;
+        }
+    }
+}
+
+void block_release(hgx_graph* g, BlockSet& b) {
+    std::lock_guard<std::mutex> lk(g->seq_mu);
+    for (auto& x : b.bufs) g->seq_hbufs.push_back(x);
+    b.bufs.clear();
+}
+
 }  // namespace hgx
 
 using namespace hgx;

@@ -137,6 +137,12 @@ typedef struct hgx_bfs_stats {
     /* partitioned BFS: host round trips of level d's exchange (count / statistics read-backs and
      * count all-gathers; the row transfers are not counted), the largest over the parts' batches */
     int32_t level_xtrips[64];
+    /* the workgroup-per-seed stage (HGX_OPT_BFS_BLOCK): device ms of its launches (timing on), their
+     * algorithmic bytes, the seeds it finished and the seeds handed to the level engine */
+    double  ms_block;
+    double  bytes_block;
+    int64_t block_seeds;
+    int64_t block_rerun;
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
@@ -471,6 +477,12 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * 1 = every seed on the round-1 key-array engine (rocPRIM sort, two host round trips a level; A/B);
  * 2 = every seed on the level-synchronous engine (tests). */
 #define HGX_OPT_SEQ_ENGINE 13
+/* HGX_OPT_BFS_BLOCK (default 1): hgx_bfs_batch on a whole snapshot first runs every seed in one
+ * workgroup (its visited set, frontier and staging in LDS, all its levels in one launch; V_d written
+ * into mapped host memory); the seeds whose traversal outgrows the workgroup (more than 1534 atoms,
+ * a level wider than 1024 atoms, or a frontier of more than 4M incidence entries) then run on the
+ * batched rows engine.  0 = every seed on the rows engine.  Results are identical either way. */
+#define HGX_OPT_BFS_BLOCK 14
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */
 int  hgx_query_coalesce_stats(hgx_graph *g, int64_t *device_batches, int64_t *caller_batches);

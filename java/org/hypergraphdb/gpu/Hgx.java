@@ -19,7 +19,7 @@ final class Hgx
     static final int OPT_BFS_FLAGS = 1, OPT_SEQ_BUDGET = 2, OPT_RANKS_ORDERED = 3, OPT_PART_SERIAL = 4;
     static final int OPT_QUERY_FUSED = 5, OPT_QUERY_INLINE = 6, OPT_PUSH_BATCH = 7, OPT_PART_EXCHANGE = 8,
                      OPT_QUERY_FLAT = 9, OPT_CODED = 10, OPT_QUERY_COALESCE = 11, OPT_PUSH_INLINE = 12,
-                     OPT_SEQ_ENGINE = 13;   // include/hgx.h
+                     OPT_SEQ_ENGINE = 13, OPT_BFS_BLOCK = 14;   // include/hgx.h
 
     // ---- snapshot (hgx_graph_create / open / destroy / update / info) ---------------------------
     static native long graphCreate(long numAtoms, int[] linkAtom, long[] tgtOff, int[] tgtIdx, int[] linkType,

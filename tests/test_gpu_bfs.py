@@ -240,6 +240,7 @@ def test_engine_option_matrix(flags):
     for i, (g, mode, lt, maxd) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
         snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
+        snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)   # the rows engine's variants (not the workgroup stage)
         seeds = rng.integers(0, g["num_atoms"], 1024 if i == 2 else 300).astype(np.int32)   # W = 16 and W < 16
         check_batch(g, seeds, maxd, mode, lt, snap, orc)
 
@@ -262,9 +263,10 @@ def test_nonfull_pull_levels(n_seeds, lt):
     """Late dense levels where most incidence sits on atoms visited by every traversal run the
     non-full pull (level kind 3); per-depth sets stay identical to the oracle's, unbounded and
     with a link type."""
-    from hypergraphdb_amd import bfs_batch, synth
+    from hypergraphdb_amd import _lib, bfs_batch, synth
     g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=14)
     snap, orc = snapshot(g), oracle(g)
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
     # seeds with (typed) incidence: every traversal covers the same component, so atoms become full
     off, tg = g["tgt_off"], g["tgt_idx"]
     rows = np.nonzero(g["link_type"] == lt)[0] if lt >= 0 else np.arange(len(off) - 1)
@@ -294,6 +296,7 @@ def test_push_batch_all_modes(batch):
     for gi, (g, lt, maxd, ns) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
         snap.set_option(_lib.HGX_OPT_PUSH_BATCH, batch)
+        snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
         if gi == 2:
             lt = int(g["subsumes_type"])
             modes = [(False, True, False, False), (False, True, True, False)]
@@ -319,6 +322,7 @@ def test_push_inline_records_all_modes(inline):
     for gi, (g, lt, maxd, ns) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
         snap.set_option(_lib.HGX_OPT_PUSH_INLINE, inline)
+        snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
         if gi == 2:
             lt = int(g["subsumes_type"])
             modes = [(False, True, False, False), (False, True, True, False)]
@@ -346,7 +350,117 @@ def test_coded_levels(coded):
     for g, lt, maxd, ns in cases:
         snap, orc = snapshot(g), oracle(g)
         snap.set_option(_lib.HGX_OPT_CODED, coded)
+        snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
         seeds = rng.integers(0, g["num_atoms"], ns).astype(np.int32)
         for flags in (0x3BE, 0x3BA, 0x1BE):
             snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
             check_batch(g, seeds, maxd, K.ALGEN_MODES[0], lt, snap, orc)
+
+
+def _all_levels(res):
+    return [gpu_levels(res, i) for i in range(res.n_seeds)]
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_workgroup_stage_vs_rows_engine(case):
+    """HGX_OPT_BFS_BLOCK: the workgroup-per-seed stage (its seeds' V_d from LDS) + the rows engine on
+    the seeds that outgrew it give exactly the rows engine's per-depth sets, counts, depth_of and
+    TEPS numerator -- every generator mode, typed links, depth limits 0..4 and unbounded, links
+    targeting links, repeated targets, seeds without incidence, duplicate seeds, inline (<= 32) and
+    device seed lists, > 4096 seeds (two launches), and batches where some seeds overflow the
+    workgroup (hubs) next to small ones."""
+    from hypergraphdb_amd import _lib, bfs_batch, synth
+    rng = np.random.default_rng(700 + case)
+    if case < 3:
+        g = K.random_graph(rng, int(rng.integers(300, 2500)), int(rng.integers(100, 1800)), max_arity=9,
+                           link_targets=case != 1, n_types=3)
+    elif case < 5:
+        g = synth.hypergraph(8000, 9000, 2, 6, 2.1, 2, seed=80 + case)
+    else:
+        g = synth.config5(scale=0.002, n_sources=300)
+    snap = snapshot(g)
+    n_seeds = [20, 700, 4500, 300, 1024, 300][case]
+    seeds = rng.integers(0, g["num_atoms"], n_seeds).astype(np.int32)
+    seeds[-1] = seeds[0]
+    mixed = False
+    for mi, mode in enumerate(K.ALGEN_MODES):
+        lt = [-1, 0, 1, -1, 2, -1][(mi + case) % 6] if case != 5 else int(g["subsumes_type"])
+        for maxd in ((None, 0, 2) if case != 2 else (None, 3)):
+            res = {}
+            for blk in (1, 0):
+                snap.set_option(_lib.HGX_OPT_BFS_BLOCK, blk)
+                r = bfs_batch(snap, seeds, maxd, gen(snap, mode, lt))
+                res[blk] = (r.counts().copy(), _all_levels(r) if case != 2 else None,
+                            r.stats()["traversed_edges"], r.stats(accounting=False), r)
+            (c1, l1, t1, s1, r1), (c0, l0, t0, s0, r0) = res[1], res[0]
+            n = max(c1.shape[1], c0.shape[1])
+            pad = lambda c: np.pad(c, ((0, 0), (0, n - c.shape[1])))
+            assert np.array_equal(pad(c1), pad(c0)), (case, mi, maxd)
+            assert l1 == l0, (case, mi, maxd)
+            assert t1 == t0, (case, mi, maxd)
+            assert s1["block_seeds"] + s1["block_rerun"] == n_seeds and s0["block_seeds"] == 0
+            mixed |= s1["block_seeds"] > 0 and s1["block_rerun"] > 0
+            for i in range(0, n_seeds, max(1, n_seeds // 7)):
+                for a in rng.integers(0, g["num_atoms"], 4).tolist() + [int(seeds[i])]:
+                    assert r1.depth_of(i, a) == r0.depth_of(i, a), (case, mi, maxd, i, a)
+            r1.close()
+            r0.close()
+    if case in (3, 4):
+        assert mixed   # hubs pushed some seeds onto the rows engine next to workgroup seeds
+    snap.close()
+
+
+def test_workgroup_stage_vs_oracle_and_capacity_edges():
+    """Seeds whose closure sits just below / above the workgroup's 1534 atoms and 1024-atom levels
+    (a path, a star, a binary tree), against the oracle."""
+    from hypergraphdb_amd import _lib, bfs_batch
+    # star: centre 0 with k leaves as one link each -> level 1 of k atoms
+    rows = []
+    for k, base in ((1024, 0), (1025, 2000)):
+        rows += [[base, base + 1 + j] for j in range(k)]
+    # path of 1600 atoms (1599 pairs past the seed: overflows on atom count, not width)
+    rows += [[4000 + j, 4001 + j] for j in range(1599)]
+    # binary tree of 1535 nodes (1534 past the root)
+    rows += [[6000 + j, 6000 + 2 * j + 1, 6000 + 2 * j + 2] for j in range(767)]
+    A = 8000
+    tgt_off = np.zeros(len(rows) + 1, np.int64)
+    tgt_off[1:] = np.cumsum([len(r) for r in rows])
+    g = dict(num_atoms=A + len(rows), link_atom=np.arange(A, A + len(rows), dtype=np.int32), tgt_off=tgt_off,
+             tgt_idx=np.concatenate(rows).astype(np.int32), link_type=None)
+    snap, orc = snapshot(g), oracle(g)
+    seeds = np.array([0, 2000, 4000, 4800, 6000, 6001, 7999], np.int32)
+    check_batch(g, seeds, None, K.ALGEN_MODES[0], -1, snap, orc)
+    check_batch(g, seeds, 5, K.ALGEN_MODES[2], -1, snap, orc)
+    r = bfs_batch(snap, seeds, None)
+    st = r.stats(accounting=False)
+    r.close()
+    assert st["block_seeds"] >= 3 and st["block_rerun"] >= 2, st
+
+
+def test_config5_full_workgroup_stage():
+    """Config 5 at full size (5M classes, the bench's 1024 classes): with the workgroup stage on,
+    hg.subsumed / hg.subsumes counts and traversed items equal the rows engine's; the big
+    hg.subsumed closures go to the rows engine, every hg.subsumes closure stays in a workgroup;
+    sampled sets against the oracle."""
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_batch, synth
+    g = synth.config5()
+    snap, orc = snapshot(g), oracle(g)
+    T = g["subsumes_type"]
+    for rev in (False, True):
+        gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
+        out = {}
+        for blk in (1, 0):
+            snap.set_option(_lib.HGX_OPT_BFS_BLOCK, blk)
+            r = bfs_batch(snap, g["seeds"], None, gen_)
+            out[blk] = (r.counts().copy(), r.stats()["traversed_edges"], r.stats(accounting=False), r)
+        (c1, t1, s1, r1), (c0, t0, _, r0) = out[1], out[0]
+        assert np.array_equal(c1, c0) and t1 == t0, rev
+        big = int((c0[:, 1:].sum(1) > 1534).sum())   # closures beyond the workgroup's atoms
+        assert s1["block_rerun"] >= big and (s1["block_rerun"] == 0) == rev, (rev, s1["block_rerun"], big)
+        for i in (0, 5, 511, 1023):
+            lv = orc.bfs_levels(int(g["seeds"][i]), -1, algen(T, False, True, rev, False))
+            for d_, exp in enumerate(lv):
+                assert np.array_equal(r1.visited(i, d_), exp), (rev, i, d_)
+        r1.close()
+        r0.close()
+    snap.close()
