@@ -79,10 +79,11 @@ def roofline(stats_list, workload):
     from hypergraphdb_amd._lib import KERNELS
     tot = {k: {"ms": 0.0, "bytes": 0.0, "launches": 0} for k in KERNELS}
     for st in stats_list:
-        for k, v in st["kernels"].items():
-            tot[k]["ms"] += v["ms"]
-            tot[k]["bytes"] += v["bytes"]
-            tot[k]["launches"] += v["launches"]
+        for k, v in st["kernels"].items():   # + hgx_bfs_block when the workgroup stage ran
+            t = tot.setdefault(k, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+            t["ms"] += v["ms"]
+            t["bytes"] += v["bytes"]
+            t["launches"] += v["launches"]
     dom = max(tot, key=lambda k: tot[k]["ms"])
     t = tot[dom]
     achieved = t["bytes"] / (t["ms"] / 1e3) / 1e9 if t["ms"] > 0 else 0.0

@@ -87,18 +87,22 @@ class BfsStats(C.Structure):
                 ("level_xpair_max", C.c_double * 64), ("level_xms", C.c_double * 64),
                 ("xwords_nonzero", C.c_double), ("xwords_total", C.c_double), ("bytes_min", C.c_double),
                 ("level_xtrips", C.c_int32 * 64), ("ms_block", C.c_double), ("bytes_block", C.c_double),
-                ("block_seeds", C.c_int64), ("block_rerun", C.c_int64)]
+                ("block_seeds", C.c_int64), ("block_rerun", C.c_int64), ("ms_coop", C.c_double),
+                ("bytes_coop", C.c_double), ("block_coop", C.c_int64)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
              "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges,
              "ms_exchange": self.ms_exchange, "bytes_exchanged": self.bytes_exchanged, "bytes_min": self.bytes_min,
-             "block_seeds": int(self.block_seeds), "block_rerun": int(self.block_rerun)}
+             "block_seeds": int(self.block_seeds), "block_rerun": int(self.block_rerun),
+             "block_coop": int(self.block_coop)}
         d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
                             "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
         if self.block_seeds or self.block_rerun:   # the workgroup-per-seed stage: one launch per 4096 seeds
             d["kernels"]["hgx_bfs_block"] = {"ms": self.ms_block, "bytes": self.bytes_block,
                                              "launches": int((self.block_seeds + self.block_rerun + 4095) // 4096)}
+        if self.block_coop:   # one persistent launch for the seeds that outgrew a workgroup
+            d["kernels"]["hgx_bfs_coop"] = {"ms": self.ms_coop, "bytes": self.bytes_coop, "launches": 1}
         n = min(max(self.n_levels_expanded, 0), 64)   # per-level arrays hold the first 64 levels
         d["union_frontier"] = [int(x) for x in self.union_frontier[:n]]
         d["level_ms"] = [round(float(x), 4) for x in self.level_ms[:n]]

@@ -5360,6 +5360,9 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         r->stats.bytes_block = b.bytes;
         r->stats.block_seeds = n_seeds - (int64_t)b.rerun.size();
         r->stats.block_rerun = (int64_t)b.rerun.size();
+        r->stats.ms_coop = b.co_ms;
+        r->stats.bytes_coop = b.co_bytes_alg;
+        r->stats.block_coop = b.n_coop;
         r->compact.assign((size_t)n_seeds, -1);
         for (size_t k = 0; k < b.rerun.size(); ++k) {
             r->compact[b.rerun[k]] = (int32_t)k;
@@ -5540,6 +5543,7 @@ int hgx_bfs_result_visited_range(hgx_bfs_result* r, int32_t seed_index, int32_t 
     std::lock_guard<std::mutex> lk(g->mu);
     *n_out = 0;
     if (r->blk && r->blk->pairs[seed_index] >= 0) {   // a workgroup seed: its level, sorted on the host
+        block_materialize(g, *r->blk);
         const BlockSet& b = *r->blk;
         if (depth > b.levels[seed_index]) return HGX_OK;
         if (depth == 0) {
@@ -5625,6 +5629,7 @@ int hgx_bfs_result_depth_of(hgx_bfs_result* r, int32_t seed_index, int32_t atom,
     if (atom < 0 || atom >= g->A) fail(HGX_E_INVALID, "atom id out of range");
     std::lock_guard<std::mutex> lk(g->mu);
     if (r->blk && r->blk->pairs[seed_index] >= 0) {   // a workgroup seed: scan its levels
+        block_materialize(g, *r->blk);
         const BlockSet& b = *r->blk;
         *depth_out = -1;
         if (b.seeds[seed_index] == atom) {

@@ -42,6 +42,8 @@ void graph_release(hgx_graph* g) {
     HGX_FREE_OWN(hasinc); HGX_FREE_OWN(inc_yf); HGX_FREE_OWN(pchunks); HGX_FREE_OWN(inc_tgt);
 #undef HGX_FREE_OWN
     if (g->zacc) (void)hipFree(g->zacc);
+    if (g->q_ticket) (void)hipFree(g->q_ticket);
+    if (g->co_vis) (void)hipFree(g->co_vis);
     if (g->fcode) (void)hipFree(g->fcode);
     if (g->lcode) (void)hipFree(g->lcode);
     for (auto& b : g->seq_hbufs) (void)hipHostFree(b.p);
@@ -529,7 +531,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: sequence engine outside 0..2");
         g->seq_engine = (int32_t)value;
     } else if (option == HGX_OPT_BFS_BLOCK) {
-        g->bfs_block = value != 0;
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: BFS block mode outside 0..2");
+        g->bfs_block = (int32_t)value;
     } else if (option == HGX_OPT_PUSH_INLINE) {
         g->push_inline = value != 0;
     } else if (option == HGX_OPT_QUERY_COALESCE) {

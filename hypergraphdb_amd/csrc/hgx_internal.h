@@ -216,6 +216,9 @@ struct hgx_graph {
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each
+    unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
+    int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
+    int32_t co_ok = -1;                             //   its grid fits the device (-1 = not checked yet)
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
     // order-exact traversal refuses to run until the caller re-asserts it.
@@ -287,6 +290,8 @@ struct hgx_graph {
     int32_t q_coalesce = 1;                     // HGX_OPT_QUERY_COALESCE: concurrent packed batches share device batches
     int64_t q_coalesce_max = 1 << 16;           //   at most this many queries per coalesced device batch
     hgx::QueryCombiner qcomb;
+    unsigned long long* q_ticket = nullptr;     // pattern placement: blocks-done ticket (device, zero between batches)
+    unsigned long long q_seq = 0;               //   sequence number of the completion flag in the result area
 
     void* alloc(size_t bytes);
     void release(void* p, size_t bytes);
@@ -322,13 +327,27 @@ struct BlockSet {
     std::vector<int32_t> rerun;                 // seed indices, ascending
     double traversed = 0, ms = 0, bytes = 0;   // items of the finished seeds; device ms; algorithmic bytes
     int32_t expanded = 0;                       // most levels expanded by one finished seed
+    // Seeds the multi-workgroup stage finished (the workgroup stage's overflow, <= kMaxCoSeeds of
+    // them): their (atom, seed | level << 8) pairs stay in device pool memory until a reader asks for
+    // a set (block_materialize); their level counts are on the host at once.
+    void* co_pairs = nullptr;
+    size_t co_bytes = 0;
+    int64_t co_n = 0;
+    std::vector<int32_t> co_idx;                // seed indices
+    std::vector<std::vector<int32_t>> co_lcnt, co_atoms;
+    bool co_host = false;
+    double co_ms = 0, co_bytes_alg = 0;         // device ms of that launch (timing on), its algorithmic bytes
+    int32_t n_coop = 0;                         // seeds it finished
 };
+constexpr int kMaxCoSeeds = 64;
 // Runs every seed on the workgroup engine (caller holds g->mu, g's device current; max_depth -1 =
 // unbounded); returns when the seeds are done.
 void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
                BlockSet& out);
-// Hands the result's mapped buffers back to the graph's pool.
+// Hands the result's mapped buffers back to the graph's pool (caller holds g->mu).
 void block_release(hgx_graph* g, BlockSet& b);
+// Per-seed atom lists of the multi-workgroup stage's seeds on the host (first reader; g->mu held).
+void block_materialize(hgx_graph* g, BlockSet& b);
 // Waits for the work enqueued on s by polling: hipStreamSynchronize sleeps and wakes tens of
 // microseconds after the last kernel, a cost per call of the short pattern batches.
 inline void spin_sync(hipStream_t s) {

@@ -1356,7 +1356,7 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
                                                   const u64* __restrict__ hitmask, int64_t* __restrict__ q_off,
                                                   const int64_t* __restrict__ bpre, const int64_t* __restrict__ blk,
                                                   const int64_t* __restrict__ lpre, int32_t nb, int64_t cap_chunks,
-                                                  int64_t cap_cand) {
+                                                  int64_t cap_cand, u64* __restrict__ ticket, u64 seq) {
     __shared__ int64_t ws[4], c_off[kPlaceChunks], qb[2];
     __shared__ int32_t c_cnt[kPlaceChunks];
     __shared__ int64_t bp[D ? kDerivedBlocks + 1 : 1];
@@ -1487,6 +1487,20 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
             u64 v = 0;
             for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
             ctr_out[threadIdx.x] = v;
+        }
+    }
+    if (ticket) {   // completion flag: the last active block to finish publishes seq into stat[7]
+        __shared__ bool last_block;
+        __syncthreads();   // this block's result stores are issued
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            const u64 n_active = nc == 0 ? 1ull : (u64)((nc + kPlaceChunks - 1) / kPlaceChunks);
+            last_block = atomicAdd(ticket, 1ull) == n_active - 1ull;
+            if (last_block) {
+                *ticket = 0ull;
+                __threadfence_system();
+                __hip_atomic_store((u64*)(stat + 7), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
 }
@@ -2694,6 +2708,19 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
         // were zeroed by the front kernel; a re-run after a workspace overflow zeroes them here)
         const bool derived = f.lpre && nblk <= kDerivedBlocks && nbp <= kPlaceDirectBlocks;
         const int4* tt = g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr;
+        // without timing events the host waits on a completion flag the placement writes into the result
+        // area (stat[7]) instead of asking the stream (each hipStreamQuery costs a few microseconds)
+        static const bool stream_wait = std::getenv("HGX_Q_STREAM_WAIT") != nullptr;   // A/B
+        const bool flag = derived && !ev.on && !stream_wait;
+        u64 flag_seq = 0;
+        if (flag) {
+            if (!g->q_ticket) {
+                HGX_HIP(hipMalloc(&g->q_ticket, sizeof(u64)));
+                HGX_HIP(hipMemsetAsync(g->q_ticket, 0, sizeof(u64), s));
+            }
+            flag_seq = ++g->q_seq;
+            __atomic_store_n((u64*)(hm + m_stat) + 7, (u64)0, __ATOMIC_RELEASE);
+        }
         if (derived) {
             ctr = f.ctr;
             if (attempt > 0) HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
@@ -2706,7 +2733,8 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
             ev.rec(2, s);
             hgx_q_place<true><<<(unsigned)nbp, 256, 0, s>>>(nullptr, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr,
                                                             ctr_d, n, nullptr, nullptr, hmask, qoff_d, nullptr, f.blk,
-                                                            f.lpre, nblk, capC, capK);
+                                                            f.lpre, nblk, capC, capK, flag ? g->q_ticket : nullptr,
+                                                            flag_seq);
             HGX_CHECK_LAUNCH();
         }
         if (!derived) {
@@ -2728,11 +2756,23 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
             }
             hgx_q_place<false><<<(unsigned)nbp, 256, 0, s>>>(nch, cnt, slots, g->link_atom, outoff, ids_d, stat_d, ctr,
                                                              ctr_d, n, chq, coff, hmask, qoff_d, bpre, nullptr, nullptr,
-                                                             0, 0, 0);
+                                                             0, 0, 0, nullptr, 0);
             HGX_CHECK_LAUNCH();
         }
         ev.rec(3, s);
-        spin_sync(s);
+        if (flag) {
+            const u64* fl = (const u64*)(hm + m_stat) + 7;
+            for (unsigned spin = 0; __atomic_load_n(fl, __ATOMIC_ACQUIRE) != flag_seq; ++spin) {
+                if ((spin & 1023u) != 1023u) continue;   // the stream is asked every 1024 polls
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipErrorNotReady) continue;
+                if (e != hipSuccess) HGX_HIP(e);
+                if (__atomic_load_n(fl, __ATOMIC_ACQUIRE) != flag_seq)
+                    fail(HGX_E_DEVICE, "hgx_pattern_batch: the completion flag never arrived");
+            }
+        } else {
+            spin_sync(s);
+        }
         const int64_t* stat = (const int64_t*)(hm + m_stat);
         const u64* ctr_h = (const u64*)(hm + m_ctr);
         const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);

@@ -713,7 +713,11 @@ constexpr int kBbPairs = kBbDisc - 1;                // atoms one seed may retur
 constexpr int kBbFront = 1024;
 constexpr int kBbCand = 2048;
 constexpr int kBbU = 2;
-constexpr int64_t kBbItemLimit = (int64_t)1 << 22;
+constexpr int64_t kBbItemLimit = (int64_t)1 << 22;   // frontier incidence entries of a level (streamed yield flags)
+// The symmetric mode has no yield flags: every entry costs a link row and its targets, and a level this
+// wide all but certainly discovers more atoms than the workgroup holds (config 2's seeds next to hubs);
+// such a seed goes straight to the rows engine instead of paying for a flush before it overflows.
+constexpr int64_t kBbItemLimitSym = (int64_t)1 << 14;
 constexpr int kBbChunk = 4096;                       // seeds per launch (mapped output per launch)
 
 struct BbArgs {
@@ -837,6 +841,7 @@ __device__ void bb_frontier(BbShared& sm, const BbArgs& a, int F) {
 // Staged items -> the generator's yields -> examined-set inserts (as sb_process, no keys).
 __device__ void bb_process(BbShared& sm, const BbArgs& a, int F, int cn, int64_t& nbytes) {
     for (int c = threadIdx.x; c < cn; c += kBbThreads) {
+        if (sm.ovf) break;   // the seed goes to the rows engine: the rest of the flush is wasted work
         const int32_t it = sm.cand[c];
         const int i = sb_search(sm.e_dp, F, it);
         const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
@@ -915,7 +920,7 @@ __device__ void bb_run(BbShared& sm, const BbArgs& a, int si) {
         n_exp = d + 1;
         nbytes += tid == 0 ? 16 * (int64_t)F + (a.yf ? T : 0) : 0;   // frontier offsets, streamed yield flags
         if (T == 0) break;
-        if (T > kBbItemLimit) {
+        if (T > (a.yf ? kBbItemLimit : kBbItemLimitSym)) {
             ovf = true;
             break;
         }
@@ -1037,6 +1042,258 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
         bb_run(sm, a, si);
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-workgroup level loop (hgx_bfs_batch): the few seeds the workgroup stage hands back (config 5:
+// six hg.subsumed closures of 2K-101K atoms over 21 levels) in ONE persistent launch of kCoBlocks
+// resident workgroups, a grid barrier between levels instead of the rows engine's launches and host
+// turn-around per level (~50 us a level for those six seeds).
+//   - visited: one bitmap per seed (kCoMaxSeeds x A bits, kept on the graph, zero between calls: the
+//     epilogue clears the words of the atoms it found); the first atomicOr that sets an atom's bit
+//     discovers it;
+//   - work items: a discovered atom appends ceil(deg / kCoChunk) items (atom, seed, chunk) to the
+//     next level's list, so a hub's incidence is spread over many waves and a level needs no prefix
+//     scan; three lists rotate (level d reads d % 3, appends to (d + 1) % 3, and clears (d + 2) % 3);
+//   - output: (atom, seed | level << 8) pairs in device memory in arrival order, per-seed atom counts
+//     at the end of every level in mapped host memory (the readout's |V_d|); per-seed lists are built
+//     on the host only when a reader asks for a set;
+//   - the barrier is a monotonic counter (agent-scope release add, acquire spin) with a 1 s limit
+//     measured on the constant clock: a launch whose workgroups cannot all become resident reports a
+//     timeout (status 4) instead of hanging, and the seeds rerun on the rows engine.
+// The generator rules are those of bb_process.  Status: 1 = a work list overflowed, 2 = the pair list
+// overflowed, 3 = more than kCoMaxLevels levels, 4 = barrier timeout.  A level's errors go to a status
+// word of its parity, which the blocks read after the next barrier: the word they decide on cannot
+// change while some block has not read it yet (the next level writes the other one).
+constexpr int kCoThreads = 512;
+constexpr int kCoWaves = kCoThreads / 64;
+constexpr int kCoBlocks = 128;
+constexpr int kCoChunk = 256;
+constexpr int kCoMaxLevels = 1024;
+constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s
+
+struct CoArgs {
+    int32_t k;                                       // seeds (<= kMaxCoSeeds)
+    const int32_t* seeds;                            // device [k]
+    const int64_t* inc_off;
+    const int32_t* inc_row;
+    const int32_t* inc_type;
+    const uint8_t* yf;
+    const int64_t* tgt_off;
+    const int32_t* tgt_idx;
+    int32_t want_type, min_arity, mode, maxd;
+    int64_t vwords;                                  // words of one seed's bitmap
+    u64* vis;                                        // [k * vwords]
+    int4* fr;                                        // [3 * fr_cap] work items (atom, seed, chunk, -)
+    int64_t fr_cap;
+    u64* ctl;                                        // [0] barrier, [1..3] work-item counts, [4] / [6] status of
+                                                     //   even / odd levels (the seeding: odd), [5] pairs
+    u64* cur;                                        // [k] atoms found per seed
+    u64* trav;                                       // [k] incidence entries of the seed's expanded atoms
+    int2* pairs;                                     // [pcap] (atom, seed | level << 8)
+    int64_t pcap;
+    int64_t* lvl_end;                                // mapped [k * kCoMaxLevels]: cur[s] after level d
+    int64_t* hmeta;                                  // mapped [4 + 2k]: status, levels, pairs, -, then
+                                                     //   (atoms, traversed items) per seed
+};
+
+__device__ __forceinline__ bool co_barrier(u64* bar, u64& gen, u64* status) {
+    __shared__ int s_to;
+    __syncthreads();   // the block's stores and atomics of this level are issued
+    if (threadIdx.x == 0) {
+        ++gen;
+        const u64 target = gen * (u64)gridDim.x;
+        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();
+        int to = 0;
+        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
+                atomicOr(status, 4ull);
+                to = 1;
+                break;
+            }
+        }
+        s_to = to;
+    }
+    __syncthreads();
+    return s_to != 0;
+}
+
+// One step of a wave over seed s's yielded targets at level d (t < 0: none on this lane): the first
+// setter of an atom's bit discovers it; the wave's discoveries take their pair slots, the seed's
+// count and their work items for level d + 1 with one atomic each (s is the same on every lane: a
+// wave works on one work item at a time).  Every lane of the wave calls it.
+__device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, int32_t d, int slot_next,
+                                        int64_t& nbytes) {
+    const int lane = threadIdx.x & 63;
+    bool nw = false;
+    if (t >= 0) {
+        u64* w = a.vis + (int64_t)s * a.vwords + (t >> 6);
+        const u64 bit = 1ull << (t & 63);
+        nw = !(*w & bit) && !(atomicOr(w, bit) & bit);
+    }
+    const u64 m = __ballot(nw);
+    if (!m) return;
+    u64* status = a.ctl + ((d & 1) ? 6 : 4);
+    const int leader = __ffsll((long long)m) - 1;
+    u64 pbase = 0;
+    if (lane == leader) {
+        const u64 c = (u64)__popcll(m);
+        atomicAdd(a.cur + s, c);
+        pbase = atomicAdd(a.ctl + 5, c);
+    }
+    pbase = __shfl(pbase, leader);
+    u64 nch = 0;
+    if (nw) {
+        const u64 pos = pbase + (u64)__popcll(m & ((1ull << lane) - 1ull));
+        if ((int64_t)pos < a.pcap) a.pairs[pos] = make_int2(t, s | (d + 1) << 8);
+        else atomicOr(status, 2ull);
+        nbytes += 8;
+        if (d + 1 < a.maxd) {
+            const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
+            nch = (u64)((deg + kCoChunk - 1) / kCoChunk);
+        }
+    }
+    u64 x = nch;   // the wave's work items: one reservation
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u64 y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    const u64 tot = __shfl(x, 63);
+    if (tot == 0) return;
+    u64 wbase = 0;
+    if (lane == 63) wbase = atomicAdd(a.ctl + 1 + slot_next, tot);
+    wbase = __shfl(wbase, 63);
+    if (nch == 0) return;
+    const u64 base = wbase + x - nch;
+    if ((int64_t)(base + nch) > a.fr_cap) {
+        atomicOr(status, 1ull);
+        return;
+    }
+    int4* fr = a.fr + slot_next * a.fr_cap;
+    for (u64 c = 0; c < nch; ++c) fr[base + c] = make_int4(t, s, (int)c, 0);
+    nbytes += 16 * (int64_t)nch;
+}
+
+__global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * kCoWaves + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * kCoWaves;
+    u64 gen = 0;
+    int64_t nbytes = 0;        // algorithmic bytes of this thread (reduced into ctl[7] at the end)
+    u64* status = a.ctl + 6;   // the seeding's errors: read at level 0
+    if (blockIdx.x == 0)   // level 0: the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46)
+        for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
+            const int32_t t = a.seeds[s];
+            atomicOr(a.vis + (int64_t)s * a.vwords + (t >> 6), 1ull << (t & 63));
+            const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
+            if (a.maxd > 0 && deg > 0) {
+                const u64 nch = (u64)((deg + kCoChunk - 1) / kCoChunk);
+                const u64 base = atomicAdd(a.ctl + 1, nch);
+                if ((int64_t)(base + nch) > a.fr_cap) {
+                    atomicOr(status, 1ull);
+                    continue;
+                }
+                for (u64 c = 0; c < nch; ++c) a.fr[base + c] = make_int4(t, s, (int)c, 0);
+            }
+        }
+    bool timed_out = co_barrier(a.ctl, gen, a.ctl + 4);
+    int32_t d = 0;
+    for (; !timed_out; ++d) {
+        const int slot = d % 3, slot_next = (d + 1) % 3;
+        const u64 nf = __hip_atomic_load(a.ctl + 1 + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // errors of level d - 1 (its parity word; level d writes the other one)
+        const u64 st = __hip_atomic_load(a.ctl + ((d & 1) ? 4 : 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st != 0 || nf == 0 || d >= a.maxd) break;   // the same decision in every block
+        if (d >= kCoMaxLevels) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + 4, 3ull);
+            break;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0)   // read at level d - 1; appended to at level d + 1
+            __hip_atomic_store(a.ctl + 1 + (d + 2) % 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int4* fr = a.fr + slot * a.fr_cap;
+        for (int64_t it = gw; it < (int64_t)nf; it += nw) {
+            const int4 e = fr[it];
+            const int32_t p = e.x, s = e.y;
+            const int64_t b = a.inc_off[p], en = a.inc_off[p + 1];
+            if (e.z == 0 && lane == 0) atomicAdd(a.trav + s, (u64)(en - b));
+            const int64_t lo = b + (int64_t)e.z * kCoChunk, hi = min(en, lo + kCoChunk);
+            nbytes += lane == 0 ? 32 + (a.yf ? hi - lo : 0) : 0;   // the item, its offsets, the streamed flags
+            for (int64_t i0 = lo; i0 < hi; i0 += 64) {   // wave-uniform: every lane reaches co_step
+                const int64_t ii = i0 + lane;
+                bool act = ii < hi && (!a.yf || ((a.yf[ii] >> a.mode) & 1));   // a target this mode can yield
+                int64_t tb = 0;
+                int32_t qlo = 0, qhi = 0;
+                if (act) {
+                    const int32_t L = a.inc_row[ii];
+                    nbytes += a.want_type >= 0 ? 8 : 4;
+                    act = a.want_type < 0 || a.inc_type[ii] == a.want_type;   // linkPredicate (:300)
+                    if (act) {
+                        tb = a.tgt_off[L];
+                        const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
+                        nbytes += 16 + 4 * (int64_t)n;
+                        act = n >= a.min_arity;                              // minArity (:309)
+                        int32_t fv = -1, lv = -1;
+                        if (act && a.mode != sSym)
+                            for (int32_t q = 0; q < n; ++q)
+                                if (a.tgt_idx[tb + q] == p) {
+                                    if (fv < 0) fv = q;
+                                    lv = q;
+                                }
+                        qhi = n;
+                        if (a.mode == sAfterFirst) qlo = fv + 1;
+                        else if (a.mode == sBeforeFirst) qhi = fv;
+                        else if (a.mode == sBeforeLast) qhi = lv;
+                        else if (a.mode == sAfterLast) qlo = lv + 1;
+                        if (!act) qhi = qlo;
+                    }
+                }
+                for (int32_t q = qlo; __ballot(q < qhi); ++q) {   // one target per lane per step
+                    int32_t t = -1;
+                    if (q < qhi) {
+                        t = a.tgt_idx[tb + q];
+                        if (t == p) t = -1;
+                    }
+                    co_step(a, s, t, d, slot_next, nbytes);
+                }
+            }
+        }
+        timed_out = co_barrier(a.ctl, gen, a.ctl + 4);
+        if (blockIdx.x == 0 && !timed_out)   // every seed's atom count after level d
+            for (int s = threadIdx.x; s < a.k; s += kCoThreads)
+                a.lvl_end[(int64_t)s * kCoMaxLevels + d] =
+                    (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (timed_out) return;   // the host clears the bitmaps
+    for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
+    if (lane == 0 && nbytes) atomicAdd(a.ctl + 7, (u64)nbytes);
+    // every block left the loop after the same barrier: clear the bitmap words of the atoms found (the
+    // host clears the whole bitmaps when a list overflowed)
+    const u64 st = __hip_atomic_load(a.ctl + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                   __hip_atomic_load(a.ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t np = min((int64_t)__hip_atomic_load(a.ctl + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.pcap);
+    if (st == 0) {
+        for (int64_t i = (int64_t)blockIdx.x * kCoThreads + threadIdx.x; i < np; i += (int64_t)gridDim.x * kCoThreads) {
+            const int2 pr = a.pairs[i];
+            a.vis[(int64_t)(pr.y & 0xFF) * a.vwords + (pr.x >> 6)] = 0ull;
+        }
+        if (blockIdx.x == 0)
+            for (int s = threadIdx.x; s < a.k; s += kCoThreads) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.hmeta[0] = (int64_t)st;
+        a.hmeta[1] = d;
+        a.hmeta[2] = np;
+    }
+    co_barrier(a.ctl, gen, a.ctl + 4);   // every block's byte count is in
+    if (blockIdx.x == 0 && threadIdx.x == 0)   // + the pairs written and the bitmap words cleared
+        a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 16 * np;
+    if (blockIdx.x == 0)
+        for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
+            a.hmeta[4 + 2 * s] = (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.hmeta[5 + 2 * s] = (int64_t)__hip_atomic_load(a.trav + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1813,6 +2070,9 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 
 }  // namespace
 
+bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t max_depth,
+              const hgx_algen_opts& o, BlockSet& out);
+
 void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
                BlockSet& out) {
     hipStream_t st = g->stream;
@@ -1855,7 +2115,8 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         char* h;
     };
     std::vector<Chunk> chunks;
-    for (int64_t c0 = 0; c0 < n_seeds; c0 += kBbChunk) {
+    // HGX_OPT_BFS_BLOCK 2 (tests): every seed straight to the multi-workgroup stage
+    for (int64_t c0 = 0; c0 < (g->bfs_block == 2 ? 0 : n_seeds); c0 += kBbChunk) {
         const int64_t nb = std::min<int64_t>(kBbChunk, n_seeds - c0);
         PoolBuf hb = take_host_buf(g, per_seed * (size_t)nb);
         out.bufs.push_back(hb);
@@ -1906,9 +2167,176 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
             out.lcnt[si] = lc + i * kBbPairs;
         }
     }
+    if (g->bfs_block == 2)
+        for (int32_t i = 0; i < n_seeds; ++i) out.rerun.push_back(i);
+    // the few seeds that outgrew a workgroup: one multi-workgroup launch, else the rows engine
+    if (!out.rerun.empty() && out.rerun.size() <= (size_t)kMaxCoSeeds && bfs_coop(g, seeds, out.rerun, max_depth, o, out)) {
+        out.n_coop = (int32_t)out.rerun.size();
+        out.rerun.clear();
+    }
+}
+
+// The multi-workgroup stage over the seeds sidx (indices into seeds); true when they finished there
+// (false: a capacity or the grid did not fit, and the rows engine takes them).
+bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t max_depth,
+              const hgx_algen_opts& o, BlockSet& out) {
+    hipStream_t st = g->stream;
+    const int32_t k = (int32_t)sidx.size();
+    if (k == 0 || k > kMaxCoSeeds) return false;
+    if (g->co_ok < 0) {   // every workgroup of the grid must be resident at once (the barrier waits for all)
+        int per_cu = 0, cus = 0;
+        HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop, kCoThreads, 0));
+        HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
+        g->co_ok = (int64_t)per_cu * cus >= 2 * kCoBlocks ? 1 : 0;
+    }
+    if (!g->co_ok) return false;
+    const int mode = seq_mode(o);
+    const int64_t vwords = g->A / 64 + 1;
+    if (g->co_vis_seeds < k) {   // zero-invariant bitmaps, grown to the seed count
+        if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
+        g->co_vis = nullptr;
+        g->co_vis_seeds = 0;
+        const int64_t want = std::max<int64_t>(k, 8);
+        HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(want * vwords)));
+        HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(want * vwords), st));
+        g->co_vis_seeds = want;
+    }
+    if (g->co_pcap == 0) g->co_pcap = (int64_t)1 << 22;
+    const int64_t fr_cap = (int64_t)1 << 20;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const int64_t pcap = g->co_pcap;
+        SeqScratch sc{g, {}};
+        int4* fr = (int4*)sc.take(sizeof(int4) * 3 * (size_t)fr_cap);
+        int2* pairs = (int2*)g->alloc(sizeof(int2) * (size_t)pcap);
+        const size_t ctl_words = 8 + 2 * (size_t)k;
+        u64* ctl = (u64*)sc.take(sizeof(u64) * ctl_words + sizeof(int32_t) * (size_t)k);
+        int32_t* dseeds = (int32_t*)(ctl + ctl_words);
+        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
+        for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
+        HGX_HIP(hipMemsetAsync(ctl, 0, sizeof(u64) * ctl_words, st));
+        HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
+        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (4 + 2 * (size_t)k + (size_t)k * kCoMaxLevels));
+        int64_t* hm = (int64_t*)hb.p;
+        void* hmd = nullptr;
+        HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
+        CoArgs a{};
+        a.k = k;
+        a.seeds = dseeds;
+        a.inc_off = g->inc_off;
+        a.inc_row = g->inc_row;
+        a.inc_type = g->inc_type;
+        a.yf = mode != sSym ? g->inc_yf : nullptr;
+        a.tgt_off = g->tgt_off;
+        a.tgt_idx = g->tgt_idx;
+        a.want_type = o.link_type;
+        a.min_arity = o.return_source ? 1 : 2;
+        a.mode = mode;
+        a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
+        a.vwords = vwords;
+        a.vis = g->co_vis;
+        a.fr = fr;
+        a.fr_cap = fr_cap;
+        a.ctl = ctl;
+        a.cur = ctl + 8;
+        a.trav = ctl + 8 + k;
+        a.pairs = pairs;
+        a.pcap = pcap;
+        a.hmeta = (int64_t*)hmd;
+        a.lvl_end = (int64_t*)hmd + 4 + 2 * k;
+        hm[0] = -1;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (g->timing) {
+            HGX_HIP(hipEventCreate(&ev[0]));
+            HGX_HIP(hipEventCreate(&ev[1]));
+            HGX_HIP(hipEventRecord(ev[0], st));
+        }
+        hgx_bfs_coop<<<kCoBlocks, kCoThreads, 0, st>>>(a);
+        HGX_CHECK_LAUNCH();
+        if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+        spin_sync(st);
+        if (ev[1]) {
+            float ms = 0;
+            HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+            out.co_ms += ms;
+            (void)hipEventDestroy(ev[0]);
+            (void)hipEventDestroy(ev[1]);
+        }
+        const int64_t status = hm[0];
+        if (status != 0) {   // the bitmaps may hold bits of atoms no pair records: clear them whole
+            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
+            g->release(pairs, sizeof(int2) * (size_t)pcap);
+            {
+                std::lock_guard<std::mutex> lk(g->seq_mu);
+                g->seq_hbufs.push_back(hb);
+            }
+            if (status == 2 && attempt == 0) {   // only the pair list was short: grow it to what was found
+                g->co_pcap = std::max<int64_t>(2 * pcap, hm[2] + hm[2] / 4);
+                continue;
+            }
+            return false;
+        }
+        // success: level counts per seed from the per-level atom counts
+        const int32_t nlev = (int32_t)hm[1];
+        out.co_pairs = pairs;
+        out.co_bytes = sizeof(int2) * (size_t)pcap;
+        out.co_n = hm[2];
+        out.co_idx = sidx;
+        out.co_lcnt.assign((size_t)k, {});
+        out.co_atoms.assign((size_t)k, {});
+        for (int32_t j = 0; j < k; ++j) {
+            const int64_t* le = hm + 4 + 2 * k + (int64_t)j * kCoMaxLevels;
+            std::vector<int32_t>& lc = out.co_lcnt[j];
+            int64_t prev = 0;
+            for (int32_t d = 0; d < nlev; ++d) {
+                lc.push_back((int32_t)(le[d] - prev));
+                prev = le[d];
+            }
+            while (!lc.empty() && lc.back() == 0) lc.pop_back();
+            const int32_t i = sidx[j];
+            out.pairs[i] = (int32_t)hm[4 + 2 * j];
+            out.levels[i] = (int32_t)lc.size();
+            out.lcnt[i] = lc.data();
+            out.atoms[i] = nullptr;   // block_materialize
+            out.traversed += (double)hm[5 + 2 * j];
+        }
+        out.expanded = std::max(out.expanded, nlev);
+        out.co_bytes_alg = (double)hm[3];
+        std::lock_guard<std::mutex> lk(g->seq_mu);
+        g->seq_hbufs.push_back(hb);
+        return true;
+    }
+    return false;
+}
+
+void block_materialize(hgx_graph* g, BlockSet& b) {
+    if (b.co_host || b.co_idx.empty()) return;
+    std::vector<int2> h((size_t)b.co_n);
+    if (b.co_n > 0) {
+        HGX_HIP(hipMemcpyAsync(h.data(), b.co_pairs, sizeof(int2) * h.size(), hipMemcpyDeviceToHost, g->stream));
+        HGX_HIP(hipStreamSynchronize(g->stream));
+    }
+    const size_t k = b.co_idx.size();
+    std::vector<std::vector<int64_t>> pos(k);
+    for (size_t j = 0; j < k; ++j) {
+        int64_t o = 0;
+        for (int32_t c : b.co_lcnt[j]) {
+            pos[j].push_back(o);
+            o += c;
+        }
+        b.co_atoms[j].assign((size_t)o, -1);
+    }
+    for (const int2& pr : h) {
+        const size_t j = (size_t)(pr.y & 0xFF);
+        const int32_t lev = pr.y >> 8;   // >= 1
+        b.co_atoms[j][(size_t)pos[j][lev - 1]++] = pr.x;
+    }
+    for (size_t j = 0; j < k; ++j) b.atoms[b.co_idx[j]] = b.co_atoms[j].data();
+    b.co_host = true;
 }
 
 void block_release(hgx_graph* g, BlockSet& b) {
+    if (b.co_pairs) g->release(b.co_pairs, b.co_bytes);
+    b.co_pairs = nullptr;
     std::lock_guard<std::mutex> lk(g->seq_mu);
     for (auto& x : b.bufs) g->seq_hbufs.push_back(x);
     b.bufs.clear();

@@ -143,6 +143,12 @@ typedef struct hgx_bfs_stats {
     double  bytes_block;
     int64_t block_seeds;
     int64_t block_rerun;
+    /* the multi-workgroup stage that takes the workgroup stage's overflow (<= 64 seeds, one persistent
+     * launch, a grid barrier per level): device ms, algorithmic bytes, seeds it finished (counted in
+     * block_seeds too) */
+    double  ms_coop;
+    double  bytes_coop;
+    int64_t block_coop;
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
@@ -481,7 +487,9 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * workgroup (its visited set, frontier and staging in LDS, all its levels in one launch; V_d written
  * into mapped host memory); the seeds whose traversal outgrows the workgroup (more than 1534 atoms,
  * a level wider than 1024 atoms, or a frontier of more than 4M incidence entries) then run on the
- * batched rows engine.  0 = every seed on the rows engine.  Results are identical either way. */
+ * batched rows engine -- up to 64 of them first on the multi-workgroup stage (one persistent launch,
+ * a grid barrier per level, per-seed visited bitmaps).  0 = every seed on the rows engine; 2 (tests) =
+ * a batch of <= 64 seeds straight to the multi-workgroup stage.  Results are identical either way. */
 #define HGX_OPT_BFS_BLOCK 14
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */

@@ -399,7 +399,7 @@ def test_workgroup_stage_vs_rows_engine(case):
             assert l1 == l0, (case, mi, maxd)
             assert t1 == t0, (case, mi, maxd)
             assert s1["block_seeds"] + s1["block_rerun"] == n_seeds and s0["block_seeds"] == 0
-            mixed |= s1["block_seeds"] > 0 and s1["block_rerun"] > 0
+            mixed |= s1["block_seeds"] > s1["block_coop"] and s1["block_rerun"] + s1["block_coop"] > 0
             for i in range(0, n_seeds, max(1, n_seeds // 7)):
                 for a in rng.integers(0, g["num_atoms"], 4).tolist() + [int(seeds[i])]:
                     assert r1.depth_of(i, a) == r0.depth_of(i, a), (case, mi, maxd, i, a)
@@ -434,7 +434,7 @@ def test_workgroup_stage_vs_oracle_and_capacity_edges():
     r = bfs_batch(snap, seeds, None)
     st = r.stats(accounting=False)
     r.close()
-    assert st["block_seeds"] >= 3 and st["block_rerun"] >= 2, st
+    assert st["block_seeds"] - st["block_coop"] >= 3 and st["block_rerun"] + st["block_coop"] >= 2, st
 
 
 def test_config5_full_workgroup_stage():
@@ -456,11 +456,59 @@ def test_config5_full_workgroup_stage():
         (c1, t1, s1, r1), (c0, t0, _, r0) = out[1], out[0]
         assert np.array_equal(c1, c0) and t1 == t0, rev
         big = int((c0[:, 1:].sum(1) > 1534).sum())   # closures beyond the workgroup's atoms
-        assert s1["block_rerun"] >= big and (s1["block_rerun"] == 0) == rev, (rev, s1["block_rerun"], big)
+        handed = s1["block_rerun"] + s1["block_coop"]   # to the multi-workgroup stage or the rows engine
+        assert handed >= big and (handed == 0) == rev, (rev, s1, big)
         for i in (0, 5, 511, 1023):
             lv = orc.bfs_levels(int(g["seeds"][i]), -1, algen(T, False, True, rev, False))
             for d_, exp in enumerate(lv):
                 assert np.array_equal(r1.visited(i, d_), exp), (rev, i, d_)
         r1.close()
         r0.close()
+    snap.close()
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_multi_workgroup_stage_vs_rows_engine(case):
+    """HGX_OPT_BFS_BLOCK 2: a batch of <= 64 seeds straight to the multi-workgroup stage (one persistent
+    launch, a grid barrier per level, per-seed visited bitmaps, hub incidence spread over work items)
+    gives the rows engine's per-depth sets, counts, depth_of and TEPS numerator in every generator
+    mode, typed links, depth limits, duplicate seeds, seeds without incidence; and the bitmaps it
+    leaves behind are clean (the next batch on the same graph is exact too)."""
+    from hypergraphdb_amd import _lib, bfs_batch, synth
+    rng = np.random.default_rng(800 + case)
+    if case < 2:
+        g = K.random_graph(rng, int(rng.integers(500, 3000)), int(rng.integers(300, 3000)), max_arity=9,
+                           link_targets=case == 0, n_types=3)
+    elif case < 4:
+        g = synth.hypergraph(20000, 40000, 2, 8, 2.1, 3, seed=90 + case)
+    else:
+        g = synth.config5(scale=0.01, n_sources=64)
+    snap = snapshot(g)
+    n_seeds = [1, 64, 40, 7, 64][case]
+    seeds = (np.asarray(g["seeds"][:n_seeds], np.int32) if case == 4
+             else rng.integers(0, g["num_atoms"], n_seeds).astype(np.int32))
+    if n_seeds > 2:
+        seeds[-1] = seeds[0]
+    modes = [(False, True, False, False), (False, True, True, False)] if case == 4 else K.ALGEN_MODES
+    for mi, mode in enumerate(modes):
+        lt = int(g["subsumes_type"]) if case == 4 else [-1, 0, 1, -1, 2][(mi + case) % 5]
+        for maxd in (None, 1, 3):
+            res = {}
+            for blk in (2, 0):
+                snap.set_option(_lib.HGX_OPT_BFS_BLOCK, blk)
+                r = bfs_batch(snap, seeds, maxd, gen(snap, mode, lt))
+                res[blk] = (r.counts().copy(), _all_levels(r), r.stats()["traversed_edges"],
+                            r.stats(accounting=False), r)
+            (c2, l2, t2, s2, r2), (c0, l0, t0, s0, r0) = res[2], res[0]
+            n = max(c2.shape[1], c0.shape[1])
+            pad = lambda c: np.pad(c, ((0, 0), (0, n - c.shape[1])))
+            assert s2["block_coop"] == n_seeds, s2
+            assert np.array_equal(pad(c2), pad(c0)), (case, mi, maxd)
+            assert l2 == l0, (case, mi, maxd)
+            assert t2 == t0, (case, mi, maxd)
+            for i in range(0, n_seeds, max(1, n_seeds // 5)):
+                for a in rng.integers(0, g["num_atoms"], 4).tolist() + [int(seeds[i])]:
+                    assert r2.depth_of(i, a) == r0.depth_of(i, a), (case, mi, maxd, i, a)
+            r2.close()
+            r0.close()
     snap.close()
