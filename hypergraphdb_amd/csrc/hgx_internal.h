@@ -218,7 +218,7 @@ struct hgx_graph {
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
-    int32_t co_ok = -1;                             //   its grid fits the device (-1 = not checked yet)
+    int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
     // order-exact traversal refuses to run until the caller re-asserts it.
@@ -330,9 +330,10 @@ struct BlockSet {
     // Seeds the multi-workgroup stage finished (the workgroup stage's overflow, <= kMaxCoSeeds of
     // them): their (atom, seed | level << 8) pairs stay in device pool memory until a reader asks for
     // a set (block_materialize); their level counts are on the host at once.
-    void* co_pairs = nullptr;
+    void* co_pairs = nullptr;                   // kCoSegs segments of co_pseg pairs, co_segn[q] used in q
     size_t co_bytes = 0;
-    int64_t co_n = 0;
+    int64_t co_n = 0, co_pseg = 0;
+    std::vector<int64_t> co_segn;
     std::vector<int32_t> co_idx;                // seed indices
     std::vector<std::vector<int32_t>> co_lcnt, co_atoms;
     bool co_host = false;

@@ -29,6 +29,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -1046,8 +1047,8 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Multi-workgroup level loop (hgx_bfs_batch): the few seeds the workgroup stage hands back (config 5:
-// six hg.subsumed closures of 2K-101K atoms over 21 levels) in ONE persistent launch of kCoBlocks
-// resident workgroups, a grid barrier between levels instead of the rows engine's launches and host
+// six hg.subsumed closures of 2K-101K atoms over 21 levels) in ONE persistent launch of up to
+// kCoMaxBlocks resident workgroups, a grid barrier between levels instead of the rows engine's launches and host
 // turn-around per level (~50 us a level for those six seeds).
 //   - visited: one bitmap per seed (kCoMaxSeeds x A bits, kept on the graph, zero between calls: the
 //     epilogue clears the words of the atoms it found); the first atomicOr that sets an atom's bit
@@ -1067,10 +1068,22 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
 // change while some block has not read it yet (the next level writes the other one).
 constexpr int kCoThreads = 512;
 constexpr int kCoWaves = kCoThreads / 64;
-constexpr int kCoBlocks = 128;
-constexpr int kCoChunk = 256;
+constexpr int kCoMinBlocks = 64, kCoMaxBlocks = 512;   // the grid: 2 per CU (512 on MI355X), resident
+constexpr int kCoChunk = 128;   // incidence entries per work item (default; HGX_CO_CHUNK for A/B)
+// Same-address atomics serialise (one per ~20 ns): the work-item / pair counters are split into
+// kCoSegs segments (block b appends to segment b % kCoSegs, its own part of the lists) and the barrier
+// into kCoBarGroups arrival counters whose last arrival reports to the top counter.
+constexpr int kCoSegs = 32;
+constexpr int kCoBarGroups = 16;
+// a segment's level counter packs its work items (high 24 bits) and the pairs found (low 40)
+constexpr int kCoItemShift = 40;
+constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
 constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s
+// ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
+// even / odd levels (the seeding: odd), [kCoBytes] algorithmic bytes, [kCoLev + slot * kCoSegs + seg]
+// level counters (3 rotating slots), then cur [k] and trav [k]
+constexpr int kCoSt = 20, kCoBytes = 22, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
 
 struct CoArgs {
     int32_t k;                                       // seeds (<= kMaxCoSeeds)
@@ -1082,31 +1095,40 @@ struct CoArgs {
     const int64_t* tgt_off;
     const int32_t* tgt_idx;
     int32_t want_type, min_arity, mode, maxd;
+    int32_t chunk;                                   // incidence entries per work item
     int64_t vwords;                                  // words of one seed's bitmap
     u64* vis;                                        // [k * vwords]
-    int4* fr;                                        // [3 * fr_cap] work items (atom, seed, chunk, -)
-    int64_t fr_cap;
-    u64* ctl;                                        // [0] barrier, [1..3] work-item counts, [4] / [6] status of
-                                                     //   even / odd levels (the seeding: odd), [5] pairs
+    int4* fr;                                        // [3 * kCoSegs * fr_seg] work items (atom, seed, chunk, -)
+    int64_t fr_seg;
+    u64* ctl;                                        // [kCoCtlWords + 2k]
     u64* cur;                                        // [k] atoms found per seed
     u64* trav;                                       // [k] incidence entries of the seed's expanded atoms
-    int2* pairs;                                     // [pcap] (atom, seed | level << 8)
-    int64_t pcap;
+    int2* pairs;                                     // [kCoSegs * pseg] (atom, seed | level << 8)
+    int64_t pseg;
+    int64_t* hmeta;                                  // mapped: [0] status, [1] levels, [2] -, [3] bytes,
+                                                     //   (atoms, traversed) per seed, pairs per segment
     int64_t* lvl_end;                                // mapped [k * kCoMaxLevels]: cur[s] after level d
-    int64_t* hmeta;                                  // mapped [4 + 2k]: status, levels, pairs, -, then
-                                                     //   (atoms, traversed items) per seed
+    int64_t* lvl_trace;                              // mapped [2 * kCoMaxLevels]: start clock, work items
 };
 
-__device__ __forceinline__ bool co_barrier(u64* bar, u64& gen, u64* status) {
+// Grid barrier: arrival at the block's group counter (acq_rel: the last arrival of a group carries
+// the group's writes on), the group's last arrival adds to the top counter, everyone polls the top
+// counter (relaxed polls, one acquire fence after: an acquire load per poll invalidates the caches on
+// every iteration of every waiting block, ~50 us a barrier measured with 128 blocks).
+__device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status) {
     __shared__ int s_to;
     __syncthreads();   // the block's stores and atomics of this level are issued
     if (threadIdx.x == 0) {
         ++gen;
-        const u64 target = gen * (u64)gridDim.x;
-        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const int grp = blockIdx.x % kCoBarGroups;
+        const u64 members = (u64)((gridDim.x - grp + kCoBarGroups - 1) / kCoBarGroups);
+        const u64 old = __hip_atomic_fetch_add(ctl + 1 + grp, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == gen * members)
+            __hip_atomic_fetch_add(ctl, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 groups = (u64)min((unsigned)kCoBarGroups, gridDim.x);
         const u64 t0 = __builtin_amdgcn_s_memrealtime();
         int to = 0;
-        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen * groups) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
                 atomicOr(status, 4ull);
@@ -1114,65 +1136,59 @@ __device__ __forceinline__ bool co_barrier(u64* bar, u64& gen, u64* status) {
                 break;
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_to = to;
     }
     __syncthreads();
     return s_to != 0;
 }
 
-// One step of a wave over seed s's yielded targets at level d (t < 0: none on this lane): the first
-// setter of an atom's bit discovers it; the wave's discoveries take their pair slots, the seed's
-// count and their work items for level d + 1 with one atomic each (s is the same on every lane: a
-// wave works on one work item at a time).  Every lane of the wave calls it.
-__device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, int32_t d, int slot_next,
-                                        int64_t& nbytes) {
+// One step of a wave over yielded targets at level d (lane: target t of seed s, t < 0: none): the first
+// setter of an atom's bit discovers it; the wave's discoveries take their pair slots and their work
+// items for level d + 1 in the block's segment with one atomic, the seeds' counts go to the block's
+// LDS counters (flushed once a level).  Every lane of the wave calls it.
+__device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, int32_t d, int slot_next, int seg,
+                                        u64 pbase_seg, int64_t& nbytes, unsigned long long* cnt_l) {
     const int lane = threadIdx.x & 63;
     bool nw = false;
-    if (t >= 0) {
+    int64_t deg = 0;
+    if (t >= 0) {   // the bit and the target's incidence range in flight together
         u64* w = a.vis + (int64_t)s * a.vwords + (t >> 6);
         const u64 bit = 1ull << (t & 63);
-        nw = !(*w & bit) && !(atomicOr(w, bit) & bit);
+        int64_t b0 = 0, b1 = 0;
+        if (d + 1 < a.maxd) {
+            b0 = a.inc_off[t];
+            b1 = a.inc_off[t + 1];
+        }
+        nw = !(atomicOr(w, bit) & bit);
+        deg = b1 - b0;
     }
     const u64 m = __ballot(nw);
     if (!m) return;
-    u64* status = a.ctl + ((d & 1) ? 6 : 4);
-    const int leader = __ffsll((long long)m) - 1;
-    u64 pbase = 0;
-    if (lane == leader) {
-        const u64 c = (u64)__popcll(m);
-        atomicAdd(a.cur + s, c);
-        pbase = atomicAdd(a.ctl + 5, c);
-    }
-    pbase = __shfl(pbase, leader);
-    u64 nch = 0;
-    if (nw) {
-        const u64 pos = pbase + (u64)__popcll(m & ((1ull << lane) - 1ull));
-        if ((int64_t)pos < a.pcap) a.pairs[pos] = make_int2(t, s | (d + 1) << 8);
-        else atomicOr(status, 2ull);
-        nbytes += 8;
-        if (d + 1 < a.maxd) {
-            const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
-            nch = (u64)((deg + kCoChunk - 1) / kCoChunk);
-        }
-    }
-    u64 x = nch;   // the wave's work items: one reservation
+    if (nw) atomicAdd(&cnt_l[s], 1ull);
+    const u64 nch = nw ? (u64)((deg + a.chunk - 1) / a.chunk) : 0ull;
+    u64 x = nch;   // the wave's work items and pairs: one packed reservation (items << 40 | pairs)
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const u64 y = __shfl_up(x, off);
         if (lane >= off) x += y;
     }
-    const u64 tot = __shfl(x, 63);
-    if (tot == 0) return;
-    u64 wbase = 0;
-    if (lane == 63) wbase = atomicAdd(a.ctl + 1 + slot_next, tot);
-    wbase = __shfl(wbase, 63);
+    u64 wb = 0;
+    if (lane == 63) wb = atomicAdd(a.ctl + kCoLev + slot_next * kCoSegs + seg, (x << kCoItemShift) | (u64)__popcll(m));
+    wb = __shfl(wb, 63);
+    if (!nw) return;
+    u64* status = a.ctl + kCoSt + (d & 1);
+    const u64 pos = pbase_seg + (wb & kCoPairMask) + (u64)__popcll(m & ((1ull << lane) - 1ull));
+    if ((int64_t)pos < a.pseg) a.pairs[(int64_t)seg * a.pseg + (int64_t)pos] = make_int2(t, s | (d + 1) << 8);
+    else atomicOr(status, 2ull);
+    nbytes += 8;
     if (nch == 0) return;
-    const u64 base = wbase + x - nch;
-    if ((int64_t)(base + nch) > a.fr_cap) {
+    const u64 base = (wb >> kCoItemShift) + x - nch;
+    if ((int64_t)(base + nch) > a.fr_seg) {
         atomicOr(status, 1ull);
         return;
     }
-    int4* fr = a.fr + slot_next * a.fr_cap;
+    int4* fr = a.fr + ((int64_t)slot_next * kCoSegs + seg) * a.fr_seg;
     for (u64 c = 0; c < nch; ++c) fr[base + c] = make_int4(t, s, (int)c, 0);
     nbytes += 16 * (int64_t)nch;
 }
@@ -1180,49 +1196,115 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
 __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * kCoWaves + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * kCoWaves;
+    const int seg = blockIdx.x % kCoSegs;
+    __shared__ unsigned long long cnt_l[kMaxCoSeeds], trav_l[kMaxCoSeeds];   // this block's per-seed counts of a level
+    __shared__ int64_t seg_pre[kCoSegs + 1];                                 // the level's items per segment, prefix
+    __shared__ u64 seg_pairs;                                                // pairs of this block's segment at the level
+    if (threadIdx.x < kMaxCoSeeds) {
+        cnt_l[threadIdx.x] = 0;
+        trav_l[threadIdx.x] = 0;
+    }
     u64 gen = 0;
-    int64_t nbytes = 0;        // algorithmic bytes of this thread (reduced into ctl[7] at the end)
-    u64* status = a.ctl + 6;   // the seeding's errors: read at level 0
-    if (blockIdx.x == 0)   // level 0: the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46)
+    int64_t nbytes = 0;   // algorithmic bytes of this thread (reduced into ctl[kCoBytes] at the end)
+    if (blockIdx.x == 0)   // level 0 (segment 0): the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46)
         for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
             const int32_t t = a.seeds[s];
             atomicOr(a.vis + (int64_t)s * a.vwords + (t >> 6), 1ull << (t & 63));
             const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
             if (a.maxd > 0 && deg > 0) {
-                const u64 nch = (u64)((deg + kCoChunk - 1) / kCoChunk);
-                const u64 base = atomicAdd(a.ctl + 1, nch);
-                if ((int64_t)(base + nch) > a.fr_cap) {
-                    atomicOr(status, 1ull);
+                const u64 nch = (u64)((deg + a.chunk - 1) / a.chunk);
+                const u64 base = atomicAdd(a.ctl + kCoLev, nch << kCoItemShift) >> kCoItemShift;
+                if ((int64_t)(base + nch) > a.fr_seg) {
+                    atomicOr(a.ctl + kCoSt + 1, 1ull);
                     continue;
                 }
                 for (u64 c = 0; c < nch; ++c) a.fr[base + c] = make_int4(t, s, (int)c, 0);
             }
         }
-    bool timed_out = co_barrier(a.ctl, gen, a.ctl + 4);
+    bool timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt);
     int32_t d = 0;
+    u64 pbase = 0;   // pairs of this block's segment found before the current level
     for (; !timed_out; ++d) {
         const int slot = d % 3, slot_next = (d + 1) % 3;
-        const u64 nf = __hip_atomic_load(a.ctl + 1 + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x < 64) {   // the level's items per segment -> prefix; this segment's new pairs
+            const u64 packed = threadIdx.x < kCoSegs
+                                   ? __hip_atomic_load(a.ctl + kCoLev + slot * kCoSegs + threadIdx.x, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0ull;
+            int64_t x = (int64_t)(packed >> kCoItemShift);
+            const int64_t v = x;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t y = __shfl_up(x, off);
+                if ((int)threadIdx.x >= off) x += y;
+            }
+            if (threadIdx.x < kCoSegs) seg_pre[threadIdx.x] = x - v;
+            if (threadIdx.x == kCoSegs - 1) seg_pre[kCoSegs] = x;
+            if ((int)threadIdx.x == seg) seg_pairs = packed & kCoPairMask;
+        }
+        __syncthreads();
+        const int64_t nf = seg_pre[kCoSegs];
+        pbase += seg_pairs;
         // errors of level d - 1 (its parity word; level d writes the other one)
-        const u64 st = __hip_atomic_load(a.ctl + ((d & 1) ? 4 : 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 st = __hip_atomic_load(a.ctl + kCoSt + ((d + 1) & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();   // seg_pre / seg_pairs are read before the next level rewrites them
         if (st != 0 || nf == 0 || d >= a.maxd) break;   // the same decision in every block
         if (d >= kCoMaxLevels) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + 4, 3ull);
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + kCoSt, 3ull);
             break;
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0)   // read at level d - 1; appended to at level d + 1
-            __hip_atomic_store(a.ctl + 1 + (d + 2) % 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int4* fr = a.fr + slot * a.fr_cap;
-        for (int64_t it = gw; it < (int64_t)nf; it += nw) {
-            const int4 e = fr[it];
-            const int32_t p = e.x, s = e.y;
-            const int64_t b = a.inc_off[p], en = a.inc_off[p + 1];
-            if (e.z == 0 && lane == 0) atomicAdd(a.trav + s, (u64)(en - b));
-            const int64_t lo = b + (int64_t)e.z * kCoChunk, hi = min(en, lo + kCoChunk);
-            nbytes += lane == 0 ? 32 + (a.yf ? hi - lo : 0) : 0;   // the item, its offsets, the streamed flags
-            for (int64_t i0 = lo; i0 < hi; i0 += 64) {   // wave-uniform: every lane reaches co_step
-                const int64_t ii = i0 + lane;
-                bool act = ii < hi && (!a.yf || ((a.yf[ii] >> a.mode) & 1));   // a target this mode can yield
+        if (blockIdx.x == 0) {   // read at level d - 1; appended to at level d + 1
+            if (threadIdx.x < kCoSegs)
+                __hip_atomic_store(a.ctl + kCoLev + ((d + 2) % 3) * kCoSegs + threadIdx.x, 0ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0) {
+                a.lvl_trace[2 * d] = (int64_t)__builtin_amdgcn_s_memrealtime();   // level start, work items
+                a.lvl_trace[2 * d + 1] = nf;
+            }
+        }
+        const int4* fr = a.fr + (int64_t)slot * kCoSegs * a.fr_seg;
+        // a wave takes `per` work items at once (one per lane, per <= 64 spreads the level over every
+        // wave of the grid) and walks their incidence entries as one flat range, 64 entries a step (most
+        // items are atoms of a few entries: one item per wave would leave most lanes idle)
+        const int64_t per = min<int64_t>(64, (nf + nw - 1) / nw);
+        for (int64_t it0 = gw * per; it0 < nf; it0 += nw * per) {
+            const int64_t it = it0 + lane;
+            int32_t ip = -1, is = 0;
+            int64_t ilo = 0, icnt = 0;
+            if (lane < per && it < nf) {
+                int lo = 0, hi = kCoSegs - 1;   // the item's segment: the last with seg_pre <= it
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (seg_pre[mid] <= it) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int4 e = fr[(int64_t)lo * a.fr_seg + (it - seg_pre[lo])];
+                ip = e.x;
+                is = e.y;
+                const int64_t b = a.inc_off[ip], en = a.inc_off[ip + 1];
+                if (e.z == 0) atomicAdd(&trav_l[is], (unsigned long long)(en - b));
+                ilo = b + (int64_t)e.z * a.chunk;
+                icnt = min(en, ilo + a.chunk) - ilo;
+                nbytes += 32 + (a.yf ? icnt : 0);   // the item, its offsets, the streamed flags
+            }
+            int64_t x = icnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            const int64_t T = __shfl(x, 63), ex = x - icnt;
+            for (int64_t f0 = 0; f0 < T; f0 += 64) {   // wave-uniform: every lane reaches co_step
+                const int64_t f = f0 + lane;
+                int o = 0;   // owner lane: the last lane whose range starts at or before f
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const int mid = o + step;
+                    if (__shfl(ex, mid) <= f) o = mid;
+                }
+                const int32_t p = __shfl(ip, o), s = __shfl(is, o);
+                const int64_t ii = __shfl(ilo, o) + (f - __shfl(ex, o));
+                bool act = f < T && (!a.yf || ((a.yf[ii] >> a.mode) & 1));   // a target this mode can yield
                 int64_t tb = 0;
                 int32_t qlo = 0, qhi = 0;
                 if (act) {
@@ -1255,11 +1337,18 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                         t = a.tgt_idx[tb + q];
                         if (t == p) t = -1;
                     }
-                    co_step(a, s, t, d, slot_next, nbytes);
+                    co_step(a, s, t, d, slot_next, seg, pbase, nbytes, cnt_l);
                 }
             }
         }
-        timed_out = co_barrier(a.ctl, gen, a.ctl + 4);
+        __syncthreads();   // the block's per-seed counts of this level -> the seed counters
+        for (int j = threadIdx.x; j < a.k; j += kCoThreads) {
+            if (cnt_l[j]) atomicAdd(a.cur + j, cnt_l[j]);
+            if (trav_l[j]) atomicAdd(a.trav + j, trav_l[j]);
+            cnt_l[j] = 0;
+            trav_l[j] = 0;
+        }
+        timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt);
         if (blockIdx.x == 0 && !timed_out)   // every seed's atom count after level d
             for (int s = threadIdx.x; s < a.k; s += kCoThreads)
                 a.lvl_end[(int64_t)s * kCoMaxLevels + d] =
@@ -1267,28 +1356,29 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
     }
     if (timed_out) return;   // the host clears the bitmaps
     for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
-    if (lane == 0 && nbytes) atomicAdd(a.ctl + 7, (u64)nbytes);
-    // every block left the loop after the same barrier: clear the bitmap words of the atoms found (the
-    // host clears the whole bitmaps when a list overflowed)
-    const u64 st = __hip_atomic_load(a.ctl + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                   __hip_atomic_load(a.ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t np = min((int64_t)__hip_atomic_load(a.ctl + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.pcap);
+    if (lane == 0 && nbytes) atomicAdd(a.ctl + kCoBytes, (u64)nbytes);
+    // every block left the loop after the same barrier: clear the bitmap words of the atoms found, the
+    // blocks of a segment splitting its pairs (the host clears the whole bitmaps when a list overflowed)
+    const u64 st = __hip_atomic_load(a.ctl + kCoSt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                   __hip_atomic_load(a.ctl + kCoSt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t np = min((int64_t)pbase, a.pseg);
     if (st == 0) {
-        for (int64_t i = (int64_t)blockIdx.x * kCoThreads + threadIdx.x; i < np; i += (int64_t)gridDim.x * kCoThreads) {
-            const int2 pr = a.pairs[i];
+        const int64_t nblk_seg = ((int64_t)gridDim.x - seg + kCoSegs - 1) / kCoSegs;
+        for (int64_t i = (int64_t)(blockIdx.x / kCoSegs) * kCoThreads + threadIdx.x; i < np; i += nblk_seg * kCoThreads) {
+            const int2 pr = a.pairs[(int64_t)seg * a.pseg + i];
             a.vis[(int64_t)(pr.y & 0xFF) * a.vwords + (pr.x >> 6)] = 0ull;
         }
         if (blockIdx.x == 0)
             for (int s = threadIdx.x; s < a.k; s += kCoThreads) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
     }
+    if (blockIdx.x < kCoSegs && threadIdx.x == 0) a.hmeta[4 + 2 * a.k + blockIdx.x] = (int64_t)pbase;   // pairs per segment
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.hmeta[0] = (int64_t)st;
         a.hmeta[1] = d;
-        a.hmeta[2] = np;
     }
-    co_barrier(a.ctl, gen, a.ctl + 4);   // every block's byte count is in
+    co_barrier(a.ctl, gen, a.ctl + kCoSt);   // every block's byte count is in
     if (blockIdx.x == 0 && threadIdx.x == 0)   // + the pairs written and the bitmap words cleared
-        a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 16 * np;
+        a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + kCoBytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0)
         for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
             a.hmeta[4 + 2 * s] = (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2183,11 +2273,12 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
     hipStream_t st = g->stream;
     const int32_t k = (int32_t)sidx.size();
     if (k == 0 || k > kMaxCoSeeds) return false;
-    if (g->co_ok < 0) {   // every workgroup of the grid must be resident at once (the barrier waits for all)
-        int per_cu = 0, cus = 0;
+    if (g->co_ok < 0) {   // every workgroup of the grid must be resident at once (the barrier waits for all):
+        int per_cu = 0, cus = 0;   // at most 2 per CU and one CU slot left for other streams' kernels
         HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop, kCoThreads, 0));
         HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
-        g->co_ok = (int64_t)per_cu * cus >= 2 * kCoBlocks ? 1 : 0;
+        const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
+        g->co_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, kCoMaxBlocks) : 0;
     }
     if (!g->co_ok) return false;
     const int mode = seq_mode(o);
@@ -2202,20 +2293,21 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         g->co_vis_seeds = want;
     }
     if (g->co_pcap == 0) g->co_pcap = (int64_t)1 << 22;
-    const int64_t fr_cap = (int64_t)1 << 20;
+    const int64_t fr_seg = ((int64_t)1 << 20) / kCoSegs;   // work items per segment and level
     for (int attempt = 0; attempt < 2; ++attempt) {
-        const int64_t pcap = g->co_pcap;
+        const int64_t pcap = g->co_pcap, pseg = pcap / kCoSegs;
         SeqScratch sc{g, {}};
-        int4* fr = (int4*)sc.take(sizeof(int4) * 3 * (size_t)fr_cap);
+        int4* fr = (int4*)sc.take(sizeof(int4) * 3 * kCoSegs * (size_t)fr_seg);
         int2* pairs = (int2*)g->alloc(sizeof(int2) * (size_t)pcap);
-        const size_t ctl_words = 8 + 2 * (size_t)k;
+        const size_t ctl_words = kCoCtlWords + 2 * (size_t)k;
         u64* ctl = (u64*)sc.take(sizeof(u64) * ctl_words + sizeof(int32_t) * (size_t)k);
         int32_t* dseeds = (int32_t*)(ctl + ctl_words);
         int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
         for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
         HGX_HIP(hipMemsetAsync(ctl, 0, sizeof(u64) * ctl_words, st));
         HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
-        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (4 + 2 * (size_t)k + (size_t)k * kCoMaxLevels));
+        const size_t m_seg = 4 + 2 * (size_t)k, m_lev = m_seg + kCoSegs;   // mapped layout (CoArgs::hmeta)
+        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (m_lev + (size_t)(k + 2) * kCoMaxLevels));
         int64_t* hm = (int64_t*)hb.p;
         void* hmd = nullptr;
         HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
@@ -2232,17 +2324,20 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.min_arity = o.return_source ? 1 : 2;
         a.mode = mode;
         a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
+        static const int chunk_env = std::getenv("HGX_CO_CHUNK") ? std::atoi(std::getenv("HGX_CO_CHUNK")) : 0;
+        a.chunk = chunk_env > 0 ? chunk_env : kCoChunk;
         a.vwords = vwords;
         a.vis = g->co_vis;
         a.fr = fr;
-        a.fr_cap = fr_cap;
+        a.fr_seg = fr_seg;
         a.ctl = ctl;
-        a.cur = ctl + 8;
-        a.trav = ctl + 8 + k;
+        a.cur = ctl + kCoCtlWords;
+        a.trav = ctl + kCoCtlWords + k;
         a.pairs = pairs;
-        a.pcap = pcap;
+        a.pseg = pseg;
         a.hmeta = (int64_t*)hmd;
-        a.lvl_end = (int64_t*)hmd + 4 + 2 * k;
+        a.lvl_end = (int64_t*)hmd + m_lev;
+        a.lvl_trace = a.lvl_end + (size_t)k * kCoMaxLevels;
         hm[0] = -1;
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (g->timing) {
@@ -2250,7 +2345,7 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             HGX_HIP(hipEventCreate(&ev[1]));
             HGX_HIP(hipEventRecord(ev[0], st));
         }
-        hgx_bfs_coop<<<kCoBlocks, kCoThreads, 0, st>>>(a);
+        hgx_bfs_coop<<<(unsigned)g->co_ok, kCoThreads, 0, st>>>(a);
         HGX_CHECK_LAUNCH();
         if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
         spin_sync(st);
@@ -2270,21 +2365,34 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
                 g->seq_hbufs.push_back(hb);
             }
             if (status == 2 && attempt == 0) {   // only the pair list was short: grow it to what was found
-                g->co_pcap = std::max<int64_t>(2 * pcap, hm[2] + hm[2] / 4);
+                int64_t most = 0;
+                for (int q = 0; q < kCoSegs; ++q) most = std::max(most, hm[m_seg + q]);
+                g->co_pcap = std::max<int64_t>(2 * pcap, kCoSegs * (most + most / 4 + 64));
                 continue;
             }
             return false;
         }
         // success: level counts per seed from the per-level atom counts
         const int32_t nlev = (int32_t)hm[1];
+        static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
+        if (trace) {   // per level: microseconds since the first level, work items
+            const int64_t* tr = hm + m_lev + (size_t)k * kCoMaxLevels;
+            std::fprintf(stderr, "[hgx coop] k=%d levels=%d:", k, nlev);
+            for (int32_t d = 0; d < nlev; ++d)
+                std::fprintf(stderr, " %.1f/%lld", (tr[2 * d] - tr[0]) / 100.0, (long long)tr[2 * d + 1]);
+            std::fprintf(stderr, "\n");
+        }
         out.co_pairs = pairs;
         out.co_bytes = sizeof(int2) * (size_t)pcap;
-        out.co_n = hm[2];
+        out.co_pseg = pseg;
+        out.co_segn.assign(hm + m_seg, hm + m_seg + kCoSegs);
+        out.co_n = 0;
+        for (int64_t c : out.co_segn) out.co_n += c;
         out.co_idx = sidx;
         out.co_lcnt.assign((size_t)k, {});
         out.co_atoms.assign((size_t)k, {});
         for (int32_t j = 0; j < k; ++j) {
-            const int64_t* le = hm + 4 + 2 * k + (int64_t)j * kCoMaxLevels;
+            const int64_t* le = hm + m_lev + (int64_t)j * kCoMaxLevels;
             std::vector<int32_t>& lc = out.co_lcnt[j];
             int64_t prev = 0;
             for (int32_t d = 0; d < nlev; ++d) {
@@ -2300,7 +2408,7 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             out.traversed += (double)hm[5 + 2 * j];
         }
         out.expanded = std::max(out.expanded, nlev);
-        out.co_bytes_alg = (double)hm[3];
+        out.co_bytes_alg = (double)hm[3] + 16.0 * (double)out.co_n;   // + the pairs and the bitmap words cleared
         std::lock_guard<std::mutex> lk(g->seq_mu);
         g->seq_hbufs.push_back(hb);
         return true;
@@ -2311,10 +2419,14 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
 void block_materialize(hgx_graph* g, BlockSet& b) {
     if (b.co_host || b.co_idx.empty()) return;
     std::vector<int2> h((size_t)b.co_n);
-    if (b.co_n > 0) {
-        HGX_HIP(hipMemcpyAsync(h.data(), b.co_pairs, sizeof(int2) * h.size(), hipMemcpyDeviceToHost, g->stream));
-        HGX_HIP(hipStreamSynchronize(g->stream));
+    size_t o = 0;
+    for (size_t q = 0; q < b.co_segn.size(); ++q) {   // each segment's pairs
+        const size_t n = (size_t)b.co_segn[q];
+        if (n) HGX_HIP(hipMemcpyAsync(h.data() + o, (const int2*)b.co_pairs + q * (size_t)b.co_pseg, sizeof(int2) * n,
+                                      hipMemcpyDeviceToHost, g->stream));
+        o += n;
     }
+    HGX_HIP(hipStreamSynchronize(g->stream));
     const size_t k = b.co_idx.size();
     std::vector<std::vector<int64_t>> pos(k);
     for (size_t j = 0; j < k; ++j) {
