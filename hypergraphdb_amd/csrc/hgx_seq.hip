@@ -1412,7 +1412,12 @@ constexpr int kLsSlots = 4;             // per-level counter slots (ring); slot 
 enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5 };
 constexpr int kLsSlotWords = 8;
 constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2;
-constexpr int kLsCtlWords = kLsStatus + 8;
+// A level's discoveries go to kLsDSegs segments of the list, one counter each (a wave appends to the
+// segment of its block): one shared counter took one same-address atomic per wave and round, which
+// serialise at ~20 ns each -- the whole of a config-2 level's expand time.
+constexpr int kLsDSegs = 32;
+constexpr int kLsDSeg = kLsStatus + 8;                           // [kLsSlots][kLsDSegs] segment counters
+constexpr int kLsCtlWords = kLsDSeg + kLsSlots * kLsDSegs;
 
 struct LsArgs {
     int64_t A;
@@ -1436,7 +1441,8 @@ struct LsArgs {
     int64_t* pre;                       // [cap + 1] exclusive degree prefix
     int64_t* tile;                      // [tcap] first entry of each item tile
     int64_t* bsum;                      // [kLsG] block sums (entries, then bitmap words)
-    int64_t* disc;                      // [cap] the level's discoveries: seed * A + atom
+    int64_t* disc;                      // [cap] the level's discoveries: seed * A + atom, kLsDSegs segments
+    int64_t segcap;                     //   of segcap entries
     u64* bm;                            // [wcap] rank bitmap
     uint32_t* wpre;                     // [wcap] popcount prefix of word w inside its block's range
     int32_t* out_link;                  // [cap] pairs, level-major (device)
@@ -1446,6 +1452,35 @@ struct LsArgs {
 };
 
 __device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
+__device__ __forceinline__ int64_t* ls_dseg(const LsArgs& a, int d) { return a.ctl + kLsDSeg + (d % kLsSlots) * kLsDSegs; }
+
+// The level's discovery count and the segments' prefix pre[0 .. kLsDSegs] (LDS; whole block).
+__device__ __forceinline__ int64_t ls_disc_prefix(const LsArgs& a, int d, int64_t* pre) {
+    if (threadIdx.x < 64) {
+        const int64_t v = threadIdx.x < kLsDSegs ? ls_dseg(a, d)[threadIdx.x] : 0;
+        int64_t x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(x, off);
+            if ((int)threadIdx.x >= off) x += y;
+        }
+        if (threadIdx.x < kLsDSegs) pre[threadIdx.x] = x - v;
+        if (threadIdx.x == kLsDSegs - 1) pre[kLsDSegs] = x;
+    }
+    __syncthreads();
+    return pre[kLsDSegs];
+}
+
+// Discovery x of the level (flat index over the segments).
+__device__ __forceinline__ int64_t ls_disc_at(const LsArgs& a, const int64_t* pre, int64_t x) {
+    int lo = 0, hi = kLsDSegs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return a.disc[(int64_t)lo * a.segcap + (x - pre[lo])];
+}
 
 __device__ __forceinline__ int64_t ls_block_sum(int64_t v, int64_t* ws) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -1530,6 +1565,7 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = sum;
     if (blockIdx.x == 0 && threadIdx.x < kLsSlotWords && threadIdx.x != lsF && threadIdx.x != lsOut)
         a.ctl[((d + 1) % kLsSlots) * kLsSlotWords + threadIdx.x] = 0;   // the next level's slot counters
+    if (blockIdx.x == 0 && threadIdx.x < kLsDSegs) ls_dseg(a, d + 1)[threadIdx.x] = 0;
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
@@ -1582,7 +1618,8 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
     const int64_t F = sl[lsF], T = sl[lsT], W = sl[lsW], nt = sl[lsTiles];
-    int64_t* dn = (int64_t*)(a.ctl + (d % kLsSlots) * kLsSlotWords + lsN);
+    const int dsg = blockIdx.x % kLsDSegs;   // this block's segment of the discovery list
+    int64_t* dn = ls_dseg(a, d) + dsg;
     const int cur = d & 1;
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
@@ -1651,8 +1688,8 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
                 base = __shfl(base, leader);
                 if (isnew) {
                     const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
-                    if ((int64_t)w < a.cap) a.disc[w] = sA + t;
-                    else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap
+                    if ((int64_t)w < a.segcap) a.disc[(int64_t)dsg * a.segcap + (int64_t)w] = sA + t;
+                    else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // a segment outgrew its share of cap
                 }
             }
         }
@@ -1660,11 +1697,11 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
-    const int64_t* sl = ls_slot(a, d);
+    __shared__ int64_t pre[kLsDSegs + 1];
     if (a.ctl[kLsStatus]) return;
-    const int64_t n = sl[lsN];
+    const int64_t n = ls_disc_prefix(a, d, pre);
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
-        const u64 kk = (a.key[a.disc[x]] >> 32) - 1ull;
+        const u64 kk = (a.key[ls_disc_at(a, pre, x)] >> 32) - 1ull;
         atomicOr(&a.bm[kk >> 6], 1ull << (kk & 63));
     }
 }
@@ -1688,11 +1725,11 @@ __global__ void __launch_bounds__(256) hgx_ls_wprefix(LsArgs a, int32_t d) {
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq) {
-    __shared__ int64_t ws[4], off[kLsG];
+    __shared__ int64_t ws[4], off[kLsG], pre[kLsDSegs + 1];
     int64_t* sl = ls_slot(a, d);
     int64_t status = a.ctl[kLsStatus];
     const int64_t W = sl[lsW], out0 = sl[lsOut];
-    int64_t n = sl[lsN];
+    int64_t n = ls_disc_prefix(a, d, pre);
     if (!status && (n > a.cap || out0 + n > a.cap)) status = 1;   // the pairs outgrow the output (every block agrees)
     if (status) n = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1700,6 +1737,7 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
         int64_t* nx = a.ctl + ((d + 1) % kLsSlots) * kLsSlotWords;
         nx[lsF] = n;
         nx[lsOut] = out0 + n;
+        sl[lsN] = n;
         // two host slots by level parity: the host reads level d while level d+1 may already be
         // publishing (it never enqueues level d+2 before it has read level d)
         u64* hf = a.hflag + 4 * (d & 1);
@@ -1712,7 +1750,7 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
     ls_block_offsets(a.bsum, off, ws);
     const int nx = (d + 1) & 1;
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
-        const int64_t sa = a.disc[x];
+        const int64_t sa = ls_disc_at(a, pre, x);
         const u64 v = a.key[sa];
         const u64 kk = (v >> 32) - 1ull;
         const int64_t w = (int64_t)(kk >> 6);
@@ -2019,6 +2057,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.tile = (int64_t*)w.take(sizeof(int64_t) * (size_t)tcap);
         a.bsum = (int64_t*)w.take(sizeof(int64_t) * kLsG);
         a.disc = (int64_t*)w.take(sizeof(int64_t) * (size_t)cap);
+        a.segcap = std::max<int64_t>(cap / kLsDSegs, 1);
         a.bm = (u64*)w.take(sizeof(u64) * (size_t)wcap);
         a.wpre = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)wcap);
         a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
