@@ -4571,7 +4571,13 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         push_volume = __atomic_load_n(slot, __ATOMIC_RELAXED);
         push_volume_nf = push_volume;
     }
-    const u64 sparse_limit = (u64)std::max<int64_t>(M / 16, 1024);
+    // HGX_SPARSE_SCALE (A/B): multiplies the push / dense threshold (M / 16 incidence entries)
+    static const double kSparseScale = [] {
+        const char* e = std::getenv("HGX_SPARSE_SCALE");
+        const double v = e ? std::atof(e) : 1.0;
+        return v > 0 ? v : 1.0;
+    }();
+    const u64 sparse_limit = (u64)std::max<int64_t>((int64_t)((double)(M / 16) * kSparseScale), 1024);
     // Full-visited skipping costs two bitmap probes per pin; it pays once a sizeable share of the
     // atoms is visited by every traversal (seeds that are full count from the start).
     u64 full_total = 0;

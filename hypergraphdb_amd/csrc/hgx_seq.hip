@@ -1415,9 +1415,12 @@ constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsR
 // A level's discoveries go to kLsDSegs segments of the list, one counter each (a wave appends to the
 // segment of its block): one shared counter took one same-address atomic per wave and round, which
 // serialise at ~20 ns each -- the whole of a config-2 level's expand time.
+// A segment holds segcap = cap / 64 entries; a wave whose segment is full appends the rest to the
+// shared overflow region of cap entries (one counter) behind the segments, so a level whose
+// discoveries all come from a few blocks still fits whenever they fit the capacity.
 constexpr int kLsDSegs = 32;
-constexpr int kLsDSeg = kLsStatus + 8;                           // [kLsSlots][kLsDSegs] segment counters
-constexpr int kLsCtlWords = kLsDSeg + kLsSlots * kLsDSegs;
+constexpr int kLsDSeg = kLsStatus + 8;                           // [kLsSlots][kLsDSegs + 1] counters (+ overflow)
+constexpr int kLsCtlWords = kLsDSeg + kLsSlots * (kLsDSegs + 1);
 
 struct LsArgs {
     int64_t A;
@@ -1441,8 +1444,8 @@ struct LsArgs {
     int64_t* pre;                       // [cap + 1] exclusive degree prefix
     int64_t* tile;                      // [tcap] first entry of each item tile
     int64_t* bsum;                      // [kLsG] block sums (entries, then bitmap words)
-    int64_t* disc;                      // [cap] the level's discoveries: seed * A + atom, kLsDSegs segments
-    int64_t segcap;                     //   of segcap entries
+    int64_t* disc;                      // the level's discoveries (seed * A + atom): kLsDSegs segments of
+    int64_t segcap;                     //   segcap entries, then an overflow region of cap entries
     u64* bm;                            // [wcap] rank bitmap
     uint32_t* wpre;                     // [wcap] popcount prefix of word w inside its block's range
     int32_t* out_link;                  // [cap] pairs, level-major (device)
@@ -1452,28 +1455,32 @@ struct LsArgs {
 };
 
 __device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
-__device__ __forceinline__ int64_t* ls_dseg(const LsArgs& a, int d) { return a.ctl + kLsDSeg + (d % kLsSlots) * kLsDSegs; }
+__device__ __forceinline__ int64_t* ls_dseg(const LsArgs& a, int d) {
+    return a.ctl + kLsDSeg + (d % kLsSlots) * (kLsDSegs + 1);
+}
 
 // The level's discovery count and the segments' prefix pre[0 .. kLsDSegs] (LDS; whole block).
 __device__ __forceinline__ int64_t ls_disc_prefix(const LsArgs& a, int d, int64_t* pre) {
-    if (threadIdx.x < 64) {
-        const int64_t v = threadIdx.x < kLsDSegs ? ls_dseg(a, d)[threadIdx.x] : 0;
+    if (threadIdx.x < 64) {   // segment counters past their capacity spilled into the overflow region
+        const int64_t ovfcap = a.cap;
+        const int64_t c = threadIdx.x <= kLsDSegs ? ls_dseg(a, d)[threadIdx.x] : 0;
+        const int64_t v = threadIdx.x < kLsDSegs ? min(c, a.segcap) : threadIdx.x == kLsDSegs ? min(c, ovfcap) : 0;
         int64_t x = v;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const int64_t y = __shfl_up(x, off);
             if ((int)threadIdx.x >= off) x += y;
         }
-        if (threadIdx.x < kLsDSegs) pre[threadIdx.x] = x - v;
-        if (threadIdx.x == kLsDSegs - 1) pre[kLsDSegs] = x;
+        if (threadIdx.x <= kLsDSegs) pre[threadIdx.x] = x - v;
+        if (threadIdx.x == kLsDSegs) pre[kLsDSegs + 1] = x;
     }
     __syncthreads();
-    return pre[kLsDSegs];
+    return pre[kLsDSegs + 1];
 }
 
-// Discovery x of the level (flat index over the segments).
+// Discovery x of the level (flat index over the segments, then the overflow region).
 __device__ __forceinline__ int64_t ls_disc_at(const LsArgs& a, const int64_t* pre, int64_t x) {
-    int lo = 0, hi = kLsDSegs - 1;
+    int lo = 0, hi = kLsDSegs;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (pre[mid] <= x) lo = mid;
@@ -1565,7 +1572,7 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = sum;
     if (blockIdx.x == 0 && threadIdx.x < kLsSlotWords && threadIdx.x != lsF && threadIdx.x != lsOut)
         a.ctl[((d + 1) % kLsSlots) * kLsSlotWords + threadIdx.x] = 0;   // the next level's slot counters
-    if (blockIdx.x == 0 && threadIdx.x < kLsDSegs) ls_dseg(a, d + 1)[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x <= kLsDSegs) ls_dseg(a, d + 1)[threadIdx.x] = 0;
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
@@ -1683,13 +1690,24 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             const u64 m = __ballot(isnew);
             if (m) {
                 const int leader = __ffsll((long long)m) - 1;
-                u64 base = 0;
-                if (lane == leader) base = atomicAdd((unsigned long long*)dn, (u64)__popcll(m));
+                const u64 cnt = (u64)__popcll(m), segcap = (u64)a.segcap;
+                u64 base = 0, ob = 0;
+                if (lane == leader) {
+                    base = atomicAdd((unsigned long long*)dn, cnt);
+                    const u64 fit = base >= segcap ? 0ull : min(cnt, segcap - base);
+                    if (fit < cnt) ob = atomicAdd((unsigned long long*)(ls_dseg(a, d) + kLsDSegs), cnt - fit);
+                }
                 base = __shfl(base, leader);
+                ob = __shfl(ob, leader);
                 if (isnew) {
                     const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
-                    if ((int64_t)w < a.segcap) a.disc[(int64_t)dsg * a.segcap + (int64_t)w] = sA + t;
-                    else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // a segment outgrew its share of cap
+                    if (w < segcap) {
+                        a.disc[(int64_t)dsg * a.segcap + (int64_t)w] = sA + t;
+                    } else {   // the segment is full: the shared overflow region
+                        const int64_t o = (int64_t)(ob + (w - max(base, segcap)));
+                        if (o < a.cap) a.disc[(int64_t)kLsDSegs * a.segcap + o] = sA + t;
+                        else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap holds
+                    }
                 }
             }
         }
@@ -1697,7 +1715,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
-    __shared__ int64_t pre[kLsDSegs + 1];
+    __shared__ int64_t pre[kLsDSegs + 2];
     if (a.ctl[kLsStatus]) return;
     const int64_t n = ls_disc_prefix(a, d, pre);
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
@@ -1725,7 +1743,7 @@ __global__ void __launch_bounds__(256) hgx_ls_wprefix(LsArgs a, int32_t d) {
 }
 
 __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq) {
-    __shared__ int64_t ws[4], off[kLsG], pre[kLsDSegs + 1];
+    __shared__ int64_t ws[4], off[kLsG], pre[kLsDSegs + 2];
     int64_t* sl = ls_slot(a, d);
     int64_t status = a.ctl[kLsStatus];
     const int64_t W = sl[lsW], out0 = sl[lsOut];
@@ -2056,8 +2074,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.pre = (int64_t*)w.take(sizeof(int64_t) * (size_t)(std::max<int64_t>(cap, nb) + 1));
         a.tile = (int64_t*)w.take(sizeof(int64_t) * (size_t)tcap);
         a.bsum = (int64_t*)w.take(sizeof(int64_t) * kLsG);
-        a.disc = (int64_t*)w.take(sizeof(int64_t) * (size_t)cap);
-        a.segcap = std::max<int64_t>(cap / kLsDSegs, 1);
+        a.segcap = cap / (2 * kLsDSegs);   // the segments (half of cap), then an overflow region of cap
+        a.disc = (int64_t*)w.take(sizeof(int64_t) * (size_t)(cap + kLsDSegs * a.segcap));
         a.bm = (u64*)w.take(sizeof(u64) * (size_t)wcap);
         a.wpre = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)wcap);
         a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
