@@ -3838,8 +3838,8 @@ struct Timer {
     hipEvent_t chain = nullptr;   // the last stop event when nothing was enqueued after it
     explicit Timer(hgx_graph* gg) : g(gg), on(gg->timing) {
         if (on) {
-            HGX_HIP(hipEventCreate(&all.a));
-            HGX_HIP(hipEventCreate(&all.b));
+            all.a = take();
+            all.b = take();
         }
     }
     ~Timer() {   // events go back to the graph's pool (the caller holds g->mu)
@@ -3847,8 +3847,8 @@ struct Timer {
             if (r.own_a) g->ev_pool.push_back(r.e.a);
             g->ev_pool.push_back(r.e.b);
         }
-        if (all.a) (void)hipEventDestroy(all.a);
-        if (all.b) (void)hipEventDestroy(all.b);
+        if (all.a) g->ev_pool.push_back(all.a);
+        if (all.b) g->ev_pool.push_back(all.b);
     }
     hipEvent_t take() {
         if (!g->ev_pool.empty()) {

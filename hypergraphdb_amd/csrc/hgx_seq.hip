@@ -1852,6 +1852,22 @@ struct SeqOut {
 
 PoolBuf take_host_buf(hgx_graph* g, size_t bytes);
 
+// Timing events from the graph's pool (caller holds g->mu): creating and destroying two events per
+// call cost more than the short launches they time.
+hipEvent_t ev_take(hgx_graph* g) {
+    if (!g->ev_pool.empty()) {
+        hipEvent_t e = g->ev_pool.back();
+        g->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HGX_HIP(hipEventCreate(&e));
+    return e;
+}
+void ev_give(hgx_graph* g, hipEvent_t e) {
+    if (e) g->ev_pool.push_back(e);
+}
+
 // Key widths of the level-synchronous engine and the block engine's yield rank (once per snapshot).
 void seq_maxes(hgx_graph* g) {
     if (g->max_deg >= 0) return;
@@ -2253,8 +2269,8 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     }
     hipEvent_t ev[2] = {nullptr, nullptr};
     if (g->timing) {
-        HGX_HIP(hipEventCreate(&ev[0]));
-        HGX_HIP(hipEventCreate(&ev[1]));
+        ev[0] = ev_take(g);
+        ev[1] = ev_take(g);
         HGX_HIP(hipEventRecord(ev[0], st));
     }
     struct Chunk {
@@ -2291,8 +2307,8 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         float ms = 0;
         HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
         out.ms = ms;
-        (void)hipEventDestroy(ev[0]);
-        (void)hipEventDestroy(ev[1]);
+        ev_give(g, ev[0]);
+        ev_give(g, ev[1]);
     }
     if (dseeds) g->release(dseeds, dseeds_n);
     for (auto& c : chunks) {
@@ -2398,8 +2414,8 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         hm[0] = -1;
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (g->timing) {
-            HGX_HIP(hipEventCreate(&ev[0]));
-            HGX_HIP(hipEventCreate(&ev[1]));
+            ev[0] = ev_take(g);
+            ev[1] = ev_take(g);
             HGX_HIP(hipEventRecord(ev[0], st));
         }
         hgx_bfs_coop<<<(unsigned)g->co_ok, kCoThreads, 0, st>>>(a);
@@ -2410,8 +2426,8 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             float ms = 0;
             HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
             out.co_ms += ms;
-            (void)hipEventDestroy(ev[0]);
-            (void)hipEventDestroy(ev[1]);
+            ev_give(g, ev[0]);
+            ev_give(g, ev[1]);
         }
         const int64_t status = hm[0];
         if (status != 0) {   // the bitmaps may hold bits of atoms no pair records: clear them whole
@@ -2583,8 +2599,8 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (g->timing) {
-        HGX_HIP(hipEventCreate(&ev0));
-        HGX_HIP(hipEventCreate(&ev1));
+        ev0 = ev_take(g);
+        ev1 = ev_take(g);
         HGX_HIP(hipEventRecord(ev0, st));
     }
     std::vector<int32_t> rerun;   // seed indices for the level-synchronous engine
@@ -2647,7 +2663,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         }
         hipEvent_t evb = nullptr;
         if (g->timing) {
-            HGX_HIP(hipEventCreate(&evb));
+            evb = ev_take(g);
             HGX_HIP(hipEventRecord(evb, st));
         }
         spin_sync(st);
@@ -2655,7 +2671,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             float ms = 0;
             HGX_HIP(hipEventElapsedTime(&ms, ev0, evb));
             r->ms_block = ms;
-            (void)hipEventDestroy(evb);
+            ev_give(g, evb);
         }
         if (dseeds) g->release(dseeds, dseeds_n);
         for (auto& c : chunks) {
@@ -2701,8 +2717,8 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         float ms = 0;
         HGX_HIP(hipEventElapsedTime(&ms, ev0, ev1));
         r->ms_total = ms;
-        (void)hipEventDestroy(ev0);
-        (void)hipEventDestroy(ev1);
+        ev_give(g, ev0);
+        ev_give(g, ev1);
     }
     r->off.assign((size_t)n_seeds + 1, 0);
     for (int32_t i = 0; i < n_seeds; ++i) r->off[i + 1] = r->off[i] + cnt[i];
