@@ -32,6 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -736,6 +739,12 @@ struct BbArgs {
     int32_t* out_cnt;                                // [n * kBbPairs]: |V_{d+1}| at d
     int64_t* meta;                                   // [4 n]: atoms (-1 = rerun), traversed items, bytes,
                                                      //        levels with news | levels expanded << 32
+    // the grid stage's selection (null: none): an overflowing seed takes slot atomicAdd(sel_n) and
+    // records its batch index (base + si) and atom there when the slot is below sel_cap
+    unsigned long long* sel_n;
+    int32_t* sel_idx;
+    int32_t* sel_seed;
+    int32_t sel_cap, base;
 };
 
 struct BbShared {
@@ -1034,6 +1043,13 @@ __device__ void bb_run(BbShared& sm, const BbArgs& a, int si) {
         a.meta[4 * (int64_t)si + 1] = trav;
         a.meta[4 * (int64_t)si + 2] = tb;
         a.meta[4 * (int64_t)si + 3] = n_lev | (n_exp << 32);
+        if (ovf && a.sel_n) {
+            const u64 j = atomicAdd(a.sel_n, 1ull);
+            if (j < (u64)a.sel_cap) {
+                a.sel_idx[j] = a.base + si;
+                a.sel_seed[j] = seed;
+            }
+        }
     }
 }
 
@@ -1048,7 +1064,7 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Multi-workgroup level loop (hgx_bfs_batch): the few seeds the workgroup stage hands back (config 5:
 // six hg.subsumed closures of 2K-101K atoms over 21 levels) in ONE persistent launch of up to
-// kCoMaxBlocks resident workgroups, a grid barrier between levels instead of the rows engine's launches and host
+// kCoBlocks resident workgroups, a grid barrier between levels instead of the rows engine's launches and host
 // turn-around per level (~50 us a level for those six seeds).
 //   - visited: one bitmap per seed (kCoMaxSeeds x A bits, kept on the graph, zero between calls: the
 //     epilogue clears the words of the atoms it found); the first atomicOr that sets an atom's bit
@@ -1068,12 +1084,17 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
 // change while some block has not read it yet (the next level writes the other one).
 constexpr int kCoThreads = 512;
 constexpr int kCoWaves = kCoThreads / 64;
-constexpr int kCoMinBlocks = 64, kCoMaxBlocks = 512;   // the grid: 2 per CU (512 on MI355X), resident
+// The grid: kCoBlocks workgroups, all resident (at most 2 per CU, one CU slot left).  Fewer, fuller
+// workgroups win: config 5's big closures took 0.75 / 0.64 / 0.59 / 0.55 / 0.58 ms with 512 / 192 /
+// 128 / 96 / 64 workgroups (the barrier and the segment counters are shared by fewer arrivals), and
+// the config-5 step 1.11 -> 0.85 ms (profiles/r04ze_coop_ab.log; HGX_CO_BLOCKS for A/B).
+constexpr int kCoMinBlocks = 64, kCoBlocks = 96, kCoMaxBlocks = 512;
 constexpr int kCoChunk = 128;   // incidence entries per work item (default; HGX_CO_CHUNK for A/B)
 // Same-address atomics serialise (one per ~20 ns): the work-item / pair counters are split into
 // kCoSegs segments (block b appends to segment b % kCoSegs, its own part of the lists) and the barrier
 // into kCoBarGroups arrival counters whose last arrival reports to the top counter.
-constexpr int kCoSegs = 32;
+constexpr int kCoSegs = 64;
+static_assert(kCoMinBlocks >= kCoSegs && kCoSegs <= 64, "every segment has a block; one wave scans the segments");
 constexpr int kCoBarGroups = 16;
 // a segment's level counter packs its work items (high 24 bits) and the pairs found (low 40)
 constexpr int kCoItemShift = 40;
@@ -1081,13 +1102,17 @@ constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
 constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s
 // ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
-// even / odd levels (the seeding: odd), [kCoBytes] algorithmic bytes, [kCoLev + slot * kCoSegs + seg]
-// level counters (3 rotating slots), then cur [k] and trav [k]
-constexpr int kCoSt = 20, kCoBytes = 22, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
+// even / odd levels (the seeding: odd), [kCoBytes] algorithmic bytes, [kCoSel] seeds the workgroup
+// stage handed over, [kCoLev + slot * kCoSegs + seg] level counters (3 rotating slots), then cur [kcap],
+// trav [kcap], and as int32: the seeds' batch indices [kcap] and atoms [kcap]
+constexpr int kCoSt = 20, kCoBytes = 22, kCoSel = 23, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
 
 struct CoArgs {
-    int32_t k;                                       // seeds (<= kMaxCoSeeds)
+    int32_t k;                                       // seeds (<= kcap); -1: the workgroup stage's overflow
+                                                     //   list (ctl[kCoSel] seeds; none run when > kcap)
+    int32_t kcap;                                    // seeds the buffers hold (<= kMaxCoSeeds)
     const int32_t* seeds;                            // device [k]
+    const int32_t* sel_idx;                          // device [kcap]: batch indices of the handed-over seeds
     const int64_t* inc_off;
     const int32_t* inc_row;
     const int32_t* inc_type;
@@ -1096,18 +1121,20 @@ struct CoArgs {
     const int32_t* tgt_idx;
     int32_t want_type, min_arity, mode, maxd;
     int32_t chunk;                                   // incidence entries per work item
+    int32_t bgroups;                                 // barrier arrival groups (1 .. kCoBarGroups)
     int64_t vwords;                                  // words of one seed's bitmap
     u64* vis;                                        // [k * vwords]
     int4* fr;                                        // [3 * kCoSegs * fr_seg] work items (atom, seed, chunk, -)
     int64_t fr_seg;
-    u64* ctl;                                        // [kCoCtlWords + 2k]
-    u64* cur;                                        // [k] atoms found per seed
-    u64* trav;                                       // [k] incidence entries of the seed's expanded atoms
+    u64* ctl;                                        // [kCoCtlWords + 2 kcap] + int32 [2 kcap]
+    u64* cur;                                        // [kcap] atoms found per seed
+    u64* trav;                                       // [kcap] incidence entries of the seed's expanded atoms
     int2* pairs;                                     // [kCoSegs * pseg] (atom, seed | level << 8)
     int64_t pseg;
-    int64_t* hmeta;                                  // mapped: [0] status, [1] levels, [2] -, [3] bytes,
-                                                     //   (atoms, traversed) per seed, pairs per segment
-    int64_t* lvl_end;                                // mapped [k * kCoMaxLevels]: cur[s] after level d
+    int64_t* hmeta;                                  // mapped: [0] status, [1] levels, [2] seeds, [3] bytes,
+                                                     //   (atoms, traversed) [kcap], pairs per segment
+                                                     //   [kCoSegs], the seeds' batch indices [kcap]
+    int64_t* lvl_end;                                // mapped [kcap * kCoMaxLevels]: cur[s] after level d
     int64_t* lvl_trace;                              // mapped [2 * kCoMaxLevels]: start clock, work items
 };
 
@@ -1115,20 +1142,27 @@ struct CoArgs {
 // the group's writes on), the group's last arrival adds to the top counter, everyone polls the top
 // counter (relaxed polls, one acquire fence after: an acquire load per poll invalidates the caches on
 // every iteration of every waiting block, ~50 us a barrier measured with 128 blocks).
-__device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status) {
+// ng = 1: every block adds to the top counter itself (one atomic on the path instead of two).
+__device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status, int ng) {
     __shared__ int s_to;
     __syncthreads();   // the block's stores and atomics of this level are issued
     if (threadIdx.x == 0) {
         ++gen;
-        const int grp = blockIdx.x % kCoBarGroups;
-        const u64 members = (u64)((gridDim.x - grp + kCoBarGroups - 1) / kCoBarGroups);
-        const u64 old = __hip_atomic_fetch_add(ctl + 1 + grp, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 == gen * members)
-            __hip_atomic_fetch_add(ctl, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        const u64 groups = (u64)min((unsigned)kCoBarGroups, gridDim.x);
+        u64 target;
+        if (ng <= 1) {
+            __hip_atomic_fetch_add(ctl, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            target = gen * gridDim.x;
+        } else {
+            const int grp = blockIdx.x % ng;
+            const u64 members = (u64)((gridDim.x - grp + ng - 1) / ng);
+            const u64 old = __hip_atomic_fetch_add(ctl + 1 + grp, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == gen * members)
+                __hip_atomic_fetch_add(ctl, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            target = gen * (u64)min((unsigned)ng, gridDim.x);
+        }
         const u64 t0 = __builtin_amdgcn_s_memrealtime();
         int to = 0;
-        while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen * groups) {
+        while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
                 atomicOr(status, 4ull);
@@ -1143,19 +1177,26 @@ __device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status) {
     return s_to != 0;
 }
 
+// A work item: atom, seed | entries << 8, first incidence entry (low, high 32 bits).  It carries its
+// range, so a level's first load is the item itself, not the atom's incidence offsets as well.
+__device__ __forceinline__ int4 co_item(int32_t t, int32_t s, int64_t lo, int64_t n) {
+    return make_int4(t, s | (int32_t)(n << 8), (int32_t)(uint32_t)lo, (int32_t)(lo >> 32));
+}
+
 // One step of a wave over yielded targets at level d (lane: target t of seed s, t < 0: none): the first
 // setter of an atom's bit discovers it; the wave's discoveries take their pair slots and their work
 // items for level d + 1 in the block's segment with one atomic, the seeds' counts go to the block's
 // LDS counters (flushed once a level).  Every lane of the wave calls it.
 __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, int32_t d, int slot_next, int seg,
-                                        u64 pbase_seg, int64_t& nbytes, unsigned long long* cnt_l) {
+                                        u64 pbase_seg, int64_t& nbytes, unsigned long long* cnt_l,
+                                        unsigned long long* trav_l) {
     const int lane = threadIdx.x & 63;
     bool nw = false;
-    int64_t deg = 0;
+    int64_t deg = 0, b0 = 0;
     if (t >= 0) {   // the bit and the target's incidence range in flight together
         u64* w = a.vis + (int64_t)s * a.vwords + (t >> 6);
         const u64 bit = 1ull << (t & 63);
-        int64_t b0 = 0, b1 = 0;
+        int64_t b1 = 0;
         if (d + 1 < a.maxd) {
             b0 = a.inc_off[t];
             b1 = a.inc_off[t + 1];
@@ -1167,6 +1208,7 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
     if (!m) return;
     if (nw) atomicAdd(&cnt_l[s], 1ull);
     const u64 nch = nw ? (u64)((deg + a.chunk - 1) / a.chunk) : 0ull;
+    if (nch) atomicAdd(&trav_l[s], (unsigned long long)deg);   // expanded at level d + 1
     u64 x = nch;   // the wave's work items and pairs: one packed reservation (items << 40 | pairs)
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1189,7 +1231,7 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
         return;
     }
     int4* fr = a.fr + ((int64_t)slot_next * kCoSegs + seg) * a.fr_seg;
-    for (u64 c = 0; c < nch; ++c) fr[base + c] = make_int4(t, s, (int)c, 0);
+    for (u64 c = 0; c < nch; ++c) fr[base + c] = co_item(t, s, b0 + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk));
     nbytes += 16 * (int64_t)nch;
 }
 
@@ -1200,28 +1242,49 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
     __shared__ unsigned long long cnt_l[kMaxCoSeeds], trav_l[kMaxCoSeeds];   // this block's per-seed counts of a level
     __shared__ int64_t seg_pre[kCoSegs + 1];                                 // the level's items per segment, prefix
     __shared__ u64 seg_pairs;                                                // pairs of this block's segment at the level
+    __shared__ u64 s_st;                                                     // the previous level's status
     if (threadIdx.x < kMaxCoSeeds) {
         cnt_l[threadIdx.x] = 0;
         trav_l[threadIdx.x] = 0;
     }
+    // the seeds: the host's list, or the workgroup stage's hand-over (written by the launches before
+    // this one on the stream; every block reads the same count and leaves together when none fit)
+    int32_t k = a.k;
+    if (k < 0) {
+        const u64 n = __hip_atomic_load(a.ctl + kCoSel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        k = n > (u64)a.kcap ? a.kcap + 1 : (int32_t)n;
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) {
+                a.hmeta[2] = (int64_t)n;
+                a.hmeta[0] = 0;
+                a.hmeta[1] = 0;
+            }
+            for (int j = threadIdx.x; j < k && j < a.kcap; j += kCoThreads)
+                a.hmeta[4 + 2 * a.kcap + kCoSegs + j] = a.sel_idx[j];
+        }
+        if (k == 0 || k > a.kcap) return;
+    }
     u64 gen = 0;
     int64_t nbytes = 0;   // algorithmic bytes of this thread (reduced into ctl[kCoBytes] at the end)
     if (blockIdx.x == 0)   // level 0 (segment 0): the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46)
-        for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
+        for (int s = threadIdx.x; s < k; s += kCoThreads) {
             const int32_t t = a.seeds[s];
             atomicOr(a.vis + (int64_t)s * a.vwords + (t >> 6), 1ull << (t & 63));
             const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
             if (a.maxd > 0 && deg > 0) {
                 const u64 nch = (u64)((deg + a.chunk - 1) / a.chunk);
+                atomicAdd(a.trav + s, (u64)deg);
                 const u64 base = atomicAdd(a.ctl + kCoLev, nch << kCoItemShift) >> kCoItemShift;
                 if ((int64_t)(base + nch) > a.fr_seg) {
                     atomicOr(a.ctl + kCoSt + 1, 1ull);
                     continue;
                 }
-                for (u64 c = 0; c < nch; ++c) a.fr[base + c] = make_int4(t, s, (int)c, 0);
+                const int64_t b = a.inc_off[t];
+                for (u64 c = 0; c < nch; ++c)
+                    a.fr[base + c] = co_item(t, s, b + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk));
             }
         }
-    bool timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt);
+    bool timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);
     int32_t d = 0;
     u64 pbase = 0;   // pairs of this block's segment found before the current level
     for (; !timed_out; ++d) {
@@ -1241,13 +1304,18 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
             if (threadIdx.x < kCoSegs) seg_pre[threadIdx.x] = x - v;
             if (threadIdx.x == kCoSegs - 1) seg_pre[kCoSegs] = x;
             if ((int)threadIdx.x == seg) seg_pairs = packed & kCoPairMask;
+        } else if (threadIdx.x == 64) {   // errors of level d - 1 (its parity word; level d writes the other one)
+            s_st = __hip_atomic_load(a.ctl + kCoSt + ((d + 1) & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (blockIdx.x == 0 && d > 0 && threadIdx.x >= 128 && (int)threadIdx.x < 128 + k) {
+            const int s = threadIdx.x - 128;   // every seed's atom count after level d - 1
+            a.lvl_end[(int64_t)s * kCoMaxLevels + d - 1] =
+                (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
+        __syncthreads();   // (the three loads above come from different waves: in flight together)
         const int64_t nf = seg_pre[kCoSegs];
         pbase += seg_pairs;
-        // errors of level d - 1 (its parity word; level d writes the other one)
-        const u64 st = __hip_atomic_load(a.ctl + kCoSt + ((d + 1) & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();   // seg_pre / seg_pairs are read before the next level rewrites them
+        const u64 st = s_st;
+        __syncthreads();   // seg_pre / seg_pairs / s_st are read before the next level rewrites them
         if (st != 0 || nf == 0 || d >= a.maxd) break;   // the same decision in every block
         if (d >= kCoMaxLevels) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + kCoSt, 3ull);
@@ -1280,12 +1348,10 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                 }
                 const int4 e = fr[(int64_t)lo * a.fr_seg + (it - seg_pre[lo])];
                 ip = e.x;
-                is = e.y;
-                const int64_t b = a.inc_off[ip], en = a.inc_off[ip + 1];
-                if (e.z == 0) atomicAdd(&trav_l[is], (unsigned long long)(en - b));
-                ilo = b + (int64_t)e.z * a.chunk;
-                icnt = min(en, ilo + a.chunk) - ilo;
-                nbytes += 32 + (a.yf ? icnt : 0);   // the item, its offsets, the streamed flags
+                is = e.y & 0xFF;
+                ilo = (int64_t)(uint32_t)e.z | (int64_t)e.w << 32;
+                icnt = (int64_t)(e.y >> 8);
+                nbytes += 16 + (a.yf ? icnt : 0);   // the item, the streamed flags
             }
             int64_t x = icnt;
 #pragma unroll
@@ -1304,13 +1370,17 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                 }
                 const int32_t p = __shfl(ip, o), s = __shfl(is, o);
                 const int64_t ii = __shfl(ilo, o) + (f - __shfl(ex, o));
-                bool act = f < T && (!a.yf || ((a.yf[ii] >> a.mode) & 1));   // a target this mode can yield
+                // the flag, the link and its type in flight together
+                const bool in = f < T;
+                const uint8_t yfl = in && a.yf ? a.yf[ii] : (uint8_t)0xFF;
+                const int32_t L = in ? a.inc_row[ii] : 0;
+                const int32_t lty = in && a.want_type >= 0 ? a.inc_type[ii] : a.want_type;
+                bool act = in && ((yfl >> a.mode) & 1);   // a target this mode can yield
                 int64_t tb = 0;
                 int32_t qlo = 0, qhi = 0;
                 if (act) {
-                    const int32_t L = a.inc_row[ii];
                     nbytes += a.want_type >= 0 ? 8 : 4;
-                    act = a.want_type < 0 || a.inc_type[ii] == a.want_type;   // linkPredicate (:300)
+                    act = lty == a.want_type;   // linkPredicate (:300)
                     if (act) {
                         tb = a.tgt_off[L];
                         const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
@@ -1337,22 +1407,18 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                         t = a.tgt_idx[tb + q];
                         if (t == p) t = -1;
                     }
-                    co_step(a, s, t, d, slot_next, seg, pbase, nbytes, cnt_l);
+                    co_step(a, s, t, d, slot_next, seg, pbase, nbytes, cnt_l, trav_l);
                 }
             }
         }
         __syncthreads();   // the block's per-seed counts of this level -> the seed counters
-        for (int j = threadIdx.x; j < a.k; j += kCoThreads) {
+        for (int j = threadIdx.x; j < k; j += kCoThreads) {
             if (cnt_l[j]) atomicAdd(a.cur + j, cnt_l[j]);
             if (trav_l[j]) atomicAdd(a.trav + j, trav_l[j]);
             cnt_l[j] = 0;
             trav_l[j] = 0;
         }
-        timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt);
-        if (blockIdx.x == 0 && !timed_out)   // every seed's atom count after level d
-            for (int s = threadIdx.x; s < a.k; s += kCoThreads)
-                a.lvl_end[(int64_t)s * kCoMaxLevels + d] =
-                    (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);
     }
     if (timed_out) return;   // the host clears the bitmaps
     for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
@@ -1369,18 +1435,18 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
             a.vis[(int64_t)(pr.y & 0xFF) * a.vwords + (pr.x >> 6)] = 0ull;
         }
         if (blockIdx.x == 0)
-            for (int s = threadIdx.x; s < a.k; s += kCoThreads) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
+            for (int s = threadIdx.x; s < k; s += kCoThreads) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
     }
-    if (blockIdx.x < kCoSegs && threadIdx.x == 0) a.hmeta[4 + 2 * a.k + blockIdx.x] = (int64_t)pbase;   // pairs per segment
+    if (blockIdx.x < kCoSegs && threadIdx.x == 0) a.hmeta[4 + 2 * a.kcap + blockIdx.x] = (int64_t)pbase;   // pairs per segment
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.hmeta[0] = (int64_t)st;
         a.hmeta[1] = d;
     }
-    co_barrier(a.ctl, gen, a.ctl + kCoSt);   // every block's byte count is in
+    co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);   // every block's byte count is in
     if (blockIdx.x == 0 && threadIdx.x == 0)   // + the pairs written and the bitmap words cleared
         a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + kCoBytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0)
-        for (int s = threadIdx.x; s < a.k; s += kCoThreads) {
+        for (int s = threadIdx.x; s < k; s += kCoThreads) {
             a.hmeta[4 + 2 * s] = (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.hmeta[5 + 2 * s] = (int64_t)__hip_atomic_load(a.trav + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2231,10 +2297,218 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
     }
 }
 
-}  // namespace
+// ---- the multi-workgroup stage, host side ----
 
+// Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
+// 2 per CU and one CU slot left for other streams' kernels.
+bool co_fits(hgx_graph* g) {
+    if (g->co_ok < 0) {
+        int per_cu = 0, cus = 0;
+        HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop, kCoThreads, 0));
+        HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
+        const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
+        static const int cap_env = std::getenv("HGX_CO_BLOCKS") ? std::atoi(std::getenv("HGX_CO_BLOCKS")) : 0;   // A/B
+        const int64_t cap = cap_env >= kCoMinBlocks ? std::min(cap_env, kCoMaxBlocks) : kCoBlocks;
+        g->co_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, cap) : 0;
+    }
+    return g->co_ok > 0;
+}
+
+// One launch of the grid stage: its scratch, pair list and mapped readout, returned to the graph's
+// pools with it unless the result took the pairs.
+struct CoRun {
+    hgx_graph* g;
+    SeqScratch sc;
+    CoArgs a{};
+    int2* pairs = nullptr;
+    int64_t pcap = 0;
+    PoolBuf hb{nullptr, 0};
+    int64_t* hm = nullptr;                  // the mapped readout (CoArgs::hmeta)
+    size_t m_seg = 0, m_sel = 0, m_lev = 0;  // its pairs-per-segment, batch-index and level-count parts
+    explicit CoRun(hgx_graph* gg) : g(gg), sc{gg, {}} {}
+    CoRun(const CoRun&) = delete;
+    CoRun& operator=(const CoRun&) = delete;
+    ~CoRun() {
+        if (pairs) g->release(pairs, sizeof(int2) * (size_t)pcap);
+        if (hb.p) {
+            std::lock_guard<std::mutex> lk(g->seq_mu);
+            g->seq_hbufs.push_back(hb);
+        }
+    }
+};
+
+// Buffers and arguments of a launch over k seeds (k = -1: the workgroup stage's hand-over, up to kcap
+// seeds); the control words are cleared on the stream.
+void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth, const hgx_algen_opts& o) {
+    hipStream_t st = g->stream;
+    const int mode = seq_mode(o);
+    const int64_t vwords = g->A / 64 + 1;
+    if (g->co_vis_seeds < kcap) {   // zero-invariant bitmaps, grown to the seed count
+        if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
+        g->co_vis = nullptr;
+        g->co_vis_seeds = 0;
+        const int64_t want = std::max<int64_t>(kcap, 8);
+        HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(want * vwords)));
+        HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(want * vwords), st));
+        g->co_vis_seeds = want;
+    }
+    if (g->co_pcap == 0) g->co_pcap = (int64_t)1 << 22;
+    const int64_t fr_seg = ((int64_t)1 << 21) / kCoSegs;   // work items per segment and level
+    r.pcap = g->co_pcap;
+    int4* fr = (int4*)r.sc.take(sizeof(int4) * 3 * kCoSegs * (size_t)fr_seg);
+    r.pairs = (int2*)g->alloc(sizeof(int2) * (size_t)r.pcap);
+    const size_t ctl_words = kCoCtlWords + 2 * (size_t)kcap;
+    const size_t ctl_bytes = sizeof(u64) * ctl_words + 2 * sizeof(int32_t) * (size_t)kcap;
+    u64* ctl = (u64*)r.sc.take(ctl_bytes);
+    int32_t* sel_idx = (int32_t*)(ctl + ctl_words);
+    HGX_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
+    r.m_seg = 4 + 2 * (size_t)kcap;
+    r.m_sel = r.m_seg + kCoSegs;
+    r.m_lev = r.m_sel + (size_t)kcap;
+    r.hb = take_host_buf(g, sizeof(int64_t) * (r.m_lev + (size_t)(kcap + 2) * kCoMaxLevels));
+    r.hm = (int64_t*)r.hb.p;
+    r.hm[0] = -1;
+    r.hm[2] = k;
+    void* hmd = nullptr;
+    HGX_HIP(hipHostGetDevicePointer(&hmd, r.hm, 0));
+    CoArgs& a = r.a;
+    a.k = k;
+    a.kcap = kcap;
+    a.sel_idx = sel_idx;
+    a.seeds = sel_idx + kcap;
+    a.inc_off = g->inc_off;
+    a.inc_row = g->inc_row;
+    a.inc_type = g->inc_type;
+    a.yf = mode != sSym ? g->inc_yf : nullptr;
+    a.tgt_off = g->tgt_off;
+    a.tgt_idx = g->tgt_idx;
+    a.want_type = o.link_type;
+    a.min_arity = o.return_source ? 1 : 2;
+    a.mode = mode;
+    a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
+    static const int chunk_env = std::getenv("HGX_CO_CHUNK") ? std::atoi(std::getenv("HGX_CO_CHUNK")) : 0;
+    a.chunk = chunk_env > 0 ? std::min(chunk_env, 1 << 20) : kCoChunk;   // entries < 2^23 (co_item)
+    static const int bg_env = std::getenv("HGX_CO_BARGROUPS") ? std::atoi(std::getenv("HGX_CO_BARGROUPS")) : 0;   // A/B
+    a.bgroups = bg_env > 0 ? std::min(bg_env, kCoBarGroups) : 1;
+    a.vwords = vwords;
+    a.vis = g->co_vis;
+    a.fr = fr;
+    a.fr_seg = fr_seg;
+    a.ctl = ctl;
+    a.cur = ctl + kCoCtlWords;
+    a.trav = ctl + kCoCtlWords + kcap;
+    a.pairs = r.pairs;
+    a.pseg = r.pcap / kCoSegs;
+    a.hmeta = (int64_t*)hmd;
+    a.lvl_end = (int64_t*)hmd + r.m_lev;
+    a.lvl_trace = a.lvl_end + (size_t)kcap * kCoMaxLevels;
+}
+
+void co_launch(hgx_graph* g, CoRun& r) {
+    hgx_bfs_coop<<<(unsigned)g->co_ok, kCoThreads, 0, g->stream>>>(r.a);
+    HGX_CHECK_LAUNCH();
+}
+
+// A finished launch (status 0) over the seeds sidx (its seed j = batch index sidx[j]) -> out; the
+// result takes the pair list.
+void co_collect(hgx_graph* g, CoRun& r, const std::vector<int32_t>& sidx, BlockSet& out) {
+    const int32_t k = (int32_t)sidx.size();
+    const int64_t* hm = r.hm;
+    const int32_t nlev = (int32_t)hm[1];   // level counts per seed from the per-level atom counts
+    static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
+    if (trace) {   // per level: microseconds since the first level, work items
+        const int64_t* tr = hm + r.m_lev + (size_t)r.a.kcap * kCoMaxLevels;
+        std::fprintf(stderr, "[hgx coop] k=%d levels=%d:", k, nlev);
+        for (int32_t d = 0; d < nlev; ++d)
+            std::fprintf(stderr, " %.1f/%lld", (tr[2 * d] - tr[0]) / 100.0, (long long)tr[2 * d + 1]);
+        std::fprintf(stderr, "\n");
+    }
+    out.co_pairs = r.pairs;
+    out.co_bytes = sizeof(int2) * (size_t)r.pcap;
+    out.co_pseg = r.a.pseg;
+    r.pairs = nullptr;
+    out.co_segn.assign(hm + r.m_seg, hm + r.m_seg + kCoSegs);
+    out.co_n = 0;
+    for (int64_t c : out.co_segn) out.co_n += c;
+    out.co_idx = sidx;
+    out.co_lcnt.assign((size_t)k, {});
+    out.co_atoms.assign((size_t)k, {});
+    for (int32_t j = 0; j < k; ++j) {
+        const int64_t* le = hm + r.m_lev + (int64_t)j * kCoMaxLevels;
+        std::vector<int32_t>& lc = out.co_lcnt[j];
+        int64_t prev = 0;
+        for (int32_t d = 0; d < nlev; ++d) {
+            lc.push_back((int32_t)(le[d] - prev));
+            prev = le[d];
+        }
+        while (!lc.empty() && lc.back() == 0) lc.pop_back();
+        const int32_t i = sidx[j];
+        out.pairs[i] = (int32_t)hm[4 + 2 * j];
+        out.levels[i] = (int32_t)lc.size();
+        out.lcnt[i] = lc.data();
+        out.atoms[i] = nullptr;   // block_materialize
+        out.traversed += (double)hm[5 + 2 * j];
+    }
+    out.expanded = std::max(out.expanded, nlev);
+    out.co_bytes_alg = (double)hm[3] + 16.0 * (double)out.co_n;   // + the pairs and the bitmap words cleared
+}
+
+// A launch that did not finish: the bitmaps may hold bits of atoms no pair records, so they are
+// cleared whole; true when only the pair list was short (grown to what was found: run again).
+bool co_failed(hgx_graph* g, CoRun& r, bool may_grow) {
+    const int64_t vwords = g->A / 64 + 1;
+    HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), g->stream));
+    if (r.hm[0] != 2 || !may_grow) return false;
+    int64_t most = 0;
+    for (int q = 0; q < kCoSegs; ++q) most = std::max(most, r.hm[r.m_seg + q]);
+    g->co_pcap = std::max<int64_t>(2 * r.pcap, kCoSegs * (most + most / 4 + 64));
+    return true;
+}
+
+float ev_ms(hgx_graph* g, hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    HGX_HIP(hipEventElapsedTime(&ms, a, b));
+    return ms;
+}
+
+// The multi-workgroup stage over the seeds sidx (indices into seeds); true when they finished there
+// (false: a capacity or the grid did not fit, and the rows engine takes them).
 bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t max_depth,
-              const hgx_algen_opts& o, BlockSet& out);
+              const hgx_algen_opts& o, BlockSet& out) {
+    hipStream_t st = g->stream;
+    const int32_t k = (int32_t)sidx.size();
+    if (k == 0 || k > kMaxCoSeeds || !co_fits(g)) return false;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        CoRun r(g);
+        co_setup(g, r, k, k, max_depth, o);
+        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
+        for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
+        HGX_HIP(hipMemcpyAsync(const_cast<int32_t*>(r.a.seeds), hs, sizeof(int32_t) * (size_t)k,
+                               hipMemcpyHostToDevice, st));
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (g->timing) {
+            ev[0] = ev_take(g);
+            ev[1] = ev_take(g);
+            HGX_HIP(hipEventRecord(ev[0], st));
+        }
+        co_launch(g, r);
+        if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+        spin_sync(st);
+        if (ev[1]) {
+            out.co_ms += ev_ms(g, ev[0], ev[1]);
+            ev_give(g, ev[0]);
+            ev_give(g, ev[1]);
+        }
+        if (r.hm[0] == 0) {
+            co_collect(g, r, sidx, out);
+            return true;
+        }
+        if (!co_failed(g, r, attempt == 0)) return false;
+    }
+    return false;
+}
+
+}  // namespace
 
 void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
                BlockSet& out) {
@@ -2258,6 +2532,18 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     a.mode = mode;
     a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
     const size_t per_seed = (size_t)kBbPairs * 8 + 32;
+    // The grid stage goes on the stream right behind the workgroup launches and reads their overflow
+    // list itself: one wait for both (HGX_CO_CHAIN=0, for A/B: a host round trip in between).
+    static const bool chain_env = !(std::getenv("HGX_CO_CHAIN") && std::atoi(std::getenv("HGX_CO_CHAIN")) == 0);
+    std::unique_ptr<CoRun> cr;
+    if (g->bfs_block == 1 && chain_env && n_seeds > 0 && co_fits(g)) {
+        cr.reset(new CoRun(g));
+        co_setup(g, *cr, -1, kMaxCoSeeds, max_depth, o);
+        a.sel_n = cr->a.ctl + kCoSel;
+        a.sel_idx = const_cast<int32_t*>(cr->a.sel_idx);
+        a.sel_seed = const_cast<int32_t*>(cr->a.seeds);
+        a.sel_cap = kMaxCoSeeds;
+    }
     int32_t* dseeds = nullptr;
     size_t dseeds_n = 0;
     if (n_seeds > kSbInline) {
@@ -2267,10 +2553,9 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         std::memcpy(hs, seeds, dseeds_n);
         HGX_HIP(hipMemcpyAsync(dseeds, hs, dseeds_n, hipMemcpyHostToDevice, st));
     }
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (g->timing) {
-        ev[0] = ev_take(g);
-        ev[1] = ev_take(g);
+        for (auto& e : ev) e = ev_take(g);
         HGX_HIP(hipEventRecord(ev[0], st));
     }
     struct Chunk {
@@ -2288,10 +2573,11 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         char* d = (char*)dv;
         // layout: meta [4 nb] int64 | atoms [nb * kBbPairs] | level counts [nb * kBbPairs]
         a.n = (int32_t)nb;
+        a.base = (int32_t)c0;
         a.meta = (int64_t*)d;
         a.out_atom = (int32_t*)(d + 32 * nb);
         a.out_cnt = a.out_atom + nb * kBbPairs;
-        if (n_seeds <= kSbInline) {
+        if (nb <= kSbInline) {   // the kernel reads the inline seeds whenever n <= kSbInline
             for (int64_t i = 0; i < nb; ++i) a.seed_inline[i] = seeds[c0 + i];
             a.seeds = nullptr;
         } else {
@@ -2302,13 +2588,16 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         chunks.push_back({c0, nb, (char*)hb.p});
     }
     if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+    if (cr) {
+        co_launch(g, *cr);
+        if (ev[2]) HGX_HIP(hipEventRecord(ev[2], st));
+    }
     spin_sync(st);
+    int64_t nsel = cr ? cr->hm[2] : 0;   // seeds the chained grid stage took (> kMaxCoSeeds: none run)
     if (ev[1]) {
-        float ms = 0;
-        HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
-        out.ms = ms;
-        ev_give(g, ev[0]);
-        ev_give(g, ev[1]);
+        out.ms = ev_ms(g, ev[0], ev[1]);
+        if (cr && nsel > 0 && nsel <= kMaxCoSeeds) out.co_ms += ev_ms(g, ev[1], ev[2]);
+        for (auto& e : ev) ev_give(g, e);
     }
     if (dseeds) g->release(dseeds, dseeds_n);
     for (auto& c : chunks) {
@@ -2332,161 +2621,27 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     }
     if (g->bfs_block == 2)
         for (int32_t i = 0; i < n_seeds; ++i) out.rerun.push_back(i);
+    if (cr) {
+        if (nsel != (int64_t)out.rerun.size())
+            throw std::runtime_error("hgx_bfs_batch: the grid stage took " + std::to_string(nsel) + " of " +
+                                     std::to_string(out.rerun.size()) + " handed-over seeds");
+        if (nsel == 0 || nsel > kMaxCoSeeds) return;   // none, or more than fit: the rows engine
+        std::vector<int32_t> sidx(cr->hm + cr->m_sel, cr->hm + cr->m_sel + nsel);   // the slots' order
+        if (cr->hm[0] == 0) {
+            co_collect(g, *cr, sidx, out);
+            out.n_coop = (int32_t)nsel;
+            out.rerun.clear();
+            return;
+        }
+        const bool again = co_failed(g, *cr, true);
+        cr.reset();
+        if (!again) return;
+    }
     // the few seeds that outgrew a workgroup: one multi-workgroup launch, else the rows engine
     if (!out.rerun.empty() && out.rerun.size() <= (size_t)kMaxCoSeeds && bfs_coop(g, seeds, out.rerun, max_depth, o, out)) {
         out.n_coop = (int32_t)out.rerun.size();
         out.rerun.clear();
     }
-}
-
-// The multi-workgroup stage over the seeds sidx (indices into seeds); true when they finished there
-// (false: a capacity or the grid did not fit, and the rows engine takes them).
-bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t max_depth,
-              const hgx_algen_opts& o, BlockSet& out) {
-    hipStream_t st = g->stream;
-    const int32_t k = (int32_t)sidx.size();
-    if (k == 0 || k > kMaxCoSeeds) return false;
-    if (g->co_ok < 0) {   // every workgroup of the grid must be resident at once (the barrier waits for all):
-        int per_cu = 0, cus = 0;   // at most 2 per CU and one CU slot left for other streams' kernels
-        HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop, kCoThreads, 0));
-        HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
-        const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
-        g->co_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, kCoMaxBlocks) : 0;
-    }
-    if (!g->co_ok) return false;
-    const int mode = seq_mode(o);
-    const int64_t vwords = g->A / 64 + 1;
-    if (g->co_vis_seeds < k) {   // zero-invariant bitmaps, grown to the seed count
-        if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
-        g->co_vis = nullptr;
-        g->co_vis_seeds = 0;
-        const int64_t want = std::max<int64_t>(k, 8);
-        HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(want * vwords)));
-        HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(want * vwords), st));
-        g->co_vis_seeds = want;
-    }
-    if (g->co_pcap == 0) g->co_pcap = (int64_t)1 << 22;
-    const int64_t fr_seg = ((int64_t)1 << 20) / kCoSegs;   // work items per segment and level
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const int64_t pcap = g->co_pcap, pseg = pcap / kCoSegs;
-        SeqScratch sc{g, {}};
-        int4* fr = (int4*)sc.take(sizeof(int4) * 3 * kCoSegs * (size_t)fr_seg);
-        int2* pairs = (int2*)g->alloc(sizeof(int2) * (size_t)pcap);
-        const size_t ctl_words = kCoCtlWords + 2 * (size_t)k;
-        u64* ctl = (u64*)sc.take(sizeof(u64) * ctl_words + sizeof(int32_t) * (size_t)k);
-        int32_t* dseeds = (int32_t*)(ctl + ctl_words);
-        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
-        for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
-        HGX_HIP(hipMemsetAsync(ctl, 0, sizeof(u64) * ctl_words, st));
-        HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
-        const size_t m_seg = 4 + 2 * (size_t)k, m_lev = m_seg + kCoSegs;   // mapped layout (CoArgs::hmeta)
-        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (m_lev + (size_t)(k + 2) * kCoMaxLevels));
-        int64_t* hm = (int64_t*)hb.p;
-        void* hmd = nullptr;
-        HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
-        CoArgs a{};
-        a.k = k;
-        a.seeds = dseeds;
-        a.inc_off = g->inc_off;
-        a.inc_row = g->inc_row;
-        a.inc_type = g->inc_type;
-        a.yf = mode != sSym ? g->inc_yf : nullptr;
-        a.tgt_off = g->tgt_off;
-        a.tgt_idx = g->tgt_idx;
-        a.want_type = o.link_type;
-        a.min_arity = o.return_source ? 1 : 2;
-        a.mode = mode;
-        a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
-        static const int chunk_env = std::getenv("HGX_CO_CHUNK") ? std::atoi(std::getenv("HGX_CO_CHUNK")) : 0;
-        a.chunk = chunk_env > 0 ? chunk_env : kCoChunk;
-        a.vwords = vwords;
-        a.vis = g->co_vis;
-        a.fr = fr;
-        a.fr_seg = fr_seg;
-        a.ctl = ctl;
-        a.cur = ctl + kCoCtlWords;
-        a.trav = ctl + kCoCtlWords + k;
-        a.pairs = pairs;
-        a.pseg = pseg;
-        a.hmeta = (int64_t*)hmd;
-        a.lvl_end = (int64_t*)hmd + m_lev;
-        a.lvl_trace = a.lvl_end + (size_t)k * kCoMaxLevels;
-        hm[0] = -1;
-        hipEvent_t ev[2] = {nullptr, nullptr};
-        if (g->timing) {
-            ev[0] = ev_take(g);
-            ev[1] = ev_take(g);
-            HGX_HIP(hipEventRecord(ev[0], st));
-        }
-        hgx_bfs_coop<<<(unsigned)g->co_ok, kCoThreads, 0, st>>>(a);
-        HGX_CHECK_LAUNCH();
-        if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
-        spin_sync(st);
-        if (ev[1]) {
-            float ms = 0;
-            HGX_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
-            out.co_ms += ms;
-            ev_give(g, ev[0]);
-            ev_give(g, ev[1]);
-        }
-        const int64_t status = hm[0];
-        if (status != 0) {   // the bitmaps may hold bits of atoms no pair records: clear them whole
-            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
-            g->release(pairs, sizeof(int2) * (size_t)pcap);
-            {
-                std::lock_guard<std::mutex> lk(g->seq_mu);
-                g->seq_hbufs.push_back(hb);
-            }
-            if (status == 2 && attempt == 0) {   // only the pair list was short: grow it to what was found
-                int64_t most = 0;
-                for (int q = 0; q < kCoSegs; ++q) most = std::max(most, hm[m_seg + q]);
-                g->co_pcap = std::max<int64_t>(2 * pcap, kCoSegs * (most + most / 4 + 64));
-                continue;
-            }
-            return false;
-        }
-        // success: level counts per seed from the per-level atom counts
-        const int32_t nlev = (int32_t)hm[1];
-        static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
-        if (trace) {   // per level: microseconds since the first level, work items
-            const int64_t* tr = hm + m_lev + (size_t)k * kCoMaxLevels;
-            std::fprintf(stderr, "[hgx coop] k=%d levels=%d:", k, nlev);
-            for (int32_t d = 0; d < nlev; ++d)
-                std::fprintf(stderr, " %.1f/%lld", (tr[2 * d] - tr[0]) / 100.0, (long long)tr[2 * d + 1]);
-            std::fprintf(stderr, "\n");
-        }
-        out.co_pairs = pairs;
-        out.co_bytes = sizeof(int2) * (size_t)pcap;
-        out.co_pseg = pseg;
-        out.co_segn.assign(hm + m_seg, hm + m_seg + kCoSegs);
-        out.co_n = 0;
-        for (int64_t c : out.co_segn) out.co_n += c;
-        out.co_idx = sidx;
-        out.co_lcnt.assign((size_t)k, {});
-        out.co_atoms.assign((size_t)k, {});
-        for (int32_t j = 0; j < k; ++j) {
-            const int64_t* le = hm + m_lev + (int64_t)j * kCoMaxLevels;
-            std::vector<int32_t>& lc = out.co_lcnt[j];
-            int64_t prev = 0;
-            for (int32_t d = 0; d < nlev; ++d) {
-                lc.push_back((int32_t)(le[d] - prev));
-                prev = le[d];
-            }
-            while (!lc.empty() && lc.back() == 0) lc.pop_back();
-            const int32_t i = sidx[j];
-            out.pairs[i] = (int32_t)hm[4 + 2 * j];
-            out.levels[i] = (int32_t)lc.size();
-            out.lcnt[i] = lc.data();
-            out.atoms[i] = nullptr;   // block_materialize
-            out.traversed += (double)hm[5 + 2 * j];
-        }
-        out.expanded = std::max(out.expanded, nlev);
-        out.co_bytes_alg = (double)hm[3] + 16.0 * (double)out.co_n;   // + the pairs and the bitmap words cleared
-        std::lock_guard<std::mutex> lk(g->seq_mu);
-        g->seq_hbufs.push_back(hb);
-        return true;
-    }
-    return false;
 }
 
 void block_materialize(hgx_graph* g, BlockSet& b) {
@@ -2651,7 +2806,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             a.out_link = (int32_t*)(d + 24 * nb);
             a.out_atom = a.out_link + nb * kSbPairs;
             a.out_dist = a.out_atom + nb * kSbPairs;
-            if (n_seeds <= kSbInline) {
+            if (nb <= kSbInline) {   // the kernel reads the inline seeds whenever n <= kSbInline
                 for (int64_t i = 0; i < nb; ++i) a.seed_inline[i] = seeds[c0 + i];
                 a.seeds = nullptr;
             } else {

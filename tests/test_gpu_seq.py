@@ -83,6 +83,16 @@ def test_random_graphs_all_modes(case):
     check_seq(g, seeds, maxd, mode, lt)
 
 
+def test_ragged_last_launch():
+    """1024 + 5 seeds: the workgroup engine's second launch holds 5 seeds, passed in the kernel
+    arguments while the first launch reads a device list."""
+    rng = np.random.default_rng(77)
+    g = K.random_graph(rng, 600, 900, max_arity=5, n_types=2)
+    seeds = rng.integers(0, g["num_atoms"], 1029).astype(np.int32)
+    check_seq(g, seeds, None, K.ALGEN_MODES[0])
+    check_seq(g, seeds, 2, K.ALGEN_MODES[3], 1)
+
+
 def test_power_law_hubs_and_chunking():
     """Hubs (long incidence rows spanning many expand tiles) and a 1 MiB working-set budget that
     forces the seeds through several chunks."""
