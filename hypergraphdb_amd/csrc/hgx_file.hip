@@ -451,6 +451,10 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->hasinc = nullptr;
     if (g->inc_yf) (void)hipFree(g->inc_yf);
     g->inc_yf = nullptr;
+    free_yield_lists(g);
+    if (g->co_vis) (void)hipFree(g->co_vis);   // per-seed bitmaps sized by the old atom count
+    g->co_vis = nullptr;
+    g->co_vis_seeds = 0;
     if (g->pchunks) (void)hipFree(g->pchunks);
     g->pchunks = nullptr;
     if (g->inc_tgt) (void)hipFree(g->inc_tgt);   // inline target records of the old incidence

@@ -44,6 +44,7 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->q_ticket) (void)hipFree(g->q_ticket);
     if (g->co_vis) (void)hipFree(g->co_vis);
+    free_yield_lists(g);
     if (g->fcode) (void)hipFree(g->fcode);
     if (g->lcode) (void)hipFree(g->lcode);
     for (auto& b : g->seq_hbufs) (void)hipHostFree(b.p);

@@ -99,6 +99,16 @@ struct PoolBuf {
     size_t n;
 };
 
+// A yield list (yield_list below): the links of each atom's incidence entries that pass one link type
+// and can yield in one generator mode, in entry order.
+struct YieldList {
+    int32_t mode, type;
+    int64_t* off;   // [A + 1]
+    int32_t* row;   // [n] link ids
+    int64_t n;
+};
+constexpr size_t kMaxYieldLists = 8;
+
 // Vertex-cut partition of a snapshot over n_parts devices (hgx_part.hip):
 // every link row lives on one part; an atom is present (local) on every part holding one of its
 // links and owned by one of them.  Local ids are assigned in global id order, so every ascending
@@ -219,6 +229,8 @@ struct hgx_graph {
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
+    std::deque<hgx::YieldList> ylists;              // yield lists (snapshot only; contexts read their base's)
+    std::mutex ylist_mu;
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
     // order-exact traversal refuses to run until the caller re-asserts it.
@@ -301,7 +313,8 @@ struct hgx_graph {
 };
 
 namespace hgx {
-void graph_release(hgx_graph* g);   // drop a reference; frees at zero
+void graph_release(hgx_graph* g);
+void free_yield_lists(hgx_graph* g);   // (hgx_graph_update: the incidence changed)   // drop a reference; frees at zero
 // Builds the BFS's first-use read-only tables (has-incidence bitmap, yield flags, push chunks) on g
 // (hgx_bfs.hip; caller holds g->mu).
 void bfs_shared_tables(hgx_graph* g);
@@ -315,6 +328,11 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Builds the ordered-mode yield flags (hgx_inc_yield, one byte per incidence entry + 64 bytes of
 // padding for 16-byte vector loads) on g if absent; caller holds g->mu (hgx_bfs.hip).
 void ensure_inc_yield(hgx_graph* g);
+// Per (generator mode, link type): for each atom the links of its incidence entries of that type that
+// can yield in that mode, in entry order (off [A + 1], row [n]); built on first use on the snapshot
+// (shared by its contexts, freed with it).  nullptr for the symmetric mode without a type (the
+// incidence itself) and once kMaxYieldLists lists exist.  Caller holds g->mu (hgx_seq.hip).
+const YieldList* yield_list(hgx_graph* g, int mode, int32_t type);
 // The set-mode workgroup engine's part of one hgx_bfs_batch (hgx_seq.hip, HGX_OPT_BFS_BLOCK): per seed
 // V_1, V_2, ... one after the other (atoms) and |V_d| (lcnt[d - 1]) in mapped host buffers the
 // result owns; the seeds whose traversal outgrew a workgroup are listed in rerun (the batched engine

@@ -62,6 +62,53 @@ int seq_mode(const hgx_algen_opts& o) {
 
 int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
+// ---------------------------------------------------------------------------------------------
+// Yield lists (hgx::yield_list): per atom, the links of its incidence entries that pass a fixed link
+// type and can yield in a fixed generator mode (yield-flag bit `mode`; every entry in the symmetric
+// mode), in entry order.  One wave per atom: count, then (after the offsets' scan) a ballot-compacted
+// fill.  A traversal over them reads only the entries that can yield: a class hub whose incidence is
+// its subclasses' links costs nothing in hg.subsumes, where none of them yields.
+__device__ __forceinline__ bool yl_pass(int64_t i, const int32_t* __restrict__ inc_type, const uint8_t* __restrict__ yf,
+                                        int mode, int32_t type) {
+    return (!yf || ((yf[i] >> mode) & 1)) && (type < 0 || inc_type[i] == type);
+}
+
+__global__ void __launch_bounds__(256) hgx_yl_count(int64_t A, const int64_t* __restrict__ inc_off,
+                                                    const int32_t* __restrict__ inc_type, const uint8_t* __restrict__ yf,
+                                                    int mode, int32_t type, int64_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t v = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < A; v += nw) {
+        const int64_t b = inc_off[v], e = inc_off[v + 1];
+        int64_t c = 0;
+        for (int64_t i = b + lane; i < e; i += 64) c += yl_pass(i, inc_type, yf, mode, type) ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+        if (lane == 0) cnt[v] = c;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[A] = 0;
+}
+
+__global__ void __launch_bounds__(256) hgx_yl_fill(int64_t A, const int64_t* __restrict__ inc_off,
+                                                   const int32_t* __restrict__ inc_row,
+                                                   const int32_t* __restrict__ inc_type, const uint8_t* __restrict__ yf,
+                                                   int mode, int32_t type, const int64_t* __restrict__ off,
+                                                   int32_t* __restrict__ row) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t v = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < A; v += nw) {
+        const int64_t b = inc_off[v], e = inc_off[v + 1];
+        int64_t o = off[v];
+        for (int64_t i0 = b; i0 < e; i0 += 64) {   // wave-uniform trip count
+            const int64_t i = i0 + lane;
+            const bool ok = i < e && yl_pass(i, inc_type, yf, mode, type);
+            const u64 m = __ballot(ok);
+            if (ok) row[o + __popcll(m & ((1ull << lane) - 1ull))] = inc_row[i];
+            o += __popcll(m);
+        }
+    }
+}
+
+
 __global__ void __launch_bounds__(256) k_seq_maxes(int64_t M, const int64_t* __restrict__ tgt_off, int64_t A,
                                                    const int64_t* __restrict__ inc_off, u64* out) {
     u64 ma = 0, md = 0;
@@ -745,6 +792,10 @@ struct BbArgs {
     int32_t* sel_idx;
     int32_t* sel_seed;
     int32_t sel_cap, base;
+    // the generator's yield list (yield_list; null: stream the incidence and its yield flags): a
+    // frontier atom's items are then only the links that can yield, already of the wanted type
+    const int64_t* y_off;
+    const int32_t* y_row;
 };
 
 struct BbShared {
@@ -819,9 +870,16 @@ __device__ void bb_frontier(BbShared& sm, const BbArgs& a, int F) {
         if (i < F) {
             const int32_t p = sm.e_atom[i];
             const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
-            sm.e_fb[i] = b;
-            dg[k] = e - b;
-            sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+            if (a.y_off) {   // items: the yield list; S: the incidence entries (traversed)
+                const int64_t yb = a.y_off[p], ye = a.y_off[p + 1];
+                sm.e_fb[i] = yb;
+                dg[k] = ye - yb;
+                sg[k] = e - b;
+            } else {
+                sm.e_fb[i] = b;
+                dg[k] = e - b;
+                sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+            }
         }
         ds += dg[k];
         ss += sg[k];
@@ -848,17 +906,24 @@ __device__ void bb_frontier(BbShared& sm, const BbArgs& a, int F) {
     __syncthreads();
 }
 
-// Staged items -> the generator's yields -> examined-set inserts (as sb_process, no keys).
-__device__ void bb_process(BbShared& sm, const BbArgs& a, int F, int cn, int64_t& nbytes) {
+// Staged items (it0 < 0; items it0 + c of a yield list otherwise) -> the generator's yields ->
+// examined-set inserts (as sb_process, no keys).
+__device__ void bb_process(BbShared& sm, const BbArgs& a, int F, int cn, int64_t& nbytes, int32_t it0) {
     for (int c = threadIdx.x; c < cn; c += kBbThreads) {
         if (sm.ovf) break;   // the seed goes to the rows engine: the rest of the flush is wasted work
-        const int32_t it = sm.cand[c];
+        const int32_t it = it0 < 0 ? sm.cand[c] : it0 + c;
         const int i = sb_search(sm.e_dp, F, it);
         const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
         const int32_t p = sm.e_atom[i];
-        const int32_t L = a.inc_row[ii];
-        nbytes += a.want_type >= 0 ? 8 : 4;
-        if (a.want_type >= 0 && a.inc_type[ii] != a.want_type) continue;   // linkPredicate (:300)
+        int32_t L;
+        if (a.y_row) {   // the list holds the wanted type only
+            L = a.y_row[ii];
+            nbytes += 4;
+        } else {
+            L = a.inc_row[ii];
+            nbytes += a.want_type >= 0 ? 8 : 4;
+            if (a.want_type >= 0 && a.inc_type[ii] != a.want_type) continue;   // linkPredicate (:300)
+        }
         const int64_t b = a.tgt_off[L];
         const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
         nbytes += 16 + 4 * (int64_t)n;
@@ -926,18 +991,27 @@ __device__ void bb_run(BbShared& sm, const BbArgs& a, int si) {
     bool ovf = false;
     for (int32_t d = 0; d < a.maxd && F > 0; ++d) {
         const int64_t T = sm.T, S = sm.S;
-        trav += T;
+        trav += a.y_off ? S : T;
         n_exp = d + 1;
-        nbytes += tid == 0 ? 16 * (int64_t)F + (a.yf ? T : 0) : 0;   // frontier offsets, streamed yield flags
+        // frontier offsets (+ the yield lists'), streamed yield flags
+        nbytes += tid == 0 ? (a.y_off ? 32 * (int64_t)F : 16 * (int64_t)F + (a.yf ? T : 0)) : 0;
         if (T == 0) break;
-        if (T > (a.yf ? kBbItemLimit : kBbItemLimitSym)) {
+        if (T > (a.mode != sSym ? kBbItemLimit : kBbItemLimitSym)) {
             ovf = true;
             break;
+        }
+        if (a.y_off) {   // every item can yield: no flags to stream, no staging
+            bb_process(sm, a, F, (int)T, nbytes, 0);
+            __syncthreads();
+            if (sm.ovf) {
+                ovf = true;
+                break;
+            }
         }
         // (1) stream the frontier's incidence and stage the entries that can yield; a lane keeps the
         // entries that did not fit the staging area and stages them after the next flush through (2)
         bool stop = false;
-        for (int64_t sb = 0; sb < S && !stop; sb += (int64_t)kBbThreads * kBbU) {
+        for (int64_t sb = 0; sb < (a.y_off ? 0 : S) && !stop; sb += (int64_t)kBbThreads * kBbU) {
             uint4 v[kBbU];
             int64_t lo_[kBbU], hi_[kBbU], ad_[kBbU], it_[kBbU];
 #pragma unroll
@@ -990,7 +1064,7 @@ __device__ void bb_run(BbShared& sm, const BbArgs& a, int si) {
                     const int cn = min(staged, kBbCand);
                     if (cn > 0 && (more || last || cn > kBbCand / 2)) {
                         // (2) the staged entries' links and yields
-                        bb_process(sm, a, F, cn, nbytes);
+                        bb_process(sm, a, F, cn, nbytes, -1);
                         __syncthreads();
                         if (tid == 0) sm.cand_n = 0;
                         __syncthreads();
@@ -1120,6 +1194,8 @@ struct CoArgs {
     const int64_t* tgt_off;
     const int32_t* tgt_idx;
     int32_t want_type, min_arity, mode, maxd;
+    const int64_t* y_off;                            // the yield list (BbArgs::y_off), or null
+    const int32_t* y_row;
     int32_t chunk;                                   // incidence entries per work item
     int32_t bgroups;                                 // barrier arrival groups (1 .. kCoBarGroups)
     int64_t vwords;                                  // words of one seed's bitmap
@@ -1192,23 +1268,31 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
                                         unsigned long long* trav_l) {
     const int lane = threadIdx.x & 63;
     bool nw = false;
-    int64_t deg = 0, b0 = 0;
+    int64_t deg = 0, b0 = 0, trv = 0;   // items (entries, or yield-list entries), incidence entries
     if (t >= 0) {   // the bit and the target's incidence range in flight together
         u64* w = a.vis + (int64_t)s * a.vwords + (t >> 6);
         const u64 bit = 1ull << (t & 63);
-        int64_t b1 = 0;
+        int64_t b1 = 0, i0 = 0, i1 = 0;
         if (d + 1 < a.maxd) {
-            b0 = a.inc_off[t];
-            b1 = a.inc_off[t + 1];
+            i0 = a.inc_off[t];
+            i1 = a.inc_off[t + 1];
+            if (a.y_off) {
+                b0 = a.y_off[t];
+                b1 = a.y_off[t + 1];
+            } else {
+                b0 = i0;
+                b1 = i1;
+            }
         }
         nw = !(atomicOr(w, bit) & bit);
         deg = b1 - b0;
+        trv = i1 - i0;
     }
     const u64 m = __ballot(nw);
     if (!m) return;
     if (nw) atomicAdd(&cnt_l[s], 1ull);
     const u64 nch = nw ? (u64)((deg + a.chunk - 1) / a.chunk) : 0ull;
-    if (nch) atomicAdd(&trav_l[s], (unsigned long long)deg);   // expanded at level d + 1
+    if (nw && trv) atomicAdd(&trav_l[s], (unsigned long long)trv);   // expanded at level d + 1
     u64 x = nch;   // the wave's work items and pairs: one packed reservation (items << 40 | pairs)
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1270,16 +1354,17 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
         for (int s = threadIdx.x; s < k; s += kCoThreads) {
             const int32_t t = a.seeds[s];
             atomicOr(a.vis + (int64_t)s * a.vwords + (t >> 6), 1ull << (t & 63));
-            const int64_t deg = a.inc_off[t + 1] - a.inc_off[t];
+            const int64_t trv = a.inc_off[t + 1] - a.inc_off[t];
+            const int64_t b = a.y_off ? a.y_off[t] : a.inc_off[t];
+            const int64_t deg = (a.y_off ? a.y_off[t + 1] : a.inc_off[t + 1]) - b;
+            if (a.maxd > 0 && trv > 0) atomicAdd(a.trav + s, (u64)trv);
             if (a.maxd > 0 && deg > 0) {
                 const u64 nch = (u64)((deg + a.chunk - 1) / a.chunk);
-                atomicAdd(a.trav + s, (u64)deg);
                 const u64 base = atomicAdd(a.ctl + kCoLev, nch << kCoItemShift) >> kCoItemShift;
                 if ((int64_t)(base + nch) > a.fr_seg) {
                     atomicOr(a.ctl + kCoSt + 1, 1ull);
                     continue;
                 }
-                const int64_t b = a.inc_off[t];
                 for (u64 c = 0; c < nch; ++c)
                     a.fr[base + c] = co_item(t, s, b + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk));
             }
@@ -1351,7 +1436,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                 is = e.y & 0xFF;
                 ilo = (int64_t)(uint32_t)e.z | (int64_t)e.w << 32;
                 icnt = (int64_t)(e.y >> 8);
-                nbytes += 16 + (a.yf ? icnt : 0);   // the item, the streamed flags
+                nbytes += 16 + (a.yf && !a.y_row ? icnt : 0);   // the item, the streamed flags
             }
             int64_t x = icnt;
 #pragma unroll
@@ -1372,14 +1457,15 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                 const int64_t ii = __shfl(ilo, o) + (f - __shfl(ex, o));
                 // the flag, the link and its type in flight together
                 const bool in = f < T;
-                const uint8_t yfl = in && a.yf ? a.yf[ii] : (uint8_t)0xFF;
-                const int32_t L = in ? a.inc_row[ii] : 0;
-                const int32_t lty = in && a.want_type >= 0 ? a.inc_type[ii] : a.want_type;
+                const bool yl = a.y_row != nullptr;   // a yield list: every entry yields, of the wanted type
+                const uint8_t yfl = in && !yl && a.yf ? a.yf[ii] : (uint8_t)0xFF;
+                const int32_t L = in ? (yl ? a.y_row[ii] : a.inc_row[ii]) : 0;
+                const int32_t lty = in && !yl && a.want_type >= 0 ? a.inc_type[ii] : a.want_type;
                 bool act = in && ((yfl >> a.mode) & 1);   // a target this mode can yield
                 int64_t tb = 0;
                 int32_t qlo = 0, qhi = 0;
                 if (act) {
-                    nbytes += a.want_type >= 0 ? 8 : 4;
+                    nbytes += yl || a.want_type < 0 ? 4 : 8;
                     act = lty == a.want_type;   // linkPredicate (:300)
                     if (act) {
                         tb = a.tgt_off[L];
@@ -2299,6 +2385,13 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 
 // ---- the multi-workgroup stage, host side ----
 
+// The yield list the workgroup and grid stages read (HGX_YIELD_LISTS=0, for A/B: stream the incidence
+// and its yield flags instead).
+const YieldList* stage_yield_list(hgx_graph* g, int mode, int32_t type) {
+    static const bool off = std::getenv("HGX_YIELD_LISTS") && std::atoi(std::getenv("HGX_YIELD_LISTS")) == 0;
+    return off ? nullptr : yield_list(g, mode, type);
+}
+
 // Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
 // 2 per CU and one CU slot left for other streams' kernels.
 bool co_fits(hgx_graph* g) {
@@ -2380,6 +2473,10 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.inc_row = g->inc_row;
     a.inc_type = g->inc_type;
     a.yf = mode != sSym ? g->inc_yf : nullptr;
+    if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+        a.y_off = yl->off;
+        a.y_row = yl->row;
+    }
     a.tgt_off = g->tgt_off;
     a.tgt_idx = g->tgt_idx;
     a.want_type = o.link_type;
@@ -2531,6 +2628,10 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     a.min_arity = o.return_source ? 1 : 2;
     a.mode = mode;
     a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
+    if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+        a.y_off = yl->off;
+        a.y_row = yl->row;
+    }
     const size_t per_seed = (size_t)kBbPairs * 8 + 32;
     // The grid stage goes on the stream right behind the workgroup launches and reads their overflow
     // list itself: one wait for both (HGX_CO_CHAIN=0, for A/B: a host round trip in between).
@@ -2642,6 +2743,48 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
         out.n_coop = (int32_t)out.rerun.size();
         out.rerun.clear();
     }
+}
+
+void free_yield_lists(hgx_graph* g) {
+    std::lock_guard<std::mutex> lk(g->ylist_mu);
+    for (YieldList& y : g->ylists) {
+        (void)hipFree(y.off);
+        (void)hipFree(y.row);
+    }
+    g->ylists.clear();
+}
+
+const YieldList* yield_list(hgx_graph* g, int mode, int32_t type) {
+    if (mode == sSym && type < 0) return nullptr;   // every entry: the incidence itself
+    hgx_graph* root = g->base ? g->base : g;         // built once on the snapshot, read by its contexts
+    std::lock_guard<std::mutex> lk(root->ylist_mu);
+    for (const YieldList& y : root->ylists)
+        if (y.mode == mode && y.type == type) return &y;
+    if (root->ylists.size() >= kMaxYieldLists) return nullptr;   // the streamed flags instead
+    if (mode != sSym) ensure_inc_yield(g);
+    hipStream_t st = g->stream;
+    const int64_t A = g->A;
+    YieldList y{mode, type, nullptr, nullptr, 0};
+    HGX_HIP(hipMalloc(&y.off, sizeof(int64_t) * (size_t)(A + 1)));
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A + 3) / 4, 16384));
+    const uint8_t* yf = mode != sSym ? g->inc_yf : nullptr;
+    int64_t* cnt = (int64_t*)g->alloc(sizeof(int64_t) * (size_t)(A + 1));
+    hgx_yl_count<<<grid, 256, 0, st>>>(A, g->inc_off, g->inc_type, yf, mode, type, cnt);
+    HGX_CHECK_LAUNCH();
+    size_t tb = 0;
+    HGX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, y.off, (int64_t)0, (size_t)A + 1, rocprim::plus<int64_t>(), st));
+    void* tmp = g->alloc(tb);
+    HGX_HIP(rocprim::exclusive_scan(tmp, tb, cnt, y.off, (int64_t)0, (size_t)A + 1, rocprim::plus<int64_t>(), st));
+    HGX_HIP(hipMemcpyAsync(&y.n, y.off + A, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HGX_HIP(hipStreamSynchronize(st));
+    g->release(tmp, tb);
+    g->release(cnt, sizeof(int64_t) * (size_t)(A + 1));
+    HGX_HIP(hipMalloc(&y.row, sizeof(int32_t) * (size_t)std::max<int64_t>(y.n, 1)));
+    hgx_yl_fill<<<grid, 256, 0, st>>>(A, g->inc_off, g->inc_row, g->inc_type, yf, mode, type, y.off, y.row);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipStreamSynchronize(st));
+    root->ylists.push_back(y);
+    return &root->ylists.back();
 }
 
 void block_materialize(hgx_graph* g, BlockSet& b) {
