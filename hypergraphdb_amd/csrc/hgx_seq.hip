@@ -346,6 +346,11 @@ struct SbArgs {
     int32_t* out_atom;
     int32_t* out_dist;
     int64_t* meta;                                  // [3 n]: pairs (-1 = fall back), traversed items, bytes
+    // the generator's yield list (yield_list; null: stream the incidence and its yield flags).  Its
+    // item numbering keeps the stream order (a subsequence of the entries, in entry order), so the
+    // keys rank the same.
+    const int64_t* y_off;
+    const int32_t* y_row;
 };
 
 struct SbShared {
@@ -436,9 +441,16 @@ __device__ void sb_frontier(SbShared& sm, const SbArgs& a, int F) {
         if (i < F) {
             const int32_t p = sm.e_atom[i];
             const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
-            sm.e_fb[i] = b;
-            dg[k] = e - b;
-            sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+            if (a.y_off) {   // items: the yield list; S: the incidence entries (traversed)
+                const int64_t yb = a.y_off[p], ye = a.y_off[p + 1];
+                sm.e_fb[i] = yb;
+                dg[k] = ye - yb;
+                sg[k] = e - b;
+            } else {
+                sm.e_fb[i] = b;
+                dg[k] = e - b;
+                sg[k] = e > b ? ((e + 15) >> 4) - (b >> 4) : 0;
+            }
         }
         ds += dg[k];
         ss += sg[k];
@@ -465,18 +477,24 @@ __device__ void sb_frontier(SbShared& sm, const SbArgs& a, int F) {
     __syncthreads();
 }
 
-// Staged items -> yields -> examined-set inserts.
+// Staged items (it0 < 0; items it0 + c of a yield list otherwise) -> yields -> examined-set inserts.
 // nbytes: the thread's algorithmic bytes (the type, row, target-offset, link-id and target loads).
-__device__ void sb_process(SbShared& sm, const SbArgs& a, int F, int cn, int64_t& nbytes) {
+__device__ void sb_process(SbShared& sm, const SbArgs& a, int F, int cn, int64_t& nbytes, int64_t it0) {
     for (int c = threadIdx.x; c < cn; c += kSbThreads) {
-        const int32_t it = sm.u.cand[c];
+        const int64_t it = it0 < 0 ? (int64_t)sm.u.cand[c] : it0 + c;
         const int i = sb_search(sm.e_dp, F, it);
         const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
         const int32_t p = sm.e_atom[i];
-        const int32_t L = a.inc_row[ii];
-        const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
-        nbytes += a.want_type >= 0 ? 8 : 4;
-        if (a.want_type >= 0 && ty != a.want_type) continue;                     // linkPredicate (:300)
+        int32_t L;
+        if (a.y_row) {   // the list holds the wanted type only
+            L = a.y_row[ii];
+            nbytes += 4;
+        } else {
+            L = a.inc_row[ii];
+            const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
+            nbytes += a.want_type >= 0 ? 8 : 4;
+            if (a.want_type >= 0 && ty != a.want_type) continue;                 // linkPredicate (:300)
+        }
         const int64_t b = a.tgt_off[L];
         const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
         const int32_t la = a.link_atom[L];
@@ -584,17 +602,23 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
     bool ovf = false;
     for (int32_t d = 0; d < a.maxd && F > 0; ++d) {
         const int64_t T = sm.T, S = sm.S;
-        trav += T;
-        nbytes += tid == 0 ? 16 * (int64_t)F + (a.yf ? T : 0) : 0;   // frontier offsets, streamed yield flags
+        trav += a.y_off ? S : T;
+        // frontier offsets (+ the yield lists'), streamed yield flags
+        nbytes += tid == 0 ? (a.y_off ? 32 * (int64_t)F : 16 * (int64_t)F + (a.yf ? T : 0)) : 0;
         if (T == 0) break;
         if (T > a.t_limit) {
             ovf = true;
             break;
         }
+        // every item of a yield list can yield: no flags to stream, no staging
+        for (int64_t c0 = 0; a.y_off && c0 < T && !sm.ovf; c0 += (int64_t)1 << 20) {
+            sb_process(sm, a, F, (int)min<int64_t>(T - c0, (int64_t)1 << 20), nbytes, c0);
+            __syncthreads();
+        }
         // (1) stream the frontier's incidence, stage the entries that can yield: kSbU segments per lane
         // loaded at once, staged one segment at a time (a stage flushes through (2) when full)
         bool stop = false;
-        for (int64_t sb = 0; sb < S && !stop; sb += (int64_t)kSbThreads * kSbU) {
+        for (int64_t sb = 0; sb < (a.y_off ? 0 : S) && !stop; sb += (int64_t)kSbThreads * kSbU) {
             uint4 v[kSbU];
             int64_t lo_[kSbU], hi_[kSbU], ad_[kSbU], it_[kSbU];
 #pragma unroll
@@ -643,7 +667,7 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
                 const bool last = sb + (int64_t)(u + 1) * kSbThreads >= S;
                 if (cn > 0 && (cn > kSbCand - kSbRound || last)) {
                     // (2) the staged entries' links and yields
-                    sb_process(sm, a, F, cn, nbytes);
+                    sb_process(sm, a, F, cn, nbytes, -1);
                     __syncthreads();
                     if (tid == 0) sm.cand_n = 0;
                     __syncthreads();
@@ -2910,6 +2934,10 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         a.inc_row = g->inc_row;
         a.inc_type = g->inc_type;
         a.yf = mode != sSym ? g->inc_yf : nullptr;
+        if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+            a.y_off = yl->off;
+            a.y_row = yl->row;
+        }
         a.tgt_off = g->tgt_off;
         a.tgt_idx = g->tgt_idx;
         a.link_atom = g->link_atom;

@@ -96,12 +96,18 @@ def merged(g, add, remove, num_atoms):
 def test_update_matches_rebuilt(case):
     """hgx_graph_update (atom added / removed events) == a snapshot built from the merged rows,
     including the lazily built type-grouped index and accumulators of the old rows."""
-    from hypergraphdb_amd import HyperGraphSnapshot, pattern_batch
+    from hypergraphdb_amd import HyperGraphSnapshot, _lib, pattern_batch
     rng = np.random.default_rng(80 + case)
     g = K.random_graph(rng, 250, 800, max_arity=6)
     snap = HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     pattern_batch(snap, random_queries(rng, g, 50))        # builds the type-grouped index
     check_batch(g, np.arange(32, dtype=np.int32), None, (True, True, False, False), snap=snap)
+    # the multi-workgroup stage's per-seed bitmaps (sized by the old atom count) and the yield lists
+    # of the old incidence must not survive the update
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 2)
+    check_batch(g, np.arange(16, dtype=np.int32), None, (False, True, False, False), lt=1, snap=snap)
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 1)
+    check_batch(g, np.arange(32, dtype=np.int32), None, (False, True, True, False), snap=snap)
     A0, grow = g["num_atoms"], [0, 40, 300][case]
     A1 = A0 + grow
     remove = rng.choice(g["link_atom"], 150, replace=False).tolist() + ([A0 + 5] if grow else [])  # + absent
@@ -116,6 +122,11 @@ def test_update_matches_rebuilt(case):
     for k in ("link_atom", "tgt_off", "tgt_idx", "link_type"):
         np.testing.assert_array_equal(getattr(snap, k), g2[k], err_msg=k)
     check_all(snap, g2, rng)
+    orc2 = oracle(g2)
+    late = np.arange(max(0, A1 - 16), A1, dtype=np.int32)   # the appended atoms (the old bitmaps' tail)
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 2)
+    check_batch(g2, late, None, (False, True, False, False), lt=1, snap=snap, orc=orc2)
+    check_batch(g2, late, None, (True, True, False, False), snap=snap, orc=orc2)
     snap.close()
 
 
