@@ -109,6 +109,18 @@ struct YieldList {
 };
 constexpr size_t kMaxYieldLists = 8;
 
+// A yield adjacency (yield_adj below): per atom, the generator's output itself -- every (target, link
+// atom) pair its incidence entries yield in one mode for one link type and minimum arity, in stream
+// order (entry order, then yield rank).  off == nullptr: refused (more than kYieldAdjBudget bytes).
+struct YieldAdj {
+    int32_t mode, type, min_arity, rev;
+    int64_t* off;   // [A + 1]
+    int32_t* tgt;   // [n]
+    int32_t* lnk;   // [n] link atom ids
+    int64_t n;
+};
+constexpr int64_t kYieldAdjBudget = (int64_t)4 << 30;
+
 // Vertex-cut partition of a snapshot over n_parts devices (hgx_part.hip):
 // every link row lives on one part; an atom is present (local) on every part holding one of its
 // links and owned by one of them.  Local ids are assigned in global id order, so every ascending
@@ -230,6 +242,7 @@ struct hgx_graph {
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
     std::deque<hgx::YieldList> ylists;              // yield lists (snapshot only; contexts read their base's)
+    std::deque<hgx::YieldAdj> yadjs;                // yield adjacencies (likewise)
     std::mutex ylist_mu;
     // HGX_OPT_RANKS_ORDERED: rank order == persistent-handle order.  Cleared by an hgx_graph_update
     // that extends the rank space (appended ranks need not sort after the existing handles); the
@@ -333,6 +346,10 @@ void ensure_inc_yield(hgx_graph* g);
 // (shared by its contexts, freed with it).  nullptr for the symmetric mode without a type (the
 // incidence itself) and once kMaxYieldLists lists exist.  Caller holds g->mu (hgx_seq.hip).
 const YieldList* yield_list(hgx_graph* g, int mode, int32_t type);
+// The generator's (target, link atom) output per atom for (mode, type, minimum arity, reverse order),
+// in stream order; built on first use on the snapshot.  nullptr for the symmetric mode without a type,
+// when refused (over kYieldAdjBudget) and once kMaxYieldLists exist.  Caller holds g->mu (hgx_seq.hip).
+const YieldAdj* yield_adj(hgx_graph* g, int mode, int32_t type, int32_t min_arity, bool rev);
 // The set-mode workgroup engine's part of one hgx_bfs_batch (hgx_seq.hip, HGX_OPT_BFS_BLOCK): per seed
 // V_1, V_2, ... one after the other (atoms) and |V_d| (lcnt[d - 1]) in mapped host buffers the
 // result owns; the seeds whose traversal outgrew a workgroup are listed in rerun (the batched engine

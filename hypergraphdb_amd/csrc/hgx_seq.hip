@@ -63,6 +63,107 @@ int seq_mode(const hgx_algen_opts& o) {
 int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
 // ---------------------------------------------------------------------------------------------
+// Yield adjacency (hgx::yield_adj): incidence entry i of atom p -> the targets it yields (link type,
+// yield flag, minimum arity, the mode's position rule, t != p -- DefaultALGenerator.getNextLink
+// :287-315 and F/BTargetSetIterator :121-285 as bb_process / sb_process apply them), counted per atom,
+// then written per atom in stream order (entry order; inside a link by yield rank: descending
+// positions in reverse order).  One wave per atom, a lane per entry.
+struct YaArgs {
+    int64_t A;
+    const int64_t* inc_off;
+    const int32_t* inc_row;
+    const int32_t* inc_type;
+    const uint8_t* yf;
+    const int64_t* tgt_off;
+    const int32_t* tgt_idx;
+    const int32_t* link_atom;
+    int32_t mode, rev, type, min_arity;
+    int64_t* cnt;          // count pass: [A + 1]
+    const int64_t* off;    // fill pass
+    int32_t* tgt;
+    int32_t* lnk;
+};
+
+__device__ __forceinline__ int32_t ya_entry(const YaArgs& a, int32_t p, int64_t i, int32_t& L, int64_t& b,
+                                            int32_t& lo, int32_t& hi) {
+    lo = hi = 0;
+    if (a.type >= 0 && a.inc_type[i] != a.type) return 0;   // linkPredicate (:300)
+    if (a.yf && !((a.yf[i] >> a.mode) & 1)) return 0;      // no target this mode can yield
+    L = a.inc_row[i];
+    b = a.tgt_off[L];
+    const int32_t n = (int32_t)(a.tgt_off[L + 1] - b);
+    if (n < a.min_arity) return 0;                           // minArity (:309)
+    hi = n;
+    if (a.mode != sSym) {
+        int32_t fv = -1, lv = -1;
+        for (int32_t q = 0; q < n; ++q)
+            if (a.tgt_idx[b + q] == p) {
+                if (fv < 0) fv = q;
+                lv = q;
+            }
+        if (a.mode == sAfterFirst) lo = fv + 1;
+        else if (a.mode == sBeforeFirst) hi = fv;
+        else if (a.mode == sBeforeLast) hi = lv;
+        else lo = lv + 1;
+    }
+    int32_t c = 0;
+    for (int32_t q = lo; q < hi; ++q) c += a.tgt_idx[b + q] != p;
+    return c;
+}
+
+__global__ void __launch_bounds__(256) hgx_ya_count(YaArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t v = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < a.A; v += nw) {
+        const int64_t b = a.inc_off[v], e = a.inc_off[v + 1];
+        int64_t c = 0;
+        for (int64_t i = b + lane; i < e; i += 64) {
+            int32_t L, lo, hi;
+            int64_t tb;
+            c += ya_entry(a, (int32_t)v, i, L, tb, lo, hi);
+        }
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+        if (lane == 0) a.cnt[v] = c;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[a.A] = 0;
+}
+
+__global__ void __launch_bounds__(256) hgx_ya_fill(YaArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t v = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < a.A; v += nw) {
+        const int64_t b = a.inc_off[v], e = a.inc_off[v + 1];
+        int64_t o = a.off[v];
+        for (int64_t i0 = b; i0 < e; i0 += 64) {   // wave-uniform trip count
+            const int64_t i = i0 + lane;
+            int32_t L = 0, lo = 0, hi = 0, c = 0;
+            int64_t tb = 0;
+            if (i < e) c = ya_entry(a, (int32_t)v, i, L, tb, lo, hi);
+            int32_t x = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int32_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            const int32_t tot = __shfl(x, 63);
+            int64_t w = o + x - c;
+            if (c) {
+                const int32_t la = a.link_atom[L];
+                for (int32_t j = 0; j < hi - lo; ++j) {
+                    const int32_t q = a.rev ? hi - 1 - j : lo + j;   // yield rank order
+                    const int32_t t = a.tgt_idx[tb + q];
+                    if (t == (int32_t)v) continue;
+                    a.tgt[w] = t;
+                    a.lnk[w] = la;
+                    ++w;
+                }
+            }
+            o += tot;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Yield lists (hgx::yield_list): per atom, the links of its incidence entries that pass a fixed link
 // type and can yield in a fixed generator mode (yield-flag bit `mode`; every entry in the symmetric
 // mode), in entry order.  One wave per atom: count, then (after the offsets' scan) a ballot-compacted
@@ -351,6 +452,10 @@ struct SbArgs {
     // keys rank the same.
     const int64_t* y_off;
     const int32_t* y_row;
+    // or the yield adjacency (yield_adj): y_off its offsets, an item is one (target, link atom) pair
+    // (kbits 0: the pair's index is its stream position)
+    const int32_t* a_tgt;
+    const int32_t* a_lnk;
 };
 
 struct SbShared {
@@ -485,6 +590,11 @@ __device__ void sb_process(SbShared& sm, const SbArgs& a, int F, int cn, int64_t
         const int i = sb_search(sm.e_dp, F, it);
         const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
         const int32_t p = sm.e_atom[i];
+        if (a.a_tgt) {   // the generator's output itself: target + link atom, key = the pair's index
+            nbytes += 8;
+            sb_insert(sm, a.a_tgt[ii], (((u64)(uint32_t)it + 1ull) << 32) | (u64)(uint32_t)a.a_lnk[ii]);
+            continue;
+        }
         int32_t L;
         if (a.y_row) {   // the list holds the wanted type only
             L = a.y_row[ii];
@@ -820,6 +930,7 @@ struct BbArgs {
     // frontier atom's items are then only the links that can yield, already of the wanted type
     const int64_t* y_off;
     const int32_t* y_row;
+    const int32_t* a_tgt;                            // or the yield adjacency (y_off its offsets): an item is a target
 };
 
 struct BbShared {
@@ -939,6 +1050,11 @@ __device__ void bb_process(BbShared& sm, const BbArgs& a, int F, int cn, int64_t
         const int i = sb_search(sm.e_dp, F, it);
         const int64_t ii = sm.e_fb[i] + (it - sm.e_dp[i]);
         const int32_t p = sm.e_atom[i];
+        if (a.a_tgt) {   // the generator's output itself
+            nbytes += 4;
+            bb_insert(sm, a.a_tgt[ii]);
+            continue;
+        }
         int32_t L;
         if (a.y_row) {   // the list holds the wanted type only
             L = a.y_row[ii];
@@ -1220,6 +1336,7 @@ struct CoArgs {
     int32_t want_type, min_arity, mode, maxd;
     const int64_t* y_off;                            // the yield list (BbArgs::y_off), or null
     const int32_t* y_row;
+    const int32_t* a_tgt;                            // or the yield adjacency's targets (y_off its offsets)
     int32_t chunk;                                   // incidence entries per work item
     int32_t bgroups;                                 // barrier arrival groups (1 .. kCoBarGroups)
     int64_t vwords;                                  // words of one seed's bitmap
@@ -1479,6 +1596,12 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                 }
                 const int32_t p = __shfl(ip, o), s = __shfl(is, o);
                 const int64_t ii = __shfl(ilo, o) + (f - __shfl(ex, o));
+                if (a.a_tgt) {   // the generator's output itself: one target per lane (wave-uniform branch)
+                    const int32_t t = f < T ? a.a_tgt[ii] : -1;
+                    nbytes += f < T ? 4 : 0;
+                    co_step(a, s, t, d, slot_next, seg, pbase, nbytes, cnt_l, trav_l);
+                    continue;
+                }
                 // the flag, the link and its type in flight together
                 const bool in = f < T;
                 const bool yl = a.y_row != nullptr;   // a yield list: every entry yields, of the wanted type
@@ -2416,6 +2539,24 @@ const YieldList* stage_yield_list(hgx_graph* g, int mode, int32_t type) {
     return off ? nullptr : yield_list(g, mode, type);
 }
 
+// The yield adjacency the stages read first (HGX_YIELD_ADJ=0, for A/B: the yield list instead).
+const YieldAdj* stage_yield_adj(hgx_graph* g, int mode, const hgx_algen_opts& o) {
+    static const bool off = std::getenv("HGX_YIELD_ADJ") && std::atoi(std::getenv("HGX_YIELD_ADJ")) == 0;
+    return off ? nullptr : yield_adj(g, mode, o.link_type, o.return_source ? 1 : 2, o.reverse_order != 0);
+}
+
+// Items of the set-mode stages: the yield adjacency, else the yield list, else the incidence.
+template <class Args>
+void stage_items(hgx_graph* g, int mode, const hgx_algen_opts& o, Args& a) {
+    if (const YieldAdj* ya = stage_yield_adj(g, mode, o)) {
+        a.y_off = ya->off;
+        a.a_tgt = ya->tgt;
+    } else if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+        a.y_off = yl->off;
+        a.y_row = yl->row;
+    }
+}
+
 // Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
 // 2 per CU and one CU slot left for other streams' kernels.
 bool co_fits(hgx_graph* g) {
@@ -2497,10 +2638,7 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.inc_row = g->inc_row;
     a.inc_type = g->inc_type;
     a.yf = mode != sSym ? g->inc_yf : nullptr;
-    if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
-        a.y_off = yl->off;
-        a.y_row = yl->row;
-    }
+    stage_items(g, mode, o, a);
     a.tgt_off = g->tgt_off;
     a.tgt_idx = g->tgt_idx;
     a.want_type = o.link_type;
@@ -2652,10 +2790,7 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     a.min_arity = o.return_source ? 1 : 2;
     a.mode = mode;
     a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
-    if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
-        a.y_off = yl->off;
-        a.y_row = yl->row;
-    }
+    stage_items(g, mode, o, a);
     const size_t per_seed = (size_t)kBbPairs * 8 + 32;
     // The grid stage goes on the stream right behind the workgroup launches and reads their overflow
     // list itself: one wait for both (HGX_CO_CHAIN=0, for A/B: a host round trip in between).
@@ -2776,6 +2911,69 @@ void free_yield_lists(hgx_graph* g) {
         (void)hipFree(y.row);
     }
     g->ylists.clear();
+    for (YieldAdj& y : g->yadjs) {
+        if (y.off) (void)hipFree(y.off);
+        if (y.tgt) (void)hipFree(y.tgt);
+        if (y.lnk) (void)hipFree(y.lnk);
+    }
+    g->yadjs.clear();
+}
+
+const YieldAdj* yield_adj(hgx_graph* g, int mode, int32_t type, int32_t min_arity, bool rev) {
+    if (mode == sSym && type < 0) return nullptr;   // every co-target of every entry: too large to keep
+    hgx_graph* root = g->base ? g->base : g;         // built once on the snapshot, read by its contexts
+    std::lock_guard<std::mutex> lk(root->ylist_mu);
+    for (const YieldAdj& y : root->yadjs)
+        if (y.mode == mode && y.type == type && y.min_arity == min_arity && y.rev == (int32_t)rev)
+            return y.off ? &y : nullptr;
+    if (root->yadjs.size() >= kMaxYieldLists) return nullptr;
+    if (mode != sSym) ensure_inc_yield(g);
+    hipStream_t st = g->stream;
+    const int64_t A = g->A;
+    YaArgs a{};
+    a.A = A;
+    a.inc_off = g->inc_off;
+    a.inc_row = g->inc_row;
+    a.inc_type = g->inc_type;
+    a.yf = mode != sSym ? g->inc_yf : nullptr;
+    a.tgt_off = g->tgt_off;
+    a.tgt_idx = g->tgt_idx;
+    a.link_atom = g->link_atom;
+    a.mode = mode;
+    a.rev = rev ? 1 : 0;
+    a.type = type;
+    a.min_arity = min_arity;
+    YieldAdj y{mode, type, min_arity, (int32_t)rev, nullptr, nullptr, nullptr, 0};
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A + 3) / 4, 16384));
+    int64_t* off = nullptr;
+    HGX_HIP(hipMalloc(&off, sizeof(int64_t) * (size_t)(A + 1)));
+    a.cnt = (int64_t*)g->alloc(sizeof(int64_t) * (size_t)(A + 1));
+    hgx_ya_count<<<grid, 256, 0, st>>>(a);
+    HGX_CHECK_LAUNCH();
+    size_t tb = 0;
+    HGX_HIP(rocprim::exclusive_scan(nullptr, tb, a.cnt, off, (int64_t)0, (size_t)A + 1, rocprim::plus<int64_t>(), st));
+    void* tmp = g->alloc(tb);
+    HGX_HIP(rocprim::exclusive_scan(tmp, tb, a.cnt, off, (int64_t)0, (size_t)A + 1, rocprim::plus<int64_t>(), st));
+    HGX_HIP(hipMemcpyAsync(&y.n, off + A, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HGX_HIP(hipStreamSynchronize(st));
+    g->release(tmp, tb);
+    g->release(a.cnt, sizeof(int64_t) * (size_t)(A + 1));
+    if (y.n * 8 > kYieldAdjBudget) {   // remembered as refused: the yield list serves instead
+        HGX_HIP(hipFree(off));
+        root->yadjs.push_back(y);
+        return nullptr;
+    }
+    y.off = off;
+    HGX_HIP(hipMalloc(&y.tgt, sizeof(int32_t) * (size_t)std::max<int64_t>(y.n, 1)));
+    HGX_HIP(hipMalloc(&y.lnk, sizeof(int32_t) * (size_t)std::max<int64_t>(y.n, 1)));
+    a.off = y.off;
+    a.tgt = y.tgt;
+    a.lnk = y.lnk;
+    hgx_ya_fill<<<grid, 256, 0, st>>>(a);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipStreamSynchronize(st));
+    root->yadjs.push_back(y);
+    return &root->yadjs.back();
 }
 
 const YieldList* yield_list(hgx_graph* g, int mode, int32_t type) {
@@ -2934,7 +3132,12 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         a.inc_row = g->inc_row;
         a.inc_type = g->inc_type;
         a.yf = mode != sSym ? g->inc_yf : nullptr;
-        if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+        const YieldAdj* ya = stage_yield_adj(g, mode, o);
+        if (ya) {
+            a.y_off = ya->off;
+            a.a_tgt = ya->tgt;
+            a.a_lnk = ya->lnk;
+        } else if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
             a.y_off = yl->off;
             a.y_row = yl->row;
         }
@@ -2945,9 +3148,9 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         a.min_arity = o.return_source ? 1 : 2;
         a.mode = mode;
         a.rev = o.reverse_order ? 1 : 0;
-        a.kbits = kbits;
+        a.kbits = ya ? 0 : kbits;   // an adjacency pair's index is its whole stream position
         a.maxd = maxd;
-        a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
+        a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> a.kbits));
         const size_t per_seed = (size_t)kSbPairs * 12 + 24;
         int32_t* dseeds = nullptr;
         size_t dseeds_n = 0;
