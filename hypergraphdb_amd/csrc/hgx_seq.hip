@@ -1339,6 +1339,7 @@ struct CoArgs {
     const int32_t* a_tgt;                            // or the yield adjacency's targets (y_off its offsets)
     int32_t chunk;                                   // incidence entries per work item
     int32_t bgroups;                                 // barrier arrival groups (1 .. kCoBarGroups)
+    int32_t lite;                                    // per-level barriers: co_barrier_lite
     int64_t vwords;                                  // words of one seed's bitmap
     u64* vis;                                        // [k * vwords]
     int4* fr;                                        // [3 * kCoSegs * fr_seg] work items (atom, seed, chunk, -)
@@ -1354,6 +1355,58 @@ struct CoArgs {
     int64_t* lvl_end;                                // mapped [kcap * kCoMaxLevels]: cur[s] after level d
     int64_t* lvl_trace;                              // mapped [2 * kCoMaxLevels]: start clock, work items
 };
+
+// Work items and pairs cross workgroups inside the launch: they are written and read with agent-scope
+// atomic stores / loads, which stay coherent across the XCDs' L2s by themselves.  So the per-level
+// barrier can be the light one (co_barrier_lite): no agent-scope release / acquire, whose L2
+// write-back and invalidate (buffer_wbl2 / buffer_inv) cost every level and leave the graph's
+// read-only arrays cold in L2 for the next one.
+__device__ __forceinline__ void co_put(int4* p, int4 v) {
+    u64* q = (u64*)p;
+    __hip_atomic_store(q, (u64)(uint32_t)v.x | (u64)(uint32_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (u64)(uint32_t)v.z | (u64)(uint32_t)v.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int4 co_get(const int4* p) {
+    u64* q = (u64*)p;
+    const u64 lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_int4((int32_t)lo, (int32_t)(lo >> 32), (int32_t)hi, (int32_t)(hi >> 32));
+}
+__device__ __forceinline__ void co_put(int2* p, int2 v) {
+    __hip_atomic_store((u64*)p, (u64)(uint32_t)v.x | (u64)(uint32_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int2 co_get(const int2* p) {
+    const u64 x = __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_int2((int32_t)x, (int32_t)(x >> 32));
+}
+
+// Light grid barrier: every thread waits for its own memory operations to complete (the agent-scope
+// stores and atomics above are then at the coherence point), the block arrives with a relaxed
+// agent-scope add, waiters poll relaxed.  Valid because everything another workgroup reads in the
+// loop is an agent-scope atomic operation (co_put / co_get, the bitmaps, counters and status words).
+__device__ __forceinline__ bool co_barrier_lite(u64* ctl, u64& gen, u64* status) {
+    __shared__ int s_to;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ++gen;
+        __hip_atomic_fetch_add(ctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 target = gen * gridDim.x;
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();
+        int to = 0;
+        while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
+                atomicOr(status, 4ull);
+                to = 1;
+                break;
+            }
+        }
+        s_to = to;
+    }
+    __syncthreads();
+    return s_to != 0;
+}
 
 // Grid barrier: arrival at the block's group counter (acq_rel: the last arrival of a group carries
 // the group's writes on), the group's last arrival adds to the top counter, everyone polls the top
@@ -1446,7 +1499,7 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
     if (!nw) return;
     u64* status = a.ctl + kCoSt + (d & 1);
     const u64 pos = pbase_seg + (wb & kCoPairMask) + (u64)__popcll(m & ((1ull << lane) - 1ull));
-    if ((int64_t)pos < a.pseg) a.pairs[(int64_t)seg * a.pseg + (int64_t)pos] = make_int2(t, s | (d + 1) << 8);
+    if ((int64_t)pos < a.pseg) co_put(a.pairs + (int64_t)seg * a.pseg + (int64_t)pos, make_int2(t, s | (d + 1) << 8));
     else atomicOr(status, 2ull);
     nbytes += 8;
     if (nch == 0) return;
@@ -1456,7 +1509,8 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
         return;
     }
     int4* fr = a.fr + ((int64_t)slot_next * kCoSegs + seg) * a.fr_seg;
-    for (u64 c = 0; c < nch; ++c) fr[base + c] = co_item(t, s, b0 + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk));
+    for (u64 c = 0; c < nch; ++c)
+        co_put(fr + base + c, co_item(t, s, b0 + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk)));
     nbytes += 16 * (int64_t)nch;
 }
 
@@ -1507,10 +1561,11 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                     continue;
                 }
                 for (u64 c = 0; c < nch; ++c)
-                    a.fr[base + c] = co_item(t, s, b + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk));
+                    co_put(a.fr + base + c, co_item(t, s, b + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk)));
             }
         }
-    bool timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);
+    const int ng = a.lite ? 1 : a.bgroups;   // the light barrier adds to the top counter directly
+    bool timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt) : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);
     int32_t d = 0;
     u64 pbase = 0;   // pairs of this block's segment found before the current level
     for (; !timed_out; ++d) {
@@ -1572,7 +1627,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
                     if (seg_pre[mid] <= it) lo = mid;
                     else hi = mid - 1;
                 }
-                const int4 e = fr[(int64_t)lo * a.fr_seg + (it - seg_pre[lo])];
+                const int4 e = co_get(fr + (int64_t)lo * a.fr_seg + (it - seg_pre[lo]));
                 ip = e.x;
                 is = e.y & 0xFF;
                 ilo = (int64_t)(uint32_t)e.z | (int64_t)e.w << 32;
@@ -1651,7 +1706,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
             cnt_l[j] = 0;
             trav_l[j] = 0;
         }
-        timed_out = co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);
+        timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt) : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);
     }
     if (timed_out) return;   // the host clears the bitmaps
     for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
@@ -1664,7 +1719,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
     if (st == 0) {
         const int64_t nblk_seg = ((int64_t)gridDim.x - seg + kCoSegs - 1) / kCoSegs;
         for (int64_t i = (int64_t)(blockIdx.x / kCoSegs) * kCoThreads + threadIdx.x; i < np; i += nblk_seg * kCoThreads) {
-            const int2 pr = a.pairs[(int64_t)seg * a.pseg + i];
+            const int2 pr = co_get(a.pairs + (int64_t)seg * a.pseg + i);
             a.vis[(int64_t)(pr.y & 0xFF) * a.vwords + (pr.x >> 6)] = 0ull;
         }
         if (blockIdx.x == 0)
@@ -1675,7 +1730,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
         a.hmeta[0] = (int64_t)st;
         a.hmeta[1] = d;
     }
-    co_barrier(a.ctl, gen, a.ctl + kCoSt, a.bgroups);   // every block's byte count is in
+    co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);   // every block's byte count is in
     if (blockIdx.x == 0 && threadIdx.x == 0)   // + the pairs written and the bitmap words cleared
         a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + kCoBytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0)
@@ -2649,6 +2704,8 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.chunk = chunk_env > 0 ? std::min(chunk_env, 1 << 20) : kCoChunk;   // entries < 2^23 (co_item)
     static const int bg_env = std::getenv("HGX_CO_BARGROUPS") ? std::atoi(std::getenv("HGX_CO_BARGROUPS")) : 0;   // A/B
     a.bgroups = bg_env > 0 ? std::min(bg_env, kCoBarGroups) : 1;
+    static const bool lite_off = std::getenv("HGX_CO_LITE") && std::atoi(std::getenv("HGX_CO_LITE")) == 0;   // A/B
+    a.lite = lite_off ? 0 : 1;
     a.vwords = vwords;
     a.vis = g->co_vis;
     a.fr = fr;
