@@ -1316,10 +1316,10 @@ constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
 constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s
 // ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
-// even / odd levels (the seeding: odd), [kCoBytes] algorithmic bytes, [kCoSel] seeds the workgroup
+// even / odd levels (the seeding: odd), [kCoSel] seeds the workgroup
 // stage handed over, [kCoLev + slot * kCoSegs + seg] level counters (3 rotating slots), then cur [kcap],
 // trav [kcap], and as int32: the seeds' batch indices [kcap] and atoms [kcap]
-constexpr int kCoSt = 20, kCoBytes = 22, kCoSel = 23, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
+constexpr int kCoSt = 20, kCoSel = 23, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
 
 struct CoArgs {
     int32_t k;                                       // seeds (<= kcap); -1: the workgroup stage's overflow
@@ -1354,6 +1354,7 @@ struct CoArgs {
                                                      //   [kCoSegs], the seeds' batch indices [kcap]
     int64_t* lvl_end;                                // mapped [kcap * kCoMaxLevels]: cur[s] after level d
     int64_t* lvl_trace;                              // mapped [2 * kCoMaxLevels]: start clock, work items
+    int64_t* blk_bytes;                              // mapped [gridDim.x]: each block's algorithmic bytes
 };
 
 // Work items and pairs cross workgroups inside the launch: they are written and read with agent-scope
@@ -1544,7 +1545,7 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
         if (k == 0 || k > a.kcap) return;
     }
     u64 gen = 0;
-    int64_t nbytes = 0;   // algorithmic bytes of this thread (reduced into ctl[kCoBytes] at the end)
+    int64_t nbytes = 0;   // algorithmic bytes of this thread (the block's sum goes to blk_bytes at the end)
     if (blockIdx.x == 0)   // level 0 (segment 0): the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46)
         for (int s = threadIdx.x; s < k; s += kCoThreads) {
             const int32_t t = a.seeds[s];
@@ -1709,10 +1710,21 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
         timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt) : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);
     }
     if (timed_out) return;   // the host clears the bitmaps
-    for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
-    if (lane == 0 && nbytes) atomicAdd(a.ctl + kCoBytes, (u64)nbytes);
-    // every block left the loop after the same barrier: clear the bitmap words of the atoms found, the
-    // blocks of a segment splitting its pairs (the host clears the whole bitmaps when a list overflowed)
+    // every block left the loop after the same barrier, which every count, status word and pair had
+    // reached: no further barrier.  The block's algorithmic bytes go to its own mapped word.
+    {
+        __shared__ int64_t bsum[kCoWaves];
+        for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_xor(nbytes, off);
+        if (lane == 0) bsum[threadIdx.x >> 6] = nbytes;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t t = 0;
+            for (int w = 0; w < kCoWaves; ++w) t += bsum[w];
+            a.blk_bytes[blockIdx.x] = t;
+        }
+    }
+    // clear the bitmap words of the atoms found, the blocks of a segment splitting its pairs (the host
+    // clears the whole bitmaps when a list overflowed)
     const u64 st = __hip_atomic_load(a.ctl + kCoSt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
                    __hip_atomic_load(a.ctl + kCoSt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t np = min((int64_t)pbase, a.pseg);
@@ -1730,9 +1742,6 @@ __global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
         a.hmeta[0] = (int64_t)st;
         a.hmeta[1] = d;
     }
-    co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);   // every block's byte count is in
-    if (blockIdx.x == 0 && threadIdx.x == 0)   // + the pairs written and the bitmap words cleared
-        a.hmeta[3] = (int64_t)__hip_atomic_load(a.ctl + kCoBytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0)
         for (int s = threadIdx.x; s < k; s += kCoThreads) {
             a.hmeta[4 + 2 * s] = (int64_t)__hip_atomic_load(a.cur + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2638,6 +2647,7 @@ struct CoRun {
     PoolBuf hb{nullptr, 0};
     int64_t* hm = nullptr;                  // the mapped readout (CoArgs::hmeta)
     size_t m_seg = 0, m_sel = 0, m_lev = 0;  // its pairs-per-segment, batch-index and level-count parts
+    size_t m_blk = 0;                        //   and the blocks' algorithmic bytes
     explicit CoRun(hgx_graph* gg) : g(gg), sc{gg, {}} {}
     CoRun(const CoRun&) = delete;
     CoRun& operator=(const CoRun&) = delete;
@@ -2678,7 +2688,8 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     r.m_seg = 4 + 2 * (size_t)kcap;
     r.m_sel = r.m_seg + kCoSegs;
     r.m_lev = r.m_sel + (size_t)kcap;
-    r.hb = take_host_buf(g, sizeof(int64_t) * (r.m_lev + (size_t)(kcap + 2) * kCoMaxLevels));
+    r.m_blk = r.m_lev + (size_t)(kcap + 2) * kCoMaxLevels;
+    r.hb = take_host_buf(g, sizeof(int64_t) * (r.m_blk + kCoMaxBlocks));
     r.hm = (int64_t*)r.hb.p;
     r.hm[0] = -1;
     r.hm[2] = k;
@@ -2718,6 +2729,7 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.hmeta = (int64_t*)hmd;
     a.lvl_end = (int64_t*)hmd + r.m_lev;
     a.lvl_trace = a.lvl_end + (size_t)kcap * kCoMaxLevels;
+    a.blk_bytes = (int64_t*)hmd + r.m_blk;
 }
 
 void co_launch(hgx_graph* g, CoRun& r) {
@@ -2766,7 +2778,9 @@ void co_collect(hgx_graph* g, CoRun& r, const std::vector<int32_t>& sidx, BlockS
         out.traversed += (double)hm[5 + 2 * j];
     }
     out.expanded = std::max(out.expanded, nlev);
-    out.co_bytes_alg = (double)hm[3] + 16.0 * (double)out.co_n;   // + the pairs and the bitmap words cleared
+    double bytes = 0;
+    for (int b = 0; b < g->co_ok; ++b) bytes += (double)hm[r.m_blk + b];
+    out.co_bytes_alg = bytes + 16.0 * (double)out.co_n;   // + the pairs and the bitmap words cleared
 }
 
 // A launch that did not finish: the bitmaps may hold bits of atoms no pair records, so they are
