@@ -489,7 +489,12 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * a level wider than 1024 atoms, or a frontier of more than 4M incidence entries) then run on the
  * batched rows engine -- up to 64 of them first on the multi-workgroup stage (one persistent launch,
  * a grid barrier per level, per-seed visited bitmaps).  0 = every seed on the rows engine; 2 (tests) =
- * a batch of <= 64 seeds straight to the multi-workgroup stage.  Results are identical either way. */
+ * a batch of <= 64 seeds straight to the multi-workgroup stage.  Results are identical either way.
+ * Memory: in an ordered generator mode, or with a link type, both stages and hgx_bfs_sequence's
+ * workgroup engine build on first use (kept on the snapshot, shared by its contexts, dropped by
+ * hgx_graph_update) the generator's output per atom for that (mode, type, minimum arity, order):
+ * (A + 1) * 8 bytes of offsets + 8 bytes per yielded (target, link) pair, skipped above 4 GB; and a
+ * list of the entries that can yield, (A + 1) * 8 + 4 per entry.  At most 8 of each per snapshot. */
 #define HGX_OPT_BFS_BLOCK 14
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */
