@@ -1815,6 +1815,11 @@ struct LsArgs {
     int32_t* out_atom;
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
     u64* hflag;                         // mapped coherent host words: {n, status, seq} x 2 (level parity)
+    // the yield adjacency (yield_adj; null: the incidence): an item is one (target, link atom) pair,
+    // its index the whole stream position (kbits 0)
+    const int64_t* y_off;
+    const int32_t* a_tgt;
+    const int32_t* a_lnk;
 };
 
 __device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
@@ -1910,7 +1915,7 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
     const int64_t lo = ls_lo(F, blockIdx.x), hi = ls_lo(F, blockIdx.x + 1);
-    int64_t sum = 0;
+    int64_t sum = 0, trv = 0;
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
         const int32_t s = fs[i];
         if (d > 0 && (i == 0 || fs[i - 1] != s)) {   // where seed s's pairs of distance d start
@@ -1926,13 +1931,25 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
         if (runs_only) continue;
         const int32_t p = fa[i];
         const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
-        a.fbase[i] = b;
-        a.deg[i] = e - b;
-        sum += e - b;
+        if (a.y_off) {   // items: the adjacency's pairs; the incidence entries count as traversed
+            const int64_t yb = a.y_off[p], ye = a.y_off[p + 1];
+            a.fbase[i] = yb;
+            a.deg[i] = ye - yb;
+            sum += ye - yb;
+            trv += e - b;
+        } else {
+            a.fbase[i] = b;
+            a.deg[i] = e - b;
+            sum += e - b;
+        }
     }
     if (runs_only) return;
     sum = ls_block_sum(sum, ws);
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = sum;
+    if (a.y_off) {
+        trv = ls_block_sum(trv, ws);
+        if (threadIdx.x == 0 && trv) atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)trv);
+    }
     if (blockIdx.x == 0 && threadIdx.x < kLsSlotWords && threadIdx.x != lsF && threadIdx.x != lsOut)
         a.ctl[((d + 1) % kLsSlots) * kLsSlotWords + threadIdx.x] = 0;   // the next level's slot counters
     if (blockIdx.x == 0 && threadIdx.x <= kLsDSegs) ls_dseg(a, d + 1)[threadIdx.x] = 0;
@@ -1965,7 +1982,7 @@ __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
         const int64_t W = (int64_t)((((u64)T << a.kbits) + 63ull) >> 6);
         sl[lsW] = W;
         sl[lsTiles] = (T + kLsTile - 1) / kLsTile;
-        atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
+        if (!a.y_off) atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
         int64_t st = 0;
         if (T > a.t_limit) st |= 16;   // keys wider than 32 bits: the key-array engine takes the chunk
         if (W > a.wcap) st |= 4;
@@ -2007,9 +2024,15 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             j = it - a.pre[i];
             p = fa[i];
             ii = a.fbase[i] + j;
-            if (a.yf && !((a.yf[ii] >> a.mode) & 1u)) live = false;                 // nothing to yield
+            if (!a.a_tgt && a.yf && !((a.yf[ii] >> a.mode) & 1u)) live = false;     // nothing to yield
         }
-        if (live) {
+        int32_t t_adj = 0;
+        if (live && a.a_tgt) {   // the generator's output itself: one yield, rank 0
+            t_adj = a.a_tgt[ii];
+            la = a.a_lnk[ii];
+            n = 1;
+            hi = 1;
+        } else if (live) {
             const int32_t L = a.inc_row[ii];
             const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
             if (a.want_type >= 0 && ty != a.want_type) live = false;             // linkPredicate (:300)
@@ -2018,7 +2041,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             la = a.link_atom[L];
             if (n < a.min_arity) live = false;                                    // minArity (:309)
         }
-        if (live) {
+        if (live && !a.a_tgt) {
             hi = n;
             if (a.mode != sSym) {
                 int32_t fv = -1, lv = -1;
@@ -2043,9 +2066,10 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             int32_t t = 0;
             if (r < cnt) {
                 const int32_t q = lo + r;
-                t = a.tgt_idx[b + q];
+                t = a.a_tgt ? t_adj : a.tgt_idx[b + q];
                 if (t != p) {
-                    const u64 v = ((kb + (u64)(a.rev ? n - 1 - q : q)) << 32) | (u64)(uint32_t)la;
+                    const u64 rk = a.a_tgt ? 0ull : (u64)(a.rev ? n - 1 - q : q);
+                    const u64 v = ((kb + rk) << 32) | (u64)(uint32_t)la;
                     u64* slot = a.key + sA + t;
                     if (*slot > v) isnew = atomicMin(slot, v) == kNoKey;
                 }
@@ -2231,6 +2255,31 @@ void ev_give(hgx_graph* g, hipEvent_t e) {
     if (e) g->ev_pool.push_back(e);
 }
 
+// The yield list the workgroup and grid stages read (HGX_YIELD_LISTS=0, for A/B: stream the incidence
+// and its yield flags instead).
+const YieldList* stage_yield_list(hgx_graph* g, int mode, int32_t type) {
+    static const bool off = std::getenv("HGX_YIELD_LISTS") && std::atoi(std::getenv("HGX_YIELD_LISTS")) == 0;
+    return off ? nullptr : yield_list(g, mode, type);
+}
+
+// The yield adjacency the stages read first (HGX_YIELD_ADJ=0, for A/B: the yield list instead).
+const YieldAdj* stage_yield_adj(hgx_graph* g, int mode, const hgx_algen_opts& o) {
+    static const bool off = std::getenv("HGX_YIELD_ADJ") && std::atoi(std::getenv("HGX_YIELD_ADJ")) == 0;
+    return off ? nullptr : yield_adj(g, mode, o.link_type, o.return_source ? 1 : 2, o.reverse_order != 0);
+}
+
+// Items of the set-mode stages: the yield adjacency, else the yield list, else the incidence.
+template <class Args>
+void stage_items(hgx_graph* g, int mode, const hgx_algen_opts& o, Args& a) {
+    if (const YieldAdj* ya = stage_yield_adj(g, mode, o)) {
+        a.y_off = ya->off;
+        a.a_tgt = ya->tgt;
+    } else if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
+        a.y_off = yl->off;
+        a.y_row = yl->row;
+    }
+}
+
 // Key widths of the level-synchronous engine and the block engine's yield rank (once per snapshot).
 void seq_maxes(hgx_graph* g) {
     if (g->max_deg >= 0) return;
@@ -2403,7 +2452,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     hipStream_t st = g->stream;
     const int64_t A = g->A;
     const int mode = seq_mode(o);
-    const int kbits = bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
+    const YieldAdj* ya = stage_yield_adj(g, mode, o);   // an adjacency pair's index is its whole stream position
+    const int kbits = ya ? 0 : bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
     if (!g->seq_flag) {   // mapped, coherent: the emit kernel's level sizes (once per graph)
         void* hp = nullptr;
         HGX_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2424,6 +2474,11 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         LsArgs a{};
         a.A = A;
         a.inc_off = g->inc_off;
+        if (ya) {
+            a.y_off = ya->off;
+            a.a_tgt = ya->tgt;
+            a.a_lnk = ya->lnk;
+        }
         a.inc_row = g->inc_row;
         a.inc_type = g->inc_type;
         a.yf = mode != sSym ? g->inc_yf : nullptr;
@@ -2596,30 +2651,6 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 
 // ---- the multi-workgroup stage, host side ----
 
-// The yield list the workgroup and grid stages read (HGX_YIELD_LISTS=0, for A/B: stream the incidence
-// and its yield flags instead).
-const YieldList* stage_yield_list(hgx_graph* g, int mode, int32_t type) {
-    static const bool off = std::getenv("HGX_YIELD_LISTS") && std::atoi(std::getenv("HGX_YIELD_LISTS")) == 0;
-    return off ? nullptr : yield_list(g, mode, type);
-}
-
-// The yield adjacency the stages read first (HGX_YIELD_ADJ=0, for A/B: the yield list instead).
-const YieldAdj* stage_yield_adj(hgx_graph* g, int mode, const hgx_algen_opts& o) {
-    static const bool off = std::getenv("HGX_YIELD_ADJ") && std::atoi(std::getenv("HGX_YIELD_ADJ")) == 0;
-    return off ? nullptr : yield_adj(g, mode, o.link_type, o.return_source ? 1 : 2, o.reverse_order != 0);
-}
-
-// Items of the set-mode stages: the yield adjacency, else the yield list, else the incidence.
-template <class Args>
-void stage_items(hgx_graph* g, int mode, const hgx_algen_opts& o, Args& a) {
-    if (const YieldAdj* ya = stage_yield_adj(g, mode, o)) {
-        a.y_off = ya->off;
-        a.a_tgt = ya->tgt;
-    } else if (const YieldList* yl = stage_yield_list(g, mode, o.link_type)) {
-        a.y_off = yl->off;
-        a.y_row = yl->row;
-    }
-}
 
 // Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
 // 2 per CU and one CU slot left for other streams' kernels.
