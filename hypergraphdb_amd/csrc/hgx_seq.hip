@@ -35,6 +35,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -61,6 +62,28 @@ int seq_mode(const hgx_algen_opts& o) {
 }
 
 int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+// fn(0 .. n-1) on up to 16 host threads (the job's CPU share; HGX_COPY_THREADS overrides), or on the
+// calling thread when `wide` is false.
+template <class F>
+void host_parallel(int64_t n, bool wide, F&& fn) {
+    static const int env = std::getenv("HGX_COPY_THREADS") ? std::atoi(std::getenv("HGX_COPY_THREADS")) : 0;
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = !wide ? 1 : (int)std::min<int64_t>(n, env > 0 ? env : std::min(hw, 16));
+    if (nt <= 1) {
+        for (int64_t k = 0; k < n; ++k) fn(k);
+        return;
+    }
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (int64_t k; (k = next.fetch_add(1)) < n;) fn(k);
+    };
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+}
 
 // ---------------------------------------------------------------------------------------------
 // Yield adjacency (hgx::yield_adj): incidence entry i of atom p -> the targets it yields (link type,
@@ -3378,26 +3401,41 @@ int hgx_seq_result_offsets(const hgx_seq_result* r, int64_t* offsets) {
 int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms, int32_t* dists) {
     HGX_API_BEGIN
     if (!r) fail(HGX_E_INVALID, "null result");
-    auto put = [&](int64_t b, const Seg& s) {
-        if (s.n <= 0) return;
-        if (links) std::memcpy(links + b, s.link, sizeof(int32_t) * s.n);
-        if (atoms) std::memcpy(atoms + b, s.atom, sizeof(int32_t) * s.n);
-        if (dists) {
-            if (s.dist) std::memcpy(dists + b, s.dist, sizeof(int32_t) * s.n);
-            else std::fill(dists + b, dists + b + s.n, s.dist_c);
-        }
+    // the copy jobs: one per segment, split into pieces of <= 4M pairs; large results are copied by
+    // several host threads (config 2's drop-in call returns 258M pairs: 3 GB of caller arrays whose
+    // pages are first touched here)
+    struct Job {
+        int64_t b;
+        const Seg* s;
+        int64_t lo, n;
+    };
+    std::vector<Job> jobs;
+    constexpr int64_t kPiece = (int64_t)1 << 22;
+    auto add = [&](int64_t b, const Seg& s) {
+        for (int64_t lo = 0; lo < s.n; lo += kPiece) jobs.push_back({b, &s, lo, std::min(kPiece, s.n - lo)});
     };
     for (int32_t i = 0; i < r->n_seeds; ++i) {
         int64_t b = r->off[i];
         if (r->lev_of[i] < 0) {
-            put(b, r->blk[i]);
+            add(b, r->blk[i]);
             continue;
         }
         for (const Seg& s : r->lev.segs[(size_t)r->lev_of[i]]) {
-            put(b, s);
+            add(b, s);
             b += s.n;
         }
     }
+    auto run = [&](const Job& j) {
+        const Seg& s = *j.s;
+        const int64_t o = j.b + j.lo;
+        if (links) std::memcpy(links + o, s.link + j.lo, sizeof(int32_t) * j.n);
+        if (atoms) std::memcpy(atoms + o, s.atom + j.lo, sizeof(int32_t) * j.n);
+        if (dists) {
+            if (s.dist) std::memcpy(dists + o, s.dist + j.lo, sizeof(int32_t) * j.n);
+            else std::fill(dists + o, dists + o + j.n, s.dist_c);
+        }
+    };
+    host_parallel((int64_t)jobs.size(), r->off.back() >= ((int64_t)1 << 24), [&](int64_t k) { run(jobs[(size_t)k]); });
     HGX_API_END
 }
 
