@@ -198,3 +198,44 @@ def test_config4_full_eight_parts_vs_replica():
     finally:
         for x in parts:
             x.close()
+
+
+def test_config2_dropin_sequence_large_readout(config2):
+    """The order-exact drop-in on config 2 (16 sources to depth 2, ~64M pairs): the multi-threaded
+    copy into the caller's arrays equals the single-threaded ranged readout window by window, and two
+    sources' whole sequences equal the oracle's (links, atoms, distances in next() order)."""
+    import ctypes as C
+    from hypergraphdb_amd import DefaultALGenerator, _lib
+    from hypergraphdb_amd._lib import check, lib, ptr
+    g, snap = config2
+    seeds = np.ascontiguousarray(g["seeds"][:16], np.int32)
+    opts = DefaultALGenerator(snap).options()
+    h = C.c_void_p()
+    check(lib().hgx_bfs_sequence(snap.handle, ptr(seeds), len(seeds), 2, C.byref(opts), C.byref(h)))
+    try:
+        ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
+        check(lib().hgx_seq_result_info(h, C.byref(ns), C.byref(npairs), C.byref(nl)))
+        n = npairs.value
+        assert n >= 1 << 24, n   # large enough for the threaded copy
+        off = np.zeros(len(seeds) + 1, np.int64)
+        check(lib().hgx_seq_result_offsets(h, ptr(off)))
+        links, atoms, dists = (np.empty(n, np.int32) for _ in range(3))
+        check(lib().hgx_seq_result_pairs(h, ptr(links), ptr(atoms), ptr(dists)))
+        rng = np.random.default_rng(5)
+        for first in [0, n - 1000] + rng.integers(0, n - 1000, 6).tolist():
+            wl, wa, wd = (np.empty(1000, np.int32) for _ in range(3))
+            got = C.c_int64()
+            vp = lambda x: C.c_void_p(ptr(x))   # (no argtypes for this symbol: keep 64-bit pointers)
+            check(lib().hgx_seq_result_pairs_range(h, C.c_int64(first), C.c_int64(1000), vp(wl), vp(wa), vp(wd),
+                                                   C.byref(got)))
+            assert got.value == 1000
+            assert np.array_equal(wl, links[first:first + 1000]) and np.array_equal(wa, atoms[first:first + 1000])
+            assert np.array_equal(wd, dists[first:first + 1000]), first
+    finally:
+        lib().hgx_seq_result_free(h)
+    orc = oracle(g)
+    for i in (0, 15):
+        l, a, d, _ = orc.bfs(int(seeds[i]), 2, algen(-1, True, True, False, False))
+        b, e = off[i], off[i + 1]
+        assert np.array_equal(atoms[b:e], a) and np.array_equal(links[b:e], l) and np.array_equal(dists[b:e], d), i
+    _ = _lib
