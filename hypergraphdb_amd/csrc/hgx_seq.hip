@@ -964,7 +964,7 @@ struct BbShared {
     int32_t e_dp[kBbFront + 1];
     int32_t e_sp[kBbFront + 1];
     int32_t cand[kBbCand];
-    int64_t wsum[kBbWaves];
+    int64_t wsum[kBbWaves], wsum2[kBbWaves];
     int64_t T, S;
     int32_t cand_n, n_disc, ovf;
 };
@@ -989,6 +989,40 @@ __device__ __forceinline__ int64_t bb_scan(BbShared& sm, int64_t v, int64_t* tot
     __syncthreads();
     *total = tot;
     return base + x - v;
+}
+
+// Two exclusive block scans in one pass (one pair of barriers instead of two).
+__device__ __forceinline__ void bb_scan2(BbShared& sm, int64_t v, int64_t u, int64_t& pv, int64_t& pu, int64_t* tv,
+                                         int64_t* tu) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v, y = u;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t xs = __shfl_up(x, off), ys = __shfl_up(y, off);
+        if (lane >= off) {
+            x += xs;
+            y += ys;
+        }
+    }
+    if (lane == 63) {
+        sm.wsum[w] = x;
+        sm.wsum2[w] = y;
+    }
+    __syncthreads();
+    int64_t bx = 0, by = 0, tx = 0, ty = 0;
+#pragma unroll
+    for (int k = 0; k < kBbWaves; ++k) {
+        const int64_t a = sm.wsum[k], b = sm.wsum2[k];
+        bx += k < w ? a : 0;
+        by += k < w ? b : 0;
+        tx += a;
+        ty += b;
+    }
+    __syncthreads();
+    *tv = tx;
+    *tu = ty;
+    pv = bx + x - v;
+    pu = by + y - u;
 }
 
 __device__ __forceinline__ uint32_t bb_hash(int32_t t) { return ((uint32_t)t * 0x9E3779B1u) >> 21; }
@@ -1042,9 +1076,8 @@ __device__ void bb_frontier(BbShared& sm, const BbArgs& a, int F) {
         ds += dg[k];
         ss += sg[k];
     }
-    int64_t T, S;
-    int64_t dp = bb_scan(sm, ds, &T);
-    int64_t sp = bb_scan(sm, ss, &S);
+    int64_t T, S, dp, sp;
+    bb_scan2(sm, ds, ss, dp, sp, &T, &S);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int i = tid * K + k;
