@@ -1352,8 +1352,9 @@ __global__ void __launch_bounds__(kBbThreads, 4) hgx_bfs_block(BbArgs a) {
 // overflowed, 3 = more than kCoMaxLevels levels, 4 = barrier timeout.  A level's errors go to a status
 // word of its parity, which the blocks read after the next barrier: the word they decide on cannot
 // change while some block has not read it yet (the next level writes the other one).
-constexpr int kCoThreads = 512;
-constexpr int kCoWaves = kCoThreads / 64;
+// 256 threads a workgroup (one wave a SIMD): config-5 step 0.412-0.423 -> 0.403 ms concurrent,
+// 0.571 -> 0.566 serial against 512 (profiles/r04zx_c5_occ_ab.log; HGX_CO_THREADS=512 for A/B)
+constexpr int kCoThreads = 256;
 // The grid: kCoBlocks workgroups, all resident (at most 2 per CU, one CU slot left).  Fewer, fuller
 // workgroups win: config 5's big closures took 0.75 / 0.64 / 0.59 / 0.55 / 0.58 ms with 512 / 192 /
 // 128 / 96 / 64 workgroups (the barrier and the segment counters are shared by fewer arrivals), and
@@ -1571,7 +1572,11 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
     nbytes += 16 * (int64_t)nch;
 }
 
-__global__ void __launch_bounds__(kCoThreads) hgx_bfs_coop(CoArgs a) {
+// NT threads a workgroup (kCoThreads; 512 for A/B, HGX_CO_THREADS)
+template <int NT>
+__global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
+    constexpr int kCoThreads = NT, kCoWaves = NT / 64;
+    static_assert(NT >= 128 + kMaxCoSeeds, "a level's start reads the seeds' counts with threads 128 ..");
     const int lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * kCoWaves + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * kCoWaves;
     const int seg = blockIdx.x % kCoSegs;
@@ -2710,10 +2715,18 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 
 // Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
 // 2 per CU and one CU slot left for other streams' kernels.
+int co_threads() {
+    static const int v = std::getenv("HGX_CO_THREADS") && std::atoi(std::getenv("HGX_CO_THREADS")) == 512 ? 512 : kCoThreads;
+    return v;
+}
+
+
 bool co_fits(hgx_graph* g) {
     if (g->co_ok < 0) {
         int per_cu = 0, cus = 0;
-        HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop, kCoThreads, 0));
+        const int nt = co_threads();
+        if (nt == 512) HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop<512>, 512, 0));
+        else HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop<kCoThreads>, kCoThreads, 0));
         HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
         const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
         static const int cap_env = std::getenv("HGX_CO_BLOCKS") ? std::atoi(std::getenv("HGX_CO_BLOCKS")) : 0;   // A/B
@@ -2820,7 +2833,8 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
 }
 
 void co_launch(hgx_graph* g, CoRun& r) {
-    hgx_bfs_coop<<<(unsigned)g->co_ok, kCoThreads, 0, g->stream>>>(r.a);
+    if (co_threads() == 512) hgx_bfs_coop<512><<<(unsigned)g->co_ok, 512, 0, g->stream>>>(r.a);
+    else hgx_bfs_coop<kCoThreads><<<(unsigned)g->co_ok, kCoThreads, 0, g->stream>>>(r.a);
     HGX_CHECK_LAUNCH();
 }
 
