@@ -415,16 +415,27 @@ def run_config5(args, ctx, barrier_sync):
         seq_sts += [st for _, st in step(concurrent=False)]
     seq_ms = (time.perf_counter() - t1) / n5 * 1e3
     seq_sts = [x.as_dict() for x in seq_sts]
+    # the timed loop runs without HIP timing events (with both directions on the GPU at once they cost
+    # ~0.07 of a ~0.4 ms step, profiles/r04zz_c5_{timing,notiming}.log); the per-kernel times behind
+    # `roofline` come from an equal loop with them, reported as ms_per_step_with_timing_events
+    for v in views:
+        v.set_timing(False)
     barrier_sync()
     t1 = time.perf_counter()
-    sts = []
     readout = 0
     for _ in range(n5):
-        for n, st in step():
+        for n, _st in step():
             readout += n
-            sts.append(st)
     barrier_sync()
     dt = ctx.max(time.perf_counter() - t1)
+    for v in views:
+        v.set_timing(True)
+    t2 = time.perf_counter()
+    sts = []
+    for _ in range(n5):
+        for n, st in step():
+            sts.append(st)
+    dt_ev = ctx.max(time.perf_counter() - t2)
     sts = [x.as_dict() for x in sts]
     drop = None if args.no_dropin else dropin_config5(args, ctx, barrier_sync, g, views, gens, pool)
     pool.shutdown()
@@ -436,6 +447,7 @@ def run_config5(args, ctx, barrier_sync):
            "ms_per_step": round(dt / n5 * 1e3, 3), "levels": max(s["n_levels_expanded"] for s in sts),
            "directions": "concurrent: hg.subsumed on the snapshot, hg.subsumes on an execution context of it",
            "ms_per_step_directions_serial": round(seq_ms, 3),
+           "ms_per_step_with_timing_events": round(dt_ev / n5 * 1e3, 3),
            "closure_atoms_per_step": closure,
            "workload": (f"config5: {g['n_nodes']} classes, HGSubsumes DAG + noise links, {len(g['seeds'])} classes x "
                         "{subsumed, subsumes}, unbounded depth"),
