@@ -44,7 +44,7 @@ EXPORTED = (
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
-    "hgx_seq_result_stats", "hgx_seq_result_engine_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_pattern_batch_ext", "hgx_query_result_count", "hgx_query_result_offsets", "hgx_query_result_ids",
+    "hgx_seq_result_stats", "hgx_seq_result_engine_stats", "hgx_seq_result_level_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_pattern_batch_ext", "hgx_query_result_count", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
     "hgx_partition_plan", "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_exchange_tables",
     "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
@@ -52,7 +52,7 @@ EXPORTED = (
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
     "hgx_graph_update", "hgx_query_coalesce_stats", "hgx_query_set_create", "hgx_pattern_batch_set",
     "hgx_query_set_free", "hgx_pattern_batch_set_into", "hgx_query_set_info", "hgx_snapshot_read_handles",
-    "hgx_snapshot_writer_begin", "hgx_snapshot_writer_handles", "hgx_snapshot_writer_end", "hgx_snapshot_writer_abort",
+    "hgx_snapshot_writer_begin", "hgx_snapshot_writer_handles", "hgx_snapshot_writer_end", "hgx_snapshot_writer_abort", "hgx_snapshot_writer_handle_bytes",
     "hgx_bfs_result_visited_range", "hgx_seq_result_pairs_range",
 )
 
@@ -88,14 +88,14 @@ class BfsStats(C.Structure):
                 ("xwords_nonzero", C.c_double), ("xwords_total", C.c_double), ("bytes_min", C.c_double),
                 ("level_xtrips", C.c_int32 * 64), ("ms_block", C.c_double), ("bytes_block", C.c_double),
                 ("block_seeds", C.c_int64), ("block_rerun", C.c_int64), ("ms_coop", C.c_double),
-                ("bytes_coop", C.c_double), ("block_coop", C.c_int64)]
+                ("bytes_coop", C.c_double), ("block_coop", C.c_int64), ("coop_fallbacks", C.c_int64)]
 
     def as_dict(self):
         d = {"n_levels_expanded": self.n_levels_expanded, "n_batches": self.n_batches, "ms_total": self.ms_total,
              "bytes_survey": self.bytes_survey, "traversed_edges": self.traversed_edges,
              "ms_exchange": self.ms_exchange, "bytes_exchanged": self.bytes_exchanged, "bytes_min": self.bytes_min,
              "block_seeds": int(self.block_seeds), "block_rerun": int(self.block_rerun),
-             "block_coop": int(self.block_coop)}
+             "block_coop": int(self.block_coop), "coop_fallbacks": int(self.coop_fallbacks)}
         d["kernels"] = {k: {"ms": self.ms_kernel[i], "launches": int(self.launches[i]),
                             "bytes": self.bytes_kernel[i]} for i, k in enumerate(KERNELS)}
         if self.block_seeds or self.block_rerun:   # the workgroup-per-seed stage: one launch per 4096 seeds
@@ -169,6 +169,7 @@ def lib():
         "hgx_seq_result_stats": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         "hgx_seq_result_engine_stats": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(C.c_double),
                                          C.POINTER(C.c_double)], C.c_int),
+        "hgx_seq_result_level_stats": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)], C.c_int),
         "hgx_seq_result_free": ([vp], None),
         "hgx_pattern_batch": ([vp, C.POINTER(AndQuery), i32, C.POINTER(vp)], C.c_int),
         "hgx_pattern_batch_packed": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),

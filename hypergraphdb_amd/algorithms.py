@@ -166,6 +166,10 @@ class SequenceResult:
             # seeds finished by the workgroup-per-seed engine / the level-synchronous reruns, and the
             # workgroup launches' device ms and algorithmic bytes
             self.n_block, self.n_level, self.ms_block, self.bytes_block = nb.value, nl.value, mb.value, bb.value
+            ml, bl, pl = C.c_double(), C.c_double(), C.c_int64()
+            check(lib().hgx_seq_result_level_stats(handle, C.byref(ml), C.byref(bl), C.byref(pl)))
+            # the level-synchronous engine: device ms, algorithmic bytes, levels that ran as pulls
+            self.ms_level, self.bytes_level, self.pull_levels = ml.value, bl.value, pl.value
         finally:
             lib().hgx_seq_result_free(handle)
 

@@ -5369,6 +5369,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
         r->stats.ms_coop = b.co_ms;
         r->stats.bytes_coop = b.co_bytes_alg;
         r->stats.block_coop = b.n_coop;
+        r->stats.coop_fallbacks = b.co_fallbacks;
         r->compact.assign((size_t)n_seeds, -1);
         for (size_t k = 0; k < b.rerun.size(); ++k) {
             r->compact[b.rerun[k]] = (int32_t)k;

@@ -256,6 +256,13 @@ int hgx_snapshot_writer_handles(hgx_snapshot_writer* w, const uint8_t* handles, 
     HGX_API_END
 }
 
+int hgx_snapshot_writer_handle_bytes(const hgx_snapshot_writer* w, int32_t* handle_bytes) {
+    HGX_API_BEGIN
+    if (!w || !handle_bytes) fail(HGX_E_INVALID, "hgx_snapshot_writer_handle_bytes: bad argument");
+    *handle_bytes = (int32_t)w->h.handle_bytes;
+    HGX_API_END
+}
+
 int hgx_snapshot_writer_end(hgx_snapshot_writer* w) {
     HGX_API_BEGIN
     if (!w) fail(HGX_E_INVALID, "hgx_snapshot_writer_end: null writer");

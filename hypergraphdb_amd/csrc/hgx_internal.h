@@ -235,12 +235,16 @@ struct hgx_graph {
     unsigned long long* seq_flag = nullptr;         // mapped coherent words: level sizes of the level engine
     unsigned long long seq_flag_seq = 0;            //   (their sequence numbers)
     int64_t ls_cap = 0, ls_wcap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
+    int64_t ls_hcap = 0, ls_fcap = 0;               //   and its two hash tables' slots (push, frontier)
+    int32_t* pin_j = nullptr;                       // [P] index of link row L in inc(t) for each pin (t, L):
+                                                    //   the level engine's pull levels (snapshot only, made on first use)
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
+    int64_t co_timeouts = 0;                        //   launches whose grid barrier timed out (seeds fell back)
     std::deque<hgx::YieldList> ylists;              // yield lists (snapshot only; contexts read their base's)
     std::deque<hgx::YieldAdj> yadjs;                // yield adjacencies (likewise)
     std::mutex ylist_mu;
@@ -374,6 +378,7 @@ struct BlockSet {
     bool co_host = false;
     double co_ms = 0, co_bytes_alg = 0;         // device ms of that launch (timing on), its algorithmic bytes
     int32_t n_coop = 0;                         // seeds it finished
+    int32_t co_fallbacks = 0;                   // its launches that timed out on a grid barrier (rows engine ran)
 };
 constexpr int kMaxCoSeeds = 64;
 // Runs every seed on the workgroup engine (caller holds g->mu, g's device current; max_depth -1 =

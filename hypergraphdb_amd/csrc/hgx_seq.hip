@@ -80,7 +80,11 @@ void host_parallel(int64_t n, bool wide, F&& fn) {
     };
     std::vector<std::thread> th;
     th.reserve((size_t)nt - 1);
-    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    } catch (const std::exception&) {
+        // no more threads (a process or memory limit): the ones started and this thread finish the jobs
+    }
     work();
     for (auto& t : th) t.join();
 }
@@ -1371,7 +1375,7 @@ constexpr int kCoBarGroups = 16;
 constexpr int kCoItemShift = 40;
 constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
-constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s
+constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s (HGX_CO_TIMEOUT: tests)
 // ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
 // even / odd levels (the seeding: odd), [kCoSel] seeds the workgroup
 // stage handed over, [kCoLev + slot * kCoSegs + seg] level counters (3 rotating slots), then cur [kcap],
@@ -1412,6 +1416,7 @@ struct CoArgs {
     int64_t* lvl_end;                                // mapped [kcap * kCoMaxLevels]: cur[s] after level d
     int64_t* lvl_trace;                              // mapped [2 * kCoMaxLevels]: start clock, work items
     int64_t* blk_bytes;                              // mapped [gridDim.x]: each block's algorithmic bytes
+    unsigned long long timeout;                      // barrier limit in s_memrealtime ticks (kCoTimeout)
 };
 
 // Work items and pairs cross workgroups inside the launch: they are written and read with agent-scope
@@ -1442,7 +1447,7 @@ __device__ __forceinline__ int2 co_get(const int2* p) {
 // stores and atomics above are then at the coherence point), the block arrives with a relaxed
 // agent-scope add, waiters poll relaxed.  Valid because everything another workgroup reads in the
 // loop is an agent-scope atomic operation (co_put / co_get, the bitmaps, counters and status words).
-__device__ __forceinline__ bool co_barrier_lite(u64* ctl, u64& gen, u64* status) {
+__device__ __forceinline__ bool co_barrier_lite(u64* ctl, u64& gen, u64* status, u64 limit) {
     __shared__ int s_to;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1454,7 +1459,7 @@ __device__ __forceinline__ bool co_barrier_lite(u64* ctl, u64& gen, u64* status)
         int to = 0;
         while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
                 atomicOr(status, 4ull);
                 to = 1;
                 break;
@@ -1471,7 +1476,7 @@ __device__ __forceinline__ bool co_barrier_lite(u64* ctl, u64& gen, u64* status)
 // counter (relaxed polls, one acquire fence after: an acquire load per poll invalidates the caches on
 // every iteration of every waiting block, ~50 us a barrier measured with 128 blocks).
 // ng = 1: every block adds to the top counter itself (one atomic on the path instead of two).
-__device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status, int ng) {
+__device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status, int ng, u64 limit) {
     __shared__ int s_to;
     __syncthreads();   // the block's stores and atomics of this level are issued
     if (threadIdx.x == 0) {
@@ -1492,7 +1497,7 @@ __device__ __forceinline__ bool co_barrier(u64* ctl, u64& gen, u64* status, int 
         int to = 0;
         while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kCoTimeout) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
                 atomicOr(status, 4ull);
                 to = 1;
                 break;
@@ -1536,7 +1541,7 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
                 b1 = i1;
             }
         }
-        nw = !(atomicOr(w, bit) & bit);
+        nw = !(atomicOr(w, bit) & bit);   // [xwg] vis
         deg = b1 - b0;
         trv = i1 - i0;
     }
@@ -1552,27 +1557,43 @@ __device__ __forceinline__ void co_step(const CoArgs& a, int32_t s, int32_t t, i
         if (lane >= off) x += y;
     }
     u64 wb = 0;
-    if (lane == 63) wb = atomicAdd(a.ctl + kCoLev + slot_next * kCoSegs + seg, (x << kCoItemShift) | (u64)__popcll(m));
+    if (lane == 63) wb = atomicAdd(a.ctl + kCoLev + slot_next * kCoSegs + seg, (x << kCoItemShift) | (u64)__popcll(m));   // [xwg]
     wb = __shfl(wb, 63);
     if (!nw) return;
     u64* status = a.ctl + kCoSt + (d & 1);
     const u64 pos = pbase_seg + (wb & kCoPairMask) + (u64)__popcll(m & ((1ull << lane) - 1ull));
-    if ((int64_t)pos < a.pseg) co_put(a.pairs + (int64_t)seg * a.pseg + (int64_t)pos, make_int2(t, s | (d + 1) << 8));
-    else atomicOr(status, 2ull);
+    if ((int64_t)pos < a.pseg) co_put(a.pairs + (int64_t)seg * a.pseg + (int64_t)pos, make_int2(t, s | (d + 1) << 8));   // [xwg]
+    else atomicOr(status, 2ull);   // [xwg]
     nbytes += 8;
     if (nch == 0) return;
     const u64 base = (wb >> kCoItemShift) + x - nch;
     if ((int64_t)(base + nch) > a.fr_seg) {
-        atomicOr(status, 1ull);
+        atomicOr(status, 1ull);   // [xwg]
         return;
     }
     int4* fr = a.fr + ((int64_t)slot_next * kCoSegs + seg) * a.fr_seg;
     for (u64 c = 0; c < nch; ++c)
-        co_put(fr + base + c, co_item(t, s, b0 + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk)));
+        co_put(fr + base + c, co_item(t, s, b0 + (int64_t)c * a.chunk, min<int64_t>(a.chunk, deg - (int64_t)c * a.chunk)));   // [xwg]
     nbytes += 16 * (int64_t)nch;
 }
 
 // NT threads a workgroup (kCoThreads; 512 for A/B, HGX_CO_THREADS)
+//
+// CROSS-WORKGROUP INVARIANT (the precondition of co_barrier_lite, which neither writes back nor
+// invalidates the non-coherent per-XCD L2s): inside the level loop every location one workgroup writes
+// and another reads is accessed ONLY through agent-scope atomics, each tagged [xwg] below --
+//   ctl counters / status words / barrier   __hip_atomic_* and atomicAdd / atomicOr (agent scope)
+//   fr (work items)                          co_put / co_get (agent-scope atomic 64-bit store / load)
+//   pairs                                    co_put / co_get
+//   vis (per-seed bitmaps)                   atomicOr (the discovery test itself)
+//   cur / trav (per-seed counts)             atomicAdd, read with __hip_atomic_load
+// Everything else is private to a workgroup (LDS, registers), read-only for the launch (the CSR, the
+// yield lists, seeds, sel_idx: written before the launch began), or written for the HOST only and read
+// after the grid has exited (hmeta, lvl_end, lvl_trace, blk_bytes: mapped memory).  The epilogue's plain
+// stores into vis happen after the last barrier, when no workgroup of this launch reads vis again.  A new
+// plain store to a shared location in the loop would break the light barrier silently on multi-XCD
+// parts; tests/test_gpu_bfs.py::test_grid_stage_stress runs the stage at config-5 scale against the rows
+// engine to catch it.
 template <int NT>
 __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
     constexpr int kCoThreads = NT, kCoWaves = NT / 64;
@@ -1595,11 +1616,7 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
         const u64 n = __hip_atomic_load(a.ctl + kCoSel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         k = n > (u64)a.kcap ? a.kcap + 1 : (int32_t)n;
         if (blockIdx.x == 0) {
-            if (threadIdx.x == 0) {
-                a.hmeta[2] = (int64_t)n;
-                a.hmeta[0] = 0;
-                a.hmeta[1] = 0;
-            }
+            if (threadIdx.x == 0) a.hmeta[2] = (int64_t)n;   // hmeta[0] stays -1 until a normal exit
             for (int j = threadIdx.x; j < k && j < a.kcap; j += kCoThreads)
                 a.hmeta[4 + 2 * a.kcap + kCoSegs + j] = a.sel_idx[j];
         }
@@ -1627,7 +1644,8 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
             }
         }
     const int ng = a.lite ? 1 : a.bgroups;   // the light barrier adds to the top counter directly
-    bool timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt) : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);
+    bool timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt, a.timeout)
+                            : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng, a.timeout);
     int32_t d = 0;
     u64 pbase = 0;   // pairs of this block's segment found before the current level
     for (; !timed_out; ++d) {
@@ -1689,7 +1707,7 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
                     if (seg_pre[mid] <= it) lo = mid;
                     else hi = mid - 1;
                 }
-                const int4 e = co_get(fr + (int64_t)lo * a.fr_seg + (it - seg_pre[lo]));
+                const int4 e = co_get(fr + (int64_t)lo * a.fr_seg + (it - seg_pre[lo]));   // [xwg]
                 ip = e.x;
                 is = e.y & 0xFF;
                 ilo = (int64_t)(uint32_t)e.z | (int64_t)e.w << 32;
@@ -1763,14 +1781,23 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
         }
         __syncthreads();   // the block's per-seed counts of this level -> the seed counters
         for (int j = threadIdx.x; j < k; j += kCoThreads) {
-            if (cnt_l[j]) atomicAdd(a.cur + j, cnt_l[j]);
-            if (trav_l[j]) atomicAdd(a.trav + j, trav_l[j]);
+            if (cnt_l[j]) atomicAdd(a.cur + j, cnt_l[j]);      // [xwg]
+            if (trav_l[j]) atomicAdd(a.trav + j, trav_l[j]);   // [xwg]
             cnt_l[j] = 0;
             trav_l[j] = 0;
         }
-        timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt) : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng);
+        timed_out = a.lite ? co_barrier_lite(a.ctl, gen, a.ctl + kCoSt, a.timeout)
+                           : co_barrier(a.ctl, gen, a.ctl + kCoSt, ng, a.timeout);
     }
-    if (timed_out) return;   // the host clears the bitmaps
+    if (timed_out) {
+        // A block that gave up on a barrier reports it in its own mapped word (the host set it to 0): the
+        // status word alone cannot carry it -- a late block may pass a barrier the others already left,
+        // or every other block may leave the loop normally after a barrier this block timed out on (a
+        // race with the last arrival), and block 0 then writes status 0.  The host reads both after the
+        // whole grid has exited, clears the bitmaps and sends the seeds to the rows engine.
+        if (threadIdx.x == 0) __hip_atomic_store(a.hmeta + 3, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     // every block left the loop after the same barrier, which every count, status word and pair had
     // reached: no further barrier.  The block's algorithmic bytes go to its own mapped word.
     {
@@ -1792,7 +1819,7 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
     if (st == 0) {
         const int64_t nblk_seg = ((int64_t)gridDim.x - seg + kCoSegs - 1) / kCoSegs;
         for (int64_t i = (int64_t)(blockIdx.x / kCoSegs) * kCoThreads + threadIdx.x; i < np; i += nblk_seg * kCoThreads) {
-            const int2 pr = co_get(a.pairs + (int64_t)seg * a.pseg + i);
+            const int2 pr = co_get(a.pairs + (int64_t)seg * a.pseg + i);   // [xwg]
             a.vis[(int64_t)(pr.y & 0xFF) * a.vwords + (pr.x >> 6)] = 0ull;
         }
         if (blockIdx.x == 0)
@@ -1813,29 +1840,48 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Level-synchronous engine (the traversals a workgroup cannot hold: more than kSbPairs pairs).
 //
-// Per level six kernels with fixed grids that read every size from device memory, so the host never
-// waits inside a level; it enqueues level d+1 before it polls level d's frontier size from mapped
-// memory (a finished traversal costs one level of no-op launches):
-//   hgx_ls_degree   frontier entries -> incidence start + degree; block sums over contiguous entry
-//                   ranges; records where each seed's pairs of the previous level start (runs)
-//   hgx_ls_prefix   degree prefix (blocks scan the block sums redundantly) + the tile -> first-entry
-//                   table of the level's flat item space; T, key-space width, capacity checks
-//   hgx_ls_expand   256-item tiles: entry by a short search inside the tile's entry range, yield
-//                   flags, link predicate, targets, position rule; atomicMin of
-//                   ((it << kbits | k) + 1) << 32 | link atom on key[seed][target]; first touch
-//                   appends (seed, target) to the level's discoveries; zeroes the rank bitmap
-//   hgx_ls_bits     one bit per discovery at its key in a bitmap over the level's key space
-//   hgx_ls_wprefix  popcount prefix of the bitmap words, per contiguous word range
-//   hgx_ls_emit     rank = popcount prefix below the key: pair `rank` of the level (link, atom),
-//                   entry `rank` of the next frontier, key[seed][atom] = 0 (examined)
-// The key order is (entry, link index, yield rank), i.e. the reference's stream order (the file
-// header); the level's pairs are seed-major because the frontier is.
+// A chunk of nb seeds runs level by level with fixed-grid kernels that read every size from device
+// memory, so the host never waits inside a level; it enqueues level d+1 before it polls level d's
+// frontier size from mapped memory (a finished traversal costs one level of no-op launches).
+//
+// State (round 5: no per-seed key table):
+//   vis    [A x W] u64  examined rows, atom-major, bit s of row t <=> seed s examined t
+//                       (HGBreadthFirstTraversal.examined, :36,:59-62); W = ceil(nb / 64)
+//   disc / dval         the level's discoveries (seed * A + atom, value), value =
+//                       ((it << kbits | k) + 1) << 32 | discovering link atom, it = the flat item index
+//                       (entry, link index) of the yield, k its rank in the link -- the reference's
+//                       stream order (file header); the minimum over a target's yields is its
+//                       discovery (DefaultALGenerator.getNextLink :287-315, HGBreadthFirstTraversal :56-64)
+// A level finds its discoveries one of two ways (hgx_ls_prefix decides on the device from the level's
+// item count T against the incidence I):
+//   push (narrow levels): every item's yields not examined yet lower the value of a level-local open-
+//        addressing hash keyed by (seed, atom) with atomicMin; the first claimer of a slot appends it
+//        (hgx_ls_expand).  The table is sized to the discovery capacity and cleared slot by slot by the
+//        level's own bits pass (no per-level memset).
+//   pull (wide levels, the incidence items of an untyped / typed generator without the yield
+//        adjacency): every atom t with a seed that has not examined it scans inc(t) -- for each link L
+//        and co-target p of t that is on some seed's frontier (the union bitmap), the seeds s with p on
+//        their frontier and t not examined get the candidate value with it = pre(s, p) + j(p, L) (the
+//        item index of p's entry for s plus the index of L in inc(p), pin_j), k = t's yield rank in L
+//        from p.  The minimum per seed is kept in LDS (a wave per light atom, a workgroup per 4096-entry
+//        chunk of a heavy atom with one global atomicMin per seed and chunk), so no global table and no
+//        atomic per yield: config 2's level 1 (64 seeds, 3.6e8 items, 1.4e9 yields) touches the CSR
+//        once instead of 1.4e9 random words of a 25.6 GB key array.
+//        Frontier rows frow [A x W], the union bitmap ubit and a small hash (seed, atom) -> pre are
+//        built from the frontier entries in the expand launch and cleared through the union list.
+// Then, both ways: hgx_ls_bits (a bit per discovery at its key over the level's key space),
+// hgx_ls_wprefix (popcount prefix), hgx_ls_emit (rank = popcount below the key: pair `rank` of the
+// level, entry `rank` of the next frontier, vis bit set).  The level's pairs are seed-major because the
+// frontier is.
 constexpr int kLsG = 256;               // blocks of the range kernels (contiguous ranges: prefix-able)
 constexpr int64_t kLsTile = 256;        // items per expand tile
 constexpr int kLsSlots = 4;             // per-level counter slots (ring); slot words:
-enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5 };
+enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5, lsPull = 6, lsU = 7 };
 constexpr int kLsSlotWords = 8;
-constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2;
+constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2,
+              kLsBytes = kLsStatus + 3, kLsPullN = kLsStatus + 4;
+// status bits: 1 discoveries > cap, 2 runs > rcap, 4 key-space bitmap > wcap, 8 tiles > tcap, 16 keys wider
+// than 32 bits, 32 push hash too full, 64 frontier hash too full
 // A level's discoveries go to kLsDSegs segments of the list, one counter each (a wave appends to the
 // segment of its block): one shared counter took one same-address atomic per wave and round, which
 // serialise at ~20 ns each -- the whole of a config-2 level's expand time.
@@ -1845,6 +1891,9 @@ constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsR
 constexpr int kLsDSegs = 32;
 constexpr int kLsDSeg = kLsStatus + 8;                           // [kLsSlots][kLsDSegs + 1] counters (+ overflow)
 constexpr int kLsCtlWords = kLsDSeg + kLsSlots * (kLsDSegs + 1);
+constexpr int kLsMaxW = 16;             // row words: chunks of <= 1024 seeds
+constexpr int kLsProbes = 64;           // hash probes before a level reports overflow (load <= 1/2)
+constexpr u64 kLsEmpty = ~0ull;
 
 struct LsArgs {
     int64_t A;
@@ -1857,7 +1906,8 @@ struct LsArgs {
     const int32_t* link_atom;
     int32_t want_type, min_arity, mode, rev, kbits;
     int64_t t_limit;                    // largest item count of a level with 32-bit keys
-    u64* key;                           // [nb * A]: ~0 fresh, 0 examined, else this level's best value
+    int32_t nb, W;                      // seeds of the chunk, row words
+    u64* vis;                           // [A * W] examined rows (zero at the call's start)
     int64_t cap;                        // frontier / discovery / output capacity (entries)
     int64_t wcap, tcap, rcap;           // bitmap words, tiles, runs
     int64_t* ctl;                       // kLsCtlWords
@@ -1869,7 +1919,8 @@ struct LsArgs {
     int64_t* tile;                      // [tcap] first entry of each item tile
     int64_t* bsum;                      // [kLsG] block sums (entries, then bitmap words)
     int64_t* disc;                      // the level's discoveries (seed * A + atom): kLsDSegs segments of
-    int64_t segcap;                     //   segcap entries, then an overflow region of cap entries
+    u64* dval;                          //   segcap entries, then an overflow region of cap entries; their
+    int64_t segcap;                     //   values (push: the hash slot until hgx_ls_bits)
     u64* bm;                            // [wcap] rank bitmap
     uint32_t* wpre;                     // [wcap] popcount prefix of word w inside its block's range
     int32_t* out_link;                  // [cap] pairs, level-major (device)
@@ -1881,6 +1932,25 @@ struct LsArgs {
     const int64_t* y_off;
     const int32_t* a_tgt;
     const int32_t* a_lnk;
+    // push: the level hash (hcap = hmask + 1 slots; key kLsEmpty / value ~0 between levels)
+    u64* hkey;
+    u64* hval;
+    int64_t hmask;
+    // pull
+    int32_t pull;                       // 0 never, 1 by the level's width, 2 every level (tests)
+    int64_t I;                          // incidence entries
+    const int32_t* pin_j;               // [P] index of link row L in inc(tgt_idx[p]) for pin p of L
+    u64* frow;                          // [A * W] frontier rows of the level (zero between levels)
+    u64* ubit;                          // [A / 64 + 1] union of the level's frontier atoms (zero between levels)
+    int32_t* ulist;                     // [cap] the union's atoms (the rows / bits to clear after the level)
+    u64* fkey;                          // frontier hash: (seed << 32 | atom) -> the item index of the first
+    uint32_t* fpre;                     //   item of that frontier entry (fmask + 1 slots, kLsEmpty keys
+    int64_t fmask;                      //   between levels)
+    int32_t fbits, hbits;               // log2 of the two hash tables' sizes
+    const HeavyChunk* chunks;           // heavy atoms' 4096-entry chunks (the graph's table)
+    int64_t n_chunks, n_heavy;
+    const int32_t* heavy_atom;          // [n_heavy]
+    u64* hbest;                         // [n_heavy * nb] heavy atoms' minimum values (~0 between levels)
 };
 
 __device__ __forceinline__ int64_t* ls_slot(const LsArgs& a, int d) { return a.ctl + (d % kLsSlots) * kLsSlotWords; }
@@ -1907,15 +1977,50 @@ __device__ __forceinline__ int64_t ls_disc_prefix(const LsArgs& a, int d, int64_
     return pre[kLsDSegs + 1];
 }
 
-// Discovery x of the level (flat index over the segments, then the overflow region).
-__device__ __forceinline__ int64_t ls_disc_at(const LsArgs& a, const int64_t* pre, int64_t x) {
+// Position of discovery x of the level (flat index over the segments, then the overflow region).
+__device__ __forceinline__ int64_t ls_disc_pos(const LsArgs& a, const int64_t* pre, int64_t x) {
     int lo = 0, hi = kLsDSegs;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (pre[mid] <= x) lo = mid;
         else hi = mid - 1;
     }
-    return a.disc[(int64_t)lo * a.segcap + (x - pre[lo])];
+    return (int64_t)lo * a.segcap + (x - pre[lo]);
+}
+
+// Appends the wave's discoveries (lanes with `isnew`: (sa, val)) to the block's segment of level d's
+// list with one atomic per wave (every lane of the wave calls it).
+__device__ __forceinline__ void ls_append(const LsArgs& a, int d, bool isnew, int64_t sa, u64 val) {
+    const u64 m = __ballot(isnew);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int dsg = blockIdx.x % kLsDSegs;
+    int64_t* dn = ls_dseg(a, d) + dsg;
+    const int leader = __ffsll((long long)m) - 1;
+    const u64 cnt = (u64)__popcll(m), segcap = (u64)a.segcap;
+    u64 base = 0, ob = 0;
+    if (lane == leader) {
+        base = atomicAdd((unsigned long long*)dn, cnt);
+        const u64 fit = base >= segcap ? 0ull : min(cnt, segcap - base);
+        if (fit < cnt) ob = atomicAdd((unsigned long long*)(ls_dseg(a, d) + kLsDSegs), cnt - fit);
+    }
+    base = __shfl(base, leader);
+    ob = __shfl(ob, leader);
+    if (isnew) {
+        const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
+        int64_t pos = -1;
+        if (w < segcap) {
+            pos = (int64_t)dsg * a.segcap + (int64_t)w;
+        } else {   // the segment is full: the shared overflow region
+            const int64_t o = (int64_t)(ob + (w - max(base, segcap)));
+            if (o < a.cap) pos = (int64_t)kLsDSegs * a.segcap + o;
+            else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap holds
+        }
+        if (pos >= 0) {
+            a.disc[pos] = sa;
+            a.dval[pos] = val;
+        }
+    }
 }
 
 __device__ __forceinline__ int64_t ls_block_sum(int64_t v, int64_t* ws) {
@@ -1965,6 +2070,12 @@ __device__ __forceinline__ int64_t ls_block_offsets(const int64_t* __restrict__ 
 }
 
 __device__ __forceinline__ int64_t ls_lo(int64_t n, int b) { return n * b / kLsG; }   // n < 2^53
+
+// the block's algorithmic bytes into the call's byte counter (one atomic per block)
+__device__ __forceinline__ void ls_add_bytes(const LsArgs& a, int64_t nbytes, int64_t* ws) {
+    const int64_t t = ls_block_sum(nbytes, ws);
+    if (threadIdx.x == 0 && t) atomicAdd((unsigned long long*)&a.ctl[kLsBytes], (unsigned long long)t);
+}
 
 __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_t runs_only) {
     __shared__ int64_t ws[4];
@@ -2043,9 +2154,12 @@ __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
         const int64_t W = (int64_t)((((u64)T << a.kbits) + 63ull) >> 6);
         sl[lsW] = W;
         sl[lsTiles] = (T + kLsTile - 1) / kLsTile;
+        // pull when the level's items are a large part of the incidence (a pull reads all of it)
+        sl[lsPull] = a.pull == 2 || (a.pull == 1 && T * 8 > a.I) ? 1 : 0;
+        if (sl[lsPull]) atomicAdd((unsigned long long*)&a.ctl[kLsPullN], 1ull);
         if (!a.y_off) atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
         int64_t st = 0;
-        if (T > a.t_limit) st |= 16;   // keys wider than 32 bits: the key-array engine takes the chunk
+        if (T > a.t_limit) st |= 16;   // keys wider than 32 bits: the chunk is split (or the key-array engine)
         if (W > a.wcap) st |= 4;
         if (sl[lsTiles] > a.tcap) st |= 8;
         if (st) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)st);
@@ -2062,30 +2176,106 @@ __device__ __forceinline__ int64_t ls_search(const int64_t* __restrict__ pre, in
     return lo;
 }
 
+__device__ __forceinline__ u64 ls_hash(u64 key, int bits) { return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits); }
+
+// The push level's hash: lowers the value of (seed, atom) `sa` to v; true (and *slot) when this call
+// claimed the slot, i.e. discovered the atom for the seed at this level.  Keys only ever go from empty to
+// sa inside a level, so a stale plain read of a key can only say "empty" (the CAS then tells the truth),
+// and a stale value is larger than the current one (only an extra atomicMin).
+__device__ __forceinline__ bool ls_hash_min(const LsArgs& a, int64_t sa, u64 v, int64_t* slot) {
+    u64 h = ls_hash((u64)sa, a.hbits);
+    for (int probe = 0; probe < kLsProbes; ++probe) {
+        u64 k = a.hkey[h];
+        if (k == kLsEmpty) {
+            k = atomicCAS((unsigned long long*)&a.hkey[h], kLsEmpty, (unsigned long long)sa);
+            if (k == kLsEmpty) {
+                atomicMin((unsigned long long*)&a.hval[h], (unsigned long long)v);
+                *slot = (int64_t)h;
+                return true;
+            }
+        }
+        if (k == (u64)sa) {
+            if (a.hval[h] > v) atomicMin((unsigned long long*)&a.hval[h], (unsigned long long)v);
+            return false;
+        }
+        h = (h + 1) & (u64)a.hmask;
+    }
+    atomicOr((unsigned long long*)&a.ctl[kLsStatus], 32ull);   // the table is too full: grow and rerun
+    return false;
+}
+
+// Push levels: one incidence item (entry i, link index j) per lane, 256-item tiles (a short search
+// inside the tile's entry range).  Pull levels: this launch builds the frontier rows, the union and
+// the (seed, atom) -> pre hash from the frontier entries instead.  Both zero the level's rank bitmap.
 __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
-    const int64_t* sl = ls_slot(a, d);
+    __shared__ int64_t ws[4];
+    int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
     const int64_t F = sl[lsF], T = sl[lsT], W = sl[lsW], nt = sl[lsTiles];
-    const int dsg = blockIdx.x % kLsDSegs;   // this block's segment of the discovery list
-    int64_t* dn = ls_dseg(a, d) + dsg;
     const int cur = d & 1;
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
     for (int64_t w = blockIdx.x * 256ll + threadIdx.x; w < W; w += (int64_t)gridDim.x * 256) a.bm[w] = 0ull;
     const int lane = threadIdx.x & 63;
+    int64_t nbytes = 0;
+    if (sl[lsPull]) {
+        // frontier rows (bit s of frow[p] <=> p is on seed s's frontier), the union list, and
+        // pre(s, p) in the frontier hash; entries in a wave-uniform loop (the union append ballots)
+        for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < F; i0 += (int64_t)gridDim.x * 256) {
+            const int64_t i = i0 + threadIdx.x;
+            bool first = false;
+            int32_t p = 0;
+            if (i < F) {
+                p = fa[i];
+                const int32_t s = fs[i];
+                atomicOr((unsigned long long*)&a.frow[(int64_t)p * a.W + (s >> 6)], 1ull << (s & 63));
+                const u64 bit = 1ull << (p & 63);
+                first = !(atomicOr((unsigned long long*)&a.ubit[p >> 6], bit) & bit);
+                const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)p;
+                u64 h = ls_hash(key, a.fbits);
+                for (int probe = 0;; ++probe) {
+                    if (atomicCAS((unsigned long long*)&a.fkey[h], kLsEmpty, (unsigned long long)key) == kLsEmpty) {
+                        a.fpre[h] = (uint32_t)a.pre[i];
+                        break;
+                    }
+                    h = (h + 1) & (u64)a.fmask;
+                    if (probe >= kLsProbes) {   // the table is too full: grow and rerun
+                        atomicOr((unsigned long long*)&a.ctl[kLsStatus], 64ull);
+                        break;
+                    }
+                }
+                nbytes += 8 + 8 + 8 + 16;
+            }
+            const u64 m = __ballot(first);
+            if (m) {
+                const int leader = __ffsll((long long)m) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd((unsigned long long*)&sl[lsU], (unsigned long long)__popcll(m));
+                base = __shfl(base, leader);
+                if (first) a.ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = p;   // base + rank < F <= cap
+            }
+        }
+        ls_add_bytes(a, nbytes, ws);
+        return;
+    }
     for (int64_t k = blockIdx.x; k < nt; k += gridDim.x) {
         const int64_t e0 = a.tile[k], e1 = k + 1 < nt ? a.tile[k + 1] : F - 1;
         const int64_t it = k * kLsTile + threadIdx.x;
         bool live = it < T;
         int64_t i = 0, j = 0, ii = 0;
-        int32_t p = -1, n = 0, la = 0, lo = 0, hi = 0;
+        int32_t p = -1, n = 0, la = 0, lo = 0, hi = 0, s = 0;
         int64_t b = 0;
         if (live) {
             i = ls_search(a.pre, e0, e1, it);
             j = it - a.pre[i];
             p = fa[i];
+            s = fs[i];
             ii = a.fbase[i] + j;
-            if (!a.a_tgt && a.yf && !((a.yf[ii] >> a.mode) & 1u)) live = false;     // nothing to yield
+            nbytes += 24;
+            if (!a.a_tgt && a.yf) {
+                nbytes += 1;
+                if (!((a.yf[ii] >> a.mode) & 1u)) live = false;     // nothing to yield
+            }
         }
         int32_t t_adj = 0;
         if (live && a.a_tgt) {   // the generator's output itself: one yield, rank 0
@@ -2093,6 +2283,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             la = a.a_lnk[ii];
             n = 1;
             hi = 1;
+            nbytes += 8;
         } else if (live) {
             const int32_t L = a.inc_row[ii];
             const int32_t ty = a.want_type >= 0 ? a.inc_type[ii] : 0;
@@ -2101,6 +2292,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
             n = (int32_t)(a.tgt_off[L + 1] - b);
             la = a.link_atom[L];
             if (n < a.min_arity) live = false;                                    // minArity (:309)
+            nbytes += (a.want_type >= 0 ? 8 : 4) + 20 + 4 * (int64_t)n;
         }
         if (live && !a.a_tgt) {
             hi = n;
@@ -2120,55 +2312,285 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
         const int32_t cnt = live && hi > lo ? hi - lo : 0;
         int32_t rounds = cnt;
         for (int off = 32; off > 0; off >>= 1) rounds = max(rounds, __shfl_xor(rounds, off));
-        const int64_t sA = live ? (int64_t)fs[i] * a.A : 0;
+        const int64_t sA = live ? (int64_t)s * a.A : 0;
         const u64 kb = ((u64)it << a.kbits) + 1ull;
         for (int32_t r = 0; r < rounds; ++r) {   // wave-uniform rounds: one append atomic per wave and round
             bool isnew = false;
             int32_t t = 0;
+            int64_t slot = 0;
             if (r < cnt) {
                 const int32_t q = lo + r;
                 t = a.a_tgt ? t_adj : a.tgt_idx[b + q];
                 if (t != p) {
-                    const u64 rk = a.a_tgt ? 0ull : (u64)(a.rev ? n - 1 - q : q);
-                    const u64 v = ((kb + rk) << 32) | (u64)(uint32_t)la;
-                    u64* slot = a.key + sA + t;
-                    if (*slot > v) isnew = atomicMin(slot, v) == kNoKey;
-                }
-            }
-            const u64 m = __ballot(isnew);
-            if (m) {
-                const int leader = __ffsll((long long)m) - 1;
-                const u64 cnt = (u64)__popcll(m), segcap = (u64)a.segcap;
-                u64 base = 0, ob = 0;
-                if (lane == leader) {
-                    base = atomicAdd((unsigned long long*)dn, cnt);
-                    const u64 fit = base >= segcap ? 0ull : min(cnt, segcap - base);
-                    if (fit < cnt) ob = atomicAdd((unsigned long long*)(ls_dseg(a, d) + kLsDSegs), cnt - fit);
-                }
-                base = __shfl(base, leader);
-                ob = __shfl(ob, leader);
-                if (isnew) {
-                    const u64 w = base + (u64)__popcll(m & ((1ull << lane) - 1ull));
-                    if (w < segcap) {
-                        a.disc[(int64_t)dsg * a.segcap + (int64_t)w] = sA + t;
-                    } else {   // the segment is full: the shared overflow region
-                        const int64_t o = (int64_t)(ob + (w - max(base, segcap)));
-                        if (o < a.cap) a.disc[(int64_t)kLsDSegs * a.segcap + o] = sA + t;
-                        else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap holds
+                    nbytes += 8;   // the examined word
+                    if (!((a.vis[(int64_t)t * a.W + (s >> 6)] >> (s & 63)) & 1ull)) {
+                        const u64 rk = a.a_tgt ? 0ull : (u64)(a.rev ? n - 1 - q : q);
+                        const u64 v = ((kb + rk) << 32) | (u64)(uint32_t)la;
+                        isnew = ls_hash_min(a, sA + t, v, &slot);
+                        nbytes += 16;
                     }
                 }
             }
+            ls_append(a, d, isnew, sA + t, (u64)slot);
+        }
+    }
+    ls_add_bytes(a, nbytes, ws);
+}
+
+// Pull of one atom t's incidence range [eb, ee) by one wave (a lane per entry): the candidate values
+// of the seeds in need[] (t not examined by them) go into best[] (LDS, per seed) with atomicMin.  The
+// rules are the expand's: link predicate, minimum arity, the positions co-target p yields (3.2), the
+// yield rank k = t's best position among them (descending ranks in reverse order), and the item index
+// it = pre(s, p) + j(p, L) of the yield.
+__device__ __forceinline__ void lp_pair(const LsArgs& a, int32_t p, int32_t q, int32_t qt, int32_t n, int64_t tb,
+                                        int32_t la, u64* best, const u64* need, int64_t& nbytes) {
+    const u64 kq = (u64)(a.rev ? n - 1 - qt : qt);
+    const uint32_t j = (uint32_t)a.pin_j[tb + q];
+    nbytes += 4 + 8 * a.W;
+    for (int w = 0; w < a.W; ++w) {
+        u64 m = a.frow[(int64_t)p * a.W + w] & need[w];
+        while (m) {
+            const int s = w * 64 + __ffsll((long long)m) - 1;
+            m &= m - 1;
+            // pre(s, p): the frontier hash (the entry exists: frow says so)
+            const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)p;
+            u64 h = ls_hash(key, a.fbits);
+            while (a.fkey[h] != key) h = (h + 1) & (u64)a.fmask;
+            const u64 it = (u64)a.fpre[h] + j;
+            const u64 v = ((((it << a.kbits) | kq) + 1ull) << 32) | (u64)(uint32_t)la;
+            atomicMin((unsigned long long*)&best[s], (unsigned long long)v);
+            nbytes += 12;
         }
     }
 }
 
+__device__ void lp_range(const LsArgs& a, int32_t t, int64_t eb, int64_t ee, u64* best, const u64* need,
+                         int64_t& nbytes) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t e = eb + lane; e < ee; e += 64) {
+        if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {                       // linkPredicate (:300)
+            nbytes += 4;
+            continue;
+        }
+        const int32_t L = a.inc_row[e];
+        const int64_t tb = a.tgt_off[L];
+        const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
+        nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
+        if (n < a.min_arity) continue;                                                 // minArity (:309)
+        nbytes += 4 * (int64_t)n + 4;
+        const int32_t la = a.link_atom[L];
+        if (n <= 8) {   // the row in registers
+            int32_t tg[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
+            u64 onf[8];   // union bits of the co-targets, loaded together
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                onf[q] = (q < n && tg[q] != t) ? a.ubit[tg[q] >> 6] >> (tg[q] & 63) : 0ull;
+            nbytes += 8 * (int64_t)n;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
+                const int32_t p = tg[q];
+                bool dup = false;                 // p's first occurrence only
+#pragma unroll
+                for (int q2 = 0; q2 < q; ++q2) dup |= tg[q2] == p;
+                if (dup) continue;
+                int32_t lp = q;
+#pragma unroll
+                for (int q2 = q + 1; q2 < 8; ++q2)
+                    if (tg[q2] == p) lp = q2;
+                int32_t lo = 0, hi = n;           // positions p yields (3.2)
+                if (a.mode == sAfterFirst) lo = q + 1;
+                else if (a.mode == sBeforeFirst) hi = q;
+                else if (a.mode == sBeforeLast) hi = lp;
+                else if (a.mode == sAfterLast) lo = lp + 1;
+                int32_t qt = -1;                  // t's best yielded position
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2)
+                    if (q2 >= lo && q2 < hi && tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
+                if (qt < 0) continue;
+                lp_pair(a, p, q, qt, n, tb, la, best, need, nbytes);
+            }
+            continue;
+        }
+        nbytes += 8 * (int64_t)n;
+        for (int32_t q = 0; q < n; ++q) {   // long rows: from memory
+            const int32_t p = a.tgt_idx[tb + q];
+            if (p == t) continue;
+            if (!((a.ubit[p >> 6] >> (p & 63)) & 1ull)) continue;
+            bool dup = false;
+            for (int32_t q2 = 0; q2 < q; ++q2) dup |= a.tgt_idx[tb + q2] == p;
+            if (dup) continue;
+            int32_t lp = q;
+            for (int32_t q2 = q + 1; q2 < n; ++q2)
+                if (a.tgt_idx[tb + q2] == p) lp = q2;
+            int32_t lo = 0, hi = n;
+            if (a.mode == sAfterFirst) lo = q + 1;
+            else if (a.mode == sBeforeFirst) hi = q;
+            else if (a.mode == sBeforeLast) hi = lp;
+            else if (a.mode == sAfterLast) lo = lp + 1;
+            int32_t qt = -1;
+            for (int32_t q2 = lo; q2 < hi; ++q2)
+                if (a.tgt_idx[tb + q2] == t && (qt < 0 || a.rev)) qt = q2;
+            if (qt < 0) continue;
+            lp_pair(a, p, q, qt, n, tb, la, best, need, nbytes);
+        }
+    }
+}
+
+// Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its waves' minima merged and lowered
+// into hbest with one global atomicMin per seed), then the light atoms (a wave each, its discoveries
+// appended right away).  LDS: 4 waves x nb values (dynamic).
+__global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
+    extern __shared__ u64 lp_best[];   // [4][nb]
+    __shared__ u64 lp_need[4][kLsMaxW];
+    __shared__ int64_t ws[4];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || !sl[lsPull]) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nb = a.nb, W = a.W;
+    u64* best = lp_best + (int64_t)wave * nb;
+    u64* need = lp_need[wave];
+    for (int s = lane; s < nb; s += 64) best[s] = ~0ull;
+    const u64 lastmask = (nb & 63) ? (1ull << (nb & 63)) - 1ull : ~0ull;
+    int64_t nbytes = 0;
+    // heavy chunks
+    for (int64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
+        const HeavyChunk ch = a.chunks[c];
+        const int32_t t = ch.atom;
+        if (lane < W) {
+            const u64 v = ~a.vis[(int64_t)t * W + lane];
+            need[lane] = lane == W - 1 ? v & lastmask : v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        u64 any = 0;
+        for (int w = 0; w < W; ++w) any |= need[w];
+        nbytes += lane == 0 ? 24 + 8 * W : 0;
+        if (any) {
+            const int64_t q = (ch.end - ch.beg + 3) / 4;
+            const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
+            lp_range(a, t, b, e, best, need, nbytes);
+        }
+        __syncthreads();
+        for (int s = threadIdx.x; s < nb; s += 256) {   // the four waves' minima -> the heavy atom's row
+            u64 v = lp_best[s];
+#pragma unroll
+            for (int k = 1; k < 4; ++k) v = min(v, lp_best[(int64_t)k * nb + s]);
+            if (v != ~0ull) {
+                atomicMin((unsigned long long*)&a.hbest[(int64_t)ch.slot * nb + s], (unsigned long long)v);
+                for (int k = 0; k < 4; ++k) lp_best[(int64_t)k * nb + s] = ~0ull;
+                nbytes += 8;
+            }
+        }
+        __syncthreads();
+    }
+    // light atoms: a wave takes 64 consecutive atoms (a lane each: degree and examined row), then pulls
+    // the ones with incidence, <= kHeavyDegree entries and a seed that has not examined them, one by one
+    const int64_t nwv = (int64_t)gridDim.x * 4;
+    for (int64_t t0 = ((int64_t)blockIdx.x * 4 + wave) * 64; t0 < a.A; t0 += nwv * 64) {
+        const int64_t t = t0 + lane;
+        int64_t eb = 0, ee = 0;
+        bool cand = false;
+        if (t < a.A) {
+            eb = a.inc_off[t];
+            ee = a.inc_off[t + 1];
+            nbytes += 8;
+            if (ee > eb && ee - eb <= kHeavyDegree) {
+                u64 any = 0;
+                for (int w = 0; w < W; ++w) {
+                    const u64 v = ~a.vis[t * W + w];
+                    any |= w == W - 1 ? v & lastmask : v;
+                }
+                nbytes += 8 * W;
+                cand = any != 0;
+            }
+        }
+        for (u64 m = __ballot(cand); m; m &= m - 1) {   // wave-uniform
+            const int l0 = __ffsll((long long)m) - 1;
+            const int32_t tt = (int32_t)(t0 + l0);
+            const int64_t b = __shfl(eb, l0), e = __shfl(ee, l0);
+            if (lane < W) {
+                const u64 v = ~a.vis[(int64_t)tt * W + lane];
+                need[lane] = lane == W - 1 ? v & lastmask : v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            lp_range(a, tt, b, e, best, need, nbytes);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int w = 0; w < W; ++w) {   // the atom's discoveries: a lane per seed
+                const int s = w * 64 + lane;
+                const u64 v = s < nb ? best[s] : ~0ull;
+                const bool isnew = v != ~0ull;
+                if (isnew) best[s] = ~0ull;
+                ls_append(a, d, isnew, (int64_t)s * a.A + tt, v);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    ls_add_bytes(a, nbytes, ws);
+}
+
+// Pull levels: the heavy atoms' rows -> their discoveries (a wave per heavy atom, a lane per seed); the
+// rows go back to ~0.
+__global__ void __launch_bounds__(256) hgx_lp_hfinal(LsArgs a, int32_t d) {
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || !sl[lsPull]) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwv = (int64_t)gridDim.x * 4;
+    for (int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); h < a.n_heavy; h += nwv) {
+        const int32_t t = a.heavy_atom[h];
+        for (int w = 0; w < a.W; ++w) {
+            const int s = w * 64 + lane;
+            u64 v = ~0ull;
+            if (s < a.nb) {
+                v = a.hbest[h * a.nb + s];
+                if (v != ~0ull) a.hbest[h * a.nb + s] = ~0ull;
+            }
+            ls_append(a, d, v != ~0ull, (int64_t)s * a.A + t, v);
+        }
+    }
+}
+
+// A bit per discovery at its key.  Push levels first take the value out of the hash slot and clear the
+// slot; pull levels clear the frontier rows, the union bitmap and the frontier hash.
 __global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
     __shared__ int64_t pre[kLsDSegs + 2];
+    const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
+    const bool pull = sl[lsPull] != 0;
     const int64_t n = ls_disc_prefix(a, d, pre);
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
-        const u64 kk = (a.key[ls_disc_at(a, pre, x)] >> 32) - 1ull;
-        atomicOr(&a.bm[kk >> 6], 1ull << (kk & 63));
+        const int64_t pos = ls_disc_pos(a, pre, x);
+        u64 v = a.dval[pos];
+        if (!pull) {   // v is the hash slot
+            const u64 hs = v;
+            v = a.hval[hs];
+            a.dval[pos] = v;
+            a.hkey[hs] = kLsEmpty;
+            a.hval[hs] = ~0ull;
+        }
+        const u64 kk = (v >> 32) - 1ull;
+        atomicOr((unsigned long long*)&a.bm[kk >> 6], 1ull << (kk & 63));
+    }
+    if (pull) {
+        const int64_t nu = sl[lsU];
+        for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < nu; u += (int64_t)gridDim.x * 256) {
+            const int32_t p = a.ulist[u];
+            for (int w = 0; w < a.W; ++w) a.frow[(int64_t)p * a.W + w] = 0ull;
+            a.ubit[p >> 6] = 0ull;
+        }
+        // the frontier hash: each entry finds its own key (still there: only its owner clears it) and
+        // clears that slot, so the table is empty again after F probes, not a pass over every slot
+        const int64_t F = sl[lsF];
+        const int32_t* fa = a.fa[d & 1];
+        const int32_t* fs = a.fs[d & 1];
+        for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < F; i += (int64_t)gridDim.x * 256) {
+            const u64 key = (u64)(uint32_t)fs[i] << 32 | (u64)(uint32_t)fa[i];
+            u64 h = ls_hash(key, a.fbits);
+            for (int64_t probe = 0; probe <= a.fmask && a.fkey[h] != key; ++probe) h = (h + 1) & (u64)a.fmask;
+            if (a.fkey[h] == key) a.fkey[h] = kLsEmpty;
+        }
     }
 }
 
@@ -2216,8 +2638,9 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
     ls_block_offsets(a.bsum, off, ws);
     const int nx = (d + 1) & 1;
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
-        const int64_t sa = ls_disc_at(a, pre, x);
-        const u64 v = a.key[sa];
+        const int64_t pos = ls_disc_pos(a, pre, x);
+        const int64_t sa = a.disc[pos];
+        const u64 v = a.dval[pos];
         const u64 kk = (v >> 32) - 1ull;
         const int64_t w = (int64_t)(kk >> 6);
         int b = (int)(w * kLsG / W);   // the block whose word range holds w
@@ -2229,14 +2652,14 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
         a.out_atom[out0 + r] = t;
         a.fa[nx][r] = t;
         a.fs[nx][r] = s;
-        a.key[sa] = 0ull;   // examined from now on
+        atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
     }
 }
 
 __global__ void hgx_ls_seed(LsArgs a, int32_t nb, const int32_t* __restrict__ seeds) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nb) {
-        a.key[(int64_t)i * a.A + seeds[i]] = 0ull;   // examined.put(start, TRUE) (:42-46)
+    if (i < nb) {   // examined.put(start, TRUE) (:42-46)
+        atomicOr((unsigned long long*)&a.vis[(int64_t)seeds[i] * a.W + (i >> 6)], 1ull << (i & 63));
         a.fa[0][i] = seeds[i];
         a.fs[0][i] = i;
     }
@@ -2245,6 +2668,28 @@ __global__ void hgx_ls_seed(LsArgs a, int32_t nb, const int32_t* __restrict__ se
         a.ctl[lsOut] = 0;
     }
 }
+
+// pin_j[p] for pin p of link row L = the index of L in inc(tgt_idx[p]) (a binary search of the target's
+// incidence row; a target repeated in L gets its one entry's index at every position)
+__global__ void __launch_bounds__(256) k_pin_j(int64_t M, const int64_t* __restrict__ tgt_off,
+                                               const int32_t* __restrict__ tgt_idx, const int64_t* __restrict__ inc_off,
+                                               const int32_t* __restrict__ inc_row, int32_t* __restrict__ pin_j) {
+    for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < M; L += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = tgt_off[L], e = tgt_off[L + 1];
+        for (int64_t q = b; q < e; ++q) {
+            const int32_t t = tgt_idx[q];
+            int64_t lo = inc_off[t], hi = inc_off[t + 1];
+            const int64_t base = lo;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (inc_row[mid] < (int32_t)L) lo = mid + 1;
+                else hi = mid;
+            }
+            pin_j[q] = (int32_t)(lo - base);
+        }
+    }
+}
+
 
 // Device buffers of one call, given back to the graph's pool at scope exit.
 struct SeqScratch {
@@ -2296,6 +2741,8 @@ struct SeqOut {
     std::vector<PoolBuf> bufs;
     double traversed = 0;
     int32_t deepest = 0;
+    double bytes = 0;                     // the level engine's algorithmic bytes (kernel counters)
+    int64_t pull_levels = 0;              // its levels that ran as pulls
 };
 
 PoolBuf take_host_buf(hgx_graph* g, size_t bytes);
@@ -2506,15 +2953,49 @@ PoolBuf take_host_buf(hgx_graph* g, size_t bytes) {
     return PoolBuf{p, bytes};
 }
 
-// The level-synchronous engine (hgx_ls_* kernels) over a chunk of seeds; false when a capacity it
-// cannot grow was exceeded (level keys wider than 32 bits): the caller then runs the key-array engine.
+// pin_j of the snapshot (built on first use on the snapshot, shared by its contexts, dropped by
+// hgx_graph_update with the other derived tables); caller holds g->mu.
+const int32_t* ensure_pin_j(hgx_graph* g) {
+    hgx_graph* root = g->base ? g->base : g;
+    std::lock_guard<std::mutex> lk(root->ylist_mu);
+    if (!root->pin_j && root->P > 0) {
+        int32_t* pj = nullptr;
+        HGX_HIP(hipMalloc(&pj, sizeof(int32_t) * (size_t)root->P));
+        k_pin_j<<<grid_for(root->M, 256, 16384), 256, 0, g->stream>>>(root->M, root->tgt_off, root->tgt_idx,
+                                                                     root->inc_off, root->inc_row, pj);
+        HGX_CHECK_LAUNCH();
+        HGX_HIP(hipStreamSynchronize(g->stream));
+        root->pin_j = pj;
+    }
+    return root->pin_j;
+}
+
+int log2_ceil(int64_t x) {
+    int b = 0;
+    while (((int64_t)1 << b) < x) ++b;
+    return b;
+}
+
+// The level-synchronous engine (hgx_ls_* / hgx_lp_* kernels) over a chunk of <= 1024 seeds; false when
+// a level's keys do not fit 32 bits (the caller splits the chunk).  Capacities start small, grow x4 on
+// overflow and are kept on the graph.
 bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t maxd, const hgx_algen_opts& o,
                        SeqOut& out, int64_t seed0) {
     hipStream_t st = g->stream;
     const int64_t A = g->A;
     const int mode = seq_mode(o);
-    const YieldAdj* ya = stage_yield_adj(g, mode, o);   // an adjacency pair's index is its whole stream position
+    // pull levels (HGX_LS_PULL: 0 never, 1 by the level's width (default), 2 every level -- tests) read
+    // the incidence items; with the yield adjacency the items are its pairs and every level pushes
+    // (forced pulls drop the adjacency, so the tests reach the pull in every generator mode)
+    const char* pe = std::getenv("HGX_LS_PULL");
+    const int pull_env = pe ? std::min(2, std::max(0, std::atoi(pe))) : 1;
+    const YieldAdj* ya = pull_env == 2 ? nullptr : stage_yield_adj(g, mode, o);   // a pair's index is its stream position
     const int kbits = ya ? 0 : bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
+    const int32_t W = (nb + 63) / 64;
+    if (W > kLsMaxW) fail(HGX_E_INVALID, "hgx_bfs_sequence: a level-engine chunk holds at most 1024 seeds");
+    const int pull = ya ? 0 : pull_env;
+    const int32_t* pin_j = pull ? ensure_pin_j(g) : nullptr;
+    hgx_graph* root = g->base ? g->base : g;
     if (!g->seq_flag) {   // mapped, coherent: the emit kernel's level sizes (once per graph)
         void* hp = nullptr;
         HGX_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2532,6 +3013,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         const int64_t wcap = std::max<int64_t>(g->ls_wcap, small ? 16 : (int64_t)1 << 18);
         const int64_t tcap = std::max<int64_t>(g->ls_tcap, small ? 8 : (int64_t)1 << 16);
         const int64_t rcap = std::max<int64_t>(g->ls_rcap, small ? 4 : (int64_t)1 << 14);
+        const int hbits = std::max<int>(log2_ceil(std::max<int64_t>(g->ls_hcap, small ? 64 : (int64_t)1 << 21)), 6);
+        const int fbits = std::max<int>(log2_ceil(std::max<int64_t>(g->ls_fcap, small ? 64 : (int64_t)1 << 16)), 6);
         LsArgs a{};
         a.A = A;
         a.inc_off = g->inc_off;
@@ -2552,13 +3035,17 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.rev = o.reverse_order ? 1 : 0;
         a.kbits = kbits;
         a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
+        if (const char* tl = std::getenv("HGX_LS_TLIMIT")) a.t_limit = std::min<int64_t>(a.t_limit, std::atoll(tl));   // tests
+        a.nb = nb;
+        a.W = W;
         a.cap = cap;
         a.wcap = wcap;
         a.tcap = tcap;
         a.rcap = rcap;
         a.hflag = hflag_d;
         SeqScratch w{g, {}};
-        a.key = (u64*)w.take(sizeof(u64) * (size_t)full);
+        const size_t rows = sizeof(u64) * (size_t)A * (size_t)W;
+        a.vis = (u64*)w.take(rows);
         a.ctl = (int64_t*)w.take(sizeof(int64_t) * kLsCtlWords);
         for (int k = 0; k < 2; ++k) {
             a.fa[k] = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
@@ -2570,27 +3057,64 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.tile = (int64_t*)w.take(sizeof(int64_t) * (size_t)tcap);
         a.bsum = (int64_t*)w.take(sizeof(int64_t) * kLsG);
         a.segcap = cap / (2 * kLsDSegs);   // the segments (half of cap), then an overflow region of cap
-        a.disc = (int64_t*)w.take(sizeof(int64_t) * (size_t)(cap + kLsDSegs * a.segcap));
+        const size_t nd = (size_t)(cap + kLsDSegs * a.segcap);
+        a.disc = (int64_t*)w.take(sizeof(int64_t) * nd);
+        a.dval = (u64*)w.take(sizeof(u64) * nd);
         a.bm = (u64*)w.take(sizeof(u64) * (size_t)wcap);
         a.wpre = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)wcap);
         a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
         a.out_atom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
         a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
+        a.hbits = hbits;
+        a.hmask = ((int64_t)1 << hbits) - 1;
+        a.hkey = (u64*)w.take(sizeof(u64) << hbits);
+        a.hval = (u64*)w.take(sizeof(u64) << hbits);
+        a.pull = pull;
+        a.I = g->I;
+        a.pin_j = pin_j;
+        if (pull) {
+            a.frow = (u64*)w.take(rows);
+            a.ubit = (u64*)w.take(sizeof(u64) * (size_t)(A / 64 + 1));
+            a.ulist = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
+            a.fbits = fbits;
+            a.fmask = ((int64_t)1 << fbits) - 1;
+            a.fkey = (u64*)w.take(sizeof(u64) << fbits);
+            a.fpre = (uint32_t*)w.take(sizeof(uint32_t) << fbits);
+            a.chunks = root->chunks;
+            a.n_chunks = root->n_chunks;
+            a.n_heavy = root->n_heavy;
+            a.heavy_atom = root->heavy_atom;
+            a.hbest = (u64*)w.take(sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1));
+            HGX_HIP(hipMemsetAsync(a.frow, 0, rows, st));
+            HGX_HIP(hipMemsetAsync(a.ubit, 0, sizeof(u64) * (size_t)(A / 64 + 1), st));
+            HGX_HIP(hipMemsetAsync(a.fkey, 0xFF, sizeof(u64) << fbits, st));
+            HGX_HIP(hipMemsetAsync(a.hbest, 0xFF, sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1), st));
+        }
         int32_t* dseeds = (int32_t*)w.take(sizeof(int32_t) * (size_t)nb);
         int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)nb);
         std::memcpy(hs, seeds, sizeof(int32_t) * (size_t)nb);
         HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)nb, hipMemcpyHostToDevice, st));
-        HGX_HIP(hipMemsetAsync(a.key, 0xFF, sizeof(u64) * (size_t)full, st));
+        // the examined rows (A x W words: 400 MB for config 2's 64 seeds, where the round-4 key array
+        // was 64 x A x 8 = 25.6 GB) and the push hash start empty; every per-level table is cleared by
+        // the level itself
+        HGX_HIP(hipMemsetAsync(a.vis, 0, rows, st));
+        HGX_HIP(hipMemsetAsync(a.hkey, 0xFF, sizeof(u64) << hbits, st));
+        HGX_HIP(hipMemsetAsync(a.hval, 0xFF, sizeof(u64) << hbits, st));
         HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(int64_t) * kLsCtlWords, st));
         hgx_ls_seed<<<grid_for(nb, 256), 256, 0, st>>>(a, nb, dseeds);
         HGX_CHECK_LAUNCH();
         const u64 base = g->seq_flag_seq;
+        const size_t lp_smem = sizeof(u64) * 4 * (size_t)nb;
         auto enqueue = [&](int32_t d) {
             // grids: thousands of idle workgroups cost ~10 us a launch on small levels;
-            // the expand's tiles are the only work that needs more than a block per CU
+            // the expand's tiles and the pull's atoms are the work that needs more than a block per CU
             hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d, 0);
             hgx_ls_prefix<<<kLsG, 256, 0, st>>>(a, d);
             hgx_ls_expand<<<1024, 256, 0, st>>>(a, d);
+            if (pull) {
+                hgx_lp_pull<<<2048, 256, lp_smem, st>>>(a, d);
+                hgx_lp_hfinal<<<256, 256, 0, st>>>(a, d);
+            }
             hgx_ls_bits<<<512, 256, 0, st>>>(a, d);
             hgx_ls_wprefix<<<kLsG, 256, 0, st>>>(a, d);
             hgx_ls_emit<<<512, 256, 0, st>>>(a, d, base + (u64)d + 1);
@@ -2631,16 +3155,20 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         spin_sync(st);
         status |= ctl[kLsStatus];
         if (status) {
-            if (status & 16) return false;   // 32-bit level keys do not fit
+            if (status & 16) return false;   // 32-bit level keys do not fit: the caller splits the chunk
             if (attempt > 16) fail(HGX_E_DEVICE, "hgx_bfs_sequence: level-synchronous capacities did not converge");
             if (status & 1) g->ls_cap = std::min(full, cap * 4);
             if (status & 2) g->ls_rcap = rcap * 4;
             if (status & 4) g->ls_wcap = wcap * 4;
             if (status & 8) g->ls_tcap = tcap * 4;
+            if (status & 32) g->ls_hcap = ((int64_t)1 << hbits) * 4;
+            if (status & 64) g->ls_fcap = ((int64_t)1 << fbits) * 4;
             continue;   // rerun the chunk with the grown capacities (kept on the graph)
         }
         const int64_t nruns = ctl[kLsRuns];
         out.traversed += (double)ctl[kLsTrav];
+        out.bytes += (double)ctl[kLsBytes];
+        out.pull_levels += ctl[kLsPullN];
         // [links total][atoms total][pad to 8 bytes][runs 3 x nruns]
         PoolBuf hb = take_host_buf(g, 8 * (size_t)total + 8 + 24 * (size_t)std::max<int64_t>(nruns, 1));
         out.bufs.push_back(hb);
@@ -2684,8 +3212,10 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     }
 }
 
-// The level-synchronous engines over any number of seeds: chunks whose key arrays fit the budget,
-// hgx_ls_* first, the key-array engine (seq_levels) for a chunk whose level keys exceed 32 bits.
+// The level-synchronous engine over any number of seeds: chunks of <= 1024 seeds; a chunk whose level
+// keys do not fit 32 bits is split in halves (its item space shrinks with its seeds), and a single seed
+// that still does not fit runs on the round-1 key-array engine (seq_levels: 64-bit keys, a rocPRIM sort
+// a level).
 void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t maxd, const hgx_algen_opts& o,
                     SeqOut& out, bool v2) {
     if (!v2) {
@@ -2695,20 +3225,31 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
     out.segs.assign((size_t)n_seeds, {});
     const int64_t A = std::max<int64_t>(g->A, 1);
     int64_t B = std::max<int64_t>(1, std::min<int64_t>(n_seeds, 1024));
-    while (B > 1 && B * A * 24 > g->seq_budget_bytes) B = (B + 1) / 2;
-    for (int64_t c0 = 0; c0 < n_seeds; c0 += B) {
-        const int32_t nb = (int32_t)std::min<int64_t>(B, n_seeds - c0);
-        if (!seq_levels2_chunk(g, seeds + c0, nb, maxd, o, out, c0)) {
-            SeqOut one;
-            seq_levels(g, seeds + c0, nb, maxd, o, one);
-            out.traversed += one.traversed;
-            out.deepest = std::max(out.deepest, one.deepest);
-            for (int32_t s = 0; s < nb; ++s) out.segs[(size_t)(c0 + s)] = std::move(one.segs[s]);
-            for (auto& b : one.bufs) out.bufs.push_back(b);
-            one.bufs.clear();
+    // the chunk's examined + frontier rows: 16 bytes per atom and 64 seeds
+    while (B > 64 && 16 * A * ((B + 63) / 64) > g->seq_budget_bytes / 2) B = (B + 1) / 2;
+    std::vector<std::pair<int64_t, int32_t>> work;   // (first seed, seeds), processed in seed order
+    for (int64_t c0 = n_seeds - (n_seeds - 1) % B - 1; n_seeds > 0 && c0 >= 0; c0 -= B)
+        work.push_back({c0, (int32_t)std::min<int64_t>(B, n_seeds - c0)});
+    while (!work.empty()) {
+        const auto [c0, nb] = work.back();
+        work.pop_back();
+        if (seq_levels2_chunk(g, seeds + c0, nb, maxd, o, out, c0)) continue;
+        if (nb > 1) {   // the second half after the first
+            const int32_t h = nb / 2;
+            work.push_back({c0 + h, nb - h});
+            work.push_back({c0, h});
+            continue;
         }
+        SeqOut one;
+        seq_levels(g, seeds + c0, 1, maxd, o, one);
+        out.traversed += one.traversed;
+        out.deepest = std::max(out.deepest, one.deepest);
+        out.segs[(size_t)c0] = std::move(one.segs[0]);
+        for (auto& b : one.bufs) out.bufs.push_back(b);
+        one.bufs.clear();
     }
 }
+
 
 // ---- the multi-workgroup stage, host side ----
 
@@ -2791,8 +3332,10 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     r.m_blk = r.m_lev + (size_t)(kcap + 2) * kCoMaxLevels;
     r.hb = take_host_buf(g, sizeof(int64_t) * (r.m_blk + kCoMaxBlocks));
     r.hm = (int64_t*)r.hb.p;
-    r.hm[0] = -1;
+    r.hm[0] = -1;   // written once, at the normal exit of block 0
+    r.hm[1] = 0;
     r.hm[2] = k;
+    r.hm[3] = 0;    // set by any block that timed out on a grid barrier
     void* hmd = nullptr;
     HGX_HIP(hipHostGetDevicePointer(&hmd, r.hm, 0));
     CoArgs& a = r.a;
@@ -2830,7 +3373,14 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.lvl_end = (int64_t*)hmd + r.m_lev;
     a.lvl_trace = a.lvl_end + (size_t)kcap * kCoMaxLevels;
     a.blk_bytes = (int64_t*)hmd + r.m_blk;
+    const char* to_s = std::getenv("HGX_CO_TIMEOUT");   // read per launch (tests toggle it)
+    const long long to_env = to_s ? std::atoll(to_s) : 0;
+    a.timeout = to_env > 0 ? (u64)to_env : kCoTimeout;   // tests force the timeout path with a few ticks
 }
+
+// A launch finished cleanly: block 0 left the level loop normally with both status words clear, and no
+// block timed out on a barrier.
+bool co_clean(const CoRun& r) { return r.hm[0] == 0 && r.hm[3] == 0; }
 
 void co_launch(hgx_graph* g, CoRun& r) {
     if (co_threads() == 512) hgx_bfs_coop<512><<<(unsigned)g->co_ok, 512, 0, g->stream>>>(r.a);
@@ -2889,7 +3439,8 @@ void co_collect(hgx_graph* g, CoRun& r, const std::vector<int32_t>& sidx, BlockS
 bool co_failed(hgx_graph* g, CoRun& r, bool may_grow) {
     const int64_t vwords = g->A / 64 + 1;
     HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), g->stream));
-    if (r.hm[0] != 2 || !may_grow) return false;
+    if (r.hm[3] != 0) ++g->co_timeouts;   // a barrier timed out: the rows engine takes the seeds
+    if (r.hm[0] != 2 || r.hm[3] != 0 || !may_grow) return false;
     int64_t most = 0;
     for (int q = 0; q < kCoSegs; ++q) most = std::max(most, r.hm[r.m_seg + q]);
     g->co_pcap = std::max<int64_t>(2 * r.pcap, kCoSegs * (most + most / 4 + 64));
@@ -2930,7 +3481,7 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             ev_give(g, ev[0]);
             ev_give(g, ev[1]);
         }
-        if (r.hm[0] == 0) {
+        if (co_clean(r)) {
             co_collect(g, r, sidx, out);
             return true;
         }
@@ -2944,6 +3495,13 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
 void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
                BlockSet& out) {
     hipStream_t st = g->stream;
+    const int64_t timeouts0 = g->co_timeouts;
+    struct Fallbacks {   // the call's grid launches that fell back (counted by co_failed)
+        hgx_graph* g;
+        int64_t t0;
+        BlockSet& out;
+        ~Fallbacks() { out.co_fallbacks = (int32_t)(g->co_timeouts - t0); }
+    } fb{g, timeouts0, out};
     const int mode = seq_mode(o);
     if (mode != sSym) ensure_inc_yield(g);
     out.seeds.assign(seeds, seeds + n_seeds);
@@ -3059,7 +3617,7 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
                                      std::to_string(out.rerun.size()) + " handed-over seeds");
         if (nsel == 0 || nsel > kMaxCoSeeds) return;   // none, or more than fit: the rows engine
         std::vector<int32_t> sidx(cr->hm + cr->m_sel, cr->hm + cr->m_sel + nsel);   // the slots' order
-        if (cr->hm[0] == 0) {
+        if (co_clean(*cr)) {
             co_collect(g, *cr, sidx, out);
             out.n_coop = (int32_t)nsel;
             out.rerun.clear();
@@ -3078,6 +3636,8 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
 
 void free_yield_lists(hgx_graph* g) {
     std::lock_guard<std::mutex> lk(g->ylist_mu);
+    if (g->pin_j && !g->base) (void)hipFree(g->pin_j);   // the level engine's pin index (the incidence changed)
+    g->pin_j = nullptr;
     for (YieldList& y : g->ylists) {
         (void)hipFree(y.off);
         (void)hipFree(y.row);
@@ -3237,6 +3797,7 @@ struct hgx_seq_result {
     hgx_graph* g = nullptr;
     double ms_total = 0, traversed = 0;
     double ms_block = 0, bytes_block = 0;   // the workgroup engine's launches: device ms, algorithmic bytes
+    double ms_level = 0;                    // the level-synchronous engine: device ms (timing on) ...
     int32_t n_block = 0, n_level = 0;       // seeds finished by each engine
     ~hgx_seq_result() {
         if (!g) return;
@@ -3402,7 +3963,22 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     if (!rerun.empty()) {
         std::vector<int32_t> rs(rerun.size());
         for (size_t k = 0; k < rerun.size(); ++k) rs[k] = seeds[rerun[k]];
+        hipEvent_t el0 = nullptr, el1 = nullptr;
+        if (g->timing) {
+            el0 = ev_take(g);
+            el1 = ev_take(g);
+            HGX_HIP(hipEventRecord(el0, st));
+        }
         seq_levels_all(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev, g->seq_engine != 1);
+        if (el0) {
+            HGX_HIP(hipEventRecord(el1, st));
+            HGX_HIP(hipEventSynchronize(el1));
+            float ms = 0;
+            HGX_HIP(hipEventElapsedTime(&ms, el0, el1));
+            r->ms_level = ms;
+            ev_give(g, el0);
+            ev_give(g, el1);
+        }
         r->traversed += r->lev.traversed;
         deepest = std::max(deepest, r->lev.deepest);
         for (size_t k = 0; k < rerun.size(); ++k) {
@@ -3539,6 +4115,15 @@ int hgx_seq_result_engine_stats(const hgx_seq_result* r, int32_t* n_block, int32
     if (n_level) *n_level = r->n_level;
     if (ms_block) *ms_block = r->ms_block;
     if (bytes_block) *bytes_block = r->bytes_block;
+    HGX_API_END
+}
+
+int hgx_seq_result_level_stats(const hgx_seq_result* r, double* ms_level, double* bytes_level, int64_t* pull_levels) {
+    HGX_API_BEGIN
+    if (!r) fail(HGX_E_INVALID, "null result");
+    if (ms_level) *ms_level = r->ms_level;
+    if (bytes_level) *bytes_level = r->lev.bytes;
+    if (pull_levels) *pull_levels = r->lev.pull_levels;
     HGX_API_END
 }
 

@@ -149,6 +149,9 @@ typedef struct hgx_bfs_stats {
     double  ms_coop;
     double  bytes_coop;
     int64_t block_coop;
+    /* multi-workgroup launches whose grid barrier timed out (their workgroups were not all resident
+     * within the limit): the bitmaps were cleared and the seeds ran on the rows engine instead */
+    int64_t coop_fallbacks;
 } hgx_bfs_stats;
 
 const char *hgx_version(void);
@@ -235,6 +238,9 @@ typedef struct hgx_snapshot_writer hgx_snapshot_writer;
 int  hgx_snapshot_writer_begin(const char *path, const hgx_graph_desc *desc, int32_t handle_bytes,
                                hgx_snapshot_writer **out);
 int  hgx_snapshot_writer_handles(hgx_snapshot_writer *w, const uint8_t *handles, int64_t n_ranks);
+/* The writer's handle width (begin's handle_bytes): a binding that receives a byte array sizes the
+ * rank count from this, not from a width the caller passes again. */
+int  hgx_snapshot_writer_handle_bytes(const hgx_snapshot_writer *w, int32_t *handle_bytes);
 int  hgx_snapshot_writer_end(hgx_snapshot_writer *w);   /* frees w */
 void hgx_snapshot_writer_abort(hgx_snapshot_writer *w);
 /* Header fields without reading the sections (any output may be NULL). */
@@ -246,7 +252,9 @@ int hgx_snapshot_read(const char *path, int32_t *link_atom, int64_t *tgt_off, in
                       int32_t *link_type, uint8_t *handles);
 /* Handles of ranks [first_rank, first_rank + n) (n * handle_bytes bytes) from the file's handle table,
  * for readers that cannot hold the whole table at once (a Java byte[] stops at 2^31 bytes: 134M
- * 16-byte UUID handles).  verify = 1 also checks the whole file's checksum (once, on the first range);
+ * 16-byte UUID handles).  verify = 1 also checks the whole file's checksum -- on EVERY call made with it
+ * (the call keeps no state), so a paged reader verifies once (the first range, or hgx_graph_open / the
+ * JNI snapshotVerify) and reads the other ranges with verify = 0;
  * HGX_E_NOTFOUND when the file has no handle table, HGX_E_INVALID for ranks outside [0, num_atoms). */
 int hgx_snapshot_read_handles(const char *path, int64_t first_rank, int64_t n, int32_t verify, uint8_t *out);
 /* Map + verify the file and build the device snapshot (as hgx_graph_create). */
@@ -318,6 +326,13 @@ int  hgx_seq_result_stats(const hgx_seq_result *r, double *ms_total, double *tra
  * pairs written).  Any output may be NULL. */
 int  hgx_seq_result_engine_stats(const hgx_seq_result *r, int32_t *n_block, int32_t *n_level, double *ms_block,
                                  double *bytes_block);
+/* The level-synchronous engine's part of the call (the seeds the workgroup engine handed over):
+ * device ms from its first operation to its last (timing enabled; it includes the pairs' copy to the
+ * host), its algorithmic bytes (kernel counters: per item its entry, row, type, target offsets and
+ * targets, per yield the examined word and the hash slot; per pulled atom its incidence range, examined
+ * row, entries, link rows, union bits, frontier rows, pin indices and hash probes; the frontier
+ * entries of the pull tables), and how many of its levels ran as pulls.  Any output may be NULL. */
+int  hgx_seq_result_level_stats(const hgx_seq_result *r, double *ms_level, double *bytes_level, int64_t *pull_levels);
 void hgx_seq_result_free(hgx_seq_result *r);
 /* Batched conjunctive pattern queries.  Result of query q = the link atoms L with
  * type(L) == type, every incident/pattern anchor in targets(L) and

@@ -405,12 +405,23 @@ JNIEXPORT void JFN(snapshotWriterHandles)(JNIEnv *e, jclass k, jlong w, jbyteArr
     pin_t hb = pin_byte(e, handles);
     if (pin_failed(&hb)) return;
     int rc = HGX_OK, ok = 1;
-    if (hb.n % handleBytes) {
+    int32_t width = 0;   /* the writer's own width sizes the read, not the caller's */
+    rc = hgx_snapshot_writer_handle_bytes((const hgx_snapshot_writer *)(intptr_t)w, &width);
+    if (rc) {
+        unpin(e, &hb);
+        throw_rc(e, rc);
+        return;
+    }
+    if (width != handleBytes) {
+        throw_msg(e, "snapshotWriterHandles: handleBytes differs from the writer's handle width");
+        ok = 0;
+    }
+    if (ok && hb.n % width) {
         throw_msg(e, "snapshotWriterHandles: not a whole number of handles");
         ok = 0;
     }
     if (ok) rc = hgx_snapshot_writer_handles((hgx_snapshot_writer *)(intptr_t)w, (const uint8_t *)hb.p,
-                                             (int64_t)hb.n / handleBytes);
+                                             (int64_t)hb.n / width);
     unpin(e, &hb);
     if (ok && rc) throw_rc(e, rc);
 }
@@ -892,10 +903,12 @@ JNIEXPORT jarray JFN(seqStats)(JNIEnv *e, jclass k, jlong sq) {
 
 JNIEXPORT jlongArray JFN(seqEngineStats)(JNIEnv *e, jclass k, jlong sq) {
     int32_t nb = 0, nl = 0;
+    int64_t pl = 0;
     int rc = hgx_seq_result_engine_stats((const hgx_seq_result *)(intptr_t)sq, &nb, &nl, NULL, NULL);
+    if (!rc) rc = hgx_seq_result_level_stats((const hgx_seq_result *)(intptr_t)sq, NULL, NULL, &pl);
     if (rc) { throw_rc(e, rc); return NULL; }
-    int64_t v[2] = {nb, nl};
-    return new_longs(e, v, 2);
+    int64_t v[3] = {nb, nl, pl};
+    return new_longs(e, v, 3);
 }
 
 JNIEXPORT jarray JFN(queryMs)(JNIEnv *e, jclass k, jlong q) {

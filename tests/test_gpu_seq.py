@@ -219,3 +219,83 @@ def test_level_engine_capacity_growth_and_depth_limits():
         snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
     finally:
         del os.environ["HGX_LS_SMALL"]
+
+
+def _seq_env(snap, seeds, maxd, g_, env):
+    """hgx_bfs_sequence on the level-synchronous engine alone (HGX_OPT_SEQ_ENGINE 2) under env vars."""
+    from hypergraphdb_amd import _lib, bfs_sequence
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
+    try:
+        return bfs_sequence(snap, seeds, maxd, g_)
+    finally:
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_level_engine_pull_and_push_levels_agree(case):
+    """Round 5: the level engine without a per-seed key array.  Every level pushed (HGX_LS_PULL 0: the
+    level hash), every level pulled (2: frontier rows, union bitmap, pin index, per-seed minima in LDS;
+    heavy atoms by 4096-entry chunks), and the default choice by width (1) give the oracle's exact
+    sequences -- links, atoms, distances, traversed items -- in every generator mode, with typed links,
+    links targeting links, repeated targets, duplicate seeds, > 64 seeds (several row words) and hubs
+    above 512 incidences (the pull's heavy chunks); starting capacities tiny (HGX_LS_SMALL) in case 4."""
+    from hypergraphdb_amd import synth
+    rng = np.random.default_rng(950 + case)
+    if case < 2:
+        g = K.random_graph(rng, int(rng.integers(800, 2500)), int(rng.integers(1500, 3000)), max_arity=9,
+                           link_targets=case == 0, n_types=3)
+    else:
+        g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=60 + case)
+    snap, orc = snapshot(g), oracle(g)
+    n_seeds = [40, 70, 130, 64, 300][case]
+    seeds = rng.integers(0, g["num_atoms"], n_seeds).astype(np.int32)
+    seeds[-1] = seeds[0]
+    extra = {"HGX_LS_SMALL": 1} if case == 4 else {}
+    pulled = 0
+    for mi, mode in enumerate(K.ALGEN_MODES):
+        if case >= 2 and mi % 3:
+            continue
+        lt = [-1, 0, 1][(mi + case) % 3]
+        for maxd in ((None, 2) if case != 3 else (3,)):
+            outs = {}
+            for pull in (0, 2, 1):
+                outs[pull] = _seq_env(snap, seeds, maxd, gen(snap, mode, lt), dict(extra, HGX_LS_PULL=pull))
+            a = outs[0]
+            for pull in (2, 1):
+                b = outs[pull]
+                assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd, pull)
+                assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd, pull)
+                assert np.array_equal(a.dists, b.dists) and a.traversed_edges == b.traversed_edges, (case, mi, maxd)
+            assert outs[0].pull_levels == 0 and outs[2].pull_levels >= 1, (outs[0].pull_levels, outs[2].pull_levels)
+            pulled += outs[2].pull_levels
+            for i in range(0, n_seeds, max(1, n_seeds // 6)):
+                l_, at, d, _ = orc.bfs(int(seeds[i]), -1 if maxd is None else maxd, algen(lt, *mode))
+                gl, ga, gd = a.pairs(i)
+                assert np.array_equal(ga, at) and np.array_equal(gl, l_) and np.array_equal(gd, d), (case, mi, maxd, i)
+    assert pulled > 0
+    snap.close()
+
+
+def test_level_engine_chunk_split_on_wide_keys():
+    """A level whose stream keys do not fit 32 bits splits the chunk (HGX_LS_TLIMIT lowers the limit to
+    force it down to single seeds; a single seed that still does not fit runs on the key-array engine):
+    the sequences stay the oracle's."""
+    from hypergraphdb_amd import synth
+    g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=61)
+    snap, orc = snapshot(g), oracle(g)
+    deg = np.bincount(np.asarray(g["tgt_idx"]), minlength=g["num_atoms"])
+    seeds = np.concatenate([np.argsort(-deg)[:4], np.arange(100, 120)]).astype(np.int32)
+    for lim in (2000, 200000):
+        res = _seq_env(snap, seeds, 3, gen(snap, K.ALGEN_MODES[0]), {"HGX_LS_TLIMIT": lim})
+        for i in range(len(seeds)):
+            l_, at, d, _ = orc.bfs(int(seeds[i]), 3)
+            gl, ga, gd = res.pairs(i)
+            assert np.array_equal(ga, at) and np.array_equal(gl, l_) and np.array_equal(gd, d), (lim, i)
+    snap.close()

@@ -34,8 +34,9 @@ def main():
             ref = (n, r.traversed_edges, r.atoms[:1000].copy())
         else:
             assert n == ref[0] and r.traversed_edges == ref[1] and np.array_equal(r.atoms[:1000], ref[2])
-        print(f"call {i}: wall {wall:.1f} ms, device {r.ms_total:.1f} ms, pairs {n}, traversed {r.traversed_edges:.3e}",
-              flush=True)
+        print(f"call {i}: wall {wall:.1f} ms, device {r.ms_total:.1f} ms (level engine {r.ms_level:.1f} ms, "
+              f"{r.bytes_level / 1e9:.2f} GB algorithmic, {r.pull_levels} pull levels), pairs {n}, "
+              f"traversed {r.traversed_edges:.3e}", flush=True)
         del r
     snap.close()
 
