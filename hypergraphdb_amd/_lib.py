@@ -44,7 +44,7 @@ EXPORTED = (
     "hgx_graph_degree", "hgx_graph_incidence", "hgx_set_timing", "hgx_set_option", "hgx_bfs_batch", "hgx_bfs_result_info",
     "hgx_bfs_result_counts", "hgx_bfs_result_visited", "hgx_bfs_result_depth_of", "hgx_bfs_result_stats",
     "hgx_bfs_result_free", "hgx_bfs_sequence", "hgx_seq_result_info", "hgx_seq_result_offsets", "hgx_seq_result_pairs",
-    "hgx_seq_result_stats", "hgx_seq_result_engine_stats", "hgx_seq_result_level_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_pattern_batch_ext", "hgx_query_result_count", "hgx_query_result_offsets", "hgx_query_result_ids",
+    "hgx_seq_result_stats", "hgx_seq_result_engine_stats", "hgx_seq_result_level_stats", "hgx_seq_result_grid_stats", "hgx_seq_result_free", "hgx_pattern_batch", "hgx_pattern_batch_packed", "hgx_pattern_batch_ext", "hgx_query_result_count", "hgx_query_result_offsets", "hgx_query_result_ids",
     "hgx_query_result_ms", "hgx_query_result_free",
     "hgx_partition_plan", "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_exchange_tables",
     "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
@@ -170,6 +170,7 @@ def lib():
         "hgx_seq_result_engine_stats": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(C.c_double),
                                          C.POINTER(C.c_double)], C.c_int),
         "hgx_seq_result_level_stats": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)], C.c_int),
+        "hgx_seq_result_grid_stats": ([vp, C.POINTER(i32), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         "hgx_seq_result_free": ([vp], None),
         "hgx_pattern_batch": ([vp, C.POINTER(AndQuery), i32, C.POINTER(vp)], C.c_int),
         "hgx_pattern_batch_packed": ([vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], C.c_int),

@@ -170,6 +170,10 @@ class SequenceResult:
             check(lib().hgx_seq_result_level_stats(handle, C.byref(ml), C.byref(bl), C.byref(pl)))
             # the level-synchronous engine: device ms, algorithmic bytes, levels that ran as pulls
             self.ms_level, self.bytes_level, self.pull_levels = ml.value, bl.value, pl.value
+            nc, mc, bc = C.c_int32(), C.c_double(), C.c_double()
+            check(lib().hgx_seq_result_grid_stats(handle, C.byref(nc), C.byref(mc), C.byref(bc)))
+            # the order-exact grid stage: seeds it finished, device ms, algorithmic bytes
+            self.n_coop, self.ms_coop, self.bytes_coop = nc.value, mc.value, bc.value
         finally:
             lib().hgx_seq_result_free(handle)
 

@@ -245,6 +245,8 @@ struct hgx_graph {
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
     int64_t co_timeouts = 0;                        //   launches whose grid barrier timed out (seeds fell back)
+    int32_t sc_ok = -1;                             // order-exact grid stage (hgx_seq_coop): its grid (0: does not fit)
+    int64_t sc_pcap = 0;                            //   its pair capacity (grown on demand)
     std::deque<hgx::YieldList> ylists;              // yield lists (snapshot only; contexts read their base's)
     std::deque<hgx::YieldAdj> yadjs;                // yield adjacencies (likewise)
     std::mutex ylist_mu;

@@ -2691,6 +2691,483 @@ __global__ void __launch_bounds__(256) k_pin_j(int64_t M, const int64_t* __restr
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// Order-exact multi-workgroup stage (hgx_seq_coop; round 5): the <= 64 seeds the
+// order-exact workgroup engine (hgx_seq_block) hands back -- config 5's six big hg.subsumed closures,
+// 2K-101K pairs over 21 levels -- in ONE persistent launch of resident workgroups instead of the level
+// engine's launches per level.  Items are yield-adjacency pairs (the generator's (target, link) output in
+// stream order, so an item's index IS its stream position and the key needs no yield rank).  A level is
+// three phases separated by the light grid barrier (co_barrier_lite; every cross-workgroup access is an
+// agent-scope atomic or co_put / co_get, [xwg] below):
+//   P1 expand   work items (a frontier entry's pairs, <= kScChunk each, carrying the entry's first item
+//               index) -> every pair (t, link) of seed s with t not examined: the level hash keyed by
+//               (s, t) keeps the minimum of ((it + 1) << 32 | link); the first claimer appends (t, s, slot)
+//               to its block's discovery segment (HGBreadthFirstTraversal.java:56-64)
+//   P2 finalise every discovery x: its value from the hash slot (which it clears), a bit at its key
+//               (= the item index) in the level's key-space bitmap, its adjacency degree added to its
+//               key's word and stored at its key, key -> x, and the examined bit
+//   P3 emit     every workgroup scans the bitmap words' popcounts and degree sums in LDS; a wave per
+//               non-empty word, a lane per key: rank = popcount below the key (the level's FIFO order),
+//               first item index of the new frontier entry = degree prefix below it (a wave scan);
+//               pair `rank` of the level, the next level's work items, per-seed pair counts
+// The key space of a level is its item count T (<= kScKeyCap, else the seeds go to the level engine).
+constexpr int kScChunk = 64;                       // adjacency pairs per work item
+constexpr int64_t kScKeyCap = (int64_t)1 << 18;    // keys (items) of one level: an LDS prefix of 4096 words
+constexpr int kScWords = (int)(kScKeyCap / 64);
+constexpr int kScProbes = 64;
+// ctl words: [0] barrier, [kScSt .. +1] status by phase parity, [kScSt + 2] sticky status, [kScItm + p*kCoSegs +
+// seg] work-item counters (parity p), [kScDis + p*kCoSegs + seg] discovery counters, then lcnt [kCoMaxLevels x 64]
+constexpr int kScSt = 4, kScItm = 8, kScDis = kScItm + 2 * kCoSegs, kScLcnt = kScDis + 2 * kCoSegs;
+constexpr int64_t kScCtlWords = kScLcnt + (int64_t)kCoMaxLevels * 64;
+
+struct ScArgs {
+    int32_t k;                                       // seeds (<= kMaxCoSeeds)
+    const int32_t* seeds;                            // device [k]
+    int64_t A;
+    const int64_t* inc_off;                          // traversed items: incidence entries of expanded atoms
+    const int64_t* y_off;                            // the yield adjacency
+    const int32_t* a_tgt;
+    const int32_t* a_lnk;
+    int32_t maxd;
+    int64_t vwords;
+    u64* vis;                                        // [k * vwords] examined bitmaps (zero between calls)
+    u64* hkey;                                       // level hash (hmask + 1 slots, empty between levels)
+    u64* hval;
+    int64_t hmask;
+    int32_t hbits;
+    int4* dseg;                                      // discoveries: kCoSegs segments of dcap entries (t, s, slot lo, hi)
+    int64_t dcap;
+    int2* dflat;                                     // [kScKeyCap] discovery x: (t, s)
+    u64* dval;                                       // [kScKeyCap] its value
+    u64* kbm;                                        // [kScWords] key-space bitmap of the level
+    u64* wdeg;                                       // [kScWords] degree sums per bitmap word
+    uint32_t* kdeg;                                  // [kScKeyCap] degree of the key's discovery
+    uint32_t* kdis;                                  // [kScKeyCap] key -> discovery index
+    int4* items;                                     // [2 parities][kCoSegs][iseg] (t, s | cnt << 8, ybase, it0)
+    int64_t iseg;
+    int32_t* out_link;                               // [pcap] pairs, level-major, rank order
+    int32_t* out_atom;
+    int32_t* out_seed;
+    int64_t pcap;
+    u64* ctl;
+    int64_t* hmeta;                                  // mapped: [0] status (-1 until block 0's normal exit), [1] levels,
+                                                     //   [2] pairs, [3] timed out, [4] traversed items
+    int64_t* blk_bytes;                              // mapped [gridDim.x]
+    u64 timeout;
+};
+
+__device__ __forceinline__ u64 sc_ld(const u64* p) { return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void sc_st(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t sc_ld32(const uint32_t* p) {
+    return __hip_atomic_load((uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sc_st32(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The 64 segment counters at c (agent-scope loads) -> exclusive prefix pre[0 .. kCoSegs] (LDS; whole block).
+__device__ __forceinline__ int64_t sc_seg_prefix(const u64* c, int64_t cap, int64_t* pre) {
+    if (threadIdx.x < 64) {
+        const u64 raw = threadIdx.x < kCoSegs ? sc_ld(c + threadIdx.x) : 0ull;   // [xwg]
+        const int64_t v = min((int64_t)raw, cap);
+        int64_t x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(x, off);
+            if ((int)threadIdx.x >= off) x += y;
+        }
+        if (threadIdx.x < kCoSegs) pre[threadIdx.x] = x - v;
+        if (threadIdx.x == kCoSegs - 1) pre[kCoSegs] = x;
+    }
+    __syncthreads();
+    return pre[kCoSegs];
+}
+
+__device__ __forceinline__ int sc_seg_of(const int64_t* pre, int64_t x) {
+    int lo = 0, hi = kCoSegs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Appends one work item per lane that has one (wave-aggregated; every lane of the wave calls it).
+__device__ __forceinline__ void sc_put_items(const ScArgs& a, int par, int seg, int32_t t, int32_t s, int64_t deg,
+                                             int64_t ybase, int64_t it0, u64* status) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nch = (deg + kScChunk - 1) / kScChunk;
+    int64_t x = nch;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    const int64_t tot = __shfl(x, 63);
+    if (!tot) return;
+    u64 b = 0;
+    if (lane == 63) b = atomicAdd(a.ctl + kScItm + par * kCoSegs + seg, (u64)tot);   // [xwg]
+    b = __shfl(b, 63);
+    const int64_t base = (int64_t)b + x - nch;
+    if (nch == 0) return;
+    if (base + nch > a.iseg) {
+        atomicOr(status, 1ull);   // [xwg]
+        return;
+    }
+    int4* L = a.items + ((int64_t)par * kCoSegs + seg) * a.iseg;
+    for (int64_t c = 0; c < nch; ++c) {
+        const int32_t cnt = (int32_t)min<int64_t>(kScChunk, deg - c * kScChunk);
+        co_put(L + base + c, make_int4(t, s | (cnt << 8), (int32_t)(ybase + c * kScChunk), (int32_t)(it0 + c * kScChunk)));   // [xwg]
+    }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
+    constexpr int kWaves = NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * kWaves + wave, nw = (int64_t)gridDim.x * kWaves;
+    const int seg = blockIdx.x % kCoSegs;
+    __shared__ u64 s_kbm[kScWords];
+    __shared__ uint32_t s_cpre[kScWords + 1], s_dpre[kScWords + 1];
+    __shared__ int64_t s_pre[kCoSegs + 1];
+    __shared__ int64_t s_T;
+    __shared__ u64 s_st;
+    __shared__ unsigned long long s_cnt[kMaxCoSeeds];
+    __shared__ int64_t s_ws[kWaves];
+    if (threadIdx.x < kMaxCoSeeds) s_cnt[threadIdx.x] = 0;
+    int64_t nbytes = 0, trav = 0;
+    u64* st_sticky = a.ctl + kScSt + 2;
+    u64 gen = 0;
+    // level 0: the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46); their items in
+    // seed order, seed s's first item index = the degrees of the seeds before it
+    int64_t T = 0;
+    for (int s = 0; s < a.k; ++s) T += a.y_off[a.seeds[s] + 1] - a.y_off[a.seeds[s]];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.k) {
+            const int32_t t = a.seeds[threadIdx.x];
+            atomicOr(a.vis + (int64_t)threadIdx.x * a.vwords + (t >> 6), 1ull << (t & 63));   // [xwg]
+        }
+        for (int s0 = 0; s0 < a.k; s0 += 64) {   // wave 0: seeds 64 at a time (wave-uniform loop)
+            if (wave != 0) break;
+            const int s = s0 + lane;
+            int32_t t = 0;
+            int64_t dg = 0, it0 = 0;
+            if (s < a.k) {
+                t = a.seeds[s];
+                dg = a.maxd > 0 ? a.y_off[t + 1] - a.y_off[t] : 0;
+                for (int q = 0; q < s; ++q) it0 += a.y_off[a.seeds[q] + 1] - a.y_off[a.seeds[q]];
+                if (a.maxd > 0) trav += a.inc_off[t + 1] - a.inc_off[t];
+            }
+            sc_put_items(a, 0, 0, t, s, dg, s < a.k ? a.y_off[t] : 0, it0, a.ctl + kScSt + 1);
+        }
+    }
+    bool timed_out = co_barrier_lite(a.ctl, gen, a.ctl + kScSt + 1, a.timeout);
+    int32_t d = 0;
+    int64_t out0 = 0;
+    int64_t Tprev = 0;
+    u64 ph = 1;   // phases completed (the seeding was phase 0... its errors: word 1)
+    for (; !timed_out; ++d) {
+        const int par = d & 1;
+        // ---- P1: expand ----
+        if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1)) | sc_ld(st_sticky);   // [xwg] the last phase's errors
+        const int64_t nf = sc_seg_prefix(a.ctl + kScItm + par * kCoSegs, a.iseg, s_pre);
+        const u64 st = s_st;
+        __syncthreads();
+        if (st) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(st_sticky, st);
+            break;
+        }
+        if (nf == 0 || d >= a.maxd) break;   // the same decision in every block
+        if (T > kScKeyCap || d >= kCoMaxLevels) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(st_sticky, 8ull);
+            break;
+        }
+        u64* stw = a.ctl + kScSt + ((ph + 1) & 1);   // this phase's error word
+        if (blockIdx.x == 0) {   // the previous level's discovery counters (read in its P2 / P3) -> 0
+            if (threadIdx.x < kCoSegs) sc_st(a.ctl + kScDis + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
+        }
+        // the previous level's bitmap words and degree sums -> 0 (read in its P3, written again in this P2)
+        for (int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x; w < (Tprev + 63) / 64; w += (int64_t)gridDim.x * NT) {
+            sc_st(a.kbm + w, 0ull);   // [xwg]
+            sc_st(a.wdeg + w, 0ull);  // [xwg]
+        }
+        {
+            const int4* L = a.items + (int64_t)par * kCoSegs * a.iseg;
+            const int64_t per = min<int64_t>(64, (nf + nw - 1) / nw);
+            for (int64_t i0 = gw * per; i0 < nf; i0 += nw * per) {
+                const int64_t i = i0 + lane;
+                int32_t is = 0;
+                int64_t yb = 0, itb = 0, cnt = 0;
+                if (lane < per && i < nf) {
+                    const int sg = sc_seg_of(s_pre, i);
+                    const int4 e = co_get(L + (int64_t)sg * a.iseg + (i - s_pre[sg]));   // [xwg]
+                    is = e.y & 0xFF;
+                    cnt = e.y >> 8;
+                    yb = (int64_t)(uint32_t)e.z;
+                    itb = (int64_t)(uint32_t)e.w;
+                    nbytes += 16;
+                }
+                int64_t x = cnt;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int64_t y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+                const int64_t TT = __shfl(x, 63), ex = x - cnt;
+                for (int64_t f0 = 0; f0 < TT; f0 += 64) {   // wave-uniform: every lane reaches the append
+                    const int64_t f = f0 + lane;
+                    int o = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1) {
+                        const int mid = o + step;
+                        if (__shfl(ex, mid) <= f) o = mid;
+                    }
+                    const int32_t s = __shfl(is, o);
+                    const int64_t off_ = f - __shfl(ex, o);
+                    const int64_t ii = __shfl(yb, o) + off_, it = __shfl(itb, o) + off_;
+                    bool isnew = false;
+                    int32_t t = 0;
+                    u64 slot = 0;
+                    if (f < TT) {
+                        t = a.a_tgt[ii];
+                        const int32_t la = a.a_lnk[ii];
+                        nbytes += 16;
+                        const u64 vw = sc_ld(a.vis + (int64_t)s * a.vwords + (t >> 6));   // [xwg]
+                        if (!((vw >> (t & 63)) & 1ull)) {
+                            const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)t;
+                            const u64 v = ((u64)(it + 1) << 32) | (u64)(uint32_t)la;
+                            u64 h = ls_hash(key, a.hbits);
+                            int probe = 0;
+                            for (; probe < kScProbes; ++probe) {
+                                u64 kk = sc_ld(a.hkey + h);   // [xwg]
+                                if (kk == kLsEmpty) {
+                                    kk = atomicCAS((unsigned long long*)(a.hkey + h), kLsEmpty, (unsigned long long)key);   // [xwg]
+                                    if (kk == kLsEmpty) {
+                                        atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
+                                        isnew = true;
+                                        slot = h;
+                                        break;
+                                    }
+                                }
+                                if (kk == key) {
+                                    if (sc_ld(a.hval + h) > v) atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
+                                    break;
+                                }
+                                h = (h + 1) & (u64)a.hmask;
+                            }
+                            if (probe == kScProbes) atomicOr(stw, 4ull);   // [xwg] the hash is too full
+                            nbytes += 24;
+                        }
+                    }
+                    const u64 m = __ballot(isnew);
+                    if (m) {
+                        const int leader = __ffsll((long long)m) - 1;
+                        u64 b = 0;
+                        if (lane == leader) b = atomicAdd(a.ctl + kScDis + par * kCoSegs + seg, (u64)__popcll(m));   // [xwg]
+                        b = __shfl(b, leader);
+                        if (isnew) {
+                            const u64 pos = b + __popcll(m & ((1ull << lane) - 1ull));
+                            if ((int64_t)pos < a.dcap)
+                                co_put(a.dseg + (int64_t)seg * a.dcap + (int64_t)pos,
+                                       make_int4(t, s, (int32_t)(uint32_t)slot, (int32_t)(slot >> 32)));   // [xwg]
+                            else
+                                atomicOr(stw, 16ull);   // [xwg]
+                            nbytes += 16;
+                        }
+                    }
+                }
+            }
+        }
+        timed_out = co_barrier_lite(a.ctl, gen, stw, a.timeout);
+        ++ph;
+        if (timed_out) break;
+        // ---- P2: finalise the discoveries ----
+        if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1));   // [xwg]
+        const int64_t n = sc_seg_prefix(a.ctl + kScDis + par * kCoSegs, a.dcap, s_pre);
+        if (s_st) break;   // (block-uniform: read before the prefix's barrier)
+        stw = a.ctl + kScSt + ((ph + 1) & 1);
+        if (blockIdx.x == 0 && threadIdx.x < kCoSegs)   // the next level's item counters (read two levels ago)
+            sc_st(a.ctl + kScItm + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
+        const bool expand_next = d + 1 < a.maxd;
+        for (int64_t x = (int64_t)blockIdx.x * NT + threadIdx.x; x < n; x += (int64_t)gridDim.x * NT) {
+            const int sg = sc_seg_of(s_pre, x);
+            const int4 e = co_get(a.dseg + (int64_t)sg * a.dcap + (x - s_pre[sg]));   // [xwg]
+            const u64 slot = (u64)(uint32_t)e.z | (u64)(uint32_t)e.w << 32;
+            const u64 v = sc_ld(a.hval + slot);   // [xwg]
+            sc_st(a.hkey + slot, kLsEmpty);       // [xwg]
+            sc_st(a.hval + slot, ~0ull);          // [xwg]
+            const uint32_t key = (uint32_t)((v >> 32) - 1ull);
+            const uint32_t dg = expand_next ? (uint32_t)(a.y_off[e.x + 1] - a.y_off[e.x]) : 0u;
+            atomicOr(a.kbm + (key >> 6), 1ull << (key & 63));                             // [xwg]
+            if (dg) atomicAdd(a.wdeg + (key >> 6), (u64)dg);                                 // [xwg]
+            sc_st32(a.kdeg + key, dg);                                                       // [xwg]
+            sc_st32(a.kdis + key, (uint32_t)x);                                              // [xwg]
+            co_put(a.dflat + x, make_int2(e.x, e.y));                                        // [xwg]
+            sc_st(a.dval + x, v);                                                            // [xwg]
+            atomicOr(a.vis + (int64_t)e.y * a.vwords + (e.x >> 6), 1ull << (e.x & 63));     // [xwg] examined from now on
+            nbytes += 16 + 8 + 16 + 8 + 8 + 4 + 4 + 8 + 8 + 8;
+        }
+        timed_out = co_barrier_lite(a.ctl, gen, stw, a.timeout);
+        ++ph;
+        if (timed_out) break;
+        // ---- P3: rank, emit, next items ----
+        if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1));   // [xwg]
+        const int64_t Wn = (T + 63) / 64;
+        {   // the words' popcounts and degree sums -> exclusive prefixes in LDS (every block)
+            constexpr int per = kScWords / NT;
+            int64_t c = 0, g2 = 0;
+            uint32_t cw[per];
+            u64 dw[per];
+#pragma unroll
+            for (int q = 0; q < per; ++q) {
+                const int64_t w = (int64_t)threadIdx.x * per + q;
+                u64 bw = 0, dd = 0;
+                if (w < Wn) {
+                    bw = sc_ld(a.kbm + w);    // [xwg]
+                    dd = sc_ld(a.wdeg + w);   // [xwg]
+                }
+                s_kbm[threadIdx.x * per + q] = bw;
+                cw[q] = (uint32_t)__popcll(bw);
+                dw[q] = dd;
+                c += cw[q];
+                g2 += (int64_t)dd;
+            }
+            // block exclusive scans of (c, g2): wave shuffles, then the wave sums through LDS
+            int64_t xc = c, xg = g2;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t yc = __shfl_up(xc, off), yg = __shfl_up(xg, off);
+                if (lane >= off) {
+                    xc += yc;
+                    xg += yg;
+                }
+            }
+            __shared__ int64_t s_wc[kWaves], s_wg[kWaves];
+            if (lane == 63) {
+                s_wc[wave] = xc;
+                s_wg[wave] = xg;
+            }
+            __syncthreads();
+            int64_t bc = 0, bg = 0, tc = 0, tg = 0;
+#pragma unroll
+            for (int q = 0; q < kWaves; ++q) {
+                bc += q < wave ? s_wc[q] : 0;
+                bg += q < wave ? s_wg[q] : 0;
+                tc += s_wc[q];
+                tg += s_wg[q];
+            }
+            int64_t rc = bc + xc - c, rg = bg + xg - g2;
+#pragma unroll
+            for (int q = 0; q < per; ++q) {
+                s_cpre[threadIdx.x * per + q] = (uint32_t)rc;
+                s_dpre[threadIdx.x * per + q] = (uint32_t)rg;
+                rc += cw[q];
+                rg += (int64_t)dw[q];
+            }
+            if (threadIdx.x == 0) {
+                s_cpre[kScWords] = (uint32_t)tc;
+                s_T = tg;
+            }
+            __syncthreads();
+        }
+        if (s_st) break;
+        stw = a.ctl + kScSt + ((ph + 1) & 1);
+        const int64_t nd = s_cpre[kScWords];   // == n
+        const int64_t Tn = s_T;                // the next level's items
+        if (out0 + nd > a.pcap) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(stw, 2ull);   // [xwg]
+        } else {
+            for (int64_t w = gw; w < Wn; w += nw) {   // a wave per non-empty word, a lane per key
+                const u64 m = s_kbm[w];
+                if (!m) continue;   // wave-uniform
+                const bool set = (m >> lane) & 1ull;
+                const uint32_t key = (uint32_t)(w * 64 + lane);
+                uint32_t x = 0, dg = 0;
+                if (set) {
+                    x = sc_ld32(a.kdis + key);   // [xwg]
+                    dg = sc_ld32(a.kdeg + key);  // [xwg]
+                }
+                int64_t ex = dg;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int64_t y = __shfl_up(ex, off);
+                    if (lane >= off) ex += y;
+                }
+                ex -= dg;
+                int32_t t = 0, s = 0;
+                if (set) {
+                    const int2 ts = co_get(a.dflat + x);   // [xwg]
+                    t = ts.x;
+                    s = ts.y;
+                    const u64 v = sc_ld(a.dval + x);      // [xwg]
+                    const int64_t r = out0 + s_cpre[w] + __popcll(m & ((1ull << lane) - 1ull));
+                    a.out_link[r] = (int32_t)(uint32_t)v;
+                    a.out_atom[r] = t;
+                    a.out_seed[r] = s;
+                    atomicAdd(&s_cnt[s], 1ull);
+                    if (d + 1 < a.maxd) trav += a.inc_off[t + 1] - a.inc_off[t];   // expanded at level d + 1
+                    nbytes += 8 + 8 + 8 + 8 + 12;
+                }
+                sc_put_items(a, par ^ 1, seg, t, s, (int64_t)dg, set ? a.y_off[t] : 0, (int64_t)s_dpre[w] + ex, stw);
+            }
+        }
+        __syncthreads();
+        for (int s = threadIdx.x; s < a.k; s += NT)
+            if (s_cnt[s]) {
+                atomicAdd(a.ctl + kScLcnt + (int64_t)d * 64 + s, s_cnt[s]);   // [xwg] read by the host
+                s_cnt[s] = 0;
+            }
+        out0 += nd;
+        Tprev = T;
+        T = Tn;
+        timed_out = co_barrier_lite(a.ctl, gen, stw, a.timeout);
+        ++ph;
+    }
+    if (timed_out) {   // reported in its own mapped word (as hgx_bfs_coop): the host falls back
+        if (threadIdx.x == 0) __hip_atomic_store(a.hmeta + 3, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    // every block left the loop after the same barrier: the bytes and the traversed items of this block
+    {
+        for (int off = 32; off > 0; off >>= 1) {
+            nbytes += __shfl_xor(nbytes, off);
+            trav += __shfl_xor(trav, off);
+        }
+        __syncthreads();
+        if (lane == 0) s_ws[wave] = nbytes;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tb = 0;
+            for (int q = 0; q < kWaves; ++q) tb += s_ws[q];
+            a.blk_bytes[blockIdx.x] = tb;
+        }
+        __syncthreads();
+        if (lane == 0) s_ws[wave] = trav;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tt = 0;
+            for (int q = 0; q < kWaves; ++q) tt += s_ws[q];
+            if (tt) atomicAdd((unsigned long long*)(a.ctl + 1), (unsigned long long)tt);   // [xwg] read by block 0 below? no: by the host
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.hmeta[1] = d;
+        a.hmeta[2] = out0;
+        a.hmeta[0] = (int64_t)(sc_ld(st_sticky) | sc_ld(a.ctl + kScSt) | sc_ld(a.ctl + kScSt + 1));
+    }
+}
+
+// The examined bits of a finished stage's pairs and seeds -> 0 (the bitmaps' zero-between-calls rule).
+__global__ void __launch_bounds__(256) k_sc_clear(int64_t n, const int32_t* __restrict__ atom, const int32_t* __restrict__ seed,
+                                                  int32_t k, const int32_t* __restrict__ seeds, int64_t vwords, u64* vis) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n + k; i += (int64_t)gridDim.x * 256) {
+        const int32_t t = i < n ? atom[i] : seeds[i - n];
+        const int32_t s = i < n ? seed[i] : (int32_t)(i - n);
+        vis[(int64_t)s * vwords + (t >> 6)] = 0ull;
+    }
+}
+
 // Device buffers of one call, given back to the graph's pool at scope exit.
 struct SeqScratch {
     hgx_graph* g;
@@ -3490,6 +3967,164 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
     return false;
 }
 
+// ---- the order-exact multi-workgroup stage, host side ----
+
+int sc_fits(hgx_graph* g) {   // its grid (0: does not fit); the same residency rule as co_fits
+    if (g->sc_ok < 0) {
+        int per_cu = 0, cus = 0;
+        HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_seq_coop<256>, 256, 0));
+        HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
+        const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
+        static const int cap_env = std::getenv("HGX_SC_BLOCKS") ? std::atoi(std::getenv("HGX_SC_BLOCKS")) : 0;   // A/B
+        const int64_t cap = cap_env >= kCoMinBlocks ? std::min(cap_env, kCoMaxBlocks) : kCoBlocks;
+        g->sc_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, cap) : 0;
+    }
+    return g->sc_ok;
+}
+
+// The stage over the seeds sidx of `seeds` (<= kMaxCoSeeds, generator with a yield adjacency): true and
+// out.segs[j] / traversed / deepest filled for seed j of sidx when it finished; false (bitmaps cleared)
+// when a capacity or the grid did not fit -- the caller runs the level engine.
+bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t maxd,
+              const hgx_algen_opts& o, SeqOut& out, double* ms) {
+    const int mode = seq_mode(o);
+    const YieldAdj* ya = stage_yield_adj(g, mode, o);
+    const int32_t k = (int32_t)sidx.size();
+    if (!ya || k == 0 || k > kMaxCoSeeds || !sc_fits(g)) return false;
+    static const bool off = std::getenv("HGX_SEQ_COOP") && std::atoi(std::getenv("HGX_SEQ_COOP")) == 0;   // A/B
+    if (off) return false;
+    hipStream_t st = g->stream;
+    const int64_t vwords = g->A / 64 + 1;
+    if (g->co_vis_seeds < kMaxCoSeeds) {   // the grid stages' zero-invariant bitmaps (shared with hgx_bfs_coop)
+        if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
+        g->co_vis = nullptr;
+        g->co_vis_seeds = 0;
+        HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords)));
+        HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords), st));
+        g->co_vis_seeds = kMaxCoSeeds;
+    }
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        SeqScratch w{g, {}};
+        ScArgs a{};
+        a.k = k;
+        a.A = g->A;
+        a.inc_off = g->inc_off;
+        a.y_off = ya->off;
+        a.a_tgt = ya->tgt;
+        a.a_lnk = ya->lnk;
+        a.maxd = maxd;
+        a.vwords = vwords;
+        a.vis = g->co_vis;
+        a.hbits = 19;                               // 512K slots: a level holds <= kScKeyCap discoveries
+        a.hmask = ((int64_t)1 << a.hbits) - 1;
+        a.hkey = (u64*)w.take(sizeof(u64) << a.hbits);
+        a.hval = (u64*)w.take(sizeof(u64) << a.hbits);
+        a.dcap = kScKeyCap / kCoSegs * 4;
+        a.dseg = (int4*)w.take(sizeof(int4) * kCoSegs * (size_t)a.dcap);
+        a.dflat = (int2*)w.take(sizeof(int2) * (size_t)kScKeyCap);
+        a.dval = (u64*)w.take(sizeof(u64) * (size_t)kScKeyCap);
+        a.kbm = (u64*)w.take(sizeof(u64) * 2 * kScWords);
+        a.wdeg = a.kbm + kScWords;
+        a.kdeg = (uint32_t*)w.take(sizeof(uint32_t) * 2 * (size_t)kScKeyCap);
+        a.kdis = a.kdeg + kScKeyCap;
+        a.iseg = (int64_t)1 << 14;
+        a.items = (int4*)w.take(sizeof(int4) * 2 * kCoSegs * (size_t)a.iseg);
+        a.pcap = std::max<int64_t>(g->sc_pcap, (int64_t)1 << 20);
+        a.out_link = (int32_t*)w.take(sizeof(int32_t) * 3 * (size_t)a.pcap);
+        a.out_atom = a.out_link + a.pcap;
+        a.out_seed = a.out_atom + a.pcap;
+        a.ctl = (u64*)w.take(sizeof(u64) * (size_t)kScCtlWords);
+        int32_t* dseeds = (int32_t*)w.take(sizeof(int32_t) * (size_t)k);
+        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
+        for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
+        HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
+        a.seeds = dseeds;
+        HGX_HIP(hipMemsetAsync(a.hkey, 0xFF, sizeof(u64) << a.hbits, st));
+        HGX_HIP(hipMemsetAsync(a.hval, 0xFF, sizeof(u64) << a.hbits, st));
+        HGX_HIP(hipMemsetAsync(a.kbm, 0, sizeof(u64) * 2 * kScWords, st));
+        HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScCtlWords, st));
+        const int nblk = g->sc_ok;
+        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + (size_t)nblk));
+        int64_t* hm = (int64_t*)hb.p;
+        hm[0] = -1;
+        hm[1] = hm[2] = hm[3] = 0;
+        void* hmd = nullptr;
+        HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
+        a.hmeta = (int64_t*)hmd;
+        a.blk_bytes = (int64_t*)hmd + 8;
+        const char* to_s = std::getenv("HGX_CO_TIMEOUT");
+        a.timeout = to_s && std::atoll(to_s) > 0 ? (u64)std::atoll(to_s) : kCoTimeout;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (g->timing) {
+            ev[0] = ev_take(g);
+            ev[1] = ev_take(g);
+            HGX_HIP(hipEventRecord(ev[0], st));
+        }
+        hgx_seq_coop<256><<<(unsigned)nblk, 256, 0, st>>>(a);
+        HGX_CHECK_LAUNCH();
+        if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+        spin_sync(st);
+        struct HostBack {   // the mapped readout goes back to the pool on every path
+            hgx_graph* g;
+            PoolBuf b;
+            ~HostBack() {
+                std::lock_guard<std::mutex> lk(g->seq_mu);
+                g->seq_hbufs.push_back(b);
+            }
+        } back{g, hb};
+        if (ev[1]) {
+            *ms += ev_ms(g, ev[0], ev[1]);
+            ev_give(g, ev[0]);
+            ev_give(g, ev[1]);
+        }
+        const bool clean = hm[0] == 0 && hm[3] == 0;
+        if (!clean) {   // the bitmaps may hold bits no pair records: cleared whole
+            if (hm[3] != 0) ++g->co_timeouts;
+            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
+            if (hm[0] == 2 && hm[3] == 0 && attempt == 0) {   // only the pairs outgrew their buffer: once more
+                g->sc_pcap = a.pcap * 4;
+                continue;
+            }
+            return false;
+        }
+        const int32_t nlev = (int32_t)hm[1];
+        const int64_t total = hm[2];
+        // pairs (+ their seeds, for clearing), the per-level per-seed counts and the traversed items
+        PoolBuf pb = take_host_buf(g, 8 * (size_t)total + 8 + 8 * ((size_t)nlev * 64 + 2));
+        out.bufs.push_back(pb);
+        int32_t* hl = (int32_t*)pb.p;
+        int32_t* ha = hl + total;
+        int64_t* hc = (int64_t*)(ha + total + (total & 1));
+        if (total) {
+            HGX_HIP(hipMemcpyAsync(hl, a.out_link, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
+            HGX_HIP(hipMemcpyAsync(ha, a.out_atom, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
+        }
+        if (nlev) HGX_HIP(hipMemcpyAsync(hc, a.ctl + kScLcnt, sizeof(int64_t) * 64 * (size_t)nlev, hipMemcpyDeviceToHost, st));
+        HGX_HIP(hipMemcpyAsync(hc + 64 * (size_t)nlev, a.ctl + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        k_sc_clear<<<grid_for(total + k, 256, 4096), 256, 0, st>>>(total, a.out_atom, a.out_seed, k, dseeds, vwords,
+                                                                   g->co_vis);
+        HGX_CHECK_LAUNCH();
+        spin_sync(st);
+        // level-major, seed-major inside a level: seed j's pairs of level d follow the earlier seeds' ones
+        int64_t o0 = 0;
+        for (int32_t d = 0; d < nlev; ++d) {
+            int64_t o = o0;
+            for (int32_t j = 0; j < k; ++j) {
+                const int64_t c = hc[64 * (size_t)d + j];
+                if (c > 0) out.segs[(size_t)sidx[j]].push_back({hl + o, ha + o, nullptr, c, d + 1});
+                if (c > 0) out.deepest = std::max(out.deepest, d + 1);
+                o += c;
+            }
+            o0 = o;
+        }
+        if (o0 != total) fail(HGX_E_DEVICE, "hgx_bfs_sequence: grid stage pair counts inconsistent");
+        out.traversed += (double)hc[64 * (size_t)nlev];
+        for (int b = 0; b < nblk; ++b) out.bytes += (double)hm[8 + b];
+        return true;
+    }
+    return false;
+}
+
 }  // namespace
 
 void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_depth, const hgx_algen_opts& o,
@@ -3798,6 +4433,8 @@ struct hgx_seq_result {
     double ms_total = 0, traversed = 0;
     double ms_block = 0, bytes_block = 0;   // the workgroup engine's launches: device ms, algorithmic bytes
     double ms_level = 0;                    // the level-synchronous engine: device ms (timing on) ...
+    double ms_coop = 0, bytes_coop = 0;     // the order-exact grid stage (hgx_seq_coop): device ms, algorithmic bytes
+    int32_t n_coop = 0;                     //   and the seeds it finished
     int32_t n_block = 0, n_level = 0;       // seeds finished by each engine
     ~hgx_seq_result() {
         if (!g) return;
@@ -3969,7 +4606,27 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             el1 = ev_take(g);
             HGX_HIP(hipEventRecord(el0, st));
         }
-        seq_levels_all(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev, g->seq_engine != 1);
+        bool done = false;
+        if (g->seq_engine == 0 && rs.size() <= (size_t)kMaxCoSeeds) {   // the grid stage first (one launch)
+            r->lev.segs.assign(rs.size(), {});
+            std::vector<int32_t> sidx(rs.size());
+            for (size_t q = 0; q < rs.size(); ++q) sidx[q] = (int32_t)q;
+            SeqOut co;
+            co.segs.assign(rs.size(), {});
+            done = seq_coop(g, rs.data(), sidx, maxd, o, co, &r->ms_coop);
+            if (done) {
+                r->lev.segs = std::move(co.segs);
+                r->lev.bufs = std::move(co.bufs);
+                r->lev.traversed = co.traversed;
+                r->lev.deepest = co.deepest;
+                r->bytes_coop = co.bytes;
+                r->n_coop = (int32_t)rs.size();
+            } else {
+                std::lock_guard<std::mutex> lk(g->seq_mu);
+                for (auto& b : co.bufs) g->seq_hbufs.push_back(b);
+            }
+        }
+        if (!done) seq_levels_all(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev, g->seq_engine != 1);
         if (el0) {
             HGX_HIP(hipEventRecord(el1, st));
             HGX_HIP(hipEventSynchronize(el1));
@@ -4115,6 +4772,15 @@ int hgx_seq_result_engine_stats(const hgx_seq_result* r, int32_t* n_block, int32
     if (n_level) *n_level = r->n_level;
     if (ms_block) *ms_block = r->ms_block;
     if (bytes_block) *bytes_block = r->bytes_block;
+    HGX_API_END
+}
+
+int hgx_seq_result_grid_stats(const hgx_seq_result* r, int32_t* n_seeds, double* ms, double* bytes) {
+    HGX_API_BEGIN
+    if (!r) fail(HGX_E_INVALID, "null result");
+    if (n_seeds) *n_seeds = r->n_coop;
+    if (ms) *ms = r->ms_coop;
+    if (bytes) *bytes = r->bytes_coop;
     HGX_API_END
 }
 

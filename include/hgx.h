@@ -332,6 +332,10 @@ int  hgx_seq_result_engine_stats(const hgx_seq_result *r, int32_t *n_block, int3
  * targets, per yield the examined word and the hash slot; per pulled atom its incidence range, examined
  * row, entries, link rows, union bits, frontier rows, pin indices and hash probes; the frontier
  * entries of the pull tables), and how many of its levels ran as pulls.  Any output may be NULL. */
+/* The order-exact grid stage (one persistent launch for <= 64 of the seeds the workgroup engine handed
+ * over, when the generator has a yield adjacency: ordered modes or a link type): seeds it finished, its
+ * device ms (timing enabled) and algorithmic bytes.  Any output may be NULL. */
+int  hgx_seq_result_grid_stats(const hgx_seq_result *r, int32_t *n_seeds, double *ms, double *bytes);
 int  hgx_seq_result_level_stats(const hgx_seq_result *r, double *ms_level, double *bytes_level, int64_t *pull_levels);
 void hgx_seq_result_free(hgx_seq_result *r);
 /* Batched conjunctive pattern queries.  Result of query q = the link atoms L with

@@ -905,10 +905,12 @@ JNIEXPORT jlongArray JFN(seqEngineStats)(JNIEnv *e, jclass k, jlong sq) {
     int32_t nb = 0, nl = 0;
     int64_t pl = 0;
     int rc = hgx_seq_result_engine_stats((const hgx_seq_result *)(intptr_t)sq, &nb, &nl, NULL, NULL);
+    int32_t nc = 0;
     if (!rc) rc = hgx_seq_result_level_stats((const hgx_seq_result *)(intptr_t)sq, NULL, NULL, &pl);
+    if (!rc) rc = hgx_seq_result_grid_stats((const hgx_seq_result *)(intptr_t)sq, &nc, NULL, NULL);
     if (rc) { throw_rc(e, rc); return NULL; }
-    int64_t v[3] = {nb, nl, pl};
-    return new_longs(e, v, 3);
+    int64_t v[4] = {nb, nl, pl, nc};
+    return new_longs(e, v, 4);
 }
 
 JNIEXPORT jarray JFN(queryMs)(JNIEnv *e, jclass k, jlong q) {

@@ -65,7 +65,7 @@ final class Hgx
     static native int[] seqDists(long s);
     static native void seqFree(long s);
     static native int[] seqRange(long s, int which, long first, int max);   // 0 links / 1 atoms / 2 dists, paged
-    static native long[] seqEngineStats(long s);                // {workgroup seeds, level-synchronous seeds, pull levels}
+    static native long[] seqEngineStats(long s);                // {workgroup seeds, level-synchronous seeds, pull levels, grid-stage seeds}
 
     // ---- conjunctive pattern batches (hgx_pattern_batch_packed / _ext + readers) -------------
     static native long patternBatch(long g, int[] type, long[] incOff, int[] inc, int[] hasOrdered, long[] patOff,

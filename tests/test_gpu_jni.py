@@ -154,7 +154,7 @@ def test_bfs_sequence_order_exact(jni, graph, gh):
             for which, col in ((0, links), (1, atoms), (2, dists)):
                 got = np.concatenate([jni.seqRange(s, which, f, 5) for f in range(0, len(col) + 5, 5)])
                 assert np.array_equal(got, col), which
-            nb, nl, _pull = jni.seqEngineStats(s).tolist()
+            nb, nl, _pull, _grid = jni.seqEngineStats(s).tolist()
             assert nb + nl == len(seeds)
         finally:
             jni.seqFree(s)

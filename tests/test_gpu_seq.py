@@ -299,3 +299,52 @@ def test_level_engine_chunk_split_on_wide_keys():
             gl, ga, gd = res.pairs(i)
             assert np.array_equal(ga, at) and np.array_equal(gl, l_) and np.array_equal(gd, d), (lim, i)
     snap.close()
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_order_exact_grid_stage_vs_oracle(case):
+    """Round 5: the seeds the order-exact workgroup engine hands back (more than 2046 pairs) run in one
+    persistent multi-workgroup launch (hgx_seq_coop: level hash, key-space bitmap ranks, a wave per
+    bitmap word) when the generator has a yield adjacency.  Exact against the oracle pair by pair (links,
+    atoms, distances, traversed items): config-5 closures at 5% scale (the root classes: 12K-250K-atom
+    closures over ~20 levels) in both directions with depth limits, a typed power-law graph, and the
+    forced barrier timeout (HGX_CO_TIMEOUT=1: the stage must fall back to the level engine, still exact,
+    and leave its bitmaps clean for the next call)."""
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, bfs_sequence, synth
+    if case < 3:
+        g = synth.config5(scale=0.05, n_sources=40)
+        T = int(g["subsumes_type"])
+        seeds = np.concatenate([np.arange(10, dtype=np.int32), np.asarray(g["seeds"], np.int32)])
+        rev = case == 1
+        snap, orc = snapshot(g), oracle(g)
+        gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
+        opts = algen(T, False, True, rev, False)
+        maxds = (None, 3) if case < 2 else (None,)
+    else:
+        g = synth.hypergraph(6000, 30000, 2, 6, 2.1, 3, seed=88)
+        snap, orc = snapshot(g), oracle(g)
+        deg = np.bincount(np.asarray(g["tgt_idx"]), minlength=g["num_atoms"])
+        seeds = np.concatenate([np.argsort(-deg)[:6], np.arange(50, 80)]).astype(np.int32)
+        gen_ = gen(snap, K.ALGEN_MODES[1], 1)
+        opts = algen(1, *K.ALGEN_MODES[1])
+        maxds = (None, 2)
+    for maxd in maxds:
+        for attempt in ((1, 0) if case == 2 else (0,)):
+            if attempt:
+                os.environ["HGX_CO_TIMEOUT"] = "1"
+            try:
+                res = bfs_sequence(snap, seeds, maxd, gen_)
+            finally:
+                os.environ.pop("HGX_CO_TIMEOUT", None)
+            trav = 0
+            for i, s in enumerate(seeds):
+                l_, a, d, tr = orc.bfs(int(s), -1 if maxd is None else maxd, opts)
+                gl, ga, gd = res.pairs(i)
+                assert np.array_equal(ga, a) and np.array_equal(gl, l_) and np.array_equal(gd, d), (case, maxd, i)
+                trav += tr
+            assert res.traversed_edges == float(trav)
+            if attempt:
+                assert res.n_coop == 0 and res.n_level >= 1, (res.n_coop, res.n_level)
+            elif case < 3:
+                assert res.n_coop >= 1 and res.n_coop == res.n_level, (res.n_coop, res.n_level)
+    snap.close()
