@@ -197,9 +197,6 @@ enum Ctr {
     cScanned,           // incidence entries scanned by the frontier push (type + yield flag)
     cNum = 16
 };
-// push levels do not use the hub counters: cAccHub carries the set bits of the new rows there (the
-// density test of a coded next level)
-constexpr int cNewBits = cAccHub;
 
 __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -1031,383 +1028,6 @@ __global__ void __launch_bounds__(256) hgx_hub_finalize(int64_t H, const int32_t
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Coded dense level (HGX_OPT_CODED; symmetric mode).  Level 1 of config 2 is dense in links (94%
-// active) but sparse in bits: its 235K frontier rows, written by the level-0 push, carry about one
-// source bit each, and so do its link rows.  Moving them as 128-byte rows cost 9.3 of the 17.9 ms of
-// a step.  Here a row with at most six bits travels as one 64-bit code (count << 60 | six 10-bit
-// source ids; count 15 = "spilled": the dense row is used), so the gather reads an 8-byte code per
-// frontier pin and writes one per link, and the pulls read an 8-byte code per incidence.  Codes of
-// the frontier atoms are written by the push finalise of the level before; the code arrays' working
-// sets fit the Infinity Cache.  Bits are merged per lane group in LDS (a 64-bit LDS OR per id).
-// ---------------------------------------------------------------------------------------------
-constexpr u64 kCodeSpill = 15ull << 60;
-__device__ __forceinline__ int code_n(u64 c) { return (int)(c >> 60); }
-__device__ __forceinline__ int code_id(u64 c, int i) { return (int)((c >> (10 * i)) & 1023ull); }
-
-// The code of the row held by this lane's G-lane group (lane sub holds words sub*WPL ..): ids in
-// ascending order, 0 for an empty row, kCodeSpill above six bits.  Every lane calls it; the shuffles
-// stay inside the group (all of whose lanes take the same branch).
-template <int W>
-__device__ __forceinline__ u64 group_encode(typename Vec<Lay<W>::WPL>::T r, int sub) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    int cnt;
-    if constexpr (WPL == 1) cnt = __popcll(r);
-    else cnt = __popcll(r.x) + __popcll(r.y);
-    int incl = cnt;
-    for (int off = 1; off < G; off <<= 1) {
-        const int y = __shfl_up(incl, off, G);
-        if (sub >= off) incl += y;
-    }
-    const int total = __shfl(incl, G - 1, G);
-    if (total > 6) return kCodeSpill;   // group-uniform
-    u64 code = 0;
-    int pos = incl - cnt;
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        u64 m;
-        if constexpr (WPL == 1) m = r;
-        else m = j == 0 ? r.x : r.y;
-        for (; m; m &= m - 1ull) {
-            const int id = (sub * WPL + j) * 64 + __ffsll((long long)m) - 1;
-            code |= (u64)id << (10 * pos);
-            ++pos;
-        }
-    }
-    for (int off = 1; off < G; off <<= 1) code |= (u64)__shfl_xor((long long)code, off, G);
-    return total ? (code | ((u64)total << 60)) : 0ull;
-}
-
-// OR the ids of a (non-spilled) code into a group's LDS row.
-__device__ __forceinline__ void code_or(u64* __restrict__ acc, u64 code) {
-    const int n = code_n(code);
-    for (int i = 0; i < n; ++i) {
-        const int id = code_id(code, i);
-        atomicOr(&acc[id >> 6], 1ull << (id & 63));
-    }
-}
-
-// Tile-staged like the dense gather: a wave loads the offsets of its 64 links at once, then target
-// k of every link of its group (G independent loads per lane), the frontier probes, the codes, and
-// only then merges: each link's ids go into its own LDS row (G rows per group), no dependent chain
-// per link.
-template <int W>
-__global__ void __launch_bounds__(256) hgx_link_gather_coded(int64_t M, const int64_t* __restrict__ tgt_off,
-                                                             const int32_t* __restrict__ tgt_idx,
-                                                             const int32_t* __restrict__ link_type, int32_t want_type,
-                                                             const u64* __restrict__ fa, const u64* __restrict__ full,
-                                                             const u64* __restrict__ lvl, const u64* __restrict__ fcode,
-                                                             u64* __restrict__ lf, u64* __restrict__ lcode,
-                                                             u64* __restrict__ la, u64* __restrict__ ctr, int flags) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
-    typedef Vec<WPL> V;
-    __shared__ u64 lrow[4][PER][G][W];   // per wave, group, link of the group: the link's row
-    const bool skip_full = flags & 4;
-    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1), wv = threadIdx.x >> 6;
-    const u64 gmask = (1ull << G) - 1ull;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    u64 (*rows)[W] = lrow[wv][g];
-    u64 n_links = 0, n_pins = 0, n_spill = 0;
-    for (int64_t tile = wave; tile * 64 < M; tile += nwave) {
-        const int64_t Lme = tile * 64 + lane;
-        int64_t bme = 0;
-        int nme = 0;
-        if (Lme < M && (want_type < 0 || link_type[Lme] == want_type)) {
-            bme = tgt_off[Lme];
-            nme = (int)(tgt_off[Lme + 1] - bme);
-        }
-#pragma unroll
-        for (int j = 0; j < G; ++j)
-            for (int w = sub; w < W; w += G) rows[j][w] = 0ull;
-        int32_t v[G];
-        int n[G];
-        int64_t bb[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {   // link j*PER + g of the tile: target sub
-            bb[j] = __shfl(bme, j * PER + g);
-            n[j] = __shfl(nme, j * PER + g);
-            v[j] = sub < n[j] ? tgt_idx[bb[j] + sub] : -1;
-        }
-        unsigned pa = 0, pnf = 0;
-#pragma unroll
-        for (int j = 0; j < G; ++j)
-            if (v[j] >= 0) {
-                if (bit(fa, v[j])) pa |= 1u << j;
-                if (!skip_full || !bit(full, v[j])) pnf |= 1u << j;
-            }
-        u64 code[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) code[j] = ((pa >> j) & 1u) ? fcode[v[j]] : 0ull;
-        __builtin_amdgcn_wave_barrier();
-        unsigned spillm = 0;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            if (code_n(code[j]) == 15) spillm |= 1u << j;
-            else if (code[j]) code_or(rows[j], code[j]);
-        }
-        __builtin_amdgcn_wave_barrier();
-        u64 word = 0;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            const int64_t L = tile * 64 + j * PER + g;
-            typename V::T racc = V::zero();
-            bool any_nf = ((__ballot((pnf >> j) & 1u) >> base) & gmask) != 0ull;
-            const int nact0 = __popcll((__ballot((pa >> j) & 1u) >> base) & gmask);
-            unsigned sm = (unsigned)((__ballot((spillm >> j) & 1u) >> base) & gmask);
-            n_spill += (sub == 0) ? (u64)__popc(sm) : 0ull;
-            while (sm) {   // group-uniform: spilled frontier rows, dense
-                const int kk = __ffs(sm) - 1;
-                sm &= sm - 1u;
-                const int32_t vk = __shfl(v[j], base + kk);
-                racc |= V::ld(lvl + (int64_t)vk * W + sub * WPL);
-            }
-            int nact = nact0;
-            if (n[j] > G) {   // a row longer than G (rare): the remaining targets one chunk at a time
-                const int64_t b = bb[j], e = b + n[j];
-                for (int64_t p = b + G; p < e; p += G) {   // group-uniform
-                    const int64_t q = p + sub;
-                    const int32_t myv = q < e ? tgt_idx[q] : -1;
-                    const bool inf = myv >= 0 && bit(fa, myv);
-                    any_nf |= group_any<G>(myv >= 0 && (!skip_full || !bit(full, myv)));
-                    const u64 cd = inf ? fcode[myv] : 0ull;
-                    const bool sp = inf && code_n(cd) == 15;
-                    if (inf && !sp) code_or(rows[j], cd);
-                    unsigned sm2 = (unsigned)((__ballot(sp) >> base) & gmask);
-                    while (sm2) {
-                        const int kk = __ffs(sm2) - 1;
-                        sm2 &= sm2 - 1u;
-                        const int32_t vk = __shfl(myv, base + kk);
-                        racc |= V::ld(lvl + (int64_t)vk * W + sub * WPL);
-                    }
-                    nact += __popcll((__ballot(inf) >> base) & gmask);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            typename V::T a;
-            if constexpr (WPL == 1) a = rows[j][sub] | racc;
-            else a = u64x2{rows[j][2 * sub], rows[j][2 * sub + 1]} | racc;
-            const bool act = nact > 0 && any_nf;
-            const u64 cd = group_encode<W>(a, sub);
-            if (act) {
-                if (code_n(cd) == 15) V::st(lf + L * W + sub * WPL, a);
-                if (sub == 0) {
-                    lcode[L] = cd;
-                    ++n_links;
-                    n_pins += (u64)nact;
-                }
-            } else if (L < M && sub == 0) {
-                lcode[L] = 0ull;
-            }
-            word |= compress_groups<G>(__ballot(act), j * PER);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) la[tile] = word;
-    }
-    wave_add_sh(ctr + cActiveLinks, n_links);
-    wave_add_sh(ctr + cActivePins, n_pins);
-    wave_add_sh(ctr + cNfRows, n_spill);
-}
-
-// Light atoms (0 < deg <= kHeavyDegree) of a coded level, tile-staged: the wave loads the offsets of
-// its 64 atoms at once; every chunk of G incidence entries of the G atoms of a group is loaded
-// together (G independent loads per lane), then their codes, then merged into the atoms' LDS rows;
-// spilled links add their dense lf rows.  Then new = row & ~vis as in the dense pull.
-template <int W>
-__global__ void __launch_bounds__(256) hgx_atom_pull_coded(int64_t A, const int64_t* __restrict__ inc_off,
-                                                           const int32_t* __restrict__ inc_row,
-                                                           const u64* __restrict__ lf, const u64* __restrict__ lcode,
-                                                           u64* __restrict__ vis, u64* __restrict__ ever,
-                                                           u64* __restrict__ full, u64* __restrict__ lvl_next,
-                                                           u64* __restrict__ fa_next, u64* __restrict__ ctr, FullMask fm,
-                                                           int flags) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, PER = 64 / G;
-    typedef Vec<WPL> V;
-    __shared__ u64 lrow[4][PER][G][W];
-    const bool skip_full = flags & 4;
-    const int lane = threadIdx.x & 63, g = lane / G, sub = lane & (G - 1), base = lane & ~(G - 1), wv = threadIdx.x >> 6;
-    const u64 gmask = (1ull << G) - 1ull;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const typename V::T FULL = full_part<W>(fm, sub);
-    u64 (*rows)[W] = lrow[wv][g];
-    u64 n_inc = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0, n_spill = 0;
-    for (int64_t tile = wave; tile * 64 < A; tile += nwave) {
-        const u64 ever_w = ever[tile], full_w = full[tile];
-        const int64_t tme = tile * 64 + lane;
-        int64_t bme = 0;
-        int dme = 0;
-        if (tme < A && !(skip_full && ((full_w >> lane) & 1ull))) {
-            bme = inc_off[tme];
-            const int64_t d = inc_off[tme + 1] - bme;
-            dme = (d > 0 && d <= kHeavyDegree) ? (int)d : 0;
-        }
-        if (__ballot(dme > 0) == 0ull) {   // nothing to pull in this tile
-            if (lane == 0) fa_next[tile] = 0ull;
-            continue;
-        }
-        int64_t bj[G];
-        int dj[G];
-        int dmax = 0;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {   // atom j*PER + g of the tile
-            bj[j] = __shfl(bme, j * PER + g);
-            dj[j] = __shfl(dme, j * PER + g);
-            dmax = max(dmax, dj[j]);
-            for (int w = sub; w < W; w += G) rows[j][w] = 0ull;
-        }
-        for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, __shfl_xor(dmax, off));
-        __builtin_amdgcn_wave_barrier();
-        typename V::T racc[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) racc[j] = V::zero();
-        for (int c0 = 0; c0 < dmax; c0 += G) {   // wave-uniform
-            int32_t L[G];
-#pragma unroll
-            for (int j = 0; j < G; ++j) L[j] = c0 + sub < dj[j] ? inc_row[bj[j] + c0 + sub] : -1;
-            u64 code[G];
-#pragma unroll
-            for (int j = 0; j < G; ++j) code[j] = L[j] >= 0 ? lcode[L[j]] : 0ull;
-            unsigned spillm = 0;
-#pragma unroll
-            for (int j = 0; j < G; ++j) {
-                if (code_n(code[j]) == 15) spillm |= 1u << j;
-                else if (code[j]) code_or(rows[j], code[j]);
-            }
-            if (__ballot(spillm != 0u)) {   // wave-uniform: spilled links' dense rows
-#pragma unroll
-                for (int j = 0; j < G; ++j) {
-                    unsigned sm = (unsigned)((__ballot((spillm >> j) & 1u) >> base) & gmask);
-                    n_spill += (sub == 0) ? (u64)__popc(sm) : 0ull;
-                    while (sm) {   // group-uniform
-                        const int kk = __ffs(sm) - 1;
-                        sm &= sm - 1u;
-                        const int32_t Lk = __shfl(L[j], base + kk);
-                        racc[j] |= V::ld(lf + (int64_t)Lk * W + sub * WPL);
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        u64 new_w = 0, fullnew_w = 0;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            const int pos = j * PER + g;
-            const int64_t t = tile * 64 + pos;
-            const int dg = dj[j];
-            typename V::T a;
-            if constexpr (WPL == 1) a = rows[j][sub] | racc[j];
-            else a = u64x2{rows[j][2 * sub], rows[j][2 * sub + 1]} | racc[j];
-            if (sub == 0) n_inc += (u64)dg;
-            const bool hasacc = group_any<G>(V::nz(a));
-            const bool ev = (ever_w >> pos) & 1ull;
-            typename V::T old = V::zero();
-            if (dg > 0 && hasacc && ev) {
-                old = V::ld(vis + t * W + sub * WPL);
-                if (sub == 0) ++n_vis;
-            }
-            const typename V::T nw = a & ~old;
-            const bool isnew = dg > 0 && group_any<G>(V::nz(nw));
-            const bool becomes_full = isnew && group_all<G>(V::eq(old | nw, FULL));
-            if (isnew) {
-                V::st(lvl_next + t * W + sub * WPL, nw);
-                V::st(vis + t * W + sub * WPL, old | nw);
-                if (sub == 0) {
-                    ++n_new;
-                    n_full += becomes_full;
-                    n_newdeg += (u64)dg;
-                    if (!becomes_full) n_newdeg_nf += (u64)dg;
-                }
-            }
-            new_w |= compress_groups<G>(__ballot(isnew), j * PER);
-            fullnew_w |= compress_groups<G>(__ballot(becomes_full), j * PER);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-            fa_next[tile] = new_w;
-            if (new_w & ~ever_w) ever[tile] = ever_w | new_w;
-            if (fullnew_w) full[tile] = full_w | fullnew_w;
-        }
-    }
-    if (sub != 0) {
-        n_inc = 0;
-        n_vis = 0;
-    }
-    wave_add_sh(ctr + cNewFull, n_full);
-    wave_add_sh(ctr + cIncLight, n_inc);
-    wave_add_sh(ctr + cVisLight, n_vis);
-    wave_add_sh(ctr + cNewLight, n_new);
-    wave_add_sh(ctr + cNewAtoms, n_new);
-    wave_add_sh(ctr + cNewDeg, n_newdeg);
-    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
-    wave_add_sh(ctr + cNfRows, n_spill);
-}
-
-// Hub chunks of a coded level: every thread ORs the ids of its entries into a private row (register
-// words selected by compare, no LDS atomics: 256 threads ORing into 16 shared words serialised),
-// spilled links their dense rows; the block reduces by shuffles and LDS, one atomicOr per nonzero
-// word into the hub accumulator.
-template <int W>
-__global__ void __launch_bounds__(256) hgx_atom_pull_heavy_coded(const HeavyChunk* __restrict__ chunks,
-                                                                 const int32_t* __restrict__ inc_row,
-                                                                 const u64* __restrict__ lf,
-                                                                 const u64* __restrict__ lcode,
-                                                                 const u64* __restrict__ full,
-                                                                 u64* __restrict__ hubacc, u64* __restrict__ ctr,
-                                                                 int flags) {
-    __shared__ u64 red[4][W];
-    const HeavyChunk c = chunks[blockIdx.x];
-    if ((flags & 4) && bit(full, c.atom)) return;   // block-uniform
-    u64 row[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) row[w] = 0ull;
-    u64 n_inc = 0, n_spill = 0;
-    for (int64_t i0 = c.beg; i0 < c.end; i0 += 4 * blockDim.x) {
-        int32_t L[4];
-        u64 code[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t i = i0 + u * blockDim.x + threadIdx.x;
-            L[u] = i < c.end ? inc_row[i] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) code[u] = L[u] >= 0 ? lcode[L[u]] : 0ull;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (L[u] < 0) continue;
-            ++n_inc;
-            const int n = code_n(code[u]);
-            if (n == 15) {
-                ++n_spill;
-#pragma unroll
-                for (int w = 0; w < W; ++w) row[w] |= lf[(int64_t)L[u] * W + w];
-            } else {
-                for (int k = 0; k < n; ++k) {
-                    const int id = code_id(code[u], k);
-                    const u64 bm = 1ull << (id & 63);
-#pragma unroll
-                    for (int w = 0; w < W; ++w)
-                        if (w == (id >> 6)) row[w] |= bm;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < W; ++w)
-        for (int off = 32; off > 0; off >>= 1) row[w] |= (u64)__shfl_xor((long long)row[w], off);
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) red[threadIdx.x >> 6][w] = row[w];
-    }
-    __syncthreads();
-    if (threadIdx.x < W) {
-        const u64 x = red[0][threadIdx.x] | red[1][threadIdx.x] | red[2][threadIdx.x] | red[3][threadIdx.x];
-        if (x) atomicOr(hubacc + (int64_t)c.slot * W + threadIdx.x, x);
-    }
-    wave_add_sh(ctr + cIncHeavy, n_inc);
-    wave_add_sh(ctr + cNfRows, n_spill);
 }
 
 // Sparse levels: mark every (typed) link incident to a frontier atom.  One wave per frontier word:
@@ -2392,7 +2012,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
                                                               u64* __restrict__ ctr, FullMask fm, int relist,
                                                               u64* __restrict__ n_spent, u64* __restrict__ ticket,
                                                               u64* __restrict__ hout, u64 seq,
-                                                              u64* __restrict__ lcount, u64* __restrict__ fcode) {
+                                                              u64* __restrict__ lcount) {
     constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
     typedef Vec<WPL> V;
     const int64_t n = (int64_t)*n_clist;
@@ -2415,7 +2035,7 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     const typename V::T FULL = full_part<W>(fm, sub);
     // the consumed frontier list's counter: zero for the next level's candidates (chained levels)
     if (n_spent && blockIdx.x == 0 && threadIdx.x == 0) *n_spent = 0ull;
-    u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0, n_bits = 0;
+    u64 n_cand = 0, n_vis = 0, n_new = 0, n_newdeg = 0, n_newdeg_nf = 0, n_full = 0;
     for (int64_t k0 = grp - (grp % (64 / G)); k0 < n; k0 += ngrp) {   // wave-uniform trip count
         const int64_t k = k0 + (grp % (64 / G));
         const bool valid = k < n;
@@ -2429,14 +2049,6 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
         const bool isnew = group_any<G>(V::nz(nw));
         const bool becomes_full = group_all<G>(V::eq(old | nw, FULL));
         int64_t dg = 0;
-        if (fcode) {   // the new row's code for a coded next level (every lane: group shuffles)
-            const u64 code = group_encode<W>(valid && isnew ? nw : V::zero(), sub);
-            if (valid && isnew && sub == 0) fcode[t] = code;
-            int nb;
-            if constexpr (WPL == 1) nb = __popcll(nw);
-            else nb = __popcll(nw.x) + __popcll(nw.y);
-            if (valid && isnew) n_bits += (u64)nb;
-        }
         if (valid && isnew) {
             V::st(lvl_next + t * W + sub * WPL, nw);
             V::st(vis + t * W + sub * WPL, old | nw);
@@ -2473,7 +2085,6 @@ __global__ void __launch_bounds__(256) hgx_push_finalize_list(int32_t* __restric
     wave_add_sh(ctr + cNewAtoms, n_new);
     wave_add_sh(ctr + cNewDeg, n_newdeg);
     wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
-    if (fcode) wave_add_sh(ctr + cNewBits, n_bits);
     if (lcount && __syncthreads_or(n_new != 0)) {   // blocks that found no new atom skip the flush
         for (int j = threadIdx.x; j < W * 64; j += blockDim.x)
             if (lc[j]) atomicAdd(lcount + j, (u64)lc[j]);
@@ -4590,7 +4201,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64 new_global = 0, part_push = 0;
         u64* h = nullptr;
         hipEvent_t ev = nullptr;
-        bool codes = false;   // the level's finalise wrote codes of its new rows
         bool flag = false;    // counters in slot[0..cNum) once slot[cNum] == seq (mapped host memory)
         u64 seq = 0;
         u64* slot = nullptr;
@@ -4601,8 +4211,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     }
     int npend = 0;
     bool stop = false;
-    bool prev_codes = false;   // the last level read wrote the codes of its new rows
-    u64 prev_bits = 0, prev_new = 0;
     u64* cur_lvl = bt.lvl[0];
     u64* cur_fa = bt.fa[0];
     const bool pipe_ok = sparse_ok && !ex && MODE != kSym && (g->bfs_flags & 512);
@@ -4648,9 +4256,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                          (unsigned long long)h_new[cNewFull]);
         push_volume = h_new[cNewDeg];
         push_volume_nf = ex ? push_volume : h_new[cNewDegNF];
-        prev_codes = p.codes;
-        prev_bits = p.codes ? h_new[cNewBits] : 0;
-        prev_new = h_new[cNewAtoms];
         full_total += h_new[cNewFull];
         if (h_new[cNewAtoms] == 0) {
             g->release(p.lvl_next, row_bytes);
@@ -4676,8 +4281,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         u64* fa = cur_fa;
         const bool scratch_zero = scratch_clean;   // first level: n_fl / n_cl still zero from the prologue
         scratch_clean = false;
-        bool codes_written = false;   // this level's finalise wrote the codes of its new rows
-        bool coded = false;
         bool flag_level = false;   // counters written by the finalise into mapped host memory
         u64 flag_seq = 0;
         u64* flag_slot = nullptr;
@@ -4798,10 +4401,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 flag_slot = g->ctr_host + (size_t)(d & 1) * kHostSlot;
                 __atomic_store_n(flag_slot + cNum, (u64)0, __ATOMIC_RELEASE);
             }
-            if constexpr (MODE == kSym && Lay<W>::G >= 4) {   // codes for a coded next level
-                codes_written = !ex && g->coded != 0;
-                if (codes_written && !g->fcode) HGX_HIP(hipMalloc(&g->fcode, sizeof(u64) * (size_t)std::max<int64_t>(A, 1)));
-            }
             u64* lcount = nullptr;   // the new level's counts accumulated by the finalise (no exchange)
             if (!ex && bt.pcnt && d + 1 < kDirectLevels) {
                 lcount = bt.pcnt + (size_t)(d + 1) * 1024;
@@ -4809,8 +4408,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }
             hgx_push_finalize_list<W><<<512, 256, 0, s>>>(cl, n_cl, g->inc_off, acc, cand, vis, ever, full,
                                                            lvl_next, fa_next, c, fm, ex ? 0 : 1, ex ? nullptr : n_fl,
-                                                           ticket, flag_level ? flag_slot : nullptr, flag_seq, lcount,
-                                                           codes_written ? g->fcode : nullptr);
+                                                           ticket, flag_level ? flag_slot : nullptr, flag_seq, lcount);
             HGX_CHECK_LAUNCH();
             g->zacc_clean = true;   // every accumulated row is in the candidate list and re-zeroed
             cand_clean = true;
@@ -4841,22 +4439,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         // gather then writes a (zero) row for every link and the pull reads rows without probing la
         // -- one dependent load fewer per incidence chunk (HGX_OPT_BFS_FLAGS bit 7).
         if (v2 && (lflags & 128) && MODE == kSym && push_volume_nf >= 2 * (u64)M) lflags |= kAllRows;
-        // coded level: the previous level was a push level whose new rows carry <= 3 bits on average
-        // (their codes written by its finalise), HGX_OPT_CODED (2 = whenever the codes exist)
-        if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
-            coded = v2 && !ex && prev_codes && g->coded != 0 &&
-                    (g->coded == 2 || prev_bits <= 3 * std::max<u64>(prev_new, 1));
-            if (coded && !g->lcode) HGX_HIP(hipMalloc(&g->lcode, sizeof(u64) * (size_t)std::max<int64_t>(M, 1)));
-        }
         Events e1 = tm.start(kKindGather, d);
-        if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
-            if (coded)
-                hgx_link_gather_coded<W><<<gather_grid, block, 0, s>>>(M, g->tgt_off, g->tgt_idx, g->link_type,
-                                                                       want_type, fa, full, lvl, g->fcode, lf,
-                                                                       g->lcode, la, c, lflags);
-        }
         if constexpr (Lay<W>::G >= 4) {
-            if (v2 && !coded)
+            if (v2)
             {
                 if (lflags & kGatherO5)   // diagnostic A/B (bit 10)
                     hgx_link_gather2_o5<W, MODE == kSym><<<gather_grid, block, 0, s>>>(
@@ -4887,12 +4472,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         } else {
         Events e2 = tm.start(kKindPull, d);
         if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
-            if (coded)
-                hgx_atom_pull_coded<W><<<pull_grid, block, 0, s>>>(A, g->inc_off, g->inc_row, lf, g->lcode, vis, ever,
-                                                                   full, lvl_next, fa_next, c, fm, lflags);
-        }
-        if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
-            if (v2 && !coded)
+            if (v2)
             {
                 // two atoms of a group interleaved (152 VGPRs, 3 waves/SIMD): config 2 pull 5.73 -> 5.23 ms
                 // a step against four (184 VGPRs, 2 waves/SIMD, dropped in r02); a tile's atoms placed in
@@ -4914,11 +4494,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         tm.stop(e2);
         if (g->n_chunks > 0) {
             Events e3 = tm.start(kKindHeavy, d);
-            if (coded)
-                hgx_atom_pull_heavy_coded<W><<<(unsigned)g->n_chunks, block, 0, s>>>(g->chunks, g->inc_row, lf, g->lcode,
-                                                                                     full, hubacc, c, lflags);
-            else
-                hgx_atom_pull_heavy<W, MODE><<<(unsigned)g->n_chunks, block, 0, s>>>(
+            hgx_atom_pull_heavy<W, MODE><<<(unsigned)g->n_chunks, block, 0, s>>>(
                     g->chunks, g->inc_row, la, lf, g->tgt_off, g->tgt_idx, fa, lvl, vis, ever, full, hubacc, c, fm,
                     lflags, cd);
             HGX_CHECK_LAUNCH();
@@ -4946,8 +4522,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         pn.d = d;
         pn.lvl_next = lvl_next;
         pn.fa_next = fa_next;
-        pn.kind = nfp ? 3 : sparse ? (opush ? 2 : 1) : (coded ? 4 : 0);
-        pn.codes = codes_written;
+        pn.kind = nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;
         pn.allrows = (lflags & kAllRows) ? 1 : 0;
         pn.new_global = new_global;
         pn.part_push = part_push;
@@ -5431,8 +5006,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             const auto& c = level_ctr[before + d];
             // hgx_link_gather: tgt_off + tgt_idx (+ link_type) + frontier/full bitmaps + gathered rows
             //                  + lf writes + la words
-            const bool coded_level = c[cDirRows] == 4;   // rows of <= 6 bits moved as 8-byte codes
-            const bool sparse_level = c[cDirRows] != 0 && !coded_level;
+            const bool sparse_level = c[cDirRows] != 0;
             const double scan_links = sparse_level ? (double)c[cActiveLinks] : (double)M;
             const double scan_pins = sparse_level ? (double)c[cActivePins] : (double)P;
             double b_gather = 8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) +
@@ -5444,15 +5018,6 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                                   rowb * c[cIncLight] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] +
                                   3.0 * A / 8.0;
             const bool opush_level = c[cDirRows] == 2 || c[cDirRows] == 3;
-            if (coded_level) {
-                // gather: offsets + pins (+ types) + frontier / full bitmaps + an 8-byte code per frontier
-                // pin + a code per link + la words; pull: offsets + light incidence + a code per incidence +
-                // the spilled rows + vis reads + lvl / vis writes + bitmaps
-                b_gather = 8.0 * (M + 1) + 4.0 * P + (typed ? 4.0 * M : 0.0) + A / 4.0 + 8.0 * c[cActivePins] +
-                           8.0 * M + M / 8.0;
-                b_pull = 8.0 * (A + 1) + 4.0 * I_light + 8.0 * c[cIncLight] + rowb * c[cNfRows] +
-                         rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
-            }
             if (c[cDirRows] == 3) {   // non-full pull: no gather
                 b_gather = 0.0;
                 // full bitmap + inc_off of the listed atoms + list write/read + entries (inc_row, inc_type,
@@ -5475,8 +5040,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             r->stats.bytes_kernel[pull_kind] += b_pull;
             double b_heavy = 0, b_hub = 0;
             if (g->n_chunks > 0 && !sparse_level) {
-                b_heavy = coded_level ? 24.0 * g->n_chunks + 4.0 * I_heavy + 8.0 * c[cIncHeavy] + rowb * g->n_chunks
-                                      : 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
+                b_heavy = 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
                 b_hub = 4.0 * g->n_heavy + 2.0 * rowb * g->n_heavy + rowb * c[cAccHub] + 2.0 * rowb * c[cNewHub];
                 r->stats.bytes_kernel[HGX_K_PULL_HEAVY] += b_heavy;
                 r->stats.bytes_kernel[HGX_K_HUB_FINALIZE] += b_hub;

@@ -467,10 +467,6 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     if (g->inc_tgt) (void)hipFree(g->inc_tgt);   // inline target records of the old incidence
     g->inc_tgt = nullptr;
     g->inc_tgt_tried = false;
-    if (g->fcode) (void)hipFree(g->fcode);   // coded-level scratch, sized by the old A / M
-    g->fcode = nullptr;
-    if (g->lcode) (void)hipFree(g->lcode);
-    g->lcode = nullptr;
     g->n_pchunks = -1;
     g->zacc_bytes = 0;
     g->zacc_clean = false;

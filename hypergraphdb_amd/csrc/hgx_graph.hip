@@ -45,8 +45,6 @@ void graph_release(hgx_graph* g) {
     if (g->q_ticket) (void)hipFree(g->q_ticket);
     if (g->co_vis) (void)hipFree(g->co_vis);
     free_yield_lists(g);
-    if (g->fcode) (void)hipFree(g->fcode);
-    if (g->lcode) (void)hipFree(g->lcode);
     for (auto& b : g->seq_hbufs) (void)hipHostFree(b.p);
     g->seq_hbufs.clear();
     if (g->pinned) (void)hipHostFree(g->pinned);
@@ -316,7 +314,7 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
     c->seq_engine = g->seq_engine;
     c->bfs_block = g->bfs_block;
-    c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline; c->coded = g->coded;
+    c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline;
     c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused; c->push_inline = g->push_inline;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
     guard.c = nullptr;
@@ -520,8 +518,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: query flat mode outside 0..2");
         g->q_flat = (int32_t)value;
     } else if (option == HGX_OPT_CODED) {
-        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: coded mode outside 0..2");
-        g->coded = (int32_t)value;
+        // removed in round 5 (measured slower): only "off" is accepted
+        if (value != 0) fail(HGX_E_UNSUPPORTED, "hgx_set_option: HGX_OPT_CODED was removed (coded levels measured slower)");
     } else if (option == HGX_OPT_PUSH_BATCH) {
         if (value < 0 || value > 64) fail(HGX_E_INVALID, "hgx_set_option: push batch outside 0..64");
         g->push_batch = (int32_t)value;

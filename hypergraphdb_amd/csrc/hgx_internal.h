@@ -309,9 +309,6 @@ struct hgx_graph {
     size_t zc_in_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
-    int32_t coded = 0;                          // HGX_OPT_CODED: 0 off (default), 1 auto, 2 always when codes exist
-    unsigned long long* fcode = nullptr;        // [A] codes of a push level's new rows (coded next level)
-    unsigned long long* lcode = nullptr;        // [M] codes of a coded level's link rows
     int32_t push_batch = 0;                     // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
     int32_t q_flat = 2;                         // HGX_OPT_QUERY_FLAT: 2 single-pass (front-scan + match with look-back),
                                                 //   1 flat match + separate scan / finish / scatter, 0 per-query chunks

@@ -3633,7 +3633,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         status |= ctl[kLsStatus];
         if (status) {
             if (status & 16) return false;   // 32-bit level keys do not fit: the caller splits the chunk
-            if (attempt > 16) fail(HGX_E_DEVICE, "hgx_bfs_sequence: level-synchronous capacities did not converge");
+            // each attempt stops at the first level that overflows, so a tiny start (HGX_LS_SMALL) may need
+            // one attempt per capacity and level; the default starts converge in a few
+            if (attempt > 48) fail(HGX_E_DEVICE, "hgx_bfs_sequence: level-synchronous capacities did not converge");
             if (status & 1) g->ls_cap = std::min(full, cap * 4);
             if (status & 2) g->ls_rcap = rcap * 4;
             if (status & 4) g->ls_wcap = wcap * 4;
@@ -4078,6 +4080,10 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             ev_give(g, ev[1]);
         }
         const bool clean = hm[0] == 0 && hm[3] == 0;
+        static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
+        if (trace)
+            std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld\n", k,
+                         (long long)hm[0], (long long)hm[3], (long long)hm[1], (long long)hm[2]);
         if (!clean) {   // the bitmaps may hold bits no pair records: cleared whole
             if (hm[3] != 0) ++g->co_timeouts;
             HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));

@@ -474,10 +474,9 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * single-workgroup scan, finish and scatter (A/B); 0 = a wavefront per chunk of one query's
  * candidates (A/B). */
 #define HGX_OPT_QUERY_FLAT 9
-/* HGX_OPT_CODED (symmetric mode; default 0 = off, A/B): 1 = a dense level right after a push level
- * whose new rows carry <= 3 source bits on average moves rows of <= 6 bits as 64-bit codes (six 10-bit
- * source ids) instead of 128-byte rows; 2 = whenever the push level wrote codes (tests).  Exact, but
- * measured slower on config 2's level 1 (16.0 vs 9.0 ms, profiles/r02zn_*_c2_levels.log). */
+/* HGX_OPT_CODED: removed in round 5.  Coded dense levels (rows of <= 6 source bits as 64-bit codes) were
+ * exact but measured slower on config 2's level 1 (16.0 vs 9.0 ms, profiles/r02zn_*_c2_levels.log;
+ * DESIGN.md 3.1 item 8b).  hgx_set_option accepts 0 only (HGX_E_UNSUPPORTED otherwise). */
 #define HGX_OPT_CODED 10
 /* HGX_OPT_QUERY_COALESCE (default 1 = on): concurrent hgx_pattern_batch_packed calls on one graph
  * share device batches.  A caller that finds the device busy queues its batch; the next caller to

@@ -335,21 +335,24 @@ def test_push_inline_records_all_modes(inline):
         snap.close()
 
 
-@pytest.mark.parametrize("coded", [2, 0])
-def test_coded_levels(coded):
-    """HGX_OPT_CODED: a dense level after a push level moves rows of <= 6 source bits as 64-bit codes
-    (six 10-bit ids; more bits spill to the dense row).  Forced on (2) wherever the push level wrote
-    codes, and off (0): the oracle's per-depth sets on power-law hubs (heavy chunks), typed links,
-    links targeting links, repeated targets, 300 / 1024 / 2100 seeds and several flag sets."""
-    from hypergraphdb_amd import _lib, synth
+def test_rows_engine_flag_sets_and_removed_coded_option():
+    """The rows engine (HGX_OPT_BFS_BLOCK 0) under three flag sets against the oracle's per-depth sets on
+    power-law hubs (heavy chunks), typed links, links targeting links, repeated targets, 300 / 1024 / 2100
+    seeds and config 2 at 1%.  HGX_OPT_CODED (coded dense levels, measured slower and removed in round 5)
+    accepts only 0."""
+    from hypergraphdb_amd import HGXUnsupported, _lib, synth
     rng = np.random.default_rng(321)
     cases = [(synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=31), -1, 3, 1024),
              (synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=32), 1, None, 300),
              (K.random_graph(rng, 1500, 6000, max_arity=12, n_types=3), -1, None, 2100),
              (synth.config2(scale=0.01), -1, 4, 1024)]
-    for g, lt, maxd, ns in cases:
+    for ci, (g, lt, maxd, ns) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
-        snap.set_option(_lib.HGX_OPT_CODED, coded)
+        snap.set_option(_lib.HGX_OPT_CODED, 0)
+        if ci == 0:
+            for v in (1, 2):
+                with pytest.raises(HGXUnsupported):
+                    snap.set_option(_lib.HGX_OPT_CODED, v)
         snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
         seeds = rng.integers(0, g["num_atoms"], ns).astype(np.int32)
         for flags in (0x3BE, 0x3BA, 0x1BE):

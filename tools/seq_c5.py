@@ -53,7 +53,8 @@ def main():
             e[name] = {"batch_wall_ms": round(float(np.median(walls)) * 1e3, 3),
                        "batch_device_ms": round(float(np.median(devs)), 3), "pairs": pairs,
                        "traversed_items": r.traversed_edges, "ms_block": round(r.ms_block, 3),
-                       "seeds_block": r.n_block, "seeds_level": r.n_level,
+                       "seeds_block": r.n_block, "seeds_level": r.n_level, "seeds_grid": r.n_coop,
+                       "ms_grid": round(r.ms_coop, 3), "ms_level": round(r.ms_level, 3),
                        "single_ms_median": round(singles[len(singles) // 2] * 1e3, 4),
                        "single_ms_p90": round(singles[int(len(singles) * 0.9)] * 1e3, 4),
                        "single_ms_max": round(singles[-1] * 1e3, 4)}

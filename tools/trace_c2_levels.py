@@ -1,6 +1,6 @@
 """Per-level times / counters of one config-2 batch (HGX_BFS_TRACE=1 adds the engine's per-level lines).
 
-  python tools/trace_c2_levels.py [HGX_OPT_CODED value]
+  python tools/trace_c2_levels.py
 """
 import os, sys
 sys.path.insert(0, '/root/repo')
@@ -9,9 +9,6 @@ from hypergraphdb_amd import synth
 g = synth.config2()
 snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
 snap.set_timing(True)
-if len(sys.argv) > 1:   # HGX_OPT_CODED value
-    from hypergraphdb_amd import _lib
-    snap.set_option(_lib.HGX_OPT_CODED, int(sys.argv[1]))
 import time
 for _ in range(4):
     t0 = time.perf_counter()
