@@ -1278,7 +1278,6 @@ __device__ __forceinline__ void cand_flush(OPushLds& sh, int& cc, int32_t* __res
 template <int W, int MODE>
 __device__ __forceinline__ void opush_entry(int32_t v, int64_t i, bool have, const int32_t* __restrict__ inc_row,
                                             const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
-                                            const int4* __restrict__ itg,
                                             int nnz, OPushLds& sh, const u64* __restrict__ full,
                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
                                             u64* __restrict__ n_clist, u64* __restrict__ acc, u64& n_links,
@@ -1286,25 +1285,14 @@ __device__ __forceinline__ void opush_entry(int32_t v, int64_t i, bool have, con
     const int lane = threadIdx.x & 63;
     const u64 lt = (1ull << lane) - 1ull;
     // A row of <= kRegRow targets is held in registers and so are the full-bitmap words of its
-    // eligible targets; longer rows take the loop below.  With the inline records (itg: entry i's
-    // <= 8 targets in 32 bytes, -1 padded, slot 0 = -2 for a longer row) the row is one load at the
-    // entry's own position instead of three dependent ones (link row, target offsets, targets).
+    // eligible targets; longer rows take the loop below.  (Inline target records in incidence order --
+    // one load instead of link row, target offsets, targets -- measured no faster on config 5 and were
+    // removed in round 5: profiles/r03n_c5.log)
     constexpr int kRegRow = 8;
     int32_t tr[kRegRow];
     int64_t b = 0;
     int n = 0, fv = -1, lv = -1;
-    bool inl = false;
-    if (have && itg) {
-        const int4 r0 = itg[2 * i], r1 = itg[2 * i + 1];
-        if (r0.x != -2) {
-            inl = true;
-            tr[0] = r0.x; tr[1] = r0.y; tr[2] = r0.z; tr[3] = r0.w;
-            tr[4] = r1.x; tr[5] = r1.y; tr[6] = r1.z; tr[7] = r1.w;
-#pragma unroll
-            for (int k = 0; k < kRegRow; ++k) n += tr[k] >= 0;
-        }
-    }
-    if (have && !inl) {
+    if (have) {
         const int32_t L = inc_row[i];
         b = tgt_off[L];
         n = (int)(tgt_off[L + 1] - b);
@@ -1314,10 +1302,8 @@ __device__ __forceinline__ void opush_entry(int32_t v, int64_t i, bool have, con
         n_pins += (u64)n;
     }
     const bool reg = n <= kRegRow;
-    if (!inl) {
 #pragma unroll
-        for (int k = 0; k < kRegRow; ++k) tr[k] = (reg && k < n) ? tgt_idx[b + k] : -1;
-    }
+    for (int k = 0; k < kRegRow; ++k) tr[k] = (reg && k < n) ? tgt_idx[b + k] : -1;
     if (reg) {
 #pragma unroll
         for (int k = 0; k < kRegRow; ++k)
@@ -1403,7 +1389,6 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
                                             const int32_t* __restrict__ inc_type, int32_t want_type,
                                             const uint8_t* __restrict__ yf,
                                             const int64_t* __restrict__ tgt_off, const int32_t* __restrict__ tgt_idx,
-                                            const int4* __restrict__ itg,
                                             int nnz, OPushLds& sh, const u64* __restrict__ full,
                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
                                             u64* __restrict__ n_clist, u64* __restrict__ acc, u64& n_links,
@@ -1416,7 +1401,7 @@ __device__ __forceinline__ void opush_links(int32_t v, int64_t start, int64_t hi
         for (int k0 = 0; k0 < ne; k0 += 64) {   // wave-uniform
             const bool have = k0 + lane < ne;
             const int64_t i = have ? start + sh.ent[k0 + lane] : 0;
-            opush_entry<W, MODE>(v, i, have, inc_row, tgt_off, tgt_idx, itg, nnz, sh, full, cand, clist, n_clist, acc,
+            opush_entry<W, MODE>(v, i, have, inc_row, tgt_off, tgt_idx, nnz, sh, full, cand, clist, n_clist, acc,
                                  n_links, n_pins, n_pairs, cc);
         }
         __builtin_amdgcn_wave_barrier();
@@ -1567,7 +1552,7 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
                                                  u64* __restrict__ acc, u64* __restrict__ ctr,
                                                  u64* __restrict__ fa_next, int64_t n_words,
                                                  const HeavyChunk* __restrict__ chunks, int64_t n_chunks,
-                                                 const u64* __restrict__ fa, const int4* __restrict__ itg) {
+                                                 const u64* __restrict__ fa) {
     __shared__ OPushLds lds[4];
     OPushLds& sh = lds[threadIdx.x >> 6];
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1585,7 +1570,7 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
         const int nnz = row_words<W>(lvl, c.atom, sh);
         if (nnz == 0) continue;
         opush_links<W, MODE>(c.atom, c.beg + (threadIdx.x >> 6) * 64, c.end, 256, inc_row, inc_type, want_type, yf,
-                             tgt_off, tgt_idx, itg, nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs,
+                             tgt_off, tgt_idx, nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs,
                              n_scan, cc);
     }
     const int64_t n = (int64_t)*n_list;
@@ -1616,7 +1601,7 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
         if (v >= 0) {
             const int nnz = row_words_of(x, sh);
             if (nnz)
-                opush_links<W, MODE>(v, beg, end, 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx, itg, nnz, sh,
+                opush_links<W, MODE>(v, beg, end, 64, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx, nnz, sh,
                                      full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
         }
         v = vn;
@@ -1952,7 +1937,7 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
                                                        const u64* __restrict__ lvl, const u64* __restrict__ full,
                                                        u64* __restrict__ cand, int32_t* __restrict__ clist,
                                                        u64* __restrict__ n_clist, u64* __restrict__ acc,
-                                                       u64* __restrict__ ctr, const int4* __restrict__ itg) {
+                                                       u64* __restrict__ ctr) {
     __shared__ OPushLds lds[4];
     const HeavyChunk c = chunks[blockIdx.x];
     if (!bit(fa, c.atom)) return;   // block-uniform
@@ -1963,7 +1948,7 @@ __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restr
     u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
     int cc = 0;
     opush_links<W, MODE>(c.atom, c.beg + wib * 64, c.end, 256, inc_row, inc_type, want_type, yf, tgt_off, tgt_idx,
-                         itg, nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
+                         nnz, sh, full, cand, clist, n_clist, acc, n_links, n_pins, n_pairs, n_scan, cc);
     cand_flush(sh, cc, clist, n_clist);
     wave_add_sh(ctr + cActiveLinks, n_links);
     wave_add_sh(ctr + cActivePins, n_pins);
@@ -3537,39 +3522,6 @@ __global__ void __launch_bounds__(256) hgx_push_heavy_find(int64_t A, const int6
     }
 }
 
-// Inline target records of the incidence index (once per snapshot, for the frontier push): entry i
-// holds the <= 8 targets of link inc_row[i] in 32 bytes, -1 padded; slot 0 = -2 for a longer row,
-// which the push reads through tgt_off.  Skipped when it would take more than a quarter of the free
-// HBM (the push then reads every row through tgt_off).
-__global__ void __launch_bounds__(256) hgx_inc_inline(int64_t I, const int32_t* __restrict__ inc_row,
-                                                      const int64_t* __restrict__ tgt_off,
-                                                      const int32_t* __restrict__ tgt_idx, int4* __restrict__ out) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t L = inc_row[i];
-        const int64_t b = tgt_off[L];
-        const int n = (int)(tgt_off[L + 1] - b);
-        int32_t t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = k < n ? tgt_idx[b + k] : -1;
-        if (n > 8) t[0] = -2;
-        out[2 * i] = make_int4(t[0], t[1], t[2], t[3]);
-        out[2 * i + 1] = make_int4(t[4], t[5], t[6], t[7]);
-    }
-}
-
-void build_inc_targets(hgx_graph* g) {
-    g->inc_tgt_tried = true;
-    if (g->inc_tgt || g->I == 0) return;
-    const size_t bytes = (size_t)32 * (size_t)g->I;
-    size_t free_b = 0, total_b = 0;
-    HGX_HIP(hipMemGetInfo(&free_b, &total_b));
-    if (bytes > free_b / 4) return;
-    HGX_HIP(hipMalloc(&g->inc_tgt, bytes));
-    hgx_inc_inline<<<grid_for(g->I, 256, 65536), 256, 0, g->stream>>>(g->I, g->inc_row, g->tgt_off, g->tgt_idx,
-                                                                    (int4*)g->inc_tgt);
-    HGX_CHECK_LAUNCH();
-}
-
 // The frontier push's chunk table (once per snapshot): kPushChunk-entry chunks of every atom with
 // more than kPushLight incidences, in atom order.
 void build_push_chunks(hgx_graph* g) {
@@ -4323,7 +4275,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // frontier-driven push (mark candidates, zero their rows, OR rows, finalise): the ordered
             // modes always, the symmetric mode with HGX_OPT_BFS_FLAGS bit 5
             const bool pre_work = !g->zacc_clean || g->zacc_bytes < row_bytes || (MODE != kSym && !g->inc_yf) ||
-                                  g->n_pchunks < 0 || (g->push_inline && !g->inc_tgt_tried) || !cand_clean || !chained;
+                                  g->n_pchunks < 0 || !cand_clean || !chained;
             if (pre_work) tm.break_chain();
             if (!g->zacc_clean || g->zacc_bytes < row_bytes) {   // (re)establish the all-zero accumulator
                 if (g->zacc_bytes < row_bytes) {
@@ -4345,8 +4297,6 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }
             const uint8_t* yf = g->inc_yf;
             if (g->n_pchunks < 0) build_push_chunks(g);
-            if (g->push_inline && !g->inc_tgt_tried) build_inc_targets(g);
-            const int4* itg = g->push_inline ? (const int4*)g->inc_tgt : nullptr;   // HGX_OPT_PUSH_INLINE (A/B)
             // chained levels need no memset: the candidate words are zero-invariant, fa_next is cleared by
             // hgx_opush and n_cl by the previous finalise
             if (!cand_clean) HGX_HIP(hipMemsetAsync(cand, 0, bm_bytes, s));
@@ -4383,12 +4333,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                 hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
                                                          g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
                                                          fa_next, (int64_t)(bm_bytes / sizeof(u64)), g->pchunks,
-                                                         fold ? g->n_pchunks : 0, fa, itg);
+                                                         fold ? g->n_pchunks : 0, fa);
             HGX_CHECK_LAUNCH();
             if (!fold && g->n_pchunks > 0) {
                 hgx_opush_heavy<W, MODE><<<(unsigned)g->n_pchunks, 256, 0, s>>>(
                     g->pchunks, fa, g->inc_row, g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl, full, cand,
-                    cl, n_cl, acc, c, itg);
+                    cl, n_cl, acc, c);
                 HGX_CHECK_LAUNCH();
             }
             // finalise; re-zeroes the accumulator rows and candidate words it consumed and, without a
@@ -5281,7 +5231,6 @@ void hgx::bfs_shared_tables(hgx_graph* g) {
     }
     if (!g->inc_yf) ensure_inc_yield(g);
     if (g->n_pchunks < 0) build_push_chunks(g);
-    if (g->push_inline && !g->inc_tgt_tried) build_inc_targets(g);
     HGX_HIP(hipStreamSynchronize(s));
 }
 

@@ -464,9 +464,6 @@ int hgx_graph_update(hgx_graph* g, int64_t num_atoms, int64_t n_add, const int32
     g->co_vis_seeds = 0;
     if (g->pchunks) (void)hipFree(g->pchunks);
     g->pchunks = nullptr;
-    if (g->inc_tgt) (void)hipFree(g->inc_tgt);   // inline target records of the old incidence
-    g->inc_tgt = nullptr;
-    g->inc_tgt_tried = false;
     g->n_pchunks = -1;
     g->zacc_bytes = 0;
     g->zacc_clean = false;

@@ -39,7 +39,7 @@ void graph_release(hgx_graph* g) {
     HGX_FREE_OWN(link_atom); HGX_FREE_OWN(tgt_off); HGX_FREE_OWN(tgt_idx); HGX_FREE_OWN(link_type);
     HGX_FREE_OWN(inc_off); HGX_FREE_OWN(inc_row); HGX_FREE_OWN(inc_type); HGX_FREE_OWN(inc_ts_row);
     HGX_FREE_OWN(inc_ts_type); HGX_FREE_OWN(inc_ts_tgt); HGX_FREE_OWN(heavy_atom); HGX_FREE_OWN(chunks);
-    HGX_FREE_OWN(hasinc); HGX_FREE_OWN(inc_yf); HGX_FREE_OWN(pchunks); HGX_FREE_OWN(inc_tgt);
+    HGX_FREE_OWN(hasinc); HGX_FREE_OWN(inc_yf); HGX_FREE_OWN(pchunks);
 #undef HGX_FREE_OWN
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->q_ticket) (void)hipFree(g->q_ticket);
@@ -308,14 +308,13 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     c->n_heavy = g->n_heavy; c->I_heavy = g->I_heavy; c->n_chunks = g->n_chunks;
     c->heavy_atom = g->heavy_atom; c->chunks = g->chunks;
     c->hasinc = g->hasinc; c->inc_yf = g->inc_yf; c->pchunks = g->pchunks; c->n_pchunks = g->n_pchunks;
-    c->inc_tgt = g->inc_tgt; c->inc_tgt_tried = g->inc_tgt_tried;
     c->max_arity = g->max_arity; c->max_deg = g->max_deg;
     // the snapshot's options at this point (set separately on the context afterwards)
     c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
     c->seq_engine = g->seq_engine;
     c->bfs_block = g->bfs_block;
     c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline;
-    c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused; c->push_inline = g->push_inline;
+    c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
     guard.c = nullptr;
     *out = c;
@@ -533,7 +532,8 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: BFS block mode outside 0..2");
         g->bfs_block = (int32_t)value;
     } else if (option == HGX_OPT_PUSH_INLINE) {
-        g->push_inline = value != 0;
+        // removed in round 5 (measured no faster): only "off" is accepted
+        if (value != 0) fail(HGX_E_UNSUPPORTED, "hgx_set_option: HGX_OPT_PUSH_INLINE was removed (measured no faster)");
     } else if (option == HGX_OPT_QUERY_COALESCE) {
         if (value < 0 || value > (1 << 24)) fail(HGX_E_INVALID, "hgx_set_option: coalesce cap outside 0..2^24");
         g->q_coalesce = value != 0;

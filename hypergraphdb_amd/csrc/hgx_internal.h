@@ -264,9 +264,6 @@ struct hgx_graph {
     uint64_t* hasinc = nullptr;          // [A/64 + 1] bit set <=> inc(atom) non-empty (non-full pull levels)
     uint8_t* inc_yf = nullptr;           // [I] ordered-mode yield flags per incidence (frontier push), made on first use
     hgx::HeavyChunk* pchunks = nullptr;  // frontier push: kPushChunk-entry chunks of atoms with deg > kPushLight
-    int32_t* inc_tgt = nullptr;          // [I * 8] frontier push: inline <= 8 targets of each incidence entry's link
-    bool inc_tgt_tried = false;          //   (built on the first push level; absent when HBM is short)
-    int32_t push_inline = 0;             // HGX_OPT_PUSH_INLINE: the push reads the inline records (A/B, default off)
     int64_t n_pchunks = -1;              // -1 = not built yet
     size_t zacc_bytes = 0;
     bool zacc_clean = false;

@@ -1881,7 +1881,7 @@ constexpr int kLsSlotWords = 8;
 constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2,
               kLsBytes = kLsStatus + 3, kLsPullN = kLsStatus + 4;
 // status bits: 1 discoveries > cap, 2 runs > rcap, 4 key-space bitmap > wcap, 8 tiles > tcap, 16 keys wider
-// than 32 bits, 32 push hash too full, 64 frontier hash too full
+// than 32 bits, 32 push hash too full, 128 a pull pass's hit list overflowed (long rows: rerun pushing)
 // A level's discoveries go to kLsDSegs segments of the list, one counter each (a wave appends to the
 // segment of its block): one shared counter took one same-address atomic per wave and round, which
 // serialise at ~20 ns each -- the whole of a config-2 level's expand time.
@@ -1943,10 +1943,10 @@ struct LsArgs {
     u64* frow;                          // [A * W] frontier rows of the level (zero between levels)
     u64* ubit;                          // [A / 64 + 1] union of the level's frontier atoms (zero between levels)
     int32_t* ulist;                     // [cap] the union's atoms (the rows / bits to clear after the level)
-    u64* fkey;                          // frontier hash: (seed << 32 | atom) -> the item index of the first
-    uint32_t* fpre;                     //   item of that frontier entry (fmask + 1 slots, kLsEmpty keys
-    int64_t fmask;                      //   between levels)
-    int32_t fbits, hbits;               // log2 of the two hash tables' sizes
+    int32_t* uidx;                      // [A] the union atom's position in ulist (valid where ubit is set)
+    uint32_t* E;                        // [ecap] row u * nb + s: the item index of the first item of the frontier
+    int64_t ecap;                       //   entry (seed s, atom ulist[u]) -- a pull level needs F * nb <= ecap
+    int32_t hbits;                      // log2 of the push hash's size
     const HeavyChunk* chunks;           // heavy atoms' 4096-entry chunks (the graph's table)
     int64_t n_chunks, n_heavy;
     const int32_t* heavy_atom;          // [n_heavy]
@@ -2155,7 +2155,7 @@ __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
         sl[lsW] = W;
         sl[lsTiles] = (T + kLsTile - 1) / kLsTile;
         // pull when the level's items are a large part of the incidence (a pull reads all of it)
-        sl[lsPull] = a.pull == 2 || (a.pull == 1 && T * 8 > a.I) ? 1 : 0;
+        sl[lsPull] = (a.pull == 2 || (a.pull == 1 && T * 8 > a.I)) && F * (int64_t)a.nb <= a.ecap ? 1 : 0;
         if (sl[lsPull]) atomicAdd((unsigned long long*)&a.ctl[kLsPullN], 1ull);
         if (!a.y_off) atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
         int64_t st = 0;
@@ -2231,20 +2231,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
                 atomicOr((unsigned long long*)&a.frow[(int64_t)p * a.W + (s >> 6)], 1ull << (s & 63));
                 const u64 bit = 1ull << (p & 63);
                 first = !(atomicOr((unsigned long long*)&a.ubit[p >> 6], bit) & bit);
-                const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)p;
-                u64 h = ls_hash(key, a.fbits);
-                for (int probe = 0;; ++probe) {
-                    if (atomicCAS((unsigned long long*)&a.fkey[h], kLsEmpty, (unsigned long long)key) == kLsEmpty) {
-                        a.fpre[h] = (uint32_t)a.pre[i];
-                        break;
-                    }
-                    h = (h + 1) & (u64)a.fmask;
-                    if (probe >= kLsProbes) {   // the table is too full: grow and rerun
-                        atomicOr((unsigned long long*)&a.ctl[kLsStatus], 64ull);
-                        break;
-                    }
-                }
-                nbytes += 8 + 8 + 8 + 16;
+                nbytes += 8 + 8 + 8;
             }
             const u64 m = __ballot(first);
             if (m) {
@@ -2252,7 +2239,11 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
                 u64 base = 0;
                 if (lane == leader) base = atomicAdd((unsigned long long*)&sl[lsU], (unsigned long long)__popcll(m));
                 base = __shfl(base, leader);
-                if (first) a.ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = p;   // base + rank < F <= cap
+                if (first) {   // base + rank < F <= cap
+                    const int64_t u = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+                    a.ulist[u] = p;
+                    a.uidx[p] = (int32_t)u;
+                }
             }
         }
         ls_add_bytes(a, nbytes, ws);
@@ -2337,152 +2328,225 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     ls_add_bytes(a, nbytes, ws);
 }
 
-// Pull of one atom t's incidence range [eb, ee) by one wave (a lane per entry): the candidate values
-// of the seeds in need[] (t not examined by them) go into best[] (LDS, per seed) with atomicMin.  The
-// rules are the expand's: link predicate, minimum arity, the positions co-target p yields (3.2), the
-// yield rank k = t's best position among them (descending ranks in reverse order), and the item index
-// it = pre(s, p) + j(p, L) of the yield.
-__device__ __forceinline__ void lp_pair(const LsArgs& a, int32_t p, int32_t q, int32_t qt, int32_t n, int64_t tb,
-                                        int32_t la, u64* best, const u64* need, int64_t& nbytes) {
-    const u64 kq = (u64)(a.rev ? n - 1 - qt : qt);
-    const uint32_t j = (uint32_t)a.pin_j[tb + q];
-    nbytes += 4 + 8 * a.W;
-    for (int w = 0; w < a.W; ++w) {
-        u64 m = a.frow[(int64_t)p * a.W + w] & need[w];
-        while (m) {
-            const int s = w * 64 + __ffsll((long long)m) - 1;
-            m &= m - 1;
-            // pre(s, p): the frontier hash (the entry exists: frow says so)
-            const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)p;
-            u64 h = ls_hash(key, a.fbits);
-            while (a.fkey[h] != key) h = (h + 1) & (u64)a.fmask;
-            const u64 it = (u64)a.fpre[h] + j;
-            const u64 v = ((((it << a.kbits) | kq) + 1ull) << 32) | (u64)(uint32_t)la;
-            atomicMin((unsigned long long*)&best[s], (unsigned long long)v);
-            nbytes += 12;
-        }
-    }
+// Pull levels, after the expand launch built the rows and the union: E[uidx[p] * nb + s] = the item
+// index of the first item of seed s's frontier entry of p.
+__global__ void __launch_bounds__(256) hgx_lp_efill(LsArgs a, int32_t d) {
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || !sl[lsPull]) return;
+    const int64_t F = sl[lsF];
+    const int32_t* fa = a.fa[d & 1];
+    const int32_t* fs = a.fs[d & 1];
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < F; i += (int64_t)gridDim.x * 256)
+        a.E[(int64_t)a.uidx[fa[i]] * a.nb + fs[i]] = (uint32_t)a.pre[i];
 }
 
-__device__ void lp_range(const LsArgs& a, int32_t t, int64_t eb, int64_t ee, u64* best, const u64* need,
-                         int64_t& nbytes) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t e = eb + lane; e < ee; e += 64) {
-        if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {                       // linkPredicate (:300)
-            nbytes += 4;
-            continue;
+// A pull hit: co-target p (union slot u) of link L yields atom t at rank kq with item offset j.
+struct LpHit {
+    int32_t p, u;
+    uint32_t j;
+    int32_t la_kq;   // link atom (the value's low word) -- kq kept beside it
+    uint32_t kq;
+};
+constexpr int kLpHits = 64 * 8;   // one pass of a wave over <= 64 entries of <= 8 targets
+
+// Phase A of a pull pass (a lane per entry e of t): every co-target p of e's link that is on some
+// seed's frontier and yields t (the expand's rules: link predicate, minimum arity, p's first
+// occurrence, the mode's positions (3.2), t's best yielded position) becomes a hit in the wave's LDS
+// list.  Long rows (> 8 targets) from memory.
+__device__ __forceinline__ void lp_hits(const LsArgs& a, int32_t t, int64_t e, bool have, LpHit* hits, int* nh,
+                                        int64_t& nbytes) {
+    if (!have) return;
+    if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {   // linkPredicate (:300)
+        nbytes += 4;
+        return;
+    }
+    const int32_t L = a.inc_row[e];
+    const int64_t tb = a.tgt_off[L];
+    const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
+    nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
+    if (n < a.min_arity) return;   // minArity (:309)
+    nbytes += 4 * (int64_t)n + 4;
+    const int32_t la = a.link_atom[L];
+    auto add = [&](int32_t p, int32_t q, int32_t qt) {
+        const int k = atomicAdd(nh, 1);
+        if (k >= kLpHits) {   // only rows of more than 8 targets can fill the list: the chunk reruns pushing
+            atomicOr((unsigned long long*)&a.ctl[kLsStatus], 128ull);
+            return;
         }
-        const int32_t L = a.inc_row[e];
-        const int64_t tb = a.tgt_off[L];
-        const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
-        nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
-        if (n < a.min_arity) continue;                                                 // minArity (:309)
-        nbytes += 4 * (int64_t)n + 4;
-        const int32_t la = a.link_atom[L];
-        if (n <= 8) {   // the row in registers
-            int32_t tg[8];
+        LpHit h;
+        h.p = p;
+        h.u = a.uidx[p];
+        h.j = (uint32_t)a.pin_j[tb + q];
+        h.la_kq = la;
+        h.kq = (uint32_t)(a.rev ? n - 1 - qt : qt);
+        hits[k] = h;
+        nbytes += 8;
+    };
+    if (n <= 8) {   // the row in registers
+        int32_t tg[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
-            u64 onf[8];   // union bits of the co-targets, loaded together
+        for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
+        u64 onf[8];   // union bits of the co-targets, loaded together
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                onf[q] = (q < n && tg[q] != t) ? a.ubit[tg[q] >> 6] >> (tg[q] & 63) : 0ull;
-            nbytes += 8 * (int64_t)n;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
-                const int32_t p = tg[q];
-                bool dup = false;                 // p's first occurrence only
-#pragma unroll
-                for (int q2 = 0; q2 < q; ++q2) dup |= tg[q2] == p;
-                if (dup) continue;
-                int32_t lp = q;
-#pragma unroll
-                for (int q2 = q + 1; q2 < 8; ++q2)
-                    if (tg[q2] == p) lp = q2;
-                int32_t lo = 0, hi = n;           // positions p yields (3.2)
-                if (a.mode == sAfterFirst) lo = q + 1;
-                else if (a.mode == sBeforeFirst) hi = q;
-                else if (a.mode == sBeforeLast) hi = lp;
-                else if (a.mode == sAfterLast) lo = lp + 1;
-                int32_t qt = -1;                  // t's best yielded position
-#pragma unroll
-                for (int q2 = 0; q2 < 8; ++q2)
-                    if (q2 >= lo && q2 < hi && tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
-                if (qt < 0) continue;
-                lp_pair(a, p, q, qt, n, tb, la, best, need, nbytes);
-            }
-            continue;
-        }
+        for (int q = 0; q < 8; ++q) onf[q] = (q < n && tg[q] != t) ? a.ubit[tg[q] >> 6] >> (tg[q] & 63) : 0ull;
         nbytes += 8 * (int64_t)n;
-        for (int32_t q = 0; q < n; ++q) {   // long rows: from memory
-            const int32_t p = a.tgt_idx[tb + q];
-            if (p == t) continue;
-            if (!((a.ubit[p >> 6] >> (p & 63)) & 1ull)) continue;
-            bool dup = false;
-            for (int32_t q2 = 0; q2 < q; ++q2) dup |= a.tgt_idx[tb + q2] == p;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
+            const int32_t p = tg[q];
+            bool dup = false;   // p's first occurrence only
+#pragma unroll
+            for (int q2 = 0; q2 < q; ++q2) dup |= tg[q2] == p;
             if (dup) continue;
             int32_t lp = q;
-            for (int32_t q2 = q + 1; q2 < n; ++q2)
-                if (a.tgt_idx[tb + q2] == p) lp = q2;
-            int32_t lo = 0, hi = n;
+#pragma unroll
+            for (int q2 = q + 1; q2 < 8; ++q2)
+                if (tg[q2] == p) lp = q2;
+            int32_t lo = 0, hi = n;   // positions p yields (3.2)
             if (a.mode == sAfterFirst) lo = q + 1;
             else if (a.mode == sBeforeFirst) hi = q;
             else if (a.mode == sBeforeLast) hi = lp;
             else if (a.mode == sAfterLast) lo = lp + 1;
-            int32_t qt = -1;
-            for (int32_t q2 = lo; q2 < hi; ++q2)
-                if (a.tgt_idx[tb + q2] == t && (qt < 0 || a.rev)) qt = q2;
-            if (qt < 0) continue;
-            lp_pair(a, p, q, qt, n, tb, la, best, need, nbytes);
+            int32_t qt = -1;   // t's best yielded position
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2)
+                if (q2 >= lo && q2 < hi && tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
+            if (qt >= 0) add(p, q, qt);
         }
+        return;
+    }
+    nbytes += 8 * (int64_t)n;
+    for (int32_t q = 0; q < n; ++q) {   // long rows: from memory, hits in batches of the list
+        const int32_t p = a.tgt_idx[tb + q];
+        if (p == t || !((a.ubit[p >> 6] >> (p & 63)) & 1ull)) continue;
+        bool dup = false;
+        for (int32_t q2 = 0; q2 < q; ++q2) dup |= a.tgt_idx[tb + q2] == p;
+        if (dup) continue;
+        int32_t lp = q;
+        for (int32_t q2 = q + 1; q2 < n; ++q2)
+            if (a.tgt_idx[tb + q2] == p) lp = q2;
+        int32_t lo = 0, hi = n;
+        if (a.mode == sAfterFirst) lo = q + 1;
+        else if (a.mode == sBeforeFirst) hi = q;
+        else if (a.mode == sBeforeLast) hi = lp;
+        else if (a.mode == sAfterLast) lo = lp + 1;
+        int32_t qt = -1;
+        for (int32_t q2 = lo; q2 < hi; ++q2)
+            if (a.tgt_idx[tb + q2] == t && (qt < 0 || a.rev)) qt = q2;
+        if (qt >= 0) add(p, q, qt);
     }
 }
 
-// Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its waves' minima merged and lowered
-// into hbest with one global atomicMin per seed), then the light atoms (a wave each, its discoveries
-// appended right away).  LDS: 4 waves x nb values (dynamic).
+// Phase B (a lane per seed: seed w * 64 + lane in register best[w]): every hit's candidate value for
+// the seeds that have p on their frontier and t not examined -- one broadcast frontier-row word and one
+// coalesced E row per hit, four hits in flight.
+template <int WW>
+__device__ __forceinline__ void lp_minima(const LsArgs& a, const LpHit* hits, int nh, const u64* needbits, u64* best,
+                                          int64_t& nbytes) {
+    const int lane = threadIdx.x & 63;
+    for (int h0 = 0; h0 < nh; h0 += 4) {   // wave-uniform
+#pragma unroll
+        for (int w = 0; w < WW; ++w) {
+            if (w >= a.W) break;
+            const int s = w * 64 + lane;
+            u64 fw[4];
+            uint32_t pre[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                fw[q] = 0ull;
+                pre[q] = 0u;
+                if (h0 + q < nh) {
+                    const LpHit& H = hits[h0 + q];
+                    fw[q] = a.frow[(int64_t)H.p * a.W + w];
+                    if (s < a.nb) pre[q] = a.E[(int64_t)H.u * a.nb + s];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (h0 + q >= nh) break;
+                if (!(((fw[q] & needbits[w]) >> lane) & 1ull)) continue;
+                const LpHit& H = hits[h0 + q];
+                const u64 it = (u64)pre[q] + H.j;
+                const u64 v = ((((it << a.kbits) | H.kq) + 1ull) << 32) | (u64)(uint32_t)H.la_kq;
+                best[w] = min(best[w], v);
+            }
+        }
+        nbytes += lane == 0 ? (int64_t)min(4, nh - h0) * (8 * a.W + 4 * (int64_t)a.nb) : 0;
+    }
+}
+
+// One wave pulls entries [eb, ee) of atom t: phase A over 64 entries at a time, phase B over its hits.
+template <int WW>
+__device__ __forceinline__ void lp_pull_range(const LsArgs& a, int32_t t, int64_t eb, int64_t ee, LpHit* hits,
+                                              int* nh, const u64* needbits, u64* best, int64_t& nbytes) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = eb; e0 < ee; e0 += 64) {   // wave-uniform
+        if (lane == 0) *nh = 0;
+        __builtin_amdgcn_wave_barrier();
+        lp_hits(a, t, e0 + lane, e0 + lane < ee, hits, nh, nbytes);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int n = min(*nh, kLpHits);
+        lp_minima<WW>(a, hits, n, needbits, best, nbytes);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its waves' minima merged through LDS
+// and lowered into hbest with one global atomicMin per seed), then the light atoms (a wave each, its
+// discoveries appended right away).  WW: row words rounded up to a power of two (register minima).
+template <int WW>
 __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
-    extern __shared__ u64 lp_best[];   // [4][nb]
-    __shared__ u64 lp_need[4][kLsMaxW];
+    extern __shared__ u64 lp_merge[];   // [4][nb]
+    __shared__ LpHit lp_hits_l[4][kLpHits];
+    __shared__ int lp_nh[4];
     __shared__ int64_t ws[4];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus] || !sl[lsPull]) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = a.nb, W = a.W;
-    u64* best = lp_best + (int64_t)wave * nb;
-    u64* need = lp_need[wave];
-    for (int s = lane; s < nb; s += 64) best[s] = ~0ull;
+    LpHit* hits = lp_hits_l[wave];
+    int* nh = &lp_nh[wave];
     const u64 lastmask = (nb & 63) ? (1ull << (nb & 63)) - 1ull : ~0ull;
+    u64 best[WW], needbits[WW];
+#pragma unroll
+    for (int w = 0; w < WW; ++w) best[w] = ~0ull;
     int64_t nbytes = 0;
     // heavy chunks
-    for (int64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
+    for (int64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {   // block-uniform
         const HeavyChunk ch = a.chunks[c];
         const int32_t t = ch.atom;
-        if (lane < W) {
-            const u64 v = ~a.vis[(int64_t)t * W + lane];
-            need[lane] = lane == W - 1 ? v & lastmask : v;
-        }
-        __builtin_amdgcn_wave_barrier();
         u64 any = 0;
-        for (int w = 0; w < W; ++w) any |= need[w];
+#pragma unroll
+        for (int w = 0; w < WW; ++w) {
+            needbits[w] = 0ull;
+            if (w < W) {
+                const u64 v = ~a.vis[(int64_t)t * W + w];
+                needbits[w] = w == W - 1 ? v & lastmask : v;
+                any |= needbits[w];
+            }
+        }
         nbytes += lane == 0 ? 24 + 8 * W : 0;
-        if (any) {
+        if (any) {   // uniform over the block (same atom)
             const int64_t q = (ch.end - ch.beg + 3) / 4;
             const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
-            lp_range(a, t, b, e, best, need, nbytes);
+            lp_pull_range<WW>(a, t, b, e, hits, nh, needbits, best, nbytes);
         }
+#pragma unroll
+        for (int w = 0; w < WW; ++w)
+            if (w < W && w * 64 + lane < nb) lp_merge[(int64_t)wave * nb + w * 64 + lane] = best[w];
         __syncthreads();
         for (int s = threadIdx.x; s < nb; s += 256) {   // the four waves' minima -> the heavy atom's row
-            u64 v = lp_best[s];
+            u64 v = lp_merge[s];
 #pragma unroll
-            for (int k = 1; k < 4; ++k) v = min(v, lp_best[(int64_t)k * nb + s]);
+            for (int k = 1; k < 4; ++k) v = min(v, lp_merge[(int64_t)k * nb + s]);
             if (v != ~0ull) {
                 atomicMin((unsigned long long*)&a.hbest[(int64_t)ch.slot * nb + s], (unsigned long long)v);
-                for (int k = 0; k < 4; ++k) lp_best[(int64_t)k * nb + s] = ~0ull;
                 nbytes += 8;
             }
         }
+#pragma unroll
+        for (int w = 0; w < WW; ++w) best[w] = ~0ull;
         __syncthreads();
     }
     // light atoms: a wave takes 64 consecutive atoms (a lane each: degree and examined row), then pulls
@@ -2510,22 +2574,23 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
             const int l0 = __ffsll((long long)m) - 1;
             const int32_t tt = (int32_t)(t0 + l0);
             const int64_t b = __shfl(eb, l0), e = __shfl(ee, l0);
-            if (lane < W) {
-                const u64 v = ~a.vis[(int64_t)tt * W + lane];
-                need[lane] = lane == W - 1 ? v & lastmask : v;
+#pragma unroll
+            for (int w = 0; w < WW; ++w) {
+                needbits[w] = 0ull;
+                if (w < W) {
+                    const u64 v = ~a.vis[(int64_t)tt * W + w];
+                    needbits[w] = w == W - 1 ? v & lastmask : v;
+                }
             }
-            __builtin_amdgcn_wave_barrier();
-            lp_range(a, tt, b, e, best, need, nbytes);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            for (int w = 0; w < W; ++w) {   // the atom's discoveries: a lane per seed
+            lp_pull_range<WW>(a, tt, b, e, hits, nh, needbits, best, nbytes);
+#pragma unroll
+            for (int w = 0; w < WW; ++w) {   // the atom's discoveries: a lane per seed
+                if (w >= W) break;
                 const int s = w * 64 + lane;
-                const u64 v = s < nb ? best[s] : ~0ull;
-                const bool isnew = v != ~0ull;
-                if (isnew) best[s] = ~0ull;
-                ls_append(a, d, isnew, (int64_t)s * a.A + tt, v);
+                const bool isnew = s < nb && best[w] != ~0ull;
+                ls_append(a, d, isnew, (int64_t)s * a.A + tt, best[w]);
+                best[w] = ~0ull;
             }
-            __builtin_amdgcn_wave_barrier();
         }
     }
     ls_add_bytes(a, nbytes, ws);
@@ -2579,17 +2644,6 @@ __global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
             const int32_t p = a.ulist[u];
             for (int w = 0; w < a.W; ++w) a.frow[(int64_t)p * a.W + w] = 0ull;
             a.ubit[p >> 6] = 0ull;
-        }
-        // the frontier hash: each entry finds its own key (still there: only its owner clears it) and
-        // clears that slot, so the table is empty again after F probes, not a pass over every slot
-        const int64_t F = sl[lsF];
-        const int32_t* fa = a.fa[d & 1];
-        const int32_t* fs = a.fs[d & 1];
-        for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < F; i += (int64_t)gridDim.x * 256) {
-            const u64 key = (u64)(uint32_t)fs[i] << 32 | (u64)(uint32_t)fa[i];
-            u64 h = ls_hash(key, a.fbits);
-            for (int64_t probe = 0; probe <= a.fmask && a.fkey[h] != key; ++probe) h = (h + 1) & (u64)a.fmask;
-            if (a.fkey[h] == key) a.fkey[h] = kLsEmpty;
         }
     }
 }
@@ -3471,6 +3525,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     const int32_t W = (nb + 63) / 64;
     if (W > kLsMaxW) fail(HGX_E_INVALID, "hgx_bfs_sequence: a level-engine chunk holds at most 1024 seeds");
     const int pull = ya ? 0 : pull_env;
+    bool pull_off = false;   // set when a pull pass overflowed its hit list (rows of > 8 targets)
     const int32_t* pin_j = pull ? ensure_pin_j(g) : nullptr;
     hgx_graph* root = g->base ? g->base : g;
     if (!g->seq_flag) {   // mapped, coherent: the emit kernel's level sizes (once per graph)
@@ -3491,7 +3546,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         const int64_t tcap = std::max<int64_t>(g->ls_tcap, small ? 8 : (int64_t)1 << 16);
         const int64_t rcap = std::max<int64_t>(g->ls_rcap, small ? 4 : (int64_t)1 << 14);
         const int hbits = std::max<int>(log2_ceil(std::max<int64_t>(g->ls_hcap, small ? 64 : (int64_t)1 << 21)), 6);
-        const int fbits = std::max<int>(log2_ceil(std::max<int64_t>(g->ls_fcap, small ? 64 : (int64_t)1 << 16)), 6);
         LsArgs a{};
         a.A = A;
         a.inc_off = g->inc_off;
@@ -3546,17 +3600,16 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.hmask = ((int64_t)1 << hbits) - 1;
         a.hkey = (u64*)w.take(sizeof(u64) << hbits);
         a.hval = (u64*)w.take(sizeof(u64) << hbits);
-        a.pull = pull;
+        a.pull = pull_off ? 0 : pull;
         a.I = g->I;
         a.pin_j = pin_j;
-        if (pull) {
+        if (a.pull) {
             a.frow = (u64*)w.take(rows);
             a.ubit = (u64*)w.take(sizeof(u64) * (size_t)(A / 64 + 1));
             a.ulist = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
-            a.fbits = fbits;
-            a.fmask = ((int64_t)1 << fbits) - 1;
-            a.fkey = (u64*)w.take(sizeof(u64) << fbits);
-            a.fpre = (uint32_t*)w.take(sizeof(uint32_t) << fbits);
+            a.uidx = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1));
+            a.ecap = std::min<int64_t>(std::max<int64_t>(cap, nb) * nb, (int64_t)1 << 28);   // <= 1 GB of rows
+            a.E = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)a.ecap);
             a.chunks = root->chunks;
             a.n_chunks = root->n_chunks;
             a.n_heavy = root->n_heavy;
@@ -3564,7 +3617,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             a.hbest = (u64*)w.take(sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1));
             HGX_HIP(hipMemsetAsync(a.frow, 0, rows, st));
             HGX_HIP(hipMemsetAsync(a.ubit, 0, sizeof(u64) * (size_t)(A / 64 + 1), st));
-            HGX_HIP(hipMemsetAsync(a.fkey, 0xFF, sizeof(u64) << fbits, st));
             HGX_HIP(hipMemsetAsync(a.hbest, 0xFF, sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1), st));
         }
         int32_t* dseeds = (int32_t*)w.take(sizeof(int32_t) * (size_t)nb);
@@ -3588,8 +3640,13 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d, 0);
             hgx_ls_prefix<<<kLsG, 256, 0, st>>>(a, d);
             hgx_ls_expand<<<1024, 256, 0, st>>>(a, d);
-            if (pull) {
-                hgx_lp_pull<<<2048, 256, lp_smem, st>>>(a, d);
+            if (a.pull) {
+                hgx_lp_efill<<<512, 256, 0, st>>>(a, d);
+                if (W <= 1) hgx_lp_pull<1><<<2048, 256, lp_smem, st>>>(a, d);
+                else if (W <= 2) hgx_lp_pull<2><<<2048, 256, lp_smem, st>>>(a, d);
+                else if (W <= 4) hgx_lp_pull<4><<<2048, 256, lp_smem, st>>>(a, d);
+                else if (W <= 8) hgx_lp_pull<8><<<2048, 256, lp_smem, st>>>(a, d);
+                else hgx_lp_pull<16><<<2048, 256, lp_smem, st>>>(a, d);
                 hgx_lp_hfinal<<<256, 256, 0, st>>>(a, d);
             }
             hgx_ls_bits<<<512, 256, 0, st>>>(a, d);
@@ -3641,7 +3698,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             if (status & 4) g->ls_wcap = wcap * 4;
             if (status & 8) g->ls_tcap = tcap * 4;
             if (status & 32) g->ls_hcap = ((int64_t)1 << hbits) * 4;
-            if (status & 64) g->ls_fcap = ((int64_t)1 << fbits) * 4;
+            if (status & 128) pull_off = true;   // a pull pass's hit list overflowed: this call pushes
             continue;   // rerun the chunk with the grown capacities (kept on the graph)
         }
         const int64_t nruns = ctl[kLsRuns];

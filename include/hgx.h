@@ -485,12 +485,9 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * compiled queries (QueryCompilation.java:76-122).  Results and errors are exactly those of separate
  * calls (a batch whose merged run reports a bad or unsupported query is re-run on its own).  0 = off. */
 #define HGX_OPT_QUERY_COALESCE 11
-/* HGX_OPT_PUSH_INLINE (A/B, default 0): 1 = frontier-push levels read each incidence entry's link
- * targets from inline 32-byte records in incidence order (built on the first push level with the
- * option on: 32 bytes per incidence entry, skipped when that exceeds a quarter of the free HBM) -- one
- * load at the entry's own position instead of three dependent ones.  Measured no faster on config 5
- * (2.14-2.25 against 2.16-2.17 ms per concurrent step, profiles/r03n_c5.log: the rows of a graph that
- * size are cache hits), so the default saves the memory. */
+/* HGX_OPT_PUSH_INLINE: removed in round 5.  Inline target records in incidence order for the frontier
+ * push measured no faster on config 5 (profiles/r03n_c5.log) and cost 32 bytes per incidence entry.
+ * hgx_set_option accepts 0 only (HGX_E_UNSUPPORTED otherwise). */
 #define HGX_OPT_PUSH_INLINE 12
 /* HGX_OPT_SEQ_ENGINE (default 0): how hgx_bfs_sequence runs.  0 = one workgroup per seed with the
  * whole traversal in LDS (hash of the examined atoms, frontier and discovery ranks on chip, pairs

@@ -308,20 +308,22 @@ def test_push_batch_all_modes(batch):
             check_batch(g, seeds, maxd, mode, lt, snap, orc)
 
 
-@pytest.mark.parametrize("inline", [1, 0])
-def test_push_inline_records_all_modes(inline):
-    """HGX_OPT_PUSH_INLINE: the frontier push reading each incidence entry's targets from the inline
-    32-byte records (1) or through tgt_off (0) gives the oracle's per-depth sets in every generator
-    mode: rows longer than 8 targets (the records' fallback), typed links, power-law hubs (chunked
-    push), links targeting links, and the config-5 ontology in both subsumption directions."""
-    from hypergraphdb_amd import _lib, synth
+def test_frontier_push_all_modes():
+    """The frontier push (rows engine) gives the oracle's per-depth sets in every generator mode: rows
+    longer than 8 targets (the loop past the register row), typed links, power-law hubs (chunked push),
+    links targeting links, and the config-5 ontology in both subsumption directions.  HGX_OPT_PUSH_INLINE
+    (inline target records, measured no faster, removed in round 5) accepts only 0."""
+    from hypergraphdb_amd import HGXUnsupported, _lib, synth
     rng = np.random.default_rng(93)
     cases = [(K.random_graph(rng, 600, 2500, max_arity=12, n_types=3), -1, None, 300),
              (synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=19), 1, 3, 1024),
              (synth.config5(scale=0.002, n_sources=500), None, None, 500)]
     for gi, (g, lt, maxd, ns) in enumerate(cases):
         snap, orc = snapshot(g), oracle(g)
-        snap.set_option(_lib.HGX_OPT_PUSH_INLINE, inline)
+        snap.set_option(_lib.HGX_OPT_PUSH_INLINE, 0)
+        if gi == 0:
+            with pytest.raises(HGXUnsupported):
+                snap.set_option(_lib.HGX_OPT_PUSH_INLINE, 1)
         snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
         if gi == 2:
             lt = int(g["subsumes_type"])

@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="both", choices=("both", "serial", "concurrent"))
     ap.add_argument("--timing", action="store_true", help="device events per level (adds event records)")
-    ap.add_argument("--inline", type=int, default=-1, help="HGX_OPT_PUSH_INLINE A/B (-1: engine default, off)")
     ap.add_argument("--split", type=int, default=1,
                     help="concurrent mode: each direction's sources in this many batches, each on its own context")
     args = ap.parse_args()
@@ -34,9 +33,6 @@ def main():
     g = synth.config5(scale=args.scale, n_sources=1024)
     snap = H.HyperGraphSnapshot(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"])
     snap.set_timing(args.timing)
-    if args.inline >= 0:   # before the contexts are made: they take the snapshot's options
-        from hypergraphdb_amd import _lib
-        snap.set_option(_lib.HGX_OPT_PUSH_INLINE, args.inline)
     K = max(1, args.split)
     views = [snap] + [snap.context() for _ in range(2 * K - 1)]
     T = g["subsumes_type"]
@@ -60,7 +56,7 @@ def main():
         # per direction: closure atoms summed over the source batches, the batches' stats
         return [(sum(res[j][0] for j in range(d, 2 * K, 2)), res[d][1]) for d in (0, 1)]
 
-    out = {"tool": "tools/c5_step.py", "scale": args.scale, "steps": args.steps, "split": K, "inline": args.inline}
+    out = {"tool": "tools/c5_step.py", "scale": args.scale, "steps": args.steps, "split": K}
     modes = {"both": (False, True), "serial": (False,), "concurrent": (True,)}[args.mode]
     ref = None
     for conc in modes:
