@@ -1907,6 +1907,7 @@ struct LsArgs {
     int32_t want_type, min_arity, mode, rev, kbits;
     int64_t t_limit;                    // largest item count of a level with 32-bit keys
     int32_t nb, W;                      // seeds of the chunk, row words
+    int32_t maxd;                       // depth limit (the last level's discoveries are not expanded)
     u64* vis;                           // [A * W] examined rows (zero at the call's start)
     int64_t cap;                        // frontier / discovery / output capacity (entries)
     int64_t wcap, tcap, rcap;           // bitmap words, tiles, runs
@@ -2340,83 +2341,88 @@ __global__ void __launch_bounds__(256) hgx_lp_efill(LsArgs a, int32_t d) {
         a.E[(int64_t)a.uidx[fa[i]] * a.nb + fs[i]] = (uint32_t)a.pre[i];
 }
 
-// A pull hit: co-target p (union slot u) of link L yields atom t at rank kq with item offset j.
+// A pull hit: co-target p (union slot u) of link L yields atom t (the walk's atom o) at rank kq with
+// item offset j; la = the link's atom id (the value's low word).
 struct LpHit {
     int32_t p, u;
     uint32_t j;
-    int32_t la_kq;   // link atom (the value's low word) -- kq kept beside it
-    uint32_t kq;
+    int32_t la;
+    uint32_t kq_o;   // kq | o << 16
 };
-constexpr int kLpHits = 64 * 8;   // one pass of a wave over <= 64 entries of <= 8 targets
+constexpr int kLpHits = 64 * 8;   // one pass of a wave: <= 64 entries of <= 8 targets (<= 7 hits each)
 
-// Phase A of a pull pass (a lane per entry e of t): every co-target p of e's link that is on some
-// seed's frontier and yields t (the expand's rules: link predicate, minimum arity, p's first
-// occurrence, the mode's positions (3.2), t's best yielded position) becomes a hit in the wave's LDS
-// list.  Long rows (> 8 targets) from memory.
-__device__ __forceinline__ void lp_hits(const LsArgs& a, int32_t t, int64_t e, bool have, LpHit* hits, int* nh,
-                                        int64_t& nbytes) {
-    if (!have) return;
+// The hits of entry e of atom t (a lane's share of a pass): every co-target p of e's link that is on
+// some seed's frontier and yields t -- the expand's rules: link predicate, minimum arity, p's first
+// occurrence, the mode's positions (3.2), t's best yielded position.  Rows of <= 8 targets: a mask of
+// the hit positions over the row in registers; longer rows set long_row (walked by lp_long_row).
+struct LpCand {
+    int32_t tg[8], qt[8];
+    uint32_t mask;
+    int64_t tb;
+    int32_t rown, la;
+};
+__device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t e, bool have, LpCand& c, bool& long_row,
+                                             int64_t& nbytes) {
+    c.mask = 0u;
+    c.tb = 0;
+    c.rown = 0;
+    c.la = 0;
+    long_row = false;
+    if (!have) return 0;
     if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {   // linkPredicate (:300)
         nbytes += 4;
-        return;
+        return 0;
     }
     const int32_t L = a.inc_row[e];
     const int64_t tb = a.tgt_off[L];
     const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
     nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
-    if (n < a.min_arity) return;   // minArity (:309)
-    nbytes += 4 * (int64_t)n + 4;
-    const int32_t la = a.link_atom[L];
-    auto add = [&](int32_t p, int32_t q, int32_t qt) {
-        const int k = atomicAdd(nh, 1);
-        if (k >= kLpHits) {   // only rows of more than 8 targets can fill the list: the chunk reruns pushing
-            atomicOr((unsigned long long*)&a.ctl[kLsStatus], 128ull);
-            return;
-        }
-        LpHit h;
-        h.p = p;
-        h.u = a.uidx[p];
-        h.j = (uint32_t)a.pin_j[tb + q];
-        h.la_kq = la;
-        h.kq = (uint32_t)(a.rev ? n - 1 - qt : qt);
-        hits[k] = h;
-        nbytes += 8;
-    };
-    if (n <= 8) {   // the row in registers
-        int32_t tg[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
-        u64 onf[8];   // union bits of the co-targets, loaded together
-#pragma unroll
-        for (int q = 0; q < 8; ++q) onf[q] = (q < n && tg[q] != t) ? a.ubit[tg[q] >> 6] >> (tg[q] & 63) : 0ull;
-        nbytes += 8 * (int64_t)n;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
-            const int32_t p = tg[q];
-            bool dup = false;   // p's first occurrence only
-#pragma unroll
-            for (int q2 = 0; q2 < q; ++q2) dup |= tg[q2] == p;
-            if (dup) continue;
-            int32_t lp = q;
-#pragma unroll
-            for (int q2 = q + 1; q2 < 8; ++q2)
-                if (tg[q2] == p) lp = q2;
-            int32_t lo = 0, hi = n;   // positions p yields (3.2)
-            if (a.mode == sAfterFirst) lo = q + 1;
-            else if (a.mode == sBeforeFirst) hi = q;
-            else if (a.mode == sBeforeLast) hi = lp;
-            else if (a.mode == sAfterLast) lo = lp + 1;
-            int32_t qt = -1;   // t's best yielded position
-#pragma unroll
-            for (int q2 = 0; q2 < 8; ++q2)
-                if (q2 >= lo && q2 < hi && tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
-            if (qt >= 0) add(p, q, qt);
-        }
-        return;
+    if (n < a.min_arity) return 0;   // minArity (:309)
+    nbytes += 4 * (int64_t)n + 4 + 8 * (int64_t)n;
+    c.tb = tb;
+    c.rown = n;
+    c.la = a.link_atom[L];
+    if (n > 8) {
+        long_row = true;
+        return 0;
     }
-    nbytes += 8 * (int64_t)n;
-    for (int32_t q = 0; q < n; ++q) {   // long rows: from memory, hits in batches of the list
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c.tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
+    u64 onf[8];   // union bits of the co-targets, loaded together
+#pragma unroll
+    for (int q = 0; q < 8; ++q) onf[q] = (q < n && c.tg[q] != t) ? a.ubit[c.tg[q] >> 6] >> (c.tg[q] & 63) : 0ull;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        c.qt[q] = -1;
+        if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
+        const int32_t p = c.tg[q];
+        bool dup = false;   // p's first occurrence only
+#pragma unroll
+        for (int q2 = 0; q2 < q; ++q2) dup |= c.tg[q2] == p;
+        if (dup) continue;
+        int32_t lp = q;
+#pragma unroll
+        for (int q2 = q + 1; q2 < 8; ++q2)
+            if (c.tg[q2] == p) lp = q2;
+        int32_t lo = 0, hi = n;   // positions p yields (3.2)
+        if (a.mode == sAfterFirst) lo = q + 1;
+        else if (a.mode == sBeforeFirst) hi = q;
+        else if (a.mode == sBeforeLast) hi = lp;
+        else if (a.mode == sAfterLast) lo = lp + 1;
+        int32_t qt = -1;   // t's best yielded position
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2)
+            if (q2 >= lo && q2 < hi && c.tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
+        c.qt[q] = qt;
+        if (qt >= 0) c.mask |= 1u << q;
+    }
+    return __popc(c.mask);
+}
+
+// Walks a long row (> 8 targets) of atom t: f(p, q, qt) for every hit (from memory).
+template <class F>
+__device__ __forceinline__ void lp_long_row(const LsArgs& a, int32_t t, int64_t tb, int32_t n, F&& f) {
+    for (int32_t q = 0; q < n; ++q) {
         const int32_t p = a.tgt_idx[tb + q];
         if (p == t || !((a.ubit[p >> 6] >> (p & 63)) & 1ull)) continue;
         bool dup = false;
@@ -2433,82 +2439,160 @@ __device__ __forceinline__ void lp_hits(const LsArgs& a, int32_t t, int64_t e, b
         int32_t qt = -1;
         for (int32_t q2 = lo; q2 < hi; ++q2)
             if (a.tgt_idx[tb + q2] == t && (qt < 0 || a.rev)) qt = q2;
-        if (qt >= 0) add(p, q, qt);
+        if (qt >= 0) f(p, q, qt);
     }
 }
 
-// Phase B (a lane per seed: seed w * 64 + lane in register best[w]): every hit's candidate value for
-// the seeds that have p on their frontier and t not examined -- one broadcast frontier-row word and one
-// coalesced E row per hit, four hits in flight.
-template <int WW>
-__device__ __forceinline__ void lp_minima(const LsArgs& a, const LpHit* hits, int nh, const u64* needbits, u64* best,
-                                          int64_t& nbytes) {
+// The pull walk of one wave over the concatenated incidence ranges of up to 64 atoms (lane o: atom
+// at, entries [eb, eb + cnt), examined words vw[]): 64 entries a pass.  Phase A, a lane per entry:
+// its hits, written into the wave's LDS list in entry order (so each atom's hits are contiguous).
+// Phase B, a lane per seed (seed w * 64 + lane keeps its minimum in register best[w]): the hits in
+// order, up to four of one atom at a time (one broadcast frontier-row word and one coalesced E row
+// each, loaded together); when the hits move on to the next atom the finished one is flushed --
+// flush(o, best), every lane calls it -- and best reset.
+template <int WW, class Flush>
+__device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb, int64_t cnt, const u64* vw, LpHit* hits,
+                                        u64* best, int64_t& nbytes, Flush&& flush) {
     const int lane = threadIdx.x & 63;
-    for (int h0 = 0; h0 < nh; h0 += 4) {   // wave-uniform
+    int64_t x = cnt;
 #pragma unroll
-        for (int w = 0; w < WW; ++w) {
-            if (w >= a.W) break;
-            const int s = w * 64 + lane;
-            u64 fw[4];
-            uint32_t pre[4];
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    const int64_t T = __shfl(x, 63), ex = x - cnt;
+    const u64 lastmask = (a.nb & 63) ? (1ull << (a.nb & 63)) - 1ull : ~0ull;
+    int cur = -1;   // the atom (lane) whose minima best[] holds (wave-uniform)
+    u64 needb[WW];  // the current atom's examined words, inverted (seeds that have not examined it)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                fw[q] = 0ull;
-                pre[q] = 0u;
-                if (h0 + q < nh) {
-                    const LpHit& H = hits[h0 + q];
-                    fw[q] = a.frow[(int64_t)H.p * a.W + w];
-                    if (s < a.nb) pre[q] = a.E[(int64_t)H.u * a.nb + s];
-                }
-            }
+    for (int w = 0; w < WW; ++w) needb[w] = 0ull;
+    for (int64_t f0 = 0; f0 < T; f0 += 64) {   // wave-uniform
+        const int64_t f = f0 + lane;
+        int o = 0;   // owner lane: the last lane whose range starts at or before f
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (h0 + q >= nh) break;
-                if (!(((fw[q] & needbits[w]) >> lane) & 1ull)) continue;
-                const LpHit& H = hits[h0 + q];
-                const u64 it = (u64)pre[q] + H.j;
-                const u64 v = ((((it << a.kbits) | H.kq) + 1ull) << 32) | (u64)(uint32_t)H.la_kq;
-                best[w] = min(best[w], v);
-            }
+        for (int step = 32; step > 0; step >>= 1) {
+            const int mid = o + step;
+            if (__shfl(ex, mid) <= f) o = mid;
         }
-        nbytes += lane == 0 ? (int64_t)min(4, nh - h0) * (8 * a.W + 4 * (int64_t)a.nb) : 0;
-    }
-}
-
-// One wave pulls entries [eb, ee) of atom t: phase A over 64 entries at a time, phase B over its hits.
-template <int WW>
-__device__ __forceinline__ void lp_pull_range(const LsArgs& a, int32_t t, int64_t eb, int64_t ee, LpHit* hits,
-                                              int* nh, const u64* needbits, u64* best, int64_t& nbytes) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t e0 = eb; e0 < ee; e0 += 64) {   // wave-uniform
-        if (lane == 0) *nh = 0;
-        __builtin_amdgcn_wave_barrier();
-        lp_hits(a, t, e0 + lane, e0 + lane < ee, hits, nh, nbytes);
+        const int32_t t = __shfl(at, o);
+        const int64_t e = __shfl(eb, o) + (f - __shfl(ex, o));
+        LpCand c;
+        bool lr;
+        const int nh = lp_hits_count(a, t, e, f < T, c, lr, nbytes);
+        int nl = 0;   // a long row's hits, counted first
+        if (lr) lp_long_row(a, t, c.tb, c.rown, [&](int32_t, int32_t, int32_t) { ++nl; });
+        const int mine = nh + nl;
+        int px = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(px, off);
+            if (lane >= off) px += y;
+        }
+        const int total = __shfl(px, 63);
+        if (total > kLpHits) {   // only long rows can fill the list: the chunk reruns pushing
+            if (lane == 0) atomicOr((unsigned long long*)&a.ctl[kLsStatus], 128ull);
+            return;
+        }
+        int pos = px - mine;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if ((c.mask >> q) & 1u) {   // the hits' union slots and pin indices
+                LpHit h;
+                h.p = c.tg[q];
+                h.u = a.uidx[c.tg[q]];
+                h.j = (uint32_t)a.pin_j[c.tb + q];
+                h.la = c.la;
+                h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - c.qt[q] : c.qt[q]) | (uint32_t)o << 16;
+                hits[pos++] = h;
+            }
+        if (lr)
+            lp_long_row(a, t, c.tb, c.rown, [&](int32_t p, int32_t q, int32_t qt) {
+                LpHit h;
+                h.p = p;
+                h.u = a.uidx[p];
+                h.j = (uint32_t)a.pin_j[c.tb + q];
+                h.la = c.la;
+                h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - qt : qt) | (uint32_t)o << 16;
+                hits[pos++] = h;
+            });
+        nbytes += 8 * (int64_t)mine;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const int n = min(*nh, kLpHits);
-        lp_minima<WW>(a, hits, n, needbits, best, nbytes);
+        for (int h0 = 0; h0 < total;) {   // phase B (wave-uniform)
+            LpHit H[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) H[q] = hits[min(h0 + q, total - 1)];
+            const int ho = (int)(H[0].kq_o >> 16);
+            int hn = 1;   // up to four consecutive hits of the same atom
+#pragma unroll
+            for (int q = 1; q < 4; ++q)
+                if (hn == q && h0 + q < total && (int)(H[q].kq_o >> 16) == ho) ++hn;
+            if (ho != cur) {   // the hits moved on to the next atom: flush the finished one
+                if (cur >= 0) {
+                    flush(cur, best);
+#pragma unroll
+                    for (int w = 0; w < WW; ++w) best[w] = ~0ull;
+                }
+                cur = ho;
+#pragma unroll
+                for (int w = 0; w < WW; ++w) {
+                    const u64 v = w < a.W ? ~__shfl(vw[w], cur) : 0ull;
+                    needb[w] = w == a.W - 1 ? v & lastmask : v;
+                }
+            }
+            u64 fw[4][WW];
+            uint32_t pre[4][WW];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int w = 0; w < WW; ++w) {
+                    fw[q][w] = 0ull;
+                    pre[q][w] = 0u;
+                    if (q < hn && w < a.W) {
+                        fw[q][w] = a.frow[(int64_t)H[q].p * a.W + w];
+                        if (w * 64 + lane < a.nb) pre[q][w] = a.E[(int64_t)H[q].u * a.nb + w * 64 + lane];
+                    }
+                }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int w = 0; w < WW; ++w) {
+                    if (q >= hn || w >= a.W || !(((fw[q][w] & needb[w]) >> lane) & 1ull)) continue;
+                    const u64 it = (u64)pre[q][w] + H[q].j;
+                    const u64 v = ((((it << a.kbits) | (H[q].kq_o & 0xFFFFu)) + 1ull) << 32) | (u64)(uint32_t)H[q].la;
+                    best[w] = min(best[w], v);
+                }
+            nbytes += lane == 0 ? (int64_t)hn * (8 * a.W + 4 * (int64_t)a.nb) : 0;
+            h0 += hn;
+        }
         __builtin_amdgcn_wave_barrier();
+    }
+    if (cur >= 0) {
+        flush(cur, best);
+#pragma unroll
+        for (int w = 0; w < WW; ++w) best[w] = ~0ull;
     }
 }
 
-// Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its waves' minima merged through LDS
-// and lowered into hbest with one global atomicMin per seed), then the light atoms (a wave each, its
-// discoveries appended right away).  WW: row words rounded up to a power of two (register minima).
+// Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its four waves walking a quarter
+// each; their minima merged through LDS and lowered into hbest with one global atomicMin per seed),
+// then the light atoms: a wave takes 64 consecutive atoms (a lane each: incidence range, examined row)
+// and walks the entries of those with incidence, <= kHeavyDegree entries and a seed that has not
+// examined them; each atom's discoveries are appended when the walk leaves it.  WW: the row words
+// rounded up to a power of two (register minima).
 template <int WW>
 __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
     extern __shared__ u64 lp_merge[];   // [4][nb]
     __shared__ LpHit lp_hits_l[4][kLpHits];
-    __shared__ int lp_nh[4];
     __shared__ int64_t ws[4];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus] || !sl[lsPull]) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nb = a.nb, W = a.W;
     LpHit* hits = lp_hits_l[wave];
-    int* nh = &lp_nh[wave];
-    const u64 lastmask = (nb & 63) ? (1ull << (nb & 63)) - 1ull : ~0ull;
-    u64 best[WW], needbits[WW];
+    for (int s = threadIdx.x; s < 4 * nb; s += 256) lp_merge[s] = ~0ull;
+    __syncthreads();
+    u64 best[WW];
 #pragma unroll
     for (int w = 0; w < WW; ++w) best[w] = ~0ull;
     int64_t nbytes = 0;
@@ -2516,82 +2600,66 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
     for (int64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {   // block-uniform
         const HeavyChunk ch = a.chunks[c];
         const int32_t t = ch.atom;
-        u64 any = 0;
+        u64 vw[WW];
 #pragma unroll
-        for (int w = 0; w < WW; ++w) {
-            needbits[w] = 0ull;
-            if (w < W) {
-                const u64 v = ~a.vis[(int64_t)t * W + w];
-                needbits[w] = w == W - 1 ? v & lastmask : v;
-                any |= needbits[w];
-            }
-        }
+        for (int w = 0; w < WW; ++w) vw[w] = w < W ? a.vis[(int64_t)t * W + w] : 0ull;
         nbytes += lane == 0 ? 24 + 8 * W : 0;
-        if (any) {   // uniform over the block (same atom)
-            const int64_t q = (ch.end - ch.beg + 3) / 4;
-            const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
-            lp_pull_range<WW>(a, t, b, e, hits, nh, needbits, best, nbytes);
-        }
+        const int64_t q = (ch.end - ch.beg + 3) / 4;
+        const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
+        // one "atom" on lane 0: this wave's quarter of the chunk
+        lp_walk<WW>(a, t, lane == 0 ? b : 0, lane == 0 ? max<int64_t>(e - b, 0) : 0, vw, hits, best, nbytes,
+                    [&](int, u64* bst) {
 #pragma unroll
-        for (int w = 0; w < WW; ++w)
-            if (w < W && w * 64 + lane < nb) lp_merge[(int64_t)wave * nb + w * 64 + lane] = best[w];
+                        for (int w = 0; w < WW; ++w)
+                            if (w < W && w * 64 + lane < nb) lp_merge[(int64_t)wave * nb + w * 64 + lane] = bst[w];
+                    });
         __syncthreads();
         for (int s = threadIdx.x; s < nb; s += 256) {   // the four waves' minima -> the heavy atom's row
-            u64 v = lp_merge[s];
+            u64 v = ~0ull;
 #pragma unroll
-            for (int k = 1; k < 4; ++k) v = min(v, lp_merge[(int64_t)k * nb + s]);
+            for (int k = 0; k < 4; ++k) {
+                v = min(v, lp_merge[(int64_t)k * nb + s]);
+                lp_merge[(int64_t)k * nb + s] = ~0ull;
+            }
             if (v != ~0ull) {
                 atomicMin((unsigned long long*)&a.hbest[(int64_t)ch.slot * nb + s], (unsigned long long)v);
                 nbytes += 8;
             }
         }
-#pragma unroll
-        for (int w = 0; w < WW; ++w) best[w] = ~0ull;
         __syncthreads();
     }
-    // light atoms: a wave takes 64 consecutive atoms (a lane each: degree and examined row), then pulls
-    // the ones with incidence, <= kHeavyDegree entries and a seed that has not examined them, one by one
+    // light atoms
     const int64_t nwv = (int64_t)gridDim.x * 4;
     for (int64_t t0 = ((int64_t)blockIdx.x * 4 + wave) * 64; t0 < a.A; t0 += nwv * 64) {
         const int64_t t = t0 + lane;
-        int64_t eb = 0, ee = 0;
-        bool cand = false;
+        int64_t eb = 0, cnt = 0;
+        u64 vw[WW];
+#pragma unroll
+        for (int w = 0; w < WW; ++w) vw[w] = ~0ull;
+        const u64 lastmask = (nb & 63) ? (1ull << (nb & 63)) - 1ull : ~0ull;
         if (t < a.A) {
             eb = a.inc_off[t];
-            ee = a.inc_off[t + 1];
+            const int64_t ee = a.inc_off[t + 1];
             nbytes += 8;
             if (ee > eb && ee - eb <= kHeavyDegree) {
                 u64 any = 0;
-                for (int w = 0; w < W; ++w) {
-                    const u64 v = ~a.vis[t * W + w];
-                    any |= w == W - 1 ? v & lastmask : v;
+#pragma unroll
+                for (int w = 0; w < WW; ++w) {
+                    vw[w] = w < W ? a.vis[t * W + w] : ~0ull;
+                    if (w < W) any |= w == W - 1 ? ~vw[w] & lastmask : ~vw[w];
                 }
                 nbytes += 8 * W;
-                cand = any != 0;
+                if (any) cnt = ee - eb;
             }
         }
-        for (u64 m = __ballot(cand); m; m &= m - 1) {   // wave-uniform
-            const int l0 = __ffsll((long long)m) - 1;
-            const int32_t tt = (int32_t)(t0 + l0);
-            const int64_t b = __shfl(eb, l0), e = __shfl(ee, l0);
-#pragma unroll
-            for (int w = 0; w < WW; ++w) {
-                needbits[w] = 0ull;
-                if (w < W) {
-                    const u64 v = ~a.vis[(int64_t)tt * W + w];
-                    needbits[w] = w == W - 1 ? v & lastmask : v;
-                }
-            }
-            lp_pull_range<WW>(a, tt, b, e, hits, nh, needbits, best, nbytes);
+        lp_walk<WW>(a, (int32_t)t, eb, cnt, vw, hits, best, nbytes, [&](int o, u64* bst) {
 #pragma unroll
             for (int w = 0; w < WW; ++w) {   // the atom's discoveries: a lane per seed
                 if (w >= W) break;
                 const int s = w * 64 + lane;
-                const bool isnew = s < nb && best[w] != ~0ull;
-                ls_append(a, d, isnew, (int64_t)s * a.A + tt, best[w]);
-                best[w] = ~0ull;
+                ls_append(a, d, s < nb && bst[w] != ~0ull, (int64_t)s * a.A + (t0 + o), bst[w]);
             }
-        }
+        });
     }
     ls_add_bytes(a, nbytes, ws);
 }
@@ -2691,6 +2759,7 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
     if (n == 0) return;
     ls_block_offsets(a.bsum, off, ws);
     const int nx = (d + 1) & 1;
+    const bool last = d + 1 >= a.maxd;
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
         const int64_t pos = ls_disc_pos(a, pre, x);
         const int64_t sa = a.disc[pos];
@@ -2704,9 +2773,11 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
         const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
         a.out_link[out0 + r] = (int32_t)(uint32_t)v;
         a.out_atom[out0 + r] = t;
-        a.fa[nx][r] = t;
-        a.fs[nx][r] = s;
-        atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
+        a.fs[nx][r] = s;   // (the last level's too: its pairs' runs)
+        if (!last) {       // the next frontier and the examined bit, unless no level follows
+            a.fa[nx][r] = t;
+            atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
+        }
     }
 }
 
@@ -3569,6 +3640,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         if (const char* tl = std::getenv("HGX_LS_TLIMIT")) a.t_limit = std::min<int64_t>(a.t_limit, std::atoll(tl));   // tests
         a.nb = nb;
         a.W = W;
+        a.maxd = maxd;
         a.cap = cap;
         a.wcap = wcap;
         a.tcap = tcap;
