@@ -234,10 +234,14 @@ struct hgx_graph {
                                                     //   level engine only, 2 level engine (hgx_ls_*) only
     unsigned long long* seq_flag = nullptr;         // mapped coherent words: level sizes of the level engine
     unsigned long long seq_flag_seq = 0;            //   (their sequence numbers)
-    int64_t ls_cap = 0, ls_wcap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
+    int64_t ls_cap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
     int64_t ls_hcap = 0, ls_fcap = 0;               //   and its two hash tables' slots (push, frontier)
     int32_t* pin_j = nullptr;                       // [P] index of link row L in inc(t) for each pin (t, L):
                                                     //   the level engine's pull levels (snapshot only, made on first use)
+    int4* pull_rec = nullptr;                       // [I x 4] per incidence entry (t, L): L's <= 8 targets, then their
+                                                    //   pin_j -- the pull walk's link data streamed in entry order
+    int2* pull_meta = nullptr;                      // [I] (link atom, arity) per incidence entry
+    int32_t pull_rec_state = 0;                     //   0 not built yet, 1 built, -1 over its memory budget
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each

@@ -1867,12 +1867,12 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
 //        chunk of a heavy atom with one global atomicMin per seed and chunk), so no global table and no
 //        atomic per yield: config 2's level 1 (64 seeds, 3.6e8 items, 1.4e9 yields) touches the CSR
 //        once instead of 1.4e9 random words of a 25.6 GB key array.
-//        Frontier rows frow [A x W], the union bitmap ubit and a small hash (seed, atom) -> pre are
-//        built from the frontier entries in the expand launch and cleared through the union list.
-// Then, both ways: hgx_ls_bits (a bit per discovery at its key over the level's key space),
-// hgx_ls_wprefix (popcount prefix), hgx_ls_emit (rank = popcount below the key: pair `rank` of the
-// level, entry `rank` of the next frontier, vis bit set).  The level's pairs are seed-major because the
-// frontier is.
+//        The union of the level's frontier atoms (bitmap ubit, list ulist, slot uidx) is built by the
+//        expand launch; hgx_lp_efill writes each union slot's frontier row frow[u] (bit s: on seed s's
+//        frontier) and item row E[u] (pre(s, p)); the count launch clears them through the union list.
+// Then, both ways, the discoveries are ranked by key (hgx_lr_*, below: key buckets, an LDS bitmap per
+// bucket; rank r = pair r of the level and entry r of the next frontier, vis bit set).  The level's
+// pairs are seed-major because the frontier is.
 constexpr int kLsG = 256;               // blocks of the range kernels (contiguous ranges: prefix-able)
 constexpr int64_t kLsTile = 256;        // items per expand tile
 constexpr int kLsSlots = 4;             // per-level counter slots (ring); slot words:
@@ -1880,7 +1880,7 @@ enum { lsF = 0, lsT = 1, lsN = 2, lsOut = 3, lsW = 4, lsTiles = 5, lsPull = 6, l
 constexpr int kLsSlotWords = 8;
 constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsRuns = kLsStatus + 2,
               kLsBytes = kLsStatus + 3, kLsPullN = kLsStatus + 4;
-// status bits: 1 discoveries > cap, 2 runs > rcap, 4 key-space bitmap > wcap, 8 tiles > tcap, 16 keys wider
+// status bits: 1 discoveries > cap, 2 runs > rcap, (4 unused since round 5), 8 tiles > tcap, 16 keys wider
 // than 32 bits, 32 push hash too full, 128 a pull pass's hit list overflowed (long rows: rerun pushing)
 // A level's discoveries go to kLsDSegs segments of the list, one counter each (a wave appends to the
 // segment of its block): one shared counter took one same-address atomic per wave and round, which
@@ -1890,8 +1890,22 @@ constexpr int kLsStatus = kLsSlots * kLsSlotWords, kLsTrav = kLsStatus + 1, kLsR
 // discoveries all come from a few blocks still fits whenever they fit the capacity.
 constexpr int kLsDSegs = 32;
 constexpr int kLsDSeg = kLsStatus + 8;                           // [kLsSlots][kLsDSegs + 1] counters (+ overflow)
-constexpr int kLsCtlWords = kLsDSeg + kLsSlots * (kLsDSegs + 1);
+constexpr int kLsProf = kLsDSeg + kLsSlots * (kLsDSegs + 1);  // [8] pull-walk phase timers (HGX_LS_PROF)
+constexpr int kLsCtlWords = kLsProf + 8;
 constexpr int kLsMaxW = 16;             // row words: chunks of <= 1024 seeds
+constexpr int kLrMaxBucketBits = 18;                            // <= 2^18 keys a bucket (a 32 KB LDS bitmap)
+constexpr int kLrMaxBuckets = 1 << (32 - kLrMaxBucketBits);     // keys < 2^32
+constexpr int kLrG = 512;                                       // blocks of count / scatter / rank
+
+__device__ __forceinline__ int lr_bucket_bits(int64_t W) {
+    const u64 keys = (u64)max<int64_t>(W, 1) * 64ull;
+    const int lg = 64 - __clzll((unsigned long long)(keys - 1ull));   // ceil(log2(keys)), keys >= 64
+    return min(max(lg - 9, 6), kLrMaxBucketBits);
+}
+__device__ __forceinline__ int lr_buckets(int64_t W, int bs) {
+    return (int)(((u64)max<int64_t>(W, 1) * 64ull + (1ull << bs) - 1ull) >> bs);
+}
+
 constexpr int kLsProbes = 64;           // hash probes before a level reports overflow (load <= 1/2)
 constexpr u64 kLsEmpty = ~0ull;
 
@@ -1910,7 +1924,7 @@ struct LsArgs {
     int32_t maxd;                       // depth limit (the last level's discoveries are not expanded)
     u64* vis;                           // [A * W] examined rows (zero at the call's start)
     int64_t cap;                        // frontier / discovery / output capacity (entries)
-    int64_t wcap, tcap, rcap;           // bitmap words, tiles, runs
+    int64_t tcap, rcap;                 // tiles, runs
     int64_t* ctl;                       // kLsCtlWords
     int32_t* fa[2];                     // frontier atom / seed (double-buffered)
     int32_t* fs[2];
@@ -1922,8 +1936,11 @@ struct LsArgs {
     int64_t* disc;                      // the level's discoveries (seed * A + atom): kLsDSegs segments of
     u64* dval;                          //   segcap entries, then an overflow region of cap entries; their
     int64_t segcap;                     //   values (push: the hash slot until hgx_ls_bits)
-    u64* bm;                            // [wcap] rank bitmap
-    uint32_t* wpre;                     // [wcap] popcount prefix of word w inside its block's range
+    uint32_t* bcnt;                     // [kLrMaxBuckets] discoveries per key bucket (hgx_lr_*; zeroed by the expand)
+    uint32_t* bcur;                     // [kLrMaxBuckets] the buckets' fill cursors
+    int64_t* bstart;                    // [kLrMaxBuckets + 1] their first rank
+    u64* bk_v;                          // the discoveries by bucket: value, seed * A + atom
+    int64_t* bk_sa;
     int32_t* out_link;                  // [cap] pairs, level-major (device)
     int32_t* out_atom;
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
@@ -1941,7 +1958,10 @@ struct LsArgs {
     int32_t pull;                       // 0 never, 1 by the level's width, 2 every level (tests)
     int64_t I;                          // incidence entries
     const int32_t* pin_j;               // [P] index of link row L in inc(tgt_idx[p]) for pin p of L
-    u64* frow;                          // [A * W] frontier rows of the level (zero between levels)
+    int32_t prof;                       // HGX_LS_PROF: the pull walk's phase timers into ctl[kLsProf ..]
+    const int4* prec;                   // pull records per incidence entry (k_pull_rec), or null
+    const int2* pmeta;
+    u64* frow;                          // [cap * W] frontier rows of the level by union slot (zero between levels)
     u64* ubit;                          // [A / 64 + 1] union of the level's frontier atoms (zero between levels)
     int32_t* ulist;                     // [cap] the union's atoms (the rows / bits to clear after the level)
     int32_t* uidx;                      // [A] the union atom's position in ulist (valid where ubit is set)
@@ -2022,6 +2042,59 @@ __device__ __forceinline__ void ls_append(const LsArgs& a, int d, bool isnew, in
             a.dval[pos] = val;
         }
     }
+}
+
+// Staged appends (the pull walk, round 5): a wave collects its discoveries in LDS and places up to
+// kLsStage of them with ONE reservation -- the per-atom append (an atomic round trip on the segment
+// counter for ~27 discoveries) was a tenth of the pull's time on config 2's drop-in level.
+constexpr int kLsStage = 128;
+__device__ __forceinline__ void ls_stage_flush(const LsArgs& a, int d, const int64_t* ssa, const u64* sv, int n) {
+    if (n == 0) return;   // (n is wave-uniform; every lane calls)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int lane = threadIdx.x & 63;
+    const int dsg = blockIdx.x % kLsDSegs;
+    const u64 cnt = (u64)n, segcap = (u64)a.segcap;
+    u64 base = 0, ob = 0;
+    if (lane == 0) {
+        base = atomicAdd((unsigned long long*)(ls_dseg(a, d) + dsg), cnt);
+        const u64 fit = base >= segcap ? 0ull : min(cnt, segcap - base);
+        if (fit < cnt) ob = atomicAdd((unsigned long long*)(ls_dseg(a, d) + kLsDSegs), cnt - fit);
+    }
+    base = __shfl(base, 0);
+    ob = __shfl(ob, 0);
+    for (int k = lane; k < n; k += 64) {
+        const u64 w = base + (u64)k;
+        int64_t pos = -1;
+        if (w < segcap) {
+            pos = (int64_t)dsg * a.segcap + (int64_t)w;
+        } else {   // the segment is full: the shared overflow region
+            const int64_t o = (int64_t)(ob + (w - max(base, segcap)));
+            if (o < a.cap) pos = (int64_t)kLsDSegs * a.segcap + o;
+            else atomicOr((unsigned long long*)&a.ctl[kLsStatus], 1ull);   // more discoveries than cap holds
+        }
+        if (pos >= 0) {
+            a.disc[pos] = ssa[k];
+            a.dval[pos] = sv[k];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void ls_append_staged(const LsArgs& a, int d, bool isnew, int64_t sa, u64 val, int64_t* ssa,
+                                                 u64* sv, int& sn) {
+    const u64 m = __ballot(isnew);
+    if (!m) return;
+    const int c = __popcll(m);
+    if (sn + c > kLsStage) {
+        ls_stage_flush(a, d, ssa, sv, sn);
+        sn = 0;
+    }
+    if (isnew) {
+        const int k = sn + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull));
+        ssa[k] = sa;
+        sv[k] = val;
+    }
+    sn += c;
 }
 
 __device__ __forceinline__ int64_t ls_block_sum(int64_t v, int64_t* ws) {
@@ -2161,7 +2234,6 @@ __global__ void __launch_bounds__(256) hgx_ls_prefix(LsArgs a, int32_t d) {
         if (!a.y_off) atomicAdd((unsigned long long*)&a.ctl[kLsTrav], (unsigned long long)T);
         int64_t st = 0;
         if (T > a.t_limit) st |= 16;   // keys wider than 32 bits: the chunk is split (or the key-array engine)
-        if (W > a.wcap) st |= 4;
         if (sl[lsTiles] > a.tcap) st |= 8;
         if (st) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)st);
     }
@@ -2216,23 +2288,24 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     const int cur = d & 1;
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
-    for (int64_t w = blockIdx.x * 256ll + threadIdx.x; w < W; w += (int64_t)gridDim.x * 256) a.bm[w] = 0ull;
+    {   // the ranking's bucket counts (hgx_lr_count adds to them)
+        const int bs = lr_bucket_bits(W), nbk = lr_buckets(W, bs);
+        for (int64_t b = blockIdx.x * 256ll + threadIdx.x; b < nbk; b += (int64_t)gridDim.x * 256) a.bcnt[b] = 0u;
+    }
     const int lane = threadIdx.x & 63;
     int64_t nbytes = 0;
     if (sl[lsPull]) {
-        // frontier rows (bit s of frow[p] <=> p is on seed s's frontier), the union list, and
-        // pre(s, p) in the frontier hash; entries in a wave-uniform loop (the union append ballots)
+        // the union of the frontier atoms (bitmap, list, slot of each); entries in a wave-uniform loop
+        // (the union append ballots); hgx_lp_efill then builds the rows by union slot
         for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < F; i0 += (int64_t)gridDim.x * 256) {
             const int64_t i = i0 + threadIdx.x;
             bool first = false;
             int32_t p = 0;
             if (i < F) {
                 p = fa[i];
-                const int32_t s = fs[i];
-                atomicOr((unsigned long long*)&a.frow[(int64_t)p * a.W + (s >> 6)], 1ull << (s & 63));
                 const u64 bit = 1ull << (p & 63);
                 first = !(atomicOr((unsigned long long*)&a.ubit[p >> 6], bit) & bit);
-                nbytes += 8 + 8 + 8;
+                nbytes += 8 + 8;
             }
             const u64 m = __ballot(first);
             if (m) {
@@ -2329,22 +2402,26 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     ls_add_bytes(a, nbytes, ws);
 }
 
-// Pull levels, after the expand launch built the rows and the union: E[uidx[p] * nb + s] = the item
-// index of the first item of seed s's frontier entry of p.
+// Pull levels, after the expand launch built the union: E[u * nb + s] = the item index of the first
+// item of seed s's frontier entry of p (u = p's union slot), and bit s of the frontier row frow[u].
 __global__ void __launch_bounds__(256) hgx_lp_efill(LsArgs a, int32_t d) {
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus] || !sl[lsPull]) return;
     const int64_t F = sl[lsF];
     const int32_t* fa = a.fa[d & 1];
     const int32_t* fs = a.fs[d & 1];
-    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < F; i += (int64_t)gridDim.x * 256)
-        a.E[(int64_t)a.uidx[fa[i]] * a.nb + fs[i]] = (uint32_t)a.pre[i];
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < F; i += (int64_t)gridDim.x * 256) {
+        const int64_t u = a.uidx[fa[i]];
+        const int32_t s = fs[i];
+        a.E[u * a.nb + s] = (uint32_t)a.pre[i];
+        atomicOr((unsigned long long*)&a.frow[u * a.W + (s >> 6)], 1ull << (s & 63));
+    }
 }
 
 // A pull hit: co-target p (union slot u) of link L yields atom t (the walk's atom o) at rank kq with
 // item offset j; la = the link's atom id (the value's low word).
 struct LpHit {
-    int32_t p, u;
+    int32_t u;       // the co-target's union slot (its frontier row frow[u] and item row E[u])
     uint32_t j;
     int32_t la;
     uint32_t kq_o;   // kq | o << 16
@@ -2356,7 +2433,7 @@ constexpr int kLpHits = 64 * 8;   // one pass of a wave: <= 64 entries of <= 8 t
 // occurrence, the mode's positions (3.2), t's best yielded position.  Rows of <= 8 targets: a mask of
 // the hit positions over the row in registers; longer rows set long_row (walked by lp_long_row).
 struct LpCand {
-    int32_t tg[8], qt[8];
+    int32_t tg[8], qt[8], pj[8];   // pj: the record's pin indices (pull records only)
     uint32_t mask;
     int64_t tb;
     int32_t rown, la;
@@ -2369,25 +2446,54 @@ __device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t
     c.la = 0;
     long_row = false;
     if (!have) return 0;
-    if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {   // linkPredicate (:300)
-        nbytes += 4;
-        return 0;
-    }
-    const int32_t L = a.inc_row[e];
-    const int64_t tb = a.tgt_off[L];
-    const int32_t n = (int32_t)(a.tgt_off[L + 1] - tb);
-    nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
-    if (n < a.min_arity) return 0;   // minArity (:309)
-    nbytes += 4 * (int64_t)n + 4 + 8 * (int64_t)n;
-    c.tb = tb;
-    c.rown = n;
-    c.la = a.link_atom[L];
-    if (n > 8) {
-        long_row = true;
-        return 0;
-    }
+    int32_t n;
+    if (a.pmeta) {   // the entry's pull record: (link atom, arity), <= 8 targets, their pin indices -- streamed
+        // in entry order and loaded together with the type (one round trip before the union probes)
+        const int32_t ty = a.want_type >= 0 ? a.inc_type[e] : 0;
+        const int2 m = a.pmeta[e];
+        const int4 r0 = a.prec[4 * e], r1 = a.prec[4 * e + 1], r2 = a.prec[4 * e + 2], r3 = a.prec[4 * e + 3];
+        if (a.want_type >= 0 && ty != a.want_type) {   // linkPredicate (:300)
+            nbytes += 4;
+            return 0;
+        }
+        n = m.y;
+        nbytes += (a.want_type >= 0 ? 4 : 0) + 8;
+        if (n < a.min_arity) return 0;   // minArity (:309)
+        c.rown = n;
+        c.la = m.x;
+        if (n > 8) {
+            const int32_t L = a.inc_row[e];
+            c.tb = a.tgt_off[L];
+            nbytes += 12 + 4 * (int64_t)n + 4 * (int64_t)n;
+            long_row = true;
+            return 0;
+        }
+        c.tg[0] = r0.x; c.tg[1] = r0.y; c.tg[2] = r0.z; c.tg[3] = r0.w;
+        c.tg[4] = r1.x; c.tg[5] = r1.y; c.tg[6] = r1.z; c.tg[7] = r1.w;
+        c.pj[0] = r2.x; c.pj[1] = r2.y; c.pj[2] = r2.z; c.pj[3] = r2.w;
+        c.pj[4] = r3.x; c.pj[5] = r3.y; c.pj[6] = r3.z; c.pj[7] = r3.w;
+        nbytes += 64 + 8 * (int64_t)n;   // the record, the targets' union words
+    } else {
+        if (a.want_type >= 0 && a.inc_type[e] != a.want_type) {   // linkPredicate (:300)
+            nbytes += 4;
+            return 0;
+        }
+        const int32_t L = a.inc_row[e];
+        const int64_t tb = a.tgt_off[L];
+        n = (int32_t)(a.tgt_off[L + 1] - tb);
+        nbytes += (a.want_type >= 0 ? 8 : 4) + 16;
+        if (n < a.min_arity) return 0;   // minArity (:309)
+        nbytes += 4 * (int64_t)n + 4 + 8 * (int64_t)n;
+        c.tb = tb;
+        c.rown = n;
+        c.la = a.link_atom[L];
+        if (n > 8) {
+            long_row = true;
+            return 0;
+        }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c.tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
+        for (int q = 0; q < 8; ++q) c.tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
+    }
     u64 onf[8];   // union bits of the co-targets, loaded together
 #pragma unroll
     for (int q = 0; q < 8; ++q) onf[q] = (q < n && c.tg[q] != t) ? a.ubit[c.tg[q] >> 6] >> (c.tg[q] & 63) : 0ull;
@@ -2416,6 +2522,10 @@ __device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t
         c.qt[q] = qt;
         if (qt >= 0) c.mask |= 1u << q;
     }
+    if (!a.pmeta && c.mask) {   // the hits' pin indices at random (no pull records)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) c.pj[q] = ((c.mask >> q) & 1u) ? a.pin_j[c.tb + q] : 0;
+    }
     return __popc(c.mask);
 }
 
@@ -2443,16 +2553,26 @@ __device__ __forceinline__ void lp_long_row(const LsArgs& a, int32_t t, int64_t 
     }
 }
 
+// Wave timers of the pull (HGX_LS_PROF, s_memrealtime ticks of 10 ns, summed over waves): phase A,
+// phase B, flushes, then passes, phase-B steps, flushes, heavy-chunk time, kernel time.
+struct LpProf {
+    int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
 // The pull walk of one wave over the concatenated incidence ranges of up to 64 atoms (lane o: atom
 // at, entries [eb, eb + cnt), examined words vw[]): 64 entries a pass.  Phase A, a lane per entry:
 // its hits, written into the wave's LDS list in entry order (so each atom's hits are contiguous).
 // Phase B, a lane per seed (seed w * 64 + lane keeps its minimum in register best[w]): the hits in
-// order, up to four of one atom at a time (one broadcast frontier-row word and one coalesced E row
-// each, loaded together); when the hits move on to the next atom the finished one is flushed --
-// flush(o, best), every lane calls it -- and best reset.
+// order, up to HB of one atom at a time (their frontier-row words and E rows -- one broadcast and one
+// coalesced load each -- all in flight together); when the hits move on to the next atom the finished
+// one is flushed -- flush(o, best), every lane calls it -- and best reset.  A hit's co-target is on
+// ~1.1 seeds' frontiers on average but the power-law hubs on 10-26 (config 2's drop-in level: 238M hits,
+// 1.7e9 (hit, seed) candidates), so the seeds stay on the lanes; HB = 16 / WW hits a step keeps the
+// wave's loads in flight (4 a step: 87 ms for that level, latency-bound at ~4 us a step).
 template <int WW, class Flush>
 __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb, int64_t cnt, const u64* vw, LpHit* hits,
-                                        u64* best, int64_t& nbytes, Flush&& flush) {
+                                        u64* best, int64_t& nbytes, LpProf& pf, Flush&& flush) {
+    constexpr int HB = WW >= 8 ? 2 : 16 / WW;
     const int lane = threadIdx.x & 63;
     int64_t x = cnt;
 #pragma unroll
@@ -2466,6 +2586,16 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
     u64 needb[WW];  // the current atom's examined words, inverted (seeds that have not examined it)
 #pragma unroll
     for (int w = 0; w < WW; ++w) needb[w] = 0ull;
+    auto flush_cur = [&]() {   // every lane
+        const int64_t t0 = a.prof ? (int64_t)wall_clock64() : 0;
+        flush(cur, best);
+#pragma unroll
+        for (int w = 0; w < WW; ++w) best[w] = ~0ull;
+        if (a.prof) {
+            pf.v[2] += (int64_t)wall_clock64() - t0;
+            pf.v[5] += 1;
+        }
+    };
     for (int64_t f0 = 0; f0 < T; f0 += 64) {   // wave-uniform
         const int64_t f = f0 + lane;
         int o = 0;   // owner lane: the last lane whose range starts at or before f
@@ -2476,6 +2606,7 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
         }
         const int32_t t = __shfl(at, o);
         const int64_t e = __shfl(eb, o) + (f - __shfl(ex, o));
+        const int64_t ta = a.prof ? (int64_t)wall_clock64() : 0;
         LpCand c;
         bool lr;
         const int nh = lp_hits_count(a, t, e, f < T, c, lr, nbytes);
@@ -2494,13 +2625,15 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
             return;
         }
         int pos = px - mine;
+        int32_t us[8];   // the hits' union slots, loaded together
+#pragma unroll
+        for (int q = 0; q < 8; ++q) us[q] = ((c.mask >> q) & 1u) ? a.uidx[c.tg[q]] : 0;
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-            if ((c.mask >> q) & 1u) {   // the hits' union slots and pin indices
+            if ((c.mask >> q) & 1u) {
                 LpHit h;
-                h.p = c.tg[q];
-                h.u = a.uidx[c.tg[q]];
-                h.j = (uint32_t)a.pin_j[c.tb + q];
+                h.u = us[q];
+                h.j = (uint32_t)c.pj[q];
                 h.la = c.la;
                 h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - c.qt[q] : c.qt[q]) | (uint32_t)o << 16;
                 hits[pos++] = h;
@@ -2508,31 +2641,31 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
         if (lr)
             lp_long_row(a, t, c.tb, c.rown, [&](int32_t p, int32_t q, int32_t qt) {
                 LpHit h;
-                h.p = p;
                 h.u = a.uidx[p];
                 h.j = (uint32_t)a.pin_j[c.tb + q];
                 h.la = c.la;
                 h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - qt : qt) | (uint32_t)o << 16;
                 hits[pos++] = h;
             });
-        nbytes += 8 * (int64_t)mine;
+        nbytes += 4 * (int64_t)mine;   // the union slots
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        const int64_t tb_ = a.prof ? (int64_t)wall_clock64() : 0;
+        if (a.prof) {
+            pf.v[0] += tb_ - ta;
+            pf.v[3] += 1;
+        }
         for (int h0 = 0; h0 < total;) {   // phase B (wave-uniform)
-            LpHit H[4];
+            LpHit H[HB];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) H[q] = hits[min(h0 + q, total - 1)];
+            for (int q = 0; q < HB; ++q) H[q] = hits[min(h0 + q, total - 1)];
             const int ho = (int)(H[0].kq_o >> 16);
-            int hn = 1;   // up to four consecutive hits of the same atom
+            int hn = 1;   // up to HB consecutive hits of the same atom
 #pragma unroll
-            for (int q = 1; q < 4; ++q)
+            for (int q = 1; q < HB; ++q)
                 if (hn == q && h0 + q < total && (int)(H[q].kq_o >> 16) == ho) ++hn;
             if (ho != cur) {   // the hits moved on to the next atom: flush the finished one
-                if (cur >= 0) {
-                    flush(cur, best);
-#pragma unroll
-                    for (int w = 0; w < WW; ++w) best[w] = ~0ull;
-                }
+                if (cur >= 0) flush_cur();
                 cur = ho;
 #pragma unroll
                 for (int w = 0; w < WW; ++w) {
@@ -2540,21 +2673,21 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
                     needb[w] = w == a.W - 1 ? v & lastmask : v;
                 }
             }
-            u64 fw[4][WW];
-            uint32_t pre[4][WW];
+            u64 fw[HB][WW];
+            uint32_t pre[HB][WW];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < HB; ++q)
 #pragma unroll
                 for (int w = 0; w < WW; ++w) {
                     fw[q][w] = 0ull;
                     pre[q][w] = 0u;
                     if (q < hn && w < a.W) {
-                        fw[q][w] = a.frow[(int64_t)H[q].p * a.W + w];
+                        fw[q][w] = a.frow[(int64_t)H[q].u * a.W + w];
                         if (w * 64 + lane < a.nb) pre[q][w] = a.E[(int64_t)H[q].u * a.nb + w * 64 + lane];
                     }
                 }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < HB; ++q)
 #pragma unroll
                 for (int w = 0; w < WW; ++w) {
                     if (q >= hn || w >= a.W || !(((fw[q][w] & needb[w]) >> lane) & 1ull)) continue;
@@ -2564,14 +2697,12 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
                 }
             nbytes += lane == 0 ? (int64_t)hn * (8 * a.W + 4 * (int64_t)a.nb) : 0;
             h0 += hn;
+            if (a.prof) pf.v[4] += 1;
         }
+        if (a.prof) pf.v[1] += (int64_t)wall_clock64() - tb_;
         __builtin_amdgcn_wave_barrier();
     }
-    if (cur >= 0) {
-        flush(cur, best);
-#pragma unroll
-        for (int w = 0; w < WW; ++w) best[w] = ~0ull;
-    }
+    if (cur >= 0) flush_cur();
 }
 
 // Pull levels: heavy atoms by 4096-entry chunks (a workgroup each, its four waves walking a quarter
@@ -2584,6 +2715,8 @@ template <int WW>
 __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
     extern __shared__ u64 lp_merge[];   // [4][nb]
     __shared__ LpHit lp_hits_l[4][kLpHits];
+    __shared__ int64_t lp_ssa[4][kLsStage];   // each wave's staged discoveries
+    __shared__ u64 lp_sv[4][kLsStage];
     __shared__ int64_t ws[4];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus] || !sl[lsPull]) return;
@@ -2591,6 +2724,11 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
     const int nb = a.nb, W = a.W;
     LpHit* hits = lp_hits_l[wave];
     for (int s = threadIdx.x; s < 4 * nb; s += 256) lp_merge[s] = ~0ull;
+    int64_t* ssa = lp_ssa[wave];
+    u64* sv = lp_sv[wave];
+    int sn = 0;   // staged discoveries of this wave (wave-uniform)
+    LpProf pf;
+    const int64_t tk0 = a.prof ? (int64_t)wall_clock64() : 0;
     __syncthreads();
     u64 best[WW];
 #pragma unroll
@@ -2607,7 +2745,7 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
         const int64_t q = (ch.end - ch.beg + 3) / 4;
         const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
         // one "atom" on lane 0: this wave's quarter of the chunk
-        lp_walk<WW>(a, t, lane == 0 ? b : 0, lane == 0 ? max<int64_t>(e - b, 0) : 0, vw, hits, best, nbytes,
+        lp_walk<WW>(a, t, lane == 0 ? b : 0, lane == 0 ? max<int64_t>(e - b, 0) : 0, vw, hits, best, nbytes, pf,
                     [&](int, u64* bst) {
 #pragma unroll
                         for (int w = 0; w < WW; ++w)
@@ -2628,6 +2766,7 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
         }
         __syncthreads();
     }
+    if (a.prof) pf.v[6] += (int64_t)wall_clock64() - tk0;
     // light atoms
     const int64_t nwv = (int64_t)gridDim.x * 4;
     for (int64_t t0 = ((int64_t)blockIdx.x * 4 + wave) * 64; t0 < a.A; t0 += nwv * 64) {
@@ -2652,14 +2791,21 @@ __global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
                 if (any) cnt = ee - eb;
             }
         }
-        lp_walk<WW>(a, (int32_t)t, eb, cnt, vw, hits, best, nbytes, [&](int o, u64* bst) {
+        lp_walk<WW>(a, (int32_t)t, eb, cnt, vw, hits, best, nbytes, pf, [&](int o, u64* bst) {
 #pragma unroll
             for (int w = 0; w < WW; ++w) {   // the atom's discoveries: a lane per seed
                 if (w >= W) break;
                 const int s = w * 64 + lane;
-                ls_append(a, d, s < nb && bst[w] != ~0ull, (int64_t)s * a.A + (t0 + o), bst[w]);
+                ls_append_staged(a, d, s < nb && bst[w] != ~0ull, (int64_t)s * a.A + (t0 + o), bst[w], ssa, sv, sn);
             }
         });
+    }
+    ls_stage_flush(a, d, ssa, sv, sn);
+    if (a.prof) {
+        pf.v[7] += (int64_t)wall_clock64() - tk0;
+        if (lane == 0)
+            for (int k = 0; k < 8; ++k)
+                if (pf.v[k]) atomicAdd((unsigned long long*)&a.ctl[kLsProf + k], (unsigned long long)pf.v[k]);
     }
     ls_add_bytes(a, nbytes, ws);
 }
@@ -2685,15 +2831,33 @@ __global__ void __launch_bounds__(256) hgx_lp_hfinal(LsArgs a, int32_t d) {
     }
 }
 
-// A bit per discovery at its key.  Push levels first take the value out of the hash slot and clear the
-// slot; pull levels clear the frontier rows, the union bitmap and the frontier hash.
-__global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
+// Ranking a level's discoveries by key (round 5; it replaced a bit per discovery in a global bitmap over
+// the level's key space, a popcount prefix per word and an emit that read the word and its prefix at
+// random: config 2's drop-in level of 258M discoveries fetched 70 GB and wrote 25 GB in that emit).
+// The key space is cut into buckets of 2^bs keys (~512 buckets of 64 .. 2^18 keys; up to 16384 buckets
+// of 2^18 keys for 32-bit keys):
+//   hgx_lr_count    per block an LDS histogram of its range of the discovery list, one global add per
+//                   bucket it touched (push levels first take the value out of the hash slot and clear
+//                   the slot; pull levels clear the frontier rows and the union bitmap)
+//   hgx_lr_scan     one block: bucket starts (the level's ranks are key order, so bucket b's ranks are
+//                   [start b, start b+1)), the level's size published to the host and the next level
+//   hgx_lr_scatter  per block the same range again: a contiguous slot range per bucket claimed with one
+//                   global add, the discoveries copied into it (runs of a bucket per block: coalesced)
+//   hgx_lr_rank     a workgroup per bucket: an LDS bitmap of its keys and a popcount prefix per word;
+//                   rank = start + prefix + bits below; pair `rank` of the level, entry `rank` of the next
+//                   frontier, the examined bit.  The writes of a bucket land in one window of the outputs.
+__global__ void __launch_bounds__(256) hgx_lr_count(LsArgs a, int32_t d) {
     __shared__ int64_t pre[kLsDSegs + 2];
+    __shared__ uint32_t hist[kLrMaxBuckets];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
     const bool pull = sl[lsPull] != 0;
-    const int64_t n = ls_disc_prefix(a, d, pre);
-    for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
+    const int bs = lr_bucket_bits(sl[lsW]);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    for (int b = threadIdx.x; b < nbk; b += 256) hist[b] = 0u;
+    const int64_t n = ls_disc_prefix(a, d, pre);   // (syncs the block)
+    const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+    for (int64_t x = lo + threadIdx.x; x < hi; x += 256) {
         const int64_t pos = ls_disc_pos(a, pre, x);
         u64 v = a.dval[pos];
         if (!pull) {   // v is the hash slot
@@ -2703,46 +2867,32 @@ __global__ void __launch_bounds__(256) hgx_ls_bits(LsArgs a, int32_t d) {
             a.hkey[hs] = kLsEmpty;
             a.hval[hs] = ~0ull;
         }
-        const u64 kk = (v >> 32) - 1ull;
-        atomicOr((unsigned long long*)&a.bm[kk >> 6], 1ull << (kk & 63));
+        atomicAdd(&hist[((v >> 32) - 1ull) >> bs], 1u);
     }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbk; b += 256)
+        if (hist[b]) atomicAdd(&a.bcnt[b], hist[b]);
     if (pull) {
         const int64_t nu = sl[lsU];
         for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < nu; u += (int64_t)gridDim.x * 256) {
             const int32_t p = a.ulist[u];
-            for (int w = 0; w < a.W; ++w) a.frow[(int64_t)p * a.W + w] = 0ull;
+            for (int w = 0; w < a.W; ++w) a.frow[u * a.W + w] = 0ull;
             a.ubit[p >> 6] = 0ull;
         }
     }
 }
 
-__global__ void __launch_bounds__(256) hgx_ls_wprefix(LsArgs a, int32_t d) {
-    __shared__ int64_t ws[4];
-    const int64_t* sl = ls_slot(a, d);
-    if (a.ctl[kLsStatus]) return;
-    const int64_t W = sl[lsW];
-    const int64_t lo = ls_lo(W, blockIdx.x), hi = ls_lo(W, blockIdx.x + 1);
-    const int64_t piece = (hi - lo + 255) / 256, p0 = lo + threadIdx.x * piece, p1 = min(hi, p0 + piece);
-    int64_t s = 0;
-    for (int64_t w = p0; w < p1; ++w) s += __popcll(a.bm[w]);
-    int64_t tot;
-    int64_t run = ls_block_scan(s, ws, &tot);
-    for (int64_t w = p0; w < p1; ++w) {
-        a.wpre[w] = (uint32_t)run;
-        run += __popcll(a.bm[w]);
-    }
-    if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq) {
-    __shared__ int64_t ws[4], off[kLsG], pre[kLsDSegs + 2];
+// One block of 1024 threads.
+__global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq) {
+    __shared__ int64_t pre[kLsDSegs + 2];
+    __shared__ int64_t wsum[16];
     int64_t* sl = ls_slot(a, d);
     int64_t status = a.ctl[kLsStatus];
-    const int64_t W = sl[lsW], out0 = sl[lsOut];
+    const int64_t out0 = sl[lsOut];
     int64_t n = ls_disc_prefix(a, d, pre);
-    if (!status && (n > a.cap || out0 + n > a.cap)) status = 1;   // the pairs outgrow the output (every block agrees)
+    if (!status && (n > a.cap || out0 + n > a.cap)) status = 1;   // the pairs outgrow the output
     if (status) n = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (threadIdx.x == 0) {
         if (status) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)status);
         int64_t* nx = a.ctl + ((d + 1) % kLsSlots) * kLsSlotWords;
         nx[lsF] = n;
@@ -2756,28 +2906,113 @@ __global__ void __launch_bounds__(256) hgx_ls_emit(LsArgs a, int32_t d, u64 seq)
         __threadfence_system();
         __hip_atomic_store(hf + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (n == 0) return;
-    ls_block_offsets(a.bsum, off, ws);
+    if (n == 0) return;   // (every thread: n is the block's)
+    const int bs = lr_bucket_bits(sl[lsW]);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    constexpr int per = kLrMaxBuckets / 1024;
+    const int b0 = threadIdx.x * per;
+    int64_t c[per], s = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        c[k] = b0 + k < nbk ? (int64_t)a.bcnt[b0 + k] : 0;
+        s += c[k];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t run = x - s;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        if (b0 + k < nbk) {
+            a.bstart[b0 + k] = run;
+            a.bcur[b0 + k] = (uint32_t)run;
+        }
+        run += c[k];
+    }
+    if (threadIdx.x == 1023) a.bstart[nbk] = run;   // == n
+}
+
+__global__ void __launch_bounds__(256) hgx_lr_scatter(LsArgs a, int32_t d) {
+    __shared__ int64_t pre[kLsDSegs + 2];
+    __shared__ uint32_t slot[kLrMaxBuckets];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus]) return;
+    const int bs = lr_bucket_bits(sl[lsW]);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    for (int b = threadIdx.x; b < nbk; b += 256) slot[b] = 0u;
+    const int64_t n = ls_disc_prefix(a, d, pre);
+    const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+    for (int64_t x = lo + threadIdx.x; x < hi; x += 256)
+        atomicAdd(&slot[((a.dval[ls_disc_pos(a, pre, x)] >> 32) - 1ull) >> bs], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbk; b += 256)   // this block's slot range of each bucket it holds
+        if (slot[b]) slot[b] = atomicAdd(&a.bcur[b], slot[b]);
+    __syncthreads();
+    for (int64_t x = lo + threadIdx.x; x < hi; x += 256) {
+        const int64_t pos = ls_disc_pos(a, pre, x);
+        const u64 v = a.dval[pos];
+        const uint32_t q = atomicAdd(&slot[((v >> 32) - 1ull) >> bs], 1u);
+        a.bk_v[q] = v;
+        a.bk_sa[q] = a.disc[pos];
+    }
+}
+
+__global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d) {
+    __shared__ u64 bm[1 << (kLrMaxBucketBits - 6)];
+    __shared__ uint32_t wp[1 << (kLrMaxBucketBits - 6)];
+    __shared__ int64_t ws[4];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || sl[lsN] == 0) return;
+    const int64_t out0 = sl[lsOut];
+    const int bs = lr_bucket_bits(sl[lsW]);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    const int nw = 1 << (bs - 6);                 // bitmap words of a bucket
+    const int per = (nw + 255) / 256;
     const int nx = (d + 1) & 1;
     const bool last = d + 1 >= a.maxd;
-    for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
-        const int64_t pos = ls_disc_pos(a, pre, x);
-        const int64_t sa = a.disc[pos];
-        const u64 v = a.dval[pos];
-        const u64 kk = (v >> 32) - 1ull;
-        const int64_t w = (int64_t)(kk >> 6);
-        int b = (int)(w * kLsG / W);   // the block whose word range holds w
-        while (b + 1 < kLsG && ls_lo(W, b + 1) <= w) ++b;
-        while (b > 0 && ls_lo(W, b) > w) --b;
-        const int64_t r = off[b] + a.wpre[w] + __popcll(a.bm[w] & ((1ull << (kk & 63)) - 1ull));
-        const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
-        a.out_link[out0 + r] = (int32_t)(uint32_t)v;
-        a.out_atom[out0 + r] = t;
-        a.fs[nx][r] = s;   // (the last level's too: its pairs' runs)
-        if (!last) {       // the next frontier and the examined bit, unless no level follows
-            a.fa[nx][r] = t;
-            atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
+    for (int b = blockIdx.x; b < nbk; b += gridDim.x) {   // block-uniform
+        const int64_t s0 = a.bstart[b], s1 = a.bstart[b + 1];
+        if (s0 == s1) continue;
+        for (int w = threadIdx.x; w < nw; w += 256) bm[w] = 0ull;
+        __syncthreads();
+        const u64 kb = (u64)b << bs;
+        for (int64_t i = s0 + threadIdx.x; i < s1; i += 256) {
+            const u64 kk = (a.bk_v[i] >> 32) - 1ull - kb;
+            atomicOr((unsigned long long*)&bm[kk >> 6], 1ull << (kk & 63));
         }
+        __syncthreads();
+        const int w0 = threadIdx.x * per;
+        int64_t c = 0;
+        for (int k = 0; k < per && w0 + k < nw; ++k) c += __popcll(bm[w0 + k]);
+        int64_t tot;
+        int64_t run = ls_block_scan(c, ws, &tot);   // (syncs)
+        for (int k = 0; k < per && w0 + k < nw; ++k) {
+            wp[w0 + k] = (uint32_t)run;
+            run += __popcll(bm[w0 + k]);
+        }
+        __syncthreads();
+        for (int64_t i = s0 + threadIdx.x; i < s1; i += 256) {
+            const u64 v = a.bk_v[i];
+            const int64_t sa = a.bk_sa[i];
+            const u64 kk = (v >> 32) - 1ull - kb;
+            const int64_t r = s0 + wp[kk >> 6] + __popcll(bm[kk >> 6] & ((1ull << (kk & 63)) - 1ull));
+            const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
+            a.out_link[out0 + r] = (int32_t)(uint32_t)v;
+            a.out_atom[out0 + r] = t;
+            a.fs[nx][r] = s;   // (the last level's too: its pairs' runs)
+            if (!last) {       // the next frontier and the examined bit, unless no level follows
+                a.fa[nx][r] = t;
+                atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
+            }
+        }
+        __syncthreads();   // bm / wp are reused by the next bucket
     }
 }
 
@@ -2811,6 +3046,40 @@ __global__ void __launch_bounds__(256) k_pin_j(int64_t M, const int64_t* __restr
                 else hi = mid;
             }
             pin_j[q] = (int32_t)(lo - base);
+        }
+    }
+}
+
+// Pull records: for incidence entry e = (t, L) -- the entry pin q of L points at, inc_off[t] + pin_j[q] --
+// rec[4e .. 4e+1] = L's targets (<= 8, -1 padded), rec[4e+2 .. 4e+3] = their pin_j, meta[e] = (link
+// atom, arity).  The pull walk reads them in entry order (streamed) instead of L's offsets, link atom,
+// target row and pin indices at random (four lines per entry for ~40 useful bytes).  A thread per link;
+// a target repeated in L writes its one entry several times with the same bytes.  Rows of > 8 targets
+// get the meta only (the walk reads them through tgt_off).
+__global__ void __launch_bounds__(256) k_pull_rec(int64_t M, const int64_t* __restrict__ tgt_off,
+                                                  const int32_t* __restrict__ tgt_idx, const int64_t* __restrict__ inc_off,
+                                                  const int32_t* __restrict__ pin_j, const int32_t* __restrict__ link_atom,
+                                                  int4* __restrict__ rec, int2* __restrict__ meta) {
+    for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < M; L += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = tgt_off[L];
+        const int32_t n = (int32_t)(tgt_off[L + 1] - b);
+        int32_t tg[8], pj[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            tg[q] = q < n ? tgt_idx[b + q] : -1;
+            pj[q] = q < n ? pin_j[b + q] : 0;
+        }
+        const int2 m = make_int2(link_atom[L], n);
+        for (int32_t q = 0; q < n; ++q) {
+            const int32_t t = q < 8 ? tg[q] : tgt_idx[b + q];
+            const int64_t e = inc_off[t] + (q < 8 ? pj[q] : pin_j[b + q]);
+            meta[e] = m;
+            if (n <= 8) {
+                rec[4 * e] = make_int4(tg[0], tg[1], tg[2], tg[3]);
+                rec[4 * e + 1] = make_int4(tg[4], tg[5], tg[6], tg[7]);
+                rec[4 * e + 2] = make_int4(pj[0], pj[1], pj[2], pj[3]);
+                rec[4 * e + 3] = make_int4(pj[4], pj[5], pj[6], pj[7]);
+            }
         }
     }
 }
@@ -3572,6 +3841,37 @@ const int32_t* ensure_pin_j(hgx_graph* g) {
     return root->pin_j;
 }
 
+// The pull records (k_pull_rec) of the snapshot, built after pin_j on the first pull call; 72 bytes per
+// incidence entry (config 2: 14.4 GB), so a snapshot whose records would take more than half of the
+// traversal budget (HGX_OPT_SEQ_BUDGET, 48 GiB by default) keeps the random reads instead
+// (HGX_LS_PULL_REC=0 as well: A/B).
+void ensure_pull_rec(hgx_graph* g, const int32_t* pin_j) {
+    hgx_graph* root = g->base ? g->base : g;
+    std::lock_guard<std::mutex> lk(root->ylist_mu);
+    if (root->pull_rec_state != 0 || root->I <= 0) return;
+    const char* ev = std::getenv("HGX_LS_PULL_REC");
+    const size_t bytes = (size_t)72 * (size_t)root->I;
+    if ((ev && std::atoi(ev) == 0) || (int64_t)bytes > g->seq_budget_bytes / 2) {
+        root->pull_rec_state = -1;
+        return;
+    }
+    int4* rec = nullptr;
+    int2* meta = nullptr;
+    if (hipMalloc(&rec, 64 * (size_t)root->I) != hipSuccess || hipMalloc(&meta, 8 * (size_t)root->I) != hipSuccess) {
+        (void)hipGetLastError();   // no room: the walk keeps its random reads
+        if (rec) (void)hipFree(rec);
+        root->pull_rec_state = -1;
+        return;
+    }
+    k_pull_rec<<<grid_for(root->M, 256, 16384), 256, 0, g->stream>>>(root->M, root->tgt_off, root->tgt_idx, root->inc_off,
+                                                                    pin_j, root->link_atom, rec, meta);
+    HGX_CHECK_LAUNCH();
+    HGX_HIP(hipStreamSynchronize(g->stream));
+    root->pull_rec = rec;
+    root->pull_meta = meta;
+    root->pull_rec_state = 1;
+}
+
 int log2_ceil(int64_t x) {
     int b = 0;
     while (((int64_t)1 << b) < x) ++b;
@@ -3613,7 +3913,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     const bool small = std::getenv("HGX_LS_SMALL") != nullptr;
     for (int attempt = 0;; ++attempt) {
         const int64_t cap = std::min(full, std::max<int64_t>(g->ls_cap, small ? 64 : (int64_t)1 << 20));
-        const int64_t wcap = std::max<int64_t>(g->ls_wcap, small ? 16 : (int64_t)1 << 18);
         const int64_t tcap = std::max<int64_t>(g->ls_tcap, small ? 8 : (int64_t)1 << 16);
         const int64_t rcap = std::max<int64_t>(g->ls_rcap, small ? 4 : (int64_t)1 << 14);
         const int hbits = std::max<int>(log2_ceil(std::max<int64_t>(g->ls_hcap, small ? 64 : (int64_t)1 << 21)), 6);
@@ -3642,7 +3941,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.W = W;
         a.maxd = maxd;
         a.cap = cap;
-        a.wcap = wcap;
         a.tcap = tcap;
         a.rcap = rcap;
         a.hflag = hflag_d;
@@ -3663,8 +3961,11 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         const size_t nd = (size_t)(cap + kLsDSegs * a.segcap);
         a.disc = (int64_t*)w.take(sizeof(int64_t) * nd);
         a.dval = (u64*)w.take(sizeof(u64) * nd);
-        a.bm = (u64*)w.take(sizeof(u64) * (size_t)wcap);
-        a.wpre = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)wcap);
+        a.bcnt = (uint32_t*)w.take(sizeof(uint32_t) * kLrMaxBuckets);
+        a.bcur = (uint32_t*)w.take(sizeof(uint32_t) * kLrMaxBuckets);
+        a.bstart = (int64_t*)w.take(sizeof(int64_t) * (kLrMaxBuckets + 1));
+        a.bk_v = (u64*)w.take(sizeof(u64) * nd);
+        a.bk_sa = (int64_t*)w.take(sizeof(int64_t) * nd);
         a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
         a.out_atom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
         a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
@@ -3675,8 +3976,15 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.pull = pull_off ? 0 : pull;
         a.I = g->I;
         a.pin_j = pin_j;
+        a.prof = std::getenv("HGX_LS_PROF") ? 1 : 0;
+        if (a.pull && pin_j) {
+            ensure_pull_rec(g, pin_j);
+            a.prec = root->pull_rec;
+            a.pmeta = root->pull_meta;
+        }
         if (a.pull) {
-            a.frow = (u64*)w.take(rows);
+            const size_t urows = sizeof(u64) * (size_t)std::max<int64_t>(std::min(cap, A), nb) * (size_t)W;   // |union| <= min(F, A)
+            a.frow = (u64*)w.take(urows);
             a.ubit = (u64*)w.take(sizeof(u64) * (size_t)(A / 64 + 1));
             a.ulist = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(cap, nb));
             a.uidx = (int32_t*)w.take(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1));
@@ -3687,7 +3995,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             a.n_heavy = root->n_heavy;
             a.heavy_atom = root->heavy_atom;
             a.hbest = (u64*)w.take(sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1));
-            HGX_HIP(hipMemsetAsync(a.frow, 0, rows, st));
+            HGX_HIP(hipMemsetAsync(a.frow, 0, urows, st));
             HGX_HIP(hipMemsetAsync(a.ubit, 0, sizeof(u64) * (size_t)(A / 64 + 1), st));
             HGX_HIP(hipMemsetAsync(a.hbest, 0xFF, sizeof(u64) * (size_t)std::max<int64_t>(root->n_heavy * nb, 1), st));
         }
@@ -3721,9 +4029,10 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 else hgx_lp_pull<16><<<2048, 256, lp_smem, st>>>(a, d);
                 hgx_lp_hfinal<<<256, 256, 0, st>>>(a, d);
             }
-            hgx_ls_bits<<<512, 256, 0, st>>>(a, d);
-            hgx_ls_wprefix<<<kLsG, 256, 0, st>>>(a, d);
-            hgx_ls_emit<<<512, 256, 0, st>>>(a, d, base + (u64)d + 1);
+            hgx_lr_count<<<kLrG, 256, 0, st>>>(a, d);
+            hgx_lr_scan<<<1, 1024, 0, st>>>(a, d, base + (u64)d + 1);
+            hgx_lr_scatter<<<kLrG, 256, 0, st>>>(a, d);
+            hgx_lr_rank<<<kLrG, 256, 0, st>>>(a, d);
             HGX_CHECK_LAUNCH();
         };
         int64_t total = 0, status = 0;
@@ -3767,7 +4076,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             if (attempt > 48) fail(HGX_E_DEVICE, "hgx_bfs_sequence: level-synchronous capacities did not converge");
             if (status & 1) g->ls_cap = std::min(full, cap * 4);
             if (status & 2) g->ls_rcap = rcap * 4;
-            if (status & 4) g->ls_wcap = wcap * 4;
             if (status & 8) g->ls_tcap = tcap * 4;
             if (status & 32) g->ls_hcap = ((int64_t)1 << hbits) * 4;
             if (status & 128) pull_off = true;   // a pull pass's hit list overflowed: this call pushes
@@ -3777,6 +4085,12 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         out.traversed += (double)ctl[kLsTrav];
         out.bytes += (double)ctl[kLsBytes];
         out.pull_levels += ctl[kLsPullN];
+        if (a.prof)
+            std::fprintf(stderr, "[hgx ls prof] pull walk (wave-ms summed): phase A %.1f, phase B %.1f, flush %.1f, heavy %.1f, "
+                                 "all %.1f; passes %lld, B iterations %lld, flushes %lld\n",
+                         ctl[kLsProf] * 1e-5, ctl[kLsProf + 1] * 1e-5, ctl[kLsProf + 2] * 1e-5, ctl[kLsProf + 6] * 1e-5,
+                         ctl[kLsProf + 7] * 1e-5, (long long)ctl[kLsProf + 3], (long long)ctl[kLsProf + 4],
+                         (long long)ctl[kLsProf + 5]);
         // [links total][atoms total][pad to 8 bytes][runs 3 x nruns]
         PoolBuf hb = take_host_buf(g, 8 * (size_t)total + 8 + 24 * (size_t)std::max<int64_t>(nruns, 1));
         out.bufs.push_back(hb);
@@ -4408,6 +4722,13 @@ void free_yield_lists(hgx_graph* g) {
     std::lock_guard<std::mutex> lk(g->ylist_mu);
     if (g->pin_j && !g->base) (void)hipFree(g->pin_j);   // the level engine's pin index (the incidence changed)
     g->pin_j = nullptr;
+    if (!g->base) {   // and its pull records
+        if (g->pull_rec) (void)hipFree(g->pull_rec);
+        if (g->pull_meta) (void)hipFree(g->pull_meta);
+    }
+    g->pull_rec = nullptr;
+    g->pull_meta = nullptr;
+    g->pull_rec_state = 0;
     for (YieldList& y : g->ylists) {
         (void)hipFree(y.off);
         (void)hipFree(y.row);
