@@ -11,7 +11,12 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# HGX_LIB_VARIANT=<name>: load tools/native/build/libhgx_<name>.so instead (A/B builds of the engine side by
+# side in one GPU session; tools only -- the tests, smoke() and bench.py never set it)
 LIB_PATH = os.path.join(_HERE, "libhgx.so")
+if os.environ.get("HGX_LIB_VARIANT"):
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "native", "build",
+                            f"libhgx_{os.environ['HGX_LIB_VARIANT']}.so")
 GEN_PATH = os.path.join(_HERE, "libhgx_gen.so")
 
 HGX_OK = 0

@@ -2047,7 +2047,7 @@ __device__ __forceinline__ void ls_append(const LsArgs& a, int d, bool isnew, in
 // Staged appends (the pull walk, round 5): a wave collects its discoveries in LDS and places up to
 // kLsStage of them with ONE reservation -- the per-atom append (an atomic round trip on the segment
 // counter for ~27 discoveries) was a tenth of the pull's time on config 2's drop-in level.
-constexpr int kLsStage = 128;
+constexpr int kLsStage = 80;   // (the pull block's LDS stays under 40 KB: 4 blocks a CU)
 __device__ __forceinline__ void ls_stage_flush(const LsArgs& a, int d, const int64_t* ssa, const u64* sv, int n) {
     if (n == 0) return;   // (n is wave-uniform; every lane calls)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2433,7 +2433,8 @@ constexpr int kLpHits = 64 * 8;   // one pass of a wave: <= 64 entries of <= 8 t
 // occurrence, the mode's positions (3.2), t's best yielded position.  Rows of <= 8 targets: a mask of
 // the hit positions over the row in registers; longer rows set long_row (walked by lp_long_row).
 struct LpCand {
-    int32_t tg[8], qt[8], pj[8];   // pj: the record's pin indices (pull records only)
+    int32_t tg[8], pj[8];   // pj: the hits' pin indices
+    uint32_t qt;            // t's best yielded position for co-target q: 4 bits each
     uint32_t mask;
     int64_t tb;
     int32_t rown, la;
@@ -2449,6 +2450,7 @@ __device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t
     int32_t n;
     if (a.pmeta) {   // the entry's pull record: (link atom, arity), <= 8 targets, their pin indices -- streamed
         // in entry order and loaded together with the type (one round trip before the union probes)
+        // (nontemporal loads of the records measured no faster: 119 vs 116 ms a config-2 drop-in call)
         const int32_t ty = a.want_type >= 0 ? a.inc_type[e] : 0;
         const int2 m = a.pmeta[e];
         const int4 r0 = a.prec[4 * e], r1 = a.prec[4 * e + 1], r2 = a.prec[4 * e + 2], r3 = a.prec[4 * e + 3];
@@ -2494,13 +2496,14 @@ __device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t
 #pragma unroll
         for (int q = 0; q < 8; ++q) c.tg[q] = q < n ? a.tgt_idx[tb + q] : -1;
     }
-    u64 onf[8];   // union bits of the co-targets, loaded together
+    uint32_t onf[8];   // union bits of the co-targets, loaded together (32-bit words: fewer registers in flight)
+    const uint32_t* ub = (const uint32_t*)a.ubit;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) onf[q] = (q < n && c.tg[q] != t) ? a.ubit[c.tg[q] >> 6] >> (c.tg[q] & 63) : 0ull;
+    for (int q = 0; q < 8; ++q) onf[q] = (q < n && c.tg[q] != t) ? ub[c.tg[q] >> 5] >> (c.tg[q] & 31) : 0u;
+    c.qt = 0u;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        c.qt[q] = -1;
-        if (!(onf[q] & 1ull)) continue;   // on no seed's frontier (or t itself, or past the row)
+        if (!(onf[q] & 1u)) continue;   // on no seed's frontier (or t itself, or past the row)
         const int32_t p = c.tg[q];
         bool dup = false;   // p's first occurrence only
 #pragma unroll
@@ -2519,8 +2522,10 @@ __device__ __forceinline__ int lp_hits_count(const LsArgs& a, int32_t t, int64_t
 #pragma unroll
         for (int q2 = 0; q2 < 8; ++q2)
             if (q2 >= lo && q2 < hi && c.tg[q2] == t && (qt < 0 || a.rev)) qt = q2;
-        c.qt[q] = qt;
-        if (qt >= 0) c.mask |= 1u << q;
+        if (qt >= 0) {
+            c.qt |= (uint32_t)qt << (4 * q);
+            c.mask |= 1u << q;
+        }
     }
     if (!a.pmeta && c.mask) {   // the hits' pin indices at random (no pull records)
 #pragma unroll
@@ -2572,7 +2577,7 @@ struct LpProf {
 template <int WW, class Flush>
 __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb, int64_t cnt, const u64* vw, LpHit* hits,
                                         u64* best, int64_t& nbytes, LpProf& pf, Flush&& flush) {
-    constexpr int HB = WW >= 8 ? 2 : 16 / WW;
+    constexpr int HB = WW >= 4 ? 2 : 8 / WW;
     const int lane = threadIdx.x & 63;
     int64_t x = cnt;
 #pragma unroll
@@ -2635,7 +2640,8 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
                 h.u = us[q];
                 h.j = (uint32_t)c.pj[q];
                 h.la = c.la;
-                h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - c.qt[q] : c.qt[q]) | (uint32_t)o << 16;
+                const int32_t qt = (int32_t)((c.qt >> (4 * q)) & 15u);
+                h.kq_o = (uint32_t)(a.rev ? c.rown - 1 - qt : qt) | (uint32_t)o << 16;
                 hits[pos++] = h;
             }
         if (lr)
@@ -2656,14 +2662,17 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
             pf.v[3] += 1;
         }
         for (int h0 = 0; h0 < total;) {   // phase B (wave-uniform)
-            LpHit H[HB];
-#pragma unroll
-            for (int q = 0; q < HB; ++q) H[q] = hits[min(h0 + q, total - 1)];
-            const int ho = (int)(H[0].kq_o >> 16);
+            // only the union slots stay in registers while the rows load (the other fields are read
+            // from LDS again after): 2 waves/SIMD at 235 VGPRs with whole hits held
+            int32_t hu[HB];
+            const int ho = (int)(hits[h0].kq_o >> 16);
             int hn = 1;   // up to HB consecutive hits of the same atom
 #pragma unroll
-            for (int q = 1; q < HB; ++q)
-                if (hn == q && h0 + q < total && (int)(H[q].kq_o >> 16) == ho) ++hn;
+            for (int q = 0; q < HB; ++q) {
+                const LpHit hq = hits[min(h0 + q, total - 1)];
+                hu[q] = hq.u;
+                if (q > 0 && hn == q && h0 + q < total && (int)(hq.kq_o >> 16) == ho) ++hn;
+            }
             if (ho != cur) {   // the hits moved on to the next atom: flush the finished one
                 if (cur >= 0) flush_cur();
                 cur = ho;
@@ -2682,19 +2691,22 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
                     fw[q][w] = 0ull;
                     pre[q][w] = 0u;
                     if (q < hn && w < a.W) {
-                        fw[q][w] = a.frow[(int64_t)H[q].u * a.W + w];
-                        if (w * 64 + lane < a.nb) pre[q][w] = a.E[(int64_t)H[q].u * a.nb + w * 64 + lane];
+                        fw[q][w] = a.frow[(int64_t)hu[q] * a.W + w];
+                        if (w * 64 + lane < a.nb) pre[q][w] = a.E[(int64_t)hu[q] * a.nb + w * 64 + lane];
                     }
                 }
 #pragma unroll
-            for (int q = 0; q < HB; ++q)
+            for (int q = 0; q < HB; ++q) {
+                if (q >= hn) break;
+                const LpHit hq = hits[h0 + q];
 #pragma unroll
                 for (int w = 0; w < WW; ++w) {
-                    if (q >= hn || w >= a.W || !(((fw[q][w] & needb[w]) >> lane) & 1ull)) continue;
-                    const u64 it = (u64)pre[q][w] + H[q].j;
-                    const u64 v = ((((it << a.kbits) | (H[q].kq_o & 0xFFFFu)) + 1ull) << 32) | (u64)(uint32_t)H[q].la;
+                    if (w >= a.W || !(((fw[q][w] & needb[w]) >> lane) & 1ull)) continue;
+                    const u64 it = (u64)pre[q][w] + hq.j;
+                    const u64 v = ((((it << a.kbits) | (hq.kq_o & 0xFFFFu)) + 1ull) << 32) | (u64)(uint32_t)hq.la;
                     best[w] = min(best[w], v);
                 }
+            }
             nbytes += lane == 0 ? (int64_t)hn * (8 * a.W + 4 * (int64_t)a.nb) : 0;
             h0 += hn;
             if (a.prof) pf.v[4] += 1;
@@ -2712,7 +2724,7 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
 // examined them; each atom's discoveries are appended when the walk leaves it.  WW: the row words
 // rounded up to a power of two (register minima).
 template <int WW>
-__global__ void __launch_bounds__(256) hgx_lp_pull(LsArgs a, int32_t d) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) hgx_lp_pull(LsArgs a, int32_t d) {
     extern __shared__ u64 lp_merge[];   // [4][nb]
     __shared__ LpHit lp_hits_l[4][kLpHits];
     __shared__ int64_t lp_ssa[4][kLsStage];   // each wave's staged discoveries
@@ -4013,6 +4025,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         hgx_ls_seed<<<grid_for(nb, 256), 256, 0, st>>>(a, nb, dseeds);
         HGX_CHECK_LAUNCH();
         const u64 base = g->seq_flag_seq;
+        static const int lr_scatter_g = std::getenv("HGX_LR_SCATTER_G") ? std::atoi(std::getenv("HGX_LR_SCATTER_G")) : kLrG;   // A/B
+        static const int lr_rank_g = std::getenv("HGX_LR_RANK_G") ? std::atoi(std::getenv("HGX_LR_RANK_G")) : kLrG;
         const size_t lp_smem = sizeof(u64) * 4 * (size_t)nb;
         auto enqueue = [&](int32_t d) {
             // grids: thousands of idle workgroups cost ~10 us a launch on small levels;
@@ -4031,8 +4045,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             }
             hgx_lr_count<<<kLrG, 256, 0, st>>>(a, d);
             hgx_lr_scan<<<1, 1024, 0, st>>>(a, d, base + (u64)d + 1);
-            hgx_lr_scatter<<<kLrG, 256, 0, st>>>(a, d);
-            hgx_lr_rank<<<kLrG, 256, 0, st>>>(a, d);
+            hgx_lr_scatter<<<lr_scatter_g, 256, 0, st>>>(a, d);
+            hgx_lr_rank<<<lr_rank_g, 256, 0, st>>>(a, d);
             HGX_CHECK_LAUNCH();
         };
         int64_t total = 0, status = 0;

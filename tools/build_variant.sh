@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build an A/B variant of libhgx.so from a modified copy of one engine source (in this container):
+#   bash tools/build_variant.sh <name> <file.hip> [<file2.hip> ...]
+# The files replace the same-named sources of hypergraphdb_amd/csrc for this build only; the result is
+# tools/native/build/libhgx_<name>.so, loaded by HGX_LIB_VARIANT=<name> (hypergraphdb_amd/_lib.py).
+set -eu
+NAME=$1
+shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+W=$(mktemp -d /tmp/hgxvar.XXXX)
+cp "$ROOT"/hypergraphdb_amd/csrc/*.hip "$ROOT"/hypergraphdb_amd/csrc/*.h "$W"/
+for f in "$@"; do cp "$f" "$W/$(basename "$f")"; done
+mkdir -p "$ROOT/tools/native/build"
+cd "$W"
+for f in hgx_graph hgx_bfs hgx_query hgx_seq hgx_part hgx_file; do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -I"$ROOT/include" -c $f.hip -o $f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/native/build/libhgx_$NAME.so" hgx_*.o \
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -rf "$W"
+echo "built tools/native/build/libhgx_$NAME.so"
