@@ -631,7 +631,7 @@ def dropin_config2(args, ctx, snap, g):
     if os.path.exists(os.path.join(ROOT, rel)):
         pj = json.load(open(os.path.join(ROOT, rel)))
         ks = pj.get("kernels", {})
-        dom = max((k for k in ks if k.startswith(("hgx_ls_", "hgx_lp_"))), key=lambda k: ks[k]["avg_ms"] * ks[k]["launches"],
+        dom = max((k for k in ks if k.startswith(("hgx_ls_", "hgx_lp_", "hgx_lr_"))), key=lambda k: ks[k]["avg_ms"] * ks[k]["launches"],
                   default=None)
         if dom and ks[dom].get("hbm_bytes_per_launch"):
             kk = ks[dom]
