@@ -6,6 +6,10 @@
 --until KERNEL keeps only the dispatches before the first launch of a kernel whose name contains
 KERNEL after the first BFS gather (bench.py runs config 2 first, then builds the config-3 snapshot:
 `--until k_validate` isolates the config-2 leg of the default bench command).
+--from-last KERNEL keeps only the dispatches from the last launch of KERNEL on (the last call of a tool
+that repeats one call: `--from-last hgx_ls_seed` is the steady-state drop-in call of tools/seq_c2.py).
+--min-ms X drops every dispatch shorter than X ms (by the trace pass; tools/seq_c5.py's single-seed calls
+beside its batched ones).
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
@@ -55,25 +59,39 @@ def cutoff(rows, until, after="hgx_link_gather"):
     return min(ids) if ids else None
 
 
-def load_counter(path, counter, until=None):
+def first_kept(rows, from_last):
+    """Dispatch id of the last launch of `from_last` (None = keep everything)."""
+    if not from_last:
+        return None
+    ids = [int(r["Dispatch_Id"]) for r in rows if from_last in r["Kernel_Name"]]
+    return max(ids) if ids else None
+
+
+def load_counter(path, counter, until=None, from_last=None):
     acc = defaultdict(list)
     if not os.path.exists(path):
         return acc
     with open(path) as f:
         rows = list(csv.DictReader(f))
     cut = cutoff(rows, until)
+    lo = first_kept(rows, from_last)
     for row in rows:
+        if lo is not None and int(row["Dispatch_Id"]) < lo:
+            continue
         if row["Counter_Name"] == counter and (cut is None or int(row["Dispatch_Id"]) < cut):
             acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
     return acc
 
 
-def load_trace(path, until=None):
+def load_trace(path, until=None, from_last=None):
     acc = defaultdict(list)
     with open(path) as f:
         rows = list(csv.DictReader(f))
     cut = cutoff(rows, until)
+    lo = first_kept(rows, from_last)
     for row in rows:
+        if lo is not None and int(row["Dispatch_Id"]) < lo:
+            continue
         if cut is None or int(row["Dispatch_Id"]) < cut:
             acc[short(row["Kernel_Name"])].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
     return acc
@@ -81,10 +99,19 @@ def load_trace(path, until=None):
 
 def main():
     argv = sys.argv[1:]
-    until = None
+    until = from_last = None
     if "--until" in argv:
         k = argv.index("--until")
         until = argv[k + 1]
+        del argv[k:k + 2]
+    min_ms = 0.0
+    if "--min-ms" in argv:
+        k = argv.index("--min-ms")
+        min_ms = float(argv[k + 1])
+        del argv[k:k + 2]
+    if "--from-last" in argv:
+        k = argv.index("--from-last")
+        from_last = argv[k + 1]
         del argv[k:k + 2]
     d, tag = argv[0], argv[1]
     workload = argv[2] if len(argv) > 2 else "config2"
@@ -94,9 +121,24 @@ def main():
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until)
-    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until)
-    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until)
+    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until, from_last)
+    if min_ms > 0:   # the passes dispatch in the same order: drop the short launches' counter values by rank
+        with open(os.path.join(d, "trace", "run_kernel_trace.csv")) as f:
+            rows = sorted(csv.DictReader(f), key=lambda r: int(r["Dispatch_Id"]))
+        short_rank = defaultdict(set)
+        seen = defaultdict(int)
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 < min_ms:
+                short_rank[k].add(seen[k])
+            seen[k] += 1
+        trace = {k: [t for t in v if t >= min_ms] for k, v in trace.items()}
+        trace = {k: v for k, v in trace.items() if v}
+    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until, from_last)
+    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until, from_last)
+    if min_ms > 0:
+        fetch = {k: [v for i, v in enumerate(vs) if i not in short_rank[k]] for k, vs in fetch.items()}
+        write = {k: [v for i, v in enumerate(vs) if i not in short_rank[k]] for k, vs in write.items()}
     # the commit of the code the passes measured (this script runs in the repository right after the
     # gpurun call that took them); bench.py copies it into the line's traffic_from, so the provenance
     # survives a GPU lease without .git
@@ -108,7 +150,8 @@ def main():
                                     timeout=10).stdout.strip())
     except Exception:
         commit, dirty = None, None
-    rows, js = [], {"tag": tag, "workload": workload, "kernels": {}, "commit": commit,
+    rows, js = [], {"tag": tag, "workload": workload, "kernels": {}, "commit": commit, "from_last": from_last,
+                    "min_ms": min_ms or None,
                     "commit_dirty": dirty,
                     "note": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE correction)"}
     for k in sorted(trace, key=lambda k: -sum(trace[k])):
@@ -129,6 +172,8 @@ def main():
         f.write(f"# rocprofv3 summary {tag} ({workload})\n\n")
         if until:
             f.write(f"Dispatches before the first `{until}` launch after the BFS only (the {workload} leg of the command).\n\n")
+        if from_last:
+            f.write(f"Dispatches from the last `{from_last}` launch on only (the command's last call).\n\n")
         f.write("Kernel trace: `rocprofv3 --kernel-trace --stats`; HBM bytes from separate `--pmc FETCH_SIZE` and\n"
                 "`--pmc WRITE_SIZE` passes, bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch.\n\n")
         f.write("| kernel | launches | total ms | avg ms | fetch B/launch | write B/launch | HBM GB/s |\n")
