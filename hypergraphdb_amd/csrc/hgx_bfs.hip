@@ -1617,314 +1617,8 @@ __global__ void __launch_bounds__(256) hgx_opush(const int32_t* __restrict__ lis
     wave_add_sh(ctr + cScanned, n_scan);
 }
 
-// Flattened frontier push (HGX_OPT_PUSH_BATCH = K > 0): a wave takes K consecutive list atoms at
-// once and expands their incidence entries into one stream (a wave prefix sum over the degrees, an
-// entry's atom found by a binary search over the prefix in LDS), so its lanes carry the entries of
-// many atoms instead of the few of one.  Stage 1 prefilters type + yield flags (kUnroll passes in
-// flight), stage 2 runs the entry chain (link row, target offsets, <= 8 targets in registers, full
-// bits) for the passing entries 64 at a time and stages the eligible (target, source) pairs in LDS,
-// stage 3 ORs each pair's source row into the target's accumulator row, one G-lane group per pair
-// (16-byte loads of the source row; a word is ORed only when it is nonzero and missing).  With one
-// wave per atom, a config-5 level of ~30K atoms of degree ~4 kept 2048 waves on ~15 sequential
-// dependent chains each, with ~4 of 64 lanes busy.
-constexpr int kFlatMax = 64;     // atoms per batch at most (one per lane)
-constexpr int kPairBuf = 512;    // (target, source) pairs staged per wave
-
-constexpr int kFlatRows = 16;   // batch atoms whose row words sit in LDS (K is clamped to this)
-
-struct FlatLds {
-    int32_t v[kFlatMax];
-    int64_t beg[kFlatMax];
-    int32_t pre[kFlatMax + 1];   // inclusive prefix of the batch's degrees, pre[0] = 0
-    int32_t ej[kEBuf];           // passing entries: batch slot of the atom
-    int64_t ei[kEBuf];           //                  incidence entry
-    int32_t pt[kPairBuf];        // pairs: target
-    int32_t ps[kPairBuf];        //        batch slot of the source atom
-    int32_t cbuf[kCBuf];         // fresh candidates not yet appended
-    uint32_t wmask[kFlatRows];   // nonzero words of each batch atom's row
-    u64 wval[kFlatRows * 16];    // the batch atoms' rows (W words each)
-    int32_t ppre[65];            // pair drain: exclusive prefix of the pairs' nonzero words
-};
-
-__device__ __forceinline__ void flat_cand_flush(FlatLds& sh, int& cc, int32_t* __restrict__ clist,
-                                                u64* __restrict__ n_clist) {
-    const int lane = threadIdx.x & 63;
-    if (cc == 0) return;
-    u64 base = 0;
-    if (lane == 0) base = atomicAdd(n_clist, (u64)cc);
-    base = __shfl(base, 0);
-    for (int i = lane; i < cc; i += 64) clist[base + i] = sh.cbuf[i];
-    __builtin_amdgcn_wave_barrier();
-    cc = 0;
-}
-
-// Stage 3: OR the source row of every staged pair into its target's accumulator row, one lane per
-// (pair, nonzero word of the source's row) -- the rows of a push level are sparse (one or two nonzero
-// words of 16 on config 5), so the words come from the batch's LDS row table and a wave pass covers
-// 64 of them; the first word of a pair sets the target's candidate bit and stages it.
-template <int W>
-__device__ __forceinline__ void flat_pairs(FlatLds& sh, int& np, int& cc, const u64* __restrict__ lvl,
-                                           u64* __restrict__ acc, u64* __restrict__ cand,
-                                           int32_t* __restrict__ clist, u64* __restrict__ n_clist) {
-    const int lane = threadIdx.x & 63;
-    const u64 lt = (1ull << lane) - 1ull;
-    (void)lvl;
-    __builtin_amdgcn_wave_barrier();
-    for (int p0 = 0; p0 < np; p0 += 64) {   // wave-uniform
-        const int p = p0 + lane;
-        const uint32_t wm = p < np ? sh.wmask[sh.ps[p]] : 0u;
-        const int cnt = __popc(wm);
-        int incl = cnt;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        const int T = __shfl(incl, 63);
-        sh.ppre[lane] = incl - cnt;
-        if (lane == 63) sh.ppre[64] = incl;
-        __builtin_amdgcn_wave_barrier();
-        for (int q0 = 0; q0 < T; q0 += 64) {   // wave-uniform
-            const int q = q0 + lane;
-            bool fresh = false;
-            int32_t t = 0;
-            if (q < T) {
-                int lo = 0, hi = 63;   // the pair holding item q
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sh.ppre[mid] <= q) lo = mid; else hi = mid - 1;
-                }
-                const int pp = p0 + lo, j = sh.ps[pp], r = q - sh.ppre[lo];
-                t = sh.pt[pp];
-                const int w = nth_set_bit((u64)sh.wmask[j], r);
-                const u64 val = sh.wval[j * W + w];
-                u64* a = acc + (int64_t)t * W + w;
-                if ((*a & val) != val) atomicOr(a, val);
-                if (r == 0) {
-                    const u64 cb = 1ull << (t & 63);
-                    if (!(cand[t >> 6] & cb)) fresh = !(atomicOr(&cand[t >> 6], cb) & cb);
-                }
-            }
-            const u64 fm = __ballot(fresh);
-            if (fm) {   // wave-uniform
-                const int nf = __popcll(fm);
-                if (cc + nf > kCBuf) flat_cand_flush(sh, cc, clist, n_clist);
-                if (fresh) sh.cbuf[cc + __popcll(fm & lt)] = t;
-                cc += nf;
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    np = 0;
-}
-
-// Stage 2 for up to 64 staged entries: the generator's eligible targets of each entry's link, as
-// (target, source) pairs.
-template <int W, int MODE>
-__device__ __forceinline__ void flat_entries(FlatLds& sh, int ne, int& np, int& cc,
-                                             const int32_t* __restrict__ inc_row, const int64_t* __restrict__ tgt_off,
-                                             const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
-                                             const u64* __restrict__ full, u64* __restrict__ acc,
-                                             u64* __restrict__ cand, int32_t* __restrict__ clist,
-                                             u64* __restrict__ n_clist, u64& n_links, u64& n_pins, u64& n_pairs) {
-    const int lane = threadIdx.x & 63;
-    const u64 lt = (1ull << lane) - 1ull;
-    constexpr int kRegRow = 8;
-    __builtin_amdgcn_wave_barrier();
-    for (int k0 = 0; k0 < ne; k0 += 64) {   // wave-uniform
-        const bool have = k0 + lane < ne;
-        int32_t v = -1, slot = 0;
-        int64_t b = 0;
-        int n = 0;
-        if (have) {
-            slot = sh.ej[k0 + lane];
-            v = sh.v[slot];
-            const int32_t L = inc_row[sh.ei[k0 + lane]];
-            b = tgt_off[L];
-            n = (int)(tgt_off[L + 1] - b);
-            ++n_links;
-            n_pins += (u64)n;
-        }
-        int32_t tr[kRegRow];
-        const bool reg = n <= kRegRow;
-#pragma unroll
-        for (int k = 0; k < kRegRow; ++k) tr[k] = (reg && k < n) ? tgt_idx[b + k] : -1;
-        int fv = -1, lv = -1;
-        if (reg) {
-#pragma unroll
-            for (int k = 0; k < kRegRow; ++k)
-                if (tr[k] == v) {
-                    if (fv < 0) fv = k;
-                    lv = k;
-                }
-        } else {
-            for (int p = 0; p < n; ++p)
-                if (tgt_idx[b + p] == v) {
-                    if (fv < 0) fv = p;
-                    lv = p;
-                }
-        }
-        unsigned em = 0;   // eligible register positions
-        if (reg) {
-            u64 fw[kRegRow];
-#pragma unroll
-            for (int k = 0; k < kRegRow; ++k) {
-                const bool e = tr[k] >= 0 && tr[k] != v && yields<MODE>(k, fv, lv);
-                fw[k] = e ? full[tr[k] >> 6] : ~0ull;
-            }
-#pragma unroll
-            for (int k = 0; k < kRegRow; ++k)
-                if (!((fw[k] >> (tr[k] & 63)) & 1ull)) em |= 1u << k;
-        }
-        int nmax = n;
-        for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
-        for (int p = 0; p < nmax; ++p) {   // wave-uniform
-            int32_t t = -1;
-            bool elig;
-            if (reg) {
-#pragma unroll
-                for (int k = 0; k < kRegRow; ++k)
-                    if (k == p) t = tr[k];
-                elig = (em >> p) & 1u;
-            } else {
-                t = p < n ? tgt_idx[b + p] : -1;
-                elig = t >= 0 && t != v && yields<MODE>(p, fv, lv) && !bit(full, t);
-            }
-            const u64 m = __ballot(elig);
-            if (m == 0ull) continue;   // wave-uniform
-            if (np + 64 > kPairBuf) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
-            n_pairs += elig;
-            if (elig) {
-                const int q = np + __popcll(m & lt);
-                sh.pt[q] = t;
-                sh.ps[q] = slot;
-            }
-            np += __popcll(m);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <int W, int MODE>
-__global__ void __launch_bounds__(256) hgx_opush_flat(const int32_t* __restrict__ list, const u64* __restrict__ n_list,
-                                                      int K, const int64_t* __restrict__ inc_off,
-                                                      const int32_t* __restrict__ inc_row,
-                                                      const int32_t* __restrict__ inc_type, int32_t want_type,
-                                                      const uint8_t* __restrict__ yf,
-                                                      const int64_t* __restrict__ tgt_off,
-                                                      const int32_t* __restrict__ tgt_idx, const u64* __restrict__ lvl,
-                                                      const u64* __restrict__ full, u64* __restrict__ cand,
-                                                      int32_t* __restrict__ clist, u64* __restrict__ n_clist,
-                                                      u64* __restrict__ acc, u64* __restrict__ ctr,
-                                                      u64* __restrict__ fa_next, int64_t n_words) {
-    constexpr int kUnroll = 4;
-    __shared__ FlatLds lds[4];
-    FlatLds& sh = lds[threadIdx.x >> 6];
-    const int lane = threadIdx.x & 63;
-    const u64 lt = (1ull << lane) - 1ull;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x)
-        fa_next[w] = 0ull;
-    const int64_t n = (int64_t)*n_list;
-    u64 n_links = 0, n_pins = 0, n_pairs = 0, n_scan = 0;
-    int cc = 0, np = 0;   // staged candidates / pairs (wave-uniform)
-    for (int64_t k0 = wave * K; k0 < n; k0 += nwave * K) {   // wave-uniform
-        const int64_t k = k0 + lane;
-        int32_t v = -1;
-        if (lane < K && k < n) v = list[k];
-        int64_t beg = 0;
-        int deg = 0;
-        if (v >= 0) {
-            beg = inc_off[v];
-            deg = (int)(inc_off[v + 1] - beg);
-        }
-        int incl = deg;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        const int E = __shfl(incl, 63);
-        if (E == 0) continue;   // wave-uniform
-        sh.v[lane] = v;
-        sh.beg[lane] = beg;
-        sh.pre[lane + 1] = incl;
-        if (lane == 0) sh.pre[0] = 0;
-        __builtin_amdgcn_wave_barrier();
-        for (int i0 = 0; i0 < K * W; i0 += 64) {   // the batch atoms' rows and their nonzero-word masks
-            const int i = i0 + lane, sl = i / W;
-            const int32_t sv = i < K * W ? sh.v[sl] : -1;
-            const u64 x = sv >= 0 ? lvl[(int64_t)sv * W + (i % W)] : 0ull;
-            if (i < K * W) sh.wval[i] = x;
-            const u64 nzb = __ballot(x != 0ull);
-            if (i < K * W && i % W == 0)
-                sh.wmask[sl] = (uint32_t)((nzb >> (lane - (lane % W))) & ((W >= 32) ? 0xffffffffull : ((1ull << W) - 1ull)));
-        }
-        __builtin_amdgcn_wave_barrier();
-        int ne = 0;   // staged passing entries (wave-uniform)
-        for (int e0 = 0; e0 < E; e0 += 64 * kUnroll) {   // wave-uniform
-            int jj[kUnroll];
-            int64_t ii[kUnroll];
-            bool pass[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int e = e0 + u * 64 + lane;
-                pass[u] = e < E;
-                int lo = 0, hi = 63;   // the batch slot j with pre[j] <= e < pre[j + 1]
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sh.pre[mid] <= e) lo = mid; else hi = mid - 1;
-                }
-                jj[u] = lo;
-                ii[u] = pass[u] ? sh.beg[lo] + (e - sh.pre[lo]) : 0;
-            }
-            if (want_type >= 0) {
-                int32_t ty[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) ty[u] = pass[u] ? inc_type[ii[u]] : want_type;
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ty[u] == want_type;
-            }
-            if constexpr (MODE != kSym) {
-                uint8_t f[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) f[u] = pass[u] ? yf[ii[u]] : (uint8_t)0;
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) pass[u] = pass[u] && ((f[u] >> MODE) & 1u);
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                n_scan += e0 + u * 64 + lane < E;
-                const u64 m = __ballot(pass[u]);
-                if (m == 0ull) continue;   // wave-uniform
-                if (ne + 64 > kEBuf) {
-                    flat_entries<W, MODE>(sh, ne, np, cc, inc_row, tgt_off, tgt_idx, lvl, full, acc, cand, clist,
-                                          n_clist, n_links, n_pins, n_pairs);
-                    ne = 0;
-                }
-                if (pass[u]) {
-                    const int q = ne + __popcll(m & lt);
-                    sh.ej[q] = jj[u];
-                    sh.ei[q] = ii[u];
-                }
-                ne += __popcll(m);
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        if (ne)
-            flat_entries<W, MODE>(sh, ne, np, cc, inc_row, tgt_off, tgt_idx, lvl, full, acc, cand, clist, n_clist,
-                                  n_links, n_pins, n_pairs);
-        // the pairs point into this batch's row table: drain them before the next batch replaces it
-        if (np) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (np) flat_pairs<W>(sh, np, cc, lvl, acc, cand, clist, n_clist);
-    flat_cand_flush(sh, cc, clist, n_clist);
-    wave_add_sh(ctr + cActiveLinks, n_links);
-    wave_add_sh(ctr + cActivePins, n_pins);
-    wave_add_sh(ctr + cIncLight, n_pairs);
-    wave_add_sh(ctr + cScanned, n_scan);
-}
+// (The flattened push of round 2, HGX_OPT_PUSH_BATCH K > 0 -- K frontier atoms a wave, their entries in
+// one stream -- was slower on the sum of config 5's directions at every K and was removed in round 5.)
 
 template <int W, int MODE>
 __global__ void __launch_bounds__(256) hgx_opush_heavy(const HeavyChunk* __restrict__ chunks,
@@ -3083,226 +2777,9 @@ __global__ void __launch_bounds__(256) hgx_x_apply(int64_t n, const u64* __restr
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Static-slot exchange of a dense level (HGX_OPT_PART_EXCHANGE).  When most ghosts have news, the
-// records' headers, the counting passes and the count round trips cost more than they save: every
-// ghost ships its whole row (zero without news) to a fixed slot of its owner's segment (xo_slot),
-// and the owner, which finds its holders' slots through its broadcast table (bc_slot, the same
-// ascending order on both sides), ORs them in, finishes the atom and writes the final row straight
-// into each holder's broadcast slot -- the reduce apply and the broadcast pack in one pass.  Three
-// launches a level (ghost pack, owner, ghost apply) instead of two three-pass packs and one apply
-// launch per source part and phase.
-// ---------------------------------------------------------------------------------------------
-constexpr int kXsU = 4;   // atoms per lane group in flight (each stage's loads issued together)
-
-// the part's segment starts (payload words) in LDS: one table lookup per record instead of a global
-// load on the dependent chain
-__device__ __forceinline__ void load_seg(int64_t* sw, const int64_t* __restrict__ seg_w, int NP) {
-    for (int q = threadIdx.x; q < NP; q += blockDim.x) sw[q] = seg_w[q];
-    __syncthreads();
-}
-
-template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_gpack(int64_t A, int NP, const u64* __restrict__ fa_next,
-                                                    const u64* __restrict__ own_bm, const int32_t* __restrict__ xo_part,
-                                                    const int32_t* __restrict__ xo_slot,
-                                                    const u64* __restrict__ lvl_next, const int64_t* __restrict__ seg_w,
-                                                    u64* __restrict__ pay) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    typedef Vec<WPL> V;
-    __shared__ int64_t sw[kMaxParts];
-    load_seg(sw, seg_w, NP);
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    for (int64_t t0 = grp; t0 < A; t0 += ngrp * kXsU) {
-        bool gh[kXsU], nw[kXsU];
-        int32_t q[kXsU], sl[kXsU];
-        typename V::T row[kXsU];
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {
-            const int64_t t = t0 + u * ngrp;
-            const bool in = t < A;
-            const u64 ow = in ? own_bm[t >> 6] : ~0ull, fw = in ? fa_next[t >> 6] : 0ull;
-            gh[u] = in && !((ow >> (t & 63)) & 1ull);
-            nw[u] = gh[u] && ((fw >> (t & 63)) & 1ull);
-            q[u] = gh[u] ? xo_part[t] : 0;
-            sl[u] = gh[u] ? xo_slot[t] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u)
-            row[u] = nw[u] ? V::ld(lvl_next + (t0 + u * ngrp) * W + sub * WPL) : V::zero();
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u)
-            if (gh[u]) V::st(pay + sw[q[u]] + (int64_t)sl[u] * W + sub * WPL, row[u]);
-    }
-}
-
-// Owner pass: reduce the holders' slots into an owned atom (new = row & ~vis), then write its final
-// news (zero when none) into every holder's broadcast slot.  kXsU atoms per group in flight, the
-// first two holders of each in registers (a present atom has 1.95 holders on config 4 at 8 parts).
-template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_owner(int64_t A, int NP, const u64* __restrict__ own_bm,
-                                                    const int64_t* __restrict__ bc_off, const int32_t* __restrict__ bc_part,
-                                                    const int32_t* __restrict__ bc_slot, const u64* __restrict__ recv,
-                                                    u64* __restrict__ send, const int64_t* __restrict__ seg_w,
-                                                    u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
-                                                    u64* __restrict__ vis, u64* __restrict__ ever, u64* __restrict__ full,
-                                                    FullMask fm) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    typedef Vec<WPL> V;
-    __shared__ int64_t sw[kMaxParts];
-    load_seg(sw, seg_w, NP);
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    const typename V::T FULL = full_part<W>(fm, sub);
-    // the trip count is the same for every lane of a wave (ballots below)
-    const int64_t gw = grp % (64 / G);
-    for (int64_t t0 = grp - gw; t0 < A; t0 += ngrp * kXsU) {
-        int64_t b[kXsU], d0[kXsU], d1[kXsU];
-        int nb[kXsU];
-        bool ev[kXsU], was[kXsU];
-        typename V::T acc[kXsU], vis0[kXsU], lv0[kXsU];
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {   // stage 1: ownership, holder range, bitmap words
-            const int64_t t = t0 + gw + u * ngrp;
-            const bool in = t < A;
-            const u64 ow = in ? own_bm[t >> 6] : 0ull;
-            const bool mine = in && ((ow >> (t & 63)) & 1ull);
-            b[u] = mine ? bc_off[t] : 0;
-            const int64_t e = mine ? bc_off[t + 1] : 0;
-            nb[u] = (int)(e - b[u]);
-            const u64 evw = mine ? ever[t >> 6] : 0ull, faw = mine ? fa_next[t >> 6] : 0ull;
-            ev[u] = nb[u] > 0 && ((evw >> (t & 63)) & 1ull);
-            was[u] = nb[u] > 0 && ((faw >> (t & 63)) & 1ull);
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {   // stage 2: the first two holders' slots, the atom's rows
-            const int64_t t = t0 + gw + u * ngrp;
-            d0[u] = nb[u] > 0 ? sw[bc_part[b[u]]] + (int64_t)bc_slot[b[u]] * W + sub * WPL : -1;
-            d1[u] = nb[u] > 1 ? sw[bc_part[b[u] + 1]] + (int64_t)bc_slot[b[u] + 1] * W + sub * WPL : -1;
-            vis0[u] = ev[u] ? V::ld(vis + t * W + sub * WPL) : V::zero();
-            lv0[u] = was[u] ? V::ld(lvl_next + t * W + sub * WPL) : V::zero();
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {   // stage 3: the holders' partial rows
-            acc[u] = d0[u] >= 0 ? V::ld(recv + d0[u]) : V::zero();
-            if (d1[u] >= 0) acc[u] |= V::ld(recv + d1[u]);
-            for (int k = 2; k < nb[u]; ++k)   // rare: a third holder and more
-                acc[u] |= V::ld(recv + sw[bc_part[b[u] + k]] + (int64_t)bc_slot[b[u] + k] * W + sub * WPL);
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {   // stage 4: finish the atom, write the broadcast slots
-            const int64_t t = t0 + gw + u * ngrp;
-            const typename V::T nw = acc[u] & ~vis0[u];
-            const bool any = group_any<G>(V::nz(nw));
-            const bool isfull = group_all<G>(V::eq(vis0[u] | nw, FULL));
-            typename V::T fin = lv0[u];
-            if (nb[u] > 0 && any) {
-                fin = lv0[u] | nw;
-                V::st(lvl_next + t * W + sub * WPL, fin);
-                V::st(vis + t * W + sub * WPL, vis0[u] | nw);
-                if (sub == 0) {
-                    if (!was[u]) set_bit(fa_next, t);
-                    if (!ev[u]) set_bit(ever, t);
-                    if (isfull) set_bit(full, t);
-                }
-            }
-            if (d0[u] >= 0) V::st(send + d0[u], fin);
-            if (d1[u] >= 0) V::st(send + d1[u], fin);
-            for (int k = 2; k < nb[u]; ++k)
-                V::st(send + sw[bc_part[b[u] + k]] + (int64_t)bc_slot[b[u] + k] * W + sub * WPL, fin);
-        }
-    }
-}
-
-// Ghost apply: the owner's final row (zero: no news) replaces the ghost's partial one.
-template <int W>
-__global__ void __launch_bounds__(256) hgx_xs_gapply(int64_t A, int NP, const u64* __restrict__ own_bm,
-                                                     const int32_t* __restrict__ xo_part,
-                                                     const int32_t* __restrict__ xo_slot, const u64* __restrict__ recv,
-                                                     const int64_t* __restrict__ seg_w, u64* __restrict__ lvl_next,
-                                                     u64* __restrict__ fa_next, u64* __restrict__ vis,
-                                                     u64* __restrict__ ever, u64* __restrict__ full, FullMask fm) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    typedef Vec<WPL> V;
-    __shared__ int64_t sw[kMaxParts];
-    load_seg(sw, seg_w, NP);
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    const typename V::T FULL = full_part<W>(fm, sub);
-    const int64_t gw = grp % (64 / G);
-    for (int64_t t0 = grp - gw; t0 < A; t0 += ngrp * kXsU) {
-        bool gh[kXsU], ev[kXsU], was[kXsU];
-        int64_t src[kXsU];
-        typename V::T row[kXsU], old[kXsU];
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {
-            const int64_t t = t0 + gw + u * ngrp;
-            const bool in = t < A;
-            const u64 ow = in ? own_bm[t >> 6] : ~0ull;
-            gh[u] = in && !((ow >> (t & 63)) & 1ull);
-            src[u] = gh[u] ? sw[xo_part[t]] + (int64_t)xo_slot[t] * W + sub * WPL : -1;
-            const u64 evw = gh[u] ? ever[t >> 6] : 0ull, faw = gh[u] ? fa_next[t >> 6] : 0ull;
-            ev[u] = gh[u] && ((evw >> (t & 63)) & 1ull);
-            was[u] = gh[u] && ((faw >> (t & 63)) & 1ull);
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {
-            const int64_t t = t0 + gw + u * ngrp;
-            row[u] = src[u] >= 0 ? V::ld(recv + src[u]) : V::zero();
-            old[u] = ev[u] ? V::ld(vis + t * W + sub * WPL) : V::zero();
-        }
-#pragma unroll
-        for (int u = 0; u < kXsU; ++u) {
-            const int64_t t = t0 + gw + u * ngrp;
-            const bool any = group_any<G>(V::nz(row[u]));
-            const bool isfull = group_all<G>(V::eq(old[u] | row[u], FULL));
-            if (gh[u] && any) {
-                V::st(lvl_next + t * W + sub * WPL, row[u]);
-                V::st(vis + t * W + sub * WPL, old[u] | row[u]);
-                if (sub == 0) {
-                    if (!was[u]) set_bit(fa_next, t);
-                    if (!ev[u]) set_bit(ever, t);
-                    if (isfull) set_bit(full, t);
-                }
-            }
-        }
-    }
-}
-
-// The exchange-mode decision of a level: out[3] += ghosts with news (fa_next & ~own), a thread per
-// bitmap word; on a 1/16 sample of the atoms (one G-lane group each) out[4] += nonzero row words of
-// the ghosts with news and out[5] += those ghosts -- the compressed records' density estimate.
-template <int W>
-__global__ void __launch_bounds__(256) hgx_ghost_news(int64_t A, const u64* __restrict__ fa,
-                                                      const u64* __restrict__ own, const u64* __restrict__ lvl,
-                                                      u64* __restrict__ out) {
-    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G;
-    typedef Vec<WPL> V;
-    const int64_t nwords = (A + 63) / 64;
-    u64 n = 0, nzw = 0, rows = 0;
-    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x)
-        n += __popcll(fa[w] & ~own[w]);
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t grp = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G;
-    const int64_t ngrp = ((int64_t)gridDim.x * blockDim.x) / G;
-    for (int64_t i = grp; i * 16 < A; i += ngrp) {
-        const int64_t t = i * 16 + (i & 15);
-        const bool take = t < A && bit(fa, t) && !bit(own, t);
-        if (take) {
-            const typename V::T r = V::ld(lvl + t * W + sub * WPL);
-            if constexpr (WPL == 1) nzw += r != 0ull;
-            else nzw += (u64)(r.x != 0ull) + (u64)(r.y != 0ull);
-            rows += sub == 0;
-        }
-    }
-    block_add_sh(out, 3, n);
-    block_add_sh(out, 4, nzw);
-    block_add_sh(out, 5, rows);
-}
+// (The static-slot exchange of round 2, HGX_OPT_PART_EXCHANGE 2 -- every ghost's whole row to a fixed slot
+// of its owner, three launches a level -- measured 42.8 against 34.0 ms a part a step and was removed in
+// round 5)
 
 // out[0] += |frontier & own| (the part's share of the group's new atoms), out[1] += sum of |inc(v)|
 // over the whole local frontier (the next level's local push volume).  A thread per bitmap word; the
@@ -3611,7 +3088,6 @@ struct Exchange {
     int64_t* seg = nullptr;             // [4 * NP] device: reduce h / p, broadcast h / p segment starts
     std::vector<int64_t> rseg, bseg;    // host copies (reduce, broadcast; records), NP + 1 entries
     double bytes_sent = 0, nz_words = 0, words = 0;
-    int static_levels = 0;              // levels exchanged through the static slots
     u64* hpin = nullptr;                // pinned landing area of the cursor / stats read-backs
     int64_t* dvec = nullptr;            // [2 * NP + 2] device count vector of the next all-gather
     int64_t* gpin = nullptr;            // [(2 * NP + 2) * NP] pinned landing area of the gathered vectors
@@ -3755,11 +3231,6 @@ struct Exchange {
         const size_t cbytes = sizeof(u64) * (NP * kCurStride + kStatShards * kStatStride);
         u64* xs = dctr + NP * kCurStride;   // sharded stats (see dctr)
         std::vector<u64> hc(NP * kCurStride + kStatShards * kStatStride), cnt(NP), wcnt(NP);
-        auto stat_sum = [&](int c) {
-            u64 t = 0;
-            for (int k = 0; k < kStatShards; ++k) t += hc[(size_t)NP * kCurStride + k * kStatStride + c];
-            return t;
-        };
         std::vector<int64_t> rcnt;
         auto apply = [&](bool reduce, const std::vector<int64_t>& rbase) {
             for (int q = 0; q < NP; ++q) {
@@ -3775,62 +3246,6 @@ struct Exchange {
             }
         };
         double pm_r = 0, pm_b = 0;
-        // exchange mode of the level (group-wide): static slots when at least half of the group's
-        // ghosts have news, compressed records otherwise (HGX_OPT_PART_EXCHANGE forces one)
-        bool stat_mode = sh.xmode == 2;
-        if (sh.xmode == 0) {   // bytes of each format: static = every ghost's row, records = the ghosts
-                               // with news (16-byte header + their nonzero words, from a 1/16 sample)
-            Events eg = tm.start(kKindExchange, d);
-            HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
-            hgx_ghost_news<Wt><<<grid_for(ceil_div(A, 16) * Lay<Wt>::G, 256, 2048), 256, 0, s>>>(
-                A, fa_next, (const u64*)sh.own_bm, lvl_next, xs);
-            HGX_CHECK_LAUNCH();
-            tm.stop(eg);
-            read_back(hc, cbytes);
-            int64_t mine2[4] = {(int64_t)stat_sum(3), rseg[NP], (int64_t)stat_sum(4), (int64_t)stat_sum(5)};
-            std::vector<int64_t> all2(4 * (size_t)NP);
-            ++trips;
-            coll([&] { tr->allgather_i64(mine2, 4, all2.data(), s); });
-            double news = 0, ghosts = 0, nzw = 0, rows = 0;
-            for (int q = 0; q < NP; ++q) {
-                news += (double)all2[4 * (size_t)q];
-                ghosts += (double)all2[4 * (size_t)q + 1];
-                nzw += (double)all2[4 * (size_t)q + 2];
-                rows += (double)all2[4 * (size_t)q + 3];
-            }
-            const double nzfrac = rows > 0 ? nzw / (rows * Wt) : 1.0;
-            const double rec_bytes = news * (16.0 + 8.0 * Wt * nzfrac), static_bytes = ghosts * 8.0 * Wt;
-            stat_mode = ghosts > 0 && static_bytes <= rec_bytes;
-        }
-        if (stat_mode) {
-            static_levels += 1;
-            // reduce: every ghost's row (zero without news) -> its slot at the owner
-            const int sgrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 4096);
-            Events e0 = tm.start(kKindExchange, d);
-            hgx_xs_gpack<Wt><<<sgrid, 256, 0, s>>>(A, NP, fa_next, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot,
-                                                   lvl_next, seg + NP, send_p);
-            HGX_CHECK_LAUNCH();
-            tm.stop(e0);
-            ship_static(rseg, sh.ghost_count, bseg, sh.bc_count, &pm_r);
-            // owners: reduce + finish + broadcast slots; then every ghost takes its final row
-            const int ogrid = grid_for(ceil_div(A, kXsU) * Lay<Wt>::G, 256, 4096);
-            Events e1 = tm.start(kKindExchange, d);
-            hgx_xs_owner<Wt><<<ogrid, 256, 0, s>>>(A, NP, (const u64*)sh.own_bm, sh.bc_off, sh.bc_part, sh.bc_slot,
-                                                   recv_p, send_p, seg + 3 * NP, lvl_next, fa_next, vis, ever, full, fm);
-            HGX_CHECK_LAUNCH();
-            tm.stop(e1);
-            ship_static(bseg, sh.bc_count, rseg, sh.ghost_count, &pm_b);
-            Events e2 = tm.start(kKindExchange, d);
-            hgx_xs_gapply<Wt><<<ogrid, 256, 0, s>>>(A, NP, (const u64*)sh.own_bm, sh.xo_part, sh.xo_slot, recv_p,
-                                                    seg + NP, lvl_next, fa_next, vis, ever, full, fm);
-            HGX_CHECK_LAUNCH();
-            HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
-            hgx_frontier_stats<<<grid_for(ceil_div(A, 64), 256, 2048), 256, 0, s>>>(
-                A, fa_next, (const u64*)sh.own_bm, g->inc_off, xs);
-            HGX_CHECK_LAUNCH();
-            tm.stop(e2);
-            return finish_level(push_volume, level_bytes, pair_max, before, pm_r + pm_b);
-        }
         // reduce: partial rows of my ghosts -> their owners
         Events e0 = tm.start(kKindExchange, d);
         HGX_HIP(hipMemsetAsync(dctr, 0, cbytes, s));
@@ -3960,25 +3375,6 @@ struct Exchange {
             tr->alltoallv(send_h, soff.data(), sbytes.data(), recv_h, roff.data(), rbytes.data(), g->stream);
             tr->alltoallv(send_p, psoff.data(), psbytes.data(), recv_p, proff.data(), prbytes.data(), g->stream);
         });
-    }
-    // One static-slot phase: scnt[q] full rows from my segment sbase[q] to q, rcnt[q] from q into
-    // rbase[q] (sizes known on both sides: no count exchange).
-    void ship_static(const std::vector<int64_t>& sbase, const std::vector<int64_t>& scnt,
-                     const std::vector<int64_t>& rbase, const std::vector<int64_t>& rcnt, double* pair_max) {
-        const int NP = g->shard->n_parts;
-        std::vector<int64_t> soff(NP), sbytes(NP), roff(NP), rbytes(NP);
-        *pair_max = 0;
-        for (int q = 0; q < NP; ++q) {
-            soff[q] = sbase[q] * W * 8;
-            sbytes[q] = scnt[q] * W * 8;
-            roff[q] = rbase[q] * W * 8;
-            rbytes[q] = rcnt[q] * W * 8;
-            bytes_sent += (double)sbytes[q];
-            words += (double)scnt[q] * W;
-            nz_words += (double)scnt[q] * W;   // static slots: every word counts as shipped
-            *pair_max = std::max(*pair_max, (double)sbytes[q]);
-        }
-        coll([&] { tr->alltoallv(send_p, soff.data(), sbytes.data(), recv_p, roff.data(), rbytes.data(), g->stream); });
     }
 };
 
@@ -4319,18 +3715,12 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             }();
             const int lgrid = kPushGrid;
             Events e2 = tm.start_chained(kKindPush, d);
-            const bool flat = g->push_batch > 0;
             // hub chunks inside hgx_opush while there are few of them (config 5: ~350 chunks, one launch
             // less per level); a block per chunk in hgx_opush_heavy when there are many (config 2:
             // ~380K chunks of 26K hubs: folded into 512 blocks the seed level took 0.58 ms against 0.41)
-            const bool fold = !flat && g->n_pchunks <= 8 * lgrid;
-            if (flat)   // flattened: K <= kFlatRows atoms per wave batch (HGX_OPT_PUSH_BATCH)
-                hgx_opush_flat<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, std::min(g->push_batch, kFlatRows), g->inc_off, g->inc_row,
-                                                              g->inc_type, want_type, yf, g->tgt_off, g->tgt_idx, lvl,
-                                                              full, cand, cl, n_cl, acc, c, fa_next,
-                                                              (int64_t)(bm_bytes / sizeof(u64)));
-            else   // hub chunks in the same launch
-                hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
+            const bool fold = g->n_pchunks <= 8 * lgrid;
+            // hub chunks in the same launch when folded
+            hgx_opush<W, MODE><<<lgrid, 256, 0, s>>>(fl, n_fl, g->inc_off, g->inc_row, g->inc_type, want_type, yf,
                                                          g->tgt_off, g->tgt_idx, lvl, full, cand, cl, n_cl, acc, c,
                                                          fa_next, (int64_t)(bm_bytes / sizeof(u64)), g->pchunks,
                                                          fold ? g->n_pchunks : 0, fa);

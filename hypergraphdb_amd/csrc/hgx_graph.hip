@@ -59,7 +59,7 @@ void graph_release(hgx_graph* g) {
     if (g->shard) {
         (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);
         (void)hipFree(g->shard->bc_off); (void)hipFree(g->shard->bc_part); (void)hipFree(g->shard->bc_lid);
-        (void)hipFree(g->shard->xo_slot); (void)hipFree(g->shard->bc_slot);
+        (void)hipFree(g->shard->bc_slot);
         (void)hipFree(g->shard->bc_atom);
         delete g->shard;
     }
@@ -314,7 +314,6 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     c->seq_engine = g->seq_engine;
     c->bfs_block = g->bfs_block;
     c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline;
-    c->push_batch = g->push_batch; c->q_flat = g->q_flat; c->q_fused = g->q_fused;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
     guard.c = nullptr;
     *out = c;
@@ -506,22 +505,25 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_PART_SERIAL applies to partition shards");
         g->shard->serial = value != 0;
     } else if (option == HGX_OPT_QUERY_FUSED) {
-        g->q_fused = value != 0;
+        // removed in round 5 (measured slower): only "off" is accepted
+        if (value != 0) fail(HGX_E_UNSUPPORTED, "hgx_set_option: HGX_OPT_QUERY_FUSED was removed (measured slower)");
     } else if (option == HGX_OPT_QUERY_INLINE) {
         g->q_inline = value != 0;
     } else if (option == HGX_OPT_PART_EXCHANGE) {
         if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_PART_EXCHANGE applies to partition shards");
-        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: exchange mode outside 0..2");
+        // 2 (static slots) was removed in round 5 (measured slower)
+        if (value == 2) fail(HGX_E_UNSUPPORTED, "hgx_set_option: the static-slot exchange (2) was removed");
+        if (value < 0 || value > 1) fail(HGX_E_INVALID, "hgx_set_option: exchange mode outside 0..1");
         g->shard->xmode = (int32_t)value;
     } else if (option == HGX_OPT_QUERY_FLAT) {
-        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: query flat mode outside 0..2");
-        g->q_flat = (int32_t)value;
+        // 0 and 1 were removed in round 5 (measured slower): only the single-pass path (2)
+        if (value != 2) fail(HGX_E_UNSUPPORTED, "hgx_set_option: only HGX_OPT_QUERY_FLAT 2 remains");
     } else if (option == HGX_OPT_CODED) {
         // removed in round 5 (measured slower): only "off" is accepted
         if (value != 0) fail(HGX_E_UNSUPPORTED, "hgx_set_option: HGX_OPT_CODED was removed (coded levels measured slower)");
     } else if (option == HGX_OPT_PUSH_BATCH) {
-        if (value < 0 || value > 64) fail(HGX_E_INVALID, "hgx_set_option: push batch outside 0..64");
-        g->push_batch = (int32_t)value;
+        // removed in round 5 (slower on the sum of config 5's directions): only 0
+        if (value != 0) fail(HGX_E_UNSUPPORTED, "hgx_set_option: HGX_OPT_PUSH_BATCH was removed (measured slower)");
     } else if (option == HGX_OPT_SEQ_BUDGET) {
         if (value < (1 << 20)) fail(HGX_E_INVALID, "hgx_set_option: sequence budget below 1 MiB");
         g->seq_budget_bytes = value;

@@ -144,10 +144,9 @@ struct ShardInfo {
     // Static exchange slots (dense levels): the j-th of my ghosts owned by q (ascending ids) sends to
     // slot j of q's receive segment from me, and q's j-th owned atom held by me (ascending ids: the
     // same atom) answers in slot j of my receive segment from q.
-    int32_t* xo_slot = nullptr;          // [A_local] ghost: its slot in the (me -> owner) segment
     int32_t* bc_slot = nullptr;          // [bc entries] its slot in the (me -> holder) segment
     int32_t* bc_atom = nullptr;          // [bc entries] the owned atom of the entry (flat broadcast pack)
-    int32_t xmode = 1;                   // HGX_OPT_PART_EXCHANGE: 1 compressed records (default), 2 static slots, 0 per level
+    int32_t xmode = 1;                   // HGX_OPT_PART_EXCHANGE: 0 / 1 compressed records (static slots removed in round 5)
     // the global -> local id of an atom present here, or -1 (binary search of l2g_host)
     int32_t local_of(int64_t v) const {
         auto it = std::lower_bound(l2g_host.begin(), l2g_host.end(), (int32_t)v);
@@ -310,12 +309,6 @@ struct hgx_graph {
     size_t zc_in_bytes = 0;
     int64_t q_cap_chunks = 0, q_cap_cand = 0;   // pattern workspace capacity (grown on demand)
     int64_t q_hits_guess = 0;                   // result ids copied back with the head of the result area
-    int32_t push_batch = 0;                     // HGX_OPT_PUSH_BATCH: frontier-push atoms per wave batch (0 = one atom per wave)
-    int32_t q_flat = 2;                         // HGX_OPT_QUERY_FLAT: 2 single-pass (front-scan + match with look-back),
-                                                //   1 flat match + separate scan / finish / scatter, 0 per-query chunks
-    bool q_fused = false;                       // HGX_OPT_QUERY_FUSED (A/B): small packed batches in the fused kernels
-    int64_t q_ovf_guess = 0;                    // fused pattern path: overflow area for queries with > 64 hits
-    int64_t q_chunk_guess = 0;                  // fused pattern path: chunk area of the chunked queries
     int32_t q_coalesce = 1;                     // HGX_OPT_QUERY_COALESCE: concurrent packed batches share device batches
     int64_t q_coalesce_max = 1 << 16;           //   at most this many queries per coalesced device batch
     hgx::QueryCombiner qcomb;

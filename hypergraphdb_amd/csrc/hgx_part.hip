@@ -723,14 +723,14 @@ int hgx_shard_graph_create(const hgx_shard* s, int32_t device, hgx_graph** out) 
     up(sh->bc_off, s->bc_off, 1);
     up(sh->bc_part, s->bc_part, 1);
     up(sh->bc_lid, s->bc_lid, 1);
-    {   // static exchange slots: rank of a ghost among my ghosts of its owner, of an owned atom among
-        // my owned atoms held by a holder (ascending local ids = ascending global ids on every part)
-        std::vector<int32_t> xo_slot(s->xo_part.size(), -1), bc_slot(s->bc_part.size(), -1),
+    {   // static broadcast slots: rank of an owned atom among my owned atoms held by a holder (ascending
+        // local ids = ascending global ids on every part); the ghost counts are checked with them
+        std::vector<int32_t> bc_slot(s->bc_part.size(), -1),
             bc_atom(s->bc_part.size(), -1);
         std::vector<int64_t> c1((size_t)s->n_parts, 0), c2((size_t)s->n_parts, 0);
         for (size_t i = 0; i < s->xo_part.size(); ++i) {
             const int32_t q = s->xo_part[i];
-            if (q >= 0) xo_slot[i] = (int32_t)c1[(size_t)q]++;
+            if (q >= 0) ++c1[(size_t)q];
             for (int64_t k = s->bc_off[i]; k < s->bc_off[i + 1]; ++k) {
                 bc_slot[(size_t)k] = (int32_t)c2[(size_t)s->bc_part[(size_t)k]]++;
                 bc_atom[(size_t)k] = (int32_t)i;
@@ -739,7 +739,6 @@ int hgx_shard_graph_create(const hgx_shard* s, int32_t device, hgx_graph** out) 
         for (int q = 0; q < s->n_parts; ++q)
             if (c1[(size_t)q] != s->ghost_count[(size_t)q] || c2[(size_t)q] != s->bc_count[(size_t)q])
                 fail(HGX_E_INVALID, "hgx_shard_graph_create: inconsistent exchange tables");
-        up(sh->xo_slot, xo_slot, 1);
         up(sh->bc_slot, bc_slot, 1);
         up(sh->bc_atom, bc_atom, 1);
     }

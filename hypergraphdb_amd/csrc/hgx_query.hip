@@ -32,9 +32,6 @@ namespace hgx {
 
 typedef unsigned long long u64;
 
-constexpr int kQChunk = 256;        // candidates per wave-chunk (4 per lane): with 1024 the 41 config-3
-                                    // queries above 1024 candidates kept the match at ~30 us of
-                                    // dependent loads per chunk
 constexpr int kMaxAnchors = 32;
 constexpr int kMaxPattern = 64;     // targets of one OrderedLinkCondition
 constexpr int kMaxPatterns = 16;    // OrderedLinkConditions in one And
@@ -278,29 +275,6 @@ __device__ __forceinline__ QPlan plan_query(const QDesc& d, bool nop, const int3
     return p;
 }
 
-__global__ void __launch_bounds__(256) hgx_q_plan(int32_t n, const QDesc* __restrict__ desc,
-                                                  const int32_t* __restrict__ anchors, const int32_t* __restrict__ types,
-                                                  const int32_t* __restrict__ nop, const int64_t* __restrict__ inc_off,
-                                                  const int32_t* __restrict__ ts_type, QPlan* __restrict__ plan,
-                                                  int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    const QDesc d = desc[q];
-    QPlan p;
-    if (d.a_end - d.a_beg <= kRegAnchors && !nop[q]) {
-        int32_t av[kRegAnchors];
-        const int na = (int)(d.a_end - d.a_beg);
-#pragma unroll
-        for (int k = 0; k < kRegAnchors; ++k) av[k] = k < na ? anchors[d.a_beg + k] : 0;
-        p = plan_regs(av, na, (d.t_end - d.t_beg == 1) ? types[d.t_beg] : -1, inc_off, ts_type);
-    } else {
-        p = plan_query(d, nop[q] != 0, anchors, types, inc_off, ts_type);
-    }
-    plan[q] = p;
-    nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
-    ncand[q] = p.n;
-}
-
 // Packed batch (hgx_pattern_batch_packed) normalised on the device, one thread per query:
 // ExpressionBasedQuery.expand adds incident(x) for every non-ANY target of the orderedLink (:730-737),
 // the toDNF HashSet drops duplicate anchors (:100).  The anchors of query q go to the fixed slot
@@ -367,44 +341,6 @@ __device__ __forceinline__ QPlan norm_query(
     return p;
 }
 
-__global__ void __launch_bounds__(256) hgx_q_norm_packed(
-    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
-    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
-    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ ts_type,
-    QDesc* __restrict__ desc, int32_t* __restrict__ anchors, int32_t* __restrict__ nop, QPlan* __restrict__ plan,
-    int32_t* __restrict__ nchunks, int64_t* __restrict__ ncand, int32_t* __restrict__ err) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    int st = 0;
-    const QPlan p = norm_query(q, A, type, inc_off, inc, has_ordered, pat_off, pat, g_inc_off, ts_type, desc, anchors,
-                               nop, st);
-    if (st) atomicMin(&err[st - 1], q);
-    plan[q] = p;
-    nchunks[q] = (int32_t)((p.n + kQChunk - 1) / kQChunk);
-    ncand[q] = p.n;
-}
-
-// Small batches (n <= kSmallBatch): one workgroup scans the chunk counts and candidate counts, writes
-// the chunk -> query map and checks both totals against the workspace capacity.  stat[0] = total
-// chunks, stat[1] = total candidates, stat[2] = 1 on overflow (the match then sees no chunks).
-constexpr int kSmallBatch = 16384;   // <= 16 queries per thread of the scan block
-constexpr int kScanBlock = 1024;
-
-// Sum of a[b, e) with the loads of each 16-element step issued together (a plain loop waits on
-// every load before the next add).
-template <typename T>
-__device__ __forceinline__ T seg_sum(const T* __restrict__ a, int64_t b, int64_t e) {
-    T s = 0;
-    for (int64_t x = b; x < e; x += 16) {
-        T v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = x + j < e ? a[x + j] : (T)0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) s += v[j];
-    }
-    return s;
-}
-
 template <typename T>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* wsum, T& total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -425,281 +361,9 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* wsum, T& total) {
     return before + incl - v;
 }
 
-__global__ void __launch_bounds__(kScanBlock) hgx_q_scan_small(int32_t n, const int32_t* __restrict__ nch,
-                                                                const int64_t* __restrict__ ncand,
-                                                                int32_t* __restrict__ choff, int64_t* __restrict__ coff,
-                                                                int32_t* __restrict__ chq, int64_t cap_chunks,
-                                                                int64_t cap_cand, int64_t* __restrict__ stat,
-                                                                u64* __restrict__ ctr) {
-    __shared__ int32_t ws32[kScanBlock / 64];
-    __shared__ int64_t ws64[kScanBlock / 64];
-    if (threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;   // the match's counter shards
-    // thread t owns the contiguous queries [t*per, (t+1)*per): its loads are independent and in flight
-    // together, then one block scan of the per-thread sums
-    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kSmallBatch)
-    const int32_t q0 = threadIdx.x * per;
-    int32_t cv[16];
-    int64_t kv[16];
-    int32_t sc = 0;
-    int64_t sk = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {   // every load issued before any is used
-        const bool in = j < per && q0 + j < n;
-        cv[j] = in ? nch[q0 + j] : 0;
-        kv[j] = in ? ncand[q0 + j] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        sc += cv[j];
-        sk += kv[j];
-    }
-    int32_t tc;
-    int64_t tk;
-    int32_t ec = block_exclusive_scan<int32_t>(sc, ws32, tc);
-    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
-    const bool over = tc > cap_chunks || tk > cap_cand;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        if (j < per && q0 + j < n) {
-            const int32_t q = q0 + j;
-            choff[q] = ec;
-            coff[q] = ek;
-            if (!over)
-                for (int32_t i = 0; i < cv[j]; ++i) chq[ec + i] = q;
-        }
-        ec += cv[j];
-        ek += kv[j];
-    }
-    if (threadIdx.x == 0) {
-        choff[n] = over ? 0 : tc;   // the match reads its chunk count here
-        coff[n] = tk;
-        stat[0] = tc;
-        stat[1] = tk;
-        stat[2] = over ? 1 : 0;
-    }
-}
-
-// Large batches: totals after the device scans, overflow check, chunk count for the match.
-__global__ void hgx_q_check(int32_t n, int32_t* __restrict__ choff, const int64_t* __restrict__ coff,
-                            int64_t cap_chunks, int64_t cap_cand, int64_t* __restrict__ stat) {
-    const int64_t c = choff[n], k = coff[n];
-    stat[0] = c;
-    stat[1] = k;
-    stat[2] = (c > cap_chunks || k > cap_cand) ? 1 : 0;
-    if (stat[2]) choff[n] = 0;
-}
-
-__global__ void hgx_q_chunk_map(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ stat,
-                                int32_t* __restrict__ chunk_q) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n || stat[2]) return;   // nothing is matched after a workspace overflow
-    for (int32_t c = chunk_off[q]; c < chunk_off[q + 1]; ++c) chunk_q[c] = q;
-}
-
-// A wave per chunk of kQChunk candidates of one query (grid-stride over chunks; the counters are
-// summed in registers and added once per wave into sharded replicas).
-//   stage 1: every lane streams kPerLane consecutive entries of the type column (16-byte loads) and
-//            keeps a bit per type-passing candidate;
-//   stage 2: the passing candidates go to an LDS list in ascending order (wave prefix sum);
-//   stage 3: the list is processed 64 at a time, one candidate per lane: link row, target offsets,
-//            target row, anchor / positioned / ordered / arity checks; hits are compacted in order.
-// The type filter passes ~1/T of the candidates, so stage 3 runs on full waves instead of lanes
-// idling behind failed type checks.  Hits of a chunk land in its own candidate range of slots.
-constexpr int kPerLane = kQChunk / 64;
-
-__global__ void __launch_bounds__(256) hgx_pattern_match(
-    const int32_t* __restrict__ n_chunks_p, const int32_t* __restrict__ chunk_q, const int32_t* __restrict__ chunk_off,
-    const int64_t* __restrict__ cand_off, const QPlan* __restrict__ plan, const QDesc* __restrict__ desc,
-    const int32_t* __restrict__ anchors, const int32_t* __restrict__ types, const int32_t* __restrict__ pos,
-    const int64_t* __restrict__ p_off, const int32_t* __restrict__ pattern, const int32_t* __restrict__ inc_row,
-    const int32_t* __restrict__ inc_type, const int32_t* __restrict__ inc_ts_row, const int64_t* __restrict__ tgt_off,
-    const int32_t* __restrict__ tgt_idx, const int4* __restrict__ ts_tgt, int32_t* __restrict__ slots,
-    int64_t* __restrict__ counts, u64* __restrict__ ctr) {
-    __shared__ int32_t lds[4][kQChunk];
-    __shared__ int32_t lds_anch[4][kMaxAnchors];
-    const int32_t n_chunks = *n_chunks_p;
-    int32_t* list = lds[threadIdx.x >> 6];
-    int32_t* anch = lds_anch[threadIdx.x >> 6];
-    const int lane = threadIdx.x & 63;
-    // wave-uniform in scalar registers: the chunk, its query, plan and descriptor come through scalar
-    // loads and leave the VGPRs to the candidate pipeline (135 -> fewer VGPRs, more waves per SIMD)
-    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const u64 lt = (1ull << lane) - 1ull;
-    uint32_t n_cand = 0, n_typed = 0;   // <= 16 per lane and chunk: no overflow at <= 2^28 chunks a wave
-    uint32_t n_inl = 0;                 // candidates served by an inline target record
-    u64 n_ar = 0, n_hits = 0;
-    for (int64_t chunk = wave; chunk < n_chunks; chunk += nwave) {
-        const int32_t q = __builtin_amdgcn_readfirstlane(chunk_q[chunk]);
-        const QPlan pl = plan[q];
-        const QDesc d = desc[q];
-        const int64_t c0 = (int64_t)(chunk - chunk_off[q]) * kQChunk;
-        const int64_t nc = pl.n - c0 < kQChunk ? pl.n - c0 : kQChunk;   // candidates of this chunk
-        const bool typed = d.t_end > d.t_beg && !pl.pad;   // a type-grouped range is all of type T
-        const int32_t* rows = pl.pad ? inc_ts_row : inc_row;
-        const int4* inl = pl.pad ? ts_tgt : nullptr;   // wave-uniform: inline records of a type-grouped range
-        // stage 1: lane l owns candidates [l*kPerLane, (l+1)*kPerLane) of the chunk
-        unsigned passm = 0;
-        const int64_t cb = c0 + lane * kPerLane;
-        if (!typed) {
-            for (int k = 0; k < kPerLane; ++k) passm |= (unsigned)(lane * kPerLane + k < nc) << k;
-        } else {
-            const int32_t* col = inc_type + pl.beg + cb;
-            if (lane * kPerLane + kPerLane <= nc && ((pl.beg + cb) & 3) == 0) {
-                int32_t t[kPerLane];
-#pragma unroll
-                for (int k = 0; k < kPerLane; k += 4) {
-                    const int4 v = *reinterpret_cast<const int4*>(col + k);
-                    t[k] = v.x; t[k + 1] = v.y; t[k + 2] = v.z; t[k + 3] = v.w;
-                }
-#pragma unroll
-                for (int k = 0; k < kPerLane; ++k) passm |= (unsigned)type_in(t[k], types, d.t_beg, d.t_end) << k;
-            } else {
-                for (int k = 0; k < kPerLane; ++k)
-                    if (lane * kPerLane + k < nc) passm |= (unsigned)type_in(col[k], types, d.t_beg, d.t_end) << k;
-            }
-        }
-        if (typed)   // streamed type column entries (a type-grouped range streams none)
-            n_cand += (uint32_t)(lane * kPerLane < nc ? (nc - lane * kPerLane < kPerLane ? nc - lane * kPerLane : kPerLane)
-                                                 : 0);
-        // stage 2: ascending list of passing candidate indices (relative to the chunk)
-        const int cnt = __popc(passm);
-        int pre = cnt;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(pre, off);
-            if (lane >= off) pre += y;
-        }
-        const int total = __shfl(pre, 63);
-        pre -= cnt;
-        for (unsigned m = passm; m; m &= m - 1u) list[pre++] = lane * kPerLane + __ffs(m) - 1;
-        __builtin_amdgcn_wave_barrier();
-        // stage 3: the query's anchors go to LDS and a single short pattern to registers (wave-uniform
-        // values); a candidate's target row of <= 8 entries is loaded once into registers and every
-        // check runs on them -- three dependent loads per candidate (link row, offsets, targets)
-        const int na = (int)(d.a_end - d.a_beg);
-        if (lane < na && lane < kMaxAnchors) anch[lane] = anchors[d.a_beg + lane];
-        const bool one_pat = d.r_end - d.r_beg == 1;
-        const int64_t pb0 = one_pat ? p_off[d.r_beg] : 0;
-        const int np0 = one_pat ? (int)(p_off[d.r_beg + 1] - pb0) : 0;
-        const bool reg_pat = one_pat && np0 <= 8;
-        int32_t pv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pv[k] = (reg_pat && k < np0) ? pattern[pb0 + k] : 0;
-        __builtin_amdgcn_wave_barrier();
-        int32_t written = 0;
-        int32_t* out = slots + cand_off[q] + c0;
-        for (int base = 0; base < total; base += 64) {   // wave-uniform
-            const int idx = base + lane;
-            bool hit = idx < total;
-            int32_t L = -1;
-            if (hit) {
-                const int64_t ci = pl.beg + c0 + list[idx];
-                L = rows[ci];
-                ++n_typed;
-                int32_t tr[8];
-                int n;
-                const int32_t* row = nullptr;   // the target row in memory (links not served inline)
-                bool have = false;
-                if (inl) {   // one streamed 32-byte record: the link's targets inline (issued with L)
-                    const int4 r0 = inl[2 * ci], r1 = inl[2 * ci + 1];
-                    tr[0] = r0.x; tr[1] = r0.y; tr[2] = r0.z; tr[3] = r0.w;
-                    tr[4] = r1.x; tr[5] = r1.y; tr[6] = r1.z; tr[7] = r1.w;
-                    have = tr[0] != -2;
-                }
-                if (have) {
-                    n = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) n += tr[i] >= 0;
-                    ++n_inl;
-                } else {
-                    const int64_t b = tgt_off[L];
-                    n = (int)(tgt_off[L + 1] - b);
-                    row = tgt_idx + b;
-                    n_ar += (u64)n;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
-                }
-                // ArityCondition: layout.length == arity + 2
-                if (d.arity >= 0) hit = n == d.arity;
-                if (n <= 8) {
-                    // IncidentCondition for every other anchor (L in inc(a) <=> a in targets(L))
-                    for (int j = 0; j < na && hit; ++j) {
-                        if (j == pl.amin) continue;
-                        const int32_t a = anch[j];
-                        bool found = false;
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) found |= (i < n) && tr[i] == a;
-                        hit = found;
-                    }
-                    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
-                        hit = positioned_regs(tr, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
-                    if (hit && reg_pat) {   // OrderedLinkCondition.satisfies on registers
-                        int j = 0;
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            int32_t pj = pv[0];
-#pragma unroll
-                            for (int k = 1; k < 8; ++k)
-                                if (j == k) pj = pv[k];
-                            if (i < n && j < np0 && (pj < 0 || pj == tr[i])) ++j;
-                        }
-                        hit = j == np0;
-                    } else {
-                        for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {   // greedy subsequence on registers
-                            const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
-                            int64_t j = 0;
-#pragma unroll
-                            for (int i = 0; i < 8; ++i)
-                                if (i < n && j < np) {
-                                    const int32_t pj = pattern[pb + j];
-                                    if (pj < 0 || pj == tr[i]) ++j;
-                                }
-                            hit = (j == np);
-                        }
-                    }
-                } else {
-                    for (int64_t j = d.a_beg; j < d.a_end && hit; ++j) {
-                        if (j - d.a_beg == pl.amin) continue;
-                        const int32_t a = anchors[j];
-                        bool found = false;
-                        for (int i = 0; i < n; ++i) found |= (row[i] == a);
-                        hit = found;
-                    }
-                    // PositionedIncidentCondition (its ORA set: inc(target) filtered by the predicate)
-                    for (int64_t s = d.s_beg; s < d.s_end && hit; ++s)
-                        hit = positioned(row, n, pos[4 * s], pos[4 * s + 1], pos[4 * s + 2], pos[4 * s + 3] != 0);
-                    // OrderedLinkCondition.satisfies: greedy subsequence with hg.anyHandle()
-                    for (int64_t r = d.r_beg; r < d.r_end && hit; ++r) {
-                        const int64_t pb = p_off[r], np = p_off[r + 1] - pb;
-                        int i = 0;
-                        int64_t j = 0;
-                        while (i < n && j < np) {
-                            const int32_t pj = pattern[pb + j];
-                            if (pj < 0 || pj == row[i]) ++j;
-                            ++i;
-                        }
-                        hit = (j == np);
-                    }
-                }
-            }
-            const u64 m = __ballot(hit);
-            if (hit) out[written + __popcll(m & lt)] = L;
-            written += __popcll(m);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) counts[chunk] = written;
-        n_hits += (u64)written;
-    }
-    u64* c = ctr + (wave & (kQShards - 1)) * kQStride;
-    wave_add_q(c + qCand, (u64)n_cand);
-    wave_add_q(c + qTyped, (u64)n_typed);
-    wave_add_q(c + qArity, n_ar);
-    wave_add_q(c + qInline, (u64)n_inl);
-    if (lane == 0 && n_hits) atomicAdd(c + qHits, n_hits);
-}
 
 // ---------------------------------------------------------------------------------------------
-// Flat match (default; HGX_OPT_QUERY_FLAT = 0 keeps the per-query chunks above).  The candidates of
+// Flat match (the only match since round 5; the per-query-chunk match of rounds 1-2 is gone).  The candidates of
 // the batch form one flat space (query q owns [coff[q], coff[q+1])) cut into chunks of 64: a wave
 // takes a chunk and each lane one candidate, whatever query it belongs to.  Half of the config-3
 // queries have one candidate: with a wave per query chunk the batch was ~11K waves each running a
@@ -764,63 +428,6 @@ __device__ __forceinline__ int64_t didx_last(const DIdx& ix, int64_t x, bool str
 #pragma unroll
     for (int i = 0; i < 4; ++i) c += __popcll(__ballot(strict ? v[i] < t : v[i] <= t));
     return base + c - 1;   // lpre is non-decreasing inside the block and lpre[base] = 0 qualifies
-}
-
-__global__ void __launch_bounds__(kScanBlock) hgx_q_scan_flat(int32_t n, const int64_t* __restrict__ ncand,
-                                                               int64_t* __restrict__ coff, int32_t* __restrict__ chq,
-                                                               int32_t* __restrict__ n_chunks_out, int64_t cap_chunks,
-                                                               int64_t cap_cand, int64_t* __restrict__ stat,
-                                                               u64* __restrict__ ctr) {
-    __shared__ int64_t ws64[kScanBlock / 64];
-    if (threadIdx.x < kQShards * kQStride) ctr[threadIdx.x] = 0ull;
-    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kSmallBatch)
-    const int32_t q0 = threadIdx.x * per;
-    int64_t kv[16];
-    int64_t sk = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) kv[j] = (j < per && q0 + j < n) ? ncand[q0 + j] : 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sk += kv[j];
-    int64_t tk;
-    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
-    const int64_t tc = (tk + kFlatChunk - 1) / kFlatChunk;
-    const bool over = tc > cap_chunks || tk > cap_cand;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        if (j < per && q0 + j < n) {
-            const int32_t q = q0 + j;
-            coff[q] = ek;
-            if (!over)   // the chunks whose first candidate is one of q's
-                for (int64_t c = (ek + kFlatChunk - 1) / kFlatChunk; c * kFlatChunk < ek + kv[j]; ++c) chq[c] = q;
-        }
-        ek += kv[j];
-    }
-    if (threadIdx.x == 0) {
-        coff[n] = tk;
-        *n_chunks_out = over ? 0 : (int32_t)tc;
-        stat[0] = tc;
-        stat[1] = tk;
-        stat[2] = over ? 1 : 0;
-    }
-}
-
-// Large batches: coff from a device scan; the chunk count / overflow check, then a thread per query
-// writes the chunk -> first query map.
-__global__ void hgx_q_check_flat(int32_t n, const int64_t* __restrict__ coff, int32_t* __restrict__ n_chunks_out,
-                                 int64_t cap_chunks, int64_t cap_cand, int64_t* __restrict__ stat) {
-    const int64_t k = coff[n], c = (k + kFlatChunk - 1) / kFlatChunk;
-    stat[0] = c;
-    stat[1] = k;
-    stat[2] = (c > cap_chunks || k > cap_cand) ? 1 : 0;
-    *n_chunks_out = stat[2] ? 0 : (int32_t)c;
-}
-
-__global__ void hgx_q_chunk_map_flat(int32_t n, const int64_t* __restrict__ coff, const int64_t* __restrict__ stat,
-                                     int32_t* __restrict__ chq) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n || stat[2]) return;
-    const int64_t b = coff[q], e = coff[q + 1];
-    for (int64_t c = (b + kFlatChunk - 1) / kFlatChunk; c * kFlatChunk < e; ++c) chq[c] = q;
 }
 
 // One candidate against its query's conditions (the target row in registers, n <= 8).
@@ -997,120 +604,6 @@ __global__ void __launch_bounds__(256) hgx_pattern_match_flat(
     wave_add_q(c + qArity, n_ar);
     wave_add_q(c + qInline, n_inl);
     wave_add_q(c + qHits, n_hits);
-}
-
-// Small flat batches: one workgroup scans the chunk hit counts, writes every query's offset from the
-// hit masks and sums the counter shards; hgx_q_scatter_flat then copies the hits, a wave per chunk.
-__global__ void __launch_bounds__(kScanBlock) hgx_q_finish_flat(
-    int32_t n, const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ coff,
-    const int64_t* __restrict__ counts, const u64* __restrict__ hitmask, const u64* __restrict__ ctr,
-    int64_t* __restrict__ outoff, int64_t* __restrict__ q_off, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
-    const int32_t* __restrict__ err) {
-    __shared__ int64_t ws[kScanBlock / 64];
-    if (stat[2]) {   // workspace overflow: nothing was matched, the host re-runs
-        if (threadIdx.x == 0) {
-            stat[3] = 0;
-            stat[4] = err ? err[0] : INT32_MAX;
-            stat[5] = err ? err[1] : INT32_MAX;
-        }
-        return;
-    }
-    const int32_t nc = *n_chunks_p;
-    const int32_t per = (nc + kScanBlock - 1) / kScanBlock;
-    const int32_t c0 = threadIdx.x * per, c1 = min(nc, c0 + per);
-    int64_t tot, e;
-    if (per <= 16) {
-        int64_t kv[16];
-        int64_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) kv[j] = c0 + j < c1 ? counts[c0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum += kv[j];
-        e = block_exclusive_scan<int64_t>(sum, ws, tot);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (c0 + j < c1) outoff[c0 + j] = e;
-            e += kv[j];
-        }
-    } else {
-        const int64_t sum = seg_sum<int64_t>(counts, c0, c1);
-        e = block_exclusive_scan<int64_t>(sum, ws, tot);
-        for (int32_t c = c0; c < c1; ++c) {
-            outoff[c] = e;
-            e += counts[c];
-        }
-    }
-    if (threadIdx.x == 0) {
-        outoff[nc] = tot;
-        stat[3] = tot;
-        stat[4] = err ? err[0] : INT32_MAX;
-        stat[5] = err ? err[1] : INT32_MAX;
-    }
-    __syncthreads();
-    {   // n <= kSmallBatch: <= 17 queries per thread, the load rounds issued together
-        constexpr int R = kSmallBatch / kScanBlock + 1;
-        int64_t cf[R], ov[R];
-        u64 hm[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int32_t q = threadIdx.x + j * kScanBlock;
-            cf[j] = q <= n ? coff[q] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int64_t k = cf[j] / kFlatChunk;
-            ov[j] = outoff[k];
-            hm[j] = k < nc ? hitmask[k] : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int32_t q = threadIdx.x + j * kScanBlock;
-            const int b = (int)(cf[j] % kFlatChunk);
-            if (q <= n) q_off[q] = ov[j] + __popcll(hm[j] & ((1ull << b) - 1ull));
-        }
-    }
-    if (threadIdx.x < qNum) {
-        u64 v = 0;
-        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
-        ctr_out[threadIdx.x] = v;
-    }
-}
-
-// Large flat batches: every query's offset from the scanned chunk counts and the hit masks.
-__global__ void hgx_q_offsets_flat(int32_t n, const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ coff,
-                                   const int64_t* __restrict__ outoff, const u64* __restrict__ hitmask,
-                                   const int64_t* __restrict__ stat, int64_t* __restrict__ q_off) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q > n || stat[2]) return;
-    const int64_t cf = coff[q], k = cf / kFlatChunk;
-    const u64 hm = k < *n_chunks_p ? hitmask[k] : 0ull;
-    q_off[q] = outoff[k] + __popcll(hm & ((1ull << (cf % kFlatChunk)) - 1ull));
-}
-
-__global__ void __launch_bounds__(256) hgx_q_scatter_flat(const int32_t* __restrict__ n_chunks_p,
-                                                          const int64_t* __restrict__ counts,
-                                                          const int64_t* __restrict__ out_off,
-                                                          const int32_t* __restrict__ slots,
-                                                          const int32_t* __restrict__ link_atom, int32_t* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    if (k >= *n_chunks_p) return;
-    if (lane < counts[k]) out[out_off[k] + lane] = link_atom[slots[k * kFlatChunk + lane]];
-}
-
-__global__ void hgx_q_finish_stat_flat(const int32_t* __restrict__ n_chunks_p, const int64_t* __restrict__ outoff,
-                                       const u64* __restrict__ ctr, int64_t* __restrict__ stat,
-                                       u64* __restrict__ ctr_out, const int32_t* __restrict__ err) {
-    if (threadIdx.x == 0) {
-        stat[3] = stat[2] ? 0 : outoff[*n_chunks_p];
-        stat[4] = err ? err[0] : INT32_MAX;
-        stat[5] = err ? err[1] : INT32_MAX;
-    }
-    if (threadIdx.x < qNum) {
-        u64 v = 0;
-        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
-        ctr_out[threadIdx.x] = v;
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1505,229 +998,7 @@ __global__ void __launch_bounds__(256) hgx_q_place(const int32_t* __restrict__ n
     }
 }
 
-// Copy each chunk's hits to its output position, mapping link rows to atom ids.
-__global__ void __launch_bounds__(256) hgx_q_scatter(const int32_t* __restrict__ n_chunks_p,
-                                                     const int32_t* __restrict__ chunk_q,
-                                                     const int32_t* __restrict__ chunk_off,
-                                                     const int64_t* __restrict__ cand_off,
-                                                     const int64_t* __restrict__ counts,
-                                                     const int64_t* __restrict__ out_off,
-                                                     const int32_t* __restrict__ slots,
-                                                     const int32_t* __restrict__ link_atom, int32_t* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t chunk = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    if (chunk >= *n_chunks_p) return;
-    const int64_t c = counts[chunk];
-    const int64_t o = out_off[chunk];
-    const int32_t q = chunk_q[chunk];
-    const int32_t* src = slots + cand_off[q] + (int64_t)(chunk - chunk_off[q]) * kQChunk;
-    for (int64_t i = lane; i < c; i += 64) out[o + i] = link_atom[src[i]];
-}
 
-__global__ void hgx_q_offsets(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ out_off,
-                              const int64_t* __restrict__ stat, int64_t* __restrict__ q_off) {
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q <= n && !stat[2]) q_off[q] = out_off[chunk_off[q]];
-}
-
-// Small batches: one workgroup scans the per-chunk hit counts, writes the per-query offsets and sums
-// the counter shards (stat[3] = total hits); hgx_q_scatter then copies the hits, a wave per chunk
-// (a chunk loop inside one workgroup serialised ~5 dependent loads per chunk: 0.77 ms at 10K queries).
-__global__ void __launch_bounds__(kScanBlock) hgx_q_finish_small(
-    int32_t n, const int32_t* __restrict__ chunk_off, const int32_t* __restrict__ chunk_q,
-    const int64_t* __restrict__ cand_off, const int64_t* __restrict__ counts, const int32_t* __restrict__ slots,
-    const int32_t* __restrict__ link_atom, const u64* __restrict__ ctr, int64_t* __restrict__ outoff,
-    int64_t* __restrict__ q_off, int32_t* __restrict__ out, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
-    const int32_t* __restrict__ err) {
-    __shared__ int64_t ws[kScanBlock / 64];
-    if (stat[2]) {   // workspace overflow: nothing was matched, the host re-runs
-        if (threadIdx.x == 0) {
-            stat[3] = 0;
-            stat[4] = err ? err[0] : INT32_MAX;
-            stat[5] = err ? err[1] : INT32_MAX;
-        }
-        return;
-    }
-    const int32_t nc = chunk_off[n];
-    const int32_t per = (nc + kScanBlock - 1) / kScanBlock;
-    const int32_t c0 = threadIdx.x * per, c1 = min(nc, c0 + per);
-    int64_t tot, e;
-    if (per <= 16) {   // counts in registers: one round of loads
-        int64_t kv[16];
-        int64_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) kv[j] = c0 + j < c1 ? counts[c0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum += kv[j];
-        e = block_exclusive_scan<int64_t>(sum, ws, tot);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (c0 + j < c1) outoff[c0 + j] = e;
-            e += kv[j];
-        }
-    } else {
-        const int64_t sum = seg_sum<int64_t>(counts, c0, c1);
-        e = block_exclusive_scan<int64_t>(sum, ws, tot);
-        for (int32_t c = c0; c < c1; ++c) {
-            outoff[c] = e;
-            e += counts[c];
-        }
-    }
-    if (threadIdx.x == 0) {
-        outoff[nc] = tot;
-        stat[3] = tot;
-        stat[4] = err ? err[0] : INT32_MAX;
-        stat[5] = err ? err[1] : INT32_MAX;
-    }
-    __syncthreads();
-    {   // n <= kSmallBatch: <= 17 offsets per thread, both load rounds issued together
-        constexpr int R = kSmallBatch / kScanBlock + 1;
-        int32_t co[R];
-        int64_t ov[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int32_t q = threadIdx.x + j * kScanBlock;
-            co[j] = q <= n ? chunk_off[q] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < R; ++j) ov[j] = outoff[co[j]];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const int32_t q = threadIdx.x + j * kScanBlock;
-            if (q <= n) q_off[q] = ov[j];
-        }
-    }
-    if (threadIdx.x < qNum) {
-        u64 v = 0;
-        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
-        ctr_out[threadIdx.x] = v;
-    }
-}
-
-__global__ void hgx_q_finish_stat(int32_t n, const int32_t* __restrict__ chunk_off, const int64_t* __restrict__ outoff,
-                                  const u64* __restrict__ ctr, int64_t* __restrict__ stat, u64* __restrict__ ctr_out,
-                                  const int32_t* __restrict__ err) {
-    if (threadIdx.x == 0) {
-        stat[3] = outoff[chunk_off[n]];
-        stat[4] = err ? err[0] : INT32_MAX;
-        stat[5] = err ? err[1] : INT32_MAX;
-    }
-    if (threadIdx.x < qNum) {
-        u64 v = 0;
-        for (int sh = 0; sh < kQShards; ++sh) v += ctr[sh * kQStride + threadIdx.x];
-        ctr_out[threadIdx.x] = v;
-    }
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// Fused small-batch path of hgx_pattern_batch_packed (two launches instead of five plus a copy):
-//   hgx_q_fused      one wavefront per query runs ExpressionBasedQuery.expand + the toDNF duplicate
-//                    drop on its anchors (lanes compare in first-occurrence order), the plan (the
-//                    anchor with the fewest incident links, AndToQuery's size order :164-180; with a
-//                    type its type-T slice found by 64 probes a round), and the match (64 candidates
-//                    at a time, the checks of hgx_pattern_match stage 3).  Up to kFusedHold hits go
-//                    to the query's own slot as atom ids; a query with more claims a range of an
-//                    overflow area (one atomic) and writes them there in a second match pass.
-//                    A query with more than kInline candidates (41 of the 10K bench queries, up to
-//                    16K candidates) is normalised into a BigQ record instead: one wave walking 16K
-//                    candidates alone kept the whole launch at 0.38 ms.
-//   hgx_q_fused_big  the records' candidates in kInline chunks, a wave per chunk, hits into the
-//                    chunk's own range.
-//   hgx_q_fused_out  one workgroup scans the per-query counts and copies every query's hits to its
-//                    place in the mapped result area (offsets, ids, status), so nothing is copied
-//                    back after the kernels.
-// A single-launch variant that placed the hits through a decoupled look-back over the previous
-// queries' counts took 35 ms for 10K queries: thousands of waves spun on acquire loads (each an L1
-// invalidate) while the prefix crawled from query 0.
-// ---------------------------------------------------------------------------------------------
-constexpr int kFusedMax = 16384;   // batches up to this size take the fused kernels
-constexpr int kFusedHold = 64;     // hits a query keeps in its own slot
-constexpr int kInline = 256;       // candidates a query's own wave matches; larger ones go to chunks
-constexpr int kMaxBig = 1024;      // chunked queries per batch (more: the batch takes the general path)
-constexpr int qProbe = qNum;       // counter slot: type-slice probes
-
-// A query with more than kInline candidates, normalised by its wave for the chunk kernel.
-struct BigQ {
-    int32_t q, amin, na, np;
-    int64_t cb, ce;
-    int32_t anch[kMaxAnchors];
-    int32_t pat[kMaxPattern];
-};
-
-struct FusedHead {       // head of the mapped result area (written by hgx_q_fused_out)
-    int64_t total;       // hits of the batch
-    int32_t err[3];      // smallest invalid / unsupported query; [2] = 1 if a query needs the general path
-    int32_t ovf;         // 1: the overflow area was too small (the batch runs again with a larger one)
-    int64_t ovf_need;    // overflow entries the batch claimed
-    int32_t chunk_need;  // > 0: the chunk area was too small for this many chunks (run again)
-    int32_t pad2;
-    u64 ctr[qNum + 1];   // candidates, -, arity sum, hits, probes
-};
-
-// Candidate checks of one link row L (every anchor but amin among its targets, every ordered
-// pattern a greedy subsequence): the logic of hgx_pattern_match stage 3 for the packed shapes.
-__device__ __forceinline__ bool fused_check(int32_t L, const int64_t* __restrict__ tgt_off,
-                                            const int32_t* __restrict__ tgt_idx, const int32_t* anch, int na,
-                                            int amin, const int32_t* spat, int np, bool reg_pat,
-                                            const int32_t (&pv)[8], u64& n_ar) {
-    const int64_t b = tgt_off[L];
-    const int n = (int)(tgt_off[L + 1] - b);
-    n_ar += (u64)n;
-    const int32_t* row = tgt_idx + b;
-    bool hit = true;
-    if (n <= 8) {
-        int32_t tr[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) tr[i] = i < n ? row[i] : -1;
-        for (int j = 0; j < na && hit; ++j) {
-            if (j == amin) continue;
-            const int32_t a = anch[j];
-            bool found = false;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) found |= (i < n) && tr[i] == a;
-            hit = found;
-        }
-        if (hit && reg_pat) {
-            int j = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                int32_t pj = pv[0];
-#pragma unroll
-                for (int k = 1; k < 8; ++k)
-                    if (j == k) pj = pv[k];
-                if (i < n && j < np && (pj < 0 || pj == tr[i])) ++j;
-            }
-            hit = j == np;
-        } else if (hit && np > 0) {
-            int i = 0, j = 0;
-            while (i < n && j < np) {
-                const int32_t pj = spat[j];
-                if (pj < 0 || pj == row[i]) ++j;
-                ++i;
-            }
-            hit = j == np;
-        }
-        return hit;
-    }
-    for (int j = 0; j < na && hit; ++j) {
-        if (j == amin) continue;
-        const int32_t a = anch[j];
-        bool found = false;
-        for (int i = 0; i < n && !found; ++i) found = row[i] == a;
-        hit = found;
-    }
-    if (hit && np > 0) {
-        int i = 0, j = 0;
-        while (i < n && j < np) {
-            const int32_t pj = spat[j];
-            if (pj < 0 || pj == row[i]) ++j;
-            ++i;
-        }
-        hit = j == np;
-    }
-    return hit;
-}
 
 // lower_bound(v1) and lower_bound(v2) (v1 < v2) in the ascending a[b, e), the bounds of a type slice.
 // A range of <= 64 entries is read in one coalesced load; a longer one is narrowed 16x a round by 16
@@ -1778,388 +1049,6 @@ __device__ __forceinline__ void slice_bounds(const int32_t* __restrict__ a, int3
         const int64_t st1 = __shfl(st, 0), st2 = __shfl(st, 32);
         if (r1 < 0) narrow(b1, e1, st1, __popcll(m & 0xffffffffull), r1);
         if (r2 < 0) narrow(b2, e2, st2, __popcll(m >> 32), r2);
-    }
-}
-
-__global__ void __launch_bounds__(256) hgx_q_fused(
-    int32_t n, int64_t A, const int32_t* __restrict__ type, const int64_t* __restrict__ inc_off,
-    const int32_t* __restrict__ inc, const int32_t* __restrict__ has_ordered, const int64_t* __restrict__ pat_off,
-    const int32_t* __restrict__ pat, const int64_t* __restrict__ g_inc_off, const int32_t* __restrict__ inc_row,
-    const int32_t* __restrict__ ts_type, const int32_t* __restrict__ ts_row, const int64_t* __restrict__ tgt_off,
-    const int32_t* __restrict__ tgt_idx, const int32_t* __restrict__ link_atom, int32_t* __restrict__ dstat,
-    u64* __restrict__ dctr, int64_t* __restrict__ counts, int32_t* __restrict__ slots, int64_t* __restrict__ ovf_pos,
-    int64_t* __restrict__ ovf_claim, int32_t* __restrict__ ovf, int64_t ovf_cap, BigQ* __restrict__ big,
-    int32_t* __restrict__ big_n) {
-    __shared__ int32_t s_anch[4][kMaxAnchors];
-    __shared__ int32_t s_pat[4][kMaxPattern];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wv));
-    if (q >= n) return;   // whole wave
-    int32_t* anch = s_anch[wv];
-    int32_t* spat = s_pat[wv];
-    const u64 lt = (1ull << lane) - 1ull;
-    // 1. the query, expanded: orderedLink targets become incident anchors (:730-737), duplicates
-    //    dropped in first-occurrence order (:100)
-    const int32_t tq = type[q];
-    const int64_t ib = inc_off[q], ie = inc_off[q + 1];
-    const bool ho = has_ordered[q] != 0;
-    const int64_t pb = pat_off[q], pe = pat_off[q + 1];
-    bool bad = tq < -1 || ie < ib || pe < pb;
-    bool unsup = false, legacy = false;
-    const int ni = bad ? 0 : (int)min<int64_t>(ie - ib, 65);
-    const int np = (bad || !ho) ? 0 : (int)min<int64_t>(pe - pb, kMaxPattern + 1);
-    if (ni > 64) legacy = true;   // long anchor lists take the general path (host fallback)
-    if (np > kMaxPattern) unsup = true;
-    const bool use = !legacy && !unsup;
-    const bool e0 = use && lane < ni, e1 = use && lane < np;
-    const int32_t v0 = e0 ? inc[ib + lane] : -2, v1 = e1 ? pat[pb + lane] : -2;
-    if (__ballot((e0 && (v0 < 0 || v0 >= A)) || (e1 && v1 != HGX_ANY_HANDLE && (v1 < 0 || v1 >= A)))) bad = true;
-    bool a0 = e0, a1 = e1 && v1 != HGX_ANY_HANDLE;
-    const int kmax = ni > np ? ni : np;
-    for (int k = 0; k < kmax; ++k) {   // wave-uniform
-        const int32_t x0 = __shfl(v0, k), x1 = __shfl(v1, k);
-        const bool k0 = k < ni, k1 = k < np && x1 != HGX_ANY_HANDLE;
-        if (k0 && k < lane && x0 == v0) a0 = false;
-        if ((k0 && x0 == v1) || (k1 && k < lane && x1 == v1)) a1 = false;
-    }
-    const u64 m0 = __ballot(a0), m1 = __ballot(a1);
-    const int n0 = __popcll(m0), na = n0 + __popcll(m1);
-    if (!bad && use && (na == 0 || na > kMaxAnchors)) unsup = true;
-    const bool isnop = ho && pe == pb;   // an empty OrderedLinkCondition compiles to HGQuery.NOP
-    const bool run = !bad && !unsup && !legacy && !isnop;
-    if (run) {
-        if (a0) anch[__popcll(m0 & lt)] = v0;
-        if (a1) anch[n0 + __popcll(m1 & lt)] = v1;
-        if (e1) spat[lane] = v1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-        if (bad) atomicMin(&dstat[0], q);
-        else if (unsup) atomicMin(&dstat[1], q);
-        else if (legacy) atomicMax(&dstat[2], 1);
-    }
-    // 2. plan
-    int64_t cb = 0, ce = 0;
-    int amin = 0;
-    u64 probes = 0;
-    if (run) {
-        const int32_t a = lane < na ? anch[lane] : 0;
-        const int64_t lo = lane < na ? g_inc_off[a] : 0, hi = lane < na ? g_inc_off[a + 1] : 0;
-        int64_t best = lane < na ? hi - lo : INT64_MAX;
-        int bi = lane;
-        for (int off = 32; off > 0; off >>= 1) {
-            const int64_t os = __shfl_xor(best, off);
-            const int oi = __shfl_xor(bi, off);
-            if (os < best || (os == best && oi < bi)) {
-                best = os;
-                bi = oi;
-            }
-        }
-        amin = __builtin_amdgcn_readfirstlane(bi);
-        cb = __shfl(lo, amin);
-        ce = __shfl(hi, amin);
-        if (tq >= 0) {   // the type-T slice of the grouped incidence
-            int64_t r1, r2;
-            slice_bounds(ts_type, tq, tq + 1, cb, ce, r1, r2, probes);
-            cb = r1;
-            ce = r2;
-        }
-    }
-    // 3. match: candidates 64 at a time, ascending; the first kFusedHold hits go to the slot
-    const int32_t* rows = tq >= 0 ? ts_row : inc_row;
-    const bool reg_pat = np <= 8;
-    int32_t pv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pv[k] = __shfl(v1, k);   // the pattern in registers (np <= 8)
-    if (run && ce - cb > kInline) {   // hand the query to the chunk kernel
-        int k = 0;
-        if (lane == 0) k = atomicAdd(big_n, 1);
-        k = __shfl(k, 0);
-        if (k < kMaxBig) {
-            BigQ* bq = big + k;
-            if (lane == 0) {
-                bq->q = q;
-                bq->amin = amin;
-                bq->na = na;
-                bq->np = np;
-                bq->cb = cb;
-                bq->ce = ce;
-            }
-            if (lane < na) bq->anch[lane] = anch[lane];
-            if (lane < np) bq->pat[lane] = spat[lane];
-            if (lane == 0) ovf_pos[q] = -(int64_t)(k + 1);
-        } else if (lane == 0) {
-            atomicMax(&dstat[2], 1);   // too many: the batch takes the general path
-        }
-        if (lane == 0) {
-            counts[q] = 0;   // the chunk kernel adds the query's hits
-            u64* c = dctr + (q & (kQShards - 1)) * kQStride;
-            atomicAdd(c + qCand, (u64)(ce - cb));
-            if (probes) atomicAdd(c + qProbe, probes);
-        }
-        return;
-    }
-    const int64_t nc = run ? ce - cb : 0;
-    if (lane == 0) ovf_pos[q] = 0;   // not chunked (an overflow range replaces it below)
-    int32_t* slot = slots + (int64_t)q * kFusedHold;
-    int64_t hits = 0;
-    u64 n_ar = 0;
-    for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
-        bool hit = false;
-        int32_t L = 0;
-        if (i0 + lane < nc) {
-            L = rows[cb + i0 + lane];
-            hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, reg_pat, pv, n_ar);
-        }
-        const u64 m = __ballot(hit);
-        const int64_t r = hits + __popcll(m & lt);
-        if (hit && r < kFusedHold) slot[r] = link_atom[L];
-        hits += __popcll(m);
-    }
-    if (hits > kFusedHold) {   // a second pass into a claimed overflow range
-        int64_t base = 0;
-        if (lane == 0) base = (int64_t)atomicAdd((unsigned long long*)ovf_claim, (unsigned long long)hits);
-        base = __shfl(base, 0);
-        if (lane == 0) ovf_pos[q] = base;
-        if (base + hits <= ovf_cap) {
-            int64_t w = 0;
-            u64 dummy = 0;
-            for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
-                bool hit = false;
-                int32_t L = 0;
-                if (i0 + lane < nc) {
-                    L = rows[cb + i0 + lane];
-                    hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, reg_pat, pv, dummy);
-                }
-                const u64 m = __ballot(hit);
-                if (hit) ovf[base + w + __popcll(m & lt)] = link_atom[L];
-                w += __popcll(m);
-            }
-        }
-    }
-    if (lane == 0) counts[q] = hits;
-    u64* c = dctr + (q & (kQShards - 1)) * kQStride;
-    for (int off = 32; off > 0; off >>= 1) n_ar += __shfl_xor(n_ar, off);
-    if (lane == 0) {
-        if (nc) atomicAdd(c + qCand, (u64)nc);
-        if (n_ar) atomicAdd(c + qArity, n_ar);
-        if (hits) atomicAdd(c + qHits, (u64)hits);
-        if (probes) atomicAdd(c + qProbe, probes);
-    }
-}
-
-// Chunks of the BigQ records: chunk c of record k covers candidates [cb + j * kInline, +kInline) with
-// j = c - chunk_off[k].  Each workgroup rebuilds the chunk offsets of the records in LDS, its waves
-// grid-stride over the chunks; a chunk's hits (atom ids, ascending) go to big_hits[c * kInline ...],
-// their number to chunk_cnt[c] and into the query's count.
-__device__ __forceinline__ int big_chunk_offsets(const BigQ* __restrict__ big, int nb, int32_t* coff) {
-    // coff[k] = first chunk of record k (nb <= kMaxBig); returns the chunk total.  256 threads.
-    __shared__ int32_t wsum[4];
-    const int per = (nb + 255) / 256;   // <= 4
-    const int k0 = threadIdx.x * per;
-    int32_t cv[4], sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        cv[j] = (j < per && k0 + j < nb) ? (int32_t)((big[k0 + j].ce - big[k0 + j].cb + kInline - 1) / kInline) : 0;
-        sum += cv[j];
-    }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int incl = sum;
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int w = 0; w < 4; ++w) {
-        before += w < wv ? wsum[w] : 0;
-        total += wsum[w];
-    }
-    int e = before + incl - sum;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (j < per && k0 + j < nb) coff[k0 + j] = e;
-        e += cv[j];
-    }
-    if (threadIdx.x == 0) coff[nb] = total;
-    __syncthreads();
-    return total;
-}
-
-__global__ void __launch_bounds__(256) hgx_q_fused_big(const BigQ* __restrict__ big, const int32_t* __restrict__ big_n,
-                                                       const int32_t* __restrict__ inc_row,
-                                                       const int32_t* __restrict__ ts_row,
-                                                       const int32_t* __restrict__ type,
-                                                       const int64_t* __restrict__ tgt_off,
-                                                       const int32_t* __restrict__ tgt_idx,
-                                                       const int32_t* __restrict__ link_atom, int64_t* __restrict__ counts,
-                                                       int32_t* __restrict__ big_hits, int32_t* __restrict__ chunk_cnt,
-                                                       int32_t chunk_cap, int32_t* __restrict__ dstat,
-                                                       u64* __restrict__ dctr) {
-    __shared__ int32_t coff[kMaxBig + 1];
-    __shared__ int32_t s_anch[4][kMaxAnchors];
-    __shared__ int32_t s_pat[4][kMaxPattern];
-    const int nb = min(*big_n, kMaxBig);
-    if (nb == 0) return;   // block-uniform
-    const int total = big_chunk_offsets(big, nb, coff);
-    if (total > chunk_cap) {   // too small a chunk area: the host runs the batch again with a larger one
-        if (blockIdx.x == 0 && threadIdx.x == 0) dstat[3] = total;
-        return;
-    }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const u64 lt = (1ull << lane) - 1ull;
-    int32_t* anch = s_anch[wv];
-    int32_t* spat = s_pat[wv];
-    u64 n_ar = 0;
-    for (int c = blockIdx.x * 4 + wv; c < total; c += gridDim.x * 4) {   // wave-uniform
-        int lo = 0, hi = nb;   // the record k with coff[k] <= c < coff[k + 1]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (coff[mid] <= c) lo = mid; else hi = mid;
-        }
-        const BigQ* bq = big + lo;
-        const int q = bq->q, amin = bq->amin, na = bq->na, np = bq->np;
-        const int64_t b0 = bq->cb + (int64_t)(c - coff[lo]) * kInline;
-        const int64_t nc = min<int64_t>(kInline, bq->ce - b0);
-        if (lane < na) anch[lane] = bq->anch[lane];
-        const int32_t pvl = lane < np ? bq->pat[lane] : -2;
-        if (lane < np) spat[lane] = pvl;
-        __builtin_amdgcn_wave_barrier();
-        int32_t pv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pv[k] = __shfl(pvl, k);
-        const int32_t* rows = type[q] >= 0 ? ts_row : inc_row;
-        int32_t* out = big_hits + (int64_t)c * kInline;
-        int64_t hits = 0;
-        for (int64_t i0 = 0; i0 < nc; i0 += 64) {   // wave-uniform
-            bool hit = false;
-            int32_t L = 0;
-            if (i0 + lane < nc) {
-                L = rows[b0 + i0 + lane];
-                hit = fused_check(L, tgt_off, tgt_idx, anch, na, amin, spat, np, np <= 8, pv, n_ar);
-            }
-            const u64 m = __ballot(hit);
-            if (hit) out[hits + __popcll(m & lt)] = link_atom[L];
-            hits += __popcll(m);
-        }
-        if (lane == 0) {
-            chunk_cnt[c] = (int32_t)hits;
-            if (hits) atomicAdd((unsigned long long*)&counts[q], (unsigned long long)hits);
-            if (hits) atomicAdd(dctr + (q & (kQShards - 1)) * kQStride + qHits, (u64)hits);
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    for (int off = 32; off > 0; off >>= 1) n_ar += __shfl_xor(n_ar, off);
-    if (lane == 0 && n_ar) atomicAdd(dctr + qArity, n_ar);
-}
-
-// One workgroup: exclusive scan of the per-query hit counts into the mapped offsets, every query's
-// hits copied from its slot (or its overflow range) to the mapped ids, and the batch status.
-__global__ void __launch_bounds__(kScanBlock) hgx_q_fused_out(int32_t n, const int64_t* __restrict__ counts,
-                                                             const int32_t* __restrict__ slots,
-                                                             const int64_t* __restrict__ ovf_pos,
-                                                             const int64_t* __restrict__ ovf_claim,
-                                                             const int32_t* __restrict__ ovf, int64_t ovf_cap,
-                                                             const BigQ* __restrict__ big,
-                                                             const int32_t* __restrict__ big_n,
-                                                             const int32_t* __restrict__ big_hits,
-                                                             const int32_t* __restrict__ chunk_cnt,
-                                                             const int32_t* __restrict__ dstat,
-                                                             const u64* __restrict__ dctr, FusedHead* __restrict__ head,
-                                                             int64_t* __restrict__ out_off, int32_t* __restrict__ out_ids,
-                                                             int64_t cap) {
-    __shared__ int64_t ws64[kScanBlock / 64];
-    __shared__ int64_t qstart[kMaxBig];
-    const int32_t per = (n + kScanBlock - 1) / kScanBlock;   // <= 16 (n <= kFusedMax)
-    const int32_t q0 = threadIdx.x * per;
-    int64_t cv[16];
-    int64_t sk = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        cv[j] = (j < per && q0 + j < n) ? counts[q0 + j] : 0;
-        sk += cv[j];
-    }
-    int64_t tk;
-    int64_t ek = block_exclusive_scan<int64_t>(sk, ws64, tk);
-    const int64_t ovf_need = *ovf_claim;
-    const bool ovf_bad = ovf_need > ovf_cap;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        if (j < per && q0 + j < n) {
-            const int32_t q = q0 + j;
-            out_off[q] = ek;
-            const int64_t h = cv[j];
-            const int64_t op = ovf_pos[q];
-            if (op < 0) {
-                qstart[-op - 1] = ek;   // a chunked query: placed below
-            } else if (tk <= cap && !ovf_bad) {
-                const int32_t* src = h <= kFusedHold ? slots + (int64_t)q * kFusedHold : ovf + op;
-                for (int64_t i = 0; i < h; ++i) out_ids[ek + i] = src[i];
-            }
-        }
-        ek += cv[j];
-    }
-    // chunked queries: each chunk's place = its query's start + the hits of the query's earlier chunks
-    // (a scan of the chunk counts); then the chunks are copied one after the other by the whole block
-    const int nb = min(*big_n, kMaxBig);
-    if (nb > 0 && tk <= cap && !ovf_bad && dstat[3] == 0) {   // block-uniform
-        __shared__ int32_t coff[kMaxBig + 1];
-        __shared__ int64_t cex[kScanBlock];
-        __shared__ int64_t cstart[kScanBlock];
-        // chunk offsets of the records (1024 threads: one record each)
-        int32_t nck = 0;
-        if ((int)threadIdx.x < nb) nck = (int32_t)((big[threadIdx.x].ce - big[threadIdx.x].cb + kInline - 1) / kInline);
-        int64_t tch;
-        const int64_t ech = block_exclusive_scan<int64_t>((int64_t)nck, ws64, tch);
-        if ((int)threadIdx.x < nb) coff[threadIdx.x] = (int32_t)ech;
-        if (threadIdx.x == 0) coff[nb] = (int32_t)tch;
-        __syncthreads();
-        for (int64_t c0 = 0; c0 < tch; c0 += kScanBlock) {   // block-uniform: kScanBlock chunks at a time
-            const int64_t c = c0 + threadIdx.x;
-            int64_t cnt = c < tch ? chunk_cnt[c] : 0;
-            int64_t tot;
-            const int64_t ex = block_exclusive_scan<int64_t>(cnt, ws64, tot);   // over this window
-            int k = 0;
-            if (c < tch) {
-                int lo = 0, hi = nb;
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (coff[mid] <= c) lo = mid; else hi = mid;
-                }
-                k = lo;
-            }
-            cex[threadIdx.x] = ex;
-            __syncthreads();
-            if (c < tch) {
-                // hits of the record's earlier chunks: those inside this window + those before it
-                const int64_t first = coff[k];
-                int64_t before = ex - (first >= c0 ? cex[first - c0] : 0);
-                if (first < c0) {   // the record started in an earlier window: add its earlier chunks
-                    for (int64_t e = first; e < c0; ++e) before += chunk_cnt[e];
-                }
-                cstart[threadIdx.x] = qstart[k] + before;
-            }
-            __syncthreads();
-            for (int64_t cc = c0; cc < c0 + kScanBlock && cc < tch; ++cc) {   // block-uniform
-                const int64_t cn = chunk_cnt[cc], st = cstart[cc - c0];
-                for (int64_t i = threadIdx.x; i < cn; i += kScanBlock) out_ids[st + i] = big_hits[cc * kInline + i];
-            }
-            __syncthreads();
-        }
-    }
-    if (threadIdx.x == 0) {
-        out_off[n] = tk;
-        head->total = tk;
-        for (int i = 0; i < 3; ++i) head->err[i] = dstat[i];
-        head->chunk_need = dstat[3];
-        head->ovf = ovf_bad ? 1 : 0;
-        head->ovf_need = ovf_need;
-    }
-    if (threadIdx.x <= qNum) {
-        u64 t = 0;
-        for (int sh = 0; sh < kQShards; ++sh) t += dctr[sh * kQStride + threadIdx.x];
-        head->ctr[threadIdx.x] = t;
     }
 }
 
@@ -2548,21 +1437,14 @@ void front_host(hgx_graph* g, int32_t n, const NormBatch& nb, Scratch& sc, Event
     f.pat = (const int32_t*)(d + o_pat);
     f.cond_bytes = 20.0 * nb.anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
                    4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
-    if (g->q_flat == 2) {   // single-pass pipeline: the plan + per-block candidate totals
-        f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
-        f.lpre = (int64_t*)sc.take(sizeof(int64_t) * (size_t)std::max(n, 1));
-        f.ctr = (u64*)sc.take(sizeof(u64) * kQShards * kQStride);
-        hgx_q_plan_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
-            n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop), g->inc_off, g->inc_ts_type, f.plan, f.ncand, f.blk,
-            f.lpre, f.ctr);
-        HGX_CHECK_LAUNCH();
-        return;
-    }
-    hgx_q_plan<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop),
-                                                         g->inc_off, g->inc_ts_type, f.plan, f.nch, f.ncand);
+    // the single-pass pipeline: the plan + per-block candidate totals
+    f.blk = (int64_t*)sc.take(sizeof(int64_t) * 3 * (size_t)ceil_div(n, kSpBlock));
+    f.lpre = (int64_t*)sc.take(sizeof(int64_t) * (size_t)std::max(n, 1));
+    f.ctr = (u64*)sc.take(sizeof(u64) * kQShards * kQStride);
+    hgx_q_plan_sp<<<(unsigned)ceil_div(n, kSpBlock), kSpBlock, 0, s>>>(
+        n, f.desc, f.anch, f.types, (const int32_t*)(d + o_nop), g->inc_off, g->inc_ts_type, f.plan, f.ncand, f.blk,
+        f.lpre, f.ctr);
     HGX_CHECK_LAUNCH();
-    f.cond_bytes = 20.0 * nb.anchors.size() + 4.0 * nb.types.size() + 4.0 * nb.pos.size() +
-                   4.0 * nb.pattern.size() + (double)sizeof(QDesc) * n;
 }
 
 // Layout of a packed batch in one staging area (pinned, mapped or device): its columns at 16-byte
@@ -2610,7 +1492,7 @@ void packed_fill(char* h, const PackedLayout& l, int32_t n, const int32_t* type,
 
 // Normalise + plan a packed batch the device can read at d (the mapped staging area, a device copy of
 // the pinned staging, or a query set resident in HBM).  sp: the single-pass front kernel.
-void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d, bool sp, Scratch& sc, Events& ev,
+void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d, Scratch& sc, Events& ev,
                   Front& f) {
     hipStream_t s = g->stream;
     QDesc* desc = (QDesc*)sc.take(sizeof(QDesc) * n);
@@ -2621,7 +1503,7 @@ void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d,
     f.ncand = (int64_t*)sc.take(sizeof(int64_t) * (n + 1));
     f.err = (int32_t*)(d + l.o_err);
     f.cond_bytes = 20.0 * (double)(l.n_inc + l.n_pat) + 4.0 * n + 4.0 * (double)l.n_pat + (double)sizeof(QDesc) * n;
-    if (sp) {   // normalise + plan straight from d; device copies of the match's columns
+    {   // normalise + plan straight from d; device copies of the match's columns
         int32_t* dty = (int32_t*)sc.take(4 * (size_t)n);
         int64_t* dpo = (int64_t*)sc.take(8 * (size_t)(n + 1));
         int32_t* dpa = (int32_t*)sc.take(4 * (size_t)std::max<int64_t>(l.n_pat, 1));
@@ -2641,17 +1523,6 @@ void front_device(hgx_graph* g, int32_t n, const PackedLayout& l, const char* d,
         f.pat = dpa;
         return;
     }
-    hgx_q_norm_packed<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(
-        n, g->A, (const int32_t*)(d + l.o_type), (const int64_t*)(d + l.o_ioff), (const int32_t*)(d + l.o_inc),
-        (const int32_t*)(d + l.o_ho), (const int64_t*)(d + l.o_poff), (const int32_t*)(d + l.o_pat), g->inc_off,
-        g->inc_ts_type, desc, anch, nop, f.plan, f.nch, f.ncand, f.err);
-    HGX_CHECK_LAUNCH();
-    f.desc = desc;
-    f.anch = anch;
-    f.types = (const int32_t*)(d + l.o_type);
-    f.pos = nullptr;
-    f.poff = (const int64_t*)(d + l.o_poff);
-    f.pat = (const int32_t*)(d + l.o_pat);
 }
 
 // Front end for the packed batch: the raw arrays go into one staging area (the single-pass kernel reads
@@ -2661,13 +1532,10 @@ void front_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* i
                   Front& f) {
     hipStream_t s = g->stream;
     const PackedLayout l = packed_layout(n, inc, inc_off, pat, pat_off, "hgx_pattern_batch_packed");
-    const bool sp = g->q_flat == 2;   // single-pass: the front kernel reads the staging area in place
-    char* h = sp ? (char*)g->zc_in_buf(l.bytes) : (char*)g->pinned_buf(l.bytes);
+    char* h = (char*)g->zc_in_buf(l.bytes);   // the front kernel reads the staging area in place
     packed_fill(h, l, n, type, inc_off, inc, has_ordered, pat_off, pat);
-    char* d = sp ? (char*)g->zc_in_dev : (char*)sc.take(l.bytes);
     ev.rec(0, s);
-    if (!sp) HGX_HIP(hipMemcpyAsync(d, h, l.bytes, hipMemcpyHostToDevice, s));
-    front_device(g, n, l, d, sp, sc, ev, f);
+    front_device(g, n, l, (char*)g->zc_in_dev, sc, ev, f);
 }
 
 // Single-pass back end (HGX_OPT_QUERY_FLAT = 2, default): scan + match + placement + offsets after the
@@ -2816,383 +1684,14 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
     }
 }
 
-// Flat back end (HGX_OPT_QUERY_FLAT = 1, A/B): the candidates of the batch in chunks of 64, a wave
-// per chunk and a lane per candidate (hgx_pattern_match_flat); the rest as back_end below.
-void back_end_flat(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
-                   double t0) {
-    (void)sc;
-    hipStream_t s = g->stream;
-    const bool small = n <= kSmallBatch;
-    if (g->q_cap_chunks < (int64_t)n / 4 + 64) g->q_cap_chunks = (int64_t)n / 4 + 64;
-    if (g->q_cap_cand < 16 * (int64_t)n + 4096) g->q_cap_cand = 16 * (int64_t)n + 4096;
-    for (int attempt = 0;; ++attempt) {
-        const int64_t capC = std::max<int64_t>(g->q_cap_chunks, ceil_div(g->q_cap_cand, kFlatChunk)), capK = g->q_cap_cand;
-        if (capC > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
-        Scratch w{g, {}};
-        int64_t* coff = (int64_t*)w.take(sizeof(int64_t) * (n + 1));
-        int32_t* chq = (int32_t*)w.take(sizeof(int32_t) * capC);
-        int32_t* nch = (int32_t*)w.take(sizeof(int32_t) * 4);
-        int32_t* slots = (int32_t*)w.take(sizeof(int32_t) * capC * kFlatChunk);
-        int64_t* cnt = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
-        u64* hmask = (u64*)w.take(sizeof(u64) * (capC + 1));
-        int64_t* outoff = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
-        u64* ctr = (u64*)w.take(sizeof(u64) * kQShards * kQStride);
-        const size_t m_stat = 0, m_ctr = 64, m_qoff = 128;
-        const size_t m_ids = m_qoff + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
-        char* rd = (char*)w.take(m_ids + 4 * (size_t)capK);
-        int64_t* stat_d = (int64_t*)(rd + m_stat);
-        u64* ctr_d = (u64*)(rd + m_ctr);
-        int64_t* qoff_d = (int64_t*)(rd + m_qoff);
-        int32_t* ids_d = (int32_t*)(rd + m_ids);
-        if (small) {
-            hgx_q_scan_flat<<<1, kScanBlock, 0, s>>>(n, f.ncand, coff, chq, nch, capC, capK, stat_d, ctr);
-            HGX_CHECK_LAUNCH();
-        } else {
-            HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
-            HGX_HIP(hipMemsetAsync(f.ncand + n, 0, sizeof(int64_t), s));
-            size_t tb = 0;
-            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
-            void* tmp = w.take(tb);
-            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
-            hgx_q_check_flat<<<1, 1, 0, s>>>(n, coff, nch, capC, capK, stat_d);
-            HGX_CHECK_LAUNCH();
-            hgx_q_chunk_map_flat<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, coff, stat_d, chq);
-            HGX_CHECK_LAUNCH();
-        }
-        ev.rec(1, s);
-        hgx_pattern_match_flat<false><<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
-            nch, n, chq, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row, g->inc_type,
-            g->inc_ts_row, g->tgt_off, g->tgt_idx, g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt,
-            hmask, ctr, nullptr, nullptr, 0, 0, 0);
-        HGX_CHECK_LAUNCH();
-        ev.rec(2, s);
-        if (small) {
-            hgx_q_finish_flat<<<1, kScanBlock, 0, s>>>(n, nch, coff, cnt, hmask, ctr, outoff, qoff_d, stat_d, ctr_d,
-                                                        f.err);
-            HGX_CHECK_LAUNCH();
-        } else {
-            size_t tb = 0;
-            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
-            void* tmp = w.take(tb);
-            HGX_HIP(hipMemsetAsync(cnt + capC, 0, sizeof(int64_t), s));
-            HGX_HIP(rocprim::exclusive_scan(tmp, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
-            hgx_q_offsets_flat<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, nch, coff, outoff, hmask, stat_d, qoff_d);
-            HGX_CHECK_LAUNCH();
-        }
-        hgx_q_scatter_flat<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(nch, cnt, outoff, slots, g->link_atom,
-                                                                              ids_d);
-        HGX_CHECK_LAUNCH();
-        if (!small) {
-            hgx_q_finish_stat_flat<<<1, 64, 0, s>>>(nch, outoff, ctr, stat_d, ctr_d, f.err);
-            HGX_CHECK_LAUNCH();
-        }
-        const int64_t guess = std::min<int64_t>(capK, std::max<int64_t>(g->q_hits_guess, 1024));
-        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
-        HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
-        ev.rec(3, s);
-        spin_sync(s);
-        const int64_t* stat = (const int64_t*)(hm + m_stat);
-        const u64* ctr_h = (const u64*)(hm + m_ctr);
-        const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
-        const int32_t* ids_h = (const int32_t*)(hm + m_ids);
-        if (stat[4] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(stat[4]));
-        if (stat[5] < n)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(stat[5]) +
-                                        " is not accelerated (no incidence anchor or condition limits)");
-        if (stat[2]) {   // workspace too small: grow to the reported totals and match again
-            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: workspace sizing failed");
-            g->q_cap_chunks = std::max<int64_t>(capC, stat[0] + stat[0] / 4 + 64);
-            g->q_cap_cand = std::max<int64_t>(capK, stat[1] + stat[1] / 4 + 4096);
-            continue;
-        }
-        const int64_t total = stat[3];
-        if (total > guess) {
-            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, ids_d + guess, 4 * (size_t)(total - guess),
-                                   hipMemcpyDeviceToHost, s));
-            HGX_HIP(hipStreamSynchronize(s));
-        }
-        g->q_hits_guess = total + total / 4;
-        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
-        r->ids.assign(ids_h, ids_h + total);
-        if (prof)
-            std::fprintf(stderr, "[hgx query] flat n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n",
-                         n, now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
-        if (ev.on) {
-            float a = 0, b = 0;
-            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
-            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
-            r->ms_total = a;
-            r->ms_match = b;
-        }
-        // algorithmic bytes of hgx_pattern_match_flat: per chunk its first query and its window of
-        // query offsets; per candidate its query's plan + descriptor (once per query) and, when its
-        // range is not type-grouped, its type; per examined candidate its link row and its inline
-        // record or tgt_off pair + target row; per chunk its count and hit mask; 4 B per hit; the
-        // conditions
-        r->bytes_match = (4.0 + 8.0 * (kFlatChunk + 1) + 16.0) * (double)stat[0] +
-                         (double)(sizeof(QPlan) + sizeof(QDesc)) * n + 4.0 * (double)ctr_h[qCand] +
-                         4.0 * (double)ctr_h[qTyped] + 32.0 * (double)ctr_h[qInline] +
-                         16.0 * ((double)ctr_h[qTyped] - (double)ctr_h[qInline]) + 4.0 * (double)ctr_h[qArity] +
-                         4.0 * (double)ctr_h[qHits] + f.cond_bytes;
-        return;
-    }
-}
-
-// Back end shared by every entry point: chunk tables, match, compaction into one result area that
-// goes back in one copy, one synchronisation.  The candidate / chunk workspace has a capacity kept on the graph;
-// a batch that exceeds it is detected on the device (nothing is matched), the capacity grows to the
-// reported totals and the back end runs again.
+// The back end of every batch: the single-pass pipeline (round 5: the per-query-chunk (HGX_OPT_QUERY_FLAT 0)
+// and separate-scan flat (1) back ends are gone; both measured slower).
 void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_query_result* r, bool prof,
               double t0) {
-    if (f.blk) return back_end_sp(g, n, f, sc, ev, r, prof, t0);
-    if (g->q_flat) return back_end_flat(g, n, f, sc, ev, r, prof, t0);
-    hipStream_t s = g->stream;
-    const bool small = n <= kSmallBatch;
-    if (g->q_cap_chunks < (int64_t)n + 64) g->q_cap_chunks = (int64_t)n + 64;
-    if (g->q_cap_cand < 16 * (int64_t)n + 4096) g->q_cap_cand = 16 * (int64_t)n + 4096;
-    for (int attempt = 0;; ++attempt) {
-        const int64_t capC = g->q_cap_chunks, capK = g->q_cap_cand;
-        if (capC > (int64_t)INT32_MAX - 1) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: candidate volume overflow");
-        Scratch w{g, {}};
-        int32_t* choff = (int32_t*)w.take(sizeof(int32_t) * (n + 1));
-        int64_t* coff = (int64_t*)w.take(sizeof(int64_t) * (n + 1));
-        int32_t* chq = (int32_t*)w.take(sizeof(int32_t) * capC);
-        int32_t* slots = (int32_t*)w.take(sizeof(int32_t) * capK);
-        int64_t* cnt = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
-        int64_t* outoff = (int64_t*)w.take(sizeof(int64_t) * (capC + 1));
-        u64* ctr = (u64*)w.take(sizeof(u64) * kQShards * kQStride);
-        // result area (device, copied back in one piece): stat[8] | ctr[4] | q_off[n+1] | ids[capK]
-        // stat: [0] chunks [1] candidates [2] overflow [3] hits [4] invalid query [5] unsupported query
-        const size_t m_stat = 0, m_ctr = 64, m_qoff = 128;
-        const size_t m_ids = m_qoff + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
-        char* rd = (char*)w.take(m_ids + 4 * (size_t)capK);
-        int64_t* stat_d = (int64_t*)(rd + m_stat);
-        u64* ctr_d = (u64*)(rd + m_ctr);
-        int64_t* qoff_d = (int64_t*)(rd + m_qoff);
-        int32_t* ids_d = (int32_t*)(rd + m_ids);
-        if (!small) HGX_HIP(hipMemsetAsync(ctr, 0, sizeof(u64) * kQShards * kQStride, s));
-        // cnt needs no clearing: the match writes the count of every chunk below the chunk total
-        if (small) {
-            hgx_q_scan_small<<<1, kScanBlock, 0, s>>>(n, f.nch, f.ncand, choff, coff, chq, capC, capK, stat_d, ctr);
-            HGX_CHECK_LAUNCH();
-        } else {
-            HGX_HIP(hipMemsetAsync(f.nch + n, 0, sizeof(int32_t), s));
-            HGX_HIP(hipMemsetAsync(f.ncand + n, 0, sizeof(int64_t), s));
-            size_t b1 = 0, b2 = 0;
-            HGX_HIP(rocprim::exclusive_scan(nullptr, b1, f.nch, choff, (int32_t)0, (size_t)n + 1, rocprim::plus<int32_t>(), s));
-            HGX_HIP(rocprim::exclusive_scan(nullptr, b2, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
-            size_t tb = std::max(b1, b2);
-            void* tmp = w.take(tb);
-            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.nch, choff, (int32_t)0, (size_t)n + 1, rocprim::plus<int32_t>(), s));
-            HGX_HIP(rocprim::exclusive_scan(tmp, tb, f.ncand, coff, (int64_t)0, (size_t)n + 1, rocprim::plus<int64_t>(), s));
-            hgx_q_check<<<1, 1, 0, s>>>(n, choff, coff, capC, capK, stat_d);
-            HGX_CHECK_LAUNCH();
-            hgx_q_chunk_map<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, choff, stat_d, chq);
-            HGX_CHECK_LAUNCH();
-        }
-        const int32_t* d_nchunks = choff + n;   // 0 after an overflow
-        ev.rec(1, s);
-        hgx_pattern_match<<<grid_for(capC * 64, 256, 4096), 256, 0, s>>>(
-            d_nchunks, chq, choff, coff, f.plan, f.desc, f.anch, f.types, f.pos, f.poff, f.pat, g->inc_row,
-            g->inc_type, g->inc_ts_row, g->tgt_off, g->tgt_idx,
-            g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr, slots, cnt, ctr);
-        HGX_CHECK_LAUNCH();
-        ev.rec(2, s);
-        if (small) {
-            hgx_q_finish_small<<<1, kScanBlock, 0, s>>>(n, choff, chq, coff, cnt, slots, g->link_atom, ctr, outoff,
-                                                        qoff_d, ids_d, stat_d, ctr_d, f.err);
-            HGX_CHECK_LAUNCH();
-            hgx_q_scatter<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(d_nchunks, chq, choff, coff, cnt, outoff,
-                                                                            slots, g->link_atom, ids_d);
-            HGX_CHECK_LAUNCH();
-        } else {
-            size_t tb = 0;
-            HGX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
-            void* tmp = w.take(tb);
-            HGX_HIP(rocprim::exclusive_scan(tmp, tb, cnt, outoff, (int64_t)0, (size_t)capC + 1, rocprim::plus<int64_t>(), s));
-            hgx_q_offsets<<<grid_for(n + 1, 256, 1 << 20), 256, 0, s>>>(n, choff, outoff, stat_d, qoff_d);
-            HGX_CHECK_LAUNCH();
-            hgx_q_scatter<<<(unsigned)ceil_div(capC * 64, 256), 256, 0, s>>>(d_nchunks, chq, choff, coff, cnt, outoff,
-                                                                            slots, g->link_atom, ids_d);
-            HGX_CHECK_LAUNCH();
-            hgx_q_finish_stat<<<1, 64, 0, s>>>(n, choff, outoff, ctr, stat_d, ctr_d, f.err);
-            HGX_CHECK_LAUNCH();
-        }
-        // one copy back: the head and as many ids as the last batches needed (a second copy if more)
-        const int64_t guess = std::min<int64_t>(capK, std::max<int64_t>(g->q_hits_guess, 1024));
-        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)capK);
-        HGX_HIP(hipMemcpyAsync(hm, rd, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
-        ev.rec(3, s);
-        spin_sync(s);
-        const int64_t* stat = (const int64_t*)(hm + m_stat);
-        const u64* ctr_h = (const u64*)(hm + m_ctr);
-        const int64_t* qoff_h = (const int64_t*)(hm + m_qoff);
-        const int32_t* ids_h = (const int32_t*)(hm + m_ids);
-        if (stat[4] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(stat[4]));
-        if (stat[5] < n)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(stat[5]) +
-                                        " is not accelerated (no incidence anchor or condition limits)");
-        if (stat[2]) {   // workspace too small: grow to the reported totals and match again
-            if (attempt > 0) fail(HGX_E_DEVICE, "hgx_pattern_batch: workspace sizing failed");
-            g->q_cap_chunks = std::max<int64_t>(capC, stat[0] + stat[0] / 4 + 64);
-            g->q_cap_cand = std::max<int64_t>(capK, stat[1] + stat[1] / 4 + 4096);
-            continue;
-        }
-        const int64_t total = stat[3];
-        if (total > guess) {
-            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, ids_d + guess, 4 * (size_t)(total - guess),
-                                   hipMemcpyDeviceToHost, s));
-            HGX_HIP(hipStreamSynchronize(s));
-        }
-        g->q_hits_guess = total + total / 4;
-        std::memcpy(r->offsets.data(), qoff_h, sizeof(int64_t) * (n + 1));
-        r->ids.assign(ids_h, ids_h + total);
-        if (prof)
-            std::fprintf(stderr, "[hgx query] n=%d host+device %.3f ms (chunks %lld, candidates %lld, hits %lld)\n", n,
-                         now_ms() - t0, (long long)stat[0], (long long)stat[1], (long long)total);
-        if (ev.on) {
-            float a = 0, b = 0;
-            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
-            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
-            r->ms_total = a;
-            r->ms_match = b;
-        }
-        // algorithmic bytes of hgx_pattern_match: per streamed candidate its type (4 B; none in a
-        // type-grouped range), per examined candidate its link row (4 B) and either its 32-byte inline
-        // record or its tgt_off pair and target row, 4 B per hit, per chunk its plan / descriptor, plus
-        // the conditions
-        r->bytes_match = 4.0 * (double)ctr_h[qCand] + 4.0 * (double)ctr_h[qTyped] +
-                         32.0 * (double)ctr_h[qInline] + 16.0 * ((double)ctr_h[qTyped] - (double)ctr_h[qInline]) +
-                         4.0 * (double)ctr_h[qArity] + 4.0 * (double)ctr_h[qHits] +
-                         (8.0 + sizeof(QPlan) + sizeof(QDesc)) * (double)stat[0] + f.cond_bytes;
-        return;
-    }
+    back_end_sp(g, n, f, sc, ev, r, prof, t0);
 }
 
 
-// The fused path of hgx_pattern_batch_packed (batches of <= kFusedMax queries): the raw arrays go up
-// in one pinned copy together with the zeroed status / counter words, hgx_q_fused + hgx_q_fused_out,
-// one synchronisation; offsets and ids are read from the mapped result area.  Returns false when a
-// query needs the general path (more than 64 incident entries), which the caller then runs.
-bool run_fused_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
-                      const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result* r,
-                      bool prof, double t0) {
-    hipStream_t s = g->stream;
-    const int64_t n_inc = inc_off[n] - inc_off[0], n_pat = pat_off[n] - pat_off[0];
-    if (inc_off[0] != 0 || pat_off[0] != 0 || n_inc < 0 || n_pat < 0 || (n_inc > 0 && !inc) || (n_pat > 0 && !pat))
-        fail(HGX_E_INVALID, "hgx_pattern_batch_packed: bad offsets");
-    Upload u;
-    const size_t o_type = u.take(4 * (size_t)n), o_ioff = u.take(8 * (size_t)(n + 1)), o_inc = u.take(4 * (size_t)n_inc),
-                 o_ho = u.take(4 * (size_t)n), o_poff = u.take(8 * (size_t)(n + 1)), o_pat = u.take(4 * (size_t)n_pat),
-                 o_stat = u.take(32), o_ctr = u.take(sizeof(u64) * kQShards * kQStride),
-                 o_ovfn = u.take(8);   // the overflow claim counter
-    char* h = (char*)g->pinned_buf(u.off);
-    // status: [0] invalid query, [1] unsupported query, [2] general path needed, [3] chunks needed
-    // beyond the chunk area, [4] chunked queries (claim counter)
-    const int32_t st0[8] = {INT32_MAX, INT32_MAX, 0, 0, 0, 0, 0, 0};
-    std::memcpy(h + o_stat, st0, 32);
-    std::memset(h + o_ctr, 0, sizeof(u64) * kQShards * kQStride + 8);
-    std::memcpy(h + o_type, type, 4 * (size_t)n);
-    std::memcpy(h + o_ioff, inc_off, 8 * (size_t)(n + 1));
-    if (n_inc) std::memcpy(h + o_inc, inc, 4 * (size_t)n_inc);
-    std::memcpy(h + o_ho, has_ordered, 4 * (size_t)n);
-    std::memcpy(h + o_poff, pat_off, 8 * (size_t)(n + 1));
-    if (n_pat) std::memcpy(h + o_pat, pat, 4 * (size_t)n_pat);
-    Scratch sc{g, {}};
-    char* d = (char*)sc.take(u.off);
-    int64_t* counts = (int64_t*)sc.take(sizeof(int64_t) * (size_t)n);
-    int32_t* slots = (int32_t*)sc.take(sizeof(int32_t) * (size_t)n * kFusedHold);
-    int64_t* ovf_pos = (int64_t*)sc.take(sizeof(int64_t) * (size_t)n);
-    BigQ* big = (BigQ*)sc.take(sizeof(BigQ) * kMaxBig);
-    int32_t* big_n = (int32_t*)(d + o_stat) + 4;
-    int64_t* ovf_claim = (int64_t*)(d + o_ovfn);   // zeroed by the upload
-    Events ev;
-    ev.init(g);
-    ev.rec(0, s);
-    HGX_HIP(hipMemcpyAsync(d, h, u.off, hipMemcpyHostToDevice, s));
-    for (int attempt = 0;; ++attempt) {
-        const int64_t cap = std::max<int64_t>(g->q_hits_guess, 4096);
-        const int64_t ovf_cap = std::max<int64_t>(g->q_ovf_guess, 1 << 16);
-        const int32_t chunk_cap = (int32_t)std::max<int64_t>(g->q_chunk_guess, 1024);
-        Scratch w{g, {}};
-        int32_t* ovf = (int32_t*)w.take(sizeof(int32_t) * (size_t)ovf_cap);
-        int32_t* big_hits = (int32_t*)w.take(sizeof(int32_t) * (size_t)chunk_cap * kInline);
-        int32_t* chunk_cnt = (int32_t*)w.take(sizeof(int32_t) * (size_t)chunk_cap);
-        const size_t m_off = (sizeof(FusedHead) + 15) & ~(size_t)15;
-        const size_t m_ids = m_off + ((8 * (size_t)(n + 1) + 15) & ~(size_t)15);
-        // result area on the device, copied back in one piece with as many ids as recent batches
-        // needed (the kernel writing small host-mapped words one by one over PCIe was slower)
-        char* dm = (char*)w.take(m_ids + 4 * (size_t)cap);
-        char* hm = (char*)g->mapped_buf(m_ids + 4 * (size_t)cap);
-        const int64_t guess = std::min<int64_t>(cap, std::max<int64_t>(g->q_hits_guess, 1024));
-        if (attempt > 0)   // fresh status and counter words
-            HGX_HIP(hipMemcpyAsync(d + o_stat, h + o_stat, o_ovfn + 8 - o_stat, hipMemcpyHostToDevice, s));
-        ev.rec(1, s);
-        hgx_q_fused<<<(unsigned)ceil_div(n, 4), 256, 0, s>>>(
-            n, g->A, (const int32_t*)(d + o_type), (const int64_t*)(d + o_ioff), (const int32_t*)(d + o_inc),
-            (const int32_t*)(d + o_ho), (const int64_t*)(d + o_poff), (const int32_t*)(d + o_pat), g->inc_off,
-            g->inc_row, g->inc_ts_type, g->inc_ts_row, g->tgt_off, g->tgt_idx, g->link_atom, (int32_t*)(d + o_stat),
-            (u64*)(d + o_ctr), counts, slots, ovf_pos, ovf_claim, ovf, ovf_cap, big, big_n);
-        HGX_CHECK_LAUNCH();
-        hgx_q_fused_big<<<512, 256, 0, s>>>(big, big_n, g->inc_row, g->inc_ts_row, (const int32_t*)(d + o_type),
-                                            g->tgt_off, g->tgt_idx, g->link_atom, counts, big_hits, chunk_cnt, chunk_cap,
-                                            (int32_t*)(d + o_stat), (u64*)(d + o_ctr));
-        HGX_CHECK_LAUNCH();
-        ev.rec(2, s);
-        hgx_q_fused_out<<<1, kScanBlock, 0, s>>>(n, counts, slots, ovf_pos, ovf_claim, ovf, ovf_cap, big, big_n,
-                                                 big_hits, chunk_cnt, (const int32_t*)(d + o_stat),
-                                                 (const u64*)(d + o_ctr), (FusedHead*)dm, (int64_t*)(dm + m_off),
-                                                 (int32_t*)(dm + m_ids), cap);
-        HGX_CHECK_LAUNCH();
-        HGX_HIP(hipMemcpyAsync(hm, dm, m_ids + 4 * (size_t)guess, hipMemcpyDeviceToHost, s));
-        ev.rec(3, s);
-        HGX_HIP(hipStreamSynchronize(s));
-        const FusedHead* hd = (const FusedHead*)hm;
-        if (hd->err[0] < n) fail(HGX_E_INVALID, "hgx_pattern_batch: bad query " + std::to_string(hd->err[0]));
-        if (hd->err[1] < n)
-            fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: query " + std::to_string(hd->err[1]) +
-                                        " is not accelerated (no incidence anchor or condition limits)");
-        if (hd->err[2]) return false;
-        const int64_t total = hd->total;
-        if (total > cap || hd->ovf || hd->chunk_need > 0) {   // an area was too small: grow it and run again
-            // (a chunk-area overflow leaves the chunked queries' hits out of the total, so growing the
-            // chunk area can take one more round to size the result area)
-            if (attempt > 1) fail(HGX_E_DEVICE, "hgx_pattern_batch: result sizing failed");
-            g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
-            g->q_ovf_guess = std::max<int64_t>(g->q_ovf_guess, hd->ovf_need + hd->ovf_need / 4);
-            g->q_chunk_guess = std::max<int64_t>(g->q_chunk_guess, (int64_t)hd->chunk_need + hd->chunk_need / 4);
-            continue;
-        }
-        if (total > guess) {
-            HGX_HIP(hipMemcpyAsync(hm + m_ids + 4 * (size_t)guess, dm + m_ids + 4 * (size_t)guess,
-                                   4 * (size_t)(total - guess), hipMemcpyDeviceToHost, s));
-            HGX_HIP(hipStreamSynchronize(s));
-        }
-        g->q_hits_guess = std::max<int64_t>(g->q_hits_guess, total + total / 4);
-        const int64_t* qoff = (const int64_t*)(hm + m_off);
-        const int32_t* ids = (const int32_t*)(hm + m_ids);
-        std::memcpy(r->offsets.data(), qoff, sizeof(int64_t) * (n + 1));
-        r->ids.assign(ids, ids + total);
-        if (prof)
-            std::fprintf(stderr, "[hgx query] fused n=%d host+device %.3f ms (candidates %llu, hits %lld)\n", n,
-                         now_ms() - t0, (unsigned long long)hd->ctr[qCand], (long long)total);
-        if (ev.on) {
-            float a = 0, b = 0;
-            HGX_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[3]));
-            HGX_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
-            r->ms_total = a;
-            r->ms_match = b;
-        }
-        // algorithmic bytes of hgx_q_fused: per query its fields (4 + 16 + 4 + 16 B), its anchor /
-        // pattern entries and 16 B of incidence bounds per entry (an upper bound of the distinct
-        // anchors), 4 B per type-slice probe; per candidate its link row, tgt_off pair and target row;
-        // per hit the link atom read and the id written; the per-query count
-        r->bytes_match = 40.0 * n + 20.0 * (double)(n_inc + n_pat) + 4.0 * (double)hd->ctr[qProbe] +
-                         20.0 * (double)hd->ctr[qCand] + 4.0 * (double)hd->ctr[qArity] + 8.0 * (double)hd->ctr[qHits] +
-                         8.0 * n;
-        return true;
-    }
-}
 
 template <class FrontFn>
 int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front, hgx_query_result* into = nullptr) {
@@ -3208,7 +1707,7 @@ int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn fron
     }
     r->n = n;
     // the single-pass back end writes caller buffers directly; the other back ends fill the vectors
-    if (!r->ext_off || g->q_flat != 2) r->offsets.assign(n + 1, 0);
+    if (!r->ext_off) r->offsets.assign(n + 1, 0);
     if (n > 0) {
         std::lock_guard<std::mutex> lk(g->mu);
         HGX_HIP(hipSetDevice(g->device));
@@ -3334,7 +1833,7 @@ void serve_group(hgx_graph* g, const std::vector<PackedReq*>& grp) {
 
 int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
                      const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat, hgx_query_result** out) {
-    if (n <= 0 || !g->q_coalesce || g->q_fused || g->shard)
+    if (n <= 0 || !g->q_coalesce || g->shard)
         return run_batch_packed_direct(g, n, type, inc_off, inc, has_ordered, pat_off, pat, out);
     PackedReq me;
     me.n = n;
@@ -3412,26 +1911,6 @@ int run_batch_packed(hgx_graph* g, int32_t n, const int32_t* type, const int64_t
 int run_batch_packed_direct(hgx_graph* g, int32_t n, const int32_t* type, const int64_t* inc_off, const int32_t* inc,
                             const int32_t* has_ordered, const int64_t* pat_off, const int32_t* pat,
                             hgx_query_result** out) {
-    if (n > 0 && n <= kFusedMax && g->q_fused && !g->shard) {
-        HGX_API_BEGIN
-        const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
-        const double t0 = now_ms();
-        std::unique_ptr<hgx_query_result> r(new hgx_query_result());
-        r->n = n;
-        r->offsets.assign(n + 1, 0);
-        bool done;
-        {
-            std::lock_guard<std::mutex> lk(g->mu);
-            HGX_HIP(hipSetDevice(g->device));
-            ensure_type_grouped(g);
-            done = run_fused_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, r.get(), prof, t0);
-        }
-        if (done) {
-            *out = r.release();
-            return HGX_OK;
-        }
-        HGX_API_END_NORETURN
-    }
     return run_batch_with(g, n, out, [&](Scratch& sc, Events& ev, Front& f) {
         front_packed(g, n, type, inc_off, inc, has_ordered, pat_off, pat, sc, ev, f);
     });
@@ -3527,14 +2006,8 @@ int hgx_pattern_batch_set(hgx_graph* g, const hgx_query_set* qs, hgx_query_resul
     l.o_poff = qs->o_poff; l.o_pat = qs->o_pat; l.o_err = qs->o_err; l.bytes = qs->bytes;
     l.n_inc = qs->n_inc; l.n_pat = qs->n_pat;
     return run_batch_with(g, qs->n, out, [&](Scratch& sc, Events& ev, Front& f) {
-        const bool sp = g->q_flat == 2;
         ev.rec(0, g->stream);
-        if (!sp) {   // the legacy front kernel reports into the set's error slot: reset it
-            int32_t* none = (int32_t*)g->pinned_buf(8);
-            none[0] = none[1] = INT32_MAX;
-            HGX_HIP(hipMemcpyAsync(qs->dev + l.o_err, none, 8, hipMemcpyHostToDevice, g->stream));
-        }
-        front_device(g, qs->n, l, qs->dev, sp, sc, ev, f);
+        front_device(g, qs->n, l, qs->dev, sc, ev, f);
     });
     HGX_API_END
 }
@@ -3562,22 +2035,11 @@ int hgx_pattern_batch_set_into(hgx_graph* g, const hgx_query_set* qs, int64_t* o
     const int rc = run_batch_with(
         g, qs->n, nullptr,
         [&](Scratch& sc, Events& ev, Front& f) {
-            const bool sp = g->q_flat == 2;
             ev.rec(0, g->stream);
-            if (!sp) {
-                int32_t* none = (int32_t*)g->pinned_buf(8);
-                none[0] = none[1] = INT32_MAX;
-                HGX_HIP(hipMemcpyAsync(qs->dev + l.o_err, none, 8, hipMemcpyHostToDevice, g->stream));
-            }
-            front_device(g, qs->n, l, qs->dev, sp, sc, ev, f);
+            front_device(g, qs->n, l, qs->dev, sc, ev, f);
         },
         &r);
     if (rc != HGX_OK) return rc;
-    if (g->q_flat != 2) {   // the other back ends filled the vectors
-        std::memcpy(offsets, r.offsets.data(), sizeof(int64_t) * r.offsets.size());
-        r.n_hits = (int64_t)r.ids.size();
-        if (r.n_hits <= ids_cap && r.n_hits > 0) std::memcpy(ids, r.ids.data(), sizeof(int32_t) * r.n_hits);
-    }
     *n_ids = r.n_hits;
     if (timing) {
         timing[0] = r.ms_total;

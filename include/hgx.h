@@ -356,9 +356,9 @@ int  hgx_pattern_batch_packed(hgx_graph *g, int32_t n, const int32_t *type, cons
  * set of compiled queries (the reference compiles a query once and executes it repeatedly,
  * TC/query/QueryCompilation.java:76-122), and the bench's config-3 step with its inputs resident in
  * HBM.  The set belongs to the device of g; it may be run on any graph or execution context of that
- * device.  Results as hgx_pattern_batch.  With HGX_OPT_QUERY_FLAT 0 or 1 (A/B paths) the set's error slot
- * lives in the set itself, so one set must not run on two graphs / contexts at the same time there;
- * the default single-pass path (2) keeps every per-run word in the running graph's scratch. */
+ * device.  Results as hgx_pattern_batch.  Every per-run word lives in the running graph's scratch, so one
+ * set may run on several graphs / contexts at the same time (round 5: the A/B paths that kept an error
+ * slot in the set itself are gone). */
 typedef struct hgx_query_set hgx_query_set;
 int  hgx_query_set_create(hgx_graph *g, int32_t n, const int32_t *type, const int64_t *inc_off, const int32_t *inc,
                           const int32_t *has_ordered, const int64_t *pat_off, const int32_t *pat,
@@ -443,36 +443,32 @@ void hgx_shard_free(hgx_shard *s);
  * device work one part at a time (clean per-part device times for a one-GPU rehearsal). */
 int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out);
 #define HGX_OPT_PART_SERIAL 4
-/* HGX_OPT_QUERY_FUSED (A/B, default 0): 1 = hgx_pattern_batch_packed runs batches of <= 16384
- * queries in three fused launches (a wavefront per query expands, plans and matches; a chunk kernel
- * takes queries above 256 candidates; one workgroup places the hits).  Measured slower than the
- * general path on config 3 (0.318 vs 0.211 ms wall, profiles/r02v_pattern_ab.log), kept for A/B. */
+/* HGX_OPT_QUERY_FUSED: removed in round 5.  The fused small-batch path (a wavefront per query expands,
+ * plans and matches; three launches) measured slower than the general path on config 3 (0.318 vs 0.211 ms
+ * wall, profiles/r02v_pattern_ab.log).  hgx_set_option accepts 0 only (HGX_E_UNSUPPORTED otherwise). */
 #define HGX_OPT_QUERY_FUSED 5
 /* HGX_OPT_QUERY_INLINE (default 1): the type-grouped incidence index carries each link's <= 8
  * targets inline (32 bytes per incidence entry, built with the index on the first pattern query),
  * so a typed candidate is one streamed record instead of two dependent random rows.  0 = read the
  * target rows through tgt_off (A/B; also what a snapshot too large for the extra bytes gets). */
 #define HGX_OPT_QUERY_INLINE 6
-/* HGX_OPT_PUSH_BATCH (default 0, 0..64; K above 16 runs as 16): K > 0 = frontier-push levels give
- * each wavefront K frontier atoms at once and spread their incidence entries over its lanes (A/B,
- * config 5 wall ms per direction subsumed / subsumes, profiles/r02zg_c5_push_ab.jsonl: K = 4, 8, 16
- * 1.68 / 2.15, 1.65 / 2.17, 1.67 / 2.48 against 1.71 / 2.05 with one wavefront per atom -- 2-4%
- * faster on subsumed, 5-21% slower on subsumes, slower on the sum; the default stays 0). */
+/* HGX_OPT_PUSH_BATCH: removed in round 5.  K > 0 gave each wavefront of a frontier-push level K atoms
+ * at once; config 5 wall ms per direction subsumed / subsumes (profiles/r02zg_c5_push_ab.jsonl): K = 4,
+ * 8, 16 1.68 / 2.15, 1.65 / 2.17, 1.67 / 2.48 against 1.71 / 2.05 with one wavefront per atom -- slower
+ * on the sum.  hgx_set_option accepts 0 only (HGX_E_UNSUPPORTED otherwise). */
 #define HGX_OPT_PUSH_BATCH 7
 /* HGX_OPT_PART_EXCHANGE (partition shards; every part of a group must use the same value -- the
  * partitioned BFS checks it collectively before any exchange and fails with HGX_E_INVALID on every
- * part when they differ):
- * 1 = compressed records (default); 2 = static slots (every ghost's whole row to a fixed slot of its
- * owner, the owner's final row back); 0 = per level, the format a sampled density estimate says moves
- * fewer bytes.  A/B on full config 4 at 8 parts: 34.0 / 42.8 / 35.5 ms per part a step
- * (profiles/r02ze_part_c4x1.json) -- the static kernels touch every ghost and owned atom. */
+ * part when they differ): 0 or 1 = compressed records (the only format since round 5).  2 = static
+ * slots (every ghost's whole row to a fixed slot of its owner) was removed: 42.8 against 34.0 ms per
+ * part a step on full config 4 at 8 parts (profiles/r02ze_part_c4x1.json); HGX_E_UNSUPPORTED. */
 #define HGX_OPT_PART_EXCHANGE 8
-/* HGX_OPT_QUERY_FLAT (default 2): pattern batches match over the batch's flat candidate space, a
- * wavefront per 64 candidates and a lane per candidate whatever query it belongs to.  2 = single pass:
- * two kernels per batch (normalise + plan + candidate scan with a decoupled look-back; match + hit
- * offsets with a decoupled look-back + result placement); 1 = the same match with a separate
- * single-workgroup scan, finish and scatter (A/B); 0 = a wavefront per chunk of one query's
- * candidates (A/B). */
+/* HGX_OPT_QUERY_FLAT (2, the only value since round 5): pattern batches match over the batch's flat
+ * candidate space, a wavefront per 64 candidates and a lane per candidate whatever query it belongs
+ * to, in a single pass: two kernels per batch (normalise + plan + candidate scan with a decoupled
+ * look-back; match + hit offsets with a decoupled look-back + result placement).  The A/B back ends 1
+ * (separate single-workgroup scan, finish and scatter) and 0 (a wavefront per chunk of one query's
+ * candidates) measured slower and were removed; they return HGX_E_UNSUPPORTED. */
 #define HGX_OPT_QUERY_FLAT 9
 /* HGX_OPT_CODED: removed in round 5.  Coded dense levels (rows of <= 6 source bits as 64-bit codes) were
  * exact but measured slower on config 2's level 1 (16.0 vs 9.0 ms, profiles/r02zn_*_c2_levels.log;

@@ -298,14 +298,12 @@ def _same(r1, r2, n):
         assert r1[q].tolist() == r2[q].tolist(), q
 
 
-def test_fused_packed_path_vs_general_and_oracle():
-    """Batches of <= 16384 packed queries run in one fused launch (a wave per query, look-back output
-    offsets).  Against the general five-launch path (HGX_OPT_QUERY_FUSED = 0) and the oracle: typed
-    orderedLink queries, untyped multi-anchor queries with repeated anchors, hub anchors with
-    thousands of hits (the second match pass and the result-area growth), empty orderedLinks (NOP),
-    several batches in a row (look-back epochs), and a batch with a 70-entry anchor list (the
-    fused kernel hands the batch to the general path)."""
-    from hypergraphdb_amd import _lib, synth
+def test_packed_batches_vs_oracle_and_removed_fused_path():
+    """Packed batches against the oracle: typed orderedLink queries, untyped multi-anchor queries with
+    repeated anchors, hub anchors with thousands of hits (result-area growth), empty orderedLinks
+    (NOP), several batches in a row, and a batch with a 70-entry anchor list.  The fused small-batch
+    path (HGX_OPT_QUERY_FUSED 1, measured slower) was removed in round 5: only 0 is accepted."""
+    from hypergraphdb_amd import HGXError, _lib, synth
     from hypergraphdb_amd.query import pattern_batch_arrays
     g = synth.config3(scale=0.01, n_queries=6000)
     snap, orc = snapshot(g), oracle(g)
@@ -326,26 +324,22 @@ def test_fused_packed_path_vs_general_and_oracle():
         else:
             qs.append((-1, [hubs[(i // 10) % 4]], (int(Q["x"][i]),)))
     arrs = _packed(qs)
-    for rep in range(2):
-        snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
-        fused = pattern_batch_arrays(snap, *arrs)
-        snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 0)
-        general = pattern_batch_arrays(snap, *arrs)
-        _same(fused, general, len(qs))
-    assert max(len(fused[q]) for q in range(len(qs))) > 64
+    first = pattern_batch_arrays(snap, *arrs)
+    again = pattern_batch_arrays(snap, *arrs)
+    _same(first, again, len(qs))
+    assert max(len(first[q]) for q in range(len(qs))) > 64
     for q in rng.choice(len(qs), 600, replace=False):
         t, inc, pat = qs[q]
-        assert fused[q].tolist() == orc.and_query(t, inc, pat).tolist(), qs[q]
-    # a 70-entry anchor list: the whole batch goes to the general path, same results
+        assert first[q].tolist() == orc.and_query(t, inc, pat).tolist(), qs[q]
     long_q = (-1, [int(Q["a"][0])] * 70, None)
-    arrs2 = _packed(qs[:100] + [long_q])
-    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
-    r1 = pattern_batch_arrays(snap, *arrs2)
-    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 0)
-    r2 = pattern_batch_arrays(snap, *arrs2)
-    _same(r1, r2, 101)
+    r1 = pattern_batch_arrays(snap, *_packed(qs[:100] + [long_q]))
+    for q in range(100):
+        assert r1[q].tolist() == first[q].tolist(), q
     assert r1[100].tolist() == orc.and_query(-1, [int(Q["a"][0])], None).tolist()
-    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
+    snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 0)
+    with pytest.raises(HGXError) as ei:
+        snap.set_option(_lib.HGX_OPT_QUERY_FUSED, 1)
+    assert ei.value.code == _lib.HGX_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("case", range(2))
@@ -388,13 +382,13 @@ def test_inline_records_vs_tgt_rows_and_oracle(case):
             assert r[q].tolist() == plain_exp[q], (inline, plain[q])
 
 
-def test_flat_and_chunked_match_paths():
-    """HGX_OPT_QUERY_FLAT: the single-pass pipeline (2: front-scan and match kernels with decoupled
-    look-backs), the flat match (a lane per candidate over the batch's candidate space,
-    per-chunk hit masks for the query offsets) and the per-query chunks give the oracle's results:
-    batches with long runs of queries without candidates (a chunk window of more than 64 queries),
-    empty orderedLinks, untyped and typed queries, and a batch above 16384 queries (device scans)."""
-    from hypergraphdb_amd import _lib, pattern_batch
+def test_single_pass_match_vs_oracle():
+    """The single-pass pipeline (front-scan and match kernels with decoupled look-backs) gives the
+    oracle's results: batches with long runs of queries without candidates (a chunk window of more
+    than 64 queries), empty orderedLinks, untyped and typed queries, and a batch above 16384 queries.
+    HGX_OPT_QUERY_FLAT 0 / 1 (the per-query chunks and the separate-scan flat back end, measured
+    slower) were removed in round 5 and are refused."""
+    from hypergraphdb_amd import HGXError, _lib, pattern_batch
     rng = np.random.default_rng(1700)
     g = K.random_graph(rng, 400, 4000, max_arity=8, n_types=3, link_targets=True)
     snap, orc = snapshot(g), oracle(g)
@@ -414,18 +408,21 @@ def test_flat_and_chunked_match_paths():
     for lo, hi in ((0, 3000), (3000, 3300), (0, 20000)):
         sub = qs[lo:hi]
         exp = [orc.and_query(t, i, p).tolist() for t, i, p in sub]
-        for flat in (2, 1, 0):
+        r = pattern_batch(snap, sub)
+        for q in range(len(sub)):
+            assert r[q].tolist() == exp[q], (lo + q, sub[q])
+    for flat in (0, 1):
+        with pytest.raises(HGXError) as ei:
             snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
-            r = pattern_batch(snap, sub)
-            for q in range(len(sub)):
-                assert r[q].tolist() == exp[q], (flat, lo + q, sub[q])
+        assert ei.value.code == _lib.HGX_E_UNSUPPORTED
+    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
 
 
 def test_single_pass_packed_batches_all_sizes():
     """The single-pass pipeline on the packed entry (device normalisation in the front-scan kernel):
     batch sizes 1..70000 (1 to 274 front blocks; chunk counts from 0 to thousands, so both look-backs
     run across many predecessors), batches whose queries all have no candidate, the workspace-growth
-    re-run, and the same results as the flat (1) and per-query (0) paths."""
+    re-run, and the same results when the batch runs again."""
     from hypergraphdb_amd import _lib
     from hypergraphdb_amd.query import pattern_batch_arrays
     rng = np.random.default_rng(1900)
@@ -454,8 +451,7 @@ def test_single_pass_packed_batches_all_sizes():
     for n in (1, 2, 63, 255, 256, 257, 1000, 5000, 70000):
         b = batch(n)
         ref = None
-        for flat in (2, 1, 0):
-            snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
+        for rep in range(2):
             r = pattern_batch_arrays(snap, *b)
             if ref is None:
                 ref = r
@@ -465,8 +461,7 @@ def test_single_pass_packed_batches_all_sizes():
                         e = orc.and_query(int(b[0][q]), [int(b[2][q])], p)
                         assert r.ids[r.offsets[q]:r.offsets[q + 1]].tolist() == e.tolist(), (n, q)
             else:
-                assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), (n, flat)
-    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
+                assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), n
     # every query without candidates (isolated anchors): zero chunks, all offsets 0
     isolated = np.array([a for a in range(A) if orc.and_query(-1, [a], None).size == 0][:50], np.int32)
     n = len(isolated)
@@ -496,9 +491,8 @@ def test_query_set_resident_batches():
                                                 (int(Q["x"][q]), -1, int(Q["y"][q]))).tolist()
     qs = QuerySet(snap, *packed)
     ctx = snap.context()
-    for flat in (2, 1, 0):
+    for flat in (2,):
         for target in (snap, ctx):
-            target.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
             for _ in range(2):
                 r = qs.run(target)
                 assert np.array_equal(r.offsets, ref.offsets) and np.array_equal(r.ids, ref.ids), (flat, target is ctx)
@@ -569,12 +563,7 @@ def test_placement_query_ranges_at_block_starts():
     n = len(anchors)
     b = (np.full(n, -1, np.int32), np.arange(n + 1, dtype=np.int64), np.array(anchors, np.int32),
          np.zeros(n, np.int32), np.zeros(n + 1, np.int64), np.zeros(0, np.int32))
-    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
     r2 = pattern_batch_arrays(snap, *b)
-    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 1)
-    r1 = pattern_batch_arrays(snap, *b)
-    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
-    assert np.array_equal(r2.offsets, r1.offsets) and np.array_equal(r2.ids, r1.ids)
     cache = {}
     for q, a in enumerate(anchors):
         if a not in cache:
@@ -591,8 +580,8 @@ def test_placement_query_ranges_at_block_starts():
 def test_large_candidate_batch_placement_prefix():
     """A batch whose candidate space spans more than 256 placement blocks (> 16384 chunks of 64
     candidates) takes the scanned block prefix in the placement (hgx_q_place_bsum / _bscan) instead of
-    every block summing all chunks before it (quadratic); results equal the flat path's (1)
-    and the oracle's for a sample, and the timing of both paths is printed for the crossover."""
+    every block summing all chunks before it (quadratic); results equal the oracle's for a
+    sample and a second run's."""
     import time
     from hypergraphdb_amd import _lib
     from hypergraphdb_amd.query import pattern_batch_arrays
@@ -608,16 +597,10 @@ def test_large_candidate_batch_placement_prefix():
     args = (types, np.arange(nq + 1, dtype=np.int64), anchors, np.zeros(nq, np.int32),
             np.zeros(nq + 1, np.int64), np.zeros(0, np.int32))
     assert int(sum(deg[anchors])) > 64 * 64 * 260   # > 260 placement blocks of candidates
-    out = {}
-    for flat in (2, 1):
-        snap.set_option(_lib.HGX_OPT_QUERY_FLAT, flat)
-        pattern_batch_arrays(snap, *args)
-        t0 = time.perf_counter()
-        r = pattern_batch_arrays(snap, *args)
-        out[flat] = (r, time.perf_counter() - t0)
-    snap.set_option(_lib.HGX_OPT_QUERY_FLAT, 2)
-    print(f"large batch: single-pass {out[2][1] * 1e3:.3f} ms, flat {out[1][1] * 1e3:.3f} ms")
-    a, b = out[2][0], out[1][0]
+    b = pattern_batch_arrays(snap, *args)
+    t0 = time.perf_counter()
+    a = pattern_batch_arrays(snap, *args)
+    print(f"large batch: single-pass {(time.perf_counter() - t0) * 1e3:.3f} ms")
     assert np.array_equal(a.offsets, b.offsets) and np.array_equal(a.ids, b.ids)
     for q in range(0, nq, 97):
         assert a[q].tolist() == orc.and_query(int(types[q]), [int(anchors[q])], None).tolist(), q

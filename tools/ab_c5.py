@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--flags", default="0x3BE")
     ap.add_argument("--sources", type=int, default=1024)
-    ap.add_argument("--push", default="0", help="HGX_OPT_PUSH_BATCH values (0 = one wavefront per atom)")
+    ap.add_argument("--push", default="0", help="HGX_OPT_PUSH_BATCH values (only 0 remains: one wavefront per atom)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, synth

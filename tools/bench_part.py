@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--sync-us", type=float, default=40.0, help="price of one host round trip of the exchange")
     ap.add_argument("--xmode", type=int, nargs="+", default=[0],
-                    help="HGX_OPT_PART_EXCHANGE values to measure at NP > 1 (0 auto, 1 records, 2 static slots)")
+                    help="HGX_OPT_PART_EXCHANGE values to measure at NP > 1 (0 / 1 records; the static slots (2) were removed)")
     args = ap.parse_args()
     from hypergraphdb_amd import _lib, synth
     from hypergraphdb_amd.partition import Shard, ShardSnapshot, partition_plan, pbfs_batch_group
