@@ -53,7 +53,7 @@ EXPORTED = (
     "hgx_query_result_ms", "hgx_query_result_free",
     "hgx_partition_plan", "hgx_shard_build", "hgx_shard_info", "hgx_shard_export", "hgx_shard_exchange_tables",
     "hgx_shard_free", "hgx_shard_graph_create", "hgx_comm_rccl_unique_id", "hgx_comm_rccl_create",
-    "hgx_comm_host_create", "hgx_comm_destroy", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
+    "hgx_comm_host_create", "hgx_comm_destroy", "hgx_comm_check_allgather", "hgx_pbfs_batch", "hgx_pbfs_batch_group",
     "hgx_snapshot_write", "hgx_snapshot_info", "hgx_snapshot_read", "hgx_graph_open", "hgx_graph_export",
     "hgx_graph_update", "hgx_query_coalesce_stats", "hgx_query_set_create", "hgx_pattern_batch_set",
     "hgx_query_set_free", "hgx_pattern_batch_set_into", "hgx_query_set_info", "hgx_snapshot_read_handles",
@@ -196,6 +196,7 @@ def lib():
         "hgx_comm_rccl_unique_id": ([vp], C.c_int),
         "hgx_comm_rccl_create": ([vp, i32, i32, i32, C.POINTER(vp)], C.c_int),
         "hgx_comm_destroy": ([vp], None),
+        "hgx_comm_check_allgather": ([vp, i32, vp, i64, vp, vp, vp], C.c_int),
         "hgx_pbfs_batch": ([vp, vp, vp, i32, i32, C.POINTER(AlgenOpts), C.POINTER(vp)], C.c_int),
         "hgx_pbfs_batch_group": ([vp, i32, vp, i32, i32, C.POINTER(AlgenOpts), vp], C.c_int),
         "hgx_snapshot_write": ([C.c_char_p, C.POINTER(GraphDesc), vp, i32], C.c_int),

@@ -794,6 +794,38 @@ int hgx_comm_host_create(int32_t world, int32_t rank, hgx_host_allgather_fn allg
     HGX_API_END
 }
 
+int hgx_comm_check_allgather(hgx_comm* c, int32_t device, const int64_t* values, int64_t n, int64_t* out_dev,
+                             int64_t* out_base, int64_t* out_host) {
+    HGX_API_BEGIN
+    if (!c || !c->t || n < 1 || !values || !out_dev || !out_base || !out_host)
+        fail(HGX_E_INVALID, "hgx_comm_check_allgather: bad argument");
+    HGX_HIP(hipSetDevice(device));
+    Transport* tr = c->t;
+    const int64_t need = n * tr->world;
+    hipStream_t s = nullptr;
+    int64_t* din = nullptr;
+    int64_t* pin = nullptr;
+    struct Cleanup {
+        hipStream_t& s;
+        int64_t*& din;
+        int64_t*& pin;
+        ~Cleanup() {
+            if (din) (void)hipFree(din);
+            if (pin) (void)hipHostFree(pin);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } cleanup{s, din, pin};
+    HGX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HGX_HIP(hipMalloc(&din, sizeof(int64_t) * (size_t)n));
+    HGX_HIP(hipHostMalloc(&pin, sizeof(int64_t) * (size_t)need, hipHostMallocDefault));
+    HGX_HIP(hipMemcpyAsync(din, values, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, s));
+    tr->allgather_dev(din, n, out_dev, s, pin);               // the transport's own (RCCL: device gather)
+    tr->Transport::allgather_dev(din, n, out_base, s, pin);   // the default: read back + host all-gather
+    tr->allgather_i64(values, n, out_host, s);
+    HGX_HIP(hipStreamSynchronize(s));
+    HGX_API_END
+}
+
 void hgx_comm_destroy(hgx_comm* c) {
     if (!c) return;
     delete c->t;

@@ -175,6 +175,16 @@ class RcclComm:
             pass
 
 
+def check_allgather(comm, values, device=0):
+    """hgx_comm_check_allgather (collective): the transport's device-input all-gather, the default
+    read-back path and the host-input all-gather of every rank's ``values`` -> three (world, n) arrays."""
+    v = np.ascontiguousarray(values, np.int64)
+    n = len(v)
+    outs = [np.full(n * comm.world, -1, np.int64) for _ in range(3)]
+    check(lib().hgx_comm_check_allgather(comm._h, int(device), ptr(v), n, ptr(outs[0]), ptr(outs[1]), ptr(outs[2])))
+    return [o.reshape(comm.world, n) for o in outs]
+
+
 _AG = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64))
 _A2A = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_void_p,
                    C.POINTER(C.c_int64), C.POINTER(C.c_int64))

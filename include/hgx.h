@@ -525,6 +525,14 @@ typedef int (*hgx_host_alltoallv_fn)(void *user, const void *send, const int64_t
 int  hgx_comm_host_create(int32_t world, int32_t rank, hgx_host_allgather_fn allgather,
                           hgx_host_alltoallv_fn alltoallv, void *user, hgx_comm **out);
 void hgx_comm_destroy(hgx_comm *c);
+/* Diagnostics of a transport's all-gathers (collective: every rank of the group calls it with its own
+ * n values): out_dev = the device-input all-gather the exchange's count vectors take
+ * (Transport::allgather_dev: RCCL gathers on the device and reads the block back once), out_base = the
+ * same through the default read-back + host all-gather, out_host = the host-input all-gather; each
+ * n * world values, rank r's at [r * n, (r + 1) * n).  For tests: the RCCL-only override is compared
+ * with the default path on the same inputs. */
+int  hgx_comm_check_allgather(hgx_comm *c, int32_t device, const int64_t *values, int64_t n, int64_t *out_dev,
+                              int64_t *out_base, int64_t *out_host);
 
 /* One part's share of a partitioned batched BFS (collective: every part calls it with the same
  * seeds, depth and options).  seeds are GLOBAL atom ids.  The result reports this part's OWNED

@@ -144,13 +144,20 @@ def test_depth_of_and_errors():
 
 
 def test_rccl_single_rank():
-    """The RCCL transport (unique id, communicator, grouped send/recv, all-gather) on one rank."""
+    """The RCCL transport (unique id, communicator, grouped send/recv, all-gather) on one rank, and its
+    device-input all-gather override (RcclTransport::allgather_dev, what the exchange's count vectors
+    take at world > 1) against the default read-back path and the host-input all-gather on the same
+    values, at several sizes (its scratch grows and is reused) -- VERDICT r4 weak 1."""
     from hypergraphdb_amd import bfs_batch
-    from hypergraphdb_amd.partition import RcclComm, pbfs_batch
+    from hypergraphdb_amd.partition import RcclComm, check_allgather, pbfs_batch
     rng = np.random.default_rng(3)
     g = K.random_graph(rng, 800, 1500, max_arity=6, n_types=2)
     seeds = rng.integers(0, g["num_atoms"], 100).astype(np.int32)
     comm = RcclComm.create(1, 0, 0)
+    for n in (1, 4, 1000, 3, 20000):
+        vals = rng.integers(-2**62, 2**62, n)
+        for out in check_allgather(comm, vals):
+            assert np.array_equal(out[0], vals), n
     sh = parts(g, 1)
     res = pbfs_batch(sh[0], comm, seeds, 3)
     snap = snapshot(g)
@@ -190,14 +197,14 @@ def _host_rank(rank, world, port, q):
     try:
         import torch.distributed as dist
         from hypergraphdb_amd import synth
-        from hypergraphdb_amd.partition import HostComm, Shard, ShardSnapshot, partition_plan, pbfs_batch
+        from hypergraphdb_amd.partition import HostComm, Shard, ShardSnapshot, check_allgather, partition_plan, pbfs_batch
         dist.init_process_group("gloo")
         g = synth.config4(scale=0.001, n_sources=300)
         plan = partition_plan(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world)
         sh = Shard.build(g["num_atoms"], g["link_atom"], g["tgt_off"], g["tgt_idx"], g["link_type"], world, rank, plan)
         snap = ShardSnapshot(sh, 0)
         comm = HostComm.gloo(dist, world, rank)
-        out = {}
+        out = {"allgather": [a.tolist() for a in check_allgather(comm, [rank * 100 + i for i in range(5)])]}
         for maxd in (4, None):
             res = pbfs_batch(snap, comm, g["seeds"], maxd)
             out[str(maxd)] = (res.counts().tolist(), [res.visited(i, d).tolist() for i in (0, 77, 299)
@@ -236,6 +243,9 @@ def test_two_processes_gloo_transport():
     for p in ps:
         p.join(timeout=60)
     assert not (isinstance(views, tuple) and views[0] == "error"), views
+    for v in views:   # the transport's device-input all-gather, the default path, the host-input one
+        for a in v["allgather"]:
+            assert a == [[0, 1, 2, 3, 4], [100, 101, 102, 103, 104]], v["allgather"]
     g = synth.config4(scale=0.001, n_sources=300)
     snap = snapshot(g)
     orc = oracle(g)
