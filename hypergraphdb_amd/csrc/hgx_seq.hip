@@ -29,6 +29,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -62,6 +63,21 @@ int seq_mode(const hgx_algen_opts& o) {
 }
 
 int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+// Host-side phase trace of hgx_bfs_sequence (HGX_SEQ_TRACE=1): microseconds since the call began.
+struct SeqTrace {
+    bool on = std::getenv("HGX_SEQ_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void operator()(const char* what) const {
+        if (on)
+            std::fprintf(stderr, "[hgx seq trace] %-28s %8.1f us\n", what,
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+thread_local SeqTrace* g_seq_trace = nullptr;
+inline void seq_mark(const char* what) {
+    if (g_seq_trace) (*g_seq_trace)(what);
+}
 
 // fn(0 .. n-1) on up to 16 host threads (the job's CPU share; HGX_COPY_THREADS overrides), or on the
 // calling thread when `wide` is false.
@@ -1896,6 +1912,9 @@ constexpr int kLsMaxW = 16;             // row words: chunks of <= 1024 seeds
 constexpr int kLrMaxBucketBits = 18;                            // <= 2^18 keys a bucket (a 32 KB LDS bitmap)
 constexpr int kLrMaxBuckets = 1 << (32 - kLrMaxBucketBits);     // keys < 2^32
 constexpr int kLrG = 512;                                       // blocks of count / scatter / rank
+constexpr int kLrParts = 4;   // rank launches a level (bucket ranges): each part's pairs are copied to the host on
+                              // stream2 while the next parts rank (the host learns the parts' rank ranges from
+                              // the scan's publication)
 
 __device__ __forceinline__ int lr_bucket_bits(int64_t W) {
     const u64 keys = (u64)max<int64_t>(W, 1) * 64ull;
@@ -1944,7 +1963,8 @@ struct LsArgs {
     int32_t* out_link;                  // [cap] pairs, level-major (device)
     int32_t* out_atom;
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
-    u64* hflag;                         // mapped coherent host words: {n, status, seq} x 2 (level parity)
+    u64* hflag;                         // mapped coherent host words: {n, status, seq, -} x 2 (level parity), then
+                                        //   the rank parts' boundaries [2][kLrParts + 1]
     // the yield adjacency (yield_adj; null: the incidence): an item is one (target, link atom) pair,
     // its index the whole stream position (kbits 0)
     const int64_t* y_off;
@@ -2904,19 +2924,22 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
     int64_t n = ls_disc_prefix(a, d, pre);
     if (!status && (n > a.cap || out0 + n > a.cap)) status = 1;   // the pairs outgrow the output
     if (status) n = 0;
+    // two host slots by level parity: the host reads level d while level d+1 may already be publishing
+    // (it never enqueues level d+2 before it has read level d)
+    u64* hf = a.hflag + 4 * (d & 1);
+    auto publish = [&]() {   // thread 0, after every word the host reads with it was stored
+        __hip_atomic_store(hf, (u64)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hf + 1, (u64)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(hf + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
     if (threadIdx.x == 0) {
         if (status) atomicOr((unsigned long long*)&a.ctl[kLsStatus], (unsigned long long)status);
         int64_t* nx = a.ctl + ((d + 1) % kLsSlots) * kLsSlotWords;
         nx[lsF] = n;
         nx[lsOut] = out0 + n;
         sl[lsN] = n;
-        // two host slots by level parity: the host reads level d while level d+1 may already be
-        // publishing (it never enqueues level d+2 before it has read level d)
-        u64* hf = a.hflag + 4 * (d & 1);
-        __hip_atomic_store(hf, (u64)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(hf + 1, (u64)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_store(hf + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (n == 0) publish();
     }
     if (n == 0) return;   // (every thread: n is the block's)
     const int bs = lr_bucket_bits(sl[lsW]);
@@ -2940,15 +2963,29 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
     __syncthreads();
     int64_t run = x - s;
     for (int k = 0; k < w; ++k) run += wsum[k];
+    u64* bnd = a.hflag + 8 + (kLrParts + 1) * (d & 1);   // the rank parts' first ranks (mapped)
+    bool wrote = false;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
         if (b0 + k < nbk) {
             a.bstart[b0 + k] = run;
             a.bcur[b0 + k] = (uint32_t)run;
+            for (int q = 0; q < kLrParts; ++q)
+                if (q * nbk / kLrParts == b0 + k) {
+                    __hip_atomic_store(bnd + q, (u64)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    wrote = true;
+                }
         }
         run += c[k];
     }
-    if (threadIdx.x == 1023) a.bstart[nbk] = run;   // == n
+    if (threadIdx.x == 1023) {
+        a.bstart[nbk] = run;   // == n
+        __hip_atomic_store(bnd + kLrParts, (u64)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        wrote = true;
+    }
+    if (wrote) __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) publish();
 }
 
 __global__ void __launch_bounds__(256) hgx_lr_scatter(LsArgs a, int32_t d) {
@@ -2976,7 +3013,8 @@ __global__ void __launch_bounds__(256) hgx_lr_scatter(LsArgs a, int32_t d) {
     }
 }
 
-__global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d) {
+// Part `part` of kLrParts: the buckets [part * nbk / kLrParts, (part + 1) * nbk / kLrParts).
+__global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t part) {
     __shared__ u64 bm[1 << (kLrMaxBucketBits - 6)];
     __shared__ uint32_t wp[1 << (kLrMaxBucketBits - 6)];
     __shared__ int64_t ws[4];
@@ -2989,7 +3027,8 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d) {
     const int per = (nw + 255) / 256;
     const int nx = (d + 1) & 1;
     const bool last = d + 1 >= a.maxd;
-    for (int b = blockIdx.x; b < nbk; b += gridDim.x) {   // block-uniform
+    const int blo = part * nbk / kLrParts, bhi = (part + 1) * nbk / kLrParts;
+    for (int b = blo + blockIdx.x; b < bhi; b += gridDim.x) {   // block-uniform
         const int64_t s0 = a.bstart[b], s1 = a.bstart[b + 1];
         if (s0 == s1) continue;
         for (int w = threadIdx.x; w < nw; w += 256) bm[w] = 0ull;
@@ -3911,12 +3950,17 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     bool pull_off = false;   // set when a pull pass overflowed its hit list (rows of > 8 targets)
     const int32_t* pin_j = pull ? ensure_pin_j(g) : nullptr;
     hgx_graph* root = g->base ? g->base : g;
-    if (!g->seq_flag) {   // mapped, coherent: the emit kernel's level sizes (once per graph)
+    if (!g->seq_flag) {   // mapped, coherent: the scan kernel's level sizes and rank-part bounds (once per graph)
         void* hp = nullptr;
-        HGX_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(hp, 0, 64);
+        HGX_HIP(hipHostMalloc(&hp, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, 256);
         g->seq_flag = (u64*)hp;
     }
+    static_assert(2 * kLrParts <= 8 && 8 + 2 * (kLrParts + 1) <= 32, "rank-part events / bounds");
+    for (hipEvent_t& e : g->ls_ev)
+        if (!e) HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!g->stream2) HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
+    hipStream_t cs = g->stream2;   // the pairs' copies to the host, a level (part) at a time
     u64* hflag_d = nullptr;
     HGX_HIP(hipHostGetDevicePointer((void**)&hflag_d, g->seq_flag, 0));
     const int64_t full = (int64_t)nb * A;
@@ -4046,8 +4090,48 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             hgx_lr_count<<<kLrG, 256, 0, st>>>(a, d);
             hgx_lr_scan<<<1, 1024, 0, st>>>(a, d, base + (u64)d + 1);
             hgx_lr_scatter<<<lr_scatter_g, 256, 0, st>>>(a, d);
-            hgx_lr_rank<<<lr_rank_g, 256, 0, st>>>(a, d);
+            for (int q = 0; q < kLrParts; ++q) {
+                hgx_lr_rank<<<lr_rank_g, 256, 0, st>>>(a, d, q);
+                HGX_HIP(hipEventRecord(g->ls_ev[kLrParts * (d & 1) + q], st));
+            }
             HGX_CHECK_LAUNCH();
+        };
+        // each level's pairs go to the host on the copy stream as soon as the host has read the level's
+        // size: a host buffer per level, one copy per rank part after that part's event (the last level's
+        // copies overlap its later rank parts and the final runs pass)
+        struct LevelBuf {
+            PoolBuf b;
+            int64_t out0, n;
+        };
+        std::vector<LevelBuf> lbufs;
+        struct GiveBack {   // an attempt that fails returns its level buffers after the copies drained
+            hgx_graph* g;
+            hipStream_t cs;
+            std::vector<LevelBuf>* v;
+            bool keep = false;
+            ~GiveBack() {
+                if (keep || v->empty()) return;
+                (void)hipStreamSynchronize(cs);
+                std::lock_guard<std::mutex> lk(g->seq_mu);
+                for (auto& x : *v) g->seq_hbufs.push_back(x.b);
+            }
+        } give_back{g, cs, &lbufs};
+        auto copy_level = [&](int32_t d, int64_t out0, int64_t n) {
+            PoolBuf hb = take_host_buf(g, 8 * (size_t)n);
+            lbufs.push_back({hb, out0, n});
+            int32_t* hl = (int32_t*)hb.p;
+            int32_t* ha = hl + n;
+            const u64* bnd = g->seq_flag + 8 + (kLrParts + 1) * (d & 1);
+            for (int q = 0; q < kLrParts; ++q) {
+                const int64_t b = (int64_t)bnd[q], e = (int64_t)bnd[q + 1];
+                if (b < 0 || e > n || e < b) fail(HGX_E_DEVICE, "hgx_bfs_sequence: rank-part bounds inconsistent");
+                if (e == b) continue;
+                HGX_HIP(hipStreamWaitEvent(cs, g->ls_ev[kLrParts * (d & 1) + q], 0));
+                HGX_HIP(hipMemcpyAsync(hl + b, a.out_link + out0 + b, sizeof(int32_t) * (size_t)(e - b),
+                                       hipMemcpyDeviceToHost, cs));
+                HGX_HIP(hipMemcpyAsync(ha + b, a.out_atom + out0 + b, sizeof(int32_t) * (size_t)(e - b),
+                                       hipMemcpyDeviceToHost, cs));
+            }
         };
         int64_t total = 0, status = 0;
         int32_t dw = 0, enq = 0;
@@ -4070,6 +4154,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             const int64_t n = (int64_t)__atomic_load_n(hf, __ATOMIC_RELAXED);
             status = (int64_t)__atomic_load_n(hf + 1, __ATOMIC_RELAXED);
             if (status) break;
+            if (n > 0) copy_level(dw, total, n);
             total += n;
             ++dw;
             if (n == 0) break;
@@ -4096,6 +4181,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             continue;   // rerun the chunk with the grown capacities (kept on the graph)
         }
         const int64_t nruns = ctl[kLsRuns];
+        give_back.keep = true;
+        for (auto& x : lbufs) out.bufs.push_back(x.b);
         out.traversed += (double)ctl[kLsTrav];
         out.bytes += (double)ctl[kLsBytes];
         out.pull_levels += ctl[kLsPullN];
@@ -4105,18 +4192,21 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                          ctl[kLsProf] * 1e-5, ctl[kLsProf + 1] * 1e-5, ctl[kLsProf + 2] * 1e-5, ctl[kLsProf + 6] * 1e-5,
                          ctl[kLsProf + 7] * 1e-5, (long long)ctl[kLsProf + 3], (long long)ctl[kLsProf + 4],
                          (long long)ctl[kLsProf + 5]);
-        // [links total][atoms total][pad to 8 bytes][runs 3 x nruns]
-        PoolBuf hb = take_host_buf(g, 8 * (size_t)total + 8 + 24 * (size_t)std::max<int64_t>(nruns, 1));
+        // the runs (3 x nruns); the pairs are in the level buffers once the copy stream drained
+        PoolBuf hb = take_host_buf(g, 24 * (size_t)std::max<int64_t>(nruns, 1));
         out.bufs.push_back(hb);
-        int32_t* hl = (int32_t*)hb.p;
-        int32_t* ha = hl + total;
-        int64_t* hr = (int64_t*)(ha + total + (total & 1));
-        if (total) {
-            HGX_HIP(hipMemcpyAsync(hl, a.out_link, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipMemcpyAsync(ha, a.out_atom, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
-        }
+        int64_t* hr = (int64_t*)hb.p;
         if (nruns) HGX_HIP(hipMemcpyAsync(hr, a.runs, sizeof(int64_t) * 3 * (size_t)nruns, hipMemcpyDeviceToHost, st));
         spin_sync(st);
+        spin_sync(cs);
+        // a pair index -> its level buffer (levels are consecutive ranges of [0, total))
+        auto at_pair = [&](int64_t b, int32_t*& pl, int32_t*& pa) {
+            size_t L = 0;
+            while (L + 1 < lbufs.size() && lbufs[L + 1].out0 <= b) ++L;
+            int32_t* hl = (int32_t*)lbufs[L].b.p;
+            pl = hl + (b - lbufs[L].out0);
+            pa = hl + lbufs[L].n + (b - lbufs[L].out0);
+        };
         // runs partition [0, total) in pair order; each seed's runs in distance order are its pairs
         std::vector<int64_t> ord((size_t)nruns);
         for (int64_t k = 0; k < nruns; ++k) ord[k] = k;
@@ -4140,7 +4230,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             for (auto& dk : per[s]) {
                 const int64_t k = dk.second, b = hr[3 * ord[k] + 2];
                 const int64_t e = k + 1 < nruns ? hr[3 * ord[k + 1] + 2] : total;
-                out.segs[(size_t)(seed0 + s)].push_back({hl + b, ha + b, nullptr, e - b, (int32_t)dk.first});
+                int32_t *pl = nullptr, *pa = nullptr;
+                at_pair(b, pl, pa);
+                out.segs[(size_t)(seed0 + s)].push_back({pl, pa, nullptr, e - b, (int32_t)dk.first});
                 out.deepest = std::max(out.deepest, (int32_t)dk.first);
             }
         }
@@ -4522,7 +4614,9 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         hgx_seq_coop<256><<<(unsigned)nblk, 256, 0, st>>>(a);
         HGX_CHECK_LAUNCH();
         if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
+        seq_mark("grid stage enqueued");
         spin_sync(st);
+        seq_mark("grid stage done");
         struct HostBack {   // the mapped readout goes back to the pool on every path
             hgx_graph* g;
             PoolBuf b;
@@ -4568,6 +4662,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
                                                                    g->co_vis);
         HGX_CHECK_LAUNCH();
         spin_sync(st);
+        seq_mark("grid stage pairs copied");
         // level-major, seed-major inside a level: seed j's pairs of level d follow the earlier seeds' ones
         int64_t o0 = 0;
         for (int32_t d = 0; d < nlev; ++d) {
@@ -4938,6 +5033,11 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         if (seeds[i] < 0 || seeds[i] >= g->A) fail(HGX_E_INVALID, "hgx_bfs_sequence: seed out of range");
     if (max_depth < -1) fail(HGX_E_INVALID, "hgx_bfs_sequence: bad max_depth");
     std::lock_guard<std::mutex> lk(g->mu);
+    SeqTrace trace;
+    g_seq_trace = trace.on ? &trace : nullptr;
+    struct TraceOff {
+        ~TraceOff() { g_seq_trace = nullptr; }
+    } trace_off;
     HGX_HIP(hipSetDevice(g->device));
     hipStream_t st = g->stream;
     const int32_t maxd = max_depth < 0 ? INT32_MAX : max_depth;
@@ -5035,7 +5135,9 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             evb = ev_take(g);
             HGX_HIP(hipEventRecord(evb, st));
         }
+        seq_mark("workgroup stage enqueued");
         spin_sync(st);
+        seq_mark("workgroup stage done");
         if (evb) {
             float ms = 0;
             HGX_HIP(hipEventElapsedTime(&ms, ev0, evb));
@@ -5127,6 +5229,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     r->off.assign((size_t)n_seeds + 1, 0);
     for (int32_t i = 0; i < n_seeds; ++i) r->off[i + 1] = r->off[i] + cnt[i];
     r->n_levels = deepest + 1;
+    seq_mark("call done");
     guard.r = nullptr;
     *out = r;
     HGX_API_END
