@@ -302,7 +302,7 @@ def run_config4(args, ctx, barrier_sync, result):
         "metric": "hyperedge TEPS", "value": edges / dt, "unit": "TEPS", "scaling": "weak",
         "ms_per_step": round(dt / args.steps * 1e3, 3), "workload": wl, "n_gpus": world,
         "parallelism": f"snapshot replicated on {world} GPU(s), {args.sources} sources per GPU",
-        "traversed_edges_per_step": edges / args.steps, "roofline": _kernel_roof(st, "config2")}
+        "traversed_edges_per_step": edges / args.steps, "roofline": _kernel_roof(st, "config4")}
     log(f"rank {rank}: config4 replicated {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step")
     snap.close()
     del snap
@@ -369,7 +369,7 @@ def run_config4(args, ctx, barrier_sync, result):
         "parity_check": ("the last timed step's per-source per-depth counts summed over the parts == the replica's "
                          "counts of the same sources on the whole snapshot (rank 0), and the summed TEPS numerator == "
                          "the replica's; checked after the timed steps"),
-        "rank0_part": info, "roofline": _kernel_roof(st, "config2")}
+        "rank0_part": info, "roofline": _kernel_roof(st, "config4")}
     if not ok:
         result["error"] = "partitioned counts differ from the replica's"
     log(f"rank {rank}: config4 partitioned {edges / dt:.3e} TEPS, {dt / args.steps * 1e3:.1f} ms/step, "
