@@ -1960,8 +1960,8 @@ struct LsArgs {
     int64_t* bstart;                    // [kLrMaxBuckets + 1] their first rank
     u64* bk_v;                          // the discoveries by bucket: value, seed * A + atom
     int64_t* bk_sa;
-    int32_t* out_link;                  // [cap] pairs, level-major (device)
-    int32_t* out_atom;
+    int2* out_pair;                     // [cap] (link atom, atom) pairs, level-major (device)
+    uint32_t* seedcnt;                  // [nb] the level's discoveries per seed (hgx_lr_count; zeroed by the expand)
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
     u64* hflag;                         // mapped coherent host words: {n, status, seq, -} x 2 (level parity), then
                                         //   the rank parts' boundaries [2][kLrParts + 1]
@@ -2171,7 +2171,7 @@ __device__ __forceinline__ void ls_add_bytes(const LsArgs& a, int64_t nbytes, in
     if (threadIdx.x == 0 && t) atomicAdd((unsigned long long*)&a.ctl[kLsBytes], (unsigned long long)t);
 }
 
-__global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_t runs_only) {
+__global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d) {
     __shared__ int64_t ws[4];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
@@ -2179,22 +2179,10 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
     const int64_t F = sl[lsF], out0 = sl[lsOut] - F;
     const int cur = d & 1;
     const int32_t* fa = a.fa[cur];
-    const int32_t* fs = a.fs[cur];
     const int64_t lo = ls_lo(F, blockIdx.x), hi = ls_lo(F, blockIdx.x + 1);
     int64_t sum = 0, trv = 0;
+    (void)out0;   // (the level's runs come from hgx_lr_scan's per-seed counts)
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-        const int32_t s = fs[i];
-        if (d > 0 && (i == 0 || fs[i - 1] != s)) {   // where seed s's pairs of distance d start
-            const int64_t r = atomicAdd((unsigned long long*)&a.ctl[kLsRuns], 1ull);
-            if (r < a.rcap) {
-                a.runs[3 * r] = d;
-                a.runs[3 * r + 1] = s;
-                a.runs[3 * r + 2] = out0 + i;
-            } else {
-                atomicOr((unsigned long long*)&a.ctl[kLsStatus], 2ull);   // more runs than rcap
-            }
-        }
-        if (runs_only) continue;
         const int32_t p = fa[i];
         const int64_t b = a.inc_off[p], e = a.inc_off[p + 1];
         if (a.y_off) {   // items: the adjacency's pairs; the incidence entries count as traversed
@@ -2209,7 +2197,6 @@ __global__ void __launch_bounds__(256) hgx_ls_degree(LsArgs a, int32_t d, int32_
             sum += e - b;
         }
     }
-    if (runs_only) return;
     sum = ls_block_sum(sum, ws);
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = sum;
     if (a.y_off) {
@@ -2311,6 +2298,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     {   // the ranking's bucket counts (hgx_lr_count adds to them)
         const int bs = lr_bucket_bits(W), nbk = lr_buckets(W, bs);
         for (int64_t b = blockIdx.x * 256ll + threadIdx.x; b < nbk; b += (int64_t)gridDim.x * 256) a.bcnt[b] = 0u;
+        for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < a.nb; q += (int64_t)gridDim.x * 256) a.seedcnt[q] = 0u;
     }
     const int lane = threadIdx.x & 63;
     int64_t nbytes = 0;
@@ -2881,12 +2869,14 @@ __global__ void __launch_bounds__(256) hgx_lp_hfinal(LsArgs a, int32_t d) {
 __global__ void __launch_bounds__(256) hgx_lr_count(LsArgs a, int32_t d) {
     __shared__ int64_t pre[kLsDSegs + 2];
     __shared__ uint32_t hist[kLrMaxBuckets];
+    __shared__ uint32_t scnt[kLsMaxW * 64];   // the block's discoveries per seed (the level's runs)
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
     const bool pull = sl[lsPull] != 0;
     const int bs = lr_bucket_bits(sl[lsW]);
     const int nbk = lr_buckets(sl[lsW], bs);
     for (int b = threadIdx.x; b < nbk; b += 256) hist[b] = 0u;
+    for (int q = threadIdx.x; q < a.nb; q += 256) scnt[q] = 0u;
     const int64_t n = ls_disc_prefix(a, d, pre);   // (syncs the block)
     const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
     for (int64_t x = lo + threadIdx.x; x < hi; x += 256) {
@@ -2900,10 +2890,13 @@ __global__ void __launch_bounds__(256) hgx_lr_count(LsArgs a, int32_t d) {
             a.hval[hs] = ~0ull;
         }
         atomicAdd(&hist[((v >> 32) - 1ull) >> bs], 1u);
+        atomicAdd(&scnt[(int)(a.disc[pos] / a.A)], 1u);
     }
     __syncthreads();
     for (int b = threadIdx.x; b < nbk; b += 256)
         if (hist[b]) atomicAdd(&a.bcnt[b], hist[b]);
+    for (int q = threadIdx.x; q < a.nb; q += 256)
+        if (scnt[q]) atomicAdd(&a.seedcnt[q], scnt[q]);
     if (pull) {
         const int64_t nu = sl[lsU];
         for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < nu; u += (int64_t)gridDim.x * 256) {
@@ -2942,6 +2935,42 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
         if (n == 0) publish();
     }
     if (n == 0) return;   // (every thread: n is the block's)
+    {   // the level's runs: seed s's pairs (distance d + 1) start after the earlier seeds' (seed-major ranks)
+        __shared__ int s_ovf;
+        if (threadIdx.x == 0) s_ovf = 0;
+        const int q = threadIdx.x;   // nb <= 1024 seeds, a thread each
+        const int64_t c = q < a.nb ? (int64_t)a.seedcnt[q] : 0;
+        int64_t x = c;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int64_t before = x - c;
+        for (int k = 0; k < w; ++k) before += wsum[k];
+        if (c > 0) {
+            const int64_t r = atomicAdd((unsigned long long*)&a.ctl[kLsRuns], 1ull);
+            if (r < a.rcap) {
+                a.runs[3 * r] = d + 1;
+                a.runs[3 * r + 1] = q;
+                a.runs[3 * r + 2] = out0 + before;
+            } else {
+                atomicOr((unsigned long long*)&a.ctl[kLsStatus], 2ull);   // more runs than rcap
+                s_ovf = 1;
+            }
+        }
+        __syncthreads();   // (wsum is reused below)
+        if (s_ovf) {   // the host grows rcap and reruns the chunk
+            if (threadIdx.x == 0) {
+                status = 2;
+                publish();
+            }
+            return;
+        }
+    }
     const int bs = lr_bucket_bits(sl[lsW]);
     const int nbk = lr_buckets(sl[lsW], bs);
     constexpr int per = kLrMaxBuckets / 1024;
@@ -3055,10 +3084,9 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
             const u64 kk = (v >> 32) - 1ull - kb;
             const int64_t r = s0 + wp[kk >> 6] + __popcll(bm[kk >> 6] & ((1ull << (kk & 63)) - 1ull));
             const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
-            a.out_link[out0 + r] = (int32_t)(uint32_t)v;
-            a.out_atom[out0 + r] = t;
-            a.fs[nx][r] = s;   // (the last level's too: its pairs' runs)
+            a.out_pair[out0 + r] = make_int2((int32_t)(uint32_t)v, t);   // one 8-byte store a pair
             if (!last) {       // the next frontier and the examined bit, unless no level follows
+                a.fs[nx][r] = s;
                 a.fa[nx][r] = t;
                 atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
             }
@@ -3654,7 +3682,30 @@ struct Seg {
     const int32_t *link, *atom, *dist;
     int64_t n;
     int32_t dist_c;
+    int32_t stride = 1;   // 2: link / atom interleaved (the level engine's (link, atom) pairs)
 };
+
+// n pairs of a segment from index so on into links / atoms (either may be null): two copies, or one pass
+// over interleaved (link, atom) pairs
+inline void copy_pairs(const Seg& s, int64_t so, int64_t n, int32_t* links, int32_t* atoms) {
+    if (s.stride == 1) {
+        if (links) std::memcpy(links, s.link + so, sizeof(int32_t) * (size_t)n);
+        if (atoms) std::memcpy(atoms, s.atom + so, sizeof(int32_t) * (size_t)n);
+        return;
+    }
+    const int2* p = (const int2*)(s.link + 2 * so);
+    if (links && atoms) {
+        for (int64_t i = 0; i < n; ++i) {
+            const int2 v = p[i];
+            links[i] = v.x;
+            atoms[i] = v.y;
+        }
+    } else if (links) {
+        for (int64_t i = 0; i < n; ++i) links[i] = p[i].x;
+    } else if (atoms) {
+        for (int64_t i = 0; i < n; ++i) atoms[i] = p[i].y;
+    }
+}
 
 // The level-synchronous engine's output: per seed its segments (one per level it reached), the
 // mapped buffers they live in (the result owns them), traversed items, deepest distance.
@@ -4022,8 +4073,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.bstart = (int64_t*)w.take(sizeof(int64_t) * (kLrMaxBuckets + 1));
         a.bk_v = (u64*)w.take(sizeof(u64) * nd);
         a.bk_sa = (int64_t*)w.take(sizeof(int64_t) * nd);
-        a.out_link = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
-        a.out_atom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
+        a.out_pair = (int2*)w.take(sizeof(int2) * (size_t)cap);
+        a.seedcnt = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)kLsMaxW * 64);
         a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
         a.hbits = hbits;
         a.hmask = ((int64_t)1 << hbits) - 1;
@@ -4075,7 +4126,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         auto enqueue = [&](int32_t d) {
             // grids: thousands of idle workgroups cost ~10 us a launch on small levels;
             // the expand's tiles and the pull's atoms are the work that needs more than a block per CU
-            hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d, 0);
+            hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, d);
             hgx_ls_prefix<<<kLsG, 256, 0, st>>>(a, d);
             hgx_ls_expand<<<1024, 256, 0, st>>>(a, d);
             if (a.pull) {
@@ -4117,19 +4168,16 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             }
         } give_back{g, cs, &lbufs};
         auto copy_level = [&](int32_t d, int64_t out0, int64_t n) {
-            PoolBuf hb = take_host_buf(g, 8 * (size_t)n);
+            PoolBuf hb = take_host_buf(g, 8 * (size_t)n);   // (link, atom) interleaved
             lbufs.push_back({hb, out0, n});
-            int32_t* hl = (int32_t*)hb.p;
-            int32_t* ha = hl + n;
+            int2* hp = (int2*)hb.p;
             const u64* bnd = g->seq_flag + 8 + (kLrParts + 1) * (d & 1);
             for (int q = 0; q < kLrParts; ++q) {
                 const int64_t b = (int64_t)bnd[q], e = (int64_t)bnd[q + 1];
                 if (b < 0 || e > n || e < b) fail(HGX_E_DEVICE, "hgx_bfs_sequence: rank-part bounds inconsistent");
                 if (e == b) continue;
                 HGX_HIP(hipStreamWaitEvent(cs, g->ls_ev[kLrParts * (d & 1) + q], 0));
-                HGX_HIP(hipMemcpyAsync(hl + b, a.out_link + out0 + b, sizeof(int32_t) * (size_t)(e - b),
-                                       hipMemcpyDeviceToHost, cs));
-                HGX_HIP(hipMemcpyAsync(ha + b, a.out_atom + out0 + b, sizeof(int32_t) * (size_t)(e - b),
+                HGX_HIP(hipMemcpyAsync(hp + b, a.out_pair + out0 + b, sizeof(int2) * (size_t)(e - b),
                                        hipMemcpyDeviceToHost, cs));
             }
         };
@@ -4158,10 +4206,6 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             total += n;
             ++dw;
             if (n == 0) break;
-            if (dw == maxd) {   // depth limit: the last level's pairs still need their runs
-                hgx_ls_degree<<<kLsG, 256, 0, st>>>(a, dw, 1);
-                HGX_CHECK_LAUNCH();
-            }
         }
         g->seq_flag_seq = base + (u64)enq + 2;
         std::vector<int64_t> ctl(kLsCtlWords);
@@ -4204,8 +4248,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             size_t L = 0;
             while (L + 1 < lbufs.size() && lbufs[L + 1].out0 <= b) ++L;
             int32_t* hl = (int32_t*)lbufs[L].b.p;
-            pl = hl + (b - lbufs[L].out0);
-            pa = hl + lbufs[L].n + (b - lbufs[L].out0);
+            pl = hl + 2 * (b - lbufs[L].out0);
+            pa = pl + 1;
         };
         // runs partition [0, total) in pair order; each seed's runs in distance order are its pairs
         std::vector<int64_t> ord((size_t)nruns);
@@ -4232,7 +4276,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 const int64_t e = k + 1 < nruns ? hr[3 * ord[k + 1] + 2] : total;
                 int32_t *pl = nullptr, *pa = nullptr;
                 at_pair(b, pl, pa);
-                out.segs[(size_t)(seed0 + s)].push_back({pl, pa, nullptr, e - b, (int32_t)dk.first});
+                out.segs[(size_t)(seed0 + s)].push_back({pl, pa, nullptr, e - b, (int32_t)dk.first, 2});
                 out.deepest = std::max(out.deepest, (int32_t)dk.first);
             }
         }
@@ -5281,8 +5325,7 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
     auto run = [&](const Job& j) {
         const Seg& s = *j.s;
         const int64_t o = j.b + j.lo;
-        if (links) std::memcpy(links + o, s.link + j.lo, sizeof(int32_t) * j.n);
-        if (atoms) std::memcpy(atoms + o, s.atom + j.lo, sizeof(int32_t) * j.n);
+        copy_pairs(s, j.lo, j.n, links ? links + o : nullptr, atoms ? atoms + o : nullptr);
         if (dists) {
             if (s.dist) std::memcpy(dists + o, s.dist + j.lo, sizeof(int32_t) * j.n);
             else std::fill(dists + o, dists + o + j.n, s.dist_c);
@@ -5304,8 +5347,7 @@ int hgx_seq_result_pairs_range(const hgx_seq_result* r, int64_t first, int64_t n
         const int64_t lo_ = std::max(b, first), hi_ = std::min(b + s.n, hi);
         if (hi_ <= lo_) return;
         const int64_t k = hi_ - lo_, so = lo_ - b, o = lo_ - first;
-        if (links) std::memcpy(links + o, s.link + so, sizeof(int32_t) * k);
-        if (atoms) std::memcpy(atoms + o, s.atom + so, sizeof(int32_t) * k);
+        copy_pairs(s, so, k, links ? links + o : nullptr, atoms ? atoms + o : nullptr);
         if (dists) {
             if (s.dist) std::memcpy(dists + o, s.dist + so, sizeof(int32_t) * k);
             else std::fill(dists + o, dists + o + k, s.dist_c);
