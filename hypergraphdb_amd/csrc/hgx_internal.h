@@ -232,7 +232,7 @@ struct hgx_graph {
     int32_t seq_engine = 0;                         // HGX_OPT_SEQ_ENGINE: 0 workgroup per seed (+ level engine), 1 key-array
                                                     //   level engine only, 2 level engine (hgx_ls_*) only
     unsigned long long* seq_flag = nullptr;         // mapped coherent words: level sizes of the level engine
-    hipEvent_t ls_ev[8] = {};                       //   its rank parts' events (2 level parities x 4 parts)
+    hipEvent_t ls_ev[16] = {};                      //   its rank parts' events (2 level parities x 8 parts)
     unsigned long long seq_flag_seq = 0;            //   (their sequence numbers)
     int64_t ls_cap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
     int64_t ls_hcap = 0, ls_fcap = 0;               //   and its two hash tables' slots (push, frontier)

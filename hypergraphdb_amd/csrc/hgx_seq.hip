@@ -39,6 +39,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "hgx_internal.h"
 
 namespace hgx {
@@ -1912,17 +1914,22 @@ constexpr int kLsMaxW = 16;             // row words: chunks of <= 1024 seeds
 constexpr int kLrMaxBucketBits = 18;                            // <= 2^18 keys a bucket (a 32 KB LDS bitmap)
 constexpr int kLrMaxBuckets = 1 << (32 - kLrMaxBucketBits);     // keys < 2^32
 constexpr int kLrG = 512;                                       // blocks of count / scatter / rank
-constexpr int kLrParts = 4;   // rank launches a level (bucket ranges): each part's pairs are copied to the host on
+constexpr int kLrU = 4;                                         // independent loads a thread in their loops
+constexpr int kLrParts = 8;   // scatter + rank launches a level (bucket ranges): each part's pairs are copied to the host on
                               // stream2 while the next parts rank (the host learns the parts' rank ranges from
                               // the scan's publication)
 
-__device__ __forceinline__ int lr_bucket_bits(int64_t W) {
+__device__ __forceinline__ int lr_bucket_bits(int64_t W, int sub) {
     const u64 keys = (u64)max<int64_t>(W, 1) * 64ull;
     const int lg = 64 - __clzll((unsigned long long)(keys - 1ull));   // ceil(log2(keys)), keys >= 64
-    return min(max(lg - 9, 6), kLrMaxBucketBits);
+    return min(max(lg - sub, 6), kLrMaxBucketBits);
 }
 __device__ __forceinline__ int lr_buckets(int64_t W, int bs) {
     return (int)(((u64)max<int64_t>(W, 1) * 64ull + (1ull << bs) - 1ull) >> bs);
+}
+// The rank part of bucket b: the q with q * nbk / kLrParts <= b < (q + 1) * nbk / kLrParts.
+__device__ __forceinline__ int lr_part(uint32_t b, int nbk) {
+    return (int)(((b + 1u) * (uint32_t)kLrParts - 1u) / (uint32_t)nbk);
 }
 
 constexpr int kLsProbes = 64;           // hash probes before a level reports overflow (load <= 1/2)
@@ -1939,6 +1946,7 @@ struct LsArgs {
     const int32_t* link_atom;
     int32_t want_type, min_arity, mode, rev, kbits;
     int64_t t_limit;                    // largest item count of a level with 32-bit keys
+    int32_t lr_sub;                     // ranking buckets ~ 2^lr_sub a level (lr_bucket_bits)
     int32_t nb, W;                      // seeds of the chunk, row words
     int32_t maxd;                       // depth limit (the last level's discoveries are not expanded)
     u64* vis;                           // [A * W] examined rows (zero at the call's start)
@@ -1958,8 +1966,10 @@ struct LsArgs {
     uint32_t* bcnt;                     // [kLrMaxBuckets] discoveries per key bucket (hgx_lr_*; zeroed by the expand)
     uint32_t* bcur;                     // [kLrMaxBuckets] the buckets' fill cursors
     int64_t* bstart;                    // [kLrMaxBuckets + 1] their first rank
-    u64* bk_v;                          // the discoveries by bucket: value, seed * A + atom
+    u64* bk_v;                          // the discoveries by rank part (hgx_lr_split): value, seed * A + atom
     int64_t* bk_sa;
+    uint32_t* pcnt;                     // [kLrG][kLrParts] count block's discoveries per rank part
+    uint32_t* pcur;                     // [kLrParts] the parts' fill cursors
     int2* out_pair;                     // [cap] (link atom, atom) pairs, level-major (device)
     uint32_t* seedcnt;                  // [nb] the level's discoveries per seed (hgx_lr_count; zeroed by the expand)
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
@@ -2296,7 +2306,7 @@ __global__ void __launch_bounds__(256) hgx_ls_expand(LsArgs a, int32_t d) {
     const int32_t* fa = a.fa[cur];
     const int32_t* fs = a.fs[cur];
     {   // the ranking's bucket counts (hgx_lr_count adds to them)
-        const int bs = lr_bucket_bits(W), nbk = lr_buckets(W, bs);
+        const int bs = lr_bucket_bits(W, a.lr_sub), nbk = lr_buckets(W, bs);
         for (int64_t b = blockIdx.x * 256ll + threadIdx.x; b < nbk; b += (int64_t)gridDim.x * 256) a.bcnt[b] = 0u;
         for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < a.nb; q += (int64_t)gridDim.x * 256) a.seedcnt[q] = 0u;
     }
@@ -2854,15 +2864,18 @@ __global__ void __launch_bounds__(256) hgx_lp_hfinal(LsArgs a, int32_t d) {
 // Ranking a level's discoveries by key (round 5; it replaced a bit per discovery in a global bitmap over
 // the level's key space, a popcount prefix per word and an emit that read the word and its prefix at
 // random: config 2's drop-in level of 258M discoveries fetched 70 GB and wrote 25 GB in that emit).
-// The key space is cut into buckets of 2^bs keys (~512 buckets of 64 .. 2^18 keys; up to 16384 buckets
-// of 2^18 keys for 32-bit keys):
+// The key space is cut into buckets of 2^bs keys (~2^lr_sub = 2048 buckets of 64 .. 2^18 keys; up to 16384
+// buckets of 2^18 keys for 32-bit keys), the buckets into kLrParts rank parts (consecutive bucket ranges):
 //   hgx_lr_count    per block an LDS histogram of its range of the discovery list, one global add per
-//                   bucket it touched (push levels first take the value out of the hash slot and clear
-//                   the slot; pull levels clear the frontier rows and the union bitmap)
+//                   bucket it touched, the block's count per part (push levels first take the value out of
+//                   the hash slot and clear the slot; pull levels clear the frontier rows and the union
+//                   bitmap)
 //   hgx_lr_scan     one block: bucket starts (the level's ranks are key order, so bucket b's ranks are
 //                   [start b, start b+1)), the level's size published to the host and the next level
-//   hgx_lr_scatter  per block the same range again: a contiguous slot range per bucket claimed with one
-//                   global add, the discoveries copied into it (runs of a bucket per block: coalesced)
+//   hgx_lr_split    per block the same range again into the parts' regions (8 write streams a block)
+//   then per part, so that part q's pairs go to the host while part q+1 is ordered:
+//   hgx_lr_scatter  per block a range of the part's region: a contiguous slot range per bucket claimed
+//                   with one global add, the discoveries copied into it (runs of a bucket per block)
 //   hgx_lr_rank     a workgroup per bucket: an LDS bitmap of its keys and a popcount prefix per word;
 //                   rank = start + prefix + bits below; pair `rank` of the level, entry `rank` of the next
 //                   frontier, the examined bit.  The writes of a bucket land in one window of the outputs.
@@ -2870,33 +2883,52 @@ __global__ void __launch_bounds__(256) hgx_lr_count(LsArgs a, int32_t d) {
     __shared__ int64_t pre[kLsDSegs + 2];
     __shared__ uint32_t hist[kLrMaxBuckets];
     __shared__ uint32_t scnt[kLsMaxW * 64];   // the block's discoveries per seed (the level's runs)
+    __shared__ uint32_t pc[kLrParts];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
     const bool pull = sl[lsPull] != 0;
-    const int bs = lr_bucket_bits(sl[lsW]);
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
     const int nbk = lr_buckets(sl[lsW], bs);
     for (int b = threadIdx.x; b < nbk; b += 256) hist[b] = 0u;
+    if (threadIdx.x < kLrParts) pc[threadIdx.x] = 0u;
     for (int q = threadIdx.x; q < a.nb; q += 256) scnt[q] = 0u;
     const int64_t n = ls_disc_prefix(a, d, pre);   // (syncs the block)
     const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
-    for (int64_t x = lo + threadIdx.x; x < hi; x += 256) {
-        const int64_t pos = ls_disc_pos(a, pre, x);
-        u64 v = a.dval[pos];
-        if (!pull) {   // v is the hash slot
-            const u64 hs = v;
-            v = a.hval[hs];
-            a.dval[pos] = v;
-            a.hkey[hs] = kLsEmpty;
-            a.hval[hs] = ~0ull;
+    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += 256 * kLrU) {   // kLrU independent loads a thread
+        int64_t pos[kLrU];
+        u64 v[kLrU];
+        int64_t sa[kLrU];
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            const int64_t x = x0 + 256 * u;
+            pos[u] = x < hi ? ls_disc_pos(a, pre, x) : -1;
+            v[u] = pos[u] >= 0 ? a.dval[pos[u]] : 0ull;
+            sa[u] = pos[u] >= 0 ? a.disc[pos[u]] : 0;
         }
-        atomicAdd(&hist[((v >> 32) - 1ull) >> bs], 1u);
-        atomicAdd(&scnt[(int)(a.disc[pos] / a.A)], 1u);
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            if (pos[u] < 0) continue;
+            if (!pull) {   // v is the hash slot
+                const u64 hs = v[u];
+                v[u] = a.hval[hs];
+                a.dval[pos[u]] = v[u];
+                a.hkey[hs] = kLsEmpty;
+                a.hval[hs] = ~0ull;
+            }
+            atomicAdd(&hist[((v[u] >> 32) - 1ull) >> bs], 1u);
+            atomicAdd(&scnt[(int)(sa[u] / a.A)], 1u);
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < nbk; b += 256)
-        if (hist[b]) atomicAdd(&a.bcnt[b], hist[b]);
+        if (hist[b]) {
+            atomicAdd(&a.bcnt[b], hist[b]);
+            atomicAdd(&pc[lr_part((uint32_t)b, nbk)], hist[b]);
+        }
     for (int q = threadIdx.x; q < a.nb; q += 256)
         if (scnt[q]) atomicAdd(&a.seedcnt[q], scnt[q]);
+    __syncthreads();
+    if (threadIdx.x < kLrParts) a.pcnt[blockIdx.x * kLrParts + threadIdx.x] = pc[threadIdx.x];   // (hgx_lr_split)
     if (pull) {
         const int64_t nu = sl[lsU];
         for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < nu; u += (int64_t)gridDim.x * 256) {
@@ -2971,7 +3003,7 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
             return;
         }
     }
-    const int bs = lr_bucket_bits(sl[lsW]);
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
     const int nbk = lr_buckets(sl[lsW], bs);
     constexpr int per = kLrMaxBuckets / 1024;
     const int b0 = threadIdx.x * per;
@@ -3002,6 +3034,7 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
             for (int q = 0; q < kLrParts; ++q)
                 if (q * nbk / kLrParts == b0 + k) {
                     __hip_atomic_store(bnd + q, (u64)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    a.pcur[q] = (uint32_t)run;
                     wrote = true;
                 }
         }
@@ -3017,28 +3050,105 @@ __global__ void __launch_bounds__(1024) hgx_lr_scan(LsArgs a, int32_t d, u64 seq
     if (threadIdx.x == 0) publish();
 }
 
-__global__ void __launch_bounds__(256) hgx_lr_scatter(LsArgs a, int32_t d) {
+// The level's discoveries into kLrParts regions by rank part (bk_v / bk_sa; part q's region is its rank
+// range [start of its first bucket, start of the next part's)): the count pass's per-block part counts give
+// each block its slot ranges, a wave claims a part's slots with one LDS add, so a wave's writes to one part
+// are consecutive.  The same block ranges as hgx_lr_count (both launch kLrG blocks).
+__global__ void __launch_bounds__(256) hgx_lr_split(LsArgs a, int32_t d) {
     __shared__ int64_t pre[kLsDSegs + 2];
-    __shared__ uint32_t slot[kLrMaxBuckets];
+    __shared__ uint32_t slot[kLrParts];
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus]) return;
-    const int bs = lr_bucket_bits(sl[lsW]);
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
     const int nbk = lr_buckets(sl[lsW], bs);
-    for (int b = threadIdx.x; b < nbk; b += 256) slot[b] = 0u;
-    const int64_t n = ls_disc_prefix(a, d, pre);
+    if (threadIdx.x < kLrParts) {
+        const uint32_t c = a.pcnt[blockIdx.x * kLrParts + threadIdx.x];
+        slot[threadIdx.x] = c ? atomicAdd(&a.pcur[threadIdx.x], c) : 0u;
+    }
+    const int64_t n = ls_disc_prefix(a, d, pre);   // (syncs the block)
     const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
-    for (int64_t x = lo + threadIdx.x; x < hi; x += 256)
-        atomicAdd(&slot[((a.dval[ls_disc_pos(a, pre, x)] >> 32) - 1ull) >> bs], 1u);
+    const int lane = threadIdx.x & 63;
+    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += 256 * kLrU) {
+        int64_t pos[kLrU];
+        u64 v[kLrU];
+        int64_t sa[kLrU];
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            const int64_t x = x0 + 256 * u;
+            pos[u] = x < hi ? ls_disc_pos(a, pre, x) : -1;
+            v[u] = pos[u] >= 0 ? a.dval[pos[u]] : 0ull;
+            sa[u] = pos[u] >= 0 ? a.disc[pos[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            const int q = pos[u] >= 0 ? lr_part((uint32_t)(((v[u] >> 32) - 1ull) >> bs), nbk) : -1;
+            u64 rem = __ballot(q >= 0);   // (the lanes still in the loop)
+            uint32_t my = 0;
+            while (rem) {   // one LDS add per part present in the wave
+                const int lead = __ffsll((long long)rem) - 1;
+                const int qq = __shfl(q, lead);
+                const u64 m = __ballot(q == qq);
+                uint32_t base = 0;
+                if (lane == lead) base = atomicAdd(&slot[qq], (uint32_t)__popcll(m));
+                base = __shfl(base, lead);
+                if (q == qq) my = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                rem &= ~m;
+            }
+            if (q >= 0) {
+                a.bk_v[my] = v[u];
+                a.bk_sa[my] = sa[u];
+            }
+        }
+    }
+}
+
+// Part `part` of kLrParts: its region of bk_v / bk_sa into bucket order, in place of the level's
+// discovery list (dval / disc, dead after hgx_lr_split), each block a contiguous range of the region with
+// a contiguous slot range per bucket claimed with one global add.
+__global__ void __launch_bounds__(256) hgx_lr_scatter(LsArgs a, int32_t d, int32_t part) {
+    __shared__ uint32_t slot[kLrMaxBuckets / kLrParts];
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || sl[lsN] == 0) return;
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    const uint32_t blo = (uint32_t)(part * nbk / kLrParts), nbp = (uint32_t)((part + 1) * nbk / kLrParts) - blo;
+    if (nbp == 0) return;
+    const int64_t p0 = a.bstart[blo], np = a.bstart[blo + nbp] - p0;
+    if (np == 0) return;
+    for (uint32_t b = threadIdx.x; b < nbp; b += 256) slot[b] = 0u;
     __syncthreads();
-    for (int b = threadIdx.x; b < nbk; b += 256)   // this block's slot range of each bucket it holds
-        if (slot[b]) slot[b] = atomicAdd(&a.bcur[b], slot[b]);
+    const int64_t lo = p0 + np * blockIdx.x / gridDim.x, hi = p0 + np * (blockIdx.x + 1) / gridDim.x;
+    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += 256 * kLrU) {
+        uint32_t b[kLrU];
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            const int64_t x = x0 + 256 * u;
+            b[u] = x < hi ? (uint32_t)(((a.bk_v[x] >> 32) - 1ull) >> bs) - blo : ~0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u)
+            if (b[u] < nbp) atomicAdd(&slot[b[u]], 1u);
+    }
     __syncthreads();
-    for (int64_t x = lo + threadIdx.x; x < hi; x += 256) {
-        const int64_t pos = ls_disc_pos(a, pre, x);
-        const u64 v = a.dval[pos];
-        const uint32_t q = atomicAdd(&slot[((v >> 32) - 1ull) >> bs], 1u);
-        a.bk_v[q] = v;
-        a.bk_sa[q] = a.disc[pos];
+    for (uint32_t b = threadIdx.x; b < nbp; b += 256)   // this block's slot range of each bucket it holds
+        if (slot[b]) slot[b] = atomicAdd(&a.bcur[blo + b], slot[b]);
+    __syncthreads();
+    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += 256 * kLrU) {
+        u64 v[kLrU];
+        int64_t sa[kLrU];
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            const int64_t x = x0 + 256 * u;
+            v[u] = x < hi ? a.bk_v[x] : 0ull;
+            sa[u] = x < hi ? a.bk_sa[x] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kLrU; ++u) {
+            if (sa[u] < 0) continue;
+            const uint32_t q = atomicAdd(&slot[(uint32_t)(((v[u] >> 32) - 1ull) >> bs) - blo], 1u);
+            a.dval[q] = v[u];
+            a.disc[q] = sa[u];
+        }
     }
 }
 
@@ -3050,7 +3160,7 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
     const int64_t* sl = ls_slot(a, d);
     if (a.ctl[kLsStatus] || sl[lsN] == 0) return;
     const int64_t out0 = sl[lsOut];
-    const int bs = lr_bucket_bits(sl[lsW]);
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
     const int nbk = lr_buckets(sl[lsW], bs);
     const int nw = 1 << (bs - 6);                 // bitmap words of a bucket
     const int per = (nw + 255) / 256;
@@ -3063,9 +3173,16 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
         for (int w = threadIdx.x; w < nw; w += 256) bm[w] = 0ull;
         __syncthreads();
         const u64 kb = (u64)b << bs;
-        for (int64_t i = s0 + threadIdx.x; i < s1; i += 256) {
-            const u64 kk = (a.bk_v[i] >> 32) - 1ull - kb;
-            atomicOr((unsigned long long*)&bm[kk >> 6], 1ull << (kk & 63));
+        for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += 256 * kLrU) {
+            u64 kk[kLrU];
+#pragma unroll
+            for (int u = 0; u < kLrU; ++u) {
+                const int64_t i = i0 + 256 * u;
+                kk[u] = i < s1 ? (a.dval[i] >> 32) - 1ull - kb : ~0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < kLrU; ++u)
+                if (kk[u] != ~0ull) atomicOr((unsigned long long*)&bm[kk[u] >> 6], 1ull << (kk[u] & 63));
         }
         __syncthreads();
         const int w0 = threadIdx.x * per;
@@ -3078,9 +3195,20 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
             run += __popcll(bm[w0 + k]);
         }
         __syncthreads();
-        for (int64_t i = s0 + threadIdx.x; i < s1; i += 256) {
-            const u64 v = a.bk_v[i];
-            const int64_t sa = a.bk_sa[i];
+        for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += 256 * kLrU) {
+          u64 vv[kLrU];
+          int64_t sv[kLrU];
+#pragma unroll
+          for (int u = 0; u < kLrU; ++u) {
+            const int64_t i = i0 + 256 * u;
+            vv[u] = i < s1 ? a.dval[i] : 0ull;
+            sv[u] = i < s1 ? a.disc[i] : -1;
+          }
+#pragma unroll
+          for (int u = 0; u < kLrU; ++u) {
+            if (sv[u] < 0) continue;
+            const u64 v = vv[u];
+            const int64_t sa = sv[u];
             const u64 kk = (v >> 32) - 1ull - kb;
             const int64_t r = s0 + wp[kk >> 6] + __popcll(bm[kk >> 6] & ((1ull << (kk & 63)) - 1ull));
             const int32_t s = (int32_t)(sa / a.A), t = (int32_t)(sa - (int64_t)s * a.A);
@@ -3090,6 +3218,7 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
                 a.fa[nx][r] = t;
                 atomicOr((unsigned long long*)&a.vis[(int64_t)t * a.W + (s >> 6)], 1ull << (s & 63));   // examined from now on
             }
+          }
         }
         __syncthreads();   // bm / wp are reused by the next bucket
     }
@@ -4007,7 +4136,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         std::memset(hp, 0, 256);
         g->seq_flag = (u64*)hp;
     }
-    static_assert(2 * kLrParts <= 8 && 8 + 2 * (kLrParts + 1) <= 32, "rank-part events / bounds");
+    static_assert(2 * kLrParts <= 16 && 8 + 2 * (kLrParts + 1) <= 32, "rank-part events / bounds");
     for (hipEvent_t& e : g->ls_ev)
         if (!e) HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!g->stream2) HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
@@ -4043,6 +4172,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.rev = o.reverse_order ? 1 : 0;
         a.kbits = kbits;
         a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
+        static const int lr_sub = std::getenv("HGX_LR_SUB") ? std::atoi(std::getenv("HGX_LR_SUB")) : 11;   // A/B (buckets ~ 2^lr_sub)
+        a.lr_sub = std::min(std::max(lr_sub, 1), 14);
         if (const char* tl = std::getenv("HGX_LS_TLIMIT")) a.t_limit = std::min<int64_t>(a.t_limit, std::atoll(tl));   // tests
         a.nb = nb;
         a.W = W;
@@ -4073,6 +4204,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.bstart = (int64_t*)w.take(sizeof(int64_t) * (kLrMaxBuckets + 1));
         a.bk_v = (u64*)w.take(sizeof(u64) * nd);
         a.bk_sa = (int64_t*)w.take(sizeof(int64_t) * nd);
+        a.pcnt = (uint32_t*)w.take(sizeof(uint32_t) * kLrG * kLrParts);
+        a.pcur = (uint32_t*)w.take(sizeof(uint32_t) * kLrParts);
         a.out_pair = (int2*)w.take(sizeof(int2) * (size_t)cap);
         a.seedcnt = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)kLsMaxW * 64);
         a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
@@ -4140,8 +4273,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             }
             hgx_lr_count<<<kLrG, 256, 0, st>>>(a, d);
             hgx_lr_scan<<<1, 1024, 0, st>>>(a, d, base + (u64)d + 1);
-            hgx_lr_scatter<<<lr_scatter_g, 256, 0, st>>>(a, d);
+            hgx_lr_split<<<kLrG, 256, 0, st>>>(a, d);   // (the count's block ranges)
             for (int q = 0; q < kLrParts; ++q) {
+                hgx_lr_scatter<<<lr_scatter_g, 256, 0, st>>>(a, d, q);
                 hgx_lr_rank<<<lr_rank_g, 256, 0, st>>>(a, d, q);
                 HGX_HIP(hipEventRecord(g->ls_ev[kLrParts * (d & 1) + q], st));
             }
@@ -4202,12 +4336,14 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             const int64_t n = (int64_t)__atomic_load_n(hf, __ATOMIC_RELAXED);
             status = (int64_t)__atomic_load_n(hf + 1, __ATOMIC_RELAXED);
             if (status) break;
+            seq_mark("level size read");
             if (n > 0) copy_level(dw, total, n);
             total += n;
             ++dw;
             if (n == 0) break;
         }
         g->seq_flag_seq = base + (u64)enq + 2;
+        seq_mark("levels read");
         std::vector<int64_t> ctl(kLsCtlWords);
         HGX_HIP(hipMemcpyAsync(ctl.data(), a.ctl, sizeof(int64_t) * kLsCtlWords, hipMemcpyDeviceToHost, st));
         spin_sync(st);
@@ -4242,7 +4378,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         int64_t* hr = (int64_t*)hb.p;
         if (nruns) HGX_HIP(hipMemcpyAsync(hr, a.runs, sizeof(int64_t) * 3 * (size_t)nruns, hipMemcpyDeviceToHost, st));
         spin_sync(st);
+        seq_mark("level kernels done");
         spin_sync(cs);
+        seq_mark("pair copies done");
         // a pair index -> its level buffer (levels are consecutive ranges of [0, total))
         auto at_pair = [&](int64_t b, int32_t*& pl, int32_t*& pa) {
             size_t L = 0;
@@ -5107,6 +5245,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         ev1 = ev_take(g);
         HGX_HIP(hipEventRecord(ev0, st));
     }
+    seq_mark("call set up");
     std::vector<int32_t> rerun;   // seed indices for the level-synchronous engine
     int32_t deepest = 0;
     if (g->seq_engine == 0 && n_seeds > 0) {
@@ -5264,6 +5403,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     if (g->timing) {
         HGX_HIP(hipEventRecord(ev1, st));
         HGX_HIP(hipEventSynchronize(ev1));
+        seq_mark("timing event done");
         float ms = 0;
         HGX_HIP(hipEventElapsedTime(&ms, ev0, ev1));
         r->ms_total = ms;
@@ -5321,6 +5461,22 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
             add(b, s);
             b += s.n;
         }
+    }
+    // large caller arrays are usually fresh (their pages first touched by the copy below): ask for
+    // transparent huge pages on their 2 MB-aligned interior, 512x fewer page faults where the kernel's THP
+    // mode is "madvise" (a hint: no effect under "never", already the case under "always")
+    static const bool thp = !(std::getenv("HGX_READOUT_THP") && std::atoi(std::getenv("HGX_READOUT_THP")) == 0);
+    if (thp && r->off.back() >= ((int64_t)1 << 24)) {
+        auto hint = [](void* p, size_t bytes) {
+            if (!p) return;
+            const uintptr_t b = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+            const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)((2u << 20) - 1);
+            if (e > b) (void)madvise((void*)b, e - b, MADV_HUGEPAGE);
+        };
+        const size_t nb = sizeof(int32_t) * (size_t)r->off.back();
+        hint(links, nb);
+        hint(atoms, nb);
+        hint(dists, nb);
     }
     auto run = [&](const Job& j) {
         const Seg& s = *j.s;
