@@ -8,6 +8,8 @@ KERNEL after the first BFS gather (bench.py runs config 2 first, then builds the
 `--until k_validate` isolates the config-2 leg of the default bench command).
 --from-last KERNEL keeps only the dispatches from the last launch of KERNEL on (the last call of a tool
 that repeats one call: `--from-last hgx_ls_seed` is the steady-state drop-in call of tools/seq_c2.py).
+--from KERNEL keeps only the dispatches from the first launch of KERNEL after the first BFS gather on
+(`--from k_validate` with `--no-queries`: the config-4 leg, whose snapshot is built after the config-2 leg).
 --min-ms X drops every dispatch shorter than X ms (by the trace pass; tools/seq_c5.py's single-seed calls
 beside its batched ones).
 
@@ -67,14 +69,14 @@ def first_kept(rows, from_last):
     return max(ids) if ids else None
 
 
-def load_counter(path, counter, until=None, from_last=None):
+def load_counter(path, counter, until=None, from_last=None, from_first=None):
     acc = defaultdict(list)
     if not os.path.exists(path):
         return acc
     with open(path) as f:
         rows = list(csv.DictReader(f))
     cut = cutoff(rows, until)
-    lo = first_kept(rows, from_last)
+    lo = first_kept(rows, from_last) if from_last else cutoff(rows, from_first)
     for row in rows:
         if lo is not None and int(row["Dispatch_Id"]) < lo:
             continue
@@ -83,12 +85,12 @@ def load_counter(path, counter, until=None, from_last=None):
     return acc
 
 
-def load_trace(path, until=None, from_last=None):
+def load_trace(path, until=None, from_last=None, from_first=None):
     acc = defaultdict(list)
     with open(path) as f:
         rows = list(csv.DictReader(f))
     cut = cutoff(rows, until)
-    lo = first_kept(rows, from_last)
+    lo = first_kept(rows, from_last) if from_last else cutoff(rows, from_first)
     for row in rows:
         if lo is not None and int(row["Dispatch_Id"]) < lo:
             continue
@@ -99,7 +101,7 @@ def load_trace(path, until=None, from_last=None):
 
 def main():
     argv = sys.argv[1:]
-    until = from_last = None
+    until = from_last = from_first = None
     if "--until" in argv:
         k = argv.index("--until")
         until = argv[k + 1]
@@ -108,6 +110,10 @@ def main():
     if "--min-ms" in argv:
         k = argv.index("--min-ms")
         min_ms = float(argv[k + 1])
+        del argv[k:k + 2]
+    if "--from" in argv:
+        k = argv.index("--from")
+        from_first = argv[k + 1]
         del argv[k:k + 2]
     if "--from-last" in argv:
         k = argv.index("--from-last")
@@ -121,7 +127,7 @@ def main():
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until, from_last)
+    trace = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"), until, from_last, from_first)
     if min_ms > 0:   # the passes dispatch in the same order: drop the short launches' counter values by rank
         with open(os.path.join(d, "trace", "run_kernel_trace.csv")) as f:
             rows = sorted(csv.DictReader(f), key=lambda r: int(r["Dispatch_Id"]))
@@ -134,8 +140,8 @@ def main():
             seen[k] += 1
         trace = {k: [t for t in v if t >= min_ms] for k, v in trace.items()}
         trace = {k: v for k, v in trace.items() if v}
-    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until, from_last)
-    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until, from_last)
+    fetch = load_counter(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", until, from_last, from_first)
+    write = load_counter(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE", until, from_last, from_first)
     if min_ms > 0:
         fetch = {k: [v for i, v in enumerate(vs) if i not in short_rank[k]] for k, vs in fetch.items()}
         write = {k: [v for i, v in enumerate(vs) if i not in short_rank[k]] for k, vs in write.items()}
@@ -151,6 +157,7 @@ def main():
     except Exception:
         commit, dirty = None, None
     rows, js = [], {"tag": tag, "workload": workload, "kernels": {}, "commit": commit, "from_last": from_last,
+                    "from": from_first,
                     "min_ms": min_ms or None,
                     "commit_dirty": dirty,
                     "note": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE correction)"}
@@ -174,6 +181,8 @@ def main():
             f.write(f"Dispatches before the first `{until}` launch after the BFS only (the {workload} leg of the command).\n\n")
         if from_last:
             f.write(f"Dispatches from the last `{from_last}` launch on only (the command's last call).\n\n")
+        if from_first:
+            f.write(f"Dispatches from the first `{from_first}` launch after the BFS on only (the {workload} leg).\n\n")
         f.write("Kernel trace: `rocprofv3 --kernel-trace --stats`; HBM bytes from separate `--pmc FETCH_SIZE` and\n"
                 "`--pmc WRITE_SIZE` passes, bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch.\n\n")
         f.write("| kernel | launches | total ms | avg ms | fetch B/launch | write B/launch | HBM GB/s |\n")
