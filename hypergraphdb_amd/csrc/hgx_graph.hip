@@ -52,6 +52,8 @@ void graph_release(hgx_graph* g) {
     if (g->seq_flag) (void)hipHostFree(g->seq_flag);
     for (hipEvent_t& e : g->ls_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t& e : g->ls_cev)
+        if (e) (void)hipEventDestroy(e);
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->zc_in) (void)hipHostFree(g->zc_in);
     if (g->stream2) (void)hipStreamSynchronize(g->stream2);

@@ -233,6 +233,7 @@ struct hgx_graph {
                                                     //   level engine only, 2 level engine (hgx_ls_*) only
     unsigned long long* seq_flag = nullptr;         // mapped coherent words: level sizes of the level engine
     hipEvent_t ls_ev[16] = {};                      //   its rank parts' events (2 level parities x 8 parts)
+    hipEvent_t ls_cev[2] = {};                      //   a level's pair copies enqueued (by level parity)
     unsigned long long seq_flag_seq = 0;            //   (their sequence numbers)
     int64_t ls_cap = 0, ls_tcap = 0, ls_rcap = 0;   // level-engine capacities grown on demand
     int64_t ls_hcap = 0, ls_fcap = 0;               //   and its two hash tables' slots (push, frontier)

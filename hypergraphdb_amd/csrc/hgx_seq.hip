@@ -1915,6 +1915,8 @@ constexpr int kLrMaxBucketBits = 18;                            // <= 2^18 keys 
 constexpr int kLrMaxBuckets = 1 << (32 - kLrMaxBucketBits);     // keys < 2^32
 constexpr int kLrG = 512;                                       // blocks of count / scatter / rank
 constexpr int kLrU = 4;                                         // independent loads a thread in their loops
+constexpr int kLpBlk = 4096;                                    // pairs of a packed block (64 run-start words)
+constexpr int kPackWords = 32;                                  // mapped words of the packed counts: [2][kLrParts] {count, seq}
 constexpr int kLrParts = 8;   // scatter + rank launches a level (bucket ranges): each part's pairs are copied to the host on
                               // stream2 while the next parts rank (the host learns the parts' rank ranges from
                               // the scan's publication)
@@ -1971,6 +1973,15 @@ struct LsArgs {
     uint32_t* pcnt;                     // [kLrG][kLrParts] count block's discoveries per rank part
     uint32_t* pcur;                     // [kLrParts] the parts' fill cursors
     int2* out_pair;                     // [cap] (link atom, atom) pairs, level-major (device)
+    // packed transfer of large levels (n >= pack_min; hgx_lr_pflag / hgx_lr_pscan / hgx_lr_pemit): per rank
+    // part its atoms, a bit per pair where the link changes (the pair starts a new link run), the links of
+    // those pairs, and per 4096-pair block the number of runs before it
+    int64_t pack_min;
+    int32_t* patom;                     // [cap] atoms, level-major like out_pair
+    int32_t* pclink;                    // [cap] a part's run links from its first pair's index on
+    u64* pflag;                         // [2 parities][kLrParts][pwcap] run-start bits of a part's pairs
+    uint32_t* pbb;                      // [2 parities][kLrParts][pbcap] runs before each 4096-pair block
+    int64_t pwcap, pbcap;
     uint32_t* seedcnt;                  // [nb] the level's discoveries per seed (hgx_lr_count; zeroed by the expand)
     int64_t* runs;                      // [rcap * 3]: (distance, seed, first pair) per seed per level
     u64* hflag;                         // mapped coherent host words: {n, status, seq, -} x 2 (level parity), then
@@ -3224,6 +3235,129 @@ __global__ void __launch_bounds__(256) hgx_lr_rank(LsArgs a, int32_t d, int32_t 
     }
 }
 
+// Packed transfer of a large level's rank part (the pairs cross PCIe at ~54 GB/s, the device-time floor
+// of config 2's drop-in call): consecutive pairs share their link 58% of the time on config 2's level 2,
+// so a part goes to the host as its atoms (4 B a pair), a run-start bit per pair, the links of the run
+// starts (4 B each) and a count per 4096-pair block: ~5.8 instead of 8 bytes a pair.
+__device__ __forceinline__ bool lr_part_range(const LsArgs& a, int32_t d, int32_t part, int64_t& out0, int64_t& pb, int64_t& np) {
+    const int64_t* sl = ls_slot(a, d);
+    if (a.ctl[kLsStatus] || sl[lsN] < a.pack_min || sl[lsN] == 0) return false;
+    const int bs = lr_bucket_bits(sl[lsW], a.lr_sub);
+    const int nbk = lr_buckets(sl[lsW], bs);
+    const int blo = part * nbk / kLrParts, bhi = (part + 1) * nbk / kLrParts;
+    out0 = sl[lsOut];
+    pb = a.bstart[blo];
+    np = a.bstart[bhi] - pb;
+    return np > 0;
+}
+
+// The part's run-start bits (word w = part pairs [64w, 64w + 64)) and each 4096-pair block's run count.
+__global__ void __launch_bounds__(256) hgx_lr_pflag(LsArgs a, int32_t d, int32_t part) {
+    __shared__ uint32_t ws[4];
+    int64_t out0, pb, np;
+    if (!lr_part_range(a, d, part, out0, pb, np)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64* fl = a.pflag + ((int64_t)(d & 1) * kLrParts + part) * a.pwcap;
+    uint32_t* bb = a.pbb + ((int64_t)(d & 1) * kLrParts + part) * a.pbcap;
+    const int2* pr = a.out_pair + out0 + pb;
+    const int64_t nblk = (np + kLpBlk - 1) / kLpBlk;
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {   // block-uniform
+        uint32_t c = 0;
+#pragma unroll 4
+        for (int k = 0; k < 16; ++k) {   // 16 words a wave
+            const int64_t w = b * 64 + wave * 16 + k;
+            const int64_t i = w * 64 + lane;
+            const bool ok = i < np;
+            const int32_t l = ok ? pr[i].x : 0;
+            int32_t prev = __shfl_up(l, 1);
+            if (lane == 0) prev = (ok && i > 0) ? pr[i - 1].x : l;
+            const u64 m = __ballot(ok && (i == 0 || l != prev));
+            if (lane == 0 && w * 64 < np) fl[w] = m;
+            c += (uint32_t)__popcll(m);
+        }
+        if (lane == 0) ws[wave] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) bb[b] = ws[0] + ws[1] + ws[2] + ws[3];
+        __syncthreads();
+    }
+}
+
+// One block of 1024 threads: the blocks' run counts -> exclusive prefix in place; the part's run count
+// published to the host (always, so that the host's wait ends: 0 when the part is not packed).
+__global__ void __launch_bounds__(1024) hgx_lr_pscan(LsArgs a, int32_t d, int32_t part, u64 seq) {
+    __shared__ int64_t wsum[16];
+    int64_t out0 = 0, pb = 0, np = 0;
+    const bool on = lr_part_range(a, d, part, out0, pb, np);
+    const int64_t nblk = on ? (np + kLpBlk - 1) / kLpBlk : 0;
+    uint32_t* bb = a.pbb + ((int64_t)(d & 1) * kLrParts + part) * a.pbcap;
+    const int64_t per = (nblk + 1023) / 1024;
+    const int64_t k0 = (int64_t)threadIdx.x * per;
+    int64_t c = 0;
+    for (int64_t k = k0; k < k0 + per && k < nblk; ++k) c += bb[k];
+    int64_t x = c;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t run = x - c;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+    for (int64_t k = k0; k < k0 + per && k < nblk; ++k) {
+        const uint32_t v = bb[k];
+        bb[k] = (uint32_t)run;
+        run += v;
+    }
+    if (threadIdx.x == 1023) {
+        u64* hp = a.hflag + kPackWords + 2 * ((d & 1) * kLrParts + part);
+        __hip_atomic_store(hp, (u64)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(hp + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The part's atoms and run links: run start i goes to pclink[out0 + pb + (runs before i)].
+__global__ void __launch_bounds__(256) hgx_lr_pemit(LsArgs a, int32_t d, int32_t part) {
+    __shared__ u64 s_fl[64];
+    __shared__ uint32_t s_pre[64];
+    int64_t out0, pb, np;
+    if (!lr_part_range(a, d, part, out0, pb, np)) return;
+    const u64* fl = a.pflag + ((int64_t)(d & 1) * kLrParts + part) * a.pwcap;
+    const uint32_t* bb = a.pbb + ((int64_t)(d & 1) * kLrParts + part) * a.pbcap;
+    const int2* pr = a.out_pair + out0 + pb;
+    int32_t* at = a.patom + out0 + pb;
+    int32_t* lk = a.pclink + out0 + pb;
+    const int64_t nblk = (np + kLpBlk - 1) / kLpBlk;
+    const int lane = threadIdx.x & 63;
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        if (threadIdx.x < 64) {
+            const int64_t w = b * 64 + lane;
+            const u64 m = w * 64 < np ? fl[w] : 0ull;
+            const uint32_t c = (uint32_t)__popcll(m);
+            uint32_t x = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            s_fl[lane] = m;
+            s_pre[lane] = bb[b] + x - c;
+        }
+        __syncthreads();
+        const int64_t i0 = b * kLpBlk, i1 = min<int64_t>(np, i0 + kLpBlk);
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+            const int2 v = pr[i];
+            at[i] = v.y;
+            const int wl = (int)((i - i0) >> 6), bit = (int)(i & 63);
+            const u64 m = s_fl[wl];
+            if ((m >> bit) & 1ull) lk[s_pre[wl] + __popcll(m & ((1ull << bit) - 1ull))] = v.x;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void hgx_ls_seed(LsArgs a, int32_t nb, const int32_t* __restrict__ seeds) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nb) {   // examined.put(start, TRUE) (:42-46)
@@ -3811,12 +3945,34 @@ struct Seg {
     const int32_t *link, *atom, *dist;
     int64_t n;
     int32_t dist_c;
-    int32_t stride = 1;   // 2: link / atom interleaved (the level engine's (link, atom) pairs)
+    int32_t stride = 1;   // 2: link / atom interleaved (the level engine's (link, atom) pairs); 0: packed
+    // packed (a large level's rank part, hgx_lr_pemit): link = the part's run links, flags = its run-start
+    // bits, bb = runs before each 4096-pair block, pi = the part index of the segment's first pair
+    const u64* flags = nullptr;
+    const uint32_t* bb = nullptr;
+    int64_t pi = 0;
 };
 
 // n pairs of a segment from index so on into links / atoms (either may be null): two copies, or one pass
 // over interleaved (link, atom) pairs
 inline void copy_pairs(const Seg& s, int64_t so, int64_t n, int32_t* links, int32_t* atoms) {
+    if (s.stride == 0) {
+        if (atoms) std::memcpy(atoms, s.atom + so, sizeof(int32_t) * (size_t)n);
+        if (!links || n <= 0) return;
+        int64_t i = s.pi + so;
+        // the run of pair i: the runs before its 4096-pair block, the run starts before it in the block, its own
+        int64_t c = s.bb[i >> 12];
+        for (int64_t w = (i >> 12) << 6; w < (i >> 6); ++w) c += __builtin_popcountll(s.flags[w]);
+        const int bit = (int)(i & 63);
+        c += __builtin_popcountll(s.flags[i >> 6] & (bit == 63 ? ~0ull : (2ull << bit) - 1ull)) - 1;
+        int64_t k = 0;
+        links[k++] = s.link[c];
+        for (++i; k < n; ++i, ++k) {
+            c += (int64_t)((s.flags[i >> 6] >> (i & 63)) & 1ull);
+            links[k] = s.link[c];
+        }
+        return;
+    }
     if (s.stride == 1) {
         if (links) std::memcpy(links, s.link + so, sizeof(int32_t) * (size_t)n);
         if (atoms) std::memcpy(atoms, s.atom + so, sizeof(int32_t) * (size_t)n);
@@ -4132,11 +4288,14 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     hgx_graph* root = g->base ? g->base : g;
     if (!g->seq_flag) {   // mapped, coherent: the scan kernel's level sizes and rank-part bounds (once per graph)
         void* hp = nullptr;
-        HGX_HIP(hipHostMalloc(&hp, 256, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(hp, 0, 256);
+        HGX_HIP(hipHostMalloc(&hp, 1024, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, 1024);
         g->seq_flag = (u64*)hp;
     }
-    static_assert(2 * kLrParts <= 16 && 8 + 2 * (kLrParts + 1) <= 32, "rank-part events / bounds");
+    static_assert(2 * kLrParts <= 16 && 8 + 2 * (kLrParts + 1) <= kPackWords && kPackWords + 4 * kLrParts <= 128,
+                  "rank-part events / bounds / packed counts");
+    for (hipEvent_t& e : g->ls_cev)
+        if (!e) HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : g->ls_ev)
         if (!e) HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!g->stream2) HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
@@ -4207,6 +4366,20 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.pcnt = (uint32_t*)w.take(sizeof(uint32_t) * kLrG * kLrParts);
         a.pcur = (uint32_t*)w.take(sizeof(uint32_t) * kLrParts);
         a.out_pair = (int2*)w.take(sizeof(int2) * (size_t)cap);
+        // levels of >= pack_min pairs go to the host packed (HGX_LS_PACK_MIN, read per call: tests pack tiny levels)
+        a.pack_min = std::getenv("HGX_LS_PACK_MIN") ? std::max<int64_t>(1, std::atoll(std::getenv("HGX_LS_PACK_MIN")))
+                                                    : (int64_t)1 << 20;
+        a.pack_min = std::max<int64_t>(a.pack_min, 1);
+        if (a.pack_min <= cap) {
+            a.patom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
+            a.pclink = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
+            a.pwcap = cap / 64 + 2;
+            a.pbcap = cap / kLpBlk + 2;
+            a.pflag = (u64*)w.take(sizeof(u64) * 2 * kLrParts * (size_t)a.pwcap);
+            a.pbb = (uint32_t*)w.take(sizeof(uint32_t) * 2 * kLrParts * (size_t)a.pbcap);
+        } else {
+            a.pack_min = INT64_MAX;   // no level can reach it
+        }
         a.seedcnt = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)kLsMaxW * 64);
         a.runs = (int64_t*)w.take(sizeof(int64_t) * 3 * (size_t)rcap);
         a.hbits = hbits;
@@ -4274,9 +4447,16 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             hgx_lr_count<<<kLrG, 256, 0, st>>>(a, d);
             hgx_lr_scan<<<1, 1024, 0, st>>>(a, d, base + (u64)d + 1);
             hgx_lr_split<<<kLrG, 256, 0, st>>>(a, d);   // (the count's block ranges)
+            // the packed parts' run bits / block counts of level d - 2 (same parity) must have reached the host
+            if (d >= 2 && a.pack_min != INT64_MAX) HGX_HIP(hipStreamWaitEvent(st, g->ls_cev[d & 1], 0));
             for (int q = 0; q < kLrParts; ++q) {
                 hgx_lr_scatter<<<lr_scatter_g, 256, 0, st>>>(a, d, q);
                 hgx_lr_rank<<<lr_rank_g, 256, 0, st>>>(a, d, q);
+                if (a.pack_min != INT64_MAX) {
+                    hgx_lr_pflag<<<kLrG, 256, 0, st>>>(a, d, q);
+                    hgx_lr_pscan<<<1, 1024, 0, st>>>(a, d, q, base + (u64)d + 1);
+                    hgx_lr_pemit<<<kLrG, 256, 0, st>>>(a, d, q);
+                }
                 HGX_HIP(hipEventRecord(g->ls_ev[kLrParts * (d & 1) + q], st));
             }
             HGX_CHECK_LAUNCH();
@@ -4284,9 +4464,17 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         // each level's pairs go to the host on the copy stream as soon as the host has read the level's
         // size: a host buffer per level, one copy per rank part after that part's event (the last level's
         // copies overlap its later rank parts and the final runs pass)
+        struct LevelPart {   // a packed level's rank part in the level buffer
+            int64_t b, e;
+            const int32_t* link;
+            const u64* flags;
+            const uint32_t* bb;
+        };
         struct LevelBuf {
             PoolBuf b;
             int64_t out0, n;
+            bool packed = false;
+            std::vector<LevelPart> parts;
         };
         std::vector<LevelBuf> lbufs;
         struct GiveBack {   // an attempt that fails returns its level buffers after the copies drained
@@ -4301,19 +4489,71 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 for (auto& x : *v) g->seq_hbufs.push_back(x.b);
             }
         } give_back{g, cs, &lbufs};
+        // waits for a mapped word the device stores with seq (the stream is asked every 1024 polls)
+        auto wait_seq = [&](const u64* p, u64 want, const char* what) {
+            for (unsigned spin = 0; __atomic_load_n(p, __ATOMIC_ACQUIRE) != want; ++spin) {
+                if ((spin & 1023u) != 1023u) continue;
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipErrorNotReady) continue;
+                if (e != hipSuccess) HGX_HIP(e);
+                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) != want) fail(HGX_E_DEVICE, std::string("hgx_bfs_sequence: ") + what);
+            }
+        };
         auto copy_level = [&](int32_t d, int64_t out0, int64_t n) {
-            PoolBuf hb = take_host_buf(g, 8 * (size_t)n);   // (link, atom) interleaved
-            lbufs.push_back({hb, out0, n});
-            int2* hp = (int2*)hb.p;
             const u64* bnd = g->seq_flag + 8 + (kLrParts + 1) * (d & 1);
+            if (n < a.pack_min) {
+                PoolBuf hb = take_host_buf(g, 8 * (size_t)n);   // (link, atom) interleaved
+                lbufs.push_back({hb, out0, n});
+                int2* hp = (int2*)hb.p;
+                for (int q = 0; q < kLrParts; ++q) {
+                    const int64_t b = (int64_t)bnd[q], e = (int64_t)bnd[q + 1];
+                    if (b < 0 || e > n || e < b) fail(HGX_E_DEVICE, "hgx_bfs_sequence: rank-part bounds inconsistent");
+                    if (e == b) continue;
+                    HGX_HIP(hipStreamWaitEvent(cs, g->ls_ev[kLrParts * (d & 1) + q], 0));
+                    HGX_HIP(hipMemcpyAsync(hp + b, a.out_pair + out0 + b, sizeof(int2) * (size_t)(e - b),
+                                           hipMemcpyDeviceToHost, cs));
+                }
+                HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
+                return;
+            }
+            // packed: atoms [n] | run links [n] | run-start words [n / 64 + kLrParts + 1] | block counts
+            const size_t nw = (size_t)(n / 64 + kLrParts + 1), nbb = (size_t)(n / kLpBlk + kLrParts + 1);
+            PoolBuf hb = take_host_buf(g, 8 * (size_t)n + 8 * nw + 4 * nbb);
+            LevelBuf lb{hb, out0, n, true, {}};
+            int32_t* h_atom = (int32_t*)hb.p;
+            int32_t* h_link = h_atom + n;
+            u64* h_flag = (u64*)(h_link + n);
+            uint32_t* h_bb = (uint32_t*)(h_flag + nw);
             for (int q = 0; q < kLrParts; ++q) {
                 const int64_t b = (int64_t)bnd[q], e = (int64_t)bnd[q + 1];
                 if (b < 0 || e > n || e < b) fail(HGX_E_DEVICE, "hgx_bfs_sequence: rank-part bounds inconsistent");
                 if (e == b) continue;
-                HGX_HIP(hipStreamWaitEvent(cs, g->ls_ev[kLrParts * (d & 1) + q], 0));
-                HGX_HIP(hipMemcpyAsync(hp + b, a.out_pair + out0 + b, sizeof(int2) * (size_t)(e - b),
-                                       hipMemcpyDeviceToHost, cs));
+                const u64* hp = g->seq_flag + kPackWords + 2 * ((d & 1) * kLrParts + q);
+                wait_seq(hp + 1, base + (u64)d + 1, "a packed part's run count never arrived");
+                const int64_t runs = (int64_t)__atomic_load_n(hp, __ATOMIC_RELAXED);
+                const int64_t np = e - b, pw = (np + 63) / 64, pbk = (np + kLpBlk - 1) / kLpBlk;
+                if (runs < 1 || runs > np) fail(HGX_E_DEVICE, "hgx_bfs_sequence: packed part inconsistent");
+                // a part's words / block counts start after the earlier parts' (b / 64 + q >= their end)
+                u64* hf = h_flag + b / 64 + q;
+                uint32_t* hbk = h_bb + b / kLpBlk + q;
+                const hipStream_t c = cs;
+                const int64_t slot = (int64_t)(d & 1) * kLrParts + q;
+                HGX_HIP(hipStreamWaitEvent(c, g->ls_ev[kLrParts * (d & 1) + q], 0));
+                // the copies start at a 64-byte boundary of the level (out0 + b0): the extra leading atoms are
+                // the previous part's, already final (same values), the extra leading links fall in the previous
+                // part's link area past its runs or are its own final values
+                const int64_t b0 = std::max<int64_t>(0, ((out0 + b) & ~(int64_t)15) - out0);
+                static const bool align = !(std::getenv("HGX_LS_PACK_ALIGN") && std::atoi(std::getenv("HGX_LS_PACK_ALIGN")) == 0);   // A/B
+                const int64_t bc = align ? b0 : b;
+                HGX_HIP(hipMemcpyAsync(h_atom + bc, a.patom + out0 + bc, sizeof(int32_t) * (size_t)(e - bc), hipMemcpyDeviceToHost, c));
+                HGX_HIP(hipMemcpyAsync(h_link + bc, a.pclink + out0 + bc, sizeof(int32_t) * (size_t)(b + runs - bc),
+                                       hipMemcpyDeviceToHost, c));
+                HGX_HIP(hipMemcpyAsync(hf, a.pflag + slot * a.pwcap, sizeof(u64) * (size_t)pw, hipMemcpyDeviceToHost, c));
+                HGX_HIP(hipMemcpyAsync(hbk, a.pbb + slot * a.pbcap, sizeof(uint32_t) * (size_t)pbk, hipMemcpyDeviceToHost, c));
+                lb.parts.push_back({b, e, h_link + b, hf, hbk});
             }
+            HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
+            lbufs.push_back(std::move(lb));
         };
         int64_t total = 0, status = 0;
         int32_t dw = 0, enq = 0;
@@ -4381,13 +4621,28 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         seq_mark("level kernels done");
         spin_sync(cs);
         seq_mark("pair copies done");
-        // a pair index -> its level buffer (levels are consecutive ranges of [0, total))
-        auto at_pair = [&](int64_t b, int32_t*& pl, int32_t*& pa) {
+        // a run [b, e) of pairs -> its segments in the level buffer (levels are consecutive ranges of
+        // [0, total); a packed level's run may cross rank parts: a segment per part)
+        auto run_segs = [&](int64_t b, int64_t e, int32_t dist, std::vector<Seg>& out_segs) {
             size_t L = 0;
             while (L + 1 < lbufs.size() && lbufs[L + 1].out0 <= b) ++L;
-            int32_t* hl = (int32_t*)lbufs[L].b.p;
-            pl = hl + 2 * (b - lbufs[L].out0);
-            pa = pl + 1;
+            const LevelBuf& lb = lbufs[L];
+            if (!lb.packed) {
+                const int32_t* pl = (const int32_t*)lb.b.p + 2 * (b - lb.out0);
+                out_segs.push_back({pl, pl + 1, nullptr, e - b, dist, 2});
+                return;
+            }
+            const int64_t rb = b - lb.out0, re = e - lb.out0;
+            const int32_t* h_atom = (const int32_t*)lb.b.p;
+            for (const LevelPart& pt : lb.parts) {
+                const int64_t lo = std::max(rb, pt.b), hi = std::min(re, pt.e);
+                if (hi <= lo) continue;
+                Seg sg{pt.link, h_atom + lo, nullptr, hi - lo, dist, 0};
+                sg.flags = pt.flags;
+                sg.bb = pt.bb;
+                sg.pi = lo - pt.b;
+                out_segs.push_back(sg);
+            }
         };
         // runs partition [0, total) in pair order; each seed's runs in distance order are its pairs
         std::vector<int64_t> ord((size_t)nruns);
@@ -4412,9 +4667,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             for (auto& dk : per[s]) {
                 const int64_t k = dk.second, b = hr[3 * ord[k] + 2];
                 const int64_t e = k + 1 < nruns ? hr[3 * ord[k + 1] + 2] : total;
-                int32_t *pl = nullptr, *pa = nullptr;
-                at_pair(b, pl, pa);
-                out.segs[(size_t)(seed0 + s)].push_back({pl, pa, nullptr, e - b, (int32_t)dk.first, 2});
+                run_segs(b, e, (int32_t)dk.first, out.segs[(size_t)(seed0 + s)]);
                 out.deepest = std::max(out.deepest, (int32_t)dk.first);
             }
         }

@@ -283,6 +283,71 @@ def test_level_engine_pull_and_push_levels_agree(case):
     snap.close()
 
 
+@pytest.mark.parametrize("case", range(3))
+def test_level_engine_packed_transfer(case):
+    """Round 5: large levels go to the host packed (atoms, run-start bits, the links of run starts, block
+    run counts; HGX_LS_PACK_MIN, default 2^20 pairs).  Packing every level (1) gives the unpacked engine's
+    exact sequences and the oracle's, through the whole-result readout and through ranged reads whose
+    windows start anywhere (inside a run of one link, at a rank-part boundary); one seed, repeated links and
+    > 64 seeds included."""
+    import ctypes as C
+    from hypergraphdb_amd import synth
+    from hypergraphdb_amd._lib import check, lib, ptr
+    rng = np.random.default_rng(970 + case)
+    g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=70 + case) if case else \
+        K.random_graph(rng, 2000, 2500, max_arity=9, link_targets=True, n_types=2)
+    snap, orc = snapshot(g), oracle(g)
+    seeds = rng.integers(0, g["num_atoms"], [1, 70, 130][case]).astype(np.int32)
+    for mi, mode in enumerate(K.ALGEN_MODES[:3]):
+        for maxd in (2, None):
+            gn = gen(snap, mode, -1)
+            a = _seq_env(snap, seeds, maxd, gn, {"HGX_LS_PACK_MIN": 1 << 40})
+            b = _seq_env(snap, seeds, maxd, gn, {"HGX_LS_PACK_MIN": 1})
+            assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd)
+            assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd)
+            assert np.array_equal(a.dists, b.dists) and a.traversed_edges == b.traversed_edges, (case, mi, maxd)
+            for i in range(0, len(seeds), max(1, len(seeds) // 4)):
+                l_, at, d, _ = orc.bfs(int(seeds[i]), -1 if maxd is None else maxd, algen(-1, *mode))
+                gl, ga, gd = b.pairs(i)
+                assert np.array_equal(ga, at) and np.array_equal(gl, l_) and np.array_equal(gd, d), (case, mi, maxd, i)
+    # ranged reads of a packed result: every start position of a sample, short and long windows
+    from hypergraphdb_amd import _lib
+    old = os.environ.get("HGX_LS_PACK_MIN")
+    os.environ["HGX_LS_PACK_MIN"] = "1"
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
+    h = C.c_void_p()
+    try:
+        opts = gen(snap, K.ALGEN_MODES[0], -1).options()
+        check(lib().hgx_bfs_sequence(snap.handle, ptr(seeds), len(seeds), -1, C.byref(opts), C.byref(h)))
+    finally:
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+        if old is None:
+            del os.environ["HGX_LS_PACK_MIN"]
+        else:
+            os.environ["HGX_LS_PACK_MIN"] = old
+    try:
+        ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
+        check(lib().hgx_seq_result_info(h, C.byref(ns), C.byref(npairs), C.byref(nl)))
+        n = npairs.value
+        links, atoms, dists = (np.empty(max(n, 1), np.int32) for _ in range(3))
+        check(lib().hgx_seq_result_pairs(h, ptr(links), ptr(atoms), ptr(dists)))
+        vp = lambda x: C.c_void_p(ptr(x))
+        starts = sorted(set(rng.integers(0, max(n, 1), 200).tolist() + [0, max(n - 1, 0)]))
+        for first in starts:
+            for win in (1, 7, 700):
+                wl, wa, wd = (np.empty(win, np.int32) for _ in range(3))
+                got = C.c_int64()
+                check(lib().hgx_seq_result_pairs_range(h, C.c_int64(first), C.c_int64(win), vp(wl), vp(wa), vp(wd),
+                                                       C.byref(got)))
+                k = got.value
+                assert k == min(win, n - first)
+                assert np.array_equal(wl[:k], links[first:first + k]), (case, first, win)
+                assert np.array_equal(wa[:k], atoms[first:first + k]) and np.array_equal(wd[:k], dists[first:first + k])
+    finally:
+        lib().hgx_seq_result_free(h)
+    snap.close()
+
+
 def test_level_engine_chunk_split_on_wide_keys():
     """A level whose stream keys do not fit 32 bits splits the chunk (HGX_LS_TLIMIT lowers the limit to
     force it down to single seeds; a single seed that still does not fit runs on the key-array engine):
