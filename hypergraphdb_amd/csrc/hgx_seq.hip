@@ -3967,9 +3967,21 @@ inline void copy_pairs(const Seg& s, int64_t so, int64_t n, int32_t* links, int3
         c += __builtin_popcountll(s.flags[i >> 6] & (bit == 63 ? ~0ull : (2ull << bit) - 1ull)) - 1;
         int64_t k = 0;
         links[k++] = s.link[c];
-        for (++i; k < n; ++i, ++k) {
-            c += (int64_t)((s.flags[i >> 6] >> (i & 63)) & 1ull);
-            links[k] = s.link[c];
+        ++i;
+        while (k < n) {   // a run-start word at a time: a word without run starts is one fill
+            const int b0 = (int)(i & 63);
+            const int64_t m = std::min<int64_t>(n - k, 64 - b0);
+            const u64 f = (s.flags[i >> 6] >> b0) & (m == 64 ? ~0ull : (1ull << m) - 1ull);
+            if (!f) {
+                std::fill(links + k, links + k + m, s.link[c]);
+            } else {
+                for (int64_t j = 0; j < m; ++j) {
+                    c += (int64_t)((f >> j) & 1ull);
+                    links[k + j] = s.link[c];
+                }
+            }
+            k += m;
+            i += m;
         }
         return;
     }
