@@ -772,6 +772,18 @@ def main():
         dry_run(args)
         return
 
+    # a progress line every 30 s on stderr: the CPU-baseline legs run minutes inside one C call (16
+    # complete config-2 traversals: ~70-110 s) and a silent run of 3 minutes is taken for a hung one
+    import threading
+    t_start = time.time()
+
+    def heartbeat():
+        while True:
+            time.sleep(30)
+            log(f"still running ({time.time() - t_start:.0f} s)")
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+
     from hypergraphdb_amd import dist as hdist
     from hypergraphdb_amd._lib import device_count, device_synchronize
 
