@@ -3951,6 +3951,7 @@ struct Seg {
     const u64* flags = nullptr;
     const uint32_t* bb = nullptr;
     int64_t pi = 0;
+    hipEvent_t ready = nullptr;   // the copy into its buffer (level engine): readers wait for it
 };
 
 // n pairs of a segment from index so on into links / atoms (either may be null): two copies, or one pass
@@ -4009,6 +4010,7 @@ inline void copy_pairs(const Seg& s, int64_t so, int64_t n, int32_t* links, int3
 struct SeqOut {
     std::vector<std::vector<Seg>> segs;   // [n seeds]
     std::vector<PoolBuf> bufs;
+    std::vector<hipEvent_t> evs;          // the segments' copy events (owned; waited for before bufs go back)
     double traversed = 0;
     int32_t deepest = 0;
     double bytes = 0;                     // the level engine's algorithmic bytes (kernel counters)
@@ -4481,12 +4483,33 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             const int32_t* link;
             const u64* flags;
             const uint32_t* bb;
+            hipEvent_t ready;
         };
         struct LevelBuf {
             PoolBuf b;
             int64_t out0, n;
             bool packed = false;
             std::vector<LevelPart> parts;
+            hipEvent_t ready = nullptr;   // (unpacked: after all its copies)
+        };
+        // the pair copies complete after the call returns (the readers wait per segment): an event after
+        // each copy group, owned by the result
+        std::vector<hipEvent_t> cevs;
+        struct EvGuard {   // an attempt that fails drops its events
+            std::vector<hipEvent_t>* v;
+            bool keep = false;
+            ~EvGuard() {
+                if (keep) return;
+                for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+                v->clear();
+            }
+        } ev_guard{&cevs};
+        auto new_copy_event = [&]() {
+            hipEvent_t e = nullptr;
+            HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            cevs.push_back(e);
+            HGX_HIP(hipEventRecord(e, cs));
+            return e;
         };
         std::vector<LevelBuf> lbufs;
         struct GiveBack {   // an attempt that fails returns its level buffers after the copies drained
@@ -4526,6 +4549,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                                            hipMemcpyDeviceToHost, cs));
                 }
                 HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
+                lbufs.back().ready = new_copy_event();
                 return;
             }
             // packed: atoms [n] | run links [n] | run-start words [n / 64 + kLrParts + 1] | block counts
@@ -4562,7 +4586,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                                        hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(hf, a.pflag + slot * a.pwcap, sizeof(u64) * (size_t)pw, hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(hbk, a.pbb + slot * a.pbcap, sizeof(uint32_t) * (size_t)pbk, hipMemcpyDeviceToHost, c));
-                lb.parts.push_back({b, e, h_link + b, hf, hbk});
+                lb.parts.push_back({b, e, h_link + b, hf, hbk, new_copy_event()});
             }
             HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
             lbufs.push_back(std::move(lb));
@@ -4615,6 +4639,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         const int64_t nruns = ctl[kLsRuns];
         give_back.keep = true;
         for (auto& x : lbufs) out.bufs.push_back(x.b);
+        ev_guard.keep = true;
+        for (hipEvent_t e : cevs) out.evs.push_back(e);
         out.traversed += (double)ctl[kLsTrav];
         out.bytes += (double)ctl[kLsBytes];
         out.pull_levels += ctl[kLsPullN];
@@ -4631,8 +4657,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         if (nruns) HGX_HIP(hipMemcpyAsync(hr, a.runs, sizeof(int64_t) * 3 * (size_t)nruns, hipMemcpyDeviceToHost, st));
         spin_sync(st);
         seq_mark("level kernels done");
-        spin_sync(cs);
-        seq_mark("pair copies done");
+        // the copies run on: later work on this stream (the scratch buffers' next users) waits for them, the
+        // readers wait per segment (Seg::ready), the result's free waits for all of them
+        if (!cevs.empty()) HGX_HIP(hipStreamWaitEvent(st, cevs.back(), 0));
         // a run [b, e) of pairs -> its segments in the level buffer (levels are consecutive ranges of
         // [0, total); a packed level's run may cross rank parts: a segment per part)
         auto run_segs = [&](int64_t b, int64_t e, int32_t dist, std::vector<Seg>& out_segs) {
@@ -4641,7 +4668,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             const LevelBuf& lb = lbufs[L];
             if (!lb.packed) {
                 const int32_t* pl = (const int32_t*)lb.b.p + 2 * (b - lb.out0);
-                out_segs.push_back({pl, pl + 1, nullptr, e - b, dist, 2});
+                Seg sg{pl, pl + 1, nullptr, e - b, dist, 2};
+                sg.ready = lb.ready;
+                out_segs.push_back(sg);
                 return;
             }
             const int64_t rb = b - lb.out0, re = e - lb.out0;
@@ -4653,6 +4682,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 sg.flags = pt.flags;
                 sg.bb = pt.bb;
                 sg.pi = lo - pt.b;
+                sg.ready = pt.ready;
                 out_segs.push_back(sg);
             }
         };
@@ -5442,14 +5472,35 @@ struct hgx_seq_result {
     SeqOut lev;                     // the level-synchronous engine's seeds (indexed by rerun order)
     std::vector<int32_t> lev_of;    // [n_seeds] index into lev.segs, or -1
     hgx_graph* g = nullptr;
-    double ms_total = 0, traversed = 0;
+    mutable double ms_total = 0;
+    double traversed = 0;
     double ms_block = 0, bytes_block = 0;   // the workgroup engine's launches: device ms, algorithmic bytes
-    double ms_level = 0;                    // the level-synchronous engine: device ms (timing on) ...
+    mutable double ms_level = 0;            // the level-synchronous engine: device ms (timing on) ...
+    // timing events of a call whose pair copies were still running when it returned (read on first use)
+    mutable hipEvent_t lz_ev0 = nullptr, lz_ev1 = nullptr, lz_el0 = nullptr, lz_el1 = nullptr;
+    void settle() const {
+        float ms = 0;
+        if (lz_el1 && hipEventSynchronize(lz_el1) == hipSuccess && hipEventElapsedTime(&ms, lz_el0, lz_el1) == hipSuccess)
+            ms_level = ms;
+        if (lz_ev1 && hipEventSynchronize(lz_ev1) == hipSuccess && hipEventElapsedTime(&ms, lz_ev0, lz_ev1) == hipSuccess)
+            ms_total = ms;
+        for (hipEvent_t* e : {&lz_ev0, &lz_ev1, &lz_el0, &lz_el1})
+            if (*e) {
+                (void)hipEventDestroy(*e);
+                *e = nullptr;
+            }
+    }
     double ms_coop = 0, bytes_coop = 0;     // the order-exact grid stage (hgx_seq_coop): device ms, algorithmic bytes
     int32_t n_coop = 0;                     //   and the seeds it finished
     int32_t n_block = 0, n_level = 0;       // seeds finished by each engine
     ~hgx_seq_result() {
         if (!g) return;
+        settle();
+        for (hipEvent_t e : lev.evs) {   // the level buffers' copies must have landed before they are reused
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
+        lev.evs.clear();
         {
             std::lock_guard<std::mutex> lk(g->seq_mu);
             for (auto& b : hbufs) g->seq_hbufs.push_back(b);
@@ -5647,7 +5698,11 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             }
         }
         if (!done) seq_levels_all(g, rs.data(), (int32_t)rs.size(), maxd, o, r->lev, g->seq_engine != 1);
-        if (el0) {
+        if (el0 && !r->lev.evs.empty()) {   // the pair copies are still running: timed on first use
+            HGX_HIP(hipEventRecord(el1, st));
+            r->lz_el0 = el0;
+            r->lz_el1 = el1;
+        } else if (el0) {
             HGX_HIP(hipEventRecord(el1, st));
             HGX_HIP(hipEventSynchronize(el1));
             float ms = 0;
@@ -5665,7 +5720,11 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             r->lev_of[rerun[k]] = (int32_t)k;
         }
     }
-    if (g->timing) {
+    if (g->timing && !r->lev.evs.empty()) {
+        HGX_HIP(hipEventRecord(ev1, st));
+        r->lz_ev0 = ev0;
+        r->lz_ev1 = ev1;
+    } else if (g->timing) {
         HGX_HIP(hipEventRecord(ev1, st));
         HGX_HIP(hipEventSynchronize(ev1));
         seq_mark("timing event done");
@@ -5743,8 +5802,13 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
         hint(atoms, nb);
         hint(dists, nb);
     }
+    std::atomic<bool> copy_failed{false};
     auto run = [&](const Job& j) {
         const Seg& s = *j.s;
+        if (s.ready && hipEventSynchronize(s.ready) != hipSuccess) {   // its copy may still be running
+            copy_failed = true;
+            return;
+        }
         const int64_t o = j.b + j.lo;
         copy_pairs(s, j.lo, j.n, links ? links + o : nullptr, atoms ? atoms + o : nullptr);
         if (dists) {
@@ -5753,6 +5817,7 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
         }
     };
     host_parallel((int64_t)jobs.size(), r->off.back() >= ((int64_t)1 << 24), [&](int64_t k) { run(jobs[(size_t)k]); });
+    if (copy_failed) fail(HGX_E_DEVICE, "hgx_seq_result_pairs: a pair copy failed");
     HGX_API_END
 }
 
@@ -5768,6 +5833,7 @@ int hgx_seq_result_pairs_range(const hgx_seq_result* r, int64_t first, int64_t n
         const int64_t lo_ = std::max(b, first), hi_ = std::min(b + s.n, hi);
         if (hi_ <= lo_) return;
         const int64_t k = hi_ - lo_, so = lo_ - b, o = lo_ - first;
+        if (s.ready) HGX_HIP(hipEventSynchronize(s.ready));
         copy_pairs(s, so, k, links ? links + o : nullptr, atoms ? atoms + o : nullptr);
         if (dists) {
             if (s.dist) std::memcpy(dists + o, s.dist + so, sizeof(int32_t) * k);
@@ -5795,6 +5861,7 @@ int hgx_seq_result_pairs_range(const hgx_seq_result* r, int64_t first, int64_t n
 int hgx_seq_result_stats(const hgx_seq_result* r, double* ms_total, double* traversed_edges) {
     HGX_API_BEGIN
     if (!r) fail(HGX_E_INVALID, "null result");
+    r->settle();
     if (ms_total) *ms_total = r->ms_total;
     if (traversed_edges) *traversed_edges = r->traversed;
     HGX_API_END
@@ -5823,6 +5890,7 @@ int hgx_seq_result_grid_stats(const hgx_seq_result* r, int32_t* n_seeds, double*
 int hgx_seq_result_level_stats(const hgx_seq_result* r, double* ms_level, double* bytes_level, int64_t* pull_levels) {
     HGX_API_BEGIN
     if (!r) fail(HGX_E_INVALID, "null result");
+    r->settle();
     if (ms_level) *ms_level = r->ms_level;
     if (bytes_level) *bytes_level = r->lev.bytes;
     if (pull_levels) *pull_levels = r->lev.pull_levels;
