@@ -303,7 +303,10 @@ void hgx_bfs_result_free(hgx_bfs_result *r);
 /* Order-exact traversal: for every seed the exact sequence of (link, atom) pairs that
  * HGBreadthFirstTraversal(seeds[i], gen, max_depth).next() returns, in the reference's FIFO order
  * (C/algorithms/HGBreadthFirstTraversal.java:49-66,143-156), plus the distance of each atom.
- * The link of a pair is the link through which the atom was first discovered. */
+ * The link of a pair is the link through which the atom was first discovered.
+ * Large results may still be arriving from the device when hgx_bfs_sequence returns: the readers
+ * (hgx_seq_result_pairs / _pairs_range) wait for the part they read, the stats functions for the timing,
+ * and hgx_seq_result_free for every copy; a later call on the same graph is ordered after them. */
 typedef struct hgx_seq_result hgx_seq_result;
 int  hgx_bfs_sequence(hgx_graph *g, const int32_t *seeds, int32_t n_seeds, int32_t max_depth,
                       const hgx_algen_opts *opts, hgx_seq_result **out);
