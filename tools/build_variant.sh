@@ -7,7 +7,10 @@ set -eu
 NAME=$1
 shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-W=$(mktemp -d /tmp/hgxvar.XXXX)
+T=$(mktemp -d /tmp/hgxvar.XXXX)
+W=$T/pkg/csrc   # hgx_internal.h includes ../../include/hgx.h
+mkdir -p "$W"
+ln -s "$ROOT/include" "$T/include"
 cp "$ROOT"/hypergraphdb_amd/csrc/*.hip "$ROOT"/hypergraphdb_amd/csrc/*.h "$W"/
 for f in "$@"; do cp "$f" "$W/$(basename "$f")"; done
 mkdir -p "$ROOT/tools/native/build"
@@ -18,5 +21,5 @@ done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/native/build/libhgx_$NAME.so" hgx_*.o \
     -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -rf "$W"
+rm -rf "$T"
 echo "built tools/native/build/libhgx_$NAME.so"
