@@ -78,12 +78,12 @@ class AndQuery(C.Structure):
 
 
 KERNELS = ("hgx_link_gather", "hgx_atom_pull", "hgx_atom_pull_heavy", "hgx_hub_finalize", "hgx_frontier_push",
-           "hgx_nf_pull")
+           "hgx_nf_pull", "hgx_fc_pull", "hgx_fc_pull_heavy")
 
 
 class BfsStats(C.Structure):
     _fields_ = [("n_levels_expanded", C.c_int32), ("n_batches", C.c_int32), ("ms_total", C.c_double),
-                ("ms_kernel", C.c_double * 6), ("launches", C.c_int64 * 6), ("bytes_kernel", C.c_double * 6),
+                ("ms_kernel", C.c_double * 8), ("launches", C.c_int64 * 8), ("bytes_kernel", C.c_double * 8),
                 ("bytes_survey", C.c_double), ("traversed_edges", C.c_double),
                 ("union_frontier", C.c_int64 * 64), ("level_ms", C.c_double * 64), ("level_new", C.c_int64 * 64),
                 ("level_bytes", C.c_double * 64), ("level_sparse", C.c_int32 * 64),

@@ -1952,6 +1952,456 @@ __global__ void __launch_bounds__(256) hgx_nf_pull(const int32_t* __restrict__ l
     wave_add_sh(ctr + cNfRows, n_rows);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Frontier-code pull (round 6; symmetric-mode dense levels over a SMALL frontier, HGX_OPT_BFS_FLAGS
+// bit 17).  Config 2's level 1 expands 235K frontier atoms whose incidence covers nearly every link:
+// the gather wrote a 128-byte lf row for each of the 40M links and the pull read one such row at
+// random per incidence entry (200M x 128 B from a 5 GB table: 33 GB of the level's traffic).  Here
+// the pull reads, per incidence entry (t, L) in entry order, a 32-byte record of L's targets
+// (hgx_fc_rec, built once per snapshot), probes their frontier bits and ORs the frontier rows of
+// the targets into t's accumulator:
+//   next(t) = OR_{L in inc(t)} OR_{u in L, u in F_d} lvl_d[u]  minus vis[t]
+// (t's own row is a subset of vis[t]).  Most frontier rows are sparse (~1.2 source bits), so each
+// becomes a 64-bit CODE of up to kFcIds 10-bit source ids (hgx_fc_codes) in a compact array indexed
+// through a per-word prefix of the frontier bitmap; codes and prefixes stay in L2, the records stream.
+// The few rows with more bits (config 2 level 1: 912 atoms, but half of the (entry, frontier target)
+// pairs -- they are the hubs) get a DENSE SLOT: an entry sets the slot's bit in its atom's dense mask
+// (one LDS atomic, as a source id), and the atom ORs the dense rows of its mask once, at the end.  Past
+// kFcDenseCap dense rows a code names its atom and the pair ORs the whole row (slow, exact).
+// ---------------------------------------------------------------------------------------------
+constexpr int kFc = 1 << 17;            // HGX_OPT_BFS_FLAGS bit 17: frontier-code pull levels
+constexpr int kFcIds = 6;               // source ids per code (6 x 10 bits + a 3-bit count)
+constexpr u64 kFcDense = 1ull << 63;    // code flag: more than kFcIds bits; low bits = dense slot
+constexpr u64 kFcRow = 1ull << 62;      //   with kFcDense: no slot left; low 32 bits = the atom (row in lvl_d)
+constexpr int kFcDenseCap = 1024;       // dense slots per level
+constexpr int kFcDW = kFcDenseCap / 64; // dense-mask words per atom
+constexpr int kFcTile = 128;            // atoms per workgroup tile of hgx_fc_pull (256 threads)
+constexpr int kFcHubs = 2048;           // hub slots: the snapshot's highest-degree atoms, looked up in LDS
+
+// Entry i = (t, L) of the incidence: the targets of link inc_row[i] other than t (t's own row is a subset
+// of vis[t]), -1 padded; a target that is one of the snapshot's kFcHubs hubs (hubs[], ascending) is
+// stored as -2 - its hub slot, so the pull finds its frontier code in LDS (a hub is a target of a large
+// share of the links: config 2's top 2048 atoms hold ~30% of the pins and most frontier hits).  A thread
+// per entry (its atom by binary search over inc_off: built once per snapshot).  A link of arity > 8 sets
+// *over (the snapshot then has no records and the level keeps gather + pull).
+__global__ void __launch_bounds__(256) hgx_fc_rec(int64_t A, int64_t I, const int64_t* __restrict__ inc_off,
+                                                  const int32_t* __restrict__ inc_row,
+                                                  const int64_t* __restrict__ tgt_off,
+                                                  const int32_t* __restrict__ tgt_idx, const int32_t* __restrict__ hubs,
+                                                  int32_t n_hubs, int4* __restrict__ rec, unsigned int* __restrict__ over) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = A;   // inc_off[lo] <= i < inc_off[hi]
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (inc_off[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const int32_t self = (int32_t)lo;
+        const int32_t L = inc_row[i];
+        const int64_t b = tgt_off[L];
+        const int64_t n = tgt_off[L + 1] - b;
+        if (n > 8) atomicOr(over, 1u);
+        int32_t t[8];
+        int m = 0;
+        for (int q = 0; q < 8 && q < n; ++q) {
+            const int32_t u = tgt_idx[b + q];
+            if (u == self) continue;
+            int a = 0, z = n_hubs;   // hubs[a] <= u < hubs[z]
+            while (z - a > 1) {
+                const int mid = (a + z) >> 1;
+                if (hubs[mid] <= u) a = mid;
+                else z = mid;
+            }
+            t[m++] = (n_hubs > 0 && hubs[a] == u) ? -2 - a : u;
+        }
+        for (; m < 8; ++m) t[m] = -1;
+        rec[2 * i] = make_int4(t[0], t[1], t[2], t[3]);
+        rec[2 * i + 1] = make_int4(t[4], t[5], t[6], t[7]);
+    }
+}
+
+// The frontier code of every hub slot this level (0: the hub is not on the frontier).
+__global__ void __launch_bounds__(256) hgx_fc_hubs(int32_t n_hubs, const int32_t* __restrict__ hubs,
+                                                   const u64x2* __restrict__ fw, const u64* __restrict__ fcode,
+                                                   u64* __restrict__ hubtab) {
+    for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < n_hubs; h += gridDim.x * blockDim.x) {
+        const int32_t u = hubs[h];
+        const u64x2 f = fw[u >> 6];
+        const bool on = (f.x >> (u & 63)) & 1ull;
+        hubtab[h] = on ? fcode[f.y + __popcll(f.x & ((1ull << (u & 63)) - 1ull))] : 0ull;
+    }
+}
+
+// degrees of n atoms (the hub choice)
+__global__ void __launch_bounds__(256) hgx_fc_deg(int64_t n, const int32_t* __restrict__ atoms,
+                                                  const int64_t* __restrict__ inc_off, int64_t* __restrict__ deg) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        deg[k] = inc_off[atoms[k] + 1] - inc_off[atoms[k]];
+}
+
+// fw[w] = (fa[w], code slot of the first frontier atom of word w): one 16-byte load answers both "is
+// v on the frontier" and "where is its code" (slot = fw[w].y + popcount(fa[w] below bit v & 63)).  Slots
+// are dense, assigned a block of 256 words at a time with one atomic (not in atom order).
+__global__ void __launch_bounds__(256) hgx_fc_slots(int64_t nwords, const u64* __restrict__ fa,
+                                                    u64x2* __restrict__ fw, u64* __restrict__ n_slots) {
+    __shared__ int wsum[4];
+    __shared__ u64 sbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t w0 = (int64_t)blockIdx.x * 256; w0 < nwords; w0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        const int64_t w = w0 + threadIdx.x;
+        const u64 x = w < nwords ? fa[w] : 0ull;
+        const int c = __popcll(x);
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int k = 0; k < 4; ++k) {
+            before += k < wv ? wsum[k] : 0;
+            total += wsum[k];
+        }
+        if (threadIdx.x == 0) sbase = total ? atomicAdd(n_slots, (u64)total) : 0ull;
+        __syncthreads();
+        if (w < nwords) fw[w] = u64x2{x, sbase + (u64)(before + incl - c)};
+        __syncthreads();   // wsum / sbase are rewritten by the next chunk
+    }
+}
+
+// The code of every frontier atom (a thread per atom; only frontier atoms load their row).  Dense rows
+// are copied to drow[slot] (slots from one counter; kFcDenseCap of them).
+template <int W>
+__global__ void __launch_bounds__(256) hgx_fc_codes(int64_t A, const u64x2* __restrict__ fw,
+                                                    const u64* __restrict__ lvl, u64* __restrict__ fcode, int64_t cap,
+                                                    u64* __restrict__ drow, unsigned int* __restrict__ n_dense,
+                                                    u64* __restrict__ ctr) {
+    u64 n_dn = 0;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < A; v += (int64_t)gridDim.x * blockDim.x) {
+        const u64x2 f = fw[v >> 6];
+        const int b = (int)(v & 63);
+        if (!((f.x >> b) & 1ull)) continue;
+        const int64_t slot = (int64_t)f.y + __popcll(f.x & ((1ull << b) - 1ull));
+        if (slot >= cap) continue;   // never (cap = the frontier size); guards the store
+        u64 r[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) r[k] = lvl[v * W + k];
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) cnt += __popcll(r[k]);
+        u64 code;
+        if (cnt > kFcIds) {
+            const unsigned ds = atomicAdd(n_dense, 1u);
+            if (ds < (unsigned)kFcDenseCap) {
+                code = kFcDense | (u64)ds;
+#pragma unroll
+                for (int k = 0; k < W; ++k) drow[(int64_t)ds * W + k] = r[k];
+            } else {
+                code = kFcDense | kFcRow | (u64)v;
+            }
+            ++n_dn;
+        } else {
+            code = (u64)cnt << 60;
+            int m = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                u64 x = r[k];
+                while (x) {
+                    code |= (u64)(k * 64 + __ffsll((long long)x) - 1) << (10 * m);
+                    ++m;
+                    x &= x - 1ull;
+                }
+            }
+        }
+        fcode[slot] = code;
+    }
+    wave_add_sh(ctr + cCand, n_dn);   // (the push levels' counter slot: frontier rows coded dense)
+}
+
+// The frontier contribution of one incidence entry's record: src(word, bits) for every source id of
+// every sparse frontier target, dense(slot) for every dense one, row(atom) past the dense slots.
+// Returns the frontier targets seen (a dependent chain of three loads: record, fw words, codes).
+template <class FS, class FD, class FR>
+__device__ __forceinline__ int fc_entry(const int4* __restrict__ rec, int64_t i, const u64x2* __restrict__ fw,
+                                        const u64* __restrict__ fcode, const u64* hubtab, FS src, FD dense, FR row) {
+    const int4 r0 = rec[2 * i], r1 = rec[2 * i + 1];
+    const int32_t t[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    u64x2 f[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = t[q] >= 0 ? fw[t[q] >> 6] : u64x2{0ull, 0ull};
+    u64 code[8];
+    unsigned hit = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        code[q] = t[q] <= -2 ? hubtab[-2 - t[q]] : 0ull;   // hub slot: its code from LDS (0 = not on the frontier)
+        if (t[q] >= 0 && ((f[q].x >> (t[q] & 63)) & 1ull)) hit |= 1u << q;
+    }
+    unsigned hhit = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (t[q] <= -2 && code[q] != 0ull) hhit |= 1u << q;
+    if (!(hit | hhit)) return 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if ((hit >> q) & 1u) code[q] = fcode[f[q].y + __popcll(f[q].x & ((1ull << (t[q] & 63)) - 1ull))];
+    hit |= hhit;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (!((hit >> q) & 1u)) continue;
+        const u64 c = code[q];
+        if (c & kFcDense) {
+            if (c & kFcRow) row((int64_t)(c & 0xffffffffull));
+            else dense((int)(c & 0xffffull));
+        } else {
+            const int n = (int)((c >> 60) & 7ull);
+            for (int m = 0; m < n; ++m) {
+                const int s = (int)((c >> (10 * m)) & 1023ull);
+                src(s >> 6, 1ull << (s & 63));
+            }
+        }
+    }
+    return __popc(hit);
+}
+
+// OR of the dense rows named by a dense mask into a G-lane group's share of a row (lane sub holds words
+// sub*WPL ..): dm = the kFcDW mask words (LDS, read by every lane of the group).
+template <int W>
+__device__ __forceinline__ typename Vec<Lay<W>::WPL>::T fc_dense_or(const u64* dm, const u64* __restrict__ drow, int sub,
+                                                                     typename Vec<Lay<W>::WPL>::T a) {
+    constexpr int WPL = Lay<W>::WPL;
+    typedef Vec<WPL> V;
+    for (int w = 0; w < kFcDW; ++w) {
+        u64 x = dm[w];
+        while (x) {
+            const int ds = w * 64 + __ffsll((long long)x) - 1;
+            x &= x - 1ull;
+            a |= V::ld(drow + (int64_t)ds * W + sub * WPL);
+        }
+    }
+    return a;
+}
+
+// Light atoms (degree <= kHeavyDegree, not yet visited by every traversal): a workgroup takes a tile
+// of kFcTile consecutive atoms, spreads the tile's incidence entries flat over its 256 threads (an
+// entry's atom by binary search over the tile's degree prefix) and ORs the source bits into the
+// atoms' LDS rows (dense frontier targets: a bit of the atom's LDS dense mask); then a G-lane group per
+// atom adds the dense rows and applies new = acc & ~vis[t] as hgx_atom_pull2 does.  The tile's
+// fa_next / ever / full words belong to the workgroup (plain stores; the hub finalise that follows sets
+// heavy atoms' bits with atomics).
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) hgx_fc_pull(int64_t A, const int64_t* __restrict__ inc_off,
+                                                   const int4* __restrict__ rec, const int32_t* __restrict__ inc_type,
+                                                   int32_t want_type, const u64x2* __restrict__ fw,
+                                                   const u64* __restrict__ fcode, const u64* __restrict__ drow,
+                                                   const u64* __restrict__ hubtab_g, int32_t n_hubs,
+                                                   const u64* __restrict__ lvl, u64* __restrict__ vis,
+                                                   u64* __restrict__ ever, u64* __restrict__ full,
+                                                   u64* __restrict__ lvl_next, u64* __restrict__ fa_next,
+                                                   u64* __restrict__ ctr, FullMask fm, int flags) {
+    constexpr int WPL = Lay<W>::WPL, G = Lay<W>::G, T = kFcTile, NW = T / 64;
+    static_assert(G >= 4, "fc pull needs G >= 4");
+    static_assert(T <= 256 && T % 64 == 0, "tile");
+    typedef Vec<WPL> V;
+    __shared__ u64 acc[T * W];
+    __shared__ u64 dmask[T * kFcDW];
+    __shared__ u64 hubtab[kFcHubs];
+    __shared__ int64_t sbeg[T];
+    __shared__ int32_t spre[T + 1];
+    __shared__ int32_t wsum[4];
+    __shared__ u64 snew[NW], sfull[NW];
+    const bool skip_full = flags & 4;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int sub = tid & (G - 1), gi = tid / G;
+    const typename V::T FULL = full_part<W>(fm, sub);
+    for (int h = tid; h < n_hubs; h += 256) hubtab[h] = hubtab_g[h];   // (the tile loop's barriers order it)
+    u64 n_ent = 0, n_front = 0, n_rows = 0, n_vis = 0, n_newdeg = 0, n_newdeg_nf = 0, n_new = 0, n_full = 0;
+    for (int64_t tile = blockIdx.x; tile * T < A; tile += gridDim.x) {   // block-uniform
+        const int64_t v = tile * T + tid;
+        int64_t b = 0;
+        int d = 0;
+        if (tid < T && v < A && !(skip_full && bit(full, v))) {
+            b = inc_off[v];
+            const int64_t dd = inc_off[v + 1] - b;
+            d = (dd > 0 && dd <= kHeavyDegree) ? (int)dd : 0;
+        }
+        int incl = d;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int k = 0; k < 4; ++k) {
+            before += k < wv ? wsum[k] : 0;
+            total += wsum[k];
+        }
+        if (total == 0) {   // block-uniform: no light entries in the tile (e.g. link atoms without incidence)
+            if (tid < NW && (tile * NW + tid) * 64 < A) fa_next[tile * NW + tid] = 0ull;
+            __syncthreads();   // wsum is rewritten by the next tile
+            continue;
+        }
+        for (int k = tid; k < T * W; k += 256) acc[k] = 0ull;
+        for (int k = tid; k < T * kFcDW; k += 256) dmask[k] = 0ull;
+        if (tid < NW) {
+            snew[tid] = 0ull;
+            sfull[tid] = 0ull;
+        }
+        if (tid < T) {
+            sbeg[tid] = b;
+            spre[tid] = before + incl - d;
+            if (tid == T - 1) spre[T] = before + incl;
+        }
+        __syncthreads();
+        for (int j = tid; j < total; j += 256) {
+            int lo = 0, hi = T;   // spre[lo] <= j < spre[hi]: the entry's atom is lo (its degree is > 0)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (spre[mid] <= j) lo = mid;
+                else hi = mid;
+            }
+            const int64_t i = sbeg[lo] + (j - spre[lo]);
+            if (want_type >= 0 && inc_type[i] != want_type) continue;
+            ++n_ent;
+            u64* arow = acc + lo * W;
+            u64* drm = dmask + lo * kFcDW;
+            n_front += (u64)fc_entry(
+                rec, i, fw, fcode, hubtab, [&](int k, u64 x) { atomicOr(arow + k, x); },
+                [&](int ds) { atomicOr(drm + (ds >> 6), 1ull << (ds & 63)); },
+                [&](int64_t u) {
+                    ++n_rows;
+#pragma unroll 1
+                    for (int k = 0; k < W; ++k) {
+                        const u64 x = lvl[u * W + k];
+                        if (x) atomicOr(arow + k, x);
+                    }
+                });
+        }
+        __syncthreads();
+        for (int a0 = 0; a0 < T; a0 += 256 / G) {   // block-uniform; a G-lane group per atom
+            const int k = a0 + gi;
+            const int64_t t = tile * T + k;
+            const int dk = k < T ? spre[k + 1] - spre[k] : 0;
+            bool isnew = false, becomes_full = false;
+            if (dk > 0) {   // group-uniform
+                const typename V::T a = fc_dense_or<W>(dmask + k * kFcDW, drow, sub, V::ld(acc + k * W + sub * WPL));
+                if (group_any<G>(V::nz(a))) {
+                    const bool ev = bit(ever, t);
+                    const typename V::T old = ev ? V::ld(vis + t * W + sub * WPL) : V::zero();
+                    const typename V::T nw = a & ~old;
+                    if (sub == 0 && ev) ++n_vis;
+                    if (group_any<G>(V::nz(nw))) {
+                        V::st(lvl_next + t * W + sub * WPL, nw);
+                        V::st(vis + t * W + sub * WPL, old | nw);
+                        isnew = true;
+                        becomes_full = group_all<G>(V::eq(old | nw, FULL));
+                    }
+                }
+            }
+            if (sub == 0 && isnew) {
+                atomicOr(&snew[k >> 6], 1ull << (k & 63));
+                if (becomes_full) atomicOr(&sfull[k >> 6], 1ull << (k & 63));
+                n_newdeg += (u64)dk;
+                if (!becomes_full) n_newdeg_nf += (u64)dk;
+            }
+        }
+        __syncthreads();
+        if (tid < NW) {
+            const int64_t w = tile * NW + tid;
+            if (w * 64 < A) {
+                const u64 nw = snew[tid], fw_ = sfull[tid];
+                fa_next[w] = nw;
+                if (nw) ever[w] |= nw;
+                if (fw_) full[w] |= fw_;
+                n_new += (u64)__popcll(nw);
+                n_full += (u64)__popcll(fw_);
+            }
+        }
+        __syncthreads();   // the LDS rows and prefixes are rewritten by the next tile
+    }
+    wave_add_sh(ctr + cIncLight, n_ent);
+    wave_add_sh(ctr + cActivePins, n_front);
+    wave_add_sh(ctr + cNfRows, n_rows);
+    wave_add_sh(ctr + cVisLight, n_vis);
+    wave_add_sh(ctr + cNewLight, n_new);
+    wave_add_sh(ctr + cNewAtoms, n_new);
+    wave_add_sh(ctr + cNewFull, n_full);
+    wave_add_sh(ctr + cNewDeg, n_newdeg);
+    wave_add_sh(ctr + cNewDegNF, n_newdeg_nf);
+}
+
+// Heavy atoms: a workgroup per kChunkEntries-entry chunk of a hub; source bits and dense-slot bits go to
+// the workgroup's LDS row and mask (every entry belongs to the same hub), which are reduced once per
+// chunk into hubacc (then hgx_hub_finalize as in the dense levels).  (Per-lane register rows with
+// select chains instead of the LDS atomics measured 10.9 against 3.2 ms on config 2's level 1.)  A chunk
+// whose hub is already covered -- by the accumulator the hub's earlier chunks filled this level,
+// together with vis -- exits before streaming its entries.
+template <int W>
+__global__ void __launch_bounds__(256) hgx_fc_pull_heavy(const HeavyChunk* __restrict__ chunks,
+                                                         const int4* __restrict__ rec,
+                                                         const int32_t* __restrict__ inc_type, int32_t want_type,
+                                                         const u64x2* __restrict__ fw, const u64* __restrict__ fcode,
+                                                         const u64* __restrict__ drow, const u64* __restrict__ hubtab_g,
+                                                         int32_t n_hubs, const u64* __restrict__ lvl,
+                                                         const u64* __restrict__ vis, const u64* __restrict__ ever,
+                                                         const u64* __restrict__ full, u64* __restrict__ hubacc,
+                                                         u64* __restrict__ ctr, FullMask fm, int flags) {
+    __shared__ u64 acc[W];
+    __shared__ u64 dmask[kFcDW];
+    __shared__ u64 hubtab[kFcHubs];
+    __shared__ int covered;
+    const HeavyChunk c = chunks[blockIdx.x];
+    if ((flags & 4) && bit(full, c.atom)) return;   // block-uniform
+    const int tid = threadIdx.x;
+    if (tid < W) acc[tid] = 0ull;
+    if (tid < kFcDW) dmask[tid] = 0ull;
+    if (tid == 0) covered = 1;
+    for (int h = tid; h < n_hubs; h += 256) hubtab[h] = hubtab_g[h];
+    __syncthreads();
+    if (tid < W) {   // word tid of the hub's row: covered by this level's accumulator + vis?
+        const bool ev = bit(ever, c.atom);
+        const u64 h = __hip_atomic_load(hubacc + (int64_t)c.slot * W + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 o = ev ? vis[(int64_t)c.atom * W + tid] : 0ull;
+        if (((h | o) & fm.w[tid]) != fm.w[tid]) covered = 0;
+    }
+    __syncthreads();
+    if (covered) return;   // block-uniform
+    u64 n_ent = 0, n_front = 0, n_rows = 0;
+    for (int64_t i = c.beg + tid; i < c.end; i += 256) {
+        if (want_type >= 0 && inc_type[i] != want_type) continue;
+        ++n_ent;
+        n_front += (u64)fc_entry(
+            rec, i, fw, fcode, hubtab, [&](int k, u64 x) { atomicOr(acc + k, x); },
+            [&](int ds) { atomicOr(dmask + (ds >> 6), 1ull << (ds & 63)); },
+            [&](int64_t u) {
+                ++n_rows;
+#pragma unroll 1
+                for (int k = 0; k < W; ++k) {
+                    const u64 x = lvl[u * W + k];
+                    if (x) atomicOr(acc + k, x);
+                }
+            });
+    }
+    __syncthreads();
+    // the chunk's row: its source bits + the dense rows of its mask, word k by thread k
+    if (tid < W) {
+        u64 x = acc[tid];
+        for (int w = 0; w < kFcDW; ++w) {
+            u64 m = dmask[w];
+            while (m) {
+                const int ds = w * 64 + __ffsll((long long)m) - 1;
+                m &= m - 1ull;
+                x |= drow[(int64_t)ds * W + tid];
+            }
+        }
+        if (x) atomicOr(hubacc + (int64_t)c.slot * W + tid, x);
+    }
+    wave_add_sh(ctr + cIncHeavy, n_ent);
+    wave_add_sh(ctr + cActivePins, n_front);
+    wave_add_sh(ctr + cNfRows, n_rows);
+}
+
 // The seeds' incidence volume (the level-0 direction choice) straight into mapped host memory: one
 // block sums the degrees, stores the total, then the sequence number the host spins on (a
 // device-to-host copy and a stream synchronisation cost ~40 us before the first level).
@@ -2982,7 +3432,79 @@ struct Timer {
 
 enum { kKindGather = HGX_K_LINK_GATHER, kKindPull = HGX_K_ATOM_PULL, kKindHeavy = HGX_K_PULL_HEAVY,
        kKindHub = HGX_K_HUB_FINALIZE, kKindPush = HGX_K_FRONTIER_PUSH, kKindNf = HGX_K_NF_PULL,
-       kKindExchange = HGX_K_COUNT };
+       kKindFc = HGX_K_FC_PULL, kKindFcHeavy = HGX_K_FC_HEAVY, kKindExchange = HGX_K_COUNT };
+
+// Frontier-code pull: a level qualifies when its frontier rows (frontier atoms x S/8 bytes) fit well
+// inside the 256 MiB Infinity Cache -- the codes then sit in L2 and the rare dense rows are cache hits.
+constexpr double kFcFrontBytes = 64.0 * (1 << 20);
+// The records cost 32 bytes per incidence entry for the snapshot's lifetime (config 2: 6.4 GB); larger
+// snapshots (config 4: 32 GB) keep gather + pull rather than hold that much next to the level rows.
+constexpr size_t kFcRecBudget = (size_t)16 << 30;
+
+// The snapshot's per-entry target records (hgx_fc_rec), built on first use on the root snapshot and
+// shared by its contexts; nullptr when over budget, when a quarter of the free device memory cannot
+// hold them, or when some link has more than 8 targets.  Caller holds g->mu.
+const int4* fc_records(hgx_graph* g, hipStream_t s) {
+    hgx_graph* root = g->base ? g->base : g;
+    std::lock_guard<std::mutex> lk(root->ylist_mu);
+    if (root->fc_rec_state == 0) {
+        root->fc_rec_state = -1;
+        const size_t bytes = (size_t)32 * (size_t)root->I;
+        size_t fr = 0, tot = 0;
+        int4* rec = nullptr;
+        if (root->I > 0 && bytes <= kFcRecBudget && hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 4 &&
+            hipMalloc(&rec, bytes) == hipSuccess) {
+            // the hubs: the kFcHubs heavy atoms of highest degree (ascending ids, for the records' binary search)
+            std::vector<int32_t> hubs;
+            if (root->n_heavy > 0) {
+                const int64_t nh = root->n_heavy;
+                std::vector<int32_t> ha((size_t)nh);
+                std::vector<int64_t> hd((size_t)nh);
+                int64_t* dd = (int64_t*)g->alloc(sizeof(int64_t) * (size_t)nh);
+                hgx_fc_deg<<<grid_for(nh, 256, 4096), 256, 0, s>>>(nh, root->heavy_atom, root->inc_off, dd);
+                HGX_CHECK_LAUNCH();
+                HGX_HIP(hipMemcpyAsync(ha.data(), root->heavy_atom, sizeof(int32_t) * (size_t)nh, hipMemcpyDeviceToHost, s));
+                HGX_HIP(hipMemcpyAsync(hd.data(), dd, sizeof(int64_t) * (size_t)nh, hipMemcpyDeviceToHost, s));
+                HGX_HIP(hipStreamSynchronize(s));
+                g->release(dd, sizeof(int64_t) * (size_t)nh);
+                std::vector<int64_t> ord((size_t)nh);
+                for (int64_t k = 0; k < nh; ++k) ord[(size_t)k] = k;
+                const size_t keep = std::min<size_t>((size_t)nh, (size_t)kFcHubs);
+                std::partial_sort(ord.begin(), ord.begin() + (int64_t)keep, ord.end(),
+                                  [&](int64_t a, int64_t b) { return hd[(size_t)a] != hd[(size_t)b] ? hd[(size_t)a] > hd[(size_t)b] : a < b; });
+                for (size_t k = 0; k < keep; ++k) hubs.push_back(ha[(size_t)ord[k]]);
+                std::sort(hubs.begin(), hubs.end());
+            }
+            int32_t* dh = nullptr;
+            if (!hubs.empty()) {
+                HGX_HIP(hipMalloc(&dh, sizeof(int32_t) * hubs.size()));
+                HGX_HIP(hipMemcpyAsync(dh, hubs.data(), sizeof(int32_t) * hubs.size(), hipMemcpyHostToDevice, s));
+            }
+            unsigned int* dov = (unsigned int*)g->alloc(16);
+            HGX_HIP(hipMemsetAsync(dov, 0, sizeof(unsigned int), s));
+            hgx_fc_rec<<<grid_for(root->I, 256, 16384), 256, 0, s>>>(root->A, root->I, root->inc_off, root->inc_row,
+                                                                      root->tgt_off, root->tgt_idx, dh,
+                                                                      (int32_t)hubs.size(), rec, dov);
+            HGX_CHECK_LAUNCH();
+            unsigned int over = 1;
+            HGX_HIP(hipMemcpyAsync(&over, dov, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+            HGX_HIP(hipStreamSynchronize(s));
+            g->release(dov, 16);
+            if (over) {
+                (void)hipFree(rec);
+                if (dh) (void)hipFree(dh);
+            } else {
+                root->fc_rec = rec;
+                root->fc_hubs = dh;
+                root->fc_nhubs = (int32_t)hubs.size();
+                root->fc_rec_state = 1;
+            }
+        } else {
+            (void)hipGetLastError();   // a failed hipMalloc: the levels keep gather + pull
+        }
+    }
+    return root->fc_rec_state == 1 ? root->fc_rec : nullptr;
+}
 
 // Atoms with more than thr incidences and their ranges (order-free compaction).
 __global__ void __launch_bounds__(256) hgx_push_heavy_find(int64_t A, const int64_t* __restrict__ inc_off,
@@ -3514,6 +4036,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
     u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
+    u64 front_atoms = seed_atoms.size();       // atoms of the current level's frontier
     if (sparse_ok) {
         u64* slot = g->ctr_host + 2 * kHostSlot;
         const u64 seq = ++g->ctr_seq;
@@ -3604,6 +4127,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
                          (unsigned long long)h_new[cNewFull]);
         push_volume = h_new[cNewDeg];
         push_volume_nf = ex ? push_volume : h_new[cNewDegNF];
+        front_atoms = h_new[cNewAtoms];
         full_total += h_new[cNewFull];
         if (h_new[cNewAtoms] == 0) {
             g->release(p.lvl_next, row_bytes);
@@ -3643,11 +4167,64 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         // late dense level with few atoms left unfull: those pull from the frontier directly
         const bool nfp = !sparse && sparse_ok && MODE == kSym && Lay<W>::G >= 4 && !ex && (lflags & 256) &&
                          (lflags & 4) && 4 * (int64_t)(I_total - full_deg_total) < I_total;
+        // dense level over a frontier whose rows fit the Infinity Cache: the frontier-code pull (bit 17)
+        const int4* fcrec = nullptr;
+        if (!nfp && !sparse && MODE == kSym && Lay<W>::G >= 4 && !ex && (lflags & kFc) &&
+            (double)front_atoms * W * 8.0 <= kFcFrontBytes)
+            fcrec = fc_records(g, s);
+        const bool fcp = fcrec != nullptr;
         if (!opush) {   // the lists are reused as scratch; the sparse gather leaves candidate bits set
             chained = false;
             if (sparse) cand_clean = false;
         }
-        if (nfp) {
+        if (fcp) {
+            if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
+                const int64_t nwords = ceil_div(A, 64);
+                const int64_t cap = std::max<int64_t>((int64_t)front_atoms, 1);
+                const size_t fw_bytes = sizeof(u64x2) * (size_t)std::max<int64_t>(nwords, 1);
+                const size_t drow_bytes = sizeof(u64) * (size_t)kFcDenseCap * W;
+                u64x2* fwd = (u64x2*)g->alloc(fw_bytes);
+                u64* fcode = (u64*)g->alloc(sizeof(u64) * (size_t)cap);
+                u64* drow = (u64*)g->alloc(drow_bytes);
+                const hgx_graph* root = g->base ? g->base : g;
+                const int32_t n_hubs = root->fc_nhubs;
+                u64* hubtab = (u64*)g->alloc(sizeof(u64) * (size_t)std::max<int32_t>(n_hubs, 1));
+                u64* n_slots = ctr + (size_t)(max_levels_cap - 1) * kCtrBlock + 8;   // scratch slots
+                unsigned int* n_dense = (unsigned int*)(n_slots + 1);
+                Events e1 = tm.start(kKindFc, d);
+                HGX_HIP(hipMemsetAsync(n_slots, 0, 2 * sizeof(u64), s));
+                hgx_fc_slots<<<grid_for(nwords, 256, 2048), 256, 0, s>>>(nwords, fa, fwd, n_slots);
+                HGX_CHECK_LAUNCH();
+                hgx_fc_codes<W><<<grid_for(A, 256, 8192), 256, 0, s>>>(A, fwd, lvl, fcode, cap, drow, n_dense, c);
+                HGX_CHECK_LAUNCH();
+                if (n_hubs > 0) {
+                    hgx_fc_hubs<<<grid_for(n_hubs, 256, 64), 256, 0, s>>>(n_hubs, root->fc_hubs, fwd, fcode, hubtab);
+                    HGX_CHECK_LAUNCH();
+                }
+                hgx_fc_pull<W><<<grid_for(ceil_div(A, kFcTile) * 256, 256, 4096), 256, 0, s>>>(
+                    A, g->inc_off, fcrec, g->inc_type, want_type, fwd, fcode, drow, hubtab, n_hubs, lvl, vis, ever,
+                    full, lvl_next, fa_next, c, fm, lflags);
+                HGX_CHECK_LAUNCH();
+                tm.stop(e1);
+                if (g->n_chunks > 0) {
+                    Events e3 = tm.start(kKindFcHeavy, d);
+                    hgx_fc_pull_heavy<W><<<(unsigned)g->n_chunks, 256, 0, s>>>(g->chunks, fcrec, g->inc_type, want_type,
+                                                                             fwd, fcode, drow, hubtab, n_hubs, lvl,
+                                                                             vis, ever, full, hubacc, c, fm, lflags);
+                    HGX_CHECK_LAUNCH();
+                    tm.stop(e3);
+                    Events e4 = tm.start(kKindHub, d);
+                    hgx_hub_finalize<W><<<hub_grid, block, 0, s>>>(g->n_heavy, g->heavy_atom, g->inc_off, hubacc, vis,
+                                                                   ever, full, lvl_next, fa_next, c, fm);
+                    HGX_CHECK_LAUNCH();
+                    tm.stop(e4);
+                }
+                g->release(fwd, fw_bytes);   // stream-ordered reuse
+                g->release(fcode, sizeof(u64) * (size_t)cap);
+                g->release(drow, drow_bytes);
+                g->release(hubtab, sizeof(u64) * (size_t)std::max<int32_t>(n_hubs, 1));
+            }
+        } else if (nfp) {
             if constexpr (Lay<W>::G >= 4 && MODE == kSym) {
                 Events e2 = tm.start(kKindNf, d);
                 HGX_HIP(hipMemsetAsync(fa_next, 0, bm_bytes, s));
@@ -3862,7 +4439,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         pn.d = d;
         pn.lvl_next = lvl_next;
         pn.fa_next = fa_next;
-        pn.kind = nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;
+        pn.kind = fcp ? 4 : nfp ? 3 : sparse ? (opush ? 2 : 1) : 0;
         pn.allrows = (lflags & kAllRows) ? 1 : 0;
         pn.new_global = new_global;
         pn.part_push = part_push;
@@ -4346,7 +4923,8 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
             const auto& c = level_ctr[before + d];
             // hgx_link_gather: tgt_off + tgt_idx (+ link_type) + frontier/full bitmaps + gathered rows
             //                  + lf writes + la words
-            const bool sparse_level = c[cDirRows] != 0;
+            const bool fc_level = c[cDirRows] == 4;   // frontier-code pull (its hub chunks ran)
+            const bool sparse_level = c[cDirRows] != 0 && !fc_level;
             const double scan_links = sparse_level ? (double)c[cActiveLinks] : (double)M;
             const double scan_pins = sparse_level ? (double)c[cActivePins] : (double)P;
             double b_gather = 8.0 * (scan_links + 1) + 4.0 * scan_pins + (typed ? 4.0 * scan_links : 0.0) +
@@ -4365,6 +4943,18 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                 b_pull = A / 8.0 + 24.0 * c[cCand] + 4.0 * A / 64.0 + (8.0 + (typed ? 4.0 : 0.0) + 16.0) * c[cIncLight] +
                          4.0 * c[cActivePins] + A / 8.0 + rowb * c[cNfRows] + rowb * c[cVisLight] +
                          2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
+            } else if (fc_level) {   // frontier-code pull: no gather, no lf
+                b_gather = 0.0;
+                // codes: frontier bitmap (twice) + prefixes + the frontier atoms' rows + their codes;
+                // pull: inc_off + full bitmap + light records (+ inc_type) + frontier words / prefixes / codes of
+                // the frontier targets + dense frontier rows + vis reads + lvl/vis writes + bitmap words
+                const double n_front = (double)(d == 0 ? bt.S : level_ctr[before + d - 1][cNewAtoms]);
+                const double e_light = (double)c[cIncLight], e_all = e_light + (double)c[cIncHeavy];
+                b_pull = 2.0 * A / 8.0 + 4.0 * A / 64.0 + n_front * (rowb + 8.0) +
+                         8.0 * (A + 1) + A / 8.0 + e_light * (32.0 + (typed ? 4.0 : 0.0)) +
+                         (8.0 + 4.0 + 8.0) * c[cActivePins] * e_light / std::max(e_all, 1.0) +
+                         rowb * c[cNfRows] * e_light / std::max(e_all, 1.0) + rowb * c[cVisLight] +
+                         2.0 * rowb * c[cNewLight] + 3.0 * A / 8.0;
             } else if (opush_level) {   // frontier push: no gather; two frontier passes + finalise
                 b_gather = 0.0;
                 // frontier scan + scanned entries (inc_type + yield flag) + links (inc_row, tgt_off pair) + pins
@@ -4374,17 +4964,26 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                          16.0 * c[cIncLight] +
                          2.0 * rowb * c[cCand] + rowb * c[cVisLight] + 2.0 * rowb * c[cNewLight] + 2.0 * A / 8.0;
             }
-            const int pull_kind = c[cDirRows] == 3 ? HGX_K_NF_PULL : c[cDirRows] == 2 ? HGX_K_FRONTIER_PUSH
-                                                                                   : HGX_K_ATOM_PULL;
+            const int pull_kind = fc_level ? HGX_K_FC_PULL : c[cDirRows] == 3 ? HGX_K_NF_PULL
+                                  : c[cDirRows] == 2 ? HGX_K_FRONTIER_PUSH : HGX_K_ATOM_PULL;
             r->stats.bytes_kernel[HGX_K_LINK_GATHER] += b_gather;
             r->stats.bytes_kernel[pull_kind] += b_pull;
             double b_heavy = 0, b_hub = 0;
             if (g->n_chunks > 0 && !sparse_level) {
-                b_heavy = 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
+                if (fc_level) {   // chunk table + the streamed records of the chunks that ran + code lookups
+                    const double e_all = (double)c[cIncLight] + (double)c[cIncHeavy];
+                    const double share = (double)c[cIncHeavy] / std::max(e_all, 1.0);
+                    b_heavy = 24.0 * g->n_chunks + rowb * g->n_chunks +
+                              c[cIncHeavy] * (32.0 + (typed ? 4.0 : 0.0)) + 20.0 * c[cActivePins] * share +
+                              rowb * c[cNfRows] * share + rowb * g->n_chunks;
+                } else {
+                    b_heavy = 24.0 * g->n_chunks + 4.0 * I_heavy + rowb * c[cIncHeavy] + rowb * g->n_chunks;
+                }
                 b_hub = 4.0 * g->n_heavy + 2.0 * rowb * g->n_heavy + rowb * c[cAccHub] + 2.0 * rowb * c[cNewHub];
-                r->stats.bytes_kernel[HGX_K_PULL_HEAVY] += b_heavy;
+                const int heavy_kind = fc_level ? HGX_K_FC_HEAVY : HGX_K_PULL_HEAVY;
+                r->stats.bytes_kernel[heavy_kind] += b_heavy;
                 r->stats.bytes_kernel[HGX_K_HUB_FINALIZE] += b_hub;
-                r->stats.launches[HGX_K_PULL_HEAVY] += 1;
+                r->stats.launches[heavy_kind] += 1;
                 r->stats.launches[HGX_K_HUB_FINALIZE] += 1;
             }
             if (d < 64) {
@@ -4392,7 +4991,7 @@ void bfs_batch_impl(hgx_graph* g, Transport* tr, const int32_t* seeds, int32_t n
                 r->stats.level_bytes[d] += b_gather + b_pull + b_heavy + b_hub;
                 r->stats.level_sparse[d] = (int32_t)c[cDirRows];
             }
-            if (!opush_level) r->stats.launches[HGX_K_LINK_GATHER] += 1;
+            if (!opush_level && !fc_level) r->stats.launches[HGX_K_LINK_GATHER] += 1;
             r->stats.launches[pull_kind] += 1;
             if (d < 64) r->stats.level_new[d] += (int64_t)c[cNewAtoms];
         }

@@ -500,8 +500,9 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
     if (!g) fail(HGX_E_INVALID, "null graph");
     std::lock_guard<std::mutex> lk(g->mu);
     if (option == HGX_OPT_BFS_FLAGS) {
-        // bits 16 and up are the engine's per-level internal flags (kAllRows, ...): never settable
-        if (value < 0 || value > 0xFFFF) fail(HGX_E_INVALID, "hgx_set_option: BFS flags outside bits 0-15");
+        // bit 16 is the engine's per-level internal flag (kAllRows): never settable; bit 17 = frontier-code pull
+        if (value < 0 || value > 0x3FFFF || (value & 0x10000))
+            fail(HGX_E_INVALID, "hgx_set_option: BFS flags outside bits 0-15 and 17");
         g->bfs_flags = (int32_t)value;
     } else if (option == HGX_OPT_RANKS_ORDERED) {
         g->ranks_ordered = value != 0;

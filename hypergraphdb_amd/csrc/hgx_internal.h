@@ -243,6 +243,11 @@ struct hgx_graph {
                                                     //   pin_j -- the pull walk's link data streamed in entry order
     int2* pull_meta = nullptr;                      // [I] (link atom, arity) per incidence entry
     int32_t pull_rec_state = 0;                     //   0 not built yet, 1 built, -1 over its memory budget
+    int4* fc_rec = nullptr;                         // [I x 2] per incidence entry: its link's <= 8 targets (-1 padded),
+    int32_t fc_rec_state = 0;                       //   the frontier-code pull's records (snapshot only, made on first
+                                                    //   use; 0 not built, 1 built, -1 over budget / arity > 8)
+    int32_t* fc_hubs = nullptr;                     //   and its hub atoms (ascending; their slots are in the records)
+    int32_t fc_nhubs = 0;
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each

@@ -5315,6 +5315,12 @@ void free_yield_lists(hgx_graph* g) {
     g->pull_rec = nullptr;
     g->pull_meta = nullptr;
     g->pull_rec_state = 0;
+    if (!g->base && g->fc_rec) (void)hipFree(g->fc_rec);   // the frontier-code pull's records
+    if (!g->base && g->fc_hubs) (void)hipFree(g->fc_hubs);
+    g->fc_rec = nullptr;
+    g->fc_hubs = nullptr;
+    g->fc_nhubs = 0;
+    g->fc_rec_state = 0;
     for (YieldList& y : g->ylists) {
         (void)hipFree(y.off);
         (void)hipFree(y.row);

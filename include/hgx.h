@@ -101,7 +101,9 @@ typedef struct hgx_and_query {
 #define HGX_K_HUB_FINALIZE  3   /* hgx_hub_finalize         */
 #define HGX_K_FRONTIER_PUSH 4   /* sparse levels: hgx_frontier_list, hgx_opush[_heavy], hgx_push_finalize_list */
 #define HGX_K_NF_PULL       5   /* late dense levels: hgx_nonfull_list, hgx_nf_pull                        */
-#define HGX_K_COUNT         6
+#define HGX_K_FC_PULL       6   /* dense levels over a small frontier: hgx_fc_slots, hgx_fc_codes, hgx_fc_pull */
+#define HGX_K_FC_HEAVY      7   /*   and their hub chunks: hgx_fc_pull_heavy, then hgx_hub_finalize          */
+#define HGX_K_COUNT         8
 typedef struct hgx_bfs_stats {
     int32_t n_levels_expanded;
     int32_t n_batches;
@@ -116,7 +118,7 @@ typedef struct hgx_bfs_stats {
     int64_t level_new[64];             /* atoms with a new bit at level d+1 (summed over batches) */
     double  level_bytes[64];           /* algorithmic bytes of all kernels of level d          */
     int32_t level_sparse[64];          /* level d ran 0 = dense, 1 = frontier links + lf push, 2 = frontier push,
-                                        * 3 = non-full pull */
+                                        * 3 = non-full pull, 4 = frontier-code pull */
     /* per level, summed over batches: [0] lf rows written, [1] frontier rows gathered,
      * [2] lf rows pulled (light), [3] vis rows read, [4] new light atoms, [5] lf rows pulled
      * (heavy chunks), [6] heavy atoms finalised, [7] new heavy atoms */
@@ -200,8 +202,12 @@ int  hgx_set_timing(hgx_graph *g, int32_t enabled);
  *                      bits 12 / 13 / 14 = nontemporal loads of the streamed CSR columns / stores of
  *                              the gather's link rows / stores of the pull's atom rows (A/B only),
  *                      bit 15 = the symmetric-mode hub pull keeps two incidence chunks in flight
- *                              without the active-link probe in all-rows levels (A/B only).
- *                      Default 0x3BE. */
+ *                              without the active-link probe in all-rows levels (A/B only),
+ *                      bit 17 = symmetric-mode dense levels whose frontier rows fit the Infinity Cache
+ *                              (<= 64 MB) pull through per-entry target records and coded frontier rows
+ *                              instead of gather + pull (records: 32 bytes per incidence entry, built on
+ *                              first use, at most 16 GiB; snapshots with links of arity > 8 keep gather + pull).
+ *                      Default 0x3BE (bit 17 is an A/B: measured slower on config 2). */
 #define HGX_OPT_BFS_FLAGS 1
 /* HGX_OPT_SEQ_BUDGET: device bytes the order-exact traversal's level-synchronous engine may use for
  * its per-seed key arrays (seeds are processed in chunks that fit; default 48 GiB). */

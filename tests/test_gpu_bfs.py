@@ -226,7 +226,8 @@ def test_depth_of_and_errors():
 
 
 @pytest.mark.parametrize("flags", [0x0, 0x1, 0x2, 0x4, 0x8, 0xF, 0xE, 0x28, 0x3E, 0x7E, 0x40, 0xBE, 0x13E, 0x1BE, 0x1B6, 0x3BE, 0x236, 0xBBE,
-                                   0x13BE, 0x23BE, 0x43BE, 0x73BE, 0x83BE, 0x83BA, 0xF3BA, 0x0BBE])
+                                   0x13BE, 0x23BE, 0x43BE, 0x73BE, 0x83BE, 0x83BA, 0xF3BA, 0x0BBE,
+                                   0x203BE, 0x2003E, 0x20008, 0x2000A, 0x203BA, 0x223BE])
 def test_engine_option_matrix(flags):
     """Every work-avoidance option (early exits, full-visited skipping, frontier-driven sparse
     levels) returns the same per-depth sets; power-law hubs + random edge cases + ordered modes."""
@@ -251,10 +252,12 @@ def test_engine_flags_reject_internal_bits():
     from hypergraphdb_amd import HGXError, _lib
     g = K.random_graph(np.random.default_rng(3), 50, 80)
     snap = snapshot(g)
-    for bad in (-1, 1 << 16, 0x183BE):
+    for bad in (-1, 1 << 16, 0x183BE, 1 << 18, 0x3FFFF):
         with pytest.raises(HGXError, match="bits 0-15"):
             snap.set_option(_lib.HGX_OPT_BFS_FLAGS, bad)
     snap.set_option(_lib.HGX_OPT_BFS_FLAGS, 0xFFFF)
+    check_batch(g, np.arange(40, dtype=np.int32), None, K.ALGEN_MODES[0], -1, snap, oracle(g))
+    snap.set_option(_lib.HGX_OPT_BFS_FLAGS, 0x2FFFF)   # bit 17 (frontier-code pull) is settable
     check_batch(g, np.arange(40, dtype=np.int32), None, K.ALGEN_MODES[0], -1, snap, oracle(g))
 
 
@@ -279,6 +282,47 @@ def test_nonfull_pull_levels(n_seeds, lt):
     res.close()
     assert 3 in kinds, kinds
     check_batch(g, seeds, None, K.ALGEN_MODES[0], lt, snap, orc)
+
+
+@pytest.mark.parametrize("n_seeds,lt,scale", [(1024, -1, 8), (300, -1, 8), (1024, 1, 8), (1024, -1, 1), (512, 2, 1)])
+def test_frontier_code_levels(n_seeds, lt, scale):
+    """Dense levels over a small frontier run the frontier-code pull (level kind 4, HGX_OPT_BFS_FLAGS bit
+    17): per-entry target records, frontier rows as <= 6-id codes or dense rows, hub chunks in registers.
+    Per-depth sets equal the oracle's and the gather + pull engine's, with few-bit rows (a large graph
+    per seed: codes) and many-bit rows (1024 seeds on a small graph: dense rows), typed and untyped."""
+    from hypergraphdb_amd import _lib, bfs_batch, synth
+    g = synth.hypergraph(3000 * scale, 20000 * scale, 2, 8, 2.1, 3, seed=21 + scale)
+    snap, orc = snapshot(g), oracle(g)
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)   # every seed on the rows engine
+    seeds = np.random.default_rng(22).choice(3000 * scale, n_seeds, replace=False).astype(np.int32)
+    sets = {}
+    for flags in (0x203BE, 0x3BE):
+        snap.set_option(_lib.HGX_OPT_BFS_FLAGS, flags)
+        res = bfs_batch(snap, seeds, 4, gen(snap, K.ALGEN_MODES[0], lt))
+        st = res.stats(accounting=False)
+        assert (4 in st["level_sparse"]) == bool(flags & 0x20000), (flags, st["level_sparse"])
+        if flags & 0x20000:
+            assert st["kernels"]["hgx_fc_pull"]["launches"] >= 1
+        sets[flags] = (res.counts(), [res.visited(i, d).tobytes() for i in range(0, n_seeds, 37) for d in range(5)])
+        res.close()
+    assert np.array_equal(sets[0x203BE][0], sets[0x3BE][0]) and sets[0x203BE][1] == sets[0x3BE][1]
+    snap.set_option(_lib.HGX_OPT_BFS_FLAGS, 0x203BE)
+    check_batch(g, seeds if n_seeds <= 512 else seeds[:: max(1, n_seeds // 96)], 4, K.ALGEN_MODES[0], lt, snap, orc)
+
+
+def test_frontier_code_refused_for_long_links():
+    """A snapshot with a link of arity > 8 has no frontier-code records: its dense levels keep gather + pull
+    (no level of kind 4) and the sets stay exact."""
+    from hypergraphdb_amd import _lib, bfs_batch
+    rng = np.random.default_rng(23)
+    g = K.random_graph(rng, 600, 3000, max_arity=12, n_types=1)
+    snap, orc = snapshot(g), oracle(g)
+    snap.set_option(_lib.HGX_OPT_BFS_BLOCK, 0)
+    seeds = rng.integers(0, g["num_atoms"], 1024).astype(np.int32)
+    res = bfs_batch(snap, seeds, 3, gen(snap, K.ALGEN_MODES[0]))
+    assert 4 not in res.stats(accounting=False)["level_sparse"]
+    res.close()
+    check_batch(g, seeds[:200], 3, K.ALGEN_MODES[0], -1, snap, orc)
 
 
 @pytest.mark.parametrize("batch", [0])
