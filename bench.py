@@ -747,6 +747,8 @@ def dry_run(args):
 
 
 def main():
+    if os.environ.get("HGX_LIB_VARIANT"):   # the bench line measures the product library, never an A/B variant
+        raise SystemExit("bench.py: HGX_LIB_VARIANT is set; unset it (A/B variants are for tools/ only)")
     launch_ranks(sys.argv[1:])
     claim_stdout()
     ap = argparse.ArgumentParser()

@@ -7,16 +7,21 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
+import sys
 
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HGX_LIB_VARIANT=<name>: load tools/native/build/libhgx_<name>.so instead (A/B builds of the engine side by
-# side in one GPU session; tools only -- the tests, smoke() and bench.py never set it)
+# side in one GPU session; tools only -- tests/conftest.py, smoke() and bench.py refuse to run with it set)
 LIB_PATH = os.path.join(_HERE, "libhgx.so")
-if os.environ.get("HGX_LIB_VARIANT"):
-    LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "native", "build",
-                            f"libhgx_{os.environ['HGX_LIB_VARIANT']}.so")
+LIB_VARIANT = os.environ.get("HGX_LIB_VARIANT") or None
+if LIB_VARIANT:
+    if not re.fullmatch(r"[A-Za-z0-9_]+", LIB_VARIANT):
+        raise ImportError(f"HGX_LIB_VARIANT={LIB_VARIANT!r}: variant names are [A-Za-z0-9_]+")
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "native", "build", f"libhgx_{LIB_VARIANT}.so")
+    print(f"hypergraphdb_amd: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
 GEN_PATH = os.path.join(_HERE, "libhgx_gen.so")
 
 HGX_OK = 0
@@ -42,6 +47,13 @@ HGX_OPT_QUERY_COALESCE = 11
 HGX_OPT_PUSH_INLINE = 12
 HGX_OPT_SEQ_ENGINE = 13
 HGX_OPT_BFS_BLOCK = 14
+HGX_OPT_CO_TIMEOUT = 15
+HGX_OPT_SEQ_PULL = 16
+HGX_OPT_SEQ_SMALL = 17
+HGX_OPT_SEQ_TLIMIT = 18
+HGX_OPT_SEQ_PACK_MIN = 19
+HGX_OPT_XB_FLAT = 20
+HGX_OPT_XB_STATIC = 21
 
 # Every symbol include/hgx.h declares (checked by tests/test_abi.py without a GPU).
 EXPORTED = (

@@ -3778,15 +3778,14 @@ struct Exchange {
         std::vector<int64_t> all;
         gather_counts(all, cnt, wcnt);
         // a dense level (at least half of my ghosts with news, rows > 70% nonzero words) packs its
-        // broadcast over the entries (hgx_xb_pack_flat); HGX_XB_FLAT=0 keeps the atom walk on every
+        // broadcast over the entries (hgx_xb_pack_flat); HGX_OPT_XB_FLAT 0 keeps the atom walk on every
         // level, 2 takes the entries on every level (A/B and tests)
         u64 sent_r = 0, sent_w = 0;
         for (int q = 0; q < NP; ++q) {
             sent_r += cnt[q];
             sent_w += wcnt[q];
         }
-        const char* fe = std::getenv("HGX_XB_FLAT");
-        const int flat_opt = fe ? std::atoi(fe) : 1;
+        const int flat_opt = g->xb_flat >= 0 ? g->xb_flat : 1;
         const bool flat = bseg[NP] > 0 && (flat_opt == 2 || (flat_opt == 1 && sent_r * 2 >= (u64)rseg[NP] &&
                                                              sent_w * 10 > sent_r * (u64)Wt * 7));
         double grp[3];
@@ -3794,10 +3793,9 @@ struct Exchange {
         // static broadcast (group-wide choice from the all-gathered reduce counts, so every part
         // agrees): at least 85% of the group's ghosts had news and their rows were > 70% nonzero
         // words -- shipping a record for every entry then costs < 18% more bytes than the news alone
-        // and saves the counting pass and the phase's count round trips.  HGX_XB_STATIC=0 never,
-        // 2 on every level (A/B and tests).
-        const char* se = std::getenv("HGX_XB_STATIC");
-        const int static_opt = se ? std::atoi(se) : 1;
+        // and saves the counting pass and the phase's count round trips.  HGX_OPT_XB_STATIC 0 never,
+        // 2 on every level (A/B and tests; every part of a group must use the same value).
+        const int static_opt = g->xb_static >= 0 ? g->xb_static : 1;
         const bool bstatic = static_opt == 2 || (static_opt == 1 && grp[2] > 0 && grp[0] >= 0.85 * grp[2] &&
                                                  grp[1] * 10.0 > grp[0] * Wt * 7.0);
         Events e1 = tm.start(kKindExchange, d);
@@ -3982,7 +3980,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // profiles/r02zj_readout_*.log): the passes share HBM and CUs with the dense levels and delay
     // them by more than they save.  Default: counted at readout time.  Push levels count their news
     // in their finalise and need no pass either way.
-    const bool eager = !tr && !g->shard && std::getenv("HGX_COUNT_EAGER") && std::getenv("HGX_COUNT_EAGER")[0] == '1';
+    const char* ce = ab_env("HGX_COUNT_EAGER");
+    const bool eager = !tr && !g->shard && ce && ce[0] == '1';
     if (eager && !g->stream2) {
         HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
         HGX_HIP(hipEventCreateWithFlags(&g->ev_count, hipEventDisableTiming));
@@ -4032,7 +4031,7 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
     // uses them): the first push level issues no memset (each costs a host API call, ~20 us between
     // the prologue's device operations on config 5)
     bool chained = false, cand_clean = cand != nullptr, scratch_clean = true;
-    const bool trace = std::getenv("HGX_BFS_TRACE") != nullptr;   // per-level counters to stderr
+    const bool trace = trace_env("HGX_BFS_TRACE");   // per-level counters to stderr
     const int64_t I_total = g->I;
     int64_t full_deg_total = 0;   // sum of |inc(v)| over the atoms visited by every traversal
     u64 push_volume = 0, push_volume_nf = 0;   // frontier incidence volume (all / not yet full atoms)
@@ -4053,9 +4052,9 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
         push_volume = __atomic_load_n(slot, __ATOMIC_RELAXED);
         push_volume_nf = push_volume;
     }
-    // HGX_SPARSE_SCALE (A/B): multiplies the push / dense threshold (M / 16 incidence entries)
+    // HGX_SPARSE_SCALE (A/B builds): multiplies the push / dense threshold (M / 16 incidence entries)
     static const double kSparseScale = [] {
-        const char* e = std::getenv("HGX_SPARSE_SCALE");
+        const char* e = ab_env("HGX_SPARSE_SCALE");
         const double v = e ? std::atof(e) : 1.0;
         return v > 0 ? v : 1.0;
     }();
@@ -4285,8 +4284,8 @@ void run_levels(hgx_graph* g, hgx_bfs_result* res, BfsBatch& bt, int32_t max_dep
             // 2048 waves grid-striding over the frontier list: config 5 levels of 20 to 35K atoms measured
             // 19-113 us against 30-142 us with 8192 waves (the launch of mostly idle workgroups and
             // the candidate-append contention) and 20-171 us with 1024 waves
-            static const int kPushGrid = [] {   // HGX_PUSH_GRID: A/B override of the push grid (blocks)
-                const char* e = std::getenv("HGX_PUSH_GRID");
+            static const int kPushGrid = [] {   // HGX_PUSH_GRID (A/B builds): override of the push grid (blocks)
+                const char* e = ab_env("HGX_PUSH_GRID");
                 const int v = e ? std::atoi(e) : 0;
                 return v >= 64 && v <= 8192 ? v : 512;
             }();

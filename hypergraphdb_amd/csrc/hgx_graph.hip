@@ -317,6 +317,13 @@ int hgx_graph_context(hgx_graph* g, hgx_graph** out) {
     c->timing = g->timing; c->bfs_flags = g->bfs_flags; c->seq_budget_bytes = g->seq_budget_bytes;
     c->seq_engine = g->seq_engine;
     c->bfs_block = g->bfs_block;
+    c->co_timeout = g->co_timeout;
+    c->seq_pull = g->seq_pull;
+    c->seq_small = g->seq_small;
+    c->seq_tlimit = g->seq_tlimit;
+    c->seq_pack_min = g->seq_pack_min;
+    c->xb_flat = g->xb_flat;
+    c->xb_static = g->xb_static;
     c->ranks_ordered = g->ranks_ordered; c->q_inline = g->q_inline;
     c->q_coalesce = g->q_coalesce; c->q_coalesce_max = g->q_coalesce_max;
     guard.c = nullptr;
@@ -545,6 +552,28 @@ int hgx_set_option(hgx_graph* g, int32_t option, int64_t value) {
         if (value < 0 || value > (1 << 24)) fail(HGX_E_INVALID, "hgx_set_option: coalesce cap outside 0..2^24");
         g->q_coalesce = value != 0;
         if (value > 1) g->q_coalesce_max = value;
+    } else if (option == HGX_OPT_CO_TIMEOUT) {
+        if (value < 0) fail(HGX_E_INVALID, "hgx_set_option: grid-stage timeout below 0");
+        g->co_timeout = value;
+    } else if (option == HGX_OPT_SEQ_PULL) {
+        if (value < 0 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: sequence pull mode outside 0..2");
+        g->seq_pull = (int32_t)value;
+    } else if (option == HGX_OPT_SEQ_SMALL) {
+        g->seq_small = value != 0;
+    } else if (option == HGX_OPT_SEQ_TLIMIT) {
+        if (value < 0) fail(HGX_E_INVALID, "hgx_set_option: stream-key limit below 0");
+        g->seq_tlimit = value;
+    } else if (option == HGX_OPT_SEQ_PACK_MIN) {
+        if (value < 0) fail(HGX_E_INVALID, "hgx_set_option: packed-transfer threshold below 0");
+        g->seq_pack_min = value;
+    } else if (option == HGX_OPT_XB_FLAT) {
+        if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_XB_FLAT applies to partition shards");
+        if (value < -1 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: broadcast pack mode outside -1..2");
+        g->xb_flat = (int32_t)value;
+    } else if (option == HGX_OPT_XB_STATIC) {
+        if (!g->shard) fail(HGX_E_INVALID, "hgx_set_option: HGX_OPT_XB_STATIC applies to partition shards");
+        if (value < -1 || value > 2) fail(HGX_E_INVALID, "hgx_set_option: static broadcast mode outside -1..2");
+        g->xb_static = (int32_t)value;
     } else fail(HGX_E_INVALID, "hgx_set_option: unknown option");
     HGX_API_END
 }

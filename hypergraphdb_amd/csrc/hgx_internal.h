@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -25,6 +26,27 @@
 #include "../../include/hgx.h"
 
 namespace hgx {
+
+// Engine knobs.  The product library reads no tuning setting from the environment (a library loaded into
+// a JVM must not change behaviour with whichever call read the environment first, and getenv racing a
+// setenv is undefined in a multi-threaded host): tunables that callers and tests set go through
+// hgx_set_option (per graph).  The measured-negative A/B variants of DESIGN.md are reachable only in A/B
+// builds (tools/build_variant.sh compiles with -DHGX_AB_KNOBS), where ab_env reads them; tracing
+// (trace_env: HGX_BFS_TRACE, HGX_SEQ_TRACE, HGX_CO_TRACE, HGX_LS_PROF, HGX_QUERY_PROFILE) stays
+// environment-driven and only adds output.
+inline const char* ab_env(const char* name) {
+#ifdef HGX_AB_KNOBS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+inline bool trace_env(const char* name) { return std::getenv(name) != nullptr; }
+inline int ab_int(const char* name, int dflt) {
+    const char* e = ab_env(name);
+    return e ? std::atoi(e) : dflt;
+}
 
 struct Error {
     int code;
@@ -251,6 +273,13 @@ struct hgx_graph {
     std::mutex seq_mu;                              // guards seq_hbufs (results hand their buffers back from any thread)
     std::vector<hgx::PoolBuf> seq_hbufs;            // mapped host buffers of order-exact results, free for reuse
     int32_t bfs_block = 1;                          // HGX_OPT_BFS_BLOCK: hgx_bfs_batch seeds first run one workgroup each
+    // test / diagnostic options (hgx.h: HGX_OPT_CO_TIMEOUT .. HGX_OPT_XB_STATIC); 0 / -1 = the engine's default
+    int64_t co_timeout = 0;                         // grid-stage barrier limit in s_memrealtime ticks (0 = 1 s)
+    int32_t seq_pull = 1;                           // level engine pull levels: 0 never, 1 by width, 2 always
+    int32_t seq_small = 0;                          // level engine: tiny starting capacities (exercise growth)
+    int64_t seq_tlimit = 0;                         // level engine: stream-key limit below the 32-bit one (0 = none)
+    int64_t seq_pack_min = 0;                       // level engine: pairs of a level that cross PCIe packed (0 = 2^20)
+    int32_t xb_flat = -1, xb_static = -1;           // partition broadcast pack variants (-1 = default)
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)

@@ -1578,7 +1578,7 @@ void back_end_sp(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx
         const int4* tt = g->q_inline ? (const int4*)g->inc_ts_tgt : nullptr;
         // without timing events the host waits on a completion flag the placement writes into the result
         // area (stat[7]) instead of asking the stream (each hipStreamQuery costs a few microseconds)
-        static const bool stream_wait = std::getenv("HGX_Q_STREAM_WAIT") != nullptr;   // A/B
+        static const bool stream_wait = ab_env("HGX_Q_STREAM_WAIT") != nullptr;   // A/B
         const bool flag = derived && !ev.on && !stream_wait;
         u64 flag_seq = 0;
         if (flag) {
@@ -1696,7 +1696,7 @@ void back_end(hgx_graph* g, int32_t n, Front& f, Scratch& sc, Events& ev, hgx_qu
 template <class FrontFn>
 int run_batch_with(hgx_graph* g, int32_t n, hgx_query_result** out, FrontFn front, hgx_query_result* into = nullptr) {
     HGX_API_BEGIN
-    const bool prof = std::getenv("HGX_QUERY_PROFILE") != nullptr;
+    const bool prof = trace_env("HGX_QUERY_PROFILE");
     const double t0 = now_ms();
     if (g->shard) fail(HGX_E_UNSUPPORTED, "hgx_pattern_batch: not available on a partition shard");
     std::unique_ptr<hgx_query_result> own;

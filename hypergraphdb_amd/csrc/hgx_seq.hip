@@ -68,7 +68,7 @@ int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
 // Host-side phase trace of hgx_bfs_sequence (HGX_SEQ_TRACE=1): microseconds since the call began.
 struct SeqTrace {
-    bool on = std::getenv("HGX_SEQ_TRACE") != nullptr;
+    bool on = trace_env("HGX_SEQ_TRACE");
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     void operator()(const char* what) const {
         if (on)
@@ -85,7 +85,7 @@ inline void seq_mark(const char* what) {
 // calling thread when `wide` is false.
 template <class F>
 void host_parallel(int64_t n, bool wide, F&& fn) {
-    static const int env = std::getenv("HGX_COPY_THREADS") ? std::atoi(std::getenv("HGX_COPY_THREADS")) : 0;
+    static const int env = ab_int("HGX_COPY_THREADS", 0);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int nt = !wide ? 1 : (int)std::min<int64_t>(n, env > 0 ? env : std::min(hw, 16));
     if (nt <= 1) {
@@ -1393,7 +1393,7 @@ constexpr int kCoBarGroups = 16;
 constexpr int kCoItemShift = 40;
 constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
-constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s (HGX_CO_TIMEOUT: tests)
+constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s (HGX_OPT_CO_TIMEOUT: tests)
 // ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
 // even / odd levels (the seeding: odd), [kCoSel] seeds the workgroup
 // stage handed over, [kCoLev + slot * kCoSegs + seg] level counters (3 rotating slots), then cur [kcap],
@@ -4038,13 +4038,13 @@ void ev_give(hgx_graph* g, hipEvent_t e) {
 // The yield list the workgroup and grid stages read (HGX_YIELD_LISTS=0, for A/B: stream the incidence
 // and its yield flags instead).
 const YieldList* stage_yield_list(hgx_graph* g, int mode, int32_t type) {
-    static const bool off = std::getenv("HGX_YIELD_LISTS") && std::atoi(std::getenv("HGX_YIELD_LISTS")) == 0;
+    static const bool off = ab_int("HGX_YIELD_LISTS", 1) == 0;
     return off ? nullptr : yield_list(g, mode, type);
 }
 
 // The yield adjacency the stages read first (HGX_YIELD_ADJ=0, for A/B: the yield list instead).
 const YieldAdj* stage_yield_adj(hgx_graph* g, int mode, const hgx_algen_opts& o) {
-    static const bool off = std::getenv("HGX_YIELD_ADJ") && std::atoi(std::getenv("HGX_YIELD_ADJ")) == 0;
+    static const bool off = ab_int("HGX_YIELD_ADJ", 1) == 0;
     return off ? nullptr : yield_adj(g, mode, o.link_type, o.return_source ? 1 : 2, o.reverse_order != 0);
 }
 
@@ -4250,7 +4250,7 @@ void ensure_pull_rec(hgx_graph* g, const int32_t* pin_j) {
     hgx_graph* root = g->base ? g->base : g;
     std::lock_guard<std::mutex> lk(root->ylist_mu);
     if (root->pull_rec_state != 0 || root->I <= 0) return;
-    const char* ev = std::getenv("HGX_LS_PULL_REC");
+    const char* ev = ab_env("HGX_LS_PULL_REC");
     const size_t bytes = (size_t)72 * (size_t)root->I;
     if ((ev && std::atoi(ev) == 0) || (int64_t)bytes > g->seq_budget_bytes / 2) {
         root->pull_rec_state = -1;
@@ -4287,11 +4287,10 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     hipStream_t st = g->stream;
     const int64_t A = g->A;
     const int mode = seq_mode(o);
-    // pull levels (HGX_LS_PULL: 0 never, 1 by the level's width (default), 2 every level -- tests) read
+    // pull levels (HGX_OPT_SEQ_PULL: 0 never, 1 by the level's width (default), 2 every level -- tests) read
     // the incidence items; with the yield adjacency the items are its pairs and every level pushes
     // (forced pulls drop the adjacency, so the tests reach the pull in every generator mode)
-    const char* pe = std::getenv("HGX_LS_PULL");
-    const int pull_env = pe ? std::min(2, std::max(0, std::atoi(pe))) : 1;
+    const int pull_env = std::min(2, std::max(0, (int)g->seq_pull));
     const YieldAdj* ya = pull_env == 2 ? nullptr : stage_yield_adj(g, mode, o);   // a pair's index is its stream position
     const int kbits = ya ? 0 : bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
     const int32_t W = (nb + 63) / 64;
@@ -4317,9 +4316,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
     u64* hflag_d = nullptr;
     HGX_HIP(hipHostGetDevicePointer((void**)&hflag_d, g->seq_flag, 0));
     const int64_t full = (int64_t)nb * A;
-    // starting capacities (grown x4 on overflow and kept on the graph); HGX_LS_SMALL (tests) starts
+    // starting capacities (grown x4 on overflow and kept on the graph); HGX_OPT_SEQ_SMALL (tests) starts
     // them tiny so that every growth path runs
-    const bool small = std::getenv("HGX_LS_SMALL") != nullptr;
+    const bool small = g->seq_small != 0;
     for (int attempt = 0;; ++attempt) {
         const int64_t cap = std::min(full, std::max<int64_t>(g->ls_cap, small ? 64 : (int64_t)1 << 20));
         const int64_t tcap = std::max<int64_t>(g->ls_tcap, small ? 8 : (int64_t)1 << 16);
@@ -4345,9 +4344,9 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.rev = o.reverse_order ? 1 : 0;
         a.kbits = kbits;
         a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> kbits));
-        static const int lr_sub = std::getenv("HGX_LR_SUB") ? std::atoi(std::getenv("HGX_LR_SUB")) : 11;   // A/B (buckets ~ 2^lr_sub)
+        static const int lr_sub = ab_int("HGX_LR_SUB", 11);   // A/B builds (buckets ~ 2^lr_sub)
         a.lr_sub = std::min(std::max(lr_sub, 1), 14);
-        if (const char* tl = std::getenv("HGX_LS_TLIMIT")) a.t_limit = std::min<int64_t>(a.t_limit, std::atoll(tl));   // tests
+        if (g->seq_tlimit > 0) a.t_limit = std::min<int64_t>(a.t_limit, g->seq_tlimit);   // HGX_OPT_SEQ_TLIMIT (tests)
         a.nb = nb;
         a.W = W;
         a.maxd = maxd;
@@ -4380,9 +4379,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.pcnt = (uint32_t*)w.take(sizeof(uint32_t) * kLrG * kLrParts);
         a.pcur = (uint32_t*)w.take(sizeof(uint32_t) * kLrParts);
         a.out_pair = (int2*)w.take(sizeof(int2) * (size_t)cap);
-        // levels of >= pack_min pairs go to the host packed (HGX_LS_PACK_MIN, read per call: tests pack tiny levels)
-        a.pack_min = std::getenv("HGX_LS_PACK_MIN") ? std::max<int64_t>(1, std::atoll(std::getenv("HGX_LS_PACK_MIN")))
-                                                    : (int64_t)1 << 20;
+        // levels of >= pack_min pairs go to the host packed (HGX_OPT_SEQ_PACK_MIN: tests pack tiny levels)
+        a.pack_min = g->seq_pack_min > 0 ? g->seq_pack_min : (int64_t)1 << 20;
         a.pack_min = std::max<int64_t>(a.pack_min, 1);
         if (a.pack_min <= cap) {
             a.patom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
@@ -4403,7 +4401,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         a.pull = pull_off ? 0 : pull;
         a.I = g->I;
         a.pin_j = pin_j;
-        a.prof = std::getenv("HGX_LS_PROF") ? 1 : 0;
+        a.prof = trace_env("HGX_LS_PROF") ? 1 : 0;
         if (a.pull && pin_j) {
             ensure_pull_rec(g, pin_j);
             a.prec = root->pull_rec;
@@ -4440,8 +4438,8 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         hgx_ls_seed<<<grid_for(nb, 256), 256, 0, st>>>(a, nb, dseeds);
         HGX_CHECK_LAUNCH();
         const u64 base = g->seq_flag_seq;
-        static const int lr_scatter_g = std::getenv("HGX_LR_SCATTER_G") ? std::atoi(std::getenv("HGX_LR_SCATTER_G")) : kLrG;   // A/B
-        static const int lr_rank_g = std::getenv("HGX_LR_RANK_G") ? std::atoi(std::getenv("HGX_LR_RANK_G")) : kLrG;
+        static const int lr_scatter_g = ab_int("HGX_LR_SCATTER_G", kLrG);   // A/B builds
+        static const int lr_rank_g = ab_int("HGX_LR_RANK_G", kLrG);
         const size_t lp_smem = sizeof(u64) * 4 * (size_t)nb;
         auto enqueue = [&](int32_t d) {
             // grids: thousands of idle workgroups cost ~10 us a launch on small levels;
@@ -4579,7 +4577,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 // the previous part's, already final (same values), the extra leading links fall in the previous
                 // part's link area past its runs or are its own final values
                 const int64_t b0 = std::max<int64_t>(0, ((out0 + b) & ~(int64_t)15) - out0);
-                static const bool align = !(std::getenv("HGX_LS_PACK_ALIGN") && std::atoi(std::getenv("HGX_LS_PACK_ALIGN")) == 0);   // A/B
+                static const bool align = ab_int("HGX_LS_PACK_ALIGN", 1) != 0;   // A/B builds
                 const int64_t bc = align ? b0 : b;
                 HGX_HIP(hipMemcpyAsync(h_atom + bc, a.patom + out0 + bc, sizeof(int32_t) * (size_t)(e - bc), hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(h_link + bc, a.pclink + out0 + bc, sizeof(int32_t) * (size_t)(b + runs - bc),
@@ -4762,7 +4760,7 @@ void seq_levels_all(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t
 // Whether the grid fits: every workgroup must be resident at once (the barrier waits for all), at most
 // 2 per CU and one CU slot left for other streams' kernels.
 int co_threads() {
-    static const int v = std::getenv("HGX_CO_THREADS") && std::atoi(std::getenv("HGX_CO_THREADS")) == 512 ? 512 : kCoThreads;
+    static const int v = ab_int("HGX_CO_THREADS", 0) == 512 ? 512 : kCoThreads;
     return v;
 }
 
@@ -4775,7 +4773,7 @@ bool co_fits(hgx_graph* g) {
         else HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_bfs_coop<kCoThreads>, kCoThreads, 0));
         HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
         const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
-        static const int cap_env = std::getenv("HGX_CO_BLOCKS") ? std::atoi(std::getenv("HGX_CO_BLOCKS")) : 0;   // A/B
+        static const int cap_env = ab_int("HGX_CO_BLOCKS", 0);   // A/B builds
         const int64_t cap = cap_env >= kCoMinBlocks ? std::min(cap_env, kCoMaxBlocks) : kCoBlocks;
         g->co_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, cap) : 0;
     }
@@ -4859,11 +4857,11 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.min_arity = o.return_source ? 1 : 2;
     a.mode = mode;
     a.maxd = max_depth < 0 ? INT32_MAX : max_depth;
-    static const int chunk_env = std::getenv("HGX_CO_CHUNK") ? std::atoi(std::getenv("HGX_CO_CHUNK")) : 0;
+    static const int chunk_env = ab_int("HGX_CO_CHUNK", 0);
     a.chunk = chunk_env > 0 ? std::min(chunk_env, 1 << 20) : kCoChunk;   // entries < 2^23 (co_item)
-    static const int bg_env = std::getenv("HGX_CO_BARGROUPS") ? std::atoi(std::getenv("HGX_CO_BARGROUPS")) : 0;   // A/B
+    static const int bg_env = ab_int("HGX_CO_BARGROUPS", 0);   // A/B builds
     a.bgroups = bg_env > 0 ? std::min(bg_env, kCoBarGroups) : 1;
-    static const bool lite_off = std::getenv("HGX_CO_LITE") && std::atoi(std::getenv("HGX_CO_LITE")) == 0;   // A/B
+    static const bool lite_off = ab_int("HGX_CO_LITE", 1) == 0;   // A/B builds
     a.lite = lite_off ? 0 : 1;
     a.vwords = vwords;
     a.vis = g->co_vis;
@@ -4878,9 +4876,8 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
     a.lvl_end = (int64_t*)hmd + r.m_lev;
     a.lvl_trace = a.lvl_end + (size_t)kcap * kCoMaxLevels;
     a.blk_bytes = (int64_t*)hmd + r.m_blk;
-    const char* to_s = std::getenv("HGX_CO_TIMEOUT");   // read per launch (tests toggle it)
-    const long long to_env = to_s ? std::atoll(to_s) : 0;
-    a.timeout = to_env > 0 ? (u64)to_env : kCoTimeout;   // tests force the timeout path with a few ticks
+    // HGX_OPT_CO_TIMEOUT (per graph, read per launch): tests force the timeout path with a few ticks
+    a.timeout = g->co_timeout > 0 ? (u64)g->co_timeout : kCoTimeout;
 }
 
 // A launch finished cleanly: block 0 left the level loop normally with both status words clear, and no
@@ -4899,7 +4896,7 @@ void co_collect(hgx_graph* g, CoRun& r, const std::vector<int32_t>& sidx, BlockS
     const int32_t k = (int32_t)sidx.size();
     const int64_t* hm = r.hm;
     const int32_t nlev = (int32_t)hm[1];   // level counts per seed from the per-level atom counts
-    static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
+    static const bool trace = trace_env("HGX_CO_TRACE");
     if (trace) {   // per level: microseconds since the first level, work items
         const int64_t* tr = hm + r.m_lev + (size_t)r.a.kcap * kCoMaxLevels;
         std::fprintf(stderr, "[hgx coop] k=%d levels=%d:", k, nlev);
@@ -5003,7 +5000,7 @@ int sc_fits(hgx_graph* g) {   // its grid (0: does not fit); the same residency 
         HGX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hgx_seq_coop<256>, 256, 0));
         HGX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device));
         const int64_t blocks = (int64_t)std::min(per_cu - 1, 2) * cus;
-        static const int cap_env = std::getenv("HGX_SC_BLOCKS") ? std::atoi(std::getenv("HGX_SC_BLOCKS")) : 0;   // A/B
+        static const int cap_env = ab_int("HGX_SC_BLOCKS", 0);   // A/B builds
         const int64_t cap = cap_env >= kCoMinBlocks ? std::min(cap_env, kCoMaxBlocks) : kCoBlocks;
         g->sc_ok = blocks >= kCoMinBlocks ? (int32_t)std::min<int64_t>(blocks, cap) : 0;
     }
@@ -5019,7 +5016,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
     const YieldAdj* ya = stage_yield_adj(g, mode, o);
     const int32_t k = (int32_t)sidx.size();
     if (!ya || k == 0 || k > kMaxCoSeeds || !sc_fits(g)) return false;
-    static const bool off = std::getenv("HGX_SEQ_COOP") && std::atoi(std::getenv("HGX_SEQ_COOP")) == 0;   // A/B
+    static const bool off = ab_int("HGX_SEQ_COOP", 1) == 0;   // A/B builds
     if (off) return false;
     hipStream_t st = g->stream;
     const int64_t vwords = g->A / 64 + 1;
@@ -5080,8 +5077,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
         a.hmeta = (int64_t*)hmd;
         a.blk_bytes = (int64_t*)hmd + 8;
-        const char* to_s = std::getenv("HGX_CO_TIMEOUT");
-        a.timeout = to_s && std::atoll(to_s) > 0 ? (u64)std::atoll(to_s) : kCoTimeout;
+        a.timeout = g->co_timeout > 0 ? (u64)g->co_timeout : kCoTimeout;   // HGX_OPT_CO_TIMEOUT (tests)
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (g->timing) {
             ev[0] = ev_take(g);
@@ -5108,7 +5104,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             ev_give(g, ev[1]);
         }
         const bool clean = hm[0] == 0 && hm[3] == 0;
-        static const bool trace = std::getenv("HGX_CO_TRACE") != nullptr;
+        static const bool trace = trace_env("HGX_CO_TRACE");
         if (trace)
             std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld\n", k,
                          (long long)hm[0], (long long)hm[3], (long long)hm[1], (long long)hm[2]);
@@ -5194,7 +5190,7 @@ void bfs_block(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_t max_
     const size_t per_seed = (size_t)kBbPairs * 8 + 32;
     // The grid stage goes on the stream right behind the workgroup launches and reads their overflow
     // list itself: one wait for both (HGX_CO_CHAIN=0, for A/B: a host round trip in between).
-    static const bool chain_env = !(std::getenv("HGX_CO_CHAIN") && std::atoi(std::getenv("HGX_CO_CHAIN")) == 0);
+    static const bool chain_env = ab_int("HGX_CO_CHAIN", 1) != 0;
     std::unique_ptr<CoRun> cr;
     if (g->bfs_block == 1 && chain_env && n_seeds > 0 && co_fits(g)) {
         cr.reset(new CoRun(g));
@@ -5482,9 +5478,13 @@ struct hgx_seq_result {
     double traversed = 0;
     double ms_block = 0, bytes_block = 0;   // the workgroup engine's launches: device ms, algorithmic bytes
     mutable double ms_level = 0;            // the level-synchronous engine: device ms (timing on) ...
-    // timing events of a call whose pair copies were still running when it returned (read on first use)
+    // timing events of a call whose pair copies were still running when it returned (read on first use).
+    // settle() runs from the const stats readers and the destructor, possibly from several threads at once
+    // (hgx.h: every entry point is thread-safe): the mutex makes the event read + destroy happen once.
     mutable hipEvent_t lz_ev0 = nullptr, lz_ev1 = nullptr, lz_el0 = nullptr, lz_el1 = nullptr;
+    mutable std::mutex lz_mu;
     void settle() const {
+        std::lock_guard<std::mutex> lk(lz_mu);
         float ms = 0;
         if (lz_el1 && hipEventSynchronize(lz_el1) == hipSuccess && hipEventElapsedTime(&ms, lz_el0, lz_el1) == hipSuccess)
             ms_level = ms;
@@ -5795,7 +5795,7 @@ int hgx_seq_result_pairs(const hgx_seq_result* r, int32_t* links, int32_t* atoms
     // large caller arrays are usually fresh (their pages first touched by the copy below): ask for
     // transparent huge pages on their 2 MB-aligned interior, 512x fewer page faults where the kernel's THP
     // mode is "madvise" (a hint: no effect under "never", already the case under "always")
-    static const bool thp = !(std::getenv("HGX_READOUT_THP") && std::atoi(std::getenv("HGX_READOUT_THP")) == 0);
+    static const bool thp = ab_int("HGX_READOUT_THP", 1) != 0;
     if (thp && r->off.back() >= ((int64_t)1 << 24)) {
         auto hint = [](void* p, size_t bytes) {
             if (!p) return;

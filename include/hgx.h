@@ -335,16 +335,16 @@ int  hgx_seq_result_stats(const hgx_seq_result *r, double *ms_total, double *tra
  * pairs written).  Any output may be NULL. */
 int  hgx_seq_result_engine_stats(const hgx_seq_result *r, int32_t *n_block, int32_t *n_level, double *ms_block,
                                  double *bytes_block);
+/* The order-exact grid stage (one persistent launch for <= 64 of the seeds the workgroup engine handed
+ * over, when the generator has a yield adjacency: ordered modes or a link type): seeds it finished, its
+ * device ms (timing enabled) and algorithmic bytes.  Any output may be NULL. */
+int  hgx_seq_result_grid_stats(const hgx_seq_result *r, int32_t *n_seeds, double *ms, double *bytes);
 /* The level-synchronous engine's part of the call (the seeds the workgroup engine handed over):
  * device ms from its first operation to its last (timing enabled; it includes the pairs' copy to the
  * host), its algorithmic bytes (kernel counters: per item its entry, row, type, target offsets and
  * targets, per yield the examined word and the hash slot; per pulled atom its incidence range, examined
  * row, entries, link rows, union bits, frontier rows, pin indices and hash probes; the frontier
  * entries of the pull tables), and how many of its levels ran as pulls.  Any output may be NULL. */
-/* The order-exact grid stage (one persistent launch for <= 64 of the seeds the workgroup engine handed
- * over, when the generator has a yield adjacency: ordered modes or a link type): seeds it finished, its
- * device ms (timing enabled) and algorithmic bytes.  Any output may be NULL. */
-int  hgx_seq_result_grid_stats(const hgx_seq_result *r, int32_t *n_seeds, double *ms, double *bytes);
 int  hgx_seq_result_level_stats(const hgx_seq_result *r, double *ms_level, double *bytes_level, int64_t *pull_levels);
 void hgx_seq_result_free(hgx_seq_result *r);
 /* Batched conjunctive pattern queries.  Result of query q = the link atoms L with
@@ -516,6 +516,27 @@ int  hgx_shard_graph_create(const hgx_shard *s, int32_t device, hgx_graph **out)
  * (A + 1) * 8 bytes of offsets + 8 bytes per yielded (target, link) pair, skipped above 4 GB; and a
  * list of the entries that can yield, (A + 1) * 8 + 4 per entry.  At most 8 of each per snapshot. */
 #define HGX_OPT_BFS_BLOCK 14
+/* Test and diagnostic options (per graph; an execution context takes its snapshot's values when made).
+ * The library reads no tuning knob from the environment (only tracing switches); the
+ * measured-negative A/B variants live in A/B builds only (tools/build_variant.sh).
+ *   HGX_OPT_CO_TIMEOUT   the grid stages' barrier limit in s_memrealtime ticks (100 MHz); 0 = 1 s.  A few
+ *                        ticks force the fallback path (the seeds rerun on the other engine, exact).
+ *   HGX_OPT_SEQ_PULL     order-exact level engine: 0 = push every level, 1 = pull wide levels (default),
+ *                        2 = pull every level.
+ *   HGX_OPT_SEQ_SMALL    1 = the level engine starts from tiny capacities (every growth path runs).
+ *   HGX_OPT_SEQ_TLIMIT   > 0 lowers the level engine's per-chunk stream-key limit (exercises chunk splits).
+ *   HGX_OPT_SEQ_PACK_MIN levels of at least this many pairs cross PCIe packed (0 = 2^20).
+ *   HGX_OPT_XB_FLAT      partition shards: the broadcast pack walks owned atoms (0), takes the broadcast
+ *                        entries on dense levels (1) or on every level (2); -1 = default (1).
+ *   HGX_OPT_XB_STATIC    partition shards: static broadcast never (0), when the group's reduce says so (1),
+ *                        every level (2); -1 = default (1).  Every part of a group must use the same value. */
+#define HGX_OPT_CO_TIMEOUT   15
+#define HGX_OPT_SEQ_PULL     16
+#define HGX_OPT_SEQ_SMALL    17
+#define HGX_OPT_SEQ_TLIMIT   18
+#define HGX_OPT_SEQ_PACK_MIN 19
+#define HGX_OPT_XB_FLAT      20
+#define HGX_OPT_XB_STATIC    21
 /* Coalescing statistics of a graph since its creation: device batches run by the packed pattern path
  * and caller batches they served (caller / device = the mean coalescing factor). */
 int  hgx_query_coalesce_stats(hgx_graph *g, int64_t *device_batches, int64_t *caller_batches);

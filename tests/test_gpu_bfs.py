@@ -566,9 +566,9 @@ def test_multi_workgroup_stage_vs_rows_engine(case):
 
 
 @pytest.mark.parametrize("blk", (1, 2))
-def test_grid_stage_barrier_timeout_falls_back(blk, monkeypatch):
+def test_grid_stage_barrier_timeout_falls_back(blk):
     """a grid-stage launch whose barrier times out (its workgroups not all resident in
-    time; forced here with a limit of one clock tick, HGX_CO_TIMEOUT) must not be reported as finished.
+    time; forced here with a limit of one clock tick, HGX_OPT_CO_TIMEOUT) must not be reported as finished.
     Its seeds rerun on the rows engine with exact results, the fallback is counted (coop_fallbacks), and
     the bitmaps it left are cleared: the next batch on the same graph, with the normal limit, is exact
     and runs on the grid stage.  blk 1: the chained hand-over behind the workgroup stage; blk 2: the
@@ -591,11 +591,8 @@ def test_grid_stage_barrier_timeout_falls_back(blk, monkeypatch):
     lv_want = {i: [ref.visited(int(i), d).copy() for d in range(c_ref.shape[1])] for i in big[:3]}
     ref.close()
     snap.set_option(_lib.HGX_OPT_BFS_BLOCK, blk)
-    for limit in ("1", None):
-        if limit:
-            monkeypatch.setenv("HGX_CO_TIMEOUT", limit)
-        else:
-            monkeypatch.delenv("HGX_CO_TIMEOUT", raising=False)
+    for limit in (1, 0):
+        snap.set_option(_lib.HGX_OPT_CO_TIMEOUT, limit)
         r = bfs_batch(snap, seeds, None, gen_)
         c = r.counts()
         n = max(c.shape[1], c_want.shape[1])

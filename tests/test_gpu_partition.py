@@ -26,7 +26,7 @@ def parts(g, NP, device=0):
     return out
 
 
-def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=None, xmode=None):
+def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=None, xmode=None, xb=None):
     from hypergraphdb_amd import _lib, bfs_batch
     from hypergraphdb_amd.partition import pbfs_batch_group
     snap = snapshot(g)
@@ -37,6 +37,10 @@ def compare(g, NP, seeds, maxd, mode=K.ALGEN_MODES[0], lt=-1, n_oracle=4, flags=
     if xmode is not None:
         for s in sh:
             s.set_option(_lib.HGX_OPT_PART_EXCHANGE, xmode)
+    if xb is not None:   # (HGX_OPT_XB_FLAT, HGX_OPT_XB_STATIC) on every part
+        for s in sh:
+            s.set_option(_lib.HGX_OPT_XB_FLAT, xb[0])
+            s.set_option(_lib.HGX_OPT_XB_STATIC, xb[1])
     ref = bfs_batch(snap, seeds, maxd, gen(snap, mode, lt))
     res = pbfs_batch_group(sh, seeds, maxd, gen(None, mode, lt))
     rc, pc = ref.counts(), res.counts()
@@ -271,34 +275,33 @@ def test_two_processes_gloo_transport():
     assert all(p.exitcode == 0 for p in ps)
 
 
-@pytest.mark.parametrize("flat,static", [("0", "0"), ("1", "0"), ("2", "0"), ("1", "1"), ("0", "2")])
-def test_broadcast_pack_forms(flat, static, monkeypatch):
-    """The broadcast pack walks owned atoms (HGX_XB_FLAT=0), takes the broadcast entries on dense
-    levels (1, the default) or on every level (2); with HGX_XB_STATIC every broadcast entry ships a
+@pytest.mark.parametrize("flat,static", [(0, 0), (1, 0), (2, 0), (1, 1), (0, 2)])
+def test_broadcast_pack_forms(flat, static):
+    """The broadcast pack walks owned atoms (HGX_OPT_XB_FLAT 0), takes the broadcast entries on dense
+    levels (1, the default) or on every level (2); with HGX_OPT_XB_STATIC every broadcast entry ships a
     record at its static slot (mask 0 without news) on the levels where the group's ghosts nearly all
     had news (1, the default) or on every level (2): identical results to the whole-snapshot engine
     and the oracle on 2, 3 and 8 parts, dense (1024 sources on a power-law hypergraph) and sparse
     levels."""
     from hypergraphdb_amd import synth
-    monkeypatch.setenv("HGX_XB_FLAT", flat)
-    monkeypatch.setenv("HGX_XB_STATIC", static)
+    xb = (flat, static)
     rng = np.random.default_rng(90)
     g = K.random_graph(rng, 1500, 2500, max_arity=7, n_types=3)
     seeds = rng.integers(0, g["num_atoms"], 300).astype(np.int32)
     for NP in (3, 8):
-        compare(g, NP, seeds, None)
-    compare(g, 3, seeds, None, K.ALGEN_MODES[6], 2)
+        compare(g, NP, seeds, None, xb=xb)
+    compare(g, 3, seeds, None, K.ALGEN_MODES[6], 2, xb=xb)
     h = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=23)
     hs = rng.integers(0, h["num_atoms"], 1024).astype(np.int32)
     for NP in (2, 8):
-        st = compare(h, NP, hs, 4)
+        st = compare(h, NP, hs, 4, xb=xb)
         assert all(s["bytes_exchanged"] > 0 for s in st)
         # host round trips of level 0 (not the final level): counted records in both phases take 6,
         # a static broadcast 4; the final level (no broadcast) 4
         for s in st:
-            if static == "2":
+            if static == 2:
                 assert s["level_xtrips"][0] == 4, s["level_xtrips"]
-            elif static == "0":
+            elif static == 0:
                 assert s["level_xtrips"][0] == 6, s["level_xtrips"]
             if len(s["level_xtrips"]) == 4:
                 assert s["level_xtrips"][3] == 4, s["level_xtrips"]

@@ -206,46 +206,46 @@ def test_level_engine_capacity_growth_and_depth_limits():
     """The level-synchronous engine grows its capacities (discoveries, bitmap words, tiles, runs)
     from small starting values on a graph whose levels exceed them, then stays exact; every depth
     limit 0..4 and unbounded, against the oracle."""
-    import os
     from hypergraphdb_amd import _lib, synth
     g = synth.hypergraph(30000, 60000, 2, 6, 2.0, 1, seed=13)
-    os.environ["HGX_LS_SMALL"] = "1"
-    try:
-        snap, orc = snapshot(g), oracle(g)
-        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
-        seeds = np.array([0, 1, 2, 29999, 15000, 0], np.int32)
-        for maxd in (0, 1, 2, 3, 4, None):
-            check_seq(g, seeds, maxd, K.ALGEN_MODES[maxd % 3 if maxd else 0], -1, snap, orc)
-        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
-    finally:
-        del os.environ["HGX_LS_SMALL"]
+    snap, orc = snapshot(g), oracle(g)
+    snap.set_option(_lib.HGX_OPT_SEQ_SMALL, 1)
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
+    seeds = np.array([0, 1, 2, 29999, 15000, 0], np.int32)
+    for maxd in (0, 1, 2, 3, 4, None):
+        check_seq(g, seeds, maxd, K.ALGEN_MODES[maxd % 3 if maxd else 0], -1, snap, orc)
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
 
 
-def _seq_env(snap, seeds, maxd, g_, env):
-    """hgx_bfs_sequence on the level-synchronous engine alone (HGX_OPT_SEQ_ENGINE 2) under env vars."""
+# the level engine's test options (hgx_set_option; the library reads no tuning knob from the environment)
+SEQ_OPTS = {"pull": "HGX_OPT_SEQ_PULL", "small": "HGX_OPT_SEQ_SMALL", "tlimit": "HGX_OPT_SEQ_TLIMIT",
+            "pack_min": "HGX_OPT_SEQ_PACK_MIN"}
+SEQ_DEFAULTS = {"pull": 1, "small": 0, "tlimit": 0, "pack_min": 0}
+
+
+def _seq_opts(snap, seeds, maxd, g_, opts):
+    """hgx_bfs_sequence on the level-synchronous engine alone (HGX_OPT_SEQ_ENGINE 2) under the given level
+    engine options (restored to the defaults afterwards)."""
     from hypergraphdb_amd import _lib, bfs_sequence
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: str(v) for k, v in env.items()})
+    for k, v in opts.items():
+        snap.set_option(getattr(_lib, SEQ_OPTS[k]), int(v))
     snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
     try:
         return bfs_sequence(snap, seeds, maxd, g_)
     finally:
         snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+        for k in opts:
+            snap.set_option(getattr(_lib, SEQ_OPTS[k]), SEQ_DEFAULTS[k])
 
 
 @pytest.mark.parametrize("case", range(5))
 def test_level_engine_pull_and_push_levels_agree(case):
-    """Round 5: the level engine without a per-seed key array.  Every level pushed (HGX_LS_PULL 0: the
+    """Round 5: the level engine without a per-seed key array.  Every level pushed (HGX_OPT_SEQ_PULL 0: the
     level hash), every level pulled (2: frontier rows, union bitmap, pin index, per-seed minima in LDS;
     heavy atoms by 4096-entry chunks), and the default choice by width (1) give the oracle's exact
     sequences -- links, atoms, distances, traversed items -- in every generator mode, with typed links,
     links targeting links, repeated targets, duplicate seeds, > 64 seeds (several row words) and hubs
-    above 512 incidences (the pull's heavy chunks); starting capacities tiny (HGX_LS_SMALL) in case 4."""
+    above 512 incidences (the pull's heavy chunks); starting capacities tiny (HGX_OPT_SEQ_SMALL) in case 4."""
     from hypergraphdb_amd import synth
     rng = np.random.default_rng(950 + case)
     if case < 2:
@@ -257,7 +257,7 @@ def test_level_engine_pull_and_push_levels_agree(case):
     n_seeds = [40, 70, 130, 64, 300][case]
     seeds = rng.integers(0, g["num_atoms"], n_seeds).astype(np.int32)
     seeds[-1] = seeds[0]
-    extra = {"HGX_LS_SMALL": 1} if case == 4 else {}
+    extra = {"small": 1} if case == 4 else {}
     pulled = 0
     for mi, mode in enumerate(K.ALGEN_MODES):
         if case >= 2 and mi % 3:
@@ -266,7 +266,7 @@ def test_level_engine_pull_and_push_levels_agree(case):
         for maxd in ((None, 2) if case != 3 else (3,)):
             outs = {}
             for pull in (0, 2, 1):
-                outs[pull] = _seq_env(snap, seeds, maxd, gen(snap, mode, lt), dict(extra, HGX_LS_PULL=pull))
+                outs[pull] = _seq_opts(snap, seeds, maxd, gen(snap, mode, lt), dict(extra, pull=pull))
             a = outs[0]
             for pull in (2, 1):
                 b = outs[pull]
@@ -286,7 +286,7 @@ def test_level_engine_pull_and_push_levels_agree(case):
 @pytest.mark.parametrize("case", range(3))
 def test_level_engine_packed_transfer(case):
     """Round 5: large levels go to the host packed (atoms, run-start bits, the links of run starts, block
-    run counts; HGX_LS_PACK_MIN, default 2^20 pairs).  Packing every level (1) gives the unpacked engine's
+    run counts; HGX_OPT_SEQ_PACK_MIN, default 2^20 pairs).  Packing every level (1) gives the unpacked engine's
     exact sequences and the oracle's, through the whole-result readout and through ranged reads whose
     windows start anywhere (inside a run of one link, at a rank-part boundary); one seed, repeated links and
     > 64 seeds included."""
@@ -301,8 +301,8 @@ def test_level_engine_packed_transfer(case):
     for mi, mode in enumerate(K.ALGEN_MODES[:3]):
         for maxd in (2, None):
             gn = gen(snap, mode, -1)
-            a = _seq_env(snap, seeds, maxd, gn, {"HGX_LS_PACK_MIN": 1 << 40})
-            b = _seq_env(snap, seeds, maxd, gn, {"HGX_LS_PACK_MIN": 1})
+            a = _seq_opts(snap, seeds, maxd, gn, {"pack_min": 1 << 40})
+            b = _seq_opts(snap, seeds, maxd, gn, {"pack_min": 1})
             assert np.array_equal(a.offsets, b.offsets), (case, mi, maxd)
             assert np.array_equal(a.atoms, b.atoms) and np.array_equal(a.links, b.links), (case, mi, maxd)
             assert np.array_equal(a.dists, b.dists) and a.traversed_edges == b.traversed_edges, (case, mi, maxd)
@@ -312,8 +312,7 @@ def test_level_engine_packed_transfer(case):
                 assert np.array_equal(ga, at) and np.array_equal(gl, l_) and np.array_equal(gd, d), (case, mi, maxd, i)
     # ranged reads of a packed result: every start position of a sample, short and long windows
     from hypergraphdb_amd import _lib
-    old = os.environ.get("HGX_LS_PACK_MIN")
-    os.environ["HGX_LS_PACK_MIN"] = "1"
+    snap.set_option(_lib.HGX_OPT_SEQ_PACK_MIN, 1)
     snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
     h = C.c_void_p()
     try:
@@ -321,10 +320,7 @@ def test_level_engine_packed_transfer(case):
         check(lib().hgx_bfs_sequence(snap.handle, ptr(seeds), len(seeds), -1, C.byref(opts), C.byref(h)))
     finally:
         snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
-        if old is None:
-            del os.environ["HGX_LS_PACK_MIN"]
-        else:
-            os.environ["HGX_LS_PACK_MIN"] = old
+        snap.set_option(_lib.HGX_OPT_SEQ_PACK_MIN, 0)
     try:
         ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
         check(lib().hgx_seq_result_info(h, C.byref(ns), C.byref(npairs), C.byref(nl)))
@@ -349,7 +345,7 @@ def test_level_engine_packed_transfer(case):
 
 
 def test_level_engine_chunk_split_on_wide_keys():
-    """A level whose stream keys do not fit 32 bits splits the chunk (HGX_LS_TLIMIT lowers the limit to
+    """A level whose stream keys do not fit 32 bits splits the chunk (HGX_OPT_SEQ_TLIMIT lowers the limit to
     force it down to single seeds; a single seed that still does not fit runs on the key-array engine):
     the sequences stay the oracle's."""
     from hypergraphdb_amd import synth
@@ -358,7 +354,7 @@ def test_level_engine_chunk_split_on_wide_keys():
     deg = np.bincount(np.asarray(g["tgt_idx"]), minlength=g["num_atoms"])
     seeds = np.concatenate([np.argsort(-deg)[:4], np.arange(100, 120)]).astype(np.int32)
     for lim in (2000, 200000):
-        res = _seq_env(snap, seeds, 3, gen(snap, K.ALGEN_MODES[0]), {"HGX_LS_TLIMIT": lim})
+        res = _seq_opts(snap, seeds, 3, gen(snap, K.ALGEN_MODES[0]), {"tlimit": lim})
         for i in range(len(seeds)):
             l_, at, d, _ = orc.bfs(int(seeds[i]), 3)
             gl, ga, gd = res.pairs(i)
@@ -373,9 +369,9 @@ def test_order_exact_grid_stage_vs_oracle(case):
     bitmap word) when the generator has a yield adjacency.  Exact against the oracle pair by pair (links,
     atoms, distances, traversed items): config-5 closures at 5% scale (the root classes: 12K-250K-atom
     closures over ~20 levels) in both directions with depth limits, a typed power-law graph, and the
-    forced barrier timeout (HGX_CO_TIMEOUT=1: the stage must fall back to the level engine, still exact,
+    forced barrier timeout (HGX_OPT_CO_TIMEOUT 1: the stage must fall back to the level engine, still exact,
     and leave its bitmaps clean for the next call)."""
-    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, bfs_batch, bfs_sequence, synth
+    from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_batch, bfs_sequence, synth
     if case < 3:
         g = synth.config5(scale=0.05, n_sources=40)
         T = int(g["subsumes_type"])
@@ -408,12 +404,11 @@ def test_order_exact_grid_stage_vs_oracle(case):
         maxds = (None, 2)
     for maxd in maxds:
         for attempt in ((1, 0) if case == 2 else (0,)):
-            if attempt:
-                os.environ["HGX_CO_TIMEOUT"] = "1"
+            snap.set_option(_lib.HGX_OPT_CO_TIMEOUT, 1 if attempt else 0)
             try:
                 res = bfs_sequence(snap, seeds, maxd, gen_)
             finally:
-                os.environ.pop("HGX_CO_TIMEOUT", None)
+                snap.set_option(_lib.HGX_OPT_CO_TIMEOUT, 0)
             trav = 0
             for i, s in enumerate(seeds):
                 l_, a, d, tr = orc.bfs(int(s), -1 if maxd is None else maxd, opts)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Kernel traces of one command under several environment settings (A/B of engine knobs), run on the
+# Kernel traces of one command under several environment settings (A/B of engine knobs; the knobs are read
+# only by A/B builds: bash tools/build_variant.sh ab, then HGX_LIB_VARIANT=ab in the settings), run on the
 # GPU box from the repo root:
 #   bash tools/ab_env.sh <tag> "<VAR=v VAR2=w>" "<VAR=x>" ... -- <script.py> [args...]
 # Each setting gets gpurun_out/ab_<tag>/<k>/ (rocprofv3 --kernel-trace --stats) and a line in
