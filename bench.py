@@ -491,6 +491,22 @@ def run_config5(args, ctx, barrier_sync):
         out["cpu_baseline"] = cpu_leg(run, "TEPS", f"the {len(g['seeds'])} closures of each direction, every "
                                       f"traversal stopped after {args.cpu_budget / 2:g}s (C restatement of the "
                                       "subsumption BFS)")
+        # the whole step on the CPU: every one of the 2 x 1024 closures to completion on the job's threads, one
+        # run (the GPU step's exact work; seconds of CPU time)
+        nt = cpu_threads()
+        tr_all, el_all = 0, 0.0
+        for rev in (False, True):
+            tm = {}
+            _, t_ = orc.bfs_many(g["seeds"], -1, 4096, algen(T, False, True, rev, False), nthreads=nt, timing=tm)
+            tr_all += int(t_.sum())
+            el_all += tm["elapsed_s"]
+        nclos = 2 * len(g["seeds"])
+        out["cpu_baseline"]["complete_traversals"] = {
+            "threads": nt, "traversals": nclos, "seconds": round(el_all, 3), "traversed_edges": tr_all,
+            "value": tr_all / el_all, "unit": "TEPS", "closures_per_s": nclos / el_all,
+            "sample": f"all {len(g['seeds'])} closures of each direction to completion (the GPU step's work), one run"}
+        log(f"cpu baseline config5: {nclos} complete closures on {nt} threads in {el_all:.2f}s "
+            f"({tr_all / el_all:.3e} TEPS, {nclos / el_all:.1f} closures/s)")
         # the drop-in's unit of work on the CPU: one order-exact traversal (the oracle's FIFO
         # HGBreadthFirstTraversal, every pair materialised) at a time on one thread, the same seeds as the
         # GPU's single-seed calls
@@ -551,20 +567,35 @@ def dropin_config5(args, ctx, barrier_sync, g, views, gens, pool):
         if not (np.array_equal(a.offsets, b.offsets) and np.array_equal(a.atoms, b.atoms) and
                 np.array_equal(a.links, b.links)):
             raise RuntimeError("dropin: a timed sequence step differs from the first")
-    # roofline of the workgroup-per-seed kernel, each direction alone (launch device time by HIP events)
+    # roofline of each direction alone (device time by HIP events): the stage with the largest device time
+    # a call -- the workgroup-per-seed kernel (hgx_seq_block), the order-exact grid stage (hgx_seq_coop, the
+    # big hg.subsumed closures) or the level engine -- with that direction's own counter pass
+    # (profiles/pmc_dropin5_<direction>.json: tools/seq_c5.py --direction under tools/profile_cmd.sh)
     roofs = {}
+    reps = 5
     for k, name in ((0, "subsumed"), (1, "subsumes")):
-        ms, by = 0.0, 0.0
-        for _ in range(5):
+        acc = {"hgx_seq_block": [0.0, 0.0], "hgx_seq_coop": [0.0, 0.0], "level engine": [0.0, 0.0]}
+        ms_call = 0.0
+        for _ in range(reps):
             r = direction(k)
-            ms += r.ms_block
-            by += r.bytes_block
+            acc["hgx_seq_block"][0] += r.ms_block
+            acc["hgx_seq_block"][1] += r.bytes_block
+            acc["hgx_seq_coop"][0] += r.ms_coop
+            acc["hgx_seq_coop"][1] += r.bytes_coop
+            acc["level engine"][0] += r.ms_level
+            acc["level engine"][1] += r.bytes_level
+            ms_call += r.ms_total
+        dom = max(acc, key=lambda x: acc[x][0])
+        ms, by = acc[dom][0] / reps, acc[dom][1] / reps
         ach = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-        roofs[name] = with_traffic({"bound": "hbm", "kernel": "hgx_seq_block", "achieved": round(ach, 1),
-                                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                                    "avg_launch_ms": round(ms / 5, 4), "bytes_per_launch": by / 5,
-                                    "seeds_workgroup_engine": r.n_block, "seeds_level_engine": r.n_level,
-                                    "ms_per_call": round(r.ms_total, 4)}, "hgx_seq_block", "dropin5", ms / 5)
+        roofs[name] = with_traffic({"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(ms, 4),
+                                    "bytes_per_launch": by, "launches_per_call": 1,
+                                    "stages_per_call": {x: {"device_ms": round(v[0] / reps, 4), "algorithmic_bytes": v[1] / reps}
+                                                        for x, v in acc.items()},
+                                    "seeds_workgroup_engine": r.n_block, "seeds_grid_stage": r.n_coop,
+                                    "seeds_level_engine": r.n_level, "ms_per_call": round(ms_call / reps, 4)},
+                                   dom, f"dropin5_{name}", ms)
     # single-seed calls: the first 200 classes, one traversal per call, each direction
     single = {"seeds": [int(x) for x in g["seeds"][:200]]}
     for k, name in ((0, "subsumed"), (1, "subsumes")):
@@ -583,7 +614,10 @@ def dropin_config5(args, ctx, barrier_sync, g, views, gens, pool):
            "traversed_items_per_step": sum(r.traversed_edges for r in ref),
            "step": "hgx_bfs_sequence of the 1024 classes per direction, the directions on two execution contexts; "
                    "every (link, atom, distance) pair in host arrays",
-           "roofline": roofs["subsumes"], "roofline_subsumed": roofs["subsumed"], "single": single}
+           # the step's bound: the direction whose dominant stage takes longer (the directions run side by side)
+           "roofline": dict(max(roofs.values(), key=lambda x: x["avg_launch_ms"]),
+                            direction=max(roofs, key=lambda n: roofs[n]["avg_launch_ms"])),
+           "roofline_subsumed": roofs["subsumed"], "roofline_subsumes": roofs["subsumes"], "single": single}
     log(f"rank {rank}: dropin config5 {out['value']:.1f} closures/s, {out['ms_per_step']} ms/step; single-seed "
         f"subsumed {single['subsumed']['ms_median']} ms, subsumes {single['subsumes']['ms_median']} ms (median)")
     return out
@@ -617,27 +651,35 @@ def dropin_config2(args, ctx, snap, g):
         kept.append(r)
     dt = time.perf_counter() - t1
     del kept, r
-    # the level engine's roofline: its algorithmic bytes (kernel counters, hgx_seq_result_level_stats) over
-    # its device time (which includes the D2H copy of the pairs), and the dominant kernel's PMC traffic
-    ach = by_lev / (ms_lev / 1e3) / 1e9 if ms_lev > 0 else 0.0
-    roof = {"bound": "hbm", "kernel": "level engine (hgx_ls_* / hgx_lp_*, one call)", "achieved": round(ach, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "frac_from": "algorithmic",
-            "bytes_per_call": by_lev / steps, "ms_per_call": round(ms_lev / steps, 3),
-            "scope": "algorithmic bytes of the level engine's kernels (device counters) over its device time, which "
-                     "includes the D2H copy of the pairs"}
-    # the dominant kernel from the committed counter passes (profiles/pmc_dropin2.json: PMC HBM bytes and
-    # the trace's average duration of the same launches)
+    # the level engine's roofline over its device time a call (which includes the D2H copy of the pairs): `traffic`
+    # = the PMC HBM bytes of every kernel of one steady call summed (profiles/pmc_dropin2.json: tools/seq_c2.py's
+    # last call under tools/profile_cmd.sh, --from-last hgx_ls_seed), `frac` = that over this run's device time;
+    # the engine's own algorithmic byte count (device counters, hgx_seq_result_level_stats) beside it
+    ms_call = ms_lev / steps
+    ach_alg = by_lev / steps / (ms_call / 1e3) / 1e9 if ms_call > 0 else 0.0
+    roof = {"bound": "hbm", "kernel": "level engine (hgx_ls_* / hgx_lp_* / hgx_lr_*, one call)", "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "ms_per_call": round(ms_call, 3), "algorithmic_bytes_per_call": by_lev / steps,
+            "achieved_algorithmic": round(ach_alg, 1), "frac_algorithmic": round(ach_alg / HBM_PEAK_GBS, 4),
+            "achieved": round(ach_alg, 1), "frac": round(ach_alg / HBM_PEAK_GBS, 4), "frac_from": "algorithmic",
+            "traffic": None, "traffic_from": None,
+            "scope": "one hgx_bfs_sequence call: bytes over the level engine's device time, which includes the D2H copy "
+                     "of the pairs"}
     rel = os.path.join("profiles", "pmc_dropin2.json")
     if os.path.exists(os.path.join(ROOT, rel)):
         pj = json.load(open(os.path.join(ROOT, rel)))
         ks = pj.get("kernels", {})
-        dom = max((k for k in ks if k.startswith(("hgx_ls_", "hgx_lp_", "hgx_lr_"))), key=lambda k: ks[k]["avg_ms"] * ks[k]["launches"],
-                  default=None)
-        if dom and ks[dom].get("hbm_bytes_per_launch"):
-            kk = ks[dom]
+        call = sum((v.get("hbm_bytes_per_launch") or 0.0) * v["launches"] for v in ks.values())
+        if call > 0 and ms_call > 0:
+            a_ = call / (ms_call / 1e3) / 1e9
+            roof.update(traffic=call, traffic_from=f"{rel}@{pj.get('commit') or _git_sha(rel)}", achieved=round(a_, 1),
+                        frac=round(a_ / HBM_PEAK_GBS, 4), frac_from="pmc",
+                        traffic_over_algorithmic=round(call / (by_lev / steps), 3) if by_lev else None,
+                        traffic_scope="PMC HBM bytes of every kernel of one steady call, summed")
+        hk = {k: v for k, v in ks.items() if k.startswith(("hgx_ls_", "hgx_lp_", "hgx_lr_")) and v.get("hbm_bytes_per_launch")}
+        dom = max(hk, key=lambda k: hk[k]["avg_ms"] * hk[k]["launches"], default=None)
+        if dom:
+            kk = hk[dom]
             a_ = kk["hbm_bytes_per_launch"] / (kk["avg_ms"] / 1e3) / 1e9
-            roof["traffic"] = kk["hbm_bytes_per_launch"]
-            roof["traffic_from"] = f"{rel}@{pj.get('commit') or _git_sha(rel)}"
             roof["dominant_kernel_pmc"] = {"kernel": dom, "traffic": kk["hbm_bytes_per_launch"],
                                            "avg_launch_ms": kk["avg_ms"], "launches": kk["launches"],
                                            "achieved": round(a_, 1), "frac": round(a_ / HBM_PEAK_GBS, 4)}

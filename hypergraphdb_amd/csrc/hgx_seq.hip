@@ -2593,6 +2593,111 @@ struct LpProf {
     int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
+// The k-th set bit (k < popcount) of w.
+__device__ __forceinline__ int lp_select_bit(u64 w, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const u64 lo = w & ((1ull << sh) - 1ull);
+        const int c = __popcll(lo);
+        if (k >= c) {
+            k -= c;
+            w >>= sh;
+            pos += sh;
+        } else {
+            w = lo;
+        }
+    }
+    return pos;
+}
+
+// Phase B of the pull walk for <= 64 seeds (round 6): a lane per (hit, seed) candidate
+// for the loads.  The lane-per-seed steps (HB = 8 hits of one atom, a frontier-row word and a 256-byte item
+// row each) took one dependent round trip per 8 hits with most lanes idle (a hit yields ~7 candidate seeds
+// of 64 on config 2's drop-in level).  Here the wave loads the frontier rows of 64 hits at once (a lane per
+// hit), masks them with the hit atom's unexamined seeds, flattens the set bits into candidates (wave
+// prefix; a candidate finds its hit by binary search over the prefix and its seed by bit selection) and
+// loads the item offsets E[u * nb + s] of kLpCB x 64 candidates at once (4 bytes each instead of whole
+// rows).  The minima stay lane-per-seed (best, flushed per atom as before): a batch's candidates are in
+// hit order, so one atom's are consecutive; per atom segment of a chunk the candidates lower the wave's LDS
+// row brow[s] (ds atomicMin), then lane s folds brow[s] into best and clears it.
+constexpr int kLpCB = 4;   // candidate chunks of 64 whose loads are in flight together
+template <class FlushCur>
+__device__ __forceinline__ void lp_phase_b1(const LsArgs& a, const LpHit* hits, int total, u64 vw0, u64 lastmask,
+                                            int& cur, u64* best, u64* brow, int64_t& nbytes, FlushCur&& flush_cur) {
+    const int lane = threadIdx.x & 63;
+    for (int g0 = 0; g0 < total; g0 += 64) {   // hits a lane each (wave-uniform)
+        const int h = g0 + lane;
+        LpHit hq = {0, 0u, 0, 0u};
+        if (h < total) hq = hits[h];
+        // (every lane shuffles: a lane shuffle reads 0 from a source lane that is inactive at the call)
+        const u64 need = ~__shfl(vw0, (int)(hq.kq_o >> 16)) & lastmask;   // the seeds that have not examined the hit's atom
+        u64 fw = 0ull;
+        if (h < total) fw = a.frow[(int64_t)hq.u] & need;                 // (W == 1: one word a union slot)
+        const int nc = __popcll(fw);
+        int px = nc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(px, off);
+            if (lane >= off) px += y;
+        }
+        const int ncand = __shfl(px, 63), exc = px - nc;
+        nbytes += h < total ? 8 : 0;
+        for (int c0 = 0; c0 < ncand; c0 += 64 * kLpCB) {   // kLpCB chunks of candidates, a lane each (wave-uniform)
+            u64 v[kLpCB];
+            int sd[kLpCB], od[kLpCB];
+#pragma unroll
+            for (int q = 0; q < kLpCB; ++q) {
+                const int c = c0 + q * 64 + lane;
+                int hl = 0;   // the candidate's hit lane: the last lane whose candidates start at or before c
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const int mid = hl + step;
+                    if (__shfl(exc, mid) <= c) hl = mid;
+                }
+                const u64 fwh = __shfl(fw, hl);
+                const int32_t u = __shfl(hq.u, hl);
+                const uint32_t j = __shfl(hq.j, hl);
+                const int32_t la = __shfl(hq.la, hl);
+                const uint32_t kq_o = __shfl(hq.kq_o, hl);
+                const int exh = __shfl(exc, hl);
+                const bool live = c < ncand;
+                sd[q] = live ? lp_select_bit(fwh, c - exh) : 0;
+                od[q] = (int)(kq_o >> 16);
+                v[q] = ~0ull;
+                if (live) {
+                    const uint32_t pre = a.E[(int64_t)u * a.nb + sd[q]];
+                    v[q] = ((((((u64)pre + j) << a.kbits) | (kq_o & 0xFFFFu)) + 1ull) << 32) | (u64)(uint32_t)la;
+                    nbytes += 4;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kLpCB; ++q) {
+                const int m = min(64, ncand - c0 - q * 64);   // live lanes of chunk q (wave-uniform)
+                if (m <= 0) break;
+                for (int k = 0; k < m;) {   // the chunk's atom segments, in order (wave-uniform)
+                    const int ok = __builtin_amdgcn_readlane(od[q], k);
+                    const u64 seg = __ballot(lane >= k && lane < m && od[q] == ok);
+                    if (ok != cur) {   // the candidates moved on to the next atom: flush the finished one
+                        if (cur >= 0) flush_cur();
+                        cur = ok;
+                    }
+                    if ((seg >> lane) & 1ull) atomicMin((unsigned long long*)&brow[sd[q]], (unsigned long long)v[q]);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < a.nb) {   // (the wave's row holds nb seeds)
+                        best[0] = min(best[0], brow[lane]);
+                        brow[lane] = ~0ull;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    k = 64 - __clzll((unsigned long long)seg);   // past the segment's last lane
+                }
+            }
+        }
+    }
+}
+
 // The pull walk of one wave over the concatenated incidence ranges of up to 64 atoms (lane o: atom
 // at, entries [eb, eb + cnt), examined words vw[]): 64 entries a pass.  Phase A, a lane per entry:
 // its hits, written into the wave's LDS list in entry order (so each atom's hits are contiguous).
@@ -2604,7 +2709,7 @@ struct LpProf {
 // 1.7e9 (hit, seed) candidates), so the seeds stay on the lanes; HB = 16 / WW hits a step keeps the
 // wave's loads in flight (4 a step: 87 ms for that level, latency-bound at ~4 us a step).
 template <int WW, class Flush>
-__device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb, int64_t cnt, const u64* vw, LpHit* hits,
+__device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb, int64_t cnt, const u64* vw, LpHit* hits, u64* brow,
                                         u64* best, int64_t& nbytes, LpProf& pf, Flush&& flush) {
     constexpr int HB = WW >= 4 ? 2 : 8 / WW;
     const int lane = threadIdx.x & 63;
@@ -2690,6 +2795,9 @@ __device__ __forceinline__ void lp_walk(const LsArgs& a, int32_t at, int64_t eb,
             pf.v[0] += tb_ - ta;
             pf.v[3] += 1;
         }
+        if constexpr (WW == 1) {   // phase B over (hit, seed) candidates (<= 64 seeds: one row word)
+            lp_phase_b1(a, hits, total, vw[0], lastmask, cur, best, brow, nbytes, flush_cur);
+        } else
         for (int h0 = 0; h0 < total;) {   // phase B (wave-uniform)
             // only the union slots stay in registers while the rows load (the other fields are read
             // from LDS again after): 2 waves/SIMD at 235 VGPRs with whole hits held
@@ -2786,7 +2894,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) h
         const int64_t q = (ch.end - ch.beg + 3) / 4;
         const int64_t b = ch.beg + wave * q, e = min(ch.end, b + q);
         // one "atom" on lane 0: this wave's quarter of the chunk
-        lp_walk<WW>(a, t, lane == 0 ? b : 0, lane == 0 ? max<int64_t>(e - b, 0) : 0, vw, hits, best, nbytes, pf,
+        lp_walk<WW>(a, t, lane == 0 ? b : 0, lane == 0 ? max<int64_t>(e - b, 0) : 0, vw, hits, lp_merge + (int64_t)wave * nb, best, nbytes, pf,
                     [&](int, u64* bst) {
 #pragma unroll
                         for (int w = 0; w < WW; ++w)
@@ -2832,7 +2940,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) h
                 if (any) cnt = ee - eb;
             }
         }
-        lp_walk<WW>(a, (int32_t)t, eb, cnt, vw, hits, best, nbytes, pf, [&](int o, u64* bst) {
+        lp_walk<WW>(a, (int32_t)t, eb, cnt, vw, hits, lp_merge + (int64_t)wave * nb, best, nbytes, pf, [&](int o, u64* bst) {
 #pragma unroll
             for (int w = 0; w < WW; ++w) {   // the atom's discoveries: a lane per seed
                 if (w >= W) break;
@@ -3752,18 +3860,27 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         const int64_t Wn = (T + 63) / 64;
         {   // the words' popcounts and degree sums -> exclusive prefixes in LDS (every block)
             constexpr int per = kScWords / NT;
-            int64_t c = 0, g2 = 0;
-            uint32_t cw[per];
-            u64 dw[per];
-#pragma unroll
-            for (int q = 0; q < per; ++q) {
-                const int64_t w = (int64_t)threadIdx.x * per + q;
+            // coalesced loads first (lane-consecutive words: a wave's load is 4 cache lines, where a thread's
+            // own run of `per` words made every lane of a load a line of its own -- 16x the memory requests
+            // of the level's bitmap, read by every block), staged in LDS: the bitmap words in s_kbm, the
+            // degree sums in s_dpre (u32 like the prefixes they become; a level's items stay < 2^32)
+            for (int64_t w = threadIdx.x; w < (int64_t)kScWords; w += NT) {
                 u64 bw = 0, dd = 0;
                 if (w < Wn) {
                     bw = sc_ld(a.kbm + w);    // [xwg]
                     dd = sc_ld(a.wdeg + w);   // [xwg]
                 }
-                s_kbm[threadIdx.x * per + q] = bw;
+                s_kbm[w] = bw;
+                s_dpre[w] = (uint32_t)dd;
+            }
+            __syncthreads();
+            int64_t c = 0, g2 = 0;
+            uint32_t cw[per];
+            u64 dw[per];
+#pragma unroll
+            for (int q = 0; q < per; ++q) {   // this thread's run of words (it alone rewrites them below)
+                const u64 bw = s_kbm[threadIdx.x * per + q];
+                const u64 dd = s_dpre[threadIdx.x * per + q];
                 cw[q] = (uint32_t)__popcll(bw);
                 dw[q] = dd;
                 c += cw[q];

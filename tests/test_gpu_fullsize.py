@@ -239,3 +239,30 @@ def test_config2_dropin_sequence_large_readout(config2):
         b, e = off[i], off[i + 1]
         assert np.array_equal(atoms[b:e], a) and np.array_equal(links[b:e], l) and np.array_equal(dists[b:e], d), i
     _ = _lib
+
+
+@pytest.mark.timeout(600)
+def test_config2_dropin_bench_batch_vs_oracle(config2):
+    """The batch bench.py's drop-in leg times (dropin.config2): the first 64 config-2 sources to depth 2 in one
+    hgx_bfs_sequence call through the default path (level engine, packed transfer of the large levels, the
+    pair copies finishing behind the call, the threaded readout), ~258M pairs.  Every one of the 64 sequences
+    equals the oracle's pair by pair (links, atoms, distances in next() order) -- so every seed whose level-2
+    pairs straddle one of the 8 rank-part boundaries is covered -- and the TEPS numerator equals the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    from hypergraphdb_amd import bfs_sequence
+    g, snap = config2
+    seeds = np.ascontiguousarray(g["seeds"][:64], np.int32)
+    res = bfs_sequence(snap, seeds, 2)
+    assert int(res.offsets[-1]) > 200_000_000
+    orc = oracle(g)
+
+    def one(i):   # og_bfs releases the GIL (ctypes): the oracle's traversals run on THREADS threads
+        l_, a, d, tr = orc.bfs(int(seeds[i]), 2, algen(-1, True, True, False, False))
+        gl, ga, gd = res.pairs(i)
+        return (len(a) == len(ga) and np.array_equal(ga, a) and np.array_equal(gl, l_) and np.array_equal(gd, d)), tr
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        out = list(ex.map(one, range(len(seeds))))
+    bad = [i for i, (ok, _) in enumerate(out) if not ok]
+    assert not bad, bad
+    assert res.traversed_edges == float(sum(tr for _, tr in out))

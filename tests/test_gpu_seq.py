@@ -344,6 +344,99 @@ def test_level_engine_packed_transfer(case):
     snap.close()
 
 
+def test_level_engine_results_outlive_later_calls():
+    """A result's pair copies may still run when hgx_bfs_sequence returns (hgx.h): its readers wait per rank part,
+    its free waits for every copy, and a later call on the same graph is ordered after them.  With every level
+    packed (HGX_OPT_SEQ_PACK_MIN 1) on the level engine (HGX_OPT_SEQ_ENGINE 2): result A is held while call B runs
+    on the same graph (its scratch and the pooled host buffers reused), result D is freed unread and call C
+    follows at once; A's stats are read before its pairs, A is read by ranges before it is read whole, and A, B
+    and C are the oracle's exact sequences (links, atoms, distances, traversed items)."""
+    import ctypes as C
+    from hypergraphdb_amd import _lib, synth
+    from hypergraphdb_amd._lib import check, lib, ptr
+    g = synth.hypergraph(3000, 20000, 2, 8, 2.1, 3, seed=75)
+    snap, orc = snapshot(g), oracle(g)
+    rng = np.random.default_rng(975)
+    sa = rng.integers(0, g["num_atoms"], 70).astype(np.int32)
+    sb = rng.integers(0, g["num_atoms"], 130).astype(np.int32)
+    sd = sb[::-1].copy()
+    sc = rng.integers(0, g["num_atoms"], 33).astype(np.int32)
+    mode = K.ALGEN_MODES[0]
+    opts = gen(snap, mode, -1).options()
+
+    def call(seeds, maxd):
+        h = C.c_void_p()
+        check(lib().hgx_bfs_sequence(snap.handle, ptr(seeds), len(seeds), maxd, C.byref(opts), C.byref(h)))
+        return h
+
+    def read_whole(h, n_seeds):
+        ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
+        check(lib().hgx_seq_result_info(h, C.byref(ns), C.byref(npairs), C.byref(nl)))
+        assert ns.value == n_seeds
+        off = np.zeros(n_seeds + 1, np.int64)
+        check(lib().hgx_seq_result_offsets(h, ptr(off)))
+        n = npairs.value
+        links, atoms, dists = (np.empty(max(n, 1), np.int32) for _ in range(3))
+        check(lib().hgx_seq_result_pairs(h, ptr(links), ptr(atoms), ptr(dists)))
+        return off, links[:n], atoms[:n], dists[:n]
+
+    def vs_oracle(seeds, maxd, off, links, atoms, dists):
+        trav = 0
+        for i, s in enumerate(seeds):
+            l_, at, d, tr = orc.bfs(int(s), maxd, algen(-1, *mode))
+            b, e = off[i], off[i + 1]
+            assert np.array_equal(atoms[b:e], at) and np.array_equal(links[b:e], l_), (i, s, maxd)
+            assert np.array_equal(dists[b:e], d), (i, s, maxd)
+            trav += tr
+        return trav
+
+    snap.set_option(_lib.HGX_OPT_SEQ_PACK_MIN, 1)
+    snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 2)
+    held = []
+    try:
+        ha = call(sa, 3)
+        held.append(ha)
+        hb = call(sb, 2)   # A unread: B reuses the graph's scratch behind A's copies
+        held.append(hb)
+        hd = call(sd, 3)
+        lib().hgx_seq_result_free(hd)   # freed unread: its buffers go back to the pool after its copies
+        hc = call(sc, -1)
+        held.append(hc)
+        # A: stats first (the lazy timing read), then ranged windows, then the whole readout
+        ms, tr = C.c_double(), C.c_double()
+        check(lib().hgx_seq_result_stats(ha, C.byref(ms), C.byref(tr)))
+        ml, bl, pl = C.c_double(), C.c_double(), C.c_int64()
+        check(lib().hgx_seq_result_level_stats(ha, C.byref(ml), C.byref(bl), C.byref(pl)))
+        ns, npairs, nl = C.c_int32(), C.c_int64(), C.c_int32()
+        check(lib().hgx_seq_result_info(ha, C.byref(ns), C.byref(npairs), C.byref(nl)))
+        n = npairs.value
+        assert n > 1000
+        vp = lambda x: C.c_void_p(ptr(x))
+        windows = {}
+        for first in sorted(set(rng.integers(0, n, 40).tolist() + [0, n - 1])):
+            wl, wa, wd = (np.empty(300, np.int32) for _ in range(3))
+            got = C.c_int64()
+            check(lib().hgx_seq_result_pairs_range(ha, C.c_int64(first), C.c_int64(300), vp(wl), vp(wa), vp(wd),
+                                                   C.byref(got)))
+            k = got.value
+            assert k == min(300, n - first)
+            windows[first] = (wl[:k].copy(), wa[:k].copy(), wd[:k].copy())
+        ra = read_whole(ha, len(sa))
+        for first, (wl, wa, wd) in windows.items():
+            k = len(wl)
+            assert np.array_equal(wl, ra[1][first:first + k]) and np.array_equal(wa, ra[2][first:first + k]), first
+            assert np.array_equal(wd, ra[3][first:first + k]), first
+        assert vs_oracle(sa, 3, *ra) == tr.value
+        vs_oracle(sb, 2, *read_whole(hb, len(sb)))
+        vs_oracle(sc, -1, *read_whole(hc, len(sc)))
+    finally:
+        for h in held:
+            lib().hgx_seq_result_free(h)
+        snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
+        snap.set_option(_lib.HGX_OPT_SEQ_PACK_MIN, 0)
+    snap.close()
+
+
 def test_level_engine_chunk_split_on_wide_keys():
     """A level whose stream keys do not fit 32 bits splits the chunk (HGX_OPT_SEQ_TLIMIT lowers the limit to
     force it down to single seeds; a single seed that still does not fit runs on the key-array engine):

@@ -3,7 +3,7 @@
 hg.subsumes drop-ins run) on config 5: batched 1024-closure calls and single-seed latency per
 direction, for the workgroup-per-seed engine (HGX_OPT_SEQ_ENGINE 0) and the level-synchronous one (1).
 
-  python tools/seq_c5.py [--scale 1.0] [--single 200] [--engines 0,1]
+  python tools/seq_c5.py [--scale 1.0] [--single 200] [--engines 0,1] [--direction subsumed|subsumes]
 """
 import argparse
 import json
@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--single", type=int, default=200)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--engines", default="0,1")
+    ap.add_argument("--direction", choices=("both", "subsumed", "subsumes"), default="both",
+                    help="one direction only (its own PMC passes: bench.py's per-direction drop-in rooflines)")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_sequence, synth
@@ -35,6 +37,8 @@ def main():
         snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, eng)
         e = {}
         for rev, name in ((False, "subsumed"), (True, "subsumes")):
+            if args.direction not in ("both", name):
+                continue
             gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
             bfs_sequence(snap, g["seeds"], None, gen_)   # warm-up (tables, buffers)
             walls, devs = [], []
@@ -55,9 +59,9 @@ def main():
                        "traversed_items": r.traversed_edges, "ms_block": round(r.ms_block, 3),
                        "seeds_block": r.n_block, "seeds_level": r.n_level, "seeds_grid": r.n_coop,
                        "ms_grid": round(r.ms_coop, 3), "ms_level": round(r.ms_level, 3),
-                       "single_ms_median": round(singles[len(singles) // 2] * 1e3, 4),
-                       "single_ms_p90": round(singles[int(len(singles) * 0.9)] * 1e3, 4),
-                       "single_ms_max": round(singles[-1] * 1e3, 4)}
+                       "single_ms_median": round(singles[len(singles) // 2] * 1e3, 4) if singles else None,
+                       "single_ms_p90": round(singles[int(len(singles) * 0.9)] * 1e3, 4) if singles else None,
+                       "single_ms_max": round(singles[-1] * 1e3, 4) if singles else None}
             print(f"engine {eng} {name}: {e[name]}", file=sys.stderr, flush=True)
         out["engines"][str(eng)] = e
     snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, 0)
