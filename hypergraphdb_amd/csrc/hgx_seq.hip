@@ -3536,32 +3536,37 @@ __global__ void __launch_bounds__(256) k_pull_rec(int64_t M, const int64_t* __re
 
 
 // ---------------------------------------------------------------------------------------------
-// Order-exact multi-workgroup stage (hgx_seq_coop; round 5): the <= 64 seeds the
-// order-exact workgroup engine (hgx_seq_block) hands back -- config 5's six big hg.subsumed closures,
-// 2K-101K pairs over 21 levels -- in ONE persistent launch of resident workgroups instead of the level
-// engine's launches per level.  Items are yield-adjacency pairs (the generator's (target, link) output in
-// stream order, so an item's index IS its stream position and the key needs no yield rank).  A level is
-// three phases separated by the light grid barrier (co_barrier_lite; every cross-workgroup access is an
-// agent-scope atomic or co_put / co_get, [xwg] below):
+// Order-exact multi-workgroup stage (hgx_seq_coop; round 5; two phases a level since
+// round 6): the <= 64 seeds the order-exact workgroup engine (hgx_seq_block) hands back -- config 5's six
+// big hg.subsumed closures, 2K-101K pairs over 21 levels -- in ONE persistent launch of resident workgroups
+// instead of the level engine's launches per level.  Items are yield-adjacency pairs (the generator's
+// (target, link) output in stream order, so an item's index IS its stream position and the key needs no
+// yield rank).  A level is two phases separated by the light grid barrier (co_barrier_lite; every
+// cross-workgroup access is an agent-scope atomic or co_put / co_get, [xwg] below):
 //   P1 expand   work items (a frontier entry's pairs, <= kScChunk each, carrying the entry's first item
 //               index) -> every pair (t, link) of seed s with t not examined: the level hash keyed by
-//               (s, t) keeps the minimum of ((it + 1) << 32 | link); the first claimer appends (t, s, slot)
-//               to its block's discovery segment (HGBreadthFirstTraversal.java:56-64)
-//   P2 finalise every discovery x: its value from the hash slot (which it clears), a bit at its key
-//               (= the item index) in the level's key-space bitmap, its adjacency degree added to its
-//               key's word and stored at its key, key -> x, and the examined bit
-//   P3 emit     every workgroup scans the bitmap words' popcounts and degree sums in LDS; a wave per
-//               non-empty word, a lane per key: rank = popcount below the key (the level's FIFO order),
-//               first item index of the new frontier entry = degree prefix below it (a wave scan);
-//               pair `rank` of the level, the next level's work items, per-seed pair counts
+//               (s, t) keeps the minimum value ((it + 1) << 32 | link) (HGBreadthFirstTraversal.java:56-64).
+//               The item whose atomicMin LOWERS the value is the slot's minimum so far: it counts its own
+//               key (= its item index) +1 and the displaced key -1 -- per key, per 64-key word, and the
+//               word's degree sum (both keys have the same target, so the same degree) -- and records its
+//               key: (t, s, link, slot) and t's degree.  Adds commute, so whatever the order of the updates
+//               every key ends at 1 exactly when it is its slot's minimum, i.e. a discovery.
+//   P2 emit     every workgroup reads the words' counts and degree sums (coalesced) into LDS prefixes; a
+//               wave per non-empty word, a lane per key: rank = the count below the key (the level's FIFO
+//               order), first item index of the new frontier entry = the degree prefix below it (a wave
+//               scan); pair `rank` of the level, the examined bit, the hash slot and the key count back to
+//               empty, the next level's work items, per-seed pair counts.
+// Round 5 had a third phase between them (the discoveries appended by their first claimers, finalised after
+// the hash settled: key bit, degree, key -> discovery): one grid barrier and one phase of dependent round
+// trips more per level.
 // The key space of a level is its item count T (<= kScKeyCap, else the seeds go to the level engine).
 constexpr int kScChunk = 64;                       // adjacency pairs per work item
 constexpr int64_t kScKeyCap = (int64_t)1 << 18;    // keys (items) of one level: an LDS prefix of 4096 words
 constexpr int kScWords = (int)(kScKeyCap / 64);
 constexpr int kScProbes = 64;
 // ctl words: [0] barrier, [kScSt .. +1] status by phase parity, [kScSt + 2] sticky status, [kScItm + p*kCoSegs +
-// seg] work-item counters (parity p), [kScDis + p*kCoSegs + seg] discovery counters, then lcnt [kCoMaxLevels x 64]
-constexpr int kScSt = 4, kScItm = 8, kScDis = kScItm + 2 * kCoSegs, kScLcnt = kScDis + 2 * kCoSegs;
+// seg] work-item counters (parity p), then lcnt [kCoMaxLevels x 64]
+constexpr int kScSt = 4, kScItm = 8, kScLcnt = kScItm + 2 * kCoSegs;
 constexpr int64_t kScCtlWords = kScLcnt + (int64_t)kCoMaxLevels * 64;
 
 struct ScArgs {
@@ -3579,14 +3584,11 @@ struct ScArgs {
     u64* hval;
     int64_t hmask;
     int32_t hbits;
-    int4* dseg;                                      // discoveries: kCoSegs segments of dcap entries (t, s, slot lo, hi)
-    int64_t dcap;
-    int2* dflat;                                     // [kScKeyCap] discovery x: (t, s)
-    u64* dval;                                       // [kScKeyCap] its value
-    u64* kbm;                                        // [kScWords] key-space bitmap of the level
-    u64* wdeg;                                       // [kScWords] degree sums per bitmap word
-    uint32_t* kdeg;                                  // [kScKeyCap] degree of the key's discovery
-    uint32_t* kdis;                                  // [kScKeyCap] key -> discovery index
+    uint32_t* kcnt;                                  // [kScKeyCap] per key: 1 <=> the key is its slot's minimum (0 between levels)
+    int4* krec;                                      // [kScKeyCap] the key's (t, s, link, slot), written by its item
+    uint32_t* kdeg;                                  // [kScKeyCap] the degree of the key's target
+    u64* wcnt;                                       // [2 parities][kScWords] keys counted per 64-key word
+    u64* wdeg;                                       // [2 parities][kScWords] their degree sums
     int4* items;                                     // [2 parities][kCoSegs][iseg] (t, s | cnt << 8, ybase, it0)
     int64_t iseg;
     int32_t* out_link;                               // [pcap] pairs, level-major, rank order
@@ -3597,6 +3599,10 @@ struct ScArgs {
     int64_t* hmeta;                                  // mapped: [0] status (-1 until block 0's normal exit), [1] levels,
                                                      //   [2] pairs, [3] timed out, [4] traversed items
     int64_t* blk_bytes;                              // mapped [gridDim.x]
+    int64_t* blk_trav;                               // mapped [gridDim.x] traversed items per block
+    int32_t* h_link;                                 // mapped [pcap] the result read out by the kernel's end: links,
+    int32_t* h_atom;                                 //   atoms (level-major, rank order)
+    int64_t* h_lcnt;                                 //   and [levels x 64] pairs per level and seed
     u64 timeout;
 };
 
@@ -3672,7 +3678,6 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + wave, nw = (int64_t)gridDim.x * kWaves;
     const int seg = blockIdx.x % kCoSegs;
-    __shared__ u64 s_kbm[kScWords];
     __shared__ uint32_t s_cpre[kScWords + 1], s_dpre[kScWords + 1];
     __shared__ int64_t s_pre[kCoSegs + 1];
     __shared__ int64_t s_T;
@@ -3711,8 +3716,11 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
     int64_t out0 = 0;
     int64_t Tprev = 0;
     u64 ph = 1;   // phases completed (the seeding was phase 0... its errors: word 1)
+    bool done = false;   // the traversal ended (no error): every block leaves with the same value
     for (; !timed_out; ++d) {
         const int par = d & 1;
+        u64* wcnt = a.wcnt + (int64_t)par * kScWords;
+        u64* wdeg = a.wdeg + (int64_t)par * kScWords;
         // ---- P1: expand ----
         if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1)) | sc_ld(st_sticky);   // [xwg] the last phase's errors
         const int64_t nf = sc_seg_prefix(a.ctl + kScItm + par * kCoSegs, a.iseg, s_pre);
@@ -3722,20 +3730,25 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(st_sticky, st);
             break;
         }
-        if (nf == 0 || d >= a.maxd) break;   // the same decision in every block
+        if (nf == 0 || d >= a.maxd) {   // the same decision in every block
+            done = true;
+            break;
+        }
         if (T > kScKeyCap || d >= kCoMaxLevels) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(st_sticky, 8ull);
             break;
         }
         u64* stw = a.ctl + kScSt + ((ph + 1) & 1);   // this phase's error word
-        if (blockIdx.x == 0) {   // the previous level's discovery counters (read in its P2 / P3) -> 0
-            if (threadIdx.x < kCoSegs) sc_st(a.ctl + kScDis + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
-        }
-        // the previous level's bitmap words and degree sums -> 0 (read in its P3, written again in this P2)
+        // the next level's item counters -> 0 (last read in the previous level's P1; appended to in this
+        // level's P2) and the previous level's word counts and degree sums -> 0 (read in its P2, written again
+        // in the next level's P1)
+        if (blockIdx.x == 0 && threadIdx.x < kCoSegs)
+            sc_st(a.ctl + kScItm + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
         for (int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x; w < (Tprev + 63) / 64; w += (int64_t)gridDim.x * NT) {
-            sc_st(a.kbm + w, 0ull);   // [xwg]
-            sc_st(a.wdeg + w, 0ull);  // [xwg]
+            sc_st(a.wcnt + (int64_t)(par ^ 1) * kScWords + w, 0ull);   // [xwg]
+            sc_st(a.wdeg + (int64_t)(par ^ 1) * kScWords + w, 0ull);   // [xwg]
         }
+        const bool expand_next = d + 1 < a.maxd;
         {
             const int4* L = a.items + (int64_t)par * kCoSegs * a.iseg;
             const int64_t per = min<int64_t>(64, (nf + nw - 1) / nw);
@@ -3759,7 +3772,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                     if (lane >= off) x += y;
                 }
                 const int64_t TT = __shfl(x, 63), ex = x - cnt;
-                for (int64_t f0 = 0; f0 < TT; f0 += 64) {   // wave-uniform: every lane reaches the append
+                for (int64_t f0 = 0; f0 < TT; f0 += 64) {   // wave-uniform
                     const int64_t f = f0 + lane;
                     int o = 0;
 #pragma unroll
@@ -3770,55 +3783,50 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                     const int32_t s = __shfl(is, o);
                     const int64_t off_ = f - __shfl(ex, o);
                     const int64_t ii = __shfl(yb, o) + off_, it = __shfl(itb, o) + off_;
-                    bool isnew = false;
-                    int32_t t = 0;
-                    u64 slot = 0;
-                    if (f < TT) {
-                        t = a.a_tgt[ii];
-                        const int32_t la = a.a_lnk[ii];
-                        nbytes += 16;
-                        const u64 vw = sc_ld(a.vis + (int64_t)s * a.vwords + (t >> 6));   // [xwg]
-                        if (!((vw >> (t & 63)) & 1ull)) {
-                            const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)t;
-                            const u64 v = ((u64)(it + 1) << 32) | (u64)(uint32_t)la;
-                            u64 h = ls_hash(key, a.hbits);
-                            int probe = 0;
-                            for (; probe < kScProbes; ++probe) {
-                                u64 kk = sc_ld(a.hkey + h);   // [xwg]
-                                if (kk == kLsEmpty) {
-                                    kk = atomicCAS((unsigned long long*)(a.hkey + h), kLsEmpty, (unsigned long long)key);   // [xwg]
-                                    if (kk == kLsEmpty) {
-                                        atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
-                                        isnew = true;
-                                        slot = h;
-                                        break;
-                                    }
-                                }
-                                if (kk == key) {
-                                    if (sc_ld(a.hval + h) > v) atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
-                                    break;
-                                }
-                                h = (h + 1) & (u64)a.hmask;
-                            }
-                            if (probe == kScProbes) atomicOr(stw, 4ull);   // [xwg] the hash is too full
-                            nbytes += 24;
+                    if (f >= TT) continue;
+                    const int32_t t = a.a_tgt[ii];
+                    const int32_t la = a.a_lnk[ii];
+                    nbytes += 8;
+                    const u64 vw = sc_ld(a.vis + (int64_t)s * a.vwords + (t >> 6));   // [xwg]
+                    nbytes += 8;
+                    if ((vw >> (t & 63)) & 1ull) continue;   // examined already
+                    const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)t;
+                    const u64 v = ((u64)(it + 1) << 32) | (u64)(uint32_t)la;
+                    u64 h = ls_hash(key, a.hbits);
+                    u64 old = 0ull;   // the slot's value before this item's atomicMin (0: no update made)
+                    int probe = 0;
+                    for (; probe < kScProbes; ++probe) {
+                        u64 kk = sc_ld(a.hkey + h);   // [xwg]
+                        if (kk == kLsEmpty)
+                            kk = atomicCAS((unsigned long long*)(a.hkey + h), kLsEmpty, (unsigned long long)key);   // [xwg]
+                        if (kk == kLsEmpty || kk == key) {   // claimed now, or the key's slot
+                            if (kk == kLsEmpty || sc_ld(a.hval + h) > v)   // [xwg]
+                                old = atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
+                            break;
                         }
+                        h = (h + 1) & (u64)a.hmask;
                     }
-                    const u64 m = __ballot(isnew);
-                    if (m) {
-                        const int leader = __ffsll((long long)m) - 1;
-                        u64 b = 0;
-                        if (lane == leader) b = atomicAdd(a.ctl + kScDis + par * kCoSegs + seg, (u64)__popcll(m));   // [xwg]
-                        b = __shfl(b, leader);
-                        if (isnew) {
-                            const u64 pos = b + __popcll(m & ((1ull << lane) - 1ull));
-                            if ((int64_t)pos < a.dcap)
-                                co_put(a.dseg + (int64_t)seg * a.dcap + (int64_t)pos,
-                                       make_int4(t, s, (int32_t)(uint32_t)slot, (int32_t)(slot >> 32)));   // [xwg]
-                            else
-                                atomicOr(stw, 16ull);   // [xwg]
-                            nbytes += 16;
-                        }
+                    nbytes += 24;
+                    if (probe == kScProbes) {
+                        atomicOr(stw, 4ull);   // [xwg] the hash is too full
+                        continue;
+                    }
+                    if (old <= v) continue;   // (old == 0: no update; else a lower value was there first)
+                    // this item is the slot's minimum so far: count its key, uncount the displaced one
+                    const uint32_t mykey = (uint32_t)it;
+                    const uint32_t dg = expand_next ? (uint32_t)(a.y_off[t + 1] - a.y_off[t]) : 0u;
+                    co_put(a.krec + mykey, make_int4(t, s, la, (int32_t)(uint32_t)h));   // [xwg]
+                    sc_st32(a.kdeg + mykey, dg);                                          // [xwg]
+                    atomicAdd(a.kcnt + mykey, 1u);                                        // [xwg]
+                    atomicAdd((unsigned long long*)(wcnt + (mykey >> 6)), 1ull);          // [xwg]
+                    if (dg) atomicAdd((unsigned long long*)(wdeg + (mykey >> 6)), (unsigned long long)dg);   // [xwg]
+                    nbytes += 16 + 4 + 4 + 8 + (dg ? 8 : 0);
+                    if (old != ~0ull) {   // the displaced minimum (same target: same degree)
+                        const uint32_t okey = (uint32_t)((old >> 32) - 1ull);
+                        atomicSub(a.kcnt + okey, 1u);                                     // [xwg]
+                        atomicAdd((unsigned long long*)(wcnt + (okey >> 6)), ~0ull);      // [xwg] -1
+                        if (dg) atomicAdd((unsigned long long*)(wdeg + (okey >> 6)), (unsigned long long)(0ull - (u64)dg));   // [xwg]
+                        nbytes += 4 + 8 + (dg ? 8 : 0);
                     }
                 }
             }
@@ -3826,65 +3834,30 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         timed_out = co_barrier_lite(a.ctl, gen, stw, a.timeout);
         ++ph;
         if (timed_out) break;
-        // ---- P2: finalise the discoveries ----
-        if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1));   // [xwg]
-        const int64_t n = sc_seg_prefix(a.ctl + kScDis + par * kCoSegs, a.dcap, s_pre);
-        if (s_st) break;   // (block-uniform: read before the prefix's barrier)
-        stw = a.ctl + kScSt + ((ph + 1) & 1);
-        if (blockIdx.x == 0 && threadIdx.x < kCoSegs)   // the next level's item counters (read two levels ago)
-            sc_st(a.ctl + kScItm + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
-        const bool expand_next = d + 1 < a.maxd;
-        for (int64_t x = (int64_t)blockIdx.x * NT + threadIdx.x; x < n; x += (int64_t)gridDim.x * NT) {
-            const int sg = sc_seg_of(s_pre, x);
-            const int4 e = co_get(a.dseg + (int64_t)sg * a.dcap + (x - s_pre[sg]));   // [xwg]
-            const u64 slot = (u64)(uint32_t)e.z | (u64)(uint32_t)e.w << 32;
-            const u64 v = sc_ld(a.hval + slot);   // [xwg]
-            sc_st(a.hkey + slot, kLsEmpty);       // [xwg]
-            sc_st(a.hval + slot, ~0ull);          // [xwg]
-            const uint32_t key = (uint32_t)((v >> 32) - 1ull);
-            const uint32_t dg = expand_next ? (uint32_t)(a.y_off[e.x + 1] - a.y_off[e.x]) : 0u;
-            atomicOr(a.kbm + (key >> 6), 1ull << (key & 63));                             // [xwg]
-            if (dg) atomicAdd(a.wdeg + (key >> 6), (u64)dg);                                 // [xwg]
-            sc_st32(a.kdeg + key, dg);                                                       // [xwg]
-            sc_st32(a.kdis + key, (uint32_t)x);                                              // [xwg]
-            co_put(a.dflat + x, make_int2(e.x, e.y));                                        // [xwg]
-            sc_st(a.dval + x, v);                                                            // [xwg]
-            atomicOr(a.vis + (int64_t)e.y * a.vwords + (e.x >> 6), 1ull << (e.x & 63));     // [xwg] examined from now on
-            nbytes += 16 + 8 + 16 + 8 + 8 + 4 + 4 + 8 + 8 + 8;
-        }
-        timed_out = co_barrier_lite(a.ctl, gen, stw, a.timeout);
-        ++ph;
-        if (timed_out) break;
-        // ---- P3: rank, emit, next items ----
+        // ---- P2: rank, emit, next items ----
         if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1));   // [xwg]
         const int64_t Wn = (T + 63) / 64;
-        {   // the words' popcounts and degree sums -> exclusive prefixes in LDS (every block)
+        {   // the words' counts and degree sums -> exclusive prefixes in LDS (every block; coalesced loads, each
+            // thread's run of `per` words then scanned in registers)
             constexpr int per = kScWords / NT;
-            // coalesced loads first (lane-consecutive words: a wave's load is 4 cache lines, where a thread's
-            // own run of `per` words made every lane of a load a line of its own -- 16x the memory requests
-            // of the level's bitmap, read by every block), staged in LDS: the bitmap words in s_kbm, the
-            // degree sums in s_dpre (u32 like the prefixes they become; a level's items stay < 2^32)
             for (int64_t w = threadIdx.x; w < (int64_t)kScWords; w += NT) {
-                u64 bw = 0, dd = 0;
+                u64 cc = 0, dd = 0;
                 if (w < Wn) {
-                    bw = sc_ld(a.kbm + w);    // [xwg]
-                    dd = sc_ld(a.wdeg + w);   // [xwg]
+                    cc = sc_ld(wcnt + w);   // [xwg]
+                    dd = sc_ld(wdeg + w);   // [xwg]
                 }
-                s_kbm[w] = bw;
-                s_dpre[w] = (uint32_t)dd;
+                s_cpre[w] = (uint32_t)cc;
+                s_dpre[w] = (uint32_t)dd;   // (a level's items stay < 2^32)
             }
             __syncthreads();
             int64_t c = 0, g2 = 0;
-            uint32_t cw[per];
-            u64 dw[per];
+            uint32_t cw[per], dw[per];
 #pragma unroll
             for (int q = 0; q < per; ++q) {   // this thread's run of words (it alone rewrites them below)
-                const u64 bw = s_kbm[threadIdx.x * per + q];
-                const u64 dd = s_dpre[threadIdx.x * per + q];
-                cw[q] = (uint32_t)__popcll(bw);
-                dw[q] = dd;
+                cw[q] = s_cpre[threadIdx.x * per + q];
+                dw[q] = s_dpre[threadIdx.x * per + q];
                 c += cw[q];
-                g2 += (int64_t)dd;
+                g2 += dw[q];
             }
             // block exclusive scans of (c, g2): wave shuffles, then the wave sums through LDS
             int64_t xc = c, xg = g2;
@@ -3916,7 +3889,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                 s_cpre[threadIdx.x * per + q] = (uint32_t)rc;
                 s_dpre[threadIdx.x * per + q] = (uint32_t)rg;
                 rc += cw[q];
-                rg += (int64_t)dw[q];
+                rg += dw[q];
             }
             if (threadIdx.x == 0) {
                 s_cpre[kScWords] = (uint32_t)tc;
@@ -3926,20 +3899,21 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         }
         if (s_st) break;
         stw = a.ctl + kScSt + ((ph + 1) & 1);
-        const int64_t nd = s_cpre[kScWords];   // == n
+        const int64_t nd = s_cpre[kScWords];   // the level's discoveries
         const int64_t Tn = s_T;                // the next level's items
         if (out0 + nd > a.pcap) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(stw, 2ull);   // [xwg]
         } else {
             for (int64_t w = gw; w < Wn; w += nw) {   // a wave per non-empty word, a lane per key
-                const u64 m = s_kbm[w];
-                if (!m) continue;   // wave-uniform
-                const bool set = (m >> lane) & 1ull;
+                if (s_cpre[w + 1] == s_cpre[w]) continue;   // wave-uniform
                 const uint32_t key = (uint32_t)(w * 64 + lane);
-                uint32_t x = 0, dg = 0;
+                const bool set = sc_ld32(a.kcnt + key) != 0u;   // [xwg] (1: the key is its slot's minimum)
+                const u64 m = __ballot(set);
+                uint32_t dg = 0;
+                int4 rec = make_int4(0, 0, 0, 0);
                 if (set) {
-                    x = sc_ld32(a.kdis + key);   // [xwg]
-                    dg = sc_ld32(a.kdeg + key);  // [xwg]
+                    rec = co_get(a.krec + key);      // [xwg] (t, s, link, slot)
+                    dg = sc_ld32(a.kdeg + key);      // [xwg]
                 }
                 int64_t ex = dg;
 #pragma unroll
@@ -3948,19 +3922,20 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                     if (lane >= off) ex += y;
                 }
                 ex -= dg;
-                int32_t t = 0, s = 0;
+                const int32_t t = rec.x, s = rec.y;
                 if (set) {
-                    const int2 ts = co_get(a.dflat + x);   // [xwg]
-                    t = ts.x;
-                    s = ts.y;
-                    const u64 v = sc_ld(a.dval + x);      // [xwg]
                     const int64_t r = out0 + s_cpre[w] + __popcll(m & ((1ull << lane) - 1ull));
-                    a.out_link[r] = (int32_t)(uint32_t)v;
-                    a.out_atom[r] = t;
-                    a.out_seed[r] = s;
+                    sc_st32((uint32_t*)a.out_link + r, (uint32_t)rec.z);   // [xwg] read out by another block at the end
+                    sc_st32((uint32_t*)a.out_atom + r, (uint32_t)t);       // [xwg]
+                    sc_st32((uint32_t*)a.out_seed + r, (uint32_t)s);       // [xwg]
                     atomicAdd(&s_cnt[s], 1ull);
+                    const u64 slot = (u64)(uint32_t)rec.w;
+                    sc_st32(a.kcnt + key, 0u);          // [xwg] the key, its hash slot: empty for the next level
+                    sc_st(a.hkey + slot, kLsEmpty);     // [xwg]
+                    sc_st(a.hval + slot, ~0ull);        // [xwg]
+                    atomicOr(a.vis + (int64_t)s * a.vwords + (t >> 6), 1ull << (t & 63));   // [xwg] examined from now on
                     if (d + 1 < a.maxd) trav += a.inc_off[t + 1] - a.inc_off[t];   // expanded at level d + 1
-                    nbytes += 8 + 8 + 8 + 8 + 12;
+                    nbytes += 4 + 16 + 4 + 12 + 4 + 16 + 8;
                 }
                 sc_put_items(a, par ^ 1, seg, t, s, (int64_t)dg, set ? a.y_off[t] : 0, (int64_t)s_dpre[w] + ex, stw);
             }
@@ -4001,23 +3976,35 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         if (threadIdx.x == 0) {
             int64_t tt = 0;
             for (int q = 0; q < kWaves; ++q) tt += s_ws[q];
-            if (tt) atomicAdd((unsigned long long*)(a.ctl + 1), (unsigned long long)tt);   // [xwg] read by block 0 below? no: by the host
+            a.blk_trav[blockIdx.x] = tt;
         }
     }
+    // the readout and the examined bits' reset, by the kernel itself (round 6: the host's copies and clear launch
+    // behind a finished stage cost ~0.24 ms of round trips): every pair, level count and examined word is final
+    // once the blocks left the loop after the same barrier; each block moves a slice of the pairs into the
+    // caller-visible mapped buffer and clears their examined bits (only after a clean end: otherwise the host
+    // clears the bitmaps whole and reruns the seeds elsewhere)
+    if (done) {
+        const int64_t n = min(out0, a.pcap);
+        const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+        for (int64_t i = lo + threadIdx.x; i < hi; i += NT) {
+            const int32_t t = (int32_t)sc_ld32((const uint32_t*)a.out_atom + i);   // [xwg]
+            a.h_link[i] = (int32_t)sc_ld32((const uint32_t*)a.out_link + i);      // [xwg]
+            a.h_atom[i] = t;
+            a.vis[(int64_t)(int32_t)sc_ld32((const uint32_t*)a.out_seed + i) * a.vwords + (t >> 6)] = 0ull;   // [xwg]
+        }
+        if (blockIdx.x == 0) {
+            for (int s = threadIdx.x; s < a.k; s += NT) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
+            for (int64_t x = threadIdx.x; x < (int64_t)d * 64; x += NT) a.h_lcnt[x] = (int64_t)sc_ld(a.ctl + kScLcnt + x);
+        }
+    }
+    __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.hmeta[1] = d;
         a.hmeta[2] = out0;
-        a.hmeta[0] = (int64_t)(sc_ld(st_sticky) | sc_ld(a.ctl + kScSt) | sc_ld(a.ctl + kScSt + 1));
-    }
-}
-
-// The examined bits of a finished stage's pairs and seeds -> 0 (the bitmaps' zero-between-calls rule).
-__global__ void __launch_bounds__(256) k_sc_clear(int64_t n, const int32_t* __restrict__ atom, const int32_t* __restrict__ seed,
-                                                  int32_t k, const int32_t* __restrict__ seeds, int64_t vwords, u64* vis) {
-    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n + k; i += (int64_t)gridDim.x * 256) {
-        const int32_t t = i < n ? atom[i] : seeds[i - n];
-        const int32_t s = i < n ? seed[i] : (int32_t)(i - n);
-        vis[(int64_t)s * vwords + (t >> 6)] = 0ull;
+        u64 sa = sc_ld(st_sticky) | sc_ld(a.ctl + kScSt) | sc_ld(a.ctl + kScSt + 1);
+        if (!done && !sa) sa = 64ull;   // (left the loop without a recorded cause: never clean)
+        a.hmeta[0] = (int64_t)sa;
     }
 }
 
@@ -5161,14 +5148,11 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.hmask = ((int64_t)1 << a.hbits) - 1;
         a.hkey = (u64*)w.take(sizeof(u64) << a.hbits);
         a.hval = (u64*)w.take(sizeof(u64) << a.hbits);
-        a.dcap = kScKeyCap / kCoSegs * 4;
-        a.dseg = (int4*)w.take(sizeof(int4) * kCoSegs * (size_t)a.dcap);
-        a.dflat = (int2*)w.take(sizeof(int2) * (size_t)kScKeyCap);
-        a.dval = (u64*)w.take(sizeof(u64) * (size_t)kScKeyCap);
-        a.kbm = (u64*)w.take(sizeof(u64) * 2 * kScWords);
-        a.wdeg = a.kbm + kScWords;
-        a.kdeg = (uint32_t*)w.take(sizeof(uint32_t) * 2 * (size_t)kScKeyCap);
-        a.kdis = a.kdeg + kScKeyCap;
+        a.krec = (int4*)w.take(sizeof(int4) * (size_t)kScKeyCap);
+        a.kcnt = (uint32_t*)w.take(sizeof(uint32_t) * 2 * (size_t)kScKeyCap);
+        a.kdeg = a.kcnt + kScKeyCap;
+        a.wcnt = (u64*)w.take(sizeof(u64) * 4 * kScWords);   // [2 parities] counts, then [2 parities] degree sums
+        a.wdeg = a.wcnt + 2 * kScWords;
         a.iseg = (int64_t)1 << 14;
         a.items = (int4*)w.take(sizeof(int4) * 2 * kCoSegs * (size_t)a.iseg);
         a.pcap = std::max<int64_t>(g->sc_pcap, (int64_t)1 << 20);
@@ -5183,10 +5167,11 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.seeds = dseeds;
         HGX_HIP(hipMemsetAsync(a.hkey, 0xFF, sizeof(u64) << a.hbits, st));
         HGX_HIP(hipMemsetAsync(a.hval, 0xFF, sizeof(u64) << a.hbits, st));
-        HGX_HIP(hipMemsetAsync(a.kbm, 0, sizeof(u64) * 2 * kScWords, st));
+        HGX_HIP(hipMemsetAsync(a.kcnt, 0, sizeof(uint32_t) * (size_t)kScKeyCap, st));
+        HGX_HIP(hipMemsetAsync(a.wcnt, 0, sizeof(u64) * 4 * kScWords, st));
         HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScCtlWords, st));
         const int nblk = g->sc_ok;
-        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + (size_t)nblk));
+        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk));
         int64_t* hm = (int64_t*)hb.p;
         hm[0] = -1;
         hm[1] = hm[2] = hm[3] = 0;
@@ -5194,6 +5179,29 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
         a.hmeta = (int64_t*)hmd;
         a.blk_bytes = (int64_t*)hmd + 8;
+        a.blk_trav = a.blk_bytes + nblk;
+        // the result, written by the kernel's end into mapped memory: links [pcap] | atoms [pcap] | level counts
+        PoolBuf pb = take_host_buf(g, 8 * (size_t)a.pcap + 8 * (size_t)kCoMaxLevels * 64);
+        struct PairsBack {   // back to the pool unless the result keeps it
+            hgx_graph* g;
+            PoolBuf b;
+            bool keep = false;
+            ~PairsBack() {
+                if (keep) return;
+                std::lock_guard<std::mutex> lk(g->seq_mu);
+                g->seq_hbufs.push_back(b);
+            }
+        } pback{g, pb};
+        int32_t* hl = (int32_t*)pb.p;
+        int32_t* ha = hl + a.pcap;
+        int64_t* hc = (int64_t*)(ha + a.pcap);
+        {
+            void* pd = nullptr;
+            HGX_HIP(hipHostGetDevicePointer(&pd, pb.p, 0));
+            a.h_link = (int32_t*)pd;
+            a.h_atom = a.h_link + a.pcap;
+            a.h_lcnt = (int64_t*)(a.h_atom + a.pcap);
+        }
         a.timeout = g->co_timeout > 0 ? (u64)g->co_timeout : kCoTimeout;   // HGX_OPT_CO_TIMEOUT (tests)
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (g->timing) {
@@ -5236,23 +5244,9 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         }
         const int32_t nlev = (int32_t)hm[1];
         const int64_t total = hm[2];
-        // pairs (+ their seeds, for clearing), the per-level per-seed counts and the traversed items
-        PoolBuf pb = take_host_buf(g, 8 * (size_t)total + 8 + 8 * ((size_t)nlev * 64 + 2));
+        if (total > a.pcap || nlev > kCoMaxLevels) fail(HGX_E_DEVICE, "hgx_bfs_sequence: grid stage sizes inconsistent");
+        pback.keep = true;
         out.bufs.push_back(pb);
-        int32_t* hl = (int32_t*)pb.p;
-        int32_t* ha = hl + total;
-        int64_t* hc = (int64_t*)(ha + total + (total & 1));
-        if (total) {
-            HGX_HIP(hipMemcpyAsync(hl, a.out_link, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
-            HGX_HIP(hipMemcpyAsync(ha, a.out_atom, sizeof(int32_t) * (size_t)total, hipMemcpyDeviceToHost, st));
-        }
-        if (nlev) HGX_HIP(hipMemcpyAsync(hc, a.ctl + kScLcnt, sizeof(int64_t) * 64 * (size_t)nlev, hipMemcpyDeviceToHost, st));
-        HGX_HIP(hipMemcpyAsync(hc + 64 * (size_t)nlev, a.ctl + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        k_sc_clear<<<grid_for(total + k, 256, 4096), 256, 0, st>>>(total, a.out_atom, a.out_seed, k, dseeds, vwords,
-                                                                   g->co_vis);
-        HGX_CHECK_LAUNCH();
-        spin_sync(st);
-        seq_mark("grid stage pairs copied");
         // level-major, seed-major inside a level: seed j's pairs of level d follow the earlier seeds' ones
         int64_t o0 = 0;
         for (int32_t d = 0; d < nlev; ++d) {
@@ -5266,8 +5260,10 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             o0 = o;
         }
         if (o0 != total) fail(HGX_E_DEVICE, "hgx_bfs_sequence: grid stage pair counts inconsistent");
-        out.traversed += (double)hc[64 * (size_t)nlev];
-        for (int b = 0; b < nblk; ++b) out.bytes += (double)hm[8 + b];
+        for (int b = 0; b < nblk; ++b) {
+            out.bytes += (double)hm[8 + b];
+            out.traversed += (double)hm[8 + nblk + b];
+        }
         return true;
     }
     return false;
