@@ -44,6 +44,7 @@ void graph_release(hgx_graph* g) {
     if (g->zacc) (void)hipFree(g->zacc);
     if (g->q_ticket) (void)hipFree(g->q_ticket);
     if (g->co_vis) (void)hipFree(g->co_vis);
+    if (g->sc_tab) (void)hipFree(g->sc_tab);
     free_yield_lists(g);
     for (auto& b : g->seq_hbufs) (void)hipHostFree(b.p);
     g->seq_hbufs.clear();

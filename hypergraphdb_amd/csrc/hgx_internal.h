@@ -281,6 +281,7 @@ struct hgx_graph {
     int64_t seq_pack_min = 0;                       // level engine: pairs of a level that cross PCIe packed (0 = 2^20)
     int32_t xb_flat = -1, xb_static = -1;           // partition broadcast pack variants (-1 = default)
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
+    unsigned long long* sc_tab = nullptr;           // order-exact grid stage: level hash, word / key counts (empty between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
     int64_t co_timeouts = 0;                        //   launches whose grid barrier timed out (seeds fell back)

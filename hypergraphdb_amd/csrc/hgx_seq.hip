@@ -3571,7 +3571,7 @@ constexpr int64_t kScCtlWords = kScLcnt + (int64_t)kCoMaxLevels * 64;
 
 struct ScArgs {
     int32_t k;                                       // seeds (<= kMaxCoSeeds)
-    const int32_t* seeds;                            // device [k]
+    int32_t seeds[kMaxCoSeeds];                      // inline in the kernel arguments (no upload)
     int64_t A;
     const int64_t* inc_off;                          // traversed items: incidence entries of expanded atoms
     const int64_t* y_off;                            // the yield adjacency
@@ -3993,6 +3993,10 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
             a.h_atom[i] = t;
             a.vis[(int64_t)(int32_t)sc_ld32((const uint32_t*)a.out_seed + i) * a.vwords + (t >> 6)] = 0ull;   // [xwg]
         }
+        // the word counts and degree sums back to 0 for the next call (the hash slots and key counts are
+        // empty again already: every claimed slot's minimum was emitted and cleared it)
+        for (int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x; w < 4 * (int64_t)kScWords; w += (int64_t)gridDim.x * NT)
+            a.wcnt[w] = 0ull;   // (wcnt and wdeg are one allocation)
         if (blockIdx.x == 0) {
             for (int s = threadIdx.x; s < a.k; s += NT) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
             for (int64_t x = threadIdx.x; x < (int64_t)d * 64; x += NT) a.h_lcnt[x] = (int64_t)sc_ld(a.ctl + kScLcnt + x);
@@ -5098,6 +5102,16 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
 
 // ---- the order-exact multi-workgroup stage, host side ----
 
+// The grid stage's persistent tables (hgx_graph::sc_tab): hash keys and values (all-ones = empty), the word
+// counts / degree sums and the key counts (zero).
+constexpr int kScHashBits = 19;
+constexpr size_t kScTabBytes = sizeof(u64) * (2 * ((size_t)1 << kScHashBits) + 4 * kScWords) + sizeof(uint32_t) * (size_t)kScKeyCap;
+void sc_tab_reset(hgx_graph* g) {
+    const size_t hb = sizeof(u64) * 2 * ((size_t)1 << kScHashBits);
+    HGX_HIP(hipMemsetAsync(g->sc_tab, 0xFF, hb, g->stream));
+    HGX_HIP(hipMemsetAsync((char*)g->sc_tab + hb, 0, kScTabBytes - hb, g->stream));
+}
+
 int sc_fits(hgx_graph* g) {   // its grid (0: does not fit); the same residency rule as co_fits
     if (g->sc_ok < 0) {
         int per_cu = 0, cus = 0;
@@ -5132,6 +5146,10 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords), st));
         g->co_vis_seeds = kMaxCoSeeds;
     }
+    if (!g->sc_tab) {   // the stage's tables, empty between calls (a clean launch leaves them so)
+        HGX_HIP(hipMalloc(&g->sc_tab, kScTabBytes));
+        sc_tab_reset(g);
+    }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SeqScratch w{g, {}};
         ScArgs a{};
@@ -5144,15 +5162,15 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.maxd = maxd;
         a.vwords = vwords;
         a.vis = g->co_vis;
-        a.hbits = 19;                               // 512K slots: a level holds <= kScKeyCap discoveries
+        a.hbits = kScHashBits;                      // 512K slots: a level holds <= kScKeyCap discoveries
         a.hmask = ((int64_t)1 << a.hbits) - 1;
-        a.hkey = (u64*)w.take(sizeof(u64) << a.hbits);
-        a.hval = (u64*)w.take(sizeof(u64) << a.hbits);
-        a.krec = (int4*)w.take(sizeof(int4) * (size_t)kScKeyCap);
-        a.kcnt = (uint32_t*)w.take(sizeof(uint32_t) * 2 * (size_t)kScKeyCap);
-        a.kdeg = a.kcnt + kScKeyCap;
-        a.wcnt = (u64*)w.take(sizeof(u64) * 4 * kScWords);   // [2 parities] counts, then [2 parities] degree sums
+        a.hkey = g->sc_tab;
+        a.hval = a.hkey + ((size_t)1 << kScHashBits);
+        a.wcnt = a.hval + ((size_t)1 << kScHashBits);   // [2 parities] counts, then [2 parities] degree sums
         a.wdeg = a.wcnt + 2 * kScWords;
+        a.kcnt = (uint32_t*)(a.wcnt + 4 * kScWords);
+        a.krec = (int4*)w.take(sizeof(int4) * (size_t)kScKeyCap);
+        a.kdeg = (uint32_t*)w.take(sizeof(uint32_t) * (size_t)kScKeyCap);
         a.iseg = (int64_t)1 << 14;
         a.items = (int4*)w.take(sizeof(int4) * 2 * kCoSegs * (size_t)a.iseg);
         a.pcap = std::max<int64_t>(g->sc_pcap, (int64_t)1 << 20);
@@ -5160,15 +5178,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.out_atom = a.out_link + a.pcap;
         a.out_seed = a.out_atom + a.pcap;
         a.ctl = (u64*)w.take(sizeof(u64) * (size_t)kScCtlWords);
-        int32_t* dseeds = (int32_t*)w.take(sizeof(int32_t) * (size_t)k);
-        int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
-        for (int32_t j = 0; j < k; ++j) hs[j] = seeds[sidx[j]];
-        HGX_HIP(hipMemcpyAsync(dseeds, hs, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
-        a.seeds = dseeds;
-        HGX_HIP(hipMemsetAsync(a.hkey, 0xFF, sizeof(u64) << a.hbits, st));
-        HGX_HIP(hipMemsetAsync(a.hval, 0xFF, sizeof(u64) << a.hbits, st));
-        HGX_HIP(hipMemsetAsync(a.kcnt, 0, sizeof(uint32_t) * (size_t)kScKeyCap, st));
-        HGX_HIP(hipMemsetAsync(a.wcnt, 0, sizeof(u64) * 4 * kScWords, st));
+        for (int32_t j = 0; j < k; ++j) a.seeds[j] = seeds[sidx[j]];
         HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScCtlWords, st));
         const int nblk = g->sc_ok;
         PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk));
@@ -5233,9 +5243,10 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         if (trace)
             std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld\n", k,
                          (long long)hm[0], (long long)hm[3], (long long)hm[1], (long long)hm[2]);
-        if (!clean) {   // the bitmaps may hold bits no pair records: cleared whole
+        if (!clean) {   // the bitmaps may hold bits no pair records, the tables entries: cleared whole
             if (hm[3] != 0) ++g->co_timeouts;
             HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
+            sc_tab_reset(g);
             if (hm[0] == 2 && hm[3] == 0 && attempt == 0) {   // only the pairs outgrew their buffer: once more
                 g->sc_pcap = a.pcap * 4;
                 continue;
