@@ -6,17 +6,19 @@
 #   python tools/pmc_summary.py gpurun_out/prof_<tag>_d2  <tag>_d2  dropin2 --from-last hgx_ls_seed
 #   python tools/pmc_summary.py gpurun_out/prof_<tag>_d5a <tag>_d5a dropin5_subsumed
 #   python tools/pmc_summary.py gpurun_out/prof_<tag>_d5b <tag>_d5b dropin5_subsumes
-#   bash tools/pmc_legs.sh <tag> [legs...]     (legs: c2 c3 d2 d5a d5b; default all)
+#   python tools/pmc_summary.py gpurun_out/prof_<tag>_c5  <tag>_c5  config5
+#   bash tools/pmc_legs.sh <tag> [legs...]     (legs: c2 c3 c5 d2 d5a d5b; default all)
 # Each pass runs under its own timeout; the chain stops at the first failure.
 set -u
 TAG=$1
 shift
-LEGS=${@:-"c2 c3 d2 d5a d5b"}
+LEGS=${@:-"c2 c3 c5 d2 d5a d5b"}
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 for L in $LEGS; do
     case $L in
         c2) CMD="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-queries --no-config4 --no-config5 --no-dropin" ;;
         c3) CMD="tools/pattern_timing.py --calls 6" ;;
+        c5) CMD="tools/c5_step.py --mode concurrent --steps 20" ;;
         d2) CMD="tools/seq_c2.py --reps 2" ;;
         d5a) CMD="tools/seq_c5.py --engines 0 --single 0 --reps 5 --direction subsumed" ;;
         d5b) CMD="tools/seq_c5.py --engines 0 --single 0 --reps 5 --direction subsumes" ;;
