@@ -3564,6 +3564,7 @@ constexpr int kScChunk = 64;                       // adjacency pairs per work i
 constexpr int64_t kScKeyCap = (int64_t)1 << 18;    // keys (items) of one level: an LDS prefix of 4096 words
 constexpr int kScWords = (int)(kScKeyCap / 64);
 constexpr int kScProbes = 64;
+constexpr int kScPairs = 2;                        // expand: pairs a lane works on together
 // ctl words: [0] barrier, [kScSt .. +1] status by phase parity, [kScSt + 2] sticky status, [kScItm + p*kCoSegs +
 // seg] work-item counters (parity p), then lcnt [kCoMaxLevels x 64]
 constexpr int kScSt = 4, kScItm = 8, kScLcnt = kScItm + 2 * kCoSegs;
@@ -3603,6 +3604,8 @@ struct ScArgs {
     int32_t* h_link;                                 // mapped [pcap] the result read out by the kernel's end: links,
     int32_t* h_atom;                                 //   atoms (level-major, rank order)
     int64_t* h_lcnt;                                 //   and [levels x 64] pairs per level and seed
+    int64_t* trace;                                  // mapped [3 x kCoMaxLevels] or null (HGX_CO_TRACE): block 0's clock
+                                                     //   at each level's start, after its P1 barrier, after its P2 work
     u64 timeout;
 };
 
@@ -3722,6 +3725,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         u64* wcnt = a.wcnt + (int64_t)par * kScWords;
         u64* wdeg = a.wdeg + (int64_t)par * kScWords;
         // ---- P1: expand ----
+        if (a.trace && blockIdx.x == 0 && threadIdx.x == 0 && d < kCoMaxLevels) a.trace[3 * d] = (int64_t)wall_clock64();
         if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1)) | sc_ld(st_sticky);   // [xwg] the last phase's errors
         const int64_t nf = sc_seg_prefix(a.ctl + kScItm + par * kCoSegs, a.iseg, s_pre);
         const u64 st = s_st;
@@ -3772,61 +3776,105 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                     if (lane >= off) x += y;
                 }
                 const int64_t TT = __shfl(x, 63), ex = x - cnt;
-                for (int64_t f0 = 0; f0 < TT; f0 += 64) {   // wave-uniform
-                    const int64_t f = f0 + lane;
-                    int o = 0;
+                // kScPairs pairs a lane per step (wave-uniform): their dependent round trips (target, examined word,
+                // slot claim, minimum) overlap instead of following each other
+                for (int64_t f0 = 0; f0 < TT; f0 += 64 * kScPairs) {
+                    int32_t ts[kScPairs], ss[kScPairs], las[kScPairs];
+                    int64_t its[kScPairs];
+                    bool ok[kScPairs];
 #pragma unroll
-                    for (int step = 32; step > 0; step >>= 1) {
-                        const int mid = o + step;
-                        if (__shfl(ex, mid) <= f) o = mid;
-                    }
-                    const int32_t s = __shfl(is, o);
-                    const int64_t off_ = f - __shfl(ex, o);
-                    const int64_t ii = __shfl(yb, o) + off_, it = __shfl(itb, o) + off_;
-                    if (f >= TT) continue;
-                    const int32_t t = a.a_tgt[ii];
-                    const int32_t la = a.a_lnk[ii];
-                    nbytes += 8;
-                    const u64 vw = sc_ld(a.vis + (int64_t)s * a.vwords + (t >> 6));   // [xwg]
-                    nbytes += 8;
-                    if ((vw >> (t & 63)) & 1ull) continue;   // examined already
-                    const u64 key = (u64)(uint32_t)s << 32 | (u64)(uint32_t)t;
-                    const u64 v = ((u64)(it + 1) << 32) | (u64)(uint32_t)la;
-                    u64 h = ls_hash(key, a.hbits);
-                    u64 old = 0ull;   // the slot's value before this item's atomicMin (0: no update made)
-                    int probe = 0;
-                    for (; probe < kScProbes; ++probe) {
-                        u64 kk = sc_ld(a.hkey + h);   // [xwg]
-                        if (kk == kLsEmpty)
-                            kk = atomicCAS((unsigned long long*)(a.hkey + h), kLsEmpty, (unsigned long long)key);   // [xwg]
-                        if (kk == kLsEmpty || kk == key) {   // claimed now, or the key's slot
-                            if (kk == kLsEmpty || sc_ld(a.hval + h) > v)   // [xwg]
-                                old = atomicMin((unsigned long long*)(a.hval + h), (unsigned long long)v);   // [xwg]
-                            break;
+                    for (int q = 0; q < kScPairs; ++q) {
+                        const int64_t f = f0 + q * 64 + lane;
+                        int o = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1) {
+                            const int mid = o + step;
+                            if (__shfl(ex, mid) <= f) o = mid;
                         }
-                        h = (h + 1) & (u64)a.hmask;
+                        ss[q] = __shfl(is, o);
+                        const int64_t off_ = f - __shfl(ex, o);
+                        const int64_t ii = __shfl(yb, o) + off_;
+                        its[q] = __shfl(itb, o) + off_;
+                        ok[q] = f < TT;
+                        ts[q] = ok[q] ? a.a_tgt[ii] : 0;
+                        las[q] = ok[q] ? a.a_lnk[ii] : 0;
+                        nbytes += ok[q] ? 8 : 0;
                     }
-                    nbytes += 24;
-                    if (probe == kScProbes) {
-                        atomicOr(stw, 4ull);   // [xwg] the hash is too full
-                        continue;
+                    u64 vws[kScPairs];
+#pragma unroll
+                    for (int q = 0; q < kScPairs; ++q)
+                        vws[q] = ok[q] ? sc_ld(a.vis + (int64_t)ss[q] * a.vwords + (ts[q] >> 6)) : ~0ull;   // [xwg]
+                    u64 keys[kScPairs], vs[kScPairs], hs[kScPairs], olds[kScPairs];
+                    bool pend[kScPairs];
+#pragma unroll
+                    for (int q = 0; q < kScPairs; ++q) {
+                        nbytes += ok[q] ? 8 : 0;
+                        pend[q] = ok[q] && !((vws[q] >> (ts[q] & 63)) & 1ull);   // not examined yet
+                        keys[q] = (u64)(uint32_t)ss[q] << 32 | (u64)(uint32_t)ts[q];
+                        vs[q] = ((u64)(its[q] + 1) << 32) | (u64)(uint32_t)las[q];
+                        hs[q] = ls_hash(keys[q], a.hbits);
+                        olds[q] = 0ull;   // the slot's value before this pair's atomicMin (0: no update made)
                     }
-                    if (old <= v) continue;   // (old == 0: no update; else a lower value was there first)
-                    // this item is the slot's minimum so far: count its key, uncount the displaced one
-                    const uint32_t mykey = (uint32_t)it;
-                    const uint32_t dg = expand_next ? (uint32_t)(a.y_off[t + 1] - a.y_off[t]) : 0u;
-                    co_put(a.krec + mykey, make_int4(t, s, la, (int32_t)(uint32_t)h));   // [xwg]
-                    sc_st32(a.kdeg + mykey, dg);                                          // [xwg]
-                    atomicAdd(a.kcnt + mykey, 1u);                                        // [xwg]
-                    atomicAdd((unsigned long long*)(wcnt + (mykey >> 6)), 1ull);          // [xwg]
-                    if (dg) atomicAdd((unsigned long long*)(wdeg + (mykey >> 6)), (unsigned long long)dg);   // [xwg]
-                    nbytes += 16 + 4 + 4 + 8 + (dg ? 8 : 0);
-                    if (old != ~0ull) {   // the displaced minimum (same target: same degree)
-                        const uint32_t okey = (uint32_t)((old >> 32) - 1ull);
-                        atomicSub(a.kcnt + okey, 1u);                                     // [xwg]
-                        atomicAdd((unsigned long long*)(wcnt + (okey >> 6)), ~0ull);      // [xwg] -1
-                        if (dg) atomicAdd((unsigned long long*)(wdeg + (okey >> 6)), (unsigned long long)(0ull - (u64)dg));   // [xwg]
-                        nbytes += 4 + 8 + (dg ? 8 : 0);
+                    // the level hash: claim (CAS) or find the key's slot, then lower its value; every pending pair's
+                    // CAS of a probe round in flight together
+                    for (int probe = 0; probe < kScProbes; ++probe) {
+                        bool any = false;
+#pragma unroll
+                        for (int q = 0; q < kScPairs; ++q) any |= pend[q];
+                        if (!any) break;
+                        u64 kk[kScPairs];
+#pragma unroll
+                        for (int q = 0; q < kScPairs; ++q)
+                            kk[q] = pend[q] ? atomicCAS((unsigned long long*)(a.hkey + hs[q]), kLsEmpty, (unsigned long long)keys[q]) : 0ull;   // [xwg]
+#pragma unroll
+                        for (int q = 0; q < kScPairs; ++q) {
+                            if (!pend[q]) continue;
+                            if (kk[q] == kLsEmpty || kk[q] == keys[q]) {   // claimed now, or the key's slot
+                                olds[q] = atomicMin((unsigned long long*)(a.hval + hs[q]), (unsigned long long)vs[q]);   // [xwg]
+                                pend[q] = false;
+                                nbytes += 24;
+                            } else {
+                                hs[q] = (hs[q] + 1) & (u64)a.hmask;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < kScPairs; ++q) {
+                        if (pend[q]) atomicOr(stw, 4ull);   // [xwg] the hash is too full
+                        const u64 old = olds[q], v = vs[q];
+                        const bool mine = ok[q] && !pend[q] && old > v;   // (old == 0: no update; else a lower value was first)
+                        const int32_t t = ts[q];
+                        const uint32_t mykey = (uint32_t)its[q];
+                        const uint32_t dg = mine && expand_next ? (uint32_t)(a.y_off[t + 1] - a.y_off[t]) : 0u;
+                        // the +1s of the wave's new minima, one atomic pair per 64-key word (a wave's pairs are
+                        // consecutive items, so their keys share one or two words)
+                        u64 rem = __ballot(mine);
+                        while (rem) {   // wave-uniform
+                            const int ld = __ffsll((long long)rem) - 1;
+                            const uint32_t wl = (uint32_t)__shfl((int)(mykey >> 6), ld);
+                            const u64 grp = __ballot(mine && (mykey >> 6) == wl);
+                            uint64_t sd = ((grp >> lane) & 1ull) ? (uint64_t)dg : 0ull;
+#pragma unroll
+                            for (int off = 32; off > 0; off >>= 1) sd += __shfl_xor(sd, off);
+                            if (lane == ld) {
+                                atomicAdd((unsigned long long*)(wcnt + wl), (unsigned long long)__popcll(grp));   // [xwg]
+                                if (sd) atomicAdd((unsigned long long*)(wdeg + wl), (unsigned long long)sd);      // [xwg]
+                            }
+                            rem &= ~grp;
+                        }
+                        if (!mine) continue;
+                        // this pair is the slot's minimum so far: count its key, uncount the displaced one
+                        co_put(a.krec + mykey, make_int4(t, ss[q], las[q], (int32_t)(uint32_t)hs[q]));   // [xwg]
+                        sc_st32(a.kdeg + mykey, dg);                                                      // [xwg]
+                        atomicAdd(a.kcnt + mykey, 1u);                                                    // [xwg]
+                        nbytes += 16 + 4 + 4 + 8 + (dg ? 8 : 0);
+                        if (old != ~0ull) {   // the displaced minimum (same target: same degree)
+                            const uint32_t okey = (uint32_t)((old >> 32) - 1ull);
+                            atomicSub(a.kcnt + okey, 1u);                                                 // [xwg]
+                            atomicAdd((unsigned long long*)(wcnt + (okey >> 6)), ~0ull);                  // [xwg] -1
+                            if (dg) atomicAdd((unsigned long long*)(wdeg + (okey >> 6)), (unsigned long long)(0ull - (u64)dg));   // [xwg]
+                            nbytes += 4 + 8 + (dg ? 8 : 0);
+                        }
                     }
                 }
             }
@@ -3835,6 +3883,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         ++ph;
         if (timed_out) break;
         // ---- P2: rank, emit, next items ----
+        if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[3 * d + 1] = (int64_t)wall_clock64();
         if (threadIdx.x == 0) s_st = sc_ld(a.ctl + kScSt + (ph & 1));   // [xwg]
         const int64_t Wn = (T + 63) / 64;
         {   // the words' counts and degree sums -> exclusive prefixes in LDS (every block; coalesced loads, each
@@ -3907,13 +3956,15 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
             for (int64_t w = gw; w < Wn; w += nw) {   // a wave per non-empty word, a lane per key
                 if (s_cpre[w + 1] == s_cpre[w]) continue;   // wave-uniform
                 const uint32_t key = (uint32_t)(w * 64 + lane);
+                // the key's count, record and degree loaded together (the record and degree only mean something
+                // where the count is 1: one round trip instead of two)
                 const bool set = sc_ld32(a.kcnt + key) != 0u;   // [xwg] (1: the key is its slot's minimum)
+                int4 rec = co_get(a.krec + key);                // [xwg] (t, s, link, slot)
+                uint32_t dg = sc_ld32(a.kdeg + key);            // [xwg]
                 const u64 m = __ballot(set);
-                uint32_t dg = 0;
-                int4 rec = make_int4(0, 0, 0, 0);
-                if (set) {
-                    rec = co_get(a.krec + key);      // [xwg] (t, s, link, slot)
-                    dg = sc_ld32(a.kdeg + key);      // [xwg]
+                if (!set) {
+                    rec = make_int4(0, 0, 0, 0);
+                    dg = 0;
                 }
                 int64_t ex = dg;
 #pragma unroll
@@ -3946,6 +3997,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
                 atomicAdd(a.ctl + kScLcnt + (int64_t)d * 64 + s, s_cnt[s]);   // [xwg] read by the host
                 s_cnt[s] = 0;
             }
+        if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[3 * d + 2] = (int64_t)wall_clock64();
         out0 += nd;
         Tprev = T;
         T = Tn;
@@ -5181,7 +5233,8 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         for (int32_t j = 0; j < k; ++j) a.seeds[j] = seeds[sidx[j]];
         HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScCtlWords, st));
         const int nblk = g->sc_ok;
-        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk));
+        static const bool trace = trace_env("HGX_CO_TRACE");
+        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk + (trace ? 3 * (size_t)kCoMaxLevels : 0)));
         int64_t* hm = (int64_t*)hb.p;
         hm[0] = -1;
         hm[1] = hm[2] = hm[3] = 0;
@@ -5190,6 +5243,7 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.hmeta = (int64_t*)hmd;
         a.blk_bytes = (int64_t*)hmd + 8;
         a.blk_trav = a.blk_bytes + nblk;
+        a.trace = trace ? a.blk_trav + nblk : nullptr;
         // the result, written by the kernel's end into mapped memory: links [pcap] | atoms [pcap] | level counts
         PoolBuf pb = take_host_buf(g, 8 * (size_t)a.pcap + 8 * (size_t)kCoMaxLevels * 64);
         struct PairsBack {   // back to the pool unless the result keeps it
@@ -5239,10 +5293,14 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             ev_give(g, ev[1]);
         }
         const bool clean = hm[0] == 0 && hm[3] == 0;
-        static const bool trace = trace_env("HGX_CO_TRACE");
-        if (trace)
-            std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld\n", k,
+        if (trace) {   // per level: P1 (expand + barrier) and P2 (emit) in microseconds of block 0's clock (100 MHz)
+            std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld; us P1/P2:", k,
                          (long long)hm[0], (long long)hm[3], (long long)hm[1], (long long)hm[2]);
+            const int64_t* tr = hm + 8 + 2 * (size_t)nblk;
+            for (int64_t d = 0; d < hm[1] && d < kCoMaxLevels; ++d)
+                std::fprintf(stderr, " %.1f/%.1f", (tr[3 * d + 1] - tr[3 * d]) * 0.01, (tr[3 * d + 2] - tr[3 * d + 1]) * 0.01);
+            std::fprintf(stderr, "\n");
+        }
         if (!clean) {   // the bitmaps may hold bits no pair records, the tables entries: cleared whole
             if (hm[3] != 0) ++g->co_timeouts;
             HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
