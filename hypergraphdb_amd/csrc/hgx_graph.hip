@@ -58,8 +58,10 @@ void graph_release(hgx_graph* g) {
     if (g->mapped) (void)hipHostFree(g->mapped);
     if (g->zc_in) (void)hipHostFree(g->zc_in);
     if (g->stream2) (void)hipStreamSynchronize(g->stream2);
+    if (g->stream3) (void)hipStreamSynchronize(g->stream3);
     if (g->ev_count) (void)hipEventDestroy(g->ev_count);
     if (g->stream2) (void)hipStreamDestroy(g->stream2);
+    if (g->stream3) (void)hipStreamDestroy(g->stream3);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     if (g->shard) {
         (void)hipFree(g->shard->own_bm); (void)hipFree(g->shard->xo_part); (void)hipFree(g->shard->xo_lid);

@@ -243,6 +243,7 @@ struct hgx_graph {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;      // readout counting next to the traversal (made on first use)
+    hipStream_t stream3 = nullptr;      // the order-exact level engine's second copy stream (made on first use)
     hipEvent_t ev_count = nullptr;      //   and its ordering event
     std::mutex mu;
     std::atomic<int> refs{1};

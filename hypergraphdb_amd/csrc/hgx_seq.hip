@@ -1977,7 +1977,8 @@ struct LsArgs {
     // part its atoms, a bit per pair where the link changes (the pair starts a new link run), the links of
     // those pairs, and per 4096-pair block the number of runs before it
     int64_t pack_min;
-    int32_t* patom;                     // [cap] atoms, level-major like out_pair
+    int32_t* patom;                     // [cap] atoms, level-major like out_pair; abytes bytes each (3 when every
+    int32_t abytes;                     //   atom id fits 24 bits: a quarter less to copy than 4-byte ids)
     int32_t* pclink;                    // [cap] a part's run links from its first pair's index on
     u64* pflag;                         // [2 parities][kLrParts][pwcap] run-start bits of a part's pairs
     uint32_t* pbb;                      // [2 parities][kLrParts][pbcap] runs before each 4096-pair block
@@ -3457,7 +3458,14 @@ __global__ void __launch_bounds__(256) hgx_lr_pemit(LsArgs a, int32_t d, int32_t
         const int64_t i0 = b * kLpBlk, i1 = min<int64_t>(np, i0 + kLpBlk);
         for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
             const int2 v = pr[i];
-            at[i] = v.y;
+            if (a.abytes == 4) {
+                at[i] = v.y;
+            } else {   // 3 bytes, little-endian, at byte 3 (out0 + pb + i)
+                uint8_t* q = (uint8_t*)a.patom + 3 * (out0 + pb + i);
+                q[0] = (uint8_t)v.y;
+                q[1] = (uint8_t)(v.y >> 8);
+                q[2] = (uint8_t)(v.y >> 16);
+            }
             const int wl = (int)((i - i0) >> 6), bit = (int)(i & 63);
             const u64 m = s_fl[wl];
             if ((m >> bit) & 1ull) lk[s_pre[wl] + __popcll(m & ((1ull << bit) - 1ull))] = v.x;
@@ -4111,6 +4119,7 @@ struct Seg {
     const u64* flags = nullptr;
     const uint32_t* bb = nullptr;
     int64_t pi = 0;
+    int32_t ab = 4;               // packed: bytes an atom (3: 24-bit little-endian ids; atom is then a byte address)
     hipEvent_t ready = nullptr;   // the copy into its buffer (level engine): readers wait for it
 };
 
@@ -4118,7 +4127,12 @@ struct Seg {
 // over interleaved (link, atom) pairs
 inline void copy_pairs(const Seg& s, int64_t so, int64_t n, int32_t* links, int32_t* atoms) {
     if (s.stride == 0) {
-        if (atoms) std::memcpy(atoms, s.atom + so, sizeof(int32_t) * (size_t)n);
+        if (atoms && s.ab == 4) {
+            std::memcpy(atoms, s.atom + so, sizeof(int32_t) * (size_t)n);
+        } else if (atoms) {
+            const uint8_t* q = (const uint8_t*)s.atom + 3 * so;
+            for (int64_t k = 0; k < n; ++k, q += 3) atoms[k] = (int32_t)((uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16);
+        }
         if (!links || n <= 0) return;
         int64_t i = s.pi + so;
         // the run of pair i: the runs before its 4096-pair block, the run starts before it in the block, its own
@@ -4473,6 +4487,11 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         if (!e) HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!g->stream2) HGX_HIP(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
     hipStream_t cs = g->stream2;   // the pairs' copies to the host, a level (part) at a time
+    // packed rank parts alternate between two copy streams (two DMA engines side by side; A/B builds:
+    // HGX_LS_COPY_STREAMS=1 keeps one)
+    static const int ncs = ab_int("HGX_LS_COPY_STREAMS", 2);
+    if (ncs > 1 && !g->stream3) HGX_HIP(hipStreamCreateWithFlags(&g->stream3, hipStreamNonBlocking));
+    hipStream_t cs2 = ncs > 1 ? g->stream3 : cs;
     u64* hflag_d = nullptr;
     HGX_HIP(hipHostGetDevicePointer((void**)&hflag_d, g->seq_flag, 0));
     const int64_t full = (int64_t)nb * A;
@@ -4542,6 +4561,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
         // levels of >= pack_min pairs go to the host packed (HGX_OPT_SEQ_PACK_MIN: tests pack tiny levels)
         a.pack_min = g->seq_pack_min > 0 ? g->seq_pack_min : (int64_t)1 << 20;
         a.pack_min = std::max<int64_t>(a.pack_min, 1);
+        a.abytes = g->A <= ((int64_t)1 << 24) ? 3 : 4;
         if (a.pack_min <= cap) {
             a.patom = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
             a.pclink = (int32_t*)w.take(sizeof(int32_t) * (size_t)cap);
@@ -4648,6 +4668,7 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
             int64_t out0, n;
             bool packed = false;
             std::vector<LevelPart> parts;
+            int ab = 4;                   // (packed) bytes an atom
             hipEvent_t ready = nullptr;   // (unpacked: after all its copies)
         };
         // the pair copies complete after the call returns (the readers wait per segment): an event after
@@ -4662,11 +4683,11 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 v->clear();
             }
         } ev_guard{&cevs};
-        auto new_copy_event = [&]() {
+        auto new_copy_event = [&](hipStream_t on) {
             hipEvent_t e = nullptr;
             HGX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             cevs.push_back(e);
-            HGX_HIP(hipEventRecord(e, cs));
+            HGX_HIP(hipEventRecord(e, on));
             return e;
         };
         std::vector<LevelBuf> lbufs;
@@ -4707,15 +4728,18 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                                            hipMemcpyDeviceToHost, cs));
                 }
                 HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
-                lbufs.back().ready = new_copy_event();
+                lbufs.back().ready = new_copy_event(cs);
                 return;
             }
-            // packed: atoms [n] | run links [n] | run-start words [n / 64 + kLrParts + 1] | block counts
+            // packed: atoms [n] (abytes each) | run links [n] | run-start words [n / 64 + kLrParts + 1] | block counts
+            const int ab = a.abytes;
             const size_t nw = (size_t)(n / 64 + kLrParts + 1), nbb = (size_t)(n / kLpBlk + kLrParts + 1);
-            PoolBuf hb = take_host_buf(g, 8 * (size_t)n + 8 * nw + 4 * nbb);
+            const size_t areg = ((size_t)ab * (size_t)n + 7) & ~(size_t)7;
+            PoolBuf hb = take_host_buf(g, areg + 4 * (size_t)n + 8 * nw + 4 * nbb);
             LevelBuf lb{hb, out0, n, true, {}};
-            int32_t* h_atom = (int32_t*)hb.p;
-            int32_t* h_link = h_atom + n;
+            lb.ab = ab;
+            char* h_atom = (char*)hb.p;
+            int32_t* h_link = (int32_t*)(h_atom + areg);
             u64* h_flag = (u64*)(h_link + n);
             uint32_t* h_bb = (uint32_t*)(h_flag + nw);
             for (int q = 0; q < kLrParts; ++q) {
@@ -4730,23 +4754,27 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 // a part's words / block counts start after the earlier parts' (b / 64 + q >= their end)
                 u64* hf = h_flag + b / 64 + q;
                 uint32_t* hbk = h_bb + b / kLpBlk + q;
-                const hipStream_t c = cs;
+                const hipStream_t c = (q & 1) ? cs2 : cs;
                 const int64_t slot = (int64_t)(d & 1) * kLrParts + q;
                 HGX_HIP(hipStreamWaitEvent(c, g->ls_ev[kLrParts * (d & 1) + q], 0));
                 // the copies start at a 64-byte boundary of the level (out0 + b0): the extra leading atoms are
                 // the previous part's, already final (same values), the extra leading links fall in the previous
                 // part's link area past its runs or are its own final values
-                const int64_t b0 = std::max<int64_t>(0, ((out0 + b) & ~(int64_t)15) - out0);
+                const int64_t al = ab == 4 ? 16 : 64;   // pairs a 64-byte boundary of the atoms spans
+                const int64_t b0 = std::max<int64_t>(0, ((out0 + b) & ~(al - 1)) - out0);
                 static const bool align = ab_int("HGX_LS_PACK_ALIGN", 1) != 0;   // A/B builds
                 const int64_t bc = align ? b0 : b;
-                HGX_HIP(hipMemcpyAsync(h_atom + bc, a.patom + out0 + bc, sizeof(int32_t) * (size_t)(e - bc), hipMemcpyDeviceToHost, c));
+                HGX_HIP(hipMemcpyAsync(h_atom + (size_t)ab * bc, (const char*)a.patom + (size_t)ab * (out0 + bc),
+                                       (size_t)ab * (size_t)(e - bc), hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(h_link + bc, a.pclink + out0 + bc, sizeof(int32_t) * (size_t)(b + runs - bc),
                                        hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(hf, a.pflag + slot * a.pwcap, sizeof(u64) * (size_t)pw, hipMemcpyDeviceToHost, c));
                 HGX_HIP(hipMemcpyAsync(hbk, a.pbb + slot * a.pbcap, sizeof(uint32_t) * (size_t)pbk, hipMemcpyDeviceToHost, c));
-                lb.parts.push_back({b, e, h_link + b, hf, hbk, new_copy_event()});
+                lb.parts.push_back({b, e, h_link + b, hf, hbk, new_copy_event(c)});
             }
+            if (cs2 != cs) HGX_HIP(hipStreamWaitEvent(cs, new_copy_event(cs2), 0));   // the level's copies joined on cs
             HGX_HIP(hipEventRecord(g->ls_cev[d & 1], cs));
+            new_copy_event(cs);   // (the last event of the call: covers both copy streams)
             lbufs.push_back(std::move(lb));
         };
         int64_t total = 0, status = 0;
@@ -4832,11 +4860,12 @@ bool seq_levels2_chunk(hgx_graph* g, const int32_t* seeds, int32_t nb, int32_t m
                 return;
             }
             const int64_t rb = b - lb.out0, re = e - lb.out0;
-            const int32_t* h_atom = (const int32_t*)lb.b.p;
+            const char* h_atom = (const char*)lb.b.p;
             for (const LevelPart& pt : lb.parts) {
                 const int64_t lo = std::max(rb, pt.b), hi = std::min(re, pt.e);
                 if (hi <= lo) continue;
-                Seg sg{pt.link, h_atom + lo, nullptr, hi - lo, dist, 0};
+                Seg sg{pt.link, (const int32_t*)(h_atom + (size_t)lb.ab * lo), nullptr, hi - lo, dist, 0};
+                sg.ab = lb.ab;
                 sg.flags = pt.flags;
                 sg.bb = pt.bb;
                 sg.pi = lo - pt.b;
