@@ -284,6 +284,7 @@ struct hgx_graph {
     unsigned long long* co_vis = nullptr;           // multi-workgroup stage: per-seed visited bitmaps (zero between calls)
     unsigned long long* sc_tab = nullptr;           // order-exact grid stage: level hash, word / key counts (empty between calls)
     int64_t co_vis_seeds = 0, co_pcap = 0;          //   seeds they hold; pair-list capacity (grown on demand)
+    int64_t co_fr = 0;                              //   work items a level holds, all segments (likewise)
     int32_t co_ok = -1;                             //   its grid in blocks (0: does not fit; -1: not checked yet)
     int64_t co_timeouts = 0;                        //   launches whose grid barrier timed out (seeds fell back)
     int32_t sc_ok = -1;                             // order-exact grid stage (hgx_seq_coop): its grid (0: does not fit)

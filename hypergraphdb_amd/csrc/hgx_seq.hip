@@ -501,6 +501,12 @@ struct SbArgs {
     // (kbits 0: the pair's index is its stream position)
     const int32_t* a_tgt;
     const int32_t* a_lnk;
+    // the seeds handed back go to the chained grid stage's list (round 6; null: the host collects them):
+    // (index of the seed in the call, seed atom) at a slot of an atomic counter (slots >= kMaxCoSeeds dropped:
+    // the stage then sees the count and leaves them to the host)
+    int32_t c0;                                     // the call's index of this launch's first seed
+    int2* chain;
+    uint32_t* chain_n;
 };
 
 struct SbShared {
@@ -912,6 +918,10 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
         a.meta[3 * (int64_t)si] = ovf ? -1 : out_n;
         a.meta[3 * (int64_t)si + 1] = trav;
         a.meta[3 * (int64_t)si + 2] = tb;
+        if (ovf && a.chain_n) {
+            const uint32_t q = atomicAdd(a.chain_n, 1u);
+            if (q < (uint32_t)kMaxCoSeeds) a.chain[q] = make_int2(a.c0 + si, seed);
+        }
     }
 }
 
@@ -1395,7 +1405,8 @@ constexpr unsigned long long kCoPairMask = (1ull << kCoItemShift) - 1ull;
 constexpr int kCoMaxLevels = 1024;
 constexpr unsigned long long kCoTimeout = 100000000ull;   // s_memrealtime ticks (100 MHz): 1 s (HGX_OPT_CO_TIMEOUT: tests)
 // ctl words: [0] barrier top, [1 .. kCoBarGroups] arrival counters, [kCoSt] / [kCoSt + 1] status of
-// even / odd levels (the seeding: odd), [kCoSel] seeds the workgroup
+// even / odd levels (the seeding: odd; bits: 1 a segment's work items outgrew it, 2 its pairs did,
+// 4 more than kCoMaxLevels levels), [kCoSel] seeds the workgroup
 // stage handed over, [kCoLev + slot * kCoSegs + seg] level counters (3 rotating slots), then cur [kcap],
 // trav [kcap], and as int32: the seeds' batch indices [kcap] and atoms [kcap]
 constexpr int kCoSt = 20, kCoSel = 23, kCoLev = 32, kCoCtlWords = kCoLev + 3 * kCoSegs;
@@ -1697,7 +1708,7 @@ __global__ void __launch_bounds__(NT) hgx_bfs_coop(CoArgs a) {
         __syncthreads();   // seg_pre / seg_pairs / s_st are read before the next level rewrites them
         if (st != 0 || nf == 0 || d >= a.maxd) break;   // the same decision in every block
         if (d >= kCoMaxLevels) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + kCoSt, 3ull);
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + kCoSt, 4ull);
             break;
         }
         if (blockIdx.x == 0) {   // read at level d - 1; appended to at level d + 1
@@ -3573,14 +3584,18 @@ constexpr int64_t kScKeyCap = (int64_t)1 << 18;    // keys (items) of one level:
 constexpr int kScWords = (int)(kScKeyCap / 64);
 constexpr int kScProbes = 64;
 constexpr int kScPairs = 2;                        // expand: pairs a lane works on together
-// ctl words: [0] barrier, [kScSt .. +1] status by phase parity, [kScSt + 2] sticky status, [kScItm + p*kCoSegs +
+// ctl words: [0] barrier, [kScSt .. +1] status by phase parity, [kScSt + 2] sticky status, [kScChain] the chained list's
+// length (low 32 bits), [kScItm + p*kCoSegs +
 // seg] work-item counters (parity p), then lcnt [kCoMaxLevels x 64]
-constexpr int kScSt = 4, kScItm = 8, kScLcnt = kScItm + 2 * kCoSegs;
+constexpr int kScSt = 4, kScChain = 7, kScItm = 8, kScLcnt = kScItm + 2 * kCoSegs;
 constexpr int64_t kScCtlWords = kScLcnt + (int64_t)kCoMaxLevels * 64;
 
 struct ScArgs {
-    int32_t k;                                       // seeds (<= kMaxCoSeeds)
+    int32_t k;                                       // seeds (<= kMaxCoSeeds); -1: chained, from the list below
     int32_t seeds[kMaxCoSeeds];                      // inline in the kernel arguments (no upload)
+    const int2* chain;                               // chained: the workgroup engine's (seed index, atom) list
+    const uint32_t* chain_n;                         //   and its length (the seeds it handed back)
+    int64_t* chain_idx;                              // mapped [kMaxCoSeeds]: the chained seeds' indices, for the host
     int64_t A;
     const int64_t* inc_off;                          // traversed items: incidence entries of expanded atoms
     const int64_t* y_off;                            // the yield adjacency
@@ -3695,31 +3710,53 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
     __shared__ u64 s_st;
     __shared__ unsigned long long s_cnt[kMaxCoSeeds];
     __shared__ int64_t s_ws[kWaves];
+    __shared__ int32_t s_seeds[kMaxCoSeeds];
     if (threadIdx.x < kMaxCoSeeds) s_cnt[threadIdx.x] = 0;
+    // the seeds: the arguments', or chained, the list the workgroup engine's launches filled (every block reads
+    // the same length: the previous kernel's writes are visible at this launch's start)
+    const int32_t k = a.k >= 0 ? a.k : (int32_t)min<uint32_t>(*a.chain_n, (uint32_t)kMaxCoSeeds + 1u);
+    if (a.k < 0 && (k == 0 || k > kMaxCoSeeds)) {   // nothing handed back, or more than one launch holds
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            a.hmeta[5] = k;
+            a.hmeta[1] = a.hmeta[2] = 0;
+            __hip_atomic_store(a.hmeta, k == 0 ? 0ll : 128ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;   // (every block: no barrier was reached)
+    }
+    if (threadIdx.x < k) {
+        if (a.k >= 0) {
+            s_seeds[threadIdx.x] = a.seeds[threadIdx.x];
+        } else {
+            const int2 c = a.chain[threadIdx.x];
+            s_seeds[threadIdx.x] = c.y;
+            if (blockIdx.x == 0) a.chain_idx[threadIdx.x] = c.x;
+        }
+    }
+    __syncthreads();
     int64_t nbytes = 0, trav = 0;
     u64* st_sticky = a.ctl + kScSt + 2;
     u64 gen = 0;
     // level 0: the seeds (examined.put(start, TRUE), HGBreadthFirstTraversal.java:42-46); their items in
     // seed order, seed s's first item index = the degrees of the seeds before it
     int64_t T = 0;
-    for (int s = 0; s < a.k; ++s) T += a.y_off[a.seeds[s] + 1] - a.y_off[a.seeds[s]];
+    for (int s = 0; s < k; ++s) T += a.y_off[s_seeds[s] + 1] - a.y_off[s_seeds[s]];
     if (blockIdx.x == 0) {
-        if (threadIdx.x < a.k) {
-            const int32_t t = a.seeds[threadIdx.x];
+        if (threadIdx.x < k) {
+            const int32_t t = s_seeds[threadIdx.x];
             atomicOr(a.vis + (int64_t)threadIdx.x * a.vwords + (t >> 6), 1ull << (t & 63));   // [xwg]
         }
-        for (int s0 = 0; s0 < a.k; s0 += 64) {   // wave 0: seeds 64 at a time (wave-uniform loop)
+        for (int s0 = 0; s0 < k; s0 += 64) {   // wave 0: seeds 64 at a time (wave-uniform loop)
             if (wave != 0) break;
             const int s = s0 + lane;
             int32_t t = 0;
             int64_t dg = 0, it0 = 0;
-            if (s < a.k) {
-                t = a.seeds[s];
+            if (s < k) {
+                t = s_seeds[s];
                 dg = a.maxd > 0 ? a.y_off[t + 1] - a.y_off[t] : 0;
-                for (int q = 0; q < s; ++q) it0 += a.y_off[a.seeds[q] + 1] - a.y_off[a.seeds[q]];
+                for (int q = 0; q < s; ++q) it0 += a.y_off[s_seeds[q] + 1] - a.y_off[s_seeds[q]];
                 if (a.maxd > 0) trav += a.inc_off[t + 1] - a.inc_off[t];
             }
-            sc_put_items(a, 0, 0, t, s, dg, s < a.k ? a.y_off[t] : 0, it0, a.ctl + kScSt + 1);
+            sc_put_items(a, 0, 0, t, s, dg, s < k ? a.y_off[t] : 0, it0, a.ctl + kScSt + 1);
         }
     }
     bool timed_out = co_barrier_lite(a.ctl, gen, a.ctl + kScSt + 1, a.timeout);
@@ -3756,6 +3793,8 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         // in the next level's P1)
         if (blockIdx.x == 0 && threadIdx.x < kCoSegs)
             sc_st(a.ctl + kScItm + (par ^ 1) * kCoSegs + threadIdx.x, 0ull);   // [xwg]
+        if (blockIdx.x == 0 && threadIdx.x < 64)   // this level's per-seed pair counts (added in its P2) -> 0
+            sc_st(a.ctl + kScLcnt + (int64_t)d * 64 + threadIdx.x, 0ull);    // [xwg]
         for (int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x; w < (Tprev + 63) / 64; w += (int64_t)gridDim.x * NT) {
             sc_st(a.wcnt + (int64_t)(par ^ 1) * kScWords + w, 0ull);   // [xwg]
             sc_st(a.wdeg + (int64_t)(par ^ 1) * kScWords + w, 0ull);   // [xwg]
@@ -4000,7 +4039,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
             }
         }
         __syncthreads();
-        for (int s = threadIdx.x; s < a.k; s += NT)
+        for (int s = threadIdx.x; s < k; s += NT)
             if (s_cnt[s]) {
                 atomicAdd(a.ctl + kScLcnt + (int64_t)d * 64 + s, s_cnt[s]);   // [xwg] read by the host
                 s_cnt[s] = 0;
@@ -4058,7 +4097,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
         for (int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x; w < 4 * (int64_t)kScWords; w += (int64_t)gridDim.x * NT)
             a.wcnt[w] = 0ull;   // (wcnt and wdeg are one allocation)
         if (blockIdx.x == 0) {
-            for (int s = threadIdx.x; s < a.k; s += NT) a.vis[(int64_t)s * a.vwords + (a.seeds[s] >> 6)] = 0ull;
+            for (int s = threadIdx.x; s < k; s += NT) a.vis[(int64_t)s * a.vwords + (s_seeds[s] >> 6)] = 0ull;
             for (int64_t x = threadIdx.x; x < (int64_t)d * 64; x += NT) a.h_lcnt[x] = (int64_t)sc_ld(a.ctl + kScLcnt + x);
         }
     }
@@ -4066,6 +4105,7 @@ __global__ void __launch_bounds__(NT) hgx_seq_coop(ScArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.hmeta[1] = d;
         a.hmeta[2] = out0;
+        a.hmeta[5] = k;
         u64 sa = sc_ld(st_sticky) | sc_ld(a.ctl + kScSt) | sc_ld(a.ctl + kScSt + 1);
         if (!done && !sa) sa = 64ull;   // (left the loop without a recorded cause: never clean)
         a.hmeta[0] = (int64_t)sa;
@@ -5009,7 +5049,8 @@ void co_setup(hgx_graph* g, CoRun& r, int32_t k, int32_t kcap, int32_t max_depth
         g->co_vis_seeds = want;
     }
     if (g->co_pcap == 0) g->co_pcap = (int64_t)1 << 22;
-    const int64_t fr_seg = ((int64_t)1 << 21) / kCoSegs;   // work items per segment and level
+    if (g->co_fr == 0) g->co_fr = (int64_t)1 << 21;
+    const int64_t fr_seg = g->co_fr / kCoSegs;   // work items per segment and level
     r.pcap = g->co_pcap;
     int4* fr = (int4*)r.sc.take(sizeof(int4) * 3 * kCoSegs * (size_t)fr_seg);
     r.pairs = (int2*)g->alloc(sizeof(int2) * (size_t)r.pcap);
@@ -5126,15 +5167,28 @@ void co_collect(hgx_graph* g, CoRun& r, const std::vector<int32_t>& sidx, BlockS
 }
 
 // A launch that did not finish: the bitmaps may hold bits of atoms no pair records, so they are
-// cleared whole; true when only the pair list was short (grown to what was found: run again).
+// cleared whole; true when only capacities were short (the pair list grown to what was found, a
+// level's work items doubled: run again).  A segment's share of a level depends on which blocks find
+// its atoms, so a level near the capacity overflows one segment on some runs and not on others.
 bool co_failed(hgx_graph* g, CoRun& r, bool may_grow) {
     const int64_t vwords = g->A / 64 + 1;
     HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), g->stream));
     if (r.hm[3] != 0) ++g->co_timeouts;   // a barrier timed out: the rows engine takes the seeds
-    if (r.hm[0] != 2 || r.hm[3] != 0 || !may_grow) return false;
-    int64_t most = 0;
-    for (int q = 0; q < kCoSegs; ++q) most = std::max(most, r.hm[r.m_seg + q]);
-    g->co_pcap = std::max<int64_t>(2 * r.pcap, kCoSegs * (most + most / 4 + 64));
+    static const bool trace = trace_env("HGX_CO_TRACE");
+    if (trace)
+        std::fprintf(stderr, "[hgx coop] k=%d status=%lld timeout=%lld\n", r.a.k, (long long)r.hm[0], (long long)r.hm[3]);
+    const int64_t st = r.hm[0];
+    if (st <= 0 || (st & ~3ll) != 0 || r.hm[3] != 0 || !may_grow) return false;
+    if (st & 2) {
+        int64_t most = 0;
+        for (int q = 0; q < kCoSegs; ++q) most = std::max(most, r.hm[r.m_seg + q]);
+        g->co_pcap = std::max<int64_t>(2 * r.pcap, kCoSegs * (most + most / 4 + 64));
+    }
+    if (st & 1) {
+        constexpr int64_t kFrMost = (int64_t)1 << 24;   // 768 MiB of work items over the three slots
+        if (g->co_fr >= kFrMost) return false;
+        g->co_fr = std::min(2 * g->co_fr, kFrMost);
+    }
     return true;
 }
 
@@ -5151,7 +5205,7 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
     hipStream_t st = g->stream;
     const int32_t k = (int32_t)sidx.size();
     if (k == 0 || k > kMaxCoSeeds || !co_fits(g)) return false;
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
         CoRun r(g);
         co_setup(g, r, k, k, max_depth, o);
         int32_t* hs = (int32_t*)g->pinned_buf(sizeof(int32_t) * (size_t)k);
@@ -5176,7 +5230,7 @@ bool bfs_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             co_collect(g, r, sidx, out);
             return true;
         }
-        if (!co_failed(g, r, attempt == 0)) return false;
+        if (!co_failed(g, r, attempt < 2)) return false;
     }
     return false;
 }
@@ -5206,35 +5260,53 @@ int sc_fits(hgx_graph* g) {   // its grid (0: does not fit); the same residency 
     return g->sc_ok;
 }
 
-// The stage over the seeds sidx of `seeds` (<= kMaxCoSeeds, generator with a yield adjacency): true and
-// out.segs[j] / traversed / deepest filled for seed j of sidx when it finished; false (bitmaps cleared)
-// when a capacity or the grid did not fit -- the caller runs the level engine.
-bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t maxd,
-              const hgx_algen_opts& o, SeqOut& out, double* ms) {
-    const int mode = seq_mode(o);
-    const YieldAdj* ya = stage_yield_adj(g, mode, o);
-    const int32_t k = (int32_t)sidx.size();
-    if (!ya || k == 0 || k > kMaxCoSeeds || !sc_fits(g)) return false;
-    static const bool off = ab_int("HGX_SEQ_COOP", 1) == 0;   // A/B builds
-    if (off) return false;
-    hipStream_t st = g->stream;
-    const int64_t vwords = g->A / 64 + 1;
-    if (g->co_vis_seeds < kMaxCoSeeds) {   // the grid stages' zero-invariant bitmaps (shared with hgx_bfs_coop)
-        if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
-        g->co_vis = nullptr;
-        g->co_vis_seeds = 0;
-        HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords)));
-        HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords), st));
-        g->co_vis_seeds = kMaxCoSeeds;
+constexpr int32_t kSeqChainMin = 64;   // seeds of a call from which the grid stage is chained (batches)
+
+// One launch of the order-exact grid stage: arguments, scratch and the mapped readout (ScRun::prepare),
+// the launch, and the collection of its result into SeqOut.  The seeds are the launch arguments' (a.k > 0)
+// or, chained behind the workgroup engine's launches (round 6), the list that engine fills with the seeds it
+// hands back (a.k == -1: the kernel reads the list's length and seeds at its start, and no host round trip
+// separates the two stages).
+struct ScRun {
+    hgx_graph* g;
+    SeqScratch w;
+    ScArgs a{};
+    int nblk = 0;
+    bool trace = false;
+    PoolBuf hb{}, pb{};
+    bool keep_pb = false;
+    int32_t* hl = nullptr;
+    int32_t* ha = nullptr;
+    int64_t* hc = nullptr;
+    int64_t* hm = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int2* chain_buf = nullptr;      // (chained) the workgroup engine's list and its length
+    uint32_t* chain_cnt = nullptr;
+    explicit ScRun(hgx_graph* gg) : g(gg), w{gg, {}} {}
+    ~ScRun() {
+        if (ev[0]) ev_give(g, ev[0]);
+        if (ev[1]) ev_give(g, ev[1]);
+        std::lock_guard<std::mutex> lk(g->seq_mu);
+        if (hb.p) g->seq_hbufs.push_back(hb);
+        if (pb.p && !keep_pb) g->seq_hbufs.push_back(pb);
     }
-    if (!g->sc_tab) {   // the stage's tables, empty between calls (a clean launch leaves them so)
-        HGX_HIP(hipMalloc(&g->sc_tab, kScTabBytes));
-        sc_tab_reset(g);
-    }
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        SeqScratch w{g, {}};
-        ScArgs a{};
-        a.k = k;
+    // chain: the seeds come from the workgroup engine's list (a.chain / a.chain_n, zeroed here)
+    void prepare(const YieldAdj* ya, int32_t maxd, bool chain) {
+        hipStream_t st = g->stream;
+        const int64_t vwords = g->A / 64 + 1;
+        if (g->co_vis_seeds < kMaxCoSeeds) {   // the grid stages' zero-invariant bitmaps (shared with hgx_bfs_coop)
+            if (g->co_vis) HGX_HIP(hipFree(g->co_vis));
+            g->co_vis = nullptr;
+            g->co_vis_seeds = 0;
+            HGX_HIP(hipMalloc(&g->co_vis, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords)));
+            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(kMaxCoSeeds * vwords), st));
+            g->co_vis_seeds = kMaxCoSeeds;
+        }
+        if (!g->sc_tab) {   // the stage's tables, empty between calls (a clean launch leaves them so)
+            HGX_HIP(hipMalloc(&g->sc_tab, kScTabBytes));
+            sc_tab_reset(g);
+        }
+        a.k = chain ? -1 : 0;
         a.A = g->A;
         a.inc_off = g->inc_off;
         a.y_off = ya->off;
@@ -5259,44 +5331,44 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         a.out_atom = a.out_link + a.pcap;
         a.out_seed = a.out_atom + a.pcap;
         a.ctl = (u64*)w.take(sizeof(u64) * (size_t)kScCtlWords);
-        for (int32_t j = 0; j < k; ++j) a.seeds[j] = seeds[sidx[j]];
-        HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScCtlWords, st));
-        const int nblk = g->sc_ok;
-        static const bool trace = trace_env("HGX_CO_TRACE");
-        PoolBuf hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk + (trace ? 3 * (size_t)kCoMaxLevels : 0)));
-        int64_t* hm = (int64_t*)hb.p;
+        // the counters, status words and (chained) the list length in word kScChain -> 0; the level counts are
+        // zeroed by each level's P1
+        HGX_HIP(hipMemsetAsync(a.ctl, 0, sizeof(u64) * (size_t)kScLcnt, st));
+        if (chain) {   // the workgroup engine's list: (seed index, seed atom) [kMaxCoSeeds]; its length in the ctl words
+            chain_buf = (int2*)w.take(sizeof(int2) * kMaxCoSeeds);
+            chain_cnt = (uint32_t*)(a.ctl + kScChain);
+            a.chain = chain_buf;
+            a.chain_n = chain_cnt;
+        }
+        nblk = g->sc_ok;
+        trace = trace_env("HGX_CO_TRACE");
+        // mapped: [0, 8) status, levels, pairs, timed out, -, seeds | bytes [nblk] | traversed [nblk] | the chained
+        // seeds' indices [kMaxCoSeeds] | trace
+        hb = take_host_buf(g, sizeof(int64_t) * (8 + 2 * (size_t)nblk + kMaxCoSeeds + (trace ? 3 * (size_t)kCoMaxLevels : 0)));
+        hm = (int64_t*)hb.p;
         hm[0] = -1;
-        hm[1] = hm[2] = hm[3] = 0;
+        hm[1] = hm[2] = hm[3] = hm[5] = 0;
         void* hmd = nullptr;
         HGX_HIP(hipHostGetDevicePointer(&hmd, hm, 0));
         a.hmeta = (int64_t*)hmd;
         a.blk_bytes = (int64_t*)hmd + 8;
         a.blk_trav = a.blk_bytes + nblk;
-        a.trace = trace ? a.blk_trav + nblk : nullptr;
+        a.chain_idx = a.blk_trav + nblk;
+        a.trace = trace ? a.chain_idx + kMaxCoSeeds : nullptr;
         // the result, written by the kernel's end into mapped memory: links [pcap] | atoms [pcap] | level counts
-        PoolBuf pb = take_host_buf(g, 8 * (size_t)a.pcap + 8 * (size_t)kCoMaxLevels * 64);
-        struct PairsBack {   // back to the pool unless the result keeps it
-            hgx_graph* g;
-            PoolBuf b;
-            bool keep = false;
-            ~PairsBack() {
-                if (keep) return;
-                std::lock_guard<std::mutex> lk(g->seq_mu);
-                g->seq_hbufs.push_back(b);
-            }
-        } pback{g, pb};
-        int32_t* hl = (int32_t*)pb.p;
-        int32_t* ha = hl + a.pcap;
-        int64_t* hc = (int64_t*)(ha + a.pcap);
-        {
-            void* pd = nullptr;
-            HGX_HIP(hipHostGetDevicePointer(&pd, pb.p, 0));
-            a.h_link = (int32_t*)pd;
-            a.h_atom = a.h_link + a.pcap;
-            a.h_lcnt = (int64_t*)(a.h_atom + a.pcap);
-        }
+        pb = take_host_buf(g, 8 * (size_t)a.pcap + 8 * (size_t)kCoMaxLevels * 64);
+        hl = (int32_t*)pb.p;
+        ha = hl + a.pcap;
+        hc = (int64_t*)(ha + a.pcap);
+        void* pd = nullptr;
+        HGX_HIP(hipHostGetDevicePointer(&pd, pb.p, 0));
+        a.h_link = (int32_t*)pd;
+        a.h_atom = a.h_link + a.pcap;
+        a.h_lcnt = (int64_t*)(a.h_atom + a.pcap);
         a.timeout = g->co_timeout > 0 ? (u64)g->co_timeout : kCoTimeout;   // HGX_OPT_CO_TIMEOUT (tests)
-        hipEvent_t ev[2] = {nullptr, nullptr};
+    }
+    void launch() {
+        hipStream_t st = g->stream;
         if (g->timing) {
             ev[0] = ev_take(g);
             ev[1] = ev_take(g);
@@ -5306,44 +5378,41 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
         HGX_CHECK_LAUNCH();
         if (ev[1]) HGX_HIP(hipEventRecord(ev[1], st));
         seq_mark("grid stage enqueued");
-        spin_sync(st);
-        seq_mark("grid stage done");
-        struct HostBack {   // the mapped readout goes back to the pool on every path
-            hgx_graph* g;
-            PoolBuf b;
-            ~HostBack() {
-                std::lock_guard<std::mutex> lk(g->seq_mu);
-                g->seq_hbufs.push_back(b);
-            }
-        } back{g, hb};
+    }
+    // After the launch finished: the k seeds' results (seed j of the launch -> out.segs[sidx[j]]).  1: done;
+    // 0: not clean (the bitmaps and tables reset; the caller runs the seeds elsewhere); 2: only the pairs
+    // outgrew their buffer (the capacity grown on the graph: run once more)
+    int collect(int32_t k, const std::vector<int32_t>& sidx, SeqOut& out, double* ms) {
+        hipStream_t st = g->stream;
         if (ev[1]) {
             *ms += ev_ms(g, ev[0], ev[1]);
             ev_give(g, ev[0]);
             ev_give(g, ev[1]);
+            ev[0] = ev[1] = nullptr;
         }
         const bool clean = hm[0] == 0 && hm[3] == 0;
         if (trace) {   // per level: P1 (expand + barrier) and P2 (emit) in microseconds of block 0's clock (100 MHz)
             std::fprintf(stderr, "[hgx seq coop] k=%d status=%lld timeout=%lld levels=%lld pairs=%lld; us P1/P2:", k,
                          (long long)hm[0], (long long)hm[3], (long long)hm[1], (long long)hm[2]);
-            const int64_t* tr = hm + 8 + 2 * (size_t)nblk;
+            const int64_t* tr = hm + 8 + 2 * (size_t)nblk + kMaxCoSeeds;
             for (int64_t d = 0; d < hm[1] && d < kCoMaxLevels; ++d)
                 std::fprintf(stderr, " %.1f/%.1f", (tr[3 * d + 1] - tr[3 * d]) * 0.01, (tr[3 * d + 2] - tr[3 * d + 1]) * 0.01);
             std::fprintf(stderr, "\n");
         }
         if (!clean) {   // the bitmaps may hold bits no pair records, the tables entries: cleared whole
             if (hm[3] != 0) ++g->co_timeouts;
-            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * vwords), st));
+            HGX_HIP(hipMemsetAsync(g->co_vis, 0, sizeof(u64) * (size_t)(g->co_vis_seeds * (g->A / 64 + 1)), st));
             sc_tab_reset(g);
-            if (hm[0] == 2 && hm[3] == 0 && attempt == 0) {   // only the pairs outgrew their buffer: once more
+            if (hm[0] == 2 && hm[3] == 0) {   // only the pairs outgrew their buffer
                 g->sc_pcap = a.pcap * 4;
-                continue;
+                return 2;
             }
-            return false;
+            return 0;
         }
         const int32_t nlev = (int32_t)hm[1];
         const int64_t total = hm[2];
         if (total > a.pcap || nlev > kCoMaxLevels) fail(HGX_E_DEVICE, "hgx_bfs_sequence: grid stage sizes inconsistent");
-        pback.keep = true;
+        keep_pb = true;
         out.bufs.push_back(pb);
         // level-major, seed-major inside a level: seed j's pairs of level d follow the earlier seeds' ones
         int64_t o0 = 0;
@@ -5362,7 +5431,32 @@ bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& si
             out.bytes += (double)hm[8 + b];
             out.traversed += (double)hm[8 + nblk + b];
         }
-        return true;
+        return 1;
+    }
+};
+
+// The stage over the seeds sidx of `seeds` (<= kMaxCoSeeds, generator with a yield adjacency): true and
+// out.segs[j] / traversed / deepest filled for seed j of sidx when it finished; false (bitmaps cleared)
+// when a capacity or the grid did not fit -- the caller runs the level engine.
+bool seq_coop(hgx_graph* g, const int32_t* seeds, const std::vector<int32_t>& sidx, int32_t maxd,
+              const hgx_algen_opts& o, SeqOut& out, double* ms) {
+    const int mode = seq_mode(o);
+    const YieldAdj* ya = stage_yield_adj(g, mode, o);
+    const int32_t k = (int32_t)sidx.size();
+    if (!ya || k == 0 || k > kMaxCoSeeds || !sc_fits(g)) return false;
+    static const bool off = ab_int("HGX_SEQ_COOP", 1) == 0;   // A/B builds
+    if (off) return false;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        ScRun r(g);
+        r.prepare(ya, maxd, false);
+        r.a.k = k;
+        for (int32_t j = 0; j < k; ++j) r.a.seeds[j] = seeds[sidx[j]];
+        r.launch();
+        spin_sync(g->stream);
+        seq_mark("grid stage done");
+        const int res = r.collect(k, sidx, out, ms);
+        if (res == 1) return true;
+        if (res == 0 || attempt == 1) return false;
     }
     return false;
 }
@@ -5781,6 +5875,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
     seq_mark("call set up");
     std::vector<int32_t> rerun;   // seed indices for the level-synchronous engine
     int32_t deepest = 0;
+    std::unique_ptr<ScRun> chained;   // the grid stage chained behind the workgroup launches
     if (g->seq_engine == 0 && n_seeds > 0) {
         const int kbits = bitlen(g->max_arity > 1 ? (u64)(g->max_arity - 1) : 0);
         SbArgs a{};
@@ -5807,6 +5902,15 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
         a.kbits = ya ? 0 : kbits;   // an adjacency pair's index is its whole stream position
         a.maxd = maxd;
         a.t_limit = std::min<int64_t>(INT32_MAX - 1, (int64_t)(0xFFFFFFFFull >> a.kbits));
+        // batches chain the grid stage behind the workgroup launches (no host round trip between the stages);
+        // a single traversal (the drop-in's next() shape) keeps its latency without the extra launch
+        static const bool chain_off = ab_int("HGX_SEQ_CHAIN", 1) == 0 || ab_int("HGX_SEQ_COOP", 1) == 0;   // A/B builds
+        if (!chain_off && ya && n_seeds >= kSeqChainMin && sc_fits(g)) {
+            chained.reset(new ScRun(g));
+            chained->prepare(ya, maxd, true);
+            a.chain = chained->chain_buf;
+            a.chain_n = chained->chain_cnt;
+        }
         const size_t per_seed = (size_t)kSbPairs * 12 + 24;
         int32_t* dseeds = nullptr;
         size_t dseeds_n = 0;
@@ -5832,6 +5936,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             char* d = (char*)dv;
             // layout: meta [3 nb] int64 | link [nb * kSbPairs] | atom [..] | dist [..]
             a.n = (int32_t)nb;
+            a.c0 = (int32_t)c0;
             a.meta = (int64_t*)d;
             a.out_link = (int32_t*)(d + 24 * nb);
             a.out_atom = a.out_link + nb * kSbPairs;
@@ -5852,6 +5957,7 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             HGX_HIP(hipEventRecord(evb, st));
         }
         seq_mark("workgroup stage enqueued");
+        if (chained) chained->launch();
         spin_sync(st);
         seq_mark("workgroup stage done");
         if (evb) {
@@ -5895,7 +6001,34 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             HGX_HIP(hipEventRecord(el0, st));
         }
         bool done = false;
-        if (g->seq_engine == 0 && rs.size() <= (size_t)kMaxCoSeeds) {   // the grid stage first (one launch)
+        if (chained) {   // the chained grid stage took exactly these seeds (its list, in arrival order)
+            const int64_t kk = chained->hm[5];
+            if (kk == (int64_t)rerun.size() && kk <= kMaxCoSeeds) {
+                std::vector<int32_t> pos((size_t)kk);
+                for (int64_t j = 0; j < kk; ++j) {   // list entry j -> its position in rerun (ascending)
+                    const int64_t idx = chained->hm[8 + 2 * (size_t)chained->nblk + j];
+                    const auto it = std::lower_bound(rerun.begin(), rerun.end(), (int32_t)idx);
+                    if (it == rerun.end() || *it != (int32_t)idx) fail(HGX_E_DEVICE, "hgx_bfs_sequence: chained seed list inconsistent");
+                    pos[j] = (int32_t)(it - rerun.begin());
+                }
+                SeqOut co;
+                co.segs.assign(rs.size(), {});
+                done = chained->collect((int32_t)kk, pos, co, &r->ms_coop) == 1;
+                if (done) {
+                    r->lev.segs = std::move(co.segs);
+                    r->lev.bufs = std::move(co.bufs);
+                    r->lev.traversed = co.traversed;
+                    r->lev.deepest = co.deepest;
+                    r->bytes_coop = co.bytes;
+                    r->n_coop = (int32_t)rs.size();
+                }
+            } else if (chained->hm[0] != 0 || chained->hm[3] != 0) {   // did not run them: state back to empty
+                SeqOut co;
+                (void)chained->collect(0, {}, co, &r->ms_coop);
+            }
+            chained.reset();
+        }
+        if (!done && g->seq_engine == 0 && rs.size() <= (size_t)kMaxCoSeeds) {   // the grid stage first (one launch)
             r->lev.segs.assign(rs.size(), {});
             std::vector<int32_t> sidx(rs.size());
             for (size_t q = 0; q < rs.size(); ++q) sidx[q] = (int32_t)q;

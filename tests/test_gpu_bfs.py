@@ -651,7 +651,7 @@ def test_grid_stage_stress(case):
         r = bfs_batch(snap, seeds, maxd, gen_)
         res[blk] = (r.counts().copy(), r.stats()["traversed_edges"], r.stats(accounting=False), r)
     (c2, t2, s2, r2), (c0, t0, _, r0) = res[2], res[0]
-    assert s2["block_coop"] == 64 and s2["coop_fallbacks"] == 0, s2
+    assert s2["block_coop"] == 64 and s2["coop_fallbacks"] == 0, {k: s2[k] for k in ("block_coop", "coop_fallbacks", "block_rerun", "block_seeds")}
     n = max(c2.shape[1], c0.shape[1])
     pad = lambda c: np.pad(c, ((0, 0), (0, n - c.shape[1])))
     assert np.array_equal(pad(c2), pad(c0)) and t2 == t0
