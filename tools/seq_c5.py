@@ -4,6 +4,8 @@ hg.subsumes drop-ins run) on config 5: batched 1024-closure calls and single-see
 direction, for the workgroup-per-seed engine (HGX_OPT_SEQ_ENGINE 0) and the level-synchronous one (1).
 
   python tools/seq_c5.py [--scale 1.0] [--single 200] [--engines 0,1] [--direction subsumed|subsumes]
+  python tools/seq_c5.py --concurrent 40     (bench.py's drop-in step: both directions side by side on
+                                              the snapshot and an execution context, median ms a step)
 """
 import argparse
 import json
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--engines", default="0,1")
     ap.add_argument("--direction", choices=("both", "subsumed", "subsumes"), default="both",
                     help="one direction only (its own PMC passes: bench.py's per-direction drop-in rooflines)")
+    ap.add_argument("--concurrent", type=int, default=0, help="steps of the two-context drop-in step")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_sequence, synth
@@ -33,6 +36,30 @@ def main():
     snap.set_timing(True)
     T = g["subsumes_type"]
     out = {"workload": f"config5 scale {args.scale}", "seeds": len(g["seeds"]), "engines": {}}
+    if args.concurrent:
+        from concurrent.futures import ThreadPoolExecutor
+        snap.set_timing(False)
+        views = [snap, snap.context()]
+        gens = [DefaultALGenerator(v, AtomTypeCondition(T), None, False, True, rev) for v, rev in zip(views, (False, True))]
+        pool = ThreadPoolExecutor(1)
+
+        def step():
+            f = pool.submit(bfs_sequence, views[1], g["seeds"], None, gens[1])
+            a = bfs_sequence(views[0], g["seeds"], None, gens[0])
+            return a, f.result()
+
+        for _ in range(5):
+            step()
+        ts = []
+        for _ in range(args.concurrent):
+            t0 = time.perf_counter()
+            step()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        out["concurrent_ms_per_step"] = {"median": round(ts[len(ts) // 2] * 1e3, 3), "min": round(ts[0] * 1e3, 3),
+                                         "mean": round(float(np.mean(ts)) * 1e3, 3), "steps": len(ts)}
+        print(json.dumps(out))
+        return
     for eng in [int(x) for x in args.engines.split(",")]:
         snap.set_option(_lib.HGX_OPT_SEQ_ENGINE, eng)
         e = {}
