@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--direction", choices=("both", "subsumed", "subsumes"), default="both",
                     help="one direction only (its own PMC passes: bench.py's per-direction drop-in rooflines)")
     ap.add_argument("--concurrent", type=int, default=0, help="steps of the two-context drop-in step")
+    ap.add_argument("--breakdown", type=int, default=0, help="calls per direction: C call vs readout times")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_sequence, synth
@@ -36,6 +37,30 @@ def main():
     snap.set_timing(True)
     T = g["subsumes_type"]
     out = {"workload": f"config5 scale {args.scale}", "seeds": len(g["seeds"]), "engines": {}}
+    if args.breakdown:   # host side of a batched call per direction: the C call vs the readout into arrays
+        import ctypes as C
+        from hypergraphdb_amd.algorithms import SequenceResult
+        from hypergraphdb_amd._lib import check, lib, ptr
+        snap.set_timing(False)
+        s_ = np.ascontiguousarray(g["seeds"], np.int32)
+        for rev, name in ((False, "subsumed"), (True, "subsumes")):
+            gen_ = DefaultALGenerator(snap, AtomTypeCondition(T), None, False, True, rev)
+            opts = gen_.options()
+            tc, tr = [], []
+            for it in range(args.breakdown + 3):
+                h = C.c_void_p()
+                t0 = time.perf_counter()
+                check(lib().hgx_bfs_sequence(snap.handle, ptr(s_), len(s_), _lib.HGX_UNBOUNDED, C.byref(opts), C.byref(h)))
+                t1 = time.perf_counter()
+                SequenceResult(h, s_)
+                t2 = time.perf_counter()
+                if it >= 3:
+                    tc.append(t1 - t0)
+                    tr.append(t2 - t1)
+            out[name] = {"call_ms_median": round(float(np.median(tc)) * 1e3, 3),
+                         "readout_ms_median": round(float(np.median(tr)) * 1e3, 3)}
+        print(json.dumps(out))
+        return
     if args.concurrent:
         from concurrent.futures import ThreadPoolExecutor
         snap.set_timing(False)
