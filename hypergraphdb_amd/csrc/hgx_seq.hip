@@ -474,6 +474,7 @@ constexpr int kSbRound = kSbThreads * 16;           // items one staging step ma
 constexpr int kSbU = 4;                             // 16-byte segments a lane loads at once
 constexpr int kSbInline = 32;                       // seeds passed in the kernel arguments
 constexpr int kSbChunk = 1024;                      // seeds per launch (mapped output per launch)
+constexpr int kSbSmallRank = 128;                    // levels of at most this many new atoms: ranked by comparisons
 
 struct SbArgs {
     int32_t n;                                      // seeds of this launch
@@ -507,6 +508,7 @@ struct SbArgs {
     int32_t c0;                                     // the call's index of this launch's first seed
     int2* chain;
     uint32_t* chain_n;
+    int64_t* clk;                                   // HGX_SB_CLOCK (tracing): [2 n] start / end ticks a seed
 };
 
 struct SbShared {
@@ -524,10 +526,10 @@ struct SbShared {
             int32_t pay[kSbFront];
         } srt;                                      // bitonic sort buffer
     } u;
-    int64_t wsum[kSbWaves];
+    int64_t wsum[kSbWaves], wsum2[kSbWaves];
     int32_t cp[kSbThreads];                         // rank bitmap: popcount prefix of each thread's words
     int64_t T, S;
-    int32_t cand_n, n_disc, ovf;
+    int32_t cand_n, n_disc, ovf, nn;               // nn: new atoms of the level (compaction reservations)
 };
 
 // exclusive block scan (every thread calls it); *total = the block sum
@@ -551,6 +553,40 @@ __device__ __forceinline__ int64_t sb_scan(SbShared& sm, int64_t v, int64_t* tot
     __syncthreads();
     *total = tot;
     return base + x - v;
+}
+
+// two exclusive block scans in one pass (the frontier's degree and segment prefixes: one pair of barriers)
+__device__ __forceinline__ void sb_scan2(SbShared& sm, int64_t v, int64_t u, int64_t* pv, int64_t* pu, int64_t* tv,
+                                         int64_t* tu) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v, y = u;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t xs = __shfl_up(x, off), ys = __shfl_up(y, off);
+        if (lane >= off) {
+            x += xs;
+            y += ys;
+        }
+    }
+    if (lane == 63) {
+        sm.wsum[w] = x;
+        sm.wsum2[w] = y;
+    }
+    __syncthreads();
+    int64_t bx = 0, by = 0, sx = 0, sy = 0;
+#pragma unroll
+    for (int k = 0; k < kSbWaves; ++k) {
+        const int64_t a = sm.wsum[k], b = sm.wsum2[k];
+        bx += k < w ? a : 0;
+        by += k < w ? b : 0;
+        sx += a;
+        sy += b;
+    }
+    __syncthreads();
+    *pv = bx + x - v;
+    *pu = by + y - u;
+    *tv = sx;
+    *tu = sy;
 }
 
 // last index i in [0, n) with pre[i] <= x (pre non-decreasing, pre[0] <= x)
@@ -611,9 +647,8 @@ __device__ void sb_frontier(SbShared& sm, const SbArgs& a, int F) {
         ds += dg[k];
         ss += sg[k];
     }
-    int64_t T, S;
-    int64_t dp = sb_scan(sm, ds, &T);
-    int64_t sp = sb_scan(sm, ss, &S);
+    int64_t T, S, dp, sp;
+    sb_scan2(sm, ds, ss, &dp, &sp, &T, &S);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = tid * 4 + k;
@@ -629,6 +664,7 @@ __device__ void sb_frontier(SbShared& sm, const SbArgs& a, int F) {
         sm.e_sp[F] = (int32_t)(S < INT32_MAX ? S : INT32_MAX);
         sm.T = T;
         sm.S = S;
+        sm.nn = 0;
     }
     __syncthreads();
 }
@@ -740,6 +776,7 @@ __device__ __forceinline__ void sb_emit(SbShared& sm, const SbArgs& a, int64_t o
 __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int32_t seed = a.n <= kSbInline ? a.seed_inline[si] : a.seeds[si];
+    if (a.clk && tid == 0) a.clk[2 * (int64_t)si] = (int64_t)__builtin_amdgcn_s_memrealtime();
     for (int i = tid; i < kSbHash; i += kSbThreads) {
         sm.h_atom[i] = -1;
         sm.h_val[i] = ~0ull;
@@ -848,12 +885,32 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
             const int sl = tid * (kSbHash / kSbThreads) + k;
             if (sm.h_atom[sl] != -1 && sm.h_val[sl] != 0ull) nm |= 1u << k;
         }
-        int64_t n_new;
-        const int64_t off = sb_scan(sm, __popc(nm), &n_new);
+        {   // the (value, slot) pairs of the new atoms compacted in any order (reservations on sm.nn): the
+            // small-level and sort paths rank them, the bitmap path re-reads the values
+            const int cnt = __popc(nm);
+            int o = cnt ? atomicAdd(&sm.nn, cnt) : 0;
+#pragma unroll
+            for (int k = 0; k < kSbHash / kSbThreads; ++k)
+                if ((nm >> k) & 1u) {
+                    const int sl = tid * (kSbHash / kSbThreads) + k;
+                    sm.u.srt.key[o] = sm.h_val[sl];
+                    sm.u.srt.pay[o++] = sl;
+                }
+        }
+        __syncthreads();
+        const int64_t n_new = sm.nn;
         if (n_new == 0) break;
         const int32_t dist = d + 1;
         const uint64_t nbits = (uint64_t)T << a.kbits;
-        if (nbits <= (uint64_t)kSbCand * 32) {   // bitmap over the key space + popcount prefix
+        if (n_new <= kSbSmallRank) {   // a small level: rank = the number of smaller values (values are
+                                       // distinct: a key names one item and yield position)
+            if (tid < n_new) {
+                const u64 v = sm.u.srt.key[tid];
+                int r = 0;
+                for (int j = 0; j < (int)n_new; ++j) r += sm.u.srt.key[j] < v ? 1 : 0;
+                sb_emit(sm, a, obase + out_n, r, sm.u.srt.pay[tid], dist);
+            }
+        } else if (nbits <= (uint64_t)kSbCand * 32) {   // bitmap over the key space + popcount prefix
             const int W = (int)((nbits + 63) >> 6);
             for (int w = tid; w < W; w += kSbThreads) sm.u.bm[w] = 0ull;
             __syncthreads();
@@ -887,17 +944,9 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
 #pragma unroll
             for (int k = 0; k < kSbHash / kSbThreads; ++k)
                 if ((nm >> k) & 1u) sb_emit(sm, a, obase + out_n, rk[k], tid * (kSbHash / kSbThreads) + k, dist);
-        } else {   // bitonic sort of the (value, slot) pairs
+        } else {   // bitonic sort of the compacted (value, slot) pairs
             int N2 = 1;
             while (N2 < n_new) N2 <<= 1;
-            int o = (int)off;
-#pragma unroll
-            for (int k = 0; k < kSbHash / kSbThreads; ++k)
-                if ((nm >> k) & 1u) {
-                    const int sl = tid * (kSbHash / kSbThreads) + k;
-                    sm.u.srt.key[o] = sm.h_val[sl];
-                    sm.u.srt.pay[o++] = sl;
-                }
             for (int r = (int)n_new + tid; r < N2; r += kSbThreads) {
                 sm.u.srt.key[r] = ~0ull;
                 sm.u.srt.pay[r] = -1;
@@ -918,6 +967,7 @@ __device__ void sb_run(SbShared& sm, const SbArgs& a, int si) {
         a.meta[3 * (int64_t)si] = ovf ? -1 : out_n;
         a.meta[3 * (int64_t)si + 1] = trav;
         a.meta[3 * (int64_t)si + 2] = tb;
+        if (a.clk) a.clk[2 * (int64_t)si + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
         if (ovf && a.chain_n) {
             const uint32_t q = atomicAdd(a.chain_n, 1u);
             if (q < (uint32_t)kMaxCoSeeds) a.chain[q] = make_int2(a.c0 + si, seed);
@@ -5926,6 +5976,9 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             char* h;
         };
         std::vector<Chunk> chunks;
+        static const bool clk_trace = trace_env("HGX_SB_CLOCK");   // per-seed start / end ticks to stderr
+        int64_t* clk = nullptr;
+        if (clk_trace) HGX_HIP(hipHostMalloc((void**)&clk, sizeof(int64_t) * 2 * (size_t)n_seeds, hipHostMallocMapped));
         for (int64_t c0 = 0; c0 < n_seeds; c0 += kSbChunk) {
             const int64_t nb = std::min<int64_t>(kSbChunk, n_seeds - c0);
             PoolBuf hb = take_host_buf(g, per_seed * (size_t)nb);
@@ -5947,6 +6000,11 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             } else {
                 a.seeds = dseeds + c0;
             }
+            if (clk) {
+                void* dc = nullptr;
+                HGX_HIP(hipHostGetDevicePointer(&dc, clk + 2 * c0, 0));
+                a.clk = (int64_t*)dc;
+            }
             hgx_seq_block<<<(unsigned)nb, kSbThreads, 0, st>>>(a);
             HGX_CHECK_LAUNCH();
             chunks.push_back({c0, nb, h});
@@ -5967,6 +6025,28 @@ int hgx_bfs_sequence(hgx_graph* g, const int32_t* seeds, int32_t n_seeds, int32_
             ev_give(g, evb);
         }
         if (dseeds) g->release(dseeds, dseeds_n);
+        if (clk) {   // per seed: start after the first start, duration (us), pairs, depth; the 12 last to end
+            int64_t t0 = INT64_MAX;
+            for (int32_t i = 0; i < n_seeds; ++i) t0 = std::min(t0, clk[2 * i]);
+            std::vector<int32_t> ord((size_t)n_seeds);
+            for (int32_t i = 0; i < n_seeds; ++i) ord[i] = i;
+            std::sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return clk[2 * x + 1] > clk[2 * y + 1]; });
+            double sum = 0;
+            for (int32_t i = 0; i < n_seeds; ++i) sum += (clk[2 * i + 1] - clk[2 * i]) * 0.01;
+            std::fprintf(stderr, "[hgx sb clock] seeds=%d mean_us=%.1f end_us=%.1f; last to end (seed: start/dur us, pairs, depth):",
+                         n_seeds, sum / std::max(1, n_seeds), (clk[2 * ord[0] + 1] - t0) * 0.01);
+            for (int32_t k = 0; k < std::min<int32_t>(12, n_seeds); ++k) {
+                const int32_t i = ord[k];
+                const Chunk& c = chunks[(size_t)(i / kSbChunk)];
+                const int64_t j = i - c.c0;
+                const int64_t np = ((const int64_t*)c.h)[3 * j];
+                const int32_t* ds = (const int32_t*)(c.h + 24 * c.nb) + 2 * c.nb * kSbPairs;
+                std::fprintf(stderr, " %d: %.1f/%.1f %lld %d;", i, (clk[2 * i] - t0) * 0.01, (clk[2 * i + 1] - clk[2 * i]) * 0.01,
+                             (long long)np, np > 0 ? ds[j * kSbPairs + np - 1] : 0);
+            }
+            std::fprintf(stderr, "\n");
+            (void)hipHostFree(clk);
+        }
         for (auto& c : chunks) {
             const int64_t* meta = (const int64_t*)c.h;
             const int32_t* lk_ = (const int32_t*)(c.h + 24 * c.nb);
