@@ -563,8 +563,11 @@ def dropin_config5(args, ctx, barrier_sync, g, views, gens, pool):
     barrier_sync()
     t1 = time.perf_counter()
     got = []
+    t_steps = []
     for _ in range(n5):
+        t_s = time.perf_counter()
         got = step()
+        t_steps.append(time.perf_counter() - t_s)
     barrier_sync()
     dt = ctx.max(time.perf_counter() - t1)
     for v in views:
@@ -622,6 +625,9 @@ def dropin_config5(args, ctx, barrier_sync, g, views, gens, pool):
     out = {"metric": "order-exact closures/s (hgx_bfs_sequence: the HGTraversal drop-in)",
            "value": ctx.sum(2 * len(g["seeds"]) * n5) / dt, "unit": "closures/s", "steps": n5,
            "ms_per_step": round(dt / n5 * 1e3, 3), "ms_per_step_with_timing_events": round(dt_ev / n5 * 1e3, 3),
+           # the step time's spread (value and ms_per_step are the whole loop's mean; a few steps take
+           # several times the median, tools/seq_c5.py --concurrent shows the same)
+           "ms_step_median": round(float(np.median(t_steps)) * 1e3, 3), "ms_step_max": round(max(t_steps) * 1e3, 3),
            "pairs_per_step": pairs, "traversed_items_per_step": sum(r.traversed_edges for r in ref),
            "step": "hgx_bfs_sequence of the 1024 classes per direction, the directions on two execution contexts; "
                    "every (link, atom, distance) pair in host arrays",

@@ -29,6 +29,8 @@ def main():
                     help="one direction only (its own PMC passes: bench.py's per-direction drop-in rooflines)")
     ap.add_argument("--concurrent", type=int, default=0, help="steps of the two-context drop-in step")
     ap.add_argument("--breakdown", type=int, default=0, help="calls per direction: C call vs readout times")
+    ap.add_argument("--set-first", type=int, default=0, help="--concurrent: set steps run before (bench.py's order)")
+    ap.add_argument("--keep", action="store_true", help="--concurrent: keep each step's results until the next one ends")
     args = ap.parse_args()
     import hypergraphdb_amd as H
     from hypergraphdb_amd import AtomTypeCondition, DefaultALGenerator, _lib, bfs_sequence, synth
@@ -73,13 +75,26 @@ def main():
             a = bfs_sequence(views[0], g["seeds"], None, gens[0])
             return a, f.result()
 
+        if args.set_first:   # bench.py's order: the set step (hgx_bfs_batch, both directions) runs first
+            def set_step():
+                f = pool.submit(H.bfs_batch, views[1], g["seeds"], None, gens[1])
+                a = H.bfs_batch(views[0], g["seeds"], None, gens[0])
+                b = f.result()
+                return int(a.counts()[:, 1:].sum()) + int(b.counts()[:, 1:].sum())
+            for _ in range(args.set_first):
+                set_step()
         for _ in range(5):
             step()
         ts = []
+        got = None
         for _ in range(args.concurrent):
             t0 = time.perf_counter()
-            step()
+            if args.keep:   # bench.py's loop: the previous step's result arrays stay alive during the step
+                got = step()
+            else:
+                step()
             ts.append(time.perf_counter() - t0)
+        del got
         ts.sort()
         out["concurrent_ms_per_step"] = {"median": round(ts[len(ts) // 2] * 1e3, 3), "min": round(ts[0] * 1e3, 3),
                                          "mean": round(float(np.mean(ts)) * 1e3, 3), "steps": len(ts)}
